@@ -1,0 +1,98 @@
+// Shared device helpers for the streamml gfx950 kernels.
+//
+// MFMA fragment conventions used throughout (v_mfma_f32_16x16x16_bf16, wave64):
+//   lane l, c = l & 15, g = l >> 4
+//   A operand  (16x16, 4 bf16/lane): A[m = c][k = 4g + j],  j = 0..3
+//   B operand  (16x16, 4 bf16/lane): B[k = 4g + j][n = c]
+//   C/D        (16x16, 4 f32/lane) : C[m = 4g + i][n = c],  i = 0..3
+//
+// "Feature-major" (transposed) orientation: a 16-feature x 16-row activation tile
+// P[f][r] held with f = 4g+i on registers and r = c on lanes.  That is both the
+// C layout of W^T . X^T and the B layout of the next layer, so layers chain with
+// no data movement.  Re-reading the same registers as an A operand gives P^T,
+// so one MFMA against the identity converts a tile to "row-major" orientation
+// (rows on registers, feature on the lane) which is what the weight-gradient
+// MFMA (contraction over rows) consumes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sml {
+
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+enum Act : int { ACT_LINEAR = 0, ACT_RELU = 1, ACT_TANH = 2, ACT_SIGMOID = 3 };
+
+__device__ __forceinline__ f32x4 mfma16(bf16x4 a, bf16x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ unsigned pack2(float lo, float hi) {
+  f32x2_t v = {lo, hi};
+  bf16x2_t b = __builtin_convertvector(v, bf16x2_t);
+  return __builtin_bit_cast(unsigned, b);
+}
+
+__device__ __forceinline__ bf16x4 pack4(f32x4 v) {
+  unsigned lo = pack2(v[0], v[1]);
+  unsigned hi = pack2(v[2], v[3]);
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 u = {lo, hi};
+  return __builtin_bit_cast(bf16x4, u);
+}
+
+__device__ __forceinline__ float bf16_to_f32(unsigned short h) {
+  return __uint_as_float(((unsigned)h) << 16);
+}
+
+__device__ __forceinline__ float tanh_fast(float z) {
+  // tanh(z) = 1 - 2 / (exp(2z) + 1); saturates correctly at +-inf.
+  float e = __expf(2.0f * z);
+  return 1.0f - 2.0f / (e + 1.0f);
+}
+
+__device__ __forceinline__ float sigmoid_fast(float z) { return 1.0f / (1.0f + __expf(-z)); }
+
+__device__ __forceinline__ float act_fwd(int a, float z) {
+  switch (a) {
+    case ACT_RELU: return fmaxf(z, 0.0f);
+    case ACT_TANH: return tanh_fast(z);
+    case ACT_SIGMOID: return sigmoid_fast(z);
+    default: return z;
+  }
+}
+
+// derivative expressed through the activation output h
+__device__ __forceinline__ float act_bwd(int a, float h) {
+  switch (a) {
+    case ACT_RELU: return h > 0.0f ? 1.0f : 0.0f;
+    case ACT_TANH: return 1.0f - h * h;
+    case ACT_SIGMOID: return h * (1.0f - h);
+    default: return 1.0f;
+  }
+}
+
+// identity B operand: B[k = 4g+j][n = c] = (4g+j == c)
+__device__ __forceinline__ bf16x4 identity_b(int c, int g) {
+  bf16x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = (4 * g + j == c) ? (short)0x3F80 : (short)0;
+  return r;
+}
+
+// transpose a feature-major bf16 tile to row-major orientation (C layout, f32)
+__device__ __forceinline__ f32x4 transpose_tile(bf16x4 t, bf16x4 ident) {
+  f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  return mfma16(t, ident, z);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace sml

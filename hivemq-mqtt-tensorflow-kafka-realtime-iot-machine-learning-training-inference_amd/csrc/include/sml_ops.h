@@ -1,0 +1,23 @@
+// Host-side launcher declarations for the streamml gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sml {
+
+// ---- dense autoencoder (ae_fused.hip) ----
+int ae_nslot();
+int ae_nparam();
+int ae_waves_per_block();
+int ae_train_grid(int64_t n, int max_blocks);
+hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
+                           const float* params, float* partials, int64_t* iter, const int* dims, const int* acts,
+                           float l1, int want_acc, int grid, hipStream_t stream);
+hipError_t ae_forward_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
+                             const float* params, float* recon, float* score, uint8_t* flag, float threshold,
+                             const int* dims, const int* acts, int max_blocks, hipStream_t stream);
+hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, float* grad_out, float* params,
+                              float* m, float* v, const int64_t* iter, float lr, float beta1, float beta2, float eps,
+                              float gscale, float* metrics_acc, int flags, hipStream_t stream);
+
+}  // namespace sml

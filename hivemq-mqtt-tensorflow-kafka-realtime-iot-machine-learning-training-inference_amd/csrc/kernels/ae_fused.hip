@@ -1,0 +1,485 @@
+// Fused dense-autoencoder kernels for gfx950 (MI355X).
+//
+// Model family: Input(D) -> Dense(n1, a1) -> Dense(n2, a2) -> Dense(n3, a3) -> Dense(D, a4)
+// (reference: AUTOENCODER-TensorFlow-IO-Kafka/cardata-v3.py:187-194, D=18, 14/7/7,
+//  tanh/relu/tanh/relu, L1 activity regulariser 1e-7 on layer 1; the creditcard
+//  notebook uses D=30).  Loss = MSE (+ l1*sum|h1| / B), metric = categorical
+// accuracy of the reconstruction -- the op census decoded from the reference's TF
+// profile trace (MatMul/BiasAdd/Tanh/Relu/SquaredDifference/
+// ActivityRegularizer/ArgMax...).
+//
+// Design (MI355X-first, not a port of the 11-GEMM TF graph):
+//  * one wave owns 16-row tiles; every layer is one or two 16x16x16 bf16 MFMAs in
+//    feature-major orientation so activations flow layer->layer in registers;
+//  * weights (as MFMA A fragments) stay in VGPRs for the whole launch;
+//  * biases ride in the padded parameter image as the row of a constant-1 input
+//    slot, so bias gradients fall out of the weight-gradient MFMA for free;
+//  * weight gradients are MFMA contractions over rows (K = 16 rows per tile),
+//    accumulated in registers across all tiles the wave visits; a per-workgroup
+//    fp32 slab is written once per launch (deterministic, no float atomics);
+//  * a second small kernel reduces the slabs and applies Adam (Keras semantics:
+//    bias-corrected lr_t, epsilon 1e-7) elementwise on the padded image.
+//
+// Padded parameter image (fp32, 1536 floats), row-major [in][out]:
+//   L1 [32][16] @0    (bias = row 31)     requires D  <= 31, n1 <= 15
+//   L2 [16][16] @512  (bias = row 15)     requires n1 <= 15, n2 <= 15
+//   L3 [16][16] @768  (bias = row 15)     requires n2 <= 15, n3 <= 15
+//   L4 [16][32] @1024 (bias = row 15)     requires n3 <= 15
+// Slab = 1536 gradient sums + 4 metric sums {sum sq err, sum |h1|, correct, rows}.
+#include "sml_common.h"
+
+using namespace sml;
+
+namespace {
+
+constexpr int WAVES = 4;  // waves per workgroup
+constexpr int OFF1 = 0, OFF2 = 512, OFF3 = 768, OFF4 = 1024;
+constexpr int NPARAM = 1536;
+constexpr int NSLOT = 1540;
+
+struct AEArgs {
+  const float* x;        // [n, ld] raw or normalised rows
+  int64_t n;
+  int64_t ld;
+  const float* scale;    // [D] per-column affine (fused normalize_fn), may be null
+  const float* shift;
+  const float* params;   // padded image
+  float* partials;       // [grid][NSLOT]
+  int64_t* iter;         // incremented by block 0 when non-null
+  int D, n1, n2, n3;
+  int a1, a2, a3, a4;
+  float l1;
+  int want_acc;
+};
+
+struct Frags {
+  bf16x4 w1t[2], w2t, w3t, w4t[2];  // forward A operands  (W^T)
+  bf16x4 w4[2], w3, w2;             // backward A operands (W)
+  f32x4 b1, b2, b3, b4[2];          // biases in C layout
+};
+
+__device__ __forceinline__ void load_frags(const AEArgs& a, int c, int g, Frags& F, bool bwd) {
+  const float* P = a.params;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = 4 * g + j;
+    // forward: A[m = out = c][k = in]
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int in = 16 * s + k;
+      F.w1t[s][j] = 0;
+      float v = (in < a.D && c < a.n1) ? P[OFF1 + in * 16 + c] : 0.f;
+      F.w1t[s][j] = __builtin_bit_cast(short, (__bf16)v);
+    }
+    F.w2t[j] = __builtin_bit_cast(short, (__bf16)((k < a.n1 && c < a.n2) ? P[OFF2 + k * 16 + c] : 0.f));
+    F.w3t[j] = __builtin_bit_cast(short, (__bf16)((k < a.n2 && c < a.n3) ? P[OFF3 + k * 16 + c] : 0.f));
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int out = 16 * t + c;
+      F.w4t[t][j] = __builtin_bit_cast(short, (__bf16)((k < a.n3 && out < a.D) ? P[OFF4 + k * 32 + out] : 0.f));
+    }
+    if (bwd) {
+      // backward: A[m = in = c][k = out]
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int out = 16 * s + k;
+        F.w4[s][j] = __builtin_bit_cast(short, (__bf16)((c < a.n3 && out < a.D) ? P[OFF4 + c * 32 + out] : 0.f));
+      }
+      F.w3[j] = __builtin_bit_cast(short, (__bf16)((c < a.n2 && k < a.n3) ? P[OFF3 + c * 16 + k] : 0.f));
+      F.w2[j] = __builtin_bit_cast(short, (__bf16)((c < a.n1 && k < a.n2) ? P[OFF2 + c * 16 + k] : 0.f));
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int f = 4 * g + i;
+    F.b1[i] = f < a.n1 ? P[OFF1 + 31 * 16 + f] : 0.f;
+    F.b2[i] = f < a.n2 ? P[OFF2 + 15 * 16 + f] : 0.f;
+    F.b3[i] = f < a.n3 ? P[OFF3 + 15 * 16 + f] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) F.b4[t][i] = (16 * t + f) < a.D ? P[OFF4 + 15 * 32 + 16 * t + f] : 0.f;
+  }
+}
+
+// Load one 16-row tile in the B-operand layout: lane (c, g) holds features
+// 16s + 4g + j of row r0 + c.  Normalisation (normalize_fn, cardata-v3.py:78-168)
+// is fused here as a per-column affine map.
+__device__ __forceinline__ void load_x(const AEArgs& a, int64_t r, bool valid, int g, f32x4 xf[2]) {
+  const float* row = a.x + r * a.ld;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f = 16 * s + 4 * g + j;
+      float v = 0.f;
+      if (valid && f < a.D) {
+        v = row[f];
+        if (a.scale) v = fmaf(v, a.scale[f], a.shift[f]);
+      }
+      xf[s][j] = v;
+    }
+  }
+}
+
+// activation + padding: real features f < n get act(z); the bias slot (15) gets 1.
+__device__ __forceinline__ f32x4 activate_pad(int act, f32x4 z, int n, int g) {
+  f32x4 h;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int f = 4 * g + i;
+    h[i] = f < n ? act_fwd(act, z[i]) : (f == 15 ? 1.0f : 0.0f);
+  }
+  return h;
+}
+
+__device__ __forceinline__ void forward_tile(const AEArgs& a, const Frags& F, int g, const f32x4 xf[2],
+                                             bf16x4& xb0, bf16x4& xb1, f32x4& h1, f32x4& h2, f32x4& h3,
+                                             bf16x4& h1b, bf16x4& h2b, bf16x4& h3b, f32x4 y[2]) {
+  f32x4 x1 = xf[1];
+  if (g == 3) x1[3] = 1.0f;  // feature 31 = constant-1 bias slot of layer 1
+  xb0 = pack4(xf[0]);
+  xb1 = pack4(x1);
+  f32x4 z1 = mfma16(F.w1t[0], xb0, F.b1);
+  z1 = mfma16(F.w1t[1], xb1, z1);
+  h1 = activate_pad(a.a1, z1, a.n1, g);
+  h1b = pack4(h1);
+  f32x4 z2 = mfma16(F.w2t, h1b, F.b2);
+  h2 = activate_pad(a.a2, z2, a.n2, g);
+  h2b = pack4(h2);
+  f32x4 z3 = mfma16(F.w3t, h2b, F.b3);
+  h3 = activate_pad(a.a3, z3, a.n3, g);
+  h3b = pack4(h3);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    f32x4 z4 = mfma16(F.w4t[t], h3b, F.b4[t]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = 16 * t + 4 * g + i;
+      y[t][i] = f < a.D ? act_fwd(a.a4, z4[i]) : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ void argmax_combine(float& bv, int& bi, float ov, int oi) {
+  if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+}
+
+__device__ __forceinline__ int row_argmax(const f32x4 v[2], int D, int g) {
+  float bv = -INFINITY;
+  int bi = 1 << 20;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = 16 * t + 4 * g + i;
+      if (f < D && v[t][i] > bv) { bv = v[t][i]; bi = f; }
+    }
+#pragma unroll
+  for (int o = 16; o <= 32; o <<= 1) {
+    float ov = __shfl_xor(bv, o, 64);
+    int oi = __shfl_xor(bi, o, 64);
+    argmax_combine(bv, bi, ov, oi);
+  }
+  return bi;
+}
+
+__global__ __launch_bounds__(WAVES * 64) void ae_train_kernel(AEArgs a) {
+  __shared__ float red[WAVES][NSLOT];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+
+  if (a.iter && blockIdx.x == 0 && threadIdx.x == 0) a.iter[0] += 1;
+
+  Frags F;
+  load_frags(a, c, g, F, true);
+  const bf16x4 I = identity_b(c, g);
+
+  f32x4 acc1[2], acc2, acc3, acc4[2];
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  acc1[0] = acc1[1] = acc2 = acc3 = acc4[0] = acc4[1] = zero4;
+  float sq = 0.f, ab = 0.f, corr = 0.f, rows = 0.f;
+  const float two_over_d = 2.0f / (float)a.D;
+
+  const int64_t ntiles = (a.n + 15) >> 4;
+  const int64_t stride = (int64_t)gridDim.x * WAVES;
+  for (int64_t t = (int64_t)blockIdx.x * WAVES + wid; t < ntiles; t += stride) {
+    const int64_t r = t * 16 + c;
+    const bool valid = r < a.n;
+    f32x4 xf[2];
+    load_x(a, r, valid, g, xf);
+
+    bf16x4 xb0, xb1, h1b, h2b, h3b;
+    f32x4 h1, h2, h3, y[2];
+    forward_tile(a, F, g, xf, xb0, xb1, h1, h2, h3, h1b, h2b, h3b, y);
+
+    // MSE loss + dL/dz4 (sum-scaled; the 1/B factor is applied in the Adam kernel)
+    f32x4 dz4[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int f = 16 * tt + 4 * g + i;
+        float d = 0.f;
+        if (valid && f < a.D) {
+          const float e = y[tt][i] - xf[tt][i];
+          sq = fmaf(e, e, sq);
+          d = two_over_d * e * act_bwd(a.a4, y[tt][i]);
+        }
+        dz4[tt][i] = d;
+      }
+    if (a.want_acc) {
+      const int iy = row_argmax(y, a.D, g);
+      const int ix = row_argmax(xf, a.D, g);
+      if (g == 0 && valid && iy == ix) corr += 1.f;
+    }
+    if (g == 0 && valid) rows += 1.f;
+
+    // backward through the layers (feature-major, in registers)
+    const bf16x4 dz4b0 = pack4(dz4[0]), dz4b1 = pack4(dz4[1]);
+    f32x4 dh3 = mfma16(F.w4[0], dz4b0, zero4);
+    dh3 = mfma16(F.w4[1], dz4b1, dh3);
+    f32x4 dz3, dz2, dz1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dz3[i] = (4 * g + i) < a.n3 ? dh3[i] * act_bwd(a.a3, h3[i]) : 0.f;
+    const bf16x4 dz3b = pack4(dz3);
+    const f32x4 dh2 = mfma16(F.w3, dz3b, zero4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dz2[i] = (4 * g + i) < a.n2 ? dh2[i] * act_bwd(a.a2, h2[i]) : 0.f;
+    const bf16x4 dz2b = pack4(dz2);
+    const f32x4 dh1 = mfma16(F.w2, dz2b, zero4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float d = 0.f;
+      if ((4 * g + i) < a.n1) {
+        float gsum = dh1[i];
+        if (valid) {
+          const float hv = h1[i];
+          ab += fabsf(hv);
+          gsum += a.l1 * (hv > 0.f ? 1.f : (hv < 0.f ? -1.f : 0.f));
+        }
+        d = gsum * act_bwd(a.a1, h1[i]);
+      }
+      dz1[i] = d;
+    }
+    const bf16x4 dz1b = pack4(dz1);
+
+    // weight gradients: contraction over the 16 rows of the tile
+    const bf16x4 xr0 = pack4(transpose_tile(xb0, I));
+    const bf16x4 xr1 = pack4(transpose_tile(xb1, I));
+    const bf16x4 dz1r = pack4(transpose_tile(dz1b, I));
+    acc1[0] = mfma16(xr0, dz1r, acc1[0]);
+    acc1[1] = mfma16(xr1, dz1r, acc1[1]);
+    const bf16x4 h1r = pack4(transpose_tile(h1b, I));
+    const bf16x4 dz2r = pack4(transpose_tile(dz2b, I));
+    acc2 = mfma16(h1r, dz2r, acc2);
+    const bf16x4 h2r = pack4(transpose_tile(h2b, I));
+    const bf16x4 dz3r = pack4(transpose_tile(dz3b, I));
+    acc3 = mfma16(h2r, dz3r, acc3);
+    const bf16x4 h3r = pack4(transpose_tile(h3b, I));
+    const bf16x4 dz4r0 = pack4(transpose_tile(dz4b0, I));
+    const bf16x4 dz4r1 = pack4(transpose_tile(dz4b1, I));
+    acc4[0] = mfma16(h3r, dz4r0, acc4[0]);
+    acc4[1] = mfma16(h3r, dz4r1, acc4[1]);
+  }
+
+  // per-wave slab in LDS (every slot written exactly once per wave)
+  float* my = red[wid];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = 4 * g + i;
+    my[OFF1 + m * 16 + c] = acc1[0][i];
+    my[OFF1 + (16 + m) * 16 + c] = acc1[1][i];
+    my[OFF2 + m * 16 + c] = acc2[i];
+    my[OFF3 + m * 16 + c] = acc3[i];
+    my[OFF4 + m * 32 + c] = acc4[0][i];
+    my[OFF4 + m * 32 + 16 + c] = acc4[1][i];
+  }
+  sq = wave_sum(sq);
+  ab = wave_sum(ab);
+  corr = wave_sum(corr);
+  rows = wave_sum(rows);
+  if (lane == 0) {
+    my[NPARAM + 0] = sq;
+    my[NPARAM + 1] = ab;
+    my[NPARAM + 2] = corr;
+    my[NPARAM + 3] = rows;
+  }
+  __syncthreads();
+  float* out = a.partials + (int64_t)blockIdx.x * NSLOT;
+  for (int s = threadIdx.x; s < NSLOT; s += WAVES * 64) {
+    float v = red[0][s];
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) v += red[w][s];
+    out[s] = v;
+  }
+}
+
+struct FwdArgs {
+  const float* x;
+  int64_t n;
+  int64_t ld;
+  const float* scale;
+  const float* shift;
+  const float* params;
+  float* recon;          // [n, D] or null
+  float* score;          // [n] per-row MSE or null
+  uint8_t* flag;         // [n] score > threshold or null
+  float threshold;
+  int D, n1, n2, n3;
+  int a1, a2, a3, a4;
+};
+
+__global__ __launch_bounds__(WAVES * 64) void ae_forward_kernel(FwdArgs fa) {
+  AEArgs a{};
+  a.x = fa.x; a.n = fa.n; a.ld = fa.ld; a.scale = fa.scale; a.shift = fa.shift; a.params = fa.params;
+  a.D = fa.D; a.n1 = fa.n1; a.n2 = fa.n2; a.n3 = fa.n3;
+  a.a1 = fa.a1; a.a2 = fa.a2; a.a3 = fa.a3; a.a4 = fa.a4;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  Frags F;
+  load_frags(a, c, g, F, false);
+  const int64_t ntiles = (a.n + 15) >> 4;
+  const int64_t stride = (int64_t)gridDim.x * WAVES;
+  const float inv_d = 1.0f / (float)a.D;
+  for (int64_t t = (int64_t)blockIdx.x * WAVES + wid; t < ntiles; t += stride) {
+    const int64_t r = t * 16 + c;
+    const bool valid = r < a.n;
+    f32x4 xf[2];
+    load_x(a, r, valid, g, xf);
+    bf16x4 xb0, xb1, h1b, h2b, h3b;
+    f32x4 h1, h2, h3, y[2];
+    forward_tile(a, F, g, xf, xb0, xb1, h1, h2, h3, h1b, h2b, h3b, y);
+    float se = 0.f;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int f = 16 * tt + 4 * g + i;
+        if (f < a.D) {
+          const float e = y[tt][i] - xf[tt][i];
+          se = fmaf(e, e, se);
+          if (valid && fa.recon) fa.recon[r * a.D + f] = y[tt][i];
+        }
+      }
+    se += __shfl_xor(se, 16, 64);
+    se += __shfl_xor(se, 32, 64);
+    if (g == 0 && valid) {
+      const float sc = se * inv_d;
+      if (fa.score) fa.score[r] = sc;
+      if (fa.flag) fa.flag[r] = sc > fa.threshold ? 1 : 0;
+    }
+  }
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------
+// Slab reduction + Adam (Keras/TF ResourceApplyAdam semantics).
+// ----------------------------------------------------------------------------
+namespace {
+struct AdamHP {
+  float lr, beta1, beta2, eps;
+};
+
+enum : int { RA_WRITE_GRAD = 1, RA_ADAM = 2, RA_METRICS = 4 };
+
+__global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restrict__ partials, int G, int S,
+                                                          int nparam, float* grad_out, float* params, float* m,
+                                                          float* v, const int64_t* iter, AdamHP hp, float gscale,
+                                                          float* metrics_acc, int flags) {
+  __shared__ float red[16][17];
+  const int sl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int slot = blockIdx.x * 16 + sl;
+  float acc = 0.f;
+  if (slot < S) {
+    int gi = grp;
+    for (; gi + 48 < G; gi += 64) {
+      const float p0 = partials[(int64_t)gi * S + slot];
+      const float p1 = partials[(int64_t)(gi + 16) * S + slot];
+      const float p2 = partials[(int64_t)(gi + 32) * S + slot];
+      const float p3 = partials[(int64_t)(gi + 48) * S + slot];
+      acc += (p0 + p1) + (p2 + p3);
+    }
+    for (; gi < G; gi += 16) acc += partials[(int64_t)gi * S + slot];
+  }
+  red[grp][sl] = acc;
+  __syncthreads();
+  if (grp != 0 || slot >= S) return;
+  float tot = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) tot += red[k][sl];
+  if (flags & RA_WRITE_GRAD) grad_out[slot] = tot;
+  if (slot < nparam) {
+    if (flags & RA_ADAM) {
+      const float t = (float)iter[0];
+      const float bc1 = 1.0f - powf(hp.beta1, t);
+      const float bc2 = 1.0f - powf(hp.beta2, t);
+      const float lr_t = hp.lr * sqrtf(bc2) / bc1;
+      const float gr = tot * gscale;
+      const float mm = hp.beta1 * m[slot] + (1.0f - hp.beta1) * gr;
+      const float vv = hp.beta2 * v[slot] + (1.0f - hp.beta2) * gr * gr;
+      m[slot] = mm;
+      v[slot] = vv;
+      params[slot] -= lr_t * mm / (sqrtf(vv) + hp.eps);
+    }
+  } else if ((flags & RA_METRICS) && metrics_acc) {
+    metrics_acc[slot - nparam] += tot;
+  }
+}
+}  // namespace
+
+// ----------------------------------------------------------------------------
+// host launchers (called from the torch binding)
+// ----------------------------------------------------------------------------
+namespace sml {
+
+int ae_nslot() { return NSLOT; }
+int ae_nparam() { return NPARAM; }
+int ae_waves_per_block() { return WAVES; }
+
+int ae_train_grid(int64_t n, int max_blocks) {
+  const int64_t ntiles = (n + 15) / 16;
+  int64_t blocks = (ntiles + WAVES - 1) / WAVES;
+  if (blocks > max_blocks) blocks = max_blocks;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
+}
+
+hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
+                           const float* params, float* partials, int64_t* iter, const int* dims, const int* acts,
+                           float l1, int want_acc, int grid, hipStream_t stream) {
+  AEArgs a{};
+  a.x = x; a.n = n; a.ld = ld; a.scale = scale; a.shift = shift; a.params = params;
+  a.partials = partials; a.iter = iter;
+  a.D = dims[0]; a.n1 = dims[1]; a.n2 = dims[2]; a.n3 = dims[3];
+  a.a1 = acts[0]; a.a2 = acts[1]; a.a3 = acts[2]; a.a4 = acts[3];
+  a.l1 = l1; a.want_acc = want_acc;
+  hipLaunchKernelGGL(ae_train_kernel, dim3(grid), dim3(WAVES * 64), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t ae_forward_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
+                             const float* params, float* recon, float* score, uint8_t* flag, float threshold,
+                             const int* dims, const int* acts, int max_blocks, hipStream_t stream) {
+  FwdArgs a{};
+  a.x = x; a.n = n; a.ld = ld; a.scale = scale; a.shift = shift; a.params = params;
+  a.recon = recon; a.score = score; a.flag = flag; a.threshold = threshold;
+  a.D = dims[0]; a.n1 = dims[1]; a.n2 = dims[2]; a.n3 = dims[3];
+  a.a1 = acts[0]; a.a2 = acts[1]; a.a3 = acts[2]; a.a4 = acts[3];
+  const int grid = ae_train_grid(n, max_blocks);
+  hipLaunchKernelGGL(ae_forward_kernel, dim3(grid), dim3(WAVES * 64), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, float* grad_out, float* params,
+                              float* m, float* v, const int64_t* iter, float lr, float beta1, float beta2, float eps,
+                              float gscale, float* metrics_acc, int flags, hipStream_t stream) {
+  AdamHP hp{lr, beta1, beta2, eps};
+  const int grid = (S + 15) / 16;
+  hipLaunchKernelGGL(reduce_adam_kernel, dim3(grid), dim3(256), 0, stream, partials, G, S, nparam, grad_out, params,
+                     m, v, iter, hp, gscale, metrics_acc, flags);
+  return hipGetLastError();
+}
+
+}  // namespace sml

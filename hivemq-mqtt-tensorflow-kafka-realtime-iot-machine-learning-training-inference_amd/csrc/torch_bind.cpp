@@ -1,0 +1,146 @@
+// PyTorch binding for the gfx950 kernels (module streamml._C).
+//
+// Every op here requires ROCm device tensors; there is deliberately no CPU
+// fallback inside the extension (the torch-CPU reference path lives in Python
+// and is only used for the CPU plumbing configuration / numerics oracles).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <hip/hip_runtime.h>
+
+#include "sml_ops.h"
+
+namespace {
+
+#define SML_CHECK_HIP(expr)                                                           \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    TORCH_CHECK(_e == hipSuccess, "HIP error: ", hipGetErrorString(_e), " @ ", #expr); \
+  } while (0)
+
+void check_dev(const at::Tensor& t, const char* name, at::ScalarType st) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a ROCm device tensor");
+  TORCH_CHECK(t.scalar_type() == st, name, " has wrong dtype ", t.scalar_type());
+  TORCH_CHECK(t.is_contiguous() || t.dim() == 2, name, " must be contiguous");
+}
+
+const float* opt_ptr(const c10::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
+}
+float* opt_mut(const c10::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
+}
+
+hipStream_t cur_stream(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_ae_dims(const std::vector<int64_t>& dims, const std::vector<int64_t>& acts) {
+  TORCH_CHECK(dims.size() == 4 && acts.size() == 4, "dims/acts must have 4 entries");
+  TORCH_CHECK(dims[0] >= 1 && dims[0] <= 31, "AE input dim must be in [1,31]");
+  for (int i = 1; i < 4; ++i) TORCH_CHECK(dims[i] >= 1 && dims[i] <= 15, "AE hidden dims must be in [1,15]");
+  for (auto a : acts) TORCH_CHECK(a >= 0 && a <= 3, "activation code must be 0..3");
+}
+
+int64_t ae_train_partials(const at::Tensor& x, const c10::optional<at::Tensor>& scale,
+                          const c10::optional<at::Tensor>& shift, const at::Tensor& params, at::Tensor& partials,
+                          const c10::optional<at::Tensor>& iter, std::vector<int64_t> dims, std::vector<int64_t> acts,
+                          double l1, bool want_acc, int64_t max_blocks) {
+  check_ae_dims(dims, acts);
+  check_dev(x, "x", at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [n, ld] with unit column stride");
+  TORCH_CHECK(x.size(1) >= dims[0], "x has fewer columns than the model input dim");
+  check_dev(params, "params", at::kFloat);
+  TORCH_CHECK(params.numel() == sml::ae_nparam(), "params must be the padded 1536-float image");
+  check_dev(partials, "partials", at::kFloat);
+  if (scale.has_value()) {
+    TORCH_CHECK(shift.has_value(), "scale requires shift");
+    check_dev(*scale, "scale", at::kFloat);
+    check_dev(*shift, "shift", at::kFloat);
+    TORCH_CHECK(scale->numel() >= dims[0] && shift->numel() >= dims[0], "scale/shift too short");
+  }
+  int64_t* iter_ptr = nullptr;
+  if (iter.has_value() && iter->defined()) {
+    check_dev(*iter, "iter", at::kLong);
+    iter_ptr = iter->data_ptr<int64_t>();
+  }
+  const int64_t n = x.size(0);
+  const int grid = sml::ae_train_grid(n, (int)max_blocks);
+  TORCH_CHECK(partials.numel() >= (int64_t)grid * sml::ae_nslot(), "partials buffer too small for grid ", grid);
+  c10::hip::HIPGuard guard(x.device().index());
+  int d[4] = {(int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3]};
+  int a[4] = {(int)acts[0], (int)acts[1], (int)acts[2], (int)acts[3]};
+  SML_CHECK_HIP(sml::ae_train_launch(x.data_ptr<float>(), n, x.stride(0), opt_ptr(scale), opt_ptr(shift),
+                                     params.data_ptr<float>(), partials.data_ptr<float>(), iter_ptr, d, a, (float)l1,
+                                     want_acc ? 1 : 0, grid, cur_stream(x)));
+  return grid;
+}
+
+void reduce_adam(const at::Tensor& partials, int64_t G, int64_t S, int64_t nparam,
+                 const c10::optional<at::Tensor>& grad_out, const c10::optional<at::Tensor>& params,
+                 const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
+                 const c10::optional<at::Tensor>& iter, double lr, double beta1, double beta2, double eps,
+                 double gscale, const c10::optional<at::Tensor>& metrics, int64_t flags) {
+  check_dev(partials, "partials", at::kFloat);
+  TORCH_CHECK(partials.numel() >= G * S, "partials smaller than G*S");
+  if (flags & 2) {
+    TORCH_CHECK(params.has_value() && m.has_value() && v.has_value() && iter.has_value(), "adam needs params/m/v/iter");
+    TORCH_CHECK(params->numel() >= nparam && m->numel() >= nparam && v->numel() >= nparam, "adam buffers too small");
+    check_dev(*iter, "iter", at::kLong);
+  }
+  if (flags & 1) TORCH_CHECK(grad_out.has_value() && grad_out->numel() >= S, "grad_out too small");
+  if (flags & 4) TORCH_CHECK(metrics.has_value() && metrics->numel() >= S - nparam, "metrics too small");
+  c10::hip::HIPGuard guard(partials.device().index());
+  const int64_t* iter_ptr = (iter.has_value() && iter->defined()) ? iter->data_ptr<int64_t>() : nullptr;
+  SML_CHECK_HIP(sml::reduce_adam_launch(partials.data_ptr<float>(), (int)G, (int)S, (int)nparam, opt_mut(grad_out),
+                                        opt_mut(params), opt_mut(m), opt_mut(v), iter_ptr, (float)lr, (float)beta1,
+                                        (float)beta2, (float)eps, (float)gscale, opt_mut(metrics), (int)flags,
+                                        cur_stream(partials)));
+}
+
+void ae_forward(const at::Tensor& x, const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift,
+                const at::Tensor& params, const c10::optional<at::Tensor>& recon,
+                const c10::optional<at::Tensor>& score, const c10::optional<at::Tensor>& flag, double threshold,
+                std::vector<int64_t> dims, std::vector<int64_t> acts, int64_t max_blocks) {
+  check_ae_dims(dims, acts);
+  check_dev(x, "x", at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [n, ld]");
+  TORCH_CHECK(x.size(1) >= dims[0], "x has fewer columns than the model input dim");
+  check_dev(params, "params", at::kFloat);
+  TORCH_CHECK(params.numel() == sml::ae_nparam(), "params must be the padded image");
+  const int64_t n = x.size(0);
+  if (recon.has_value()) TORCH_CHECK(recon->numel() >= n * dims[0] && recon->is_contiguous(), "recon too small");
+  if (score.has_value()) TORCH_CHECK(score->numel() >= n, "score too small");
+  uint8_t* flag_ptr = nullptr;
+  if (flag.has_value() && flag->defined()) {
+    TORCH_CHECK(flag->scalar_type() == at::kByte && flag->numel() >= n, "flag must be uint8[n]");
+    flag_ptr = flag->data_ptr<uint8_t>();
+  }
+  if (scale.has_value()) TORCH_CHECK(shift.has_value(), "scale requires shift");
+  c10::hip::HIPGuard guard(x.device().index());
+  int d[4] = {(int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3]};
+  int a[4] = {(int)acts[0], (int)acts[1], (int)acts[2], (int)acts[3]};
+  SML_CHECK_HIP(sml::ae_forward_launch(x.data_ptr<float>(), n, x.stride(0), opt_ptr(scale), opt_ptr(shift),
+                                       params.data_ptr<float>(), opt_mut(recon), opt_mut(score), flag_ptr,
+                                       (float)threshold, d, a, (int)max_blocks, cur_stream(x)));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "streamml gfx950 HIP kernels";
+  m.attr("AE_NSLOT") = sml::ae_nslot();
+  m.attr("AE_NPARAM") = sml::ae_nparam();
+  m.def("ae_train_partials", &ae_train_partials, "fused AE fwd+bwd -> per-workgroup gradient slabs",
+        py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("partials"), py::arg("iter"),
+        py::arg("dims"), py::arg("acts"), py::arg("l1"), py::arg("want_acc"), py::arg("max_blocks"));
+  m.def("ae_train_grid", &sml::ae_train_grid, "grid size the AE train kernel uses", py::arg("n"),
+        py::arg("max_blocks"));
+  m.def("reduce_adam", &reduce_adam, "slab reduction + optional Adam", py::arg("partials"), py::arg("G"),
+        py::arg("S"), py::arg("nparam"), py::arg("grad_out"), py::arg("params"), py::arg("m"), py::arg("v"),
+        py::arg("iter"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("gscale"),
+        py::arg("metrics"), py::arg("flags"));
+  m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),
+        py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("recon"), py::arg("score"), py::arg("flag"),
+        py::arg("threshold"), py::arg("dims"), py::arg("acts"), py::arg("max_blocks"));
+}

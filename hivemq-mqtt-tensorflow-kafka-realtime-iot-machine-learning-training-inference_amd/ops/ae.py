@@ -1,0 +1,210 @@
+"""Device runtime for the fused dense-autoencoder kernels (``csrc/kernels/ae_fused.hip``).
+
+One optimizer step on ``n`` rows is two launches (plus one all-reduce under DP):
+
+1. ``ae_train_partials``: fwd + bwd of every 16-row tile on MFMA, weight
+   gradients accumulated in registers, one fp32 slab per workgroup;
+2. ``reduce_adam``: slab reduction and the Keras/TF Adam update applied to the
+   padded parameter image (``iterations`` counter lives on device).
+
+With data parallelism the reduction writes the flat gradient bucket
+(1536 gradient sums + 4 metric sums = 6160 bytes), which is all-reduced once per
+step over RCCL, then a second ``reduce_adam`` (G = 1) applies Adam.  Metrics are
+accumulated on device and read once per epoch, never per step.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ._ext import load_c
+
+ACT_CODES = {"linear": 0, None: 0, "relu": 1, "tanh": 2, "sigmoid": 3}
+NPARAM = 1536
+NSLOT = 1540
+# offsets / shapes of the padded image [in_pad][out_pad] and the bias row
+LAYOUT = [(0, 32, 16, 31), (512, 16, 16, 15), (768, 16, 16, 15), (1024, 16, 32, 15)]
+
+RA_WRITE_GRAD, RA_ADAM, RA_METRICS = 1, 2, 4
+
+
+@dataclass
+class AESpec:
+    """Dense autoencoder D -> n1 -> n2 -> n3 -> D (reference cardata-v3.py:187-194)."""
+
+    input_dim: int = 18
+    encoding_dim: int = 14
+    hidden_dim: int = 7
+    activations: Tuple[str, str, str, str] = ("tanh", "relu", "tanh", "relu")
+    activity_l1: float = 1e-7
+
+    @property
+    def dims(self) -> List[int]:
+        return [self.input_dim, self.encoding_dim, self.hidden_dim, self.hidden_dim]
+
+    @property
+    def layer_sizes(self) -> List[Tuple[int, int]]:
+        d, e, h = self.input_dim, self.encoding_dim, self.hidden_dim
+        return [(d, e), (e, h), (h, h), (h, d)]
+
+    @property
+    def act_codes(self) -> List[int]:
+        return [ACT_CODES[a] for a in self.activations]
+
+    @property
+    def n_params(self) -> int:
+        return sum(i * o + o for i, o in self.layer_sizes)
+
+    def check_fused(self) -> None:
+        if not (1 <= self.input_dim <= 31 and 1 <= self.encoding_dim <= 15 and 1 <= self.hidden_dim <= 15):
+            raise ValueError("fused AE kernel supports input_dim <= 31 and hidden sizes <= 15, got "
+                             f"{self.layer_sizes}")
+
+
+def pack_image(weights: Sequence[np.ndarray]) -> np.ndarray:
+    """Keras ``[k0, b0, k1, b1, k2, b2, k3, b3]`` (kernel [in, out]) -> padded 1536 image."""
+    img = np.zeros(NPARAM, dtype=np.float32)
+    for li, (off, ip, op, brow) in enumerate(LAYOUT):
+        k = np.asarray(weights[2 * li], dtype=np.float32)
+        b = np.asarray(weights[2 * li + 1], dtype=np.float32)
+        i, o = k.shape
+        view = img[off:off + ip * op].reshape(ip, op)
+        view[:i, :o] = k
+        view[brow, :o] = b
+    return img
+
+
+def unpack_image(img: np.ndarray, spec: AESpec) -> List[np.ndarray]:
+    """Padded image -> Keras weight list ``[k0, b0, ..., k3, b3]``."""
+    img = np.asarray(img, dtype=np.float32).reshape(-1)
+    out: List[np.ndarray] = []
+    for (off, ip, op, brow), (i, o) in zip(LAYOUT, spec.layer_sizes):
+        view = img[off:off + ip * op].reshape(ip, op)
+        out.append(view[:i, :o].copy())
+        out.append(view[brow, :o].copy())
+    return out
+
+
+class FusedAE:
+    """Holds the on-device state of one autoencoder replica and runs fused steps."""
+
+    def __init__(self, spec: AESpec, weights: Sequence[np.ndarray], device,
+                 lr: float = 1e-3, beta_1: float = 0.9, beta_2: float = 0.999, epsilon: float = 1e-7,
+                 max_blocks: int = 1024, want_acc: bool = True,
+                 scale: Optional[np.ndarray] = None, shift: Optional[np.ndarray] = None):
+        spec.check_fused()
+        self.C = load_c()
+        self.spec = spec
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("FusedAE runs on a ROCm device only")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.lr, self.beta_1, self.beta_2, self.epsilon = lr, beta_1, beta_2, epsilon
+        self.max_blocks = int(max_blocks)
+        self.want_acc = want_acc
+        dev = self.device
+        self.params = torch.from_numpy(pack_image(weights)).to(dev)
+        self.m = torch.zeros(NPARAM, device=dev)
+        self.v = torch.zeros(NPARAM, device=dev)
+        self.iter = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.partials = torch.zeros(self.max_blocks * NSLOT, device=dev)
+        self.grad = torch.zeros(NSLOT, device=dev)
+        self.metrics = torch.zeros(NSLOT - NPARAM, device=dev)   # epoch accumulators
+        self.set_normalizer(scale, shift)
+
+    # -- normalisation fused into the first load ------------------------------------
+    def set_normalizer(self, scale: Optional[np.ndarray], shift: Optional[np.ndarray]) -> None:
+        if scale is None:
+            self.scale = self.shift = None
+        else:
+            self.scale = torch.as_tensor(np.asarray(scale, dtype=np.float32), device=self.device)
+            self.shift = torch.as_tensor(np.asarray(shift, dtype=np.float32), device=self.device)
+
+    # -- state -------------------------------------------------------------------------
+    def get_weights(self) -> List[np.ndarray]:
+        return unpack_image(self.params.detach().cpu().numpy(), self.spec)
+
+    def set_weights(self, weights: Sequence[np.ndarray]) -> None:
+        self.params.copy_(torch.from_numpy(pack_image(weights)))
+
+    def get_optimizer_state(self) -> Tuple[int, List[np.ndarray], List[np.ndarray]]:
+        it = int(self.iter.item())
+        return (it, unpack_image(self.m.cpu().numpy(), self.spec), unpack_image(self.v.cpu().numpy(), self.spec))
+
+    def set_optimizer_state(self, it: int, m: Sequence[np.ndarray], v: Sequence[np.ndarray]) -> None:
+        self.iter.fill_(int(it))
+        self.m.copy_(torch.from_numpy(pack_image(m)))
+        self.v.copy_(torch.from_numpy(pack_image(v)))
+
+    # -- kernels ---------------------------------------------------------------------
+    def _check_x(self, x: torch.Tensor) -> None:
+        if x.device != self.device or x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1:
+            raise ValueError("x must be a float32 [n, >=D] tensor with unit column stride on "
+                             f"{self.device}, got {x.dtype} {tuple(x.shape)} on {x.device}")
+        if x.size(1) < self.spec.input_dim:
+            raise ValueError("x has too few columns")
+
+    def grad_partials(self, x: torch.Tensor, bump_iter: bool = True) -> int:
+        """Launch 1: fwd+bwd -> per-workgroup slabs; returns the grid size G."""
+        self._check_x(x)
+        return self.C.ae_train_partials(x, self.scale, self.shift, self.params, self.partials,
+                                        self.iter if bump_iter else None, self.spec.dims, self.spec.act_codes,
+                                        float(self.spec.activity_l1), bool(self.want_acc), self.max_blocks)
+
+    def reduce(self, G: int, flags: int, gscale: float = 1.0, partials: Optional[torch.Tensor] = None) -> None:
+        src = self.partials if partials is None else partials
+        self.C.reduce_adam(src, int(G), NSLOT, NPARAM, self.grad, self.params, self.m, self.v, self.iter,
+                           self.lr, self.beta_1, self.beta_2, self.epsilon, float(gscale), self.metrics, int(flags))
+
+    def step(self, x: torch.Tensor, global_batch: Optional[int] = None, allreduce=None) -> None:
+        """One full optimizer step on ``x`` (all rows of the local micro-batch).
+
+        ``global_batch`` defaults to ``len(x)``; under DP pass the global batch and
+        an ``allreduce(tensor)`` callable (sum over replicas, in place).
+        """
+        n = x.size(0)
+        gb = n if global_batch is None else int(global_batch)
+        G = self.grad_partials(x)
+        if allreduce is None:
+            self.reduce(G, RA_ADAM | RA_METRICS, gscale=1.0 / gb)
+        else:
+            self.reduce(G, RA_WRITE_GRAD)
+            allreduce(self.grad)
+            self.reduce(1, RA_ADAM | RA_METRICS, gscale=1.0 / gb, partials=self.grad)
+
+    def gradients(self, x: torch.Tensor, global_batch: Optional[int] = None) -> Tuple[List[np.ndarray], np.ndarray]:
+        """Mean-over-batch gradients (Keras weight order) + raw metric sums; no update."""
+        G = self.grad_partials(x, bump_iter=False)
+        self.reduce(G, RA_WRITE_GRAD)
+        gb = x.size(0) if global_batch is None else global_batch
+        g = self.grad.detach().cpu().numpy()
+        return unpack_image(g[:NPARAM] / gb, self.spec), g[NPARAM:].copy()
+
+    def reset_metrics(self) -> None:
+        self.metrics.zero_()
+
+    def read_metrics(self) -> dict:
+        """Epoch metrics in Keras terms from the device accumulators (one host sync)."""
+        sq, ab, corr, rows = [float(v) for v in self.metrics.cpu().tolist()]
+        D = self.spec.input_dim
+        rows = max(rows, 1.0)
+        loss = (sq / D + self.spec.activity_l1 * ab) / rows
+        return {"loss": loss, "mse": sq / (D * rows), "accuracy": corr / rows, "rows": rows}
+
+    def forward(self, x: torch.Tensor, recon: bool = True, score: bool = True,
+                threshold: Optional[float] = None):
+        """Inference: reconstruction [n, D], per-row MSE score [n], anomaly flag [n]."""
+        self._check_x(x)
+        n = x.size(0)
+        D = self.spec.input_dim
+        r = torch.empty((n, D), device=self.device) if recon else None
+        s = torch.empty(n, device=self.device) if score else None
+        f = torch.empty(n, dtype=torch.uint8, device=self.device) if threshold is not None else None
+        self.C.ae_forward(x, self.scale, self.shift, self.params, r, s, f,
+                          float(threshold if threshold is not None else 0.0), self.spec.dims,
+                          self.spec.act_codes, self.max_blocks)
+        return r, s, f

@@ -1,0 +1,38 @@
+#!/usr/bin/env bash
+# One GPU-box session: gpu tests, smoke, bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; a fault / abort / timeout ends the script.
+# Ordinary test failures (pytest exit 1) do not stop the later measurement steps.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+fatal() {  # exit codes that mean the GPU step crashed / hung
+  case "$1" in 124|134|137|139) return 0 ;; *) return 1 ;; esac
+}
+
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -n 5 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL in $name (rc=$rc): stopping"; exit $rc; fi
+  return $rc
+}
+
+STEPS=${STEPS:-"tests smoke bench prof"}
+for s in $STEPS; do
+  case $s in
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    prof)
+      (cd /tmp && step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+          python3 "$ROOT/bench.py" --steps 50 --warmup 5 --infer-events 100 ${BENCH_ARGS:-}) ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo "== done"
