@@ -78,7 +78,9 @@ def build_c(verbose: bool = False, force: bool = False) -> str:
         objs.append(obj)
         if force or _newer([src] + hdrs, obj):
             jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
-                         f"-I{inc}", "-Wno-unused-result", "-munsafe-fp-atomics"])
+                         f"-I{inc}", "-Wno-unused-result", "-munsafe-fp-atomics",
+                         # MFMA results straight into VGPRs: no v_accvgpr_read per use
+                         "-mllvm", "-amdgpu-mfma-vgpr-form"])
     bind = os.path.join(CSRC, "torch_bind.cpp")
     bind_obj = os.path.join(BUILD, "torch_bind.o")
     objs.append(bind_obj)

@@ -48,20 +48,36 @@ __device__ __forceinline__ float bf16_to_f32(unsigned short h) {
   return __uint_as_float(((unsigned)h) << 16);
 }
 
+__device__ __forceinline__ float rcp_fast(float x) { return __builtin_amdgcn_rcpf(x); }
+
 __device__ __forceinline__ float tanh_fast(float z) {
-  // tanh(z) = 1 - 2 / (exp(2z) + 1); saturates correctly at +-inf.
-  float e = __expf(2.0f * z);
-  return 1.0f - 2.0f / (e + 1.0f);
+  // tanh(z) = 1 - 2 / (exp(2z) + 1); exp(2z) = exp2(z * 2*log2(e)).
+  // Saturates correctly at +-inf (rcp(inf) = 0).
+  const float e = __builtin_amdgcn_exp2f(z * 2.8853900817779268f);
+  return fmaf(-2.0f, rcp_fast(e + 1.0f), 1.0f);
 }
 
-__device__ __forceinline__ float sigmoid_fast(float z) { return 1.0f / (1.0f + __expf(-z)); }
+// max(z, 0) in one v_med3_f32 (fmaxf adds a NaN-canonicalising v_max)
+__device__ __forceinline__ float relu_fast(float z) { return __builtin_amdgcn_fmed3f(z, 0.0f, 3.402823466e38f); }
+
+__device__ __forceinline__ float sigmoid_fast(float z) { return rcp_fast(1.0f + __expf(-z)); }
 
 __device__ __forceinline__ float act_fwd(int a, float z) {
   switch (a) {
-    case ACT_RELU: return fmaxf(z, 0.0f);
+    case ACT_RELU: return relu_fast(z);
     case ACT_TANH: return tanh_fast(z);
     case ACT_SIGMOID: return sigmoid_fast(z);
     default: return z;
+  }
+}
+
+// d * act'(.) expressed through the activation output h
+__device__ __forceinline__ float act_grad(int a, float h, float d) {
+  switch (a) {
+    case ACT_RELU: return h > 0.0f ? d : 0.0f;
+    case ACT_TANH: return d * fmaf(-h, h, 1.0f);
+    case ACT_SIGMOID: return d * h * (1.0f - h);
+    default: return d;
   }
 }
 
@@ -88,6 +104,22 @@ __device__ __forceinline__ f32x4 transpose_tile(bf16x4 t, bf16x4 ident) {
   f32x4 z = {0.f, 0.f, 0.f, 0.f};
   return mfma16(t, ident, z);
 }
+
+// Lane exchange across 16-lane rows / 32-lane halves with the gfx950 VALU
+// permlane swaps (no LDS traffic).  xor16(v) returns v of lane (l ^ 16),
+// xor32(v) returns v of lane (l ^ 32).
+__device__ __forceinline__ float xor16(float v, int lane) {
+  const unsigned u = __float_as_uint(v);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __uint_as_float(((lane >> 4) & 1) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float xor32(float v, int lane) {
+  const unsigned u = __float_as_uint(v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __uint_as_float(lane >= 32 ? r[0] : r[1]);
+}
+__device__ __forceinline__ int xor16i(int v, int lane) { return __float_as_int(xor16(__int_as_float(v), lane)); }
+__device__ __forceinline__ int xor32i(int v, int lane) { return __float_as_int(xor32(__int_as_float(v), lane)); }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -20,4 +20,7 @@ hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, f
                               float* m, float* v, const int64_t* iter, float lr, float beta1, float beta2, float eps,
                               float gscale, float* metrics_acc, int flags, hipStream_t stream);
 
+// ---- utilities (util.hip) ----
+hipError_t lane_xor_probe_launch(float* out, hipStream_t stream);
+
 }  // namespace sml

@@ -52,12 +52,40 @@ struct AEArgs {
   int want_acc;
 };
 
-struct Frags {
+// Activation codes are compile-time when PACK >= 0 (a1 | a2<<2 | a3<<4 | a4<<6),
+// runtime otherwise.  The reference model (tanh, relu, tanh, relu) is PACK 0x66.
+constexpr int PACK_REF = ACT_TANH | (ACT_RELU << 2) | (ACT_TANH << 4) | (ACT_RELU << 6);
+constexpr int PACK_DYN = -1;
+
+template <int PACK>
+__device__ __forceinline__ int act_of(const AEArgs& a, int i) {
+  if constexpr (PACK >= 0) {
+    return (PACK >> (2 * i)) & 3;
+  } else {
+    return i == 0 ? a.a1 : i == 1 ? a.a2 : i == 2 ? a.a3 : a.a4;
+  }
+}
+
+struct Frags {  // register-resident operands for one launch
   bf16x4 w1t[2], w2t, w3t, w4t[2];  // forward A operands  (W^T)
   bf16x4 w4[2], w3, w2;             // backward A operands (W)
   f32x4 b1, b2, b3, b4[2];          // biases in C layout
+  f32x4 sc[2], sh[2];               // normaliser in B layout (feature 16s + 4g + j)
 };
 
+__device__ __forceinline__ short bfbits(float v) { return __builtin_bit_cast(short, (__bf16)v); }
+
+template <int PACK>
+constexpr bool zero_preserving() {
+  if (PACK < 0) return false;
+  for (int i = 0; i < 4; ++i)
+    if (((PACK >> (2 * i)) & 3) == ACT_SIGMOID) return false;
+  return true;
+}
+
+// FOLD: biases enter the forward MFMAs through the constant-1 input slot
+// (row 31 of L1, row 15 of L2..L4) instead of an fp32 accumulator init.
+template <bool FOLD>
 __device__ __forceinline__ void load_frags(const AEArgs& a, int c, int g, Frags& F, bool bwd) {
   const float* P = a.params;
 #pragma unroll
@@ -67,55 +95,67 @@ __device__ __forceinline__ void load_frags(const AEArgs& a, int c, int g, Frags&
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int in = 16 * s + k;
-      F.w1t[s][j] = 0;
-      float v = (in < a.D && c < a.n1) ? P[OFF1 + in * 16 + c] : 0.f;
-      F.w1t[s][j] = __builtin_bit_cast(short, (__bf16)v);
+      const bool row_ok = in < a.D || (FOLD && in == 31);
+      F.w1t[s][j] = bfbits((row_ok && c < a.n1) ? P[OFF1 + in * 16 + c] : 0.f);
     }
-    F.w2t[j] = __builtin_bit_cast(short, (__bf16)((k < a.n1 && c < a.n2) ? P[OFF2 + k * 16 + c] : 0.f));
-    F.w3t[j] = __builtin_bit_cast(short, (__bf16)((k < a.n2 && c < a.n3) ? P[OFF3 + k * 16 + c] : 0.f));
+    const bool k15 = FOLD && k == 15;
+    F.w2t[j] = bfbits(((k < a.n1 || k15) && c < a.n2) ? P[OFF2 + k * 16 + c] : 0.f);
+    F.w3t[j] = bfbits(((k < a.n2 || k15) && c < a.n3) ? P[OFF3 + k * 16 + c] : 0.f);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int out = 16 * t + c;
-      F.w4t[t][j] = __builtin_bit_cast(short, (__bf16)((k < a.n3 && out < a.D) ? P[OFF4 + k * 32 + out] : 0.f));
+      F.w4t[t][j] = bfbits(((k < a.n3 || k15) && out < a.D) ? P[OFF4 + k * 32 + out] : 0.f);
     }
     if (bwd) {
-      // backward: A[m = in = c][k = out]
+      // backward: A[m = in = c][k = out]; bias rows never propagate gradients
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int out = 16 * s + k;
-        F.w4[s][j] = __builtin_bit_cast(short, (__bf16)((c < a.n3 && out < a.D) ? P[OFF4 + c * 32 + out] : 0.f));
+        F.w4[s][j] = bfbits((c < a.n3 && out < a.D) ? P[OFF4 + c * 32 + out] : 0.f);
       }
-      F.w3[j] = __builtin_bit_cast(short, (__bf16)((c < a.n2 && k < a.n3) ? P[OFF3 + c * 16 + k] : 0.f));
-      F.w2[j] = __builtin_bit_cast(short, (__bf16)((c < a.n1 && k < a.n2) ? P[OFF2 + c * 16 + k] : 0.f));
+      F.w3[j] = bfbits((c < a.n2 && k < a.n3) ? P[OFF3 + c * 16 + k] : 0.f);
+      F.w2[j] = bfbits((c < a.n1 && k < a.n2) ? P[OFF2 + c * 16 + k] : 0.f);
     }
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int f = 4 * g + i;
-    F.b1[i] = f < a.n1 ? P[OFF1 + 31 * 16 + f] : 0.f;
-    F.b2[i] = f < a.n2 ? P[OFF2 + 15 * 16 + f] : 0.f;
-    F.b3[i] = f < a.n3 ? P[OFF3 + 15 * 16 + f] : 0.f;
+    F.b1[i] = (!FOLD && f < a.n1) ? P[OFF1 + 31 * 16 + f] : 0.f;
+    F.b2[i] = (!FOLD && f < a.n2) ? P[OFF2 + 15 * 16 + f] : 0.f;
+    F.b3[i] = (!FOLD && f < a.n3) ? P[OFF3 + 15 * 16 + f] : 0.f;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) F.b4[t][i] = (16 * t + f) < a.D ? P[OFF4 + 15 * 32 + 16 * t + f] : 0.f;
+    for (int t = 0; t < 2; ++t) {
+      const int ft = 16 * t + f;
+      F.b4[t][i] = (!FOLD && ft < a.D) ? P[OFF4 + 15 * 32 + ft] : 0.f;
+      F.sc[t][i] = ft < a.D ? (a.scale ? a.scale[ft] : 1.0f) : 0.f;
+      F.sh[t][i] = (ft < a.D && a.scale) ? a.shift[ft] : 0.f;
+    }
   }
 }
 
-// Load one 16-row tile in the B-operand layout: lane (c, g) holds features
-// 16s + 4g + j of row r0 + c.  Normalisation (normalize_fn, cardata-v3.py:78-168)
-// is fused here as a per-column affine map.
-__device__ __forceinline__ void load_x(const AEArgs& a, int64_t r, bool valid, int g, f32x4 xf[2]) {
-  const float* row = a.x + r * a.ld;
+// Raw tile fetch in the B-operand layout: lane (c, g) holds features 16s + 4g + j
+// of row r.  Branch-free: column indices are clamped into the row and the
+// out-of-range features are zeroed by the caller's loop-invariant mask (the
+// normaliser's scale/shift are 0 there), so no load sits behind a divergent
+// branch.  Rows r >= n are clamped to row n-1 (only the ragged tail has them).
+// VEC: 8-byte loads of feature pairs (row stride and D even, 8-byte aligned base).
+template <bool VEC>
+__device__ __forceinline__ void fetch_x(const AEArgs& a, int64_t r, int g, f32x4 xr[2]) {
+  const int64_t rr = r < a.n ? r : a.n - 1;
+  const float* row = a.x + rr * a.ld;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
+    if constexpr (VEC) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int f = 16 * s + 4 * g + j;
-      float v = 0.f;
-      if (valid && f < a.D) {
-        v = row[f];
-        if (a.scale) v = fmaf(v, a.scale[f], a.shift[f]);
+      for (int p = 0; p < 2; ++p) {
+        const int f = min(16 * s + 4 * g + 2 * p, a.D - 2);
+        const float2 v = *reinterpret_cast<const float2*>(row + f);
+        xr[s][2 * p] = v.x;
+        xr[s][2 * p + 1] = v.y;
       }
-      xf[s][j] = v;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xr[s][j] = row[min(16 * s + 4 * g + j, a.D - 1)];
     }
   }
 }
@@ -131,6 +171,7 @@ __device__ __forceinline__ f32x4 activate_pad(int act, f32x4 z, int n, int g) {
   return h;
 }
 
+template <int PACK>
 __device__ __forceinline__ void forward_tile(const AEArgs& a, const Frags& F, int g, const f32x4 xf[2],
                                              bf16x4& xb0, bf16x4& xb1, f32x4& h1, f32x4& h2, f32x4& h3,
                                              bf16x4& h1b, bf16x4& h2b, bf16x4& h3b, f32x4 y[2]) {
@@ -140,21 +181,22 @@ __device__ __forceinline__ void forward_tile(const AEArgs& a, const Frags& F, in
   xb1 = pack4(x1);
   f32x4 z1 = mfma16(F.w1t[0], xb0, F.b1);
   z1 = mfma16(F.w1t[1], xb1, z1);
-  h1 = activate_pad(a.a1, z1, a.n1, g);
+  h1 = activate_pad(act_of<PACK>(a, 0), z1, a.n1, g);
   h1b = pack4(h1);
   f32x4 z2 = mfma16(F.w2t, h1b, F.b2);
-  h2 = activate_pad(a.a2, z2, a.n2, g);
+  h2 = activate_pad(act_of<PACK>(a, 1), z2, a.n2, g);
   h2b = pack4(h2);
   f32x4 z3 = mfma16(F.w3t, h2b, F.b3);
-  h3 = activate_pad(a.a3, z3, a.n3, g);
+  h3 = activate_pad(act_of<PACK>(a, 2), z3, a.n3, g);
   h3b = pack4(h3);
+  const int a4 = act_of<PACK>(a, 3);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     f32x4 z4 = mfma16(F.w4t[t], h3b, F.b4[t]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = 16 * t + 4 * g + i;
-      y[t][i] = f < a.D ? act_fwd(a.a4, z4[i]) : 0.f;
+      y[t][i] = f < a.D ? act_fwd(a4, z4[i]) : 0.f;
     }
   }
 }
@@ -182,7 +224,153 @@ __device__ __forceinline__ int row_argmax(const f32x4 v[2], int D, int g) {
   return bi;
 }
 
+// Branch-free argmax over the 8 features a lane holds + its 3 partner lanes
+// (row r = lane & 15 is spread over lane groups g = 0..3).  Ties -> lowest index
+// (tf.argmax).  `pn` is 0 for real features and -inf for padded ones.
+__device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], const f32x4 pn[2], int g, int lane) {
+  float vv[8];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) vv[4 * t + i] = v[t][i] + pn[t][i];
+  float m = fmaxf(fmaxf(fmaxf(vv[0], vv[1]), fmaxf(vv[2], vv[3])), fmaxf(fmaxf(vv[4], vv[5]), fmaxf(vv[6], vv[7])));
+  m = fmaxf(m, xor16(m, lane));
+  m = fmaxf(m, xor32(m, lane));
+  int idx = 64;
+#pragma unroll
+  for (int q = 7; q >= 0; --q) {
+    const int f = 16 * (q >> 2) + 4 * g + (q & 3);
+    idx = (vv[q] == m) ? f : idx;
+  }
+  idx = min(idx, xor16i(idx, lane));
+  idx = min(idx, xor32i(idx, lane));
+  return idx;
+}
+
+// One 16-row tile: forward, loss, metrics, backward, weight-gradient MFMAs.
+// FAST (zero-preserving activations): no per-feature masks -- padded features
+// stay exactly 0 because their weights are 0 and act(0) = 0; only the bias slot
+// is set.  TAIL: rows beyond n are masked (only the last tile of a launch).
+template <int PACK, bool FAST, bool TAIL>
+__device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, const bf16x4 I, int c, int g, int lane,
+                                           bool valid, const f32x4 xf[2], const f32x4 pn[2], float pad1,
+                                           f32x4 acc1[2], f32x4& acc2, f32x4& acc3, f32x4 acc4[2], float& sq,
+                                           float& ab, float& corr, float& rows) {
+  const int a1 = act_of<PACK>(a, 0), a2 = act_of<PACK>(a, 1), a3 = act_of<PACK>(a, 2), a4 = act_of<PACK>(a, 3);
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const float two_over_d = 2.0f / (float)a.D;
+  const bool pad_lane = (g == 3);
+  const bool vm = !TAIL || valid;
+
+  bf16x4 xb0, xb1, h1b, h2b, h3b;
+  f32x4 h1, h2, h3, y[2];
+  if constexpr (FAST) {
+    // padded features are exactly 0 (zero weights, act(0) = 0); feature 15 of
+    // each hidden layer / 31 of the input is the constant-1 bias slot: +pad1.
+    f32x4 x1 = xf[1];
+    x1[3] += pad1;
+    xb0 = pack4(xf[0]);
+    xb1 = pack4(x1);
+    f32x4 z1 = mfma16(F.w1t[0], xb0, zero4);
+    z1 = mfma16(F.w1t[1], xb1, z1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h1[i] = act_fwd(a1, z1[i]);
+    h1[3] += pad1;
+    h1b = pack4(h1);
+    const f32x4 z2 = mfma16(F.w2t, h1b, zero4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h2[i] = act_fwd(a2, z2[i]);
+    h2[3] += pad1;
+    h2b = pack4(h2);
+    const f32x4 z3 = mfma16(F.w3t, h2b, zero4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h3[i] = act_fwd(a3, z3[i]);
+    h3[3] += pad1;
+    h3b = pack4(h3);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const f32x4 z4 = mfma16(F.w4t[t], h3b, zero4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) y[t][i] = act_fwd(a4, z4[i]);
+    }
+  } else {
+    forward_tile<PACK>(a, F, g, xf, xb0, xb1, h1, h2, h3, h1b, h2b, h3b, y);
+  }
+
+  // MSE loss + dL/dz4 (sum-scaled; the 1/B factor is applied in the Adam kernel)
+  f32x4 dz4[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float e = y[t][i] - xf[t][i];
+      if constexpr (!FAST) e = (16 * t + 4 * g + i) < a.D ? e : 0.f;
+      if constexpr (TAIL) e = vm ? e : 0.f;
+      sq = fmaf(e, e, sq);
+      dz4[t][i] = act_grad(a4, y[t][i], two_over_d * e);
+    }
+  if (a.want_acc) {
+    const int iy = row_argmax_fast(y, pn, g, lane);
+    const int ix = row_argmax_fast(xf, pn, g, lane);
+    corr += (g == 0 && vm && iy == ix) ? 1.f : 0.f;
+  }
+  rows += (g == 0 && vm) ? 1.f : 0.f;
+
+  // backward through the layers (feature-major, in registers)
+  const bf16x4 dz4b0 = pack4(dz4[0]), dz4b1 = pack4(dz4[1]);
+  f32x4 dh3 = mfma16(F.w4[0], dz4b0, zero4);
+  dh3 = mfma16(F.w4[1], dz4b1, dh3);
+  f32x4 dz3, dz2, dz1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    dz3[i] = act_grad(a3, h3[i], dh3[i]);
+    if constexpr (!FAST) dz3[i] = (4 * g + i) < a.n3 ? dz3[i] : 0.f;
+  }
+  const bf16x4 dz3b = pack4(dz3);
+  const f32x4 dh2 = mfma16(F.w3, dz3b, zero4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    dz2[i] = act_grad(a2, h2[i], dh2[i]);
+    if constexpr (!FAST) dz2[i] = (4 * g + i) < a.n2 ? dz2[i] : 0.f;
+  }
+  const bf16x4 dz2b = pack4(dz2);
+  const f32x4 dh1 = mfma16(F.w2, dz2b, zero4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float hv = h1[i];
+    const bool real = FAST ? !(i == 3 && pad_lane) : ((4 * g + i) < a.n1);
+    const bool use = real && vm;
+    ab += use ? fabsf(hv) : 0.f;
+    // Keras L1 activity regulariser gradient: l1 * sign(h1) (sign(0) = 0)
+    const float sgn = (use && hv != 0.f) ? __builtin_copysignf(1.0f, hv) : 0.f;
+    float d = act_grad(a1, hv, fmaf(a.l1, sgn, dh1[i]));
+    if constexpr (!FAST) d = real ? d : 0.f;
+    dz1[i] = d;
+  }
+  const bf16x4 dz1b = pack4(dz1);
+
+  // weight gradients: contraction over the 16 rows of the tile
+  const bf16x4 xr0 = pack4(transpose_tile(xb0, I));
+  const bf16x4 xr1 = pack4(transpose_tile(xb1, I));
+  const bf16x4 dz1r = pack4(transpose_tile(dz1b, I));
+  acc1[0] = mfma16(xr0, dz1r, acc1[0]);
+  acc1[1] = mfma16(xr1, dz1r, acc1[1]);
+  const bf16x4 h1r = pack4(transpose_tile(h1b, I));
+  const bf16x4 dz2r = pack4(transpose_tile(dz2b, I));
+  acc2 = mfma16(h1r, dz2r, acc2);
+  const bf16x4 h2r = pack4(transpose_tile(h2b, I));
+  const bf16x4 dz3r = pack4(transpose_tile(dz3b, I));
+  acc3 = mfma16(h2r, dz3r, acc3);
+  const bf16x4 h3r = pack4(transpose_tile(h3b, I));
+  const bf16x4 dz4r0 = pack4(transpose_tile(dz4b0, I));
+  const bf16x4 dz4r1 = pack4(transpose_tile(dz4b1, I));
+  acc4[0] = mfma16(h3r, dz4r0, acc4[0]);
+  acc4[1] = mfma16(h3r, dz4r1, acc4[1]);
+}
+
+template <int PACK, bool VEC>
 __global__ __launch_bounds__(WAVES * 64) void ae_train_kernel(AEArgs a) {
+  constexpr bool FAST = zero_preserving<PACK>();
   __shared__ float red[WAVES][NSLOT];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -191,95 +379,45 @@ __global__ __launch_bounds__(WAVES * 64) void ae_train_kernel(AEArgs a) {
   if (a.iter && blockIdx.x == 0 && threadIdx.x == 0) a.iter[0] += 1;
 
   Frags F;
-  load_frags(a, c, g, F, true);
+  load_frags<FAST>(a, c, g, F, true);
   const bf16x4 I = identity_b(c, g);
+  const float pad1 = (g == 3) ? 1.0f : 0.0f;
+  f32x4 pn[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pn[t][i] = (16 * t + 4 * g + i) < a.D ? 0.f : -INFINITY;
 
   f32x4 acc1[2], acc2, acc3, acc4[2];
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
   acc1[0] = acc1[1] = acc2 = acc3 = acc4[0] = acc4[1] = zero4;
   float sq = 0.f, ab = 0.f, corr = 0.f, rows = 0.f;
-  const float two_over_d = 2.0f / (float)a.D;
 
-  const int64_t ntiles = (a.n + 15) >> 4;
+  const int64_t nfull = a.n >> 4;
   const int64_t stride = (int64_t)gridDim.x * WAVES;
-  for (int64_t t = (int64_t)blockIdx.x * WAVES + wid; t < ntiles; t += stride) {
-    const int64_t r = t * 16 + c;
+  const int64_t first = (int64_t)blockIdx.x * WAVES + wid;
+  f32x4 xnext[2];
+  if (first < nfull) fetch_x<VEC>(a, first * 16 + c, g, xnext);
+  for (int64_t t = first; t < nfull; t += stride) {
+    f32x4 xf[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xnext[s][j], F.sc[s][j], F.sh[s][j]);
+    if (t + stride < nfull) fetch_x<VEC>(a, (t + stride) * 16 + c, g, xnext);  // prefetch
+    train_tile<PACK, FAST, false>(a, F, I, c, g, lane, true, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
+  }
+  // ragged last tile: handled by the wave that would own tile index nfull
+  if ((a.n & 15) && first == nfull % stride) {
+    const int64_t r = nfull * 16 + c;
     const bool valid = r < a.n;
     f32x4 xf[2];
-    load_x(a, r, valid, g, xf);
-
-    bf16x4 xb0, xb1, h1b, h2b, h3b;
-    f32x4 h1, h2, h3, y[2];
-    forward_tile(a, F, g, xf, xb0, xb1, h1, h2, h3, h1b, h2b, h3b, y);
-
-    // MSE loss + dL/dz4 (sum-scaled; the 1/B factor is applied in the Adam kernel)
-    f32x4 dz4[2];
+    fetch_x<VEC>(a, r, g, xf);
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int f = 16 * tt + 4 * g + i;
-        float d = 0.f;
-        if (valid && f < a.D) {
-          const float e = y[tt][i] - xf[tt][i];
-          sq = fmaf(e, e, sq);
-          d = two_over_d * e * act_bwd(a.a4, y[tt][i]);
-        }
-        dz4[tt][i] = d;
-      }
-    if (a.want_acc) {
-      const int iy = row_argmax(y, a.D, g);
-      const int ix = row_argmax(xf, a.D, g);
-      if (g == 0 && valid && iy == ix) corr += 1.f;
-    }
-    if (g == 0 && valid) rows += 1.f;
-
-    // backward through the layers (feature-major, in registers)
-    const bf16x4 dz4b0 = pack4(dz4[0]), dz4b1 = pack4(dz4[1]);
-    f32x4 dh3 = mfma16(F.w4[0], dz4b0, zero4);
-    dh3 = mfma16(F.w4[1], dz4b1, dh3);
-    f32x4 dz3, dz2, dz1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dz3[i] = (4 * g + i) < a.n3 ? dh3[i] * act_bwd(a.a3, h3[i]) : 0.f;
-    const bf16x4 dz3b = pack4(dz3);
-    const f32x4 dh2 = mfma16(F.w3, dz3b, zero4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dz2[i] = (4 * g + i) < a.n2 ? dh2[i] * act_bwd(a.a2, h2[i]) : 0.f;
-    const bf16x4 dz2b = pack4(dz2);
-    const f32x4 dh1 = mfma16(F.w2, dz2b, zero4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float d = 0.f;
-      if ((4 * g + i) < a.n1) {
-        float gsum = dh1[i];
-        if (valid) {
-          const float hv = h1[i];
-          ab += fabsf(hv);
-          gsum += a.l1 * (hv > 0.f ? 1.f : (hv < 0.f ? -1.f : 0.f));
-        }
-        d = gsum * act_bwd(a.a1, h1[i]);
-      }
-      dz1[i] = d;
-    }
-    const bf16x4 dz1b = pack4(dz1);
-
-    // weight gradients: contraction over the 16 rows of the tile
-    const bf16x4 xr0 = pack4(transpose_tile(xb0, I));
-    const bf16x4 xr1 = pack4(transpose_tile(xb1, I));
-    const bf16x4 dz1r = pack4(transpose_tile(dz1b, I));
-    acc1[0] = mfma16(xr0, dz1r, acc1[0]);
-    acc1[1] = mfma16(xr1, dz1r, acc1[1]);
-    const bf16x4 h1r = pack4(transpose_tile(h1b, I));
-    const bf16x4 dz2r = pack4(transpose_tile(dz2b, I));
-    acc2 = mfma16(h1r, dz2r, acc2);
-    const bf16x4 h2r = pack4(transpose_tile(h2b, I));
-    const bf16x4 dz3r = pack4(transpose_tile(dz3b, I));
-    acc3 = mfma16(h2r, dz3r, acc3);
-    const bf16x4 h3r = pack4(transpose_tile(h3b, I));
-    const bf16x4 dz4r0 = pack4(transpose_tile(dz4b0, I));
-    const bf16x4 dz4r1 = pack4(transpose_tile(dz4b1, I));
-    acc4[0] = mfma16(h3r, dz4r0, acc4[0]);
-    acc4[1] = mfma16(h3r, dz4r1, acc4[1]);
+      for (int j = 0; j < 4; ++j) xf[s][j] = valid ? fmaf(xf[s][j], F.sc[s][j], F.sh[s][j]) : 0.f;
+    train_tile<PACK, FAST, true>(a, F, I, c, g, lane, valid, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
   }
 
   // per-wave slab in LDS (every slot written exactly once per wave)
@@ -329,6 +467,7 @@ struct FwdArgs {
   int a1, a2, a3, a4;
 };
 
+template <int PACK, bool VEC>
 __global__ __launch_bounds__(WAVES * 64) void ae_forward_kernel(FwdArgs fa) {
   AEArgs a{};
   a.x = fa.x; a.n = fa.n; a.ld = fa.ld; a.scale = fa.scale; a.shift = fa.shift; a.params = fa.params;
@@ -338,7 +477,7 @@ __global__ __launch_bounds__(WAVES * 64) void ae_forward_kernel(FwdArgs fa) {
   const int wid = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
   Frags F;
-  load_frags(a, c, g, F, false);
+  load_frags<false>(a, c, g, F, false);
   const int64_t ntiles = (a.n + 15) >> 4;
   const int64_t stride = (int64_t)gridDim.x * WAVES;
   const float inv_d = 1.0f / (float)a.D;
@@ -346,10 +485,14 @@ __global__ __launch_bounds__(WAVES * 64) void ae_forward_kernel(FwdArgs fa) {
     const int64_t r = t * 16 + c;
     const bool valid = r < a.n;
     f32x4 xf[2];
-    load_x(a, r, valid, g, xf);
+    fetch_x<VEC>(a, r, g, xf);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xf[s][j], F.sc[s][j], F.sh[s][j]);
     bf16x4 xb0, xb1, h1b, h2b, h3b;
     f32x4 h1, h2, h3, y[2];
-    forward_tile(a, F, g, xf, xb0, xb1, h1, h2, h3, h1b, h2b, h3b, y);
+    forward_tile<PACK>(a, F, g, xf, xb0, xb1, h1, h2, h3, h1b, h2b, h3b, y);
     float se = 0.f;
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
@@ -384,38 +527,12 @@ struct AdamHP {
 
 enum : int { RA_WRITE_GRAD = 1, RA_ADAM = 2, RA_METRICS = 4 };
 
-__global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restrict__ partials, int G, int S,
-                                                          int nparam, float* grad_out, float* params, float* m,
-                                                          float* v, const int64_t* iter, AdamHP hp, float gscale,
-                                                          float* metrics_acc, int flags) {
-  __shared__ float red[16][17];
-  const int sl = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const int slot = blockIdx.x * 16 + sl;
-  float acc = 0.f;
-  if (slot < S) {
-    int gi = grp;
-    for (; gi + 48 < G; gi += 64) {
-      const float p0 = partials[(int64_t)gi * S + slot];
-      const float p1 = partials[(int64_t)(gi + 16) * S + slot];
-      const float p2 = partials[(int64_t)(gi + 32) * S + slot];
-      const float p3 = partials[(int64_t)(gi + 48) * S + slot];
-      acc += (p0 + p1) + (p2 + p3);
-    }
-    for (; gi < G; gi += 16) acc += partials[(int64_t)gi * S + slot];
-  }
-  red[grp][sl] = acc;
-  __syncthreads();
-  if (grp != 0 || slot >= S) return;
-  float tot = 0.f;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) tot += red[k][sl];
+__device__ __forceinline__ void adam_one(float tot, int slot, int nparam, float* grad_out, float* params, float* m,
+                                         float* v, float lr_t, const AdamHP& hp, float gscale, float* metrics_acc,
+                                         int flags) {
   if (flags & RA_WRITE_GRAD) grad_out[slot] = tot;
   if (slot < nparam) {
     if (flags & RA_ADAM) {
-      const float t = (float)iter[0];
-      const float bc1 = 1.0f - powf(hp.beta1, t);
-      const float bc2 = 1.0f - powf(hp.beta2, t);
-      const float lr_t = hp.lr * sqrtf(bc2) / bc1;
       const float gr = tot * gscale;
       const float mm = hp.beta1 * m[slot] + (1.0f - hp.beta1) * gr;
       const float vv = hp.beta2 * v[slot] + (1.0f - hp.beta2) * gr * gr;
@@ -426,6 +543,46 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
   } else if ((flags & RA_METRICS) && metrics_acc) {
     metrics_acc[slot - nparam] += tot;
   }
+}
+
+// Block = 16 groups x 16 float4 slot-quads.  Each thread sums its quad over
+// G / 16 slabs with 8 independent 16-byte loads in flight, then the 16 groups
+// combine in LDS in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restrict__ partials, int G, int S,
+                                                          int nparam, float* grad_out, float* params, float* m,
+                                                          float* v, const int64_t* iter, AdamHP hp, float gscale,
+                                                          float* metrics_acc, int flags) {
+  __shared__ f32x4 red[16][16];
+  const int q = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int slot0 = (blockIdx.x * 16 + q) * 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (slot0 < S) {
+    for (int gi = grp; gi < G; gi += 16 * 8) {
+      f32x4 vals[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int idx = gi + 16 * u;
+        vals[u] = idx < G ? *reinterpret_cast<const f32x4*>(partials + (int64_t)idx * S + slot0)
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += vals[u];
+    }
+  }
+  red[grp][q] = acc;
+  __syncthreads();
+  if (grp != 0 || slot0 >= S) return;
+  f32x4 tot = red[0][q];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) tot += red[k][q];
+  float lr_t = 0.f;
+  if (flags & RA_ADAM) {
+    const float t = (float)iter[0];
+    lr_t = hp.lr * sqrtf(1.0f - powf(hp.beta2, t)) / (1.0f - powf(hp.beta1, t));
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    adam_one(tot[e], slot0 + e, nparam, grad_out, params, m, v, lr_t, hp, gscale, metrics_acc, flags);
 }
 }  // namespace
 
@@ -455,7 +612,15 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
   a.D = dims[0]; a.n1 = dims[1]; a.n2 = dims[2]; a.n3 = dims[3];
   a.a1 = acts[0]; a.a2 = acts[1]; a.a3 = acts[2]; a.a4 = acts[3];
   a.l1 = l1; a.want_acc = want_acc;
-  hipLaunchKernelGGL(ae_train_kernel, dim3(grid), dim3(WAVES * 64), 0, stream, a);
+  const bool vec = ((ld & 1) == 0) && ((dims[0] & 1) == 0) && dims[0] >= 2 &&
+                   ((reinterpret_cast<uintptr_t>(x) & 7) == 0);
+  const int pack = acts[0] | (acts[1] << 2) | (acts[2] << 4) | (acts[3] << 6);
+  if (pack == PACK_REF) {
+    if (vec) hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
+    else hipLaunchKernelGGL((ae_train_kernel<PACK_REF, false>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL((ae_train_kernel<PACK_DYN, false>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
+  }
   return hipGetLastError();
 }
 
@@ -468,7 +633,15 @@ hipError_t ae_forward_launch(const float* x, int64_t n, int64_t ld, const float*
   a.D = dims[0]; a.n1 = dims[1]; a.n2 = dims[2]; a.n3 = dims[3];
   a.a1 = acts[0]; a.a2 = acts[1]; a.a3 = acts[2]; a.a4 = acts[3];
   const int grid = ae_train_grid(n, max_blocks);
-  hipLaunchKernelGGL(ae_forward_kernel, dim3(grid), dim3(WAVES * 64), 0, stream, a);
+  const bool vec = ((ld & 1) == 0) && ((dims[0] & 1) == 0) && dims[0] >= 2 &&
+                   ((reinterpret_cast<uintptr_t>(x) & 7) == 0);
+  const int pack = acts[0] | (acts[1] << 2) | (acts[2] << 4) | (acts[3] << 6);
+  if (pack == PACK_REF) {
+    if (vec) hipLaunchKernelGGL((ae_forward_kernel<PACK_REF, true>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
+    else hipLaunchKernelGGL((ae_forward_kernel<PACK_REF, false>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL((ae_forward_kernel<PACK_DYN, false>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
+  }
   return hipGetLastError();
 }
 
@@ -476,7 +649,8 @@ hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, f
                               float* m, float* v, const int64_t* iter, float lr, float beta1, float beta2, float eps,
                               float gscale, float* metrics_acc, int flags, hipStream_t stream) {
   AdamHP hp{lr, beta1, beta2, eps};
-  const int grid = (S + 15) / 16;
+  if (S % 4 != 0) return hipErrorInvalidValue;
+  const int grid = (S / 4 + 15) / 16;
   hipLaunchKernelGGL(reduce_adam_kernel, dim3(grid), dim3(256), 0, stream, partials, G, S, nparam, grad_out, params,
                      m, v, iter, hp, gscale, metrics_acc, flags);
   return hipGetLastError();

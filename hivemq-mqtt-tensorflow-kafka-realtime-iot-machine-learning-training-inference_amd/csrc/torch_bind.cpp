@@ -125,6 +125,14 @@ void ae_forward(const at::Tensor& x, const c10::optional<at::Tensor>& scale, con
                                        (float)threshold, d, a, (int)max_blocks, cur_stream(x)));
 }
 
+at::Tensor lane_xor_probe(const at::Tensor& like) {
+  TORCH_CHECK(like.is_cuda(), "needs a device tensor for placement");
+  c10::hip::HIPGuard guard(like.device().index());
+  auto out = at::empty({128}, like.options().dtype(at::kFloat));
+  SML_CHECK_HIP(sml::lane_xor_probe_launch(out.data_ptr<float>(), cur_stream(like)));
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -140,6 +148,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("S"), py::arg("nparam"), py::arg("grad_out"), py::arg("params"), py::arg("m"), py::arg("v"),
         py::arg("iter"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("gscale"),
         py::arg("metrics"), py::arg("flags"));
+  m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),
         py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("recon"), py::arg("score"), py::arg("flag"),
         py::arg("threshold"), py::arg("dims"), py::arg("acts"), py::arg("max_blocks"));

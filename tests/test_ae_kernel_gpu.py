@@ -47,29 +47,42 @@ def test_gradients_match_torch(cuda_device, D, n):
 
 
 def test_training_trajectory_matches_torch(cuda_device):
+    """Adam after a few steps: bf16 MFMA run vs fp32 torch run of the same stream.
+
+    Adam's early steps are ~lr*sign(g) per parameter, so parameters whose
+    gradient is ~0 can legitimately differ by up to 2*lr*steps between a bf16
+    and an fp32 run; we bound the bulk (99th percentile) tightly, the max by
+    that envelope, and the loss trajectory.
+    """
     spec = AESpec()
     w = _weights(spec, seed=3)
     scale, shift = normalize_affine()
     rng = np.random.default_rng(7)
-    raw =(rng.uniform(0, 1, size=(4 * 512, 18)) * 40).astype(np.float32)
+    steps, bs = 8, 512
+    raw = (rng.uniform(0, 1, size=(steps * bs, 18)) * 40).astype(np.float32)
     xn = (raw * scale + shift).astype(np.float32)
     fused = FusedAE(spec, w, cuda_device, max_blocks=32, scale=scale, shift=shift)
     ref_w = [torch.tensor(a, requires_grad=True) for a in w]
     opt = KerasAdam(ref_w)
     xr_dev = torch.from_numpy(raw).to(cuda_device)
-    for s in range(4):
-        fused.step(xr_dev[s * 512:(s + 1) * 512])
-        xb = torch.from_numpy(xn[s * 512:(s + 1) * 512])
+    ref_losses = []
+    for s in range(steps):
+        fused.step(xr_dev[s * bs:(s + 1) * bs])
+        xb = torch.from_numpy(xn[s * bs:(s + 1) * bs])
         loss, _, _ = ae_loss_torch(xb, ref_w, spec.activations, spec.activity_l1)
+        ref_losses.append(float(loss) * bs)
         opt.apply(torch.autograd.grad(loss, ref_w))
     torch.cuda.synchronize()
     got = fused.get_weights()
-    assert int(fused.iter.item()) == 4
-    for a, b in zip(got, ref_w):
-        # Adam steps are ~lr-sized; compare the parameter deltas
-        assert np.max(np.abs(a - b.detach().numpy())) < 2e-4
+    assert int(fused.iter.item()) == steps
+    diffs = np.concatenate([np.abs(a - b.detach().numpy()).ravel() for a, b in zip(got, ref_w)])
+    assert np.median(diffs) < 1e-4, np.median(diffs)
+    assert np.percentile(diffs, 99) < 1e-3, np.percentile(diffs, 99)
+    assert diffs.max() <= 2 * 1e-3 * steps
     m = fused.read_metrics()
-    assert m["rows"] == 4 * 512
+    assert m["rows"] == steps * bs
+    ref_loss = sum(ref_losses) / (steps * bs)
+    assert abs(m["loss"] - ref_loss) / ref_loss < 2e-2, (m["loss"], ref_loss)
 
 
 def test_forward_and_score(cuda_device):
@@ -96,3 +109,29 @@ def test_pack_roundtrip_on_device(cuda_device):
     for a, b in zip(fused.get_weights(), w):
         np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(unpack_image(pack_image(w), spec)[0], w[0])
+
+
+def test_lane_exchange_helpers(cuda_device):
+    from streamml.ops import load_c
+    out = load_c().lane_xor_probe(torch.empty(1, device=cuda_device)).cpu().numpy()
+    lanes = np.arange(64)
+    np.testing.assert_array_equal(out[:64], lanes ^ 16)
+    np.testing.assert_array_equal(out[64:], lanes ^ 32)
+
+
+def test_accuracy_metric_exact(cuda_device):
+    """Rows with a clear argmax: categorical accuracy must match exactly."""
+    spec = AESpec()
+    w = _weights(spec, seed=21)
+    n = 512
+    rng = np.random.default_rng(9)
+    x = rng.uniform(-1, 1, size=(n, 18)).astype(np.float32)
+    fused = FusedAE(spec, w, cuda_device)
+    _, metr = fused.gradients(torch.from_numpy(x).to(cuda_device))
+    y, _ = ae_forward_torch(torch.from_numpy(x), [torch.from_numpy(a) for a in w], spec.activations)
+    y = y.numpy()
+    ysorted = np.sort(y, axis=1)
+    clear = (ysorted[:, -1] - ysorted[:, -2]) > 2e-2
+    ref = (np.argmax(y, 1) == np.argmax(x, 1))
+    # rows without a clear winner may legitimately flip under bf16
+    assert abs(metr[2] - ref.sum()) <= (~clear).sum()

@@ -32,6 +32,12 @@ for s in $STEPS; do
     prof)
       (cd /tmp && step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
           python3 "$ROOT/bench.py" --steps 50 --warmup 5 --infer-events 100 ${BENCH_ARGS:-}) ;;
+    sweep) step ae_sweep 600 python tools/ae_sweep.py ${SWEEP_ARGS:-} ;;
+    counters) step counters 120 rocprofv3 -L ;;
+    pmc)
+      (cd /tmp && step pmc 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc" -o run \
+          --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU \
+          SQ_INSTS_LDS SQ_INSTS_VMEM_RD -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --infer-events 0) ;;
     *) echo "unknown step $s" ;;
   esac
 done
