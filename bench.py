@@ -38,11 +38,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--batch-per-gpu", type=int, default=1 << 20)
-    p.add_argument("--dataset-rows", type=int, default=1 << 24, help="rows resident per GPU")
+    p.add_argument("--batch-per-gpu", type=int, default=1 << 22)
+    p.add_argument("--dataset-rows", type=int, default=1 << 25, help="rows resident per GPU (ring)")
     p.add_argument("--max-blocks", type=int, default=1024)
     p.add_argument("--infer-events", type=int, default=1000)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--graph", action="store_true",
+                   help="replay one captured hipGraph step (replay floor ~10 us; eager is faster at these sizes)")
     return p.parse_args()
 
 
@@ -101,10 +103,37 @@ def main():
     allreduce = dp.allreduce_sum_ if world > 1 else None
     gb = B * world
 
+    fused.attach_ring(data, B)
+
+    def eager_step():
+        fused.step_ring(global_batch=gb, allreduce=allreduce)
+
+    graph = None
+    if args.graph:
+        # warm up on a side stream, then capture ONE full step (train kernel,
+        # slab reduce, RCCL all-reduce, Adam + cursor advance) as a hipGraph
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                eager_step()
+        torch.cuda.current_stream().wait_stream(side)
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                eager_step()
+        except Exception as e:  # capture unsupported (e.g. collective) -> eager
+            if rank == 0:
+                print(f"[bench] graph capture failed ({e!r}); running eager", file=sys.stderr)
+            graph = None
+        torch.cuda.synchronize()
+
     def run(nsteps, start):
-        for s in range(start, start + nsteps):
-            i = s % nslices
-            fused.step(data[i * B:(i + 1) * B], global_batch=gb, allreduce=allreduce)
+        for _ in range(nsteps):
+            if graph is not None:
+                graph.replay()
+            else:
+                eager_step()
 
     run(args.warmup, 0)
     dp.barrier(device)
@@ -120,6 +149,7 @@ def main():
     p50 = p99 = None
     if rank == 0:
         p50, p99 = measure_infer_p50(fused, device, args.infer_events)
+    del nslices
     rows_per_s = gb * args.steps / elapsed
     if rank == 0:
         out = {
@@ -144,6 +174,7 @@ def main():
             },
             "p50_infer_us": p50,
             "p99_infer_us": p99,
+            "hip_graph": graph is not None,
             "final_epoch_loss": metrics["loss"],
             "final_accuracy": metrics["accuracy"],
         }

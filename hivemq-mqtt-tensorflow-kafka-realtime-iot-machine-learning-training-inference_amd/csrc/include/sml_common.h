@@ -121,6 +121,25 @@ __device__ __forceinline__ float xor32(float v, int lane) {
 __device__ __forceinline__ int xor16i(int v, int lane) { return __float_as_int(xor16(__int_as_float(v), lane)); }
 __device__ __forceinline__ int xor32i(int v, int lane) { return __float_as_int(xor32(__int_as_float(v), lane)); }
 
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+// 16x16 bf16 tile transpose through LDS (gfx950 ds_read_b64_tr_b16).
+// In : feature-major tile, lane (c, g) holds P[f = 4g+i][r = c], i = 0..3.
+// Out: row-major tile,     lane (c, g) holds P[f = c][r = 4g+q], q = 0..3,
+//      i.e. the MFMA A operand P^T[m = feature][k = row] / B operand
+//      P[k = row][n = feature] that a contraction over rows needs.
+// The wave-private 512-byte image is [r][f] (32-byte rows): the write is one
+// 8-byte ds_write per lane; the read is one ds_read_b64_tr_b16 per lane, lane
+// 4q+p of each 16-lane group addressing row 4g+q, columns 4p..4p+3.
+// LDS ops of one wave complete in order, so no wait is needed between the write
+// and the transposed read beyond the one the compiler places before the use.
+__device__ __forceinline__ bf16x4 lds_transpose(bf16x4 v, char* wave_scratch, int c, int g) {
+  lds_bf16x4* wr = (lds_bf16x4*)(wave_scratch + c * 32 + 8 * g);
+  *wr = v;
+  lds_bf16x4* rd = (lds_bf16x4*)(wave_scratch + (4 * g + (c >> 2)) * 32 + 8 * (c & 3));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(rd);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

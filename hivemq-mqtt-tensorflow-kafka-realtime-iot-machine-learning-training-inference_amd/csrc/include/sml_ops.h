@@ -11,14 +11,15 @@ int ae_nparam();
 int ae_waves_per_block();
 int ae_train_grid(int64_t n, int max_blocks);
 hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
-                           const float* params, float* partials, int64_t* iter, const int* dims, const int* acts,
-                           float l1, int want_acc, int grid, hipStream_t stream);
+                           const float* params, float* partials, int64_t* iter, const int64_t* cursor,
+                           const int* dims, const int* acts, float l1, int want_acc, int grid, hipStream_t stream);
 hipError_t ae_forward_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
                              const float* params, float* recon, float* score, uint8_t* flag, float threshold,
                              const int* dims, const int* acts, int max_blocks, hipStream_t stream);
 hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, float* grad_out, float* params,
                               float* m, float* v, const int64_t* iter, float lr, float beta1, float beta2, float eps,
-                              float gscale, float* metrics_acc, int flags, hipStream_t stream);
+                              float gscale, float* metrics_acc, int flags, int64_t* cursor, int64_t cursor_step,
+                              int64_t cursor_ring, hipStream_t stream);
 
 // ---- utilities (util.hip) ----
 hipError_t lane_xor_probe_launch(float* out, hipStream_t stream);

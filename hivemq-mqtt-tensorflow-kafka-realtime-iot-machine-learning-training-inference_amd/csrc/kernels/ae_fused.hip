@@ -46,6 +46,7 @@ struct AEArgs {
   const float* params;   // padded image
   float* partials;       // [grid][NSLOT]
   int64_t* iter;         // incremented by block 0 when non-null
+  const int64_t* cursor; // device ring cursor: rows start at x + cursor[0]*ld (null = 0)
   int D, n1, n2, n3;
   int a1, a2, a3, a4;
   float l1;
@@ -252,7 +253,7 @@ __device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], const f32x4 pn[
 // stay exactly 0 because their weights are 0 and act(0) = 0; only the bias slot
 // is set.  TAIL: rows beyond n are masked (only the last tile of a launch).
 template <int PACK, bool FAST, bool TAIL>
-__device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, const bf16x4 I, int c, int g, int lane,
+__device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char* scr, int c, int g, int lane,
                                            bool valid, const f32x4 xf[2], const f32x4 pn[2], float pad1,
                                            f32x4 acc1[2], f32x4& acc2, f32x4& acc3, f32x4 acc4[2], float& sq,
                                            float& ab, float& corr, float& rows) {
@@ -349,38 +350,44 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, cons
   }
   const bf16x4 dz1b = pack4(dz1);
 
-  // weight gradients: contraction over the 16 rows of the tile
-  const bf16x4 xr0 = pack4(transpose_tile(xb0, I));
-  const bf16x4 xr1 = pack4(transpose_tile(xb1, I));
-  const bf16x4 dz1r = pack4(transpose_tile(dz1b, I));
+  // weight gradients: contraction over the 16 rows of the tile (operands
+  // re-laid out rows-on-K through LDS transposed reads; 512 B per slot)
+  const bf16x4 xr0 = lds_transpose(xb0, scr + 0 * 512, c, g);
+  const bf16x4 xr1 = lds_transpose(xb1, scr + 1 * 512, c, g);
+  const bf16x4 dz1r = lds_transpose(dz1b, scr + 2 * 512, c, g);
+  const bf16x4 h1r = lds_transpose(h1b, scr + 3 * 512, c, g);
+  const bf16x4 dz2r = lds_transpose(dz2b, scr + 4 * 512, c, g);
+  const bf16x4 h2r = lds_transpose(h2b, scr + 5 * 512, c, g);
+  const bf16x4 dz3r = lds_transpose(dz3b, scr + 6 * 512, c, g);
+  const bf16x4 h3r = lds_transpose(h3b, scr + 7 * 512, c, g);
+  const bf16x4 dz4r0 = lds_transpose(dz4b0, scr + 8 * 512, c, g);
+  const bf16x4 dz4r1 = lds_transpose(dz4b1, scr + 9 * 512, c, g);
   acc1[0] = mfma16(xr0, dz1r, acc1[0]);
   acc1[1] = mfma16(xr1, dz1r, acc1[1]);
-  const bf16x4 h1r = pack4(transpose_tile(h1b, I));
-  const bf16x4 dz2r = pack4(transpose_tile(dz2b, I));
   acc2 = mfma16(h1r, dz2r, acc2);
-  const bf16x4 h2r = pack4(transpose_tile(h2b, I));
-  const bf16x4 dz3r = pack4(transpose_tile(dz3b, I));
   acc3 = mfma16(h2r, dz3r, acc3);
-  const bf16x4 h3r = pack4(transpose_tile(h3b, I));
-  const bf16x4 dz4r0 = pack4(transpose_tile(dz4b0, I));
-  const bf16x4 dz4r1 = pack4(transpose_tile(dz4b1, I));
   acc4[0] = mfma16(h3r, dz4r0, acc4[0]);
   acc4[1] = mfma16(h3r, dz4r1, acc4[1]);
 }
 
+// 3 waves/SIMD: caps the allocation at 168 VGPRs (no spills); 171 would drop to 2.
 template <int PACK, bool VEC>
-__global__ __launch_bounds__(WAVES * 64) void ae_train_kernel(AEArgs a) {
+__global__ __launch_bounds__(WAVES * 64, 3) void ae_train_kernel(AEArgs a) {
   constexpr bool FAST = zero_preserving<PACK>();
-  __shared__ float red[WAVES][NSLOT];
+  static_assert(WAVES * 10 * 512 <= WAVES * NSLOT * 4, "transpose scratch must fit in the slab buffer");
+  // one LDS array: per-wave transpose scratch during the tile loop, per-wave
+  // gradient slabs afterwards
+  __shared__ __attribute__((aligned(16))) float smem[WAVES * NSLOT];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
+  char* scr = reinterpret_cast<char*>(smem) + wid * (10 * 512);
+  if (a.cursor) a.x += a.cursor[0] * a.ld;  // streaming ring consumer (uniform scalar load)
 
   if (a.iter && blockIdx.x == 0 && threadIdx.x == 0) a.iter[0] += 1;
 
   Frags F;
   load_frags<FAST>(a, c, g, F, true);
-  const bf16x4 I = identity_b(c, g);
   const float pad1 = (g == 3) ? 1.0f : 0.0f;
   f32x4 pn[2];
 #pragma unroll
@@ -405,7 +412,7 @@ __global__ __launch_bounds__(WAVES * 64) void ae_train_kernel(AEArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xnext[s][j], F.sc[s][j], F.sh[s][j]);
     if (t + stride < nfull) fetch_x<VEC>(a, (t + stride) * 16 + c, g, xnext);  // prefetch
-    train_tile<PACK, FAST, false>(a, F, I, c, g, lane, true, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
+    train_tile<PACK, FAST, false>(a, F, scr, c, g, lane, true, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
   }
   // ragged last tile: handled by the wave that would own tile index nfull
   if ((a.n & 15) && first == nfull % stride) {
@@ -417,11 +424,12 @@ __global__ __launch_bounds__(WAVES * 64) void ae_train_kernel(AEArgs a) {
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int j = 0; j < 4; ++j) xf[s][j] = valid ? fmaf(xf[s][j], F.sc[s][j], F.sh[s][j]) : 0.f;
-    train_tile<PACK, FAST, true>(a, F, I, c, g, lane, valid, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
+    train_tile<PACK, FAST, true>(a, F, scr, c, g, lane, valid, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
   }
 
   // per-wave slab in LDS (every slot written exactly once per wave)
-  float* my = red[wid];
+  __syncthreads();  // all waves done with their transpose scratch
+  float* my = smem + wid * NSLOT;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = 4 * g + i;
@@ -445,9 +453,9 @@ __global__ __launch_bounds__(WAVES * 64) void ae_train_kernel(AEArgs a) {
   __syncthreads();
   float* out = a.partials + (int64_t)blockIdx.x * NSLOT;
   for (int s = threadIdx.x; s < NSLOT; s += WAVES * 64) {
-    float v = red[0][s];
+    float v = smem[s];
 #pragma unroll
-    for (int w = 1; w < WAVES; ++w) v += red[w][s];
+    for (int w = 1; w < WAVES; ++w) v += smem[w * NSLOT + s];
     out[s] = v;
   }
 }
@@ -525,7 +533,13 @@ struct AdamHP {
   float lr, beta1, beta2, eps;
 };
 
-enum : int { RA_WRITE_GRAD = 1, RA_ADAM = 2, RA_METRICS = 4 };
+enum : int { RA_WRITE_GRAD = 1, RA_ADAM = 2, RA_METRICS = 4, RA_ADVANCE = 8 };
+
+struct CursorAdv {
+  int64_t* cursor;   // ring cursor advanced by `step` rows modulo `ring` after the update
+  int64_t step;
+  int64_t ring;
+};
 
 __device__ __forceinline__ void adam_one(float tot, int slot, int nparam, float* grad_out, float* params, float* m,
                                          float* v, float lr_t, const AdamHP& hp, float gscale, float* metrics_acc,
@@ -551,8 +565,12 @@ __device__ __forceinline__ void adam_one(float tot, int slot, int nparam, float*
 __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restrict__ partials, int G, int S,
                                                           int nparam, float* grad_out, float* params, float* m,
                                                           float* v, const int64_t* iter, AdamHP hp, float gscale,
-                                                          float* metrics_acc, int flags) {
+                                                          float* metrics_acc, int flags, CursorAdv adv) {
   __shared__ f32x4 red[16][16];
+  if ((flags & RA_ADVANCE) && adv.cursor && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t nx = adv.cursor[0] + adv.step;
+    adv.cursor[0] = nx >= adv.ring ? nx - adv.ring : nx;
+  }
   const int q = threadIdx.x & 15, grp = threadIdx.x >> 4;
   const int slot0 = (blockIdx.x * 16 + q) * 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -604,11 +622,11 @@ int ae_train_grid(int64_t n, int max_blocks) {
 }
 
 hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
-                           const float* params, float* partials, int64_t* iter, const int* dims, const int* acts,
-                           float l1, int want_acc, int grid, hipStream_t stream) {
+                           const float* params, float* partials, int64_t* iter, const int64_t* cursor,
+                           const int* dims, const int* acts, float l1, int want_acc, int grid, hipStream_t stream) {
   AEArgs a{};
   a.x = x; a.n = n; a.ld = ld; a.scale = scale; a.shift = shift; a.params = params;
-  a.partials = partials; a.iter = iter;
+  a.partials = partials; a.iter = iter; a.cursor = cursor;
   a.D = dims[0]; a.n1 = dims[1]; a.n2 = dims[2]; a.n3 = dims[3];
   a.a1 = acts[0]; a.a2 = acts[1]; a.a3 = acts[2]; a.a4 = acts[3];
   a.l1 = l1; a.want_acc = want_acc;
@@ -647,12 +665,14 @@ hipError_t ae_forward_launch(const float* x, int64_t n, int64_t ld, const float*
 
 hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, float* grad_out, float* params,
                               float* m, float* v, const int64_t* iter, float lr, float beta1, float beta2, float eps,
-                              float gscale, float* metrics_acc, int flags, hipStream_t stream) {
+                              float gscale, float* metrics_acc, int flags, int64_t* cursor, int64_t cursor_step,
+                              int64_t cursor_ring, hipStream_t stream) {
   AdamHP hp{lr, beta1, beta2, eps};
+  CursorAdv adv{cursor, cursor_step, cursor_ring};
   if (S % 4 != 0) return hipErrorInvalidValue;
   const int grid = (S / 4 + 15) / 16;
   hipLaunchKernelGGL(reduce_adam_kernel, dim3(grid), dim3(256), 0, stream, partials, G, S, nparam, grad_out, params,
-                     m, v, iter, hp, gscale, metrics_acc, flags);
+                     m, v, iter, hp, gscale, metrics_acc, flags, adv);
   return hipGetLastError();
 }
 

@@ -45,7 +45,8 @@ void check_ae_dims(const std::vector<int64_t>& dims, const std::vector<int64_t>&
 int64_t ae_train_partials(const at::Tensor& x, const c10::optional<at::Tensor>& scale,
                           const c10::optional<at::Tensor>& shift, const at::Tensor& params, at::Tensor& partials,
                           const c10::optional<at::Tensor>& iter, std::vector<int64_t> dims, std::vector<int64_t> acts,
-                          double l1, bool want_acc, int64_t max_blocks) {
+                          double l1, bool want_acc, int64_t max_blocks, int64_t n_rows,
+                          const c10::optional<at::Tensor>& cursor) {
   check_ae_dims(dims, acts);
   check_dev(x, "x", at::kFloat);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [n, ld] with unit column stride");
@@ -64,14 +65,24 @@ int64_t ae_train_partials(const at::Tensor& x, const c10::optional<at::Tensor>& 
     check_dev(*iter, "iter", at::kLong);
     iter_ptr = iter->data_ptr<int64_t>();
   }
-  const int64_t n = x.size(0);
+  const int64_t n = n_rows >= 0 ? n_rows : x.size(0);
+  const int64_t* cur_ptr = nullptr;
+  if (cursor.has_value() && cursor->defined()) {
+    check_dev(*cursor, "cursor", at::kLong);
+    // the ring contract (checked by the caller): cursor + n <= rows, cursor a multiple of n
+    TORCH_CHECK(n > 0 && x.size(0) % n == 0, "ring rows must be a multiple of the batch");
+    cur_ptr = cursor->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(n <= x.size(0), "n_rows larger than x");
+  }
   const int grid = sml::ae_train_grid(n, (int)max_blocks);
   TORCH_CHECK(partials.numel() >= (int64_t)grid * sml::ae_nslot(), "partials buffer too small for grid ", grid);
   c10::hip::HIPGuard guard(x.device().index());
   int d[4] = {(int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3]};
   int a[4] = {(int)acts[0], (int)acts[1], (int)acts[2], (int)acts[3]};
   SML_CHECK_HIP(sml::ae_train_launch(x.data_ptr<float>(), n, x.stride(0), opt_ptr(scale), opt_ptr(shift),
-                                     params.data_ptr<float>(), partials.data_ptr<float>(), iter_ptr, d, a, (float)l1,
+                                     params.data_ptr<float>(), partials.data_ptr<float>(), iter_ptr, cur_ptr, d, a,
+                                     (float)l1,
                                      want_acc ? 1 : 0, grid, cur_stream(x)));
   return grid;
 }
@@ -80,7 +91,8 @@ void reduce_adam(const at::Tensor& partials, int64_t G, int64_t S, int64_t npara
                  const c10::optional<at::Tensor>& grad_out, const c10::optional<at::Tensor>& params,
                  const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
                  const c10::optional<at::Tensor>& iter, double lr, double beta1, double beta2, double eps,
-                 double gscale, const c10::optional<at::Tensor>& metrics, int64_t flags) {
+                 double gscale, const c10::optional<at::Tensor>& metrics, int64_t flags,
+                 const c10::optional<at::Tensor>& cursor, int64_t cursor_step, int64_t cursor_ring) {
   check_dev(partials, "partials", at::kFloat);
   TORCH_CHECK(partials.numel() >= G * S, "partials smaller than G*S");
   if (flags & 2) {
@@ -95,7 +107,8 @@ void reduce_adam(const at::Tensor& partials, int64_t G, int64_t S, int64_t npara
   SML_CHECK_HIP(sml::reduce_adam_launch(partials.data_ptr<float>(), (int)G, (int)S, (int)nparam, opt_mut(grad_out),
                                         opt_mut(params), opt_mut(m), opt_mut(v), iter_ptr, (float)lr, (float)beta1,
                                         (float)beta2, (float)eps, (float)gscale, opt_mut(metrics), (int)flags,
-                                        cur_stream(partials)));
+                                        (cursor.has_value() && cursor->defined()) ? cursor->data_ptr<int64_t>() : nullptr,
+                                        cursor_step, cursor_ring, cur_stream(partials)));
 }
 
 void ae_forward(const at::Tensor& x, const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift,
@@ -141,13 +154,15 @@ PYBIND11_MODULE(_C, m) {
   m.attr("AE_NPARAM") = sml::ae_nparam();
   m.def("ae_train_partials", &ae_train_partials, "fused AE fwd+bwd -> per-workgroup gradient slabs",
         py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("partials"), py::arg("iter"),
-        py::arg("dims"), py::arg("acts"), py::arg("l1"), py::arg("want_acc"), py::arg("max_blocks"));
+        py::arg("dims"), py::arg("acts"), py::arg("l1"), py::arg("want_acc"), py::arg("max_blocks"),
+        py::arg("n_rows") = -1, py::arg("cursor") = py::none());
   m.def("ae_train_grid", &sml::ae_train_grid, "grid size the AE train kernel uses", py::arg("n"),
         py::arg("max_blocks"));
   m.def("reduce_adam", &reduce_adam, "slab reduction + optional Adam", py::arg("partials"), py::arg("G"),
         py::arg("S"), py::arg("nparam"), py::arg("grad_out"), py::arg("params"), py::arg("m"), py::arg("v"),
         py::arg("iter"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("gscale"),
-        py::arg("metrics"), py::arg("flags"));
+        py::arg("metrics"), py::arg("flags"), py::arg("cursor") = py::none(), py::arg("cursor_step") = 0,
+        py::arg("cursor_ring") = 0);
   m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),
         py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("recon"), py::arg("score"), py::arg("flag"),

@@ -28,7 +28,7 @@ NSLOT = 1540
 # offsets / shapes of the padded image [in_pad][out_pad] and the bias row
 LAYOUT = [(0, 32, 16, 31), (512, 16, 16, 15), (768, 16, 16, 15), (1024, 16, 32, 15)]
 
-RA_WRITE_GRAD, RA_ADAM, RA_METRICS = 1, 2, 4
+RA_WRITE_GRAD, RA_ADAM, RA_METRICS, RA_ADVANCE = 1, 2, 4, 8
 
 
 @dataclass
@@ -114,6 +114,9 @@ class FusedAE:
         self.partials = torch.zeros(self.max_blocks * NSLOT, device=dev)
         self.grad = torch.zeros(NSLOT, device=dev)
         self.metrics = torch.zeros(NSLOT - NPARAM, device=dev)   # epoch accumulators
+        self.cursor = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ring: Optional[torch.Tensor] = None
+        self.ring_batch = 0
         self.set_normalizer(scale, shift)
 
     # -- normalisation fused into the first load ------------------------------------
@@ -157,8 +160,39 @@ class FusedAE:
 
     def reduce(self, G: int, flags: int, gscale: float = 1.0, partials: Optional[torch.Tensor] = None) -> None:
         src = self.partials if partials is None else partials
+        ring = self.ring.size(0) if self.ring is not None else 0
         self.C.reduce_adam(src, int(G), NSLOT, NPARAM, self.grad, self.params, self.m, self.v, self.iter,
-                           self.lr, self.beta_1, self.beta_2, self.epsilon, float(gscale), self.metrics, int(flags))
+                           self.lr, self.beta_1, self.beta_2, self.epsilon, float(gscale), self.metrics, int(flags),
+                           self.cursor, int(self.ring_batch), int(ring))
+
+    # -- streaming ring consumption (device cursor; graph-capturable) ------------
+    def attach_ring(self, ring: torch.Tensor, batch: int) -> None:
+        """Consume ``batch`` rows per step from a device-resident ring of raw rows.
+
+        The read position lives on the device (``self.cursor``) and is advanced by
+        the Adam kernel, so a whole step -- launches and the all-reduce -- can be
+        captured once in a hipGraph and replayed with no host work per step.
+        """
+        self._check_x(ring)
+        if batch <= 0 or ring.size(0) % batch:
+            raise ValueError("ring rows must be a positive multiple of the batch")
+        self.ring, self.ring_batch = ring, int(batch)
+        self.cursor.zero_()
+
+    def step_ring(self, global_batch: Optional[int] = None, allreduce=None) -> None:
+        if self.ring is None:
+            raise RuntimeError("attach_ring() first")
+        B = self.ring_batch
+        gb = B if global_batch is None else int(global_batch)
+        G = self.C.ae_train_partials(self.ring, self.scale, self.shift, self.params, self.partials, self.iter,
+                                     self.spec.dims, self.spec.act_codes, float(self.spec.activity_l1),
+                                     bool(self.want_acc), self.max_blocks, B, self.cursor)
+        if allreduce is None:
+            self.reduce(G, RA_ADAM | RA_METRICS | RA_ADVANCE, gscale=1.0 / gb)
+        else:
+            self.reduce(G, RA_WRITE_GRAD)
+            allreduce(self.grad)
+            self.reduce(1, RA_ADAM | RA_METRICS | RA_ADVANCE, gscale=1.0 / gb, partials=self.grad)
 
     def step(self, x: torch.Tensor, global_batch: Optional[int] = None, allreduce=None) -> None:
         """One full optimizer step on ``x`` (all rows of the local micro-batch).
