@@ -432,7 +432,6 @@ class Writer {
  private:
   std::string out_;
   std::vector<std::string> vstrings_;
-  std::map<const std::string*, std::pair<uint64_t, uint32_t>> vref_;
 
   struct GroupInfo {
     uint64_t btree = UNDEF, heap = UNDEF;
@@ -468,20 +467,20 @@ class Writer {
 
   // one global heap collection (>= 4096 bytes) holding every vlen string
   uint64_t gcol_ = UNDEF;
-  std::vector<uint32_t> gidx_;
-  size_t gnext_ = 0;
+  std::map<std::string, uint32_t> gidx_;  // string content -> heap object index
   void write_global_heap() {
     if (vstrings_.empty()) return;
     std::string body;
     uint32_t idx = 1;
     for (const auto& s : vstrings_) {
+      if (gidx_.count(s)) continue;  // identical strings share one heap object
       app(body, idx, 2);
       app(body, 1, 2);   // reference count
       app(body, 0, 4);
       app(body, s.size(), 8);
       body += s;
       pad8(body);
-      gidx_.push_back(idx++);
+      gidx_[s] = idx++;
     }
     uint64_t total = 16 + body.size();
     uint64_t csize = std::max<uint64_t>(4096, ((total + 16 + 4095) / 4096) * 4096);
@@ -542,9 +541,9 @@ class Writer {
     d.push_back((char)(cset & 0xf));
     d.push_back(0);
     app(d, 16, 4);              // 4-byte length + 8-byte collection address + 4-byte index
-    // base type: 1-byte character, same as libhdf5's H5T_C_S1 base of vlen strings
-    std::string base = dt_fixed_string(1, 0, cset);
-    d += base;
+    // base type: 1-byte unsigned fixed-point -- byte-identical to what h5py 2.x
+    // wrote for the reference models/*.h5 string attributes
+    d += dt_numeric('u', 1);
     return d;
   }
   static std::string dtype_of(const Value& v) {
@@ -576,7 +575,7 @@ class Writer {
     for (const auto& s : v.strings) {
       app(d, s.size(), 4);
       app(d, gcol_, 8);
-      app(d, gidx_.at(gnext_++), 4);
+      app(d, gidx_.at(s), 4);
     }
     return d;
   }

@@ -1,0 +1,401 @@
+// pybind11 bindings of the host I/O codecs (module streamml._io).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "avro.h"
+#include "h5.h"
+#include "kafka.h"
+
+namespace py = pybind11;
+using namespace sml;
+
+namespace {
+
+// ---------------------------------------------------------------- HDF5 ------
+py::object value_to_py(const h5::Value& v) {
+  py::dict d;
+  py::list shape;
+  for (auto x : v.shape) shape.append(x);
+  d["shape"] = shape;
+  d["null"] = v.is_null;
+  switch (v.kind) {
+    case h5::Value::NUMERIC: {
+      d["kind"] = "numeric";
+      std::string dt = std::string("<") + v.dtype + std::to_string(v.itemsize);
+      d["dtype"] = dt;
+      d["data"] = py::bytes(v.data);
+      break;
+    }
+    case h5::Value::FIXED_STRING:
+      d["kind"] = "fixed_str";
+      d["size"] = v.itemsize;
+      d["pad"] = v.str_pad;
+      d["cset"] = v.cset;
+      d["data"] = py::bytes(v.data);
+      break;
+    case h5::Value::VLEN_STRING: {
+      d["kind"] = "vlen_str";
+      d["cset"] = v.cset;
+      py::list vals;
+      for (const auto& s : v.strings) vals.append(py::bytes(s));
+      d["values"] = vals;
+      break;
+    }
+  }
+  return std::move(d);
+}
+
+h5::Value value_from_py(const py::dict& d) {
+  h5::Value v;
+  const std::string kind = py::str(d["kind"]);
+  for (auto x : d["shape"].cast<py::list>()) v.shape.push_back(x.cast<uint64_t>());
+  if (kind == "numeric") {
+    v.kind = h5::Value::NUMERIC;
+    const std::string dt = py::str(d["dtype"]);  // e.g. "<f4"
+    if (dt.size() < 3 || dt[0] != '<') throw std::runtime_error("h5: dtype must be little-endian like '<f4'");
+    v.dtype = dt[1];
+    v.itemsize = std::stoi(dt.substr(2));
+    v.data = d["data"].cast<std::string>();
+  } else if (kind == "fixed_str") {
+    v.kind = h5::Value::FIXED_STRING;
+    v.itemsize = d["size"].cast<int>();
+    v.str_pad = d.contains("pad") ? d["pad"].cast<int>() : 1;
+    v.cset = d.contains("cset") ? d["cset"].cast<int>() : 0;
+    v.data = d["data"].cast<std::string>();
+  } else if (kind == "vlen_str") {
+    v.kind = h5::Value::VLEN_STRING;
+    v.cset = d.contains("cset") ? d["cset"].cast<int>() : 1;
+    for (auto s : d["values"].cast<py::list>()) v.strings.push_back(s.cast<std::string>());
+  } else {
+    throw std::runtime_error("h5: unknown value kind " + kind);
+  }
+  return v;
+}
+
+py::dict node_to_py(const h5::Node& n) {
+  py::dict d;
+  py::dict attrs;
+  for (const auto& a : n.attrs) attrs[py::str(a.first)] = value_to_py(a.second);
+  d["attrs"] = attrs;
+  if (n.is_group) {
+    d["type"] = "group";
+    py::dict kids;
+    for (const auto& c : n.children) kids[py::str(c.first)] = node_to_py(c.second);
+    d["children"] = kids;
+  } else {
+    d["type"] = "dataset";
+    d["value"] = value_to_py(n.value);
+  }
+  return d;
+}
+
+h5::Node node_from_py(const py::dict& d) {
+  h5::Node n;
+  const std::string type = d.contains("type") ? std::string(py::str(d["type"])) : "group";
+  n.is_group = type == "group";
+  if (d.contains("attrs"))
+    for (auto kv : d["attrs"].cast<py::dict>())
+      n.attrs.emplace_back(kv.first.cast<std::string>(), value_from_py(kv.second.cast<py::dict>()));
+  if (n.is_group) {
+    if (d.contains("children"))
+      for (auto kv : d["children"].cast<py::dict>())
+        n.children.emplace_back(kv.first.cast<std::string>(), node_from_py(kv.second.cast<py::dict>()));
+  } else {
+    n.value = value_from_py(d["value"].cast<py::dict>());
+  }
+  return n;
+}
+
+// ---------------------------------------------------------------- Avro ------
+std::vector<avro::Field> fields_from_py(const py::list& lst) {
+  std::vector<avro::Field> out;
+  for (auto item : lst) {
+    auto t = item.cast<py::tuple>();
+    avro::Field f;
+    f.name = t[0].cast<std::string>();
+    f.kind = t[1].cast<int>();
+    f.null_branch = t[2].cast<int>();
+    f.fixed_size = t.size() > 3 ? t[3].cast<int>() : 0;
+    f.n_symbols = t.size() > 4 ? t[4].cast<int>() : 0;
+    out.push_back(f);
+  }
+  return out;
+}
+
+py::dict batch_to_py(avro::DecodedBatch& b) {
+  py::dict d;
+  const size_t n = b.n, k = b.n_numeric;
+  py::array_t<float> num({n, k});
+  if (n * k) std::memcpy(num.mutable_data(), b.numeric.data(), n * k * sizeof(float));
+  d["numeric"] = num;
+  if (!b.numeric64.empty()) {
+    py::array_t<double> num64({n, k});
+    std::memcpy(num64.mutable_data(), b.numeric64.data(), n * k * sizeof(double));
+    d["numeric64"] = num64;
+  }
+  py::array_t<uint8_t> nul({n, k});
+  if (n * k) std::memcpy(nul.mutable_data(), b.null_mask.data(), n * k);
+  d["null"] = nul;
+  py::list text, tnull;
+  for (size_t c = 0; c < b.text.size(); ++c) {
+    py::list col;
+    for (auto& s : b.text[c]) col.append(py::bytes(s));
+    text.append(col);
+    py::array_t<uint8_t> tn(n);
+    if (n) std::memcpy(tn.mutable_data(), b.text_null[c].data(), n);
+    tnull.append(tn);
+  }
+  d["text"] = text;
+  d["text_null"] = tnull;
+  py::array_t<int32_t> sid(n);
+  if (n) std::memcpy(sid.mutable_data(), b.schema_id.data(), n * 4);
+  d["schema_id"] = sid;
+  py::array_t<uint8_t> ok(n);
+  if (n) std::memcpy(ok.mutable_data(), b.ok.data(), n);
+  d["ok"] = ok;
+  d["n_errors"] = b.n_errors;
+  return d;
+}
+
+py::dict fetch_to_py(kafka::FetchResult& r) {
+  py::dict d;
+  d["values"] = py::bytes(r.values);
+  py::array_t<int64_t> vo(r.value_offsets.size());
+  std::memcpy(vo.mutable_data(), r.value_offsets.data(), r.value_offsets.size() * 8);
+  d["value_offsets"] = vo;
+  py::array_t<int64_t> off(r.offsets.size());
+  if (!r.offsets.empty()) std::memcpy(off.mutable_data(), r.offsets.data(), r.offsets.size() * 8);
+  d["offsets"] = off;
+  py::array_t<int64_t> ts(r.timestamps.size());
+  if (!r.timestamps.empty()) std::memcpy(ts.mutable_data(), r.timestamps.data(), r.timestamps.size() * 8);
+  d["timestamps"] = ts;
+  py::list keys;
+  for (auto& k : r.keys) keys.append(py::bytes(k));
+  d["keys"] = keys;
+  d["high_watermark"] = r.high_watermark;
+  return d;
+}
+
+std::vector<kafka::Record> records_from_py(const py::list& values, const py::object& keys, const py::object& ts) {
+  std::vector<kafka::Record> recs(values.size());
+  py::list kl = keys.is_none() ? py::list() : keys.cast<py::list>();
+  py::list tl = ts.is_none() ? py::list() : ts.cast<py::list>();
+  for (size_t i = 0; i < recs.size(); ++i) {
+    recs[i].value = values[i].cast<std::string>();
+    if (!keys.is_none() && !kl[i].is_none()) {
+      recs[i].key = kl[i].cast<std::string>();
+      recs[i].key_null = false;
+    }
+    recs[i].timestamp = ts.is_none() ? 0 : tl[i].cast<int64_t>();
+  }
+  return recs;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_io, m) {
+  m.doc() = "streamml host I/O: HDF5, Avro/Confluent, Kafka wire protocol";
+
+  py::register_exception<h5::Error>(m, "H5Error");
+  py::register_exception<avro::Error>(m, "AvroError");
+  py::register_exception<kafka::Error>(m, "KafkaError");
+
+  // HDF5
+  m.def("h5_read", [](const std::string& path) { return node_to_py(h5::read_file(path)); }, py::arg("path"));
+  m.def("h5_read_bytes", [](const py::bytes& b) { return node_to_py(h5::read_bytes(b.cast<std::string>())); },
+        py::arg("data"));
+  m.def("h5_write", [](const std::string& path, const py::dict& root) { h5::write_file(path, node_from_py(root)); },
+        py::arg("path"), py::arg("root"));
+  m.def("h5_write_bytes", [](const py::dict& root) { return py::bytes(h5::write_bytes(node_from_py(root))); },
+        py::arg("root"));
+
+  // Avro
+  py::class_<avro::Codec>(m, "AvroCodec")
+      .def(py::init([](const py::list& f) { return new avro::Codec(fields_from_py(f)); }), py::arg("fields"))
+      .def_property_readonly("n_numeric", &avro::Codec::n_numeric)
+      .def_property_readonly("n_text", &avro::Codec::n_text)
+      .def(
+          "decode",
+          [](const avro::Codec& c, const py::bytes& buf, py::array_t<int64_t, py::array::c_style> offsets,
+             bool framing, bool strict, bool want_f64) {
+            std::string_view sv = buf;  // no copy
+            const size_t n = offsets.size() ? (size_t)offsets.size() - 1 : 0;
+            avro::DecodedBatch b;
+            {
+              py::gil_scoped_release rel;
+              b = c.decode(reinterpret_cast<const uint8_t*>(sv.data()), sv.size(), offsets.data(), n, framing, strict,
+                           want_f64);
+            }
+            return batch_to_py(b);
+          },
+          py::arg("buf"), py::arg("offsets"), py::arg("framing") = true, py::arg("strict") = false,
+          py::arg("want_f64") = false)
+      .def(
+          "encode",
+          [](const avro::Codec& c, py::array_t<double, py::array::c_style | py::array::forcecast> numeric,
+             py::object null_mask, const py::list& text, py::object text_null, bool framing, int32_t schema_id) {
+            const size_t n = numeric.ndim() ? (size_t)numeric.shape(0) : 0;
+            if (numeric.ndim() != 2 || (size_t)numeric.shape(1) != c.n_numeric())
+              throw avro::Error("avro encode: numeric must be [n, n_numeric]");
+            std::vector<uint8_t> nm;
+            if (!null_mask.is_none()) {
+              auto a = null_mask.cast<py::array_t<uint8_t, py::array::c_style | py::array::forcecast>>();
+              nm.assign(a.data(), a.data() + a.size());
+            }
+            std::vector<std::vector<std::string>> tx;
+            for (auto col : text) {
+              std::vector<std::string> v;
+              for (auto s : col.cast<py::list>()) v.push_back(s.cast<std::string>());
+              tx.push_back(std::move(v));
+            }
+            std::vector<std::vector<uint8_t>> tn;
+            if (!text_null.is_none())
+              for (auto col : text_null.cast<py::list>()) {
+                auto a = col.cast<py::array_t<uint8_t, py::array::c_style | py::array::forcecast>>();
+                tn.emplace_back(a.data(), a.data() + a.size());
+              }
+            std::string out;
+            std::vector<int64_t> offs;
+            c.encode(numeric.data(), nm.empty() ? nullptr : nm.data(), tx, tn, n, framing, schema_id, out, offs);
+            py::array_t<int64_t> po(offs.size());
+            std::memcpy(po.mutable_data(), offs.data(), offs.size() * 8);
+            return py::make_tuple(py::bytes(out), po);
+          },
+          py::arg("numeric"), py::arg("null_mask") = py::none(), py::arg("text") = py::list(),
+          py::arg("text_null") = py::none(), py::arg("framing") = true, py::arg("schema_id") = 1);
+
+  // Kafka
+  m.def("crc32c", [](const py::bytes& b) {
+    std::string_view s = b;
+    return kafka::crc32c(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+  });
+  py::class_<kafka::Client>(m, "KafkaClient")
+      .def(py::init([](const std::string& bootstrap, const std::string& client_id, const std::string& mech,
+                       const std::string& user, const std::string& pw, int timeout_ms) {
+             kafka::ClientConfig c;
+             c.client_id = client_id;
+             c.sasl_mechanism = mech;
+             c.sasl_username = user;
+             c.sasl_password = pw;
+             c.timeout_ms = timeout_ms;
+             return new kafka::Client(bootstrap, c);
+           }),
+           py::arg("bootstrap"), py::arg("client_id") = "streamml", py::arg("sasl_mechanism") = "",
+           py::arg("sasl_username") = "", py::arg("sasl_password") = "", py::arg("timeout_ms") = 30000)
+      .def("partitions", [](kafka::Client& c) {
+        py::gil_scoped_release rel;
+        return c.partitions();
+      })
+      .def("list_offset",
+           [](kafka::Client& c, const std::string& t, int p, int64_t time) {
+             py::gil_scoped_release rel;
+             return c.list_offset(t, p, time);
+           },
+           py::arg("topic"), py::arg("partition"), py::arg("time"))
+      .def("fetch",
+           [](kafka::Client& c, const std::string& t, int p, int64_t off, int32_t max_bytes, int32_t wait) {
+             kafka::FetchResult r;
+             {
+               py::gil_scoped_release rel;
+               r = c.fetch(t, p, off, max_bytes, wait);
+             }
+             return fetch_to_py(r);
+           },
+           py::arg("topic"), py::arg("partition"), py::arg("offset"), py::arg("max_bytes") = 1 << 20,
+           py::arg("max_wait_ms") = 100)
+      .def("fetch_decode",
+           [](kafka::Client& c, const avro::Codec& codec, const std::string& t, int p, int64_t off,
+              int32_t max_bytes, int32_t wait, bool framing) {
+             kafka::FetchResult r;
+             avro::DecodedBatch b;
+             {
+               py::gil_scoped_release rel;
+               r = c.fetch(t, p, off, max_bytes, wait);
+               b = codec.decode(reinterpret_cast<const uint8_t*>(r.values.data()), r.values.size(),
+                                r.value_offsets.data(), r.size(), framing, false, false);
+             }
+             py::dict d = batch_to_py(b);
+             py::array_t<int64_t> offs(r.offsets.size());
+             if (!r.offsets.empty()) std::memcpy(offs.mutable_data(), r.offsets.data(), r.offsets.size() * 8);
+             d["offsets"] = offs;
+             py::list keys;
+             for (auto& k : r.keys) keys.append(py::bytes(k));
+             d["keys"] = keys;
+             d["high_watermark"] = r.high_watermark;
+             d["bytes"] = r.values.size();
+             return d;
+           },
+           py::arg("codec"), py::arg("topic"), py::arg("partition"), py::arg("offset"),
+           py::arg("max_bytes") = 1 << 20, py::arg("max_wait_ms") = 100, py::arg("framing") = true)
+      .def("produce",
+           [](kafka::Client& c, const std::string& t, int p, const py::list& values, py::object keys, py::object ts,
+              int acks) {
+             auto recs = records_from_py(values, keys, ts);
+             py::gil_scoped_release rel;
+             return c.produce(t, p, recs, (int16_t)acks);
+           },
+           py::arg("topic"), py::arg("partition"), py::arg("values"), py::arg("keys") = py::none(),
+           py::arg("timestamps") = py::none(), py::arg("acks") = 1)
+      .def("commit",
+           [](kafka::Client& c, const std::string& g, const std::string& t, int p, int64_t off) {
+             py::gil_scoped_release rel;
+             c.commit(g, t, p, off);
+           })
+      .def("committed",
+           [](kafka::Client& c, const std::string& g, const std::string& t, int p) {
+             py::gil_scoped_release rel;
+             return c.committed(g, t, p);
+           })
+      .def_property_readonly("bytes_received", &kafka::Client::bytes_received);
+
+  py::class_<kafka::Broker>(m, "KafkaBroker")
+      .def(py::init([](int port, const std::string& user, const std::string& pw, int64_t retention) {
+             kafka::BrokerConfig c;
+             c.port = port;
+             c.sasl_username = user;
+             c.sasl_password = pw;
+             c.retention_records = retention;
+             return new kafka::Broker(c);
+           }),
+           py::arg("port") = 0, py::arg("sasl_username") = "", py::arg("sasl_password") = "",
+           py::arg("retention_records") = -1)
+      .def_property_readonly("port", &kafka::Broker::port)
+      .def("create_topic", &kafka::Broker::create_topic)
+      .def("append",
+           [](kafka::Broker& b, const std::string& t, int p, const py::list& values, py::object keys,
+              py::object ts) { return b.append(t, p, records_from_py(values, keys, ts)); },
+           py::arg("topic"), py::arg("partition"), py::arg("values"), py::arg("keys") = py::none(),
+           py::arg("timestamps") = py::none())
+      .def("append_buffer",
+           [](kafka::Broker& b, const std::string& t, int p, const py::bytes& buf,
+              py::array_t<int64_t, py::array::c_style> offsets, int64_t ts0) {
+             std::string_view sv = buf;
+             std::vector<kafka::Record> recs((size_t)std::max<py::ssize_t>(0, offsets.size() - 1));
+             for (size_t i = 0; i < recs.size(); ++i) {
+               recs[i].value.assign(sv.data() + offsets.data()[i], (size_t)(offsets.data()[i + 1] - offsets.data()[i]));
+               recs[i].timestamp = ts0;
+             }
+             py::gil_scoped_release rel;
+             return b.append(t, p, recs);
+           },
+           py::arg("topic"), py::arg("partition"), py::arg("buf"), py::arg("offsets"), py::arg("timestamp") = 0)
+      .def("end_offset", &kafka::Broker::end_offset)
+      .def("start_offset", &kafka::Broker::start_offset)
+      .def("read",
+           [](kafka::Broker& b, const std::string& t, int p, int64_t off, size_t maxn) {
+             auto recs = b.read(t, p, off, maxn);
+             py::list out;
+             for (auto& r : recs) out.append(py::make_tuple(r.offset, py::bytes(r.key), py::bytes(r.value)));
+             return out;
+           })
+      .def("set_faults", &kafka::Broker::set_faults, py::arg("fail_every") = 0, py::arg("delay_ms") = 0)
+      .def_property_readonly("fetch_count", &kafka::Broker::fetch_count)
+      .def_property_readonly("injected_failures", &kafka::Broker::injected_failures)
+      .def("stop", [](kafka::Broker& b) {
+        py::gil_scoped_release rel;
+        b.stop();
+      });
+}

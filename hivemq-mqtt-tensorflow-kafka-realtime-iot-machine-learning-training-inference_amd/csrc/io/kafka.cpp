@@ -1,0 +1,1020 @@
+// Kafka wire protocol client + in-process broker (see kafka.h).
+#include "kafka.h"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <sstream>
+
+#include "avro.h"  // zigzag varints
+
+namespace sml {
+namespace kafka {
+
+// ---------------------------------------------------------------------------
+// CRC-32C (Castagnoli), table driven
+// ---------------------------------------------------------------------------
+namespace {
+struct Crc32cTable {
+  uint32_t t[256];
+  Crc32cTable() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
+      t[i] = c;
+    }
+  }
+};
+const Crc32cTable kCrc;
+}  // namespace
+
+uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc) {
+  crc = ~crc;
+  for (size_t i = 0; i < n; ++i) crc = kCrc.t[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
+  return ~crc;
+}
+
+// ---------------------------------------------------------------------------
+// big-endian writer / reader
+// ---------------------------------------------------------------------------
+namespace {
+struct W {
+  std::string s;
+  void i8(int8_t v) { s.push_back((char)v); }
+  void i16(int16_t v) { u(v, 2); }
+  void i32(int32_t v) { u(v, 4); }
+  void i64(int64_t v) { u(v, 8); }
+  void u(uint64_t v, int n) {
+    for (int i = n - 1; i >= 0; --i) s.push_back((char)((v >> (8 * i)) & 0xff));
+  }
+  void str(const std::string& v) {
+    i16((int16_t)v.size());
+    s += v;
+  }
+  void nullstr() { i16(-1); }
+  void bytes(const std::string& v) {
+    i32((int32_t)v.size());
+    s += v;
+  }
+  void arr(int32_t n) { i32(n); }
+  size_t pos() const { return s.size(); }
+  void put32(size_t at, int32_t v) {
+    for (int i = 3; i >= 0; --i) s[at + 3 - i] = (char)((v >> (8 * i)) & 0xff);
+  }
+};
+
+struct R {
+  const uint8_t* p;
+  size_t n;
+  size_t i = 0;
+  void need(size_t k) const {
+    if (k > n - i) throw Error("kafka: truncated message");
+  }
+  uint64_t u(int k) {
+    need((size_t)k);
+    uint64_t v = 0;
+    for (int j = 0; j < k; ++j) v = (v << 8) | p[i + j];
+    i += (size_t)k;
+    return v;
+  }
+  int8_t i8() { return (int8_t)u(1); }
+  int16_t i16() { return (int16_t)u(2); }
+  int32_t i32() { return (int32_t)u(4); }
+  int64_t i64() { return (int64_t)u(8); }
+  std::string str() {
+    const int16_t len = i16();
+    if (len < 0) return std::string();
+    need((size_t)len);
+    std::string v(reinterpret_cast<const char*>(p + i), (size_t)len);
+    i += (size_t)len;
+    return v;
+  }
+  // returns pointer + length of a BYTES field (length -1 => null => n = 0)
+  std::pair<const uint8_t*, size_t> bytes() {
+    const int32_t len = i32();
+    if (len < 0) return {nullptr, 0};
+    need((size_t)len);
+    auto r = std::make_pair(p + i, (size_t)len);
+    i += (size_t)len;
+    return r;
+  }
+  int32_t arr() {
+    const int32_t n_ = i32();
+    if (n_ > (int32_t)(n - i)) throw Error("kafka: implausible array length");
+    return n_;
+  }
+  int64_t varlong() {
+    int64_t v;
+    const size_t k = avro::read_varlong(p + i, n - i, &v);
+    if (!k) throw Error("kafka: bad varint");
+    i += k;
+    return v;
+  }
+};
+
+void vl(std::string& s, int64_t v) { avro::write_varlong(s, v); }
+
+enum Api : int16_t {
+  API_PRODUCE = 0, API_FETCH = 1, API_LIST_OFFSETS = 2, API_METADATA = 3, API_OFFSET_COMMIT = 8,
+  API_OFFSET_FETCH = 9, API_FIND_COORDINATOR = 10, API_SASL_HANDSHAKE = 17, API_API_VERSIONS = 18,
+  API_SASL_AUTH = 36,
+};
+enum Err : int16_t {
+  E_NONE = 0, E_OFFSET_OUT_OF_RANGE = 1, E_UNKNOWN_TOPIC = 3, E_NOT_LEADER = 6,
+  E_ILLEGAL_SASL_STATE = 34, E_UNSUPPORTED_SASL = 33, E_SASL_AUTH_FAILED = 58,
+};
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// record batch v2
+// ---------------------------------------------------------------------------
+std::string encode_record_batch(int64_t base_offset, const std::vector<Record>& recs) {
+  if (recs.empty()) return std::string();
+  const int64_t first_ts = recs.front().timestamp;
+  int64_t max_ts = first_ts;
+  std::string body;  // from attributes to the end (CRC scope)
+  W h;
+  h.i16(0);                                   // attributes: no compression
+  h.i32((int32_t)(recs.size() - 1));          // lastOffsetDelta
+  h.i64(first_ts);
+  for (const auto& r : recs) max_ts = std::max(max_ts, r.timestamp);
+  h.i64(max_ts);
+  h.i64(-1);                                  // producerId
+  h.i16(-1);                                  // producerEpoch
+  h.i32(-1);                                  // baseSequence
+  h.i32((int32_t)recs.size());
+  body = h.s;
+  for (size_t k = 0; k < recs.size(); ++k) {
+    const Record& r = recs[k];
+    std::string rec;
+    rec.push_back(0);                         // attributes
+    vl(rec, r.timestamp - first_ts);
+    vl(rec, (int64_t)k);
+    if (r.key_null) vl(rec, -1);
+    else { vl(rec, (int64_t)r.key.size()); rec += r.key; }
+    vl(rec, (int64_t)r.value.size());
+    rec += r.value;
+    vl(rec, 0);                               // headers
+    vl(body, (int64_t)rec.size());
+    body += rec;
+  }
+  const uint32_t crc = crc32c(reinterpret_cast<const uint8_t*>(body.data()), body.size());
+  W b;
+  b.i64(base_offset);
+  b.i32((int32_t)(4 + 1 + 4 + body.size()));  // batchLength: epoch + magic + crc + body
+  b.i32(0);                                   // partitionLeaderEpoch
+  b.i8(2);                                    // magic
+  b.u(crc, 4);
+  b.s += body;
+  return b.s;
+}
+
+void decode_record_batches(const uint8_t* p, size_t n, int64_t min_offset, FetchResult& out) {
+  size_t pos = 0;
+  while (n - pos >= 12) {
+    R hdr{p + pos, n - pos};
+    const int64_t base = hdr.i64();
+    const int32_t blen = hdr.i32();
+    if (blen < 0 || (size_t)blen > n - pos - 12) break;  // partial trailing batch
+    R b{p + pos + 12, (size_t)blen};
+    b.i32();  // leader epoch
+    const int8_t magic = b.i8();
+    if (magic != 2) throw Error("kafka: unsupported record batch magic " + std::to_string(magic));
+    const uint32_t crc = (uint32_t)b.u(4);
+    const uint32_t calc = crc32c(p + pos + 12 + b.i, (size_t)blen - b.i);
+    if (crc != calc) throw Error("kafka: record batch CRC mismatch");
+    const int16_t attrs = b.i16();
+    if (attrs & 0x7) throw Error("kafka: compressed record batches are not supported");
+    b.i32();                     // lastOffsetDelta
+    const int64_t first_ts = b.i64();
+    b.i64();                     // max ts
+    b.i64();
+    b.i16();
+    b.i32();
+    const int32_t count = b.i32();
+    const bool control = attrs & 0x20;
+    for (int32_t k = 0; k < count; ++k) {
+      const int64_t len = b.varlong();
+      if (len < 0 || (size_t)len > b.n - b.i) throw Error("kafka: bad record length");
+      R r{b.p + b.i, (size_t)len};
+      b.i += (size_t)len;
+      r.i8();
+      const int64_t ts_delta = r.varlong();
+      const int64_t off_delta = r.varlong();
+      const int64_t klen = r.varlong();
+      std::string key;
+      if (klen >= 0) {
+        r.need((size_t)klen);
+        key.assign(reinterpret_cast<const char*>(r.p + r.i), (size_t)klen);
+        r.i += (size_t)klen;
+      }
+      const int64_t vlen = r.varlong();
+      const int64_t off = base + off_delta;
+      if (control || off < min_offset) {
+        if (vlen > 0) r.i += (size_t)vlen;
+        continue;
+      }
+      if (vlen > 0) {
+        r.need((size_t)vlen);
+        out.values.append(reinterpret_cast<const char*>(r.p + r.i), (size_t)vlen);
+        r.i += (size_t)vlen;
+      }
+      out.value_offsets.push_back((int64_t)out.values.size());
+      out.offsets.push_back(off);
+      out.timestamps.push_back(first_ts + ts_delta);
+      out.keys.push_back(std::move(key));
+    }
+    pos += 12 + (size_t)blen;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// connection
+// ---------------------------------------------------------------------------
+class Connection {
+ public:
+  Connection(const std::string& host, int port, int timeout_ms) {
+    addrinfo hints{};
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    addrinfo* res = nullptr;
+    const std::string ps = std::to_string(port);
+    if (getaddrinfo(host.c_str(), ps.c_str(), &hints, &res) != 0 || !res)
+      throw Error("kafka: cannot resolve " + host);
+    fd_ = ::socket(res->ai_family, res->ai_socktype, res->ai_protocol);
+    if (fd_ < 0) {
+      freeaddrinfo(res);
+      throw Error("kafka: socket() failed");
+    }
+    timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
+    setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+    int one = 1;
+    setsockopt(fd_, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    const int rc = ::connect(fd_, res->ai_addr, res->ai_addrlen);
+    freeaddrinfo(res);
+    if (rc != 0) {
+      ::close(fd_);
+      fd_ = -1;
+      throw Error("kafka: connect to " + host + ":" + ps + " failed");
+    }
+  }
+  ~Connection() {
+    if (fd_ >= 0) ::close(fd_);
+  }
+  void send_all(const std::string& s) {
+    size_t off = 0;
+    while (off < s.size()) {
+      const ssize_t k = ::send(fd_, s.data() + off, s.size() - off, MSG_NOSIGNAL);
+      if (k <= 0) throw Error("kafka: send failed");
+      off += (size_t)k;
+    }
+  }
+  void recv_all(char* p, size_t n) {
+    size_t off = 0;
+    while (off < n) {
+      const ssize_t k = ::recv(fd_, p + off, n - off, 0);
+      if (k <= 0) throw Error("kafka: connection closed / timed out");
+      off += (size_t)k;
+    }
+  }
+  bool authed = false;
+
+ private:
+  int fd_ = -1;
+};
+
+// ---------------------------------------------------------------------------
+// client
+// ---------------------------------------------------------------------------
+Client::Client(const std::string& bootstrap, ClientConfig cfg) : cfg_(std::move(cfg)) {
+  std::stringstream ss(bootstrap);
+  std::string item;
+  while (std::getline(ss, item, ',')) {
+    if (item.empty()) continue;
+    const auto c = item.rfind(':');
+    if (c == std::string::npos) throw Error("kafka: bootstrap server needs host:port: " + item);
+    bootstrap_.push_back({item.substr(0, c), std::stoi(item.substr(c + 1))});
+  }
+  if (bootstrap_.empty()) throw Error("kafka: no bootstrap servers");
+}
+
+Client::~Client() = default;
+
+std::unique_ptr<Connection> Client::open(const BrokerAddr& a) {
+  auto c = std::make_unique<Connection>(a.host, a.port, cfg_.timeout_ms);
+  if (!cfg_.sasl_mechanism.empty()) {
+    W hs;
+    hs.str(cfg_.sasl_mechanism);
+    std::string resp = call(*c, API_SASL_HANDSHAKE, 1, hs.s);
+    R r{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
+    const int16_t ec = r.i16();
+    if (ec != E_NONE) throw Error("kafka: SASL handshake rejected", ec);
+    std::string tok;
+    tok.push_back('\0');
+    tok += cfg_.sasl_username;
+    tok.push_back('\0');
+    tok += cfg_.sasl_password;
+    W au;
+    au.bytes(tok);
+    resp = call(*c, API_SASL_AUTH, 0, au.s);
+    R ra{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
+    const int16_t ec2 = ra.i16();
+    if (ec2 != E_NONE) throw Error("kafka: SASL/PLAIN authentication failed", ec2);
+    c->authed = true;
+  }
+  return c;
+}
+
+std::string Client::call(Connection& c, int16_t api, int16_t ver, const std::string& body) {
+  W w;
+  w.i32(0);  // size placeholder
+  w.i16(api);
+  w.i16(ver);
+  const int32_t corr = corr_++;
+  w.i32(corr);
+  w.str(cfg_.client_id);
+  w.s += body;
+  w.put32(0, (int32_t)(w.s.size() - 4));
+  c.send_all(w.s);
+  char hdr[8];
+  c.recv_all(hdr, 8);
+  const int32_t size = (int32_t)(((uint32_t)(uint8_t)hdr[0] << 24) | ((uint32_t)(uint8_t)hdr[1] << 16) |
+                                 ((uint32_t)(uint8_t)hdr[2] << 8) | (uint8_t)hdr[3]);
+  const int32_t rcorr = (int32_t)(((uint32_t)(uint8_t)hdr[4] << 24) | ((uint32_t)(uint8_t)hdr[5] << 16) |
+                                  ((uint32_t)(uint8_t)hdr[6] << 8) | (uint8_t)hdr[7]);
+  if (size < 4 || size > (1 << 30)) throw Error("kafka: bad response size");
+  if (rcorr != corr) throw Error("kafka: correlation id mismatch");
+  std::string resp((size_t)size - 4, '\0');
+  if (!resp.empty()) c.recv_all(&resp[0], resp.size());
+  bytes_rx_ += (uint64_t)size + 4;
+  return resp;
+}
+
+Connection& Client::any_conn() {
+  if (!any_) {
+    std::string last;
+    for (const auto& b : bootstrap_) {
+      try {
+        any_ = open(b);
+        break;
+      } catch (const Error& e) {
+        last = e.what();
+      }
+    }
+    if (!any_) throw Error("kafka: no bootstrap server reachable: " + last);
+  }
+  return *any_;
+}
+
+void Client::refresh_metadata() {
+  W w;
+  w.arr(-1);  // all topics
+  const std::string resp = call(any_conn(), API_METADATA, 1, w.s);
+  R r{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
+  brokers_.clear();
+  leaders_.clear();
+  for (int32_t nb = r.arr(), i = 0; i < nb; ++i) {
+    const int32_t id = r.i32();
+    std::string host = r.str();
+    const int32_t port = r.i32();
+    r.str();  // rack
+    brokers_[id] = {host, port};
+  }
+  r.i32();  // controller
+  for (int32_t nt = r.arr(), i = 0; i < nt; ++i) {
+    r.i16();
+    const std::string name = r.str();
+    r.i8();
+    std::vector<int32_t> lead;
+    for (int32_t np = r.arr(), k = 0; k < np; ++k) {
+      r.i16();
+      const int32_t pid = r.i32();
+      const int32_t leader = r.i32();
+      for (int32_t x = r.arr(), q = 0; q < x; ++q) r.i32();
+      for (int32_t x = r.arr(), q = 0; q < x; ++q) r.i32();
+      if ((int32_t)lead.size() <= pid) lead.resize((size_t)pid + 1, -1);
+      lead[(size_t)pid] = leader;
+    }
+    leaders_[name] = lead;
+  }
+  conns_.clear();
+}
+
+std::map<std::string, int> Client::partitions() {
+  std::lock_guard<std::mutex> g(mu_);
+  refresh_metadata();
+  std::map<std::string, int> out;
+  for (const auto& kv : leaders_) out[kv.first] = (int)kv.second.size();
+  return out;
+}
+
+Connection& Client::conn_for(const std::string& topic, int partition) {
+  auto it = leaders_.find(topic);
+  if (it == leaders_.end() || partition >= (int)it->second.size()) {
+    refresh_metadata();
+    it = leaders_.find(topic);
+    if (it == leaders_.end()) throw Error("kafka: unknown topic " + topic, E_UNKNOWN_TOPIC);
+    if (partition >= (int)it->second.size()) throw Error("kafka: unknown partition", E_UNKNOWN_TOPIC);
+  }
+  const int32_t leader = it->second[(size_t)partition];
+  auto ct = conns_.find(leader);
+  if (ct == conns_.end()) {
+    auto bt = brokers_.find(leader);
+    if (bt == brokers_.end()) throw Error("kafka: leader not in metadata", E_NOT_LEADER);
+    ct = conns_.emplace(leader, open({bt->second.host, bt->second.port})).first;
+  }
+  return *ct->second;
+}
+
+int64_t Client::list_offset(const std::string& topic, int partition, int64_t time) {
+  std::lock_guard<std::mutex> g(mu_);
+  W w;
+  w.i32(-1);
+  w.arr(1);
+  w.str(topic);
+  w.arr(1);
+  w.i32(partition);
+  w.i64(time);
+  const std::string resp = call(conn_for(topic, partition), API_LIST_OFFSETS, 1, w.s);
+  R r{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
+  r.arr();
+  r.str();
+  r.arr();
+  r.i32();
+  const int16_t ec = r.i16();
+  if (ec != E_NONE) throw Error("kafka: ListOffsets error " + std::to_string(ec), ec);
+  r.i64();
+  return r.i64();
+}
+
+FetchResult Client::fetch(const std::string& topic, int partition, int64_t offset, int32_t max_bytes,
+                          int32_t max_wait_ms) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (int attempt = 0;; ++attempt) {
+    W w;
+    w.i32(-1);          // replica id
+    w.i32(max_wait_ms);
+    w.i32(1);           // min bytes
+    w.i32(max_bytes);
+    w.i8(0);            // read uncommitted
+    w.arr(1);
+    w.str(topic);
+    w.arr(1);
+    w.i32(partition);
+    w.i64(offset);
+    w.i32(max_bytes);
+    FetchResult out;
+    std::string resp;
+    try {
+      resp = call(conn_for(topic, partition), API_FETCH, 4, w.s);
+    } catch (const Error& e) {
+      if (attempt >= cfg_.max_retries) throw;
+      conns_.clear();
+      any_.reset();
+      refresh_metadata();
+      continue;
+    }
+    R r{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
+    r.i32();  // throttle
+    r.arr();
+    r.str();
+    r.arr();
+    r.i32();
+    const int16_t ec = r.i16();
+    out.high_watermark = r.i64();
+    r.i64();  // last stable
+    const int32_t naborted = r.i32();
+    for (int32_t k = 0; k < naborted; ++k) {
+      r.i64();
+      r.i64();
+    }
+    auto rec = r.bytes();
+    out.error_code = ec;
+    if (ec == E_NOT_LEADER && attempt < cfg_.max_retries) {  // leadership moved: refresh and retry
+      refresh_metadata();
+      continue;
+    }
+    if (ec != E_NONE) throw Error("kafka: Fetch error " + std::to_string(ec), ec);
+    if (rec.first) decode_record_batches(rec.first, rec.second, offset, out);
+    return out;
+  }
+}
+
+int64_t Client::produce(const std::string& topic, int partition, const std::vector<Record>& recs, int16_t acks) {
+  std::lock_guard<std::mutex> g(mu_);
+  W w;
+  w.nullstr();  // transactional id
+  w.i16(acks);
+  w.i32(cfg_.timeout_ms);
+  w.arr(1);
+  w.str(topic);
+  w.arr(1);
+  w.i32(partition);
+  w.bytes(encode_record_batch(0, recs));
+  const std::string resp = call(conn_for(topic, partition), API_PRODUCE, 3, w.s);
+  if (acks == 0) return -1;
+  R r{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
+  r.arr();
+  r.str();
+  r.arr();
+  r.i32();
+  const int16_t ec = r.i16();
+  const int64_t base = r.i64();
+  if (ec != E_NONE) throw Error("kafka: Produce error " + std::to_string(ec), ec);
+  return base;
+}
+
+void Client::commit(const std::string& group, const std::string& topic, int partition, int64_t offset) {
+  std::lock_guard<std::mutex> g(mu_);
+  W w;
+  w.str(group);
+  w.i32(-1);
+  w.str("");
+  w.i64(-1);
+  w.arr(1);
+  w.str(topic);
+  w.arr(1);
+  w.i32(partition);
+  w.i64(offset);
+  w.nullstr();
+  const std::string resp = call(any_conn(), API_OFFSET_COMMIT, 2, w.s);
+  R r{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
+  r.arr();
+  r.str();
+  r.arr();
+  r.i32();
+  const int16_t ec = r.i16();
+  if (ec != E_NONE) throw Error("kafka: OffsetCommit error " + std::to_string(ec), ec);
+}
+
+int64_t Client::committed(const std::string& group, const std::string& topic, int partition) {
+  std::lock_guard<std::mutex> g(mu_);
+  W w;
+  w.str(group);
+  w.arr(1);
+  w.str(topic);
+  w.arr(1);
+  w.i32(partition);
+  const std::string resp = call(any_conn(), API_OFFSET_FETCH, 1, w.s);
+  R r{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
+  r.arr();
+  r.str();
+  r.arr();
+  r.i32();
+  const int64_t off = r.i64();
+  r.str();
+  const int16_t ec = r.i16();
+  if (ec != E_NONE) throw Error("kafka: OffsetFetch error " + std::to_string(ec), ec);
+  return off;
+}
+
+// ---------------------------------------------------------------------------
+// in-process broker
+// ---------------------------------------------------------------------------
+Broker::Broker(BrokerConfig cfg) : cfg_(std::move(cfg)) {
+  listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
+  if (listen_fd_ < 0) throw Error("broker: socket() failed");
+  int one = 1;
+  setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in addr{};
+  addr.sin_family = AF_INET;
+  addr.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  addr.sin_port = htons((uint16_t)cfg_.port);
+  if (::bind(listen_fd_, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0 || ::listen(listen_fd_, 64) != 0) {
+    ::close(listen_fd_);
+    throw Error("broker: cannot listen on 127.0.0.1:" + std::to_string(cfg_.port));
+  }
+  socklen_t len = sizeof(addr);
+  getsockname(listen_fd_, reinterpret_cast<sockaddr*>(&addr), &len);
+  port_ = ntohs(addr.sin_port);
+  running_ = true;
+  accept_thread_ = std::thread([this] { accept_loop(); });
+}
+
+Broker::~Broker() { stop(); }
+
+void Broker::stop() {
+  if (!running_.exchange(false)) return;
+  ::shutdown(listen_fd_, SHUT_RDWR);
+  ::close(listen_fd_);
+  if (accept_thread_.joinable()) accept_thread_.join();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (int fd : client_fds_) ::shutdown(fd, SHUT_RDWR);
+  }
+  for (auto& t : workers_)
+    if (t.joinable()) t.join();
+  workers_.clear();
+}
+
+void Broker::accept_loop() {
+  while (running_) {
+    const int fd = ::accept(listen_fd_, nullptr, nullptr);
+    if (fd < 0) {
+      if (!running_) break;
+      continue;
+    }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    std::lock_guard<std::mutex> g(mu_);
+    client_fds_.push_back(fd);
+    workers_.emplace_back([this, fd] { serve(fd); });
+  }
+}
+
+void Broker::create_topic(const std::string& name, int partitions) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto& t = topics_[name];
+  if ((int)t.size() < partitions) t.resize((size_t)partitions);
+}
+
+int64_t Broker::append(const std::string& topic, int partition, const std::vector<Record>& recs) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = topics_.find(topic);
+  if (it == topics_.end() || partition < 0 || partition >= (int)it->second.size())
+    throw Error("broker: unknown topic/partition", E_UNKNOWN_TOPIC);
+  Partition& p = it->second[(size_t)partition];
+  const int64_t base = p.start + (int64_t)p.log.size();
+  for (size_t k = 0; k < recs.size(); ++k) {
+    Record r = recs[k];
+    r.offset = base + (int64_t)k;
+    p.log.push_back(std::move(r));
+  }
+  if (cfg_.retention_records > 0 && (int64_t)p.log.size() > cfg_.retention_records) {
+    const int64_t drop = (int64_t)p.log.size() - cfg_.retention_records;
+    p.log.erase(p.log.begin(), p.log.begin() + drop);
+    p.start += drop;
+  }
+  return base;
+}
+
+int64_t Broker::end_offset(const std::string& topic, int partition) {
+  std::lock_guard<std::mutex> g(mu_);
+  const Partition& p = topics_.at(topic).at((size_t)partition);
+  return p.start + (int64_t)p.log.size();
+}
+
+int64_t Broker::start_offset(const std::string& topic, int partition) {
+  std::lock_guard<std::mutex> g(mu_);
+  return topics_.at(topic).at((size_t)partition).start;
+}
+
+std::vector<Record> Broker::read(const std::string& topic, int partition, int64_t offset, size_t max_records) {
+  std::lock_guard<std::mutex> g(mu_);
+  const Partition& p = topics_.at(topic).at((size_t)partition);
+  std::vector<Record> out;
+  for (int64_t o = std::max(offset, p.start); o < p.start + (int64_t)p.log.size() && out.size() < max_records; ++o)
+    out.push_back(p.log[(size_t)(o - p.start)]);
+  return out;
+}
+
+void Broker::serve(int fd) {
+  bool authed = cfg_.sasl_username.empty();
+  bool handshaken = false;
+  std::string buf;
+  while (running_) {
+    uint8_t hdr[4];
+    size_t got = 0;
+    while (got < 4) {
+      const ssize_t k = ::recv(fd, hdr + got, 4 - got, 0);
+      if (k <= 0) goto done;
+      got += (size_t)k;
+    }
+    {
+      const int32_t size = (int32_t)(((uint32_t)hdr[0] << 24) | ((uint32_t)hdr[1] << 16) | ((uint32_t)hdr[2] << 8) | hdr[3]);
+      if (size < 8 || size > (1 << 28)) goto done;
+      buf.resize((size_t)size);
+      got = 0;
+      while (got < (size_t)size) {
+        const ssize_t k = ::recv(fd, &buf[got], (size_t)size - got, 0);
+        if (k <= 0) goto done;
+        got += (size_t)k;
+      }
+      std::string resp_body;
+      int32_t corr = 0;
+      try {
+        R r{reinterpret_cast<const uint8_t*>(buf.data()), buf.size()};
+        const int16_t api = r.i16();
+        const int16_t ver = r.i16();
+        corr = r.i32();
+        r.str();  // client id
+        resp_body = handle(api, ver, r.p + r.i, r.n - r.i, authed, handshaken);
+      } catch (const std::exception&) {
+        goto done;  // malformed request: drop the connection (like a real broker)
+      }
+      W w;
+      w.i32((int32_t)(resp_body.size() + 4));
+      w.i32(corr);
+      w.s += resp_body;
+      size_t off = 0;
+      while (off < w.s.size()) {
+        const ssize_t k = ::send(fd, w.s.data() + off, w.s.size() - off, MSG_NOSIGNAL);
+        if (k <= 0) goto done;
+        off += (size_t)k;
+      }
+    }
+  }
+done:
+  ::close(fd);
+  std::lock_guard<std::mutex> g(mu_);
+  client_fds_.erase(std::remove(client_fds_.begin(), client_fds_.end(), fd), client_fds_.end());
+}
+
+std::string Broker::handle(int16_t api, int16_t ver, const uint8_t* body, size_t n, bool& authed,
+                           bool& handshaken) {
+  R r{body, n};
+  W w;
+  if (api == API_API_VERSIONS) {
+    w.i16(E_NONE);
+    const int16_t apis[][3] = {{API_PRODUCE, 3, 3}, {API_FETCH, 4, 4}, {API_LIST_OFFSETS, 1, 1},
+                               {API_METADATA, 1, 1}, {API_OFFSET_COMMIT, 2, 2}, {API_OFFSET_FETCH, 1, 1},
+                               {API_FIND_COORDINATOR, 1, 1}, {API_SASL_HANDSHAKE, 1, 1},
+                               {API_API_VERSIONS, 0, 0}, {API_SASL_AUTH, 0, 0}};
+    w.arr(10);
+    for (auto& a : apis) {
+      w.i16(a[0]);
+      w.i16(a[1]);
+      w.i16(a[2]);
+    }
+    return w.s;
+  }
+  if (api == API_SASL_HANDSHAKE) {
+    const std::string mech = r.str();
+    const bool ok = mech == "PLAIN";
+    handshaken = ok;
+    w.i16(ok ? E_NONE : E_UNSUPPORTED_SASL);
+    w.arr(1);
+    w.str("PLAIN");
+    return w.s;
+  }
+  if (api == API_SASL_AUTH) {
+    auto tok = r.bytes();
+    std::string t(reinterpret_cast<const char*>(tok.first), tok.second);
+    // [authzid] \0 user \0 pass
+    const auto a = t.find('\0');
+    const auto b = a == std::string::npos ? std::string::npos : t.find('\0', a + 1);
+    bool ok = false;
+    if (handshaken && b != std::string::npos)
+      ok = t.substr(a + 1, b - a - 1) == cfg_.sasl_username && t.substr(b + 1) == cfg_.sasl_password;
+    authed = authed || ok;
+    w.i16(handshaken ? (ok ? E_NONE : E_SASL_AUTH_FAILED) : E_ILLEGAL_SASL_STATE);
+    w.nullstr();
+    w.bytes("");
+    return w.s;
+  }
+  if (!authed) throw Error("broker: unauthenticated request");
+  std::lock_guard<std::mutex> g(mu_);
+  switch (api) {
+    case API_METADATA: {
+      const int32_t nt = r.i32();
+      std::vector<std::string> want;
+      for (int32_t i = 0; i < nt; ++i) want.push_back(r.str());
+      w.arr(1);
+      w.i32(0);
+      w.str("127.0.0.1");
+      w.i32(port_);
+      w.nullstr();
+      w.i32(0);  // controller
+      std::vector<std::string> names;
+      if (nt < 0) for (const auto& kv : topics_) names.push_back(kv.first);
+      else names = want;
+      w.arr((int32_t)names.size());
+      for (const auto& name : names) {
+        auto it = topics_.find(name);
+        w.i16(it == topics_.end() ? E_UNKNOWN_TOPIC : E_NONE);
+        w.str(name);
+        w.i8(0);
+        const int32_t np = it == topics_.end() ? 0 : (int32_t)it->second.size();
+        w.arr(np);
+        for (int32_t p = 0; p < np; ++p) {
+          w.i16(E_NONE);
+          w.i32(p);
+          w.i32(0);
+          w.arr(1);
+          w.i32(0);
+          w.arr(1);
+          w.i32(0);
+        }
+      }
+      return w.s;
+    }
+    case API_LIST_OFFSETS: {
+      r.i32();
+      const int32_t nt = r.arr();
+      w.arr(nt);
+      for (int32_t i = 0; i < nt; ++i) {
+        const std::string name = r.str();
+        const int32_t np = r.arr();
+        w.str(name);
+        w.arr(np);
+        for (int32_t k = 0; k < np; ++k) {
+          const int32_t p = r.i32();
+          const int64_t t = r.i64();
+          auto it = topics_.find(name);
+          w.i32(p);
+          if (it == topics_.end() || p < 0 || p >= (int32_t)it->second.size()) {
+            w.i16(E_UNKNOWN_TOPIC);
+            w.i64(-1);
+            w.i64(-1);
+            continue;
+          }
+          const Partition& part = it->second[(size_t)p];
+          w.i16(E_NONE);
+          w.i64(-1);
+          w.i64(t == -2 ? part.start : part.start + (int64_t)part.log.size());
+        }
+      }
+      return w.s;
+    }
+    case API_FETCH: {
+      const uint64_t nth = ++fetches_;
+      r.i32();
+      const int32_t max_wait = r.i32();
+      r.i32();
+      r.i32();
+      r.i8();
+      const int32_t nt = r.arr();
+      w.i32(0);
+      w.arr(nt);
+      for (int32_t i = 0; i < nt; ++i) {
+        const std::string name = r.str();
+        const int32_t np = r.arr();
+        w.str(name);
+        w.arr(np);
+        for (int32_t k = 0; k < np; ++k) {
+          const int32_t p = r.i32();
+          const int64_t off = r.i64();
+          const int32_t pmax = r.i32();
+          w.i32(p);
+          auto it = topics_.find(name);
+          const int fe = fail_every_.load();
+          if (fe > 0 && nth % (uint64_t)fe == 0) {
+            ++failures_;
+            w.i16(E_NOT_LEADER);
+            w.i64(-1);
+            w.i64(-1);
+            w.i32(0);
+            w.i32(-1);
+            continue;
+          }
+          if (it == topics_.end() || p < 0 || p >= (int32_t)it->second.size()) {
+            w.i16(E_UNKNOWN_TOPIC);
+            w.i64(-1);
+            w.i64(-1);
+            w.i32(0);
+            w.i32(-1);
+            continue;
+          }
+          const Partition& part = it->second[(size_t)p];
+          const int64_t end = part.start + (int64_t)part.log.size();
+          if (off < part.start || off > end) {
+            w.i16(E_OFFSET_OUT_OF_RANGE);
+            w.i64(end);
+            w.i64(end);
+            w.i32(0);
+            w.i32(-1);
+            continue;
+          }
+          std::string batches;
+          int64_t o = off;
+          while (o < end && (batches.empty() || (int64_t)batches.size() < pmax)) {
+            std::vector<Record> chunk;
+            size_t bytes = 0;
+            while (o < end && chunk.size() < 1024 && (batches.size() + bytes < (size_t)pmax || chunk.empty())) {
+              const Record& src = part.log[(size_t)(o - part.start)];
+              bytes += src.value.size() + src.key.size() + 16;
+              chunk.push_back(src);
+              ++o;
+            }
+            batches += encode_record_batch(chunk.front().offset, chunk);
+          }
+          w.i16(E_NONE);
+          w.i64(end);
+          w.i64(end);
+          w.i32(0);  // no aborted transactions
+          w.bytes(batches);
+        }
+      }
+      const int dm = delay_ms_.load();
+      if (dm > 0 || (max_wait > 0 && false)) std::this_thread::sleep_for(std::chrono::milliseconds(dm));
+      return w.s;
+    }
+    case API_PRODUCE: {
+      r.str();
+      const int16_t acks = r.i16();
+      (void)acks;
+      r.i32();
+      const int32_t nt = r.arr();
+      w.arr(nt);
+      for (int32_t i = 0; i < nt; ++i) {
+        const std::string name = r.str();
+        const int32_t np = r.arr();
+        w.str(name);
+        w.arr(np);
+        for (int32_t k = 0; k < np; ++k) {
+          const int32_t p = r.i32();
+          auto recs = r.bytes();
+          FetchResult tmp;
+          decode_record_batches(recs.first, recs.second, INT64_MIN, tmp);
+          auto it = topics_.find(name);
+          w.i32(p);
+          if (it == topics_.end() || p < 0 || p >= (int32_t)it->second.size()) {
+            w.i16(E_UNKNOWN_TOPIC);
+            w.i64(-1);
+            w.i64(-1);
+            continue;
+          }
+          Partition& part = it->second[(size_t)p];
+          const int64_t base = part.start + (int64_t)part.log.size();
+          for (size_t q = 0; q < tmp.size(); ++q) {
+            Record rec;
+            rec.offset = base + (int64_t)q;
+            rec.timestamp = tmp.timestamps[q];
+            rec.key = tmp.keys[q];
+            rec.key_null = tmp.keys[q].empty();
+            rec.value.assign(tmp.values.data() + tmp.value_offsets[q],
+                             (size_t)(tmp.value_offsets[q + 1] - tmp.value_offsets[q]));
+            part.log.push_back(std::move(rec));
+          }
+          if (cfg_.retention_records > 0 && (int64_t)part.log.size() > cfg_.retention_records) {
+            const int64_t drop = (int64_t)part.log.size() - cfg_.retention_records;
+            part.log.erase(part.log.begin(), part.log.begin() + drop);
+            part.start += drop;
+          }
+          w.i16(E_NONE);
+          w.i64(base);
+          w.i64(-1);
+        }
+      }
+      w.i32(0);  // throttle
+      return w.s;
+    }
+    case API_FIND_COORDINATOR: {
+      r.str();
+      w.i32(0);
+      w.i16(E_NONE);
+      w.nullstr();
+      w.i32(0);
+      w.str("127.0.0.1");
+      w.i32(port_);
+      return w.s;
+    }
+    case API_OFFSET_COMMIT: {
+      const std::string group = r.str();
+      r.i32();
+      r.str();
+      r.i64();
+      const int32_t nt = r.arr();
+      w.arr(nt);
+      for (int32_t i = 0; i < nt; ++i) {
+        const std::string name = r.str();
+        const int32_t np = r.arr();
+        w.str(name);
+        w.arr(np);
+        for (int32_t k = 0; k < np; ++k) {
+          const int32_t p = r.i32();
+          const int64_t off = r.i64();
+          r.str();
+          group_offsets_[group + "/" + name + "/" + std::to_string(p)] = off;
+          w.i32(p);
+          w.i16(E_NONE);
+        }
+      }
+      return w.s;
+    }
+    case API_OFFSET_FETCH: {
+      const std::string group = r.str();
+      const int32_t nt = r.arr();
+      w.arr(nt);
+      for (int32_t i = 0; i < nt; ++i) {
+        const std::string name = r.str();
+        const int32_t np = r.arr();
+        w.str(name);
+        w.arr(np);
+        for (int32_t k = 0; k < np; ++k) {
+          const int32_t p = r.i32();
+          auto it = group_offsets_.find(group + "/" + name + "/" + std::to_string(p));
+          w.i32(p);
+          w.i64(it == group_offsets_.end() ? -1 : it->second);
+          w.nullstr();
+          w.i16(E_NONE);
+        }
+      }
+      return w.s;
+    }
+    default:
+      (void)ver;
+      throw Error("broker: unsupported api " + std::to_string(api));
+  }
+}
+
+}  // namespace kafka
+}  // namespace sml

@@ -1,0 +1,161 @@
+// Kafka wire protocol: client + in-process broker.
+//
+// The reference consumes Kafka through tensorflow-io's KafkaDataset (C++ over
+// librdkafka, `KafkaDataset(["topic:0:offset"], servers, group, eof, config_global)`,
+// AUTOENCODER-TensorFlow-IO-Kafka/cardata-v3.py:44-47) and produces results with
+// KafkaOutputSequence (cardata-v3.py:238-252).  librdkafka is not available here,
+// so this is a from-scratch implementation of the protocol subset those paths use:
+//
+//   ApiVersions v0, Metadata v1, ListOffsets v1, Fetch v4, Produce v3,
+//   SaslHandshake v1 + SaslAuthenticate v0 (SASL/PLAIN, as in the reference's
+//   `security.protocol=sasl_plaintext, sasl.mechanisms=PLAIN`),
+//   FindCoordinator v1, OffsetCommit v2, OffsetFetch v1 (consumer-group offsets),
+//   record batches v2 (magic 2, CRC-32C, uncompressed).
+//
+// `Broker` is an in-process partitioned append-only log that serves the same
+// protocol on 127.0.0.1 so the client is always exercised over real sockets.  It
+// has fault-injection knobs (failed / delayed fetches) for the recovery tests
+// (SURVEY.md 5.3).
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace sml {
+namespace kafka {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(const std::string& m, int c = -1) : std::runtime_error(m), code(c) {}
+};
+
+uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc = 0);
+
+struct Record {
+  int64_t offset = 0;
+  int64_t timestamp = 0;
+  std::string key;
+  std::string value;
+  bool key_null = true;
+};
+
+// Flat batch of fetched records: values back to back (value i spans
+// [value_offsets[i], value_offsets[i+1])), plus per-record metadata.
+struct FetchResult {
+  std::string values;
+  std::vector<int64_t> value_offsets{0};
+  std::vector<int64_t> offsets;
+  std::vector<int64_t> timestamps;
+  std::vector<std::string> keys;
+  int64_t high_watermark = -1;
+  int error_code = 0;
+  size_t size() const { return offsets.size(); }
+};
+
+// record batch v2 codec
+std::string encode_record_batch(int64_t base_offset, const std::vector<Record>& recs);
+void decode_record_batches(const uint8_t* p, size_t n, int64_t min_offset, FetchResult& out);
+
+struct ClientConfig {
+  std::string client_id = "streamml";
+  std::string sasl_mechanism;  // "" or "PLAIN"
+  std::string sasl_username, sasl_password;
+  int timeout_ms = 30000;
+  int max_retries = 5;
+};
+
+class Connection;
+
+class Client {
+ public:
+  Client(const std::string& bootstrap, ClientConfig cfg);
+  ~Client();
+
+  std::map<std::string, int> partitions();                      // topic -> #partitions
+  int64_t list_offset(const std::string& topic, int partition, int64_t time);  // -2 earliest, -1 latest
+  FetchResult fetch(const std::string& topic, int partition, int64_t offset, int32_t max_bytes = 1 << 20,
+                    int32_t max_wait_ms = 100);
+  int64_t produce(const std::string& topic, int partition, const std::vector<Record>& recs, int16_t acks = 1);
+  void commit(const std::string& group, const std::string& topic, int partition, int64_t offset);
+  int64_t committed(const std::string& group, const std::string& topic, int partition);
+  void refresh_metadata();
+  uint64_t bytes_received() const { return bytes_rx_; }
+
+ private:
+  struct BrokerAddr {
+    std::string host;
+    int port;
+  };
+  ClientConfig cfg_;
+  std::vector<BrokerAddr> bootstrap_;
+  std::map<int32_t, BrokerAddr> brokers_;
+  std::map<std::string, std::vector<int32_t>> leaders_;  // topic -> leader per partition
+  std::map<int32_t, std::unique_ptr<Connection>> conns_;
+  std::unique_ptr<Connection> any_;
+  int32_t corr_ = 1;
+  uint64_t bytes_rx_ = 0;
+  std::mutex mu_;
+
+  Connection& conn_for(const std::string& topic, int partition);
+  Connection& any_conn();
+  std::unique_ptr<Connection> open(const BrokerAddr& a);
+  std::string call(Connection& c, int16_t api, int16_t ver, const std::string& body);
+};
+
+struct BrokerConfig {
+  int port = 0;  // 0 = ephemeral
+  std::string sasl_username, sasl_password;  // empty = no auth
+  int64_t retention_records = -1;           // -1 = unbounded
+};
+
+class Broker {
+ public:
+  explicit Broker(BrokerConfig cfg);
+  ~Broker();
+  int port() const { return port_; }
+  void create_topic(const std::string& name, int partitions);
+  int64_t append(const std::string& topic, int partition, const std::vector<Record>& recs);
+  int64_t end_offset(const std::string& topic, int partition);
+  int64_t start_offset(const std::string& topic, int partition);
+  std::vector<Record> read(const std::string& topic, int partition, int64_t offset, size_t max_records);
+  // fault injection: every `fail_every`-th fetch returns NOT_LEADER_OR_FOLLOWER;
+  // every fetch is delayed by `delay_ms`.
+  void set_faults(int fail_every, int delay_ms) {
+    fail_every_ = fail_every;
+    delay_ms_ = delay_ms;
+  }
+  uint64_t fetch_count() const { return fetches_; }
+  uint64_t injected_failures() const { return failures_; }
+  void stop();
+
+ private:
+  struct Partition {
+    std::vector<Record> log;
+    int64_t start = 0;  // offset of log[0]
+  };
+  BrokerConfig cfg_;
+  int listen_fd_ = -1;
+  int port_ = 0;
+  std::atomic<bool> running_{false};
+  std::thread accept_thread_;
+  std::vector<std::thread> workers_;
+  std::vector<int> client_fds_;
+  std::mutex mu_;
+  std::map<std::string, std::vector<Partition>> topics_;
+  std::map<std::string, int64_t> group_offsets_;  // "group/topic/partition" -> offset
+  std::atomic<int> fail_every_{0}, delay_ms_{0};
+  std::atomic<uint64_t> fetches_{0}, failures_{0};
+
+  void accept_loop();
+  void serve(int fd);
+  std::string handle(int16_t api, int16_t ver, const uint8_t* body, size_t n, bool& authed, bool& handshaken);
+};
+
+}  // namespace kafka
+}  // namespace sml
