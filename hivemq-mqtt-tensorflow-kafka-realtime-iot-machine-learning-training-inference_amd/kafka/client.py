@@ -1,0 +1,161 @@
+"""Native Kafka client / in-process broker wrappers and config parsing."""
+from __future__ import annotations
+
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from ..ops._ext import load_io
+
+
+def _io():
+    return load_io()
+
+
+class KafkaError(RuntimeError):
+    pass
+
+
+def parse_config(config: Optional[Sequence[str]]) -> Dict[str, str]:
+    """librdkafka ``key=value`` strings (cardata-v3.py:7-15) -> dict."""
+    out: Dict[str, str] = {}
+    for item in config or []:
+        if "=" not in item:
+            raise ValueError(f"bad config entry {item!r} (expected key=value)")
+        k, v = item.split("=", 1)
+        out[k.strip()] = v.strip()
+    return out
+
+
+def parse_topic_spec(spec: str) -> Tuple[str, int, int]:
+    """``"topic:partition:offset"`` (tfio convention) -> (topic, partition, offset)."""
+    parts = spec.split(":")
+    topic = parts[0]
+    partition = int(parts[1]) if len(parts) > 1 and parts[1] != "" else 0
+    offset = int(parts[2]) if len(parts) > 2 and parts[2] != "" else 0
+    return topic, partition, offset
+
+
+class FakeBroker:
+    """In-process partitioned append-only log serving the Kafka protocol on 127.0.0.1."""
+
+    def __init__(self, port: int = 0, sasl_username: str = "", sasl_password: str = "",
+                 retention_records: int = -1):
+        self._b = _io().KafkaBroker(port, sasl_username, sasl_password, retention_records)
+
+    @property
+    def port(self) -> int:
+        return self._b.port
+
+    @property
+    def address(self) -> str:
+        return f"127.0.0.1:{self.port}"
+
+    def create_topic(self, name: str, partitions: int = 1) -> None:
+        self._b.create_topic(name, partitions)
+
+    def append(self, topic: str, partition: int, values: Sequence[bytes], keys=None, timestamps=None) -> int:
+        return self._b.append(topic, partition, list(values), None if keys is None else list(keys),
+                              None if timestamps is None else [int(t) for t in timestamps])
+
+    def append_buffer(self, topic: str, partition: int, buf: bytes, offsets, timestamp: int = 0) -> int:
+        import numpy as np
+        return self._b.append_buffer(topic, partition, buf, np.ascontiguousarray(offsets, dtype=np.int64), timestamp)
+
+    def end_offset(self, topic: str, partition: int = 0) -> int:
+        return self._b.end_offset(topic, partition)
+
+    def start_offset(self, topic: str, partition: int = 0) -> int:
+        return self._b.start_offset(topic, partition)
+
+    def read(self, topic: str, partition: int = 0, offset: int = 0, max_records: int = 1 << 30):
+        return self._b.read(topic, partition, offset, max_records)
+
+    def set_faults(self, fail_every: int = 0, delay_ms: int = 0) -> None:
+        self._b.set_faults(fail_every, delay_ms)
+
+    @property
+    def fetch_count(self) -> int:
+        return self._b.fetch_count
+
+    @property
+    def injected_failures(self) -> int:
+        return self._b.injected_failures
+
+    def stop(self) -> None:
+        self._b.stop()
+
+
+_FAKES: Dict[str, FakeBroker] = {}
+_FAKES_LOCK = threading.Lock()
+
+
+def fake_broker(name: str = "default", **kw) -> FakeBroker:
+    """Process-wide named in-process broker (created on first use)."""
+    with _FAKES_LOCK:
+        b = _FAKES.get(name)
+        if b is None:
+            b = FakeBroker(**kw)
+            _FAKES[name] = b
+        return b
+
+
+def resolve_servers(servers: str) -> str:
+    if servers.startswith("fake://"):
+        name = servers[len("fake://"):] or "default"
+        return fake_broker(name).address
+    return servers
+
+
+class KafkaClient:
+    """Thin wrapper over the native client; SASL/PLAIN taken from librdkafka-style config."""
+
+    def __init__(self, servers: str, config: Optional[Sequence[str]] = None, client_id: str = "streamml",
+                 timeout_ms: int = 30000):
+        cfg = parse_config(config)
+        proto = cfg.get("security.protocol", "plaintext").lower()
+        mech = ""
+        if proto in ("sasl_plaintext", "sasl_ssl"):
+            if proto == "sasl_ssl":
+                raise KafkaError("TLS is not supported by the native client")
+            mech = cfg.get("sasl.mechanisms", cfg.get("sasl.mechanism", "PLAIN")).upper()
+            if mech != "PLAIN":
+                raise KafkaError(f"SASL mechanism {mech} not supported (PLAIN only)")
+        self.servers = resolve_servers(servers)
+        self._c = _io().KafkaClient(self.servers, cfg.get("client.id", client_id), mech,
+                                    cfg.get("sasl.username", ""), cfg.get("sasl.password", ""),
+                                    int(cfg.get("socket.timeout.ms", timeout_ms)))
+
+    @property
+    def native(self):
+        return self._c
+
+    def partitions(self) -> Dict[str, int]:
+        return self._c.partitions()
+
+    def earliest(self, topic: str, partition: int = 0) -> int:
+        return self._c.list_offset(topic, partition, -2)
+
+    def latest(self, topic: str, partition: int = 0) -> int:
+        return self._c.list_offset(topic, partition, -1)
+
+    def fetch(self, topic: str, partition: int, offset: int, max_bytes: int = 1 << 20, max_wait_ms: int = 100):
+        return self._c.fetch(topic, partition, offset, max_bytes, max_wait_ms)
+
+    def fetch_decode(self, codec, topic: str, partition: int, offset: int, max_bytes: int = 1 << 20,
+                     max_wait_ms: int = 100, framing: bool = True):
+        return self._c.fetch_decode(codec.native, topic, partition, offset, max_bytes, max_wait_ms, framing)
+
+    def produce(self, topic: str, partition: int, values: Sequence[bytes], keys=None, timestamps=None,
+                acks: int = 1) -> int:
+        return self._c.produce(topic, partition, list(values), None if keys is None else list(keys),
+                               None if timestamps is None else [int(t) for t in timestamps], acks)
+
+    def commit(self, group: str, topic: str, partition: int, offset: int) -> None:
+        self._c.commit(group, topic, partition, offset)
+
+    def committed(self, group: str, topic: str, partition: int) -> int:
+        return self._c.committed(group, topic, partition)
+
+    @property
+    def bytes_received(self) -> int:
+        return self._c.bytes_received

@@ -1,0 +1,140 @@
+"""``KafkaDataset``: bounded/unbounded partition readers with tfio semantics.
+
+Reference call (cardata-v3.py:44-47):
+``KafkaDataset(["SENSOR_DATA_S_AVRO:0:0"], servers=..., group="cardata-autoencoder",
+eof=True, config_global=kafka_config)``.  ``eof=True`` stops at the partition end
+observed when iteration starts, so every ``fit`` epoch re-reads the same bounded
+stream (python-scripts/README.md:116).  Differences by design:
+
+* iteration yields *batches* of records (values + offsets) fetched in one
+  network round trip instead of one tf.string per message; ``decode=True`` with a
+  codec returns the decoded columnar arrays directly (no per-message Python);
+* consumed offsets can be committed to the group (``commit=True``) so a
+  restarted job resumes where it stopped (SURVEY.md 5.3 recovery story);
+* several ``topic:partition:offset`` specs are read round-robin (the reference
+  hard-codes partition 0, cardata-v3.py:46).
+"""
+from __future__ import annotations
+
+import time
+from typing import Iterator, List, Optional, Sequence
+
+import numpy as np
+
+from .client import KafkaClient, parse_topic_spec
+
+
+class KafkaDataset:
+    def __init__(self, topics: Sequence[str], servers: str = "fake://", group: Optional[str] = None,
+                 eof: bool = True, config_global: Optional[Sequence[str]] = None, codec=None,
+                 max_bytes: int = 4 << 20, max_wait_ms: int = 100, framing: bool = True,
+                 commit: bool = False, resume: bool = False, idle_timeout_s: Optional[float] = None):
+        self.specs = [parse_topic_spec(t) for t in topics]
+        self.servers = servers
+        self.group = group
+        self.eof = eof
+        self.config = list(config_global or [])
+        self.codec = codec
+        self.max_bytes = int(max_bytes)
+        self.max_wait_ms = int(max_wait_ms)
+        self.framing = framing
+        self.commit = commit and group is not None
+        self.resume = resume and group is not None
+        self.idle_timeout_s = idle_timeout_s
+        self._client: Optional[KafkaClient] = None
+        self.records_read = 0
+        self.bytes_read = 0
+
+    @property
+    def client(self) -> KafkaClient:
+        if self._client is None:
+            self._client = KafkaClient(self.servers, self.config)
+        return self._client
+
+    def _start_offset(self, topic: str, partition: int, offset: int) -> int:
+        c = self.client
+        if self.resume:
+            got = c.committed(self.group, topic, partition)
+            if got >= 0:
+                return got
+        if offset < 0:  # -1 latest, -2 earliest (librdkafka convention)
+            return c.latest(topic, partition) if offset == -1 else c.earliest(topic, partition)
+        return max(offset, c.earliest(topic, partition))
+
+    def __iter__(self) -> Iterator[dict]:
+        c = self.client
+        cursors: List[List] = []
+        for topic, partition, offset in self.specs:
+            start = self._start_offset(topic, partition, offset)
+            end = c.latest(topic, partition) if self.eof else None
+            cursors.append([topic, partition, start, end])
+        last_data = time.monotonic()
+        while cursors:
+            progressed = False
+            for cur in list(cursors):
+                topic, partition, pos, end = cur
+                if end is not None and pos >= end:
+                    cursors.remove(cur)
+                    continue
+                if self.codec is not None:
+                    batch = c.fetch_decode(self.codec, topic, partition, pos, self.max_bytes, self.max_wait_ms,
+                                           self.framing)
+                    offs = batch["offsets"]
+                    self.bytes_read += int(batch["bytes"])
+                    batch["text"] = dict(zip(self.codec.text_fields, batch["text"]))
+                    batch["text_null"] = dict(zip(self.codec.text_fields, batch["text_null"]))
+                else:
+                    batch = c.fetch(topic, partition, pos, self.max_bytes, self.max_wait_ms)
+                    offs = batch["offsets"]
+                    self.bytes_read += len(batch["values"])
+                if len(offs) == 0:
+                    continue
+                if end is not None and offs[-1] >= end:  # trim to the eof boundary
+                    keep = int(np.searchsorted(offs, end))
+                    batch = _trim(batch, keep)
+                    offs = batch["offsets"]
+                    if keep == 0:
+                        cursors.remove(cur)
+                        continue
+                cur[2] = int(offs[-1]) + 1
+                self.records_read += len(offs)
+                progressed = True
+                batch["topic"], batch["partition"] = topic, partition
+                yield batch
+                if self.commit:
+                    c.commit(self.group, topic, partition, cur[2])
+            if progressed:
+                last_data = time.monotonic()
+            elif self.idle_timeout_s is not None and time.monotonic() - last_data > self.idle_timeout_s:
+                return
+
+    def messages(self) -> Iterator[bytes]:
+        """Per-message iteration (the tfio element view); slow path for small streams."""
+        for b in self:
+            if "values" in b:
+                vo = b["value_offsets"]
+                for i in range(len(vo) - 1):
+                    yield b["values"][vo[i]:vo[i + 1]]
+            else:
+                raise TypeError("messages() needs a dataset without a codec")
+
+
+def _trim(batch: dict, keep: int) -> dict:
+    out = dict(batch)
+    if "values" in batch:
+        vo = batch["value_offsets"]
+        out["values"] = batch["values"][:vo[keep]]
+        out["value_offsets"] = vo[:keep + 1]
+        out["timestamps"] = batch["timestamps"][:keep]
+    else:
+        for k in ("numeric", "null", "schema_id", "ok"):
+            out[k] = batch[k][:keep]
+        if "numeric64" in batch:
+            out["numeric64"] = batch["numeric64"][:keep]
+        out["text"] = {k: v[:keep] for k, v in batch["text"].items()} if isinstance(batch["text"], dict) else \
+            [v[:keep] for v in batch["text"]]
+        out["text_null"] = {k: v[:keep] for k, v in batch["text_null"].items()} \
+            if isinstance(batch["text_null"], dict) else [v[:keep] for v in batch["text_null"]]
+    out["offsets"] = batch["offsets"][:keep]
+    out["keys"] = batch["keys"][:keep]
+    return out
