@@ -81,11 +81,18 @@ def build_c(verbose: bool = False, force: bool = False) -> str:
                          f"-I{inc}", "-Wno-unused-result", "-munsafe-fp-atomics",
                          # MFMA results straight into VGPRs: no v_accvgpr_read per use
                          "-mllvm", "-amdgpu-mfma-vgpr-form"])
+    # host runtime pieces that use the HIP runtime API (no device code, no torch)
+    for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
+        obj = os.path.join(BUILD, "rt_" + os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _newer([src] + hdrs + glob.glob(os.path.join(CSRC, "runtime", "*.h")), obj):
+            jobs.append([CXX, "-O2", "-std=c++17", "-fPIC", "-c", src, "-o", obj, f"-I{inc}", f"-I{ROCM}/include",
+                         "-D__HIP_PLATFORM_AMD__=1", "-Wall"])
     bind = os.path.join(CSRC, "torch_bind.cpp")
     bind_obj = os.path.join(BUILD, "torch_bind.o")
     objs.append(bind_obj)
     abi = "1" if torch.compiled_with_cxx11_abi() else "0"
-    if force or _newer([bind] + hdrs, bind_obj):
+    if force or _newer([bind] + hdrs + glob.glob(os.path.join(CSRC, "runtime", "*.h")), bind_obj):
         cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-c", bind, "-o", bind_obj, f"-I{inc}", f"-I{_py_include()}",
                f"-I{ROCM}/include", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",

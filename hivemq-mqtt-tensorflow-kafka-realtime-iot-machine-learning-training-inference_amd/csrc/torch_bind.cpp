@@ -9,6 +9,10 @@
 #include <hip/hip_runtime.h>
 
 #include "sml_ops.h"
+#include "../runtime/ring.h"
+
+#include <pybind11/numpy.h>
+#include <cstring>
 
 namespace {
 
@@ -146,6 +150,45 @@ at::Tensor lane_xor_probe(const at::Tensor& like) {
   return out;
 }
 
+// Python face of the pinned staging ring: fill (host memcpy, GIL released),
+// submit (hipMemcpyAsync on the ring's copy stream), wait / release against the
+// caller's current HIP stream.
+struct RingPy {
+  std::unique_ptr<sml::PinnedRing> r;
+  int device;
+  RingPy(int slots, int64_t slot_bytes, int dev) : device(dev) {
+    c10::hip::HIPGuard guard(dev);
+    r = std::make_unique<sml::PinnedRing>(slots, (size_t)slot_bytes, dev);
+  }
+  int64_t fill(int slot, py::array arr) {
+    py::buffer_info bi = arr.request();
+    if (!(arr.flags() & py::array::c_style)) throw std::invalid_argument("fill: array must be C-contiguous");
+    const size_t bytes = (size_t)bi.size * (size_t)bi.itemsize;
+    if (bytes > r->slot_bytes()) throw std::invalid_argument("fill: array larger than a ring slot");
+    const void* src = bi.ptr;
+    {
+      py::gil_scoped_release rel;
+      void* dst = r->host(slot);
+      std::memcpy(dst, src, bytes);
+    }
+    return (int64_t)bytes;
+  }
+  void submit(int slot, const at::Tensor& dst, int64_t bytes) {
+    TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "submit: dst must be a contiguous device tensor");
+    TORCH_CHECK(bytes <= (int64_t)(dst.numel() * dst.element_size()), "submit: dst too small");
+    c10::hip::HIPGuard guard(device);
+    r->submit(slot, dst.data_ptr(), (size_t)bytes);
+  }
+  void wait(int slot) {
+    c10::hip::HIPGuard guard(device);
+    r->wait(slot, c10::hip::getCurrentHIPStream(device).stream());
+  }
+  void release(int slot) {
+    c10::hip::HIPGuard guard(device);
+    r->release(slot, c10::hip::getCurrentHIPStream(device).stream());
+  }
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -163,6 +206,15 @@ PYBIND11_MODULE(_C, m) {
         py::arg("iter"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("gscale"),
         py::arg("metrics"), py::arg("flags"), py::arg("cursor") = py::none(), py::arg("cursor_step") = 0,
         py::arg("cursor_ring") = 0);
+  py::class_<RingPy>(m, "PinnedRing")
+      .def(py::init<int, int64_t, int>(), py::arg("slots"), py::arg("slot_bytes"), py::arg("device"))
+      .def("fill", &RingPy::fill, py::arg("slot"), py::arg("array"))
+      .def("submit", &RingPy::submit, py::arg("slot"), py::arg("dst"), py::arg("bytes"))
+      .def("wait", &RingPy::wait, py::arg("slot"))
+      .def("release", &RingPy::release, py::arg("slot"))
+      .def_property_readonly("slots", [](const RingPy& r) { return r.r->slots(); })
+      .def_property_readonly("slot_bytes", [](const RingPy& r) { return (int64_t)r.r->slot_bytes(); })
+      .def_property_readonly("bytes_copied", [](const RingPy& r) { return (uint64_t)r.r->bytes_copied(); });
   m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),
         py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("recon"), py::arg("score"), py::arg("flag"),

@@ -1,0 +1,386 @@
+"""Dense autoencoder with a Keras-like API (compile / fit / predict / evaluate / save / load).
+
+Reference model (AUTOENCODER-TensorFlow-IO-Kafka/cardata-v3.py:176-222):
+
+    Input(18) -> Dense(14, tanh, activity_regularizer=L1(1e-7)) -> Dense(7, relu)
+              -> Dense(7, tanh) -> Dense(18, relu)
+    compile(metrics=['accuracy'], loss='mean_squared_error', optimizer='adam')
+    fit(zip((x, x)).batch(100).take(100), epochs=20, verbose=2); save('model1.h5')
+
+(the creditcard notebooks use the same stack with D = 30).  On a ROCm device
+every step runs the fused HIP train kernel (:mod:`streamml.ops.ae`); on CPU the
+torch reference (:mod:`streamml.models.reference`) with identical semantics.
+Raw sensor rows can be fed directly: ``input_normalizer="cardata"`` applies the
+reference ``normalize_fn`` inside the kernel's first load.
+"""
+from __future__ import annotations
+
+import math
+import sys
+import time
+from typing import List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from ..ckpt import h5 as ckh5
+from ..data.cardata import normalize_affine
+from ..nn import keras_config as kc
+from ..nn.callbacks import Callback, History
+from ..ops.ae import AESpec, FusedAE
+from .reference import TorchAE, init_dense_weights
+
+
+def _resolve_device(device) -> torch.device:
+    if device in (None, "auto"):
+        return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    return torch.device(device)
+
+
+class Autoencoder:
+    def __init__(self, input_dim: int = 18, encoding_dim: int = 14, hidden_dim: int = 7,
+                 activations: Sequence[str] = ("tanh", "relu", "tanh", "relu"), activity_l1: float = 1e-7,
+                 device="auto", seed: int = 0, layer_names: Optional[Sequence[str]] = None,
+                 input_normalizer: Optional[str] = None, name: str = "model", max_blocks: int = 1024):
+        self.spec = AESpec(input_dim, encoding_dim, hidden_dim, tuple(activations), activity_l1)
+        self.device = _resolve_device(device)
+        self.name = name
+        self.layer_names = list(layer_names or ["input_1", "dense", "dense_1", "dense_2", "dense_3"])
+        self.weight_names = [f"{n}/{w}:0" for n in self.layer_names[1:] for w in ("kernel", "bias")]
+        self.input_normalizer = input_normalizer
+        self.max_blocks = max_blocks
+        self.hp = dict(lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7)
+        self.loss, self.metrics = "mean_squared_error", ["accuracy"]
+        self._weights = init_dense_weights(self.spec.layer_sizes, seed=seed)
+        self._backend = None
+        self._opt_state = None
+        self.stop_training = False
+        self.compiled = False
+
+    # ------------------------------------------------------------------ setup
+    def _normalizer(self):
+        if self.input_normalizer in (None, "none"):
+            return None, None
+        if self.input_normalizer == "cardata":
+            if self.spec.input_dim != 18:
+                raise ValueError("cardata normaliser needs input_dim 18")
+            return normalize_affine()
+        raise ValueError(f"unknown input_normalizer {self.input_normalizer!r}")
+
+    def compile(self, optimizer="adam", loss="mean_squared_error", metrics=("accuracy",), learning_rate=None,
+                **adam_kw) -> "Autoencoder":
+        if str(optimizer).lower() != "adam":
+            raise ValueError("only the Adam optimizer is implemented (the reference uses 'adam')")
+        if loss not in ("mean_squared_error", "mse"):
+            raise ValueError("only mean_squared_error is implemented (the reference loss)")
+        self.loss, self.metrics = "mean_squared_error", list(metrics)
+        if learning_rate is not None:
+            self.hp["lr"] = float(learning_rate)
+        self.hp.update({k: float(v) for k, v in adam_kw.items() if k in ("beta_1", "beta_2", "epsilon")})
+        self._build()
+        self.compiled = True
+        return self
+
+    def _build(self) -> None:
+        weights = self.get_weights() if self._backend is not None else self._weights
+        opt = self._backend.get_optimizer_state() if self._backend is not None else self._opt_state
+        sc, sh = self._normalizer()
+        if self.device.type == "cuda":
+            self._backend = FusedAE(self.spec, weights, self.device, max_blocks=self.max_blocks,
+                                    want_acc="accuracy" in self.metrics, scale=sc, shift=sh, **self.hp)
+        else:
+            self._backend = TorchAE(self.spec.layer_sizes, self.spec.activations, self.spec.activity_l1, weights,
+                                    device=self.device, **self.hp)
+            self._cpu_norm = (sc, sh)
+        if opt is not None:
+            self._backend.set_optimizer_state(*opt)
+
+    @property
+    def backend(self):
+        if self._backend is None:
+            self._build()
+        return self._backend
+
+    # ------------------------------------------------------------------ weights
+    def get_weights(self) -> List[np.ndarray]:
+        return self._backend.get_weights() if self._backend is not None else [w.copy() for w in self._weights]
+
+    def set_weights(self, weights: Sequence[np.ndarray]) -> None:
+        self._weights = [np.asarray(w, np.float32).copy() for w in weights]
+        if self._backend is not None:
+            self._backend.set_weights(self._weights)
+
+    @property
+    def iterations(self) -> int:
+        if self._backend is None:
+            return int(self._opt_state[0]) if self._opt_state else 0
+        return int(self._backend.get_optimizer_state()[0])
+
+    def count_params(self) -> int:
+        return self.spec.n_params
+
+    def summary(self, print_fn=print) -> str:
+        lines = [f'Model: "{self.name}"', "_" * 65, f"{'Layer (type)':<29}{'Output Shape':<22}{'Param #':>10}",
+                 "=" * 65, f"{self.layer_names[0] + ' (InputLayer)':<29}{str((None, self.spec.input_dim)):<22}{0:>10}"]
+        for n, (i, o) in zip(self.layer_names[1:], self.spec.layer_sizes):
+            lines.append(f"{n + ' (Dense)':<29}{str((None, o)):<22}{i * o + o:>10}")
+        lines += ["=" * 65, f"Total params: {self.count_params():,}", f"Trainable params: {self.count_params():,}",
+                  "Non-trainable params: 0", "_" * 65]
+        text = "\n".join(lines)
+        if print_fn:
+            print_fn(text)
+        return text
+
+    # ------------------------------------------------------------------ data helpers
+    def _to_device(self, x) -> torch.Tensor:
+        if isinstance(x, torch.Tensor):
+            t = x.to(self.device, torch.float32)
+        else:
+            t = torch.as_tensor(np.ascontiguousarray(x, dtype=np.float32), device=self.device)
+        return t.contiguous()
+
+    def _cpu_x(self, x) -> torch.Tensor:
+        x = x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x, np.float32)
+        sc, sh = self._cpu_norm
+        if sc is not None:
+            x = x * sc + sh
+        return torch.as_tensor(np.asarray(x, np.float32))
+
+    def _dist(self):
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return dist.get_rank(), dist.get_world_size()
+        return 0, 1
+
+    # ------------------------------------------------------------------ training
+    def fit(self, x=None, y=None, epochs: int = 1, batch_size: int = 32, verbose: int = 1,
+            callbacks: Optional[Sequence[Callback]] = None, validation_data=None, shuffle: bool = True,
+            steps_per_epoch: Optional[int] = None, seed: int = 0) -> History:
+        """Train on an array (``y`` must be ``x`` or None: autoencoder) or a Stream.
+
+        Under ``torch.distributed`` (RCCL) every rank trains on its own shard:
+        arrays are split contiguously by rank, Streams are expected to be
+        rank-sharded already; gradients are all-reduced once per step and the
+        global batch is ``batch_size * world_size``.
+        """
+        from ..data.stream import Stream
+        from ..parallel.dp import allreduce_sum_
+
+        if not self.compiled:
+            self.compile()
+        if y is not None and y is not x:
+            raise ValueError("autoencoder fit expects y == x (or y=None)")
+        rank, world = self._dist()
+        allreduce = allreduce_sum_ if world > 1 else None
+        hist = History()
+        cbs = [hist] + list(callbacks or [])
+        for cb in cbs:
+            cb.set_model(self)
+        self.stop_training = False
+        be = self.backend
+        for cb in cbs:
+            cb.on_train_begin()
+        is_stream = isinstance(x, Stream)
+        if not is_stream:
+            arr = x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x, np.float32)
+            if world > 1:
+                from ..parallel.dp import shard_range
+                s0, s1 = shard_range(len(arr), rank, world)
+                arr = arr[s0:s1]
+            xd = self._to_device(arr) if self.device.type == "cuda" else self._cpu_x(arr)
+        rng = np.random.default_rng(seed + rank)
+        for epoch in range(epochs):
+            t0 = time.perf_counter()
+            for cb in cbs:
+                cb.on_epoch_begin(epoch)
+            be.reset_metrics()
+            steps = 0
+            if is_stream:
+                for xb in self._stream_batches(x, batch_size):
+                    if steps_per_epoch is not None and steps >= steps_per_epoch:
+                        break
+                    be.step(xb, global_batch=len(xb) * world, allreduce=allreduce) if self.device.type == "cuda" \
+                        else be.step(xb)
+                    steps += 1
+            else:
+                n = len(xd)
+                order = None
+                if shuffle:
+                    perm = rng.permutation(n)
+                    order = torch.as_tensor(perm, device=xd.device)
+                nb = math.ceil(n / batch_size)
+                if steps_per_epoch is not None:
+                    nb = min(nb, steps_per_epoch)
+                xs = xd[order] if order is not None else xd
+                for b in range(nb):
+                    xb = xs[b * batch_size:(b + 1) * batch_size]
+                    if self.device.type == "cuda":
+                        be.step(xb, global_batch=len(xb) * world, allreduce=allreduce)
+                    else:
+                        be.step(xb)
+                    steps += 1
+            m = be.read_metrics()
+            logs = {"loss": m["loss"]}
+            if "accuracy" in self.metrics:
+                logs["accuracy"] = m["accuracy"]
+            if validation_data is not None:
+                vx = validation_data[0] if isinstance(validation_data, (tuple, list)) else validation_data
+                vl, va = self.evaluate(vx, batch_size=max(batch_size, 65536), verbose=0)
+                logs["val_loss"] = vl
+                if "accuracy" in self.metrics:
+                    logs["val_accuracy"] = va
+            dt = time.perf_counter() - t0
+            logs["_seconds"] = dt
+            logs["_rows"] = m["rows"]
+            if verbose and rank == 0:
+                shown = " - ".join(f"{k}: {v:.4f}" for k, v in logs.items() if not k.startswith("_"))
+                if verbose == 2:
+                    print(f"Epoch {epoch + 1}/{epochs}\n{steps} steps - {dt:.2f}s - {shown}", flush=True)
+                else:
+                    print(f"Epoch {epoch + 1}/{epochs} - {shown}", flush=True)
+            for cb in cbs:
+                cb.on_epoch_end(epoch, {k: v for k, v in logs.items()})
+            if self.stop_training:
+                break
+        for cb in cbs:
+            cb.on_train_end()
+        return hist
+
+    def _stream_batches(self, stream, batch_size: int):
+        """Yield device (or CPU) batches of raw rows from a Stream."""
+        st = stream.batch(batch_size)
+        if self.device.type == "cuda":
+            from ..data.loader import DeviceLoader
+            for xb, _ in DeviceLoader(st, self.device, max_rows=batch_size, features=self.spec.input_dim):
+                yield xb
+        else:
+            for c in st:
+                yield self._cpu_x(c.x)
+
+    # ------------------------------------------------------------------ inference
+    def _forward_batches(self, x, batch_size: int):
+        arr = x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x, np.float32)
+        for s in range(0, len(arr), batch_size):
+            xb = arr[s:s + batch_size]
+            if self.device.type == "cuda":
+                r, sc, _ = self.backend.forward(self._to_device(xb))
+                yield xb, r.cpu().numpy(), sc.cpu().numpy()
+            else:
+                xn = self._cpu_x(xb)
+                y = self.backend.forward(xn)
+                yield xb, y.numpy(), ((y - xn) ** 2).mean(dim=1).numpy()
+
+    def predict(self, x, batch_size: int = 32, callbacks: Optional[Sequence[Callback]] = None,
+                verbose: int = 0) -> np.ndarray:
+        """Reconstructions (what the reference streams to Kafka, cardata-v3.py:243-249)."""
+        from ..data.stream import Stream
+        if not self.compiled:
+            self.compile()
+        cbs = list(callbacks or [])
+        for cb in cbs:
+            cb.set_model(self)
+        outs = []
+        if isinstance(x, Stream):
+            batches = ((c.x,) for c in x.batch(batch_size))
+            it = (self._forward_batches(b[0], batch_size) for b in batches)
+            gen = (r for g in it for r in g)
+        else:
+            gen = self._forward_batches(x, batch_size)
+        for bi, (_, rec, sc) in enumerate(gen):
+            outs.append(rec)
+            for cb in cbs:
+                cb.on_predict_batch_end(bi, {"outputs": rec, "scores": sc})
+        for cb in cbs:
+            cb.on_predict_end()
+        return np.concatenate(outs) if outs else np.zeros((0, self.spec.input_dim), np.float32)
+
+    def score(self, x, batch_size: int = 1 << 20) -> np.ndarray:
+        """Per-row reconstruction MSE = anomaly score (notebook ...ipynb:1014-1015)."""
+        if not self.compiled:
+            self.compile()
+        return np.concatenate([sc for _, _, sc in self._forward_batches(x, batch_size)])
+
+    def detect(self, x, threshold: float = 5.0, batch_size: int = 1 << 20) -> np.ndarray:
+        """Anomaly flags with the notebook's fixed threshold (``threshold_fixed = 5``)."""
+        return self.score(x, batch_size) > threshold
+
+    def evaluate(self, x, y=None, batch_size: int = 65536, verbose: int = 0) -> Tuple[float, float]:
+        """Keras ``evaluate``: (loss, accuracy) without updating weights."""
+        if not self.compiled:
+            self.compile()
+        arr = x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x, np.float32)
+        D = self.spec.input_dim
+        if self.device.type == "cuda":
+            tot = np.zeros(4)
+            for s in range(0, len(arr), batch_size):
+                _, metr = self.backend.gradients(self._to_device(arr[s:s + batch_size]))
+                tot += metr
+            sq, ab, corr, rows = tot
+            rows = max(rows, 1.0)
+            return float((sq / D + self.spec.activity_l1 * ab) / rows), float(corr / rows)
+        from .reference import ae_loss_torch
+        xn = self._cpu_x(arr)
+        with torch.no_grad():
+            loss, _, acc = ae_loss_torch(xn, self.backend.w, self.spec.activations, self.spec.activity_l1)
+        return float(loss), float(acc)
+
+    # ------------------------------------------------------------------ persistence
+    def model_config(self) -> dict:
+        dense = []
+        for li, (n, (_, o)) in enumerate(zip(self.layer_names[1:], self.spec.layer_sizes)):
+            dense.append(kc.dense_config(n, o, self.spec.activations[li],
+                                         self.spec.activity_l1 if li == 0 else None))
+        return kc.functional_dense_model(self.name, self.layer_names[0], self.spec.input_dim, dense)
+
+    def save(self, path: str, include_optimizer: bool = True) -> None:
+        """Keras-compatible ``.h5`` (cardata-v3.py:227 ``autoencoder.save``)."""
+        w = self.get_weights()
+        layers = [(self.layer_names[0], [])]
+        for li, n in enumerate(self.layer_names[1:]):
+            layers.append((n, [(self.weight_names[2 * li], w[2 * li]), (self.weight_names[2 * li + 1], w[2 * li + 1])]))
+        opt = None
+        if include_optimizer and self._backend is not None:
+            it, m, v = self._backend.get_optimizer_state()
+            names = ckh5.adam_weight_names(self.weight_names)
+            opt = list(zip(names, [np.array(it, dtype=np.int64)] + list(m) + list(v)))
+        ckh5.save_keras_h5(path, self.model_config(),
+                           layers, kc.training_config(self.hp["lr"], self.hp["beta_1"], self.hp["beta_2"],
+                                                      self.hp["epsilon"], metrics=self.metrics), opt)
+
+    @classmethod
+    def load(cls, path: str, device="auto", input_normalizer: Optional[str] = None, compile: bool = True,
+             **kw) -> "Autoencoder":
+        """``tf.keras.models.load_model`` equivalent (cardata-v3.py:261)."""
+        ck = ckh5.load_keras_h5(path)
+        in_name, in_dim, dense = kc.parse_dense_model(ck.model_config)
+        if len(dense) != 4:
+            raise ValueError(f"expected a 4-Dense autoencoder, found {len(dense)} Dense layers")
+        acts = tuple(d["activation"] for d in dense)
+        l1 = 0.0
+        ar = dense[0].get("activity_regularizer")
+        if ar:
+            l1 = float(ar["config"].get("l1", 0.0))
+        units = [int(d["units"]) for d in dense]
+        if units[3] != in_dim or units[1] != units[2]:
+            raise ValueError(f"unsupported autoencoder shape {in_dim}->{units}")
+        m = cls(in_dim, units[0], units[1], acts, l1, device=device,
+                layer_names=[in_name or "input_1"] + [d["name"] for d in dense],
+                input_normalizer=input_normalizer, name=ck.model_config["config"].get("name", "model"), **kw)
+        # weight dataset names come from the file (quirk: dense_4 -> dense_4_1/...)
+        m.weight_names = [wn for ln in m.layer_names[1:] for wn, _ in ck.weights[ln]]
+        m.set_weights(ck.flat_weights())
+        hp = kc.optimizer_hparams(ck.training_config)
+        m.hp.update(hp)
+        if ck.optimizer_weights:
+            arrays = [a for _, a in ck.optimizer_weights]
+            k = len(m.weight_names)
+            if len(arrays) == 1 + 2 * k:
+                m._opt_state = (int(np.asarray(arrays[0]).reshape(-1)[0]), arrays[1:1 + k], arrays[1 + k:])
+        if compile:
+            metrics = (ck.training_config or {}).get("metrics", ["accuracy"]) or []
+            m.compile(metrics=metrics)
+        return m
+
+
+def load_model(path: str, **kw) -> Autoencoder:
+    return Autoencoder.load(path, **kw)

@@ -1,0 +1,166 @@
+"""Prometheus text-exposition metrics for the streaming engine.
+
+The reference's observability is platform-level Prometheus + Grafana (HiveMQ /
+device-simulator dashboards, hivemq/hivemq.json, test-generator/devsim.json;
+ServiceMonitor at 5 s, kube-cli.sh:272-288).  The ML engine exports analogous
+counters: ingest_records_total, ingest_bytes_total,
+h2d_bytes_total, train_rows_total, train_step_latency_us{quantile},
+allreduce_us, infer_event_latency_us{quantile}, anomaly_events_total,
+ring_buffer_occupancy ...  ``serve(port)`` exposes them at /metrics.
+"""
+from __future__ import annotations
+
+import threading
+from http.server import BaseHTTPRequestHandler, HTTPServer
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+
+class _Metric:
+    kind = "untyped"
+
+    def __init__(self, name: str, help: str = "", labels: Sequence[str] = ()):
+        self.name, self.help, self.labelnames = name, help, tuple(labels)
+        self._lock = threading.Lock()
+
+    def _key(self, labels: Dict[str, str]) -> Tuple[str, ...]:
+        return tuple(str(labels.get(n, "")) for n in self.labelnames)
+
+    def _fmt_labels(self, key: Tuple[str, ...], extra: Optional[Dict[str, str]] = None) -> str:
+        items = list(zip(self.labelnames, key)) + list((extra or {}).items())
+        if not items:
+            return ""
+        return "{" + ",".join(f'{k}="{v}"' for k, v in items) + "}"
+
+
+class Counter(_Metric):
+    kind = "counter"
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self._v: Dict[Tuple[str, ...], float] = {}
+
+    def inc(self, amount: float = 1.0, **labels) -> None:
+        if amount < 0:
+            raise ValueError("counters only increase")
+        k = self._key(labels)
+        with self._lock:
+            self._v[k] = self._v.get(k, 0.0) + amount
+
+    def value(self, **labels) -> float:
+        return self._v.get(self._key(labels), 0.0)
+
+    def expose(self) -> List[str]:
+        return [f"{self.name}{self._fmt_labels(k)} {v:.17g}" for k, v in sorted(self._v.items())]
+
+
+class Gauge(Counter):
+    kind = "gauge"
+
+    def set(self, value: float, **labels) -> None:
+        with self._lock:
+            self._v[self._key(labels)] = float(value)
+
+    def inc(self, amount: float = 1.0, **labels) -> None:
+        k = self._key(labels)
+        with self._lock:
+            self._v[k] = self._v.get(k, 0.0) + amount
+
+
+class Summary(_Metric):
+    """Sliding-window quantiles (p50/p90/p99) + _sum/_count."""
+
+    kind = "summary"
+
+    def __init__(self, name, help="", labels=(), window: int = 10000,
+                 quantiles: Sequence[float] = (0.5, 0.9, 0.99)):
+        super().__init__(name, help, labels)
+        self.window, self.quantiles = int(window), tuple(quantiles)
+        self._obs: Dict[Tuple[str, ...], List[float]] = {}
+        self._sum: Dict[Tuple[str, ...], float] = {}
+        self._count: Dict[Tuple[str, ...], int] = {}
+
+    def observe(self, value: float, **labels) -> None:
+        k = self._key(labels)
+        with self._lock:
+            buf = self._obs.setdefault(k, [])
+            buf.append(float(value))
+            if len(buf) > self.window:
+                del buf[: len(buf) - self.window]
+            self._sum[k] = self._sum.get(k, 0.0) + value
+            self._count[k] = self._count.get(k, 0) + 1
+
+    def quantile(self, q: float, **labels) -> float:
+        buf = self._obs.get(self._key(labels), [])
+        return float(np.percentile(buf, 100 * q)) if buf else float("nan")
+
+    def expose(self) -> List[str]:
+        out = []
+        for k, buf in sorted(self._obs.items()):
+            for q in self.quantiles:
+                v = float(np.percentile(buf, 100 * q)) if buf else float("nan")
+                out.append(f"{self.name}{self._fmt_labels(k, {'quantile': str(q)})} {v:.17g}")
+            out.append(f"{self.name}_sum{self._fmt_labels(k)} {self._sum[k]:.17g}")
+            out.append(f"{self.name}_count{self._fmt_labels(k)} {self._count[k]}")
+        return out
+
+
+class Registry:
+    def __init__(self):
+        self._m: Dict[str, _Metric] = {}
+        self._lock = threading.Lock()
+
+    def _get(self, cls, name, help, labels, **kw):
+        with self._lock:
+            m = self._m.get(name)
+            if m is None:
+                m = cls(name, help, labels, **kw)
+                self._m[name] = m
+            elif not isinstance(m, cls):
+                raise TypeError(f"metric {name} already registered as {type(m).__name__}")
+            return m
+
+    def counter(self, name, help="", labels=()) -> Counter:
+        return self._get(Counter, name, help, labels)
+
+    def gauge(self, name, help="", labels=()) -> Gauge:
+        return self._get(Gauge, name, help, labels)
+
+    def summary(self, name, help="", labels=(), **kw) -> Summary:
+        return self._get(Summary, name, help, labels, **kw)
+
+    def exposition(self) -> str:
+        lines = []
+        for name, m in sorted(self._m.items()):
+            if m.help:
+                lines.append(f"# HELP {name} {m.help}")
+            lines.append(f"# TYPE {name} {m.kind}")
+            lines += m.expose()
+        return "\n".join(lines) + "\n"
+
+    def serve(self, port: int = 0, addr: str = "127.0.0.1") -> HTTPServer:
+        reg = self
+
+        class H(BaseHTTPRequestHandler):
+            def do_GET(self):  # noqa: N802
+                if self.path.rstrip("/") not in ("/metrics", ""):
+                    self.send_response(404)
+                    self.end_headers()
+                    return
+                body = reg.exposition().encode()
+                self.send_response(200)
+                self.send_header("Content-Type", "text/plain; version=0.0.4")
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+            def log_message(self, *a):
+                pass
+
+        srv = HTTPServer((addr, port), H)
+        threading.Thread(target=srv.serve_forever, daemon=True).start()
+        return srv
+
+
+REGISTRY = Registry()
