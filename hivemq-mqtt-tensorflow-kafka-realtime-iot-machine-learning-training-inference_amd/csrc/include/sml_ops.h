@@ -21,6 +21,12 @@ hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, f
                               float gscale, float* metrics_acc, int flags, int64_t* cursor, int64_t cursor_step,
                               int64_t cursor_ring, hipStream_t stream);
 
+// ---- LSTM recurrence (lstm.hip) ----
+hipError_t lstm_fwd_launch(const float* zx, const float* Uw, const float* h0, const float* c0, float* hseq,
+                           float* cseq, float* gates, int64_t B, int T, int U, int act, hipStream_t stream);
+hipError_t lstm_bwd_launch(const float* dh, const float* gates, const float* cseq, const float* c0, const float* Uw,
+                           float* dz, float* dh0, float* dc0, int64_t B, int T, int U, int act, hipStream_t stream);
+
 // ---- utilities (util.hip) ----
 hipError_t lane_xor_probe_launch(float* out, hipStream_t stream);
 

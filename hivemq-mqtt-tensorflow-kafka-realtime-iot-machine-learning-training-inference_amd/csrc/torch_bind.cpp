@@ -142,6 +142,57 @@ void ae_forward(const at::Tensor& x, const c10::optional<at::Tensor>& scale, con
                                        (float)threshold, d, a, (int)max_blocks, cur_stream(x)));
 }
 
+std::vector<at::Tensor> lstm_fwd(const at::Tensor& zx, const at::Tensor& Uw, const c10::optional<at::Tensor>& h0,
+                                 const c10::optional<at::Tensor>& c0, int64_t act) {
+  check_dev(zx, "zx", at::kFloat);
+  check_dev(Uw, "U", at::kFloat);
+  TORCH_CHECK(zx.dim() == 3 && zx.is_contiguous(), "zx must be contiguous [B, T, 4u]");
+  TORCH_CHECK(Uw.dim() == 2 && Uw.is_contiguous() && Uw.size(1) == 4 * Uw.size(0), "U must be [u, 4u]");
+  const int64_t B = zx.size(0), T = zx.size(1), U = Uw.size(0);
+  TORCH_CHECK(zx.size(2) == 4 * U, "zx last dim must be 4u");
+  TORCH_CHECK(U == 16 || U == 32 || U == 64, "LSTM units must be 16, 32 or 64");
+  TORCH_CHECK(act == 1 || act == 2, "LSTM activation must be relu or tanh");
+  TORCH_CHECK(T >= 1 && B >= 1, "empty input");
+  if (h0.has_value()) TORCH_CHECK(h0->is_contiguous() && h0->numel() == B * U, "h0 must be [B, u]");
+  if (c0.has_value()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * U, "c0 must be [B, u]");
+  c10::hip::HIPGuard guard(zx.device().index());
+  auto h = at::empty({B, T, U}, zx.options());
+  auto c = at::empty({B, T, U}, zx.options());
+  auto gt = at::empty({B, T, 4 * U}, zx.options());
+  SML_CHECK_HIP(sml::lstm_fwd_launch(zx.data_ptr<float>(), Uw.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0),
+                                     h.data_ptr<float>(), c.data_ptr<float>(), gt.data_ptr<float>(), B, (int)T,
+                                     (int)U, (int)act, cur_stream(zx)));
+  return {h, c, gt};
+}
+
+std::vector<at::Tensor> lstm_bwd(const at::Tensor& dh, const at::Tensor& gates, const at::Tensor& cseq,
+                                 const c10::optional<at::Tensor>& c0, const at::Tensor& Uw, int64_t act,
+                                 bool want_state_grads) {
+  check_dev(dh, "dh", at::kFloat);
+  check_dev(gates, "gates", at::kFloat);
+  check_dev(cseq, "cseq", at::kFloat);
+  check_dev(Uw, "U", at::kFloat);
+  const int64_t B = dh.size(0), T = dh.size(1), U = Uw.size(0);
+  TORCH_CHECK(dh.is_contiguous() && gates.is_contiguous() && cseq.is_contiguous(), "inputs must be contiguous");
+  TORCH_CHECK(dh.sizes() == cseq.sizes() && gates.size(2) == 4 * U && dh.size(2) == U, "shape mismatch");
+  TORCH_CHECK(U == 16 || U == 32 || U == 64, "LSTM units must be 16, 32 or 64");
+  if (c0.has_value()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * U, "c0 must be [B, u]");
+  c10::hip::HIPGuard guard(dh.device().index());
+  auto dz = at::empty({B, T, 4 * U}, dh.options());
+  at::Tensor dh0, dc0;
+  if (want_state_grads) {
+    dh0 = at::empty({B, U}, dh.options());
+    dc0 = at::empty({B, U}, dh.options());
+  }
+  SML_CHECK_HIP(sml::lstm_bwd_launch(dh.data_ptr<float>(), gates.data_ptr<float>(), cseq.data_ptr<float>(),
+                                     opt_ptr(c0), Uw.data_ptr<float>(), dz.data_ptr<float>(),
+                                     want_state_grads ? dh0.data_ptr<float>() : nullptr,
+                                     want_state_grads ? dc0.data_ptr<float>() : nullptr, B, (int)T, (int)U,
+                                     (int)act, cur_stream(dh)));
+  if (want_state_grads) return {dz, dh0, dc0};
+  return {dz};
+}
+
 at::Tensor lane_xor_probe(const at::Tensor& like) {
   TORCH_CHECK(like.is_cuda(), "needs a device tensor for placement");
   c10::hip::HIPGuard guard(like.device().index());
@@ -215,6 +266,10 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("slots", [](const RingPy& r) { return r.r->slots(); })
       .def_property_readonly("slot_bytes", [](const RingPy& r) { return (int64_t)r.r->slot_bytes(); })
       .def_property_readonly("bytes_copied", [](const RingPy& r) { return (uint64_t)r.r->bytes_copied(); });
+  m.def("lstm_fwd", &lstm_fwd, "fused LSTM recurrence forward (h, c, gates)", py::arg("zx"), py::arg("U"),
+        py::arg("h0") = py::none(), py::arg("c0") = py::none(), py::arg("act") = 1);
+  m.def("lstm_bwd", &lstm_bwd, "fused LSTM BPTT -> pre-activation gate grads", py::arg("dh"), py::arg("gates"),
+        py::arg("cseq"), py::arg("c0"), py::arg("U"), py::arg("act") = 1, py::arg("want_state_grads") = false);
   m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),
         py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("recon"), py::arg("score"), py::arg("flag"),

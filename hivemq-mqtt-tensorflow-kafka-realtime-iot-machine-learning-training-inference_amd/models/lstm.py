@@ -1,0 +1,307 @@
+"""LSTM sequence predictor (reference LSTM-TensorFlow-IO-Kafka/cardata-v2.py).
+
+Reference stack (cardata-v2.py:177-183, look_back = 1, batch_size = 1):
+
+    LSTM(32, relu, return_sequences=True, input_shape=(look_back, 18))
+    LSTM(16, relu)
+    RepeatVector(look_back)
+    LSTM(16, relu, return_sequences=True)
+    LSTM(32, relu, return_sequences=True)
+    TimeDistributed(Dense(18))
+    compile(metrics=['accuracy'], loss='mean_squared_error', optimizer='adam')
+
+18 642 parameters.  Task: given a window of ``look_back`` normalised events,
+predict the next event (``dataset.skip(look_back)``, :199-206).  BASELINE config 3
+uses the 2-layer variant ``LSTM(32, seq) -> LSTM(16) -> Dense(18)`` with
+``seq_len = 50`` (:func:`LSTMPredictor.two_layer`).
+
+Every LSTM layer runs as :func:`streamml.ops.lstm.lstm` (fused HIP recurrence on
+ROCm); dense heads are bf16 GEMMs; all parameters live in one flat buffer so the
+optimizer step is one HIP Adam launch and DP is one RCCL all-reduce.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..ckpt import h5 as ckh5
+from ..nn import keras_config as kc
+from ..nn.callbacks import Callback, History
+from ..ops.adam import FlatAdam, FlatParams
+from ..ops.lstm import lstm as lstm_op
+
+# layer spec: ("lstm", units, return_sequences, activation) | ("repeat", n) | ("dense", units, time_distributed)
+REFERENCE_STACK = [("lstm", 32, True, "relu"), ("lstm", 16, False, "relu"), ("repeat", None),
+                   ("lstm", 16, True, "relu"), ("lstm", 32, True, "relu"), ("dense", 18, True)]
+TWO_LAYER_STACK = [("lstm", 32, True, "relu"), ("lstm", 16, False, "relu"), ("dense", 18, False)]
+
+
+def _orthogonal(rows: int, cols: int, rng: np.random.Generator) -> np.ndarray:
+    a = rng.standard_normal((max(rows, cols), min(rows, cols)))
+    q, r = np.linalg.qr(a)
+    q = q * np.sign(np.diag(r))
+    return (q if rows >= cols else q.T)[:rows, :cols].astype(np.float32)
+
+
+def _glorot(fi: int, fo: int, rng) -> np.ndarray:
+    lim = math.sqrt(6.0 / (fi + fo))
+    return rng.uniform(-lim, lim, size=(fi, fo)).astype(np.float32)
+
+
+def _bf16_mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    if a.is_cuda:
+        return (a.to(torch.bfloat16) @ b.to(torch.bfloat16)).float()
+    return a @ b
+
+
+class LSTMPredictor:
+    def __init__(self, look_back: int = 1, features: int = 18, stack=None, device="auto", seed: int = 0,
+                 name: str = "sequential", lr: float = 1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
+        if device in (None, "auto"):
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(device)
+        self.look_back, self.features, self.name = int(look_back), int(features), name
+        self.stack = [tuple(s) for s in (stack or REFERENCE_STACK)]
+        self.hp = dict(lr=lr, beta_1=beta_1, beta_2=beta_2, epsilon=epsilon)
+        rng = np.random.default_rng(seed)
+        shapes, init, self.layers = [], [], []
+        counts: Dict[str, int] = {}
+        dim = self.features
+        seq = True   # current tensor has a time axis
+        for spec in self.stack:
+            kind = spec[0]
+            lname = kind if kind != "dense" or not spec[2] else "time_distributed"
+            k = counts.get(lname, 0)
+            counts[lname] = k + 1
+            lname = lname if k == 0 else f"{lname}_{k}"
+            if kind == "lstm":
+                u = int(spec[1])
+                if not seq:
+                    raise ValueError("LSTM needs a sequence input (add a RepeatVector)")
+                W, Uw, b = _glorot(dim, 4 * u, rng), _orthogonal(u, 4 * u, rng), np.zeros(4 * u, np.float32)
+                b[u:2 * u] = 1.0   # unit_forget_bias
+                self.layers.append(dict(kind="lstm", name=lname, units=u, return_sequences=bool(spec[2]),
+                                        activation=spec[3], params=len(shapes), n=3, in_dim=dim))
+                shapes += [(dim, 4 * u), (u, 4 * u), (4 * u,)]
+                init += [W, Uw, b]
+                dim, seq = u, bool(spec[2])
+            elif kind == "repeat":
+                n = int(spec[1] or self.look_back)
+                self.layers.append(dict(kind="repeat", name=lname if k == 0 else lname, n=n))
+                seq = True
+            elif kind == "dense":
+                u = int(spec[1])
+                td = bool(spec[2])
+                self.layers.append(dict(kind="dense", name=lname, units=u, td=td, params=len(shapes), n=2,
+                                        in_dim=dim))
+                shapes += [(dim, u), (u,)]
+                init += [_glorot(dim, u, rng), np.zeros(u, np.float32)]
+                dim = u
+            else:
+                raise ValueError(f"unknown layer kind {kind}")
+        for L in self.layers:
+            if L["kind"] == "repeat":
+                L["name"] = "repeat_vector" if L["name"] == "repeat" else L["name"].replace("repeat", "repeat_vector")
+        self.fp = FlatParams(shapes, self.device, init)
+        self.opt = FlatAdam(self.fp, **self.hp)
+        self._acc = np.zeros(4)   # loss*n, correct, n, batches
+        self.stop_training = False
+
+    @classmethod
+    def reference(cls, look_back: int = 1, **kw) -> "LSTMPredictor":
+        return cls(look_back=look_back, stack=REFERENCE_STACK, **kw)
+
+    @classmethod
+    def two_layer(cls, look_back: int = 50, **kw) -> "LSTMPredictor":
+        return cls(look_back=look_back, stack=TWO_LAYER_STACK, **kw)
+
+    # ------------------------------------------------------------------ model
+    def count_params(self) -> int:
+        return int(self.fp.n)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        P = self.fp.params
+        h = x
+        for L in self.layers:
+            if L["kind"] == "lstm":
+                W, Uw, b = P[L["params"]:L["params"] + 3]
+                hs = lstm_op(h, W, Uw, b, L["activation"])
+                h = hs if L["return_sequences"] else hs[:, -1]
+            elif L["kind"] == "repeat":
+                h = h.unsqueeze(1).expand(h.shape[0], L["n"], h.shape[-1]).contiguous()
+            else:
+                K, b = P[L["params"]:L["params"] + 2]
+                shp = h.shape
+                h = (_bf16_mm(h.reshape(-1, shp[-1]), K) + b).reshape(*shp[:-1], K.shape[1])
+        return h
+
+    def _loss(self, y_pred: torch.Tensor, y: torch.Tensor):
+        if y_pred.dim() == 3 and y.dim() == 2:
+            y = y.unsqueeze(1)          # (n, 1, F) target broadcasts over the output steps (Keras MSE)
+        yb = torch.broadcast_to(y, y_pred.shape)
+        loss = ((y_pred - yb) ** 2).mean()
+        correct = (torch.argmax(y_pred, -1) == torch.argmax(yb, -1)).float()
+        return loss, correct.mean(dim=tuple(range(1, correct.dim()))).sum() if correct.dim() > 1 else correct.sum()
+
+    def train_step(self, x: torch.Tensor, y: torch.Tensor, global_batch: Optional[int] = None, allreduce=None):
+        n = x.shape[0]
+        self.fp.zero_grad()
+        y_pred = self.forward(x)
+        loss, correct = self._loss(y_pred, y)
+        scale = n / float(global_batch or n)   # mean over the global batch under DP
+        (loss * scale).backward()
+        self.opt.step(allreduce=allreduce)
+        return loss.detach(), correct.detach()
+
+    # ------------------------------------------------------------------ training
+    def fit(self, x, y=None, epochs: int = 1, batch_size: int = 1, verbose: int = 1, take: Optional[int] = None,
+            callbacks: Optional[Sequence[Callback]] = None, shuffle: bool = False, normalize: bool = True):
+        """``x``: windows [n, T, F] + ``y`` next rows [n, F], or a Stream (windows built here)."""
+        from ..data.stream import Stream
+        from ..parallel.dp import allreduce_sum_
+        import torch.distributed as dist
+
+        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        allreduce = allreduce_sum_ if world > 1 else None
+        hist = History()
+        cbs = [hist] + list(callbacks or [])
+        for cb in cbs:
+            cb.set_model(self)
+        if isinstance(x, Stream):
+            st = x.normalize() if normalize else x
+            wins = [w for w in st.windows(self.look_back)]
+            xs = np.concatenate([w[0] for w in wins]) if wins else np.zeros((0, self.look_back, self.features))
+            ys = np.concatenate([w[1] for w in wins]) if wins else np.zeros((0, self.features))
+        else:
+            xs, ys = np.asarray(x, np.float32), np.asarray(y, np.float32)
+        xd = torch.as_tensor(xs, dtype=torch.float32, device=self.device)
+        yd = torch.as_tensor(ys, dtype=torch.float32, device=self.device)
+        n = len(xd)
+        nb = math.ceil(n / batch_size)
+        if take is not None:
+            nb = min(nb, take)
+        for epoch in range(epochs):
+            t0 = time.perf_counter()
+            tot_loss = torch.zeros((), device=self.device)
+            tot_corr = torch.zeros((), device=self.device)
+            rows = 0
+            order = torch.randperm(n, device=self.device) if shuffle else None
+            for b in range(nb):
+                sl = slice(b * batch_size, (b + 1) * batch_size)
+                xb = xd[order[sl]] if order is not None else xd[sl]
+                yb = yd[order[sl]] if order is not None else yd[sl]
+                loss, corr = self.train_step(xb, yb, global_batch=len(xb) * world, allreduce=allreduce)
+                tot_loss += loss * len(xb)
+                tot_corr += corr
+                rows += len(xb)
+            logs = {"loss": float(tot_loss) / max(rows, 1), "accuracy": float(tot_corr) / max(rows, 1),
+                    "_seconds": time.perf_counter() - t0, "_rows": rows}
+            if verbose:
+                print(f"Epoch {epoch + 1}/{epochs} - {nb} steps - loss: {logs['loss']:.4f} - "
+                      f"accuracy: {logs['accuracy']:.4f}", flush=True)
+            for cb in cbs:
+                cb.on_epoch_end(epoch, logs)
+            if self.stop_training:
+                break
+        return hist
+
+    @torch.no_grad()
+    def predict(self, x, batch_size: int = 1024, callbacks: Optional[Sequence[Callback]] = None) -> np.ndarray:
+        xs = np.asarray(x, np.float32)
+        outs = []
+        for bi, s in enumerate(range(0, len(xs), batch_size)):
+            xb = torch.as_tensor(xs[s:s + batch_size], device=self.device)
+            out = self.forward(xb).cpu().numpy()
+            outs.append(out)
+            for cb in callbacks or []:
+                cb.set_model(self)
+                cb.on_predict_batch_end(bi, {"outputs": out.reshape(len(out), -1, self.features)[:, -1]})
+        for cb in callbacks or []:
+            cb.on_predict_end()
+        return np.concatenate(outs) if outs else np.zeros((0,), np.float32)
+
+    # ------------------------------------------------------------------ persistence
+    def weight_names(self) -> List[Tuple[str, List[str]]]:
+        out = []
+        for L in self.layers:
+            if L["kind"] == "lstm":
+                out.append((L["name"], [f"{L['name']}/kernel:0", f"{L['name']}/recurrent_kernel:0",
+                                        f"{L['name']}/bias:0"]))
+            elif L["kind"] == "dense":
+                out.append((L["name"], [f"{L['name']}/kernel:0", f"{L['name']}/bias:0"]))
+            else:
+                out.append((L["name"], []))
+        return out
+
+    def model_config(self) -> dict:
+        layers = []
+        first = True
+        for L in self.layers:
+            if L["kind"] == "lstm":
+                cfg = kc.lstm_config(L["name"], L["units"], L["activation"], L["return_sequences"],
+                                     [None, self.look_back, self.features] if first else None)
+                layers.append({"class_name": "LSTM", "config": cfg})
+            elif L["kind"] == "repeat":
+                layers.append({"class_name": "RepeatVector", "config": {"name": L["name"], "trainable": True,
+                                                                        "dtype": "float32", "n": L["n"]}})
+            else:
+                d = kc.dense_config(L["name"] if not L["td"] else "dense", L["units"], "linear")
+                if L["td"]:
+                    layers.append({"class_name": "TimeDistributed", "config": {
+                        "name": L["name"], "trainable": True, "dtype": "float32",
+                        "layer": {"class_name": "Dense", "config": d}}})
+                else:
+                    layers.append({"class_name": "Dense", "config": d})
+            first = False
+        return kc.sequential(self.name, layers)
+
+    def save(self, path: str, include_optimizer: bool = True) -> None:
+        arrays = self.fp.get()
+        layers, k = [], 0
+        flat_names = []
+        for lname, wnames in self.weight_names():
+            ws = []
+            for wn in wnames:
+                ws.append((wn, arrays[k]))
+                flat_names.append(wn)
+                k += 1
+            layers.append((lname, ws))
+        opt = None
+        if include_optimizer:
+            it, m, v = self.opt.state()
+            opt = list(zip(ckh5.adam_weight_names(flat_names), [np.array(it, np.int64)] + m + v))
+        ckh5.save_keras_h5(path, self.model_config(), layers,
+                           kc.training_config(self.hp["lr"], self.hp["beta_1"], self.hp["beta_2"],
+                                              self.hp["epsilon"]), opt)
+
+    @classmethod
+    def load(cls, path: str, device="auto") -> "LSTMPredictor":
+        ck = ckh5.load_keras_h5(path)
+        cfg = ck.model_config["config"]
+        stack, look_back, features = [], 1, 18
+        for i, lyr in enumerate(cfg["layers"]):
+            c = lyr["config"]
+            if lyr["class_name"] == "LSTM":
+                if "batch_input_shape" in c:
+                    look_back, features = int(c["batch_input_shape"][1]), int(c["batch_input_shape"][2])
+                stack.append(("lstm", int(c["units"]), bool(c["return_sequences"]), c["activation"]))
+            elif lyr["class_name"] == "RepeatVector":
+                stack.append(("repeat", int(c["n"])))
+            elif lyr["class_name"] == "TimeDistributed":
+                stack.append(("dense", int(c["layer"]["config"]["units"]), True))
+            elif lyr["class_name"] == "Dense":
+                stack.append(("dense", int(c["units"]), False))
+            else:
+                raise ValueError(f"unsupported layer {lyr['class_name']}")
+        m = cls(look_back=look_back, features=features, stack=stack, device=device, name=cfg.get("name", "sequential"),
+                **kc.optimizer_hparams(ck.training_config))
+        m.fp.set(ck.flat_weights())
+        if ck.optimizer_weights and len(ck.optimizer_weights) == 1 + 2 * len(m.fp.shapes):
+            arr = [a for _, a in ck.optimizer_weights]
+            k = len(m.fp.shapes)
+            m.opt.load_state(int(np.asarray(arr[0]).reshape(-1)[0]), arr[1:1 + k], arr[1 + k:])
+        return m

@@ -1,0 +1,47 @@
+"""Fused HIP LSTM recurrence vs the plain PyTorch fp32 reference."""
+import numpy as np
+import pytest
+import torch
+
+from streamml.models.lstm import LSTMPredictor
+from streamml.ops.lstm import LSTMFunction, lstm_reference
+
+pytestmark = pytest.mark.gpu
+
+
+def _relerr(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-12)
+
+
+@pytest.mark.parametrize("u,act,B,T", [(32, "relu", 100, 7), (16, "tanh", 37, 50), (32, "tanh", 64, 50),
+                                       (64, "relu", 20, 4)])
+def test_lstm_fwd_bwd_vs_reference(cuda_device, u, act, B, T):
+    rng = np.random.default_rng(u + T)
+    inp = 18
+    x = torch.tensor(rng.uniform(-1, 1, (B, T, inp)), dtype=torch.float32)
+    W = torch.tensor(rng.standard_normal((inp, 4 * u)) * 0.25, dtype=torch.float32)
+    U = torch.tensor(rng.standard_normal((u, 4 * u)) * 0.25, dtype=torch.float32)
+    b = torch.tensor(rng.standard_normal(4 * u) * 0.1, dtype=torch.float32)
+    gy = torch.tensor(rng.standard_normal((B, T, u)), dtype=torch.float32)
+    ref_in = [t.clone().requires_grad_(True) for t in (x, W, U, b)]
+    yr = lstm_reference(*ref_in, activation=act)
+    (yr * gy).sum().backward()
+    dev_in = [t.to(cuda_device).requires_grad_(True) for t in (x, W, U, b)]
+    yd = LSTMFunction.apply(*dev_in, 1 if act == "relu" else 2)
+    (yd * gy.to(cuda_device)).sum().backward()
+    assert _relerr(yd.detach().cpu(), yr.detach()) < 2e-2
+    for d, r in zip(dev_in, ref_in):
+        assert _relerr(d.grad.cpu(), r.grad) < 4e-2, (d.shape,)
+
+
+def test_lstm_predictor_gpu_trains_and_matches_cpu_start(cuda_device):
+    rng = np.random.default_rng(0)
+    xs = rng.uniform(-1, 1, (512, 50, 18)).astype(np.float32)
+    ys = rng.uniform(-1, 1, (512, 18)).astype(np.float32)
+    mg = LSTMPredictor.two_layer(look_back=50, device=cuda_device, seed=3)
+    mc = LSTMPredictor.two_layer(look_back=50, device="cpu", seed=3)
+    pg, pc = mg.predict(xs[:64]), mc.predict(xs[:64])
+    assert _relerr(pg, pc) < 3e-2
+    h = mg.fit(xs, ys, epochs=4, batch_size=128, verbose=0)
+    assert h.history["loss"][-1] < h.history["loss"][0]
