@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: streaming inference -- load a .h5 autoencoder, per-event MSE anomaly score.
+
+Measures (1) p50 / p99 per-event latency at a fixed offered rate (default the
+reference fleet's 10 000 msg/s, scenario.xml: 100 000 cars x 1 msg / 10 s): each
+event is copied from pinned host memory, scored by the fused HIP forward kernel
+and the score copied back; latency is event-available -> score-on-host.
+(2) batched scoring throughput (events/s) for micro-batches of a stream.
+With torchrun, every rank serves its own car-key shard (shard-by-key) and rank
+0 reports the aggregate.  The reference publishes no latency number.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default=None, help=".h5 to load (default: save a fresh 18-dim AE first)")
+    ap.add_argument("--events", type=int, default=2000)
+    ap.add_argument("--qps", type=float, default=10000.0)
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--threshold", type=float, default=5.0)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    from streamml.data.cardata import synthetic_device_tensor
+    from streamml.models.autoencoder import Autoencoder, load_model
+    from streamml.parallel import dp
+
+    env = dp.init_from_env("cuda")
+    dev = env.device
+    path = args.model
+    if path is None:
+        path = os.path.join(tempfile.gettempdir(), f"bench_ae_{os.getpid()}.h5")
+        if env.rank == 0 or True:
+            Autoencoder(device="cpu").save(path)
+    m = load_model(path, device=dev, input_normalizer="cardata")
+    be = m.backend
+    ev = synthetic_device_tensor(args.events + 100, dev, seed=env.rank, shard=env.rank,
+                                 n_shards=env.world_size).cpu().numpy()
+    host = torch.empty((1, 18), dtype=torch.float32).pin_memory()
+    out = torch.empty(1, dtype=torch.float32).pin_memory()
+    xdev = torch.empty((1, 18), dtype=torch.float32, device=dev)
+    lat = []
+    period = 1.0 / args.qps
+    t_next = time.perf_counter()
+    for i in range(args.events + 100):
+        while time.perf_counter() < t_next:
+            pass
+        host.copy_(torch.from_numpy(ev[i:i + 1]))
+        t0 = time.perf_counter()
+        xdev.copy_(host, non_blocking=True)
+        _, s, _ = be.forward(xdev, recon=False, score=True)
+        out.copy_(s, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        t1 = time.perf_counter()
+        if i >= 100:
+            lat.append((t1 - t0) * 1e6)
+        t_next += period
+    lat = np.asarray(lat)
+    # batched throughput
+    big = synthetic_device_tensor(args.batch * 8, dev, seed=1)
+    for _ in range(3):
+        be.forward(big[:args.batch], recon=False, score=True, threshold=args.threshold)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(40):
+        j = k % 8
+        be.forward(big[j * args.batch:(j + 1) * args.batch], recon=False, score=True, threshold=args.threshold)
+    torch.cuda.synchronize()
+    eps = args.batch * 40 / (time.perf_counter() - t0)
+    eps_all = dp.allreduce_max(eps, dev) if False else eps
+    if env.world_size > 1:
+        t = torch.tensor([eps], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t)
+        eps_all = float(t.item())
+    if env.rank == 0:
+        print(json.dumps({"metric": "p50 per-event inference latency (AE score)", "value": float(np.percentile(lat, 50)),
+                          "unit": "us", "higher_is_better": False, "p99_us": float(np.percentile(lat, 99)),
+                          "offered_qps": args.qps, "events": args.events, "n_gpus": env.world_size,
+                          "batched_events_per_s": eps_all, "batch": args.batch, "data": "synthetic"}))
+    dp.shutdown()
+
+
+if __name__ == "__main__":
+    main()

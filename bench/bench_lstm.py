@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""BASELINE config 3: LSTM sensor predictor (seq_len=50, 2-layer) bf16, synthetic stream, 1x MI355X.
+
+Model: LSTM(32, relu, return_sequences) -> LSTM(16, relu) -> Dense(18) predicting
+the next car event from a 50-event window (LSTM-.../cardata-v2.py task with
+look_back=50).  Each timed step = forward (bf16 input-projection GEMMs + fused HIP
+recurrence) + backward (fused HIP BPTT + weight-gradient GEMMs) + HIP Adam.
+Prints one JSON line: windows/s and events/s (= windows/s * seq_len).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--seq-len", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--stack", default="two_layer", choices=["two_layer", "reference"])
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    from streamml.data.cardata import normalize_affine, synthetic_device_tensor
+    from streamml.models.lstm import LSTMPredictor
+
+    dev = torch.device("cuda", 0)
+    T, B = args.seq_len, args.batch
+    ctor = LSTMPredictor.two_layer if args.stack == "two_layer" else LSTMPredictor.reference
+    m = ctor(look_back=T, device=dev)
+    sc, sh = normalize_affine()
+    raw = synthetic_device_tensor(B * 4 + T + 1, dev, seed=0)
+    xn = raw * torch.tensor(sc, dtype=torch.float32, device=dev) + torch.tensor(sh, dtype=torch.float32, device=dev)
+    # sliding windows [n, T, 18] -> next row targets
+    n = B * 4
+    idx = torch.arange(n, device=dev)[:, None] + torch.arange(T, device=dev)[None, :]
+    X = xn[idx].contiguous()
+    Y = xn[torch.arange(n, device=dev) + T].contiguous()
+    for s in range(args.warmup):
+        i = s % 4
+        m.train_step(X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        i = s % 4
+        loss, _ = m.train_step(X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    wps = B * args.steps / dt
+    print(json.dumps({"metric": "LSTM train windows/s (seq_len=%d, %s)" % (T, args.stack), "value": wps,
+                      "unit": "windows/s", "events_per_s": wps * T, "ms_per_step": dt / args.steps * 1e3,
+                      "batch": B, "seq_len": T, "params": m.count_params(), "dtype": "bf16",
+                      "final_loss": float(loss), "n_gpus": 1, "data": "synthetic"}))
+
+
+if __name__ == "__main__":
+    main()

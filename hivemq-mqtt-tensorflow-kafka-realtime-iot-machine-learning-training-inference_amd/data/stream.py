@@ -57,8 +57,12 @@ class Chunk:
     def select(self, mask_or_idx) -> "Chunk":
         keys = None
         if self.keys is not None:
-            idx = np.nonzero(mask_or_idx)[0] if np.asarray(mask_or_idx).dtype == bool else mask_or_idx
-            keys = [self.keys[i] for i in idx]
+            if isinstance(mask_or_idx, slice):
+                keys = self.keys[mask_or_idx]
+            else:
+                sel = np.asarray(mask_or_idx)
+                idx = np.nonzero(sel)[0] if sel.dtype == bool else sel
+                keys = [self.keys[i] for i in idx]
         return Chunk(self.x[mask_or_idx], self.label[mask_or_idx], keys,
                      None if self.offsets is None else self.offsets[mask_or_idx], dict(self.meta))
 

@@ -82,3 +82,11 @@ def test_partition_by_key():
     c = KafkaClient("fake://pbk")
     counts = [c.latest("sensor-data", p) for p in range(4)]
     assert sum(counts) == 2000 and min(counts) > 0
+
+
+def test_select_slice_with_keys():
+    c = S.Chunk(np.zeros((5, 18), np.float32), np.zeros(5, np.uint8), list("abcde"), np.arange(5))
+    assert c.select(slice(1, 3)).keys == ["b", "c"]
+    assert c.select(np.array([True, False, True, False, False])).keys == ["a", "c"]
+    b = list(S.Stream(lambda: iter([c, c])).batch(3))
+    assert [x.keys for x in b] == [list("abc"), list("dea"), list("bcd"), ["e"]]

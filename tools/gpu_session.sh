@@ -32,6 +32,12 @@ for s in $STEPS; do
     prof)
       (cd /tmp && step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
           python3 "$ROOT/bench.py" --steps 50 --warmup 5 --infer-events 100 ${BENCH_ARGS:-}) ;;
+    lstm) step bench_lstm 600 python bench/bench_lstm.py ${LSTM_ARGS:-} ;;
+    infer) step bench_infer 600 python bench/bench_infer.py ${INFER_ARGS:-} ;;
+    ingest) step bench_ingest 900 python bench/bench_ingest.py ${INGEST_ARGS:-} ;;
+    proflstm)
+      (cd /tmp && step rocprof_lstm 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_lstm" -o run -- \
+          python3 "$ROOT/bench/bench_lstm.py" --steps 10 --warmup 2) ;;
     sweep) step ae_sweep 600 python tools/ae_sweep.py ${SWEEP_ARGS:-} ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc)
