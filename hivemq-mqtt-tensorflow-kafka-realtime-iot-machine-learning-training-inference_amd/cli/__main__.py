@@ -1,0 +1,49 @@
+"""``python -m streamml.cli <command> ...`` dispatcher.
+
+Commands (reference script in parentheses):
+
+  cardata-v3   <servers> <topic> <offset> <result_topic> <mode> <model-file> <project>
+               (AUTOENCODER-TensorFlow-IO-Kafka/cardata-v3.py)
+  cardata-v1   <servers> <topic> <offset> [result_topic]   (AUTOENCODER-.../cardata-v1.py)
+  lstm-v2      <servers> <topic> <offset> <result_topic> <mode> <model-file>
+               (LSTM-TensorFlow-IO-Kafka/cardata-v2.py)
+  lstm-v1      <servers> <topic> <offset> [result_topic]   (LSTM-.../cardata-v1.py)
+  creditcard   [servers] [--evaluate]     (autoencoder-anomaly-detection/*.py, notebooks)
+  mnist        [servers] [--simplified]   (tensorflow-kafka-mnist*.py, confluent-tensorflow-io-kafka*.py)
+  produce      <servers> <topic> [--source ...]   (test-data feeders)
+  broker       [--port 9092] [--sasl user:pw] [--preload TOPIC=ROWS]
+"""
+from __future__ import annotations
+
+import sys
+
+from . import common
+
+
+def _commands():
+    from . import cardata_autoencoder as ae
+    from . import cardata_lstm as ls
+    from . import creditcard, mnist, tools
+    return {
+        "cardata-v3": ae.main_v3,
+        "cardata-v1": ae.main_v1,
+        "lstm-v2": ls.main_v2,
+        "lstm-v1": ls.main_v1,
+        "creditcard": creditcard.main,
+        "mnist": mnist.main,
+        "produce": tools.main_produce,
+        "broker": tools.main_broker,
+    }
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmds = _commands()
+    if not argv or argv[0] not in cmds:
+        print(__doc__)
+        return 1
+    return common.run(cmds[argv[0]], argv[1:])
+
+
+if __name__ == "__main__":
+    sys.exit(main())

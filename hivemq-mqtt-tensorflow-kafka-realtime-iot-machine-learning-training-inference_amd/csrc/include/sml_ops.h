@@ -27,6 +27,10 @@ hipError_t lstm_fwd_launch(const float* zx, const float* Uw, const float* h0, co
 hipError_t lstm_bwd_launch(const float* dh, const float* gates, const float* cseq, const float* c0, const float* Uw,
                            float* dz, float* dh0, float* dc0, int64_t B, int T, int U, int act, hipStream_t stream);
 
+// ---- softmax + sparse categorical cross-entropy (softmax_xent.hip) ----
+hipError_t softmax_xent_launch(const float* logits, const int64_t* labels, int64_t B, int C, float gscale,
+                               float* dlogits, float* probs, float* acc, hipStream_t stream);
+
 // ---- utilities (util.hip) ----
 hipError_t lane_xor_probe_launch(float* out, hipStream_t stream);
 

@@ -374,13 +374,18 @@ Connection& Client::any_conn() {
   return *any_;
 }
 
-void Client::refresh_metadata() {
+void Client::refresh_metadata(const std::string& topic) {
   W w;
-  w.arr(-1);  // all topics
+  if (topic.empty()) {
+    w.arr(-1);  // all topics
+  } else {
+    w.arr(1);
+    w.str(topic);
+  }
   const std::string resp = call(any_conn(), API_METADATA, 1, w.s);
   R r{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
   brokers_.clear();
-  leaders_.clear();
+  if (topic.empty()) leaders_.clear();
   for (int32_t nb = r.arr(), i = 0; i < nb; ++i) {
     const int32_t id = r.i32();
     std::string host = r.str();
@@ -390,7 +395,7 @@ void Client::refresh_metadata() {
   }
   r.i32();  // controller
   for (int32_t nt = r.arr(), i = 0; i < nt; ++i) {
-    r.i16();
+    const int16_t terr = r.i16();
     const std::string name = r.str();
     r.i8();
     std::vector<int32_t> lead;
@@ -403,7 +408,7 @@ void Client::refresh_metadata() {
       if ((int32_t)lead.size() <= pid) lead.resize((size_t)pid + 1, -1);
       lead[(size_t)pid] = leader;
     }
-    leaders_[name] = lead;
+    if (terr == E_NONE && !lead.empty()) leaders_[name] = lead;
   }
   conns_.clear();
 }
@@ -419,8 +424,14 @@ std::map<std::string, int> Client::partitions() {
 Connection& Client::conn_for(const std::string& topic, int partition) {
   auto it = leaders_.find(topic);
   if (it == leaders_.end() || partition >= (int)it->second.size()) {
-    refresh_metadata();
-    it = leaders_.find(topic);
+    // a named Metadata request auto-creates the topic on brokers that allow it; a
+    // freshly created topic may report LEADER_NOT_AVAILABLE once, so ask twice.
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      refresh_metadata(topic);
+      it = leaders_.find(topic);
+      if (it != leaders_.end()) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(50 * (attempt + 1)));
+    }
     if (it == leaders_.end()) throw Error("kafka: unknown topic " + topic, E_UNKNOWN_TOPIC);
     if (partition >= (int)it->second.size()) throw Error("kafka: unknown partition", E_UNKNOWN_TOPIC);
   }
@@ -786,6 +797,9 @@ std::string Broker::handle(int16_t api, int16_t ver, const uint8_t* body, size_t
       std::vector<std::string> names;
       if (nt < 0) for (const auto& kv : topics_) names.push_back(kv.first);
       else names = want;
+      if (cfg_.auto_create_topics)
+        for (const auto& name : want)
+          if (!name.empty() && topics_.find(name) == topics_.end()) topics_[name].resize(1);
       w.arr((int32_t)names.size());
       for (const auto& name : names) {
         auto it = topics_.find(name);

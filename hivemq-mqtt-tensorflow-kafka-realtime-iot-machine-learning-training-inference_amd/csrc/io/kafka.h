@@ -84,7 +84,9 @@ class Client {
   int64_t produce(const std::string& topic, int partition, const std::vector<Record>& recs, int16_t acks = 1);
   void commit(const std::string& group, const std::string& topic, int partition, int64_t offset);
   int64_t committed(const std::string& group, const std::string& topic, int partition);
-  void refresh_metadata();
+  // topic empty: all topics (replaces the cache); else that topic only (merged; on
+  // brokers with auto.create.topics.enable this creates it, as librdkafka does).
+  void refresh_metadata(const std::string& topic = std::string());
   uint64_t bytes_received() const { return bytes_rx_; }
 
  private:
@@ -112,6 +114,7 @@ struct BrokerConfig {
   int port = 0;  // 0 = ephemeral
   std::string sasl_username, sasl_password;  // empty = no auth
   int64_t retention_records = -1;           // -1 = unbounded
+  bool auto_create_topics = true;            // Kafka's auto.create.topics.enable default
 };
 
 class Broker {

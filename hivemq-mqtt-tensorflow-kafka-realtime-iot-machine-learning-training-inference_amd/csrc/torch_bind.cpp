@@ -193,6 +193,33 @@ std::vector<at::Tensor> lstm_bwd(const at::Tensor& dh, const at::Tensor& gates, 
   return {dz};
 }
 
+// Fused softmax + sparse CE: writes dlogits (= (softmax - onehot) * gscale) and/or
+// probabilities, and accumulates [loss_sum, correct] into acc.
+void softmax_xent(const at::Tensor& logits, const at::Tensor& labels, double gscale,
+                  const c10::optional<at::Tensor>& dlogits, const c10::optional<at::Tensor>& probs,
+                  const c10::optional<at::Tensor>& acc) {
+  check_dev(logits, "logits", at::kFloat);
+  check_dev(labels, "labels", at::kLong);
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "logits must be contiguous [B, C]");
+  const int64_t B = logits.size(0), C = logits.size(1);
+  TORCH_CHECK(labels.numel() == B && labels.is_contiguous(), "labels must be [B]");
+  TORCH_CHECK(C == 2 || C == 10 || C == 16 || C == 32, "softmax_xent supports C in {2, 10, 16, 32}");
+  for (const auto* t : {&dlogits, &probs}) {
+    if (t->has_value()) {
+      check_dev(**t, "out", at::kFloat);
+      TORCH_CHECK((*t)->is_contiguous() && (*t)->sizes() == logits.sizes(), "output must match logits");
+    }
+  }
+  if (acc.has_value()) {
+    check_dev(*acc, "acc", at::kFloat);
+    TORCH_CHECK(acc->numel() >= 2, "acc must hold 2 floats");
+  }
+  c10::hip::HIPGuard guard(logits.device().index());
+  SML_CHECK_HIP(sml::softmax_xent_launch(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), B, (int)C,
+                                         (float)gscale, opt_mut(dlogits), opt_mut(probs), opt_mut(acc),
+                                         cur_stream(logits)));
+}
+
 at::Tensor lane_xor_probe(const at::Tensor& like) {
   TORCH_CHECK(like.is_cuda(), "needs a device tensor for placement");
   c10::hip::HIPGuard guard(like.device().index());
@@ -270,6 +297,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("h0") = py::none(), py::arg("c0") = py::none(), py::arg("act") = 1);
   m.def("lstm_bwd", &lstm_bwd, "fused LSTM BPTT -> pre-activation gate grads", py::arg("dh"), py::arg("gates"),
         py::arg("cseq"), py::arg("c0"), py::arg("U"), py::arg("act") = 1, py::arg("want_state_grads") = false);
+  m.def("softmax_xent", &softmax_xent, "fused softmax + sparse categorical CE fwd/bwd", py::arg("logits"),
+        py::arg("labels"), py::arg("gscale"), py::arg("dlogits") = py::none(), py::arg("probs") = py::none(),
+        py::arg("acc") = py::none());
   m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),
         py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("recon"), py::arg("score"), py::arg("flag"),

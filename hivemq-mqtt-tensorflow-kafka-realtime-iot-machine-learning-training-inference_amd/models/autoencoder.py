@@ -199,8 +199,7 @@ class Autoencoder:
                 for xb in self._stream_batches(x, batch_size):
                     if steps_per_epoch is not None and steps >= steps_per_epoch:
                         break
-                    be.step(xb, global_batch=len(xb) * world, allreduce=allreduce) if self.device.type == "cuda" \
-                        else be.step(xb)
+                    be.step(xb, global_batch=len(xb) * world, allreduce=allreduce)
                     steps += 1
             else:
                 n = len(xd)
@@ -214,12 +213,12 @@ class Autoencoder:
                 xs = xd[order] if order is not None else xd
                 for b in range(nb):
                     xb = xs[b * batch_size:(b + 1) * batch_size]
-                    if self.device.type == "cuda":
-                        be.step(xb, global_batch=len(xb) * world, allreduce=allreduce)
-                    else:
-                        be.step(xb)
+                    be.step(xb, global_batch=len(xb) * world, allreduce=allreduce)
                     steps += 1
             m = be.read_metrics()
+            if world > 1:
+                from ..parallel.dp import reduce_metrics
+                m = reduce_metrics(m, self.device)
             logs = {"loss": m["loss"]}
             if "accuracy" in self.metrics:
                 logs["accuracy"] = m["accuracy"]

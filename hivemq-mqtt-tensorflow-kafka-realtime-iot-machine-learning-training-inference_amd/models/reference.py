@@ -102,11 +102,17 @@ class TorchAE:
         g = torch.autograd.grad(loss, self.w)
         return g, loss.detach(), mse.detach(), acc.detach()
 
-    def step(self, x: torch.Tensor) -> None:
+    def step(self, x: torch.Tensor, global_batch: Optional[int] = None, allreduce=None) -> None:
+        """One Adam step; under DP the local mean gradient is rescaled to this shard's share of the
+        global-batch mean and summed over replicas in ONE flat all-reduce (same contract as FusedAE)."""
         x = x.to(self.device, self.dtype)
         g, loss, mse, acc = self.grads(x)
-        self.opt.apply(g)
         n = x.shape[0]
+        if allreduce is not None:
+            flat = torch.cat([gi.reshape(-1) for gi in g]) * (n / float(global_batch or n))
+            allreduce(flat)
+            g = [c.view_as(w) for c, w in zip(torch.split(flat, [w.numel() for w in self.w]), self.w)]
+        self.opt.apply(g)
         self._acc[0] += float(loss) * n
         self._acc[1] += float(mse) * n
         self._acc[2] += float(acc) * n

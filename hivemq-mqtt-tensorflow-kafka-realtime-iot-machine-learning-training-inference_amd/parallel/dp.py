@@ -88,6 +88,20 @@ def allreduce_max(value: float, device: torch.device) -> float:
     return value
 
 
+def reduce_metrics(metrics: dict, device: torch.device, weight_key: str = "rows") -> dict:
+    """Row-weighted average of per-replica epoch metrics (one small all-reduce per epoch)."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return dict(metrics)
+    keys = [k for k in metrics if k != weight_key]
+    w = float(metrics.get(weight_key, 1.0))
+    t = torch.tensor([float(metrics[k]) * w for k in keys] + [w], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    tot = float(t[-1].item())
+    out = {k: float(t[i].item()) / max(tot, 1e-30) for i, k in enumerate(keys)}
+    out[weight_key] = tot
+    return out
+
+
 def barrier(device: Optional[torch.device] = None) -> None:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         if device is not None and device.type == "cuda":
