@@ -31,6 +31,18 @@ hipError_t lstm_bwd_launch(const float* dh, const float* gates, const float* cse
 hipError_t softmax_xent_launch(const float* logits, const int64_t* labels, int64_t B, int C, float gscale,
                                float* dlogits, float* probs, float* acc, hipStream_t stream);
 
+// ---- tall-skinny dense layers (dense.hip) ----
+int dense_tiles(int d);
+bool dense_supported(int K, int N);
+int dense_wgrad_slab(int K, int N);
+int dense_wgrad_grid(int64_t M, int max_blocks);
+int slab_sum_scratch(int G, int S);
+hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, float* out, hipStream_t stream);
+hipError_t rowgemm_launch(const void* X, int x_bf16, int64_t M, int K, int64_t ldx, const float* W, const float* bias,
+                          int N, int act, void* Y, int y_bf16, int64_t ldy, int max_blocks, hipStream_t stream);
+hipError_t wgrad_launch(const void* X, int x_bf16, int64_t M, int K, int64_t ldx, int shift_T, const void* DY,
+                        int dy_bf16, int N, int64_t ldy, int want_db, float* partials, int grid, hipStream_t stream);
+
 // ---- utilities (util.hip) ----
 hipError_t lane_xor_probe_launch(float* out, hipStream_t stream);
 

@@ -220,6 +220,60 @@ void softmax_xent(const at::Tensor& logits, const at::Tensor& labels, double gsc
                                          cur_stream(logits)));
 }
 
+// K1: Y = act(X . W + b) for tall-skinny X [M, K] (fp32 or bf16), W [K, N] fp32.
+at::Tensor dense_fwd(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::Tensor>& bias, int64_t act,
+                     bool out_bf16, int64_t max_blocks) {
+  TORCH_CHECK(x.is_cuda() && W.is_cuda(), "dense_fwd needs ROCm device tensors");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be fp32 or bf16");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [M, K] with unit inner stride");
+  check_dev(W, "W", at::kFloat);
+  TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.size(0) == x.size(1), "W must be contiguous [K, N]");
+  const int64_t M = x.size(0), K = x.size(1), N = W.size(1);
+  TORCH_CHECK(sml::dense_supported((int)K, (int)N), "dense_fwd: K=", K, " N=", N, " exceeds the register tile");
+  if (bias.has_value()) {
+    check_dev(*bias, "bias", at::kFloat);
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "bias must be [N]");
+  }
+  TORCH_CHECK(act >= 0 && act <= 3, "act must be 0..3");
+  c10::hip::HIPGuard guard(x.device().index());
+  auto y = at::empty({M, N}, x.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  SML_CHECK_HIP(sml::rowgemm_launch(x.data_ptr(), x.scalar_type() == at::kBFloat16, M, (int)K, x.stride(0),
+                                    W.data_ptr<float>(), opt_ptr(bias), (int)N, (int)act, y.data_ptr(), out_bf16, N,
+                                    (int)max_blocks, cur_stream(x)));
+  return y;
+}
+
+// K2 (weight half): dW = X^T . dY, db = colsum(dY) over M rows (split-row MFMA + slab reduce).
+// shift_T > 0: X row r is read as X[r - 1] (zero when r % shift_T == 0).
+std::vector<at::Tensor> dense_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t shift_T, bool want_db,
+                                    int64_t max_blocks) {
+  TORCH_CHECK(x.is_cuda() && dy.is_cuda(), "dense_wgrad needs ROCm device tensors");
+  for (const auto* t : {&x, &dy}) {
+    TORCH_CHECK(t->scalar_type() == at::kFloat || t->scalar_type() == at::kBFloat16, "inputs must be fp32 or bf16");
+    TORCH_CHECK(t->dim() == 2 && t->stride(1) == 1, "inputs must be 2-D with unit inner stride");
+  }
+  TORCH_CHECK(x.size(0) == dy.size(0), "row count mismatch");
+  const int64_t M = x.size(0), K = x.size(1), N = dy.size(1);
+  TORCH_CHECK(sml::dense_supported((int)K, (int)N), "dense_wgrad: K=", K, " N=", N, " exceeds the register tile");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int S = sml::dense_wgrad_slab((int)K, (int)N);
+  const int G = sml::dense_wgrad_grid(M, (int)max_blocks);
+  auto opts = x.options().dtype(at::kFloat);
+  auto partials = at::empty({G, S}, opts);
+  auto out = at::empty({S}, opts);
+  auto scratch = at::empty({std::max(1, sml::slab_sum_scratch(G, S))}, opts);
+  auto st = cur_stream(x);
+  SML_CHECK_HIP(sml::wgrad_launch(x.data_ptr(), x.scalar_type() == at::kBFloat16, M, (int)K, x.stride(0),
+                                  (int)shift_T, dy.data_ptr(), dy.scalar_type() == at::kBFloat16, (int)N,
+                                  dy.stride(0), want_db ? 1 : 0, partials.data_ptr<float>(), G, st));
+  SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
+                                     out.data_ptr<float>(), st));
+  const int64_t KP = 16 * sml::dense_tiles((int)K), NP = 16 * sml::dense_tiles((int)N);
+  auto dW = out.narrow(0, 0, KP * NP).view({KP, NP}).narrow(0, 0, K).narrow(1, 0, N);
+  auto db = out.narrow(0, KP * NP, N);
+  return {dW, db};
+}
+
 at::Tensor lane_xor_probe(const at::Tensor& like) {
   TORCH_CHECK(like.is_cuda(), "needs a device tensor for placement");
   c10::hip::HIPGuard guard(like.device().index());
@@ -300,6 +354,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("softmax_xent", &softmax_xent, "fused softmax + sparse categorical CE fwd/bwd", py::arg("logits"),
         py::arg("labels"), py::arg("gscale"), py::arg("dlogits") = py::none(), py::arg("probs") = py::none(),
         py::arg("acc") = py::none());
+  m.def("dense_fwd", &dense_fwd, "K1 tall-skinny dense forward act(X.W + b) on MFMA", py::arg("x"), py::arg("W"),
+        py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("out_bf16") = false, py::arg("max_blocks") = 1024);
+  m.def("dense_wgrad", &dense_wgrad, "K2 weight gradient X^T.dY (+ colsum dY) over rows", py::arg("x"),
+        py::arg("dy"), py::arg("shift_T") = 0, py::arg("want_db") = true, py::arg("max_blocks") = 512);
+  m.def("dense_supported", &sml::dense_supported, "whether (K, N) fits the register-resident tile", py::arg("K"),
+        py::arg("N"));
   m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),
         py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("recon"), py::arg("score"), py::arg("flag"),

@@ -32,6 +32,7 @@ from ..ckpt import h5 as ckh5
 from ..nn import keras_config as kc
 from ..nn.callbacks import Callback, History
 from ..ops.adam import FlatAdam, FlatParams
+from ..ops.dense import dense as dense_op
 from ..ops.lstm import lstm as lstm_op
 
 # layer spec: ("lstm", units, return_sequences, activation) | ("repeat", n) | ("dense", units, time_distributed)
@@ -135,8 +136,7 @@ class LSTMPredictor:
                 h = h.unsqueeze(1).expand(h.shape[0], L["n"], h.shape[-1]).contiguous()
             else:
                 K, b = P[L["params"]:L["params"] + 2]
-                shp = h.shape
-                h = (_bf16_mm(h.reshape(-1, shp[-1]), K) + b).reshape(*shp[:-1], K.shape[1])
+                h = dense_op(h, K, b)          # K1/K2 tall-skinny MFMA kernels on ROCm
         return h
 
     def _loss(self, y_pred: torch.Tensor, y: torch.Tensor):

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import torch
 
+from . import dense as dn
 from ._ext import load_c
 
 ACT = {"relu": 1, "tanh": 2}
@@ -45,19 +46,28 @@ def lstm_reference(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.T
 
 
 def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """bf16 MFMA GEMM via hipBLASLt, fp32 result."""
+    """bf16 MFMA GEMM via hipBLASLt, fp32 result (shapes beyond the K1/K2 register tile)."""
     return (a.to(torch.bfloat16) @ b.to(torch.bfloat16)).float()
 
 
 class LSTMFunction(torch.autograd.Function):
+    """Input projection / weight gradients / dX on the K1/K2 tall-skinny kernels
+    (hipBLASLt when a layer is too wide for them), recurrence on lstm_fwd/lstm_bwd."""
+
     @staticmethod
     def forward(ctx, x, W, U, b, act_code: int):
         B, T, inp = x.shape
         u = U.shape[0]
-        zx = (_mm(x.reshape(B * T, inp), W) + b).reshape(B, T, 4 * u).contiguous()
+        x2 = x.reshape(B * T, inp)
+        fast = dn.supported(inp, 4 * u) and dn.supported(4 * u, inp)
+        if fast:
+            zx = dn.rowgemm(x2, W, b).reshape(B, T, 4 * u)
+        else:
+            zx = (_mm(x2, W) + b).reshape(B, T, 4 * u).contiguous()
         h, c, gates = load_c().lstm_fwd(zx, U.contiguous(), None, None, act_code)
         ctx.save_for_backward(x, W, U, h, c, gates)
         ctx.act = act_code
+        ctx.fast = fast
         return h
 
     @staticmethod
@@ -67,12 +77,21 @@ class LSTMFunction(torch.autograd.Function):
         u = U.shape[0]
         (dz,) = load_c().lstm_bwd(dh.contiguous().float(), gates, c, None, U.contiguous(), ctx.act, False)
         dz2 = dz.reshape(B * T, 4 * u)
-        dW = _mm(x.reshape(B * T, inp).t(), dz2) if ctx.needs_input_grad[1] else None
+        x2 = x.reshape(B * T, inp)
+        h2 = h.reshape(B * T, u)
+        dW = dU = db = dx = None
+        if ctx.fast:
+            if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
+                dW, db = dn.wgrad(x2, dz2)                       # one pass: X^T.dz and colsum(dz)
+            if ctx.needs_input_grad[2]:
+                dU, _ = dn.wgrad(h2, dz2, shift_T=T, want_db=False)   # h_{t-1}^T . dz, no copy of h
+            if ctx.needs_input_grad[0]:
+                dx = dn.rowgemm(dz2, W.t().contiguous()).reshape(B, T, inp)
+            return dx, dW, dU, db, None
+        dW = _mm(x2.t(), dz2) if ctx.needs_input_grad[1] else None
         if ctx.needs_input_grad[2]:
             hprev = torch.cat([h.new_zeros(B, 1, u), h[:, :-1]], dim=1).reshape(B * T, u)
             dU = _mm(hprev.t(), dz2)
-        else:
-            dU = None
         db = dz2.sum(0) if ctx.needs_input_grad[3] else None
         dx = _mm(dz2, W.t()).reshape(B, T, inp) if ctx.needs_input_grad[0] else None
         return dx, dW, dU, db, None

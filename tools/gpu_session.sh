@@ -38,6 +38,14 @@ for s in $STEPS; do
     proflstm)
       (cd /tmp && step rocprof_lstm 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_lstm" -o run -- \
           python3 "$ROOT/bench/bench_lstm.py" --steps 10 --warmup 2) ;;
+    cli)
+      step cli_ae_train 600 python -m streamml.cli cardata-v3 synthetic://50000 SENSOR_DATA_S_AVRO 0 model-predictions \
+          train model1.h5 demo --workdir "$OUT/cli" --store "$OUT/cli/store" &&
+      step cli_ae_predict 600 python -m streamml.cli cardata-v3 synthetic://50000 SENSOR_DATA_S_AVRO 0 \
+          model-predictions predict model1.h5 demo --workdir "$OUT/cli" --store "$OUT/cli/store" &&
+      step cli_lstm 600 python -m streamml.cli lstm-v1 synthetic://5000 SENSOR_DATA_S_AVRO 0 out --epochs 1 --take 300 &&
+      step cli_mnist 600 python -m streamml.cli mnist --epochs 1 --steps-per-epoch 3000 --rows 20000 &&
+      step cli_creditcard 600 python -m streamml.cli creditcard --evaluate --rows 100000 --epochs 3 ;;
     sweep) step ae_sweep 600 python tools/ae_sweep.py ${SWEEP_ARGS:-} ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc)

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Per-kernel register / LDS / occupancy table for a HIP source, from the compiler's
+``-Rpass-analysis=kernel-resource-usage`` remarks (no GPU needed).
+
+    python tools/kernel_resources.py <package>/csrc/kernels/dense.hip [filter-substring]
+"""
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "hivemq-mqtt-tensorflow-kafka-realtime-iot-machine-learning-training-inference_amd")
+
+
+def demangle(names):
+    try:
+        out = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True,
+                             text=True, check=True).stdout.splitlines()
+        return out
+    except Exception:
+        return names
+
+
+def main():
+    src = sys.argv[1]
+    filt = sys.argv[2] if len(sys.argv) > 2 else ""
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-munsafe-fp-atomics", "-mllvm",
+           "-amdgpu-mfma-vgpr-form", "-I", os.path.join(PKG, "csrc", "include"), "-c", src, "-o", "/dev/null",
+           "--offload-device-only", "-Rpass-analysis=kernel-resource-usage"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    rows, cur = [], None
+    for line in r.stderr.splitlines():
+        m = re.search(r"remark: (.*?) \[-Rpass", line)
+        if not m:
+            continue
+        msg = m.group(1)
+        if msg.startswith("Function Name:"):
+            cur = {"name": msg.split(":", 1)[1].strip()}
+            rows.append(cur)
+        elif cur is not None and ":" in msg:
+            k, v = msg.split(":", 1)
+            cur[k.strip()] = v.strip()
+    names = demangle([r["name"] for r in rows])
+    print(f"{'kernel':70s} {'VGPR':>5s} {'AGPR':>5s} {'spillV':>6s} {'spillS':>6s} {'occ':>4s} {'LDS':>7s}")
+    for r, n in zip(rows, names):
+        n = re.sub(r"sml::\(anonymous namespace\)::", "", n)
+        n = re.sub(r"\(.*\)$", "", n)
+        if filt and filt not in n:
+            continue
+        print(f"{n[:70]:70s} {r.get('VGPRs', '?'):>5s} {r.get('AGPRs', '?'):>5s} {r.get('VGPRs Spill', '?'):>6s} "
+              f"{r.get('SGPRs Spill', '?'):>6s} {r.get('Occupancy [waves/SIMD]', '?'):>4s} "
+              f"{r.get('LDS Size [bytes/block]', '?'):>7s}")
+    return r.returncode if False else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
