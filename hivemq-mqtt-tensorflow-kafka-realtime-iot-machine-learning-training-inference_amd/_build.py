@@ -77,10 +77,13 @@ def build_c(verbose: bool = False, force: bool = False) -> str:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _newer([src] + hdrs, obj):
+            with open(src) as f:
+                head = f.read(512)
+            # MFMA results straight into VGPRs (no v_accvgpr_read per use), except for
+            # kernels that keep large accumulator sets in AGPRs
+            vgpr_form = [] if "sml-build: agpr-accumulators" in head else ["-mllvm", "-amdgpu-mfma-vgpr-form"]
             jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
-                         f"-I{inc}", "-Wno-unused-result", "-munsafe-fp-atomics",
-                         # MFMA results straight into VGPRs: no v_accvgpr_read per use
-                         "-mllvm", "-amdgpu-mfma-vgpr-form"])
+                         f"-I{inc}", "-Wno-unused-result", "-munsafe-fp-atomics", *vgpr_form])
     # host runtime pieces that use the HIP runtime API (no device code, no torch)
     for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
         obj = os.path.join(BUILD, "rt_" + os.path.basename(src) + ".o")

@@ -43,6 +43,18 @@ hipError_t rowgemm_launch(const void* X, int x_bf16, int64_t M, int K, int64_t l
 hipError_t wgrad_launch(const void* X, int x_bf16, int64_t M, int K, int64_t ldx, int shift_T, const void* DY,
                         int dy_bf16, int N, int64_t ldy, int want_db, float* partials, int grid, hipStream_t stream);
 
+// ---- fully fused LSTM layer (lstm_fused.hip) ----
+bool lstm_fused_supported(int U, int IN);
+int lstm_fused_slab(int U, int IN);
+int lstm_fused_waves(int64_t B);
+hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw, const float* b, const float* h0,
+                                 const float* c0, float* hseq, float* cseq, void* gates_bf16, int64_t B, int T,
+                                 int IN, int U, int act, hipStream_t stream);
+hipError_t lstm_fused_bwd_launch(const float* dh, const void* gates_bf16, const float* cseq, const float* hseq,
+                                 const float* x, const float* h0, const float* c0, const float* W, const float* Uw,
+                                 float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
+                                 int act, hipStream_t stream);
+
 // ---- utilities (util.hip) ----
 hipError_t lane_xor_probe_launch(float* out, hipStream_t stream);
 

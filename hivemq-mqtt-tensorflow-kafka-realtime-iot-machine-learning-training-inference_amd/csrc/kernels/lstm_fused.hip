@@ -1,0 +1,450 @@
+// sml-build: agpr-accumulators
+//
+// Fully fused LSTM layer kernels for gfx950: ONE launch for the forward pass
+// and ONE for the backward pass of a Keras LSTM layer (reference
+// LSTM-TensorFlow-IO-Kafka/cardata-v2.py:177-183: activation relu|tanh,
+// recurrent_activation sigmoid, gate order i,f,c,o).
+//
+// Why: at the BASELINE config-3 shapes (B*T = 409 600 rows, 4u = 128 gates) the
+// unfused layer moved ~2 GB per training step through HBM (x.W written as Zx and
+// re-read, fp32 gates, dz written and re-read by three weight-gradient / dX
+// GEMMs).  Fused, a layer reads x, h, c and bf16 gates once per pass:
+//
+//   forward, per step t (one wave = 16 sequences, h / c in VGPRs):
+//     z^T[4u,16] = b + W^T . x_t^T + U^T . h_{t-1}^T     (all on MFMA)
+//     gates -> bf16 store (for BPTT), c_t, h_t -> fp32 store
+//   backward, per step t = T-1 .. 0:
+//     dz_t from (dh_t + U.dz_{t+1}) and the stored gates / cell state
+//     dh_{t-1}^T = U . dz_t^T                (critical path, MFMA)
+//     dX_t^T     = W . dz_t^T                (MFMA, optional)
+//     dW^T += dz_t^T . x_t,  dU^T += dz_t^T . h_{t-1},  db += colsum(dz_t)
+//       -> register accumulators (AGPRs) over the wave's 16 sequences x T
+//          steps; the contraction over sequences needs dz_t^T as an A operand,
+//          obtained with one LDS transpose per gate tile (ds_read_b64_tr_b16).
+//     Each wave writes one fp32 slab of [dW^T | dU^T | db]; slab_sum_kernel
+//     (dense.hip) reduces the slabs deterministically.
+//
+// MFMA orientation (v_mfma_f32_16x16x16_bf16, lane c = l & 15, g = l >> 4):
+//   C tile mt of z: lane (c, g) holds gate 16mt + 4g + i of sequence s0 + c, so
+//   the four gates of unit u sit in tiles q*UB + u/16 of the same lane/register.
+// This file is compiled without -amdgpu-mfma-vgpr-form so the weight-gradient
+// accumulators can live in AGPRs (launch_bounds(256, 1): 512 registers/lane).
+#include "sml_common.h"
+#include "sml_ops.h"
+
+using namespace sml;
+
+namespace {
+
+constexpr int WAVES = 4;
+
+__device__ __forceinline__ float act_f(int a, float z) { return a == ACT_RELU ? relu_fast(z) : tanh_fast(z); }
+__device__ __forceinline__ float act_d(int a, float z, float y) {
+  return a == ACT_RELU ? (z > 0.f ? 1.f : 0.f) : fmaf(-y, y, 1.0f);
+}
+
+__device__ __forceinline__ bf16x4 ld_bf16x4(const __bf16* p) { return *reinterpret_cast<const bf16x4*>(p); }
+__device__ __forceinline__ f32x4 unpack4(bf16x4 v) {
+  f32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = bf16_to_f32((unsigned short)v[j]);
+  return r;
+}
+
+struct FusedFwdArgs {
+  const float* x;      // [B, T, IN]
+  const float* W;      // [IN, 4U]
+  const float* Uw;     // [U, 4U]
+  const float* b;      // [4U]
+  const float* h0;     // [B, U] or null
+  const float* c0;     // [B, U] or null
+  float* hseq;         // [B, T, U]
+  float* cseq;         // [B, T, U]
+  __bf16* gates;       // [B, T, 4U]  post-activation i, f, c~, o
+  int64_t B;
+  int T, IN, act;
+};
+
+template <int U, int KT>
+__global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdArgs a) {
+  constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int64_t s0 = ((int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * 16;
+  if (s0 >= a.B) return;  // wave-uniform
+  const int64_t seq = s0 + c;
+  const bool valid = seq < a.B;
+  const int64_t sq = valid ? seq : a.B - 1;
+  const int IN = a.IN, T = a.T;
+
+  // A fragments: W^T[m = gate][k = feature], U^T[m = gate][k = unit]
+  bf16x4 wt[MT][KT], ut[MT][UB];
+  f32x4 bias[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      f32x4 t4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 16 * kt + 4 * g + j;
+        t4[j] = k < IN ? a.W[(int64_t)k * G4 + 16 * mt + c] : 0.f;
+      }
+      wt[mt][kt] = pack4(t4);
+    }
+#pragma unroll
+    for (int s = 0; s < UB; ++s) {
+      f32x4 t4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t4[j] = a.Uw[(16 * s + 4 * g + j) * G4 + 16 * mt + c];
+      ut[mt][s] = pack4(t4);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[mt][i] = a.b[16 * mt + 4 * g + i];
+  }
+  f32x4 h[UB], cs[UB];
+  bf16x4 hb[UB];
+#pragma unroll
+  for (int b = 0; b < UB; ++b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = 16 * b + 4 * g + i;
+      h[b][i] = a.h0 ? a.h0[sq * U + u] : 0.f;
+      cs[b][i] = a.c0 ? a.c0[sq * U + u] : 0.f;
+    }
+    hb[b] = pack4(h[b]);
+  }
+  // x_t^T as B operand: B[k = feature 16kt + 4g + j][n = sequence c]
+  const float* xrow = a.x + sq * (int64_t)T * IN;
+  auto load_x = [&](int t, f32x4* v) {
+    const float* p = xrow + (int64_t)t * IN;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 16 * kt + 4 * g + j;
+        v[kt][j] = k < IN ? p[k] : 0.f;
+      }
+  };
+  f32x4 xn[KT];
+  load_x(0, xn);
+  for (int t = 0; t < T; ++t) {
+    bf16x4 xb[KT];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) xb[kt] = pack4(xn[kt]);
+    if (t + 1 < T) load_x(t + 1, xn);   // next step's input, in flight during this step
+    f32x4 z[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      z[mt] = bias[mt];
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) z[mt] = mfma16(wt[mt][kt], xb[kt], z[mt]);
+#pragma unroll
+      for (int s = 0; s < UB; ++s) z[mt] = mfma16(ut[mt][s], hb[s], z[mt]);
+    }
+    const int64_t bg = (sq * T + t) * (int64_t)G4;
+    const int64_t bu = (sq * T + t) * (int64_t)U;
+#pragma unroll
+    for (int b = 0; b < UB; ++b) {
+      f32x4 gi, gf, gc, go;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        gi[i] = sigmoid_fast(z[b][i]);
+        gf[i] = sigmoid_fast(z[UB + b][i]);
+        gc[i] = act_f(a.act, z[2 * UB + b][i]);
+        go[i] = sigmoid_fast(z[3 * UB + b][i]);
+        cs[b][i] = fmaf(gf[i], cs[b][i], gi[i] * gc[i]);
+        h[b][i] = go[i] * act_f(a.act, cs[b][i]);
+      }
+      if (valid) {
+        const int off = 16 * b + 4 * g;
+        *reinterpret_cast<bf16x4*>(a.gates + bg + off) = pack4(gi);
+        *reinterpret_cast<bf16x4*>(a.gates + bg + U + off) = pack4(gf);
+        *reinterpret_cast<bf16x4*>(a.gates + bg + 2 * U + off) = pack4(gc);
+        *reinterpret_cast<bf16x4*>(a.gates + bg + 3 * U + off) = pack4(go);
+        *reinterpret_cast<f32x4*>(a.cseq + bu + off) = cs[b];
+        *reinterpret_cast<f32x4*>(a.hseq + bu + off) = h[b];
+      }
+      hb[b] = pack4(h[b]);
+    }
+  }
+}
+
+struct FusedBwdArgs {
+  const float* dh;     // [B, T, U]  gradient w.r.t. the h sequence
+  const __bf16* gates; // [B, T, 4U]
+  const float* cseq;   // [B, T, U]
+  const float* hseq;   // [B, T, U]
+  const float* x;      // [B, T, IN]
+  const float* h0;     // [B, U] or null
+  const float* c0;     // [B, U] or null
+  const float* W;      // [IN, 4U]
+  const float* Uw;     // [U, 4U]
+  float* dx;           // [B, T, IN] or null
+  float* dh0;          // [B, U] or null
+  float* dc0;          // [B, U] or null
+  float* partials;     // [nwaves, S]: dW^T [4U][16KT] | dU^T [4U][U] | db [4U]
+  int64_t B;
+  int T, IN, act;
+};
+
+template <int U, int KT>
+__global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdArgs a) {
+  constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
+  constexpr int LDW = 16 * KT;
+  constexpr int S = G4 * (LDW + U + 1);
+  __shared__ __attribute__((aligned(16))) char scratch[WAVES][MT * 512];
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int w = threadIdx.x >> 6;
+  const int64_t wave_id = (int64_t)blockIdx.x * WAVES + w;
+  const int64_t s0 = wave_id * 16;
+  if (s0 >= a.B) return;
+  const int64_t seq = s0 + c;
+  const bool valid = seq < a.B;
+  const int64_t sq = valid ? seq : a.B - 1;
+  const int IN = a.IN, T = a.T;
+  char* scr = scratch[w];
+
+  // A fragments: U[m = unit][k = gate] (for dh), W[m = feature][k = gate] (for dX)
+  bf16x4 uf[UB][MT];
+#pragma unroll
+  for (int b = 0; b < UB; ++b)
+#pragma unroll
+    for (int kt = 0; kt < MT; ++kt) {
+      f32x4 t4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t4[j] = a.Uw[(16 * b + c) * G4 + 16 * kt + 4 * g + j];
+      uf[b][kt] = pack4(t4);
+    }
+  const bool want_dx = a.dx != nullptr;
+  bf16x4 wf[KT][MT];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      f32x4 t4;
+      const int f = 16 * kt + c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t4[j] = (want_dx && f < IN) ? a.W[(int64_t)f * G4 + 16 * mt + 4 * g + j] : 0.f;
+      wf[kt][mt] = pack4(t4);
+    }
+  bf16x4 onesb;   // B[k][n] = (n == 0): C[m][0] = sum_k A[m][k]
+#pragma unroll
+  for (int j = 0; j < 4; ++j) onesb[j] = (c == 0) ? (short)0x3F80 : (short)0;
+
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 accW[MT][KT], accU[MT][UB], accb[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) accW[mt][kt] = zero4;
+#pragma unroll
+    for (int kb = 0; kb < UB; ++kb) accU[mt][kb] = zero4;
+    accb[mt] = zero4;
+  }
+  f32x4 dhr[UB], dcn[UB];
+#pragma unroll
+  for (int b = 0; b < UB; ++b) dhr[b] = dcn[b] = zero4;
+
+  // per-step operands; "C layout" ones indexed by this lane's sequence, the
+  // weight-gradient B operands by rows (sequences) s0 + 4g + j
+  struct Step {
+    bf16x4 gi[UB], gf[UB], gc[UB], go[UB];
+    f32x4 ct[UB], cprev[UB], dho[UB];
+    f32x4 hprev[UB];   // B[k = seq 4g + j][n = unit 16kb + c]
+    f32x4 xt[KT];      // B[k = seq 4g + j][n = feature 16kt + c]
+  };
+  auto load_step = [&](int t, Step& st) {
+    const int64_t bg = (sq * T + t) * (int64_t)G4;
+    const int64_t bu = (sq * T + t) * (int64_t)U;
+#pragma unroll
+    for (int b = 0; b < UB; ++b) {
+      const int off = 16 * b + 4 * g;
+      st.gi[b] = ld_bf16x4(a.gates + bg + off);
+      st.gf[b] = ld_bf16x4(a.gates + bg + U + off);
+      st.gc[b] = ld_bf16x4(a.gates + bg + 2 * U + off);
+      st.go[b] = ld_bf16x4(a.gates + bg + 3 * U + off);
+      st.ct[b] = *reinterpret_cast<const f32x4*>(a.cseq + bu + off);
+      if (t > 0) st.cprev[b] = *reinterpret_cast<const f32x4*>(a.cseq + bu - U + off);
+      else if (a.c0) st.cprev[b] = *reinterpret_cast<const f32x4*>(a.c0 + sq * U + off);
+      else st.cprev[b] = zero4;
+      st.dho[b] = valid ? *reinterpret_cast<const f32x4*>(a.dh + bu + off) : zero4;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t r = s0 + 4 * g + j;
+      const bool rok = r < a.B;
+      const int64_t rr = rok ? r : 0;
+#pragma unroll
+      for (int kb = 0; kb < UB; ++kb) {
+        const int u = 16 * kb + c;
+        float hv = 0.f;
+        if (rok) {
+          if (t > 0) hv = a.hseq[(rr * T + t - 1) * (int64_t)U + u];
+          else if (a.h0) hv = a.h0[rr * U + u];
+        }
+        st.hprev[kb][j] = hv;
+      }
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const int f = 16 * kt + c;
+        st.xt[kt][j] = (rok && f < IN) ? a.x[(rr * T + t) * (int64_t)IN + f] : 0.f;
+      }
+    }
+  };
+
+  Step cur, nxt;
+  load_step(T - 1, nxt);
+  for (int t = T - 1; t >= 0; --t) {
+    cur = nxt;
+    if (t > 0) load_step(t - 1, nxt);          // in flight during this step
+    const f32x4* cp = cur.cprev;                // c_{t-1}
+    f32x4 dzt[MT];
+#pragma unroll
+    for (int b = 0; b < UB; ++b) {
+      const f32x4 gi = unpack4(cur.gi[b]), gf = unpack4(cur.gf[b]), gc = unpack4(cur.gc[b]),
+                  go = unpack4(cur.go[b]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float dh = cur.dho[b][i] + dhr[b][i];
+        const float ct = cur.ct[b][i];
+        const float ac = act_f(a.act, ct);
+        const float dc = dcn[b][i] + dh * go[i] * act_d(a.act, ct, ac);
+        dzt[b][i] = dc * gc[i] * gi[i] * (1.f - gi[i]);
+        dzt[UB + b][i] = dc * cp[b][i] * gf[i] * (1.f - gf[i]);
+        const float gcd = a.act == ACT_RELU ? (gc[i] > 0.f ? 1.f : 0.f) : fmaf(-gc[i], gc[i], 1.f);
+        dzt[2 * UB + b][i] = dc * gi[i] * gcd;
+        dzt[3 * UB + b][i] = dh * ac * go[i] * (1.f - go[i]);
+        dcn[b][i] = dc * gf[i];
+      }
+    }
+    if (!valid) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) dzt[mt] = zero4;
+    }
+    bf16x4 dzb[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) dzb[mt] = pack4(dzt[mt]);
+    // critical path: recurrent gradient for step t-1
+#pragma unroll
+    for (int b = 0; b < UB; ++b) {
+      f32x4 acc = zero4;
+#pragma unroll
+      for (int kt = 0; kt < MT; ++kt) acc = mfma16(uf[b][kt], dzb[kt], acc);
+      dhr[b] = acc;
+    }
+    // input gradient dX_t^T = W . dz_t^T
+    if (want_dx) {
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        f32x4 acc = zero4;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc = mfma16(wf[kt][mt], dzb[mt], acc);
+        if (valid) {
+          float* p = a.dx + (sq * T + t) * (int64_t)IN;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int f = 16 * kt + 4 * g + i;
+            if (f < IN) p[f] = acc[i];
+          }
+        }
+      }
+    }
+    // weight gradients: dz_t^T as A operand (one LDS transpose per gate tile)
+    bf16x4 hB[UB], xB[KT];
+#pragma unroll
+    for (int kb = 0; kb < UB; ++kb) hB[kb] = pack4(cur.hprev[kb]);
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) xB[kt] = pack4(cur.xt[kt]);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const bf16x4 adz = lds_transpose(dzb[mt], scr + mt * 512, c, g);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) accW[mt][kt] = mfma16(adz, xB[kt], accW[mt][kt]);
+#pragma unroll
+      for (int kb = 0; kb < UB; ++kb) accU[mt][kb] = mfma16(adz, hB[kb], accU[mt][kb]);
+      accb[mt] = mfma16(adz, onesb, accb[mt]);
+    }
+  }
+  if (valid) {
+#pragma unroll
+    for (int b = 0; b < UB; ++b) {
+      const int off = 16 * b + 4 * g;
+      if (a.dh0) *reinterpret_cast<f32x4*>(a.dh0 + sq * U + off) = dhr[b];
+      if (a.dc0) *reinterpret_cast<f32x4*>(a.dc0 + sq * U + off) = dcn[b];
+    }
+  }
+  // this wave's slab (C layout: row m = gate 16mt + 4g + i, column = lane c)
+  float* out = a.partials + wave_id * (int64_t)S;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = 16 * mt + 4 * g + i;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) out[m * LDW + 16 * kt + c] = accW[mt][kt][i];
+#pragma unroll
+      for (int kb = 0; kb < UB; ++kb) out[G4 * LDW + m * U + 16 * kb + c] = accU[mt][kb][i];
+      if (c == 0) out[G4 * LDW + G4 * U + m] = accb[mt][i];
+    }
+}
+
+template <int U, int KT>
+hipError_t launch_fwd(const FusedFwdArgs& a, hipStream_t st) {
+  const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
+  hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int U, int KT>
+hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
+  const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
+  hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  return hipGetLastError();
+}
+
+template <typename F>
+hipError_t dispatch(int U, int IN, F&& f) {
+  const int KT = (IN + 15) / 16;
+#define SML_UK(u, k) \
+  if (U == u && KT <= k) return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{});
+  SML_UK(16, 1) SML_UK(16, 2) SML_UK(16, 4)
+  SML_UK(32, 1) SML_UK(32, 2)
+#undef SML_UK
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+namespace sml {
+
+bool lstm_fused_supported(int U, int IN) {
+  const int KT = (IN + 15) / 16;
+  // larger (U, IN) would spill the backward kernel's weight-gradient accumulators
+  // (U = 64 layers use the unfused recurrence + K1/K2 path)
+  return IN >= 1 && (U == 16 ? KT <= 4 : (U == 32 ? KT <= 2 : false));
+}
+
+int lstm_fused_slab(int U, int IN) {
+  const int KT = (IN + 15) / 16;
+  const int kt = KT <= 1 ? 1 : (KT <= 2 ? 2 : 4);   // the dispatch bucket
+  return 4 * U * (16 * kt + U + 1);
+}
+
+int lstm_fused_waves(int64_t B) { return (int)(((B + 16 * WAVES - 1) / (16 * WAVES)) * WAVES); }
+
+hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw, const float* b, const float* h0,
+                                 const float* c0, float* hseq, float* cseq, void* gates_bf16, int64_t B, int T,
+                                 int IN, int U, int act, hipStream_t stream) {
+  FusedFwdArgs a{x, W, Uw, b, h0, c0, hseq, cseq, (__bf16*)gates_bf16, B, T, IN, act};
+  return dispatch(U, IN, [&](auto u, auto k) { return launch_fwd<decltype(u)::value, decltype(k)::value>(a, stream); });
+}
+
+hipError_t lstm_fused_bwd_launch(const float* dh, const void* gates_bf16, const float* cseq, const float* hseq,
+                                 const float* x, const float* h0, const float* c0, const float* W, const float* Uw,
+                                 float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
+                                 int act, hipStream_t stream) {
+  FusedBwdArgs a{dh, (const __bf16*)gates_bf16, cseq, hseq, x, h0, c0, W, Uw, dx, dh0, dc0, partials, B, T, IN, act};
+  return dispatch(U, IN, [&](auto u, auto k) { return launch_bwd<decltype(u)::value, decltype(k)::value>(a, stream); });
+}
+
+}  // namespace sml

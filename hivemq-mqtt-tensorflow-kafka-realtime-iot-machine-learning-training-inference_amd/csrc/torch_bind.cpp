@@ -274,6 +274,82 @@ std::vector<at::Tensor> dense_wgrad(const at::Tensor& x, const at::Tensor& dy, i
   return {dW, db};
 }
 
+// Fully fused LSTM layer forward: x [B, T, IN] -> (h [B,T,U], c [B,T,U], gates bf16 [B,T,4U]).
+std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& Uw,
+                                       const at::Tensor& b, const c10::optional<at::Tensor>& h0,
+                                       const c10::optional<at::Tensor>& c0, int64_t act) {
+  check_dev(x, "x", at::kFloat);
+  check_dev(W, "W", at::kFloat);
+  check_dev(Uw, "U", at::kFloat);
+  check_dev(b, "b", at::kFloat);
+  TORCH_CHECK(x.dim() == 3 && x.is_contiguous(), "x must be contiguous [B, T, IN]");
+  const int64_t B = x.size(0), T = x.size(1), IN = x.size(2), U = Uw.size(0);
+  TORCH_CHECK(W.is_contiguous() && W.size(0) == IN && W.size(1) == 4 * U, "W must be [IN, 4U]");
+  TORCH_CHECK(Uw.is_contiguous() && Uw.size(1) == 4 * U, "U must be [U, 4U]");
+  TORCH_CHECK(b.is_contiguous() && b.numel() == 4 * U, "b must be [4U]");
+  TORCH_CHECK(sml::lstm_fused_supported((int)U, (int)IN), "fused LSTM: unsupported U=", U, " IN=", IN);
+  TORCH_CHECK(act == 1 || act == 2, "LSTM activation must be relu or tanh");
+  TORCH_CHECK(B >= 1 && T >= 1, "empty input");
+  if (h0.has_value()) TORCH_CHECK(h0->is_contiguous() && h0->numel() == B * U, "h0 must be [B, U]");
+  if (c0.has_value()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * U, "c0 must be [B, U]");
+  c10::hip::HIPGuard guard(x.device().index());
+  auto h = at::empty({B, T, U}, x.options());
+  auto c = at::empty({B, T, U}, x.options());
+  auto gt = at::empty({B, T, 4 * U}, x.options().dtype(at::kBFloat16));
+  SML_CHECK_HIP(sml::lstm_fused_fwd_launch(x.data_ptr<float>(), W.data_ptr<float>(), Uw.data_ptr<float>(),
+                                           b.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0), h.data_ptr<float>(),
+                                           c.data_ptr<float>(), gt.data_ptr(), B, (int)T, (int)IN, (int)U, (int)act,
+                                           cur_stream(x)));
+  return {h, c, gt};
+}
+
+// Fully fused LSTM layer backward -> [dx (or undefined), dW [IN,4U], dU [U,4U], db [4U], dh0, dc0].
+std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& gates, const at::Tensor& cseq,
+                                       const at::Tensor& hseq, const at::Tensor& x,
+                                       const c10::optional<at::Tensor>& h0, const c10::optional<at::Tensor>& c0,
+                                       const at::Tensor& W, const at::Tensor& Uw, int64_t act, bool want_dx,
+                                       bool want_state_grads) {
+  check_dev(dh, "dh", at::kFloat);
+  check_dev(cseq, "c", at::kFloat);
+  check_dev(hseq, "h", at::kFloat);
+  check_dev(x, "x", at::kFloat);
+  check_dev(W, "W", at::kFloat);
+  check_dev(Uw, "U", at::kFloat);
+  TORCH_CHECK(gates.is_cuda() && gates.scalar_type() == at::kBFloat16 && gates.is_contiguous(), "gates: bf16");
+  const int64_t B = x.size(0), T = x.size(1), IN = x.size(2), U = Uw.size(0);
+  TORCH_CHECK(dh.is_contiguous() && cseq.is_contiguous() && hseq.is_contiguous() && x.is_contiguous(),
+              "inputs must be contiguous");
+  TORCH_CHECK(dh.size(0) == B && dh.size(1) == T && dh.size(2) == U && cseq.sizes() == dh.sizes() &&
+              hseq.sizes() == dh.sizes() && gates.size(2) == 4 * U, "shape mismatch");
+  TORCH_CHECK(sml::lstm_fused_supported((int)U, (int)IN), "fused LSTM: unsupported U=", U, " IN=", IN);
+  c10::hip::HIPGuard guard(x.device().index());
+  auto opts = x.options();
+  at::Tensor dx, dh0, dc0;
+  if (want_dx) dx = at::empty({B, T, IN}, opts);
+  if (want_state_grads) {
+    dh0 = at::empty({B, U}, opts);
+    dc0 = at::empty({B, U}, opts);
+  }
+  const int S = sml::lstm_fused_slab((int)U, (int)IN);
+  const int G = sml::lstm_fused_waves(B);
+  auto partials = at::zeros({G, S}, opts);   // waves past B leave their slab zero
+  auto out = at::empty({S}, opts);
+  auto scratch = at::empty({std::max(1, sml::slab_sum_scratch(G, S))}, opts);
+  auto st = cur_stream(x);
+  SML_CHECK_HIP(sml::lstm_fused_bwd_launch(
+      dh.data_ptr<float>(), gates.data_ptr(), cseq.data_ptr<float>(), hseq.data_ptr<float>(), x.data_ptr<float>(),
+      opt_ptr(h0), opt_ptr(c0), W.data_ptr<float>(), Uw.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
+      want_state_grads ? dh0.data_ptr<float>() : nullptr, want_state_grads ? dc0.data_ptr<float>() : nullptr,
+      partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U, (int)act, st));
+  SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
+                                     out.data_ptr<float>(), st));
+  const int64_t G4 = 4 * U, LDW = (S / G4) - U - 1;
+  auto dW = out.narrow(0, 0, G4 * LDW).view({G4, LDW}).narrow(1, 0, IN).t().contiguous();
+  auto dU = out.narrow(0, G4 * LDW, G4 * U).view({G4, U}).t().contiguous();
+  auto db = out.narrow(0, G4 * LDW + G4 * U, G4);
+  return {dx, dW, dU, db, dh0, dc0};
+}
+
 at::Tensor lane_xor_probe(const at::Tensor& like) {
   TORCH_CHECK(like.is_cuda(), "needs a device tensor for placement");
   c10::hip::HIPGuard guard(like.device().index());
@@ -357,9 +433,18 @@ PYBIND11_MODULE(_C, m) {
   m.def("dense_fwd", &dense_fwd, "K1 tall-skinny dense forward act(X.W + b) on MFMA", py::arg("x"), py::arg("W"),
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("out_bf16") = false, py::arg("max_blocks") = 1024);
   m.def("dense_wgrad", &dense_wgrad, "K2 weight gradient X^T.dY (+ colsum dY) over rows", py::arg("x"),
-        py::arg("dy"), py::arg("shift_T") = 0, py::arg("want_db") = true, py::arg("max_blocks") = 512);
+        py::arg("dy"), py::arg("shift_T") = 0, py::arg("want_db") = true, py::arg("max_blocks") = 1024);
   m.def("dense_supported", &sml::dense_supported, "whether (K, N) fits the register-resident tile", py::arg("K"),
         py::arg("N"));
+  m.def("lstm_fused_fwd", &lstm_fused_fwd, "fully fused LSTM layer forward (x.W + recurrence in one kernel)",
+        py::arg("x"), py::arg("W"), py::arg("U"), py::arg("b"), py::arg("h0") = py::none(),
+        py::arg("c0") = py::none(), py::arg("act") = 1);
+  m.def("lstm_fused_bwd", &lstm_fused_bwd, "fully fused LSTM layer backward (BPTT + dW/dU/db + dX in one kernel)",
+        py::arg("dh"), py::arg("gates"), py::arg("c"), py::arg("h"), py::arg("x"), py::arg("h0") = py::none(),
+        py::arg("c0") = py::none(), py::arg("W"), py::arg("U"), py::arg("act") = 1, py::arg("want_dx") = true,
+        py::arg("want_state_grads") = false);
+  m.def("lstm_fused_supported", &sml::lstm_fused_supported, "whether (U, IN) has a fused LSTM kernel", py::arg("U"),
+        py::arg("IN"));
   m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),
         py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("recon"), py::arg("score"), py::arg("flag"),

@@ -19,6 +19,7 @@ from typing import Iterator, Optional, Tuple
 import numpy as np
 import torch
 
+from ..obs.metrics import ENGINE
 from ..ops._ext import load_c
 from .stream import Chunk, Stream
 
@@ -83,6 +84,8 @@ class DeviceLoader:
                     self.ring.release(prev)   # consumer kernels for `prev` are enqueued by now
                 self.ring.wait(slot)
                 self.rows += n
+                ENGINE.h2d_bytes.inc(n * self.features * 4)
+                ENGINE.ring_occupancy.set(q.qsize())
                 yield self.bufs[slot][:n], c
                 prev = slot
                 i += 1

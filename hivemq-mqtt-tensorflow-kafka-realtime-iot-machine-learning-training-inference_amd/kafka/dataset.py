@@ -21,6 +21,7 @@ from typing import Iterator, List, Optional, Sequence
 
 import numpy as np
 
+from ..obs.metrics import ENGINE
 from .client import KafkaClient, parse_topic_spec
 
 
@@ -69,6 +70,7 @@ class KafkaDataset:
             end = c.latest(topic, partition) if self.eof else None
             cursors.append([topic, partition, start, end])
         last_data = time.monotonic()
+        m_rec, m_bytes, m_dec = ENGINE.ingest_records, ENGINE.ingest_bytes, ENGINE.decode_seconds
         while cursors:
             progressed = False
             for cur in list(cursors):
@@ -76,17 +78,22 @@ class KafkaDataset:
                 if end is not None and pos >= end:
                     cursors.remove(cur)
                     continue
+                t_fetch = time.perf_counter()
                 if self.codec is not None:
                     batch = c.fetch_decode(self.codec, topic, partition, pos, self.max_bytes, self.max_wait_ms,
                                            self.framing)
                     offs = batch["offsets"]
-                    self.bytes_read += int(batch["bytes"])
+                    nbytes = int(batch["bytes"])
+                    self.bytes_read += nbytes
+                    if int(batch.get("n_errors", 0)):
+                        ENGINE.decode_errors.inc(int(batch["n_errors"]), topic=topic)
                     batch["text"] = dict(zip(self.codec.text_fields, batch["text"]))
                     batch["text_null"] = dict(zip(self.codec.text_fields, batch["text_null"]))
                 else:
                     batch = c.fetch(topic, partition, pos, self.max_bytes, self.max_wait_ms)
                     offs = batch["offsets"]
-                    self.bytes_read += len(batch["values"])
+                    nbytes = len(batch["values"])
+                    self.bytes_read += nbytes
                 if len(offs) == 0:
                     continue
                 if end is not None and offs[-1] >= end:  # trim to the eof boundary
@@ -98,6 +105,9 @@ class KafkaDataset:
                         continue
                 cur[2] = int(offs[-1]) + 1
                 self.records_read += len(offs)
+                m_rec.inc(len(offs), topic=topic)
+                m_bytes.inc(nbytes, topic=topic)
+                m_dec.inc(time.perf_counter() - t_fetch, topic=topic)
                 progressed = True
                 batch["topic"], batch["partition"] = topic, partition
                 yield batch

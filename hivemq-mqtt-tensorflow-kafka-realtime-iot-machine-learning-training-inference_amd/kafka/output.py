@@ -14,6 +14,8 @@ from typing import Dict, Optional, Sequence, Union
 from .client import KafkaClient
 
 
+from ..obs.metrics import ENGINE
+
 class KafkaOutputSequence:
     def __init__(self, topic: str, servers: str = "fake://", configuration: Optional[Sequence[str]] = None,
                  partition: int = 0, batch_records: int = 4096, acks: int = 1):
@@ -47,6 +49,7 @@ class KafkaOutputSequence:
         keys = None if all(k is None for k in self._ready_keys) else self._ready_keys
         self._client.produce(self.topic, self.partition, self._ready, keys, None, self.acks)
         self.produced += len(self._ready)
+        ENGINE.produced_records.inc(len(self._ready), topic=self.topic)
         self._ready, self._ready_keys = [], []
 
     def flush(self) -> None:

@@ -27,6 +27,7 @@ from ..ckpt import h5 as ckh5
 from ..data.cardata import normalize_affine
 from ..nn import keras_config as kc
 from ..nn.callbacks import Callback, History
+from ..obs.metrics import ENGINE
 from ..ops.ae import AESpec, FusedAE
 from .reference import TorchAE, init_dense_weights
 
@@ -231,6 +232,11 @@ class Autoencoder:
             dt = time.perf_counter() - t0
             logs["_seconds"] = dt
             logs["_rows"] = m["rows"]
+            ENGINE.train_rows.inc(m["rows"], model=self.name)
+            ENGINE.train_steps.inc(steps, model=self.name)
+            if steps:
+                ENGINE.train_step_latency.observe(dt / steps * 1e6, model=self.name)
+            ENGINE.epoch_loss.set(m["loss"], model=self.name)
             if verbose and rank == 0:
                 shown = " - ".join(f"{k}: {v:.4f}" for k, v in logs.items() if not k.startswith("_"))
                 if verbose == 2:
@@ -287,6 +293,7 @@ class Autoencoder:
             gen = self._forward_batches(x, batch_size)
         for bi, (_, rec, sc) in enumerate(gen):
             outs.append(rec)
+            ENGINE.infer_rows.inc(len(rec), model=self.name)
             for cb in cbs:
                 cb.on_predict_batch_end(bi, {"outputs": rec, "scores": sc})
         for cb in cbs:
@@ -301,7 +308,9 @@ class Autoencoder:
 
     def detect(self, x, threshold: float = 5.0, batch_size: int = 1 << 20) -> np.ndarray:
         """Anomaly flags with the notebook's fixed threshold (``threshold_fixed = 5``)."""
-        return self.score(x, batch_size) > threshold
+        flags = self.score(x, batch_size) > threshold
+        ENGINE.anomaly_events.inc(int(flags.sum()), model=self.name)
+        return flags
 
     def evaluate(self, x, y=None, batch_size: int = 65536, verbose: int = 0) -> Tuple[float, float]:
         """Keras ``evaluate``: (loss, accuracy) without updating weights."""

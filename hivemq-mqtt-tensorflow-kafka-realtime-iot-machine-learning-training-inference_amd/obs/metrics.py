@@ -164,3 +164,32 @@ class Registry:
 
 
 REGISTRY = Registry()
+
+
+# ---------------------------------------------------------------------------
+# the engine's standard metrics, registered once on REGISTRY
+# ---------------------------------------------------------------------------
+class EngineMetrics:
+    """Handles to the engine metrics; hot paths touch these at batch / epoch
+    granularity only (never per event, never with a device sync)."""
+
+    def __init__(self, reg: Registry):
+        self.ingest_records = reg.counter("ingest_records_total", "records fetched from Kafka", ("topic",))
+        self.ingest_bytes = reg.counter("ingest_bytes_total", "record bytes fetched from Kafka", ("topic",))
+        self.decode_seconds = reg.counter("decode_seconds_total", "host time in fetch + Avro decode", ("topic",))
+        self.decode_errors = reg.counter("decode_errors_total", "records that failed Avro decoding", ("topic",))
+        self.h2d_bytes = reg.counter("h2d_bytes_total", "bytes staged host->device through the pinned ring")
+        self.ring_occupancy = reg.gauge("ring_buffer_occupancy", "filled pinned-ring slots awaiting the consumer")
+        self.train_rows = reg.counter("train_rows_total", "rows consumed by optimizer steps", ("model",))
+        self.train_steps = reg.counter("train_steps_total", "optimizer steps", ("model",))
+        self.train_step_latency = reg.summary("train_step_latency_us", "mean step time per epoch (us)", ("model",))
+        self.epoch_loss = reg.gauge("train_epoch_loss", "last epoch loss", ("model",))
+        self.allreduce_bytes = reg.counter("allreduce_bytes_total", "bytes all-reduced across replicas")
+        self.allreduce_calls = reg.counter("allreduce_calls_total", "all-reduce launches")
+        self.infer_rows = reg.counter("infer_rows_total", "rows scored / reconstructed", ("model",))
+        self.infer_latency = reg.summary("infer_event_latency_us", "per-event inference latency (us)")
+        self.anomaly_events = reg.counter("anomaly_events_total", "events flagged anomalous", ("model",))
+        self.produced_records = reg.counter("produced_records_total", "records produced to Kafka", ("topic",))
+
+
+ENGINE = EngineMetrics(REGISTRY)

@@ -1,10 +1,16 @@
-"""LSTM layer = one library GEMM for the input projection + fused HIP recurrence.
+"""LSTM layer on HIP: fully fused layer kernels (default) or projection + recurrence.
 
-Forward:  Zx = X.W + b over all B*T rows (bf16 GEMM, hipBLASLt), then the
+Default path (:class:`FusedLSTMFunction`, ``csrc/kernels/lstm_fused.hip``): one
+kernel for the forward pass (input projection, recurrence, bf16 gate save) and one
+for the backward pass (BPTT, weight gradients accumulated in registers, dX).
+Fallback for shapes without a fused instance (:class:`LSTMFunction`): K1/K2
+projection kernels + the recurrence-only kernels described below.
+
+Fallback forward: Zx = X.W + b over all B*T rows (K1 ``dense_fwd``), then the
 ``lstm_fwd`` kernel runs the recurrence (U.h MFMAs + gates + state update per
-step, h/c in registers).  Backward: the ``lstm_bwd`` kernel walks time backwards
-producing the pre-activation gate gradients dz for every step; dW, dU, db and dX
-are then plain GEMMs / reductions over the B*T rows.
+step, h/c in registers).  Fallback backward: the ``lstm_bwd`` kernel walks time
+backwards producing the pre-activation gate gradients dz for every step; dW, dU,
+db and dX are then K2 ``dense_wgrad`` / K1 passes over the B*T rows.
 
 Keras LSTM semantics (recurrent_activation sigmoid, gate order i,f,c,o,
 ``activation`` for the candidate and the cell output), reference
@@ -97,8 +103,37 @@ class LSTMFunction(torch.autograd.Function):
         return dx, dW, dU, db, None
 
 
-def lstm(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor, activation: str = "relu") -> torch.Tensor:
-    """Device-dispatching LSTM layer: fused HIP path on ROCm, torch reference on CPU."""
+class FusedLSTMFunction(torch.autograd.Function):
+    """Whole layer in two launches: ``lstm_fused_fwd`` (x.W + recurrence, bf16 gates
+    saved) and ``lstm_fused_bwd`` (BPTT + dW/dU/db accumulated in registers + dX)."""
+
+    @staticmethod
+    def forward(ctx, x, W, U, b, act_code: int):
+        h, c, gates = load_c().lstm_fused_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), None, None,
+                                              act_code)
+        ctx.save_for_backward(x, W, U, h, c, gates)
+        ctx.act = act_code
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, W, U, h, c, gates = ctx.saved_tensors
+        dx, dW, dU, db, _, _ = load_c().lstm_fused_bwd(dh.contiguous().float(), gates, c, h, x, None, None,
+                                                       W.contiguous(), U.contiguous(), ctx.act,
+                                                       bool(ctx.needs_input_grad[0]), False)
+        return (dx if ctx.needs_input_grad[0] else None), dW, dU, db, None
+
+
+def fused_supported(units: int, in_features: int) -> bool:
+    return bool(load_c().lstm_fused_supported(int(units), int(in_features)))
+
+
+def lstm(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor, activation: str = "relu",
+         fused: bool = True) -> torch.Tensor:
+    """Device-dispatching LSTM layer: fused HIP kernels on ROCm, torch reference on CPU."""
     if x.is_cuda:
-        return LSTMFunction.apply(x.contiguous().float(), W, U, b, ACT[activation])
+        xc = x.contiguous().float()
+        if fused and fused_supported(U.shape[0], x.shape[-1]):
+            return FusedLSTMFunction.apply(xc, W, U, b, ACT[activation])
+        return LSTMFunction.apply(xc, W, U, b, ACT[activation])
     return lstm_reference(x, W, U, b, activation)

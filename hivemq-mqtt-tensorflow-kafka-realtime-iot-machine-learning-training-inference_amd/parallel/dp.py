@@ -21,6 +21,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from ..obs.metrics import ENGINE
+
 
 @dataclass
 class DistEnv:
@@ -71,6 +73,8 @@ def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
     """In-place SUM all-reduce of one flat bucket (no-op without a process group)."""
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        ENGINE.allreduce_calls.inc()
+        ENGINE.allreduce_bytes.inc(t.numel() * t.element_size())
     return t
 
 

@@ -4,7 +4,7 @@ import pytest
 import torch
 
 from streamml.models.lstm import LSTMPredictor
-from streamml.ops.lstm import LSTMFunction, lstm_reference
+from streamml.ops.lstm import FusedLSTMFunction, LSTMFunction, fused_supported, lstm_reference
 
 pytestmark = pytest.mark.gpu
 
@@ -14,11 +14,14 @@ def _relerr(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-12)
 
 
-@pytest.mark.parametrize("u,act,B,T", [(32, "relu", 100, 7), (16, "tanh", 37, 50), (32, "tanh", 64, 50),
-                                       (64, "relu", 20, 4)])
-def test_lstm_fwd_bwd_vs_reference(cuda_device, u, act, B, T):
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("u,act,B,T,inp", [(32, "relu", 100, 7, 18), (16, "tanh", 37, 50, 18),
+                                           (32, "tanh", 64, 50, 32), (64, "relu", 20, 4, 18),
+                                           (16, "relu", 130, 9, 32), (16, "relu", 16, 3, 64)])
+def test_lstm_fwd_bwd_vs_reference(cuda_device, u, act, B, T, inp, fused):
+    if fused and not fused_supported(u, inp):
+        pytest.skip("no fused instance for this shape")
     rng = np.random.default_rng(u + T)
-    inp = 18
     x = torch.tensor(rng.uniform(-1, 1, (B, T, inp)), dtype=torch.float32)
     W = torch.tensor(rng.standard_normal((inp, 4 * u)) * 0.25, dtype=torch.float32)
     U = torch.tensor(rng.standard_normal((u, 4 * u)) * 0.25, dtype=torch.float32)
@@ -28,7 +31,8 @@ def test_lstm_fwd_bwd_vs_reference(cuda_device, u, act, B, T):
     yr = lstm_reference(*ref_in, activation=act)
     (yr * gy).sum().backward()
     dev_in = [t.to(cuda_device).requires_grad_(True) for t in (x, W, U, b)]
-    yd = LSTMFunction.apply(*dev_in, 1 if act == "relu" else 2)
+    fn = FusedLSTMFunction if fused else LSTMFunction
+    yd = fn.apply(*dev_in, 1 if act == "relu" else 2)
     (yd * gy.to(cuda_device)).sum().backward()
     assert _relerr(yd.detach().cpu(), yr.detach()) < 2e-2
     for d, r in zip(dev_in, ref_in):

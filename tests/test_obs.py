@@ -1,0 +1,108 @@
+"""Observability: engine metrics wiring, Prometheus exposition + HTTP endpoint, rocprof helpers,
+TensorBoard event round trip against the reference's own TF2 event files."""
+import glob
+import os
+import urllib.request
+
+import numpy as np
+import pytest
+
+from streamml.obs import profile as prof
+from streamml.obs.metrics import ENGINE, REGISTRY
+
+REF_LOGS = "/root/reference/python-scripts/autoencoder-anomaly-detection/logs"
+
+
+def test_engine_metrics_wired_through_pipeline():
+    from streamml.data import produce as prod
+    from streamml.data import stream as st
+    from streamml.kafka import KafkaOutputSequence, fake_broker
+    from streamml.models.autoencoder import Autoencoder
+    b0 = ENGINE.ingest_records.value(topic="obs-t")
+    fake_broker("obs").create_topic("obs-t", 1)
+    prod.produce(st.synthetic(3000, chunk=1000), "fake://obs", "obs-t", create=False)
+    rows = st.kafka("fake://obs", ["obs-t:0:0"]).collect()
+    assert len(rows) == 3000
+    assert ENGINE.ingest_records.value(topic="obs-t") - b0 == 3000
+    assert ENGINE.ingest_bytes.value(topic="obs-t") > 3000 * 50
+    ae = Autoencoder(device="cpu", input_normalizer="cardata", name="obs-ae")
+    ae.compile()
+    t0 = ENGINE.train_rows.value(model="obs-ae")
+    ae.fit(rows.x, epochs=1, batch_size=100, verbose=0)
+    assert ENGINE.train_rows.value(model="obs-ae") - t0 == 3000
+    assert ENGINE.train_steps.value(model="obs-ae") >= 30
+    ae.detect(rows.x[:100], threshold=-1.0)
+    assert ENGINE.anomaly_events.value(model="obs-ae") >= 100
+    out = KafkaOutputSequence("obs-out", "fake://obs")
+    for i in range(5):
+        out.setitem(i, f"m{i}")
+    out.flush()
+    assert ENGINE.produced_records.value(topic="obs-out") >= 5
+    text = REGISTRY.exposition()
+    for name in ("ingest_records_total", "train_rows_total", "train_step_latency_us", "anomaly_events_total",
+                 "h2d_bytes_total", "ring_buffer_occupancy"):
+        assert name in text
+
+
+def test_metrics_http_endpoint():
+    srv = REGISTRY.serve(0)
+    try:
+        port = srv.server_address[1]
+        body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=10).read().decode()
+        assert "# TYPE ingest_records_total counter" in body
+    finally:
+        srv.shutdown()
+
+
+def test_rocprof_command_rules(tmp_path):
+    cmd = prof.rocprof_command(["python3", "bench.py", "--steps", "5"], str(tmp_path))
+    assert cmd[:2] == ["rocprofv3", "--kernel-trace"] and "--stats" in cmd
+    i = cmd.index("--")
+    assert cmd[i + 1] == "python3"
+    pmc = prof.rocprof_command(["python3", "bench.py"], str(tmp_path), pmc=prof.PMC_DEFAULT)
+    assert "--pmc" in pmc and "--stats" not in pmc and "--sys-trace" not in pmc
+    with pytest.raises(ValueError):
+        prof.rocprof_command(["env", "A=1", "python3"], str(tmp_path))
+
+
+def test_kernel_stats_markdown(tmp_path):
+    p = tmp_path / "k.csv"
+    p.write_text('"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+                 '"void sml::(anonymous namespace)::wgrad_kernel<2, 8, float, float>(float const*, long)",24,'
+                 '4118044,171585.1,24.18,1,2,3\n'
+                 '"void (anonymous namespace)::lstm_bwd_kernel<32>((anonymous namespace)::LstmBwdArgs<32>)",12,'
+                 '2550705,212558.7,14.98,1,2,3\n')
+    rows = prof.load_kernel_stats(str(p))
+    assert rows[0]["calls"] == 24 and abs(rows[0]["avg_us"] - 171.5851) < 1e-3
+    md = prof.stats_markdown(rows)
+    assert "`wgrad_kernel<2, 8, float, float>`" in md and "`lstm_bwd_kernel<32>`" in md
+
+
+def test_device_timer_cpu_noop():
+    t = prof.DeviceTimer()
+    with t.section("x"):
+        pass
+    assert isinstance(t.summary(), dict)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_LOGS), reason="reference logs not mounted")
+def test_tensorboard_roundtrip_with_reference_tags(tmp_path):
+    from streamml.nn.callbacks import TensorBoard
+    from streamml.obs.tfevents import read_scalars
+    ref = glob.glob(os.path.join(REF_LOGS, "train", "events.out.tfevents.*.v2"))
+    ref_tags = set()
+    for f in ref:
+        ref_tags |= {t for _, _, t, _ in read_scalars(f)}
+    tb = TensorBoard(str(tmp_path))
+    for e in range(3):
+        tb.on_epoch_end(e, {"loss": 1.0 / (e + 1), "accuracy": 0.5 + 0.1 * e, "val_loss": 0.9, "val_accuracy": 0.6})
+    tb.on_train_end()
+    ours = glob.glob(str(tmp_path / "train" / "events.out.tfevents.*"))
+    assert ours
+    got = read_scalars(ours[0])
+    tags = {t for _, _, t, _ in got}
+    assert {"epoch_loss", "epoch_accuracy"} <= tags
+    if ref_tags:
+        assert {"epoch_loss", "epoch_accuracy"} <= ref_tags
+    vals = [v for _, _, t, v in got if t == "epoch_loss"]
+    np.testing.assert_allclose(vals, [1.0, 0.5, 1.0 / 3], rtol=1e-6)

@@ -44,7 +44,7 @@ def main():
     names = demangle([r["name"] for r in rows])
     print(f"{'kernel':70s} {'VGPR':>5s} {'AGPR':>5s} {'spillV':>6s} {'spillS':>6s} {'occ':>4s} {'LDS':>7s}")
     for r, n in zip(rows, names):
-        n = re.sub(r"sml::\(anonymous namespace\)::", "", n)
+        n = n.replace("(anonymous namespace)::", "").replace("sml::", "")
         n = re.sub(r"\(.*\)$", "", n)
         if filt and filt not in n:
             continue
