@@ -12,6 +12,7 @@ Commands (reference script in parentheses):
   mnist        [servers] [--simplified]   (tensorflow-kafka-mnist*.py, confluent-tensorflow-io-kafka*.py)
   produce      <servers> <topic> [--source ...]   (test-data feeders)
   broker       [--port 9092] [--sasl user:pw] [--preload TOPIC=ROWS]
+  train        [--config job.yaml] [--key=value ...] [--ckpt-dir D]   restartable (torchrun) training job
 """
 from __future__ import annotations
 
@@ -23,7 +24,7 @@ from . import common
 def _commands():
     from . import cardata_autoencoder as ae
     from . import cardata_lstm as ls
-    from . import creditcard, mnist, tools
+    from . import creditcard, mnist, tools, train
     return {
         "cardata-v3": ae.main_v3,
         "cardata-v1": ae.main_v1,
@@ -33,6 +34,7 @@ def _commands():
         "mnist": mnist.main,
         "produce": tools.main_produce,
         "broker": tools.main_broker,
+        "train": train.main,
     }
 
 

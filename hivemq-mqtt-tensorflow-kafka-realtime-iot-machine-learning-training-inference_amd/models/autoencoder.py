@@ -156,7 +156,7 @@ class Autoencoder:
     # ------------------------------------------------------------------ training
     def fit(self, x=None, y=None, epochs: int = 1, batch_size: int = 32, verbose: int = 1,
             callbacks: Optional[Sequence[Callback]] = None, validation_data=None, shuffle: bool = True,
-            steps_per_epoch: Optional[int] = None, seed: int = 0) -> History:
+            steps_per_epoch: Optional[int] = None, seed: int = 0, initial_epoch: int = 0) -> History:
         """Train on an array (``y`` must be ``x`` or None: autoencoder) or a Stream.
 
         Under ``torch.distributed`` (RCCL) every rank trains on its own shard:
@@ -189,8 +189,10 @@ class Autoencoder:
                 s0, s1 = shard_range(len(arr), rank, world)
                 arr = arr[s0:s1]
             xd = self._to_device(arr) if self.device.type == "cuda" else self._cpu_x(arr)
-        rng = np.random.default_rng(seed + rank)
-        for epoch in range(epochs):
+        from ..parallel.fault import maybe_inject
+        gstep = int(getattr(self, "_global_step", 0))
+        for epoch in range(initial_epoch, epochs):
+            rng = np.random.default_rng([seed, rank, epoch])   # epoch-keyed: a resumed run reshuffles identically
             t0 = time.perf_counter()
             for cb in cbs:
                 cb.on_epoch_begin(epoch)
@@ -200,8 +202,10 @@ class Autoencoder:
                 for xb in self._stream_batches(x, batch_size):
                     if steps_per_epoch is not None and steps >= steps_per_epoch:
                         break
+                    maybe_inject(gstep, rank)
                     be.step(xb, global_batch=len(xb) * world, allreduce=allreduce)
                     steps += 1
+                    gstep += 1
             else:
                 n = len(xd)
                 order = None
@@ -214,8 +218,11 @@ class Autoencoder:
                 xs = xd[order] if order is not None else xd
                 for b in range(nb):
                     xb = xs[b * batch_size:(b + 1) * batch_size]
+                    maybe_inject(gstep, rank)
                     be.step(xb, global_batch=len(xb) * world, allreduce=allreduce)
                     steps += 1
+                    gstep += 1
+            self._global_step = gstep
             m = be.read_metrics()
             if world > 1:
                 from ..parallel.dp import reduce_metrics

@@ -159,7 +159,8 @@ class LSTMPredictor:
 
     # ------------------------------------------------------------------ training
     def fit(self, x, y=None, epochs: int = 1, batch_size: int = 1, verbose: int = 1, take: Optional[int] = None,
-            callbacks: Optional[Sequence[Callback]] = None, shuffle: bool = False, normalize: bool = True):
+            callbacks: Optional[Sequence[Callback]] = None, shuffle: bool = False, normalize: bool = True,
+            initial_epoch: int = 0, seed: int = 0):
         """``x``: windows [n, T, F] + ``y`` next rows [n, F], or a Stream (windows built here)."""
         from ..data.stream import Stream
         from ..parallel.dp import allreduce_sum_
@@ -178,23 +179,34 @@ class LSTMPredictor:
             ys = np.concatenate([w[1] for w in wins]) if wins else np.zeros((0, self.features))
         else:
             xs, ys = np.asarray(x, np.float32), np.asarray(y, np.float32)
+        if world > 1:   # each replica trains on its contiguous shard (same contract as Autoencoder.fit)
+            from ..parallel.dp import shard_range
+            s0, s1 = shard_range(len(xs), dist.get_rank(), world)
+            xs, ys = xs[s0:s1], ys[s0:s1]
         xd = torch.as_tensor(xs, dtype=torch.float32, device=self.device)
         yd = torch.as_tensor(ys, dtype=torch.float32, device=self.device)
         n = len(xd)
         nb = math.ceil(n / batch_size)
         if take is not None:
             nb = min(nb, take)
-        for epoch in range(epochs):
+        from ..parallel.fault import maybe_inject
+        rank = dist.get_rank() if world > 1 else 0
+        gstep = 0
+        for epoch in range(initial_epoch, epochs):
             t0 = time.perf_counter()
             tot_loss = torch.zeros((), device=self.device)
             tot_corr = torch.zeros((), device=self.device)
             rows = 0
-            order = torch.randperm(n, device=self.device) if shuffle else None
+            order = None
+            if shuffle:   # epoch-keyed permutation: resumable
+                order = torch.as_tensor(np.random.default_rng([seed, rank, epoch]).permutation(n), device=self.device)
             for b in range(nb):
                 sl = slice(b * batch_size, (b + 1) * batch_size)
                 xb = xd[order[sl]] if order is not None else xd[sl]
                 yb = yd[order[sl]] if order is not None else yd[sl]
+                maybe_inject(gstep, rank)
                 loss, corr = self.train_step(xb, yb, global_batch=len(xb) * world, allreduce=allreduce)
+                gstep += 1
                 tot_loss += loss * len(xb)
                 tot_corr += corr
                 rows += len(xb)

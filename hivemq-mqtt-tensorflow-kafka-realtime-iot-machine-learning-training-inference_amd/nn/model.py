@@ -382,7 +382,7 @@ class Model:
 
     def fit(self, x=None, y=None, batch_size: int = 32, epochs: int = 1, verbose: int = 1,
             callbacks: Optional[Sequence[Callback]] = None, validation_data=None, shuffle: bool = True,
-            steps_per_epoch: Optional[int] = None, seed: int = 0) -> History:
+            steps_per_epoch: Optional[int] = None, seed: int = 0, initial_epoch: int = 0) -> History:
         if not self.compiled:
             self.compile()
         if self._fused is not None:
@@ -390,7 +390,7 @@ class Model:
                 raise ValueError("autoencoder fit expects y == x")
             hist = self._fused.fit(x, epochs=epochs, batch_size=batch_size, verbose=verbose, callbacks=callbacks,
                                    validation_data=validation_data, shuffle=shuffle,
-                                   steps_per_epoch=steps_per_epoch, seed=seed)
+                                   steps_per_epoch=steps_per_epoch, seed=seed, initial_epoch=initial_epoch)
             self._sync_from_fused()
             return hist
         import torch.distributed as dist
@@ -403,9 +403,11 @@ class Model:
         for cb in cbs:
             cb.set_model(self)
             cb.on_train_begin()
-        rng = np.random.default_rng(seed + rank)
+        from ..parallel.fault import maybe_inject
+        gstep = int(getattr(self, "_global_step", 0))
         self.stop_training = False
-        for epoch in range(epochs):
+        for epoch in range(initial_epoch, epochs):
+            rng = np.random.default_rng([seed, rank, epoch])   # epoch-keyed shuffles: resumable
             t0 = time.perf_counter()
             for cb in cbs:
                 cb.on_epoch_begin(epoch)
@@ -414,8 +416,11 @@ class Model:
             for xb, yb in self._batches(x, y, batch_size, shuffle, rng, world, rank):
                 if steps_per_epoch is not None and steps >= steps_per_epoch:
                     break
+                maybe_inject(gstep, rank)
                 self.train_on_batch(xb, yb, global_batch=xb.shape[0] * world, allreduce=allreduce)
                 steps += 1
+                gstep += 1
+            self._global_step = gstep
             a = self._acc.double().cpu().numpy()
             m = {"loss": a[0] / max(a[2], 1), "accuracy": a[1] / max(a[2], 1), "rows": a[2]}
             if world > 1:

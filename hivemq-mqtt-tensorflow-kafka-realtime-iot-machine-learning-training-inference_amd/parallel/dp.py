@@ -41,12 +41,14 @@ class DistEnv:
         return self.rank == 0
 
 
-def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600) -> DistEnv:
+def init_from_env(device_type: Optional[str] = None, timeout_s: Optional[int] = None) -> DistEnv:
     """Initialise the process group from torchrun's RANK/WORLD_SIZE/LOCAL_RANK.
 
     Single-process runs (no WORLD_SIZE or WORLD_SIZE=1) do not create a group.
     ``device_type`` defaults to ``cuda`` (ROCm) when available, else ``cpu``.
     """
+    if timeout_s is None:   # collective watchdog: a dead / hung peer raises instead of hanging
+        timeout_s = int(os.environ.get("SML_PG_TIMEOUT_S", "600"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -62,6 +64,13 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: int = 600) -> Di
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+        if restart is not None and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+            # torchrun keeps one store across restarts: key this attempt's rendezvous by the
+            # restart count so a restarted group never reads the dead attempt's addresses
+            base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world, False,
+                                 timeout=datetime.timedelta(seconds=timeout_s))
+            kw["store"] = dist.PrefixStore(f"/sml/attempt_{restart}", base)
         if backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
@@ -82,6 +91,44 @@ def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.broadcast(t, src=src)
     return t
+
+
+def sync_model_from_rank0(model) -> None:
+    """Broadcast rank 0's parameters AND optimizer state to every replica (after init / load)."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return
+    fp = getattr(model, "fp", None)
+    if fp is not None and getattr(model, "_fused", None) is None:
+        for t in (fp.flat, fp.m, fp.v, fp.iter):
+            dist.broadcast(t, src=0)
+        return
+    inner = getattr(model, "_fused", None) or model
+    import numpy as np
+    dev = inner.device
+    ws = inner.get_weights()
+    flat = torch.as_tensor(np.concatenate([w.ravel() for w in ws]), device=dev)
+    dist.broadcast(flat, src=0)
+    out, o = [], 0
+    for w in ws:
+        out.append(flat[o:o + w.size].cpu().numpy().reshape(w.shape))
+        o += w.size
+    inner.set_weights(out)
+    be = getattr(inner, "backend", None)
+    if be is not None and hasattr(be, "get_optimizer_state"):
+        it, m, v = be.get_optimizer_state()
+        st = torch.as_tensor(np.concatenate([np.array([it], np.float64)] + [a.ravel().astype(np.float64) for a in m + v]),
+                             device=dev)
+        dist.broadcast(st, src=0)
+        st = st.cpu().numpy()
+        it2, o = int(st[0]), 1
+        mm, vv = [], []
+        for a in m:
+            mm.append(st[o:o + a.size].reshape(a.shape).astype(np.float32))
+            o += a.size
+        for a in v:
+            vv.append(st[o:o + a.size].reshape(a.shape).astype(np.float32))
+            o += a.size
+        be.set_optimizer_state(it2, mm, vv)
 
 
 def allreduce_max(value: float, device: torch.device) -> float:

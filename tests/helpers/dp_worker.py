@@ -25,10 +25,8 @@ def main(out_dir: str) -> None:
     from streamml.models.lstm import LSTMPredictor
     xs = rng.uniform(-1, 1, size=(64, 4, 18)).astype(np.float32)
     ys = rng.uniform(-1, 1, size=(64, 18)).astype(np.float32)
-    from streamml.parallel.dp import shard_range
-    s0, s1 = shard_range(len(xs), rank, env.world_size)
     m = LSTMPredictor.reference(look_back=4, device="cpu", seed=1)
-    m.fit(xs[s0:s1], ys[s0:s1], epochs=1, batch_size=8, verbose=0)
+    m.fit(xs, ys, epochs=1, batch_size=8, verbose=0)   # fit shards by rank itself
     np.savez(os.path.join(out_dir, f"lstm_{rank}.npz"), *m.fp.get())
     # --- MNIST MLP: local batch 16
     from streamml.data.mnist import synthetic_mnist
