@@ -64,6 +64,17 @@ def main():
             lat.append((t1 - t0) * 1e6)
         t_next += period
     lat = np.asarray(lat)
+    # persistent scorer: resident wave polling a host-mapped ring (no launch / copy per event)
+    from streamml.ops.serve import ScoringServer
+    with ScoringServer(m, threshold=args.threshold, slots=4096) as srv:
+        srv.latency_us(ev[:100], qps=args.qps)                  # warm
+        launches0 = srv.launches
+        plat, pdev = srv.latency_us(ev[100:100 + args.events], qps=args.qps, device_breakdown=True)
+        relaunches = srv.launches - launches0
+        t0 = time.perf_counter()
+        for k in range(20):
+            srv.score(ev[:4096])
+        srv_eps = 20 * 4096 / (time.perf_counter() - t0)
     # batched throughput
     big = synthetic_device_tensor(args.batch * 8, dev, seed=1)
     for _ in range(3):
@@ -81,8 +92,14 @@ def main():
         torch.distributed.all_reduce(t)
         eps_all = float(t.item())
     if env.rank == 0:
-        print(json.dumps({"metric": "p50 per-event inference latency (AE score)", "value": float(np.percentile(lat, 50)),
-                          "unit": "us", "higher_is_better": False, "p99_us": float(np.percentile(lat, 99)),
+        print(json.dumps({"metric": "p50 per-event inference latency (AE score)",
+                          "value": float(np.percentile(plat, 50)), "unit": "us", "higher_is_better": False,
+                          "p99_us": float(np.percentile(plat, 99)), "path": "persistent kernel, host-mapped ring",
+                          "launch_path_p50_us": float(np.percentile(lat, 50)),
+                          "launch_path_p99_us": float(np.percentile(lat, 99)),
+                          "persistent_burst_events_per_s": srv_eps,
+                          "persistent_device_p50_us": float(np.percentile(pdev, 50)),
+                          "persistent_relaunches": relaunches,
                           "offered_qps": args.qps, "events": args.events, "n_gpus": env.world_size,
                           "batched_events_per_s": eps_all, "batch": args.batch, "data": "synthetic"}))
     dp.shutdown()

@@ -55,6 +55,28 @@ hipError_t lstm_fused_bwd_launch(const float* dh, const void* gates_bf16, const 
                                  float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
                                  int act, hipStream_t stream);
 
+// ---- persistent per-event scorer (ae_serve.hip); structures live in host-mapped memory ----
+struct alignas(128) ServeCtl {
+  uint64_t head;            // host: events published (monotonic)
+  uint64_t pad0[15];
+  uint64_t done;            // device: events completed (monotonic)
+  uint64_t pad1[15];
+  uint32_t stop;            // host: ask the kernel to exit
+  uint32_t alive;           // device: 1 while the kernel runs
+  uint32_t pad2[30];
+};
+struct ServeResult {
+  uint64_t seq;             // event sequence number this slot holds
+  float score;              // mean squared reconstruction error
+  uint32_t flag;            // score > threshold
+  uint64_t t_seen;          // device s_memrealtime (100 MHz) when the wave picked the event up
+  uint64_t t_done;          // ... when its result stores were issued
+  float recon[32];
+};
+hipError_t ae_serve_launch(ServeCtl* ctl, const float* req, ServeResult* res, int nslots, const float* wts,
+                           const float* scale, const float* shift, const int* dims, const int* acts, float threshold,
+                           double idle_seconds, hipStream_t stream);
+
 // ---- utilities (util.hip) ----
 hipError_t lane_xor_probe_launch(float* out, hipStream_t stream);
 

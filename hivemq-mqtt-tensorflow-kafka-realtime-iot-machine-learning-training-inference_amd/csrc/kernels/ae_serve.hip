@@ -1,0 +1,160 @@
+// Persistent per-event anomaly scorer (BASELINE config 5).
+//
+// The reference scores events through model.predict on tf.data batches and a
+// Python OutputCallback (cardata-v3.py:235-280); per-event latency is not even
+// measurable there.  The launch-per-event path here (H2D copy + fused forward
+// kernel + D2H copy) costs three runtime round trips per event.  This kernel
+// removes all of them: ONE wave stays resident, polls a host-mapped request
+// ring (fine-grained pinned memory, cache-bypassing system-scope loads), scores the
+// pending events -- one event per lane, so a burst of up to 64 events costs the
+// same as one -- and writes score / anomaly flag / reconstruction straight back
+// into host-mapped memory, then bumps the completion counter once those stores
+// are acknowledged.
+//
+// Weights (Keras order W1 b1 .. W4 b4, <= 31/15/15/15 units) and the input
+// normaliser live in LDS; every lane reads the same weight address, so the LDS
+// reads are broadcasts.
+//
+// Exit conditions every wave reaches: the host's stop flag, or `idle_us` without
+// a request (measured on the 100 MHz s_memrealtime counter) -- a forgotten
+// server never keeps the GPU busy, and the host relaunches on demand.
+#include "sml_common.h"
+#include "sml_ops.h"
+
+namespace sml {
+namespace {
+
+constexpr int MAXD = 32, MAXH = 16;
+
+// Host-mapped traffic uses RELAXED system-scope atomics: they compile to
+// cache-bypassing (sc0 sc1) loads / stores, so polling never invalidates and
+// publishing never writes back the whole L2 (which an acquire / release at
+// system scope would do on every iteration).  Ordering of the result stores
+// before the completion counter is enforced with s_waitcnt vmcnt(0).
+__device__ __forceinline__ uint64_t ld_sys(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t ld_sys32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float ld_sysf(const float* p) {
+  return __uint_as_float(ld_sys32(reinterpret_cast<const uint32_t*>(p)));
+}
+__device__ __forceinline__ void st_sysf(float* p, float v) { st_sys32(reinterpret_cast<uint32_t*>(p), __float_as_uint(v)); }
+__device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <int IN, int OUT>
+__device__ __forceinline__ void dense_lane(const float* __restrict__ W, const float* __restrict__ b, int in_n,
+                                           int out_n, const float* x, float* y, int act) {
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) {
+    float acc = 0.f;
+    if (o < out_n) {
+      acc = b[o];
+#pragma unroll
+      for (int i = 0; i < IN; ++i)
+        if (i < in_n) acc = fmaf(x[i], W[i * out_n + o], acc);
+      acc = act_fwd(act, acc);
+    }
+    y[o] = acc;
+  }
+}
+
+__global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const float* __restrict__ req,
+                                                       ServeResult* res, int nslots, const float* __restrict__ wts,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int D, int n1, int n2,
+                                                       int a1, int a2, int a3, int a4, float threshold,
+                                                       uint64_t idle_ticks) {
+  __shared__ float lw[MAXD * MAXH + MAXH + MAXH * MAXH + MAXH + MAXH * MAXH + MAXH + MAXH * MAXD + MAXD];
+  __shared__ float lsc[MAXD], lsh[MAXD];
+  const int lane = threadIdx.x;
+  const int nw = D * n1 + n1 + n1 * n2 + n2 + n2 * n2 + n2 + n2 * D + D;
+  for (int i = lane; i < nw; i += 64) lw[i] = wts[i];
+  for (int i = lane; i < D; i += 64) {
+    lsc[i] = scale ? scale[i] : 1.f;
+    lsh[i] = shift ? shift[i] : 0.f;
+  }
+  __syncthreads();
+  const float* W1 = lw;
+  const float* b1 = W1 + D * n1;
+  const float* W2 = b1 + n1;
+  const float* b2 = W2 + n1 * n2;
+  const float* W3 = b2 + n2;
+  const float* b3 = W3 + n2 * n2;
+  const float* W4 = b3 + n2;
+  const float* b4 = W4 + n2 * D;
+
+  uint64_t tail = ld_sys(&ctl->done);
+  uint64_t last = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) st_sys32(&ctl->alive, 1u);
+  while (true) {
+    const uint64_t head = ld_sys(&ctl->head);
+    if (head > tail) {
+      const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
+      const uint64_t k = head - tail < 64 ? head - tail : 64;
+      if ((uint64_t)lane < k) {
+        const uint64_t ev = tail + lane;
+        const int slot = (int)(ev % (uint64_t)nslots);
+        const float* xr = req + (int64_t)slot * MAXD;
+        float x[MAXD], h1[MAXH], h2[MAXH], h3[MAXH], y[MAXD];
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i) x[i] = i < D ? fmaf(ld_sysf(xr + i), lsc[i], lsh[i]) : 0.f;
+        dense_lane<MAXD, MAXH>(W1, b1, D, n1, x, h1, a1);
+        dense_lane<MAXH, MAXH>(W2, b2, n1, n2, h1, h2, a2);
+        dense_lane<MAXH, MAXH>(W3, b3, n2, n2, h2, h3, a3);
+        dense_lane<MAXH, MAXD>(W4, b4, n2, D, h3, y, a4);
+        float se = 0.f;
+        ServeResult* r = res + slot;
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i) {
+          if (i < D) {
+            const float d = y[i] - x[i];
+            se = fmaf(d, d, se);
+            st_sysf(&r->recon[i], y[i]);
+          }
+        }
+        const float score = se / (float)D;
+        st_sysf(&r->score, score);
+        st_sys32(&r->flag, score > threshold ? 1u : 0u);
+        st_sys(&r->t_seen, t_seen);
+        st_sys(&r->t_done, __builtin_amdgcn_s_memrealtime());
+        st_sys(&r->seq, ev);
+      }
+      wait_stores();          // every lane's result stores acknowledged ...
+      __syncthreads();
+      tail += k;
+      if (lane == 0) st_sys(&ctl->done, tail);   // ... before the completion counter moves
+      last = __builtin_amdgcn_s_memrealtime();
+    } else {
+      if (ld_sys32(&ctl->stop)) break;
+      if (__builtin_amdgcn_s_memrealtime() - last > idle_ticks) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  wait_stores();
+  if (lane == 0) st_sys32(&ctl->alive, 0u);
+}
+
+}  // namespace
+
+hipError_t ae_serve_launch(ServeCtl* ctl, const float* req, ServeResult* res, int nslots, const float* wts,
+                           const float* scale, const float* shift, const int* dims, const int* acts, float threshold,
+                           double idle_seconds, hipStream_t stream) {
+  if (dims[0] < 1 || dims[0] > MAXD || dims[1] < 1 || dims[1] > MAXH || dims[2] < 1 || dims[2] > MAXH)
+    return hipErrorInvalidValue;
+  if (nslots < 64) return hipErrorInvalidValue;
+  const uint64_t ticks = (uint64_t)(idle_seconds * 100e6);   // s_memrealtime runs at 100 MHz
+  hipLaunchKernelGGL(ae_serve_kernel, dim3(1), dim3(64), 0, stream, ctl, req, res, nslots, wts, scale, shift,
+                     dims[0], dims[1], dims[2], acts[0], acts[1], acts[2], acts[3], threshold, ticks);
+  return hipGetLastError();
+}
+
+}  // namespace sml

@@ -19,7 +19,7 @@
 //       accumulated in registers over the block's rows (the block's waves split
 //       the output tiles), and written as one fp32 slab per block;
 //       slab_sum_kernel reduces the slabs deterministically.
-//       db is one extra MFMA per tile against a "ones" A fragment.
+//       db is summed in exact fp32 from the same loaded values.
 //       ``shift_T`` > 0 reads X[r - 1] (zero when r % T == 0): the h_{t-1}
 //       operand of the LSTM recurrent-weight gradient without materialising it.
 //
@@ -186,16 +186,13 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(const TX* __restrict__ 
   const int nw = w % WN, rw = w / WN;
 
   f32x4 acc[KT][NTW];
-  f32x4 accb[NTW];
+  float accb[NTW];   // db in exact fp32: lane (c, g) sums column c over its rows 4g..4g+3
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
     for (int q = 0; q < NTW; ++q) acc[kt][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int q = 0; q < NTW; ++q) accb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x4 ones;   // A[m = c][k] = (c == 0)  ->  C[m = 0][n] = sum_k B[k][n]
-#pragma unroll
-  for (int j = 0; j < 4; ++j) ones[j] = (c == 0) ? (short)0x3F80 : (short)0;
+  for (int q = 0; q < NTW; ++q) accb[q] = 0.f;
 
   const int64_t ntiles = (M + 15) / 16;
   const int64_t first = (int64_t)blockIdx.x * WR + rw;
@@ -230,19 +227,27 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(const TX* __restrict__ 
   if (first < ntiles) fetch(first, nx, ny);
   for (int64_t tile = first; tile < ntiles; tile += stride) {
     bf16x4 af[KT], bf[NTW];
+    f32x4 cy[NTW];
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) af[kt] = pack4(nx[kt]);
 #pragma unroll
-    for (int q = 0; q < NTW; ++q) bf[q] = pack4(ny[q]);
-    if (tile + stride < ntiles) fetch(tile + stride, nx, ny);   // in flight during the MFMAs
-    if (want_db) {
-#pragma unroll
-      for (int q = 0; q < NTW; ++q) accb[q] = mfma16(ones, bf[q], accb[q]);
+    for (int q = 0; q < NTW; ++q) {
+      cy[q] = ny[q];
+      bf[q] = pack4(ny[q]);
     }
+    if (tile + stride < ntiles) fetch(tile + stride, nx, ny);   // in flight during the MFMAs
+#pragma unroll
+    for (int q = 0; q < NTW; ++q) accb[q] += (cy[q][0] + cy[q][1]) + (cy[q][2] + cy[q][3]);
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
       for (int q = 0; q < NTW; ++q) acc[kt][q] = mfma16(af[kt], bf[q], acc[kt][q]);
+  }
+  // fold the four row groups g of each column: lanes c, c+16, c+32, c+48
+#pragma unroll
+  for (int q = 0; q < NTW; ++q) {
+    accb[q] += xor16(accb[q], lane);
+    accb[q] += xor32(accb[q], lane);
   }
 
   float* out = partials + (int64_t)blockIdx.x * S;
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(const TX* __restrict__ 
         for (int i = 0; i < 4; ++i) out[(16 * kt + 4 * g + i) * LDN + 16 * (nw * NTW + q) + c] = acc[kt][q][i];
     if (g == 0) {
 #pragma unroll
-      for (int q = 0; q < NTW; ++q) out[16 * KT * LDN + 16 * (nw * NTW + q) + c] = want_db ? accb[q][0] : 0.0f;
+      for (int q = 0; q < NTW; ++q) out[16 * KT * LDN + 16 * (nw * NTW + q) + c] = want_db ? accb[q] : 0.0f;
     }
   } else {
     // WR row phases share fragments: add them in fixed wave order through LDS
@@ -276,7 +281,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(const TX* __restrict__ 
 #pragma unroll
           for (int q = 0; q < NTW; ++q) {
             float& d = slab[16 * KT * LDN + 16 * (nw * NTW + q) + c];
-            d = (p == 0 ? 0.0f : d) + (want_db ? accb[q][0] : 0.0f);
+            d = (p == 0 ? 0.0f : d) + (want_db ? accb[q] : 0.0f);
           }
         }
       }

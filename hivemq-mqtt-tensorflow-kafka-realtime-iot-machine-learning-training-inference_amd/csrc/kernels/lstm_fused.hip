@@ -17,7 +17,7 @@
 //     dz_t from (dh_t + U.dz_{t+1}) and the stored gates / cell state
 //     dh_{t-1}^T = U . dz_t^T                (critical path, MFMA)
 //     dX_t^T     = W . dz_t^T                (MFMA, optional)
-//     dW^T += dz_t^T . x_t,  dU^T += dz_t^T . h_{t-1},  db += colsum(dz_t)
+//     dW^T += dz_t^T . x_t,  dU^T += dz_t^T . h_{t-1},  db += colsum(dz_t) (fp32)
 //       -> register accumulators (AGPRs) over the wave's 16 sequences x T
 //          steps; the contraction over sequences needs dz_t^T as an A operand,
 //          obtained with one LDS transpose per gate tile (ds_read_b64_tr_b16).
@@ -227,12 +227,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       for (int j = 0; j < 4; ++j) t4[j] = (want_dx && f < IN) ? a.W[(int64_t)f * G4 + 16 * mt + 4 * g + j] : 0.f;
       wf[kt][mt] = pack4(t4);
     }
-  bf16x4 onesb;   // B[k][n] = (n == 0): C[m][0] = sum_k A[m][k]
-#pragma unroll
-  for (int j = 0; j < 4; ++j) onesb[j] = (c == 0) ? (short)0x3F80 : (short)0;
 
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  f32x4 accW[MT][KT], accU[MT][UB], accb[MT];
+  f32x4 accW[MT][KT], accU[MT][UB];
+  f32x4 accb[MT];   // db in exact fp32: per lane (sequence c) over time, folded across lanes at the end
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -323,7 +321,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     }
     bf16x4 dzb[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) dzb[mt] = pack4(dzt[mt]);
+    for (int mt = 0; mt < MT; ++mt) {
+      dzb[mt] = pack4(dzt[mt]);
+      accb[mt] += dzt[mt];
+    }
     // critical path: recurrent gradient for step t-1
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
@@ -362,7 +363,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       for (int kt = 0; kt < KT; ++kt) accW[mt][kt] = mfma16(adz, xB[kt], accW[mt][kt]);
 #pragma unroll
       for (int kb = 0; kb < UB; ++kb) accU[mt][kb] = mfma16(adz, hB[kb], accU[mt][kb]);
-      accb[mt] = mfma16(adz, onesb, accb[mt]);
+
     }
   }
   if (valid) {
@@ -373,6 +374,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       if (a.dc0) *reinterpret_cast<f32x4*>(a.dc0 + sq * U + off) = dcn[b];
     }
   }
+  // db: sum the 16 sequence lanes c of each row group (butterfly within 16 lanes)
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = accb[mt][i];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+      accb[mt][i] = v;
+    }
   // this wave's slab (C layout: row m = gate 16mt + 4g + i, column = lane c)
   float* out = a.partials + wave_id * (int64_t)S;
 #pragma unroll

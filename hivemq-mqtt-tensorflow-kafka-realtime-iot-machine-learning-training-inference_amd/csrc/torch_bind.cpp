@@ -10,6 +10,7 @@
 
 #include "sml_ops.h"
 #include "../runtime/ring.h"
+#include "../runtime/serve.h"
 
 #include <pybind11/numpy.h>
 #include <cstring>
@@ -397,6 +398,62 @@ struct RingPy {
   }
 };
 
+// Python face of the persistent scorer: numpy in / numpy out, GIL released while
+// the host thread spins on the completion counter.
+struct ServePy {
+  std::unique_ptr<sml::AEServe> s;
+  ServePy(int device, int nslots, py::array_t<float, py::array::c_style | py::array::forcecast> weights,
+          std::vector<int> dims, std::vector<int> acts, py::object scale, py::object shift, double threshold,
+          double idle_seconds) {
+    if (dims.size() != 3 || acts.size() != 4) throw std::invalid_argument("dims = [D, n1, n2], acts = 4 codes");
+    std::vector<float> w(weights.data(), weights.data() + weights.size());
+    std::vector<float> sc, sh;
+    if (!scale.is_none()) {
+      auto a = scale.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+      auto b = shift.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+      sc.assign(a.data(), a.data() + a.size());
+      sh.assign(b.data(), b.data() + b.size());
+    }
+    c10::hip::HIPGuard guard(device);
+    s = std::make_unique<sml::AEServe>(device, nslots, w, dims.data(), acts.data(), sc, sh, (float)threshold,
+                                       idle_seconds);
+  }
+  py::tuple infer(py::array_t<float, py::array::c_style | py::array::forcecast> rows, bool want_recon,
+                  double timeout_s) {
+    if (rows.ndim() != 2 || rows.shape(1) != s->D()) throw std::invalid_argument("rows must be [k, D]");
+    const int k = (int)rows.shape(0);
+    py::array_t<float> scores(k);
+    py::array_t<uint32_t> flags(k);
+    py::array_t<float> recon(want_recon ? std::vector<ssize_t>{k, s->D()} : std::vector<ssize_t>{0});
+    const float* src = rows.data();
+    float* ps = scores.mutable_data();
+    uint32_t* pf = flags.mutable_data();
+    float* pr = want_recon ? recon.mutable_data() : nullptr;
+    {
+      py::gil_scoped_release rel;
+      s->infer(src, k, ps, pf, pr, timeout_s);
+    }
+    return py::make_tuple(scores, flags, recon);
+  }
+  // -> int64 [n, 2]: host round-trip ns, device processing ns
+  py::array_t<int64_t> latency_run(py::array_t<float, py::array::c_style | py::array::forcecast> rows,
+                                   int64_t gap_ns) {
+    if (rows.ndim() != 2 || rows.shape(1) != s->D()) throw std::invalid_argument("rows must be [n, D]");
+    std::vector<int64_t> lat, dev;
+    {
+      py::gil_scoped_release rel;
+      lat = s->latency_run(rows.data(), (int)rows.shape(0), gap_ns, &dev);
+    }
+    py::array_t<int64_t> out(std::vector<ssize_t>{(ssize_t)lat.size(), 2});
+    int64_t* o = out.mutable_data();
+    for (size_t i = 0; i < lat.size(); ++i) {
+      o[2 * i] = lat[i];
+      o[2 * i + 1] = dev[i];
+    }
+    return out;
+  }
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -445,6 +502,16 @@ PYBIND11_MODULE(_C, m) {
         py::arg("want_state_grads") = false);
   m.def("lstm_fused_supported", &sml::lstm_fused_supported, "whether (U, IN) has a fused LSTM kernel", py::arg("U"),
         py::arg("IN"));
+  py::class_<ServePy>(m, "AEServe", "persistent per-event autoencoder scorer over host-mapped rings")
+      .def(py::init<int, int, py::array_t<float, py::array::c_style | py::array::forcecast>, std::vector<int>,
+                    std::vector<int>, py::object, py::object, double, double>(),
+           py::arg("device"), py::arg("nslots"), py::arg("weights"), py::arg("dims"), py::arg("acts"),
+           py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("threshold") = 5.0,
+           py::arg("idle_seconds") = 2.0)
+      .def("infer", &ServePy::infer, py::arg("rows"), py::arg("want_recon") = false, py::arg("timeout_s") = 10.0)
+      .def("latency_run", &ServePy::latency_run, py::arg("rows"), py::arg("gap_ns") = 0)
+      .def("stop", [](ServePy& p) { p.s->stop(); })
+      .def_property_readonly("launches", [](ServePy& p) { return p.s->launches(); });
   m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),
         py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("recon"), py::arg("score"), py::arg("flag"),
