@@ -13,6 +13,7 @@ Commands (reference script in parentheses):
   produce      <servers> <topic> [--source ...]   (test-data feeders)
   broker       [--port 9092] [--sasl user:pw] [--preload TOPIC=ROWS]
   train        [--config job.yaml] [--key=value ...] [--ckpt-dir D]   restartable (torchrun) training job
+  ksql         <servers> <source_topic> <target_topic> [--window 300]   per-car tumbling event counts
 """
 from __future__ import annotations
 
@@ -35,6 +36,7 @@ def _commands():
         "produce": tools.main_produce,
         "broker": tools.main_broker,
         "train": train.main,
+        "ksql": tools.main_ksql,
     }
 
 

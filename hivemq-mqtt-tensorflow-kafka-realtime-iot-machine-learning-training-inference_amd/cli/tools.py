@@ -97,5 +97,24 @@ def main_produce(argv: Sequence[str]) -> int:
     return 0
 
 
+
+def main_ksql(argv: Sequence[str]) -> int:
+    """``ksql <servers> <source_topic> <target_topic> [--window 300]``: the reference's
+    SENSOR_DATA_EVENTS_PER_5MIN_T table (01_installConfluentPlatform.sh:256) as a job."""
+    common.print_options(argv)
+    usage = "Usage: ksql <servers> <source_topic> <target_topic> [--window SECONDS]"
+
+    def flags(p):
+        p.add_argument("--window", type=int, default=300)
+        p.add_argument("--grace", type=int, default=None)
+
+    ns = common.parse(argv, usage, ["servers", "source", "target"], add_flags=flags)
+    from ..data.ksql import run_events_per_window
+    cfg = common.kafka_config(ns.servers, ns.kafka_config)
+    n = run_events_per_window(ns.servers, ns.source, ns.target, ns.window, config=cfg, grace_s=ns.grace)
+    print(f"{n} window counts produced into '{ns.target}'", flush=True)
+    return 0
+
+
 if __name__ == "__main__":
     sys.exit(common.run(main_produce))

@@ -56,17 +56,24 @@ def produce(stream: Stream, servers: str, topic: str, schema="cardata-v1", parti
     for c in stream:
         buf, offs = encode_chunk(codec, c.x, c.label, framing, schema_id)
         vals = [buf[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
-        if c.keys is not None and nparts > 1:
-            keys = [k.encode() if isinstance(k, str) else k for k in c.keys]
+        keys = c.keys
+        if keys is None and "device" in c.meta:   # the simulator's MQTT client id is the record key
+            keys = [f"electric-vehicle-{int(d):05d}" for d in c.meta["device"]]
+        keys = None if keys is None else [k.encode() if isinstance(k, str) else k for k in keys]
+        ts = c.meta.get("timestamp")
+        # Kafka timestamps are epoch milliseconds; the car events carry epoch seconds
+        ts = None if ts is None else (np.asarray(ts, dtype=np.int64) * (1000 if np.max(ts) < 1e11 else 1))
+        if keys is not None and nparts > 1:
             parts = np.array([zlib.crc32(k) % nparts for k in keys])
             for p in range(nparts):
                 idx = np.nonzero(parts == p)[0]
                 if len(idx):
-                    client.produce(topic, p, [vals[i] for i in idx], [keys[i] for i in idx])
+                    client.produce(topic, p, [vals[i] for i in idx], [keys[i] for i in idx],
+                                   None if ts is None else ts[idx])
         else:
-            keys = None if c.keys is None else [k.encode() if isinstance(k, str) else k for k in c.keys]
             step = 8192
             for s in range(0, len(vals), step):
-                client.produce(topic, partition, vals[s:s + step], None if keys is None else keys[s:s + step])
+                client.produce(topic, partition, vals[s:s + step], None if keys is None else keys[s:s + step],
+                               None if ts is None else ts[s:s + step])
         total += len(vals)
     return total
