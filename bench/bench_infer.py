@@ -69,7 +69,7 @@ def main():
     with ScoringServer(m, threshold=args.threshold, slots=4096) as srv:
         srv.latency_us(ev[:100], qps=args.qps)                  # warm
         launches0 = srv.launches
-        plat, pdev = srv.latency_us(ev[100:100 + args.events], qps=args.qps, device_breakdown=True)
+        plat, pdev, pload, pcomp = srv.latency_us(ev[100:100 + args.events], qps=args.qps, device_breakdown=True)
         relaunches = srv.launches - launches0
         t0 = time.perf_counter()
         for k in range(20):
@@ -99,6 +99,8 @@ def main():
                           "launch_path_p99_us": float(np.percentile(lat, 99)),
                           "persistent_burst_events_per_s": srv_eps,
                           "persistent_device_p50_us": float(np.percentile(pdev, 50)),
+                          "persistent_device_load_p50_us": float(np.percentile(pload, 50)),
+                          "persistent_device_compute_p50_us": float(np.percentile(pcomp, 50)),
                           "persistent_relaunches": relaunches,
                           "offered_qps": args.qps, "events": args.events, "n_gpus": env.world_size,
                           "batched_events_per_s": eps_all, "batch": args.batch, "data": "synthetic"}))

@@ -71,6 +71,8 @@ struct ServeResult {
   uint32_t flag;            // score > threshold
   uint64_t t_seen;          // device s_memrealtime (100 MHz) when the wave picked the event up
   uint64_t t_done;          // ... when its result stores were issued
+  uint64_t t_loaded;        // ... when the request row had arrived
+  uint64_t t_comp;          // ... when the forward pass finished
   float recon[32];
 };
 hipError_t ae_serve_launch(ServeCtl* ctl, const float* req, ServeResult* res, int nslots, const float* wts,

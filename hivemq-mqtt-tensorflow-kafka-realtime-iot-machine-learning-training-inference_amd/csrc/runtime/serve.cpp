@@ -5,6 +5,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <algorithm>
 
 namespace sml {
 namespace {
@@ -142,7 +143,11 @@ std::vector<int64_t> AEServe::latency_run(const float* rows, int n, int64_t gap_
     lat[i] = std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
     if (dev_ns) {
       const ServeResult& r = result(s);
-      (*dev_ns)[i] = (int64_t)(r.t_done - r.t_seen) * 10;   // 100 MHz ticks -> ns
+      // 100 MHz ticks -> ns, packed: [total | load | compute] in three 21-bit fields (ns / 10)
+      const int64_t tot = (int64_t)(r.t_done - r.t_seen), ld = (int64_t)(r.t_loaded - r.t_seen),
+                    cp = (int64_t)(r.t_comp - r.t_loaded);
+      (*dev_ns)[i] = (std::min<int64_t>(tot, 0x1fffff) << 42) | (std::min<int64_t>(ld, 0x1fffff) << 21) |
+                     std::min<int64_t>(cp, 0x1fffff);
     }
     next = t0 + std::chrono::nanoseconds(gap_ns);
   }

@@ -444,11 +444,14 @@ struct ServePy {
       py::gil_scoped_release rel;
       lat = s->latency_run(rows.data(), (int)rows.shape(0), gap_ns, &dev);
     }
-    py::array_t<int64_t> out(std::vector<ssize_t>{(ssize_t)lat.size(), 2});
+    // columns: host round trip, device total, device load, device compute (ns)
+    py::array_t<int64_t> out(std::vector<ssize_t>{(ssize_t)lat.size(), 4});
     int64_t* o = out.mutable_data();
     for (size_t i = 0; i < lat.size(); ++i) {
-      o[2 * i] = lat[i];
-      o[2 * i + 1] = dev[i];
+      o[4 * i] = lat[i];
+      o[4 * i + 1] = ((dev[i] >> 42) & 0x1fffff) * 10;
+      o[4 * i + 2] = ((dev[i] >> 21) & 0x1fffff) * 10;
+      o[4 * i + 3] = (dev[i] & 0x1fffff) * 10;
     }
     return out;
   }

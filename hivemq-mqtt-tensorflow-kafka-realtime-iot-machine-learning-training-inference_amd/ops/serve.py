@@ -50,7 +50,9 @@ class ScoringServer:
         with ``device_breakdown`` also the on-device processing time of each event (us)."""
         gap = int(1e9 / qps) if qps > 0 else 0
         out = self._s.latency_run(np.ascontiguousarray(np.asarray(rows, np.float32)), gap) / 1e3
-        return (out[:, 0], out[:, 1]) if device_breakdown else out[:, 0]
+        if device_breakdown:   # (host round trip, device total, device row-load, device compute)
+            return out[:, 0], out[:, 1], out[:, 2], out[:, 3]
+        return out[:, 0]
 
     @property
     def launches(self) -> int:
