@@ -79,6 +79,11 @@ hipError_t ae_serve_launch(ServeCtl* ctl, const float* req, ServeResult* res, in
                            const float* scale, const float* shift, const int* dims, const int* acts, float threshold,
                            double idle_seconds, hipStream_t stream);
 
+// ---- fused MSE + categorical accuracy (loss.hip) ----
+bool mse_acc_supported(int F);
+hipError_t mse_acc_launch(const float* yp, const float* y, int64_t rows, int F, int bcast, float gscale, float* grad,
+                          float* acc, hipStream_t stream);
+
 // ---- utilities (util.hip) ----
 hipError_t lane_xor_probe_launch(float* out, hipStream_t stream);
 

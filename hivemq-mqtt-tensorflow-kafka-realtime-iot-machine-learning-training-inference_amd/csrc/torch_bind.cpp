@@ -351,6 +351,29 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& g
   return {dx, dW, dU, db, dh0, dc0};
 }
 
+// K3 + K6: (y_pred - y) * gscale -> grad, [sum sq err, #correct rows] += into acc.
+void mse_acc(const at::Tensor& yp, const at::Tensor& y, int64_t bcast, double gscale,
+             const c10::optional<at::Tensor>& grad, const c10::optional<at::Tensor>& acc) {
+  check_dev(yp, "y_pred", at::kFloat);
+  check_dev(y, "y", at::kFloat);
+  TORCH_CHECK(yp.is_contiguous() && y.is_contiguous(), "inputs must be contiguous");
+  const int64_t F = yp.size(-1);
+  const int64_t rows = yp.numel() / F;
+  TORCH_CHECK(y.size(-1) == F && bcast >= 1 && y.numel() / F * bcast == rows, "target rows * bcast != prediction rows");
+  TORCH_CHECK(sml::mse_acc_supported((int)F), "mse_acc: unsupported feature count ", F);
+  if (grad.has_value()) {
+    check_dev(*grad, "grad", at::kFloat);
+    TORCH_CHECK(grad->is_contiguous() && grad->numel() == yp.numel(), "grad must match y_pred");
+  }
+  if (acc.has_value()) {
+    check_dev(*acc, "acc", at::kFloat);
+    TORCH_CHECK(acc->numel() >= 2, "acc needs 2 floats");
+  }
+  c10::hip::HIPGuard guard(yp.device().index());
+  SML_CHECK_HIP(sml::mse_acc_launch(yp.data_ptr<float>(), y.data_ptr<float>(), rows, (int)F, (int)bcast,
+                                    (float)gscale, opt_mut(grad), opt_mut(acc), cur_stream(yp)));
+}
+
 at::Tensor lane_xor_probe(const at::Tensor& like) {
   TORCH_CHECK(like.is_cuda(), "needs a device tensor for placement");
   c10::hip::HIPGuard guard(like.device().index());
@@ -515,6 +538,9 @@ PYBIND11_MODULE(_C, m) {
       .def("latency_run", &ServePy::latency_run, py::arg("rows"), py::arg("gap_ns") = 0)
       .def("stop", [](ServePy& p) { p.s->stop(); })
       .def_property_readonly("launches", [](ServePy& p) { return p.s->launches(); });
+  m.def("mse_acc", &mse_acc, "fused MSE fwd/bwd + categorical accuracy (K3 + K6)", py::arg("y_pred"), py::arg("y"),
+        py::arg("bcast") = 1, py::arg("gscale") = 1.0, py::arg("grad") = py::none(), py::arg("acc") = py::none());
+  m.def("mse_acc_supported", &sml::mse_acc_supported, "feature counts with a fused MSE kernel", py::arg("F"));
   m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),
         py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("recon"), py::arg("score"), py::arg("flag"),

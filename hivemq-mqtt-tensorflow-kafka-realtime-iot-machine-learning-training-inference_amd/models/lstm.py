@@ -33,6 +33,7 @@ from ..nn import keras_config as kc
 from ..nn.callbacks import Callback, History
 from ..ops.adam import FlatAdam, FlatParams
 from ..ops.dense import dense as dense_op
+from ..ops.loss import mse_accuracy
 from ..ops.lstm import lstm as lstm_op
 
 # layer spec: ("lstm", units, return_sequences, activation) | ("repeat", n) | ("dense", units, time_distributed)
@@ -140,12 +141,9 @@ class LSTMPredictor:
         return h
 
     def _loss(self, y_pred: torch.Tensor, y: torch.Tensor):
-        if y_pred.dim() == 3 and y.dim() == 2:
-            y = y.unsqueeze(1)          # (n, 1, F) target broadcasts over the output steps (Keras MSE)
-        yb = torch.broadcast_to(y, y_pred.shape)
-        loss = ((y_pred - yb) ** 2).mean()
-        correct = (torch.argmax(y_pred, -1) == torch.argmax(yb, -1)).float()
-        return loss, correct.mean(dim=tuple(range(1, correct.dim()))).sum() if correct.dim() > 1 else correct.sum()
+        """Keras MSE (an (n, F) target broadcasts over (n, T, F) output steps) + accuracy count:
+        one fused HIP kernel on ROCm (K3 + K6), torch ops on CPU."""
+        return mse_accuracy(y_pred, y)
 
     def train_step(self, x: torch.Tensor, y: torch.Tensor, global_batch: Optional[int] = None, allreduce=None):
         n = x.shape[0]

@@ -295,6 +295,9 @@ class Model:
                 yl = y.reshape(-1).long()
                 loss = -torch.log(yp.clamp(1e-7, 1 - 1e-7)).gather(-1, yl[:, None]).mean()
                 correct = (yp.argmax(-1) == yl).sum()
+            elif self.loss == "mean_squared_error":
+                from ..ops.loss import mse_accuracy          # fused K3 + K6 on ROCm
+                loss, correct = mse_accuracy(yp, y.to(yp.dtype))
             else:
                 yt = torch.broadcast_to(yt, yp.shape)
                 if self.loss == "mean_squared_error":
