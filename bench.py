@@ -38,11 +38,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--batch-per-gpu", type=int, default=1 << 22)
+    p.add_argument("--batch-per-gpu", type=int, default=1 << 23)
     p.add_argument("--dataset-rows", type=int, default=1 << 25, help="rows resident per GPU (ring)")
-    p.add_argument("--max-blocks", type=int, default=1024)
+    p.add_argument("--max-blocks", type=int, default=0, help="0 = resident capacity (3 blocks per CU)")
     p.add_argument("--infer-events", type=int, default=1000)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--dump-params", default=None,
+                   help="write this rank's final parameter image to <path>.rank<R>.npy (replica checks)")
     p.add_argument("--graph", action="store_true",
                    help="replay one captured hipGraph step (replay floor ~10 us; eager is faster at these sizes)")
     return p.parse_args()
@@ -158,6 +160,8 @@ def main():
     elapsed = dp.allreduce_max(t1 - t0, device)
 
     metrics = fused.read_metrics()
+    if args.dump_params:
+        np.save(f"{args.dump_params}.rank{rank}.npy", fused.params.detach().cpu().numpy())
     p50 = p99 = None
     infer_path = None
     if rank == 0 and args.infer_events > 0:

@@ -26,6 +26,8 @@
 //   L3 [16][16] @768  (bias = row 15)     requires n2 <= 15, n3 <= 15
 //   L4 [16][32] @1024 (bias = row 15)     requires n3 <= 15
 // Slab = 1536 gradient sums + 4 metric sums {sum sq err, sum |h1|, correct, rows}.
+#include <cstdlib>
+
 #include "sml_common.h"
 
 using namespace sml;
@@ -36,6 +38,11 @@ constexpr int WAVES = 4;  // waves per workgroup
 constexpr int OFF1 = 0, OFF2 = 512, OFF3 = 768, OFF4 = 1024;
 constexpr int NPARAM = 1536;
 constexpr int NSLOT = 1540;
+// LDS-DMA input ring (PF > 0 variants): per wave RING_BYTES after the slab area.
+// A 16-row tile of contiguous rows is 64*D bytes (D = 18: 1152 B), moved by two
+// global_load_lds_dwordx4 (64 lanes x 16 B + (4D - 64) lanes x 16 B).
+constexpr int SLAB_BYTES = WAVES * NSLOT * 4;  // 24640, a multiple of 16
+constexpr int RING_BYTES = 6144;
 
 struct AEArgs {
   const float* x;        // [n, ld] raw or normalised rows
@@ -84,6 +91,14 @@ constexpr bool zero_preserving() {
   return true;
 }
 
+// Branch-free guarded parameter load: the address is clamped to a valid element and
+// the value selected afterwards (a `cond ? P[i] : 0` makes hipcc branch around every
+// load and wait vmcnt(0) for each one -- ~50 serial L2 round trips per wave).
+__device__ __forceinline__ float ldsel(const float* P, bool cond, int idx) {
+  const float v = P[cond ? idx : 0];
+  return cond ? v : 0.f;
+}
+
 // FOLD: biases enter the forward MFMAs through the constant-1 input slot
 // (row 31 of L1, row 15 of L2..L4) instead of an fp32 accumulator init.
 template <bool FOLD>
@@ -97,39 +112,44 @@ __device__ __forceinline__ void load_frags(const AEArgs& a, int c, int g, Frags&
     for (int s = 0; s < 2; ++s) {
       const int in = 16 * s + k;
       const bool row_ok = in < a.D || (FOLD && in == 31);
-      F.w1t[s][j] = bfbits((row_ok && c < a.n1) ? P[OFF1 + in * 16 + c] : 0.f);
+      F.w1t[s][j] = bfbits(ldsel(P, row_ok && c < a.n1, OFF1 + in * 16 + c));
     }
     const bool k15 = FOLD && k == 15;
-    F.w2t[j] = bfbits(((k < a.n1 || k15) && c < a.n2) ? P[OFF2 + k * 16 + c] : 0.f);
-    F.w3t[j] = bfbits(((k < a.n2 || k15) && c < a.n3) ? P[OFF3 + k * 16 + c] : 0.f);
+    F.w2t[j] = bfbits(ldsel(P, (k < a.n1 || k15) && c < a.n2, OFF2 + k * 16 + c));
+    F.w3t[j] = bfbits(ldsel(P, (k < a.n2 || k15) && c < a.n3, OFF3 + k * 16 + c));
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int out = 16 * t + c;
-      F.w4t[t][j] = bfbits(((k < a.n3 || k15) && out < a.D) ? P[OFF4 + k * 32 + out] : 0.f);
+      F.w4t[t][j] = bfbits(ldsel(P, (k < a.n3 || k15) && out < a.D, OFF4 + k * 32 + out));
     }
     if (bwd) {
       // backward: A[m = in = c][k = out]; bias rows never propagate gradients
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int out = 16 * s + k;
-        F.w4[s][j] = bfbits((c < a.n3 && out < a.D) ? P[OFF4 + c * 32 + out] : 0.f);
+        F.w4[s][j] = bfbits(ldsel(P, c < a.n3 && out < a.D, OFF4 + c * 32 + out));
       }
-      F.w3[j] = bfbits((c < a.n2 && k < a.n3) ? P[OFF3 + c * 16 + k] : 0.f);
-      F.w2[j] = bfbits((c < a.n1 && k < a.n2) ? P[OFF2 + c * 16 + k] : 0.f);
+      F.w3[j] = bfbits(ldsel(P, c < a.n2 && k < a.n3, OFF3 + c * 16 + k));
+      F.w2[j] = bfbits(ldsel(P, c < a.n1 && k < a.n2, OFF2 + c * 16 + k));
     }
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int f = 4 * g + i;
-    F.b1[i] = (!FOLD && f < a.n1) ? P[OFF1 + 31 * 16 + f] : 0.f;
-    F.b2[i] = (!FOLD && f < a.n2) ? P[OFF2 + 15 * 16 + f] : 0.f;
-    F.b3[i] = (!FOLD && f < a.n3) ? P[OFF3 + 15 * 16 + f] : 0.f;
+    F.b1[i] = ldsel(P, !FOLD && f < a.n1, OFF1 + 31 * 16 + f);
+    F.b2[i] = ldsel(P, !FOLD && f < a.n2, OFF2 + 15 * 16 + f);
+    F.b3[i] = ldsel(P, !FOLD && f < a.n3, OFF3 + 15 * 16 + f);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int ft = 16 * t + f;
-      F.b4[t][i] = (!FOLD && ft < a.D) ? P[OFF4 + 15 * 32 + ft] : 0.f;
-      F.sc[t][i] = ft < a.D ? (a.scale ? a.scale[ft] : 1.0f) : 0.f;
-      F.sh[t][i] = (ft < a.D && a.scale) ? a.shift[ft] : 0.f;
+      F.b4[t][i] = ldsel(P, !FOLD && ft < a.D, OFF4 + 15 * 32 + ft);
+      // unconditional loads from a valid address (the params image when there is no
+      // normaliser), selected afterwards
+      const bool has = a.scale != nullptr;
+      const float sv = (has ? a.scale : P)[ft < a.D ? ft : 0];
+      const float hv = (has ? a.shift : P)[ft < a.D ? ft : 0];
+      F.sc[t][i] = ft < a.D ? (has ? sv : 1.0f) : 0.f;
+      F.sh[t][i] = (ft < a.D && has) ? hv : 0.f;
     }
   }
 }
@@ -159,6 +179,39 @@ __device__ __forceinline__ void fetch_x(const AEArgs& a, int64_t r, int g, f32x4
       for (int j = 0; j < 4; ++j) xr[s][j] = row[min(16 * s + 4 * g + j, a.D - 1)];
     }
   }
+}
+
+// Asynchronous global -> LDS copy of 16 B per lane (LDS destination = M0 + 16*lane).
+// Issued from inline asm on purpose: the compiler cannot tell that the ring a wave
+// reads is disjoint from the DMA target, and would drain the whole pipeline with a
+// vmcnt(0) in front of every LDS read in the loop (the transposes included).  The
+// ring's ordering is explicit instead: a counted `s_waitcnt vmcnt(N)` per tile.
+// m0 is otherwise unused by this kernel (gfx9+ LDS instructions do not read it).
+// Address = wave-uniform base (SGPR pair) + per-lane 32-bit offset; LDS destination =
+// M0 + 16*lane.  Both uniform operands must already be wave-uniform values.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is deliberately clobbered (see above)
+__device__ __forceinline__ void glds16(const void* gbase, unsigned voff, unsigned lds_addr) {
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff), "s"(gbase)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// One tile from a wave's LDS ring slot in the B-operand layout (cf. fetch_x):
+// lane (c, g) reads features 16s + 4g + 2p.. of row c with 8-byte ds_reads;
+// columns past D are clamped into the row (their scale is 0).
+__device__ __forceinline__ void ring_x(const AEArgs& a, const char* slot, int c, int g, f32x4 xr[2]) {
+  typedef __attribute__((address_space(3))) const f32x2_t lds_f2;
+  const char* row = slot + c * 4 * a.D;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int f = min(16 * s + 4 * g + 2 * p, a.D - 2);
+      const f32x2_t v = *(lds_f2*)(row + 4 * f);
+      xr[s][2 * p] = v[0];
+      xr[s][2 * p + 1] = v[1];
+    }
 }
 
 // activation + padding: real features f < n get act(z); the bias slot (15) gets 1.
@@ -371,13 +424,18 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
 }
 
 // 3 waves/SIMD: caps the allocation at 168 VGPRs (no spills); 171 would drop to 2.
-template <int PACK, bool VEC>
+// PF > 0: the input rows stream through a per-wave LDS ring PF tiles deep, filled
+// by LDS-DMA (no VGPRs held for the prefetch, PF-1 tiles in flight per wave);
+// requires contiguous rows (ld == D), 17 <= D <= 31 and D even.  PF = 0: one tile
+// of register prefetch (any ld / D).
+template <int PACK, bool VEC, int PF>
 __global__ __launch_bounds__(WAVES * 64, 3) void ae_train_kernel(AEArgs a) {
   constexpr bool FAST = zero_preserving<PACK>();
-  static_assert(WAVES * 10 * 512 <= WAVES * NSLOT * 4, "transpose scratch must fit in the slab buffer");
+  static_assert(WAVES * 10 * 512 <= SLAB_BYTES, "transpose scratch must fit in the slab buffer");
+  static_assert(PF * 64 * 17 <= RING_BYTES, "ring slots must fit the smallest ring tile");
   // one LDS array: per-wave transpose scratch during the tile loop, per-wave
-  // gradient slabs afterwards
-  __shared__ __attribute__((aligned(16))) float smem[WAVES * NSLOT];
+  // gradient slabs afterwards, then (PF > 0) the per-wave input rings
+  __shared__ __attribute__((aligned(16))) float smem[(SLAB_BYTES + (PF > 0 ? WAVES * RING_BYTES : 0)) / 4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
@@ -403,16 +461,63 @@ __global__ __launch_bounds__(WAVES * 64, 3) void ae_train_kernel(AEArgs a) {
   const int64_t nfull = a.n >> 4;
   const int64_t stride = (int64_t)gridDim.x * WAVES;
   const int64_t first = (int64_t)blockIdx.x * WAVES + wid;
-  f32x4 xnext[2];
-  if (first < nfull) fetch_x<VEC>(a, first * 16 + c, g, xnext);
-  for (int64_t t = first; t < nfull; t += stride) {
-    f32x4 xf[2];
+  if constexpr (PF > 0) {
+    // LDS-DMA ring: tile first + k*stride lives in slot k % PF.  Every issue is
+    // exactly two VMEM instructions (tiles past the end are clamped to the last
+    // full tile, never skipped), so "tile k landed" is vmcnt(2 * (PF - 1)).
+    const int slotb = 64 * a.D;
+    const int nl2 = 4 * a.D - 64;  // lanes of the second 16-B-per-lane DMA (>= 4)
+    const int uwid = __builtin_amdgcn_readfirstlane(wid);  // keep the ring bookkeeping scalar
+    const int ring_off = SLAB_BYTES + uwid * RING_BYTES;
+    const unsigned ring_lds =
+        (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem) + ring_off;
+    const char* ring = reinterpret_cast<const char*>(smem) + ring_off;
+    const int64_t ufirst = (int64_t)blockIdx.x * WAVES + uwid;
+    const unsigned voff = lane * 16;
+    // Retire the prologue's parameter loads with a compiler-visible wait: the
+    // waitcnt pass cannot see the asm DMA counts, and a load still pending at the
+    // loop entry would otherwise put a vmcnt(0) (a full ring drain) in every iteration.
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+    if (nfull > 0) {
+      auto issue = [&](int64_t tt, int slot) {
+        tt = tt < nfull ? tt : nfull - 1;
+        const char* src = reinterpret_cast<const char*>(a.x + tt * 16 * a.ld);
+        const unsigned dst = ring_lds + slot * slotb;
+        glds16(src, voff, dst);
+        if (lane < nl2) glds16(src + 1024, voff, dst + 1024);
+      };
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int k = 0; k < PF - 1; ++k) issue(ufirst + k * stride, k);
+      int rd = 0, wr = PF - 1;
+      for (int64_t t = ufirst; t < nfull; t += stride) {
+        issue(t + (PF - 1) * stride, wr);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (PF - 1)) : "memory");
+        f32x4 xf[2];
+        ring_x(a, ring + rd * slotb, c, g, xf);
+        rd = rd + 1 == PF ? 0 : rd + 1;
+        wr = wr + 1 == PF ? 0 : wr + 1;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xnext[s][j], F.sc[s][j], F.sh[s][j]);
-    if (t + stride < nfull) fetch_x<VEC>(a, (t + stride) * 16 + c, g, xnext);  // prefetch
-    train_tile<PACK, FAST, false>(a, F, scr, c, g, lane, true, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xf[s][j], F.sc[s][j], F.sh[s][j]);
+        train_tile<PACK, FAST, false>(a, F, scr, c, g, lane, true, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr,
+                                      rows);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the ring is retired
+    }
+  } else {
+    f32x4 xnext[2];
+    if (first < nfull) fetch_x<VEC>(a, first * 16 + c, g, xnext);
+    for (int64_t t = first; t < nfull; t += stride) {
+      f32x4 xf[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xnext[s][j], F.sc[s][j], F.sh[s][j]);
+      if (t + stride < nfull) fetch_x<VEC>(a, (t + stride) * 16 + c, g, xnext);  // prefetch
+      train_tile<PACK, FAST, false>(a, F, scr, c, g, lane, true, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr,
+                                    rows);
+    }
   }
   // ragged last tile: handled by the wave that would own tile index nfull
   if ((a.n & 15) && first == nfull % stride) {
@@ -609,6 +714,15 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
 // ----------------------------------------------------------------------------
 namespace sml {
 
+// SML_AE_RING=0 selects the register-prefetch variant (A/B comparisons).
+static bool ring_pf_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SML_AE_RING");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int ae_nslot() { return NSLOT; }
 int ae_nparam() { return NPARAM; }
 int ae_waves_per_block() { return WAVES; }
@@ -632,12 +746,20 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
   a.l1 = l1; a.want_acc = want_acc;
   const bool vec = ((ld & 1) == 0) && ((dims[0] & 1) == 0) && dims[0] >= 2 &&
                    ((reinterpret_cast<uintptr_t>(x) & 7) == 0);
+  // LDS-DMA ring: contiguous rows, 17 <= D <= 31 (two DMAs per tile), 16-B aligned
+  // tiles (the ring cursor moves in whole batches, so n * ld * 4 must stay 16-B aligned)
+  const int D = dims[0];
+  const bool ring_ok = vec && ld == D && D >= 17 && D <= 31 && ((reinterpret_cast<uintptr_t>(x) & 15) == 0) &&
+                       (cursor == nullptr || ((n * ld) & 3) == 0) && ring_pf_enabled();
   const int pack = acts[0] | (acts[1] << 2) | (acts[2] << 4) | (acts[3] << 6);
+  const dim3 gd(grid), bd(WAVES * 64);
   if (pack == PACK_REF) {
-    if (vec) hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
-    else hipLaunchKernelGGL((ae_train_kernel<PACK_REF, false>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
+    if (ring_ok && 5 * 64 * D <= RING_BYTES) hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 5>), gd, bd, 0, stream, a);
+    else if (ring_ok) hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3>), gd, bd, 0, stream, a);
+    else if (vec) hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 0>), gd, bd, 0, stream, a);
+    else hipLaunchKernelGGL((ae_train_kernel<PACK_REF, false, 0>), gd, bd, 0, stream, a);
   } else {
-    hipLaunchKernelGGL((ae_train_kernel<PACK_DYN, false>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
+    hipLaunchKernelGGL((ae_train_kernel<PACK_DYN, false, 0>), gd, bd, 0, stream, a);
   }
   return hipGetLastError();
 }

@@ -42,7 +42,7 @@ class Autoencoder:
     def __init__(self, input_dim: int = 18, encoding_dim: int = 14, hidden_dim: int = 7,
                  activations: Sequence[str] = ("tanh", "relu", "tanh", "relu"), activity_l1: float = 1e-7,
                  device="auto", seed: int = 0, layer_names: Optional[Sequence[str]] = None,
-                 input_normalizer: Optional[str] = None, name: str = "model", max_blocks: int = 1024):
+                 input_normalizer: Optional[str] = None, name: str = "model", max_blocks: Optional[int] = None):
         self.spec = AESpec(input_dim, encoding_dim, hidden_dim, tuple(activations), activity_l1)
         self.device = _resolve_device(device)
         self.name = name

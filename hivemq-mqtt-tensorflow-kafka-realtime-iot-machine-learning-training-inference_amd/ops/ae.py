@@ -29,6 +29,20 @@ NSLOT = 1540
 LAYOUT = [(0, 32, 16, 31), (512, 16, 16, 15), (768, 16, 16, 15), (1024, 16, 32, 15)]
 
 RA_WRITE_GRAD, RA_ADAM, RA_METRICS, RA_ADVANCE = 1, 2, 4, 8
+# ae_train_kernel: 168 VGPRs -> 3 waves/SIMD -> 3 four-wave workgroups per CU.  A grid
+# of exactly the resident capacity gives every wave the same tile count with no
+# second dispatch round (sweep on MI355X, B = 4M rows: 768 blocks 176.6 us vs
+# 1024 blocks 180.9 us; profiles/r01_v4/ae_sweep.json).
+TRAIN_BLOCKS_PER_CU = 3
+
+
+def default_train_blocks(device) -> int:
+    """Resident-capacity grid for the fused train kernel on ``device``."""
+    try:
+        cus = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
+    except Exception:  # noqa: BLE001 - no device properties (CPU build): MI355X has 256 CUs
+        cus = 256
+    return TRAIN_BLOCKS_PER_CU * int(cus)
 
 
 @dataclass
@@ -93,7 +107,7 @@ class FusedAE:
 
     def __init__(self, spec: AESpec, weights: Sequence[np.ndarray], device,
                  lr: float = 1e-3, beta_1: float = 0.9, beta_2: float = 0.999, epsilon: float = 1e-7,
-                 max_blocks: int = 1024, want_acc: bool = True,
+                 max_blocks: Optional[int] = None, want_acc: bool = True,
                  scale: Optional[np.ndarray] = None, shift: Optional[np.ndarray] = None):
         spec.check_fused()
         self.C = load_c()
@@ -104,7 +118,7 @@ class FusedAE:
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.lr, self.beta_1, self.beta_2, self.epsilon = lr, beta_1, beta_2, epsilon
-        self.max_blocks = int(max_blocks)
+        self.max_blocks = int(max_blocks) if max_blocks else default_train_blocks(self.device)
         self.want_acc = want_acc
         dev = self.device
         self.params = torch.from_numpy(pack_image(weights)).to(dev)

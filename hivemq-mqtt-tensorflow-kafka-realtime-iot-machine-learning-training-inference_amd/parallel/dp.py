@@ -55,9 +55,13 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: Optional[int] = 
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
-        backend = "nccl"   # RCCL on ROCm
+        # SML_SHARE_GPU0=1 maps every rank onto GPU 0 (multi-rank rehearsal on a
+        # one-GPU box; RCCL refuses two ranks on one device, so that mode uses gloo)
+        shared = os.environ.get("SML_SHARE_GPU0") == "1"
+        local_dev = 0 if shared else local
+        torch.cuda.set_device(local_dev)
+        device = torch.device("cuda", local_dev)
+        backend = os.environ.get("SML_DIST_BACKEND", "gloo" if shared else "nccl")   # nccl = RCCL on ROCm
     else:
         device = torch.device("cpu")
         backend = "gloo"
@@ -155,7 +159,7 @@ def reduce_metrics(metrics: dict, device: torch.device, weight_key: str = "rows"
 
 def barrier(device: Optional[torch.device] = None) -> None:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        if device is not None and device.type == "cuda":
+        if device is not None and device.type == "cuda" and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()

@@ -173,3 +173,25 @@ def test_ring_cursor_and_graph_replay(cuda_device):
     torch.cuda.synchronize()
     torch.testing.assert_close(a.params, b.params, rtol=0, atol=0)
     assert int(b.iter.item()) == int(a.iter.item()) == 7
+
+
+@pytest.mark.parametrize("D,n,blocks", [(18, 16 * 1000 + 5, 7), (18, 4096, 768), (30, 16 * 333, 5), (18, 40, 64)])
+def test_lds_dma_ring_matches_register_path(cuda_device, D, n, blocks):
+    """The LDS-DMA input ring (contiguous rows) and the register-prefetch path
+    (rows with a wider stride) run the same tile math in the same order: their
+    gradient slabs must agree bit for bit, including ragged tails, waves with no
+    tiles and rings clamped past the last tile."""
+    spec = AESpec(input_dim=D)
+    w = _weights(spec, seed=11)
+    rng = np.random.default_rng(13)
+    x = rng.uniform(-1, 1, size=(n, D)).astype(np.float32)
+    wide = np.zeros((n, D + 2), np.float32)
+    wide[:, :D] = x
+    fused = FusedAE(spec, w, cuda_device, max_blocks=blocks)
+    g_ring, m_ring = fused.gradients(torch.from_numpy(x).to(cuda_device))
+    xw = torch.from_numpy(wide).to(cuda_device)[:, :D]
+    assert xw.stride(0) == D + 2
+    g_reg, m_reg = fused.gradients(xw)
+    for a, b in zip(g_ring, g_reg):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(m_ring, m_reg)
