@@ -14,6 +14,9 @@ Commands (reference script in parentheses):
   broker       [--port 9092] [--sasl user:pw] [--preload TOPIC=ROWS]
   train        [--config job.yaml] [--key=value ...] [--ckpt-dir D]   restartable (torchrun) training job
   ksql         <servers> <source_topic> <target_topic> [--window 300]   per-car tumbling event counts
+  ksql-avro    <servers> [--source sensor-data] [--target SENSOR_DATA_S_AVRO]   KSQL JSON -> Avro (+ REKEY)
+  mqtt-broker  [--port 1883] [--kafka SERVERS] [--kafka-extension kafka-config.yaml]   HiveMQ + Kafka extension
+  devsim       run -s scenario.xml [--broker host:port] [--clients N]   HiveMQ device simulator
 """
 from __future__ import annotations
 
@@ -25,7 +28,7 @@ from . import common
 def _commands():
     from . import cardata_autoencoder as ae
     from . import cardata_lstm as ls
-    from . import creditcard, mnist, tools, train
+    from . import creditcard, mnist, mqtt, tools, train
     return {
         "cardata-v3": ae.main_v3,
         "cardata-v1": ae.main_v1,
@@ -37,6 +40,9 @@ def _commands():
         "broker": tools.main_broker,
         "train": train.main,
         "ksql": tools.main_ksql,
+        "ksql-avro": mqtt.main_ksql_avro,
+        "mqtt-broker": mqtt.main_broker,
+        "devsim": mqtt.main_devsim,
     }
 
 

@@ -8,6 +8,7 @@
 #include "avro.h"
 #include "h5.h"
 #include "kafka.h"
+#include "mqtt.h"
 
 namespace py = pybind11;
 using namespace sml;
@@ -398,4 +399,212 @@ PYBIND11_MODULE(_io, m) {
         py::gil_scoped_release rel;
         b.stop();
       });
+
+  // MQTT (broker + Kafka bridge, client, device simulator)
+  m.def("mqtt_topic_matches", &mqtt::topic_matches, py::arg("filter"), py::arg("topic"));
+  m.def("mqtt_valid_filter", &mqtt::valid_filter, py::arg("filter"));
+  m.def("kafka_partition", &mqtt::kafka_partition, py::arg("key"), py::arg("partitions"),
+        "Kafka default partitioner: murmur2(key) & 0x7fffffff % partitions");
+  m.def("murmur2", &mqtt::murmur2, py::arg("key"));
+  m.def("mqtt_encode_publish", [](const std::string& topic, const py::bytes& payload, int qos, bool retain,
+                                  int packet_id, int version) {
+    mqtt::Message msg;
+    msg.topic = topic;
+    msg.payload = payload;
+    msg.qos = qos;
+    msg.retain = retain;
+    msg.packet_id = (uint16_t)packet_id;
+    return py::bytes(mqtt::encode_publish(msg, version));
+  }, py::arg("topic"), py::arg("payload"), py::arg("qos") = 0, py::arg("retain") = false,
+        py::arg("packet_id") = 0, py::arg("version") = 5);
+  m.def("mqtt_parse_packet", [](const py::bytes& b, int version) -> py::object {
+    std::string_view sv = b;
+    mqtt::Packet pk;
+    const size_t used = mqtt::parse_packet(reinterpret_cast<const uint8_t*>(sv.data()), sv.size(), pk);
+    if (!used) return py::none();
+    py::dict d;
+    d["type"] = (int)pk.type;
+    d["flags"] = (int)pk.flags;
+    d["size"] = used;
+    d["body"] = py::bytes(pk.body);
+    if (pk.type == mqtt::PUBLISH) {
+      mqtt::Message msg = mqtt::decode_publish(pk, version);
+      d["topic"] = msg.topic;
+      d["payload"] = py::bytes(msg.payload);
+      d["qos"] = msg.qos;
+      d["retain"] = msg.retain;
+      d["packet_id"] = (int)msg.packet_id;
+    }
+    return d;
+  }, py::arg("data"), py::arg("version") = 5);
+
+  py::class_<mqtt::Broker>(m, "MqttBroker")
+      .def(py::init([](int port, const std::string& user, const std::string& pw, int max_qos,
+                       const std::string& kafka_bootstrap, const py::list& mappings, const std::string& k_mech,
+                       const std::string& k_user, const std::string& k_pw, int batch, int linger_ms) {
+             mqtt::BrokerConfig c;
+             c.port = port;
+             c.username = user;
+             c.password = pw;
+             c.max_qos = max_qos;
+             c.kafka_bootstrap = kafka_bootstrap;
+             c.kafka.client_id = "mqtt-kafka-bridge";
+             c.kafka.sasl_mechanism = k_mech;
+             c.kafka.sasl_username = k_user;
+             c.kafka.sasl_password = k_pw;
+             c.bridge_batch = batch;
+             c.bridge_linger_ms = linger_ms;
+             for (auto item : mappings) {
+               auto t = item.cast<py::tuple>();  // (id, [filters], kafka_topic)
+               mqtt::TopicMapping tm;
+               tm.id = t[0].cast<std::string>();
+               tm.filters = t[1].cast<std::vector<std::string>>();
+               tm.kafka_topic = t[2].cast<std::string>();
+               c.mappings.push_back(tm);
+             }
+             py::gil_scoped_release rel;
+             return new mqtt::Broker(c);
+           }),
+           py::arg("port") = 0, py::arg("username") = "", py::arg("password") = "", py::arg("max_qos") = 2,
+           py::arg("kafka_bootstrap") = "", py::arg("mappings") = py::list(), py::arg("kafka_sasl_mechanism") = "",
+           py::arg("kafka_sasl_username") = "", py::arg("kafka_sasl_password") = "", py::arg("bridge_batch") = 1024,
+           py::arg("bridge_linger_ms") = 2)
+      .def_property_readonly("port", &mqtt::Broker::port)
+      .def("publish",
+           [](mqtt::Broker& b, const std::string& topic, const py::bytes& payload, int qos, bool retain) {
+             mqtt::Message msg;
+             msg.topic = topic;
+             msg.payload = payload;
+             msg.qos = qos;
+             msg.retain = retain;
+             py::gil_scoped_release rel;
+             b.publish(msg);
+           },
+           py::arg("topic"), py::arg("payload"), py::arg("qos") = 0, py::arg("retain") = false)
+      .def("stats", [](mqtt::Broker& b) {
+        const auto st = b.stats();
+        py::dict d;
+        d["incoming_publish"] = st.incoming_publish;
+        d["outgoing_publish"] = st.outgoing_publish;
+        d["connections_current"] = st.connections_current;
+        d["connections_total"] = st.connections_total;
+        d["retained"] = st.retained;
+        d["kafka_sent"] = st.kafka_sent;
+        d["kafka_failed"] = st.kafka_failed;
+        d["kafka_queued"] = st.kafka_queued;
+        return d;
+      })
+      .def("mapping_counts", &mqtt::Broker::mapping_counts)
+      .def("flush",
+           [](mqtt::Broker& b, int timeout_ms) {
+             py::gil_scoped_release rel;
+             return b.flush(timeout_ms);
+           },
+           py::arg("timeout_ms") = 10000)
+      .def("stop", [](mqtt::Broker& b) {
+        py::gil_scoped_release rel;
+        b.stop();
+      });
+
+  py::class_<mqtt::Client>(m, "MqttClient")
+      .def(py::init<>())
+      .def("connect",
+           [](mqtt::Client& c, const std::string& host, int port, const std::string& cid, int version, int keepalive,
+              bool clean, const std::string& user, const std::string& pw, int timeout_ms) {
+             py::gil_scoped_release rel;
+             return c.connect(host, port, cid, version, (uint16_t)keepalive, clean, user, pw, timeout_ms);
+           },
+           py::arg("host"), py::arg("port"), py::arg("client_id"), py::arg("version") = 5,
+           py::arg("keepalive") = 60, py::arg("clean") = true, py::arg("username") = "", py::arg("password") = "",
+           py::arg("timeout_ms") = 5000)
+      .def("publish",
+           [](mqtt::Client& c, const std::string& topic, const py::bytes& payload, int qos, bool retain) {
+             std::string p = payload;
+             py::gil_scoped_release rel;
+             c.publish(topic, p, qos, retain);
+           },
+           py::arg("topic"), py::arg("payload"), py::arg("qos") = 0, py::arg("retain") = false)
+      .def("subscribe",
+           [](mqtt::Client& c, const std::vector<std::pair<std::string, int>>& f) {
+             py::gil_scoped_release rel;
+             return c.subscribe(f);
+           })
+      .def("unsubscribe",
+           [](mqtt::Client& c, const std::vector<std::string>& f) {
+             py::gil_scoped_release rel;
+             c.unsubscribe(f);
+           })
+      .def("receive",
+           [](mqtt::Client& c, int timeout_ms) -> py::object {
+             mqtt::Message msg;
+             bool ok;
+             {
+               py::gil_scoped_release rel;
+               ok = c.receive(msg, timeout_ms);
+             }
+             if (!ok) return py::none();
+             return py::make_tuple(msg.topic, py::bytes(msg.payload), msg.qos, msg.retain);
+           },
+           py::arg("timeout_ms") = 1000)
+      .def("ping",
+           [](mqtt::Client& c, int timeout_ms) {
+             py::gil_scoped_release rel;
+             return c.ping(timeout_ms);
+           },
+           py::arg("timeout_ms") = 2000)
+      .def("disconnect",
+           [](mqtt::Client& c) {
+             py::gil_scoped_release rel;
+             c.disconnect();
+           })
+      .def_property_readonly("connected", &mqtt::Client::connected)
+      .def_property_readonly("session_present", &mqtt::Client::session_present);
+
+  m.def("mqtt_simulate",
+        [](const py::dict& d) {
+          mqtt::SimConfig c;
+          if (d.contains("host")) c.host = d["host"].cast<std::string>();
+          if (d.contains("port")) c.port = d["port"].cast<int>();
+          if (d.contains("client_prefix")) c.client_prefix = d["client_prefix"].cast<std::string>();
+          if (d.contains("id_digits")) c.id_digits = d["id_digits"].cast<int>();
+          if (d.contains("id_offset")) c.id_offset = d["id_offset"].cast<int>();
+          if (d.contains("topic_prefix")) c.topic_prefix = d["topic_prefix"].cast<std::string>();
+          if (d.contains("clients")) c.clients = d["clients"].cast<int>();
+          if (d.contains("messages_per_client")) c.messages_per_client = d["messages_per_client"].cast<int>();
+          if (d.contains("interval_s")) c.interval_s = d["interval_s"].cast<double>();
+          if (d.contains("ramp_s")) c.ramp_s = d["ramp_s"].cast<double>();
+          if (d.contains("qos")) c.qos = d["qos"].cast<int>();
+          if (d.contains("version")) c.version = d["version"].cast<int>();
+          if (d.contains("threads")) c.threads = d["threads"].cast<int>();
+          if (d.contains("seed")) c.seed = d["seed"].cast<uint64_t>();
+          if (d.contains("failure_rate")) c.failure_rate = d["failure_rate"].cast<double>();
+          if (d.contains("username")) c.username = d["username"].cast<std::string>();
+          if (d.contains("password")) c.password = d["password"].cast<std::string>();
+          if (d.contains("lo")) c.lo = d["lo"].cast<std::vector<double>>();
+          if (d.contains("hi")) c.hi = d["hi"].cast<std::vector<double>>();
+          if (d.contains("is_int")) c.is_int = d["is_int"].cast<std::vector<int>>();
+          mqtt::SimStats st;
+          {
+            py::gil_scoped_release rel;
+            st = mqtt::simulate(c);
+          }
+          py::dict out;
+          out["connected"] = st.connected;
+          out["connect_failed"] = st.connect_failed;
+          out["published"] = st.published;
+          out["acked"] = st.acked;
+          out["publish_failed"] = st.publish_failed;
+          out["elapsed_s"] = st.elapsed_s;
+          return out;
+        },
+        py::arg("config"));
+  m.def("mqtt_car_payload", [](const py::dict& d, uint64_t car, uint64_t seq, int64_t ts) {
+    mqtt::SimConfig c;
+    if (d.contains("seed")) c.seed = d["seed"].cast<uint64_t>();
+    if (d.contains("failure_rate")) c.failure_rate = d["failure_rate"].cast<double>();
+    if (d.contains("lo")) c.lo = d["lo"].cast<std::vector<double>>();
+    if (d.contains("hi")) c.hi = d["hi"].cast<std::vector<double>>();
+    if (d.contains("is_int")) c.is_int = d["is_int"].cast<std::vector<int>>();
+    return py::bytes(mqtt::car_payload_json(c, car, seq, ts));
+  });
 }

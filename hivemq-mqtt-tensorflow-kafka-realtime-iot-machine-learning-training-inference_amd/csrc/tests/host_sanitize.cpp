@@ -8,8 +8,11 @@
 //             Avro records, Kafka record batches and HDF5 images to the decoders;
 //             every malformed input must end in a clean exception, never UB.
 //   threads:  one in-process broker, several producer and consumer threads on
-//             separate client connections, concurrent appends / fetches / commits.
+//             separate client connections, concurrent appends / fetches / commits;
+//             then the MQTT broker (epoll I/O threads) with its Kafka bridge under
+//             concurrent publishers, a shared-subscription group and the simulator.
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -20,6 +23,7 @@
 #include "../io/avro.h"
 #include "../io/h5.h"
 #include "../io/kafka.h"
+#include "../io/mqtt.h"
 
 using namespace sml;
 
@@ -165,6 +169,48 @@ void fuzz_h5(std::mt19937_64& rng) {
   std::printf("h5: ok (%d rejected)\n", errs);
 }
 
+
+void fuzz_mqtt(std::mt19937_64& rng) {
+  // valid packets first, then mutations through the framing parser and PUBLISH decoder
+  std::vector<std::string> seeds;
+  for (int v : {4, 5})
+    for (int q = 0; q < 3; ++q) {
+      mqtt::Message m;
+      m.topic = "vehicles/sensor/data/electric-vehicle-0000" + std::to_string(q);
+      m.payload = std::string(40 + 300 * q, 'x');
+      m.qos = q;
+      m.packet_id = (uint16_t)(q + 1);
+      seeds.push_back(mqtt::encode_publish(m, v));
+      seeds.push_back(mqtt::encode_connect("c" + std::to_string(q), v, 60, q != 1, q ? "u" : "", q ? "p" : ""));
+      seeds.push_back(mqtt::encode_subscribe((uint16_t)(q + 9), {{"a/+/#", q}, {"$share/g/b", 1}}, v));
+    }
+  int errs = 0, parsed = 0;
+  for (int it = 0; it < 20000; ++it) {
+    std::string b = seeds[rng() % seeds.size()];
+    if (it % 10) mutate(b, rng);
+    try {
+      mqtt::Packet pk;
+      const size_t used = mqtt::parse_packet(reinterpret_cast<const uint8_t*>(b.data()), b.size(), pk);
+      CHECK(used <= b.size());
+      if (used && pk.type == mqtt::PUBLISH) {
+        mqtt::Message m = mqtt::decode_publish(pk, (it & 1) ? 5 : 4);
+        CHECK(m.topic.size() + m.payload.size() <= pk.body.size());
+      }
+      if (used) ++parsed;
+    } catch (const std::exception&) {
+      ++errs;
+    }
+  }
+  for (int it = 0; it < 5000; ++it) {  // topic matcher on random filters/topics
+    std::string f, t;
+    const char alpha[] = "ab/+#$";
+    for (int k = rng() % 8; k > 0; --k) f.push_back(alpha[rng() % 6]);
+    for (int k = rng() % 8; k > 0; --k) t.push_back(alpha[rng() % 3]);
+    if (mqtt::valid_filter(f)) (void)mqtt::topic_matches(f, t);
+  }
+  std::printf("mqtt: ok (%d parsed, %d rejected)\n", parsed, errs);
+}
+
 void threads_broker() {
   kafka::BrokerConfig bc;
   bc.sasl_username = "test";
@@ -226,6 +272,59 @@ void threads_broker() {
   std::printf("threads: ok (produced %d, consumed %d)\n", produced.load(), consumed.load());
 }
 
+
+void threads_mqtt() {
+  kafka::BrokerConfig kbc;
+  kafka::Broker kb(kbc);
+  kb.create_topic("sensor-data", 4);
+  mqtt::BrokerConfig mc;
+  mc.kafka_bootstrap = "127.0.0.1:" + std::to_string(kb.port());
+  mc.mappings.push_back({"sensor-data", {"vehicles/sensor/data/#"}, "sensor-data"});
+  mqtt::Broker broker(mc);
+  std::atomic<int> got{0}, errors{0};
+  std::atomic<bool> done{false};
+  std::vector<std::thread> th;
+  for (int c = 0; c < 3; ++c) {  // shared-subscription consumers
+    th.emplace_back([&, c] {
+      try {
+        mqtt::Client cl;
+        cl.connect("127.0.0.1", broker.port(), "consumer-" + std::to_string(c), 5);
+        cl.subscribe({{"$share/consumers/vehicles/sensor/data/#", 1}});
+        mqtt::Message m;
+        while (!done || cl.receive(m, 200)) {
+          if (cl.receive(m, 50)) ++got;
+        }
+        cl.disconnect();
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "mqtt consumer: %s\n", e.what());
+        ++errors;
+      }
+    });
+  }
+  std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  mqtt::SimConfig sc;
+  sc.port = broker.port();
+  sc.clients = 40;
+  sc.messages_per_client = 10;
+  sc.interval_s = 0.002;
+  sc.qos = 1;
+  sc.threads = 4;
+  const auto st = mqtt::simulate(sc);
+  CHECK(st.published == 400 && st.acked == 400 && st.connect_failed == 0);
+  CHECK(broker.flush(10000));
+  std::this_thread::sleep_for(std::chrono::milliseconds(300));
+  done = true;
+  for (auto& t : th) t.join();
+  int64_t in_kafka = 0;
+  for (int p = 0; p < 4; ++p) in_kafka += kb.end_offset("sensor-data", p);
+  broker.stop();
+  kb.stop();
+  CHECK(errors == 0);
+  CHECK(in_kafka == 400);
+  CHECK(got == 400);
+  std::printf("threads mqtt: ok (kafka %lld, shared consumers %d)\n", (long long)in_kafka, got.load());
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -235,8 +334,10 @@ int main(int argc, char** argv) {
     fuzz_avro(rng);
     fuzz_kafka_batches(rng);
     fuzz_h5(rng);
+    fuzz_mqtt(rng);
   } else if (mode == "threads") {
     threads_broker();
+    threads_mqtt();
   } else {
     std::fprintf(stderr, "usage: %s fuzz|threads\n", argv[0]);
     return 2;

@@ -121,6 +121,11 @@ def _aliases() -> Dict[str, str]:
         "controlUnitFirmware": "control_unit_firmware", "failureOccurred": "failure_occurred",
     }
     al.update(extra)
+    # lower-case KSQL DDL column names (CREATE STREAM SENSOR_DATA_S (... tire_pressure11 INT,
+    # accelerometer11_value DOUBLE ...), 01_installConfluentPlatform.sh:235)
+    for k, v in extra.items():
+        if k.isupper():
+            al[k.lower()] = v
     return al
 
 

@@ -8,8 +8,12 @@
 4. ``SENSOR_DATA_EVENTS_PER_5MIN_T`` -- ``SELECT car, count(*) as event_count ...
    WINDOW TUMBLING (SIZE 5 MINUTE) GROUP BY car``.
 
-Steps 1-3 are the producer (``data.produce``: Avro + Confluent framing, keyed by
-car, ``hash(key) % partitions``).  Step 4 is :class:`TumblingCounter`, a
+Steps 1-3 run as :func:`run_json_to_avro` on the JSON records the MQTT->Kafka bridge
+writes to ``sensor-data`` (``streamml.mqtt``): parse, re-encode as Confluent-framed Avro
+(KSQL's nullable ``KsqlDataSourceSchema``), keep the Kafka key (the MQTT topic = ROWKEY)
+and partition the REKEY stream by it with Kafka's murmur2 partitioner.  Synthetic
+sources skip the JSON stage (``data.produce`` writes the Avro streams directly).  Step 4
+is :class:`TumblingCounter`, a
 vectorised (numpy ``unique``) per-key tumbling-window count; :func:`run_events_per_window`
 drives it as a Kafka-to-Kafka job whose output records are keyed
 ``<car>@<window_start_ms>`` with JSON values, the shape KSQL's windowed table
@@ -101,3 +105,79 @@ def run_events_per_window(servers: str, source_topic: str, target_topic: str, wi
     emit(sorted(((k, w, c) for (k, w), c in tc.counts.items()), key=lambda r: (r[1], r[0])))
     tc.counts.clear()
     return produced
+
+
+def _parse_json_rows(values: bytes, voffs):
+    """JSON car events (SENSOR_DATA_S columns) -> raw feature rows [n, 18] + label codes.
+
+    Field names are matched through :func:`streamml.data.cardata.canonical` (KSQL
+    upper-case, snake_case and camelCase all map).  Missing numeric fields become
+    NaN (KSQL nulls); unparsable records are skipped and counted."""
+    from .cardata import FEATURES, LABEL, canonical
+    from .stream import LABEL_FALSE, LABEL_MISSING, LABEL_TRUE
+    n = len(voffs) - 1
+    x = np.full((n, len(FEATURES)), np.nan, dtype=np.float64)
+    lab = np.full(n, LABEL_MISSING, dtype=np.uint8)
+    ok = np.ones(n, dtype=bool)
+    col = {f: i for i, f in enumerate(FEATURES)}
+    bad = 0
+    for i in range(n):
+        try:
+            rec = json.loads(values[voffs[i]:voffs[i + 1]])
+        except ValueError:
+            ok[i] = False
+            bad += 1
+            continue
+        for k, v in rec.items():
+            c = canonical(k)
+            if c == LABEL:
+                lab[i] = LABEL_TRUE if str(v).lower() == "true" else (LABEL_FALSE if str(v).lower() == "false"
+                                                                    else LABEL_MISSING)
+            elif c in col and v is not None:
+                x[i, col[c]] = float(v)
+    return x[ok], lab[ok], bad, ok
+
+
+def run_json_to_avro(servers: str, source_topic: str = "sensor-data", target_topic: str = "SENSOR_DATA_S_AVRO",
+                     rekey_topic: Optional[str] = "SENSOR_DATA_S_AVRO_REKEY", schema: str = "ksql-cardata-v1",
+                     config=None, eof: bool = True, target_partitions: int = 1,
+                     rekey_partitions: Optional[int] = None, idle_timeout_s: Optional[float] = None) -> dict:
+    """KSQL steps 1-3 (01_installConfluentPlatform.sh:235-249) as one streaming job.
+
+    ``SENSOR_DATA_S`` (JSON on ``source_topic``) -> ``SENSOR_DATA_S_AVRO`` (Avro, partition
+    ``target_partitions`` spread by key) and ``SENSOR_DATA_S_AVRO_REKEY`` (same records,
+    ``PARTITION BY CAR`` where CAR = ROWKEY = the MQTT topic the bridge used as key).
+    Record timestamps are carried over.  Returns counts."""
+    from ..kafka import KafkaClient, KafkaDataset
+    from ..mqtt import kafka_partition
+    from .avro import AvroCodec
+    from .produce import encode_chunk
+    cl = KafkaClient(servers, config)
+    parts = cl.partitions()
+    nsrc = parts.get(source_topic, 1)
+    codec = AvroCodec(schema)
+    npart_t = max(1, int(target_partitions))
+    npart_r = int(rekey_partitions or parts.get(rekey_topic, npart_t) if rekey_topic else 1)
+    stats = {"read": 0, "written": 0, "rekeyed": 0, "bad": 0}
+    specs = [f"{source_topic}:{p}:0" for p in range(nsrc)]
+    for b in KafkaDataset(specs, servers=servers, eof=eof, config_global=config, idle_timeout_s=idle_timeout_s):
+        voffs = np.asarray(b["value_offsets"], dtype=np.int64)
+        x, lab, bad, ok = _parse_json_rows(b["values"], voffs)
+        stats["read"] += len(voffs) - 1
+        stats["bad"] += bad
+        if len(x) == 0:
+            continue
+        keys = [k for k, good in zip(b["keys"], ok) if good]
+        ts = np.asarray(b["timestamps"], dtype=np.int64)[ok]
+        buf, offs = encode_chunk(codec, x, lab, framing=True)
+        vals = [buf[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+        for topic, npart, counter in ((target_topic, npart_t, "written"), (rekey_topic, npart_r, "rekeyed")):
+            if not topic:
+                continue
+            pidx = np.array([kafka_partition(k, npart) for k in keys]) if npart > 1 else np.zeros(len(keys), int)
+            for p in range(npart):
+                idx = np.nonzero(pidx == p)[0]
+                if len(idx):
+                    cl.produce(topic, p, [vals[i] for i in idx], [keys[i] for i in idx], ts[idx])
+            stats[counter] += len(vals)
+    return stats

@@ -1,5 +1,6 @@
-"""Host-code sanitizers: the native Avro / Kafka record-batch / HDF5
-parsers fuzzed under ASan+UBSan, and the threaded broker + clients under TSan.
+"""Host-code sanitizers: the native Avro / Kafka record-batch / HDF5 /
+MQTT parsers fuzzed under ASan+UBSan, and the threaded Kafka broker + clients and the
+MQTT broker + Kafka bridge + simulator under TSan.
 Plain C++ harness (csrc/tests/host_sanitize.cpp), no Python extension, no GPU."""
 import hashlib
 import os
@@ -13,14 +14,14 @@ PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                    "hivemq-mqtt-tensorflow-kafka-realtime-iot-machine-learning-training-inference_amd")
 CSRC = os.path.join(PKG, "csrc")
 SRCS = [os.path.join(CSRC, "tests", "host_sanitize.cpp")] + \
-    [os.path.join(CSRC, "io", f) for f in ("avro.cpp", "kafka.cpp", "h5.cpp")]
+    [os.path.join(CSRC, "io", f) for f in ("avro.cpp", "kafka.cpp", "h5.cpp", "mqtt.cpp")]
 
 
 def _build(flags, name):
     if shutil.which("g++") is None:
         pytest.skip("g++ not available")
     h = hashlib.sha1()
-    for p in SRCS + [os.path.join(CSRC, "io", f) for f in ("avro.h", "kafka.h", "h5.h")]:
+    for p in SRCS + [os.path.join(CSRC, "io", f) for f in ("avro.h", "kafka.h", "h5.h", "mqtt.h")]:
         with open(p, "rb") as f:
             h.update(f.read())
     h.update(" ".join(flags).encode())
