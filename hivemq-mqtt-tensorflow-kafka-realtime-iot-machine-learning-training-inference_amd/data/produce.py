@@ -4,12 +4,11 @@ Replaces the reference's test feeders: the kafka-python CSV
 producer (autoencoder-anomaly-detection/Sensor-Kafka-Producer-From-CSV.py:5-15),
 ``kafka-avro-console-producer`` of JSON lines (LSTM-.../cardata-v1.sh:6) and the
 KSQL JSON->Avro conversion (01_installConfluentPlatform.sh:242).  Records are
-keyed by car id and routed to ``hash(key) % partitions`` (KSQL ``PARTITION BY
-CAR``, :249) when the topic has several partitions.
+keyed by car id and routed with Kafka's default partitioner (murmur2 of the key,
+as KSQL ``PARTITION BY CAR`` does, :249) when the topic has several partitions.
 """
 from __future__ import annotations
 
-import zlib
 from typing import Optional, Sequence
 
 import numpy as np
@@ -64,7 +63,8 @@ def produce(stream: Stream, servers: str, topic: str, schema="cardata-v1", parti
         # Kafka timestamps are epoch milliseconds; the car events carry epoch seconds
         ts = None if ts is None else (np.asarray(ts, dtype=np.int64) * (1000 if np.max(ts) < 1e11 else 1))
         if keys is not None and nparts > 1:
-            parts = np.array([zlib.crc32(k) % nparts for k in keys])
+            from ..mqtt import kafka_partition
+            parts = np.array([kafka_partition(k, nparts) for k in keys])
             for p in range(nparts):
                 idx = np.nonzero(parts == p)[0]
                 if len(idx):

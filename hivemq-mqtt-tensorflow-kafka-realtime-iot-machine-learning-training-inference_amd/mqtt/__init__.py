@@ -99,7 +99,7 @@ class MqttBroker:
     def __init__(self, port: int = 0, kafka: Optional[str] = None,
                  mappings: Optional[Sequence[TopicMapping]] = None, username: str = "", password: str = "",
                  max_qos: int = 2, kafka_config: Optional[Sequence[str]] = None, bridge_batch: int = 1024,
-                 bridge_linger_ms: int = 2):
+                 bridge_linger_ms: int = 2, metrics: bool = True):
         from ..kafka.client import parse_config, resolve_servers
         if mappings is None:
             mappings = [TopicMapping(SENSOR_KAFKA_TOPIC, [SENSOR_TOPIC_FILTER], SENSOR_KAFKA_TOPIC)]
@@ -113,6 +113,39 @@ class MqttBroker:
                                    [(m.id, list(m.filters), m.kafka_topic) for m in self.mappings], mech,
                                    kcfg.get("sasl.username", ""), kcfg.get("sasl.password", ""), bridge_batch,
                                    bridge_linger_ms)
+        self._metrics_key = None
+        if metrics:
+            self._register_metrics()
+
+    def _register_metrics(self) -> None:
+        """Expose the broker's counters under the HiveMQ / Kafka-extension metric names the
+        reference's Grafana dashboard queries (infrastructure/hivemq/hivemq.json)."""
+        import weakref
+        from ..obs.metrics import REGISTRY
+        ref = weakref.ref(self)
+        port = self.port
+
+        def collect():
+            b = ref()
+            if b is None:
+                return []
+            st = b._b.stats()
+            lab = {"broker": str(port)}
+            out = [("com_hivemq_messages_incoming_publish_count", "counter", st["incoming_publish"], lab),
+                   ("com_hivemq_messages_outgoing_publish_count", "counter", st["outgoing_publish"], lab),
+                   ("com_hivemq_networking_connections_current", "gauge", st["connections_current"], lab),
+                   ("com_hivemq_networking_connections_total_count", "counter", st["connections_total"], lab),
+                   ("com_hivemq_messages_retained_current", "gauge", st["retained"], lab),
+                   ("kafka_extension_total_success_count", "counter", st["kafka_sent"], lab),
+                   ("kafka_extension_total_failure_count", "counter", st["kafka_failed"], lab),
+                   ("kafka_extension_queue_current", "gauge", st["kafka_queued"], lab)]
+            for mid, n in b._b.mapping_counts().items():
+                name = "kafka_extension_topic_mapping_" + re.sub(r"[^a-zA-Z0-9_]", "_", mid) + "_send_count"
+                out.append((name, "counter", n, lab))
+            return out
+
+        self._metrics_key = f"mqtt-broker-{port}-{id(self)}"
+        REGISTRY.add_collector(self._metrics_key, collect)
 
     @property
     def port(self) -> int:
@@ -138,6 +171,10 @@ class MqttBroker:
 
     def stop(self) -> None:
         self._b.stop()
+        if self._metrics_key:
+            from ..obs.metrics import REGISTRY
+            REGISTRY.remove_collector(self._metrics_key)
+            self._metrics_key = None
 
     def __enter__(self):
         return self
@@ -309,7 +346,16 @@ def simulate(scenario: Scenario, host: Optional[str] = None, port: Optional[int]
         "lo": [float(SYNTH_RANGES[f][0]) for f in FEATURES], "hi": [float(SYNTH_RANGES[f][1]) for f in FEATURES],
         "is_int": [1 if f in INT_FEATURES else 0 for f in FEATURES],
     }
-    return _io().mqtt_simulate(cfg)
+    st = _io().mqtt_simulate(cfg)
+    # device-simulator agent counters (infrastructure/test-generator/devsim.json)
+    from ..obs.metrics import REGISTRY
+    for name, v in (("agent_connect_successful_count", st["connected"]),
+                    ("agent_connect_failed_count", st["connect_failed"]),
+                    ("agent_publish_outgoing_count", st["published"] + st["publish_failed"]),
+                    ("agent_publish_successful_count", st["published"]),
+                    ("agent_publish_error_count", st["publish_failed"])):
+        REGISTRY.counter(name, "device simulator (streamml.mqtt.simulate)").inc(float(v))
+    return st
 
 
 def car_payload(car: int, seq: int, ts_ms: int = 0, seed: int = 0, failure_rate: float = 0.01) -> bytes:

@@ -109,7 +109,18 @@ class Summary(_Metric):
 class Registry:
     def __init__(self):
         self._m: Dict[str, _Metric] = {}
+        self._collectors: Dict[str, object] = {}
         self._lock = threading.Lock()
+
+    def add_collector(self, key: str, fn) -> None:
+        """``fn() -> [(name, kind, value, labels_dict)]`` sampled at every scrape (native
+        components -- the MQTT broker's counters -- are read, not mirrored)."""
+        with self._lock:
+            self._collectors[key] = fn
+
+    def remove_collector(self, key: str) -> None:
+        with self._lock:
+            self._collectors.pop(key, None)
 
     def _get(self, cls, name, help, labels, **kw):
         with self._lock:
@@ -137,6 +148,20 @@ class Registry:
                 lines.append(f"# HELP {name} {m.help}")
             lines.append(f"# TYPE {name} {m.kind}")
             lines += m.expose()
+        with self._lock:
+            collectors = list(self._collectors.values())
+        sampled: Dict[str, Tuple[str, List[str]]] = {}
+        for fn in collectors:
+            try:
+                samples = fn()
+            except Exception:  # noqa: BLE001 - a stopped component drops out of the scrape
+                continue
+            for name, kind, value, labels in samples:
+                lab = "{" + ",".join(f'{k}="{v}"' for k, v in sorted(labels.items())) + "}" if labels else ""
+                sampled.setdefault(name, (kind, []))[1].append(f"{name}{lab} {float(value):.17g}")
+        for name, (kind, rows) in sorted(sampled.items()):
+            lines.append(f"# TYPE {name} {kind}")
+            lines += rows
         return "\n".join(lines) + "\n"
 
     def serve(self, port: int = 0, addr: str = "127.0.0.1") -> HTTPServer:

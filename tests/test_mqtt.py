@@ -290,3 +290,17 @@ def test_cli_devsim_and_broker(tmp_path):
         out = srv.communicate(timeout=30)[0]
     final = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
     assert final["incoming_publish"] == 150 and final["kafka_sent"] == 150
+
+
+def test_prometheus_exposes_hivemq_and_devsim_metrics():
+    from streamml.obs.metrics import REGISTRY
+    with MqttBroker(kafka="fake://mqtt-metrics") as b:
+        sc = Scenario().scaled(clients=5, messages=2, interval_s=0.001)
+        simulate(sc, "127.0.0.1", b.port, threads=2)
+        assert b.flush(5.0)
+        text = REGISTRY.exposition()
+        lab = f'{{broker="{b.port}"}}'
+        assert f"com_hivemq_messages_incoming_publish_count{lab} 10" in text
+        assert f"kafka_extension_topic_mapping_sensor_data_send_count{lab} 10" in text
+        assert "agent_publish_successful_count" in text
+    assert f'broker="{b.port}"' not in REGISTRY.exposition()      # stopped brokers leave the scrape
