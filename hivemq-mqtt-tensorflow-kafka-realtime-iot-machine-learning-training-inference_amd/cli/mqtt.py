@@ -42,6 +42,7 @@ def main_broker(argv: Sequence[str]) -> int:
     p.add_argument("--partitions", type=int, default=10, help="partitions of auto-created fake:// topics "
                                                                 "(the reference creates sensor-data with 10)")
     p.add_argument("--duration", type=float, default=None)
+    p.add_argument("--metrics-port", type=int, default=0, help="serve Prometheus /metrics on this port (0 = off)")
     ns = p.parse_args(list(argv))
     from ..kafka import fake_broker
     from ..mqtt import MqttBroker, TopicMapping, load_topic_mappings
@@ -68,6 +69,9 @@ def main_broker(argv: Sequence[str]) -> int:
                    max_qos=ns.max_qos, kafka_config=cfg)
     print(f"MQTT broker listening {b.port} (bridge: {kafka or 'off'}; mappings: "
           f"{[(m.filters, m.kafka_topic) for m in b.mappings]})", flush=True)
+    if ns.metrics_port:
+        from ..obs.metrics import REGISTRY
+        REGISTRY.serve(ns.metrics_port, addr="0.0.0.0")
     stop = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):
         signal.signal(sig, lambda *_: stop.set())
@@ -96,6 +100,8 @@ def main_devsim(argv: Sequence[str]) -> int:
     p.add_argument("--interval", type=float, default=None, help="seconds between a car's messages")
     p.add_argument("--ramp", type=float, default=None)
     p.add_argument("--threads", type=int, default=8)
+    p.add_argument("--agents", type=int, default=1, help="split the fleet over this many simulator processes")
+    p.add_argument("--agent-index", type=int, default=0, help="which share of the fleet this process runs")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--failure-rate", type=float, default=0.01)
     p.add_argument("--user", default="")
@@ -110,8 +116,12 @@ def main_devsim(argv: Sequence[str]) -> int:
         port = int(ps)
     print(f"scenario: {sc.clients} cars x {sc.messages_per_client} msgs @ 1/{sc.interval_s:g}s QoS {sc.qos} "
           f"MQTT {'5' if sc.version == 5 else '3.1.1'} -> {host}:{port}", flush=True)
-    st = simulate(sc, host, port, threads=ns.threads, seed=ns.seed, failure_rate=ns.failure_rate,
-                  username=ns.user, password=ns.password)
+    if not 0 <= ns.agent_index < ns.agents:
+        raise SystemExit("--agent-index must be in [0, --agents)")
+    lo = sc.clients * ns.agent_index // ns.agents
+    hi = sc.clients * (ns.agent_index + 1) // ns.agents
+    st = simulate(sc.scaled(clients=hi - lo), host, port, threads=ns.threads, seed=ns.seed,
+                  failure_rate=ns.failure_rate, username=ns.user, password=ns.password, id_offset=lo)
     st["msgs_per_s"] = st["published"] / max(st["elapsed_s"], 1e-9)
     print(json.dumps(st), flush=True)
     return 0 if st["connect_failed"] == 0 and st["publish_failed"] == 0 else 2

@@ -107,11 +107,14 @@ def main_ksql(argv: Sequence[str]) -> int:
     def flags(p):
         p.add_argument("--window", type=int, default=300)
         p.add_argument("--grace", type=int, default=None)
+        p.add_argument("--follow", action="store_true", help="keep consuming (persistent query) instead of "
+                                                              "stopping at the partition end")
 
     ns = common.parse(argv, usage, ["servers", "source", "target"], add_flags=flags)
     from ..data.ksql import run_events_per_window
     cfg = common.kafka_config(ns.servers, ns.kafka_config)
-    n = run_events_per_window(ns.servers, ns.source, ns.target, ns.window, config=cfg, grace_s=ns.grace)
+    n = run_events_per_window(ns.servers, ns.source, ns.target, ns.window, config=cfg, grace_s=ns.grace,
+                              eof=not ns.follow)
     print(f"{n} window counts produced into '{ns.target}'", flush=True)
     return 0
 

@@ -1199,7 +1199,8 @@ SimStats simulate(const SimConfig& cfg, std::atomic<bool>* stop) {
           std::this_thread::sleep_until(at(base + cfg.ramp_s * i / std::max(1, cfg.clients) + k * cfg.interval_s));
           const std::string name = client_name(cfg, (uint64_t)i);
           try {
-            c->publish(cfg.topic_prefix + name, car_payload_json(cfg, (uint64_t)i, (uint64_t)k, now_ms()), cfg.qos);
+            c->publish(cfg.topic_prefix + name,
+                       car_payload_json(cfg, (uint64_t)(i + cfg.id_offset), (uint64_t)k, now_ms()), cfg.qos);
             published++;
             if (cfg.qos > 0) acked++;
           } catch (const std::exception&) {

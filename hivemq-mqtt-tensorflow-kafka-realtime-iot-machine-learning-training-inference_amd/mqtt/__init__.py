@@ -328,17 +328,19 @@ class Scenario:
 
 
 def simulate(scenario: Scenario, host: Optional[str] = None, port: Optional[int] = None, threads: int = 4,
-             seed: int = 0, failure_rate: float = 0.01, username: str = "", password: str = "") -> Dict[str, float]:
+             seed: int = 0, failure_rate: float = 0.01, username: str = "", password: str = "",
+             id_offset: int = 0) -> Dict[str, float]:
     """Run the fleet: connect every client, publish ``messages_per_client`` car payloads each.
 
     Payloads are JSON objects with the 18 sensor fields + ``failure_occurred`` of the KSQL
     stream ``SENSOR_DATA_S``; each car has a stable operating point plus per-event noise
-    drawn inside the ranges of :data:`streamml.data.cardata.SYNTH_RANGES`.
+    drawn inside the ranges of :data:`streamml.data.cardata.SYNTH_RANGES`.  ``id_offset``
+    numbers this process's cars from there (several simulator agents share one fleet).
     """
     from ..data.cardata import FEATURES, INT_FEATURES, SYNTH_RANGES
     cfg = {
         "host": host or scenario.broker[0], "port": int(port or scenario.broker[1]),
-        "client_prefix": scenario.client_prefix, "id_digits": scenario.id_digits,
+        "client_prefix": scenario.client_prefix, "id_digits": scenario.id_digits, "id_offset": int(id_offset),
         "topic_prefix": scenario.topic_prefix, "clients": scenario.clients,
         "messages_per_client": scenario.messages_per_client, "interval_s": scenario.interval_s,
         "ramp_s": scenario.ramp_s, "qos": scenario.qos, "version": scenario.version, "threads": threads,
