@@ -17,6 +17,7 @@ Commands (reference script in parentheses):
   ksql-avro    <servers> [--source sensor-data] [--target SENSOR_DATA_S_AVRO]   KSQL JSON -> Avro (+ REKEY)
   mqtt-broker  [--port 1883] [--kafka SERVERS] [--kafka-extension kafka-config.yaml]   HiveMQ + Kafka extension
   devsim       run -s scenario.xml [--broker host:port] [--clients N]   HiveMQ device simulator
+  connect      <servers> --config connector.json [--sink-store DIR]   Kafka Connect sinks (MongoDB, GCS Avro)
 """
 from __future__ import annotations
 
@@ -43,6 +44,7 @@ def _commands():
         "ksql-avro": mqtt.main_ksql_avro,
         "mqtt-broker": mqtt.main_broker,
         "devsim": mqtt.main_devsim,
+        "connect": mqtt.main_connect,
     }
 
 

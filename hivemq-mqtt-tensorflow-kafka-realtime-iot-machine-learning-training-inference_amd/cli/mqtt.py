@@ -14,6 +14,10 @@
 
 ``ksql-avro <servers> [--source sensor-data] [--target SENSOR_DATA_S_AVRO] [--rekey ...]``
     KSQL's JSON -> Avro -> PARTITION BY CAR streams (01_installConfluentPlatform.sh:235-249).
+
+``connect <servers> --config connector.json [--sink-store DIR|gs://bucket] [--follow]``
+    The Kafka Connect sinks (infrastructure/kafka-connect/): MongoSinkConnector ->
+    digital-twin document store, GcsSinkConnector -> Avro data lake.
 """
 from __future__ import annotations
 
@@ -143,6 +147,26 @@ def main_ksql_avro(argv: Sequence[str]) -> int:
     cfg = common.kafka_config(ns.servers, ns.kafka_config)
     st = run_json_to_avro(ns.servers, ns.source, ns.target, ns.rekey or None, config=cfg, eof=not ns.follow,
                           idle_timeout_s=ns.idle_timeout)
+    print(json.dumps(st), flush=True)
+    return 0
+
+
+def main_connect(argv: Sequence[str]) -> int:
+    common.print_options(argv)
+    usage = "Usage: connect <servers> --config connector.json [--sink-store DIR|gs://bucket] [--follow]"
+
+    def flags(p):
+        p.add_argument("--config", required=True, help="connector JSON or the ConfigMap that carries it")
+        p.add_argument("--sink-store", default="./connect-sink", help="local root or gs://bucket")
+        p.add_argument("--schema", default="ksql-cardata-v1")
+        p.add_argument("--follow", action="store_true")
+        p.add_argument("--idle-timeout", type=float, default=None)
+
+    ns = common.parse(argv, usage, ["servers"], add_flags=flags)
+    from ..connect import load_connector_config, run_sink
+    cfg = common.kafka_config(ns.servers, ns.kafka_config)
+    st = run_sink(load_connector_config(ns.config), ns.servers, ns.sink_store, eof=not ns.follow, kafka_config=cfg,
+                  schema=ns.schema, idle_timeout_s=ns.idle_timeout)
     print(json.dumps(st), flush=True)
     return 0
 
