@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch-per-gpu", type=int, default=1 << 23)
     p.add_argument("--dataset-rows", type=int, default=1 << 25, help="rows resident per GPU (ring)")
-    p.add_argument("--max-blocks", type=int, default=0, help="0 = resident capacity (3 blocks per CU)")
+    p.add_argument("--max-blocks", type=int, default=0, help="0 = two rounds of the resident capacity")
     p.add_argument("--infer-events", type=int, default=1000)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--dump-params", default=None,

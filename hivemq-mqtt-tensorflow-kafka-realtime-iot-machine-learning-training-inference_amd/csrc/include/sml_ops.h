@@ -7,6 +7,7 @@ namespace sml {
 
 // ---- dense autoencoder (ae_fused.hip) ----
 int ae_nslot();
+int ae_train_blocks_per_cu();  // resident 256-thread workgroups per CU of the selected variant
 int ae_nparam();
 int ae_waves_per_block();
 int ae_train_grid(int64_t n, int max_blocks);

@@ -38,11 +38,10 @@ constexpr int WAVES = 4;  // waves per workgroup
 constexpr int OFF1 = 0, OFF2 = 512, OFF3 = 768, OFF4 = 1024;
 constexpr int NPARAM = 1536;
 constexpr int NSLOT = 1540;
-// LDS-DMA input ring (PF > 0 variants): per wave RING_BYTES after the slab area.
+// LDS-DMA input ring (PF > 0 variants): per wave ring_bytes<OCC>() after the slab area.
 // A 16-row tile of contiguous rows is 64*D bytes (D = 18: 1152 B), moved by two
 // global_load_lds_dwordx4 (64 lanes x 16 B + (4D - 64) lanes x 16 B).
 constexpr int SLAB_BYTES = WAVES * NSLOT * 4;  // 24640, a multiple of 16
-constexpr int RING_BYTES = 6144;
 
 struct AEArgs {
   const float* x;        // [n, ld] raw or normalised rows
@@ -78,7 +77,6 @@ struct Frags {  // register-resident operands for one launch
   bf16x4 w1t[2], w2t, w3t, w4t[2];  // forward A operands  (W^T)
   bf16x4 w4[2], w3, w2;             // backward A operands (W)
   f32x4 b1, b2, b3, b4[2];          // biases in C layout
-  f32x4 sc[2], sh[2];               // normaliser in B layout (feature 16s + 4g + j)
 };
 
 __device__ __forceinline__ short bfbits(float v) { return __builtin_bit_cast(short, (__bf16)v); }
@@ -143,14 +141,40 @@ __device__ __forceinline__ void load_frags(const AEArgs& a, int c, int g, Frags&
     for (int t = 0; t < 2; ++t) {
       const int ft = 16 * t + f;
       F.b4[t][i] = ldsel(P, !FOLD && ft < a.D, OFF4 + 15 * 32 + ft);
-      // unconditional loads from a valid address (the params image when there is no
-      // normaliser), selected afterwards
-      const bool has = a.scale != nullptr;
-      const float sv = (has ? a.scale : P)[ft < a.D ? ft : 0];
-      const float hv = (has ? a.shift : P)[ft < a.D ? ft : 0];
-      F.sc[t][i] = ft < a.D ? (has ? sv : 1.0f) : 0.f;
-      F.sh[t][i] = (ft < a.D && has) ? hv : 0.f;
     }
+  }
+}
+
+// fused normalize_fn (cardata-v3.py:78-168) as a per-feature affine: feature f of the
+// raw row -> x * scale[f] + shift[f]; features >= D get scale 0 (and so read as 0)
+__device__ __forceinline__ float norm_scale(const AEArgs& a, int f) {
+  if (f >= a.D) return 0.f;
+  return a.scale ? a.scale[f] : 1.0f;
+}
+__device__ __forceinline__ float norm_shift(const AEArgs& a, int f) {
+  return (f < a.D && a.scale) ? a.shift[f] : 0.f;
+}
+
+// register copy of the normaliser in the B layout (lane (c, g): features 16s + 4g + j)
+__device__ __forceinline__ void norm_regs(const AEArgs& a, int g, f32x4 sc[2], f32x4 sh[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sc[s][j] = norm_scale(a, 16 * s + 4 * g + j);
+      sh[s][j] = norm_shift(a, 16 * s + 4 * g + j);
+    }
+}
+
+// The train kernel keeps the normaliser in LDS (NORM_BYTES: scale[32] then shift[32])
+// and re-reads it per tile with four 16-byte ds_reads instead of pinning 16 VGPRs.
+constexpr int NORM_BYTES = 256;
+__device__ __forceinline__ void norm_lds(const char* norm, int g, f32x4 sc[2], f32x4 sh[2]) {
+  typedef __attribute__((address_space(3))) const f32x4 lds_f4;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    sc[s] = *(lds_f4*)(norm + (16 * s + 4 * g) * 4);
+    sh[s] = *(lds_f4*)(norm + 128 + (16 * s + 4 * g) * 4);
   }
 }
 
@@ -280,16 +304,31 @@ __device__ __forceinline__ int row_argmax(const f32x4 v[2], int D, int g) {
 
 // Branch-free argmax over the 8 features a lane holds + its 3 partner lanes
 // (row r = lane & 15 is spread over lane groups g = 0..3).  Ties -> lowest index
-// (tf.argmax).  `pn` is 0 for real features and -inf for padded ones.
-__device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], const f32x4 pn[2], int g, int lane) {
+// (tf.argmax).  Features >= D are masked to -inf (lane-uniform compares, hoisted).
+// max of three floats in one v_max3_f32.  Inline asm on purpose: fmaxf() makes the
+// compiler canonicalise operands it cannot prove canonical (the MFMA/med3 outputs)
+// with an extra v_max each; the data here is finite, so plain IEEE max3 is exact.
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Branch-free argmax over the 8 features a lane holds + its 3 partner lanes
+// (row r = lane & 15 is spread over lane groups g = 0..3).  Ties -> lowest index
+// (tf.argmax).  Features >= D are masked to -inf; LOW_REAL (D >= 16, all ring
+// variants) skips the mask on the first 16 features, which are then always real.
+template <bool LOW_REAL>
+__device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], int D, int g, int lane) {
   float vv[8];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) vv[4 * t + i] = v[t][i] + pn[t][i];
-  float m = fmaxf(fmaxf(fmaxf(vv[0], vv[1]), fmaxf(vv[2], vv[3])), fmaxf(fmaxf(vv[4], vv[5]), fmaxf(vv[6], vv[7])));
-  m = fmaxf(m, xor16(m, lane));
-  m = fmaxf(m, xor32(m, lane));
+    for (int i = 0; i < 4; ++i)
+      vv[4 * t + i] = ((t == 0 && LOW_REAL) || (16 * t + 4 * g + i) < D) ? v[t][i] : -INFINITY;
+  float m = max3f(max3f(vv[0], vv[1], vv[2]), max3f(vv[3], vv[4], vv[5]), max3f(vv[6], vv[7], vv[7]));
+  m = max3f(m, xor16(m, lane), m);
+  m = max3f(m, xor32(m, lane), m);
   int idx = 64;
 #pragma unroll
   for (int q = 7; q >= 0; --q) {
@@ -305,9 +344,9 @@ __device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], const f32x4 pn[
 // FAST (zero-preserving activations): no per-feature masks -- padded features
 // stay exactly 0 because their weights are 0 and act(0) = 0; only the bias slot
 // is set.  TAIL: rows beyond n are masked (only the last tile of a launch).
-template <int PACK, bool FAST, bool TAIL>
+template <int PACK, bool FAST, bool TAIL, bool LOW_REAL = false>
 __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char* scr, int c, int g, int lane,
-                                           bool valid, const f32x4 xf[2], const f32x4 pn[2], float pad1,
+                                           bool valid, const f32x4 xf[2], float pad1,
                                            f32x4 acc1[2], f32x4& acc2, f32x4& acc3, f32x4 acc4[2], float& sq,
                                            float& ab, float& corr, float& rows) {
   const int a1 = act_of<PACK>(a, 0), a2 = act_of<PACK>(a, 1), a3 = act_of<PACK>(a, 2), a4 = act_of<PACK>(a, 3);
@@ -364,8 +403,8 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
       dz4[t][i] = act_grad(a4, y[t][i], two_over_d * e);
     }
   if (a.want_acc) {
-    const int iy = row_argmax_fast(y, pn, g, lane);
-    const int ix = row_argmax_fast(xf, pn, g, lane);
+    const int iy = row_argmax_fast<LOW_REAL>(y, a.D, g, lane);
+    const int ix = row_argmax_fast<LOW_REAL>(xf, a.D, g, lane);
     corr += (g == 0 && vm && iy == ix) ? 1.f : 0.f;
   }
   rows += (g == 0 && vm) ? 1.f : 0.f;
@@ -428,30 +467,37 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
 // by LDS-DMA (no VGPRs held for the prefetch, PF-1 tiles in flight per wave);
 // requires contiguous rows (ld == D), 17 <= D <= 31 and D even.  PF = 0: one tile
 // of register prefetch (any ld / D).
-template <int PACK, bool VEC, int PF>
-__global__ __launch_bounds__(WAVES * 64, 3) void ae_train_kernel(AEArgs a) {
+// OCC = waves per SIMD the variant is built for: 3 (168-VGPR budget, 6 KB ring per
+// wave) or 4 (128-VGPR budget, 3968-B ring per wave so four workgroups fit in LDS).
+template <int OCC>
+constexpr int ring_bytes() { return OCC >= 4 ? 3968 : 6144; }
+
+template <int PACK, bool VEC, int PF, int OCC>
+__global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   constexpr bool FAST = zero_preserving<PACK>();
+  constexpr int RING = ring_bytes<OCC>();
   static_assert(WAVES * 10 * 512 <= SLAB_BYTES, "transpose scratch must fit in the slab buffer");
-  static_assert(PF * 64 * 17 <= RING_BYTES, "ring slots must fit the smallest ring tile");
+  static_assert(PF == 0 || PF * 64 * 17 <= RING, "ring slots must fit the smallest ring tile");
   // one LDS array: per-wave transpose scratch during the tile loop, per-wave
-  // gradient slabs afterwards, then (PF > 0) the per-wave input rings
-  __shared__ __attribute__((aligned(16))) float smem[(SLAB_BYTES + (PF > 0 ? WAVES * RING_BYTES : 0)) / 4];
+  // gradient slabs afterwards | the normaliser | (PF > 0) the per-wave input rings
+  __shared__ __attribute__((aligned(16))) float smem[(SLAB_BYTES + NORM_BYTES + (PF > 0 ? WAVES * RING : 0)) / 4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
   char* scr = reinterpret_cast<char*>(smem) + wid * (10 * 512);
+  const char* norm = reinterpret_cast<const char*>(smem) + SLAB_BYTES;
   if (a.cursor) a.x += a.cursor[0] * a.ld;  // streaming ring consumer (uniform scalar load)
 
   if (a.iter && blockIdx.x == 0 && threadIdx.x == 0) a.iter[0] += 1;
+  if (threadIdx.x < 64) {
+    const int f = threadIdx.x & 31;
+    smem[SLAB_BYTES / 4 + threadIdx.x] = threadIdx.x < 32 ? norm_scale(a, f) : norm_shift(a, f);
+  }
 
   Frags F;
   load_frags<FAST>(a, c, g, F, true);
   const float pad1 = (g == 3) ? 1.0f : 0.0f;
-  f32x4 pn[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pn[t][i] = (16 * t + 4 * g + i) < a.D ? 0.f : -INFINITY;
+  __syncthreads();  // normaliser visible (before any LDS-DMA is in flight)
 
   f32x4 acc1[2], acc2, acc3, acc4[2];
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
@@ -468,7 +514,7 @@ __global__ __launch_bounds__(WAVES * 64, 3) void ae_train_kernel(AEArgs a) {
     const int slotb = 64 * a.D;
     const int nl2 = 4 * a.D - 64;  // lanes of the second 16-B-per-lane DMA (>= 4)
     const int uwid = __builtin_amdgcn_readfirstlane(wid);  // keep the ring bookkeeping scalar
-    const int ring_off = SLAB_BYTES + uwid * RING_BYTES;
+    const int ring_off = SLAB_BYTES + NORM_BYTES + uwid * RING;
     const unsigned ring_lds =
         (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem) + ring_off;
     const char* ring = reinterpret_cast<const char*>(smem) + ring_off;
@@ -492,16 +538,17 @@ __global__ __launch_bounds__(WAVES * 64, 3) void ae_train_kernel(AEArgs a) {
       for (int64_t t = ufirst; t < nfull; t += stride) {
         issue(t + (PF - 1) * stride, wr);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (PF - 1)) : "memory");
-        f32x4 xf[2];
+        f32x4 xf[2], sc[2], sh[2];
         ring_x(a, ring + rd * slotb, c, g, xf);
+        norm_lds(norm, g, sc, sh);
         rd = rd + 1 == PF ? 0 : rd + 1;
         wr = wr + 1 == PF ? 0 : wr + 1;
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xf[s][j], F.sc[s][j], F.sh[s][j]);
-        train_tile<PACK, FAST, false>(a, F, scr, c, g, lane, true, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr,
-                                      rows);
+          for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xf[s][j], sc[s][j], sh[s][j]);
+        train_tile<PACK, FAST, false, true>(a, F, scr, c, g, lane, true, xf, pad1, acc1, acc2, acc3, acc4, sq, ab,
+                                            corr, rows);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the ring is retired
     }
@@ -509,13 +556,14 @@ __global__ __launch_bounds__(WAVES * 64, 3) void ae_train_kernel(AEArgs a) {
     f32x4 xnext[2];
     if (first < nfull) fetch_x<VEC>(a, first * 16 + c, g, xnext);
     for (int64_t t = first; t < nfull; t += stride) {
-      f32x4 xf[2];
+      f32x4 xf[2], sc[2], sh[2];
+      norm_lds(norm, g, sc, sh);
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xnext[s][j], F.sc[s][j], F.sh[s][j]);
+        for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xnext[s][j], sc[s][j], sh[s][j]);
       if (t + stride < nfull) fetch_x<VEC>(a, (t + stride) * 16 + c, g, xnext);  // prefetch
-      train_tile<PACK, FAST, false>(a, F, scr, c, g, lane, true, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr,
+      train_tile<PACK, FAST, false>(a, F, scr, c, g, lane, true, xf, pad1, acc1, acc2, acc3, acc4, sq, ab, corr,
                                     rows);
     }
   }
@@ -523,13 +571,14 @@ __global__ __launch_bounds__(WAVES * 64, 3) void ae_train_kernel(AEArgs a) {
   if ((a.n & 15) && first == nfull % stride) {
     const int64_t r = nfull * 16 + c;
     const bool valid = r < a.n;
-    f32x4 xf[2];
+    f32x4 xf[2], sc[2], sh[2];
     fetch_x<VEC>(a, r, g, xf);
+    norm_lds(norm, g, sc, sh);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xf[s][j] = valid ? fmaf(xf[s][j], F.sc[s][j], F.sh[s][j]) : 0.f;
-    train_tile<PACK, FAST, true>(a, F, scr, c, g, lane, valid, xf, pn, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
+      for (int j = 0; j < 4; ++j) xf[s][j] = valid ? fmaf(xf[s][j], sc[s][j], sh[s][j]) : 0.f;
+    train_tile<PACK, FAST, true>(a, F, scr, c, g, lane, valid, xf, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
   }
 
   // per-wave slab in LDS (every slot written exactly once per wave)
@@ -591,6 +640,8 @@ __global__ __launch_bounds__(WAVES * 64) void ae_forward_kernel(FwdArgs fa) {
   const int c = lane & 15, g = lane >> 4;
   Frags F;
   load_frags<false>(a, c, g, F, false);
+  f32x4 nsc[2], nsh[2];
+  norm_regs(a, g, nsc, nsh);
   const int64_t ntiles = (a.n + 15) >> 4;
   const int64_t stride = (int64_t)gridDim.x * WAVES;
   const float inv_d = 1.0f / (float)a.D;
@@ -602,7 +653,7 @@ __global__ __launch_bounds__(WAVES * 64) void ae_forward_kernel(FwdArgs fa) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xf[s][j], F.sc[s][j], F.sh[s][j]);
+      for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xf[s][j], nsc[s][j], nsh[s][j]);
     bf16x4 xb0, xb1, h1b, h2b, h3b;
     f32x4 h1, h2, h3, y[2];
     forward_tile<PACK>(a, F, g, xf, xb0, xb1, h1, h2, h3, h1b, h2b, h3b, y);
@@ -723,6 +774,18 @@ static bool ring_pf_enabled() {
   return on;
 }
 
+// SML_AE_OCC=3|4 picks the waves-per-SIMD variant of the ring kernel.  Default 4:
+// 128 VGPRs, 4 workgroups/CU; on MI355X 27.1 vs 25.7 G rows/s at B = 8M
+// (profiles/r01_v4/sweep_occ*.log).
+static int train_occupancy() {
+  static const int occ = [] {
+    const char* e = getenv("SML_AE_OCC");
+    return (e && e[0] == '3') ? 3 : 4;
+  }();
+  return occ;
+}
+int ae_train_blocks_per_cu() { return train_occupancy(); }
+
 int ae_nslot() { return NSLOT; }
 int ae_nparam() { return NPARAM; }
 int ae_waves_per_block() { return WAVES; }
@@ -753,13 +816,19 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
                        (cursor == nullptr || ((n * ld) & 3) == 0) && ring_pf_enabled();
   const int pack = acts[0] | (acts[1] << 2) | (acts[2] << 4) | (acts[3] << 6);
   const dim3 gd(grid), bd(WAVES * 64);
+  const int occ = train_occupancy();
   if (pack == PACK_REF) {
-    if (ring_ok && 5 * 64 * D <= RING_BYTES) hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 5>), gd, bd, 0, stream, a);
-    else if (ring_ok) hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3>), gd, bd, 0, stream, a);
-    else if (vec) hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 0>), gd, bd, 0, stream, a);
-    else hipLaunchKernelGGL((ae_train_kernel<PACK_REF, false, 0>), gd, bd, 0, stream, a);
+    if (ring_ok && occ == 4 && 3 * 64 * D <= ring_bytes<4>())
+      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4>), gd, bd, 0, stream, a);
+    else if (ring_ok && occ == 4)
+      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 2, 4>), gd, bd, 0, stream, a);
+    else if (ring_ok && 5 * 64 * D <= ring_bytes<3>())
+      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 5, 3>), gd, bd, 0, stream, a);
+    else if (ring_ok) hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 3>), gd, bd, 0, stream, a);
+    else if (vec) hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 0, 3>), gd, bd, 0, stream, a);
+    else hipLaunchKernelGGL((ae_train_kernel<PACK_REF, false, 0, 3>), gd, bd, 0, stream, a);
   } else {
-    hipLaunchKernelGGL((ae_train_kernel<PACK_DYN, false, 0>), gd, bd, 0, stream, a);
+    hipLaunchKernelGGL((ae_train_kernel<PACK_DYN, false, 0, 3>), gd, bd, 0, stream, a);
   }
   return hipGetLastError();
 }

@@ -490,6 +490,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("partials"), py::arg("iter"),
         py::arg("dims"), py::arg("acts"), py::arg("l1"), py::arg("want_acc"), py::arg("max_blocks"),
         py::arg("n_rows") = -1, py::arg("cursor") = py::none());
+  m.def("ae_train_blocks_per_cu", &sml::ae_train_blocks_per_cu,
+        "workgroups per CU the selected AE train-kernel variant keeps resident (SML_AE_OCC)");
   m.def("ae_train_grid", &sml::ae_train_grid, "grid size the AE train kernel uses", py::arg("n"),
         py::arg("max_blocks"));
   m.def("reduce_adam", &reduce_adam, "slab reduction + optional Adam", py::arg("partials"), py::arg("G"),

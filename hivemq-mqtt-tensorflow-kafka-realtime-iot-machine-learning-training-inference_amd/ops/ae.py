@@ -29,20 +29,21 @@ NSLOT = 1540
 LAYOUT = [(0, 32, 16, 31), (512, 16, 16, 15), (768, 16, 16, 15), (1024, 16, 32, 15)]
 
 RA_WRITE_GRAD, RA_ADAM, RA_METRICS, RA_ADVANCE = 1, 2, 4, 8
-# ae_train_kernel: 168 VGPRs -> 3 waves/SIMD -> 3 four-wave workgroups per CU.  A grid
-# of exactly the resident capacity gives every wave the same tile count with no
-# second dispatch round (sweep on MI355X, B = 4M rows: 768 blocks 176.6 us vs
-# 1024 blocks 180.9 us; profiles/r01_v4/ae_sweep.json).
-TRAIN_BLOCKS_PER_CU = 3
+# ae_train_kernel keeps 3 (<= 168 VGPRs) or 4 (<= 128 VGPRs, SML_AE_OCC=4) four-wave
+# workgroups resident per CU.  A grid of exactly the resident capacity gives every wave
+# the same tile count with no second dispatch round (sweep on MI355X, B = 4M rows:
+# 768 blocks 176.6 us vs 1024 blocks 180.9 us at 3/CU; profiles/r01_v4/).
 
 
 def default_train_blocks(device) -> int:
-    """Resident-capacity grid for the fused train kernel on ``device``."""
+    """Two rounds of the resident capacity: each workgroup's share halves, so CUs that
+    finish early pick up second-round workgroups (B = 8M rows: 2048 blocks 304 us vs
+    1024 blocks 310 us at 4/CU; profiles/r01_v4/sweep_occ4.log)."""
     try:
         cus = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
     except Exception:  # noqa: BLE001 - no device properties (CPU build): MI355X has 256 CUs
         cus = 256
-    return TRAIN_BLOCKS_PER_CU * int(cus)
+    return 2 * int(load_c().ae_train_blocks_per_cu()) * int(cus)
 
 
 @dataclass
