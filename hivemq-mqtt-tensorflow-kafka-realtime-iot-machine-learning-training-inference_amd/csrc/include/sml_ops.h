@@ -38,6 +38,7 @@ bool dense_supported(int K, int N);
 int dense_wgrad_slab(int K, int N);
 int dense_wgrad_grid(int64_t M, int max_blocks);
 int slab_sum_scratch(int G, int S);
+int slab_sum_level_launch(const float* in, int G, int S, float* out, hipStream_t stream);
 hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, float* out, hipStream_t stream);
 hipError_t rowgemm_launch(const void* X, int x_bf16, int64_t M, int K, int64_t ldx, const float* W, const float* bias,
                           int N, int act, void* Y, int y_bf16, int64_t ldy, int max_blocks, hipStream_t stream);

@@ -318,20 +318,30 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
 // (row r = lane & 15 is spread over lane groups g = 0..3).  Ties -> lowest index
 // (tf.argmax).  Features >= D are masked to -inf; LOW_REAL (D >= 16, all ring
 // variants) skips the mask on the first 16 features, which are then always real.
-template <bool LOW_REAL>
+// Feature 16 + 4g + i of the upper half is real for some lane iff 16 + i < D; with a
+// compile-time D (DC > 0) the halves i >= DC - 16 are dropped from every loop.
+template <int DC>
+__device__ __forceinline__ constexpr bool live_hi(int i) { return DC == 0 || 16 + i < DC; }
+
+template <bool LOW_REAL, int DC = 0>
 __device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], int D, int g, int lane) {
   float vv[8];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      vv[4 * t + i] = ((t == 0 && LOW_REAL) || (16 * t + 4 * g + i) < D) ? v[t][i] : -INFINITY;
-  float m = max3f(max3f(vv[0], vv[1], vv[2]), max3f(vv[3], vv[4], vv[5]), max3f(vv[6], vv[7], vv[7]));
+      vv[4 * t + i] = (t == 1 && !live_hi<DC>(i))                          ? -INFINITY
+                      : ((t == 0 && LOW_REAL) || (16 * t + 4 * g + i) < D) ? v[t][i]
+                                                                            : -INFINITY;
+  float m = max3f(max3f(vv[0], vv[1], vv[2]), vv[3], live_hi<DC>(0) ? vv[4] : vv[3]);
+  if (live_hi<DC>(1) || live_hi<DC>(2)) m = max3f(m, live_hi<DC>(1) ? vv[5] : m, live_hi<DC>(2) ? vv[6] : m);
+  if (live_hi<DC>(3)) m = max3f(m, vv[7], m);
   m = max3f(m, xor16(m, lane), m);
   m = max3f(m, xor32(m, lane), m);
   int idx = 64;
 #pragma unroll
   for (int q = 7; q >= 0; --q) {
+    if (q >= 4 && !live_hi<DC>(q - 4)) continue;
     const int f = 16 * (q >> 2) + 4 * g + (q & 3);
     idx = (vv[q] == m) ? f : idx;
   }
@@ -344,7 +354,7 @@ __device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], int D, int g, i
 // FAST (zero-preserving activations): no per-feature masks -- padded features
 // stay exactly 0 because their weights are 0 and act(0) = 0; only the bias slot
 // is set.  TAIL: rows beyond n are masked (only the last tile of a launch).
-template <int PACK, bool FAST, bool TAIL, bool LOW_REAL = false>
+template <int PACK, bool FAST, bool TAIL, bool LOW_REAL = false, int DC = 0>
 __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char* scr, int c, int g, int lane,
                                            bool valid, const f32x4 xf[2], float pad1,
                                            f32x4 acc1[2], f32x4& acc2, f32x4& acc3, f32x4 acc4[2], float& sq,
@@ -384,7 +394,7 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
     for (int t = 0; t < 2; ++t) {
       const f32x4 z4 = mfma16(F.w4t[t], h3b, zero4);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) y[t][i] = act_fwd(a4, z4[i]);
+      for (int i = 0; i < 4; ++i) y[t][i] = (t == 0 || live_hi<DC>(i)) ? act_fwd(a4, z4[i]) : 0.f;
     }
   } else {
     forward_tile<PACK>(a, F, g, xf, xb0, xb1, h1, h2, h3, h1b, h2b, h3b, y);
@@ -396,6 +406,10 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      if (t == 1 && !live_hi<DC>(i)) {  // compile-time padding (no real feature on any lane)
+        dz4[t][i] = 0.f;
+        continue;
+      }
       float e = y[t][i] - xf[t][i];
       if constexpr (!FAST) e = (16 * t + 4 * g + i) < a.D ? e : 0.f;
       if constexpr (TAIL) e = vm ? e : 0.f;
@@ -403,8 +417,8 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
       dz4[t][i] = act_grad(a4, y[t][i], two_over_d * e);
     }
   if (a.want_acc) {
-    const int iy = row_argmax_fast<LOW_REAL>(y, a.D, g, lane);
-    const int ix = row_argmax_fast<LOW_REAL>(xf, a.D, g, lane);
+    const int iy = row_argmax_fast<LOW_REAL, DC>(y, a.D, g, lane);
+    const int ix = row_argmax_fast<LOW_REAL, DC>(xf, a.D, g, lane);
     corr += (g == 0 && vm && iy == ix) ? 1.f : 0.f;
   }
   rows += (g == 0 && vm) ? 1.f : 0.f;
@@ -472,7 +486,7 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
 template <int OCC>
 constexpr int ring_bytes() { return OCC >= 4 ? 3968 : 6144; }
 
-template <int PACK, bool VEC, int PF, int OCC>
+template <int PACK, bool VEC, int PF, int OCC, int DC = 0>
 __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   constexpr bool FAST = zero_preserving<PACK>();
   constexpr int RING = ring_bytes<OCC>();
@@ -546,9 +560,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xf[s][j], sc[s][j], sh[s][j]);
-        train_tile<PACK, FAST, false, true>(a, F, scr, c, g, lane, true, xf, pad1, acc1, acc2, acc3, acc4, sq, ab,
-                                            corr, rows);
+          for (int j = 0; j < 4; ++j) xf[s][j] = (s == 0 || live_hi<DC>(j)) ? fmaf(xf[s][j], sc[s][j], sh[s][j]) : 0.f;
+        train_tile<PACK, FAST, false, true, DC>(a, F, scr, c, g, lane, true, xf, pad1, acc1, acc2, acc3, acc4, sq,
+                                                ab, corr, rows);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the ring is retired
     }
@@ -818,7 +832,9 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
   const dim3 gd(grid), bd(WAVES * 64);
   const int occ = train_occupancy();
   if (pack == PACK_REF) {
-    if (ring_ok && occ == 4 && 3 * 64 * D <= ring_bytes<4>())
+    if (ring_ok && occ == 4 && D == 18)  // the cardata-v1 reference model: D fixed at compile time
+      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18>), gd, bd, 0, stream, a);
+    else if (ring_ok && occ == 4 && 3 * 64 * D <= ring_bytes<4>())
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4>), gd, bd, 0, stream, a);
     else if (ring_ok && occ == 4)
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 2, 4>), gd, bd, 0, stream, a);

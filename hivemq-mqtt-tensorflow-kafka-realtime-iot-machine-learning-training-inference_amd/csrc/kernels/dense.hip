@@ -398,6 +398,14 @@ hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, 
   return hipGetLastError();
 }
 
+// one level: out[gy][S] = sums of chunks of kSlabChunk slabs; returns gy (-1 on bad args)
+int slab_sum_level_launch(const float* in, int G, int S, float* out, hipStream_t stream) {
+  if (S % 4 != 0 || G < 1) return -1;
+  const int gy = (G + kSlabChunk - 1) / kSlabChunk;
+  hipLaunchKernelGGL(slab_sum_kernel, dim3((S / 4 + 63) / 64, gy), dim3(256), 0, stream, in, G, S, out);
+  return gy;
+}
+
 bool dense_supported(int K, int N) {
   const int KT = round_tiles(K), NT = round_tiles(N);
   return K <= 16 * KT && N <= 16 * NT && KT * NT <= 32 && KT <= 8 && NT <= 16 && !(KT >= 4 && NT == 16);

@@ -97,9 +97,24 @@ void reduce_adam(const at::Tensor& partials, int64_t G, int64_t S, int64_t npara
                  const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
                  const c10::optional<at::Tensor>& iter, double lr, double beta1, double beta2, double eps,
                  double gscale, const c10::optional<at::Tensor>& metrics, int64_t flags,
-                 const c10::optional<at::Tensor>& cursor, int64_t cursor_step, int64_t cursor_ring) {
+                 const c10::optional<at::Tensor>& cursor, int64_t cursor_step, int64_t cursor_ring,
+                 const c10::optional<at::Tensor>& scratch) {
   check_dev(partials, "partials", at::kFloat);
   TORCH_CHECK(partials.numel() >= G * S, "partials smaller than G*S");
+  const float* src = partials.data_ptr<float>();
+  if (scratch.has_value() && scratch->defined() && G > 64) {
+    // wide grids: one parallel level of the deterministic slab sum first (G -> ceil(G/32)
+    // slabs over G/32 x S/256 workgroups), so the Adam kernel reads 32x fewer bytes
+    check_dev(*scratch, "scratch", at::kFloat);
+    const int64_t gy = (G + 31) / 32;
+    TORCH_CHECK(scratch->numel() >= gy * S, "reduce scratch too small");
+    c10::hip::HIPGuard guard(partials.device().index());
+    const int got = sml::slab_sum_level_launch(src, (int)G, (int)S, scratch->data_ptr<float>(), cur_stream(partials));
+    TORCH_CHECK(got == gy, "slab_sum_level_launch failed");
+    SML_CHECK_HIP(hipGetLastError());
+    src = scratch->data_ptr<float>();
+    G = gy;
+  }
   if (flags & 2) {
     TORCH_CHECK(params.has_value() && m.has_value() && v.has_value() && iter.has_value(), "adam needs params/m/v/iter");
     TORCH_CHECK(params->numel() >= nparam && m->numel() >= nparam && v->numel() >= nparam, "adam buffers too small");
@@ -109,7 +124,7 @@ void reduce_adam(const at::Tensor& partials, int64_t G, int64_t S, int64_t npara
   if (flags & 4) TORCH_CHECK(metrics.has_value() && metrics->numel() >= S - nparam, "metrics too small");
   c10::hip::HIPGuard guard(partials.device().index());
   const int64_t* iter_ptr = (iter.has_value() && iter->defined()) ? iter->data_ptr<int64_t>() : nullptr;
-  SML_CHECK_HIP(sml::reduce_adam_launch(partials.data_ptr<float>(), (int)G, (int)S, (int)nparam, opt_mut(grad_out),
+  SML_CHECK_HIP(sml::reduce_adam_launch(src, (int)G, (int)S, (int)nparam, opt_mut(grad_out),
                                         opt_mut(params), opt_mut(m), opt_mut(v), iter_ptr, (float)lr, (float)beta1,
                                         (float)beta2, (float)eps, (float)gscale, opt_mut(metrics), (int)flags,
                                         (cursor.has_value() && cursor->defined()) ? cursor->data_ptr<int64_t>() : nullptr,
@@ -498,7 +513,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("S"), py::arg("nparam"), py::arg("grad_out"), py::arg("params"), py::arg("m"), py::arg("v"),
         py::arg("iter"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("gscale"),
         py::arg("metrics"), py::arg("flags"), py::arg("cursor") = py::none(), py::arg("cursor_step") = 0,
-        py::arg("cursor_ring") = 0);
+        py::arg("cursor_ring") = 0, py::arg("scratch") = py::none());
   py::class_<RingPy>(m, "PinnedRing")
       .def(py::init<int, int64_t, int>(), py::arg("slots"), py::arg("slot_bytes"), py::arg("device"))
       .def("fill", &RingPy::fill, py::arg("slot"), py::arg("array"))

@@ -127,6 +127,7 @@ class FusedAE:
         self.v = torch.zeros(NPARAM, device=dev)
         self.iter = torch.zeros(1, dtype=torch.int64, device=dev)
         self.partials = torch.zeros(self.max_blocks * NSLOT, device=dev)
+        self.reduce_scratch = torch.zeros(((self.max_blocks + 31) // 32) * NSLOT, device=dev)
         self.grad = torch.zeros(NSLOT, device=dev)
         self.metrics = torch.zeros(NSLOT - NPARAM, device=dev)   # epoch accumulators
         self.cursor = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -178,7 +179,8 @@ class FusedAE:
         ring = self.ring.size(0) if self.ring is not None else 0
         self.C.reduce_adam(src, int(G), NSLOT, NPARAM, self.grad, self.params, self.m, self.v, self.iter,
                            self.lr, self.beta_1, self.beta_2, self.epsilon, float(gscale), self.metrics, int(flags),
-                           self.cursor, int(self.ring_batch), int(ring))
+                           self.cursor, int(self.ring_batch), int(ring),
+                           self.reduce_scratch if partials is None else None)
 
     # -- streaming ring consumption (device cursor; graph-capturable) ------------
     def attach_ring(self, ring: torch.Tensor, batch: int) -> None:
