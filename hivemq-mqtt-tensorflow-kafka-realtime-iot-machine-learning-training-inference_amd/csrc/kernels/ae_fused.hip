@@ -99,9 +99,15 @@ __device__ __forceinline__ float ldsel(const float* P, bool cond, int idx) {
 
 // FOLD: biases enter the forward MFMAs through the constant-1 input slot
 // (row 31 of L1, row 15 of L2..L4) instead of an fp32 accumulator init.
-template <bool FOLD>
+// PRE: layers 1 and 3 are tanh; their forward weights (and folded biases) are stored
+// pre-multiplied by 2*log2(e), so the MFMA already yields the exp2 argument of
+// tanh(z) = 1 - 2 / (2^(2 log2(e) z) + 1) (one v_mul per activation saved).
+constexpr float kTanhExp2 = 2.8853900817779268f;
+
+template <bool FOLD, bool PRE = false>
 __device__ __forceinline__ void load_frags(const AEArgs& a, int c, int g, Frags& F, bool bwd) {
   const float* P = a.params;
+  const float k1 = PRE ? kTanhExp2 : 1.0f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int k = 4 * g + j;
@@ -110,11 +116,11 @@ __device__ __forceinline__ void load_frags(const AEArgs& a, int c, int g, Frags&
     for (int s = 0; s < 2; ++s) {
       const int in = 16 * s + k;
       const bool row_ok = in < a.D || (FOLD && in == 31);
-      F.w1t[s][j] = bfbits(ldsel(P, row_ok && c < a.n1, OFF1 + in * 16 + c));
+      F.w1t[s][j] = bfbits(k1 * ldsel(P, row_ok && c < a.n1, OFF1 + in * 16 + c));
     }
     const bool k15 = FOLD && k == 15;
     F.w2t[j] = bfbits(ldsel(P, (k < a.n1 || k15) && c < a.n2, OFF2 + k * 16 + c));
-    F.w3t[j] = bfbits(ldsel(P, (k < a.n2 || k15) && c < a.n3, OFF3 + k * 16 + c));
+    F.w3t[j] = bfbits(k1 * ldsel(P, (k < a.n2 || k15) && c < a.n3, OFF3 + k * 16 + c));
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int out = 16 * t + c;
@@ -323,6 +329,25 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
 template <int DC>
 __device__ __forceinline__ constexpr bool live_hi(int i) { return DC == 0 || 16 + i < DC; }
 
+// Reductions over the 4 lanes of a row (l, l^16, l^32, l^48) with the gfx950 row
+// swaps: permlane16_swap(a, b) of two copies leaves {rows 0,0,2,2} in one result and
+// {rows 1,1,3,3} in the other, so their max is the xor-16 butterfly with no select;
+// permlane32_swap does the same across halves.
+__device__ __forceinline__ float bfly_max(float m) {
+  const unsigned u = __float_as_uint(m);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  m = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  const unsigned v = __float_as_uint(m);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return max3f(__uint_as_float(r32[0]), __uint_as_float(r32[1]), __uint_as_float(r32[1]));
+}
+__device__ __forceinline__ int bfly_min(int x) {
+  const auto r16 = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+  x = min((int)r16[0], (int)r16[1]);
+  const auto r32 = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+  return min((int)r32[0], (int)r32[1]);
+}
+
 template <bool LOW_REAL, int DC = 0>
 __device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], int D, int g, int lane) {
   float vv[8];
@@ -336,8 +361,7 @@ __device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], int D, int g, i
   float m = max3f(max3f(vv[0], vv[1], vv[2]), vv[3], live_hi<DC>(0) ? vv[4] : vv[3]);
   if (live_hi<DC>(1) || live_hi<DC>(2)) m = max3f(m, live_hi<DC>(1) ? vv[5] : m, live_hi<DC>(2) ? vv[6] : m);
   if (live_hi<DC>(3)) m = max3f(m, vv[7], m);
-  m = max3f(m, xor16(m, lane), m);
-  m = max3f(m, xor32(m, lane), m);
+  m = bfly_max(m);
   int idx = 64;
 #pragma unroll
   for (int q = 7; q >= 0; --q) {
@@ -345,21 +369,30 @@ __device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], int D, int g, i
     const int f = 16 * (q >> 2) + 4 * g + (q & 3);
     idx = (vv[q] == m) ? f : idx;
   }
-  idx = min(idx, xor16i(idx, lane));
-  idx = min(idx, xor32i(idx, lane));
-  return idx;
+  return bfly_min(idx);
 }
 
 // One 16-row tile: forward, loss, metrics, backward, weight-gradient MFMAs.
 // FAST (zero-preserving activations): no per-feature masks -- padded features
 // stay exactly 0 because their weights are 0 and act(0) = 0; only the bias slot
 // is set.  TAIL: rows beyond n are masked (only the last tile of a launch).
+// tanh of an argument already multiplied by 2*log2(e) (see load_frags<., true>)
+__device__ __forceinline__ float tanh_exp2(float z2) {
+  return fmaf(-2.0f, rcp_fast(__builtin_amdgcn_exp2f(z2) + 1.0f), 1.0f);
+}
+
+template <int PACK>
+constexpr bool prescaled_tanh() {
+  return PACK >= 0 && ((PACK & 3) == ACT_TANH) && (((PACK >> 4) & 3) == ACT_TANH) && zero_preserving<PACK>();
+}
+
 template <int PACK, bool FAST, bool TAIL, bool LOW_REAL = false, int DC = 0>
 __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char* scr, int c, int g, int lane,
                                            bool valid, const f32x4 xf[2], float pad1,
                                            f32x4 acc1[2], f32x4& acc2, f32x4& acc3, f32x4 acc4[2], float& sq,
                                            float& ab, float& corr, float& rows) {
   const int a1 = act_of<PACK>(a, 0), a2 = act_of<PACK>(a, 1), a3 = act_of<PACK>(a, 2), a4 = act_of<PACK>(a, 3);
+  constexpr bool PRE = FAST && prescaled_tanh<PACK>();
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const float two_over_d = 2.0f / (float)a.D;
   const bool pad_lane = (g == 3);
@@ -377,7 +410,7 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
     f32x4 z1 = mfma16(F.w1t[0], xb0, zero4);
     z1 = mfma16(F.w1t[1], xb1, z1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) h1[i] = act_fwd(a1, z1[i]);
+    for (int i = 0; i < 4; ++i) h1[i] = PRE ? tanh_exp2(z1[i]) : act_fwd(a1, z1[i]);
     h1[3] += pad1;
     h1b = pack4(h1);
     const f32x4 z2 = mfma16(F.w2t, h1b, zero4);
@@ -387,7 +420,7 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
     h2b = pack4(h2);
     const f32x4 z3 = mfma16(F.w3t, h2b, zero4);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) h3[i] = act_fwd(a3, z3[i]);
+    for (int i = 0; i < 4; ++i) h3[i] = PRE ? tanh_exp2(z3[i]) : act_fwd(a3, z3[i]);
     h3[3] += pad1;
     h3b = pack4(h3);
 #pragma unroll
@@ -509,7 +542,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   }
 
   Frags F;
-  load_frags<FAST>(a, c, g, F, true);
+  load_frags<FAST, FAST && prescaled_tanh<PACK>()>(a, c, g, F, true);
   const float pad1 = (g == 3) ? 1.0f : 0.0f;
   __syncthreads();  // normaliser visible (before any LDS-DMA is in flight)
 
