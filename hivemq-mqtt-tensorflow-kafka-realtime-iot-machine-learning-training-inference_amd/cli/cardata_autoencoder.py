@@ -53,7 +53,8 @@ def _train(ns, servers, cfg, epochs, batch_size, out_path):
                      seed=ns.seed)
     ae.compile(metrics=["accuracy"], loss="mean_squared_error", optimizer="adam")
     ae.summary()
-    training = _stream(ns, servers, cfg).filter_normal()
+    # filter(y == "false") (cardata-v3.py:212): on a GPU the K8 kernel compacts on the device
+    training = _stream(ns, servers, cfg).filter_normal(device=True)
     t0 = time.perf_counter()
     ae.fit(training, epochs=epochs, batch_size=batch_size, steps_per_epoch=ns.take, verbose=2)
     print(f"Training complete ({time.perf_counter() - t0:.2f}s)", flush=True)

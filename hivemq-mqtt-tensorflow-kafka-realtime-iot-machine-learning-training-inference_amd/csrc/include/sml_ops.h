@@ -89,4 +89,10 @@ hipError_t mse_acc_launch(const float* yp, const float* y, int64_t rows, int F, 
 // ---- utilities (util.hip) ----
 hipError_t lane_xor_probe_launch(float* out, hipStream_t stream);
 
+// K8 normalize + label filter + order-preserving compaction (preprocess.hip)
+int filter_blocks(int64_t n);
+hipError_t normalize_filter_launch(const float* x, int64_t n, int64_t ld, int D, const uint8_t* labels, int keep,
+                                   const float* scale, const float* shift, int* counts, float* out,
+                                   int64_t* out_index, int64_t* total, hipStream_t stream);
+
 }  // namespace sml

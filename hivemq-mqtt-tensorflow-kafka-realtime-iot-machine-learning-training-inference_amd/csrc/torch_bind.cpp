@@ -92,6 +92,39 @@ int64_t ae_train_partials(const at::Tensor& x, const c10::optional<at::Tensor>& 
   return grid;
 }
 
+// K8: returns (out [n, D] with the kept rows first, source index [n] (or empty), total [1] int64)
+std::vector<at::Tensor> normalize_filter(const at::Tensor& x, int64_t D, const c10::optional<at::Tensor>& labels,
+                                         int64_t keep, const c10::optional<at::Tensor>& scale,
+                                         const c10::optional<at::Tensor>& shift, bool want_index) {
+  check_dev(x, "x", at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(1) >= D && D >= 1 && D <= 64, "x must be [n, >=D], D<=64");
+  const int64_t n = x.size(0);
+  const uint8_t* lab = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    TORCH_CHECK(labels->is_cuda() && labels->scalar_type() == at::kByte && labels->numel() == n &&
+                    labels->is_contiguous(), "labels must be a uint8 device tensor with one code per row");
+    lab = labels->data_ptr<uint8_t>();
+  }
+  TORCH_CHECK(lab != nullptr || keep < 0, "filtering needs labels");
+  if (scale.has_value() && scale->defined()) {
+    TORCH_CHECK(shift.has_value() && shift->defined() && scale->numel() >= D && shift->numel() >= D,
+                "scale/shift need D entries");
+    check_dev(*scale, "scale", at::kFloat);
+    check_dev(*shift, "shift", at::kFloat);
+  }
+  c10::hip::HIPGuard guard(x.device().index());
+  auto fo = x.options();
+  auto out = at::empty({n, D}, fo);
+  auto idx = want_index ? at::empty({n}, fo.dtype(at::kLong)) : at::empty({0}, fo.dtype(at::kLong));
+  auto total = at::empty({1}, fo.dtype(at::kLong));
+  auto counts = at::empty({std::max(1, sml::filter_blocks(n))}, fo.dtype(at::kInt));
+  SML_CHECK_HIP(sml::normalize_filter_launch(x.data_ptr<float>(), n, x.stride(0), (int)D, lab, (int)keep,
+                                             opt_ptr(scale), opt_ptr(shift), counts.data_ptr<int>(),
+                                             out.data_ptr<float>(), want_index ? idx.data_ptr<int64_t>() : nullptr,
+                                             total.data_ptr<int64_t>(), cur_stream(x)));
+  return {out, idx, total};
+}
+
 void reduce_adam(const at::Tensor& partials, int64_t G, int64_t S, int64_t nparam,
                  const c10::optional<at::Tensor>& grad_out, const c10::optional<at::Tensor>& params,
                  const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
@@ -505,6 +538,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("partials"), py::arg("iter"),
         py::arg("dims"), py::arg("acts"), py::arg("l1"), py::arg("want_acc"), py::arg("max_blocks"),
         py::arg("n_rows") = -1, py::arg("cursor") = py::none());
+  m.def("normalize_filter", &normalize_filter, "K8: normalise + keep rows with label == keep, order-preserving",
+        py::arg("x"), py::arg("D"), py::arg("labels"), py::arg("keep"), py::arg("scale"), py::arg("shift"),
+        py::arg("want_index") = false);
   m.def("ae_train_blocks_per_cu", &sml::ae_train_blocks_per_cu,
         "workgroups per CU the selected AE train-kernel variant keeps resident (SML_AE_OCC)");
   m.def("ae_train_grid", &sml::ae_train_grid, "grid size the AE train kernel uses", py::arg("n"),

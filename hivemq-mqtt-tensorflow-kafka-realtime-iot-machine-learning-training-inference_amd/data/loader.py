@@ -27,8 +27,14 @@ _END = object()
 
 
 class DeviceLoader:
+    """``keep_label``: filter on the device instead of the host -- raw rows AND their
+    label codes go through the ring, K8 ``normalize_filter`` compacts the rows whose
+    label is ``keep_label`` in order, and a device re-batcher emits exactly
+    ``batch_rows`` rows per batch (the reference's ``filter(...)`` then ``batch(B)``,
+    cardata-v3.py:212-218).  Yields ``(rows, None)`` in that mode."""
+
     def __init__(self, stream: Stream, device, max_rows: int, slots: int = 3, prefetch: int = 4,
-                 features: int = 18):
+                 features: int = 18, keep_label: Optional[int] = None, batch_rows: Optional[int] = None):
         self.stream = stream
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -44,6 +50,12 @@ class DeviceLoader:
         self.bufs = [torch.empty((self.max_rows, self.features), dtype=torch.float32, device=self.device)
                      for _ in range(self.slots)]
         self.rows = 0
+        self.keep_label = keep_label
+        self.batch_rows = int(batch_rows or max_rows)
+        if keep_label is not None:
+            self.lab_host = [torch.empty(self.max_rows, dtype=torch.uint8).pin_memory() for _ in range(self.slots)]
+            self.lab_dev = [torch.empty(self.max_rows, dtype=torch.uint8, device=self.device)
+                            for _ in range(self.slots)]
 
     def _producer(self, q: "queue.Queue", stop: threading.Event) -> None:
         try:
@@ -60,7 +72,35 @@ class DeviceLoader:
         finally:
             q.put(_END)
 
-    def __iter__(self) -> Iterator[Tuple[torch.Tensor, Chunk]]:
+    def __iter__(self):
+        if self.keep_label is None:
+            return self._iter_rows()
+        return self._iter_filtered()
+
+    def _iter_filtered(self) -> Iterator[Tuple[torch.Tensor, None]]:
+        """Device filter + exact re-batching (staging buffer of up to 2 batches)."""
+        from ..ops.preprocess import normalize_filter
+        B = self.batch_rows
+        stage = torch.empty((B + self.max_rows, self.features), dtype=torch.float32, device=self.device)
+        have = 0
+        for xb, c in self._iter_rows(with_labels=True):
+            slot = self._last_slot
+            kept, _ = normalize_filter(xb, self.lab_dev[slot][:len(xb)], int(self.keep_label))
+            k = kept.size(0)
+            if k:
+                stage[have:have + k].copy_(kept)
+                have += k
+            while have >= B:
+                out = stage[:B].clone()
+                rest = have - B
+                if rest:
+                    stage[:rest].copy_(stage[B:have].clone())
+                have = rest
+                yield out, None
+        if have:
+            yield stage[:have].clone(), None
+
+    def _iter_rows(self, with_labels: bool = False) -> Iterator[Tuple[torch.Tensor, Chunk]]:
         q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
         stop = threading.Event()
         th = threading.Thread(target=self._producer, args=(q, stop), daemon=True)
@@ -80,6 +120,10 @@ class DeviceLoader:
                 x = np.ascontiguousarray(c.x, dtype=np.float32)
                 self.ring.fill(slot, x)
                 self.ring.submit(slot, self.bufs[slot], n * self.features * 4)
+                if with_labels:
+                    self.lab_host[slot][:n].copy_(torch.from_numpy(np.ascontiguousarray(c.label, np.uint8)))
+                    self.lab_dev[slot][:n].copy_(self.lab_host[slot][:n], non_blocking=True)
+                    self._last_slot = slot
                 if prev is not None:
                     self.ring.release(prev)   # consumer kernels for `prev` are enqueued by now
                 self.ring.wait(slot)

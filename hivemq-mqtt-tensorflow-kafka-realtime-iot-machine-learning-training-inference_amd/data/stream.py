@@ -90,17 +90,24 @@ class Stream:
     def map(self, fn: Callable[[Chunk], Chunk]) -> "Stream":
         return Stream(lambda: (fn(c) for c in self))
 
-    def filter_label(self, keep: int = LABEL_FALSE) -> "Stream":
-        """``filter(lambda x, y: y == "false")`` (cardata-v3.py:212)."""
+    def filter_label(self, keep: int = LABEL_FALSE, device: bool = False) -> "Stream":
+        """``filter(lambda x, y: y == "false")`` (cardata-v3.py:212).
+
+        ``device=True`` marks the filter as deferrable: host iteration still filters
+        here, but a GPU consumer (``DeviceLoader`` via ``Autoencoder.fit``) ships the
+        unfiltered rows + labels and compacts them with the K8 HIP kernel instead."""
         def gen():
             for c in self:
                 m = c.label == keep
                 if m.any():
                     yield c.select(m)
-        return Stream(gen)
+        out = Stream(gen)
+        if device:
+            out.device_filter = (self, int(keep))
+        return out
 
-    def filter_normal(self) -> "Stream":
-        return self.filter_label(LABEL_FALSE)
+    def filter_normal(self, device: bool = False) -> "Stream":
+        return self.filter_label(LABEL_FALSE, device=device)
 
     def normalize(self) -> "Stream":
         """Host-side ``normalize_fn`` (CPU path / oracles only)."""

@@ -260,6 +260,16 @@ class Autoencoder:
 
     def _stream_batches(self, stream, batch_size: int):
         """Yield device (or CPU) batches of raw rows from a Stream."""
+        deferred = getattr(stream, "device_filter", None)
+        if deferred is not None and self.device.type == "cuda":
+            # K8 on the device: unfiltered rows + labels through the ring, compaction
+            # and exact re-batching on the GPU (same batches as filter -> batch(B))
+            from ..data.loader import DeviceLoader
+            parent, keep = deferred
+            for xb, _ in DeviceLoader(parent.batch(batch_size), self.device, max_rows=batch_size,
+                                      features=self.spec.input_dim, keep_label=keep, batch_rows=batch_size):
+                yield xb
+            return
         st = stream.batch(batch_size)
         if self.device.type == "cuda":
             from ..data.loader import DeviceLoader
