@@ -59,7 +59,7 @@ struct FusedFwdArgs {
   const float* h0;     // [B, U] or null
   const float* c0;     // [B, U] or null
   float* hseq;         // [B, T, U]
-  float* cseq;         // [B, T, U]
+  __bf16* cseq;        // [B, T, U]   cell state, bf16 (read only by the backward kernel)
   __bf16* gates;       // [B, T, 4U]  post-activation i, f, c~, o
   int64_t B;
   int T, IN, act;
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
         *reinterpret_cast<bf16x4*>(a.gates + bg + U + off) = pack4(gf);
         *reinterpret_cast<bf16x4*>(a.gates + bg + 2 * U + off) = pack4(gc);
         *reinterpret_cast<bf16x4*>(a.gates + bg + 3 * U + off) = pack4(go);
-        *reinterpret_cast<f32x4*>(a.cseq + bu + off) = cs[b];
+        *reinterpret_cast<bf16x4*>(a.cseq + bu + off) = pack4(cs[b]);
         *reinterpret_cast<f32x4*>(a.hseq + bu + off) = h[b];
       }
       hb[b] = pack4(h[b]);
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
 struct FusedBwdArgs {
   const float* dh;     // [B, T, U]  gradient w.r.t. the h sequence
   const __bf16* gates; // [B, T, 4U]
-  const float* cseq;   // [B, T, U]
+  const __bf16* cseq;  // [B, T, U]
   const float* hseq;   // [B, T, U]
   const float* x;      // [B, T, IN]
   const float* h0;     // [B, U] or null
@@ -182,7 +182,7 @@ struct FusedBwdArgs {
   float* dx;           // [B, T, IN] or null
   float* dh0;          // [B, U] or null
   float* dc0;          // [B, U] or null
-  float* partials;     // [nwaves, S]: dW^T [4U][16KT] | dU^T [4U][U] | db [4U]
+  float* partials;     // [nblocks, S]: dW^T [4U][16KT] | dU^T [4U][U] | db [4U] (one slab per workgroup)
   int64_t B;
   int T, IN, act;
 };
@@ -193,16 +193,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   constexpr int LDW = 16 * KT;
   constexpr int S = G4 * (LDW + U + 1);
   __shared__ __attribute__((aligned(16))) char scratch[WAVES][MT * 512];
+  __shared__ __attribute__((aligned(16))) float slab[S];   // the workgroup's combined weight-gradient slab
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int w = threadIdx.x >> 6;
   const int64_t wave_id = (int64_t)blockIdx.x * WAVES + w;
   const int64_t s0 = wave_id * 16;
-  if (s0 >= a.B) return;
+  const bool active = s0 < a.B;  // waves past B contribute zeros (they still join the slab barriers)
   const int64_t seq = s0 + c;
   const bool valid = seq < a.B;
   const int64_t sq = valid ? seq : a.B - 1;
   const int IN = a.IN, T = a.T;
   char* scr = scratch[w];
+  for (int i = threadIdx.x; i < S; i += WAVES * 64) slab[i] = 0.f;
 
   // A fragments: U[m = unit][k = gate] (for dh), W[m = feature][k = gate] (for dX)
   bf16x4 uf[UB][MT];
@@ -245,9 +247,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 
   // per-step operands; "C layout" ones indexed by this lane's sequence, the
   // weight-gradient B operands by rows (sequences) s0 + 4g + j
+  // c_t is carried from the previous (later) step's c_{t-1} load: every c is read once
   struct Step {
     bf16x4 gi[UB], gf[UB], gc[UB], go[UB];
-    f32x4 ct[UB], cprev[UB], dho[UB];
+    bf16x4 cprev[UB];
+    f32x4 dho[UB];
     f32x4 hprev[UB];   // B[k = seq 4g + j][n = unit 16kb + c]
     f32x4 xt[KT];      // B[k = seq 4g + j][n = feature 16kt + c]
   };
@@ -261,10 +265,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       st.gf[b] = ld_bf16x4(a.gates + bg + U + off);
       st.gc[b] = ld_bf16x4(a.gates + bg + 2 * U + off);
       st.go[b] = ld_bf16x4(a.gates + bg + 3 * U + off);
-      st.ct[b] = *reinterpret_cast<const f32x4*>(a.cseq + bu + off);
-      if (t > 0) st.cprev[b] = *reinterpret_cast<const f32x4*>(a.cseq + bu - U + off);
-      else if (a.c0) st.cprev[b] = *reinterpret_cast<const f32x4*>(a.c0 + sq * U + off);
-      else st.cprev[b] = zero4;
+      if (t > 0) st.cprev[b] = ld_bf16x4(a.cseq + bu - U + off);
+      else if (a.c0) st.cprev[b] = pack4(*reinterpret_cast<const f32x4*>(a.c0 + sq * U + off));
+      else st.cprev[b] = pack4(zero4);
       st.dho[b] = valid ? *reinterpret_cast<const f32x4*>(a.dh + bu + off) : zero4;
     }
 #pragma unroll
@@ -291,11 +294,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   };
 
   Step cur, nxt;
-  load_step(T - 1, nxt);
-  for (int t = T - 1; t >= 0; --t) {
+  f32x4 ctc[UB];   // c_t
+#pragma unroll
+  for (int b = 0; b < UB; ++b) ctc[b] = unpack4(ld_bf16x4(a.cseq + (sq * T + T - 1) * (int64_t)U + 16 * b + 4 * g));
+  if (active) load_step(T - 1, nxt);
+  for (int t = T - 1; t >= 0 && active; --t) {
     cur = nxt;
     if (t > 0) load_step(t - 1, nxt);          // in flight during this step
-    const f32x4* cp = cur.cprev;                // c_{t-1}
+    f32x4 cp[UB];                               // c_{t-1}
+#pragma unroll
+    for (int b = 0; b < UB; ++b) cp[b] = unpack4(cur.cprev[b]);
     f32x4 dzt[MT];
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
@@ -304,7 +312,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float dh = cur.dho[b][i] + dhr[b][i];
-        const float ct = cur.ct[b][i];
+        const float ct = ctc[b][i];
         const float ac = act_f(a.act, ct);
         const float dc = dcn[b][i] + dh * go[i] * act_d(a.act, ct, ac);
         dzt[b][i] = dc * gc[i] * gi[i] * (1.f - gi[i]);
@@ -314,6 +322,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
         dzt[3 * UB + b][i] = dh * ac * go[i] * (1.f - go[i]);
         dcn[b][i] = dc * gf[i];
       }
+      ctc[b] = cp[b];   // c_{t-1} is the next (earlier) step's c_t
     }
     if (!valid) {
 #pragma unroll
@@ -366,7 +375,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 
     }
   }
-  if (valid) {
+  if (valid && active) {
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
       const int off = 16 * b + 4 * g;
@@ -384,19 +393,29 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
       accb[mt][i] = v;
     }
-  // this wave's slab (C layout: row m = gate 16mt + 4g + i, column = lane c)
-  float* out = a.partials + wave_id * (int64_t)S;
+  // the 4 waves add their accumulators into the workgroup slab in LDS in a fixed
+  // order (deterministic), then the workgroup writes ONE slab (4x fewer bytes for
+  // the slab reduction than a slab per wave).  C layout: row m = gate 16mt + 4g + i,
+  // column = lane c.
+  for (int turn = 0; turn < WAVES; ++turn) {
+    __syncthreads();
+    if (turn == w && active) {
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = 16 * mt + 4 * g + i;
+        for (int i = 0; i < 4; ++i) {
+          const int m = 16 * mt + 4 * g + i;
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt) out[m * LDW + 16 * kt + c] = accW[mt][kt][i];
+          for (int kt = 0; kt < KT; ++kt) slab[m * LDW + 16 * kt + c] += accW[mt][kt][i];
 #pragma unroll
-      for (int kb = 0; kb < UB; ++kb) out[G4 * LDW + m * U + 16 * kb + c] = accU[mt][kb][i];
-      if (c == 0) out[G4 * LDW + G4 * U + m] = accb[mt][i];
+          for (int kb = 0; kb < UB; ++kb) slab[G4 * LDW + m * U + 16 * kb + c] += accU[mt][kb][i];
+          if (c == 0) slab[G4 * LDW + G4 * U + m] += accb[mt][i];
+        }
     }
+  }
+  __syncthreads();
+  float* out = a.partials + (int64_t)blockIdx.x * S;
+  for (int i = threadIdx.x; i < S; i += WAVES * 64) out[i] = slab[i];
 }
 
 template <int U, int KT>
@@ -442,19 +461,21 @@ int lstm_fused_slab(int U, int IN) {
 }
 
 int lstm_fused_waves(int64_t B) { return (int)(((B + 16 * WAVES - 1) / (16 * WAVES)) * WAVES); }
+int lstm_fused_slabs(int64_t B) { return (int)((B + 16 * WAVES - 1) / (16 * WAVES)); }
 
 hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw, const float* b, const float* h0,
-                                 const float* c0, float* hseq, float* cseq, void* gates_bf16, int64_t B, int T,
+                                 const float* c0, float* hseq, void* cseq_bf16, void* gates_bf16, int64_t B, int T,
                                  int IN, int U, int act, hipStream_t stream) {
-  FusedFwdArgs a{x, W, Uw, b, h0, c0, hseq, cseq, (__bf16*)gates_bf16, B, T, IN, act};
+  FusedFwdArgs a{x, W, Uw, b, h0, c0, hseq, (__bf16*)cseq_bf16, (__bf16*)gates_bf16, B, T, IN, act};
   return dispatch(U, IN, [&](auto u, auto k) { return launch_fwd<decltype(u)::value, decltype(k)::value>(a, stream); });
 }
 
-hipError_t lstm_fused_bwd_launch(const float* dh, const void* gates_bf16, const float* cseq, const float* hseq,
+hipError_t lstm_fused_bwd_launch(const float* dh, const void* gates_bf16, const void* cseq_bf16, const float* hseq,
                                  const float* x, const float* h0, const float* c0, const float* W, const float* Uw,
                                  float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
                                  int act, hipStream_t stream) {
-  FusedBwdArgs a{dh, (const __bf16*)gates_bf16, cseq, hseq, x, h0, c0, W, Uw, dx, dh0, dc0, partials, B, T, IN, act};
+  FusedBwdArgs a{dh,       (const __bf16*)gates_bf16, (const __bf16*)cseq_bf16, hseq, x, h0, c0, W, Uw, dx, dh0, dc0,
+                 partials, B,  T,  IN, act};
   return dispatch(U, IN, [&](auto u, auto k) { return launch_bwd<decltype(u)::value, decltype(k)::value>(a, stream); });
 }
 

@@ -343,11 +343,11 @@ std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W,
   if (c0.has_value()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * U, "c0 must be [B, U]");
   c10::hip::HIPGuard guard(x.device().index());
   auto h = at::empty({B, T, U}, x.options());
-  auto c = at::empty({B, T, U}, x.options());
+  auto c = at::empty({B, T, U}, x.options().dtype(at::kBFloat16));   // cell state: saved for BPTT only
   auto gt = at::empty({B, T, 4 * U}, x.options().dtype(at::kBFloat16));
   SML_CHECK_HIP(sml::lstm_fused_fwd_launch(x.data_ptr<float>(), W.data_ptr<float>(), Uw.data_ptr<float>(),
                                            b.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0), h.data_ptr<float>(),
-                                           c.data_ptr<float>(), gt.data_ptr(), B, (int)T, (int)IN, (int)U, (int)act,
+                                           c.data_ptr(), gt.data_ptr(), B, (int)T, (int)IN, (int)U, (int)act,
                                            cur_stream(x)));
   return {h, c, gt};
 }
@@ -359,7 +359,7 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& g
                                        const at::Tensor& W, const at::Tensor& Uw, int64_t act, bool want_dx,
                                        bool want_state_grads) {
   check_dev(dh, "dh", at::kFloat);
-  check_dev(cseq, "c", at::kFloat);
+  check_dev(cseq, "c", at::kBFloat16);
   check_dev(hseq, "h", at::kFloat);
   check_dev(x, "x", at::kFloat);
   check_dev(W, "W", at::kFloat);
@@ -380,13 +380,13 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& g
     dc0 = at::empty({B, U}, opts);
   }
   const int S = sml::lstm_fused_slab((int)U, (int)IN);
-  const int G = sml::lstm_fused_waves(B);
-  auto partials = at::zeros({G, S}, opts);   // waves past B leave their slab zero
+  const int G = sml::lstm_fused_slabs(B);
+  auto partials = at::empty({G, S}, opts);   // every workgroup writes its slab (idle waves add nothing)
   auto out = at::empty({S}, opts);
   auto scratch = at::empty({std::max(1, sml::slab_sum_scratch(G, S))}, opts);
   auto st = cur_stream(x);
   SML_CHECK_HIP(sml::lstm_fused_bwd_launch(
-      dh.data_ptr<float>(), gates.data_ptr(), cseq.data_ptr<float>(), hseq.data_ptr<float>(), x.data_ptr<float>(),
+      dh.data_ptr<float>(), gates.data_ptr(), cseq.data_ptr(), hseq.data_ptr<float>(), x.data_ptr<float>(),
       opt_ptr(h0), opt_ptr(c0), W.data_ptr<float>(), Uw.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
       want_state_grads ? dh0.data_ptr<float>() : nullptr, want_state_grads ? dc0.data_ptr<float>() : nullptr,
       partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U, (int)act, st));
