@@ -56,7 +56,7 @@ hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw
 hipError_t lstm_fused_bwd_launch(const float* dh, const void* gates_bf16, const void* cseq_bf16, const float* hseq,
                                  const float* x, const float* h0, const float* c0, const float* W, const float* Uw,
                                  float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
-                                 int act, hipStream_t stream);
+                                 int act, int dh_last_only, hipStream_t stream);
 
 // ---- persistent per-event scorer (ae_serve.hip); structures live in host-mapped memory ----
 struct alignas(128) ServeCtl {

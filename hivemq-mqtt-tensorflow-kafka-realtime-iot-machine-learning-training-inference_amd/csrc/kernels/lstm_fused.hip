@@ -170,7 +170,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
 }
 
 struct FusedBwdArgs {
-  const float* dh;     // [B, T, U]  gradient w.r.t. the h sequence
+  const float* dh;     // [B, T, U]  gradient w.r.t. the h sequence ([B, U] of h_T when dh_last_only)
   const __bf16* gates; // [B, T, 4U]
   const __bf16* cseq;  // [B, T, U]
   const float* hseq;   // [B, T, U]
@@ -185,6 +185,7 @@ struct FusedBwdArgs {
   float* partials;     // [nblocks, S]: dW^T [4U][16KT] | dU^T [4U][U] | db [4U] (one slab per workgroup)
   int64_t B;
   int T, IN, act;
+  int dh_last_only;    // return_sequences=False: only h_T received a gradient (no [B, T, U] zeros read)
 };
 
 template <int U, int KT>
@@ -268,7 +269,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       if (t > 0) st.cprev[b] = ld_bf16x4(a.cseq + bu - U + off);
       else if (a.c0) st.cprev[b] = pack4(*reinterpret_cast<const f32x4*>(a.c0 + sq * U + off));
       else st.cprev[b] = pack4(zero4);
-      st.dho[b] = valid ? *reinterpret_cast<const f32x4*>(a.dh + bu + off) : zero4;
+      if (a.dh_last_only) st.dho[b] = (valid && t == T - 1) ? *reinterpret_cast<const f32x4*>(a.dh + sq * U + off) : zero4;
+      else st.dho[b] = valid ? *reinterpret_cast<const f32x4*>(a.dh + bu + off) : zero4;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -473,9 +475,9 @@ hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw
 hipError_t lstm_fused_bwd_launch(const float* dh, const void* gates_bf16, const void* cseq_bf16, const float* hseq,
                                  const float* x, const float* h0, const float* c0, const float* W, const float* Uw,
                                  float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
-                                 int act, hipStream_t stream) {
+                                 int act, int dh_last_only, hipStream_t stream) {
   FusedBwdArgs a{dh,       (const __bf16*)gates_bf16, (const __bf16*)cseq_bf16, hseq, x, h0, c0, W, Uw, dx, dh0, dc0,
-                 partials, B,  T,  IN, act};
+                 partials, B,  T,  IN, act, dh_last_only};
   return dispatch(U, IN, [&](auto u, auto k) { return launch_bwd<decltype(u)::value, decltype(k)::value>(a, stream); });
 }
 

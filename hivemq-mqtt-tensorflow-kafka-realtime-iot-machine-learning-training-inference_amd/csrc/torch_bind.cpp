@@ -357,7 +357,7 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& g
                                        const at::Tensor& hseq, const at::Tensor& x,
                                        const c10::optional<at::Tensor>& h0, const c10::optional<at::Tensor>& c0,
                                        const at::Tensor& W, const at::Tensor& Uw, int64_t act, bool want_dx,
-                                       bool want_state_grads) {
+                                       bool want_state_grads, bool dh_last_only) {
   check_dev(dh, "dh", at::kFloat);
   check_dev(cseq, "c", at::kBFloat16);
   check_dev(hseq, "h", at::kFloat);
@@ -368,8 +368,13 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& g
   const int64_t B = x.size(0), T = x.size(1), IN = x.size(2), U = Uw.size(0);
   TORCH_CHECK(dh.is_contiguous() && cseq.is_contiguous() && hseq.is_contiguous() && x.is_contiguous(),
               "inputs must be contiguous");
-  TORCH_CHECK(dh.size(0) == B && dh.size(1) == T && dh.size(2) == U && cseq.sizes() == dh.sizes() &&
-              hseq.sizes() == dh.sizes() && gates.size(2) == 4 * U, "shape mismatch");
+  TORCH_CHECK(hseq.size(0) == B && hseq.size(1) == T && hseq.size(2) == U && cseq.sizes() == hseq.sizes() &&
+              gates.size(2) == 4 * U, "shape mismatch");
+  if (dh_last_only) {
+    TORCH_CHECK(dh.dim() == 2 && dh.size(0) == B && dh.size(1) == U, "dh must be [B, U] (h_T only)");
+  } else {
+    TORCH_CHECK(dh.sizes() == hseq.sizes(), "dh must be [B, T, U]");
+  }
   TORCH_CHECK(sml::lstm_fused_supported((int)U, (int)IN), "fused LSTM: unsupported U=", U, " IN=", IN);
   c10::hip::HIPGuard guard(x.device().index());
   auto opts = x.options();
@@ -389,7 +394,7 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& g
       dh.data_ptr<float>(), gates.data_ptr(), cseq.data_ptr(), hseq.data_ptr<float>(), x.data_ptr<float>(),
       opt_ptr(h0), opt_ptr(c0), W.data_ptr<float>(), Uw.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
       want_state_grads ? dh0.data_ptr<float>() : nullptr, want_state_grads ? dc0.data_ptr<float>() : nullptr,
-      partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U, (int)act, st));
+      partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U, (int)act, dh_last_only ? 1 : 0, st));
   SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
                                      out.data_ptr<float>(), st));
   const int64_t G4 = 4 * U, LDW = (S / G4) - U - 1;
@@ -578,7 +583,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_fused_bwd", &lstm_fused_bwd, "fully fused LSTM layer backward (BPTT + dW/dU/db + dX in one kernel)",
         py::arg("dh"), py::arg("gates"), py::arg("c"), py::arg("h"), py::arg("x"), py::arg("h0") = py::none(),
         py::arg("c0") = py::none(), py::arg("W"), py::arg("U"), py::arg("act") = 1, py::arg("want_dx") = true,
-        py::arg("want_state_grads") = false);
+        py::arg("want_state_grads") = false, py::arg("dh_last_only") = false);
   m.def("lstm_fused_supported", &sml::lstm_fused_supported, "whether (U, IN) has a fused LSTM kernel", py::arg("U"),
         py::arg("IN"));
   py::class_<ServePy>(m, "AEServe", "persistent per-event autoencoder scorer over host-mapped rings")

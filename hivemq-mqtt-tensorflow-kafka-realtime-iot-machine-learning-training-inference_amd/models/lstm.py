@@ -131,8 +131,7 @@ class LSTMPredictor:
         for L in self.layers:
             if L["kind"] == "lstm":
                 W, Uw, b = P[L["params"]:L["params"] + 3]
-                hs = lstm_op(h, W, Uw, b, L["activation"])
-                h = hs if L["return_sequences"] else hs[:, -1]
+                h = lstm_op(h, W, Uw, b, L["activation"], return_sequences=L["return_sequences"])
             elif L["kind"] == "repeat":
                 h = h.unsqueeze(1).expand(h.shape[0], L["n"], h.shape[-1]).contiguous()
             else:

@@ -215,8 +215,7 @@ class LSTM(Layer):
     def forward(self, params, x, training):
         from ..ops.lstm import lstm as lstm_op
         W, U, b = params
-        hs = lstm_op(x, W, U, b, self.activation)
-        return hs if self.return_sequences else hs[:, -1]
+        return lstm_op(x, W, U, b, self.activation, return_sequences=self.return_sequences)
 
     def get_config(self):
         return kc.lstm_config(self.name, self.units, self.activation, self.return_sequences,

@@ -105,23 +105,27 @@ class LSTMFunction(torch.autograd.Function):
 
 class FusedLSTMFunction(torch.autograd.Function):
     """Whole layer in two launches: ``lstm_fused_fwd`` (x.W + recurrence, bf16 gates
-    saved) and ``lstm_fused_bwd`` (BPTT + dW/dU/db accumulated in registers + dX)."""
+    and cell state saved) and ``lstm_fused_bwd`` (BPTT + dW/dU/db accumulated in
+    registers + dX).  ``last_only`` (Keras ``return_sequences=False``) returns h_T
+    [B, U]; its backward reads only that [B, U] gradient instead of a [B, T, U]
+    tensor of zeros."""
 
     @staticmethod
-    def forward(ctx, x, W, U, b, act_code: int):
+    def forward(ctx, x, W, U, b, act_code: int, last_only: bool = False):
         h, c, gates = load_c().lstm_fused_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), None, None,
                                               act_code)
         ctx.save_for_backward(x, W, U, h, c, gates)
         ctx.act = act_code
-        return h
+        ctx.last_only = bool(last_only)
+        return h[:, -1].contiguous() if last_only else h
 
     @staticmethod
     def backward(ctx, dh):
         x, W, U, h, c, gates = ctx.saved_tensors
         dx, dW, dU, db, _, _ = load_c().lstm_fused_bwd(dh.contiguous().float(), gates, c, h, x, None, None,
                                                        W.contiguous(), U.contiguous(), ctx.act,
-                                                       bool(ctx.needs_input_grad[0]), False)
-        return (dx if ctx.needs_input_grad[0] else None), dW, dU, db, None
+                                                       bool(ctx.needs_input_grad[0]), False, ctx.last_only)
+        return (dx if ctx.needs_input_grad[0] else None), dW, dU, db, None, None
 
 
 def fused_supported(units: int, in_features: int) -> bool:
@@ -129,11 +133,14 @@ def fused_supported(units: int, in_features: int) -> bool:
 
 
 def lstm(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor, activation: str = "relu",
-         fused: bool = True) -> torch.Tensor:
-    """Device-dispatching LSTM layer: fused HIP kernels on ROCm, torch reference on CPU."""
+         fused: bool = True, return_sequences: bool = True) -> torch.Tensor:
+    """Device-dispatching LSTM layer: fused HIP kernels on ROCm, torch reference on CPU.
+    ``return_sequences=False`` returns h_T [B, U] (Keras semantics)."""
     if x.is_cuda:
         xc = x.contiguous().float()
         if fused and fused_supported(U.shape[0], x.shape[-1]):
-            return FusedLSTMFunction.apply(xc, W, U, b, ACT[activation])
-        return LSTMFunction.apply(xc, W, U, b, ACT[activation])
-    return lstm_reference(x, W, U, b, activation)
+            return FusedLSTMFunction.apply(xc, W, U, b, ACT[activation], not return_sequences)
+        hs = LSTMFunction.apply(xc, W, U, b, ACT[activation])
+    else:
+        hs = lstm_reference(x, W, U, b, activation)
+    return hs if return_sequences else hs[:, -1]

@@ -50,3 +50,23 @@ def test_lstm_predictor_gpu_trains_and_matches_cpu_start(cuda_device):
     assert _relerr(pg, pc) < 3e-2
     h = mg.fit(xs, ys, epochs=4, batch_size=128, verbose=0)
     assert h.history["loss"][-1] < h.history["loss"][0]
+
+
+@pytest.mark.parametrize("u,B,T,inp", [(16, 130, 9, 32), (32, 64, 50, 18)])
+def test_fused_last_only_matches_full_sequence_grad(cuda_device, u, B, T, inp):
+    """return_sequences=False: the [B, U] h_T gradient path equals slicing the full sequence."""
+    rng = np.random.default_rng(u * B)
+    x = torch.tensor(rng.uniform(-1, 1, (B, T, inp)), dtype=torch.float32, device=cuda_device)
+    W = torch.tensor(rng.standard_normal((inp, 4 * u)) * 0.25, dtype=torch.float32, device=cuda_device)
+    U = torch.tensor(rng.standard_normal((u, 4 * u)) * 0.25, dtype=torch.float32, device=cuda_device)
+    b = torch.tensor(rng.standard_normal(4 * u) * 0.1, dtype=torch.float32, device=cuda_device)
+    gy = torch.tensor(rng.standard_normal((B, u)), dtype=torch.float32, device=cuda_device)
+    grads = []
+    for last_only in (False, True):
+        ins = [t.clone().requires_grad_(True) for t in (x, W, U, b)]
+        y = FusedLSTMFunction.apply(*ins, 1, last_only)
+        y = y if last_only else y[:, -1]
+        (y * gy).sum().backward()
+        grads.append([t.grad.cpu() for t in ins])
+    for a, b_ in zip(*grads):
+        torch.testing.assert_close(a, b_, rtol=0, atol=0)
