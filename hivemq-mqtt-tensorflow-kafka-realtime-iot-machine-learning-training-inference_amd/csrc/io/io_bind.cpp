@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cctype>
 #include <cstring>
 
 #include "avro.h"
@@ -126,7 +127,22 @@ std::vector<avro::Field> fields_from_py(const py::list& lst) {
   return out;
 }
 
-py::dict batch_to_py(avro::DecodedBatch& b) {
+// failure_occurred-style label code of a text value: "false" -> 0, "true" -> 1, else 2
+// (case-insensitive, surrounding whitespace ignored) -- the stream's LABEL_* codes
+uint8_t label_code(const std::string& v) {
+  size_t a = 0, e = v.size();
+  while (a < e && std::isspace((unsigned char)v[a])) ++a;
+  while (e > a && std::isspace((unsigned char)v[e - 1])) --e;
+  auto eq = [&](const char* w, size_t n) {
+    if (e - a != n) return false;
+    for (size_t i = 0; i < n; ++i)
+      if (std::tolower((unsigned char)v[a + i]) != w[i]) return false;
+    return true;
+  };
+  return eq("false", 5) ? 0 : eq("true", 4) ? 1 : 2;
+}
+
+py::dict batch_to_py(avro::DecodedBatch& b, bool with_text = true) {
   py::dict d;
   const size_t n = b.n, k = b.n_numeric;
   py::array_t<float> num({n, k});
@@ -140,17 +156,23 @@ py::dict batch_to_py(avro::DecodedBatch& b) {
   py::array_t<uint8_t> nul({n, k});
   if (n * k) std::memcpy(nul.mutable_data(), b.null_mask.data(), n * k);
   d["null"] = nul;
-  py::list text, tnull;
+  py::list text, tnull, tcodes;
   for (size_t c = 0; c < b.text.size(); ++c) {
-    py::list col;
-    for (auto& s : b.text[c]) col.append(py::bytes(s));
-    text.append(col);
-    py::array_t<uint8_t> tn(n);
+    if (with_text) {
+      py::list col;
+      for (auto& s : b.text[c]) col.append(py::bytes(s));
+      text.append(col);
+    }
+    py::array_t<uint8_t> tn(n), tc(n);
     if (n) std::memcpy(tn.mutable_data(), b.text_null[c].data(), n);
+    uint8_t* pc = tc.mutable_data();
+    for (py::ssize_t i = 0; i < n; ++i) pc[i] = b.text_null[c][(size_t)i] ? 2 : label_code(b.text[c][(size_t)i]);
     tnull.append(tn);
+    tcodes.append(tc);
   }
   d["text"] = text;
   d["text_null"] = tnull;
+  d["text_codes"] = tcodes;   // per text column: LABEL_FALSE / LABEL_TRUE / LABEL_MISSING codes
   py::array_t<int32_t> sid(n);
   if (n) std::memcpy(sid.mutable_data(), b.schema_id.data(), n * 4);
   d["schema_id"] = sid;
@@ -309,7 +331,7 @@ PYBIND11_MODULE(_io, m) {
            py::arg("max_wait_ms") = 100)
       .def("fetch_decode",
            [](kafka::Client& c, const avro::Codec& codec, const std::string& t, int p, int64_t off,
-              int32_t max_bytes, int32_t wait, bool framing) {
+              int32_t max_bytes, int32_t wait, bool framing, bool with_text, bool str_keys) {
              kafka::FetchResult r;
              avro::DecodedBatch b;
              {
@@ -318,19 +340,25 @@ PYBIND11_MODULE(_io, m) {
                b = codec.decode(reinterpret_cast<const uint8_t*>(r.values.data()), r.values.size(),
                                 r.value_offsets.data(), r.size(), framing, false, false);
              }
-             py::dict d = batch_to_py(b);
+             py::dict d = batch_to_py(b, with_text);
              py::array_t<int64_t> offs(r.offsets.size());
              if (!r.offsets.empty()) std::memcpy(offs.mutable_data(), r.offsets.data(), r.offsets.size() * 8);
              d["offsets"] = offs;
              py::list keys;
-             for (auto& k : r.keys) keys.append(py::bytes(k));
+             if (str_keys) {
+               for (auto& k : r.keys) keys.append(py::reinterpret_steal<py::object>(
+                   PyUnicode_DecodeUTF8(k.data(), (py::ssize_t)k.size(), "replace")));
+             } else {
+               for (auto& k : r.keys) keys.append(py::bytes(k));
+             }
              d["keys"] = keys;
              d["high_watermark"] = r.high_watermark;
              d["bytes"] = r.values.size();
              return d;
            },
            py::arg("codec"), py::arg("topic"), py::arg("partition"), py::arg("offset"),
-           py::arg("max_bytes") = 1 << 20, py::arg("max_wait_ms") = 100, py::arg("framing") = true)
+           py::arg("max_bytes") = 1 << 20, py::arg("max_wait_ms") = 100, py::arg("framing") = true,
+           py::arg("with_text") = true, py::arg("str_keys") = false)
       .def("produce",
            [](kafka::Client& c, const std::string& t, int p, const py::list& values, py::object keys, py::object ts,
               int acks) {

@@ -33,13 +33,41 @@ struct Crc32cTable {
   }
 };
 const Crc32cTable kCrc;
-}  // namespace
 
-uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc) {
+uint32_t crc32c_table(const uint8_t* p, size_t n, uint32_t crc) {
   crc = ~crc;
   for (size_t i = 0; i < n; ++i) crc = kCrc.t[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
   return ~crc;
 }
+
+#if defined(__x86_64__)
+// SSE4.2 crc32 instruction (CRC-32C polynomial): 8 bytes per instruction instead of
+// one table lookup per byte.  Every record batch is checksummed twice (producer /
+// broker encode, consumer verify), so on the ingest path this is the hot loop.
+__attribute__((target("sse4.2"))) uint32_t crc32c_hw(const uint8_t* p, size_t n, uint32_t crc) {
+  uint64_t c = ~crc & 0xffffffffu;
+  while (n >= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    c = __builtin_ia32_crc32di(c, v);
+    p += 8;
+    n -= 8;
+  }
+  uint32_t c32 = (uint32_t)c;
+  while (n--) c32 = __builtin_ia32_crc32qi(c32, *p++);
+  return ~c32;
+}
+#endif
+}  // namespace
+
+uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc) {
+#if defined(__x86_64__)
+  static const bool hw = __builtin_cpu_supports("sse4.2");
+  if (hw) return crc32c_hw(p, n, crc);
+#endif
+  return crc32c_table(p, n, crc);
+}
+
 
 // ---------------------------------------------------------------------------
 // big-endian writer / reader

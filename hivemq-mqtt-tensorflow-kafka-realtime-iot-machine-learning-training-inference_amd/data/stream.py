@@ -242,7 +242,7 @@ def json_lines(path: str, chunk: int = 65536) -> Stream:
 def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optional[str] = None,
           eof: bool = True, config: Optional[Sequence[str]] = None, max_bytes: int = 4 << 20,
           framing: bool = True, commit: bool = False, resume: bool = False,
-          idle_timeout_s: Optional[float] = None) -> Stream:
+          idle_timeout_s: Optional[float] = None, workers: int = 1) -> Stream:
     """Kafka topic(s) of (Confluent-framed) Avro car records -> raw feature chunks."""
     from ..kafka import KafkaDataset
     from .avro import AvroCodec
@@ -257,18 +257,20 @@ def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optio
     label_field = next((f for f in codec.text_fields if canonical(f) == LABEL), None)
 
     def gen():
+        # label codes and str keys come straight from C++ (no per-record Python objects
+        # for the text column, no second pass over the keys)
         ds = KafkaDataset(topics, servers=servers, group=group, eof=eof, config_global=config, codec=codec,
                           max_bytes=max_bytes, framing=framing, commit=commit, resume=resume,
-                          idle_timeout_s=idle_timeout_s)
+                          idle_timeout_s=idle_timeout_s, with_text=False, str_keys=True, workers=workers)
         for b in ds:
             ok = b["ok"].astype(bool)
             x = b["numeric"][:, cols]
             if label_field is not None:
-                lab = label_codes(b["text"][label_field], b["text_null"][label_field])
+                lab = np.array(b["text_codes"][label_field], dtype=np.uint8, copy=True)
             else:
                 lab = np.zeros(len(x), np.uint8)
             lab[~ok] = LABEL_MISSING
-            keys = [k.decode(errors="replace") for k in b["keys"]]
+            keys = b["keys"]
             yield Chunk(np.ascontiguousarray(x), lab, keys, b["offsets"],
                         meta={"topic": b["topic"], "partition": b["partition"], "errors": int(b["n_errors"])})
     return Stream(gen)

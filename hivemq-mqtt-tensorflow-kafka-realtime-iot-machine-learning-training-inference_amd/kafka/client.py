@@ -142,8 +142,12 @@ class KafkaClient:
         return self._c.fetch(topic, partition, offset, max_bytes, max_wait_ms)
 
     def fetch_decode(self, codec, topic: str, partition: int, offset: int, max_bytes: int = 1 << 20,
-                     max_wait_ms: int = 100, framing: bool = True):
-        return self._c.fetch_decode(codec.native, topic, partition, offset, max_bytes, max_wait_ms, framing)
+                     max_wait_ms: int = 100, framing: bool = True, with_text: bool = True, str_keys: bool = False):
+        """Fetch + Avro decode in C++ (GIL released).  ``with_text=False`` skips building
+        per-record bytes objects for text columns (their label codes are always in
+        ``text_codes``); ``str_keys`` returns record keys as ``str``."""
+        return self._c.fetch_decode(codec.native, topic, partition, offset, max_bytes, max_wait_ms, framing,
+                                    with_text, str_keys)
 
     def produce(self, topic: str, partition: int, values: Sequence[bytes], keys=None, timestamps=None,
                 acks: int = 1) -> int:

@@ -12,7 +12,8 @@ stream (python-scripts/README.md:116).  Differences by design:
 * consumed offsets can be committed to the group (``commit=True``) so a
   restarted job resumes where it stopped (SURVEY.md 5.3 recovery story);
 * several ``topic:partition:offset`` specs are read round-robin (the reference
-  hard-codes partition 0, cardata-v3.py:46).
+  hard-codes partition 0, cardata-v3.py:46), or concurrently by ``workers``
+  threads with a connection each (partition-parallel consumption).
 """
 from __future__ import annotations
 
@@ -29,7 +30,8 @@ class KafkaDataset:
     def __init__(self, topics: Sequence[str], servers: str = "fake://", group: Optional[str] = None,
                  eof: bool = True, config_global: Optional[Sequence[str]] = None, codec=None,
                  max_bytes: int = 4 << 20, max_wait_ms: int = 100, framing: bool = True,
-                 commit: bool = False, resume: bool = False, idle_timeout_s: Optional[float] = None):
+                 commit: bool = False, resume: bool = False, idle_timeout_s: Optional[float] = None,
+                 with_text: bool = True, str_keys: bool = False, workers: int = 1):
         self.specs = [parse_topic_spec(t) for t in topics]
         self.servers = servers
         self.group = group
@@ -42,6 +44,9 @@ class KafkaDataset:
         self.commit = commit and group is not None
         self.resume = resume and group is not None
         self.idle_timeout_s = idle_timeout_s
+        self.with_text = with_text
+        self.str_keys = str_keys
+        self.workers = max(1, int(workers))
         self._client: Optional[KafkaClient] = None
         self.records_read = 0
         self.bytes_read = 0
@@ -62,61 +67,137 @@ class KafkaDataset:
             return c.latest(topic, partition) if offset == -1 else c.earliest(topic, partition)
         return max(offset, c.earliest(topic, partition))
 
-    def __iter__(self) -> Iterator[dict]:
-        c = self.client
+    def _step(self, c: KafkaClient, cur: List) -> Optional[dict]:
+        """One fetch(+decode) for a cursor ``[topic, partition, pos, end]``; advances it.
+        Returns the batch, ``None`` when nothing arrived, or ``False`` when the cursor is done."""
+        topic, partition, pos, end = cur
+        if end is not None and pos >= end:
+            return False
+        t_fetch = time.perf_counter()
+        if self.codec is not None:
+            batch = c.fetch_decode(self.codec, topic, partition, pos, self.max_bytes, self.max_wait_ms,
+                                   self.framing, self.with_text, self.str_keys)
+            nbytes = int(batch["bytes"])
+            if int(batch.get("n_errors", 0)):
+                ENGINE.decode_errors.inc(int(batch["n_errors"]), topic=topic)
+            batch["text"] = dict(zip(self.codec.text_fields, batch["text"]))
+            batch["text_null"] = dict(zip(self.codec.text_fields, batch["text_null"]))
+            batch["text_codes"] = dict(zip(self.codec.text_fields, batch["text_codes"]))
+        else:
+            batch = c.fetch(topic, partition, pos, self.max_bytes, self.max_wait_ms)
+            nbytes = len(batch["values"])
+        offs = batch["offsets"]
+        self.bytes_read += nbytes
+        if len(offs) == 0:
+            return None
+        if end is not None and offs[-1] >= end:  # trim to the eof boundary
+            keep = int(np.searchsorted(offs, end))
+            if keep == 0:
+                cur[2] = end
+                return False
+            batch = _trim(batch, keep)
+            offs = batch["offsets"]
+        cur[2] = int(offs[-1]) + 1
+        self.records_read += len(offs)
+        ENGINE.ingest_records.inc(len(offs), topic=topic)
+        ENGINE.ingest_bytes.inc(nbytes, topic=topic)
+        ENGINE.decode_seconds.inc(time.perf_counter() - t_fetch, topic=topic)
+        batch["topic"], batch["partition"] = topic, partition
+        return batch
+
+    def _cursors(self, c: KafkaClient) -> List[List]:
         cursors: List[List] = []
         for topic, partition, offset in self.specs:
             start = self._start_offset(topic, partition, offset)
             end = c.latest(topic, partition) if self.eof else None
             cursors.append([topic, partition, start, end])
+        return cursors
+
+    def __iter__(self) -> Iterator[dict]:
+        c = self.client
+        cursors = self._cursors(c)
+        if self.workers > 1 and len(cursors) > 1:
+            yield from self._iter_parallel(c, cursors)
+            return
         last_data = time.monotonic()
-        m_rec, m_bytes, m_dec = ENGINE.ingest_records, ENGINE.ingest_bytes, ENGINE.decode_seconds
         while cursors:
             progressed = False
             for cur in list(cursors):
-                topic, partition, pos, end = cur
-                if end is not None and pos >= end:
+                batch = self._step(c, cur)
+                if batch is False:
                     cursors.remove(cur)
                     continue
-                t_fetch = time.perf_counter()
-                if self.codec is not None:
-                    batch = c.fetch_decode(self.codec, topic, partition, pos, self.max_bytes, self.max_wait_ms,
-                                           self.framing)
-                    offs = batch["offsets"]
-                    nbytes = int(batch["bytes"])
-                    self.bytes_read += nbytes
-                    if int(batch.get("n_errors", 0)):
-                        ENGINE.decode_errors.inc(int(batch["n_errors"]), topic=topic)
-                    batch["text"] = dict(zip(self.codec.text_fields, batch["text"]))
-                    batch["text_null"] = dict(zip(self.codec.text_fields, batch["text_null"]))
-                else:
-                    batch = c.fetch(topic, partition, pos, self.max_bytes, self.max_wait_ms)
-                    offs = batch["offsets"]
-                    nbytes = len(batch["values"])
-                    self.bytes_read += nbytes
-                if len(offs) == 0:
+                if batch is None:
                     continue
-                if end is not None and offs[-1] >= end:  # trim to the eof boundary
-                    keep = int(np.searchsorted(offs, end))
-                    batch = _trim(batch, keep)
-                    offs = batch["offsets"]
-                    if keep == 0:
-                        cursors.remove(cur)
-                        continue
-                cur[2] = int(offs[-1]) + 1
-                self.records_read += len(offs)
-                m_rec.inc(len(offs), topic=topic)
-                m_bytes.inc(nbytes, topic=topic)
-                m_dec.inc(time.perf_counter() - t_fetch, topic=topic)
                 progressed = True
-                batch["topic"], batch["partition"] = topic, partition
                 yield batch
                 if self.commit:
-                    c.commit(self.group, topic, partition, cur[2])
+                    c.commit(self.group, cur[0], cur[1], cur[2])
             if progressed:
                 last_data = time.monotonic()
             elif self.idle_timeout_s is not None and time.monotonic() - last_data > self.idle_timeout_s:
                 return
+
+    def _iter_parallel(self, c: KafkaClient, cursors: List[List]) -> Iterator[dict]:
+        """Partition-parallel consumption: ``workers`` threads, each with its own client
+        connection, fetch + decode disjoint partitions concurrently (the native calls
+        release the GIL) -- the consumer-group scale-out of the reference's 10-partition
+        topics, inside one process.  Batches arrive in completion order per partition
+        (per-partition order is kept); offsets are committed after each batch is consumed."""
+        import queue
+        import threading
+        nw = min(self.workers, len(cursors))
+        q: "queue.Queue" = queue.Queue(maxsize=2 * nw)
+        stop = threading.Event()
+        done = object()
+
+        def work(mine: List[List]) -> None:
+            try:
+                cl = KafkaClient(self.servers, self.config)
+                last = time.monotonic()
+                live = list(mine)
+                while live and not stop.is_set():
+                    progressed = False
+                    for cur in list(live):
+                        batch = self._step(cl, cur)
+                        if batch is False:
+                            live.remove(cur)
+                        elif batch is not None:
+                            progressed = True
+                            while not stop.is_set():
+                                try:
+                                    q.put((batch, cur[2]), timeout=0.1)
+                                    break
+                                except queue.Full:
+                                    continue
+                    if progressed:
+                        last = time.monotonic()
+                    elif self.idle_timeout_s is not None and time.monotonic() - last > self.idle_timeout_s:
+                        break
+            except BaseException as e:  # surfaced in the consumer
+                q.put((e, None))
+            finally:
+                q.put((done, None))
+
+        threads = [threading.Thread(target=work, args=(cursors[i::nw],), daemon=True) for i in range(nw)]
+        for t in threads:
+            t.start()
+        finished = 0
+        try:
+            while finished < nw:
+                item, pos = q.get()
+                if item is done:
+                    finished += 1
+                    continue
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+                if self.commit:
+                    c.commit(self.group, item["topic"], item["partition"], pos)
+        finally:
+            stop.set()
+            for t in threads:
+                t.join(timeout=5)
 
     def messages(self) -> Iterator[bytes]:
         """Per-message iteration (the tfio element view); slow path for small streams."""
@@ -145,6 +226,9 @@ def _trim(batch: dict, keep: int) -> dict:
             [v[:keep] for v in batch["text"]]
         out["text_null"] = {k: v[:keep] for k, v in batch["text_null"].items()} \
             if isinstance(batch["text_null"], dict) else [v[:keep] for v in batch["text_null"]]
+        if "text_codes" in batch:
+            tc = batch["text_codes"]
+            out["text_codes"] = {k: v[:keep] for k, v in tc.items()} if isinstance(tc, dict) else [v[:keep] for v in tc]
     out["offsets"] = batch["offsets"][:keep]
     out["keys"] = batch["keys"][:keep]
     return out
