@@ -106,3 +106,18 @@ def test_tensorboard_roundtrip_with_reference_tags(tmp_path):
         assert {"epoch_loss", "epoch_accuracy"} <= ref_tags
     vals = [v for _, _, t, v in got if t == "epoch_loss"]
     np.testing.assert_allclose(vals, [1.0, 0.5, 1.0 / 3], rtol=1e-6)
+
+
+def test_grafana_dashboard_queries_exported_metrics():
+    """Every panel of deploy/grafana/streamml.json queries a metric this package exports
+    (engine metrics + the MQTT broker collector), and the committed copy is current."""
+    import json
+    from streamml.mqtt import MqttBroker
+    from streamml.obs import dashboard, metrics
+    with MqttBroker(port=0):
+        text = metrics.REGISTRY.exposition()
+    for name in dashboard.metric_names():
+        assert f"# TYPE {name} " in text or f"\n{name} " in text or f"\n{name}{{" in text, name
+    committed = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                            "deploy", "grafana", "streamml.json")))
+    assert committed == dashboard.build()
