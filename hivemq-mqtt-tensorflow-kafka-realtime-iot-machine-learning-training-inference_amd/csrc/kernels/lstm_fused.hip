@@ -24,6 +24,14 @@
 //     Each wave writes one fp32 slab of [dW^T | dU^T | db]; slab_sum_kernel
 //     (dense.hip) reduces the slabs deterministically.
 //
+// Saved-state layout ("fragment-native"): gates and cell state are only ever read
+// back by the backward kernel, by the same lane of the same wave that wrote them,
+// so they are stored in MFMA C-fragment order, not [B, T, 4U]:
+//   gates[wave][t][tile 0..MT)[lane 0..64)[4] bf16,  cseq[wave][t][tile 0..UB)[lane][4]
+// Every store / load of a 16-sequence tile is then ONE contiguous 512-byte access per
+// wave instead of 16 scattered 32-byte pieces (rows T*4U*2 bytes apart), and the
+// buffers are padded to whole waves (16 sequences) so no lane needs a bounds check.
+//
 // MFMA orientation (v_mfma_f32_16x16x16_bf16, lane c = l & 15, g = l >> 4):
 //   C tile mt of z: lane (c, g) holds gate 16mt + 4g + i of sequence s0 + c, so
 //   the four gates of unit u sit in tiles q*UB + u/16 of the same lane/register.
@@ -59,10 +67,11 @@ struct FusedFwdArgs {
   const float* h0;     // [B, U] or null
   const float* c0;     // [B, U] or null
   float* hseq;         // [B, T, U]
-  __bf16* cseq;        // [B, T, U]   cell state, bf16 (read only by the backward kernel)
-  __bf16* gates;       // [B, T, 4U]  post-activation i, f, c~, o
+  __bf16* cseq;        // [B/16, T, U/16, 64, 4]   cell state, bf16, fragment-native (backward only)
+  __bf16* gates;       // [B/16, T, 4U/16, 64, 4]  post-activation i, f, c~, o, fragment-native
   int64_t B;
   int T, IN, act;
+  int xvec;            // x row access width in floats (4 / 2 / 1), from IN and x's alignment
 };
 
 template <int U, int KT>
@@ -115,16 +124,27 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
   }
   // x_t^T as B operand: B[k = feature 16kt + 4g + j][n = sequence c]
   const float* xrow = a.x + sq * (int64_t)T * IN;
+  const int xvec = a.xvec;   // wave-uniform
   auto load_x = [&](int t, f32x4* v) {
     const float* p = xrow + (int64_t)t * IN;
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt)
+    for (int kt = 0; kt < KT; ++kt) {
+      const int k0 = 16 * kt + 4 * g;
+      if (xvec == 4) {                       // one dwordx4 per tile
+        v[kt] = k0 < IN ? *reinterpret_cast<const f32x4*>(p + k0) : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else if (xvec == 2) {                // two dwordx2 (rows 8-byte aligned)
+        const f32x2_t lo = k0 < IN ? *reinterpret_cast<const f32x2_t*>(p + k0) : f32x2_t{0.f, 0.f};
+        const f32x2_t hi = k0 + 2 < IN ? *reinterpret_cast<const f32x2_t*>(p + k0 + 2) : f32x2_t{0.f, 0.f};
+        v[kt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = 16 * kt + 4 * g + j;
-        v[kt][j] = k < IN ? p[k] : 0.f;
+        for (int j = 0; j < 4; ++j) v[kt][j] = k0 + j < IN ? p[k0 + j] : 0.f;
       }
+    }
   };
+  const int64_t wv = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  __bf16* gw = a.gates + wv * T * (int64_t)(MT * 256) + lane * 4;
+  __bf16* cw = a.cseq + wv * T * (int64_t)(UB * 256) + lane * 4;
   f32x4 xn[KT];
   load_x(0, xn);
   for (int t = 0; t < T; ++t) {
@@ -141,8 +161,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
 #pragma unroll
       for (int s = 0; s < UB; ++s) z[mt] = mfma16(ut[mt][s], hb[s], z[mt]);
     }
-    const int64_t bg = (sq * T + t) * (int64_t)G4;
     const int64_t bu = (sq * T + t) * (int64_t)U;
+    __bf16* gt = gw + (int64_t)t * (MT * 256);
+    __bf16* ct = cw + (int64_t)t * (UB * 256);
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
       f32x4 gi, gf, gc, go;
@@ -155,15 +176,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
         cs[b][i] = fmaf(gf[i], cs[b][i], gi[i] * gc[i]);
         h[b][i] = go[i] * act_f(a.act, cs[b][i]);
       }
-      if (valid) {
-        const int off = 16 * b + 4 * g;
-        *reinterpret_cast<bf16x4*>(a.gates + bg + off) = pack4(gi);
-        *reinterpret_cast<bf16x4*>(a.gates + bg + U + off) = pack4(gf);
-        *reinterpret_cast<bf16x4*>(a.gates + bg + 2 * U + off) = pack4(gc);
-        *reinterpret_cast<bf16x4*>(a.gates + bg + 3 * U + off) = pack4(go);
-        *reinterpret_cast<bf16x4*>(a.cseq + bu + off) = pack4(cs[b]);
-        *reinterpret_cast<f32x4*>(a.hseq + bu + off) = h[b];
-      }
+      // padded lanes (seq >= B) write their own padded slots: no bounds check
+      *reinterpret_cast<bf16x4*>(gt + b * 256) = pack4(gi);
+      *reinterpret_cast<bf16x4*>(gt + (UB + b) * 256) = pack4(gf);
+      *reinterpret_cast<bf16x4*>(gt + (2 * UB + b) * 256) = pack4(gc);
+      *reinterpret_cast<bf16x4*>(gt + (3 * UB + b) * 256) = pack4(go);
+      *reinterpret_cast<bf16x4*>(ct + b * 256) = pack4(cs[b]);
+      if (valid) *reinterpret_cast<f32x4*>(a.hseq + bu + 16 * b + 4 * g) = h[b];
       hb[b] = pack4(h[b]);
     }
   }
@@ -171,8 +190,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
 
 struct FusedBwdArgs {
   const float* dh;     // [B, T, U]  gradient w.r.t. the h sequence ([B, U] of h_T when dh_last_only)
-  const __bf16* gates; // [B, T, 4U]
-  const __bf16* cseq;  // [B, T, U]
+  const __bf16* gates; // fragment-native, as written by the forward kernel
+  const __bf16* cseq;  // fragment-native
   const float* hseq;   // [B, T, U]
   const float* x;      // [B, T, IN]
   const float* h0;     // [B, U] or null
@@ -186,6 +205,7 @@ struct FusedBwdArgs {
   int64_t B;
   int T, IN, act;
   int dh_last_only;    // return_sequences=False: only h_T received a gradient (no [B, T, U] zeros read)
+  int xvec;            // dx row access width in floats (4 / 2 / 1)
 };
 
 template <int U, int KT>
@@ -256,17 +276,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     f32x4 hprev[UB];   // B[k = seq 4g + j][n = unit 16kb + c]
     f32x4 xt[KT];      // B[k = seq 4g + j][n = feature 16kt + c]
   };
+  const __bf16* gw = a.gates + wave_id * T * (int64_t)(MT * 256) + lane * 4;
+  const __bf16* cw = a.cseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
+  const int xvec = a.xvec;   // wave-uniform
   auto load_step = [&](int t, Step& st) {
-    const int64_t bg = (sq * T + t) * (int64_t)G4;
     const int64_t bu = (sq * T + t) * (int64_t)U;
+    const __bf16* gt = gw + (int64_t)t * (MT * 256);
+    const __bf16* cp = cw + (int64_t)(t - 1) * (UB * 256);
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
       const int off = 16 * b + 4 * g;
-      st.gi[b] = ld_bf16x4(a.gates + bg + off);
-      st.gf[b] = ld_bf16x4(a.gates + bg + U + off);
-      st.gc[b] = ld_bf16x4(a.gates + bg + 2 * U + off);
-      st.go[b] = ld_bf16x4(a.gates + bg + 3 * U + off);
-      if (t > 0) st.cprev[b] = ld_bf16x4(a.cseq + bu - U + off);
+      st.gi[b] = ld_bf16x4(gt + b * 256);
+      st.gf[b] = ld_bf16x4(gt + (UB + b) * 256);
+      st.gc[b] = ld_bf16x4(gt + (2 * UB + b) * 256);
+      st.go[b] = ld_bf16x4(gt + (3 * UB + b) * 256);
+      if (t > 0) st.cprev[b] = ld_bf16x4(cp + b * 256);
       else if (a.c0) st.cprev[b] = pack4(*reinterpret_cast<const f32x4*>(a.c0 + sq * U + off));
       else st.cprev[b] = pack4(zero4);
       if (a.dh_last_only) st.dho[b] = (valid && t == T - 1) ? *reinterpret_cast<const f32x4*>(a.dh + sq * U + off) : zero4;
@@ -298,7 +322,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   Step cur, nxt;
   f32x4 ctc[UB];   // c_t
 #pragma unroll
-  for (int b = 0; b < UB; ++b) ctc[b] = unpack4(ld_bf16x4(a.cseq + (sq * T + T - 1) * (int64_t)U + 16 * b + 4 * g));
+  for (int b = 0; b < UB; ++b)
+    ctc[b] = active ? unpack4(ld_bf16x4(cw + (int64_t)(T - 1) * (UB * 256) + b * 256)) : zero4;
   if (active) load_step(T - 1, nxt);
   for (int t = T - 1; t >= 0 && active; --t) {
     cur = nxt;
@@ -353,10 +378,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
         for (int mt = 0; mt < MT; ++mt) acc = mfma16(wf[kt][mt], dzb[mt], acc);
         if (valid) {
           float* p = a.dx + (sq * T + t) * (int64_t)IN;
+          const int f0 = 16 * kt + 4 * g;
+          if (xvec == 4) {
+            if (f0 < IN) *reinterpret_cast<f32x4*>(p + f0) = acc;
+          } else if (xvec == 2) {
+            if (f0 < IN) *reinterpret_cast<f32x2_t*>(p + f0) = f32x2_t{acc[0], acc[1]};
+            if (f0 + 2 < IN) *reinterpret_cast<f32x2_t*>(p + f0 + 2) = f32x2_t{acc[2], acc[3]};
+          } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int f = 16 * kt + 4 * g + i;
-            if (f < IN) p[f] = acc[i];
+            for (int i = 0; i < 4; ++i)
+              if (f0 + i < IN) p[f0 + i] = acc[i];
           }
         }
       }
@@ -445,6 +476,13 @@ hipError_t dispatch(int U, int IN, F&& f) {
   return hipErrorInvalidValue;
 }
 
+int row_vec(const void* p, int IN) {
+  const uintptr_t u = (uintptr_t)p;
+  if ((IN & 3) == 0 && (u & 15) == 0) return 4;
+  if ((IN & 1) == 0 && (u & 7) == 0) return 2;
+  return 1;
+}
+
 }  // namespace
 
 namespace sml {
@@ -468,7 +506,7 @@ int lstm_fused_slabs(int64_t B) { return (int)((B + 16 * WAVES - 1) / (16 * WAVE
 hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw, const float* b, const float* h0,
                                  const float* c0, float* hseq, void* cseq_bf16, void* gates_bf16, int64_t B, int T,
                                  int IN, int U, int act, hipStream_t stream) {
-  FusedFwdArgs a{x, W, Uw, b, h0, c0, hseq, (__bf16*)cseq_bf16, (__bf16*)gates_bf16, B, T, IN, act};
+  FusedFwdArgs a{x, W, Uw, b, h0, c0, hseq, (__bf16*)cseq_bf16, (__bf16*)gates_bf16, B, T, IN, act, row_vec(x, IN)};
   return dispatch(U, IN, [&](auto u, auto k) { return launch_fwd<decltype(u)::value, decltype(k)::value>(a, stream); });
 }
 
@@ -477,7 +515,7 @@ hipError_t lstm_fused_bwd_launch(const float* dh, const void* gates_bf16, const 
                                  float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
                                  int act, int dh_last_only, hipStream_t stream) {
   FusedBwdArgs a{dh,       (const __bf16*)gates_bf16, (const __bf16*)cseq_bf16, hseq, x, h0, c0, W, Uw, dx, dh0, dc0,
-                 partials, B,  T,  IN, act, dh_last_only};
+                 partials, B,  T,  IN, act, dh_last_only, dx ? row_vec(dx, IN) : 1};
   return dispatch(U, IN, [&](auto u, auto k) { return launch_bwd<decltype(u)::value, decltype(k)::value>(a, stream); });
 }
 

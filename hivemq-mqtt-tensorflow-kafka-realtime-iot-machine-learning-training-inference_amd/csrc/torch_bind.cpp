@@ -343,8 +343,11 @@ std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W,
   if (c0.has_value()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * U, "c0 must be [B, U]");
   c10::hip::HIPGuard guard(x.device().index());
   auto h = at::empty({B, T, U}, x.options());
-  auto c = at::empty({B, T, U}, x.options().dtype(at::kBFloat16));   // cell state: saved for BPTT only
-  auto gt = at::empty({B, T, 4 * U}, x.options().dtype(at::kBFloat16));
+  // cell state and gates: saved for BPTT only, in the kernels' fragment-native order,
+  // padded to whole 16-sequence waves (lstm_fused.hip header)
+  const int64_t Bp = (B + 15) / 16 * 16;
+  auto c = at::empty({Bp, T, U}, x.options().dtype(at::kBFloat16));
+  auto gt = at::empty({Bp, T, 4 * U}, x.options().dtype(at::kBFloat16));
   SML_CHECK_HIP(sml::lstm_fused_fwd_launch(x.data_ptr<float>(), W.data_ptr<float>(), Uw.data_ptr<float>(),
                                            b.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0), h.data_ptr<float>(),
                                            c.data_ptr(), gt.data_ptr(), B, (int)T, (int)IN, (int)U, (int)act,
@@ -368,8 +371,11 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& g
   const int64_t B = x.size(0), T = x.size(1), IN = x.size(2), U = Uw.size(0);
   TORCH_CHECK(dh.is_contiguous() && cseq.is_contiguous() && hseq.is_contiguous() && x.is_contiguous(),
               "inputs must be contiguous");
-  TORCH_CHECK(hseq.size(0) == B && hseq.size(1) == T && hseq.size(2) == U && cseq.sizes() == hseq.sizes() &&
-              gates.size(2) == 4 * U, "shape mismatch");
+  const int64_t Bp = (B + 15) / 16 * 16;
+  TORCH_CHECK(hseq.size(0) == B && hseq.size(1) == T && hseq.size(2) == U, "h shape mismatch");
+  TORCH_CHECK(cseq.dim() == 3 && cseq.size(0) == Bp && cseq.size(1) == T && cseq.size(2) == U && gates.dim() == 3 &&
+              gates.size(0) == Bp && gates.size(1) == T && gates.size(2) == 4 * U,
+              "c / gates must be the padded buffers lstm_fused_fwd returned");
   if (dh_last_only) {
     TORCH_CHECK(dh.dim() == 2 && dh.size(0) == B && dh.size(1) == U, "dh must be [B, U] (h_T only)");
   } else {
