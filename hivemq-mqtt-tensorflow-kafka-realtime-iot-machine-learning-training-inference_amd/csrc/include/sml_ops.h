@@ -51,10 +51,10 @@ int lstm_fused_slab(int U, int IN);
 int lstm_fused_waves(int64_t B);
 int lstm_fused_slabs(int64_t B);  // one weight-gradient slab per workgroup
 hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw, const float* b, const float* h0,
-                                 const float* c0, float* hseq, void* cseq_bf16, void* gates_bf16, int64_t B, int T,
-                                 int IN, int U, int act, hipStream_t stream);
-hipError_t lstm_fused_bwd_launch(const float* dh, const void* gates_bf16, const void* cseq_bf16, const float* hseq,
-                                 const float* x, const float* h0, const float* c0, const float* W, const float* Uw,
+                                 const float* c0, float* hseq, void* cseq_bf16, int64_t B, int T, int IN, int U,
+                                 int act, hipStream_t stream);
+hipError_t lstm_fused_bwd_launch(const float* dh, const void* cseq_bf16, const float* hseq, const float* x,
+                                 const float* h0, const float* c0, const float* W, const float* Uw, const float* b,
                                  float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
                                  int act, int dh_last_only, hipStream_t stream);
 

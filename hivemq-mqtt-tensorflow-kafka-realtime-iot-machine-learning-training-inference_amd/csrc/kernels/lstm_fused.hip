@@ -8,13 +8,17 @@
 // Why: at the BASELINE config-3 shapes (B*T = 409 600 rows, 4u = 128 gates) the
 // unfused layer moved ~2 GB per training step through HBM (x.W written as Zx and
 // re-read, fp32 gates, dz written and re-read by three weight-gradient / dX
-// GEMMs).  Fused, a layer reads x, h, c and bf16 gates once per pass:
+// GEMMs).  Fused, the forward writes h (fp32, the layer output) and a bf16 cell
+// state; the backward reads x, h, c and dh once and RECOMPUTES the gates:
 //
 //   forward, per step t (one wave = 16 sequences, h / c in VGPRs):
 //     z^T[4u,16] = b + W^T . x_t^T + U^T . h_{t-1}^T     (all on MFMA)
-//     gates -> bf16 store (for BPTT), c_t, h_t -> fp32 store
+//     c_t -> bf16 store (for BPTT), h_t -> fp32 store
 //   backward, per step t = T-1 .. 0:
-//     dz_t from (dh_t + U.dz_{t+1}) and the stored gates / cell state
+//     z^T recomputed from x_t, h_{t-1} (which the weight gradients read anyway):
+//       (KT + U/16) * 4U/16 MFMAs instead of 8U bytes per sequence-step written by
+//       the forward and read back here -- the kernels are HBM-bound, MFMA is idle
+//     dz_t from (dh_t + U.dz_{t+1}), the gates and the cell state
 //     dh_{t-1}^T = U . dz_t^T                (critical path, MFMA)
 //     dX_t^T     = W . dz_t^T                (MFMA, optional)
 //     dW^T += dz_t^T . x_t,  dU^T += dz_t^T . h_{t-1},  db += colsum(dz_t) (fp32)
@@ -24,13 +28,13 @@
 //     Each wave writes one fp32 slab of [dW^T | dU^T | db]; slab_sum_kernel
 //     (dense.hip) reduces the slabs deterministically.
 //
-// Saved-state layout ("fragment-native"): gates and cell state are only ever read
-// back by the backward kernel, by the same lane of the same wave that wrote them,
-// so they are stored in MFMA C-fragment order, not [B, T, 4U]:
-//   gates[wave][t][tile 0..MT)[lane 0..64)[4] bf16,  cseq[wave][t][tile 0..UB)[lane][4]
+// Saved-state layout ("fragment-native"): the cell state is only ever read back by
+// the backward kernel, by the same lane of the same wave that wrote it, so it is
+// stored in MFMA C-fragment order, not [B, T, U]:
+//   cseq[wave][t][tile 0..U/16)[lane 0..64)[4] bf16
 // Every store / load of a 16-sequence tile is then ONE contiguous 512-byte access per
-// wave instead of 16 scattered 32-byte pieces (rows T*4U*2 bytes apart), and the
-// buffers are padded to whole waves (16 sequences) so no lane needs a bounds check.
+// wave instead of 16 scattered 32-byte pieces (rows T*U*2 bytes apart), and the
+// buffer is padded to whole waves (16 sequences) so no lane needs a bounds check.
 //
 // MFMA orientation (v_mfma_f32_16x16x16_bf16, lane c = l & 15, g = l >> 4):
 //   C tile mt of z: lane (c, g) holds gate 16mt + 4g + i of sequence s0 + c, so
@@ -59,6 +63,39 @@ __device__ __forceinline__ f32x4 unpack4(bf16x4 v) {
   return r;
 }
 
+// The lane id through an empty asm: the compiler cannot treat addresses built from it
+// as loop-invariant, so LDS operand reads are not hoisted into (scarce) registers.
+__device__ __forceinline__ int opaque_lane(int lane) {
+  asm volatile("" : "+v"(lane));
+  return lane;
+}
+
+// Four consecutive row elements p[k0 .. k0+3], XV floats per load, in two halves:
+// load_row4 issues the loads from clamped in-row addresses (never out of bounds, never
+// under a lane mask) and mask_row4 zeroes the columns past IN.  The mask is applied
+// where the value is CONSUMED: a select right after the load would make the wave wait
+// for the load there, which is what the prefetch exists to avoid.
+template <int XV>
+__device__ __forceinline__ f32x4 load_row4(const float* p, int k0, int IN) {
+  if constexpr (XV == 4) {
+    return *reinterpret_cast<const f32x4*>(p + (k0 < IN ? k0 : 0));
+  } else if constexpr (XV == 2) {
+    const f32x2_t lo = *reinterpret_cast<const f32x2_t*>(p + (k0 < IN ? k0 : 0));
+    const f32x2_t hi = *reinterpret_cast<const f32x2_t*>(p + (k0 + 2 < IN ? k0 + 2 : 0));
+    return f32x4{lo[0], lo[1], hi[0], hi[1]};
+  } else {
+    f32x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = p[k0 + j < IN ? k0 + j : 0];
+    return r;
+  }
+}
+__device__ __forceinline__ f32x4 mask_row4(f32x4 r, int k0, int IN) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = k0 + j < IN ? r[j] : 0.f;
+  return r;
+}
+
 struct FusedFwdArgs {
   const float* x;      // [B, T, IN]
   const float* W;      // [IN, 4U]
@@ -68,13 +105,11 @@ struct FusedFwdArgs {
   const float* c0;     // [B, U] or null
   float* hseq;         // [B, T, U]
   __bf16* cseq;        // [B/16, T, U/16, 64, 4]   cell state, bf16, fragment-native (backward only)
-  __bf16* gates;       // [B/16, T, 4U/16, 64, 4]  post-activation i, f, c~, o, fragment-native
   int64_t B;
   int T, IN, act;
-  int xvec;            // x row access width in floats (4 / 2 / 1), from IN and x's alignment
 };
 
-template <int U, int KT>
+template <int U, int KT, int XV, int ACT>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdArgs a) {
   constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
@@ -124,34 +159,20 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
   }
   // x_t^T as B operand: B[k = feature 16kt + 4g + j][n = sequence c]
   const float* xrow = a.x + sq * (int64_t)T * IN;
-  const int xvec = a.xvec;   // wave-uniform
   auto load_x = [&](int t, f32x4* v) {
     const float* p = xrow + (int64_t)t * IN;
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-      const int k0 = 16 * kt + 4 * g;
-      if (xvec == 4) {                       // one dwordx4 per tile
-        v[kt] = k0 < IN ? *reinterpret_cast<const f32x4*>(p + k0) : f32x4{0.f, 0.f, 0.f, 0.f};
-      } else if (xvec == 2) {                // two dwordx2 (rows 8-byte aligned)
-        const f32x2_t lo = k0 < IN ? *reinterpret_cast<const f32x2_t*>(p + k0) : f32x2_t{0.f, 0.f};
-        const f32x2_t hi = k0 + 2 < IN ? *reinterpret_cast<const f32x2_t*>(p + k0 + 2) : f32x2_t{0.f, 0.f};
-        v[kt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[kt][j] = k0 + j < IN ? p[k0 + j] : 0.f;
-      }
-    }
+    for (int kt = 0; kt < KT; ++kt) v[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN);
   };
   const int64_t wv = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
-  __bf16* gw = a.gates + wv * T * (int64_t)(MT * 256) + lane * 4;
   __bf16* cw = a.cseq + wv * T * (int64_t)(UB * 256) + lane * 4;
   f32x4 xn[KT];
   load_x(0, xn);
   for (int t = 0; t < T; ++t) {
     bf16x4 xb[KT];
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) xb[kt] = pack4(xn[kt]);
-    if (t + 1 < T) load_x(t + 1, xn);   // next step's input, in flight during this step
+    for (int kt = 0; kt < KT; ++kt) xb[kt] = pack4(mask_row4(xn[kt], 16 * kt + 4 * g, IN));
+    load_x(t + 1 < T ? t + 1 : t, xn);   // next step's input, in flight during this step (branch-free)
     f32x4 z[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -162,7 +183,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
       for (int s = 0; s < UB; ++s) z[mt] = mfma16(ut[mt][s], hb[s], z[mt]);
     }
     const int64_t bu = (sq * T + t) * (int64_t)U;
-    __bf16* gt = gw + (int64_t)t * (MT * 256);
     __bf16* ct = cw + (int64_t)t * (UB * 256);
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
@@ -171,16 +191,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
       for (int i = 0; i < 4; ++i) {
         gi[i] = sigmoid_fast(z[b][i]);
         gf[i] = sigmoid_fast(z[UB + b][i]);
-        gc[i] = act_f(a.act, z[2 * UB + b][i]);
+        gc[i] = act_f(ACT, z[2 * UB + b][i]);
         go[i] = sigmoid_fast(z[3 * UB + b][i]);
         cs[b][i] = fmaf(gf[i], cs[b][i], gi[i] * gc[i]);
-        h[b][i] = go[i] * act_f(a.act, cs[b][i]);
+        h[b][i] = go[i] * act_f(ACT, cs[b][i]);
       }
-      // padded lanes (seq >= B) write their own padded slots: no bounds check
-      *reinterpret_cast<bf16x4*>(gt + b * 256) = pack4(gi);
-      *reinterpret_cast<bf16x4*>(gt + (UB + b) * 256) = pack4(gf);
-      *reinterpret_cast<bf16x4*>(gt + (2 * UB + b) * 256) = pack4(gc);
-      *reinterpret_cast<bf16x4*>(gt + (3 * UB + b) * 256) = pack4(go);
+      // padded lanes (seq >= B) write their own padded slot: no bounds check
       *reinterpret_cast<bf16x4*>(ct + b * 256) = pack4(cs[b]);
       if (valid) *reinterpret_cast<f32x4*>(a.hseq + bu + 16 * b + 4 * g) = h[b];
       hb[b] = pack4(h[b]);
@@ -190,14 +206,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
 
 struct FusedBwdArgs {
   const float* dh;     // [B, T, U]  gradient w.r.t. the h sequence ([B, U] of h_T when dh_last_only)
-  const __bf16* gates; // fragment-native, as written by the forward kernel
-  const __bf16* cseq;  // fragment-native
+  const __bf16* cseq;  // fragment-native, as written by the forward kernel
   const float* hseq;   // [B, T, U]
   const float* x;      // [B, T, IN]
   const float* h0;     // [B, U] or null
   const float* c0;     // [B, U] or null
   const float* W;      // [IN, 4U]
   const float* Uw;     // [U, 4U]
+  const float* bias;   // [4U]
   float* dx;           // [B, T, IN] or null
   float* dh0;          // [B, U] or null
   float* dc0;          // [B, U] or null
@@ -205,51 +221,72 @@ struct FusedBwdArgs {
   int64_t B;
   int T, IN, act;
   int dh_last_only;    // return_sequences=False: only h_T received a gradient (no [B, T, U] zeros read)
-  int xvec;            // dx row access width in floats (4 / 2 / 1)
+  int dxvec;           // dx row write width in floats
 };
 
-template <int U, int KT>
+template <int U, int KT, int XV, int ACT>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdArgs a) {
   constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
   constexpr int LDW = 16 * KT;
   constexpr int S = G4 * (LDW + U + 1);
-  __shared__ __attribute__((aligned(16))) char scratch[WAVES][MT * 512];
+  constexpr int NTR = MT + KT + UB;                 // LDS transposes per step: dz tiles, x tiles, h tiles
+  __shared__ __attribute__((aligned(16))) char scratch[WAVES][NTR * 512];
   __shared__ __attribute__((aligned(16))) float slab[S];   // the workgroup's combined weight-gradient slab
+  // Weight A fragments, shared by the 4 waves, [tile][lane] bf16x4 (conflict-free
+  // ds_read_b64), read in the loop through an opaque lane offset so the compiler cannot
+  // hoist all of them into registers (that costs ~130 registers and spills):
+  //   wfwd: W^T / U^T (forward orientation, gate recompute), ufl: U (dh), wfl: W (dX)
+  __shared__ __attribute__((aligned(16))) bf16x4 wfwd[MT * (KT + UB) * 64];
+  __shared__ __attribute__((aligned(16))) bf16x4 ufl[UB * MT * 64];
+  __shared__ __attribute__((aligned(16))) bf16x4 wfl[KT * MT * 64];
+  __shared__ __attribute__((aligned(16))) float sbias[G4];
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int w = threadIdx.x >> 6;
   const int64_t wave_id = (int64_t)blockIdx.x * WAVES + w;
   const int64_t s0 = wave_id * 16;
-  const bool active = s0 < a.B;  // waves past B contribute zeros (they still join the slab barriers)
+  const bool active = s0 < a.B;  // waves past B contribute zeros (they still join the block barriers)
   const int64_t seq = s0 + c;
   const bool valid = seq < a.B;
   const int64_t sq = valid ? seq : a.B - 1;
   const int IN = a.IN, T = a.T;
   char* scr = scratch[w];
   for (int i = threadIdx.x; i < S; i += WAVES * 64) slab[i] = 0.f;
+  for (int i = threadIdx.x; i < G4; i += WAVES * 64) sbias[i] = a.bias[i];
+  // tile (mt, k) of [W^T | U^T]: k < KT -> W^T[m = gate 16mt + c][feature 16k + 4g + j],
+  //                              k >= KT -> U^T[m = gate][unit 16(k-KT) + 4g + j]
+  for (int tile = w; tile < MT * (KT + UB); tile += WAVES) {
+    const int mt = tile / (KT + UB), k = tile % (KT + UB);
+    f32x4 t4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (k < KT) {
+        const int f = 16 * k + 4 * g + j;
+        t4[j] = f < IN ? a.W[(int64_t)f * G4 + 16 * mt + c] : 0.f;
+      } else {
+        t4[j] = a.Uw[(16 * (k - KT) + 4 * g + j) * G4 + 16 * mt + c];
+      }
+    }
+    wfwd[tile * 64 + lane] = pack4(t4);
+  }
 
-  // A fragments: U[m = unit][k = gate] (for dh), W[m = feature][k = gate] (for dX)
-  bf16x4 uf[UB][MT];
-#pragma unroll
-  for (int b = 0; b < UB; ++b)
-#pragma unroll
-    for (int kt = 0; kt < MT; ++kt) {
-      f32x4 t4;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) t4[j] = a.Uw[(16 * b + c) * G4 + 16 * kt + 4 * g + j];
-      uf[b][kt] = pack4(t4);
-    }
+  // A fragments: U[m = unit 16b + c][k = gate 16kt + 4g + j] (for dh), W[m = feature][k = gate] (for dX)
   const bool want_dx = a.dx != nullptr;
-  bf16x4 wf[KT][MT];
+  for (int tile = w; tile < UB * MT; tile += WAVES) {
+    const int b = tile / MT, kt = tile % MT;
+    f32x4 t4;
 #pragma unroll
-  for (int kt = 0; kt < KT; ++kt)
+    for (int j = 0; j < 4; ++j) t4[j] = a.Uw[(16 * b + c) * G4 + 16 * kt + 4 * g + j];
+    ufl[tile * 64 + lane] = pack4(t4);
+  }
+  for (int tile = w; tile < KT * MT; tile += WAVES) {
+    const int kt = tile / MT, mt = tile % MT;
+    const int f = 16 * kt + c;
+    f32x4 t4;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      f32x4 t4;
-      const int f = 16 * kt + c;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) t4[j] = (want_dx && f < IN) ? a.W[(int64_t)f * G4 + 16 * mt + 4 * g + j] : 0.f;
-      wf[kt][mt] = pack4(t4);
-    }
+    for (int j = 0; j < 4; ++j) t4[j] = (want_dx && f < IN) ? a.W[(int64_t)f * G4 + 16 * mt + 4 * g + j] : 0.f;
+    wfl[tile * 64 + lane] = pack4(t4);
+  }
+  __syncthreads();   // weight fragments / sbias visible
 
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
   f32x4 accW[MT][KT], accU[MT][UB];
@@ -266,88 +303,127 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
   for (int b = 0; b < UB; ++b) dhr[b] = dcn[b] = zero4;
 
-  // per-step operands; "C layout" ones indexed by this lane's sequence, the
-  // weight-gradient B operands by rows (sequences) s0 + 4g + j
-  // c_t is carried from the previous (later) step's c_{t-1} load: every c is read once
+  // Per-step operands, all in C orientation (lane c = this lane's sequence): the
+  // forward's inputs x_t and h_{t-1} (gates are recomputed from them instead of being
+  // stored: 8U bytes per sequence-step less written AND read), c_{t-1}, dh_t.
+  // c_t is carried from the previous (later) step's c_{t-1} load: every c is read once.
   struct Step {
-    bf16x4 gi[UB], gf[UB], gc[UB], go[UB];
     bf16x4 cprev[UB];
     f32x4 dho[UB];
-    f32x4 hprev[UB];   // B[k = seq 4g + j][n = unit 16kb + c]
-    f32x4 xt[KT];      // B[k = seq 4g + j][n = feature 16kt + c]
+    f32x4 hp[UB];      // h_{t-1}[sequence c][unit 16b + 4g + i]
+    f32x4 xt[KT];      // x_t[sequence c][feature 16kt + 4g + j]
   };
-  const __bf16* gw = a.gates + wave_id * T * (int64_t)(MT * 256) + lane * 4;
   const __bf16* cw = a.cseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
-  const int xvec = a.xvec;   // wave-uniform
-  auto load_step = [&](int t, Step& st) {
-    const int64_t bu = (sq * T + t) * (int64_t)U;
-    const __bf16* gt = gw + (int64_t)t * (MT * 256);
+  // Loads are unconditional from in-bounds addresses (padding lanes read row B-1),
+  // with zeros selected afterwards: no exec-masked branches and no waits in the loop.
+  auto load_common = [&](int t, Step& st) {   // raw values; masks are applied in step()
+    const float* dhp = a.dh_last_only ? a.dh + sq * U : a.dh + (sq * T + t) * (int64_t)U;
+#pragma unroll
+    for (int b = 0; b < UB; ++b) st.dho[b] = *reinterpret_cast<const f32x4*>(dhp + 16 * b + 4 * g);
+    const float* p = a.x + (sq * T + t) * (int64_t)IN;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) st.xt[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN);
+  };
+  auto load_step = [&](int t, Step& st) {   // t >= 1
     const __bf16* cp = cw + (int64_t)(t - 1) * (UB * 256);
+    const float* hrow = a.hseq + (sq * T + t - 1) * (int64_t)U;
+#pragma unroll
+    for (int b = 0; b < UB; ++b) {
+      st.cprev[b] = ld_bf16x4(cp + b * 256);
+      st.hp[b] = *reinterpret_cast<const f32x4*>(hrow + 16 * b + 4 * g);
+    }
+    load_common(t, st);
+  };
+  auto load_step0 = [&](Step& st) {         // t = 0: initial state (once per sequence)
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
       const int off = 16 * b + 4 * g;
-      st.gi[b] = ld_bf16x4(gt + b * 256);
-      st.gf[b] = ld_bf16x4(gt + (UB + b) * 256);
-      st.gc[b] = ld_bf16x4(gt + (2 * UB + b) * 256);
-      st.go[b] = ld_bf16x4(gt + (3 * UB + b) * 256);
-      if (t > 0) st.cprev[b] = ld_bf16x4(cp + b * 256);
-      else if (a.c0) st.cprev[b] = pack4(*reinterpret_cast<const f32x4*>(a.c0 + sq * U + off));
-      else st.cprev[b] = pack4(zero4);
-      if (a.dh_last_only) st.dho[b] = (valid && t == T - 1) ? *reinterpret_cast<const f32x4*>(a.dh + sq * U + off) : zero4;
-      else st.dho[b] = valid ? *reinterpret_cast<const f32x4*>(a.dh + bu + off) : zero4;
+      st.cprev[b] = a.c0 ? pack4(*reinterpret_cast<const f32x4*>(a.c0 + sq * U + off)) : pack4(zero4);
+      st.hp[b] = a.h0 ? *reinterpret_cast<const f32x4*>(a.h0 + sq * U + off) : zero4;
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t r = s0 + 4 * g + j;
-      const bool rok = r < a.B;
-      const int64_t rr = rok ? r : 0;
-#pragma unroll
-      for (int kb = 0; kb < UB; ++kb) {
-        const int u = 16 * kb + c;
-        float hv = 0.f;
-        if (rok) {
-          if (t > 0) hv = a.hseq[(rr * T + t - 1) * (int64_t)U + u];
-          else if (a.h0) hv = a.h0[rr * U + u];
-        }
-        st.hprev[kb][j] = hv;
-      }
-#pragma unroll
-      for (int kt = 0; kt < KT; ++kt) {
-        const int f = 16 * kt + c;
-        st.xt[kt][j] = (rok && f < IN) ? a.x[(rr * T + t) * (int64_t)IN + f] : 0.f;
-      }
-    }
+    load_common(0, st);
+  };
+  auto load_any = [&](int t, Step& st) {
+    if (t > 0) load_step(t, st);
+    else load_step0(st);
   };
 
-  Step cur, nxt;
   f32x4 ctc[UB];   // c_t
 #pragma unroll
   for (int b = 0; b < UB; ++b)
     ctc[b] = active ? unpack4(ld_bf16x4(cw + (int64_t)(T - 1) * (UB * 256) + b * 256)) : zero4;
-  if (active) load_step(T - 1, nxt);
-  for (int t = T - 1; t >= 0 && active; --t) {
-    cur = nxt;
-    if (t > 0) load_step(t - 1, nxt);          // in flight during this step
+
+  // Weight gradients, contracted over the wave's 16 sequences: dz_t^T as A operand and
+  // x_t / h_{t-1} as B operands [k = sequence][n = feature | unit], each one LDS transpose
+  // of the C-orientation tile (padding lanes carry dz = 0, so their rows add nothing).
+  // Software-pipelined one step behind the recurrence: step t issues the (independent)
+  // weight-gradient MFMAs of step t+1 between its gate-recompute MFMAs and its gate
+  // arithmetic, so the MFMA and VALU pipes overlap inside one wave (the kernel runs at
+  // one wave per SIMD: there is no other wave to hide either behind).
+  bf16x4 pdz[MT], pxb[KT], phb[UB];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) pdz[mt] = pack4(zero4);
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) pxb[kt] = pack4(zero4);
+#pragma unroll
+  for (int s = 0; s < UB; ++s) phb[s] = pack4(zero4);
+  auto wgrad = [&]() {
+    bf16x4 hB[UB], xB[KT];
+#pragma unroll
+    for (int kb = 0; kb < UB; ++kb) hB[kb] = lds_transpose(phb[kb], scr + (MT + KT + kb) * 512, c, g);
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) xB[kt] = lds_transpose(pxb[kt], scr + (MT + kt) * 512, c, g);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const bf16x4 adz = lds_transpose(pdz[mt], scr + mt * 512, c, g);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) accW[mt][kt] = mfma16(adz, xB[kt], accW[mt][kt]);
+#pragma unroll
+      for (int kb = 0; kb < UB; ++kb) accU[mt][kb] = mfma16(adz, hB[kb], accU[mt][kb]);
+    }
+  };
+
+  auto step = [&](int t, const Step& cur) {
+    const int ol = opaque_lane(lane);   // re-materialised per step: fragment reads stay in the loop
+    // gate recompute: z^T = b + W^T . x_t^T + U^T . h_{t-1}^T, the forward's exact
+    // operands and accumulation order (bit-identical pre-activations)
+    bf16x4 xb[KT], hb[UB];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) xb[kt] = pack4(mask_row4(cur.xt[kt], 16 * kt + 4 * g, IN));
+    const bool take_dh = valid && (!a.dh_last_only || t == T - 1);
+#pragma unroll
+    for (int s = 0; s < UB; ++s) hb[s] = pack4(cur.hp[s]);
+    f32x4 z[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      z[mt] = *reinterpret_cast<const f32x4*>(sbias + 16 * mt + (ol >> 4) * 4);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) z[mt] = mfma16(wfwd[(mt * (KT + UB) + kt) * 64 + ol], xb[kt], z[mt]);
+#pragma unroll
+      for (int s = 0; s < UB; ++s) z[mt] = mfma16(wfwd[(mt * (KT + UB) + KT + s) * 64 + ol], hb[s], z[mt]);
+    }
+    wgrad();                                    // step t+1's weight gradients (zeros on the first step)
     f32x4 cp[UB];                               // c_{t-1}
 #pragma unroll
     for (int b = 0; b < UB; ++b) cp[b] = unpack4(cur.cprev[b]);
     f32x4 dzt[MT];
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
-      const f32x4 gi = unpack4(cur.gi[b]), gf = unpack4(cur.gf[b]), gc = unpack4(cur.gc[b]),
-                  go = unpack4(cur.go[b]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float dh = cur.dho[b][i] + dhr[b][i];
+        // fp32 gates, exactly the values the forward used for c_t / h_t
+        const float gi = sigmoid_fast(z[b][i]), gf = sigmoid_fast(z[UB + b][i]);
+        const float gc = act_f(ACT, z[2 * UB + b][i]), go = sigmoid_fast(z[3 * UB + b][i]);
+        const float dh = (take_dh ? cur.dho[b][i] : 0.f) + dhr[b][i];
         const float ct = ctc[b][i];
-        const float ac = act_f(a.act, ct);
-        const float dc = dcn[b][i] + dh * go[i] * act_d(a.act, ct, ac);
-        dzt[b][i] = dc * gc[i] * gi[i] * (1.f - gi[i]);
-        dzt[UB + b][i] = dc * cp[b][i] * gf[i] * (1.f - gf[i]);
-        const float gcd = a.act == ACT_RELU ? (gc[i] > 0.f ? 1.f : 0.f) : fmaf(-gc[i], gc[i], 1.f);
-        dzt[2 * UB + b][i] = dc * gi[i] * gcd;
-        dzt[3 * UB + b][i] = dh * ac * go[i] * (1.f - go[i]);
-        dcn[b][i] = dc * gf[i];
+        const float ac = act_f(ACT, ct);
+        const float dc = dcn[b][i] + dh * go * act_d(ACT, ct, ac);
+        dzt[b][i] = dc * gc * gi * (1.f - gi);
+        dzt[UB + b][i] = dc * cp[b][i] * gf * (1.f - gf);
+        const float gcd = ACT == ACT_RELU ? (gc > 0.f ? 1.f : 0.f) : fmaf(-gc, gc, 1.f);
+        dzt[2 * UB + b][i] = dc * gi * gcd;
+        dzt[3 * UB + b][i] = dh * ac * go * (1.f - go);
+        dcn[b][i] = dc * gf;
       }
       ctc[b] = cp[b];   // c_{t-1} is the next (earlier) step's c_t
     }
@@ -366,7 +442,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     for (int b = 0; b < UB; ++b) {
       f32x4 acc = zero4;
 #pragma unroll
-      for (int kt = 0; kt < MT; ++kt) acc = mfma16(uf[b][kt], dzb[kt], acc);
+      for (int kt = 0; kt < MT; ++kt) acc = mfma16(ufl[(b * MT + kt) * 64 + ol], dzb[kt], acc);
       dhr[b] = acc;
     }
     // input gradient dX_t^T = W . dz_t^T
@@ -375,13 +451,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       for (int kt = 0; kt < KT; ++kt) {
         f32x4 acc = zero4;
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc = mfma16(wf[kt][mt], dzb[mt], acc);
+        for (int mt = 0; mt < MT; ++mt) acc = mfma16(wfl[(kt * MT + mt) * 64 + ol], dzb[mt], acc);
         if (valid) {
           float* p = a.dx + (sq * T + t) * (int64_t)IN;
           const int f0 = 16 * kt + 4 * g;
-          if (xvec == 4) {
+          if (a.dxvec == 4) {
             if (f0 < IN) *reinterpret_cast<f32x4*>(p + f0) = acc;
-          } else if (xvec == 2) {
+          } else if (a.dxvec == 2) {
             if (f0 < IN) *reinterpret_cast<f32x2_t*>(p + f0) = f32x2_t{acc[0], acc[1]};
             if (f0 + 2 < IN) *reinterpret_cast<f32x2_t*>(p + f0 + 2) = f32x2_t{acc[2], acc[3]};
           } else {
@@ -392,21 +468,25 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
         }
       }
     }
-    // weight gradients: dz_t^T as A operand (one LDS transpose per gate tile)
-    bf16x4 hB[UB], xB[KT];
+    // operands of this step's weight gradients, consumed one step later
 #pragma unroll
-    for (int kb = 0; kb < UB; ++kb) hB[kb] = pack4(cur.hprev[kb]);
+    for (int mt = 0; mt < MT; ++mt) pdz[mt] = dzb[mt];
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) xB[kt] = pack4(cur.xt[kt]);
+    for (int kt = 0; kt < KT; ++kt) pxb[kt] = xb[kt];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const bf16x4 adz = lds_transpose(dzb[mt], scr + mt * 512, c, g);
-#pragma unroll
-      for (int kt = 0; kt < KT; ++kt) accW[mt][kt] = mfma16(adz, xB[kt], accW[mt][kt]);
-#pragma unroll
-      for (int kb = 0; kb < UB; ++kb) accU[mt][kb] = mfma16(adz, hB[kb], accU[mt][kb]);
+    for (int s = 0; s < UB; ++s) phb[s] = hb[s];
+  };
 
+  // the next step's operands are in flight while the current one computes
+  if (active) {
+    Step cur, nxt;
+    load_any(T - 1, nxt);
+    for (int t = T - 1; t >= 0; --t) {
+      cur = nxt;
+      if (t >= 1) load_any(t - 1, nxt);
+      step(t, cur);
     }
+    wgrad();                                    // step 0's weight gradients
   }
   if (valid && active) {
 #pragma unroll
@@ -451,25 +531,40 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   for (int i = threadIdx.x; i < S; i += WAVES * 64) out[i] = slab[i];
 }
 
-template <int U, int KT>
+// activation as a template parameter: a runtime switch became ~40 scalar branches
+// per step, which split the time loop into basic blocks the scheduler cannot overlap
+template <int U, int KT, int XV>
 hipError_t launch_fwd(const FusedFwdArgs& a, hipStream_t st) {
   const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
-  hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  if (a.act == ACT_RELU)
+    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, ACT_RELU>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, ACT_TANH>), dim3(grid), dim3(WAVES * 64), 0, st, a);
   return hipGetLastError();
 }
 
-template <int U, int KT>
+template <int U, int KT, int XV>
 hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
   const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
-  hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  if (a.act == ACT_RELU)
+    hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, ACT_RELU>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, ACT_TANH>), dim3(grid), dim3(WAVES * 64), 0, st, a);
   return hipGetLastError();
 }
 
+// (U, KT bucket, x row vector width) -> instance
 template <typename F>
-hipError_t dispatch(int U, int IN, F&& f) {
+hipError_t dispatch(int U, int IN, int xv, F&& f) {
   const int KT = (IN + 15) / 16;
-#define SML_UK(u, k) \
-  if (U == u && KT <= k) return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{});
+#define SML_UK(u, k)                                                                                              \
+  if (U == u && KT <= k) {                                                                                        \
+    if (xv == 4) return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{},                     \
+                          std::integral_constant<int, 4>{});                                                      \
+    if (xv == 2) return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{},                     \
+                          std::integral_constant<int, 2>{});                                                      \
+    return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{}, std::integral_constant<int, 1>{}); \
+  }
   SML_UK(16, 1) SML_UK(16, 2) SML_UK(16, 4)
   SML_UK(32, 1) SML_UK(32, 2)
 #undef SML_UK
@@ -504,19 +599,23 @@ int lstm_fused_waves(int64_t B) { return (int)(((B + 16 * WAVES - 1) / (16 * WAV
 int lstm_fused_slabs(int64_t B) { return (int)((B + 16 * WAVES - 1) / (16 * WAVES)); }
 
 hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw, const float* b, const float* h0,
-                                 const float* c0, float* hseq, void* cseq_bf16, void* gates_bf16, int64_t B, int T,
-                                 int IN, int U, int act, hipStream_t stream) {
-  FusedFwdArgs a{x, W, Uw, b, h0, c0, hseq, (__bf16*)cseq_bf16, (__bf16*)gates_bf16, B, T, IN, act, row_vec(x, IN)};
-  return dispatch(U, IN, [&](auto u, auto k) { return launch_fwd<decltype(u)::value, decltype(k)::value>(a, stream); });
+                                 const float* c0, float* hseq, void* cseq_bf16, int64_t B, int T, int IN, int U, int act,
+                                 hipStream_t stream) {
+  FusedFwdArgs a{x, W, Uw, b, h0, c0, hseq, (__bf16*)cseq_bf16, B, T, IN, act};
+  return dispatch(U, IN, row_vec(x, IN), [&](auto u, auto k, auto v) {
+    return launch_fwd<decltype(u)::value, decltype(k)::value, decltype(v)::value>(a, stream);
+  });
 }
 
-hipError_t lstm_fused_bwd_launch(const float* dh, const void* gates_bf16, const void* cseq_bf16, const float* hseq,
-                                 const float* x, const float* h0, const float* c0, const float* W, const float* Uw,
+hipError_t lstm_fused_bwd_launch(const float* dh, const void* cseq_bf16, const float* hseq, const float* x,
+                                 const float* h0, const float* c0, const float* W, const float* Uw, const float* b,
                                  float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
                                  int act, int dh_last_only, hipStream_t stream) {
-  FusedBwdArgs a{dh,       (const __bf16*)gates_bf16, (const __bf16*)cseq_bf16, hseq, x, h0, c0, W, Uw, dx, dh0, dc0,
-                 partials, B,  T,  IN, act, dh_last_only, dx ? row_vec(dx, IN) : 1};
-  return dispatch(U, IN, [&](auto u, auto k) { return launch_bwd<decltype(u)::value, decltype(k)::value>(a, stream); });
+  FusedBwdArgs a{dh, (const __bf16*)cseq_bf16, hseq, x, h0, c0, W, Uw, b, dx, dh0, dc0, partials, B, T, IN, act,
+                 dh_last_only, dx ? row_vec(dx, IN) : 1};
+  return dispatch(U, IN, row_vec(x, IN), [&](auto u, auto k, auto v) {
+    return launch_bwd<decltype(u)::value, decltype(k)::value, decltype(v)::value>(a, stream);
+  });
 }
 
 }  // namespace sml

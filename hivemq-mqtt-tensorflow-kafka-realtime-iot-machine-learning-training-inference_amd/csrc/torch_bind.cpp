@@ -323,7 +323,7 @@ std::vector<at::Tensor> dense_wgrad(const at::Tensor& x, const at::Tensor& dy, i
   return {dW, db};
 }
 
-// Fully fused LSTM layer forward: x [B, T, IN] -> (h [B,T,U], c [B,T,U], gates bf16 [B,T,4U]).
+// Fully fused LSTM layer forward: x [B, T, IN] -> (h [B,T,U], c: bf16 cell state for lstm_fused_bwd).
 std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& Uw,
                                        const at::Tensor& b, const c10::optional<at::Tensor>& h0,
                                        const c10::optional<at::Tensor>& c0, int64_t act) {
@@ -343,23 +343,21 @@ std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W,
   if (c0.has_value()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * U, "c0 must be [B, U]");
   c10::hip::HIPGuard guard(x.device().index());
   auto h = at::empty({B, T, U}, x.options());
-  // cell state and gates: saved for BPTT only, in the kernels' fragment-native order,
-  // padded to whole 16-sequence waves (lstm_fused.hip header)
+  // cell state: saved for BPTT only, in the kernels' fragment-native order, padded to
+  // whole 16-sequence waves (lstm_fused.hip header); the gates are recomputed there
   const int64_t Bp = (B + 15) / 16 * 16;
   auto c = at::empty({Bp, T, U}, x.options().dtype(at::kBFloat16));
-  auto gt = at::empty({Bp, T, 4 * U}, x.options().dtype(at::kBFloat16));
   SML_CHECK_HIP(sml::lstm_fused_fwd_launch(x.data_ptr<float>(), W.data_ptr<float>(), Uw.data_ptr<float>(),
                                            b.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0), h.data_ptr<float>(),
-                                           c.data_ptr(), gt.data_ptr(), B, (int)T, (int)IN, (int)U, (int)act,
-                                           cur_stream(x)));
-  return {h, c, gt};
+                                           c.data_ptr(), B, (int)T, (int)IN, (int)U, (int)act, cur_stream(x)));
+  return {h, c};
 }
 
 // Fully fused LSTM layer backward -> [dx (or undefined), dW [IN,4U], dU [U,4U], db [4U], dh0, dc0].
-std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& gates, const at::Tensor& cseq,
-                                       const at::Tensor& hseq, const at::Tensor& x,
-                                       const c10::optional<at::Tensor>& h0, const c10::optional<at::Tensor>& c0,
-                                       const at::Tensor& W, const at::Tensor& Uw, int64_t act, bool want_dx,
+std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& cseq, const at::Tensor& hseq,
+                                       const at::Tensor& x, const c10::optional<at::Tensor>& h0,
+                                       const c10::optional<at::Tensor>& c0, const at::Tensor& W, const at::Tensor& Uw,
+                                       const at::Tensor& b, int64_t act, bool want_dx,
                                        bool want_state_grads, bool dh_last_only) {
   check_dev(dh, "dh", at::kFloat);
   check_dev(cseq, "c", at::kBFloat16);
@@ -367,15 +365,16 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& g
   check_dev(x, "x", at::kFloat);
   check_dev(W, "W", at::kFloat);
   check_dev(Uw, "U", at::kFloat);
-  TORCH_CHECK(gates.is_cuda() && gates.scalar_type() == at::kBFloat16 && gates.is_contiguous(), "gates: bf16");
+  check_dev(b, "b", at::kFloat);
   const int64_t B = x.size(0), T = x.size(1), IN = x.size(2), U = Uw.size(0);
   TORCH_CHECK(dh.is_contiguous() && cseq.is_contiguous() && hseq.is_contiguous() && x.is_contiguous(),
               "inputs must be contiguous");
   const int64_t Bp = (B + 15) / 16 * 16;
   TORCH_CHECK(hseq.size(0) == B && hseq.size(1) == T && hseq.size(2) == U, "h shape mismatch");
-  TORCH_CHECK(cseq.dim() == 3 && cseq.size(0) == Bp && cseq.size(1) == T && cseq.size(2) == U && gates.dim() == 3 &&
-              gates.size(0) == Bp && gates.size(1) == T && gates.size(2) == 4 * U,
-              "c / gates must be the padded buffers lstm_fused_fwd returned");
+  TORCH_CHECK(cseq.dim() == 3 && cseq.size(0) == Bp && cseq.size(1) == T && cseq.size(2) == U,
+              "c must be the padded buffer lstm_fused_fwd returned");
+  TORCH_CHECK(W.is_contiguous() && W.size(0) == IN && W.size(1) == 4 * U && Uw.is_contiguous() &&
+              Uw.size(1) == 4 * U && b.is_contiguous() && b.numel() == 4 * U, "weight shape mismatch");
   if (dh_last_only) {
     TORCH_CHECK(dh.dim() == 2 && dh.size(0) == B && dh.size(1) == U, "dh must be [B, U] (h_T only)");
   } else {
@@ -397,8 +396,8 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& g
   auto scratch = at::empty({std::max(1, sml::slab_sum_scratch(G, S))}, opts);
   auto st = cur_stream(x);
   SML_CHECK_HIP(sml::lstm_fused_bwd_launch(
-      dh.data_ptr<float>(), gates.data_ptr(), cseq.data_ptr(), hseq.data_ptr<float>(), x.data_ptr<float>(),
-      opt_ptr(h0), opt_ptr(c0), W.data_ptr<float>(), Uw.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
+      dh.data_ptr<float>(), cseq.data_ptr(), hseq.data_ptr<float>(), x.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0),
+      W.data_ptr<float>(), Uw.data_ptr<float>(), b.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
       want_state_grads ? dh0.data_ptr<float>() : nullptr, want_state_grads ? dc0.data_ptr<float>() : nullptr,
       partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U, (int)act, dh_last_only ? 1 : 0, st));
   SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
@@ -586,9 +585,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_fused_fwd", &lstm_fused_fwd, "fully fused LSTM layer forward (x.W + recurrence in one kernel)",
         py::arg("x"), py::arg("W"), py::arg("U"), py::arg("b"), py::arg("h0") = py::none(),
         py::arg("c0") = py::none(), py::arg("act") = 1);
-  m.def("lstm_fused_bwd", &lstm_fused_bwd, "fully fused LSTM layer backward (BPTT + dW/dU/db + dX in one kernel)",
-        py::arg("dh"), py::arg("gates"), py::arg("c"), py::arg("h"), py::arg("x"), py::arg("h0") = py::none(),
-        py::arg("c0") = py::none(), py::arg("W"), py::arg("U"), py::arg("act") = 1, py::arg("want_dx") = true,
+  m.def("lstm_fused_bwd", &lstm_fused_bwd,
+        "fully fused LSTM layer backward (gate recompute + BPTT + dW/dU/db + dX in one kernel)", py::arg("dh"),
+        py::arg("c"), py::arg("h"), py::arg("x"), py::arg("h0") = py::none(), py::arg("c0") = py::none(),
+        py::arg("W"), py::arg("U"), py::arg("b"), py::arg("act") = 1, py::arg("want_dx") = true,
         py::arg("want_state_grads") = false, py::arg("dh_last_only") = false);
   m.def("lstm_fused_supported", &sml::lstm_fused_supported, "whether (U, IN) has a fused LSTM kernel", py::arg("U"),
         py::arg("IN"));

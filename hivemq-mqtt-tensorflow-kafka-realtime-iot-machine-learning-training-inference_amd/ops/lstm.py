@@ -104,26 +104,25 @@ class LSTMFunction(torch.autograd.Function):
 
 
 class FusedLSTMFunction(torch.autograd.Function):
-    """Whole layer in two launches: ``lstm_fused_fwd`` (x.W + recurrence, bf16 gates
-    and cell state saved) and ``lstm_fused_bwd`` (BPTT + dW/dU/db accumulated in
-    registers + dX).  ``last_only`` (Keras ``return_sequences=False``) returns h_T
+    """Whole layer in two launches: ``lstm_fused_fwd`` (x.W + recurrence, bf16 cell
+    state saved) and ``lstm_fused_bwd`` (gate recompute + BPTT + dW/dU/db accumulated
+    in registers + dX).  ``last_only`` (Keras ``return_sequences=False``) returns h_T
     [B, U]; its backward reads only that [B, U] gradient instead of a [B, T, U]
     tensor of zeros."""
 
     @staticmethod
     def forward(ctx, x, W, U, b, act_code: int, last_only: bool = False):
-        h, c, gates = load_c().lstm_fused_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), None, None,
-                                              act_code)
-        ctx.save_for_backward(x, W, U, h, c, gates)
+        h, c = load_c().lstm_fused_fwd(x, W.contiguous(), U.contiguous(), b.contiguous(), None, None, act_code)
+        ctx.save_for_backward(x, W, U, b, h, c)
         ctx.act = act_code
         ctx.last_only = bool(last_only)
         return h[:, -1].contiguous() if last_only else h
 
     @staticmethod
     def backward(ctx, dh):
-        x, W, U, h, c, gates = ctx.saved_tensors
-        dx, dW, dU, db, _, _ = load_c().lstm_fused_bwd(dh.contiguous().float(), gates, c, h, x, None, None,
-                                                       W.contiguous(), U.contiguous(), ctx.act,
+        x, W, U, b, h, c = ctx.saved_tensors
+        dx, dW, dU, db, _, _ = load_c().lstm_fused_bwd(dh.contiguous().float(), c, h, x, None, None,
+                                                       W.contiguous(), U.contiguous(), b.contiguous(), ctx.act,
                                                        bool(ctx.needs_input_grad[0]), False, ctx.last_only)
         return (dx if ctx.needs_input_grad[0] else None), dW, dU, db, None, None
 

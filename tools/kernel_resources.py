@@ -25,8 +25,10 @@ def demangle(names):
 def main():
     src = sys.argv[1]
     filt = sys.argv[2] if len(sys.argv) > 2 else ""
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-munsafe-fp-atomics", "-mllvm",
-           "-amdgpu-mfma-vgpr-form", "-I", os.path.join(PKG, "csrc", "include"), "-c", src, "-o", "/dev/null",
+    with open(src) as f:   # same flags as _build.py (AGPR accumulators for files that ask for them)
+        vgpr_form = [] if "sml-build: agpr-accumulators" in f.read(512) else ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-munsafe-fp-atomics", *vgpr_form,
+           "-I", os.path.join(PKG, "csrc", "include"), "-c", src, "-o", "/dev/null",
            "--offload-device-only", "-Rpass-analysis=kernel-resource-usage"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     rows, cur = [], None
