@@ -1,0 +1,88 @@
+// Shared device helpers for the fused LSTM layer kernels (lstm_fused.hip: backward,
+// lstm_fused_fwd.hip: forward).  Included by exactly those two translation units; the
+// two are separate files because they want different MFMA register forms (the forward
+// keeps its gate accumulators in VGPRs, the backward its weight-gradient accumulators
+// in AGPRs -- see the build marker at the top of lstm_fused.hip).
+#pragma once
+#include "sml_common.h"
+#include "sml_ops.h"
+
+namespace sml_lstm {
+
+using namespace sml;
+
+constexpr int WAVES = 4;
+
+__device__ __forceinline__ float act_f(int a, float z) { return a == ACT_RELU ? relu_fast(z) : tanh_fast(z); }
+__device__ __forceinline__ float act_d(int a, float z, float y) {
+  return a == ACT_RELU ? (z > 0.f ? 1.f : 0.f) : fmaf(-y, y, 1.0f);
+}
+
+__device__ __forceinline__ bf16x4 ld_bf16x4(const __bf16* p) { return *reinterpret_cast<const bf16x4*>(p); }
+__device__ __forceinline__ f32x4 unpack4(bf16x4 v) {
+  f32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = bf16_to_f32((unsigned short)v[j]);
+  return r;
+}
+
+// The lane id through an empty asm: the compiler cannot treat addresses built from it
+// as loop-invariant, so LDS operand reads are not hoisted into (scarce) registers.
+__device__ __forceinline__ int opaque_lane(int lane) {
+  asm volatile("" : "+v"(lane));
+  return lane;
+}
+
+// Four consecutive row elements p[k0 .. k0+3], XV floats per load, in two halves:
+// load_row4 issues the loads from clamped in-row addresses (never out of bounds, never
+// under a lane mask) and mask_row4 zeroes the columns past IN.  The mask is applied
+// where the value is CONSUMED: a select right after the load would make the wave wait
+// for the load there, which is what the prefetch exists to avoid.
+template <int XV>
+__device__ __forceinline__ f32x4 load_row4(const float* p, int k0, int IN) {
+  if constexpr (XV == 4) {
+    return *reinterpret_cast<const f32x4*>(p + (k0 < IN ? k0 : 0));
+  } else if constexpr (XV == 2) {
+    const f32x2_t lo = *reinterpret_cast<const f32x2_t*>(p + (k0 < IN ? k0 : 0));
+    const f32x2_t hi = *reinterpret_cast<const f32x2_t*>(p + (k0 + 2 < IN ? k0 + 2 : 0));
+    return f32x4{lo[0], lo[1], hi[0], hi[1]};
+  } else {
+    f32x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = p[k0 + j < IN ? k0 + j : 0];
+    return r;
+  }
+}
+__device__ __forceinline__ f32x4 mask_row4(f32x4 r, int k0, int IN) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = k0 + j < IN ? r[j] : 0.f;
+  return r;
+}
+
+// (U, KT bucket, x row vector width) -> kernel instance
+template <typename F>
+hipError_t dispatch(int U, int IN, int xv, F&& f) {
+  const int KT = (IN + 15) / 16;
+#define SML_UK(u, k)                                                                                              \
+  if (U == u && KT <= k) {                                                                                        \
+    if (xv == 4) return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{},                     \
+                          std::integral_constant<int, 4>{});                                                      \
+    if (xv == 2) return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{},                     \
+                          std::integral_constant<int, 2>{});                                                      \
+    return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{}, std::integral_constant<int, 1>{}); \
+  }
+  SML_UK(16, 1) SML_UK(16, 2) SML_UK(16, 4)
+  SML_UK(32, 1) SML_UK(32, 2)
+#undef SML_UK
+  return hipErrorInvalidValue;
+}
+
+// widest row access (floats) that IN and the base pointer's alignment allow
+inline int row_vec(const void* p, int IN) {
+  const uintptr_t u = (uintptr_t)p;
+  if ((IN & 3) == 0 && (u & 15) == 0) return 4;
+  if ((IN & 1) == 0 && (u & 7) == 0) return 2;
+  return 1;
+}
+
+}  // namespace sml_lstm

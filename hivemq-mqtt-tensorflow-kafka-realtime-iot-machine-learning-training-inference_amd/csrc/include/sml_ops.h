@@ -48,6 +48,7 @@ hipError_t wgrad_launch(const void* X, int x_bf16, int64_t M, int K, int64_t ldx
 // ---- fully fused LSTM layer (lstm_fused.hip) ----
 bool lstm_fused_supported(int U, int IN);
 int lstm_fused_slab(int U, int IN);
+int lstm_fused_dx_ld(int IN);     // row stride of the padded dx buffer the backward kernel writes
 int lstm_fused_waves(int64_t B);
 int lstm_fused_slabs(int64_t B);  // one weight-gradient slab per workgroup
 hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw, const float* b, const float* h0,

@@ -39,170 +39,16 @@
 // MFMA orientation (v_mfma_f32_16x16x16_bf16, lane c = l & 15, g = l >> 4):
 //   C tile mt of z: lane (c, g) holds gate 16mt + 4g + i of sequence s0 + c, so
 //   the four gates of unit u sit in tiles q*UB + u/16 of the same lane/register.
-// This file is compiled without -amdgpu-mfma-vgpr-form so the weight-gradient
-// accumulators can live in AGPRs (launch_bounds(256, 1): 512 registers/lane).
-#include "sml_common.h"
-#include "sml_ops.h"
+// This file (the backward) is compiled without -amdgpu-mfma-vgpr-form so the
+// weight-gradient accumulators can live in AGPRs (launch_bounds(256, 1): 512
+// registers/lane); the forward is lstm_fused_fwd.hip (VGPR form), shared helpers
+// are in include/lstm_fused_impl.h.
+#include "lstm_fused_impl.h"
 
 using namespace sml;
+using namespace sml_lstm;
 
 namespace {
-
-constexpr int WAVES = 4;
-
-__device__ __forceinline__ float act_f(int a, float z) { return a == ACT_RELU ? relu_fast(z) : tanh_fast(z); }
-__device__ __forceinline__ float act_d(int a, float z, float y) {
-  return a == ACT_RELU ? (z > 0.f ? 1.f : 0.f) : fmaf(-y, y, 1.0f);
-}
-
-__device__ __forceinline__ bf16x4 ld_bf16x4(const __bf16* p) { return *reinterpret_cast<const bf16x4*>(p); }
-__device__ __forceinline__ f32x4 unpack4(bf16x4 v) {
-  f32x4 r;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) r[j] = bf16_to_f32((unsigned short)v[j]);
-  return r;
-}
-
-// The lane id through an empty asm: the compiler cannot treat addresses built from it
-// as loop-invariant, so LDS operand reads are not hoisted into (scarce) registers.
-__device__ __forceinline__ int opaque_lane(int lane) {
-  asm volatile("" : "+v"(lane));
-  return lane;
-}
-
-// Four consecutive row elements p[k0 .. k0+3], XV floats per load, in two halves:
-// load_row4 issues the loads from clamped in-row addresses (never out of bounds, never
-// under a lane mask) and mask_row4 zeroes the columns past IN.  The mask is applied
-// where the value is CONSUMED: a select right after the load would make the wave wait
-// for the load there, which is what the prefetch exists to avoid.
-template <int XV>
-__device__ __forceinline__ f32x4 load_row4(const float* p, int k0, int IN) {
-  if constexpr (XV == 4) {
-    return *reinterpret_cast<const f32x4*>(p + (k0 < IN ? k0 : 0));
-  } else if constexpr (XV == 2) {
-    const f32x2_t lo = *reinterpret_cast<const f32x2_t*>(p + (k0 < IN ? k0 : 0));
-    const f32x2_t hi = *reinterpret_cast<const f32x2_t*>(p + (k0 + 2 < IN ? k0 + 2 : 0));
-    return f32x4{lo[0], lo[1], hi[0], hi[1]};
-  } else {
-    f32x4 r;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = p[k0 + j < IN ? k0 + j : 0];
-    return r;
-  }
-}
-__device__ __forceinline__ f32x4 mask_row4(f32x4 r, int k0, int IN) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) r[j] = k0 + j < IN ? r[j] : 0.f;
-  return r;
-}
-
-struct FusedFwdArgs {
-  const float* x;      // [B, T, IN]
-  const float* W;      // [IN, 4U]
-  const float* Uw;     // [U, 4U]
-  const float* b;      // [4U]
-  const float* h0;     // [B, U] or null
-  const float* c0;     // [B, U] or null
-  float* hseq;         // [B, T, U]
-  __bf16* cseq;        // [B/16, T, U/16, 64, 4]   cell state, bf16, fragment-native (backward only)
-  int64_t B;
-  int T, IN, act;
-};
-
-template <int U, int KT, int XV, int ACT>
-__global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdArgs a) {
-  constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
-  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int64_t s0 = ((int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * 16;
-  if (s0 >= a.B) return;  // wave-uniform
-  const int64_t seq = s0 + c;
-  const bool valid = seq < a.B;
-  const int64_t sq = valid ? seq : a.B - 1;
-  const int IN = a.IN, T = a.T;
-
-  // A fragments: W^T[m = gate][k = feature], U^T[m = gate][k = unit]
-  bf16x4 wt[MT][KT], ut[MT][UB];
-  f32x4 bias[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-      f32x4 t4;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = 16 * kt + 4 * g + j;
-        t4[j] = k < IN ? a.W[(int64_t)k * G4 + 16 * mt + c] : 0.f;
-      }
-      wt[mt][kt] = pack4(t4);
-    }
-#pragma unroll
-    for (int s = 0; s < UB; ++s) {
-      f32x4 t4;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) t4[j] = a.Uw[(16 * s + 4 * g + j) * G4 + 16 * mt + c];
-      ut[mt][s] = pack4(t4);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bias[mt][i] = a.b[16 * mt + 4 * g + i];
-  }
-  f32x4 h[UB], cs[UB];
-  bf16x4 hb[UB];
-#pragma unroll
-  for (int b = 0; b < UB; ++b) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int u = 16 * b + 4 * g + i;
-      h[b][i] = a.h0 ? a.h0[sq * U + u] : 0.f;
-      cs[b][i] = a.c0 ? a.c0[sq * U + u] : 0.f;
-    }
-    hb[b] = pack4(h[b]);
-  }
-  // x_t^T as B operand: B[k = feature 16kt + 4g + j][n = sequence c]
-  const float* xrow = a.x + sq * (int64_t)T * IN;
-  auto load_x = [&](int t, f32x4* v) {
-    const float* p = xrow + (int64_t)t * IN;
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt) v[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN);
-  };
-  const int64_t wv = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
-  __bf16* cw = a.cseq + wv * T * (int64_t)(UB * 256) + lane * 4;
-  f32x4 xn[KT];
-  load_x(0, xn);
-  for (int t = 0; t < T; ++t) {
-    bf16x4 xb[KT];
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt) xb[kt] = pack4(mask_row4(xn[kt], 16 * kt + 4 * g, IN));
-    load_x(t + 1 < T ? t + 1 : t, xn);   // next step's input, in flight during this step (branch-free)
-    f32x4 z[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      z[mt] = bias[mt];
-#pragma unroll
-      for (int kt = 0; kt < KT; ++kt) z[mt] = mfma16(wt[mt][kt], xb[kt], z[mt]);
-#pragma unroll
-      for (int s = 0; s < UB; ++s) z[mt] = mfma16(ut[mt][s], hb[s], z[mt]);
-    }
-    const int64_t bu = (sq * T + t) * (int64_t)U;
-    __bf16* ct = cw + (int64_t)t * (UB * 256);
-#pragma unroll
-    for (int b = 0; b < UB; ++b) {
-      f32x4 gi, gf, gc, go;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        gi[i] = sigmoid_fast(z[b][i]);
-        gf[i] = sigmoid_fast(z[UB + b][i]);
-        gc[i] = act_f(ACT, z[2 * UB + b][i]);
-        go[i] = sigmoid_fast(z[3 * UB + b][i]);
-        cs[b][i] = fmaf(gf[i], cs[b][i], gi[i] * gc[i]);
-        h[b][i] = go[i] * act_f(ACT, cs[b][i]);
-      }
-      // padded lanes (seq >= B) write their own padded slot: no bounds check
-      *reinterpret_cast<bf16x4*>(ct + b * 256) = pack4(cs[b]);
-      if (valid) *reinterpret_cast<f32x4*>(a.hseq + bu + 16 * b + 4 * g) = h[b];
-      hb[b] = pack4(h[b]);
-    }
-  }
-}
 
 struct FusedBwdArgs {
   const float* dh;     // [B, T, U]  gradient w.r.t. the h sequence ([B, U] of h_T when dh_last_only)
@@ -214,14 +60,13 @@ struct FusedBwdArgs {
   const float* W;      // [IN, 4U]
   const float* Uw;     // [U, 4U]
   const float* bias;   // [4U]
-  float* dx;           // [B, T, IN] or null
+  float* dx;           // [B16, T, 16*KT] (padded rows / columns, the caller narrows) or null
   float* dh0;          // [B, U] or null
   float* dc0;          // [B, U] or null
   float* partials;     // [nblocks, S]: dW^T [4U][16KT] | dU^T [4U][U] | db [4U] (one slab per workgroup)
   int64_t B;
   int T, IN, act;
   int dh_last_only;    // return_sequences=False: only h_T received a gradient (no [B, T, U] zeros read)
-  int dxvec;           // dx row write width in floats
 };
 
 template <int U, int KT, int XV, int ACT>
@@ -452,20 +297,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
         f32x4 acc = zero4;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc = mfma16(wfl[(kt * MT + mt) * 64 + ol], dzb[mt], acc);
-        if (valid) {
-          float* p = a.dx + (sq * T + t) * (int64_t)IN;
-          const int f0 = 16 * kt + 4 * g;
-          if (a.dxvec == 4) {
-            if (f0 < IN) *reinterpret_cast<f32x4*>(p + f0) = acc;
-          } else if (a.dxvec == 2) {
-            if (f0 < IN) *reinterpret_cast<f32x2_t*>(p + f0) = f32x2_t{acc[0], acc[1]};
-            if (f0 + 2 < IN) *reinterpret_cast<f32x2_t*>(p + f0 + 2) = f32x2_t{acc[2], acc[3]};
-          } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              if (f0 + i < IN) p[f0 + i] = acc[i];
-          }
-        }
+        // dx is [B16, T, 16*KT]: every lane stores its whole 16-byte piece, unmasked
+        *reinterpret_cast<f32x4*>(a.dx + (seq * T + t) * (int64_t)(16 * KT) + 16 * kt + 4 * g) = acc;
       }
     }
     // operands of this step's weight gradients, consumed one step later
@@ -534,16 +367,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 // activation as a template parameter: a runtime switch became ~40 scalar branches
 // per step, which split the time loop into basic blocks the scheduler cannot overlap
 template <int U, int KT, int XV>
-hipError_t launch_fwd(const FusedFwdArgs& a, hipStream_t st) {
-  const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
-  if (a.act == ACT_RELU)
-    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, ACT_RELU>), dim3(grid), dim3(WAVES * 64), 0, st, a);
-  else
-    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, ACT_TANH>), dim3(grid), dim3(WAVES * 64), 0, st, a);
-  return hipGetLastError();
-}
-
-template <int U, int KT, int XV>
 hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
   const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
   if (a.act == ACT_RELU)
@@ -551,31 +374,6 @@ hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
   else
     hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, ACT_TANH>), dim3(grid), dim3(WAVES * 64), 0, st, a);
   return hipGetLastError();
-}
-
-// (U, KT bucket, x row vector width) -> instance
-template <typename F>
-hipError_t dispatch(int U, int IN, int xv, F&& f) {
-  const int KT = (IN + 15) / 16;
-#define SML_UK(u, k)                                                                                              \
-  if (U == u && KT <= k) {                                                                                        \
-    if (xv == 4) return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{},                     \
-                          std::integral_constant<int, 4>{});                                                      \
-    if (xv == 2) return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{},                     \
-                          std::integral_constant<int, 2>{});                                                      \
-    return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{}, std::integral_constant<int, 1>{}); \
-  }
-  SML_UK(16, 1) SML_UK(16, 2) SML_UK(16, 4)
-  SML_UK(32, 1) SML_UK(32, 2)
-#undef SML_UK
-  return hipErrorInvalidValue;
-}
-
-int row_vec(const void* p, int IN) {
-  const uintptr_t u = (uintptr_t)p;
-  if ((IN & 3) == 0 && (u & 15) == 0) return 4;
-  if ((IN & 1) == 0 && (u & 7) == 0) return 2;
-  return 1;
 }
 
 }  // namespace
@@ -595,24 +393,20 @@ int lstm_fused_slab(int U, int IN) {
   return 4 * U * (16 * kt + U + 1);
 }
 
+int lstm_fused_dx_ld(int IN) {
+  const int KT = (IN + 15) / 16;
+  return 16 * (KT <= 1 ? 1 : (KT <= 2 ? 2 : 4));
+}
+
 int lstm_fused_waves(int64_t B) { return (int)(((B + 16 * WAVES - 1) / (16 * WAVES)) * WAVES); }
 int lstm_fused_slabs(int64_t B) { return (int)((B + 16 * WAVES - 1) / (16 * WAVES)); }
-
-hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw, const float* b, const float* h0,
-                                 const float* c0, float* hseq, void* cseq_bf16, int64_t B, int T, int IN, int U, int act,
-                                 hipStream_t stream) {
-  FusedFwdArgs a{x, W, Uw, b, h0, c0, hseq, (__bf16*)cseq_bf16, B, T, IN, act};
-  return dispatch(U, IN, row_vec(x, IN), [&](auto u, auto k, auto v) {
-    return launch_fwd<decltype(u)::value, decltype(k)::value, decltype(v)::value>(a, stream);
-  });
-}
 
 hipError_t lstm_fused_bwd_launch(const float* dh, const void* cseq_bf16, const float* hseq, const float* x,
                                  const float* h0, const float* c0, const float* W, const float* Uw, const float* b,
                                  float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
                                  int act, int dh_last_only, hipStream_t stream) {
   FusedBwdArgs a{dh, (const __bf16*)cseq_bf16, hseq, x, h0, c0, W, Uw, b, dx, dh0, dc0, partials, B, T, IN, act,
-                 dh_last_only, dx ? row_vec(dx, IN) : 1};
+                 dh_last_only};
   return dispatch(U, IN, row_vec(x, IN), [&](auto u, auto k, auto v) {
     return launch_bwd<decltype(u)::value, decltype(k)::value, decltype(v)::value>(a, stream);
   });

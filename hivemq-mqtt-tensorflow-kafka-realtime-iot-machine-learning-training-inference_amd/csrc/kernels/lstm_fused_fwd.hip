@@ -1,0 +1,155 @@
+// Fused LSTM layer forward (the backward and the design notes are in lstm_fused.hip):
+// x.W + recurrence + cell-state save in ONE launch, one wave per 16 sequences.
+#include "lstm_fused_impl.h"
+
+using namespace sml;
+using namespace sml_lstm;
+
+namespace {
+
+struct FusedFwdArgs {
+  const float* x;      // [B, T, IN]
+  const float* W;      // [IN, 4U]
+  const float* Uw;     // [U, 4U]
+  const float* b;      // [4U]
+  const float* h0;     // [B, U] or null
+  const float* c0;     // [B, U] or null
+  float* hseq;         // [B16, T, U], B16 = B rounded up to 16 (rows past B are scratch)
+  __bf16* cseq;        // [B/16, T, U/16, 64, 4]   cell state, bf16, fragment-native (backward only)
+  int64_t B;
+  int T, IN, act;
+};
+
+template <int U, int KT, int XV, int ACT>
+__global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdArgs a) {
+  constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int64_t s0 = ((int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * 16;
+  if (s0 >= a.B) return;  // wave-uniform
+  const int64_t seq = s0 + c;
+  const bool valid = seq < a.B;
+  const int64_t sq = valid ? seq : a.B - 1;
+  const int IN = a.IN, T = a.T;
+
+  // A fragments: W^T[m = gate][k = feature], U^T[m = gate][k = unit]
+  bf16x4 wt[MT][KT], ut[MT][UB];
+  f32x4 bias[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      f32x4 t4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 16 * kt + 4 * g + j;
+        t4[j] = k < IN ? a.W[(int64_t)k * G4 + 16 * mt + c] : 0.f;
+      }
+      wt[mt][kt] = pack4(t4);
+    }
+#pragma unroll
+    for (int s = 0; s < UB; ++s) {
+      f32x4 t4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t4[j] = a.Uw[(16 * s + 4 * g + j) * G4 + 16 * mt + c];
+      ut[mt][s] = pack4(t4);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[mt][i] = a.b[16 * mt + 4 * g + i];
+  }
+  f32x4 h[UB], cs[UB];
+  bf16x4 hb[UB];
+#pragma unroll
+  for (int b = 0; b < UB; ++b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = 16 * b + 4 * g + i;
+      h[b][i] = a.h0 ? a.h0[sq * U + u] : 0.f;
+      cs[b][i] = a.c0 ? a.c0[sq * U + u] : 0.f;
+    }
+    hb[b] = pack4(h[b]);
+  }
+  // x_t^T as B operand: B[k = feature 16kt + 4g + j][n = sequence c]
+  const float* xrow = a.x + sq * (int64_t)T * IN;
+  auto load_x = [&](int t, f32x4* v) {
+    const float* p = xrow + (int64_t)t * IN;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) v[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN);
+  };
+  const int64_t wv = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  __bf16* cw = a.cseq + wv * T * (int64_t)(UB * 256) + lane * 4;
+  // x prefetch PF steps ahead in a register ring; the loop is unrolled by PF so every
+  // ring slot is a fixed register set (a rotating copy would wait for the newest load)
+  constexpr int PF = 2;
+  f32x4 xr[PF][KT];
+#pragma unroll
+  for (int p = 0; p < PF; ++p) load_x(p < T ? p : T - 1, xr[p]);
+  auto fwd_step = [&](int t, f32x4* xin) {
+    bf16x4 xb[KT];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) xb[kt] = pack4(mask_row4(xin[kt], 16 * kt + 4 * g, IN));
+    load_x(t + PF < T ? t + PF : T - 1, xin);   // in flight for PF steps
+    f32x4 z[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      z[mt] = bias[mt];
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) z[mt] = mfma16(wt[mt][kt], xb[kt], z[mt]);
+#pragma unroll
+      for (int s = 0; s < UB; ++s) z[mt] = mfma16(ut[mt][s], hb[s], z[mt]);
+    }
+    // hseq and cseq are padded to whole waves: padding lanes write their own rows,
+    // so no store sits under a lane mask (a masked store makes the number of
+    // outstanding memory ops path-dependent and the compiler then waits for all)
+    float* ht = a.hseq + (seq * T + t) * (int64_t)U + 4 * g;
+    __bf16* ct = cw + (int64_t)t * (UB * 256);
+#pragma unroll
+    for (int b = 0; b < UB; ++b) {
+      f32x4 gi, gf, gc, go;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        gi[i] = sigmoid_fast(z[b][i]);
+        gf[i] = sigmoid_fast(z[UB + b][i]);
+        gc[i] = act_f(ACT, z[2 * UB + b][i]);
+        go[i] = sigmoid_fast(z[3 * UB + b][i]);
+        cs[b][i] = fmaf(gf[i], cs[b][i], gi[i] * gc[i]);
+        h[b][i] = go[i] * act_f(ACT, cs[b][i]);
+      }
+      *reinterpret_cast<bf16x4*>(ct + b * 256) = pack4(cs[b]);
+      *reinterpret_cast<f32x4*>(ht + 16 * b) = h[b];
+      hb[b] = pack4(h[b]);
+    }
+  };
+  int t0 = 0;
+  for (; t0 + PF <= T; t0 += PF) {   // whole groups: straight-line, fixed ring slots
+#pragma unroll
+    for (int p = 0; p < PF; ++p) fwd_step(t0 + p, xr[p]);
+  }
+#pragma unroll
+  for (int p = 0; p < PF - 1; ++p)    // remainder (T % PF steps)
+    if (t0 + p < T) fwd_step(t0 + p, xr[p]);
+}
+
+template <int U, int KT, int XV>
+hipError_t launch_fwd(const FusedFwdArgs& a, hipStream_t st) {
+  const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
+  if (a.act == ACT_RELU)
+    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, ACT_RELU>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, ACT_TANH>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+namespace sml {
+
+hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw, const float* b, const float* h0,
+                                 const float* c0, float* hseq, void* cseq_bf16, int64_t B, int T, int IN, int U, int act,
+                                 hipStream_t stream) {
+  FusedFwdArgs a{x, W, Uw, b, h0, c0, hseq, (__bf16*)cseq_bf16, B, T, IN, act};
+  return dispatch(U, IN, row_vec(x, IN), [&](auto u, auto k, auto v) {
+    return launch_fwd<decltype(u)::value, decltype(k)::value, decltype(v)::value>(a, stream);
+  });
+}
+
+}  // namespace sml

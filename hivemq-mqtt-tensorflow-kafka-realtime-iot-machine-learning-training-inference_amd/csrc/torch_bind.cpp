@@ -342,15 +342,16 @@ std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W,
   if (h0.has_value()) TORCH_CHECK(h0->is_contiguous() && h0->numel() == B * U, "h0 must be [B, U]");
   if (c0.has_value()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * U, "c0 must be [B, U]");
   c10::hip::HIPGuard guard(x.device().index());
-  auto h = at::empty({B, T, U}, x.options());
-  // cell state: saved for BPTT only, in the kernels' fragment-native order, padded to
-  // whole 16-sequence waves (lstm_fused.hip header); the gates are recomputed there
+  // h and the cell state are padded to whole 16-sequence waves (the kernel stores
+  // unmasked); c is saved for BPTT only, in the kernels' fragment-native order
+  // (lstm_fused.hip header); the gates are recomputed there
   const int64_t Bp = (B + 15) / 16 * 16;
+  auto h = at::empty({Bp, T, U}, x.options());
   auto c = at::empty({Bp, T, U}, x.options().dtype(at::kBFloat16));
   SML_CHECK_HIP(sml::lstm_fused_fwd_launch(x.data_ptr<float>(), W.data_ptr<float>(), Uw.data_ptr<float>(),
                                            b.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0), h.data_ptr<float>(),
                                            c.data_ptr(), B, (int)T, (int)IN, (int)U, (int)act, cur_stream(x)));
-  return {h, c};
+  return {h.narrow(0, 0, B), c};
 }
 
 // Fully fused LSTM layer backward -> [dx (or undefined), dW [IN,4U], dU [U,4U], db [4U], dh0, dc0].
@@ -384,7 +385,8 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
   c10::hip::HIPGuard guard(x.device().index());
   auto opts = x.options();
   at::Tensor dx, dh0, dc0;
-  if (want_dx) dx = at::empty({B, T, IN}, opts);
+  at::Tensor dx_pad;
+  if (want_dx) dx_pad = at::empty({(B + 15) / 16 * 16, T, (int64_t)sml::lstm_fused_dx_ld((int)IN)}, opts);
   if (want_state_grads) {
     dh0 = at::empty({B, U}, opts);
     dc0 = at::empty({B, U}, opts);
@@ -397,7 +399,7 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
   auto st = cur_stream(x);
   SML_CHECK_HIP(sml::lstm_fused_bwd_launch(
       dh.data_ptr<float>(), cseq.data_ptr(), hseq.data_ptr<float>(), x.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0),
-      W.data_ptr<float>(), Uw.data_ptr<float>(), b.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
+      W.data_ptr<float>(), Uw.data_ptr<float>(), b.data_ptr<float>(), want_dx ? dx_pad.data_ptr<float>() : nullptr,
       want_state_grads ? dh0.data_ptr<float>() : nullptr, want_state_grads ? dc0.data_ptr<float>() : nullptr,
       partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U, (int)act, dh_last_only ? 1 : 0, st));
   SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
@@ -406,6 +408,10 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
   auto dW = out.narrow(0, 0, G4 * LDW).view({G4, LDW}).narrow(1, 0, IN).t().contiguous();
   auto dU = out.narrow(0, G4 * LDW, G4 * U).view({G4, U}).t().contiguous();
   auto db = out.narrow(0, G4 * LDW + G4 * U, G4);
+  if (want_dx) {
+    dx = dx_pad.narrow(0, 0, B);
+    if (dx_pad.size(2) != IN) dx = dx.narrow(2, 0, IN).contiguous();
+  }
   return {dx, dW, dU, db, dh0, dc0};
 }
 
