@@ -59,17 +59,52 @@ __device__ __forceinline__ f32x4 mask_row4(f32x4 r, int k0, int IN) {
   return r;
 }
 
-// (U, KT bucket, x row vector width) -> kernel instance
+// bf16 rows (inter-layer activations): XV elements per load, 8 / 4 / 2 bytes
+typedef short bf16x2_t __attribute__((ext_vector_type(2)));
+template <int XV>
+__device__ __forceinline__ bf16x4 load_row4(const __bf16* p, int k0, int IN) {
+  if constexpr (XV == 4) {
+    return *reinterpret_cast<const bf16x4*>(p + (k0 < IN ? k0 : 0));
+  } else if constexpr (XV == 2) {
+    const bf16x2_t lo = *reinterpret_cast<const bf16x2_t*>(p + (k0 < IN ? k0 : 0));
+    const bf16x2_t hi = *reinterpret_cast<const bf16x2_t*>(p + (k0 + 2 < IN ? k0 + 2 : 0));
+    return bf16x4{lo[0], lo[1], hi[0], hi[1]};
+  } else {
+    const short* q = reinterpret_cast<const short*>(p);
+    bf16x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = q[k0 + j < IN ? k0 + j : 0];
+    return r;
+  }
+}
+
+// the MFMA B operand of a raw row piece: columns past IN zeroed, bf16
+__device__ __forceinline__ bf16x4 row_operand(f32x4 raw, int k0, int IN) { return pack4(mask_row4(raw, k0, IN)); }
+__device__ __forceinline__ bf16x4 row_operand(bf16x4 raw, int k0, int IN) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) raw[j] = k0 + j < IN ? raw[j] : (short)0;
+  return raw;
+}
+
+// x element type -> raw register type of a 4-element row piece
+template <typename XT> struct RowRaw { using type = f32x4; };
+template <> struct RowRaw<__bf16> { using type = bf16x4; };
+
+// (U, KT bucket, x row vector width, x element type) -> kernel instance
 template <typename F>
-hipError_t dispatch(int U, int IN, int xv, F&& f) {
+hipError_t dispatch(int U, int IN, int xv, bool x_bf16, F&& f) {
   const int KT = (IN + 15) / 16;
-#define SML_UK(u, k)                                                                                              \
-  if (U == u && KT <= k) {                                                                                        \
-    if (xv == 4) return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{},                     \
-                          std::integral_constant<int, 4>{});                                                      \
-    if (xv == 2) return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{},                     \
-                          std::integral_constant<int, 2>{});                                                      \
-    return f(std::integral_constant<int, u>{}, std::integral_constant<int, k>{}, std::integral_constant<int, 1>{}); \
+  auto with_t = [&](auto u, auto k, auto v) {
+    if (x_bf16) return f(u, k, v, (const __bf16*)nullptr);
+    return f(u, k, v, (const float*)nullptr);
+  };
+#define SML_UK(u, k)                                                                                          \
+  if (U == u && KT <= k) {                                                                                    \
+    using UC = std::integral_constant<int, u>;                                                                \
+    using KC = std::integral_constant<int, k>;                                                                \
+    if (xv == 4) return with_t(UC{}, KC{}, std::integral_constant<int, 4>{});                                 \
+    if (xv == 2) return with_t(UC{}, KC{}, std::integral_constant<int, 2>{});                                 \
+    return with_t(UC{}, KC{}, std::integral_constant<int, 1>{});                                              \
   }
   SML_UK(16, 1) SML_UK(16, 2) SML_UK(16, 4)
   SML_UK(32, 1) SML_UK(32, 2)
@@ -77,11 +112,11 @@ hipError_t dispatch(int U, int IN, int xv, F&& f) {
   return hipErrorInvalidValue;
 }
 
-// widest row access (floats) that IN and the base pointer's alignment allow
-inline int row_vec(const void* p, int IN) {
+// widest row access (elements, up to 4) that IN and the base pointer's alignment allow
+inline int row_vec(const void* p, int IN, int elem_bytes) {
   const uintptr_t u = (uintptr_t)p;
-  if ((IN & 3) == 0 && (u & 15) == 0) return 4;
-  if ((IN & 1) == 0 && (u & 7) == 0) return 2;
+  if ((IN & 3) == 0 && (u & (4 * elem_bytes - 1)) == 0) return 4;
+  if ((IN & 1) == 0 && (u & (2 * elem_bytes - 1)) == 0) return 2;
   return 1;
 }
 

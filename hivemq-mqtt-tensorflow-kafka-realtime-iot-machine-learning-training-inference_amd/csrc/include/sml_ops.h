@@ -51,13 +51,14 @@ int lstm_fused_slab(int U, int IN);
 int lstm_fused_dx_ld(int IN);     // row stride of the padded dx buffer the backward kernel writes
 int lstm_fused_waves(int64_t B);
 int lstm_fused_slabs(int64_t B);  // one weight-gradient slab per workgroup
-hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw, const float* b, const float* h0,
-                                 const float* c0, float* hseq, void* cseq_bf16, int64_t B, int T, int IN, int U,
-                                 int act, hipStream_t stream);
-hipError_t lstm_fused_bwd_launch(const float* dh, const void* cseq_bf16, const float* hseq, const float* x,
-                                 const float* h0, const float* c0, const float* W, const float* Uw, const float* b,
-                                 float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
-                                 int act, int dh_last_only, hipStream_t stream);
+// x: fp32 or bf16 (x_bf16); h and dh are bf16 (lstm_fused.hip header), dx has x's dtype
+hipError_t lstm_fused_fwd_launch(const void* x, bool x_bf16, const float* W, const float* Uw, const float* b,
+                                 const float* h0, const float* c0, void* hseq_bf16, void* cseq_bf16, int64_t B, int T,
+                                 int IN, int U, int act, hipStream_t stream);
+hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, const void* hseq_bf16, const void* x,
+                                 bool x_bf16, const float* h0, const float* c0, const float* W, const float* Uw,
+                                 const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,
+                                 int IN, int U, int act, int dh_last_only, hipStream_t stream);
 
 // ---- persistent per-event scorer (ae_serve.hip); structures live in host-mapped memory ----
 struct alignas(128) ServeCtl {

@@ -8,12 +8,17 @@
 // Why: at the BASELINE config-3 shapes (B*T = 409 600 rows, 4u = 128 gates) the
 // unfused layer moved ~2 GB per training step through HBM (x.W written as Zx and
 // re-read, fp32 gates, dz written and re-read by three weight-gradient / dX
-// GEMMs).  Fused, the forward writes h (fp32, the layer output) and a bf16 cell
-// state; the backward reads x, h, c and dh once and RECOMPUTES the gates:
+// GEMMs).  Fused, the forward writes h (the layer output) and the cell state, both
+// bf16; the backward reads x, h, c and dh once and RECOMPUTES the gates:
 //
 //   forward, per step t (one wave = 16 sequences, h / c in VGPRs):
 //     z^T[4u,16] = b + W^T . x_t^T + U^T . h_{t-1}^T     (all on MFMA)
-//     c_t -> bf16 store (for BPTT), h_t -> fp32 store
+//     c_t -> bf16 store (for BPTT), h_t -> bf16 store
+//
+// Inter-layer tensors are bf16 (h, and dh / dx between two LSTM layers): every
+// consumer of h rounds it to bf16 for an MFMA anyway (the recurrence itself, the next
+// layer's x.W, this layer's recompute and dU), so fp32 storage bought no accuracy
+// and cost half of the layer's HBM bytes.  The model input x may stay fp32.
 //   backward, per step t = T-1 .. 0:
 //     z^T recomputed from x_t, h_{t-1} (which the weight gradients read anyway):
 //       (KT + U/16) * 4U/16 MFMAs instead of 8U bytes per sequence-step written by
@@ -51,16 +56,16 @@ using namespace sml_lstm;
 namespace {
 
 struct FusedBwdArgs {
-  const float* dh;     // [B, T, U]  gradient w.r.t. the h sequence ([B, U] of h_T when dh_last_only)
+  const __bf16* dh;    // [B, T, U] bf16 gradient w.r.t. the h sequence ([B, U] of h_T when dh_last_only)
   const __bf16* cseq;  // fragment-native, as written by the forward kernel
-  const float* hseq;   // [B, T, U]
-  const float* x;      // [B, T, IN]
+  const __bf16* hseq;  // [B, T, U] bf16 (the forward's output)
+  const void* x;       // [B, T, IN] fp32 or bf16
   const float* h0;     // [B, U] or null
   const float* c0;     // [B, U] or null
   const float* W;      // [IN, 4U]
   const float* Uw;     // [U, 4U]
   const float* bias;   // [4U]
-  float* dx;           // [B16, T, 16*KT] (padded rows / columns, the caller narrows) or null
+  void* dx;            // [B16, T, 16*KT] in x's dtype (padded rows / columns, the caller narrows) or null
   float* dh0;          // [B, U] or null
   float* dc0;          // [B, U] or null
   float* partials;     // [nblocks, S]: dW^T [4U][16KT] | dU^T [4U][U] | db [4U] (one slab per workgroup)
@@ -69,8 +74,9 @@ struct FusedBwdArgs {
   int dh_last_only;    // return_sequences=False: only h_T received a gradient (no [B, T, U] zeros read)
 };
 
-template <int U, int KT, int XV, int ACT>
+template <int U, int KT, int XV, typename XT, int ACT>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdArgs a) {
+  using XR = typename RowRaw<XT>::type;
   constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
   constexpr int LDW = 16 * KT;
   constexpr int S = G4 * (LDW + U + 1);
@@ -154,28 +160,28 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   // c_t is carried from the previous (later) step's c_{t-1} load: every c is read once.
   struct Step {
     bf16x4 cprev[UB];
-    f32x4 dho[UB];
-    f32x4 hp[UB];      // h_{t-1}[sequence c][unit 16b + 4g + i]
-    f32x4 xt[KT];      // x_t[sequence c][feature 16kt + 4g + j]
+    bf16x4 dho[UB];
+    bf16x4 hp[UB];     // h_{t-1}[sequence c][unit 16b + 4g + i]
+    XR xt[KT];         // x_t[sequence c][feature 16kt + 4g + j]
   };
   const __bf16* cw = a.cseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
   // Loads are unconditional from in-bounds addresses (padding lanes read row B-1),
   // with zeros selected afterwards: no exec-masked branches and no waits in the loop.
   auto load_common = [&](int t, Step& st) {   // raw values; masks are applied in step()
-    const float* dhp = a.dh_last_only ? a.dh + sq * U : a.dh + (sq * T + t) * (int64_t)U;
+    const __bf16* dhp = a.dh_last_only ? a.dh + sq * U : a.dh + (sq * T + t) * (int64_t)U;
 #pragma unroll
-    for (int b = 0; b < UB; ++b) st.dho[b] = *reinterpret_cast<const f32x4*>(dhp + 16 * b + 4 * g);
-    const float* p = a.x + (sq * T + t) * (int64_t)IN;
+    for (int b = 0; b < UB; ++b) st.dho[b] = ld_bf16x4(dhp + 16 * b + 4 * g);
+    const XT* p = static_cast<const XT*>(a.x) + (sq * T + t) * (int64_t)IN;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) st.xt[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN);
   };
   auto load_step = [&](int t, Step& st) {   // t >= 1
     const __bf16* cp = cw + (int64_t)(t - 1) * (UB * 256);
-    const float* hrow = a.hseq + (sq * T + t - 1) * (int64_t)U;
+    const __bf16* hrow = a.hseq + (sq * T + t - 1) * (int64_t)U;
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
       st.cprev[b] = ld_bf16x4(cp + b * 256);
-      st.hp[b] = *reinterpret_cast<const f32x4*>(hrow + 16 * b + 4 * g);
+      st.hp[b] = ld_bf16x4(hrow + 16 * b + 4 * g);
     }
     load_common(t, st);
   };
@@ -184,7 +190,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     for (int b = 0; b < UB; ++b) {
       const int off = 16 * b + 4 * g;
       st.cprev[b] = a.c0 ? pack4(*reinterpret_cast<const f32x4*>(a.c0 + sq * U + off)) : pack4(zero4);
-      st.hp[b] = a.h0 ? *reinterpret_cast<const f32x4*>(a.h0 + sq * U + off) : zero4;
+      st.hp[b] = pack4(a.h0 ? *reinterpret_cast<const f32x4*>(a.h0 + sq * U + off) : zero4);
     }
     load_common(0, st);
   };
@@ -234,10 +240,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     // operands and accumulation order (bit-identical pre-activations)
     bf16x4 xb[KT], hb[UB];
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) xb[kt] = pack4(mask_row4(cur.xt[kt], 16 * kt + 4 * g, IN));
+    for (int kt = 0; kt < KT; ++kt) xb[kt] = row_operand(cur.xt[kt], 16 * kt + 4 * g, IN);
     const bool take_dh = valid && (!a.dh_last_only || t == T - 1);
 #pragma unroll
-    for (int s = 0; s < UB; ++s) hb[s] = pack4(cur.hp[s]);
+    for (int s = 0; s < UB; ++s) hb[s] = cur.hp[s];
     f32x4 z[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -248,9 +254,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       for (int s = 0; s < UB; ++s) z[mt] = mfma16(wfwd[(mt * (KT + UB) + KT + s) * 64 + ol], hb[s], z[mt]);
     }
     wgrad();                                    // step t+1's weight gradients (zeros on the first step)
-    f32x4 cp[UB];                               // c_{t-1}
+    f32x4 cp[UB], dhi[UB];                      // c_{t-1}, incoming dh_t
 #pragma unroll
-    for (int b = 0; b < UB; ++b) cp[b] = unpack4(cur.cprev[b]);
+    for (int b = 0; b < UB; ++b) {
+      cp[b] = unpack4(cur.cprev[b]);
+      dhi[b] = unpack4(cur.dho[b]);
+    }
     f32x4 dzt[MT];
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
@@ -259,7 +268,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
         // fp32 gates, exactly the values the forward used for c_t / h_t
         const float gi = sigmoid_fast(z[b][i]), gf = sigmoid_fast(z[UB + b][i]);
         const float gc = act_f(ACT, z[2 * UB + b][i]), go = sigmoid_fast(z[3 * UB + b][i]);
-        const float dh = (take_dh ? cur.dho[b][i] : 0.f) + dhr[b][i];
+        const float dh = (take_dh ? dhi[b][i] : 0.f) + dhr[b][i];
         const float ct = ctc[b][i];
         const float ac = act_f(ACT, ct);
         const float dc = dcn[b][i] + dh * go * act_d(ACT, ct, ac);
@@ -297,8 +306,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
         f32x4 acc = zero4;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc = mfma16(wfl[(kt * MT + mt) * 64 + ol], dzb[mt], acc);
-        // dx is [B16, T, 16*KT]: every lane stores its whole 16-byte piece, unmasked
-        *reinterpret_cast<f32x4*>(a.dx + (seq * T + t) * (int64_t)(16 * KT) + 16 * kt + 4 * g) = acc;
+        // dx is [B16, T, 16*KT]: every lane stores its whole piece, unmasked
+        const int64_t o = (seq * T + t) * (int64_t)(16 * KT) + 16 * kt + 4 * g;
+        if constexpr (std::is_same_v<XT, float>) *reinterpret_cast<f32x4*>(static_cast<float*>(a.dx) + o) = acc;
+        else *reinterpret_cast<bf16x4*>(static_cast<__bf16*>(a.dx) + o) = pack4(acc);
       }
     }
     // operands of this step's weight gradients, consumed one step later
@@ -366,13 +377,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 
 // activation as a template parameter: a runtime switch became ~40 scalar branches
 // per step, which split the time loop into basic blocks the scheduler cannot overlap
-template <int U, int KT, int XV>
+template <int U, int KT, int XV, typename XT>
 hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
   const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
   if (a.act == ACT_RELU)
-    hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, ACT_RELU>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+    hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU>), dim3(grid), dim3(WAVES * 64), 0, st, a);
   else
-    hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, ACT_TANH>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+    hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH>), dim3(grid), dim3(WAVES * 64), 0, st, a);
   return hipGetLastError();
 }
 
@@ -401,14 +412,15 @@ int lstm_fused_dx_ld(int IN) {
 int lstm_fused_waves(int64_t B) { return (int)(((B + 16 * WAVES - 1) / (16 * WAVES)) * WAVES); }
 int lstm_fused_slabs(int64_t B) { return (int)((B + 16 * WAVES - 1) / (16 * WAVES)); }
 
-hipError_t lstm_fused_bwd_launch(const float* dh, const void* cseq_bf16, const float* hseq, const float* x,
-                                 const float* h0, const float* c0, const float* W, const float* Uw, const float* b,
-                                 float* dx, float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int U,
-                                 int act, int dh_last_only, hipStream_t stream) {
-  FusedBwdArgs a{dh, (const __bf16*)cseq_bf16, hseq, x, h0, c0, W, Uw, b, dx, dh0, dc0, partials, B, T, IN, act,
-                 dh_last_only};
-  return dispatch(U, IN, row_vec(x, IN), [&](auto u, auto k, auto v) {
-    return launch_bwd<decltype(u)::value, decltype(k)::value, decltype(v)::value>(a, stream);
+hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, const void* hseq_bf16, const void* x,
+                                 bool x_bf16, const float* h0, const float* c0, const float* W, const float* Uw,
+                                 const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,
+                                 int IN, int U, int act, int dh_last_only, hipStream_t stream) {
+  FusedBwdArgs a{(const __bf16*)dh_bf16, (const __bf16*)cseq_bf16, (const __bf16*)hseq_bf16, x, h0, c0, W, Uw, b, dx,
+                 dh0, dc0, partials, B, T, IN, act, dh_last_only};
+  return dispatch(U, IN, row_vec(x, IN, x_bf16 ? 2 : 4), x_bf16, [&](auto u, auto k, auto v, auto xt) {
+    using XT = std::remove_const_t<std::remove_pointer_t<decltype(xt)>>;
+    return launch_bwd<decltype(u)::value, decltype(k)::value, decltype(v)::value, XT>(a, stream);
   });
 }
 

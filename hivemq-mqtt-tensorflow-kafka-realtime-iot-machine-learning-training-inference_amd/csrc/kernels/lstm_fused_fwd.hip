@@ -8,20 +8,23 @@ using namespace sml_lstm;
 namespace {
 
 struct FusedFwdArgs {
-  const float* x;      // [B, T, IN]
+  const void* x;       // [B, T, IN] fp32 (model input) or bf16 (a lower LSTM layer's h)
   const float* W;      // [IN, 4U]
   const float* Uw;     // [U, 4U]
   const float* b;      // [4U]
   const float* h0;     // [B, U] or null
   const float* c0;     // [B, U] or null
-  float* hseq;         // [B16, T, U], B16 = B rounded up to 16 (rows past B are scratch)
+  __bf16* hseq;        // [B16, T, U] bf16, B16 = B rounded up to 16 (rows past B are scratch).
+                       // bf16 loses nothing downstream: every consumer (the next layer's x,
+                       // this layer's backward, a Dense head) feeds it to bf16 MFMAs
   __bf16* cseq;        // [B/16, T, U/16, 64, 4]   cell state, bf16, fragment-native (backward only)
   int64_t B;
   int T, IN, act;
 };
 
-template <int U, int KT, int XV, int ACT>
+template <int U, int KT, int XV, typename XT, int ACT>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdArgs a) {
+  using XR = typename RowRaw<XT>::type;
   constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int64_t s0 = ((int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * 16;
@@ -69,9 +72,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
     hb[b] = pack4(h[b]);
   }
   // x_t^T as B operand: B[k = feature 16kt + 4g + j][n = sequence c]
-  const float* xrow = a.x + sq * (int64_t)T * IN;
-  auto load_x = [&](int t, f32x4* v) {
-    const float* p = xrow + (int64_t)t * IN;
+  const XT* xrow = static_cast<const XT*>(a.x) + sq * (int64_t)T * IN;
+  auto load_x = [&](int t, XR* v) {
+    const XT* p = xrow + (int64_t)t * IN;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) v[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN);
   };
@@ -80,13 +83,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
   // x prefetch PF steps ahead in a register ring; the loop is unrolled by PF so every
   // ring slot is a fixed register set (a rotating copy would wait for the newest load)
   constexpr int PF = 2;
-  f32x4 xr[PF][KT];
+  XR xr[PF][KT];
 #pragma unroll
   for (int p = 0; p < PF; ++p) load_x(p < T ? p : T - 1, xr[p]);
-  auto fwd_step = [&](int t, f32x4* xin) {
+  auto fwd_step = [&](int t, XR* xin) {
     bf16x4 xb[KT];
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) xb[kt] = pack4(mask_row4(xin[kt], 16 * kt + 4 * g, IN));
+    for (int kt = 0; kt < KT; ++kt) xb[kt] = row_operand(xin[kt], 16 * kt + 4 * g, IN);
     load_x(t + PF < T ? t + PF : T - 1, xin);   // in flight for PF steps
     f32x4 z[MT];
 #pragma unroll
@@ -100,7 +103,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
     // hseq and cseq are padded to whole waves: padding lanes write their own rows,
     // so no store sits under a lane mask (a masked store makes the number of
     // outstanding memory ops path-dependent and the compiler then waits for all)
-    float* ht = a.hseq + (seq * T + t) * (int64_t)U + 4 * g;
+    __bf16* ht = a.hseq + (seq * T + t) * (int64_t)U + 4 * g;
     __bf16* ct = cw + (int64_t)t * (UB * 256);
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
@@ -114,9 +117,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
         cs[b][i] = fmaf(gf[i], cs[b][i], gi[i] * gc[i]);
         h[b][i] = go[i] * act_f(ACT, cs[b][i]);
       }
-      *reinterpret_cast<bf16x4*>(ct + b * 256) = pack4(cs[b]);
-      *reinterpret_cast<f32x4*>(ht + 16 * b) = h[b];
       hb[b] = pack4(h[b]);
+      *reinterpret_cast<bf16x4*>(ct + b * 256) = pack4(cs[b]);
+      *reinterpret_cast<bf16x4*>(ht + 16 * b) = hb[b];
     }
   };
   int t0 = 0;
@@ -129,13 +132,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
     if (t0 + p < T) fwd_step(t0 + p, xr[p]);
 }
 
-template <int U, int KT, int XV>
+template <int U, int KT, int XV, typename XT>
 hipError_t launch_fwd(const FusedFwdArgs& a, hipStream_t st) {
   const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
   if (a.act == ACT_RELU)
-    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, ACT_RELU>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, XT, ACT_RELU>), dim3(grid), dim3(WAVES * 64), 0, st, a);
   else
-    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, ACT_TANH>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, XT, ACT_TANH>), dim3(grid), dim3(WAVES * 64), 0, st, a);
   return hipGetLastError();
 }
 
@@ -143,12 +146,13 @@ hipError_t launch_fwd(const FusedFwdArgs& a, hipStream_t st) {
 
 namespace sml {
 
-hipError_t lstm_fused_fwd_launch(const float* x, const float* W, const float* Uw, const float* b, const float* h0,
-                                 const float* c0, float* hseq, void* cseq_bf16, int64_t B, int T, int IN, int U, int act,
-                                 hipStream_t stream) {
-  FusedFwdArgs a{x, W, Uw, b, h0, c0, hseq, (__bf16*)cseq_bf16, B, T, IN, act};
-  return dispatch(U, IN, row_vec(x, IN), [&](auto u, auto k, auto v) {
-    return launch_fwd<decltype(u)::value, decltype(k)::value, decltype(v)::value>(a, stream);
+hipError_t lstm_fused_fwd_launch(const void* x, bool x_bf16, const float* W, const float* Uw, const float* b,
+                                 const float* h0, const float* c0, void* hseq_bf16, void* cseq_bf16, int64_t B, int T,
+                                 int IN, int U, int act, hipStream_t stream) {
+  FusedFwdArgs a{x, W, Uw, b, h0, c0, (__bf16*)hseq_bf16, (__bf16*)cseq_bf16, B, T, IN, act};
+  return dispatch(U, IN, row_vec(x, IN, x_bf16 ? 2 : 4), x_bf16, [&](auto u, auto k, auto v, auto xt) {
+    using XT = std::remove_const_t<std::remove_pointer_t<decltype(xt)>>;
+    return launch_fwd<decltype(u)::value, decltype(k)::value, decltype(v)::value, XT>(a, stream);
   });
 }
 

@@ -323,11 +323,13 @@ std::vector<at::Tensor> dense_wgrad(const at::Tensor& x, const at::Tensor& dy, i
   return {dW, db};
 }
 
-// Fully fused LSTM layer forward: x [B, T, IN] -> (h [B,T,U], c: bf16 cell state for lstm_fused_bwd).
+// Fully fused LSTM layer forward: x [B, T, IN] fp32 or bf16 -> (h [B,T,U] bf16, c: bf16
+// cell state for lstm_fused_bwd).
 std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& Uw,
                                        const at::Tensor& b, const c10::optional<at::Tensor>& h0,
                                        const c10::optional<at::Tensor>& c0, int64_t act) {
-  check_dev(x, "x", at::kFloat);
+  TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
+              "x must be a float32 or bfloat16 device tensor");
   check_dev(W, "W", at::kFloat);
   check_dev(Uw, "U", at::kFloat);
   check_dev(b, "b", at::kFloat);
@@ -346,24 +348,28 @@ std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W,
   // unmasked); c is saved for BPTT only, in the kernels' fragment-native order
   // (lstm_fused.hip header); the gates are recomputed there
   const int64_t Bp = (B + 15) / 16 * 16;
-  auto h = at::empty({Bp, T, U}, x.options());
-  auto c = at::empty({Bp, T, U}, x.options().dtype(at::kBFloat16));
-  SML_CHECK_HIP(sml::lstm_fused_fwd_launch(x.data_ptr<float>(), W.data_ptr<float>(), Uw.data_ptr<float>(),
-                                           b.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0), h.data_ptr<float>(),
-                                           c.data_ptr(), B, (int)T, (int)IN, (int)U, (int)act, cur_stream(x)));
+  auto bf = x.options().dtype(at::kBFloat16);
+  auto h = at::empty({Bp, T, U}, bf);
+  auto c = at::empty({Bp, T, U}, bf);
+  SML_CHECK_HIP(sml::lstm_fused_fwd_launch(x.data_ptr(), x.scalar_type() == at::kBFloat16, W.data_ptr<float>(),
+                                           Uw.data_ptr<float>(), b.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0),
+                                           h.data_ptr(), c.data_ptr(), B, (int)T, (int)IN, (int)U, (int)act,
+                                           cur_stream(x)));
   return {h.narrow(0, 0, B), c};
 }
 
-// Fully fused LSTM layer backward -> [dx (or undefined), dW [IN,4U], dU [U,4U], db [4U], dh0, dc0].
+// Fully fused LSTM layer backward -> [dx (x's dtype, or undefined), dW [IN,4U], dU [U,4U],
+// db [4U], dh0, dc0].  dh: bf16 [B, T, U], or [B, U] (h_T only) when dh_last_only.
 std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& cseq, const at::Tensor& hseq,
                                        const at::Tensor& x, const c10::optional<at::Tensor>& h0,
                                        const c10::optional<at::Tensor>& c0, const at::Tensor& W, const at::Tensor& Uw,
-                                       const at::Tensor& b, int64_t act, bool want_dx,
-                                       bool want_state_grads, bool dh_last_only) {
-  check_dev(dh, "dh", at::kFloat);
+                                       const at::Tensor& b, int64_t act, bool want_dx, bool want_state_grads,
+                                       bool dh_last_only) {
+  check_dev(dh, "dh", at::kBFloat16);
   check_dev(cseq, "c", at::kBFloat16);
-  check_dev(hseq, "h", at::kFloat);
-  check_dev(x, "x", at::kFloat);
+  check_dev(hseq, "h", at::kBFloat16);
+  TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
+              "x must be a float32 or bfloat16 device tensor");
   check_dev(W, "W", at::kFloat);
   check_dev(Uw, "U", at::kFloat);
   check_dev(b, "b", at::kFloat);
@@ -383,10 +389,10 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
   }
   TORCH_CHECK(sml::lstm_fused_supported((int)U, (int)IN), "fused LSTM: unsupported U=", U, " IN=", IN);
   c10::hip::HIPGuard guard(x.device().index());
-  auto opts = x.options();
+  auto opts = x.options().dtype(at::kFloat);
   at::Tensor dx, dh0, dc0;
   at::Tensor dx_pad;
-  if (want_dx) dx_pad = at::empty({(B + 15) / 16 * 16, T, (int64_t)sml::lstm_fused_dx_ld((int)IN)}, opts);
+  if (want_dx) dx_pad = at::empty({Bp, T, (int64_t)sml::lstm_fused_dx_ld((int)IN)}, x.options());
   if (want_state_grads) {
     dh0 = at::empty({B, U}, opts);
     dc0 = at::empty({B, U}, opts);
@@ -398,10 +404,11 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
   auto scratch = at::empty({std::max(1, sml::slab_sum_scratch(G, S))}, opts);
   auto st = cur_stream(x);
   SML_CHECK_HIP(sml::lstm_fused_bwd_launch(
-      dh.data_ptr<float>(), cseq.data_ptr(), hseq.data_ptr<float>(), x.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0),
-      W.data_ptr<float>(), Uw.data_ptr<float>(), b.data_ptr<float>(), want_dx ? dx_pad.data_ptr<float>() : nullptr,
-      want_state_grads ? dh0.data_ptr<float>() : nullptr, want_state_grads ? dc0.data_ptr<float>() : nullptr,
-      partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U, (int)act, dh_last_only ? 1 : 0, st));
+      dh.data_ptr(), cseq.data_ptr(), hseq.data_ptr(), x.data_ptr(), x.scalar_type() == at::kBFloat16, opt_ptr(h0),
+      opt_ptr(c0), W.data_ptr<float>(), Uw.data_ptr<float>(), b.data_ptr<float>(),
+      want_dx ? dx_pad.data_ptr() : nullptr, want_state_grads ? dh0.data_ptr<float>() : nullptr,
+      want_state_grads ? dc0.data_ptr<float>() : nullptr, partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U,
+      (int)act, dh_last_only ? 1 : 0, st));
   SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
                                      out.data_ptr<float>(), st));
   const int64_t G4 = 4 * U, LDW = (S / G4) - U - 1;

@@ -106,9 +106,11 @@ class LSTMFunction(torch.autograd.Function):
 class FusedLSTMFunction(torch.autograd.Function):
     """Whole layer in two launches: ``lstm_fused_fwd`` (x.W + recurrence, bf16 cell
     state saved) and ``lstm_fused_bwd`` (gate recompute + BPTT + dW/dU/db accumulated
-    in registers + dX).  ``last_only`` (Keras ``return_sequences=False``) returns h_T
-    [B, U]; its backward reads only that [B, U] gradient instead of a [B, T, U]
-    tensor of zeros."""
+    in registers + dX).  ``x`` may be fp32 (model input) or bf16 (a lower layer's h);
+    the h sequence comes back in bf16 -- every consumer feeds it to bf16 MFMAs -- and
+    ``dx`` in x's dtype.  ``last_only`` (Keras ``return_sequences=False``) returns h_T
+    [B, U] in fp32; its backward reads only that [B, U] gradient instead of a
+    [B, T, U] tensor of zeros."""
 
     @staticmethod
     def forward(ctx, x, W, U, b, act_code: int, last_only: bool = False):
@@ -116,12 +118,12 @@ class FusedLSTMFunction(torch.autograd.Function):
         ctx.save_for_backward(x, W, U, b, h, c)
         ctx.act = act_code
         ctx.last_only = bool(last_only)
-        return h[:, -1].contiguous() if last_only else h
+        return h[:, -1].float() if last_only else h
 
     @staticmethod
     def backward(ctx, dh):
         x, W, U, b, h, c = ctx.saved_tensors
-        dx, dW, dU, db, _, _ = load_c().lstm_fused_bwd(dh.contiguous().float(), c, h, x, None, None,
+        dx, dW, dU, db, _, _ = load_c().lstm_fused_bwd(dh.contiguous().to(torch.bfloat16), c, h, x, None, None,
                                                        W.contiguous(), U.contiguous(), b.contiguous(), ctx.act,
                                                        bool(ctx.needs_input_grad[0]), False, ctx.last_only)
         return (dx if ctx.needs_input_grad[0] else None), dW, dU, db, None, None
@@ -136,10 +138,12 @@ def lstm(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor, act
     """Device-dispatching LSTM layer: fused HIP kernels on ROCm, torch reference on CPU.
     ``return_sequences=False`` returns h_T [B, U] (Keras semantics)."""
     if x.is_cuda:
-        xc = x.contiguous().float()
         if fused and fused_supported(U.shape[0], x.shape[-1]):
+            xc = x.contiguous()
+            if xc.dtype not in (torch.float32, torch.bfloat16):
+                xc = xc.float()
             return FusedLSTMFunction.apply(xc, W, U, b, ACT[activation], not return_sequences)
-        hs = LSTMFunction.apply(xc, W, U, b, ACT[activation])
+        hs = LSTMFunction.apply(x.contiguous().float(), W, U, b, ACT[activation])
     else:
         hs = lstm_reference(x, W, U, b, activation)
     return hs if return_sequences else hs[:, -1]

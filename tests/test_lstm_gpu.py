@@ -34,7 +34,7 @@ def test_lstm_fwd_bwd_vs_reference(cuda_device, u, act, B, T, inp, fused):
     fn = FusedLSTMFunction if fused else LSTMFunction
     yd = fn.apply(*dev_in, 1 if act == "relu" else 2)
     (yd * gy.to(cuda_device)).sum().backward()
-    assert _relerr(yd.detach().cpu(), yr.detach()) < 2e-2
+    assert _relerr(yd.detach().float().cpu(), yr.detach()) < 2e-2
     for d, r in zip(dev_in, ref_in):
         # bf16 MFMA operands through 2 x T dependent recurrent products: a few % is the bf16 floor
         assert _relerr(d.grad.cpu(), r.grad) < 6e-2, (d.shape,)
@@ -70,3 +70,32 @@ def test_fused_last_only_matches_full_sequence_grad(cuda_device, u, B, T, inp):
         grads.append([t.grad.cpu() for t in ins])
     for a, b_ in zip(*grads):
         torch.testing.assert_close(a, b_, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh"])
+def test_fused_stack_bf16_activations_vs_fp32_reference(cuda_device, act):
+    """Two fused layers (the bench / cardata-v2 stack shape): layer 1 takes the fp32 model
+    input and emits a bf16 h sequence, layer 2 consumes it (bf16 x path, bf16 dx back
+    into layer 1's dh) and returns h_T in fp32.  Every gradient vs an fp32 PyTorch chain."""
+    rng = np.random.default_rng(7)
+    B, T, IN, U1, U2 = 96, 20, 18, 32, 16
+    mk = lambda *s_, sc=0.25: torch.tensor(rng.standard_normal(s_) * sc, dtype=torch.float32)
+    x = torch.tensor(rng.uniform(-1, 1, (B, T, IN)), dtype=torch.float32)
+    params = [mk(IN, 4 * U1), mk(U1, 4 * U1), mk(4 * U1, sc=0.1), mk(U1, 4 * U2), mk(U2, 4 * U2), mk(4 * U2, sc=0.1)]
+    gy = torch.tensor(rng.standard_normal((B, U2)), dtype=torch.float32)
+    code = 1 if act == "relu" else 2
+
+    ref = [p.clone().requires_grad_(True) for p in params]
+    h1 = lstm_reference(x, *ref[:3], activation=act)
+    yr = lstm_reference(h1, *ref[3:], activation=act)[:, -1]
+    (yr * gy).sum().backward()
+
+    dev = [p.to(cuda_device).requires_grad_(True) for p in params]
+    h1d = FusedLSTMFunction.apply(x.to(cuda_device), *dev[:3], code, False)
+    assert h1d.dtype == torch.bfloat16
+    yd = FusedLSTMFunction.apply(h1d, *dev[3:], code, True)
+    assert yd.dtype == torch.float32
+    (yd * gy.to(cuda_device)).sum().backward()
+    assert _relerr(yd.detach().cpu(), yr.detach()) < 3e-2
+    for d, r in zip(dev, ref):
+        assert _relerr(d.grad.cpu(), r.grad) < 8e-2, (d.shape,)
