@@ -291,13 +291,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       dzb[mt] = pack4(dzt[mt]);
       accb[mt] += dzt[mt];
     }
-    // critical path: recurrent gradient for step t-1
+    // critical path: recurrent gradient for step t-1, as two half-depth MFMA chains
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
-      f32x4 acc = zero4;
+      f32x4 acc0 = zero4, acc1 = zero4;
 #pragma unroll
-      for (int kt = 0; kt < MT; ++kt) acc = mfma16(ufl[(b * MT + kt) * 64 + ol], dzb[kt], acc);
-      dhr[b] = acc;
+      for (int kt = 0; kt < MT; kt += 2) {
+        acc0 = mfma16(ufl[(b * MT + kt) * 64 + ol], dzb[kt], acc0);
+        acc1 = mfma16(ufl[(b * MT + kt + 1) * 64 + ol], dzb[kt + 1], acc1);
+      }
+      dhr[b] = acc0 + acc1;
     }
     // input gradient dX_t^T = W . dz_t^T
     if (want_dx) {
@@ -321,7 +324,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     for (int s = 0; s < UB; ++s) phb[s] = hb[s];
   };
 
-  // the next step's operands are in flight while the current one computes
+  // the next step's operands are in flight while the current one computes (a deeper,
+  // unrolled three-buffer prefetch measured slower for U = 32: 626 vs 525 us)
   if (active) {
     Step cur, nxt;
     load_any(T - 1, nxt);
