@@ -13,6 +13,11 @@ Two shared objects are produced next to this file:
   on CPU-only machines.
 
 Usage: ``python -m streamml._build`` or ``streamml._build.build_all()``.
+
+``python -m streamml._build --checked`` additionally builds ``_C_dbg.so``: the same
+kernels compiled with ``-DSML_KERNEL_CHECKS=1`` (device-side ``SML_DCHECK`` bounds
+asserts, see ``include/sml_common.h``), loaded instead of ``_C`` when the process
+runs with ``SML_KERNEL_CHECKS=1`` (a bounds-checked debug build).
 """
 from __future__ import annotations
 
@@ -61,20 +66,23 @@ def _py_include() -> str:
     return sysconfig.get_paths()["include"]
 
 
-def build_c(verbose: bool = False, force: bool = False) -> str:
-    """Build ``_C.so`` (HIP kernels + torch binding)."""
+def build_c(verbose: bool = False, force: bool = False, checked: bool = False) -> str:
+    """Build ``_C.so`` (HIP kernels + torch binding); ``checked`` builds ``_C_dbg.so``."""
     import torch
     from torch.utils import cpp_extension
 
-    os.makedirs(BUILD, exist_ok=True)
+    name = "_C_dbg" if checked else "_C"
+    obj_dir = os.path.join(BUILD, "checked") if checked else BUILD
+    os.makedirs(obj_dir, exist_ok=True)
     inc = os.path.join(CSRC, "include")
     hdrs = _headers(inc)
     kern_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    out = os.path.join(PKG, "_C.so")
+    out = os.path.join(PKG, name + ".so")
+    dflags = ["-DSML_KERNEL_CHECKS=1"] if checked else []
     jobs = []
     objs = []
     for src in kern_srcs:
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _newer([src] + hdrs, obj):
             with open(src) as f:
@@ -83,7 +91,7 @@ def build_c(verbose: bool = False, force: bool = False) -> str:
             # kernels that keep large accumulator sets in AGPRs
             vgpr_form = [] if "sml-build: agpr-accumulators" in head else ["-mllvm", "-amdgpu-mfma-vgpr-form"]
             jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
-                         f"-I{inc}", "-Wno-unused-result", "-munsafe-fp-atomics", *vgpr_form])
+                         f"-I{inc}", "-Wno-unused-result", "-munsafe-fp-atomics", *vgpr_form, *dflags])
     # host runtime pieces that use the HIP runtime API (no device code, no torch)
     for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
         obj = os.path.join(BUILD, "rt_" + os.path.basename(src) + ".o")
@@ -92,13 +100,13 @@ def build_c(verbose: bool = False, force: bool = False) -> str:
             jobs.append([CXX, "-O2", "-std=c++17", "-fPIC", "-c", src, "-o", obj, f"-I{inc}", f"-I{ROCM}/include",
                          "-D__HIP_PLATFORM_AMD__=1", "-Wall"])
     bind = os.path.join(CSRC, "torch_bind.cpp")
-    bind_obj = os.path.join(BUILD, "torch_bind.o")
+    bind_obj = os.path.join(obj_dir, "torch_bind.o")
     objs.append(bind_obj)
     abi = "1" if torch.compiled_with_cxx11_abi() else "0"
     if force or _newer([bind] + hdrs + glob.glob(os.path.join(CSRC, "runtime", "*.h")), bind_obj):
         cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-c", bind, "-o", bind_obj, f"-I{inc}", f"-I{_py_include()}",
                f"-I{ROCM}/include", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-DTORCH_EXTENSION_NAME={name}", "-DTORCH_API_INCLUDE_EXTENSION_H",
                "-w"]
         for p in cpp_extension.include_paths():
             cmd.append(f"-I{p}")
@@ -147,11 +155,13 @@ def _san_flags() -> List[str]:
     return [f"-fsanitize={s}", "-fno-omit-frame-pointer", "-g"] if s else []
 
 
-def build_all(verbose: bool = False, force: bool = False) -> None:
+def build_all(verbose: bool = False, force: bool = False, checked: bool = False) -> None:
     build_io(verbose=verbose, force=force)
     build_c(verbose=verbose, force=force)
+    if checked:
+        build_c(verbose=verbose, force=force, checked=True)
 
 
 if __name__ == "__main__":
-    build_all(verbose="-v" in sys.argv, force="-f" in sys.argv)
-    print("built:", [p for p in (os.path.join(PKG, "_C.so"), os.path.join(PKG, "_io.so")) if os.path.exists(p)])
+    build_all(verbose="-v" in sys.argv, force="-f" in sys.argv, checked="--checked" in sys.argv)
+    print("built:", [p for p in (os.path.join(PKG, n) for n in ("_C.so", "_C_dbg.so", "_io.so")) if os.path.exists(p)])

@@ -60,14 +60,14 @@ __device__ __forceinline__ f32x4 mask_row4(f32x4 r, int k0, int IN) {
 }
 
 // bf16 rows (inter-layer activations): XV elements per load, 8 / 4 / 2 bytes
-typedef short bf16x2_t __attribute__((ext_vector_type(2)));
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
 template <int XV>
 __device__ __forceinline__ bf16x4 load_row4(const __bf16* p, int k0, int IN) {
   if constexpr (XV == 4) {
     return *reinterpret_cast<const bf16x4*>(p + (k0 < IN ? k0 : 0));
   } else if constexpr (XV == 2) {
-    const bf16x2_t lo = *reinterpret_cast<const bf16x2_t*>(p + (k0 < IN ? k0 : 0));
-    const bf16x2_t hi = *reinterpret_cast<const bf16x2_t*>(p + (k0 + 2 < IN ? k0 + 2 : 0));
+    const s16x2_t lo = *reinterpret_cast<const s16x2_t*>(p + (k0 < IN ? k0 : 0));
+    const s16x2_t hi = *reinterpret_cast<const s16x2_t*>(p + (k0 + 2 < IN ? k0 + 2 : 0));
     return bf16x4{lo[0], lo[1], hi[0], hi[1]};
   } else {
     const short* q = reinterpret_cast<const short*>(p);

@@ -17,6 +17,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// SML_DCHECK: device-side bounds / invariant assert, compiled in only by the checked
+// build (python -m streamml._build --checked -> _C_dbg.so, loaded when the process
+// runs with SML_KERNEL_CHECKS=1).  A failed check prints the condition and traps the
+// wave, so the fault names its cause.  Release builds compile it away.
+#if defined(SML_KERNEL_CHECKS) && SML_KERNEL_CHECKS
+#define SML_DCHECK(cond)                                                           \
+  do {                                                                             \
+    if (!(cond)) {                                                                 \
+      printf("SML_DCHECK failed: %s (%s:%d)\n", #cond, __FILE__, __LINE__);        \
+      __builtin_trap();                                                            \
+    }                                                                              \
+  } while (0)
+#else
+#define SML_DCHECK(cond) ((void)0)
+#endif
+
 namespace sml {
 
 typedef short bf16x4 __attribute__((ext_vector_type(4)));

@@ -143,6 +143,7 @@ __global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const float
         const bool act_g = (uint64_t)grp < k;
         const uint64_t ev = tail + grp;
         const int slot = (int)(ev % (uint64_t)nslots);
+        SML_DCHECK(slot >= 0 && slot < nslots);
         float(*buf)[MAXD] = grp_buf[grp];
         if (act_g && o < MAXD / 4) {
           f32x4 q = ld_sys4_issue(req + (int64_t)slot * MAXD + 4 * o);
@@ -192,6 +193,7 @@ __global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const float
       } else if ((uint64_t)lane < k) {
         const uint64_t ev = tail + lane;
         const int slot = (int)(ev % (uint64_t)nslots);
+        SML_DCHECK(slot >= 0 && slot < nslots);
         const float* xr = req + (int64_t)slot * MAXD;
         float x[MAXD], h1[MAXH], h2[MAXH], h3[MAXH], y[XD];
         f32x4 q[MAXD / 4];

@@ -79,6 +79,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
     for (int kt = 0; kt < KT; ++kt) v[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN);
   };
   const int64_t wv = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  SML_DCHECK(wv * 16 < a.B + 15 && seq < (a.B + 15) / 16 * 16);   // inside the padded h / c buffers
   __bf16* cw = a.cseq + wv * T * (int64_t)(UB * 256) + lane * 4;
   // x prefetch PF steps ahead in a register ring; the loop is unrolled by PF so every
   // ring slot is a fixed register set (a rotating copy would wait for the newest load)

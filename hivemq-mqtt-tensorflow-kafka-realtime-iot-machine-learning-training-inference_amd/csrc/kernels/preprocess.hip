@@ -71,6 +71,7 @@ __global__ __launch_bounds__(kThreads) void filter_scatter_kernel(
     const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
     if (kp) {
       const int64_t dst = (int64_t)(running + woff + before);
+      SML_DCHECK(dst <= r && dst < n);   // compaction never moves a row forward
       const float* src = x + r * ld;
       float* o = out + dst * D;
       for (int f = 0; f < D; ++f) o[f] = fmaf(src[f], s_sc[f], s_sh[f]);

@@ -21,6 +21,7 @@ PinnedRing::PinnedRing(int slots, size_t slot_bytes, int device) : device_(devic
   released_.assign((size_t)slots, nullptr);
   pending_copy_.assign((size_t)slots, false);
   pending_release_.assign((size_t)slots, false);
+  state_.assign((size_t)slots, SlotState::kIdle);
   for (int i = 0; i < slots; ++i) {
     RING_CHECK(hipHostMalloc(&host_[(size_t)i], slot_bytes_, hipHostMallocDefault));
     RING_CHECK(hipEventCreateWithFlags(&copied_[(size_t)i], hipEventDisableTiming));
@@ -50,6 +51,10 @@ void* PinnedRing::host(int slot) {
 void PinnedRing::submit(int slot, void* dst, size_t bytes) {
   check(slot);
   if (bytes > slot_bytes_) throw std::invalid_argument("PinnedRing: copy larger than a slot");
+  if (state_[(size_t)slot] != SlotState::kIdle)
+    throw std::logic_error("PinnedRing: submit on slot " + std::to_string(slot) +
+                           (state_[(size_t)slot] == SlotState::kCopying ? " whose previous copy was never consumed"
+                                                                        : " still held by the consumer (release it first)"));
   RING_CHECK(hipSetDevice(device_));
   if (pending_release_[(size_t)slot]) {  // device buffer still in use by the consumer
     RING_CHECK(hipStreamWaitEvent(copy_, released_[(size_t)slot], 0));
@@ -58,18 +63,26 @@ void PinnedRing::submit(int slot, void* dst, size_t bytes) {
   RING_CHECK(hipMemcpyAsync(dst, host_[(size_t)slot], bytes, hipMemcpyHostToDevice, copy_));
   RING_CHECK(hipEventRecord(copied_[(size_t)slot], copy_));
   pending_copy_[(size_t)slot] = true;
+  state_[(size_t)slot] = SlotState::kCopying;
   bytes_ += bytes;
 }
 
 void PinnedRing::wait(int slot, hipStream_t stream) {
   check(slot);
+  if (state_[(size_t)slot] == SlotState::kIdle)
+    throw std::logic_error("PinnedRing: wait on slot " + std::to_string(slot) + " with no copy submitted");
   RING_CHECK(hipStreamWaitEvent(stream, copied_[(size_t)slot], 0));
+  state_[(size_t)slot] = SlotState::kConsuming;
 }
 
 void PinnedRing::release(int slot, hipStream_t stream) {
   check(slot);
+  if (state_[(size_t)slot] != SlotState::kConsuming)
+    throw std::logic_error("PinnedRing: release of slot " + std::to_string(slot) +
+                           " whose copy the consumer never waited for");
   RING_CHECK(hipEventRecord(released_[(size_t)slot], stream));
   pending_release_[(size_t)slot] = true;
+  state_[(size_t)slot] = SlotState::kIdle;
 }
 
 }  // namespace sml

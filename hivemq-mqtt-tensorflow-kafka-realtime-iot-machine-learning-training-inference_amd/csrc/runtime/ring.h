@@ -35,6 +35,14 @@ class PinnedRing {
   void wait(int slot, hipStream_t stream);
   // Consumer is done with the device buffer of `slot` once `stream` reaches here.
   void release(int slot, hipStream_t stream);
+  //
+  // Ordering contract, asserted on every call (every H2D copy records an
+  // event that the compute stream waits on), per slot:
+  //     IDLE --submit--> COPYING --wait--> CONSUMING --release--> IDLE
+  // submit on a slot the consumer still holds (the copy would race its kernels),
+  // release of a slot whose copy the consumer never waited for (its kernels may
+  // have read stale data), or wait on a slot with no copy in flight throw
+  // std::logic_error instead of silently corrupting a batch.
   hipStream_t copy_stream() const { return copy_; }
   uint64_t bytes_copied() const { return bytes_; }
 
@@ -44,6 +52,8 @@ class PinnedRing {
   std::vector<void*> host_;
   std::vector<hipEvent_t> copied_, released_;
   std::vector<bool> pending_copy_, pending_release_;
+  enum class SlotState : uint8_t { kIdle, kCopying, kConsuming };
+  std::vector<SlotState> state_;
   hipStream_t copy_ = nullptr;
   uint64_t bytes_ = 0;
   void check(int slot) const {

@@ -13,14 +13,29 @@
 #include "../runtime/serve.h"
 
 #include <pybind11/numpy.h>
+#include <cstdlib>
 #include <cstring>
 
 namespace {
 
-#define SML_CHECK_HIP(expr)                                                           \
-  do {                                                                                \
-    hipError_t _e = (expr);                                                           \
-    TORCH_CHECK(_e == hipSuccess, "HIP error: ", hipGetErrorString(_e), " @ ", #expr); \
+// SML_SYNC_CHECK=1: launch-blocking debug mode -- every launch is
+// followed by a device synchronize, so an asynchronous kernel fault is reported
+// against the op that caused it instead of a later, unrelated call.
+static bool sync_check() {
+  const char* v = std::getenv("SML_SYNC_CHECK");
+  return v && *v && *v != '0';
+}
+
+#define SML_CHECK_HIP(expr)                                                                           \
+  do {                                                                                                \
+    hipError_t _e = (expr);                                                                           \
+    TORCH_CHECK(_e == hipSuccess, "HIP error: ", hipGetErrorString(_e), " @ ", #expr);                \
+    if (sync_check()) {                                                                               \
+      _e = hipDeviceSynchronize();                                                                    \
+      if (_e == hipSuccess) _e = hipGetLastError();                                                   \
+      TORCH_CHECK(_e == hipSuccess, "HIP error (SML_SYNC_CHECK): ", hipGetErrorString(_e), " after ", \
+                  #expr);                                                                             \
+    }                                                                                                 \
   } while (0)
 
 void check_dev(const at::Tensor& t, const char* name, at::ScalarType st) {
@@ -553,7 +568,7 @@ struct ServePy {
 
 }  // namespace
 
-PYBIND11_MODULE(_C, m) {
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "streamml gfx950 HIP kernels";
   m.attr("AE_NSLOT") = sml::ae_nslot();
   m.attr("AE_NPARAM") = sml::ae_nparam();

@@ -119,13 +119,15 @@ class DeviceLoader:
                 n = len(c)
                 x = np.ascontiguousarray(c.x, dtype=np.float32)
                 self.ring.fill(slot, x)
+                if prev is not None:
+                    # consumer kernels for `prev` are enqueued by now; releasing before the
+                    # next submit also orders a reused slot's copy after them (slots=1)
+                    self.ring.release(prev)
                 self.ring.submit(slot, self.bufs[slot], n * self.features * 4)
                 if with_labels:
                     self.lab_host[slot][:n].copy_(torch.from_numpy(np.ascontiguousarray(c.label, np.uint8)))
                     self.lab_dev[slot][:n].copy_(self.lab_host[slot][:n], non_blocking=True)
                     self._last_slot = slot
-                if prev is not None:
-                    self.ring.release(prev)   # consumer kernels for `prev` are enqueued by now
                 self.ring.wait(slot)
                 self.rows += n
                 ENGINE.h2d_bytes.inc(n * self.features * 4)
@@ -133,9 +135,9 @@ class DeviceLoader:
                 yield self.bufs[slot][:n], c
                 prev = slot
                 i += 1
-            if prev is not None:
-                self.ring.release(prev)
         finally:
+            if prev is not None:   # also when the consumer stops early (take / break)
+                self.ring.release(prev)
             stop.set()
             while th.is_alive():
                 try:

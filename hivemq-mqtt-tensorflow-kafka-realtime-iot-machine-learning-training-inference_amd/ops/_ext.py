@@ -23,24 +23,31 @@ def _try_build(which: str) -> None:
         return
     from .. import _build
     if which == "c":
-        _build.build_c()
+        _build.build_c(checked=kernel_checks())
     else:
         _build.build_io()
 
 
+def kernel_checks() -> bool:
+    """``SML_KERNEL_CHECKS=1``: load ``_C_dbg`` (kernels with device-side SML_DCHECK
+    asserts, ``python -m streamml._build --checked``) instead of ``_C``."""
+    return os.environ.get("SML_KERNEL_CHECKS", "0") not in ("", "0")
+
+
 def load_c():
-    """Return the ``streamml._C`` module, building it in-tree if absent."""
+    """Return the ``streamml._C`` module (or ``_C_dbg``), building it in-tree if absent."""
     global _C, _C_ERR
     with _lock:
         if _C is not None:
             return _C
+        mod = "streamml._C_dbg" if kernel_checks() else "streamml._C"
         try:
-            _C = importlib.import_module("streamml._C")
+            _C = importlib.import_module(mod)
         except ImportError as e:  # pragma: no cover - exercised only without a build
             _C_ERR = e
             try:
                 _try_build("c")
-                _C = importlib.import_module("streamml._C")
+                _C = importlib.import_module(mod)
             except Exception as e2:
                 raise RuntimeError(
                     "streamml._C (gfx950 HIP kernels) is not built and could not be built: "

@@ -48,3 +48,23 @@ def test_broker_client_threads_tsan():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "PASS threads" in r.stdout
     assert "WARNING: ThreadSanitizer" not in r.stderr
+
+
+def test_checked_kernel_build_compiles_device_asserts(tmp_path):
+    """SML_KERNEL_CHECKS=1 compiles SML_DCHECK into the device code; release compiles it away."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    pkg = PKG
+    src = os.path.join(pkg, "csrc", "kernels", "preprocess.hip")
+    outs = {}
+    for flag in ("0", "1"):
+        out = str(tmp_path / f"pre{flag}.s")
+        subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-DSML_KERNEL_CHECKS={flag}",
+                        "-I", os.path.join(pkg, "csrc", "include"), "--offload-device-only", "-S", src, "-o", out],
+                       check=True, capture_output=True, timeout=300)
+        outs[flag] = open(out).read()
+    assert "SML_DCHECK failed" in outs["1"] and "s_trap" in outs["1"]
+    assert "SML_DCHECK failed" not in outs["0"]
