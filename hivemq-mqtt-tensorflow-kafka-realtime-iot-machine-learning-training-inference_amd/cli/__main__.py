@@ -18,6 +18,8 @@ Commands (reference script in parentheses):
   mqtt-broker  [--port 1883] [--kafka SERVERS] [--kafka-extension kafka-config.yaml]   HiveMQ + Kafka extension
   devsim       run -s scenario.xml [--broker host:port] [--clients N]   HiveMQ device simulator
   connect      <servers> --config connector.json [--sink-store DIR]   Kafka Connect sinks (MongoDB, GCS Avro)
+  serve        <servers> <topic> <result_topic> <model-file> [--replicas W --replica-index R]
+               long-running shard-by-key anomaly scorer (one replica per GPU; model-predictions Deployment)
 """
 from __future__ import annotations
 
@@ -29,7 +31,7 @@ from . import common
 def _commands():
     from . import cardata_autoencoder as ae
     from . import cardata_lstm as ls
-    from . import creditcard, mnist, mqtt, tools, train
+    from . import creditcard, mnist, mqtt, serve, tools, train
     return {
         "cardata-v3": ae.main_v3,
         "cardata-v1": ae.main_v1,
@@ -45,6 +47,7 @@ def _commands():
         "mqtt-broker": mqtt.main_broker,
         "devsim": mqtt.main_devsim,
         "connect": mqtt.main_connect,
+        "serve": serve.main,
     }
 
 

@@ -71,8 +71,9 @@ def kafka_config(servers: str, choice: str) -> Optional[List[str]]:
 
 
 def prepare_servers(servers: str, topic: str, seed: int = 0, schema: str = "cardata-v1",
-                    rows: Optional[int] = None) -> str:
-    """Resolve ``synthetic://[rows]`` into a pre-filled in-process broker; others pass through."""
+                    rows: Optional[int] = None, partitions: int = 1) -> str:
+    """Resolve ``synthetic://[rows]`` into a pre-filled in-process broker (records keyed by
+    car and spread over ``partitions`` with the Kafka murmur2 partitioner); others pass through."""
     if not servers.startswith("synthetic://"):
         return servers
     from ..data import produce as prod
@@ -85,8 +86,9 @@ def prepare_servers(servers: str, topic: str, seed: int = 0, schema: str = "card
     b = fake_broker(name)
     if _has_topic(b, topic) and b.end_offset(topic, 0) > 0:   # already filled in this process
         return f"fake://{name}"
-    b.create_topic(topic, 1)
-    prod.produce(st.synthetic(n, chunk=8192, seed=seed), f"fake://{name}", topic, schema=schema, create=False)
+    b.create_topic(topic, max(1, int(partitions)))
+    prod.produce(st.synthetic(n, chunk=8192, seed=seed), f"fake://{name}", topic, schema=schema, create=False,
+                 partitions=max(1, int(partitions)))
     return f"fake://{name}"
 
 

@@ -1,0 +1,160 @@
+"""``serve``: long-running, sharded streaming anomaly scorer (BASELINE config 5).
+
+The reference scales inference by running ``cardata-v3.py ... predict`` as a K8s
+Deployment that K8s restarts after every bounded run (python-scripts/README.md:24,
+AUTOENCODER-TensorFlow-IO-Kafka/model-predictions.yaml). Each run reads partition 0
+only (cardata-v3.py:46) and writes reconstructions (cardata-v3.py:243-249). Here:
+
+* one replica per GPU. Replica ``r`` of ``W`` owns the Kafka partitions ``p`` with
+  ``p % W == r``. The producers (MQTT bridge, ``produce``) partition by murmur2(car key),
+  so this is shard-by-key: every car's events reach the same GPU, in order;
+* the replica follows the log (no eof) and commits its offsets to the consumer group
+  after each produced batch. A restarted replica resumes where it stopped, with no K8s
+  restart loop and no re-scoring;
+* every event is scored on the GPU (reconstruction MSE, K12), flagged with the
+  notebook's fixed threshold (``threshold_fixed = 5``), and written to the result
+  topic keyed by car: ``{"car", "partition", "offset", "score", "anomaly"}``, plus the
+  reconstruction with ``--emit both`` (what the reference streams).
+
+Replica identity comes from ``--replica-index/--replicas``, else torchrun's
+``RANK/WORLD_SIZE``, else ``REPLICA_INDEX/REPLICAS`` (a StatefulSet ordinal), else 0/1.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from . import common
+
+USAGE = ("python -m streamml.cli serve <servers> <topic> <result_topic> <model-file> "
+         "[--project P] [--replicas W --replica-index R] [--threshold 5] [--max-events N]")
+
+
+def shard_partitions(n_partitions: int, rank: int, world: int) -> List[int]:
+    """Partitions owned by replica ``rank`` of ``world`` (round-robin, so W > P leaves
+    replicas idle instead of splitting a partition and breaking per-key order)."""
+    return [p for p in range(int(n_partitions)) if p % int(world) == int(rank)]
+
+
+def replica_identity(ns) -> Tuple[int, int]:
+    if ns.replicas is not None:
+        return int(ns.replica_index or 0), int(ns.replicas)
+    for r_key, w_key in (("RANK", "WORLD_SIZE"), ("REPLICA_INDEX", "REPLICAS")):
+        if w_key in os.environ:
+            return int(os.environ.get(r_key, "0")), int(os.environ[w_key])
+    return 0, 1
+
+
+def _flags(p) -> None:
+    p.add_argument("--project", default="car-demo", help="model store bucket suffix (cardata-v3 <project>)")
+    p.add_argument("--group", default="streamml-serve", help="consumer group for committed offsets")
+    p.add_argument("--replicas", type=int, default=None)
+    p.add_argument("--replica-index", type=int, default=None)
+    p.add_argument("--partitions", type=int, default=None, help="partition count (default: broker metadata)")
+    p.add_argument("--from-beginning", action="store_true",
+                   help="ignore committed offsets and start at the earliest record")
+    p.add_argument("--threshold", type=float, default=5.0)
+    p.add_argument("--emit", choices=["score", "both"], default="score")
+    p.add_argument("--max-batch", type=int, default=1 << 16, help="rows per device scoring call")
+    p.add_argument("--max-events", type=int, default=0, help="stop after this many events (0 = run forever)")
+    p.add_argument("--idle-timeout", type=float, default=None, help="stop after this many idle seconds")
+    p.add_argument("--synthetic-partitions", type=int, default=8)
+    p.add_argument("--metrics-port", type=int, default=0)
+    p.add_argument("--schema", default="cardata-v1")
+
+
+def main(argv: Sequence[str]) -> int:
+    common.print_options(argv)
+    ns = common.parse(argv, USAGE, ["servers", "topic", "result_topic", "model_file"], add_flags=_flags)
+    from ..data.stream import LABEL_MISSING, kafka
+    from ..kafka import KafkaClient, KafkaOutputSequence
+    from ..models.autoencoder import load_model
+    from ..obs.metrics import ENGINE, REGISTRY
+    from ..utils.model_store import autoencoder_store
+
+    rank, world = replica_identity(ns)
+    servers = common.prepare_servers(ns.servers, ns.topic, seed=ns.synthetic_seed, schema=ns.schema,
+                                     partitions=ns.synthetic_partitions)
+    cfg = common.kafka_config(ns.servers, ns.kafka_config)
+    device = ns.device
+    if device == "auto":
+        import torch
+        device = f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}" if torch.cuda.is_available() else "cpu"
+
+    path = common.model_path(ns.workdir, ns.model_file)
+    if not os.path.exists(path):
+        autoencoder_store(ns.project, ns.store).download("/" + ns.model_file, path)
+    model = load_model(path, device=device, input_normalizer="cardata")
+    if ns.metrics_port and rank == 0:
+        REGISTRY.serve(ns.metrics_port, addr="0.0.0.0")
+
+    meta = KafkaClient(servers, cfg).partitions()
+    n_parts = ns.partitions or meta.get(ns.topic, 1)
+    if ns.result_topic not in meta and servers.startswith("fake://"):
+        from ..kafka import fake_broker
+        try:   # the reference creates model-predictions with the source topic's partition count
+            fake_broker(servers[len("fake://"):] or "default").create_topic(ns.result_topic, n_parts)
+        except Exception:
+            pass   # another replica created it first
+        meta = KafkaClient(servers, cfg).partitions()
+    result_parts = max(1, meta.get(ns.result_topic, 1))
+    mine = shard_partitions(n_parts, rank, world)
+    print(f"replica {rank}/{world}: partitions {mine} of {n_parts} on {device}", flush=True)
+    summary = {"replica": rank, "replicas": world, "partitions": mine, "events": 0, "anomalies": 0}
+    if not mine:
+        print(json.dumps(summary), flush=True)
+        return 0
+
+    start = -2 if ns.from_beginning else 0
+    topics = [f"{ns.topic}:{p}:{start}" for p in mine]
+    stream = kafka(servers, topics, schema=ns.schema, group=ns.group, eof=False, config=cfg, commit=True,
+                   resume=not ns.from_beginning, idle_timeout_s=ns.idle_timeout)
+    sinks, next_index = {}, {}
+    t0 = time.perf_counter()
+    for chunk in stream:
+        part = int(chunk.meta.get("partition", 0))
+        sink = sinks.get(part)
+        if sink is None:   # results keep the source partition: a car's scores stay ordered
+            sink = sinks[part] = KafkaOutputSequence(ns.result_topic, servers, cfg, partition=part % result_parts)
+            next_index[part] = 0
+        ok = chunk.label != LABEL_MISSING          # undecodable records are skipped, not scored
+        if not ok.all():
+            chunk = chunk.select(ok)
+        if len(chunk) == 0:
+            continue
+        t_batch = time.perf_counter()
+        recon = None
+        if ns.emit == "both":
+            recon, scores = model.reconstruct_and_score(chunk.x, batch_size=ns.max_batch)
+        else:
+            scores = model.score(chunk.x, batch_size=ns.max_batch)
+        flags = scores > ns.threshold
+        dt_us = (time.perf_counter() - t_batch) * 1e6 / len(chunk)
+        keys = chunk.keys or [None] * len(chunk)
+        offs = chunk.offsets if chunk.offsets is not None else np.arange(len(chunk))
+        for i in range(len(chunk)):
+            rec = {"car": keys[i], "partition": part, "offset": int(offs[i]), "score": float(scores[i]),
+                   "anomaly": bool(flags[i])}
+            if recon is not None:
+                rec["reconstruction"] = np.array2string(recon[i])
+            sink.setitem(next_index[part], json.dumps(rec), key=keys[i])
+            next_index[part] += 1
+        sink.flush()   # produced before the dataset commits this batch's offsets (at-least-once)
+        n_flag = int(flags.sum())
+        ENGINE.infer_rows.inc(len(chunk), model=model.name)
+        ENGINE.anomaly_events.inc(n_flag, model=model.name)
+        ENGINE.infer_latency.observe(dt_us)
+        summary["events"] += len(chunk)
+        summary["anomalies"] += n_flag
+        if ns.max_events and summary["events"] >= ns.max_events:
+            break
+    for sink in sinks.values():
+        sink.flush()
+    wall = time.perf_counter() - t0
+    summary["events_per_s"] = summary["events"] / wall if wall > 0 else 0.0
+    print(json.dumps(summary), flush=True)
+    return 0

@@ -323,6 +323,13 @@ class Autoencoder:
             self.compile()
         return np.concatenate([sc for _, _, sc in self._forward_batches(x, batch_size)])
 
+    def reconstruct_and_score(self, x, batch_size: int = 1 << 20) -> Tuple[np.ndarray, np.ndarray]:
+        """Reconstructions and anomaly scores from one device pass (K12)."""
+        if not self.compiled:
+            self.compile()
+        parts = list(self._forward_batches(x, batch_size))
+        return np.concatenate([r for _, r, _ in parts]), np.concatenate([sc for _, _, sc in parts])
+
     def detect(self, x, threshold: float = 5.0, batch_size: int = 1 << 20) -> np.ndarray:
         """Anomaly flags with the notebook's fixed threshold (``threshold_fixed = 5``)."""
         flags = self.score(x, batch_size) > threshold

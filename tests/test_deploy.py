@@ -16,7 +16,7 @@ DEPLOY = os.path.join(ROOT, "deploy")
 def _containers():
     for path in sorted(glob.glob(os.path.join(DEPLOY, "k8s", "*.yaml"))):
         for doc in yaml.safe_load_all(open(path)):
-            if not doc or doc.get("kind") not in ("Job", "Deployment", "Pod"):
+            if not doc or doc.get("kind") not in ("Job", "Deployment", "StatefulSet", "Pod"):
                 continue
             spec = doc["spec"]
             pod = spec["template"]["spec"] if "template" in spec else spec
