@@ -99,3 +99,23 @@ def test_fused_stack_bf16_activations_vs_fp32_reference(cuda_device, act):
     assert _relerr(yd.detach().cpu(), yr.detach()) < 3e-2
     for d, r in zip(dev, ref):
         assert _relerr(d.grad.cpu(), r.grad) < 8e-2, (d.shape,)
+
+
+def test_graph_replayed_train_steps_match_eager(cuda_device):
+    """utils.graphs.capture_steps: whole LSTM train steps (fwd + bwd + Adam) replayed as HIP
+    graphs give bit-identical parameters to the same steps run eagerly."""
+    from streamml.utils.graphs import capture_steps
+    rng = np.random.default_rng(1)
+    X = torch.tensor(rng.uniform(-1, 1, (2, 256, 20, 18)), dtype=torch.float32, device=cuda_device)
+    Y = torch.tensor(rng.uniform(-1, 1, (2, 256, 18)), dtype=torch.float32, device=cuda_device)
+    eager = LSTMPredictor.two_layer(look_back=20, device=cuda_device, seed=11)
+    graphed = LSTMPredictor.two_layer(look_back=20, device=cuda_device, seed=11)
+    step = capture_steps([lambda i=i: graphed.train_step(X[i], Y[i]) for i in range(2)], warmup=1)
+    for i in range(2):                      # the capture warm-up ran each batch once
+        eager.train_step(X[i], Y[i])
+    for s in range(6):
+        loss_g, _ = step(s)
+        loss_e, _ = eager.train_step(X[s % 2], Y[s % 2])
+    torch.cuda.synchronize()
+    torch.testing.assert_close(graphed.fp.flat, eager.fp.flat, rtol=0, atol=0)
+    torch.testing.assert_close(loss_g, loss_e, rtol=0, atol=0)
