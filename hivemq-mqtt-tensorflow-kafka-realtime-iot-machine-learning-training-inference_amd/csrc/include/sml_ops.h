@@ -70,17 +70,27 @@ struct alignas(128) ServeCtl {
   uint32_t alive;           // device: 1 while the kernel runs
   uint32_t pad2[30];
 };
-struct ServeResult {
-  uint64_t seq;             // event sequence number this slot holds
-  float score;              // mean squared reconstruction error
-  uint32_t flag;            // score > threshold
-  uint64_t t_seen;          // device s_memrealtime (100 MHz) when the wave picked the event up
-  uint64_t t_done;          // ... when its result stores were issued
-  uint64_t t_loaded;        // ... when the request row had arrived
-  uint64_t t_comp;          // ... when the forward pass finished
-  float recon[32];
+// Request and result slots use low-latency ("LL") framing: every 8-byte word carries
+// 4 bytes of payload and a 4-byte tag = (uint32)(event + 1).  One 8-byte-atomic PCIe
+// read then tells whether the word already belongs to the event being waited for, so
+// neither side needs a separate ready flag, fence or acknowledgement round trip: the
+// GPU polls the request words themselves and has the row in registers the moment the
+// tags match; the host polls the result words in its own memory.
+struct ServeReq {
+  uint64_t w[32];           // w[i] = tag << 32 | float bits of x[i]  (i < D)
 };
-hipError_t ae_serve_launch(ServeCtl* ctl, const float* req, ServeResult* res, int nslots, const float* wts,
+enum : int {                // ServeResult word indices
+  kServeScore = 32,         // mean squared reconstruction error
+  kServeFlag = 33,          // score > threshold
+  kServeTLoad = 34,         // device ticks (100 MHz) from pick-up to row in registers
+  kServeTComp = 35,         // ... to forward pass done
+  kServeTDone = 36,         // ... to result stores issued
+  kServeWords = 37
+};
+struct ServeResult {
+  uint64_t w[40];           // [0, D): reconstruction, then the fields above; all tagged
+};
+hipError_t ae_serve_launch(ServeCtl* ctl, const ServeReq* req, ServeResult* res, int nslots, const float* wts,
                            const float* scale, const float* shift, const int* dims, const int* acts, float threshold,
                            double idle_seconds, hipStream_t stream);
 

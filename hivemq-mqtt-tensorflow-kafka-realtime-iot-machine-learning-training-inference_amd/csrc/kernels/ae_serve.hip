@@ -4,14 +4,17 @@
 // Python OutputCallback (cardata-v3.py:235-280); per-event latency is not even
 // measurable there.  The launch-per-event path here (H2D copy + fused forward
 // kernel + D2H copy) costs three runtime round trips per event.  This kernel
-// removes all of them: ONE wave stays resident, polls a host-mapped request
-// ring (fine-grained pinned memory, cache-bypassing system-scope loads), scores the
-// pending events -- one event per lane, so a burst of up to 64 events costs the
-// same as one; a single event (the common case at a fixed QPS) is instead spread
-// over 16 lanes, one output unit each -- and writes score / anomaly flag /
-// reconstruction straight back
-// into host-mapped memory, then bumps the completion counter once those stores
-// are acknowledged.
+// removes all of them: ONE wave stays resident and polls the host-mapped request
+// ring (fine-grained pinned memory, cache-bypassing system-scope loads).
+//
+// Slots are LL-framed (sml_ops.h): each 8-byte word is 4 payload bytes + a 4-byte
+// event tag.  The wave polls the next slot's words THEMSELVES, so the poll that finds
+// the event also delivers its row -- no separate "head moved, now fetch the row" PCIe
+// round trip -- and it writes tagged result words that the host polls in its own
+// memory, so there is no wait for the stores' acknowledgement either.  A single
+// event (the common case at a fixed QPS) is spread over 16 lanes, one output unit
+// each; a backlog of more than 4 (seen through the host's head counter) is scored one
+// event per lane, up to 64 per pass.
 //
 // Weights (Keras order W1 b1 .. W4 b4, <= 31/15/15/15 units) and the input
 // normaliser live in LDS; every lane reads the same weight address, so the LDS
@@ -51,11 +54,21 @@ __device__ __forceinline__ float ld_sysf(const float* p) {
 __device__ __forceinline__ void st_sysf(float* p, float v) { st_sys32(reinterpret_cast<uint32_t*>(p), __float_as_uint(v)); }
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Row-sized host-mapped reads: 16-byte cache-bypassing (sc0 sc1) loads issued
-// back to back and completed by ONE s_waitcnt.  (Atomic loads are serialised by
-// the compiler -- one PCIe round trip per float.)
-__device__ __forceinline__ f32x4 ld_sys4_issue(const float* p) {
-  f32x4 v;
+// One poll: this lane's tagged word of the next request slot and the host's head
+// counter, as cache-bypassing loads issued without a wait (the caller waits with a
+// counted s_waitcnt tied to the outputs, so several polls can be in flight).
+__device__ __forceinline__ void poll_issue(uint64_t& w, uint64_t& hd, const uint64_t* wp, const uint64_t* hp) {
+  asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1" : "=v"(w) : "v"(wp) : "memory");
+  asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1" : "=v"(hd) : "v"(hp) : "memory");
+}
+
+// Two tagged request words (16 bytes) with one cache-bypassing load, issued without a
+// wait so a whole row's loads are in flight together (relaxed atomic loads are
+// serialised by the compiler: one PCIe round trip per word).  Each 8-byte word is
+// checked against its own tag, so the pair need not be read atomically.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 ld_sys_pair_issue(const uint64_t* p) {
+  u32x4 v;
   asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(v) : "v"(p) : "memory");
   return v;
 }
@@ -101,7 +114,7 @@ __device__ __forceinline__ void dense_group(const float* __restrict__ W, const f
 // CD / C1 / C2 > 0 fix (D, n1, n2) at compile time (compact straight-line code for
 // the reference configs: car data 18-14-7, credit card 30-14-7); 0 = runtime dims.
 template <int CD, int C1, int C2>
-__global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const float* __restrict__ req,
+__global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const ServeReq* __restrict__ req,
                                                        ServeResult* res, int nslots, const float* __restrict__ wts,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int D_, int n1_, int n2_,
@@ -111,7 +124,7 @@ __global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const float
   const int D = CD > 0 ? CD : D_, n1 = C1 > 0 ? C1 : n1_, n2 = C2 > 0 ? C2 : n2_;
   __shared__ float lw[MAXD * MAXH + MAXH + MAXH * MAXH + MAXH + MAXH * MAXH + MAXH + MAXH * MAXD + MAXD];
   __shared__ float lsc[MAXD], lsh[MAXD];
-  __shared__ float grp_buf[4][5][MAXD];   // group path: x, h1, h2, h3, y rows of up to 4 events
+  __shared__ float grp_buf[1][5][MAXD];   // latency path: x, h1, h2, h3, y rows of the event
   const int lane = threadIdx.x;
   const int nw = D * n1 + n1 + n1 * n2 + n2 + n2 * n2 + n2 + n2 * D + D;
   for (int i = lane; i < nw; i += 64) lw[i] = wts[i];
@@ -132,86 +145,127 @@ __global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const float
   uint64_t tail = ld_sys(&ctl->done);
   uint64_t last = __builtin_amdgcn_s_memrealtime();
   if (lane == 0) st_sys32(&ctl->alive, 1u);
-  while (true) {
-    const uint64_t head = ld_sys(&ctl->head);
-    if (head > tail) {
+  auto tagged = [](uint32_t tag, float v) { return ((uint64_t)tag << 32) | (uint64_t)__float_as_uint(v); };
+  auto tagged_u = [](uint32_t tag, uint32_t v) { return ((uint64_t)tag << 32) | (uint64_t)v; };
+  bool quit = false;
+  while (!quit) {
+    // Pipelined polling: three polls of the next slot (word `lane` + the head counter)
+    // in flight, spaced about a third of a PCIe round trip apart, so an event is seen
+    // ~RTT/3 after its row lands instead of up to a whole round trip later.  Each
+    // consumed poll is re-issued at once, which keeps the spacing.
+    const int slot0 = (int)(tail % (uint64_t)nslots);
+    SML_DCHECK(slot0 >= 0 && slot0 < nslots);
+    const uint32_t want = (uint32_t)(tail + 1);
+    const uint64_t* wp = &req[slot0].w[lane & (MAXD - 1)];
+    const uint64_t* hp = &ctl->head;
+    uint64_t w0, h0, w1, h1, w2, h2;
+    poll_issue(w0, h0, wp, hp);
+    __builtin_amdgcn_s_sleep(8);
+    poll_issue(w1, h1, wp, hp);
+    __builtin_amdgcn_s_sleep(8);
+    poll_issue(w2, h2, wp, hp);
+    uint64_t wv = 0, head = 0;
+    auto ready = [&](uint64_t w, uint64_t hd) {
+      const bool ok = lane >= D || (uint32_t)(w >> 32) == want;
+      return __ballot(ok) == ~0ull || hd > tail + 4;
+    };
+    for (uint32_t it = 0;; ++it) {
+      asm volatile("s_waitcnt vmcnt(4)" : "+v"(w0), "+v"(h0)::"memory");
+      if (ready(w0, h0)) { wv = w0; head = h0; break; }
+      poll_issue(w0, h0, wp, hp);
+      asm volatile("s_waitcnt vmcnt(4)" : "+v"(w1), "+v"(h1)::"memory");
+      if (ready(w1, h1)) { wv = w1; head = h1; break; }
+      poll_issue(w1, h1, wp, hp);
+      asm volatile("s_waitcnt vmcnt(4)" : "+v"(w2), "+v"(h2)::"memory");
+      if (ready(w2, h2)) { wv = w2; head = h2; break; }
+      poll_issue(w2, h2, wp, hp);
+      if ((it & 63) == 63) {   // exit conditions every wave reaches
+        if (ld_sys32(&ctl->stop) || __builtin_amdgcn_s_memrealtime() - last > idle_ticks) { quit = true; break; }
+      }
+    }
+    // the polls still in flight must land before their registers are reused
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(w0), "+v"(h0), "+v"(w1), "+v"(h1), "+v"(w2), "+v"(h2)::"memory");
+    if (quit) break;
+    const bool ok = lane >= D || (uint32_t)(wv >> 32) == want;
+    if (__ballot(ok) == ~0ull && head <= tail + 4) {
+      // latency path: the row arrived with the poll; 16 lanes, output-parallel layers
+      const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
+      float(*buf)[MAXD] = grp_buf[0];
+      if (lane < MAXD) buf[0][lane] = lane < D ? fmaf(__uint_as_float((uint32_t)wv), lsc[lane], lsh[lane]) : 0.f;
+      __syncthreads();
+      const int o = lane & 15;
+      const bool g0 = lane < 16;
+      if (g0) dense_group(W1, b1, D, n1, buf[0], buf[1], o, a1);
+      __syncthreads();
+      if (g0) dense_group(W2, b2, n1, n2, buf[1], buf[2], o, a2);
+      __syncthreads();
+      if (g0) dense_group(W3, b3, n2, n2, buf[2], buf[3], o, a3);
+      __syncthreads();
+      if (g0) dense_group(W4, b4, n2, D, buf[3], buf[4], o, a4);
+      __syncthreads();
+      const uint64_t t_comp = __builtin_amdgcn_s_memrealtime();
+      if (g0) {
+        ServeResult* r = res + slot0;
+        float se = 0.f;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int u = o + 16 * hh;
+          if (u < D) {
+            const float yv = buf[4][u], d = yv - buf[0][u];
+            se = fmaf(d, d, se);
+            st_sys(&r->w[u], tagged(want, yv));
+          }
+        }
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) se += __shfl_xor(se, m, 16);
+        if (o == 0) {
+          const float score = se / (float)D;
+          st_sys(&r->w[kServeScore], tagged(want, score));
+          st_sys(&r->w[kServeFlag], tagged_u(want, score > threshold ? 1u : 0u));
+          st_sys(&r->w[kServeTLoad], tagged_u(want, 0u));
+          st_sys(&r->w[kServeTComp], tagged_u(want, (uint32_t)(t_comp - t_seen)));
+          st_sys(&r->w[kServeTDone], tagged_u(want, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seen)));
+        }
+      }
+      tail += 1;
+      if (lane == 0) st_sys(&ctl->done, tail);   // back-pressure hint only: results carry their own tags
+      last = __builtin_amdgcn_s_memrealtime();
+    } else if (head > tail + 4) {
+      // backlog: one event per lane, up to 64 per pass (rows were published before head)
       const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
       const uint64_t k = head - tail < 64 ? head - tail : 64;
-      if (k <= 4) {
-        // latency path: one 16-lane group per event, output-parallel layers
-        const int grp = lane >> 4, o = lane & 15;
-        const bool act_g = (uint64_t)grp < k;
-        const uint64_t ev = tail + grp;
-        const int slot = (int)(ev % (uint64_t)nslots);
-        SML_DCHECK(slot >= 0 && slot < nslots);
-        float(*buf)[MAXD] = grp_buf[grp];
-        if (act_g && o < MAXD / 4) {
-          f32x4 q = ld_sys4_issue(req + (int64_t)slot * MAXD + 4 * o);
-          asm volatile("s_waitcnt vmcnt(0)" : "+v"(q)::"memory");
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int i = 4 * o + j;
-            buf[0][i] = i < D ? fmaf(q[j], lsc[i], lsh[i]) : 0.f;
-          }
-        }
-        __syncthreads();
-        const uint64_t t_loaded = __builtin_amdgcn_s_memrealtime();
-        if (act_g) dense_group(W1, b1, D, n1, buf[0], buf[1], o, a1);
-        __syncthreads();
-        if (act_g) dense_group(W2, b2, n1, n2, buf[1], buf[2], o, a2);
-        __syncthreads();
-        if (act_g) dense_group(W3, b3, n2, n2, buf[2], buf[3], o, a3);
-        __syncthreads();
-        if (act_g) dense_group(W4, b4, n2, D, buf[3], buf[4], o, a4);
-        __syncthreads();
-        const uint64_t t_comp = __builtin_amdgcn_s_memrealtime();
-        if (act_g) {
-          ServeResult* r = res + slot;
-          float se = 0.f;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int u = o + 16 * h;
-            if (u < D) {
-              const float yv = buf[4][u], d = yv - buf[0][u];
-              se = fmaf(d, d, se);
-              st_sysf(&r->recon[u], yv);
-            }
-          }
-#pragma unroll
-          for (int m = 1; m < 16; m <<= 1) se += __shfl_xor(se, m, 16);
-          if (o == 0) {
-            const float score = se / (float)D;
-            st_sysf(&r->score, score);
-            st_sys32(&r->flag, score > threshold ? 1u : 0u);
-            st_sys(&r->t_seen, t_seen);
-            st_sys(&r->t_loaded, t_loaded);
-            st_sys(&r->t_comp, t_comp);
-            st_sys(&r->t_done, __builtin_amdgcn_s_memrealtime());
-            st_sys(&r->seq, ev);
-          }
-        }
-      } else if ((uint64_t)lane < k) {
+      if ((uint64_t)lane < k) {
         const uint64_t ev = tail + lane;
+        const uint32_t tag = (uint32_t)(ev + 1);
         const int slot = (int)(ev % (uint64_t)nslots);
         SML_DCHECK(slot >= 0 && slot < nslots);
-        const float* xr = req + (int64_t)slot * MAXD;
         float x[MAXD], h1[MAXH], h2[MAXH], h3[MAXH], y[XD];
-        f32x4 q[MAXD / 4];
+        u32x4 q[MAXD / 2];
 #pragma unroll
-        for (int v = 0; v < MAXD / 4; ++v) q[v] = ld_sys4_issue(xr + 4 * v);   // slot padding is readable
+        for (int v = 0; v < MAXD / 2; ++v) q[v] = ld_sys_pair_issue(&req[slot].w[2 * v]);   // slot padding readable
         asm volatile("s_waitcnt vmcnt(0)"
                      : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5]), "+v"(q[6]),
-                       "+v"(q[7])::"memory");
-        const uint64_t t_loaded = __builtin_amdgcn_s_memrealtime();
+                       "+v"(q[7]), "+v"(q[8]), "+v"(q[9]), "+v"(q[10]), "+v"(q[11]), "+v"(q[12]), "+v"(q[13]),
+                       "+v"(q[14]), "+v"(q[15])::"memory");
 #pragma unroll
-        for (int i = 0; i < MAXD; ++i) x[i] = i < D ? fmaf(q[i / 4][i % 4], lsc[i], lsh[i]) : 0.f;
+        for (int i = 0; i < MAXD; ++i) {
+          uint32_t bits = q[i / 2][2 * (i % 2)], t = q[i / 2][2 * (i % 2) + 1];
+          if (i < D && t != tag) {
+            // the host publishes head after the rows, so this normally never runs; bounded
+            // so that a wave always reaches the exit conditions
+            uint64_t v = ld_sys(&req[slot].w[i]);
+            for (int spin = 0; (uint32_t)(v >> 32) != tag && spin < (1 << 20); ++spin) v = ld_sys(&req[slot].w[i]);
+            bits = (uint32_t)v;
+          }
+          x[i] = i < D ? fmaf(__uint_as_float(bits), lsc[i], lsh[i]) : 0.f;
+        }
+        const uint64_t t_loaded = __builtin_amdgcn_s_memrealtime();
         dense_lane<XD, X1>(W1, b1, D, n1, x, h1, a1);
         dense_lane<X1, X2>(W2, b2, n1, n2, h1, h2, a2);
         dense_lane<X2, X2>(W3, b3, n2, n2, h2, h3, a3);
         dense_lane<X2, XD>(W4, b4, n2, D, h3, y, a4);
-        float se = 0.f;
-        ServeResult* r = res + slot;
         const uint64_t t_comp = __builtin_amdgcn_s_memrealtime();
+        float se = 0.f;
 #pragma unroll
         for (int i = 0; i < MAXD; ++i) {
           if (i < D) {
@@ -219,28 +273,21 @@ __global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const float
             se = fmaf(d, d, se);
           }
         }
-        // relaxed system-scope scalar stores: issued back to back (no per-store wait)
+        ServeResult* r = res + slot;
 #pragma unroll
         for (int i = 0; i < XD; ++i)
-          if (i < D) st_sysf(&r->recon[i], y[i]);
+          if (i < D) st_sys(&r->w[i], tagged(tag, y[i]));
         const float score = se / (float)D;
-        st_sysf(&r->score, score);
-        st_sys32(&r->flag, score > threshold ? 1u : 0u);
-        st_sys(&r->t_seen, t_seen);
-        st_sys(&r->t_loaded, t_loaded);
-        st_sys(&r->t_comp, t_comp);
-        st_sys(&r->t_done, __builtin_amdgcn_s_memrealtime());
-        st_sys(&r->seq, ev);
+        st_sys(&r->w[kServeScore], tagged(tag, score));
+        st_sys(&r->w[kServeFlag], tagged_u(tag, score > threshold ? 1u : 0u));
+        st_sys(&r->w[kServeTLoad], tagged_u(tag, (uint32_t)(t_loaded - t_seen)));
+        st_sys(&r->w[kServeTComp], tagged_u(tag, (uint32_t)(t_comp - t_seen)));
+        st_sys(&r->w[kServeTDone], tagged_u(tag, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seen)));
       }
-      wait_stores();          // every lane's result stores acknowledged ...
       __syncthreads();
       tail += k;
-      if (lane == 0) st_sys(&ctl->done, tail);   // ... before the completion counter moves
+      if (lane == 0) st_sys(&ctl->done, tail);
       last = __builtin_amdgcn_s_memrealtime();
-    } else {
-      if (ld_sys32(&ctl->stop)) break;
-      if (__builtin_amdgcn_s_memrealtime() - last > idle_ticks) break;
-      __builtin_amdgcn_s_sleep(2);
     }
   }
   __syncthreads();
@@ -250,7 +297,7 @@ __global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const float
 
 }  // namespace
 
-hipError_t ae_serve_launch(ServeCtl* ctl, const float* req, ServeResult* res, int nslots, const float* wts,
+hipError_t ae_serve_launch(ServeCtl* ctl, const ServeReq* req, ServeResult* res, int nslots, const float* wts,
                            const float* scale, const float* shift, const int* dims, const int* acts, float threshold,
                            double idle_seconds, hipStream_t stream) {
   if (dims[0] < 1 || dims[0] > MAXD || dims[1] < 1 || dims[1] > MAXH || dims[2] < 1 || dims[2] > MAXH)

@@ -40,10 +40,10 @@ AEServe::AEServe(int device, int nslots, const std::vector<float>& weights, cons
   ck(hipSetDevice(device), "hipSetDevice");
   const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
   ck(hipHostMalloc((void**)&ctl_, sizeof(ServeCtl), fl), "hipHostMalloc ctl");
-  ck(hipHostMalloc((void**)&req_, sizeof(float) * 32 * (size_t)nslots, fl), "hipHostMalloc req");
+  ck(hipHostMalloc((void**)&req_, sizeof(ServeReq) * (size_t)nslots, fl), "hipHostMalloc req");
   ck(hipHostMalloc((void**)&res_, sizeof(ServeResult) * (size_t)nslots, fl), "hipHostMalloc res");
   std::memset(ctl_, 0, sizeof(ServeCtl));
-  std::memset(req_, 0, sizeof(float) * 32 * (size_t)nslots);
+  std::memset(req_, 0, sizeof(ServeReq) * (size_t)nslots);   // tag 0 = empty (tags start at 1)
   std::memset(res_, 0, sizeof(ServeResult) * (size_t)nslots);
   ck(hipHostGetDevicePointer((void**)&ctl_d_, ctl_, 0), "device ptr ctl");
   ck(hipHostGetDevicePointer((void**)&req_d_, req_, 0), "device ptr req");
@@ -88,30 +88,81 @@ uint64_t AEServe::submit(const float* rows, int k) {
   if (k <= 0) return head_;
   if (k > nslots_) throw std::invalid_argument("AEServe: more rows than slots");
   // back-pressure: never overwrite a slot whose event is not done
-  while (head_ + (uint64_t)k - load_acq(&ctl_->done) > (uint64_t)nslots_) wait(head_ + k - nslots_, 10.0);
+  if (head_ + (uint64_t)k > (uint64_t)nslots_) wait_done(head_ + (uint64_t)k - (uint64_t)nslots_, 10.0);
   const uint64_t first = head_;
   for (int i = 0; i < k; ++i) {
-    float* dst = req_ + (size_t)((first + i) % (uint64_t)nslots_) * 32;
-    std::memcpy(dst, rows + (size_t)i * D_, sizeof(float) * D_);
+    const uint64_t ev = first + (uint64_t)i;
+    ServeReq& dst = req_[ev % (uint64_t)nslots_];
+    const uint64_t tag = (uint64_t)(uint32_t)(ev + 1) << 32;
+    const float* row = rows + (size_t)i * D_;
+    for (int j = 0; j < D_; ++j) {   // 8-byte atomic stores: a word is never seen half-written
+      uint32_t bits;
+      std::memcpy(&bits, &row[j], 4);
+      __atomic_store_n(&dst.w[j], tag | bits, __ATOMIC_RELAXED);
+    }
   }
   head_ += k;
-  store_rel(&ctl_->head, head_);
+  store_rel(&ctl_->head, head_);   // after the rows: the backlog path trusts rows below head
   return first;
+}
+
+bool AEServe::complete(uint64_t seq) const {
+  const ServeResult& r = res_[seq % (uint64_t)nslots_];
+  const uint32_t tag = (uint32_t)(seq + 1);
+  for (int i = kServeScore; i < kServeWords; ++i)
+    if ((uint32_t)(__atomic_load_n(&r.w[i], __ATOMIC_RELAXED) >> 32) != tag) return false;
+  for (int i = 0; i < D_; ++i)
+    if ((uint32_t)(__atomic_load_n(&r.w[i], __ATOMIC_RELAXED) >> 32) != tag) return false;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  return true;
+}
+
+uint32_t AEServe::word(uint64_t seq, int i) const {
+  return (uint32_t)__atomic_load_n(&res_[seq % (uint64_t)nslots_].w[i], __ATOMIC_RELAXED);
+}
+
+float AEServe::score(uint64_t seq) const {
+  const uint32_t b = word(seq, kServeScore);
+  float f;
+  std::memcpy(&f, &b, 4);
+  return f;
+}
+
+void AEServe::wait_done(uint64_t n, double timeout_s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  uint32_t spins = 0;
+  while (load_acq(&ctl_->done) < n) {
+    cpu_relax();
+    if ((++spins & 0x3ff) == 0) {
+      if (hipStreamQuery(stream_) == hipSuccess && load_acq(&ctl_->done) < n) launch();
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > timeout_s) throw std::runtime_error("AEServe: timed out waiting for free slots");
+    }
+  }
 }
 
 void AEServe::wait(uint64_t seq_end, double timeout_s) {
   const auto t0 = std::chrono::steady_clock::now();
   uint32_t spins = 0;
-  while (load_acq(&ctl_->done) < seq_end) {
+  uint64_t ev = complete_ < seq_end ? std::max<uint64_t>(complete_, seq_end > (uint64_t)nslots_ ?
+                                                                       seq_end - (uint64_t)nslots_ : 0)
+                                    : seq_end;
+  while (ev < seq_end) {
+    if (complete(ev)) {
+      ++ev;
+      continue;
+    }
     cpu_relax();
     if ((++spins & 0x3ff) == 0) {
       // the kernel exits after idle_seconds without work, or may have raced its
-      // exit with our publish: relaunch it once it has really finished
-      if (hipStreamQuery(stream_) == hipSuccess && load_acq(&ctl_->done) < seq_end) launch();
+      // exit with our publish: relaunch it once it has really finished (it resumes
+      // at `done`, written after each event's result stores were issued)
+      if (hipStreamQuery(stream_) == hipSuccess && !complete(ev)) launch();
       const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (el > timeout_s) throw std::runtime_error("AEServe: timed out waiting for results");
     }
   }
+  complete_ = std::max(complete_, seq_end);
 }
 
 void AEServe::infer(const float* rows, int k, float* scores, uint32_t* flags, float* recon, double timeout_s) {
@@ -121,10 +172,14 @@ void AEServe::infer(const float* rows, int k, float* scores, uint32_t* flags, fl
     const uint64_t first = submit(rows + (size_t)off * D_, n);
     wait(first + n, timeout_s);
     for (int i = 0; i < n; ++i) {
-      const ServeResult& r = result(first + i);
-      if (scores) scores[off + i] = r.score;
-      if (flags) flags[off + i] = r.flag;
-      if (recon) std::memcpy(recon + (size_t)(off + i) * D_, r.recon, sizeof(float) * D_);
+      const uint64_t ev = first + (uint64_t)i;
+      if (scores) scores[off + i] = score(ev);
+      if (flags) flags[off + i] = word(ev, kServeFlag);
+      if (recon)
+        for (int j = 0; j < D_; ++j) {
+          const uint32_t b = word(ev, j);
+          std::memcpy(&recon[(size_t)(off + i) * D_ + j], &b, 4);
+        }
     }
     off += n;
   }
@@ -142,10 +197,9 @@ std::vector<int64_t> AEServe::latency_run(const float* rows, int n, int64_t gap_
     const auto t1 = std::chrono::steady_clock::now();
     lat[i] = std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
     if (dev_ns) {
-      const ServeResult& r = result(s);
       // 100 MHz ticks -> ns, packed: [total | load | compute] in three 21-bit fields (ns / 10)
-      const int64_t tot = (int64_t)(r.t_done - r.t_seen), ld = (int64_t)(r.t_loaded - r.t_seen),
-                    cp = (int64_t)(r.t_comp - r.t_loaded);
+      const int64_t tot = word(s, kServeTDone), ld = word(s, kServeTLoad),
+                    cp = (int64_t)word(s, kServeTComp) - (int64_t)word(s, kServeTLoad);
       (*dev_ns)[i] = (std::min<int64_t>(tot, 0x1fffff) << 42) | (std::min<int64_t>(ld, 0x1fffff) << 21) |
                      std::min<int64_t>(cp, 0x1fffff);
     }

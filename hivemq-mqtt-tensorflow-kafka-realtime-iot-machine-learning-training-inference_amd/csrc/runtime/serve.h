@@ -2,10 +2,12 @@
 //
 // Request slots, result slots and the control block are fine-grained pinned host
 // memory mapped into the GPU's address space, so an event travels host -> GPU ->
-// host with no hipMemcpy and no kernel launch: submit() writes the rows and
-// publishes the new head with a release store; the resident wave picks them up,
-// and wait() spins on the completion counter.  If the kernel exited (idle timeout
-// or a race with its exit), wait() relaunches it; it resumes at `done`.
+// host with no hipMemcpy and no kernel launch.  Slots are LL-framed (sml_ops.h):
+// submit() writes each row as tagged 8-byte words and then publishes the new head;
+// the resident wave polls the next slot's words directly; wait() polls the tagged
+// result words in host memory.  `done` is only a back-pressure / restart hint.  If
+// the kernel exited (idle timeout or a race with its exit), wait() relaunches it; it
+// resumes at `done`.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -27,9 +29,15 @@ class AEServe {
 
   // Publish k rows of D floats; returns the sequence number of the first one.
   uint64_t submit(const float* rows, int k);
-  // Block until every event < seq_end is done (throws after timeout_s).
+  // Block until the results of the events in [seq_end - nslots, seq_end) have landed
+  // (throws after timeout_s).
   void wait(uint64_t seq_end, double timeout_s);
   const ServeResult& result(uint64_t seq) const { return res_[seq % (uint64_t)nslots_]; }
+  // all tagged words of event seq's result have landed
+  bool complete(uint64_t seq) const;
+  // payload of result word i of event seq (call after complete())
+  uint32_t word(uint64_t seq, int i) const;
+  float score(uint64_t seq) const;
   // submit + wait + copy scores / flags (/ recon) for k rows.
   void infer(const float* rows, int k, float* scores, uint32_t* flags, float* recon, double timeout_s);
   // Per-event latency (ns) of n events submitted one at a time, spaced by gap_ns.
@@ -41,15 +49,17 @@ class AEServe {
 
  private:
   void launch();
+  // back-pressure: block until the device consumed every event < n (its request slot is free)
+  void wait_done(uint64_t n, double timeout_s);
   int device_, nslots_, D_;
   int dims_[3], acts_[4];
   float threshold_;
   double idle_s_;
   ServeCtl* ctl_ = nullptr;
-  float* req_ = nullptr;
+  ServeReq* req_ = nullptr;
   ServeResult* res_ = nullptr;
   ServeCtl* ctl_d_ = nullptr;
-  float* req_d_ = nullptr;
+  ServeReq* req_d_ = nullptr;
   ServeResult* res_d_ = nullptr;
   float* wts_d_ = nullptr;
   float* scale_d_ = nullptr;
@@ -57,6 +67,7 @@ class AEServe {
   hipStream_t stream_ = nullptr;
   uint64_t head_ = 0;
   uint64_t launches_ = 0;
+  uint64_t complete_ = 0;   // events known complete (prefix)
 };
 
 }  // namespace sml
