@@ -90,27 +90,6 @@ __device__ __forceinline__ void dense_lane(const float* __restrict__ W, const fl
   }
 }
 
-// Output-parallel layer for the latency path: the 16 lanes of a group share one
-// event; lane o computes units o and o + 16 of act(in . W + b).  Inputs and
-// outputs go through the group's LDS row (one broadcast read per input).
-__device__ __forceinline__ void dense_group(const float* __restrict__ W, const float* __restrict__ b, int in_n,
-                                            int out_n, const float* in, float* out, int o, int act) {
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int u = o + 16 * h;
-    if (u < out_n) {
-      float acc0 = b[u], acc1 = 0.f;
-      int i = 0;
-      for (; i + 1 < in_n; i += 2) {   // two independent chains halve the FMA latency
-        acc0 = fmaf(in[i], W[i * out_n + u], acc0);
-        acc1 = fmaf(in[i + 1], W[(i + 1) * out_n + u], acc1);
-      }
-      if (i < in_n) acc0 = fmaf(in[i], W[i * out_n + u], acc0);
-      out[u] = act_fwd(act, acc0 + acc1);
-    }
-  }
-}
-
 // CD / C1 / C2 > 0 fix (D, n1, n2) at compile time (compact straight-line code for
 // the reference configs: car data 18-14-7, credit card 30-14-7); 0 = runtime dims.
 template <int CD, int C1, int C2>
@@ -124,7 +103,6 @@ __global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const Serve
   const int D = CD > 0 ? CD : D_, n1 = C1 > 0 ? C1 : n1_, n2 = C2 > 0 ? C2 : n2_;
   __shared__ float lw[MAXD * MAXH + MAXH + MAXH * MAXH + MAXH + MAXH * MAXH + MAXH + MAXH * MAXD + MAXD];
   __shared__ float lsc[MAXD], lsh[MAXD];
-  __shared__ float grp_buf[1][5][MAXD];   // latency path: x, h1, h2, h3, y rows of the event
   const int lane = threadIdx.x;
   const int nw = D * n1 + n1 + n1 * n2 + n2 + n2 * n2 + n2 + n2 * D + D;
   for (int i = lane; i < nw; i += 64) lw[i] = wts[i];
@@ -141,6 +119,20 @@ __global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const Serve
   const float* b3 = W3 + n2 * n2;
   const float* W4 = b3 + n2;
   const float* b4 = W4 + n2 * D;
+  // latency path: lane u keeps column u of every layer's weights (and its biases) in registers
+  float rw1[XD], rw2[X1], rw3[X2], rw4[X2], rb[4];
+#pragma unroll
+  for (int i = 0; i < XD; ++i) rw1[i] = (i < D && lane < n1) ? W1[i * n1 + lane] : 0.f;
+#pragma unroll
+  for (int i = 0; i < X1; ++i) rw2[i] = (i < n1 && lane < n2) ? W2[i * n2 + lane] : 0.f;
+#pragma unroll
+  for (int i = 0; i < X2; ++i) rw3[i] = (i < n2 && lane < n2) ? W3[i * n2 + lane] : 0.f;
+#pragma unroll
+  for (int i = 0; i < X2; ++i) rw4[i] = (i < n2 && lane < D) ? W4[i * D + lane] : 0.f;
+  rb[0] = lane < n1 ? b1[lane] : 0.f;
+  rb[1] = lane < n2 ? b2[lane] : 0.f;
+  rb[2] = lane < n2 ? b3[lane] : 0.f;
+  rb[3] = lane < D ? b4[lane] : 0.f;
 
   uint64_t tail = ld_sys(&ctl->done);
   uint64_t last = __builtin_amdgcn_s_memrealtime();
@@ -188,44 +180,40 @@ __global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const Serve
     if (quit) break;
     const bool ok = lane >= D || (uint32_t)(wv >> 32) == want;
     if (__ballot(ok) == ~0ull && head <= tail + 4) {
-      // latency path: the row arrived with the poll; 16 lanes, output-parallel layers
+      // latency path: the row arrived with the poll, x_i in lane i.  Lane u computes
+      // output unit u of every layer from its register-resident weight column, taking
+      // the previous layer's activations straight from their lanes (v_readlane into an
+      // SGPR operand): no LDS round trip, no barrier, no second pass.
       const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
-      float(*buf)[MAXD] = grp_buf[0];
-      if (lane < MAXD) buf[0][lane] = lane < D ? fmaf(__uint_as_float((uint32_t)wv), lsc[lane], lsh[lane]) : 0.f;
-      __syncthreads();
-      const int o = lane & 15;
-      const bool g0 = lane < 16;
-      if (g0) dense_group(W1, b1, D, n1, buf[0], buf[1], o, a1);
-      __syncthreads();
-      if (g0) dense_group(W2, b2, n1, n2, buf[1], buf[2], o, a2);
-      __syncthreads();
-      if (g0) dense_group(W3, b3, n2, n2, buf[2], buf[3], o, a3);
-      __syncthreads();
-      if (g0) dense_group(W4, b4, n2, D, buf[3], buf[4], o, a4);
-      __syncthreads();
+      const int li = lane < MAXD ? lane : MAXD - 1;
+      const float xv = lane < D ? fmaf(__uint_as_float((uint32_t)wv), lsc[li], lsh[li]) : 0.f;
+      auto layer = [&](float in, const float* w_col, float bias, int in_n, int out_n, int act, auto INC) {
+        constexpr int IN_MAX = decltype(INC)::value;
+        float acc0 = bias, acc1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < IN_MAX; i += 2) {
+          if (i < in_n) acc0 = fmaf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(in), i)), w_col[i], acc0);
+          if (i + 1 < in_n)
+            acc1 = fmaf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(in), i + 1)), w_col[i + 1], acc1);
+        }
+        return lane < out_n ? act_fwd(act, acc0 + acc1) : 0.f;
+      };
+      const float v1 = layer(xv, rw1, rb[0], D, n1, a1, std::integral_constant<int, XD>{});
+      const float v2 = layer(v1, rw2, rb[1], n1, n2, a2, std::integral_constant<int, X1>{});
+      const float v3 = layer(v2, rw3, rb[2], n2, n2, a3, std::integral_constant<int, X2>{});
+      const float yv = layer(v3, rw4, rb[3], n2, D, a4, std::integral_constant<int, X2>{});
       const uint64_t t_comp = __builtin_amdgcn_s_memrealtime();
-      if (g0) {
-        ServeResult* r = res + slot0;
-        float se = 0.f;
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int u = o + 16 * hh;
-          if (u < D) {
-            const float yv = buf[4][u], d = yv - buf[0][u];
-            se = fmaf(d, d, se);
-            st_sys(&r->w[u], tagged(want, yv));
-          }
-        }
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) se += __shfl_xor(se, m, 16);
-        if (o == 0) {
-          const float score = se / (float)D;
-          st_sys(&r->w[kServeScore], tagged(want, score));
-          st_sys(&r->w[kServeFlag], tagged_u(want, score > threshold ? 1u : 0u));
-          st_sys(&r->w[kServeTLoad], tagged_u(want, 0u));
-          st_sys(&r->w[kServeTComp], tagged_u(want, (uint32_t)(t_comp - t_seen)));
-          st_sys(&r->w[kServeTDone], tagged_u(want, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seen)));
-        }
+      const float d = lane < D ? yv - xv : 0.f;
+      const float se = wave_sum(d * d);
+      ServeResult* r = res + slot0;
+      if (lane < D) st_sys(&r->w[lane], tagged(want, yv));
+      if (lane == 0) {
+        const float score = se / (float)D;
+        st_sys(&r->w[kServeScore], tagged(want, score));
+        st_sys(&r->w[kServeFlag], tagged_u(want, score > threshold ? 1u : 0u));
+        st_sys(&r->w[kServeTLoad], tagged_u(want, 0u));
+        st_sys(&r->w[kServeTComp], tagged_u(want, (uint32_t)(t_comp - t_seen)));
+        st_sys(&r->w[kServeTDone], tagged_u(want, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seen)));
       }
       tail += 1;
       if (lane == 0) st_sys(&ctl->done, tail);   // back-pressure hint only: results carry their own tags
