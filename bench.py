@@ -38,8 +38,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--batch-per-gpu", type=int, default=1 << 23)
-    p.add_argument("--dataset-rows", type=int, default=1 << 25, help="rows resident per GPU (ring)")
+    # 32 M rows (2.3 GB of raw input) per GPU per step: sized for 288 GB of HBM, it amortises the
+    # per-step slab reduction + Adam launches and makes the one gradient all-reduce per step
+    # (2.3 KB, latency-bound over xGMI) a ~1 % cost at 8 GPUs.  Measured on 1x MI355X:
+    # 8 M rows 30.1, 16 M 31.9, 32 M 32.9 G rows/s (profiles/r01_v5/SUMMARY.md).
+    p.add_argument("--batch-per-gpu", type=int, default=1 << 25)
+    p.add_argument("--dataset-rows", type=int, default=1 << 26, help="rows resident per GPU (ring of batches)")
     p.add_argument("--max-blocks", type=int, default=0, help="0 = two rounds of the resident capacity")
     p.add_argument("--infer-events", type=int, default=1000)
     p.add_argument("--seed", type=int, default=0)
