@@ -1,3 +1,4 @@
+// sml-build: no-slp
 // Fused dense-autoencoder kernels for gfx950 (MI355X).
 //
 // Model family: Input(D) -> Dense(n1, a1) -> Dense(n2, a2) -> Dense(n3, a3) -> Dense(D, a4)

@@ -26,7 +26,10 @@ def main():
     src = sys.argv[1]
     filt = sys.argv[2] if len(sys.argv) > 2 else ""
     with open(src) as f:   # same flags as _build.py (AGPR accumulators for files that ask for them)
-        vgpr_form = [] if "sml-build: agpr-accumulators" in f.read(512) else ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+        head = f.read(512)
+        vgpr_form = [] if "sml-build: agpr-accumulators" in head else ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+        if "sml-build: no-slp" in head:
+            vgpr_form += ["-fno-slp-vectorize"]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-munsafe-fp-atomics", *vgpr_form,
            "-I", os.path.join(PKG, "csrc", "include"), "-c", src, "-o", "/dev/null",
            "--offload-device-only", "-Rpass-analysis=kernel-resource-usage"]
