@@ -290,25 +290,6 @@ __device__ __forceinline__ void argmax_combine(float& bv, int& bi, float ov, int
   if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
 }
 
-__device__ __forceinline__ int row_argmax(const f32x4 v[2], int D, int g) {
-  float bv = -INFINITY;
-  int bi = 1 << 20;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = 16 * t + 4 * g + i;
-      if (f < D && v[t][i] > bv) { bv = v[t][i]; bi = f; }
-    }
-#pragma unroll
-  for (int o = 16; o <= 32; o <<= 1) {
-    float ov = __shfl_xor(bv, o, 64);
-    int oi = __shfl_xor(bi, o, 64);
-    argmax_combine(bv, bi, ov, oi);
-  }
-  return bi;
-}
-
 // Branch-free argmax over the 8 features a lane holds + its 3 partner lanes
 // (row r = lane & 15 is spread over lane groups g = 0..3).  Ties -> lowest index
 // (tf.argmax).  Features >= D are masked to -inf (lane-uniform compares, hoisted).
@@ -350,7 +331,7 @@ __device__ __forceinline__ int bfly_min(int x) {
 }
 
 template <bool LOW_REAL, int DC = 0>
-__device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], int D, int g, int lane) {
+__device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], int D, int g) {
   float vv[8];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -451,8 +432,8 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
       dz4[t][i] = act_grad(a4, y[t][i], two_over_d * e);
     }
   if (a.want_acc) {
-    const int iy = row_argmax_fast<LOW_REAL, DC>(y, a.D, g, lane);
-    const int ix = row_argmax_fast<LOW_REAL, DC>(xf, a.D, g, lane);
+    const int iy = row_argmax_fast<LOW_REAL, DC>(y, a.D, g);
+    const int ix = row_argmax_fast<LOW_REAL, DC>(xf, a.D, g);
     corr += (g == 0 && vm && iy == ix) ? 1.f : 0.f;
   }
   rows += (g == 0 && vm) ? 1.f : 0.f;

@@ -48,10 +48,6 @@ __device__ __forceinline__ void st_sys(uint64_t* p, uint64_t v) {
 __device__ __forceinline__ void st_sys32(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ float ld_sysf(const float* p) {
-  return __uint_as_float(ld_sys32(reinterpret_cast<const uint32_t*>(p)));
-}
-__device__ __forceinline__ void st_sysf(float* p, float v) { st_sys32(reinterpret_cast<uint32_t*>(p), __float_as_uint(v)); }
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // One poll: this lane's tagged word of the next request slot and the host's head

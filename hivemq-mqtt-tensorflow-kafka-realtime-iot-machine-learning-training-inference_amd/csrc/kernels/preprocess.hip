@@ -47,8 +47,9 @@ __global__ __launch_bounds__(kThreads) void filter_scatter_kernel(
   __shared__ float s_sc[64], s_sh[64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (threadIdx.x < 64) {
-    s_sc[threadIdx.x] = threadIdx.x < D ? (scale ? scale[threadIdx.x] : 1.0f) : 0.f;
-    s_sh[threadIdx.x] = (threadIdx.x < D && scale) ? shift[threadIdx.x] : 0.f;
+    const int f = (int)threadIdx.x;
+    s_sc[f] = f < D ? (scale ? scale[f] : 1.0f) : 0.f;
+    s_sh[f] = (f < D && scale) ? shift[f] : 0.f;
   }
   if (threadIdx.x == 0) {
     int b = 0;
