@@ -22,6 +22,13 @@ hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, f
                               float gscale, float* metrics_acc, int flags, int64_t* cursor, int64_t cursor_step,
                               int64_t cursor_ring, hipStream_t stream);
 
+// ---- persistent small-batch AE trainer (ae_minibatch.hip): nsteps Keras steps in one launch ----
+int ae_minibatch_max_batch();
+hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t* cursor, const float* scale,
+                               const float* shift, float* params, float* m, float* v, int64_t* iter, float* metrics,
+                               int B, int nsteps, const int* dims, const int* acts, float l1, float lr, float beta1,
+                               float beta2, float eps, float gscale, int want_acc, hipStream_t stream);
+
 // ---- LSTM recurrence (lstm.hip) ----
 hipError_t lstm_fwd_launch(const float* zx, const float* Uw, const float* h0, const float* c0, float* hseq,
                            float* cseq, float* gates, int64_t B, int T, int U, int act, hipStream_t stream);

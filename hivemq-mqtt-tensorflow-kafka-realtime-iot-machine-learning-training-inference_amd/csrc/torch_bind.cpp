@@ -179,6 +179,42 @@ void reduce_adam(const at::Tensor& partials, int64_t G, int64_t S, int64_t npara
                                         cursor_step, cursor_ring, cur_stream(partials)));
 }
 
+void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c10::optional<at::Tensor>& scale,
+                          const c10::optional<at::Tensor>& shift, const at::Tensor& params, const at::Tensor& m,
+                          const at::Tensor& v, const at::Tensor& iter, const c10::optional<at::Tensor>& metrics,
+                          int64_t batch, int64_t nsteps, std::vector<int64_t> dims, std::vector<int64_t> acts,
+                          double l1, double lr, double beta1, double beta2, double eps, double gscale, bool want_acc) {
+  check_ae_dims(dims, acts);
+  check_dev(x, "x", at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [ring, ld]");
+  TORCH_CHECK(x.size(1) >= dims[0], "x has fewer columns than the model input dim");
+  TORCH_CHECK(batch >= 1 && batch <= sml::ae_minibatch_max_batch(), "batch must be in [1, ",
+              sml::ae_minibatch_max_batch(), "]");
+  TORCH_CHECK(nsteps >= 1 && nsteps <= (1 << 30), "nsteps out of range");
+  TORCH_CHECK(x.size(0) >= batch && x.size(0) % batch == 0, "ring rows must be a positive multiple of the batch");
+  check_dev(cursor, "cursor", at::kLong);
+  check_dev(iter, "iter", at::kLong);
+  TORCH_CHECK(cursor.numel() == 1 && iter.numel() == 1, "cursor / iter must be 1-element int64");
+  for (const at::Tensor* t : {&params, &m, &v}) {
+    check_dev(*t, "params/m/v", at::kFloat);
+    TORCH_CHECK(t->numel() == sml::ae_nparam() && t->is_contiguous(), "params/m/v must be the padded image");
+  }
+  if (metrics.has_value()) TORCH_CHECK(metrics->numel() >= 4, "metrics needs 4 slots");
+  if (scale.has_value()) TORCH_CHECK(shift.has_value() && scale->numel() >= dims[0] && shift->numel() >= dims[0],
+                                     "scale requires shift, both [D]");
+  // the cursor is read on the device; its host-side validity is the caller's contract
+  // (FusedAE keeps it a multiple of the batch below the ring size)
+  c10::hip::HIPGuard guard(x.device().index());
+  int d[4] = {(int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3]};
+  int a[4] = {(int)acts[0], (int)acts[1], (int)acts[2], (int)acts[3]};
+  SML_CHECK_HIP(sml::ae_minibatch_launch(x.data_ptr<float>(), x.stride(0), x.size(0), cursor.data_ptr<int64_t>(),
+                                         opt_ptr(scale), opt_ptr(shift), params.data_ptr<float>(),
+                                         m.data_ptr<float>(), v.data_ptr<float>(), iter.data_ptr<int64_t>(),
+                                         opt_mut(metrics), (int)batch, (int)nsteps, d, a, (float)l1, (float)lr,
+                                         (float)beta1, (float)beta2, (float)eps, (float)gscale, (int)want_acc,
+                                         cur_stream(x)));
+}
+
 void ae_forward(const at::Tensor& x, const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift,
                 const at::Tensor& params, const c10::optional<at::Tensor>& recon,
                 const c10::optional<at::Tensor>& score, const c10::optional<at::Tensor>& flag, double threshold,
@@ -576,6 +612,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("partials"), py::arg("iter"),
         py::arg("dims"), py::arg("acts"), py::arg("l1"), py::arg("want_acc"), py::arg("max_blocks"),
         py::arg("n_rows") = -1, py::arg("cursor") = py::none());
+  m.def("ae_minibatch_max_batch", &sml::ae_minibatch_max_batch, "largest batch the persistent small-batch trainer takes");
+  m.def("ae_train_minibatches", &ae_train_minibatches,
+        "persistent small-batch AE trainer: nsteps sequential Keras steps (fwd+bwd+Adam) in one launch",
+        py::arg("x"), py::arg("cursor"), py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("m"),
+        py::arg("v"), py::arg("iter"), py::arg("metrics"), py::arg("batch"), py::arg("nsteps"), py::arg("dims"),
+        py::arg("acts"), py::arg("l1"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
+        py::arg("gscale"), py::arg("want_acc"));
   m.def("normalize_filter", &normalize_filter, "K8: normalise + keep rows with label == keep, order-preserving",
         py::arg("x"), py::arg("D"), py::arg("labels"), py::arg("keep"), py::arg("scale"), py::arg("shift"),
         py::arg("want_index") = false);

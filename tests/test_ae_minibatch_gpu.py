@@ -1,0 +1,97 @@
+"""Persistent small-batch AE trainer (csrc/kernels/ae_minibatch.hip) vs a plain PyTorch
+fp32 run of the same Keras steps (batch 32, one Adam update per batch).
+
+The kernel is fp32 end to end, so after many steps the parameters must agree with the
+torch oracle to summation-order rounding (no bf16 envelope as in test_ae_kernel_gpu)."""
+import numpy as np
+import pytest
+import torch
+
+from streamml.data.cardata import normalize_affine
+from streamml.models.reference import TorchAE, init_dense_weights
+from streamml.ops.ae import AESpec, FusedAE
+
+pytestmark = pytest.mark.gpu
+
+
+def _weights(spec, seed):
+    w = init_dense_weights(spec.layer_sizes, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    for i in range(1, 8, 2):
+        w[i] = rng.uniform(-0.2, 0.2, size=w[i].shape).astype(np.float32)
+    return w
+
+
+def _oracle(spec, w, xn, B, nsteps):
+    ref = TorchAE(spec.layer_sizes, spec.activations, spec.activity_l1, w)
+    n = xn.shape[0]
+    for s in range(nsteps):
+        r0 = (s * B) % n
+        ref.step(torch.from_numpy(xn[r0:r0 + B]))
+    return ref
+
+
+@pytest.mark.parametrize("D,B,nsteps,launches", [(18, 32, 50, 1), (18, 32, 64, 4), (30, 32, 40, 2),
+                                                 (18, 48, 30, 1), (18, 7, 25, 1)])
+def test_minibatch_steps_match_torch(cuda_device, D, B, nsteps, launches):
+    spec = AESpec(input_dim=D)
+    w = _weights(spec, seed=11)
+    rng = np.random.default_rng(3)
+    ring_rows = B * 20                       # wraps for nsteps > 20
+    raw = rng.uniform(0, 40, size=(ring_rows, D)).astype(np.float32)
+    if D == 18:
+        scale, shift = normalize_affine()
+    else:
+        scale = (np.full(D, 1 / 40.0)).astype(np.float32)
+        shift = np.zeros(D, np.float32)
+    xn = (raw * scale + shift).astype(np.float32)
+
+    fused = FusedAE(spec, w, cuda_device, scale=scale, shift=shift)
+    fused.attach_ring(torch.from_numpy(raw).to(cuda_device), B)
+    per = nsteps // launches
+    for _ in range(launches):
+        fused.train_minibatches(per)
+    torch.cuda.synchronize()
+    ref = _oracle(spec, w, xn, B, per * launches)
+
+    assert int(fused.iter.item()) == per * launches
+    assert int(fused.cursor.item()) == (per * launches * B) % ring_rows
+    for got, want in zip(fused.get_weights(), ref.get_weights()):
+        assert got.shape == want.shape
+        np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-5)
+    it, m, v = fused.get_optimizer_state()
+    for got, want in zip(m, ref.opt.m):
+        np.testing.assert_allclose(got, want.numpy(), rtol=2e-3, atol=1e-6)
+
+    mt = fused.read_metrics()
+    rm = ref.read_metrics()
+    assert mt["rows"] == per * launches * B
+    assert abs(mt["loss"] - rm["loss"]) <= 1e-4 * max(1.0, abs(rm["loss"]))
+    assert abs(mt["accuracy"] - rm["accuracy"]) < 1e-6
+
+
+def test_minibatch_matches_launch_per_step_path(cuda_device):
+    """Same stream through train_minibatches and step_ring (bf16 MFMA path): close, not equal."""
+    spec = AESpec()
+    w = _weights(spec, seed=4)
+    scale, shift = normalize_affine()
+    raw = torch.rand((32 * 16, 18), device=cuda_device) * 40.0
+    a = FusedAE(spec, w, cuda_device, scale=scale, shift=shift)
+    b = FusedAE(spec, w, cuda_device, scale=scale, shift=shift)
+    a.attach_ring(raw, 32)
+    b.attach_ring(raw, 32)
+    a.train_minibatches(16)
+    for _ in range(16):
+        b.step_ring()
+    torch.cuda.synchronize()
+    for ga, gb in zip(a.get_weights(), b.get_weights()):
+        assert np.max(np.abs(ga - gb)) < 2 * 1e-3 * 16   # Adam moves each weight <= ~lr per step
+    assert int(a.cursor.item()) == int(b.cursor.item()) == 0
+
+
+def test_minibatch_rejects_bad_batch(cuda_device):
+    spec = AESpec()
+    fused = FusedAE(spec, init_dense_weights(spec.layer_sizes, seed=0), cuda_device)
+    fused.attach_ring(torch.zeros((64 * 4, 18), device=cuda_device), 64)
+    with pytest.raises(ValueError):
+        fused.train_minibatches(2)
