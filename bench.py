@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--dataset-rows", type=int, default=1 << 26, help="rows resident per GPU (ring of batches)")
     p.add_argument("--max-blocks", type=int, default=0, help="0 = two rounds of the resident capacity")
     p.add_argument("--infer-events", type=int, default=1000)
+    p.add_argument("--batch32-steps", type=int, default=20000,
+                   help="steps per launch of the Keras batch-32 side measurement (0 = skip)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--dump-params", default=None,
                    help="write this rank's final parameter image to <path>.rank<R>.npy (replica checks)")
@@ -91,6 +93,30 @@ def measure_infer_p50(fused, device, n_events: int, model=None, qps: float = 100
             lat.append((t1 - t0) * 1e6)
     lat = np.asarray(lat)
     return float(np.percentile(lat, 50)), float(np.percentile(lat, 99))
+
+
+def measure_batch32(spec, data, device, steps, scale, shift, seed, launches=5):
+    """Side measurement at the reference's own optimizer granularity: one Adam step per
+    32 rows (Keras fit(batch_size=32)), ``steps`` sequential steps per launch of the
+    persistent small-batch kernel (csrc/kernels/ae_minibatch.hip, fp32)."""
+    import torch
+
+    from streamml.models.reference import init_dense_weights
+    from streamml.ops.ae import FusedAE
+
+    ae = FusedAE(spec, init_dense_weights(spec.layer_sizes, seed=seed), device, scale=scale, shift=shift)
+    ae.attach_ring(data, 32)
+    ae.train_minibatches(steps)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(launches):
+        ae.train_minibatches(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    n = steps * launches
+    return {"rows_per_s": n * 32 / dt, "us_per_step": dt / n * 1e6, "vs_baseline": n * 32 / dt / BASELINE_ROWS_PER_S,
+            "steps": n, "dtype": "fp32", "path": "persistent small-batch kernel (ae_minibatch.hip), 1 GPU",
+            "final_loss": ae.read_metrics()["loss"]}
 
 
 def main():
@@ -180,6 +206,9 @@ def main():
             print(f"[bench] persistent scorer unavailable ({e!r}); launch-per-event path", file=sys.stderr)
             p50, p99 = measure_infer_p50(fused, device, args.infer_events)
             infer_path = "launch-per-event"
+    b32 = None
+    if rank == 0 and args.batch32_steps > 0:
+        b32 = measure_batch32(spec, data, device, args.batch32_steps, scale, shift, args.seed)
     del nslices
     rows_per_s = gb * args.steps / elapsed
     if rank == 0:
@@ -209,6 +238,7 @@ def main():
             "hip_graph": graph is not None,
             "final_epoch_loss": metrics["loss"],
             "final_accuracy": metrics["accuracy"],
+            "keras_batch32": b32,
         }
         print(json.dumps(out), flush=True)
     dp.shutdown()

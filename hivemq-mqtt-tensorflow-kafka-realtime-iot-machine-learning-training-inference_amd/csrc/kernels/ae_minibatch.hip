@@ -12,7 +12,7 @@
 // registers one step ahead.  All arithmetic is fp32 (bit-for-bit Keras semantics
 // are limited only by summation order), so this is also the exact-semantics path.
 //
-// Layout (per workgroup, 256 threads = 4 waves):
+// Layout (per workgroup, 512 threads = 8 waves):
 //   weights in LDS, re-strided so every phase reads conflict-free:
 //     W1 [32][16] (bias row 31), W2/W3 [16][17] (bias row 15), W4 [16][33] (bias row 15)
 //   activations [B][stride] with a constant-1 column at the end (bias gradient =
@@ -27,7 +27,7 @@ using namespace sml;
 
 namespace {
 
-constexpr int NT = 256;
+constexpr int NT = 512;   // 8 waves: two per SIMD, so one wave's LDS / VALU latency hides behind the other's
 constexpr int MAXB = 48;   // Keras default batch 32 fits; Smem stays under the 64 KB dynamic-LDS default
 constexpr int XS = 33;   // input / output row stride (col 32 = 1.0)
 constexpr int HS = 17;   // hidden row stride         (col 16 = 1.0)
@@ -50,6 +50,7 @@ struct MBArgs {
   int B, nsteps, D, n1, n2, n3, a1, a2, a3, a4;
   float l1, lr, beta1, beta2, eps, gscale;
   int want_acc;
+  unsigned long long* prof;   // optional [9]: per-phase s_memtime cycles summed over steps (wave 0), + total
 };
 
 struct Smem {   // ~47 KB
@@ -58,7 +59,7 @@ struct Smem {   // ~47 KB
   float h1[MAXB * HS], h2[MAXB * HS], h3[MAXB * HS];
   float y[MAXB * XS];
   float dz4[MAXB * XS], dz3[MAXB * HS], dz2[MAXB * HS], dz1[MAXB * HS];
-  float red[4][NT / 64];
+  float red[3][NT / 64];
 };
 
 // image slot -> LDS weight index
@@ -72,7 +73,7 @@ __device__ __forceinline__ int lds_of_slot(int s) {
 
 // A 16x16 tile of the padded image whose gradient one wave computes with fp32 MFMAs
 // (v_mfma_f32_16x16x4f32: K = 4 batch rows per instruction).  Tiles: 0/1 = L1 rows
-// 0-15 / 16-31, 2 = L2, 3 = L3, 4/5 = L4 cols 0-15 / 16-31; wave w owns w and w+4.
+// 0-15 / 16-31, 2 = L2, 3 = L3, 4/5 = L4 cols 0-15 / 16-31; wave w < 6 owns tile w.
 struct Tile {
   int act, as;      // activation base (float offset into Smem; L1: buffer 0) and row stride
   int acol;         // this lane's activation column (image row m = row0 + c; bias row -> ones column)
@@ -115,35 +116,57 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // trip count is exact and lets every LDS read issue up front).
 template <int N>
 __device__ __forceinline__ float dotn(const float* act, const float* w, int wstride) {
-  float acc = 0.f;
+  float acc0 = 0.f, acc1 = 0.f;   // two chains: half the dependent-FMA latency
 #pragma unroll
-  for (int i = 0; i < N; ++i) acc = fmaf(act[i], w[i * wstride], acc);
-  return acc;
+  for (int i = 0; i < N; i += 2) {
+    acc0 = fmaf(act[i], w[i * wstride], acc0);
+    if (i + 1 < N) acc1 = fmaf(act[i + 1], w[(i + 1) * wstride], acc1);
+  }
+  return acc0 + acc1;
 }
 
-// KD: trip count over input features (D rounded to a compiled width); TB: batch (0 = runtime)
-template <int KD, int TB>
+// Activation codes: compile-time when PACK >= 0 (a1 | a2<<2 | a3<<4 | a4<<6), else runtime.
+constexpr int PACK_REF = ACT_TANH | (ACT_RELU << 2) | (ACT_TANH << 4) | (ACT_RELU << 6);
+template <int PACK>
+__device__ __forceinline__ int act_code(const MBArgs& a, int l) {
+  if constexpr (PACK >= 0) return (PACK >> (2 * l)) & 3;
+  else return l == 0 ? a.a1 : l == 1 ? a.a2 : l == 2 ? a.a3 : a.a4;
+}
+
+// Work items o = t + NT*u, u < N, fully unrolled so every item's LDS reads issue together.
+template <int N, class F>
+__device__ __forceinline__ void for_items(int t, int limit, F&& f) {
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    const int o = t + NT * u;
+    if (o < limit) f(o);
+  }
+}
+constexpr int I16 = (MAXB * 16 + NT - 1) / NT;
+
+// KD: trip count over input features (D rounded to a compiled width); TB: batch (0 = runtime);
+// PACK: activation codes (-1 = runtime)
+template <int KD, int TB, int PACK>
 __global__ __launch_bounds__(NT) void ae_minibatch_kernel(MBArgs a) {
   extern __shared__ float smem_raw[];
   Smem& S = *reinterpret_cast<Smem*>(smem_raw);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int B = TB ? TB : a.B, D = a.D, n1 = a.n1, n2 = a.n2, n3 = a.n3;
+  const int a1 = act_code<PACK>(a, 0), a2 = act_code<PACK>(a, 1), a3 = act_code<PACK>(a, 2), a4 = act_code<PACK>(a, 3);
   const float* sbase = smem_raw;
+  constexpr int IKD = (MAXB * KD + NT - 1) / NT;
+  static_assert(KD == 32 || KD < 32, "KD <= 32");
 
   // ---- gradient tiles + their Adam moments (registers for the whole launch) ----
   const int c = lane & 15, g = lane >> 4;
-  const bool two = wave < 2;
-  Tile tl[2];
-  float mo[2][4], vo[2][4];
+  const bool has_tile = wave < 6;
+  const Tile T = make_tile(has_tile ? wave : 0, c, g, S, sbase);
+  float mo[4], vo[4], wo[4];   // Adam moments + the parameters themselves (sole writer)
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    tl[k] = make_tile(k == 0 || !two ? wave : wave + 4, c, g, S, sbase);   // waves 2-3: one tile
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bool live = k == 0 || two;
-      mo[k][i] = live ? a.m[tl[k].slot[i]] : 0.f;
-      vo[k][i] = live ? a.v[tl[k].slot[i]] : 0.f;
-    }
+  for (int i = 0; i < 4; ++i) {
+    mo[i] = has_tile ? a.m[T.slot[i]] : 0.f;
+    vo[i] = has_tile ? a.v[T.slot[i]] : 0.f;
+    wo[i] = has_tile ? a.params[T.slot[i]] : 0.f;
   }
 
   // ---- weights -> LDS (padding zero), zeroed activations, constant-1 bias columns ----
@@ -161,7 +184,7 @@ __global__ __launch_bounds__(NT) void ae_minibatch_kernel(MBArgs a) {
   }
 
   // ---- input tiles: element e = t + NT*u of the MAXB x 32 tile (cols >= D -> 0) ----
-  constexpr int XU = MAXB * 32 / NT;   // 6 elements per thread
+  constexpr int XU = MAXB * 32 / NT;   // 3 elements per thread
   static_assert(MAXB * 32 % NT == 0, "input tile must split evenly over the threads");
   float sc[XU], sh[XU];
 #pragma unroll
@@ -199,95 +222,113 @@ __global__ __launch_bounds__(NT) void ae_minibatch_kernel(MBArgs a) {
   float sq = 0.f, ab = 0.f, corr = 0.f;
   const float two_over_d = 2.0f / (float)D;
   const int64_t it0 = a.iter[0];
+  // Adam bias corrections beta^t as running fp64 products (powf per step costs ~350
+  // instructions on the critical path; fp64 keeps the product exact to ~1e-16 * t)
+  double b1t = pow((double)a.beta1, (double)it0), b2t = pow((double)a.beta2, (double)it0);
+  const bool prof = a.prof != nullptr && t == 0;
+  unsigned long long pc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tp = 0, t_start = 0;
+  auto mark = [&](int k) {
+    if (prof) {
+      const unsigned long long now = __builtin_readcyclecounter();
+      pc[k] += now - tp;
+      tp = now;
+    }
+  };
   __syncthreads();
+  if (prof) t_start = tp = __builtin_readcyclecounter();
 
   for (int step = 0; step < a.nsteps; ++step) {
     const float* X = S.x[step & 1];
     // P1: h1 = act1(x W1 + b1)
-    for (int o = t; o < B * 16; o += NT) {
+    for_items<I16>(t, B * 16, [&](int o) {
       const int r = o >> 4, j = o & 15;
       const float z = dotn<KD>(X + r * XS, S.w + LW1 + j, 16) + S.w[LW1 + 31 * 16 + j];
-      const float h = j < n1 ? act_fwd(a.a1, z) : 0.f;
+      const float h = j < n1 ? act_fwd(a1, z) : 0.f;
       ab += fabsf(h);
       S.h1[r * HS + j] = h;
-    }
+    });
     lds_barrier();
+    mark(0);
     // P2, P3
-    for (int o = t; o < B * 16; o += NT) {
+    for_items<I16>(t, B * 16, [&](int o) {
       const int r = o >> 4, j = o & 15;
       const float z = dotn<16>(S.h1 + r * HS, S.w + LW2 + j, HS) + S.w[LW2 + 15 * HS + j];
-      S.h2[r * HS + j] = j < n2 ? act_fwd(a.a2, z) : 0.f;
-    }
+      S.h2[r * HS + j] = j < n2 ? act_fwd(a2, z) : 0.f;
+    });
     lds_barrier();
-    for (int o = t; o < B * 16; o += NT) {
+    mark(1);
+    for_items<I16>(t, B * 16, [&](int o) {
       const int r = o >> 4, j = o & 15;
       const float z = dotn<16>(S.h2 + r * HS, S.w + LW3 + j, HS) + S.w[LW3 + 15 * HS + j];
-      S.h3[r * HS + j] = j < n3 ? act_fwd(a.a3, z) : 0.f;
-    }
+      S.h3[r * HS + j] = j < n3 ? act_fwd(a3, z) : 0.f;
+    });
     lds_barrier();
-    // P4: y = act4(h3 W4 + b4); MSE; dz4 (sum-scaled, 1/B in gscale)
-    for (int o = t; o < B * 32; o += NT) {
-      const int r = o >> 5, j = o & 31;
+    mark(2);
+    // P4: y = act4(h3 W4 + b4); MSE; dz4 (sum-scaled, 1/B in gscale).  Items cover the
+    // KD real-or-padding columns only; columns >= KD stay at their zero initialisation.
+    for_items<IKD>(t, B * KD, [&](int o) {
+      const int r = o / KD, j = o - r * KD;
       const float z = dotn<16>(S.h3 + r * HS, S.w + LW4 + j, XS) + S.w[LW4 + 15 * XS + j];
-      const float y = j < D ? act_fwd(a.a4, z) : 0.f;
+      const float y = j < D ? act_fwd(a4, z) : 0.f;
       const float e = y - X[r * XS + j];
       sq = fmaf(e, e, sq);
       S.y[r * XS + j] = y;
-      S.dz4[r * XS + j] = j < D ? act_grad(a.a4, y, two_over_d * e) : 0.f;
-    }
+      S.dz4[r * XS + j] = j < D ? act_grad(a4, y, two_over_d * e) : 0.f;
+    });
     lds_barrier();
-    // P5: dz3 = act3'(dz4 W4^T); the last B threads also score argmax accuracy
-    for (int o = t; o < B * 16; o += NT) {
+    mark(3);
+    // P5: dz3 = act3'(dz4 W4^T)
+    for_items<I16>(t, B * 16, [&](int o) {
       const int r = o >> 4, i = o & 15;
-      const float d = act_grad(a.a3, S.h3[r * HS + i], dotn<KD>(S.dz4 + r * XS, S.w + LW4 + i * XS, 1));
+      const float d = act_grad(a3, S.h3[r * HS + i], dotn<KD>(S.dz4 + r * XS, S.w + LW4 + i * XS, 1));
       S.dz3[r * HS + i] = i < n3 ? d : 0.f;
-    }
-    if (a.want_acc && t >= NT - B) {
-      const int r = t - (NT - B);
-      int iy = 0, ix = 0;
-      float by = S.y[r * XS], bx = X[r * XS];
-      for (int f = 1; f < D; ++f) {   // ties -> lowest index (tf.argmax)
-        const float yv = S.y[r * XS + f], xv = X[r * XS + f];
-        if (yv > by) { by = yv; iy = f; }
-        if (xv > bx) { bx = xv; ix = f; }
-      }
-      corr += iy == ix ? 1.f : 0.f;
-    }
+    });
     lds_barrier();
+    mark(4);
     // P6: dz2 = act2'(dz3 W3^T)
-    for (int o = t; o < B * 16; o += NT) {
+    for_items<I16>(t, B * 16, [&](int o) {
       const int r = o >> 4, i = o & 15;
-      const float d = act_grad(a.a2, S.h2[r * HS + i], dotn<16>(S.dz3 + r * HS, S.w + LW3 + i * HS, 1));
+      const float d = act_grad(a2, S.h2[r * HS + i], dotn<16>(S.dz3 + r * HS, S.w + LW3 + i * HS, 1));
       S.dz2[r * HS + i] = i < n2 ? d : 0.f;
-    }
+    });
     lds_barrier();
+    mark(5);
     // P7: dz1 = act1'(dz2 W2^T + l1 * sign(h1))   (Keras L1 activity regulariser)
-    for (int o = t; o < B * 16; o += NT) {
+    for_items<I16>(t, B * 16, [&](int o) {
       const int r = o >> 4, i = o & 15;
       const float h = S.h1[r * HS + i];
       const float sgn = h != 0.f ? __builtin_copysignf(1.0f, h) : 0.f;
-      const float d = act_grad(a.a1, h, fmaf(a.l1, sgn, dotn<16>(S.dz2 + r * HS, S.w + LW2 + i * HS, 1)));
+      const float d = act_grad(a1, h, fmaf(a.l1, sgn, dotn<16>(S.dz2 + r * HS, S.w + LW2 + i * HS, 1)));
       S.dz1[r * HS + i] = i < n1 ? d : 0.f;
-    }
+    });
     lds_barrier();
+    mark(6);
     // P8: weight gradients = act^T . dz over the B rows (fp32 MFMA, K = 4 rows per
-    // instruction), Keras Adam on the tile in registers; next input tile to the other
-    // buffer; prefetch the one after.
-    const float tt = (float)(it0 + step + 1);
-    const float lr_t = a.lr * sqrtf(1.0f - powf(a.beta2, tt)) / (1.0f - powf(a.beta1, tt));
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (k == 1 && !two) break;
-      const Tile& T = tl[k];
+    // instruction), Keras Adam on the tile in registers (waves 0-5); argmax accuracy
+    // (waves 6-7, which own no tile); next input tile to the other buffer; prefetch.
+    if (step + 1 < a.nsteps) {   // next tile -> the other buffer (not read this phase)
+      stash(S.x[(step + 1) & 1]);
+      cur = nxt;
+      nxt = advance(cur);
+    }
+    b1t *= (double)a.beta1;
+    b2t *= (double)a.beta2;
+    const float lr_t = a.lr * sqrtf((float)(1.0 - b2t)) / (float)(1.0 - b1t);
+    if (has_tile) {
       const float* av = sbase + T.act + ((step & 1) && T.xb ? MAXB * XS : 0) + T.acol;
       const float* dv = sbase + T.dz;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if constexpr (TB > 0) {
+        f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};   // two independent MFMA chains, summed at the end
 #pragma unroll
-        for (int s4 = 0; s4 < TB / 4; ++s4) {
+        for (int s4 = 0; s4 < TB / 4; s4 += 2) {
           const int r = 4 * s4 + g;
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r * T.as], dv[r * T.ds], acc, 0, 0, 0);
+          if (s4 + 1 < TB / 4)
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[(r + 4) * T.as], dv[(r + 4) * T.ds], acc1, 0, 0, 0);
         }
+        acc += acc1;
       } else {
         for (int s4 = 0; s4 < (B + 3) / 4; ++s4) {
           const int r = 4 * s4 + g;
@@ -298,31 +339,39 @@ __global__ __launch_bounds__(NT) void ae_minibatch_kernel(MBArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float gr = acc[i] * a.gscale;
-        const float mm = a.beta1 * mo[k][i] + (1.0f - a.beta1) * gr;
-        const float vv = a.beta2 * vo[k][i] + (1.0f - a.beta2) * gr * gr;
-        mo[k][i] = mm;
-        vo[k][i] = vv;
-        S.w[T.w[i]] -= lr_t * mm / (sqrtf(vv) + a.eps);
+        const float mm = a.beta1 * mo[i] + (1.0f - a.beta1) * gr;
+        const float vv = a.beta2 * vo[i] + (1.0f - a.beta2) * gr * gr;
+        mo[i] = mm;
+        vo[i] = vv;
+        wo[i] -= lr_t * mm * __builtin_amdgcn_rcpf(sqrtf(vv) + a.eps);
+        S.w[T.w[i]] = wo[i];
       }
+    } else if (a.want_acc && t - 6 * 64 < B) {
+      const int r = t - 6 * 64;
+      int iy = 0, ix = 0;
+      float by = S.y[r * XS], bx = X[r * XS];
+#pragma unroll
+      for (int f = 1; f < KD; ++f) {   // ties -> lowest index (tf.argmax)
+        if (f < D) {
+          const float yv = S.y[r * XS + f], xv = X[r * XS + f];
+          if (yv > by) { by = yv; iy = f; }
+          if (xv > bx) { bx = xv; ix = f; }
+        }
+      }
+      corr += iy == ix ? 1.f : 0.f;
     }
-    if (step + 1 < a.nsteps) {
-      stash(S.x[(step + 1) & 1]);
-      cur = nxt;
-      nxt = advance(cur);
-      if (step + 2 < a.nsteps) fetch(nxt);
-    }
+    if (step + 2 < a.nsteps) fetch(nxt);
     lds_barrier();
+    mark(7);
   }
 
   // ---- write back: the whole image (padding slots keep zero gradients), moments, metrics ----
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    if (k == 1 && !two) break;
+  if (has_tile) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      a.params[tl[k].slot[i]] = S.w[tl[k].w[i]];
-      a.m[tl[k].slot[i]] = mo[k][i];
-      a.v[tl[k].slot[i]] = vo[k][i];
+      a.params[T.slot[i]] = wo[i];
+      a.m[T.slot[i]] = mo[i];
+      a.v[T.slot[i]] = vo[i];
     }
   }
   float vals[3] = {sq, ab, corr};
@@ -334,10 +383,19 @@ __global__ __launch_bounds__(NT) void ae_minibatch_kernel(MBArgs a) {
     if (lane == 0) S.red[k][wave] = s;
   }
   __syncthreads();
+  if (prof) {
+    pc[8] = __builtin_readcyclecounter() - t_start;
+    for (int k = 0; k < 9; ++k) a.prof[k] += pc[k];
+  }
   if (t == 0) {
     if (a.metrics) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) a.metrics[k] += S.red[k][0] + S.red[k][1] + S.red[k][2] + S.red[k][3];
+      for (int k = 0; k < 3; ++k) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) s += S.red[k][w];
+        a.metrics[k] += s;
+      }
       a.metrics[3] += (float)B * (float)a.nsteps;
     }
     a.iter[0] = it0 + a.nsteps;
@@ -354,13 +412,16 @@ int ae_minibatch_max_batch() { return MAXB; }
 hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t* cursor, const float* scale,
                                const float* shift, float* params, float* m, float* v, int64_t* iter, float* metrics,
                                int B, int nsteps, const int* dims, const int* acts, float l1, float lr, float beta1,
-                               float beta2, float eps, float gscale, int want_acc, hipStream_t stream) {
+                               float beta2, float eps, float gscale, int want_acc, unsigned long long* prof,
+                               hipStream_t stream) {
   if (B < 1 || B > MAXB || nsteps < 1 || ring < B || ring % B) return hipErrorInvalidValue;
   if (dims[0] > 31) return hipErrorInvalidValue;
   MBArgs a{x, ld, ring, cursor, scale, shift, params, m, v, iter, metrics, B, nsteps, dims[0], dims[1], dims[2],
-           dims[3], acts[0], acts[1], acts[2], acts[3], l1, lr, beta1, beta2, eps, gscale, want_acc};
-  auto k = dims[0] == 18 ? (B == 32 ? ae_minibatch_kernel<18, 32> : ae_minibatch_kernel<18, 0>)
-                         : (B == 32 ? ae_minibatch_kernel<32, 32> : ae_minibatch_kernel<32, 0>);
+           dims[3], acts[0], acts[1], acts[2], acts[3], l1, lr, beta1, beta2, eps, gscale, want_acc, prof};
+  const bool ref = acts[0] == ACT_TANH && acts[1] == ACT_RELU && acts[2] == ACT_TANH && acts[3] == ACT_RELU;
+  auto k = ae_minibatch_kernel<32, 0, -1>;   // any shape / activations
+  if (ref && dims[0] == 18) k = B == 32 ? ae_minibatch_kernel<18, 32, PACK_REF> : ae_minibatch_kernel<18, 0, PACK_REF>;
+  else if (ref) k = B == 32 ? ae_minibatch_kernel<32, 32, PACK_REF> : ae_minibatch_kernel<32, 0, PACK_REF>;
   hipLaunchKernelGGL(k, dim3(1), dim3(NT), sizeof(Smem), stream, a);
   return hipGetLastError();
 }

@@ -183,7 +183,8 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
                           const c10::optional<at::Tensor>& shift, const at::Tensor& params, const at::Tensor& m,
                           const at::Tensor& v, const at::Tensor& iter, const c10::optional<at::Tensor>& metrics,
                           int64_t batch, int64_t nsteps, std::vector<int64_t> dims, std::vector<int64_t> acts,
-                          double l1, double lr, double beta1, double beta2, double eps, double gscale, bool want_acc) {
+                          double l1, double lr, double beta1, double beta2, double eps, double gscale, bool want_acc,
+                          const c10::optional<at::Tensor>& prof) {
   check_ae_dims(dims, acts);
   check_dev(x, "x", at::kFloat);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [ring, ld]");
@@ -202,6 +203,12 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
   if (metrics.has_value()) TORCH_CHECK(metrics->numel() >= 4, "metrics needs 4 slots");
   if (scale.has_value()) TORCH_CHECK(shift.has_value() && scale->numel() >= dims[0] && shift->numel() >= dims[0],
                                      "scale requires shift, both [D]");
+  unsigned long long* prof_ptr = nullptr;
+  if (prof.has_value() && prof->defined()) {
+    check_dev(*prof, "prof", at::kLong);
+    TORCH_CHECK(prof->numel() >= 9, "prof needs 9 int64 slots");
+    prof_ptr = reinterpret_cast<unsigned long long*>(prof->data_ptr<int64_t>());
+  }
   // the cursor is read on the device; its host-side validity is the caller's contract
   // (FusedAE keeps it a multiple of the batch below the ring size)
   c10::hip::HIPGuard guard(x.device().index());
@@ -212,7 +219,7 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
                                          m.data_ptr<float>(), v.data_ptr<float>(), iter.data_ptr<int64_t>(),
                                          opt_mut(metrics), (int)batch, (int)nsteps, d, a, (float)l1, (float)lr,
                                          (float)beta1, (float)beta2, (float)eps, (float)gscale, (int)want_acc,
-                                         cur_stream(x)));
+                                         prof_ptr, cur_stream(x)));
 }
 
 void ae_forward(const at::Tensor& x, const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift,
@@ -618,7 +625,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("cursor"), py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("m"),
         py::arg("v"), py::arg("iter"), py::arg("metrics"), py::arg("batch"), py::arg("nsteps"), py::arg("dims"),
         py::arg("acts"), py::arg("l1"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
-        py::arg("gscale"), py::arg("want_acc"));
+        py::arg("gscale"), py::arg("want_acc"), py::arg("prof") = py::none());
   m.def("normalize_filter", &normalize_filter, "K8: normalise + keep rows with label == keep, order-preserving",
         py::arg("x"), py::arg("D"), py::arg("labels"), py::arg("keep"), py::arg("scale"), py::arg("shift"),
         py::arg("want_index") = false);

@@ -211,7 +211,7 @@ class FusedAE:
             allreduce(self.grad)
             self.reduce(1, RA_ADAM | RA_METRICS | RA_ADVANCE, gscale=1.0 / gb, partials=self.grad)
 
-    def train_minibatches(self, nsteps: int) -> None:
+    def train_minibatches(self, nsteps: int, prof: Optional[torch.Tensor] = None) -> None:
         """``nsteps`` sequential optimizer steps of ``ring_batch`` rows each, in ONE launch.
 
         Keras ``fit(batch_size=32)`` semantics (one Adam update per small batch, the
@@ -219,6 +219,7 @@ class FusedAE:
         persistent kernel in ``csrc/kernels/ae_minibatch.hip`` keeps parameters, Adam
         moments and activations on chip and consumes the attached ring from the device
         cursor.  fp32 arithmetic.  Single replica (no all-reduce between the steps).
+        ``prof`` (int64 [9], optional) accumulates per-phase shader cycles of wave 0.
         """
         if self.ring is None:
             raise RuntimeError("attach_ring() first")
@@ -228,7 +229,7 @@ class FusedAE:
         self.C.ae_train_minibatches(self.ring, self.cursor, self.scale, self.shift, self.params, self.m, self.v,
                                     self.iter, self.metrics, B, int(nsteps), self.spec.dims, self.spec.act_codes,
                                     float(self.spec.activity_l1), self.lr, self.beta_1, self.beta_2, self.epsilon,
-                                    1.0 / B, bool(self.want_acc))
+                                    1.0 / B, bool(self.want_acc), prof)
 
     def step(self, x: torch.Tensor, global_batch: Optional[int] = None, allreduce=None) -> None:
         """One full optimizer step on ``x`` (all rows of the local micro-batch).

@@ -31,15 +31,22 @@ def _oracle(spec, w, xn, B, nsteps):
     return ref
 
 
-@pytest.mark.parametrize("D,B,nsteps,launches", [(18, 32, 50, 1), (18, 32, 64, 4), (30, 32, 40, 2),
-                                                 (18, 48, 30, 1), (18, 7, 25, 1)])
-def test_minibatch_steps_match_torch(cuda_device, D, B, nsteps, launches):
-    spec = AESpec(input_dim=D)
+REF_ACTS = ("tanh", "relu", "tanh", "relu")
+
+
+@pytest.mark.parametrize("D,B,nsteps,launches,acts", [
+    (18, 32, 50, 1, REF_ACTS), (18, 32, 64, 4, REF_ACTS), (30, 32, 40, 2, REF_ACTS), (18, 48, 30, 1, REF_ACTS),
+    (18, 7, 25, 1, REF_ACTS),
+    (18, 32, 30, 1, ("sigmoid", "linear", "relu", "sigmoid")),   # runtime-activation instantiation
+    (11, 20, 30, 3, ("relu", "tanh", "linear", "tanh")),
+])
+def test_minibatch_steps_match_torch(cuda_device, D, B, nsteps, launches, acts):
+    spec = AESpec(input_dim=D, activations=acts)
     w = _weights(spec, seed=11)
     rng = np.random.default_rng(3)
     ring_rows = B * 20                       # wraps for nsteps > 20
     raw = rng.uniform(0, 40, size=(ring_rows, D)).astype(np.float32)
-    if D == 18:
+    if D == 18 and acts == REF_ACTS:
         scale, shift = normalize_affine()
     else:
         scale = (np.full(D, 1 / 40.0)).astype(np.float32)
