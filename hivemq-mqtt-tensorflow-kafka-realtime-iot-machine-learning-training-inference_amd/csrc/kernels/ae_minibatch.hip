@@ -50,7 +50,8 @@ struct MBArgs {
   int B, nsteps, D, n1, n2, n3, a1, a2, a3, a4;
   float l1, lr, beta1, beta2, eps, gscale;
   int want_acc;
-  unsigned long long* prof;   // optional [9]: per-phase s_memtime cycles summed over steps (wave 0), + total
+  unsigned long long* prof;   // optional [11]: per-phase cycles summed over steps (wave 0): 8 phases, total,
+                              // P8's input stash, P8's gradient MFMAs + Adam
 };
 
 struct Smem {   // ~47 KB
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(NT) void ae_minibatch_kernel(MBArgs a) {
   // instructions on the critical path; fp64 keeps the product exact to ~1e-16 * t)
   double b1t = pow((double)a.beta1, (double)it0), b2t = pow((double)a.beta2, (double)it0);
   const bool prof = a.prof != nullptr && t == 0;
-  unsigned long long pc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long pc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tp = 0, t_start = 0;
   auto mark = [&](int k) {
     if (prof) {
@@ -312,23 +313,26 @@ __global__ __launch_bounds__(NT) void ae_minibatch_kernel(MBArgs a) {
       cur = nxt;
       nxt = advance(cur);
     }
+    mark(9);
     b1t *= (double)a.beta1;
     b2t *= (double)a.beta2;
-    const float lr_t = a.lr * sqrtf((float)(1.0 - b2t)) / (float)(1.0 - b1t);
+    const float lr_t = a.lr * __builtin_amdgcn_sqrtf((float)(1.0 - b2t)) * __builtin_amdgcn_rcpf((float)(1.0 - b1t));
     if (has_tile) {
       const float* av = sbase + T.act + ((step & 1) && T.xb ? MAXB * XS : 0) + T.acol;
       const float* dv = sbase + T.dz;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if constexpr (TB > 0) {
-        f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};   // two independent MFMA chains, summed at the end
+        constexpr int CH = TB / 4 >= 4 ? 4 : TB / 4;   // independent MFMA chains, summed at the end
+        f32x4 part[CH];
 #pragma unroll
-        for (int s4 = 0; s4 < TB / 4; s4 += 2) {
+        for (int c4 = 0; c4 < CH; ++c4) part[c4] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s4 = 0; s4 < TB / 4; ++s4) {
           const int r = 4 * s4 + g;
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r * T.as], dv[r * T.ds], acc, 0, 0, 0);
-          if (s4 + 1 < TB / 4)
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[(r + 4) * T.as], dv[(r + 4) * T.ds], acc1, 0, 0, 0);
+          part[s4 % CH] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r * T.as], dv[r * T.ds], part[s4 % CH], 0, 0, 0);
         }
-        acc += acc1;
+#pragma unroll
+        for (int c4 = 0; c4 < CH; ++c4) acc += part[c4];
       } else {
         for (int s4 = 0; s4 < (B + 3) / 4; ++s4) {
           const int r = 4 * s4 + g;
@@ -343,20 +347,22 @@ __global__ __launch_bounds__(NT) void ae_minibatch_kernel(MBArgs a) {
         const float vv = a.beta2 * vo[i] + (1.0f - a.beta2) * gr * gr;
         mo[i] = mm;
         vo[i] = vv;
-        wo[i] -= lr_t * mm * __builtin_amdgcn_rcpf(sqrtf(vv) + a.eps);
+        wo[i] -= lr_t * mm * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv) + a.eps);   // v_sqrt / v_rcp, ~1 ulp
         S.w[T.w[i]] = wo[i];
       }
+      mark(10);
     } else if (a.want_acc && t - 6 * 64 < B) {
       const int r = t - 6 * 64;
       int iy = 0, ix = 0;
       float by = S.y[r * XS], bx = X[r * XS];
 #pragma unroll
-      for (int f = 1; f < KD; ++f) {   // ties -> lowest index (tf.argmax)
-        if (f < D) {
-          const float yv = S.y[r * XS + f], xv = X[r * XS + f];
-          if (yv > by) { by = yv; iy = f; }
-          if (xv > bx) { bx = xv; ix = f; }
-        }
+      for (int f = 1; f < KD; ++f) {   // ties -> lowest index (tf.argmax); branch-free selects
+        const float yv = S.y[r * XS + f], xv = X[r * XS + f];
+        const bool gy = f < D && yv > by, gx = f < D && xv > bx;
+        by = gy ? yv : by;
+        iy = gy ? f : iy;
+        bx = gx ? xv : bx;
+        ix = gx ? f : ix;
       }
       corr += iy == ix ? 1.f : 0.f;
     }
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(NT) void ae_minibatch_kernel(MBArgs a) {
   __syncthreads();
   if (prof) {
     pc[8] = __builtin_readcyclecounter() - t_start;
-    for (int k = 0; k < 9; ++k) a.prof[k] += pc[k];
+    for (int k = 0; k < 11; ++k) a.prof[k] += pc[k];
   }
   if (t == 0) {
     if (a.metrics) {

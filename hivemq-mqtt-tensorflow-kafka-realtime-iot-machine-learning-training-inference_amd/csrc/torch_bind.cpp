@@ -206,7 +206,7 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
   unsigned long long* prof_ptr = nullptr;
   if (prof.has_value() && prof->defined()) {
     check_dev(*prof, "prof", at::kLong);
-    TORCH_CHECK(prof->numel() >= 9, "prof needs 9 int64 slots");
+    TORCH_CHECK(prof->numel() >= 11, "prof needs 11 int64 slots");
     prof_ptr = reinterpret_cast<unsigned long long*>(prof->data_ptr<int64_t>());
   }
   // the cursor is read on the device; its host-side validity is the caller's contract

@@ -219,7 +219,7 @@ class FusedAE:
         persistent kernel in ``csrc/kernels/ae_minibatch.hip`` keeps parameters, Adam
         moments and activations on chip and consumes the attached ring from the device
         cursor.  fp32 arithmetic.  Single replica (no all-reduce between the steps).
-        ``prof`` (int64 [9], optional) accumulates per-phase shader cycles of wave 0.
+        ``prof`` (int64 [11], optional) accumulates per-phase shader cycles of wave 0.
         """
         if self.ring is None:
             raise RuntimeError("attach_ring() first")
