@@ -20,7 +20,11 @@ timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d "$GRAFT_REPO
 cd "$GRAFT_REPO_ROOT"
 step bench_lstm 600 python bench/bench_lstm.py
 step bench_infer 600 python bench/bench_infer.py
+step bench_minibatch 300 python bench/bench_minibatch.py
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_lstm" -o run \
    -- python3 "$GRAFT_REPO_ROOT/bench/bench_lstm.py" --steps 10 --warmup 2 > "$GRAFT_REPO_ROOT/gpurun_out/rocprof_lstm.log" 2>&1 \
    || { echo "rocprof lstm failed"; exit 1; }
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_mb" -o run \
+   -- python3 "$GRAFT_REPO_ROOT/bench/bench_minibatch.py" --launches 2 > "$GRAFT_REPO_ROOT/gpurun_out/rocprof_mb.log" 2>&1 \
+   || { echo "rocprof minibatch failed"; exit 1; }
 echo "== done"
