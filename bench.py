@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--dataset-rows", type=int, default=1 << 26, help="rows resident per GPU (ring of batches)")
     p.add_argument("--max-blocks", type=int, default=0, help="0 = two rounds of the resident capacity")
     p.add_argument("--infer-events", type=int, default=1000)
+    p.add_argument("--fleet-models", type=int, default=1024,
+                   help="side measurement: batch-32 training of this many independent models at once (0 = skip)")
     p.add_argument("--batch32-steps", type=int, default=20000,
                    help="steps per launch of the Keras batch-32 side measurement (0 = skip)")
     p.add_argument("--seed", type=int, default=0)
@@ -117,6 +119,30 @@ def measure_batch32(spec, data, device, steps, scale, shift, seed, launches=5):
     return {"rows_per_s": n * 32 / dt, "us_per_step": dt / n * 1e6, "vs_baseline": n * 32 / dt / BASELINE_ROWS_PER_S,
             "steps": n, "dtype": "fp32", "path": "persistent small-batch kernel (ae_minibatch.hip), 1 GPU",
             "final_loss": ae.read_metrics()["loss"]}
+
+
+def measure_batch32_fleet(spec, data, device, steps, scale, shift, n_models=1024, launches=3):
+    """The same Keras batch-32 semantics for a fleet of independent models (one per car /
+    device group), one workgroup each (ops/ae_fleet.py): aggregate rows/s over the fleet."""
+    import torch
+
+    from streamml.ops.ae_fleet import AEFleet
+
+    fleet = AEFleet.from_seeds(spec, range(n_models), device, scale=scale, shift=shift)
+    n = (data.size(0) // 32) * 32
+    stride = (n // n_models // 32) * 32
+    fleet.attach_rings(data[:n], 32, offsets=[i * stride for i in range(n_models)])
+    fleet.train_minibatches(steps)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(launches):
+        fleet.train_minibatches(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    rows = n_models * steps * launches * 32
+    return {"rows_per_s": rows / dt, "models": n_models, "us_per_step_per_model": dt / (steps * launches) * 1e6,
+            "vs_baseline": rows / dt / BASELINE_ROWS_PER_S, "steps_per_model": steps * launches, "dtype": "fp32",
+            "path": "fleet mode of ae_minibatch.hip (one workgroup per independent model), 1 GPU"}
 
 
 def main():
@@ -209,6 +235,9 @@ def main():
     b32 = None
     if rank == 0 and args.batch32_steps > 0:
         b32 = measure_batch32(spec, data, device, args.batch32_steps, scale, shift, args.seed)
+        if args.fleet_models > 0:
+            b32["fleet"] = measure_batch32_fleet(spec, data, device, max(args.batch32_steps // 10, 1), scale, shift,
+                                                 args.fleet_models)
     del nslices
     rows_per_s = gb * args.steps / elapsed
     if rank == 0:

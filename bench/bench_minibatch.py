@@ -74,16 +74,47 @@ def measure(device, batch=32, steps_per_launch=20000, launches=5, launch_steps=2
     return out
 
 
+def measure_fleet(device, n_models, batch=32, steps_per_launch=2000, launches=3):
+    """Fleet mode: ``n_models`` independent models, one workgroup each (ops/ae_fleet.py)."""
+    import torch
+
+    from streamml.data.cardata import normalize_affine, synthetic_device_tensor
+    from streamml.ops.ae import AESpec
+    from streamml.ops.ae_fleet import AEFleet
+
+    spec = AESpec()
+    scale, shift = normalize_affine()
+    rows = batch * 32768
+    data = synthetic_device_tensor(rows, device, seed=0, n_devices=100_000)
+    fleet = AEFleet.from_seeds(spec, range(n_models), device, scale=scale, shift=shift)
+    stride = (rows // n_models // batch) * batch
+    fleet.attach_rings(data, batch, offsets=[i * stride for i in range(n_models)])
+    fleet.train_minibatches(steps_per_launch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(launches):
+        fleet.train_minibatches(steps_per_launch)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    n = launches * steps_per_launch
+    return {"models": n_models, "rows_per_s": n_models * n * batch / dt, "us_per_step_per_model": dt / n * 1e6,
+            "mean_final_loss": sum(m["loss"] for m in fleet.read_metrics()) / n_models}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--steps-per-launch", type=int, default=20000)
     ap.add_argument("--launches", type=int, default=5)
+    ap.add_argument("--fleet", default="256,512,768,1024,1536",
+                    help="comma-separated fleet sizes for the multi-model sweep ('' = skip)")
     args = ap.parse_args()
     import torch
 
     dev = torch.device("cuda", 0)
     r = measure(dev, args.batch, args.steps_per_launch, args.launches)
+    if args.fleet:
+        r["fleet"] = [measure_fleet(dev, int(m), args.batch) for m in args.fleet.split(",")]
     base = 62661.0
     print(json.dumps({"metric": "AE train rows/s at Keras batch 32 (one Adam step per batch)",
                       "value": r["persistent_rows_per_s"], "unit": "rows/s", "vs_baseline": r["persistent_rows_per_s"] / base,

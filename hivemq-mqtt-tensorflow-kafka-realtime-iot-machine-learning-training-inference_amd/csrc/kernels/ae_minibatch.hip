@@ -21,6 +21,10 @@
 //   its Adam m / v in registers for the whole launch.
 // Per step: 8 phases separated by 8 barriers (fwd L1..L4 + loss, bwd L4..L2 with
 // argmax accuracy, then gradients + Adam + the next input tile).
+// Fleet mode: a grid of M workgroups trains M independent models at once (per-device
+// digital-twin models, ensembles, learning-rate sweeps), one per workgroup, each with
+// its own parameters, optimizer state, ring cursor and metrics.  A single model
+// occupies one CU; M >= 256 fills the chip (~47 KB LDS -> 3 workgroups per CU).
 #include "sml_common.h"
 
 using namespace sml;
@@ -51,7 +55,11 @@ struct MBArgs {
   float l1, lr, beta1, beta2, eps, gscale;
   int want_acc;
   unsigned long long* prof;   // optional [11]: per-phase cycles summed over steps (wave 0): 8 phases, total,
-                              // P8's input stash, P8's gradient MFMAs + Adam
+                              // P8's input stash, P8's gradient MFMAs + Adam (model 0 only)
+  // fleet mode: workgroup b trains model b.  params / m / v are [M][NPARAM], iter /
+  // cursor [M], metrics [M][4]; model b reads x + b * xmodel (0 = one shared ring).
+  int64_t xmodel;
+  const float* lrs;     // optional [M] per-model learning rates (hyper-parameter sweeps)
 };
 
 struct Smem {   // ~47 KB
@@ -146,10 +154,25 @@ __device__ __forceinline__ void for_items(int t, int limit, F&& f) {
 constexpr int I16 = (MAXB * 16 + NT - 1) / NT;
 
 // KD: trip count over input features (D rounded to a compiled width); TB: batch (0 = runtime);
-// PACK: activation codes (-1 = runtime)
-template <int KD, int TB, int PACK>
-__global__ __launch_bounds__(NT) void ae_minibatch_kernel(MBArgs a) {
+// PACK: activation codes (-1 = runtime); WPE: minimum waves per SIMD the register
+// allocation must allow (2 = one workgroup per CU, the latency-optimal single-model
+// build; 4 = <= 128 VGPRs, two fleet models per CU)
+template <int KD, int TB, int PACK, int WPE = 2>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void ae_minibatch_kernel(MBArgs a0) {
   extern __shared__ float smem_raw[];
+  MBArgs a = a0;   // fleet mode: rebase every per-model pointer on the workgroup's model
+  {
+    const int mdl = blockIdx.x;
+    a.x += mdl * a.xmodel;
+    a.params += mdl * NPARAM;
+    a.m += mdl * NPARAM;
+    a.v += mdl * NPARAM;
+    a.iter += mdl;
+    if (a.cursor) a.cursor += mdl;
+    if (a.metrics) a.metrics += 4 * mdl;
+    if (a.lrs) a.lr = a.lrs[mdl];
+    if (mdl) a.prof = nullptr;
+  }
   Smem& S = *reinterpret_cast<Smem*>(smem_raw);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int B = TB ? TB : a.B, D = a.D, n1 = a.n1, n2 = a.n2, n3 = a.n3;
@@ -226,7 +249,7 @@ __global__ __launch_bounds__(NT) void ae_minibatch_kernel(MBArgs a) {
   // Adam bias corrections beta^t as running fp64 products (powf per step costs ~350
   // instructions on the critical path; fp64 keeps the product exact to ~1e-16 * t)
   double b1t = pow((double)a.beta1, (double)it0), b2t = pow((double)a.beta2, (double)it0);
-  const bool prof = a.prof != nullptr && t == 0;
+  const bool prof = WPE == 2 && a.prof != nullptr && t == 0;   // fleet build: no profiling registers
   unsigned long long pc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tp = 0, t_start = 0;
   auto mark = [&](int k) {
@@ -419,16 +442,21 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
                                const float* shift, float* params, float* m, float* v, int64_t* iter, float* metrics,
                                int B, int nsteps, const int* dims, const int* acts, float l1, float lr, float beta1,
                                float beta2, float eps, float gscale, int want_acc, unsigned long long* prof,
-                               hipStream_t stream) {
+                               int nmodels, int64_t xmodel, const float* lrs, hipStream_t stream) {
   if (B < 1 || B > MAXB || nsteps < 1 || ring < B || ring % B) return hipErrorInvalidValue;
-  if (dims[0] > 31) return hipErrorInvalidValue;
+  if (dims[0] > 31 || nmodels < 1 || nmodels > (1 << 20) || xmodel < 0) return hipErrorInvalidValue;
   MBArgs a{x, ld, ring, cursor, scale, shift, params, m, v, iter, metrics, B, nsteps, dims[0], dims[1], dims[2],
-           dims[3], acts[0], acts[1], acts[2], acts[3], l1, lr, beta1, beta2, eps, gscale, want_acc, prof};
+           dims[3], acts[0], acts[1], acts[2], acts[3], l1, lr, beta1, beta2, eps, gscale, want_acc, prof,
+           xmodel, lrs};
   const bool ref = acts[0] == ACT_TANH && acts[1] == ACT_RELU && acts[2] == ACT_TANH && acts[3] == ACT_RELU;
   auto k = ae_minibatch_kernel<32, 0, -1>;   // any shape / activations
   if (ref && dims[0] == 18) k = B == 32 ? ae_minibatch_kernel<18, 32, PACK_REF> : ae_minibatch_kernel<18, 0, PACK_REF>;
   else if (ref) k = B == 32 ? ae_minibatch_kernel<32, 32, PACK_REF> : ae_minibatch_kernel<32, 0, PACK_REF>;
-  hipLaunchKernelGGL(k, dim3(1), dim3(NT), sizeof(Smem), stream, a);
+  // a fleet larger than one model per CU: the 128-VGPR build puts two models on each CU
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (ref && dims[0] == 18 && B == 32 && nmodels > cus) k = ae_minibatch_kernel<18, 32, PACK_REF, 4>;
+  hipLaunchKernelGGL(k, dim3(nmodels), dim3(NT), sizeof(Smem), stream, a);
   return hipGetLastError();
 }
 

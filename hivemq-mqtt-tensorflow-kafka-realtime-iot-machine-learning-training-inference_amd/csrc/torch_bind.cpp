@@ -184,42 +184,62 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
                           const at::Tensor& v, const at::Tensor& iter, const c10::optional<at::Tensor>& metrics,
                           int64_t batch, int64_t nsteps, std::vector<int64_t> dims, std::vector<int64_t> acts,
                           double l1, double lr, double beta1, double beta2, double eps, double gscale, bool want_acc,
-                          const c10::optional<at::Tensor>& prof) {
+                          const c10::optional<at::Tensor>& prof, const c10::optional<at::Tensor>& lrs) {
+  // One model: params/m/v [1536], cursor/iter [1], x [ring, ld].  Fleet of M models:
+  // params/m/v [M, 1536], cursor/iter [M], metrics [M, 4], x [ring, ld] (shared) or [M, ring, ld].
   check_ae_dims(dims, acts);
   check_dev(x, "x", at::kFloat);
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [ring, ld]");
-  TORCH_CHECK(x.size(1) >= dims[0], "x has fewer columns than the model input dim");
+  TORCH_CHECK(x.dim() == 2 || x.dim() == 3, "x must be [ring, ld] or [M, ring, ld]");
+  TORCH_CHECK(x.stride(-1) == 1, "x must have unit column stride");
+  const int64_t np = sml::ae_nparam();
+  TORCH_CHECK(params.numel() % np == 0 && params.numel() > 0, "params must be [M, padded image]");
+  const int64_t M = params.numel() / np;
+  const int64_t ring = x.size(-2), ld = x.stride(-2);
+  TORCH_CHECK(x.dim() == 2 || (x.size(0) == M && x.stride(1) * x.size(1) <= x.stride(0)),
+              "per-model rings must be [M, ring, ld] with non-overlapping models");
+  TORCH_CHECK(x.size(-1) >= dims[0], "x has fewer columns than the model input dim");
   TORCH_CHECK(batch >= 1 && batch <= sml::ae_minibatch_max_batch(), "batch must be in [1, ",
               sml::ae_minibatch_max_batch(), "]");
   TORCH_CHECK(nsteps >= 1 && nsteps <= (1 << 30), "nsteps out of range");
-  TORCH_CHECK(x.size(0) >= batch && x.size(0) % batch == 0, "ring rows must be a positive multiple of the batch");
+  TORCH_CHECK(ring >= batch && ring % batch == 0, "ring rows must be a positive multiple of the batch");
   check_dev(cursor, "cursor", at::kLong);
   check_dev(iter, "iter", at::kLong);
-  TORCH_CHECK(cursor.numel() == 1 && iter.numel() == 1, "cursor / iter must be 1-element int64");
+  TORCH_CHECK(cursor.numel() == M && iter.numel() == M && cursor.is_contiguous() && iter.is_contiguous(),
+              "cursor / iter must be contiguous int64 [M]");
   for (const at::Tensor* t : {&params, &m, &v}) {
     check_dev(*t, "params/m/v", at::kFloat);
-    TORCH_CHECK(t->numel() == sml::ae_nparam() && t->is_contiguous(), "params/m/v must be the padded image");
+    TORCH_CHECK(t->numel() == M * np && t->is_contiguous(), "params/m/v must be the padded image [M, 1536]");
   }
-  if (metrics.has_value()) TORCH_CHECK(metrics->numel() >= 4, "metrics needs 4 slots");
+  if (metrics.has_value()) {
+    check_dev(*metrics, "metrics", at::kFloat);
+    TORCH_CHECK(metrics->is_contiguous() && metrics->numel() >= 4 * M, "metrics needs 4 slots per model");
+  }
   if (scale.has_value()) TORCH_CHECK(shift.has_value() && scale->numel() >= dims[0] && shift->numel() >= dims[0],
                                      "scale requires shift, both [D]");
+  const float* lrs_ptr = nullptr;
+  if (lrs.has_value() && lrs->defined()) {
+    check_dev(*lrs, "lrs", at::kFloat);
+    TORCH_CHECK(lrs->numel() == M && lrs->is_contiguous(), "lrs must be float32 [M]");
+    lrs_ptr = lrs->data_ptr<float>();
+  }
   unsigned long long* prof_ptr = nullptr;
   if (prof.has_value() && prof->defined()) {
     check_dev(*prof, "prof", at::kLong);
     TORCH_CHECK(prof->numel() >= 11, "prof needs 11 int64 slots");
     prof_ptr = reinterpret_cast<unsigned long long*>(prof->data_ptr<int64_t>());
   }
-  // the cursor is read on the device; its host-side validity is the caller's contract
-  // (FusedAE keeps it a multiple of the batch below the ring size)
+  // the cursors are read on the device; their host-side validity is the caller's contract
+  // (FusedAE / AEFleet keep each one a multiple of the batch below the ring size)
   c10::hip::HIPGuard guard(x.device().index());
   int d[4] = {(int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3]};
   int a[4] = {(int)acts[0], (int)acts[1], (int)acts[2], (int)acts[3]};
-  SML_CHECK_HIP(sml::ae_minibatch_launch(x.data_ptr<float>(), x.stride(0), x.size(0), cursor.data_ptr<int64_t>(),
+  SML_CHECK_HIP(sml::ae_minibatch_launch(x.data_ptr<float>(), ld, ring, cursor.data_ptr<int64_t>(),
                                          opt_ptr(scale), opt_ptr(shift), params.data_ptr<float>(),
                                          m.data_ptr<float>(), v.data_ptr<float>(), iter.data_ptr<int64_t>(),
                                          opt_mut(metrics), (int)batch, (int)nsteps, d, a, (float)l1, (float)lr,
                                          (float)beta1, (float)beta2, (float)eps, (float)gscale, (int)want_acc,
-                                         prof_ptr, cur_stream(x)));
+                                         prof_ptr, (int)M, x.dim() == 3 ? x.stride(0) : 0, lrs_ptr,
+                                         cur_stream(x)));
 }
 
 void ae_forward(const at::Tensor& x, const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift,
@@ -625,7 +645,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("cursor"), py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("m"),
         py::arg("v"), py::arg("iter"), py::arg("metrics"), py::arg("batch"), py::arg("nsteps"), py::arg("dims"),
         py::arg("acts"), py::arg("l1"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
-        py::arg("gscale"), py::arg("want_acc"), py::arg("prof") = py::none());
+        py::arg("gscale"), py::arg("want_acc"), py::arg("prof") = py::none(), py::arg("lrs") = py::none());
   m.def("normalize_filter", &normalize_filter, "K8: normalise + keep rows with label == keep, order-preserving",
         py::arg("x"), py::arg("D"), py::arg("labels"), py::arg("keep"), py::arg("scale"), py::arg("shift"),
         py::arg("want_index") = false);

@@ -1,0 +1,147 @@
+"""Fleet training: many independent small autoencoders on one GPU, Keras batch semantics.
+
+The reference trains ONE dense autoencoder with ``fit(batch_size=32)``
+(``python-scripts/AUTOENCODER-TensorFlow-IO-Kafka/cardata-v3.py:187-203``), streaming
+from one topic.  In an IoT deployment the natural scale-out of that workload is many
+models at once: one anomaly model per car / device group (a "digital twin" per
+partition, as the MongoDB sink of the reference's Connect setup keys documents by car),
+an ensemble, or a learning-rate sweep.  Each such model is far too small to use a GPU
+on its own (one batch-32 step is ~1 MFLOP), so the fleet runs them side by side:
+
+* ``csrc/kernels/ae_minibatch.hip`` in fleet mode -- workgroup ``b`` trains model ``b``
+  for ``nsteps`` sequential Keras steps with its parameters, Adam moments and
+  activations resident in LDS / VGPRs; a grid of M >= 256 workgroups fills the 256
+  CUs (~47 KB LDS each, so 3 models share a CU);
+* state is stacked: ``params/m/v [M, 1536]`` (the padded image of ``ops/ae.py``),
+  ``iter/cursor [M]``, ``metrics [M, 4]``; model ``b`` reads either its own ring
+  ``rings[b]`` (per-device streams) or one shared ring from its own cursor;
+* optional per-model learning rates (``lrs``) for sweeps.
+
+Every model follows exactly the single-model path (``FusedAE.train_minibatches``):
+the fleet kernel is the same instantiation with a per-workgroup pointer rebase, so a
+model trained in a fleet is bit-identical to the same model trained alone
+(``tests/test_ae_fleet_gpu.py``).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ._ext import load_c
+from .ae import NPARAM, AESpec, FusedAE, pack_image, unpack_image
+
+
+class AEFleet:
+    """M independent autoencoders of one architecture, trained concurrently."""
+
+    def __init__(self, spec: AESpec, weights: Sequence[Sequence[np.ndarray]], device,
+                 lr=1e-3, beta_1: float = 0.9, beta_2: float = 0.999, epsilon: float = 1e-7,
+                 want_acc: bool = True, scale: Optional[np.ndarray] = None, shift: Optional[np.ndarray] = None):
+        spec.check_fused()
+        if len(weights) == 0:
+            raise ValueError("a fleet needs at least one model")
+        self.C = load_c()
+        self.spec = spec
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("AEFleet runs on a ROCm device only")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.n_models = M = len(weights)
+        self.beta_1, self.beta_2, self.epsilon = beta_1, beta_2, epsilon
+        self.want_acc = want_acc
+        dev = self.device
+        self.params = torch.from_numpy(np.stack([pack_image(w) for w in weights])).to(dev)
+        self.m = torch.zeros(M, NPARAM, device=dev)
+        self.v = torch.zeros(M, NPARAM, device=dev)
+        self.iter = torch.zeros(M, dtype=torch.int64, device=dev)
+        self.cursor = torch.zeros(M, dtype=torch.int64, device=dev)
+        self.metrics = torch.zeros(M, 4, device=dev)
+        if np.ndim(lr) == 0:
+            self.lr, self.lrs = float(lr), None
+        else:
+            lrs = np.asarray(lr, dtype=np.float32)
+            if lrs.shape != (M,):
+                raise ValueError(f"lr must be a scalar or [{M}] per-model rates")
+            self.lr, self.lrs = float(lrs[0]), torch.from_numpy(lrs).to(dev)
+        if scale is None:
+            self.scale = self.shift = None
+        else:
+            self.scale = torch.as_tensor(np.asarray(scale, dtype=np.float32), device=dev)
+            self.shift = torch.as_tensor(np.asarray(shift, dtype=np.float32), device=dev)
+        self.ring: Optional[torch.Tensor] = None
+        self.ring_batch = 0
+
+    @classmethod
+    def from_seeds(cls, spec: AESpec, seeds: Sequence[int], device, **kw) -> "AEFleet":
+        from ..models.reference import init_dense_weights
+        return cls(spec, [init_dense_weights(spec.layer_sizes, seed=int(s)) for s in seeds], device, **kw)
+
+    # -- data ------------------------------------------------------------------------
+    def attach_rings(self, rings: torch.Tensor, batch: int, offsets: Optional[Sequence[int]] = None) -> None:
+        """``rings``: ``[M, ring, ld]`` (model ``b`` consumes ``rings[b]``) or ``[ring, ld]``
+        shared by every model, each from its own start row ``offsets[b]`` (multiples of
+        ``batch``; default 0)."""
+        M, D = self.n_models, self.spec.input_dim
+        if rings.device != self.device or rings.dtype != torch.float32 or rings.stride(-1) != 1:
+            raise ValueError("rings must be float32 with unit column stride on " + str(self.device))
+        if rings.dim() == 3:
+            if rings.size(0) != M:
+                raise ValueError(f"per-model rings need a leading dim of {M}")
+        elif rings.dim() != 2:
+            raise ValueError("rings must be [M, ring, ld] or [ring, ld]")
+        n = rings.size(-2)
+        if rings.size(-1) < D:
+            raise ValueError("rings have too few columns")
+        if batch <= 0 or batch > self.C.ae_minibatch_max_batch() or n % batch:
+            raise ValueError(f"batch must be in [1, {self.C.ae_minibatch_max_batch()}] and divide the ring rows")
+        offs = np.zeros(M, np.int64) if offsets is None else np.asarray(offsets, dtype=np.int64)
+        if offs.shape != (M,) or (offs % batch).any() or (offs < 0).any() or (offs >= n).any():
+            raise ValueError("offsets must be [M] multiples of the batch inside the ring")
+        self.ring, self.ring_batch = rings, int(batch)
+        self.cursor.copy_(torch.from_numpy(offs))
+
+    # -- training ----------------------------------------------------------------------
+    def train_minibatches(self, nsteps: int) -> None:
+        """``nsteps`` Keras steps of ``ring_batch`` rows for EVERY model, in one launch."""
+        if self.ring is None:
+            raise RuntimeError("attach_rings() first")
+        B = self.ring_batch
+        self.C.ae_train_minibatches(self.ring, self.cursor, self.scale, self.shift, self.params, self.m, self.v,
+                                    self.iter, self.metrics, B, int(nsteps), self.spec.dims, self.spec.act_codes,
+                                    float(self.spec.activity_l1), self.lr, self.beta_1, self.beta_2, self.epsilon,
+                                    1.0 / B, bool(self.want_acc), None, self.lrs)
+
+    # -- state -------------------------------------------------------------------------
+    def get_weights(self, i: int) -> List[np.ndarray]:
+        return unpack_image(self.params[i].detach().cpu().numpy(), self.spec)
+
+    def set_weights(self, i: int, weights: Sequence[np.ndarray]) -> None:
+        self.params[i].copy_(torch.from_numpy(pack_image(weights)))
+
+    def model(self, i: int, **kw) -> FusedAE:
+        """Model ``i`` as a standalone ``FusedAE`` (weights, Adam state and iteration
+        copied), e.g. to score a car's events with ``forward`` / the serving path."""
+        ae = FusedAE(self.spec, self.get_weights(i), self.device, lr=float(self.lrs[i]) if self.lrs is not None
+                     else self.lr, beta_1=self.beta_1, beta_2=self.beta_2, epsilon=self.epsilon,
+                     want_acc=self.want_acc, scale=None if self.scale is None else self.scale.cpu().numpy(),
+                     shift=None if self.shift is None else self.shift.cpu().numpy(), **kw)
+        ae.m.copy_(self.m[i])
+        ae.v.copy_(self.v[i])
+        ae.iter.copy_(self.iter[i:i + 1])
+        return ae
+
+    def reset_metrics(self) -> None:
+        self.metrics.zero_()
+
+    def read_metrics(self) -> List[dict]:
+        """Per-model epoch metrics in Keras terms (one host sync for the whole fleet)."""
+        D, l1 = self.spec.input_dim, self.spec.activity_l1
+        out = []
+        for sq, ab, corr, rows in self.metrics.cpu().tolist():
+            rows = max(rows, 1.0)
+            out.append({"loss": (sq / D + l1 * ab) / rows, "mse": sq / (D * rows), "accuracy": corr / rows,
+                        "rows": rows})
+        return out
