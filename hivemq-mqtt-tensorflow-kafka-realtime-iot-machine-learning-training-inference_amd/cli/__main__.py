@@ -20,6 +20,7 @@ Commands (reference script in parentheses):
   connect      <servers> --config connector.json [--sink-store DIR]   Kafka Connect sinks (MongoDB, GCS Avro)
   serve        <servers> <topic> <result_topic> <model-file> [--replicas W --replica-index R]
                long-running shard-by-key anomaly scorer (one replica per GPU; model-predictions Deployment)
+  fleet        <csv|synthetic> [--models N] [--epochs E]   one AE per car, all trained at once on one GPU
 """
 from __future__ import annotations
 
@@ -31,7 +32,7 @@ from . import common
 def _commands():
     from . import cardata_autoencoder as ae
     from . import cardata_lstm as ls
-    from . import creditcard, mnist, mqtt, serve, tools, train
+    from . import creditcard, fleet, mnist, mqtt, serve, tools, train
     return {
         "cardata-v3": ae.main_v3,
         "cardata-v1": ae.main_v1,
@@ -48,6 +49,7 @@ def _commands():
         "devsim": mqtt.main_devsim,
         "connect": mqtt.main_connect,
         "serve": serve.main,
+        "fleet": fleet.main,
     }
 
 

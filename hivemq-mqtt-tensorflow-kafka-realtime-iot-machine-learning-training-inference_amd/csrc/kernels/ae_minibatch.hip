@@ -88,8 +88,10 @@ struct Tile {
   int acol;         // this lane's activation column (image row m = row0 + c; bias row -> ones column)
   int dz, ds;       // upstream-gradient base + this lane's column, row stride
   int xb;           // L1: activation lives in the current input buffer
-  int slot[4];      // image slots of C[4g+i][c]
-  int w[4];         // their LDS weight indices
+  int slot0, sst;   // image slots of C[4g+i][c]: slot0 + i * sst (consecutive image rows)
+  int w0, wst;      // their LDS weight indices: w0 + i * wst
+  __device__ __forceinline__ int slot(int i) const { return slot0 + i * sst; }
+  __device__ __forceinline__ int w(int i) const { return w0 + i * wst; }
 };
 
 __device__ __forceinline__ Tile make_tile(int id, int c, int g, const Smem& S, const float* sbase) {
@@ -109,11 +111,10 @@ __device__ __forceinline__ Tile make_tile(int id, int c, int g, const Smem& S, c
   const int m = row0 + c;
   T.acol = m == bias_row ? (id <= 1 ? 32 : 16) : m;
   T.dz += col0 + c;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    T.slot[i] = img + (row0 + 4 * g + i) * istride + col0 + c;
-    T.w[i] = lds_of_slot(T.slot[i]);
-  }
+  T.slot0 = img + (row0 + 4 * g) * istride + col0 + c;
+  T.sst = istride;
+  T.w0 = lds_of_slot(T.slot0);
+  T.wst = id <= 1 ? 16 : id <= 3 ? HS : XS;   // LDS row strides of W1 / W2,W3 / W4
   return T;
 }
 
@@ -188,9 +189,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   float mo[4], vo[4], wo[4];   // Adam moments + the parameters themselves (sole writer)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    mo[i] = has_tile ? a.m[T.slot[i]] : 0.f;
-    vo[i] = has_tile ? a.v[T.slot[i]] : 0.f;
-    wo[i] = has_tile ? a.params[T.slot[i]] : 0.f;
+    mo[i] = has_tile ? a.m[T.slot(i)] : 0.f;
+    vo[i] = has_tile ? a.v[T.slot(i)] : 0.f;
+    wo[i] = has_tile ? a.params[T.slot(i)] : 0.f;
   }
 
   // ---- weights -> LDS (padding zero), zeroed activations, constant-1 bias columns ----
@@ -371,7 +372,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         mo[i] = mm;
         vo[i] = vv;
         wo[i] -= lr_t * mm * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv) + a.eps);   // v_sqrt / v_rcp, ~1 ulp
-        S.w[T.w[i]] = wo[i];
+        S.w[T.w(i)] = wo[i];
       }
       mark(10);
     } else if (a.want_acc && t - 6 * 64 < B) {
@@ -398,9 +399,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   if (has_tile) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      a.params[T.slot[i]] = wo[i];
-      a.m[T.slot[i]] = mo[i];
-      a.v[T.slot[i]] = vo[i];
+      a.params[T.slot(i)] = wo[i];
+      a.m[T.slot(i)] = mo[i];
+      a.v[T.slot(i)] = vo[i];
     }
   }
   float vals[3] = {sq, ab, corr};

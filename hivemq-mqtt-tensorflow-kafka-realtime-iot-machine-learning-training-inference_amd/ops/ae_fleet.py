@@ -11,16 +11,19 @@ on its own (one batch-32 step is ~1 MFLOP), so the fleet runs them side by side:
 * ``csrc/kernels/ae_minibatch.hip`` in fleet mode -- workgroup ``b`` trains model ``b``
   for ``nsteps`` sequential Keras steps with its parameters, Adam moments and
   activations resident in LDS / VGPRs; a grid of M >= 256 workgroups fills the 256
-  CUs (~47 KB LDS each, so 3 models share a CU);
+  CUs.  The latency-optimal single-model build (~160 VGPRs) fits one 8-wave model per
+  CU; fleets larger than the CU count switch to a 128-VGPR build that fits two
+  (1 MI355X: 2.19 G rows/s at M = 256, 2.81 G rows/s at M = 1024; profiles/r01_v7);
 * state is stacked: ``params/m/v [M, 1536]`` (the padded image of ``ops/ae.py``),
   ``iter/cursor [M]``, ``metrics [M, 4]``; model ``b`` reads either its own ring
   ``rings[b]`` (per-device streams) or one shared ring from its own cursor;
 * optional per-model learning rates (``lrs``) for sweeps.
 
-Every model follows exactly the single-model path (``FusedAE.train_minibatches``):
-the fleet kernel is the same instantiation with a per-workgroup pointer rebase, so a
-model trained in a fleet is bit-identical to the same model trained alone
-(``tests/test_ae_fleet_gpu.py``).
+Every model follows the single-model path (``FusedAE.train_minibatches``): for
+M <= #CUs the fleet kernel is the same instantiation with a per-workgroup pointer
+rebase, so a model trained in a fleet is bit-identical to the same model trained
+alone; the two-per-CU build agrees to fp32 rounding (<= 3e-8 measured) and with the
+torch Keras-Adam oracle (``tests/test_ae_fleet_gpu.py``).
 """
 from __future__ import annotations
 
@@ -31,6 +34,56 @@ import torch
 
 from ._ext import load_c
 from .ae import NPARAM, AESpec, FusedAE, pack_image, unpack_image
+
+
+def _fnv1a(key) -> int:
+    b = key.encode() if isinstance(key, str) else bytes(key)
+    h = 0xCBF29CE484222325
+    for c in b:
+        h ^= c
+        h = (h * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def rings_by_key(raw: np.ndarray, keys, batch: int = 32, n_models: Optional[int] = None):
+    """Route a keyed stream to per-model rings: ``(rings [M, R, D] float32, members)``.
+
+    ``n_models=None``: one model per distinct key (``members[b] = [key]``, keys in order
+    of first appearance -- e.g. one anomaly model per car of the reference's
+    ``testdata/car-sensor-data.csv``).  Otherwise key -> model ``fnv1a(key) % n_models``
+    (the same stable hash as ``parallel.dp.shard_by_key``), so a key always lands on the
+    same model across restarts and hosts.  Each model's rows keep stream order; a ring
+    is the longest group rounded up to a multiple of ``batch``, and shorter groups are
+    repeated cyclically to fill it (a ring replays anyway), so every model takes the
+    same number of steps per pass.
+    """
+    raw = np.asarray(raw, dtype=np.float32)
+    keys = np.asarray(keys)
+    if raw.ndim != 2 or len(keys) != raw.shape[0]:
+        raise ValueError("raw must be [n, D] with one key per row")
+    uniq, first, inv = np.unique(keys, return_index=True, return_inverse=True)
+    order = np.argsort(first)                    # distinct keys in order of first appearance
+    if n_models is None:
+        rank = np.empty(len(uniq), np.int64)
+        rank[order] = np.arange(len(uniq))
+        model_of_row = rank[inv]
+        members = [[uniq[j].item()] for j in order]
+    else:
+        if n_models < 1:
+            raise ValueError("n_models must be >= 1")
+        mk = np.array([_fnv1a(str(k)) % n_models for k in uniq], np.int64)
+        model_of_row = mk[inv]
+        members = [[uniq[j].item() for j in order if mk[j] == b] for b in range(n_models)]
+        empty = [b for b in range(n_models) if not members[b]]
+        if empty:
+            raise ValueError(f"models {empty[:8]} receive no keys: use fewer models or n_models=None")
+    M = len(members)
+    groups = [np.flatnonzero(model_of_row == b) for b in range(M)]
+    R = -(-max(len(g) for g in groups) // batch) * batch
+    rings = np.empty((M, R, raw.shape[1]), np.float32)
+    for b, g in enumerate(groups):
+        rings[b] = raw[np.resize(g, R)]          # cyclic repeat of the group's rows
+    return rings, members
 
 
 class AEFleet:

@@ -129,3 +129,24 @@ def test_fleet_beyond_resident_capacity(cuda_device):
     ae = fleet.model(517)
     r_fleet, s_fleet, _ = ae.forward(x)
     assert torch.isfinite(s_fleet).all()
+
+
+def test_fleet_cli_one_model_per_car(cuda_device, tmp_path):
+    """``python -m streamml.cli fleet <csv>``: one AE per car of the reference CSV, saved as Keras HDF5."""
+    import json
+    import os
+
+    from streamml.cli.__main__ import main
+    from streamml.data.cardata import load_csv
+    from streamml.models.autoencoder import load_model
+
+    csv = os.path.join(os.path.dirname(__file__), "fixtures", "car-sensor-data.csv")
+    out = tmp_path / "fleet"
+    assert main(["fleet", csv, "--epochs", "2", "--out", str(out)]) == 0
+    index = json.loads((out / "index.json").read_text())
+    _, _, cars = load_csv(csv)
+    assert sorted(index) == sorted(set(cars.tolist()))
+    for name, rec in index.items():
+        assert rec["keys"] == [name] and np.isfinite(rec["loss"])
+    m = load_model(str(out / index[cars[0]]["file"]), device="cpu")
+    assert len(m.get_weights()) == 8
