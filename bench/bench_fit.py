@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""The reference's own training job on the real entry point: ``Autoencoder.fit``.
+
+cardata-v3 trains ``fit(zip((x, x)).batch(100).take(100), epochs=20)`` on the
+label-filtered Kafka stream (AUTOENCODER-TensorFlow-IO-Kafka/cardata-v3.py:176-177,
+212-222).  Two numbers:
+
+* ``fit_batch100``: ``fit(array, batch_size=100, shuffle=True)`` -- one Keras Adam
+  update per 100 rows, every step on the persistent kernel (rows/s);
+* ``stream_e2e``: in-process Kafka broker (``partitions`` partitions of Confluent-framed
+  Avro) -> fetch + decode -> pinned ring -> H2D -> K8 filter -> ``fit(batch_size=100)``
+  (rows/s of consumed events), plus each host stage alone.
+
+``measure(...)`` is also called by ``bench.py`` for its ``fit_batch100`` / ``stream_e2e``
+fields.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def fit_array(device, rows: int = 2_000_000, batch: int = 100, engine: str = "auto", seed: int = 0) -> dict:
+    import numpy as np
+    import torch
+
+    from streamml.data.cardata import SyntheticCarSource
+    from streamml.models.autoencoder import Autoencoder
+
+    raw, _, _, _ = SyntheticCarSource.scenario("full", seed=seed, failure_rate=0.0).generate(rows)
+    m = Autoencoder(device=device, input_normalizer="cardata", seed=seed)
+    m.compile()
+    x = torch.as_tensor(np.ascontiguousarray(raw, np.float32), device=device)
+    m.fit(x[:batch * 200], epochs=1, batch_size=batch, verbose=0, engine=engine)   # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    h = m.fit(x, epochs=1, batch_size=batch, verbose=0, engine=engine)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    steps = -(-rows // batch)
+    return {"rows_per_s": rows / dt, "us_per_step": dt / steps * 1e6, "steps": steps, "batch": batch,
+            "engine": m.last_fit_engine, "loss": h.history["loss"][-1], "dtype": "fp32"}
+
+
+def stream_e2e(device, rows: int = 2_000_000, batch: int = 100, partitions: int = 8, workers: int = 8,
+               fetch_bytes: int = 4 << 20, failure_rate: float = 0.01, native: bool = True) -> dict:
+    import torch
+
+    from streamml.data import stream as S
+    from streamml.data.avro import AvroCodec
+    from streamml.data.produce import encode_chunk
+    from streamml.kafka import fake_broker
+    from streamml.models.autoencoder import Autoencoder
+
+    name = f"bench-e2e-{rows}-{partitions}"
+    b = fake_broker(name)
+    topic = "SENSOR_DATA_S_AVRO"
+    b.create_topic(topic, partitions)
+    codec = AvroCodec("cardata-v1")
+    t0 = time.perf_counter()
+    for i, c in enumerate(S.synthetic(rows, chunk=250_000, seed=0, failure_rate=failure_rate)):
+        buf, offs = encode_chunk(codec, c.x, c.label)
+        b.append_buffer(topic, i % partitions, buf, offs)
+    t_produce = time.perf_counter() - t0
+    specs = [f"{topic}:{p}:0" for p in range(partitions)]
+    src = S.kafka(f"fake://{name}", specs, max_bytes=fetch_bytes, workers=workers, native=native)
+    out = {"rows": rows, "batch": batch, "partitions": partitions, "workers": workers,
+           "produce_rows_per_s": rows / t_produce, "native_feed": bool(native)}
+    # stage 1: fetch + decode alone (host)
+    t0 = time.perf_counter()
+    n = src.count_rows() if hasattr(src, "count_rows") else sum(len(c) for c in src)
+    out["fetch_decode_rows_per_s"] = n / (time.perf_counter() - t0)
+    # stage 2: + pinned ring + H2D (+ K8 filter) into device chunks, no training
+    m = Autoencoder(device=device, input_normalizer="cardata")
+    m.compile()
+    training = src.filter_normal(device=True)
+    t0 = time.perf_counter()
+    kept = 0
+    for xd in m._stream_device_chunks(training):
+        kept += int(xd.size(0))
+    torch.cuda.synchronize()
+    out["ingest_h2d_rows_per_s"] = n / (time.perf_counter() - t0)
+    # stage 3: the training kernel alone on the same number of rows (device resident)
+    out["train_only"] = fit_array(device, rows=max(kept, batch * 300), batch=batch)
+    # end to end
+    m.fit(training, epochs=1, batch_size=batch, verbose=0, steps_per_epoch=50)   # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    h = m.fit(training, epochs=1, batch_size=batch, verbose=0)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out.update({"rows_per_s": n / dt, "kept_rows": kept, "trained_rows_per_s": kept / dt,
+                "engine": m.last_fit_engine, "loss": h.history["loss"][-1]})
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=2_000_000)
+    ap.add_argument("--batch", type=int, default=100)
+    ap.add_argument("--partitions", type=int, default=8)
+    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--python-feed", action="store_true", help="chunk-by-chunk Python Kafka path")
+    ap.add_argument("--skip-stream", action="store_true")
+    args = ap.parse_args()
+    import torch
+    dev = torch.device("cuda", 0)
+    res = {"fit_batch100": fit_array(dev, args.rows, args.batch)}
+    res["fit_batch32"] = fit_array(dev, args.rows // 2, 32)
+    res["fit_launch_batch100"] = fit_array(dev, args.rows // 10, args.batch, engine="launch")
+    if not args.skip_stream:
+        res["stream_e2e"] = stream_e2e(dev, args.rows, args.batch, args.partitions, args.workers,
+                                       native=not args.python_feed)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -47,17 +47,15 @@ def measure(device, batch=32, steps_per_launch=20000, launches=5, launch_steps=2
     out["persistent_rows_per_s"] = n * batch / dt
     out["persistent_us_per_step"] = dt / n * 1e6
     out["persistent_final_loss"] = ae.read_metrics()["loss"]
-    # one profiled launch: per-phase shader cycles of wave 0 (fwd L1-L4, bwd L4-L2, grads+Adam)
+    # one profiled launch: per-phase shader cycles of wave 0 (phase A = register fwd/bwd
+    # chain of its 16 rows, barrier, phase B = weight-gradient MFMAs + Adam, barrier)
     prof = torch.zeros(11, dtype=torch.int64, device=device)
     ae.train_minibatches(steps_per_launch, prof=prof)
     torch.cuda.synchronize()
     pc = prof.cpu().tolist()
-    names = ["fwd1", "fwd2", "fwd3", "fwd4_loss", "bwd_dz3_acc", "bwd_dz2", "bwd_dz1", "wgrad_adam"]
+    names = ["phaseA_fwd_bwd", "barrier1", "phaseB_wgrad_adam", "barrier2"]
     out["phase_cycles_per_step"] = {n: pc[i] / steps_per_launch for i, n in enumerate(names)}
     out["cycles_per_step"] = pc[8] / steps_per_launch
-    out["p8_split_cycles_per_step"] = {"stash_next_tile": pc[9] / steps_per_launch,
-                                       "wgrad_mfma_adam": pc[10] / steps_per_launch,
-                                       "prefetch_issue_and_barrier": pc[7] / steps_per_launch}
 
     ae2 = FusedAE(spec, init_dense_weights(spec.layer_sizes, seed=0), device, scale=scale, shift=shift)
     ae2.attach_ring(data, batch)

@@ -1,44 +1,69 @@
+// sml-build: no-slp
 // Persistent small-batch autoencoder trainer for gfx950 (MI355X).
 //
-// The reference trains its dense autoencoder with Keras `fit(batch_size=32)`
-// (AUTOENCODER-TensorFlow-IO-Kafka/cardata-v3.py:187-203, the creditcard notebook's
-// batch 32): one Adam update per 32 rows.  At that batch size a launch-per-step
-// design (ae_fused.hip: train kernel + slab-reduce/Adam kernel) is launch-bound at
-// ~10 us per step.  This kernel keeps the whole optimizer loop on the device: ONE
-// workgroup runs `nsteps` sequential Keras steps -- normalise, forward, MSE + L1
-// activity loss, backward, weight gradients, Adam -- with the parameters, the Adam
-// moments and every activation resident on chip (LDS / VGPRs).  Nothing returns to
-// HBM between steps except the next batch's rows, which are prefetched into
-// registers one step ahead.  All arithmetic is fp32 (bit-for-bit Keras semantics
-// are limited only by summation order), so this is also the exact-semantics path.
+// The reference trains its dense autoencoder with Keras `fit`: batch 100 in
+// cardata-v3 (AUTOENCODER-TensorFlow-IO-Kafka/cardata-v3.py:176-177, 212-222), batch 32
+// in cardata-v1 and the creditcard notebooks -- one Adam update per small batch.  A
+// launch-per-step design is launch-bound there (~10 us per step).  This kernel keeps the
+// whole optimizer loop on the device: ONE workgroup runs `nsteps` sequential Keras steps
+// -- normalise, forward, MSE + L1 activity loss, categorical accuracy, backward, weight
+// gradients, Adam -- with parameters, Adam moments and activations on chip.  Only the
+// next batch's rows come from HBM, prefetched into registers one step ahead.  All
+// arithmetic is fp32 (v_mfma_f32_16x16x4_f32 is an exact fp32 fma chain), so this is
+// also the exact-semantics path: it matches an fp32 PyTorch Keras-Adam run to
+// summation-order rounding.
 //
-// Layout (per workgroup, 512 threads = 8 waves):
-//   weights in LDS, re-strided so every phase reads conflict-free:
-//     W1 [32][16] (bias row 31), W2/W3 [16][17] (bias row 15), W4 [16][33] (bias row 15)
-//   activations [B][stride] with a constant-1 column at the end (bias gradient =
-//   the same dot product as a weight gradient), double-buffered input tiles.
-//   Each real parameter (571 for 18-14-7-7-18) is owned by one thread, which keeps
-//   its Adam m / v in registers for the whole launch.
-// Per step: 8 phases separated by 8 barriers (fwd L1..L4 + loss, bwd L4..L2 with
-// argmax accuracy, then gradients + Adam + the next input tile).
+// Step structure (512 threads = 8 waves, batch B <= 128 = 8 row tiles of 16):
+//   phase A  wave w owns rows 16w..16w+15.  The forward and the activation-gradient
+//            backward run entirely in registers on fp32 MFMA in FEATURE-MAJOR
+//            orientation: a layer computes Z^T = W^T . H^T, whose C/D layout
+//            (lane (c, g) holds Z^T[4g+i][row c]) is exactly the B-operand layout of the
+//            next layer's K-steps (K-step s takes register s&3 of output tile s>>2, so
+//            lane group g contributes feature f(s,g) = 16(s>>2) + 4g + (s&3)); the A
+//            operand (weights) is read in that same permuted K order from LDS images
+//            stored in fragment order (one contiguous 256-byte block per K-step: no
+//            bank conflicts).  Bias = the accumulator's initial value.  Loss, L1
+//            activity term and argmax accuracy are lane-local + two permlane swaps.
+//            The wave then stores its activations / gradients [row][feature] to LDS.
+//   barrier
+//   phase B  waves 0-5 each own one 16x16 tile of the padded parameter image: weight
+//            gradient act^T . dz over the B rows (fp32 MFMA, K = 4 rows per
+//            instruction, bias rows read a constant 1), then Keras Adam on the 4
+//            parameters per lane they hold in registers for the whole launch, and
+//            write the new values into the forward / backward weight fragments.
+//   barrier
+// Two barriers per step (the round-1 version had eight, one per layer phase, and did
+// every dot product on the VALU: 12 us per batch-100 step).
+//
 // Fleet mode: a grid of M workgroups trains M independent models at once (per-device
 // digital-twin models, ensembles, learning-rate sweeps), one per workgroup, each with
-// its own parameters, optimizer state, ring cursor and metrics.  A single model
-// occupies one CU; M >= 256 fills the chip (~47 KB LDS -> 3 workgroups per CU).
+// its own parameters, optimizer state, ring cursor and metrics.
 #include "sml_common.h"
 
 using namespace sml;
 
 namespace {
 
-constexpr int NT = 512;   // 8 waves: two per SIMD, so one wave's LDS / VALU latency hides behind the other's
-constexpr int MAXB = 48;   // Keras default batch 32 fits; Smem stays under the 64 KB dynamic-LDS default
-constexpr int XS = 33;   // input / output row stride (col 32 = 1.0)
-constexpr int HS = 17;   // hidden row stride         (col 16 = 1.0)
-// image offsets (ae_fused.hip): L1 [32][16] @0, L2 [16][16] @512, L3 @768, L4 [16][32] @1024
+constexpr int NT = 512;   // 8 waves: one 16-row tile each in phase A
+// LDS capacity classes (rows per step): 48 keeps Smem small so two fleet models share a
+// CU (Keras default batch 32); 128 covers cardata-v3's batch 100 (one workgroup per CU).
+constexpr int MB_SMALL = 48, MB_LARGE = 128, MAXB = MB_LARGE;
+// activation row strides in LDS (floats): 16 and 48 are 16 (mod 32), so the phase-B
+// reads of rows r and r+1 by the two 16-lane halves of a ds_read_b32 group never share a bank
+constexpr int XS = 48;   // x / dz4 rows (<= 32 features)
+constexpr int HS = 16;   // hidden rows (<= 16 features)
+// padded parameter image (ae_fused.hip / ops/ae.py LAYOUT): L1 [32][16] @0 (bias row 31),
+// L2 [16][16] @512, L3 @768 (bias row 15), L4 [16][32] @1024 (bias row 15)
 constexpr int IMG2 = 512, IMG3 = 768, IMG4 = 1024, NPARAM = 1536;
-// LDS weight offsets (floats)
-constexpr int LW1 = 0, LW2 = 512, LW3 = LW2 + 16 * HS, LW4 = LW3 + 16 * HS, LW_END = LW4 + 16 * XS;
+// LDS weight fragments (floats), one 64-float block per K-step, in lane order
+constexpr int F1 = 0;                 // fwd L1: [8 K-steps][64]    A = W1[f(s,g)][c]
+constexpr int F2 = F1 + 8 * 64;       // fwd L2: [4][64]            A = W2[4g+s][c]
+constexpr int F3 = F2 + 4 * 64;       // fwd L3: [4][64]
+constexpr int F4 = F3 + 4 * 64;       // fwd L4: [2 tiles][4][64]   A = W4[4g+s][16t+c]
+constexpr int G4 = F4 + 8 * 64;       // bwd dz3: [8][64]           A = W4[c][f(s,g)]
+constexpr int G3 = G4 + 8 * 64;       // bwd dz2: [4][64]           A = W3[c][4g+s]
+constexpr int G2 = G3 + 4 * 64;       // bwd dz1: [4][64]           A = W2[c][4g+s]
+constexpr int BB1 = G2 + 4 * 64, BB2 = BB1 + 16, BB3 = BB2 + 16, BB4 = BB3 + 16, W_END = BB4 + 32;
 
 struct MBArgs {
   const float* x;       // ring [ring][ld] of raw rows
@@ -54,67 +79,82 @@ struct MBArgs {
   int B, nsteps, D, n1, n2, n3, a1, a2, a3, a4;
   float l1, lr, beta1, beta2, eps, gscale;
   int want_acc;
-  unsigned long long* prof;   // optional [11]: per-phase cycles summed over steps (wave 0): 8 phases, total,
-                              // P8's input stash, P8's gradient MFMAs + Adam (model 0 only)
+  unsigned long long* prof;   // optional [11]: per-phase cycles summed over steps (wave 0, model 0):
+                              // 0 phase A, 1 barrier 1, 2 phase B (gradients + Adam), 3 barrier 2, 8 total
   // fleet mode: workgroup b trains model b.  params / m / v are [M][NPARAM], iter /
   // cursor [M], metrics [M][4]; model b reads x + b * xmodel (0 = one shared ring).
   int64_t xmodel;
   const float* lrs;     // optional [M] per-model learning rates (hyper-parameter sweeps)
 };
 
-struct Smem {   // ~47 KB
-  float w[LW_END];
-  float x[2][MAXB * XS];
-  float h1[MAXB * HS], h2[MAXB * HS], h3[MAXB * HS];
-  float y[MAXB * XS];
-  float dz4[MAXB * XS], dz3[MAXB * HS], dz2[MAXB * HS], dz1[MAXB * HS];
+template <int MB>
+struct Smem {   // MB 48: ~47 KB, MB 128: ~108 KB
+  float w[W_END];
+  float x[MB * XS];                     // normalised inputs (phase-B activation of L1)
+  float h1[MB * HS], h2[MB * HS], h3[MB * HS];
+  float dz4[MB * XS];
+  float dz3[MB * HS], dz2[MB * HS], dz1[MB * HS];
   float red[3][NT / 64];
 };
 
-// image slot -> LDS weight index
-__device__ __forceinline__ int lds_of_slot(int s) {
-  if (s < IMG2) return LW1 + s;
-  if (s < IMG3) { const int k = s - IMG2; return LW2 + (k >> 4) * HS + (k & 15); }
-  if (s < IMG4) { const int k = s - IMG3; return LW3 + (k >> 4) * HS + (k & 15); }
-  const int k = s - IMG4;
-  return LW4 + (k >> 5) * XS + (k & 31);
+// logical feature of K-step s for lane group g (the C/D register order of the producer)
+__host__ __device__ constexpr int feat(int s, int g) { return 16 * (s >> 2) + 4 * g + (s & 3); }
+
+// LDS positions of parameter image slot p in the forward-operand and backward-operand
+// fragment images (-1 = not used there).  Bias rows go to the bias vectors only.
+__device__ __forceinline__ void lds_slots(int p, int& fw, int& bw) {
+  fw = bw = -1;
+  if (p < IMG2) {
+    const int k = p >> 4, j = p & 15;
+    if (k == 31) { fw = BB1 + j; return; }
+    fw = F1 + (4 * (k >> 4) + (k & 3)) * 64 + 16 * ((k & 15) >> 2) + j;
+  } else if (p < IMG4) {
+    const bool l2 = p < IMG3;
+    const int base = l2 ? IMG2 : IMG3;
+    const int k = (p - base) >> 4, j = (p - base) & 15;
+    if (k == 15) { fw = (l2 ? BB2 : BB3) + j; return; }
+    fw = (l2 ? F2 : F3) + (k & 3) * 64 + 16 * (k >> 2) + j;
+    bw = (l2 ? G2 : G3) + (j & 3) * 64 + 16 * (j >> 2) + k;
+  } else {
+    const int k = (p - IMG4) >> 5, j = (p - IMG4) & 31;
+    if (k == 15) { fw = BB4 + j; return; }
+    fw = F4 + (4 * (j >> 4) + (k & 3)) * 64 + 16 * (k >> 2) + (j & 15);
+    bw = G4 + (4 * (j >> 4) + (j & 3)) * 64 + 16 * ((j & 15) >> 2) + k;
+  }
 }
 
-// A 16x16 tile of the padded image whose gradient one wave computes with fp32 MFMAs
-// (v_mfma_f32_16x16x4f32: K = 4 batch rows per instruction).  Tiles: 0/1 = L1 rows
-// 0-15 / 16-31, 2 = L2, 3 = L3, 4/5 = L4 cols 0-15 / 16-31; wave w < 6 owns tile w.
+// One 16x16 tile of the padded image whose gradient a phase-B wave computes with fp32
+// MFMAs (K = 4 batch rows per instruction).  Tiles: 0/1 = L1 rows 0-15 / 16-31, 2 = L2,
+// 3 = L3, 4/5 = L4 cols 0-15 / 16-31; wave w < 6 owns tile w.
 struct Tile {
-  int act, as;      // activation base (float offset into Smem; L1: buffer 0) and row stride
-  int acol;         // this lane's activation column (image row m = row0 + c; bias row -> ones column)
+  int act, as;      // activation base (float offset into Smem) + this lane's column, row stride
+  bool ones;        // this lane's image row is a bias row: activation = 1
   int dz, ds;       // upstream-gradient base + this lane's column, row stride
-  int xb;           // L1: activation lives in the current input buffer
   int slot0, sst;   // image slots of C[4g+i][c]: slot0 + i * sst (consecutive image rows)
-  int w0, wst;      // their LDS weight indices: w0 + i * wst
   __device__ __forceinline__ int slot(int i) const { return slot0 + i * sst; }
-  __device__ __forceinline__ int w(int i) const { return w0 + i * wst; }
 };
 
-__device__ __forceinline__ Tile make_tile(int id, int c, int g, const Smem& S, const float* sbase) {
+template <class SM>
+__device__ __forceinline__ Tile make_tile(int id, int c, int g, const SM& S, const float* sbase) {
   Tile T;
   int row0 = 0, col0 = 0, img = 0, istride = 16, bias_row = 15;
   if (id <= 1) {
-    row0 = 16 * id; img = 0; bias_row = 31;
-    T.act = (int)(S.x[0] - sbase); T.as = XS; T.dz = (int)(S.dz1 - sbase); T.ds = HS; T.xb = 1;
+    row0 = 16 * id; bias_row = 31;
+    T.act = (int)(S.x - sbase); T.as = XS; T.dz = (int)(S.dz1 - sbase); T.ds = HS;
   } else if (id == 2) {
-    img = IMG2; T.act = (int)(S.h1 - sbase); T.as = HS; T.dz = (int)(S.dz2 - sbase); T.ds = HS; T.xb = 0;
+    img = IMG2; T.act = (int)(S.h1 - sbase); T.as = HS; T.dz = (int)(S.dz2 - sbase); T.ds = HS;
   } else if (id == 3) {
-    img = IMG3; T.act = (int)(S.h2 - sbase); T.as = HS; T.dz = (int)(S.dz3 - sbase); T.ds = HS; T.xb = 0;
+    img = IMG3; T.act = (int)(S.h2 - sbase); T.as = HS; T.dz = (int)(S.dz3 - sbase); T.ds = HS;
   } else {
     col0 = 16 * (id - 4); img = IMG4; istride = 32;
-    T.act = (int)(S.h3 - sbase); T.as = HS; T.dz = (int)(S.dz4 - sbase); T.ds = XS; T.xb = 0;
+    T.act = (int)(S.h3 - sbase); T.as = HS; T.dz = (int)(S.dz4 - sbase); T.ds = XS;
   }
   const int m = row0 + c;
-  T.acol = m == bias_row ? (id <= 1 ? 32 : 16) : m;
+  T.ones = m == bias_row;
+  T.act += T.ones ? 0 : m;
   T.dz += col0 + c;
   T.slot0 = img + (row0 + 4 * g) * istride + col0 + c;
   T.sst = istride;
-  T.w0 = lds_of_slot(T.slot0);
-  T.wst = id <= 1 ? 16 : id <= 3 ? HS : XS;   // LDS row strides of W1 / W2,W3 / W4
   return T;
 }
 
@@ -122,17 +162,8 @@ __device__ __forceinline__ Tile make_tile(int id, int c, int g, const Smem& S, c
 // (__syncthreads' release fence would also drain vmcnt).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Fixed-trip dot product (padding columns of activations are zero, so a padded
-// trip count is exact and lets every LDS read issue up front).
-template <int N>
-__device__ __forceinline__ float dotn(const float* act, const float* w, int wstride) {
-  float acc0 = 0.f, acc1 = 0.f;   // two chains: half the dependent-FMA latency
-#pragma unroll
-  for (int i = 0; i < N; i += 2) {
-    acc0 = fmaf(act[i], w[i * wstride], acc0);
-    if (i + 1 < N) acc1 = fmaf(act[i + 1], w[(i + 1) * wstride], acc1);
-  }
-  return acc0 + acc1;
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 // Activation codes: compile-time when PACK >= 0 (a1 | a2<<2 | a3<<4 | a4<<6), else runtime.
@@ -143,24 +174,35 @@ __device__ __forceinline__ int act_code(const MBArgs& a, int l) {
   else return l == 0 ? a.a1 : l == 1 ? a.a2 : l == 2 ? a.a3 : a.a4;
 }
 
-// Work items o = t + NT*u, u < N, fully unrolled so every item's LDS reads issue together.
-template <int N, class F>
-__device__ __forceinline__ void for_items(int t, int limit, F&& f) {
-#pragma unroll
-  for (int u = 0; u < N; ++u) {
-    const int o = t + NT * u;
-    if (o < limit) f(o);
-  }
-}
-constexpr int I16 = (MAXB * 16 + NT - 1) / NT;
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
-// KD: trip count over input features (D rounded to a compiled width); TB: batch (0 = runtime);
+// one hidden-width layer in registers: Z^T = W^T . H^T + b (4 K-steps over 16 features)
+__device__ __forceinline__ f32x4 layer16(const float* frag, const float* bias, int lane, int g, const f32x4& h) {
+  f32x4 acc = ld4(bias + 4 * g);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = mfma4(frag[s * 64 + lane], h[s], acc);
+  return acc;
+}
+
+// argmax merge with the partner lane's (value, index): ties -> lowest index (tf.argmax)
+__device__ __forceinline__ void amax_merge(float& b, int& i, float ob, int oi) {
+  const bool take = ob > b || (ob == b && oi < i);
+  b = take ? ob : b;
+  i = take ? oi : i;
+}
+
+// KD: compiled input width class (<= 18 -> 6 K-steps, 32 -> 8); TB: batch (0 = runtime);
 // PACK: activation codes (-1 = runtime); WPE: minimum waves per SIMD the register
 // allocation must allow (2 = one workgroup per CU, the latency-optimal single-model
-// build; 4 = <= 128 VGPRs, two fleet models per CU)
-template <int KD, int TB, int PACK, int WPE = 2>
+// build; 4 = <= 128 VGPRs, two fleet models per CU); MB: LDS capacity class (rows)
+template <int KD, int TB, int PACK, int WPE = 2, int MB = MB_SMALL>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void ae_minibatch_kernel(MBArgs a0) {
-  extern __shared__ float smem_raw[];
+  static_assert(TB <= MB, "compiled batch exceeds the LDS capacity class");
+  static_assert(KD <= 32, "input width <= 32");
+  constexpr int KSX = KD <= 16 ? 4 : 4 + (KD - 16 < 4 ? KD - 16 : 4);   // K-steps over the input features
+  using Smem = ::Smem<MB>;
+  extern __shared__ __attribute__((aligned(16))) float smem_raw[];
   MBArgs a = a0;   // fleet mode: rebase every per-model pointer on the workgroup's model
   {
     const int mdl = blockIdx.x;
@@ -176,73 +218,57 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   }
   Smem& S = *reinterpret_cast<Smem*>(smem_raw);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c = lane & 15, g = lane >> 4;
   const int B = TB ? TB : a.B, D = a.D, n1 = a.n1, n2 = a.n2, n3 = a.n3;
   const int a1 = act_code<PACK>(a, 0), a2 = act_code<PACK>(a, 1), a3 = act_code<PACK>(a, 2), a4 = act_code<PACK>(a, 3);
   const float* sbase = smem_raw;
-  constexpr int IKD = (MAXB * KD + NT - 1) / NT;
-  static_assert(KD == 32 || KD < 32, "KD <= 32");
 
-  // ---- gradient tiles + their Adam moments (registers for the whole launch) ----
-  const int c = lane & 15, g = lane >> 4;
+  // ---- zero the weight fragments (padding entries are never written) ----
+  for (int e = t; e < W_END; e += NT) S.w[e] = 0.f;
+  __syncthreads();
+
+  // ---- phase-B tiles + their Adam moments (registers for the whole launch) ----
   const bool has_tile = wave < 6;
   const Tile T = make_tile(has_tile ? wave : 0, c, g, S, sbase);
   float mo[4], vo[4], wo[4];   // Adam moments + the parameters themselves (sole writer)
+  int fpos[4], bpos[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    mo[i] = has_tile ? a.m[T.slot(i)] : 0.f;
-    vo[i] = has_tile ? a.v[T.slot(i)] : 0.f;
-    wo[i] = has_tile ? a.params[T.slot(i)] : 0.f;
+    const int p = T.slot(i);
+    mo[i] = has_tile ? a.m[p] : 0.f;
+    vo[i] = has_tile ? a.v[p] : 0.f;
+    wo[i] = has_tile ? a.params[p] : 0.f;
+    lds_slots(p, fpos[i], bpos[i]);
+    if (has_tile) {
+      if (fpos[i] >= 0) S.w[fpos[i]] = wo[i];
+      if (bpos[i] >= 0) S.w[bpos[i]] = wo[i];
+    }
   }
 
-  // ---- weights -> LDS (padding zero), zeroed activations, constant-1 bias columns ----
-  for (int s = t; s < NPARAM; s += NT) S.w[lds_of_slot(s)] = a.params[s];
-  for (int e = t; e < MAXB * XS; e += NT) {
-    const float one = (e % XS) == 32 ? 1.f : 0.f;
-    S.x[0][e] = one;
-    S.x[1][e] = one;
-    S.dz4[e] = 0.f;
-  }
-  for (int e = t; e < MAXB * HS; e += NT) {
-    const float one = (e % HS) == 16 ? 1.f : 0.f;
-    S.h1[e] = one; S.h2[e] = one; S.h3[e] = one;
-    S.dz1[e] = 0.f; S.dz2[e] = 0.f; S.dz3[e] = 0.f;
-  }
-
-  // ---- input tiles: element e = t + NT*u of the MAXB x 32 tile (cols >= D -> 0) ----
-  constexpr int XU = MAXB * 32 / NT;   // 3 elements per thread
-  static_assert(MAXB * 32 % NT == 0, "input tile must split evenly over the threads");
-  float sc[XU], sh[XU];
+  // ---- phase-A input operands: lane (c, g) of wave w holds row 16w + c, features f(s, g) ----
+  const int row_l = 16 * wave + c;           // this lane's row within the batch
+  const bool has_rows = 16 * wave < B;       // wave-uniform
+  const bool row_ok = row_l < B;
+  float sc[KSX], sh[KSX];
+  bool fok[KSX];
 #pragma unroll
-  for (int u = 0; u < XU; ++u) {
-    const int f = (t + NT * u) & 31;
-    sc[u] = f < D ? (a.scale ? a.scale[f] : 1.f) : 0.f;
-    sh[u] = (f < D && a.scale) ? a.shift[f] : 0.f;
+  for (int s = 0; s < KSX; ++s) {
+    const int f = feat(s, g);
+    fok[s] = f < D;
+    sc[s] = fok[s] ? (a.scale ? a.scale[f] : 1.f) : 0.f;
+    sh[s] = (fok[s] && a.scale) ? a.shift[f] : 0.f;
   }
   int64_t cur = a.cursor ? a.cursor[0] : 0;
-  float xr[XU];
-  auto fetch = [&](int64_t c0) {
-#pragma unroll
-    for (int u = 0; u < XU; ++u) {
-      const int e = t + NT * u, r = e >> 5, f = e & 31;
-      // clamped address (always in bounds), masked where the value is used
-      const int64_t row = c0 + (r < B ? r : 0);
-      xr[u] = __builtin_nontemporal_load(a.x + row * a.ld + (f < D ? f : 0));
-    }
-  };
-  auto stash = [&](float* xt) {
-#pragma unroll
-    for (int u = 0; u < XU; ++u) {
-      const int e = t + NT * u, r = e >> 5, f = e & 31;
-      if (r < B) xt[r * XS + f] = f < D ? fmaf(xr[u], sc[u], sh[u]) : 0.f;
-    }
-  };
   auto advance = [&](int64_t c0) { c0 += B; return c0 >= a.ring ? c0 - a.ring : c0; };
-
-  __syncthreads();
-  fetch(cur);
-  stash(S.x[0]);
+  float xr[KSX];
+  auto fetch = [&](int64_t c0) {
+    // clamped address (always in bounds), masked where the value is used
+    const float* rp = a.x + (c0 + (row_ok ? row_l : 0)) * a.ld;
+#pragma unroll
+    for (int s = 0; s < KSX; ++s) xr[s] = __builtin_nontemporal_load(rp + (fok[s] ? feat(s, g) : 0));
+  };
+  if (has_rows) fetch(cur);
   int64_t nxt = advance(cur);
-  if (a.nsteps > 1) fetch(nxt);
 
   float sq = 0.f, ab = 0.f, corr = 0.f;
   const float two_over_d = 2.0f / (float)D;
@@ -264,105 +290,150 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   if (prof) t_start = tp = __builtin_readcyclecounter();
 
   for (int step = 0; step < a.nsteps; ++step) {
-    const float* X = S.x[step & 1];
-    // P1: h1 = act1(x W1 + b1)
-    for_items<I16>(t, B * 16, [&](int o) {
-      const int r = o >> 4, j = o & 15;
-      const float z = dotn<KD>(X + r * XS, S.w + LW1 + j, 16) + S.w[LW1 + 31 * 16 + j];
-      const float h = j < n1 ? act_fwd(a1, z) : 0.f;
-      ab += fabsf(h);
-      S.h1[r * HS + j] = h;
-    });
-    lds_barrier();
+    // ================= phase A: forward + activation gradients of this wave's 16 rows =================
+    if (has_rows) {
+      float xv[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) xv[s] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KSX; ++s) xv[s] = (row_ok && fok[s]) ? fmaf(xr[s], sc[s], sh[s]) : 0.f;
+      if (step + 1 < a.nsteps) {   // next step's rows: in flight across phase B
+        fetch(nxt);
+        cur = nxt;
+        nxt = advance(cur);
+      }
+      // L1: h1^T = act1(W1^T x^T + b1)
+      f32x4 z1 = ld4(S.w + BB1 + 4 * g);
+#pragma unroll
+      for (int s = 0; s < KSX; ++s) z1 = mfma4(S.w[F1 + s * 64 + lane], xv[s], z1);
+      f32x4 h1, h2, h3;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float h = (4 * g + i < n1) ? act_fwd(a1, z1[i]) : 0.f;
+        h1[i] = h;
+        ab += row_ok ? fabsf(h) : 0.f;
+      }
+      // L2, L3
+      const f32x4 z2 = layer16(S.w + F2, S.w + BB2, lane, g, h1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h2[i] = (4 * g + i < n2) ? act_fwd(a2, z2[i]) : 0.f;
+      const f32x4 z3 = layer16(S.w + F3, S.w + BB3, lane, g, h2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h3[i] = (4 * g + i < n3) ? act_fwd(a3, z3[i]) : 0.f;
+      // L4 (two output tiles), MSE, dz4 = act4'(y) * 2 (y - x) / D   (1/B applied in Adam)
+      f32x4 y[2], dz4[2];
+#pragma unroll
+      for (int t4 = 0; t4 < 2; ++t4) {
+        f32x4 acc = ld4(S.w + BB4 + 16 * t4 + 4 * g);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma4(S.w[F4 + (4 * t4 + s) * 64 + lane], h3[s], acc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int f = 16 * t4 + 4 * g + i;
+          const bool ok = f < D && row_ok;
+          const float yy = f < D ? act_fwd(a4, acc[i]) : 0.f;
+          const float e = ok ? yy - xv[4 * t4 + i] : 0.f;
+          sq = fmaf(e, e, sq);
+          y[t4][i] = yy;
+          dz4[t4][i] = ok ? act_grad(a4, yy, two_over_d * e) : 0.f;
+        }
+      }
+      // categorical accuracy: argmax over features of y and x for this lane's row
+      if (a.want_acc) {
+        float by = -3.402823466e38f, bx = -3.402823466e38f;
+        int iy = 64, ix = 64;
+#pragma unroll
+        for (int t4 = 0; t4 < 2; ++t4)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int f = 16 * t4 + 4 * g + i;   // ascending: strict > keeps the lowest index
+            const bool gy = f < D && y[t4][i] > by, gx = f < D && xv[4 * t4 + i] > bx;
+            by = gy ? y[t4][i] : by;
+            iy = gy ? f : iy;
+            bx = gx ? xv[4 * t4 + i] : bx;
+            ix = gx ? f : ix;
+          }
+        // the row's four lane groups: lanes c, c+16, c+32, c+48
+        amax_merge(by, iy, xor16(by, lane), xor16i(iy, lane));
+        amax_merge(bx, ix, xor16(bx, lane), xor16i(ix, lane));
+        amax_merge(by, iy, xor32(by, lane), xor32i(iy, lane));
+        amax_merge(bx, ix, xor32(bx, lane), xor32i(ix, lane));
+        corr += (g == 0 && row_ok && iy == ix) ? 1.f : 0.f;
+      }
+      // backward: dz3 = act3'(h3) * (W4 dz4^T), dz2 = act2'(h2) * (W3 dz3^T),
+      //           dz1 = act1'(h1) * (W2 dz2^T + l1 sign(h1))   (Keras L1 activity regulariser)
+      f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KSX; ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
+      f32x4 dz3, dz2, dz1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dz3[i] = (4 * g + i < n3) ? act_grad(a3, h3[i], acc3[i]) : 0.f;
+      f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc2 = mfma4(S.w[G3 + s * 64 + lane], dz3[s], acc2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dz2[i] = (4 * g + i < n2) ? act_grad(a2, h2[i], acc2[i]) : 0.f;
+      f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc1 = mfma4(S.w[G2 + s * 64 + lane], dz2[s], acc1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float h = h1[i];
+        const float sgn = h != 0.f ? __builtin_copysignf(1.0f, h) : 0.f;
+        dz1[i] = (4 * g + i < n1 && row_ok) ? act_grad(a1, h, fmaf(a.l1, sgn, acc1[i])) : 0.f;
+      }
+      // rows -> LDS [row][feature] for the weight-gradient contraction (16-byte stores)
+      const int r = row_l;
+      st4(S.x + r * XS + 4 * g, f32x4{xv[0], xv[1], xv[2], xv[3]});
+      st4(S.x + r * XS + 16 + 4 * g, f32x4{xv[4], xv[5], xv[6], xv[7]});
+      st4(S.h1 + r * HS + 4 * g, h1);
+      st4(S.h2 + r * HS + 4 * g, h2);
+      st4(S.h3 + r * HS + 4 * g, h3);
+      st4(S.dz4 + r * XS + 4 * g, dz4[0]);
+      st4(S.dz4 + r * XS + 16 + 4 * g, dz4[1]);
+      st4(S.dz3 + r * HS + 4 * g, dz3);
+      st4(S.dz2 + r * HS + 4 * g, dz2);
+      st4(S.dz1 + r * HS + 4 * g, dz1);
+    }
     mark(0);
-    // P2, P3
-    for_items<I16>(t, B * 16, [&](int o) {
-      const int r = o >> 4, j = o & 15;
-      const float z = dotn<16>(S.h1 + r * HS, S.w + LW2 + j, HS) + S.w[LW2 + 15 * HS + j];
-      S.h2[r * HS + j] = j < n2 ? act_fwd(a2, z) : 0.f;
-    });
     lds_barrier();
     mark(1);
-    for_items<I16>(t, B * 16, [&](int o) {
-      const int r = o >> 4, j = o & 15;
-      const float z = dotn<16>(S.h2 + r * HS, S.w + LW3 + j, HS) + S.w[LW3 + 15 * HS + j];
-      S.h3[r * HS + j] = j < n3 ? act_fwd(a3, z) : 0.f;
-    });
-    lds_barrier();
-    mark(2);
-    // P4: y = act4(h3 W4 + b4); MSE; dz4 (sum-scaled, 1/B in gscale).  Items cover the
-    // KD real-or-padding columns only; columns >= KD stay at their zero initialisation.
-    for_items<IKD>(t, B * KD, [&](int o) {
-      const int r = o / KD, j = o - r * KD;
-      const float z = dotn<16>(S.h3 + r * HS, S.w + LW4 + j, XS) + S.w[LW4 + 15 * XS + j];
-      const float y = j < D ? act_fwd(a4, z) : 0.f;
-      const float e = y - X[r * XS + j];
-      sq = fmaf(e, e, sq);
-      S.y[r * XS + j] = y;
-      S.dz4[r * XS + j] = j < D ? act_grad(a4, y, two_over_d * e) : 0.f;
-    });
-    lds_barrier();
-    mark(3);
-    // P5: dz3 = act3'(dz4 W4^T)
-    for_items<I16>(t, B * 16, [&](int o) {
-      const int r = o >> 4, i = o & 15;
-      const float d = act_grad(a3, S.h3[r * HS + i], dotn<KD>(S.dz4 + r * XS, S.w + LW4 + i * XS, 1));
-      S.dz3[r * HS + i] = i < n3 ? d : 0.f;
-    });
-    lds_barrier();
-    mark(4);
-    // P6: dz2 = act2'(dz3 W3^T)
-    for_items<I16>(t, B * 16, [&](int o) {
-      const int r = o >> 4, i = o & 15;
-      const float d = act_grad(a2, S.h2[r * HS + i], dotn<16>(S.dz3 + r * HS, S.w + LW3 + i * HS, 1));
-      S.dz2[r * HS + i] = i < n2 ? d : 0.f;
-    });
-    lds_barrier();
-    mark(5);
-    // P7: dz1 = act1'(dz2 W2^T + l1 * sign(h1))   (Keras L1 activity regulariser)
-    for_items<I16>(t, B * 16, [&](int o) {
-      const int r = o >> 4, i = o & 15;
-      const float h = S.h1[r * HS + i];
-      const float sgn = h != 0.f ? __builtin_copysignf(1.0f, h) : 0.f;
-      const float d = act_grad(a1, h, fmaf(a.l1, sgn, dotn<16>(S.dz2 + r * HS, S.w + LW2 + i * HS, 1)));
-      S.dz1[r * HS + i] = i < n1 ? d : 0.f;
-    });
-    lds_barrier();
-    mark(6);
-    // P8: weight gradients = act^T . dz over the B rows (fp32 MFMA, K = 4 rows per
-    // instruction), Keras Adam on the tile in registers (waves 0-5); argmax accuracy
-    // (waves 6-7, which own no tile); next input tile to the other buffer; prefetch.
-    if (step + 1 < a.nsteps) {   // next tile -> the other buffer (not read this phase)
-      stash(S.x[(step + 1) & 1]);
-      cur = nxt;
-      nxt = advance(cur);
-    }
-    mark(9);
+    // ================= phase B: weight gradients + Adam (waves 0-5) =================
     b1t *= (double)a.beta1;
     b2t *= (double)a.beta2;
-    const float lr_t = a.lr * __builtin_amdgcn_sqrtf((float)(1.0 - b2t)) * __builtin_amdgcn_rcpf((float)(1.0 - b1t));
     if (has_tile) {
-      const float* av = sbase + T.act + ((step & 1) && T.xb ? MAXB * XS : 0) + T.acol;
+      const float lr_t = a.lr * __builtin_amdgcn_sqrtf((float)(1.0 - b2t)) * __builtin_amdgcn_rcpf((float)(1.0 - b1t));
+      const float* av = sbase + T.act;
       const float* dv = sbase + T.dz;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if constexpr (TB > 0) {
-        constexpr int CH = TB / 4 >= 4 ? 4 : TB / 4;   // independent MFMA chains, summed at the end
+        constexpr int NS = (TB + 3) / 4;
+        constexpr int CH = NS >= 4 ? 4 : NS;   // independent MFMA chains, summed at the end
         f32x4 part[CH];
 #pragma unroll
         for (int c4 = 0; c4 < CH; ++c4) part[c4] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s4 = 0; s4 < TB / 4; ++s4) {
-          const int r = 4 * s4 + g;
-          part[s4 % CH] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r * T.as], dv[r * T.ds], part[s4 % CH], 0, 0, 0);
+        for (int s4 = 0; s4 < NS; ++s4) {
+          const int r = 4 * s4 + g;   // rows in [B, 4*NS) hold zero gradients
+          const float x0 = T.ones ? 1.f : av[r * T.as];
+          part[s4 % CH] = mfma4(x0, dv[r * T.ds], part[s4 % CH]);
         }
 #pragma unroll
         for (int c4 = 0; c4 < CH; ++c4) acc += part[c4];
       } else {
-        for (int s4 = 0; s4 < (B + 3) / 4; ++s4) {
+        f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
+        const int ns = (B + 3) / 4;
+        int s4 = 0;
+        for (; s4 + 1 < ns; s4 += 2) {
           const int r = 4 * s4 + g;
-          const float x0 = r < B ? av[r * T.as] : 0.f, d0 = r < B ? dv[r * T.ds] : 0.f;
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, d0, acc, 0, 0, 0);
+          acc = mfma4(T.ones ? 1.f : av[r * T.as], dv[r * T.ds], acc);
+          acc2 = mfma4(T.ones ? 1.f : av[(r + 4) * T.as], dv[(r + 4) * T.ds], acc2);
         }
+        if (s4 < ns) {
+          const int r = 4 * s4 + g;
+          acc = mfma4(T.ones ? 1.f : av[r * T.as], dv[r * T.ds], acc);
+        }
+        acc += acc2;
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -372,27 +443,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         mo[i] = mm;
         vo[i] = vv;
         wo[i] -= lr_t * mm * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv) + a.eps);   // v_sqrt / v_rcp, ~1 ulp
-        S.w[T.w(i)] = wo[i];
+        if (fpos[i] >= 0) S.w[fpos[i]] = wo[i];
+        if (bpos[i] >= 0) S.w[bpos[i]] = wo[i];
       }
-      mark(10);
-    } else if (a.want_acc && t - 6 * 64 < B) {
-      const int r = t - 6 * 64;
-      int iy = 0, ix = 0;
-      float by = S.y[r * XS], bx = X[r * XS];
-#pragma unroll
-      for (int f = 1; f < KD; ++f) {   // ties -> lowest index (tf.argmax); branch-free selects
-        const float yv = S.y[r * XS + f], xv = X[r * XS + f];
-        const bool gy = f < D && yv > by, gx = f < D && xv > bx;
-        by = gy ? yv : by;
-        iy = gy ? f : iy;
-        bx = gx ? xv : bx;
-        ix = gx ? f : ix;
-      }
-      corr += iy == ix ? 1.f : 0.f;
     }
-    if (step + 2 < a.nsteps) fetch(nxt);
+    mark(2);
     lds_barrier();
-    mark(7);
+    mark(3);
   }
 
   // ---- write back: the whole image (padding slots keep zero gradients), moments, metrics ----
@@ -450,14 +507,31 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
            dims[3], acts[0], acts[1], acts[2], acts[3], l1, lr, beta1, beta2, eps, gscale, want_acc, prof,
            xmodel, lrs};
   const bool ref = acts[0] == ACT_TANH && acts[1] == ACT_RELU && acts[2] == ACT_TANH && acts[3] == ACT_RELU;
-  auto k = ae_minibatch_kernel<32, 0, -1>;   // any shape / activations
-  if (ref && dims[0] == 18) k = B == 32 ? ae_minibatch_kernel<18, 32, PACK_REF> : ae_minibatch_kernel<18, 0, PACK_REF>;
-  else if (ref) k = B == 32 ? ae_minibatch_kernel<32, 32, PACK_REF> : ae_minibatch_kernel<32, 0, PACK_REF>;
-  // a fleet larger than one model per CU: the 128-VGPR build puts two models on each CU
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (ref && dims[0] == 18 && B == 32 && nmodels > cus) k = ae_minibatch_kernel<18, 32, PACK_REF, 4>;
-  hipLaunchKernelGGL(k, dim3(nmodels), dim3(NT), sizeof(Smem), stream, a);
+  void (*k)(MBArgs) = nullptr;
+  size_t lds = 0;
+  if (B <= MB_SMALL) {
+    lds = sizeof(Smem<MB_SMALL>);
+    k = ae_minibatch_kernel<32, 0, -1>;   // any shape / activations
+    if (ref && dims[0] <= 18) k = B == 32 ? ae_minibatch_kernel<18, 32, PACK_REF> : ae_minibatch_kernel<18, 0, PACK_REF>;
+    else if (ref) k = B == 32 ? ae_minibatch_kernel<32, 32, PACK_REF> : ae_minibatch_kernel<32, 0, PACK_REF>;
+    // a fleet larger than one model per CU: the 128-VGPR build puts two models on each CU
+    if (ref && dims[0] <= 18 && B == 32 && nmodels > cus) k = ae_minibatch_kernel<18, 32, PACK_REF, 4>;
+  } else {
+    // cardata-v3's fit(batch_size=100) and anything up to 128 rows: one workgroup per CU
+    lds = sizeof(Smem<MB_LARGE>);
+    k = ae_minibatch_kernel<32, 0, -1, 2, MB_LARGE>;
+    if (ref && dims[0] <= 18)
+      k = B == 100 ? ae_minibatch_kernel<18, 100, PACK_REF, 2, MB_LARGE> : ae_minibatch_kernel<18, 0, PACK_REF, 2, MB_LARGE>;
+    else if (ref) k = ae_minibatch_kernel<32, 0, PACK_REF, 2, MB_LARGE>;
+  }
+  if (lds > 65536) {   // > 64 KB of dynamic LDS must be opted into per kernel
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(nmodels), dim3(NT), lds, stream, a);
   return hipGetLastError();
 }
 

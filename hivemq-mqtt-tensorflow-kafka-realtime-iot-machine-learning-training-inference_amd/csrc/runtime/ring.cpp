@@ -19,8 +19,8 @@ PinnedRing::PinnedRing(int slots, size_t slot_bytes, int device) : device_(devic
   host_.assign((size_t)slots, nullptr);
   copied_.assign((size_t)slots, nullptr);
   released_.assign((size_t)slots, nullptr);
-  pending_copy_.assign((size_t)slots, false);
-  pending_release_.assign((size_t)slots, false);
+  pending_copy_.assign((size_t)slots, 0);
+  pending_release_.assign((size_t)slots, 0);
   state_.assign((size_t)slots, SlotState::kIdle);
   for (int i = 0; i < slots; ++i) {
     RING_CHECK(hipHostMalloc(&host_[(size_t)i], slot_bytes_, hipHostMallocDefault));
@@ -41,9 +41,15 @@ PinnedRing::~PinnedRing() {
 
 void* PinnedRing::host(int slot) {
   check(slot);
-  if (pending_copy_[(size_t)slot]) {  // host buffer still being read by the DMA engine
+  bool pending;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    pending = pending_copy_[(size_t)slot] != 0;
+  }
+  if (pending) {  // host buffer still being read by the DMA engine (wait outside the lock)
     RING_CHECK(hipEventSynchronize(copied_[(size_t)slot]));
-    pending_copy_[(size_t)slot] = false;
+    std::lock_guard<std::mutex> g(mu_);
+    pending_copy_[(size_t)slot] = 0;
   }
   return host_[(size_t)slot];
 }
@@ -51,6 +57,7 @@ void* PinnedRing::host(int slot) {
 void PinnedRing::submit(int slot, void* dst, size_t bytes) {
   check(slot);
   if (bytes > slot_bytes_) throw std::invalid_argument("PinnedRing: copy larger than a slot");
+  std::lock_guard<std::mutex> g(mu_);
   if (state_[(size_t)slot] != SlotState::kIdle)
     throw std::logic_error("PinnedRing: submit on slot " + std::to_string(slot) +
                            (state_[(size_t)slot] == SlotState::kCopying ? " whose previous copy was never consumed"
@@ -58,17 +65,18 @@ void PinnedRing::submit(int slot, void* dst, size_t bytes) {
   RING_CHECK(hipSetDevice(device_));
   if (pending_release_[(size_t)slot]) {  // device buffer still in use by the consumer
     RING_CHECK(hipStreamWaitEvent(copy_, released_[(size_t)slot], 0));
-    pending_release_[(size_t)slot] = false;
+    pending_release_[(size_t)slot] = 0;
   }
   RING_CHECK(hipMemcpyAsync(dst, host_[(size_t)slot], bytes, hipMemcpyHostToDevice, copy_));
   RING_CHECK(hipEventRecord(copied_[(size_t)slot], copy_));
-  pending_copy_[(size_t)slot] = true;
+  pending_copy_[(size_t)slot] = 1;
   state_[(size_t)slot] = SlotState::kCopying;
   bytes_ += bytes;
 }
 
 void PinnedRing::wait(int slot, hipStream_t stream) {
   check(slot);
+  std::lock_guard<std::mutex> g(mu_);
   if (state_[(size_t)slot] == SlotState::kIdle)
     throw std::logic_error("PinnedRing: wait on slot " + std::to_string(slot) + " with no copy submitted");
   RING_CHECK(hipStreamWaitEvent(stream, copied_[(size_t)slot], 0));
@@ -77,11 +85,12 @@ void PinnedRing::wait(int slot, hipStream_t stream) {
 
 void PinnedRing::release(int slot, hipStream_t stream) {
   check(slot);
+  std::lock_guard<std::mutex> g(mu_);
   if (state_[(size_t)slot] != SlotState::kConsuming)
     throw std::logic_error("PinnedRing: release of slot " + std::to_string(slot) +
                            " whose copy the consumer never waited for");
   RING_CHECK(hipEventRecord(released_[(size_t)slot], stream));
-  pending_release_[(size_t)slot] = true;
+  pending_release_[(size_t)slot] = 1;
   state_[(size_t)slot] = SlotState::kIdle;
 }
 

@@ -12,6 +12,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <mutex>
 #include <stdexcept>
 #include <vector>
 
@@ -43,6 +44,12 @@ class PinnedRing {
   // release of a slot whose copy the consumer never waited for (its kernels may
   // have read stale data), or wait on a slot with no copy in flight throw
   // std::logic_error instead of silently corrupting a batch.
+  //
+  // Thread safety: one producer thread may host()/submit() slots while one consumer
+  // thread wait()s / release()s OTHER slots (per-slot state is byte-sized and guarded
+  // by a mutex; the blocking copy-event wait in host() runs outside it).  The caller
+  // still orders release(slot) before the next submit(slot) (DeviceLoader: a
+  // free-slot semaphore), so the copy stream never waits on an unrecorded event.
   hipStream_t copy_stream() const { return copy_; }
   uint64_t bytes_copied() const { return bytes_; }
 
@@ -51,11 +58,12 @@ class PinnedRing {
   size_t slot_bytes_;
   std::vector<void*> host_;
   std::vector<hipEvent_t> copied_, released_;
-  std::vector<bool> pending_copy_, pending_release_;
+  std::vector<uint8_t> pending_copy_, pending_release_;   // not vector<bool>: slots change from two threads
   enum class SlotState : uint8_t { kIdle, kCopying, kConsuming };
   std::vector<SlotState> state_;
   hipStream_t copy_ = nullptr;
   uint64_t bytes_ = 0;
+  std::mutex mu_;
   void check(int slot) const {
     if (slot < 0 || slot >= (int)host_.size()) throw std::out_of_range("PinnedRing: bad slot");
   }

@@ -541,23 +541,31 @@ struct RingPy {
     c10::hip::HIPGuard guard(dev);
     r = std::make_unique<sml::PinnedRing>(slots, (size_t)slot_bytes, dev);
   }
-  int64_t fill(int slot, py::array arr) {
+  int64_t fill(int slot, py::array arr, int64_t offset) {
     py::buffer_info bi = arr.request();
     if (!(arr.flags() & py::array::c_style)) throw std::invalid_argument("fill: array must be C-contiguous");
     const size_t bytes = (size_t)bi.size * (size_t)bi.itemsize;
-    if (bytes > r->slot_bytes()) throw std::invalid_argument("fill: array larger than a ring slot");
+    if (offset < 0 || (size_t)offset + bytes > r->slot_bytes())
+      throw std::invalid_argument("fill: array does not fit the ring slot at that offset");
     const void* src = bi.ptr;
     {
       py::gil_scoped_release rel;
-      void* dst = r->host(slot);
-      std::memcpy(dst, src, bytes);
+      char* dst = static_cast<char*>(r->host(slot));   // waits for the slot's previous H2D
+      std::memcpy(dst + offset, src, bytes);
     }
     return (int64_t)bytes;
+  }
+  // Host address of a slot once its previous H2D has landed: native producers (the
+  // C++ ingest feed) write decoded rows straight into the page-locked buffer.
+  uint64_t host_ptr(int slot) {
+    py::gil_scoped_release rel;
+    return reinterpret_cast<uint64_t>(r->host(slot));
   }
   void submit(int slot, const at::Tensor& dst, int64_t bytes) {
     TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "submit: dst must be a contiguous device tensor");
     TORCH_CHECK(bytes <= (int64_t)(dst.numel() * dst.element_size()), "submit: dst too small");
     c10::hip::HIPGuard guard(device);
+    py::gil_scoped_release rel;
     r->submit(slot, dst.data_ptr(), (size_t)bytes);
   }
   void wait(int slot) {
@@ -660,7 +668,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cursor_ring") = 0, py::arg("scratch") = py::none());
   py::class_<RingPy>(m, "PinnedRing")
       .def(py::init<int, int64_t, int>(), py::arg("slots"), py::arg("slot_bytes"), py::arg("device"))
-      .def("fill", &RingPy::fill, py::arg("slot"), py::arg("array"))
+      .def("fill", &RingPy::fill, py::arg("slot"), py::arg("array"), py::arg("offset") = 0)
+      .def("host_ptr", &RingPy::host_ptr, py::arg("slot"))
       .def("submit", &RingPy::submit, py::arg("slot"), py::arg("dst"), py::arg("bytes"))
       .def("wait", &RingPy::wait, py::arg("slot"))
       .def("release", &RingPy::release, py::arg("slot"))

@@ -242,8 +242,10 @@ def json_lines(path: str, chunk: int = 65536) -> Stream:
 def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optional[str] = None,
           eof: bool = True, config: Optional[Sequence[str]] = None, max_bytes: int = 4 << 20,
           framing: bool = True, commit: bool = False, resume: bool = False,
-          idle_timeout_s: Optional[float] = None, workers: int = 1) -> Stream:
+          idle_timeout_s: Optional[float] = None, workers: int = 1, native: bool = False) -> Stream:
     """Kafka topic(s) of (Confluent-framed) Avro car records -> raw feature chunks."""
+    if native:
+        raise NotImplementedError("native ingest feed not built yet")
     from ..kafka import KafkaDataset
     from .avro import AvroCodec
 

@@ -156,8 +156,16 @@ class Autoencoder:
     # ------------------------------------------------------------------ training
     def fit(self, x=None, y=None, epochs: int = 1, batch_size: int = 32, verbose: int = 1,
             callbacks: Optional[Sequence[Callback]] = None, validation_data=None, shuffle: bool = True,
-            steps_per_epoch: Optional[int] = None, seed: int = 0, initial_epoch: int = 0) -> History:
+            steps_per_epoch: Optional[int] = None, seed: int = 0, initial_epoch: int = 0,
+            engine: str = "auto") -> History:
         """Train on an array (``y`` must be ``x`` or None: autoencoder) or a Stream.
+
+        ``engine``: ``"persistent"`` runs every Keras step of an epoch on the persistent
+        small-batch kernel (``ae_minibatch.hip``: one launch per up to 16k steps, fp32,
+        batch <= 128 -- the reference's batch 32 and cardata-v3's batch 100,
+        cardata-v3.py:176-177, 212-222); ``"launch"`` issues the two-launch fused step
+        (bf16 MFMA train kernel + slab-reduce/Adam) per batch, for any batch size;
+        ``"auto"`` picks ``persistent`` on a single ROCm replica when the batch fits.
 
         Under ``torch.distributed`` (RCCL) every rank trains on its own shard:
         arrays are split contiguously by rank, Streams are expected to be
@@ -190,6 +198,8 @@ class Autoencoder:
                 arr = arr[s0:s1]
             xd = self._to_device(arr) if self.device.type == "cuda" else self._cpu_x(arr)
         from ..parallel.fault import maybe_inject
+        persistent = self._use_persistent(engine, batch_size, world)
+        self.last_fit_engine = "persistent" if persistent else ("launch" if self.device.type == "cuda" else "torch-cpu")
         gstep = int(getattr(self, "_global_step", 0))
         for epoch in range(initial_epoch, epochs):
             rng = np.random.default_rng([seed, rank, epoch])   # epoch-keyed: a resumed run reshuffles identically
@@ -198,7 +208,20 @@ class Autoencoder:
                 cb.on_epoch_begin(epoch)
             be.reset_metrics()
             steps = 0
-            if is_stream:
+            if persistent and is_stream:
+                steps = self._fit_stream_persistent(x, batch_size, steps_per_epoch, gstep, rank)
+                gstep += steps
+            elif persistent:
+                n = len(xd)
+                nb = math.ceil(n / batch_size)
+                if steps_per_epoch is not None:
+                    nb = min(nb, steps_per_epoch)
+                xs = xd[torch.as_tensor(rng.permutation(n), device=xd.device)] if shuffle else xd
+                for s in range(gstep, gstep + nb):   # injection points, before the epoch's launches
+                    maybe_inject(s, rank)
+                steps, _ = be.train_rows(xs[:min(n, nb * batch_size)], batch_size)
+                gstep += steps
+            elif is_stream:
                 for xb in self._stream_batches(x, batch_size):
                     if steps_per_epoch is not None and steps >= steps_per_epoch:
                         break
@@ -257,6 +280,83 @@ class Autoencoder:
         for cb in cbs:
             cb.on_train_end()
         return hist
+
+    def _use_persistent(self, engine: str, batch_size: int, world: int) -> bool:
+        if engine not in ("auto", "persistent", "launch"):
+            raise ValueError(f"engine must be auto / persistent / launch, got {engine!r}")
+        if engine == "launch" or self.device.type != "cuda":
+            if engine == "persistent" and self.device.type != "cuda":
+                raise ValueError("engine='persistent' needs a ROCm device")
+            return False
+        fits = world == 1 and 1 <= batch_size <= self.backend.max_minibatch()
+        if engine == "persistent" and not fits:
+            raise ValueError(f"engine='persistent' needs one replica and batch_size <= "
+                             f"{self.backend.max_minibatch()} (got batch {batch_size}, world {world})")
+        return fits
+
+    def _stream_device_chunks(self, stream, chunk_rows: int = 1 << 16):
+        """Device chunks of raw rows from a Stream (no host re-batching): the pinned ring
+        moves whole chunks, a deferred ``filter_normal(device=True)`` runs as K8 on them."""
+        from ..data.loader import DeviceLoader
+        feed = getattr(stream, "native_feed", None)
+        if feed is not None:
+            yield from feed.device_chunks(self.device)
+            return
+        deferred = getattr(stream, "device_filter", None)
+        if deferred is not None:
+            parent, keep = deferred
+            yield from DeviceLoader(parent, self.device, max_rows=chunk_rows, features=self.spec.input_dim,
+                                    keep_label=keep).chunks()
+            return
+        yield from DeviceLoader(stream, self.device, max_rows=chunk_rows, features=self.spec.input_dim).chunks()
+
+    def _fit_stream_persistent(self, stream, B: int, max_steps: Optional[int], gstep: int, rank: int) -> int:
+        """One streaming epoch on the persistent kernel: whole device chunks go to
+        ``train_rows`` (hundreds of Keras steps per launch); the < B rows left at a chunk
+        boundary are carried to the next chunk, so the batches are exactly the
+        reference's ``batch(B)`` over the (filtered) stream; ``max_steps`` = ``take(n)``."""
+        from ..parallel.fault import maybe_inject
+        be = self.backend
+        D = self.spec.input_dim
+        carry = torch.empty((B, D), dtype=torch.float32, device=self.device)
+        have, steps = 0, 0
+
+        def budget():
+            return None if max_steps is None else max_steps - steps
+
+        for xd in self._stream_device_chunks(stream):
+            if max_steps is not None and steps >= max_steps:
+                break
+            k, pos = xd.size(0), 0
+            if have:   # complete the carried batch first
+                t = min(B - have, k)
+                carry[have:have + t].copy_(xd[:t])
+                have += t
+                pos = t
+                if have < B:
+                    continue
+                maybe_inject(gstep + steps, rank)
+                s, _ = be.train_rows(carry, B, max_steps=budget())
+                steps += s
+                have = 0
+            nfull = (k - pos) // B
+            if max_steps is not None:
+                nfull = min(nfull, max_steps - steps)
+            if nfull:
+                for s in range(gstep + steps, gstep + steps + nfull):
+                    maybe_inject(s, rank)
+                s, _ = be.train_rows(xd[pos:pos + nfull * B], B)
+                steps += s
+                pos += nfull * B
+            rest = k - pos
+            if rest and (max_steps is None or steps < max_steps):
+                carry[:rest].copy_(xd[pos:])
+                have = rest
+        if have and (max_steps is None or steps < max_steps):
+            maybe_inject(gstep + steps, rank)
+            s, _ = be.train_rows(carry[:have], B)   # Keras' short final batch
+            steps += s
+        return steps
 
     def _stream_batches(self, stream, batch_size: int):
         """Yield device (or CPU) batches of raw rows from a Stream."""

@@ -224,10 +224,56 @@ class FusedAE:
         if self.ring is None:
             raise RuntimeError("attach_ring() first")
         B = self.ring_batch
-        if B > self.C.ae_minibatch_max_batch():
-            raise ValueError(f"batch {B} > {self.C.ae_minibatch_max_batch()}: use step_ring()")
-        self.C.ae_train_minibatches(self.ring, self.cursor, self.scale, self.shift, self.params, self.m, self.v,
-                                    self.iter, self.metrics, B, int(nsteps), self.spec.dims, self.spec.act_codes,
+        if B > self.max_minibatch():
+            raise ValueError(f"batch {B} > {self.max_minibatch()}: use step_ring()")
+        self._launch_minibatch(self.ring, self.cursor, B, int(nsteps), prof)
+
+    def max_minibatch(self) -> int:
+        """Largest batch the persistent small-batch trainer takes (128: cardata-v3's 100 fits)."""
+        return int(self.C.ae_minibatch_max_batch())
+
+    def train_rows(self, x: torch.Tensor, batch: int, max_steps: Optional[int] = None,
+                   chunk_steps: int = 1 << 14) -> Tuple[int, int]:
+        """Keras ``fit`` over the rows of ``x`` in order: one Adam update per ``batch`` rows,
+        the last batch short if ``len(x)`` is not a multiple (Keras' partial final batch),
+        all on the persistent kernel (``csrc/kernels/ae_minibatch.hip``).
+
+        Launches: ``ceil(full_batches / chunk_steps)`` for the full batches (each launch
+        runs ``chunk_steps`` sequential steps with parameters, moments and activations on
+        chip) plus one for the partial batch.  Returns ``(steps, rows)`` consumed, capped
+        by ``max_steps`` (the reference's ``take(100)``, cardata-v3.py:218).
+        """
+        self._check_x(x)
+        B = int(batch)
+        if not 1 <= B <= self.max_minibatch():
+            raise ValueError(f"batch {B} outside [1, {self.max_minibatch()}]")
+        n = int(x.size(0))
+        nfull, rem = divmod(n, B)
+        if max_steps is not None:
+            if nfull >= max_steps:
+                nfull, rem = int(max_steps), 0
+            elif nfull + (1 if rem else 0) > max_steps:
+                rem = 0
+        if not hasattr(self, "_tcur"):
+            self._tcur = torch.zeros(1, dtype=torch.int64, device=self.device)
+        steps = 0
+        if nfull:
+            ring = x[:nfull * B]
+            self._tcur.zero_()
+            while steps < nfull:
+                k = min(int(chunk_steps), nfull - steps)
+                self._launch_minibatch(ring, self._tcur, B, k)
+                steps += k
+        if rem:
+            self._tcur.zero_()
+            self._launch_minibatch(x[nfull * B:nfull * B + rem], self._tcur, rem, 1)
+            steps += 1
+        return steps, nfull * B + rem
+
+    def _launch_minibatch(self, ring: torch.Tensor, cursor: torch.Tensor, B: int, nsteps: int,
+                          prof: Optional[torch.Tensor] = None) -> None:
+        self.C.ae_train_minibatches(ring, cursor, self.scale, self.shift, self.params, self.m, self.v,
+                                    self.iter, self.metrics, int(B), int(nsteps), self.spec.dims, self.spec.act_codes,
                                     float(self.spec.activity_l1), self.lr, self.beta_1, self.beta_2, self.epsilon,
                                     1.0 / B, bool(self.want_acc), prof)
 

@@ -36,7 +36,8 @@ REF_ACTS = ("tanh", "relu", "tanh", "relu")
 
 @pytest.mark.parametrize("D,B,nsteps,launches,acts", [
     (18, 32, 50, 1, REF_ACTS), (18, 32, 64, 4, REF_ACTS), (30, 32, 40, 2, REF_ACTS), (18, 48, 30, 1, REF_ACTS),
-    (18, 7, 25, 1, REF_ACTS),
+    (18, 7, 25, 1, REF_ACTS), (18, 100, 30, 2, REF_ACTS), (18, 128, 20, 1, REF_ACTS), (18, 77, 12, 1, REF_ACTS),
+    (30, 100, 16, 1, REF_ACTS),
     (18, 32, 30, 1, ("sigmoid", "linear", "relu", "sigmoid")),   # runtime-activation instantiation
     (11, 20, 30, 3, ("relu", "tanh", "linear", "tanh")),
 ])
@@ -99,6 +100,6 @@ def test_minibatch_matches_launch_per_step_path(cuda_device):
 def test_minibatch_rejects_bad_batch(cuda_device):
     spec = AESpec()
     fused = FusedAE(spec, init_dense_weights(spec.layer_sizes, seed=0), cuda_device)
-    fused.attach_ring(torch.zeros((64 * 4, 18), device=cuda_device), 64)
+    fused.attach_ring(torch.zeros((129 * 4, 18), device=cuda_device), 129)
     with pytest.raises(ValueError):
         fused.train_minibatches(2)

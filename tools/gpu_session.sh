@@ -26,7 +26,9 @@ step() {  # step <name> <timeout> <cmd...>
 STEPS=${STEPS:-"tests smoke bench prof"}
 for s in $STEPS; do
   case $s in
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    testsel) step pytest_sel 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    fit) step bench_fit 600 python bench/bench_fit.py ${FIT_ARGS:-} ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)
