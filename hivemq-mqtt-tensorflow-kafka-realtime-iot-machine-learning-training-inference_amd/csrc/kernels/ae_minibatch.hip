@@ -22,15 +22,16 @@
 //            lane group g contributes feature f(s,g) = 16(s>>2) + 4g + (s&3)); the A
 //            operand (weights) is read in that same permuted K order from LDS images
 //            stored in fragment order (one contiguous 256-byte block per K-step: no
-//            bank conflicts).  Bias = the accumulator's initial value.  Loss, L1
-//            activity term and argmax accuracy are lane-local + two permlane swaps.
-//            The wave then stores its activations / gradients [row][feature] to LDS.
+//            bank conflicts).  Bias = the accumulator's initial value.  Loss and the L1
+//            activity term are lane-local.  The wave then stores its activations /
+//            gradients / reconstructions [row][feature] to LDS.
 //   barrier
 //   phase B  waves 0-5 each own one 16x16 tile of the padded parameter image: weight
 //            gradient act^T . dz over the B rows (fp32 MFMA, K = 4 rows per
 //            instruction, bias rows read a constant 1), then Keras Adam on the 4
 //            parameters per lane they hold in registers for the whole launch, and
-//            write the new values into the forward / backward weight fragments.
+//            write the new values into the forward / backward weight fragments;
+//            waves 6-7 take the argmax accuracy of one row per lane meanwhile.
 //   barrier
 // Two barriers per step (the round-1 version had eight, one per layer phase, and did
 // every dot product on the VALU: 12 us per batch-100 step).
@@ -94,6 +95,8 @@ struct Smem {   // MB 48: ~47 KB, MB 128: ~108 KB
   float h1[MB * HS], h2[MB * HS], h3[MB * HS];
   float dz4[MB * XS];
   float dz3[MB * HS], dz2[MB * HS], dz1[MB * HS];
+  float y[MB * XS];                     // reconstructions (phase-B argmax accuracy)
+  float one[4];                         // constant 1 (bias-row activation), dummy store slot
   float red[3][NT / 64];
 };
 
@@ -101,9 +104,10 @@ struct Smem {   // MB 48: ~47 KB, MB 128: ~108 KB
 __host__ __device__ constexpr int feat(int s, int g) { return 16 * (s >> 2) + 4 * g + (s & 3); }
 
 // LDS positions of parameter image slot p in the forward-operand and backward-operand
-// fragment images (-1 = not used there).  Bias rows go to the bias vectors only.
-__device__ __forceinline__ void lds_slots(int p, int& fw, int& bw) {
-  fw = bw = -1;
+// fragment images (`none` = not used there: a dummy word, so the stores need no branch).
+// Bias rows go to the bias vectors only.
+__device__ __forceinline__ void lds_slots(int p, int& fw, int& bw, int none) {
+  fw = bw = none;
   if (p < IMG2) {
     const int k = p >> 4, j = p & 15;
     if (k == 31) { fw = BB1 + j; return; }
@@ -127,8 +131,8 @@ __device__ __forceinline__ void lds_slots(int p, int& fw, int& bw) {
 // MFMAs (K = 4 batch rows per instruction).  Tiles: 0/1 = L1 rows 0-15 / 16-31, 2 = L2,
 // 3 = L3, 4/5 = L4 cols 0-15 / 16-31; wave w < 6 owns tile w.
 struct Tile {
-  int act, as;      // activation base (float offset into Smem) + this lane's column, row stride
-  bool ones;        // this lane's image row is a bias row: activation = 1
+  int act, as;      // activation base (float offset into Smem) + this lane's column, row stride;
+                    // a bias-row lane reads the constant-1 word with stride 0 (branch-free)
   int dz, ds;       // upstream-gradient base + this lane's column, row stride
   int slot0, sst;   // image slots of C[4g+i][c]: slot0 + i * sst (consecutive image rows)
   __device__ __forceinline__ int slot(int i) const { return slot0 + i * sst; }
@@ -150,8 +154,12 @@ __device__ __forceinline__ Tile make_tile(int id, int c, int g, const SM& S, con
     T.act = (int)(S.h3 - sbase); T.as = HS; T.dz = (int)(S.dz4 - sbase); T.ds = XS;
   }
   const int m = row0 + c;
-  T.ones = m == bias_row;
-  T.act += T.ones ? 0 : m;
+  if (m == bias_row) {
+    T.act = (int)(S.one - sbase);
+    T.as = 0;
+  } else {
+    T.act += m;
+  }
   T.dz += col0 + c;
   T.slot0 = img + (row0 + 4 * g) * istride + col0 + c;
   T.sst = istride;
@@ -183,13 +191,6 @@ __device__ __forceinline__ f32x4 layer16(const float* frag, const float* bias, i
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc = mfma4(frag[s * 64 + lane], h[s], acc);
   return acc;
-}
-
-// argmax merge with the partner lane's (value, index): ties -> lowest index (tf.argmax)
-__device__ __forceinline__ void amax_merge(float& b, int& i, float ob, int oi) {
-  const bool take = ob > b || (ob == b && oi < i);
-  b = take ? ob : b;
-  i = take ? oi : i;
 }
 
 // KD: compiled input width class (<= 18 -> 6 K-steps, 32 -> 8); TB: batch (0 = runtime);
@@ -238,12 +239,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     mo[i] = has_tile ? a.m[p] : 0.f;
     vo[i] = has_tile ? a.v[p] : 0.f;
     wo[i] = has_tile ? a.params[p] : 0.f;
-    lds_slots(p, fpos[i], bpos[i]);
+    lds_slots(p, fpos[i], bpos[i], (int)(S.one + 1 - S.w));
     if (has_tile) {
-      if (fpos[i] >= 0) S.w[fpos[i]] = wo[i];
-      if (bpos[i] >= 0) S.w[bpos[i]] = wo[i];
+      S.w[fpos[i]] = wo[i];
+      S.w[bpos[i]] = wo[i];
     }
   }
+  if (t == 0) S.one[0] = 1.f;
 
   // ---- phase-A input operands: lane (c, g) of wave w holds row 16w + c, features f(s, g) ----
   const int row_l = 16 * wave + c;           // this lane's row within the batch
@@ -289,6 +291,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   __syncthreads();
   if (prof) t_start = tp = __builtin_readcyclecounter();
 
+  // Reference activations (tanh / relu / linear: act(0) == 0): padded features stay exactly
+  // zero by induction (zero padded weights -> zero activations -> zero padded gradients), so
+  // only the batch-row mask is needed; sigmoid (act(0) = 0.5) or runtime codes mask features.
+  constexpr bool FMASK = PACK < 0 || ((PACK & 3) == ACT_SIGMOID) || (((PACK >> 2) & 3) == ACT_SIGMOID) ||
+                         (((PACK >> 4) & 3) == ACT_SIGMOID) || (((PACK >> 6) & 3) == ACT_SIGMOID);
+  const float rowf = row_ok ? 1.f : 0.f;
+  const float l1r = row_ok ? a.l1 : 0.f;
+  auto fm = [&](bool keep, float v) { return FMASK ? (keep ? v : 0.f) : v; };
+
   for (int step = 0; step < a.nsteps; ++step) {
     // ================= phase A: forward + activation gradients of this wave's 16 rows =================
     if (has_rows) {
@@ -309,17 +320,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       f32x4 h1, h2, h3;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float h = (4 * g + i < n1) ? act_fwd(a1, z1[i]) : 0.f;
+        const float h = fm(4 * g + i < n1, act_fwd(a1, z1[i]));
         h1[i] = h;
-        ab += row_ok ? fabsf(h) : 0.f;
+        ab = fmaf(fabsf(h), rowf, ab);
       }
       // L2, L3
       const f32x4 z2 = layer16(S.w + F2, S.w + BB2, lane, g, h1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) h2[i] = (4 * g + i < n2) ? act_fwd(a2, z2[i]) : 0.f;
+      for (int i = 0; i < 4; ++i) h2[i] = fm(4 * g + i < n2, act_fwd(a2, z2[i]));
       const f32x4 z3 = layer16(S.w + F3, S.w + BB3, lane, g, h2);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) h3[i] = (4 * g + i < n3) ? act_fwd(a3, z3[i]) : 0.f;
+      for (int i = 0; i < 4; ++i) h3[i] = fm(4 * g + i < n3, act_fwd(a3, z3[i]));
       // L4 (two output tiles), MSE, dz4 = act4'(y) * 2 (y - x) / D   (1/B applied in Adam)
       f32x4 y[2], dz4[2];
 #pragma unroll
@@ -330,35 +341,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int f = 16 * t4 + 4 * g + i;
-          const bool ok = f < D && row_ok;
-          const float yy = f < D ? act_fwd(a4, acc[i]) : 0.f;
-          const float e = ok ? yy - xv[4 * t4 + i] : 0.f;
+          const float yy = fm(f < D, act_fwd(a4, acc[i]));
+          const float e = row_ok ? yy - xv[4 * t4 + i] : 0.f;   // padded features: 0 - 0
           sq = fmaf(e, e, sq);
           y[t4][i] = yy;
-          dz4[t4][i] = ok ? act_grad(a4, yy, two_over_d * e) : 0.f;
+          dz4[t4][i] = act_grad(a4, yy, two_over_d * e);
         }
-      }
-      // categorical accuracy: argmax over features of y and x for this lane's row
-      if (a.want_acc) {
-        float by = -3.402823466e38f, bx = -3.402823466e38f;
-        int iy = 64, ix = 64;
-#pragma unroll
-        for (int t4 = 0; t4 < 2; ++t4)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int f = 16 * t4 + 4 * g + i;   // ascending: strict > keeps the lowest index
-            const bool gy = f < D && y[t4][i] > by, gx = f < D && xv[4 * t4 + i] > bx;
-            by = gy ? y[t4][i] : by;
-            iy = gy ? f : iy;
-            bx = gx ? xv[4 * t4 + i] : bx;
-            ix = gx ? f : ix;
-          }
-        // the row's four lane groups: lanes c, c+16, c+32, c+48
-        amax_merge(by, iy, xor16(by, lane), xor16i(iy, lane));
-        amax_merge(bx, ix, xor16(bx, lane), xor16i(ix, lane));
-        amax_merge(by, iy, xor32(by, lane), xor32i(iy, lane));
-        amax_merge(bx, ix, xor32(bx, lane), xor32i(ix, lane));
-        corr += (g == 0 && row_ok && iy == ix) ? 1.f : 0.f;
       }
       // backward: dz3 = act3'(h3) * (W4 dz4^T), dz2 = act2'(h2) * (W3 dz3^T),
       //           dz1 = act1'(h1) * (W2 dz2^T + l1 sign(h1))   (Keras L1 activity regulariser)
@@ -367,12 +355,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       for (int s = 0; s < KSX; ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
       f32x4 dz3, dz2, dz1;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dz3[i] = (4 * g + i < n3) ? act_grad(a3, h3[i], acc3[i]) : 0.f;
+      for (int i = 0; i < 4; ++i) dz3[i] = fm(4 * g + i < n3, act_grad(a3, h3[i], acc3[i]));
       f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) acc2 = mfma4(S.w[G3 + s * 64 + lane], dz3[s], acc2);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dz2[i] = (4 * g + i < n2) ? act_grad(a2, h2[i], acc2[i]) : 0.f;
+      for (int i = 0; i < 4; ++i) dz2[i] = fm(4 * g + i < n2, act_grad(a2, h2[i], acc2[i]));
       f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) acc1 = mfma4(S.w[G2 + s * 64 + lane], dz2[s], acc1);
@@ -380,9 +368,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       for (int i = 0; i < 4; ++i) {
         const float h = h1[i];
         const float sgn = h != 0.f ? __builtin_copysignf(1.0f, h) : 0.f;
-        dz1[i] = (4 * g + i < n1 && row_ok) ? act_grad(a1, h, fmaf(a.l1, sgn, acc1[i])) : 0.f;
+        dz1[i] = fm(4 * g + i < n1, act_grad(a1, h, fmaf(l1r, sgn, acc1[i])));
       }
-      // rows -> LDS [row][feature] for the weight-gradient contraction (16-byte stores)
+      // rows -> LDS [row][feature] for the weight-gradient contraction and the accuracy (16-byte stores)
       const int r = row_l;
       st4(S.x + r * XS + 4 * g, f32x4{xv[0], xv[1], xv[2], xv[3]});
       st4(S.x + r * XS + 16 + 4 * g, f32x4{xv[4], xv[5], xv[6], xv[7]});
@@ -394,6 +382,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       st4(S.dz3 + r * HS + 4 * g, dz3);
       st4(S.dz2 + r * HS + 4 * g, dz2);
       st4(S.dz1 + r * HS + 4 * g, dz1);
+      if (a.want_acc) {
+        st4(S.y + r * XS + 4 * g, y[0]);
+        st4(S.y + r * XS + 16 + 4 * g, y[1]);
+      }
     }
     mark(0);
     lds_barrier();
@@ -415,8 +407,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
         for (int s4 = 0; s4 < NS; ++s4) {
           const int r = 4 * s4 + g;   // rows in [B, 4*NS) hold zero gradients
-          const float x0 = T.ones ? 1.f : av[r * T.as];
-          part[s4 % CH] = mfma4(x0, dv[r * T.ds], part[s4 % CH]);
+          part[s4 % CH] = mfma4(av[r * T.as], dv[r * T.ds], part[s4 % CH]);
         }
 #pragma unroll
         for (int c4 = 0; c4 < CH; ++c4) acc += part[c4];
@@ -426,12 +417,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         int s4 = 0;
         for (; s4 + 1 < ns; s4 += 2) {
           const int r = 4 * s4 + g;
-          acc = mfma4(T.ones ? 1.f : av[r * T.as], dv[r * T.ds], acc);
-          acc2 = mfma4(T.ones ? 1.f : av[(r + 4) * T.as], dv[(r + 4) * T.ds], acc2);
+          acc = mfma4(av[r * T.as], dv[r * T.ds], acc);
+          acc2 = mfma4(av[(r + 4) * T.as], dv[(r + 4) * T.ds], acc2);
         }
         if (s4 < ns) {
           const int r = 4 * s4 + g;
-          acc = mfma4(T.ones ? 1.f : av[r * T.as], dv[r * T.ds], acc);
+          acc = mfma4(av[r * T.as], dv[r * T.ds], acc);
         }
         acc += acc2;
       }
@@ -443,9 +434,26 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         mo[i] = mm;
         vo[i] = vv;
         wo[i] -= lr_t * mm * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv) + a.eps);   // v_sqrt / v_rcp, ~1 ulp
-        if (fpos[i] >= 0) S.w[fpos[i]] = wo[i];
-        if (bpos[i] >= 0) S.w[bpos[i]] = wo[i];
+        S.w[fpos[i]] = wo[i];
+        S.w[bpos[i]] = wo[i];
       }
+    } else if (a.want_acc && t - 6 * 64 < B) {
+      // categorical accuracy (waves 6-7, one row per lane): argmax of y and x, ties -> lowest index
+      const int r = t - 6 * 64;
+      const float* yr = S.y + r * XS;
+      const float* xq = S.x + r * XS;
+      float by = yr[0], bx = xq[0];
+      int iy = 0, ix = 0;
+#pragma unroll
+      for (int f = 1; f < KD; ++f) {   // branch-free selects
+        const float yv = yr[f], xw = xq[f];
+        const bool gy = f < D && yv > by, gx = f < D && xw > bx;
+        by = gy ? yv : by;
+        iy = gy ? f : iy;
+        bx = gx ? xw : bx;
+        ix = gx ? f : ix;
+      }
+      corr += iy == ix ? 1.f : 0.f;
     }
     mark(2);
     lds_barrier();
@@ -507,8 +515,6 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
            dims[3], acts[0], acts[1], acts[2], acts[3], l1, lr, beta1, beta2, eps, gscale, want_acc, prof,
            xmodel, lrs};
   const bool ref = acts[0] == ACT_TANH && acts[1] == ACT_RELU && acts[2] == ACT_TANH && acts[3] == ACT_RELU;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   void (*k)(MBArgs) = nullptr;
   size_t lds = 0;
   if (B <= MB_SMALL) {
@@ -516,8 +522,8 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
     k = ae_minibatch_kernel<32, 0, -1>;   // any shape / activations
     if (ref && dims[0] <= 18) k = B == 32 ? ae_minibatch_kernel<18, 32, PACK_REF> : ae_minibatch_kernel<18, 0, PACK_REF>;
     else if (ref) k = B == 32 ? ae_minibatch_kernel<32, 32, PACK_REF> : ae_minibatch_kernel<32, 0, PACK_REF>;
-    // a fleet larger than one model per CU: the 128-VGPR build puts two models on each CU
-    if (ref && dims[0] <= 18 && B == 32 && nmodels > cus) k = ae_minibatch_kernel<18, 32, PACK_REF, 4>;
+    // (a 128-VGPR two-models-per-CU build measured no faster for fleets beyond the CU count:
+    // 3.92 vs 3.96 G rows/s at 1024 / 256 models, profiles/r02)
   } else {
     // cardata-v3's fit(batch_size=100) and anything up to 128 rows: one workgroup per CU
     lds = sizeof(Smem<MB_LARGE>);
