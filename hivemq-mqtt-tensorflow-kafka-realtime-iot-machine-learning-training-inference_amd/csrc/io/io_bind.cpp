@@ -7,6 +7,7 @@
 #include <cstring>
 
 #include "avro.h"
+#include "feed.h"
 #include "h5.h"
 #include "kafka.h"
 #include "mqtt.h"
@@ -379,6 +380,82 @@ PYBIND11_MODULE(_io, m) {
              return c.committed(g, t, p);
            })
       .def_property_readonly("bytes_received", &kafka::Client::bytes_received);
+
+  // native ingest feed: worker threads decode Kafka records straight into caller slabs
+  m.def("label_code", [](const py::bytes& b) {
+    std::string_view s = b;
+    return (int)feed::label_code(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+  });
+  py::class_<feed::Feed>(m, "KafkaFeed")
+      .def(py::init([](const std::string& bootstrap, const std::string& client_id, const std::string& mech,
+                       const std::string& user, const std::string& pw, int timeout_ms, const py::list& fields,
+                       std::vector<int> feature_fields, int label_field, int keep_label, bool framing,
+                       int32_t max_bytes, int32_t max_wait_ms, int workers, double idle_timeout_s,
+                       const std::vector<std::tuple<std::string, int, int64_t, int64_t>>& parts) {
+             kafka::ClientConfig c;
+             c.client_id = client_id;
+             c.sasl_mechanism = mech;
+             c.sasl_username = user;
+             c.sasl_password = pw;
+             c.timeout_ms = timeout_ms;
+             feed::FeedConfig fc;
+             fc.feature_fields = std::move(feature_fields);
+             fc.label_field = label_field;
+             fc.keep_label = keep_label;
+             fc.framing = framing;
+             fc.max_bytes = max_bytes;
+             fc.max_wait_ms = max_wait_ms;
+             fc.workers = workers;
+             fc.idle_timeout_s = idle_timeout_s;
+             std::vector<feed::PartSpec> ps;
+             for (const auto& t : parts) ps.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t)});
+             return new feed::Feed(bootstrap, c, fields_from_py(fields), fc, ps);
+           }),
+           py::arg("bootstrap"), py::arg("client_id"), py::arg("sasl_mechanism"), py::arg("sasl_username"),
+           py::arg("sasl_password"), py::arg("timeout_ms"), py::arg("fields"), py::arg("feature_fields"),
+           py::arg("label_field"), py::arg("keep_label"), py::arg("framing"), py::arg("max_bytes"),
+           py::arg("max_wait_ms"), py::arg("workers"), py::arg("idle_timeout_s"), py::arg("parts"))
+      .def("start",
+           [](feed::Feed& f, const std::vector<uint64_t>& slabs, int64_t cap) {
+             std::vector<uintptr_t> v(slabs.begin(), slabs.end());
+             f.start(v, cap);
+           },
+           py::arg("slabs"), py::arg("cap_rows"))
+      .def("pop",
+           [](feed::Feed& f, int timeout_ms) {
+             int slab = -1;
+             int64_t rows = 0;
+             int r;
+             {
+               py::gil_scoped_release rel;
+               r = f.pop(slab, rows, timeout_ms);
+             }
+             return py::make_tuple(r, slab, rows);
+           },
+           py::arg("timeout_ms") = -1)
+      .def("recycle", &feed::Feed::recycle, py::arg("slab"))
+      .def("stop",
+           [](feed::Feed& f) {
+             py::gil_scoped_release rel;
+             f.stop();
+           })
+      .def("positions", &feed::Feed::positions)
+      .def_property_readonly("features", &feed::Feed::features)
+      .def("stats", [](const feed::Feed& f) {
+        const feed::Stats s = f.stats();
+        py::dict d;
+        d["records"] = s.records;
+        d["rows"] = s.rows;
+        d["dropped"] = s.dropped;
+        d["errors"] = s.errors;
+        d["bytes"] = s.bytes;
+        d["fetches"] = s.fetches;
+        d["slabs"] = s.slabs;
+        d["fetch_s"] = s.fetch_s;
+        d["decode_s"] = s.decode_s;
+        d["wait_slab_s"] = s.wait_slab_s;
+        return d;
+      });
 
   py::class_<kafka::Broker>(m, "KafkaBroker")
       .def(py::init([](int port, const std::string& user, const std::string& pw, int64_t retention) {

@@ -6,6 +6,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -138,12 +139,14 @@ struct R {
     if (n_ > (int32_t)(n - i)) throw Error("kafka: implausible array length");
     return n_;
   }
-  int64_t varlong() {
-    int64_t v;
-    const size_t k = avro::read_varlong(p + i, n - i, &v);
-    if (!k) throw Error("kafka: bad varint");
-    i += k;
-    return v;
+  int64_t varlong() {   // zigzag varint, inline (hot in the record-set walk)
+    uint64_t v = 0;
+    for (int shift = 0; shift < 70 && i < n; shift += 7) {
+      const uint8_t b = p[i++];
+      v |= (uint64_t)(b & 0x7f) << shift;
+      if (!(b & 0x80)) return (int64_t)((v >> 1) ^ (~(v & 1) + 1));
+    }
+    throw Error("kafka: bad varint");
   }
 };
 
@@ -164,22 +167,26 @@ enum Err : int16_t {
 // record batch v2
 // ---------------------------------------------------------------------------
 std::string encode_record_batch(int64_t base_offset, const std::vector<Record>& recs) {
-  if (recs.empty()) return std::string();
-  const int64_t first_ts = recs.front().timestamp;
+  return encode_record_batch(base_offset, recs.data(), recs.size());
+}
+
+std::string encode_record_batch(int64_t base_offset, const Record* recs, size_t n) {
+  if (n == 0) return std::string();
+  const int64_t first_ts = recs[0].timestamp;
   int64_t max_ts = first_ts;
   std::string body;  // from attributes to the end (CRC scope)
   W h;
   h.i16(0);                                   // attributes: no compression
-  h.i32((int32_t)(recs.size() - 1));          // lastOffsetDelta
+  h.i32((int32_t)(n - 1));                    // lastOffsetDelta
   h.i64(first_ts);
-  for (const auto& r : recs) max_ts = std::max(max_ts, r.timestamp);
+  for (size_t k = 0; k < n; ++k) max_ts = std::max(max_ts, recs[k].timestamp);
   h.i64(max_ts);
   h.i64(-1);                                  // producerId
   h.i16(-1);                                  // producerEpoch
   h.i32(-1);                                  // baseSequence
-  h.i32((int32_t)recs.size());
+  h.i32((int32_t)n);
   body = h.s;
-  for (size_t k = 0; k < recs.size(); ++k) {
+  for (size_t k = 0; k < n; ++k) {
     const Record& r = recs[k];
     std::string rec;
     rec.push_back(0);                         // attributes
@@ -263,6 +270,65 @@ void decode_record_batches(const uint8_t* p, size_t n, int64_t min_offset, Fetch
   }
 }
 
+bool RecordSetCursor::next(RecordView& out) {
+  for (;;) {
+    while (left_ > 0) {
+      --left_;
+      R b{bp_, bn_};
+      b.i = bi_;
+      const int64_t len = b.varlong();
+      if (len < 0 || (size_t)len > b.n - b.i) throw Error("kafka: bad record length");
+      R r{b.p + b.i, (size_t)len};
+      bi_ = b.i + (size_t)len;
+      r.i8();
+      const int64_t ts_delta = r.varlong();
+      const int64_t off_delta = r.varlong();
+      const int64_t klen = r.varlong();
+      const uint8_t* key = nullptr;
+      if (klen >= 0) {
+        r.need((size_t)klen);
+        key = r.p + r.i;
+        r.i += (size_t)klen;
+      }
+      const int64_t vlen = r.varlong();
+      if (vlen > 0) r.need((size_t)vlen);
+      if (control_) continue;
+      out.offset = base_ + off_delta;
+      out.timestamp = first_ts_ + ts_delta;
+      out.key = key;
+      out.key_len = klen;
+      out.value = r.p + r.i;
+      out.value_len = vlen > 0 ? vlen : 0;
+      return true;
+    }
+    if (n_ - pos_ < 12) return false;
+    R hdr{p_ + pos_, n_ - pos_};
+    base_ = hdr.i64();
+    const int32_t blen = hdr.i32();
+    if (blen < 0 || (size_t)blen > n_ - pos_ - 12) return false;  // partial trailing batch
+    R b{p_ + pos_ + 12, (size_t)blen};
+    b.i32();  // leader epoch
+    const int8_t magic = b.i8();
+    if (magic != 2) throw Error("kafka: unsupported record batch magic " + std::to_string(magic));
+    const uint32_t crc = (uint32_t)b.u(4);
+    if (crc != crc32c(p_ + pos_ + 12 + b.i, (size_t)blen - b.i)) throw Error("kafka: record batch CRC mismatch");
+    const int16_t attrs = b.i16();
+    if (attrs & 0x7) throw Error("kafka: compressed record batches are not supported");
+    b.i32();
+    first_ts_ = b.i64();
+    b.i64();
+    b.i64();
+    b.i16();
+    b.i32();
+    left_ = b.i32();
+    control_ = attrs & 0x20;
+    bp_ = b.p;
+    bn_ = b.n;
+    bi_ = b.i;
+    pos_ += 12 + (size_t)blen;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // connection
 // ---------------------------------------------------------------------------
@@ -286,6 +352,8 @@ class Connection {
     setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
     int one = 1;
     setsockopt(fd_, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    int sz = 4 << 20;   // multi-megabyte fetch responses in few recv() calls
+    setsockopt(fd_, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
     const int rc = ::connect(fd_, res->ai_addr, res->ai_addrlen);
     freeaddrinfo(res);
     if (rc != 0) {
@@ -384,6 +452,32 @@ std::string Client::call(Connection& c, int16_t api, int16_t ver, const std::str
   if (!resp.empty()) c.recv_all(&resp[0], resp.size());
   bytes_rx_ += (uint64_t)size + 4;
   return resp;
+}
+
+size_t Client::call_into(Connection& c, int16_t api, int16_t ver, const std::string& body, std::string& resp) {
+  W w;
+  w.i32(0);
+  w.i16(api);
+  w.i16(ver);
+  const int32_t corr = corr_++;
+  w.i32(corr);
+  w.str(cfg_.client_id);
+  w.s += body;
+  w.put32(0, (int32_t)(w.s.size() - 4));
+  c.send_all(w.s);
+  char hdr[8];
+  c.recv_all(hdr, 8);
+  const int32_t size = (int32_t)(((uint32_t)(uint8_t)hdr[0] << 24) | ((uint32_t)(uint8_t)hdr[1] << 16) |
+                                 ((uint32_t)(uint8_t)hdr[2] << 8) | (uint8_t)hdr[3]);
+  const int32_t rcorr = (int32_t)(((uint32_t)(uint8_t)hdr[4] << 24) | ((uint32_t)(uint8_t)hdr[5] << 16) |
+                                  ((uint32_t)(uint8_t)hdr[6] << 8) | (uint8_t)hdr[7]);
+  if (size < 4 || size > (1 << 30)) throw Error("kafka: bad response size");
+  if (rcorr != corr) throw Error("kafka: correlation id mismatch");
+  const size_t n = (size_t)size - 4;
+  if (resp.size() < n) resp.resize(n + n / 4);
+  if (n) c.recv_all(&resp[0], n);
+  bytes_rx_ += (uint64_t)size + 4;
+  return n;
 }
 
 Connection& Client::any_conn() {
@@ -547,6 +641,58 @@ FetchResult Client::fetch(const std::string& topic, int partition, int64_t offse
   }
 }
 
+int64_t Client::fetch_raw(const std::string& topic, int partition, int64_t offset, int32_t max_bytes,
+                          int32_t max_wait_ms, std::string& resp, size_t& rec_off, size_t& rec_len) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (int attempt = 0;; ++attempt) {
+    W w;
+    w.i32(-1);
+    w.i32(max_wait_ms);
+    w.i32(1);
+    w.i32(max_bytes);
+    w.i8(0);
+    w.arr(1);
+    w.str(topic);
+    w.arr(1);
+    w.i32(partition);
+    w.i64(offset);
+    w.i32(max_bytes);
+    size_t used = 0;
+    try {
+      used = call_into(conn_for(topic, partition), API_FETCH, 4, w.s, resp);
+    } catch (const Error& e) {
+      if (attempt >= cfg_.max_retries) throw;
+      conns_.clear();
+      any_.reset();
+      refresh_metadata();
+      continue;
+    }
+    R r{reinterpret_cast<const uint8_t*>(resp.data()), used};
+    r.i32();
+    r.arr();
+    r.str();
+    r.arr();
+    r.i32();
+    const int16_t ec = r.i16();
+    const int64_t hwm = r.i64();
+    r.i64();
+    const int32_t naborted = r.i32();
+    for (int32_t k = 0; k < naborted; ++k) {
+      r.i64();
+      r.i64();
+    }
+    if (ec == E_NOT_LEADER && attempt < cfg_.max_retries) {
+      refresh_metadata();
+      continue;
+    }
+    if (ec != E_NONE) throw Error("kafka: Fetch error " + std::to_string(ec), ec);
+    auto rec = r.bytes();
+    rec_off = rec.first ? (size_t)(rec.first - reinterpret_cast<const uint8_t*>(resp.data())) : 0;
+    rec_len = rec.second;
+    return hwm;
+  }
+}
+
 int64_t Client::produce(const std::string& topic, int partition, const std::vector<Record>& recs, int16_t acks) {
   std::lock_guard<std::mutex> g(mu_);
   W w;
@@ -663,6 +809,8 @@ void Broker::accept_loop() {
     }
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    int sz = 4 << 20;
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
     std::lock_guard<std::mutex> g(mu_);
     client_fds_.push_back(fd);
     workers_.emplace_back([this, fd] { serve(fd); });
@@ -675,30 +823,40 @@ void Broker::create_topic(const std::string& name, int partitions) {
   if ((int)t.size() < partitions) t.resize((size_t)partitions);
 }
 
+int64_t Broker::append_locked(Partition& p, const Record* recs, size_t n) {
+  const int64_t base = p.end;
+  for (size_t k = 0; k < n; k += kSegmentRecords) {
+    const size_t m = std::min(kSegmentRecords, n - k);
+    Segment sg;
+    sg.base = p.end;
+    sg.count = (int32_t)m;
+    sg.bytes = std::make_shared<const std::string>(encode_record_batch(p.end, recs + k, m));
+    p.segs.push_back(std::move(sg));
+    p.end += (int64_t)m;
+  }
+  // retention: whole segments, oldest first, while the rest still holds the limit (Kafka
+  // deletes log segments, not records)
+  if (cfg_.retention_records > 0) {
+    size_t drop = 0;
+    while (drop + 1 < p.segs.size() && p.end - (p.segs[drop].base + p.segs[drop].count) >= cfg_.retention_records)
+      ++drop;
+    if (drop) p.segs.erase(p.segs.begin(), p.segs.begin() + (std::ptrdiff_t)drop);
+  }
+  p.start = p.segs.empty() ? p.end : p.segs.front().base;
+  return base;
+}
+
 int64_t Broker::append(const std::string& topic, int partition, const std::vector<Record>& recs) {
   std::lock_guard<std::mutex> g(mu_);
   auto it = topics_.find(topic);
   if (it == topics_.end() || partition < 0 || partition >= (int)it->second.size())
     throw Error("broker: unknown topic/partition", E_UNKNOWN_TOPIC);
-  Partition& p = it->second[(size_t)partition];
-  const int64_t base = p.start + (int64_t)p.log.size();
-  for (size_t k = 0; k < recs.size(); ++k) {
-    Record r = recs[k];
-    r.offset = base + (int64_t)k;
-    p.log.push_back(std::move(r));
-  }
-  if (cfg_.retention_records > 0 && (int64_t)p.log.size() > cfg_.retention_records) {
-    const int64_t drop = (int64_t)p.log.size() - cfg_.retention_records;
-    p.log.erase(p.log.begin(), p.log.begin() + drop);
-    p.start += drop;
-  }
-  return base;
+  return append_locked(it->second[(size_t)partition], recs.data(), recs.size());
 }
 
 int64_t Broker::end_offset(const std::string& topic, int partition) {
   std::lock_guard<std::mutex> g(mu_);
-  const Partition& p = topics_.at(topic).at((size_t)partition);
-  return p.start + (int64_t)p.log.size();
+  return topics_.at(topic).at((size_t)partition).end;
 }
 
 int64_t Broker::start_offset(const std::string& topic, int partition) {
@@ -707,11 +865,124 @@ int64_t Broker::start_offset(const std::string& topic, int partition) {
 }
 
 std::vector<Record> Broker::read(const std::string& topic, int partition, int64_t offset, size_t max_records) {
-  std::lock_guard<std::mutex> g(mu_);
-  const Partition& p = topics_.at(topic).at((size_t)partition);
+  std::vector<std::shared_ptr<const std::string>> segs;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    const Partition& p = topics_.at(topic).at((size_t)partition);
+    for (const Segment& sg : p.segs)
+      if (sg.base + sg.count > offset) segs.push_back(sg.bytes);
+  }
   std::vector<Record> out;
-  for (int64_t o = std::max(offset, p.start); o < p.start + (int64_t)p.log.size() && out.size() < max_records; ++o)
-    out.push_back(p.log[(size_t)(o - p.start)]);
+  for (const auto& sp : segs) {
+    RecordSetCursor cur(reinterpret_cast<const uint8_t*>(sp->data()), sp->size());
+    RecordView v;
+    while (out.size() < max_records && cur.next(v)) {
+      if (v.offset < offset) continue;
+      Record r;
+      r.offset = v.offset;
+      r.timestamp = v.timestamp;
+      r.key_null = v.key_len < 0;
+      if (v.key_len > 0) r.key.assign(reinterpret_cast<const char*>(v.key), (size_t)v.key_len);
+      r.value.assign(reinterpret_cast<const char*>(v.value), (size_t)v.value_len);
+      out.push_back(std::move(r));
+    }
+    if (out.size() >= max_records) break;
+  }
+  return out;
+}
+
+size_t Broker::FetchReply::total() const {
+  size_t t = meta.size();
+  for (const auto& sp : splice) t += sp.second->size();
+  return t;
+}
+
+Broker::FetchReply Broker::handle_fetch(const uint8_t* body, size_t n) {
+  R r{body, n};
+  const uint64_t nth = ++fetches_;
+  r.i32();
+  r.i32();   // max wait: the log is local, every fetch answers at once
+  r.i32();
+  r.i32();
+  r.i8();
+  struct Want {
+    std::string topic;
+    int32_t partition, pmax;
+    int64_t off;
+    int16_t err = E_NONE;
+    int64_t hwm = -1;
+    std::vector<std::shared_ptr<const std::string>> segs;
+  };
+  std::vector<std::pair<std::string, std::vector<Want>>> req;
+  const int32_t nt = r.arr();
+  for (int32_t i = 0; i < nt; ++i) {
+    req.emplace_back(r.str(), std::vector<Want>());
+    const int32_t np = r.arr();
+    for (int32_t k = 0; k < np; ++k) {
+      Want wt;
+      wt.topic = req.back().first;
+      wt.partition = r.i32();
+      wt.off = r.i64();
+      wt.pmax = r.i32();
+      req.back().second.push_back(std::move(wt));
+    }
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);   // only to pick the segments: the copy runs unlocked
+    const int fe = fail_every_.load();
+    for (auto& tp : req)
+      for (Want& wt : tp.second) {
+        auto it = topics_.find(wt.topic);
+        if (fe > 0 && nth % (uint64_t)fe == 0) {
+          ++failures_;
+          wt.err = E_NOT_LEADER;
+          continue;
+        }
+        if (it == topics_.end() || wt.partition < 0 || wt.partition >= (int32_t)it->second.size()) {
+          wt.err = E_UNKNOWN_TOPIC;
+          continue;
+        }
+        const Partition& part = it->second[(size_t)wt.partition];
+        wt.hwm = part.end;
+        if (wt.off < part.start || wt.off > part.end) {
+          wt.err = E_OFFSET_OUT_OF_RANGE;
+          continue;
+        }
+        auto sg = std::upper_bound(part.segs.begin(), part.segs.end(), wt.off,
+                                   [](int64_t o, const Segment& s_) { return o < s_.base + s_.count; });
+        size_t bytes = 0;
+        for (; sg != part.segs.end() && (bytes == 0 || bytes < (size_t)std::max(wt.pmax, 0)); ++sg) {
+          wt.segs.push_back(sg->bytes);
+          bytes += sg->bytes->size();
+        }
+      }
+  }
+  FetchReply out;
+  W w;
+  w.i32(0);
+  w.arr(nt);
+  for (auto& tp : req) {
+    w.str(tp.first);
+    w.arr((int32_t)tp.second.size());
+    for (Want& wt : tp.second) {
+      w.i32(wt.partition);
+      w.i16(wt.err);
+      w.i64(wt.hwm);
+      w.i64(wt.hwm);
+      w.i32(0);  // no aborted transactions
+      if (wt.err != E_NONE) {
+        w.i32(-1);
+        continue;
+      }
+      size_t total = 0;
+      for (const auto& sp : wt.segs) total += sp->size();
+      w.i32((int32_t)total);
+      for (auto& sp : wt.segs) out.splice.emplace_back(w.s.size(), std::move(sp));
+    }
+  }
+  const int dm = delay_ms_.load();
+  if (dm > 0) std::this_thread::sleep_for(std::chrono::milliseconds(dm));
+  out.meta = std::move(w.s);
   return out;
 }
 
@@ -739,25 +1010,68 @@ void Broker::serve(int fd) {
       }
       std::string resp_body;
       int32_t corr = 0;
+      FetchReply fr;
+      bool is_fetch = false;
       try {
         R r{reinterpret_cast<const uint8_t*>(buf.data()), buf.size()};
         const int16_t api = r.i16();
         const int16_t ver = r.i16();
         corr = r.i32();
         r.str();  // client id
-        resp_body = handle(api, ver, r.p + r.i, r.n - r.i, authed, handshaken);
+        is_fetch = api == API_FETCH && authed;
+        if (is_fetch) fr = handle_fetch(r.p + r.i, r.n - r.i);
+        else resp_body = handle(api, ver, r.p + r.i, r.n - r.i, authed, handshaken);
       } catch (const std::exception&) {
         goto done;  // malformed request: drop the connection (like a real broker)
+      }
+      if (is_fetch) {
+        // zero-copy reply: header + framing + segment bytes gathered by the kernel
+        W h;
+        h.i32((int32_t)(fr.total() + 4));
+        h.i32(corr);
+        std::vector<iovec> iov;
+        iov.push_back({&h.s[0], h.s.size()});
+        size_t at = 0;
+        for (const auto& sp : fr.splice) {
+          if (sp.first > at) iov.push_back({&fr.meta[at], sp.first - at});
+          iov.push_back({const_cast<char*>(sp.second->data()), sp.second->size()});
+          at = sp.first;
+        }
+        if (fr.meta.size() > at) iov.push_back({&fr.meta[at], fr.meta.size() - at});
+        size_t k0 = 0;
+        while (k0 < iov.size()) {
+          msghdr mh{};
+          mh.msg_iov = &iov[k0];
+          mh.msg_iovlen = std::min<size_t>(iov.size() - k0, 512);
+          ssize_t k = ::sendmsg(fd, &mh, MSG_NOSIGNAL);
+          if (k <= 0) goto done;
+          while (k > 0 && k0 < iov.size()) {   // advance over what was sent
+            if ((size_t)k >= iov[k0].iov_len) {
+              k -= (ssize_t)iov[k0].iov_len;
+              ++k0;
+            } else {
+              iov[k0].iov_base = static_cast<char*>(iov[k0].iov_base) + k;
+              iov[k0].iov_len -= (size_t)k;
+              k = 0;
+            }
+          }
+        }
+        continue;
       }
       W w;
       w.i32((int32_t)(resp_body.size() + 4));
       w.i32(corr);
-      w.s += resp_body;
-      size_t off = 0;
-      while (off < w.s.size()) {
-        const ssize_t k = ::send(fd, w.s.data() + off, w.s.size() - off, MSG_NOSIGNAL);
-        if (k <= 0) goto done;
-        off += (size_t)k;
+      // header, then the body straight from its buffer (no concatenated copy of a
+      // multi-megabyte fetch response)
+      for (int part = 0; part < 2; ++part) {
+        const std::string& out = part == 0 ? w.s : resp_body;
+        size_t off = 0;
+        while (off < out.size()) {
+          const ssize_t k = ::send(fd, out.data() + off, out.size() - off,
+                                   MSG_NOSIGNAL | (part == 0 && !resp_body.empty() ? MSG_MORE : 0));
+          if (k <= 0) goto done;
+          off += (size_t)k;
+        }
       }
     }
   }
@@ -810,6 +1124,19 @@ std::string Broker::handle(int16_t api, int16_t ver, const uint8_t* body, size_t
     return w.s;
   }
   if (!authed) throw Error("broker: unauthenticated request");
+  if (api == API_FETCH) {   // served by handle_fetch + sendmsg in serve(); kept for completeness
+    FetchReply fr = handle_fetch(body, n);
+    std::string flat;
+    flat.reserve(fr.total());
+    size_t at = 0;
+    for (const auto& sp : fr.splice) {
+      flat.append(fr.meta, at, sp.first - at);
+      flat += *sp.second;
+      at = sp.first;
+    }
+    flat.append(fr.meta, at, std::string::npos);
+    return flat;
+  }
   std::lock_guard<std::mutex> g(mu_);
   switch (api) {
     case API_METADATA: {
@@ -871,82 +1198,9 @@ std::string Broker::handle(int16_t api, int16_t ver, const uint8_t* body, size_t
           const Partition& part = it->second[(size_t)p];
           w.i16(E_NONE);
           w.i64(-1);
-          w.i64(t == -2 ? part.start : part.start + (int64_t)part.log.size());
+          w.i64(t == -2 ? part.start : part.end);
         }
       }
-      return w.s;
-    }
-    case API_FETCH: {
-      const uint64_t nth = ++fetches_;
-      r.i32();
-      const int32_t max_wait = r.i32();
-      r.i32();
-      r.i32();
-      r.i8();
-      const int32_t nt = r.arr();
-      w.i32(0);
-      w.arr(nt);
-      for (int32_t i = 0; i < nt; ++i) {
-        const std::string name = r.str();
-        const int32_t np = r.arr();
-        w.str(name);
-        w.arr(np);
-        for (int32_t k = 0; k < np; ++k) {
-          const int32_t p = r.i32();
-          const int64_t off = r.i64();
-          const int32_t pmax = r.i32();
-          w.i32(p);
-          auto it = topics_.find(name);
-          const int fe = fail_every_.load();
-          if (fe > 0 && nth % (uint64_t)fe == 0) {
-            ++failures_;
-            w.i16(E_NOT_LEADER);
-            w.i64(-1);
-            w.i64(-1);
-            w.i32(0);
-            w.i32(-1);
-            continue;
-          }
-          if (it == topics_.end() || p < 0 || p >= (int32_t)it->second.size()) {
-            w.i16(E_UNKNOWN_TOPIC);
-            w.i64(-1);
-            w.i64(-1);
-            w.i32(0);
-            w.i32(-1);
-            continue;
-          }
-          const Partition& part = it->second[(size_t)p];
-          const int64_t end = part.start + (int64_t)part.log.size();
-          if (off < part.start || off > end) {
-            w.i16(E_OFFSET_OUT_OF_RANGE);
-            w.i64(end);
-            w.i64(end);
-            w.i32(0);
-            w.i32(-1);
-            continue;
-          }
-          std::string batches;
-          int64_t o = off;
-          while (o < end && (batches.empty() || (int64_t)batches.size() < pmax)) {
-            std::vector<Record> chunk;
-            size_t bytes = 0;
-            while (o < end && chunk.size() < 1024 && (batches.size() + bytes < (size_t)pmax || chunk.empty())) {
-              const Record& src = part.log[(size_t)(o - part.start)];
-              bytes += src.value.size() + src.key.size() + 16;
-              chunk.push_back(src);
-              ++o;
-            }
-            batches += encode_record_batch(chunk.front().offset, chunk);
-          }
-          w.i16(E_NONE);
-          w.i64(end);
-          w.i64(end);
-          w.i32(0);  // no aborted transactions
-          w.bytes(batches);
-        }
-      }
-      const int dm = delay_ms_.load();
-      if (dm > 0 || (max_wait > 0 && false)) std::this_thread::sleep_for(std::chrono::milliseconds(dm));
       return w.s;
     }
     case API_PRODUCE: {
@@ -974,23 +1228,16 @@ std::string Broker::handle(int16_t api, int16_t ver, const uint8_t* body, size_t
             w.i64(-1);
             continue;
           }
-          Partition& part = it->second[(size_t)p];
-          const int64_t base = part.start + (int64_t)part.log.size();
+          std::vector<Record> recs_in(tmp.size());
           for (size_t q = 0; q < tmp.size(); ++q) {
-            Record rec;
-            rec.offset = base + (int64_t)q;
+            Record& rec = recs_in[q];
             rec.timestamp = tmp.timestamps[q];
             rec.key = tmp.keys[q];
             rec.key_null = tmp.keys[q].empty();
             rec.value.assign(tmp.values.data() + tmp.value_offsets[q],
                              (size_t)(tmp.value_offsets[q + 1] - tmp.value_offsets[q]));
-            part.log.push_back(std::move(rec));
           }
-          if (cfg_.retention_records > 0 && (int64_t)part.log.size() > cfg_.retention_records) {
-            const int64_t drop = (int64_t)part.log.size() - cfg_.retention_records;
-            part.log.erase(part.log.begin(), part.log.begin() + drop);
-            part.start += drop;
-          }
+          const int64_t base = append_locked(it->second[(size_t)p], recs_in.data(), recs_in.size());
           w.i16(E_NONE);
           w.i64(base);
           w.i64(-1);

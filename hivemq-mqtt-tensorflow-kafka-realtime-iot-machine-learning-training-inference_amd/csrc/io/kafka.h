@@ -60,7 +60,33 @@ struct FetchResult {
 
 // record batch v2 codec
 std::string encode_record_batch(int64_t base_offset, const std::vector<Record>& recs);
+std::string encode_record_batch(int64_t base_offset, const Record* recs, size_t n);
 void decode_record_batches(const uint8_t* p, size_t n, int64_t min_offset, FetchResult& out);
+
+// Zero-copy iteration over the records of a fetched record set (v2 batches, CRC
+// checked once per batch): values and keys are pointers into the caller's buffer.
+struct RecordView {
+  int64_t offset = 0, timestamp = 0;
+  const uint8_t* key = nullptr;
+  int64_t key_len = -1;   // -1 = null key
+  const uint8_t* value = nullptr;
+  int64_t value_len = 0;
+};
+class RecordSetCursor {
+ public:
+  RecordSetCursor() = default;
+  RecordSetCursor(const uint8_t* p, size_t n) : p_(p), n_(n) {}
+  // next data record (control batches / records skipped); false at the end of the set
+  bool next(RecordView& out);
+ private:
+  const uint8_t* p_ = nullptr;
+  size_t n_ = 0, pos_ = 0;      // next batch header
+  const uint8_t* bp_ = nullptr;  // current batch records area
+  size_t bn_ = 0, bi_ = 0;
+  int32_t left_ = 0;
+  int64_t base_ = 0, first_ts_ = 0;
+  bool control_ = false;
+};
 
 struct ClientConfig {
   std::string client_id = "streamml";
@@ -81,6 +107,11 @@ class Client {
   int64_t list_offset(const std::string& topic, int partition, int64_t time);  // -2 earliest, -1 latest
   FetchResult fetch(const std::string& topic, int partition, int64_t offset, int32_t max_bytes = 1 << 20,
                     int32_t max_wait_ms = 100);
+  // Fetch without materialising records: `resp` keeps the whole response; the record set
+  // is resp[rec_off, rec_off + rec_len) (iterate it with RecordSetCursor).  Returns the
+  // partition's high watermark.
+  int64_t fetch_raw(const std::string& topic, int partition, int64_t offset, int32_t max_bytes,
+                    int32_t max_wait_ms, std::string& resp, size_t& rec_off, size_t& rec_len);
   int64_t produce(const std::string& topic, int partition, const std::vector<Record>& recs, int16_t acks = 1);
   void commit(const std::string& group, const std::string& topic, int partition, int64_t offset);
   int64_t committed(const std::string& group, const std::string& topic, int partition);
@@ -108,6 +139,9 @@ class Client {
   Connection& any_conn();
   std::unique_ptr<Connection> open(const BrokerAddr& a);
   std::string call(Connection& c, int16_t api, int16_t ver, const std::string& body);
+  // same, into a caller buffer that is only ever grown (no per-call allocation / zero-fill);
+  // returns the response length
+  size_t call_into(Connection& c, int16_t api, int16_t ver, const std::string& body, std::string& resp);
 };
 
 struct BrokerConfig {
@@ -138,10 +172,31 @@ class Broker {
   void stop();
 
  private:
-  struct Partition {
-    std::vector<Record> log;
-    int64_t start = 0;  // offset of log[0]
+  // The log is kept the way Kafka keeps it: as encoded record batches, served to
+  // fetches verbatim (a fetch copies whole batches; the consumer skips the records
+  // below its offset).  Segments are immutable and shared, so a fetch assembles its
+  // response outside the broker lock.
+  static constexpr size_t kSegmentRecords = 1024;
+  struct Segment {
+    int64_t base = 0;
+    int32_t count = 0;
+    std::shared_ptr<const std::string> bytes;
   };
+  struct Partition {
+    std::vector<Segment> segs;
+    int64_t start = 0;  // offset of the first retained record
+    int64_t end = 0;    // next offset to assign
+  };
+  int64_t append_locked(Partition& p, const Record* recs, size_t n);
+  // A fetch reply: the response framing in `meta`, with the (shared, immutable) segment
+  // bytes of each partition spliced in at byte offset `at` of `meta` -- sent with
+  // sendmsg() straight from the log segments, never concatenated.
+  struct FetchReply {
+    std::string meta;
+    std::vector<std::pair<size_t, std::shared_ptr<const std::string>>> splice;
+    size_t total() const;
+  };
+  FetchReply handle_fetch(const uint8_t* body, size_t n);
   BrokerConfig cfg_;
   int listen_fd_ = -1;
   int port_ = 0;

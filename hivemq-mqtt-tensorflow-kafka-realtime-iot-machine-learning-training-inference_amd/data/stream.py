@@ -243,9 +243,12 @@ def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optio
           eof: bool = True, config: Optional[Sequence[str]] = None, max_bytes: int = 4 << 20,
           framing: bool = True, commit: bool = False, resume: bool = False,
           idle_timeout_s: Optional[float] = None, workers: int = 1, native: bool = False) -> Stream:
-    """Kafka topic(s) of (Confluent-framed) Avro car records -> raw feature chunks."""
-    if native:
-        raise NotImplementedError("native ingest feed not built yet")
+    """Kafka topic(s) of (Confluent-framed) Avro car records -> raw feature chunks.
+
+    ``native=True``: the partition-parallel C++ feed (:mod:`streamml.kafka.feed`) decodes
+    records straight into page-locked slabs; the Stream still iterates host chunks, and a
+    GPU ``fit`` picks up ``stream.native_feed`` to stream slabs to the device with no
+    Python-side row handling (``filter_normal(device=True)`` becomes a decode-time filter)."""
     from ..kafka import KafkaDataset
     from .avro import AvroCodec
 
@@ -257,6 +260,22 @@ def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optio
             raise ValueError(f"schema has no field for feature {name}")
         cols.append(match[0])
     label_field = next((f for f in codec.text_fields if canonical(f) == LABEL), None)
+
+    if native:
+        from ..kafka.feed import NativeFeed
+        names = [f.name for f in codec.fields]
+        feature_idx = [names.index(codec.numeric_fields[c]) for c in cols]
+        label_idx = names.index(label_field) if label_field is not None else -1
+        spec = NativeFeed(servers, topics, codec, feature_idx, label_idx, config=config, workers=workers,
+                          max_bytes=max_bytes, eof=eof, framing=framing, group=group, resume=resume,
+                          commit=commit, idle_timeout_s=idle_timeout_s)
+
+        def native_gen():
+            for rows, labs in spec.host_chunks():
+                yield Chunk(rows, labs)
+        out = Stream(native_gen)
+        out.native_feed = spec
+        return out
 
     def gen():
         # label codes and str keys come straight from C++ (no per-record Python objects

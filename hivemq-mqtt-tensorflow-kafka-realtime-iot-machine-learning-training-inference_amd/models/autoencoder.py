@@ -298,11 +298,13 @@ class Autoencoder:
         """Device chunks of raw rows from a Stream (no host re-batching): the pinned ring
         moves whole chunks, a deferred ``filter_normal(device=True)`` runs as K8 on them."""
         from ..data.loader import DeviceLoader
-        feed = getattr(stream, "native_feed", None)
-        if feed is not None:
-            yield from feed.device_chunks(self.device)
-            return
         deferred = getattr(stream, "device_filter", None)
+        base, keep = deferred if deferred is not None else (stream, None)
+        feed = getattr(base, "native_feed", None)
+        if feed is not None and feed.features == self.spec.input_dim:
+            # native Kafka feed: decode-time label filter, slabs straight to the device
+            yield from feed.device_chunks(self.device, keep_label=keep)
+            return
         if deferred is not None:
             parent, keep = deferred
             yield from DeviceLoader(parent, self.device, max_rows=chunk_rows, features=self.spec.input_dim,

@@ -91,3 +91,52 @@ def test_fit_auto_engine_picks_persistent(cuda_device, monkeypatch):
     assert calls, "fit(batch_size=100) did not use the persistent kernel"
     with pytest.raises(ValueError):
         m.fit(np.zeros((1000, 18), np.float32), batch_size=256, verbose=0, engine="persistent")
+
+
+def test_fit_native_kafka_feed_matches_torch(cuda_device):
+    """Kafka (in-process broker) -> native C++ feed (decode-time label filter, pinned slabs,
+    H2D) -> persistent-kernel fit: the same Keras trajectory as the fp32 oracle on the
+    filtered rows (one partition, so the row order is the log order)."""
+    from streamml.data.avro import AvroCodec
+    from streamml.data.produce import encode_chunk
+    from streamml.kafka import fake_broker
+    b = fake_broker("fit-native-gpu")
+    b.create_topic("SENSOR_DATA_S_AVRO", 1)
+    codec = AvroCodec("cardata-v1")
+    src = S.synthetic(25_000, chunk=5_000, seed=11, failure_rate=0.05)
+    for c in src:
+        buf, offs = encode_chunk(codec, c.x, c.label)
+        b.append_buffer("SENSOR_DATA_S_AVRO", 0, buf, offs)
+    st = S.kafka("fake://fit-native-gpu", ["SENSOR_DATA_S_AVRO:0:0"], native=True)
+    B, take = 100, 150
+    m = Autoencoder(device=cuda_device, input_normalizer="cardata", seed=2)
+    w0 = m.get_weights()
+    m.compile()
+    m.fit(st.filter_normal(device=True), epochs=1, batch_size=B, steps_per_epoch=take, verbose=0,
+          engine="persistent")
+    kept = src.filter_normal().collect().x
+    sc, sh = normalize_affine()
+    ref = _oracle(w0, (kept * sc + sh).astype(np.float32), B, take)
+    _compare(m, ref, take)
+    assert st.native_feed.last_stats["records"] > 0
+
+
+def test_native_device_chunks_equal_host_rows(cuda_device):
+    from streamml.data.avro import AvroCodec
+    from streamml.data.produce import encode_chunk
+    from streamml.kafka import fake_broker
+    b = fake_broker("chunks-native-gpu")
+    b.create_topic("T", 3)
+    codec = AvroCodec("cardata-v1")
+    for i, c in enumerate(S.synthetic(40_000, chunk=4_000, seed=5, failure_rate=0.1)):
+        buf, offs = encode_chunk(codec, c.x, c.label)
+        b.append_buffer("T", i % 3, buf, offs)
+    specs = [f"T:{p}:0" for p in range(3)]
+    feed = S.kafka("fake://chunks-native-gpu", specs, workers=3, native=True).native_feed
+    dev = torch.cat([x.clone() for x in feed.device_chunks(cuda_device, keep_label=0, slab_rows=4096)])
+    host = np.concatenate([r for r, _ in feed.host_chunks(keep_label=0)])
+    got = dev.cpu().numpy()
+    key = lambda x: x[np.lexsort(x.T[::-1])]
+    assert got.shape == host.shape
+    np.testing.assert_array_equal(key(got), key(host))
+    assert feed.last_stats["dropped"] > 0

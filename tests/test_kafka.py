@@ -83,7 +83,8 @@ def test_eof_bounded_and_reiterable(broker):
 
 def test_fault_injection_retries(broker):
     c = KafkaClient(broker.address)
-    c.produce("t", 0, [b"x"] * 50)
+    for _ in range(50):   # one record batch (log segment) each: a fetch returns whole batches
+        c.produce("t", 0, [b"x"])
     broker.set_faults(fail_every=2)
     ds = KafkaDataset(["t:0:0"], servers=broker.address, max_bytes=40)
     assert len(list(ds.messages())) == 50
