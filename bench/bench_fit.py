@@ -85,6 +85,13 @@ def stream_e2e(device, rows: int = 2_000_000, batch: int = 100, partitions: int 
         kept += int(xd.size(0))
     torch.cuda.synchronize()
     out["ingest_h2d_rows_per_s"] = n / (time.perf_counter() - t0)
+    feed = getattr(src, "native_feed", None)
+    if feed is not None:
+        st = feed.last_stats
+        out["feed_stats"] = st
+        w = max(st.get("workers", 1), 1)
+        out["per_worker_fetch_rows_per_s"] = st["records"] / max(st["fetch_s"] / w, 1e-9) / w
+        out["per_worker_decode_rows_per_s"] = st["records"] / max(st["decode_s"] / w, 1e-9) / w
     # stage 3: the training kernel alone on the same number of rows (device resident)
     out["train_only"] = fit_array(device, rows=max(kept, batch * 300), batch=batch)
     # end to end
@@ -104,7 +111,7 @@ def main():
     ap.add_argument("--rows", type=int, default=2_000_000)
     ap.add_argument("--batch", type=int, default=100)
     ap.add_argument("--partitions", type=int, default=8)
-    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--workers", default="8", help="comma-separated feed worker counts to sweep")
     ap.add_argument("--python-feed", action="store_true", help="chunk-by-chunk Python Kafka path")
     ap.add_argument("--skip-stream", action="store_true")
     args = ap.parse_args()
@@ -114,8 +121,8 @@ def main():
     res["fit_batch32"] = fit_array(dev, args.rows // 2, 32)
     res["fit_launch_batch100"] = fit_array(dev, args.rows // 10, args.batch, engine="launch")
     if not args.skip_stream:
-        res["stream_e2e"] = stream_e2e(dev, args.rows, args.batch, args.partitions, args.workers,
-                                       native=not args.python_feed)
+        res["stream_e2e"] = [stream_e2e(dev, args.rows, args.batch, args.partitions, int(w),
+                                        native=not args.python_feed) for w in str(args.workers).split(",")]
     print(json.dumps(res))
 
 

@@ -40,6 +40,7 @@
 // digital-twin models, ensembles, learning-rate sweeps), one per workgroup, each with
 // its own parameters, optimizer state, ring cursor and metrics.
 #include "sml_common.h"
+#include "sml_p2p.h"
 
 using namespace sml;
 
@@ -86,6 +87,14 @@ struct MBArgs {
   // cursor [M], metrics [M][4]; model b reads x + b * xmodel (0 = one shared ring).
   int64_t xmodel;
   const float* lrs;     // optional [M] per-model learning rates (hyper-parameter sweeps)
+  // data parallelism at Keras granularity (runtime/p2p.h): every step's gradient tile is
+  // pushed to every peer rank's receive buffer and the world's partials are summed in
+  // rank order before Adam.  Rank = dp_rank0 + blockIdx.x (one process per GPU launches
+  // one workgroup; in-launch ranks = a fleet of replicas).  dp_ranks <= 1: off.
+  uint64_t* const* dp_peers;
+  int dp_ranks, dp_rank0;
+  int* dp_status;           // set to 1 when a peer's gradient never arrived (timeout)
+  long long dp_timeout;     // s_memrealtime ticks (100 MHz)
 };
 
 template <int MB>
@@ -98,6 +107,7 @@ struct Smem {   // MB 48: ~47 KB, MB 128: ~108 KB
   float y[MB * XS];                     // reconstructions (phase-B argmax accuracy)
   float one[4];                         // constant 1 (bias-row activation), dummy store slot
   float red[3][NT / 64];
+  int abort;                            // DP: a gradient exchange timed out (all waves stop)
 };
 
 // logical feature of K-step s for lane group g (the C/D register order of the producer)
@@ -245,7 +255,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       S.w[bpos[i]] = wo[i];
     }
   }
-  if (t == 0) S.one[0] = 1.f;
+  if (t == 0) {
+    S.one[0] = 1.f;
+    S.abort = 0;
+  }
+  const bool dp = a.dp_ranks > 1;
+  const int dp_rank = a.dp_rank0 + (int)blockIdx.x;
 
   // ---- phase-A input operands: lane (c, g) of wave w holds row 16w + c, features f(s, g) ----
   const int row_l = 16 * wave + c;           // this lane's row within the batch
@@ -426,6 +441,45 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         }
         acc += acc2;
       }
+      if (dp) {
+        // push this rank's partial tile to every peer, then sum the world's partials in
+        // rank order (bit-identical on every rank) -- one xGMI hop, no launch, no RCCL call
+        const int64_t itg = it0 + step;
+        const uint32_t tag = p2p_tag(itg);
+        const int par = (int)(itg & 1);
+        for (int r = 0; r < a.dp_ranks; ++r) {
+          if (r == dp_rank) continue;
+          uint64_t* pb = a.dp_peers[r];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) p2p_put(pb + p2p_index(par, dp_rank, a.dp_ranks, NPARAM, T.slot(i)), tag, acc[i]);
+        }
+        const uint64_t* own = a.dp_peers[dp_rank];
+        f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+        bool failed = false;
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        for (int r = 0; r < a.dp_ranks; ++r) {
+          float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+          if (r != dp_rank) {
+            bool got[4] = {false, false, false, false};
+            for (;;) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                if (!got[i]) got[i] = p2p_try(own + p2p_index(par, r, a.dp_ranks, NPARAM, T.slot(i)), tag, v[i]);
+              if (__all(got[0] && got[1] && got[2] && got[3])) break;   // wave-uniform exit
+              __builtin_amdgcn_s_sleep(1);
+              if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.dp_timeout) {
+                failed = true;
+                break;
+              }
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sum[i] += v[i];
+          if (failed) break;
+        }
+        acc = sum;
+        if (failed && lane == 0) S.abort = 1;
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float gr = acc[i] * a.gscale;
@@ -458,6 +512,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     mark(2);
     lds_barrier();
     mark(3);
+    if (dp && S.abort) break;   // read after the barrier: every wave leaves together
   }
 
   // ---- write back: the whole image (padding slots keep zero gradients), moments, metrics ----
@@ -495,6 +550,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
     a.iter[0] = it0 + a.nsteps;
     if (a.cursor) a.cursor[0] = nxt;
+    if (dp && S.abort) __hip_atomic_store(a.dp_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -508,12 +564,15 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
                                const float* shift, float* params, float* m, float* v, int64_t* iter, float* metrics,
                                int B, int nsteps, const int* dims, const int* acts, float l1, float lr, float beta1,
                                float beta2, float eps, float gscale, int want_acc, unsigned long long* prof,
-                               int nmodels, int64_t xmodel, const float* lrs, hipStream_t stream) {
+                               int nmodels, int64_t xmodel, const float* lrs, uint64_t* const* dp_peers,
+                               int dp_ranks, int dp_rank0, int* dp_status, long long dp_timeout, hipStream_t stream) {
   if (B < 1 || B > MAXB || nsteps < 1 || ring < B || ring % B) return hipErrorInvalidValue;
   if (dims[0] > 31 || nmodels < 1 || nmodels > (1 << 20) || xmodel < 0) return hipErrorInvalidValue;
+  if (dp_ranks > 1 && (!dp_peers || !dp_status || dp_rank0 < 0 || dp_rank0 + nmodels > dp_ranks))
+    return hipErrorInvalidValue;
   MBArgs a{x, ld, ring, cursor, scale, shift, params, m, v, iter, metrics, B, nsteps, dims[0], dims[1], dims[2],
            dims[3], acts[0], acts[1], acts[2], acts[3], l1, lr, beta1, beta2, eps, gscale, want_acc, prof,
-           xmodel, lrs};
+           xmodel, lrs, dp_peers, dp_ranks, dp_rank0, dp_status, dp_timeout};
   const bool ref = acts[0] == ACT_TANH && acts[1] == ACT_RELU && acts[2] == ACT_TANH && acts[3] == ACT_RELU;
   void (*k)(MBArgs) = nullptr;
   size_t lds = 0;

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include "sml_ops.h"
+#include "../runtime/p2p.h"
+#include "sml_p2p.h"
 #include "../runtime/ring.h"
 #include "../runtime/serve.h"
 
@@ -184,7 +186,9 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
                           const at::Tensor& v, const at::Tensor& iter, const c10::optional<at::Tensor>& metrics,
                           int64_t batch, int64_t nsteps, std::vector<int64_t> dims, std::vector<int64_t> acts,
                           double l1, double lr, double beta1, double beta2, double eps, double gscale, bool want_acc,
-                          const c10::optional<at::Tensor>& prof, const c10::optional<at::Tensor>& lrs) {
+                          const c10::optional<at::Tensor>& prof, const c10::optional<at::Tensor>& lrs,
+                          uint64_t dp_peers, int64_t dp_ranks, int64_t dp_rank0, uint64_t dp_status,
+                          int64_t dp_timeout_ticks) {
   // One model: params/m/v [1536], cursor/iter [1], x [ring, ld].  Fleet of M models:
   // params/m/v [M, 1536], cursor/iter [M], metrics [M, 4], x [ring, ld] (shared) or [M, ring, ld].
   check_ae_dims(dims, acts);
@@ -239,6 +243,8 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
                                          opt_mut(metrics), (int)batch, (int)nsteps, d, a, (float)l1, (float)lr,
                                          (float)beta1, (float)beta2, (float)eps, (float)gscale, (int)want_acc,
                                          prof_ptr, (int)M, x.dim() == 3 ? x.stride(0) : 0, lrs_ptr,
+                                         reinterpret_cast<uint64_t* const*>(dp_peers), (int)dp_ranks, (int)dp_rank0,
+                                         reinterpret_cast<int*>(dp_status), (long long)dp_timeout_ticks,
                                          cur_stream(x)));
 }
 
@@ -534,6 +540,38 @@ at::Tensor lane_xor_probe(const at::Tensor& like) {
 // Python face of the pinned staging ring: fill (host memcpy, GIL released),
 // submit (hipMemcpyAsync on the ring's copy stream), wait / release against the
 // caller's current HIP stream.
+// P2P gradient-exchange buffers (runtime/p2p.h)
+struct P2PPy {
+  std::unique_ptr<sml::P2PExchange> x;
+  P2PPy(int device, int rank, int world, int64_t slots) {
+    c10::hip::HIPGuard guard(device);
+    x = std::make_unique<sml::P2PExchange>(device, rank, world, slots);
+  }
+  explicit P2PPy(sml::P2PExchange* p) : x(p) {}
+  static P2PPy* local(int device, int world, int64_t slots) {
+    c10::hip::HIPGuard guard(device);
+    return new P2PPy(sml::P2PExchange::local(device, world, slots));
+  }
+  py::bytes handle() const { return py::bytes(x->handle()); }
+  void open(const std::vector<std::string>& h) {
+    py::gil_scoped_release rel;
+    x->open(h);
+  }
+};
+
+void p2p_allreduce(at::Tensor& t, P2PPy& ex, double timeout_s) {
+  check_dev(t, "x", at::kFloat);
+  TORCH_CHECK(t.is_contiguous(), "x must be contiguous");
+  TORCH_CHECK(ex.x->ready(), "exchange not opened");
+  TORCH_CHECK(t.numel() <= ex.x->slots(), "x larger than the exchange buffers (", ex.x->slots(), " slots)");
+  const uint64_t e = ex.x->next_epoch();
+  c10::hip::HIPGuard guard(t.device().index());
+  SML_CHECK_HIP(sml::p2p_allreduce_launch(t.data_ptr<float>(), t.numel(), ex.x->peers_dev(), ex.x->world(),
+                                          ex.x->rank(), ex.x->slots(), sml::p2p_call_tag((int64_t)e),
+                                          (int)(e & 1), ex.x->status_dev(), (long long)(timeout_s * 1e8),
+                                          cur_stream(t)));
+}
+
 struct RingPy {
   std::unique_ptr<sml::PinnedRing> r;
   int device;
@@ -653,7 +691,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("cursor"), py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("m"),
         py::arg("v"), py::arg("iter"), py::arg("metrics"), py::arg("batch"), py::arg("nsteps"), py::arg("dims"),
         py::arg("acts"), py::arg("l1"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
-        py::arg("gscale"), py::arg("want_acc"), py::arg("prof") = py::none(), py::arg("lrs") = py::none());
+        py::arg("gscale"), py::arg("want_acc"), py::arg("prof") = py::none(), py::arg("lrs") = py::none(),
+        py::arg("dp_peers") = 0, py::arg("dp_ranks") = 1, py::arg("dp_rank0") = 0, py::arg("dp_status") = 0,
+        py::arg("dp_timeout_ticks") = 0);
   m.def("normalize_filter", &normalize_filter, "K8: normalise + keep rows with label == keep, order-preserving",
         py::arg("x"), py::arg("D"), py::arg("labels"), py::arg("keep"), py::arg("scale"), py::arg("shift"),
         py::arg("want_index") = false);
@@ -666,6 +706,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("iter"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("gscale"),
         py::arg("metrics"), py::arg("flags"), py::arg("cursor") = py::none(), py::arg("cursor_step") = 0,
         py::arg("cursor_ring") = 0, py::arg("scratch") = py::none());
+  py::class_<P2PPy>(m, "P2PExchange")
+      .def(py::init<int, int, int, int64_t>(), py::arg("device"), py::arg("rank"), py::arg("world"),
+           py::arg("slots"))
+      .def_static("local", &P2PPy::local, py::arg("device"), py::arg("world"), py::arg("slots"),
+                  py::return_value_policy::take_ownership)
+      .def("handle", &P2PPy::handle)
+      .def("open", &P2PPy::open, py::arg("handles"))
+      .def("status", [](const P2PPy& p) { return p.x->status(); })
+      .def("reset_status", [](P2PPy& p) { p.x->reset_status(); })
+      .def("clear", [](P2PPy& p) { p.x->clear(); })
+      .def_property_readonly("ready", [](const P2PPy& p) { return p.x->ready(); })
+      .def_property_readonly("rank", [](const P2PPy& p) { return p.x->rank(); })
+      .def_property_readonly("world", [](const P2PPy& p) { return p.x->world(); })
+      .def_property_readonly("slots", [](const P2PPy& p) { return p.x->slots(); })
+      .def_property_readonly("peers_ptr", [](const P2PPy& p) { return reinterpret_cast<uint64_t>(p.x->peers_dev()); })
+      .def_property_readonly("status_ptr", [](const P2PPy& p) { return reinterpret_cast<uint64_t>(p.x->status_dev()); });
+  m.def("p2p_allreduce", &p2p_allreduce, "in-place sum over the P2P exchange's ranks (one launch, one xGMI hop)",
+        py::arg("x"), py::arg("exchange"), py::arg("timeout_s") = 10.0);
   py::class_<RingPy>(m, "PinnedRing")
       .def(py::init<int, int64_t, int>(), py::arg("slots"), py::arg("slot_bytes"), py::arg("device"))
       .def("fill", &RingPy::fill, py::arg("slot"), py::arg("array"), py::arg("offset") = 0)

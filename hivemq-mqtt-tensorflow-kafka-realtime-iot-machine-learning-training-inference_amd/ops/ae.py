@@ -233,7 +233,7 @@ class FusedAE:
         return int(self.C.ae_minibatch_max_batch())
 
     def train_rows(self, x: torch.Tensor, batch: int, max_steps: Optional[int] = None,
-                   chunk_steps: int = 1 << 14) -> Tuple[int, int]:
+                   chunk_steps: int = 1 << 14, dp=None) -> Tuple[int, int]:
         """Keras ``fit`` over the rows of ``x`` in order: one Adam update per ``batch`` rows,
         the last batch short if ``len(x)`` is not a multiple (Keras' partial final batch),
         all on the persistent kernel (``csrc/kernels/ae_minibatch.hip``).
@@ -242,6 +242,11 @@ class FusedAE:
         runs ``chunk_steps`` sequential steps with parameters, moments and activations on
         chip) plus one for the partial batch.  Returns ``(steps, rows)`` consumed, capped
         by ``max_steps`` (the reference's ``take(100)``, cardata-v3.py:218).
+
+        ``dp`` (:class:`~streamml.parallel.p2p.P2PGroup`, one process per GPU): every step's
+        gradient is summed over the ranks inside the kernel (xGMI push + rank-order sum);
+        every rank must run the same number of full batches (the caller agrees on it, see
+        ``Autoencoder.fit``), and the partial batch is dropped.
         """
         self._check_x(x)
         B = int(batch)
@@ -256,13 +261,15 @@ class FusedAE:
                 rem = 0
         if not hasattr(self, "_tcur"):
             self._tcur = torch.zeros(1, dtype=torch.int64, device=self.device)
+        if dp is not None:
+            rem = 0
         steps = 0
         if nfull:
             ring = x[:nfull * B]
             self._tcur.zero_()
             while steps < nfull:
                 k = min(int(chunk_steps), nfull - steps)
-                self._launch_minibatch(ring, self._tcur, B, k)
+                self._launch_minibatch(ring, self._tcur, B, k, dp=dp)
                 steps += k
         if rem:
             self._tcur.zero_()
@@ -271,11 +278,21 @@ class FusedAE:
         return steps, nfull * B + rem
 
     def _launch_minibatch(self, ring: torch.Tensor, cursor: torch.Tensor, B: int, nsteps: int,
-                          prof: Optional[torch.Tensor] = None) -> None:
+                          prof: Optional[torch.Tensor] = None, dp=None) -> None:
+        kw, gscale = {}, 1.0 / B
+        if dp is not None:
+            if dp.in_launch:
+                raise ValueError("a single FusedAE replica needs a process-group P2PGroup (one rank per process)")
+            it0 = int(self.iter.item())
+            kw = dp.kernel_args(it0)
+            gscale = 1.0 / (B * dp.world)
         self.C.ae_train_minibatches(ring, cursor, self.scale, self.shift, self.params, self.m, self.v,
                                     self.iter, self.metrics, int(B), int(nsteps), self.spec.dims, self.spec.act_codes,
                                     float(self.spec.activity_l1), self.lr, self.beta_1, self.beta_2, self.epsilon,
-                                    1.0 / B, bool(self.want_acc), prof)
+                                    gscale, bool(self.want_acc), prof, None, **kw)
+        if dp is not None:
+            dp.note_iter(it0 + int(nsteps) - 1)
+            dp.check()
 
     def step(self, x: torch.Tensor, global_batch: Optional[int] = None, allreduce=None) -> None:
         """One full optimizer step on ``x`` (all rows of the local micro-batch).

@@ -157,15 +157,30 @@ class AEFleet:
         self.cursor.copy_(torch.from_numpy(offs))
 
     # -- training ----------------------------------------------------------------------
-    def train_minibatches(self, nsteps: int) -> None:
-        """``nsteps`` Keras steps of ``ring_batch`` rows for EVERY model, in one launch."""
+    def train_minibatches(self, nsteps: int, dp=None) -> None:
+        """``nsteps`` Keras steps of ``ring_batch`` rows for EVERY model, in one launch.
+
+        ``dp``: a :meth:`~streamml.parallel.p2p.P2PGroup.local` group of ``n_models`` ranks --
+        the models are then data-parallel REPLICAS of one model (workgroup b = rank b, each
+        on its own data): every step's gradient is summed over the replicas on chip before
+        Adam (global batch = models x batch), and the replicas stay bit-identical."""
         if self.ring is None:
             raise RuntimeError("attach_rings() first")
         B = self.ring_batch
+        kw, gscale = {}, 1.0 / B
+        if dp is not None:
+            if not dp.in_launch or dp.world != self.n_models:
+                raise ValueError("in-launch data parallelism needs P2PGroup.local(device, n_models)")
+            it0 = int(self.iter[0].item())
+            kw = dp.kernel_args(it0)
+            gscale = 1.0 / (B * dp.world)
         self.C.ae_train_minibatches(self.ring, self.cursor, self.scale, self.shift, self.params, self.m, self.v,
                                     self.iter, self.metrics, B, int(nsteps), self.spec.dims, self.spec.act_codes,
                                     float(self.spec.activity_l1), self.lr, self.beta_1, self.beta_2, self.epsilon,
-                                    1.0 / B, bool(self.want_acc), None, self.lrs)
+                                    gscale, bool(self.want_acc), None, self.lrs, **kw)
+        if dp is not None:
+            dp.note_iter(it0 + int(nsteps) - 1)
+            dp.check()
 
     # -- state -------------------------------------------------------------------------
     def get_weights(self, i: int) -> List[np.ndarray]:
