@@ -55,6 +55,12 @@ def parse():
                    help="write this rank's final parameter image to <path>.rank<R>.npy (replica checks)")
     p.add_argument("--graph", action="store_true",
                    help="replay one captured hipGraph step (replay floor ~10 us; eager is faster at these sizes)")
+    p.add_argument("--dp-steps", type=int, default=20000,
+                   help="Keras batch-32 steps per launch of the multi-GPU in-kernel P2P DP measurement (0 = skip)")
+    p.add_argument("--fit-rows", type=int, default=2_000_000,
+                   help="rows of the Autoencoder.fit(batch_size=100) measurement (0 = skip)")
+    p.add_argument("--stream-rows", type=int, default=2_000_000,
+                   help="events of the Kafka -> native feed -> fit end-to-end measurement (0 = skip)")
     return p.parse_args()
 
 
@@ -119,6 +125,67 @@ def measure_batch32(spec, data, device, steps, scale, shift, seed, launches=5):
     return {"rows_per_s": n * 32 / dt, "us_per_step": dt / n * 1e6, "vs_baseline": n * 32 / dt / BASELINE_ROWS_PER_S,
             "steps": n, "dtype": "fp32", "path": "persistent small-batch kernel (ae_minibatch.hip), 1 GPU",
             "final_loss": ae.read_metrics()["loss"]}
+
+
+def measure_batch_dp(spec, data, device, steps, scale, shift, seed, world, batch=32, launches=3):
+    """Keras batch-32 training with data parallelism at optimizer granularity: every step's
+    gradient tile is pushed to every peer over xGMI and summed in rank order INSIDE the
+    persistent kernel (parallel/p2p.py) -- no launch, no RCCL call per step.  Collective:
+    every rank calls it.  Whole-job rows/s (world x batch rows per step)."""
+    import torch
+
+    from streamml.models.reference import init_dense_weights
+    from streamml.ops.ae import FusedAE
+    from streamml.parallel import dp as dpm
+    from streamml.parallel.p2p import P2PGroup
+
+    group, err = P2PGroup.try_create(device)
+    if group is None:
+        return {"error": f"P2P exchange unavailable: {err!r}"}
+    ae = FusedAE(spec, init_dense_weights(spec.layer_sizes, seed=seed), device, scale=scale, shift=shift)
+    n = (data.size(0) // batch) * batch
+    ae.attach_ring(data[:n], batch)
+    ae.train_minibatches(min(steps, 2000), dp=group)   # warm-up
+    dpm.barrier(device)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(launches):
+        ae.train_minibatches(steps, dp=group)
+    torch.cuda.synchronize()
+    dt = dpm.allreduce_max(time.perf_counter() - t0, device)
+    # replicas must be bit-identical: compare a checksum of the parameter image
+    chk = torch.tensor([float(ae.params.double().sum())], dtype=torch.float64, device=device)
+    lo, hi = chk.clone(), chk.clone()
+    import torch.distributed as dist
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    n_steps = steps * launches
+    rows = world * batch * n_steps
+    return {"rows_per_s": rows / dt, "us_per_step": dt / n_steps * 1e6, "vs_baseline": rows / dt / BASELINE_ROWS_PER_S,
+            "steps": n_steps, "global_batch": world * batch, "dtype": "fp32", "replicas_identical": bool(lo == hi),
+            "path": f"persistent kernel, in-kernel P2P gradient exchange over xGMI, dp{world}"}
+
+
+def _bench_fit_module():
+    """bench/bench_fit.py by path (``bench`` the package name is shadowed by this file)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("sml_bench_fit", os.path.join(ROOT, "bench", "bench_fit.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def measure_fit(device, rows, batch=100, seed=0):
+    """The reference's own job on the real entry point: Autoencoder.fit(batch_size=100)
+    (cardata-v3.py:176-177, 212-222) on an array -- every Keras step on the persistent kernel."""
+    return _bench_fit_module().fit_array(device, rows=rows, batch=batch, seed=seed)
+
+
+def measure_stream_e2e(device, rows, batch=100):
+    """In-process Kafka (16 partitions of Confluent Avro) -> native C++ feed (decode-time
+    label filter, pinned slabs, H2D in flight) -> fit(batch_size=100): events/s end to end,
+    with the rate of each stage alone."""
+    return _bench_fit_module().stream_e2e(device, rows=rows, batch=batch, partitions=16, workers=8, native=True)
 
 
 def measure_batch32_fleet(spec, data, device, steps, scale, shift, n_models=1024, launches=3):
@@ -232,12 +299,26 @@ def main():
             print(f"[bench] persistent scorer unavailable ({e!r}); launch-per-event path", file=sys.stderr)
             p50, p99 = measure_infer_p50(fused, device, args.infer_events)
             infer_path = "launch-per-event"
+    def guarded(fn, *a, **kw):   # a side measurement never takes the headline down
+        try:
+            return fn(*a, **kw)
+        except Exception as e:  # noqa: BLE001
+            return {"error": repr(e)[:400]}
+
     b32 = None
     if rank == 0 and args.batch32_steps > 0:
-        b32 = measure_batch32(spec, data, device, args.batch32_steps, scale, shift, args.seed)
+        b32 = guarded(measure_batch32, spec, data, device, args.batch32_steps, scale, shift, args.seed)
         if args.fleet_models > 0:
-            b32["fleet"] = measure_batch32_fleet(spec, data, device, max(args.batch32_steps // 10, 1), scale, shift,
-                                                 args.fleet_models)
+            b32["fleet"] = guarded(measure_batch32_fleet, spec, data, device, max(args.batch32_steps // 10, 1),
+                                   scale, shift, args.fleet_models)
+    b32_dp = {"skipped": "single GPU (no peers)"}
+    if world > 1 and args.dp_steps > 0:
+        b32_dp = guarded(measure_batch_dp, spec, data, device, args.dp_steps, scale, shift, args.seed, world)
+    fit100 = stream = None
+    if rank == 0 and args.fit_rows > 0:
+        fit100 = guarded(measure_fit, device, args.fit_rows)
+    if rank == 0 and args.stream_rows > 0:
+        stream = guarded(measure_stream_e2e, device, args.stream_rows)
     del nslices
     rows_per_s = gb * args.steps / elapsed
     if rank == 0:
@@ -253,6 +334,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": rows_per_s / BASELINE_ROWS_PER_S,
             "dtype": "bf16",
+            "input_dtype": "fp32 raw sensor rows (normalize_fn fused into the kernel's load; bf16 MFMA, fp32 accumulate)",
             "data": "synthetic (raw car-sensor rows, 100k simulated devices, HBM-resident, random-init weights)",
             "config": {
                 "model": "dense-autoencoder 18-14-7-7-18 (cardata-v1, tanh/relu/tanh/relu, L1 1e-7, MSE, Adam)",
@@ -268,6 +350,11 @@ def main():
             "final_epoch_loss": metrics["loss"],
             "final_accuracy": metrics["accuracy"],
             "keras_batch32": b32,
+            "keras_batch32_dp": b32_dp,
+            "fit_batch100_rows_per_s": None if not fit100 or "error" in fit100 else fit100["rows_per_s"],
+            "fit_batch100": fit100,
+            "stream_e2e_rows_per_s": None if not stream or "error" in stream else stream["rows_per_s"],
+            "stream_e2e": stream,
         }
         print(json.dumps(out), flush=True)
     dp.shutdown()

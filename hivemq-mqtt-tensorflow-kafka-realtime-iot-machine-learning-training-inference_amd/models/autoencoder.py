@@ -157,7 +157,7 @@ class Autoencoder:
     def fit(self, x=None, y=None, epochs: int = 1, batch_size: int = 32, verbose: int = 1,
             callbacks: Optional[Sequence[Callback]] = None, validation_data=None, shuffle: bool = True,
             steps_per_epoch: Optional[int] = None, seed: int = 0, initial_epoch: int = 0,
-            engine: str = "auto") -> History:
+            engine: str = "auto", dp: str = "auto") -> History:
         """Train on an array (``y`` must be ``x`` or None: autoencoder) or a Stream.
 
         ``engine``: ``"persistent"`` runs every Keras step of an epoch on the persistent
@@ -167,10 +167,18 @@ class Autoencoder:
         (bf16 MFMA train kernel + slab-reduce/Adam) per batch, for any batch size;
         ``"auto"`` picks ``persistent`` on a single ROCm replica when the batch fits.
 
-        Under ``torch.distributed`` (RCCL) every rank trains on its own shard:
-        arrays are split contiguously by rank, Streams are expected to be
-        rank-sharded already; gradients are all-reduced once per step and the
-        global batch is ``batch_size * world_size``.
+        Under ``torch.distributed`` every rank trains on its own shard: arrays are split
+        contiguously by rank, Streams are expected to be rank-sharded already; the global
+        batch is ``batch_size * world_size``.  ``dp`` picks the gradient exchange:
+
+        * ``"p2p"`` -- inside the persistent kernel, every Keras step (xGMI push of the
+          gradient tile to every peer + rank-order sum, :mod:`streamml.parallel.p2p`);
+          ranks agree on the step count per launch (full batches only);
+        * ``"rccl"`` -- the launch-per-step path with one flat RCCL all-reduce per step;
+        * ``"local_sgd:K"`` -- documented semantics change: K
+          independent persistent-kernel steps per rank, then the parameters are averaged;
+        * ``"auto"`` -- ``p2p`` when the persistent kernel applies and the IPC exchange can
+          be set up on every rank, else ``rccl``.
         """
         from ..data.stream import Stream
         from ..parallel.dp import allreduce_sum_
@@ -191,15 +199,25 @@ class Autoencoder:
             cb.on_train_begin()
         is_stream = isinstance(x, Stream)
         if not is_stream:
-            arr = x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x, np.float32)
+            on_dev = isinstance(x, torch.Tensor) and x.device == self.device and self.device.type == "cuda"
+            arr = x.detach() if on_dev else (x.detach().cpu().numpy() if isinstance(x, torch.Tensor)
+                                              else np.asarray(x, np.float32))
             if world > 1:
                 from ..parallel.dp import shard_range
                 s0, s1 = shard_range(len(arr), rank, world)
                 arr = arr[s0:s1]
+            # device arrays stay on the device (no host round trip)
             xd = self._to_device(arr) if self.device.type == "cuda" else self._cpu_x(arr)
         from ..parallel.fault import maybe_inject
-        persistent = self._use_persistent(engine, batch_size, world)
+        persistent = self._use_persistent(engine, batch_size, world, dp)
+        exch, local_k = None, 0
+        if persistent and world > 1:
+            exch, local_k = self._dp_setup(dp)
+            if exch is None and not local_k:
+                persistent = False   # p2p unavailable on some rank: RCCL launch path
         self.last_fit_engine = "persistent" if persistent else ("launch" if self.device.type == "cuda" else "torch-cpu")
+        if persistent and world > 1:
+            self.last_fit_engine += "+p2p" if exch is not None else f"+local_sgd:{local_k}"
         gstep = int(getattr(self, "_global_step", 0))
         for epoch in range(initial_epoch, epochs):
             rng = np.random.default_rng([seed, rank, epoch])   # epoch-keyed: a resumed run reshuffles identically
@@ -209,17 +227,26 @@ class Autoencoder:
             be.reset_metrics()
             steps = 0
             if persistent and is_stream:
-                steps = self._fit_stream_persistent(x, batch_size, steps_per_epoch, gstep, rank)
+                if world > 1:
+                    steps = self._fit_stream_dp(x, batch_size, steps_per_epoch, exch, local_k)
+                else:
+                    steps = self._fit_stream_persistent(x, batch_size, steps_per_epoch, gstep, rank)
                 gstep += steps
             elif persistent:
                 n = len(xd)
                 nb = math.ceil(n / batch_size)
+                if world > 1:   # every rank runs the same number of full batches
+                    from ..parallel.dp import agree
+                    nb = agree([n // batch_size], self.device)[0]
                 if steps_per_epoch is not None:
                     nb = min(nb, steps_per_epoch)
-                xs = xd[torch.as_tensor(rng.permutation(n), device=xd.device)] if shuffle else xd
+                xs = xd[self._device_perm(n, seed, rank, epoch)] if shuffle else xd
                 for s in range(gstep, gstep + nb):   # injection points, before the epoch's launches
                     maybe_inject(s, rank)
-                steps, _ = be.train_rows(xs[:min(n, nb * batch_size)], batch_size)
+                if world > 1:
+                    steps = self._dp_train(xs[:nb * batch_size], batch_size, exch, local_k)
+                else:
+                    steps, _ = be.train_rows(xs[:min(n, nb * batch_size)], batch_size)
                 gstep += steps
             elif is_stream:
                 for xb in self._stream_batches(x, batch_size):
@@ -281,18 +308,89 @@ class Autoencoder:
             cb.on_train_end()
         return hist
 
-    def _use_persistent(self, engine: str, batch_size: int, world: int) -> bool:
+    def _device_perm(self, n: int, seed: int, rank: int, epoch: int) -> torch.Tensor:
+        """Epoch shuffle generated on the device (deterministic in (seed, rank, epoch), so a
+        resumed run reshuffles identically) -- no host permutation, no H2D of indices."""
+        g = torch.Generator(device=self.device)
+        g.manual_seed((int(seed) * 1_000_003 + int(rank) * 7_919 + int(epoch)) & 0x7FFFFFFFFFFF)
+        return torch.randperm(n, generator=g, device=self.device)
+
+    def _use_persistent(self, engine: str, batch_size: int, world: int, dp: str = "auto") -> bool:
         if engine not in ("auto", "persistent", "launch"):
             raise ValueError(f"engine must be auto / persistent / launch, got {engine!r}")
+        if not (dp in ("auto", "p2p", "rccl") or dp.startswith("local_sgd:")):
+            raise ValueError(f"dp must be auto / p2p / rccl / local_sgd:K, got {dp!r}")
         if engine == "launch" or self.device.type != "cuda":
             if engine == "persistent" and self.device.type != "cuda":
                 raise ValueError("engine='persistent' needs a ROCm device")
             return False
-        fits = world == 1 and 1 <= batch_size <= self.backend.max_minibatch()
+        fits = 1 <= batch_size <= self.backend.max_minibatch() and (world == 1 or dp != "rccl")
         if engine == "persistent" and not fits:
-            raise ValueError(f"engine='persistent' needs one replica and batch_size <= "
-                             f"{self.backend.max_minibatch()} (got batch {batch_size}, world {world})")
+            raise ValueError(f"engine='persistent' needs batch_size <= {self.backend.max_minibatch()} and, "
+                             f"under DP, dp='p2p' / 'local_sgd:K' (got batch {batch_size}, dp {dp!r})")
         return fits
+
+    def _dp_setup(self, dp: str):
+        """(P2PGroup or None, local-SGD period or 0); collective over the process group."""
+        if dp.startswith("local_sgd:"):
+            k = int(dp.split(":", 1)[1])
+            if k < 1:
+                raise ValueError("local_sgd:K needs K >= 1")
+            return None, k
+        if getattr(self, "_p2p", None) is None:
+            from ..parallel.p2p import P2PGroup
+            self._p2p, err = P2PGroup.try_create(self.device)
+            if self._p2p is None:
+                if dp == "p2p":
+                    raise RuntimeError(f"dp='p2p': the IPC exchange could not be set up ({err!r})")
+                import warnings
+                warnings.warn(f"P2P exchange unavailable ({err!r}); falling back to RCCL per step")
+        return self._p2p, 0
+
+    def _dp_train(self, rows: torch.Tensor, B: int, exch, local_k: int) -> int:
+        """Train ``len(rows) // B`` steps (the same count on every rank) under DP."""
+        be = self.backend
+        n = rows.size(0) // B
+        if exch is not None:
+            steps, _ = be.train_rows(rows[:n * B], B, dp=exch)
+            return steps
+        import torch.distributed as dist
+        world = dist.get_world_size()
+        done = 0
+        while done < n:   # local SGD: K independent steps, then average the parameters
+            k = min(local_k, n - done)
+            be.train_rows(rows[done * B:(done + k) * B], B)
+            dist.all_reduce(be.params, op=dist.ReduceOp.SUM)
+            be.params.div_(world)
+            done += k
+        return n
+
+    def _fit_stream_dp(self, stream, B: int, max_steps: Optional[int], exch, local_k: int) -> int:
+        """Streaming epoch under DP: ranks agree, per device chunk, on how many full batches
+        every rank can run (an all-reduce of two ints per chunk -- hundreds of steps);
+        rows a rank cannot use yet are kept for the next round; the epoch ends for everyone
+        when any rank's stream is exhausted (its leftover rows and the others' are dropped)."""
+        from ..parallel.dp import agree
+        D = self.spec.input_dim
+        stage = torch.empty((0, D), dtype=torch.float32, device=self.device)
+        it = iter(self._stream_device_chunks(stream))
+        steps, exhausted = 0, False
+        while True:
+            if not exhausted:
+                try:
+                    xd = next(it)
+                    stage = torch.cat([stage, xd]) if stage.size(0) else xd.clone()
+                except StopIteration:
+                    exhausted = True
+            avail = stage.size(0) // B
+            if max_steps is not None:
+                avail = min(avail, max_steps - steps)
+            mn, any_done = agree([avail, int(exhausted)], self.device, ["min", "max"])
+            if mn > 0:
+                steps += self._dp_train(stage[:mn * B], B, exch, local_k)
+                stage = stage[mn * B:].clone()
+            if any_done or (max_steps is not None and steps >= max_steps):
+                return steps
 
     def _stream_device_chunks(self, stream, chunk_rows: int = 1 << 16):
         """Device chunks of raw rows from a Stream (no host re-batching): the pinned ring

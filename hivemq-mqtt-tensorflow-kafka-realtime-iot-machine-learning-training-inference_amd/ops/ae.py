@@ -211,14 +211,15 @@ class FusedAE:
             allreduce(self.grad)
             self.reduce(1, RA_ADAM | RA_METRICS | RA_ADVANCE, gscale=1.0 / gb, partials=self.grad)
 
-    def train_minibatches(self, nsteps: int, prof: Optional[torch.Tensor] = None) -> None:
+    def train_minibatches(self, nsteps: int, prof: Optional[torch.Tensor] = None, dp=None) -> None:
         """``nsteps`` sequential optimizer steps of ``ring_batch`` rows each, in ONE launch.
 
         Keras ``fit(batch_size=32)`` semantics (one Adam update per small batch, the
         reference's setting: cardata-v3.py:187-203) without a launch per step: the
         persistent kernel in ``csrc/kernels/ae_minibatch.hip`` keeps parameters, Adam
         moments and activations on chip and consumes the attached ring from the device
-        cursor.  fp32 arithmetic.  Single replica (no all-reduce between the steps).
+        cursor.  fp32 arithmetic.  ``dp`` (a process-group ``P2PGroup``): every step's
+        gradient is summed over the ranks inside the kernel (global batch = world x batch).
         ``prof`` (int64 [11], optional) accumulates per-phase shader cycles of wave 0.
         """
         if self.ring is None:
@@ -226,7 +227,7 @@ class FusedAE:
         B = self.ring_batch
         if B > self.max_minibatch():
             raise ValueError(f"batch {B} > {self.max_minibatch()}: use step_ring()")
-        self._launch_minibatch(self.ring, self.cursor, B, int(nsteps), prof)
+        self._launch_minibatch(self.ring, self.cursor, B, int(nsteps), prof, dp=dp)
 
     def max_minibatch(self) -> int:
         """Largest batch the persistent small-batch trainer takes (128: cardata-v3's 100 fits)."""

@@ -135,6 +135,23 @@ def sync_model_from_rank0(model) -> None:
         be.set_optimizer_state(it2, mm, vv)
 
 
+def agree(values, device: torch.device, ops=None):
+    """Element-wise collective agreement on small ints (default MIN): every rank returns the
+    same list.  One all-reduce (no-op without a process group)."""
+    vals = [int(v) for v in values]
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return vals
+    ops = ops or ["min"] * len(vals)
+    out = []
+    t = torch.tensor(vals, dtype=torch.int64, device=device)
+    for op in sorted(set(ops)):
+        u = t.clone()
+        dist.all_reduce(u, op=dist.ReduceOp.MIN if op == "min" else dist.ReduceOp.MAX)
+        out.append((op, u.cpu().tolist()))
+    res = dict(out)
+    return [res[o][i] for i, o in enumerate(ops)]
+
+
 def allreduce_max(value: float, device: torch.device) -> float:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         t = torch.tensor([value], dtype=torch.float64, device=device)

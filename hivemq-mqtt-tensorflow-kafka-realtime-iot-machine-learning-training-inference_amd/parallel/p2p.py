@@ -59,6 +59,38 @@ class P2PGroup:
         dist.barrier(group=group)
 
     @classmethod
+    def try_create(cls, device, slots: int = NSLOTS, group=None, timeout_s: float = 10.0):
+        """Collective: every rank gets a group, or every rank gets ``None`` (e.g. no IPC /
+        peer access on this platform) -- never a mix that would strand a peer's kernel."""
+        import torch.distributed as dist
+
+        from .dp import agree
+        ok, err, g = 1, None, None
+        C = load_c()
+        dev = torch.device(device)
+        try:
+            x = C.P2PExchange(dev.index if dev.index is not None else torch.cuda.current_device(),
+                              dist.get_rank(group), dist.get_world_size(group), int(slots))
+            h = bytes(x.handle())
+        except Exception as e:  # noqa: BLE001 - agreed on below
+            ok, err, h, x = 0, e, b"", None
+        handles = [None] * dist.get_world_size(group)
+        dist.all_gather_object(handles, h, group=group)
+        if agree([ok], dev)[0]:
+            try:
+                x.open(list(handles))
+            except Exception as e:  # noqa: BLE001
+                ok, err = 0, e
+        if not agree([ok], dev)[0]:
+            return None, err
+        g = cls.__new__(cls)
+        g.device = dev if dev.index is not None else torch.device("cuda", torch.cuda.current_device())
+        g.timeout_s, g._last_iter, g.x = float(timeout_s), -1, x
+        g.rank, g.world, g.group, g.in_launch = dist.get_rank(group), dist.get_world_size(group), group, False
+        dist.barrier(group=group)
+        return g, None
+
+    @classmethod
     def local(cls, device, world: int, slots: int = NSLOTS, timeout_s: float = 10.0) -> "P2PGroup":
         """Every rank's buffer in this process: ranks = workgroups of one launch."""
         return cls(device, slots, timeout_s=timeout_s, _local_world=int(world))

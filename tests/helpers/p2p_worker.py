@@ -51,10 +51,29 @@ def main():
     steps2, _ = ae.train_rows(raw, 32, dp=group, chunk_steps=7)   # several launches, tags continue
     torch.cuda.synchronize()
     np.save(f"{out}.rank{rank}.npy", ae.params.cpu().numpy())
+    # the user-facing entry point: Autoencoder.fit under DP (array shards, a rank-sharded
+    # stream, and the local-SGD mode)
+    from streamml.data import stream as S
+    from streamml.models.autoencoder import Autoencoder
+    full = np.random.default_rng(7).uniform(0, 40, (32 * 60 + 17, 18)).astype(np.float32)
+    engines = {}
+    for mode in ("p2p", "local_sgd:5"):
+        m = Autoencoder(device=dev, input_normalizer="cardata", seed=3)
+        m.compile()
+        m.fit(full, epochs=2, batch_size=32, shuffle=False, verbose=0, dp=mode)
+        engines[mode] = m.last_fit_engine
+        np.save(f"{out}.fit_{mode.replace(':', '')}.rank{rank}.npy", m.backend.params.cpu().numpy())
+    m = Autoencoder(device=dev, input_normalizer="cardata", seed=3)
+    m.compile()
+    st = S.synthetic(20_000 + 3_000 * rank, chunk=4_096, seed=rank).filter_normal(device=True)
+    m.fit(st, epochs=1, batch_size=100, verbose=0, dp="p2p")
+    np.save(f"{out}.fit_stream.rank{rank}.npy", m.backend.params.cpu().numpy())
+    engines["stream"] = m.last_fit_engine
+    engines["stream_iters"] = m.iterations
     if rank == 0:
         with open(out + ".json", "w") as f:
             json.dump({"allreduce_ok": ar_ok, "allreduce_us": ar_us, "steps": steps + steps2,
-                       "iter": int(ae.iter.item())}, f)
+                       "iter": int(ae.iter.item()), "engines": engines}, f)
     dp.barrier(dev)
     dp.shutdown()
 

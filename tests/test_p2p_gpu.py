@@ -90,6 +90,10 @@ def test_two_processes_ipc_shared_gpu(tmp_path, cuda_device):
     assert info["steps"] == 80 and info["iter"] == 80, info
     p0, p1 = np.load(out + ".rank0.npy"), np.load(out + ".rank1.npy")
     np.testing.assert_array_equal(p0, p1)
+    assert info["engines"]["p2p"] == "persistent+p2p" and info["engines"]["local_sgd:5"] == "persistent+local_sgd:5"
+    assert info["engines"]["stream"] == "persistent+p2p" and info["engines"]["stream_iters"] >= 190
+    for tag in ("fit_p2p", "fit_local_sgd5", "fit_stream"):
+        np.testing.assert_array_equal(np.load(f"{out}.{tag}.rank0.npy"), np.load(f"{out}.{tag}.rank1.npy"))
     # the same two shards through in-launch replicas give the same parameters
     spec = AESpec()
     sc, sh = normalize_affine()
