@@ -260,8 +260,8 @@ class Autoencoder:
                 n = len(xd)
                 order = None
                 if shuffle:
-                    perm = rng.permutation(n)
-                    order = torch.as_tensor(perm, device=xd.device)
+                    order = (self._device_perm(n, seed, rank, epoch) if xd.device.type == "cuda"
+                             else torch.as_tensor(rng.permutation(n), device=xd.device))
                 nb = math.ceil(n / batch_size)
                 if steps_per_epoch is not None:
                     nb = min(nb, steps_per_epoch)
