@@ -34,11 +34,32 @@ def parse_args(argv: Sequence[str]):
     return p.parse_args(list(argv))
 
 
-def model_name(members, i: int) -> str:
-    """File stem of model ``i``: its key when it owns exactly one, else ``modelNNNNN``."""
-    if len(members[i]) == 1:
-        return re.sub(r"[^A-Za-z0-9_.-]", "_", str(members[i][0]))
-    return f"model{i:05d}"
+def model_name(members, i: int, used=None) -> str:
+    """File stem of model ``i``: its key when it owns exactly one, else ``modelNNNNN``.
+    ``used`` (a set) de-duplicates stems that sanitise alike (``car/1`` vs ``car_1``, or a
+    key literally named ``model00003``): a later collision gets ``-<i>`` appended."""
+    stem = re.sub(r"[^A-Za-z0-9_.-]", "_", str(members[i][0])) if len(members[i]) == 1 else f"model{i:05d}"
+    if used is not None:
+        if stem in used:
+            stem = f"{stem}-{i}"
+        used.add(stem)
+    return stem
+
+
+def training_rows(ns):
+    """(raw rows, car keys) of NORMAL events only: the reference trains its anomaly model on
+    ``failure_occurred == "false"`` rows (cardata-v3.py:211-212); the CSV has no failure
+    column, so every CSV row counts as normal."""
+    import numpy as np
+
+    from ..data.cardata import SyntheticCarSource, load_csv
+    if ns.source == "synthetic":
+        src = SyntheticCarSource(seed=ns.seed, n_devices=ns.synthetic_devices)
+        raw, fail, dev_id, _ = src.generate(ns.synthetic_rows)
+        raw, dev_id = raw[~fail], dev_id[~fail]
+        return raw, np.array([f"electric-vehicle-{d:05d}" for d in dev_id])
+    raw, _, keys = load_csv(ns.source)
+    return raw, keys
 
 
 def main(argv: Sequence[str]) -> int:
@@ -46,41 +67,37 @@ def main(argv: Sequence[str]) -> int:
     import numpy as np
     import torch
 
-    from ..data.cardata import SyntheticCarSource, load_csv, normalize_affine
+    from ..data.cardata import normalize_affine
     from ..models.autoencoder import Autoencoder
     from ..ops.ae import AESpec
-    from ..ops.ae_fleet import AEFleet, rings_by_key
+    from ..ops.ae_fleet import AEFleet, ragged_rings_by_key
 
-    if ns.source == "synthetic":
-        src = SyntheticCarSource(seed=ns.seed, n_devices=ns.synthetic_devices)
-        raw, _, dev_id, _ = src.generate(ns.synthetic_rows)
-        keys = np.array([f"electric-vehicle-{d:05d}" for d in dev_id])
-    else:
-        raw, _, keys = load_csv(ns.source)
-    rings, members = rings_by_key(raw, keys, batch=ns.batch, n_models=ns.models)
-    M, R = rings.shape[0], rings.shape[1]
+    raw, keys = training_rows(ns)
+    flat, table, members = ragged_rings_by_key(raw, keys, batch=ns.batch, n_models=ns.models)
+    M = len(members)
     spec = AESpec(input_dim=raw.shape[1])
     scale, shift = normalize_affine()
     dev = torch.device(ns.device)
     fleet = AEFleet.from_seeds(spec, [ns.seed + i for i in range(M)], dev, lr=ns.lr, scale=scale, shift=shift)
-    fleet.attach_rings(torch.from_numpy(rings).to(dev), ns.batch)
-    steps = R // ns.batch
-    print(f"fleet: {M} models, {R} rows per model ring, {steps} steps of {ns.batch} rows per epoch", flush=True)
+    fleet.attach_ragged(torch.from_numpy(flat).to(dev), ns.batch, table)
+    steps = fleet.epoch_steps()
+    print(f"fleet: {M} models, {len(flat)} rows, {int(steps.min())}-{int(steps.max())} steps of {ns.batch} rows "
+          f"per model per epoch", flush=True)
     ms = []
     for ep in range(ns.epochs):
         fleet.reset_metrics()
-        fleet.train_minibatches(steps)
+        fleet.train_epoch()
         ms = fleet.read_metrics()
         losses = np.array([m["loss"] for m in ms])
         print(f"Epoch {ep + 1}/{ns.epochs} - loss mean {losses.mean():.4f} min {losses.min():.4f} "
               f"max {losses.max():.4f}", flush=True)
     os.makedirs(ns.out, exist_ok=True)
-    index = {}
+    index, used = {}, set()
     for i in range(M):
-        name = model_name(members, i)
+        name = model_name(members, i, used)
         path = os.path.join(ns.out, name + ".h5")
         am = Autoencoder(input_dim=spec.input_dim, device="cpu")
-        am.compile()
+        am.compile(learning_rate=ns.lr)   # the saved training_config records the rate actually used
         am.set_weights(fleet.get_weights(i))
         am.save(path, include_optimizer=False)
         index[name] = {"file": os.path.basename(path), "keys": [str(k) for k in members[i]],

@@ -28,8 +28,9 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
                                const float* shift, float* params, float* m, float* v, int64_t* iter, float* metrics,
                                int B, int nsteps, const int* dims, const int* acts, float l1, float lr, float beta1,
                                float beta2, float eps, float gscale, int want_acc, unsigned long long* prof,
-                               int nmodels, int64_t xmodel, const float* lrs, uint64_t* const* dp_peers,
-                               int dp_ranks, int dp_rank0, int* dp_status, long long dp_timeout, hipStream_t stream);
+                               int nmodels, int64_t xmodel, const float* lrs, const int64_t* ragged,
+                               uint64_t* const* dp_peers, int dp_ranks, int dp_rank0, int* dp_status,
+                               long long dp_timeout, hipStream_t stream);
 
 // ---- LSTM recurrence (lstm.hip) ----
 hipError_t lstm_fwd_launch(const float* zx, const float* Uw, const float* h0, const float* c0, float* hseq,

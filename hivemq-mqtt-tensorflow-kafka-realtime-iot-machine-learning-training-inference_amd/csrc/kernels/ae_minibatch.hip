@@ -87,6 +87,8 @@ struct MBArgs {
   // cursor [M], metrics [M][4]; model b reads x + b * xmodel (0 = one shared ring).
   int64_t xmodel;
   const float* lrs;     // optional [M] per-model learning rates (hyper-parameter sweeps)
+  const int64_t* ragged;   // optional [M][3] {first row, ring rows, steps}: models of different
+                           // sizes in one flat row array, each taking its own number of steps
   // data parallelism at Keras granularity (runtime/p2p.h): every step's gradient tile is
   // pushed to every peer rank's receive buffer and the world's partials are summed in
   // rank order before Adam.  Rank = dp_rank0 + blockIdx.x (one process per GPU launches
@@ -218,6 +220,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   {
     const int mdl = blockIdx.x;
     a.x += mdl * a.xmodel;
+    if (a.ragged) {
+      const int64_t* rg = a.ragged + 3 * mdl;
+      a.x += rg[0] * a.ld;
+      a.ring = rg[1];
+      a.nsteps = (int)rg[2];
+    }
     a.params += mdl * NPARAM;
     a.m += mdl * NPARAM;
     a.v += mdl * NPARAM;
@@ -549,7 +557,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       a.metrics[3] += (float)B * (float)a.nsteps;
     }
     a.iter[0] = it0 + a.nsteps;
-    if (a.cursor) a.cursor[0] = nxt;
+    if (a.cursor) a.cursor[0] = a.nsteps > 0 ? nxt : cur;
     if (dp && S.abort) __hip_atomic_store(a.dp_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -564,15 +572,17 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
                                const float* shift, float* params, float* m, float* v, int64_t* iter, float* metrics,
                                int B, int nsteps, const int* dims, const int* acts, float l1, float lr, float beta1,
                                float beta2, float eps, float gscale, int want_acc, unsigned long long* prof,
-                               int nmodels, int64_t xmodel, const float* lrs, uint64_t* const* dp_peers,
-                               int dp_ranks, int dp_rank0, int* dp_status, long long dp_timeout, hipStream_t stream) {
-  if (B < 1 || B > MAXB || nsteps < 1 || ring < B || ring % B) return hipErrorInvalidValue;
+                               int nmodels, int64_t xmodel, const float* lrs, const int64_t* ragged,
+                               uint64_t* const* dp_peers, int dp_ranks, int dp_rank0, int* dp_status,
+                               long long dp_timeout, hipStream_t stream) {
+  // ragged: per-model ring / steps were validated on the host (torch_bind.cpp)
+  if (B < 1 || B > MAXB || nsteps < 1 || (!ragged && (ring < B || ring % B))) return hipErrorInvalidValue;
   if (dims[0] > 31 || nmodels < 1 || nmodels > (1 << 20) || xmodel < 0) return hipErrorInvalidValue;
   if (dp_ranks > 1 && (!dp_peers || !dp_status || dp_rank0 < 0 || dp_rank0 + nmodels > dp_ranks))
     return hipErrorInvalidValue;
   MBArgs a{x, ld, ring, cursor, scale, shift, params, m, v, iter, metrics, B, nsteps, dims[0], dims[1], dims[2],
            dims[3], acts[0], acts[1], acts[2], acts[3], l1, lr, beta1, beta2, eps, gscale, want_acc, prof,
-           xmodel, lrs, dp_peers, dp_ranks, dp_rank0, dp_status, dp_timeout};
+           xmodel, lrs, ragged, dp_peers, dp_ranks, dp_rank0, dp_status, dp_timeout};
   const bool ref = acts[0] == ACT_TANH && acts[1] == ACT_RELU && acts[2] == ACT_TANH && acts[3] == ACT_RELU;
   void (*k)(MBArgs) = nullptr;
   size_t lds = 0;

@@ -188,7 +188,7 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
                           double l1, double lr, double beta1, double beta2, double eps, double gscale, bool want_acc,
                           const c10::optional<at::Tensor>& prof, const c10::optional<at::Tensor>& lrs,
                           uint64_t dp_peers, int64_t dp_ranks, int64_t dp_rank0, uint64_t dp_status,
-                          int64_t dp_timeout_ticks) {
+                          int64_t dp_timeout_ticks, const c10::optional<at::Tensor>& ragged) {
   // One model: params/m/v [1536], cursor/iter [1], x [ring, ld].  Fleet of M models:
   // params/m/v [M, 1536], cursor/iter [M], metrics [M, 4], x [ring, ld] (shared) or [M, ring, ld].
   check_ae_dims(dims, acts);
@@ -205,7 +205,23 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
   TORCH_CHECK(batch >= 1 && batch <= sml::ae_minibatch_max_batch(), "batch must be in [1, ",
               sml::ae_minibatch_max_batch(), "]");
   TORCH_CHECK(nsteps >= 1 && nsteps <= (1 << 30), "nsteps out of range");
-  TORCH_CHECK(ring >= batch && ring % batch == 0, "ring rows must be a positive multiple of the batch");
+  const int64_t* ragged_ptr = nullptr;
+  if (ragged.has_value() && ragged->defined()) {
+    // [M][3] {first row, ring rows, steps} on the device; validated here from a host copy
+    check_dev(*ragged, "ragged", at::kLong);
+    TORCH_CHECK(x.dim() == 2 && ragged->numel() == 3 * M && ragged->is_contiguous(),
+                "ragged needs a flat [rows, ld] x and an int64 [M, 3] table");
+    auto h = ragged->cpu();
+    const int64_t* r = h.data_ptr<int64_t>();
+    for (int64_t i = 0; i < M; ++i) {
+      TORCH_CHECK(r[3 * i] >= 0 && r[3 * i + 1] >= batch && r[3 * i + 1] % batch == 0 &&
+                      r[3 * i] + r[3 * i + 1] <= x.size(0) && r[3 * i + 2] >= 0 && r[3 * i + 2] <= (1 << 30),
+                  "ragged row ", i, ": needs 0 <= first, ring a positive multiple of the batch inside x, steps >= 0");
+    }
+    ragged_ptr = ragged->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(ring >= batch && ring % batch == 0, "ring rows must be a positive multiple of the batch");
+  }
   check_dev(cursor, "cursor", at::kLong);
   check_dev(iter, "iter", at::kLong);
   TORCH_CHECK(cursor.numel() == M && iter.numel() == M && cursor.is_contiguous() && iter.is_contiguous(),
@@ -242,7 +258,7 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
                                          m.data_ptr<float>(), v.data_ptr<float>(), iter.data_ptr<int64_t>(),
                                          opt_mut(metrics), (int)batch, (int)nsteps, d, a, (float)l1, (float)lr,
                                          (float)beta1, (float)beta2, (float)eps, (float)gscale, (int)want_acc,
-                                         prof_ptr, (int)M, x.dim() == 3 ? x.stride(0) : 0, lrs_ptr,
+                                         prof_ptr, (int)M, x.dim() == 3 ? x.stride(0) : 0, lrs_ptr, ragged_ptr,
                                          reinterpret_cast<uint64_t* const*>(dp_peers), (int)dp_ranks, (int)dp_rank0,
                                          reinterpret_cast<int*>(dp_status), (long long)dp_timeout_ticks,
                                          cur_stream(x)));
@@ -693,7 +709,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("acts"), py::arg("l1"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
         py::arg("gscale"), py::arg("want_acc"), py::arg("prof") = py::none(), py::arg("lrs") = py::none(),
         py::arg("dp_peers") = 0, py::arg("dp_ranks") = 1, py::arg("dp_rank0") = 0, py::arg("dp_status") = 0,
-        py::arg("dp_timeout_ticks") = 0);
+        py::arg("dp_timeout_ticks") = 0, py::arg("ragged") = py::none());
   m.def("normalize_filter", &normalize_filter, "K8: normalise + keep rows with label == keep, order-preserving",
         py::arg("x"), py::arg("D"), py::arg("labels"), py::arg("keep"), py::arg("scale"), py::arg("shift"),
         py::arg("want_index") = false);

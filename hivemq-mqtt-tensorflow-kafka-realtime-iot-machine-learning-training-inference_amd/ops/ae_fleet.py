@@ -45,24 +45,10 @@ def _fnv1a(key) -> int:
     return h
 
 
-def rings_by_key(raw: np.ndarray, keys, batch: int = 32, n_models: Optional[int] = None):
-    """Route a keyed stream to per-model rings: ``(rings [M, R, D] float32, members)``.
-
-    ``n_models=None``: one model per distinct key (``members[b] = [key]``, keys in order
-    of first appearance -- e.g. one anomaly model per car of the reference's
-    ``testdata/car-sensor-data.csv``).  Otherwise key -> model ``fnv1a(key) % n_models``
-    (the same stable hash as ``parallel.dp.shard_by_key``), so a key always lands on the
-    same model across restarts and hosts.  Each model's rows keep stream order; a ring
-    is the longest group rounded up to a multiple of ``batch``, and shorter groups are
-    repeated cyclically to fill it (a ring replays anyway), so every model takes the
-    same number of steps per pass.
-    """
-    raw = np.asarray(raw, dtype=np.float32)
+def _groups_by_key(keys, n_models):
     keys = np.asarray(keys)
-    if raw.ndim != 2 or len(keys) != raw.shape[0]:
-        raise ValueError("raw must be [n, D] with one key per row")
     uniq, first, inv = np.unique(keys, return_index=True, return_inverse=True)
-    order = np.argsort(first)                    # distinct keys in order of first appearance
+    order = np.argsort(first)
     if n_models is None:
         rank = np.empty(len(uniq), np.int64)
         rank[order] = np.arange(len(uniq))
@@ -77,13 +63,54 @@ def rings_by_key(raw: np.ndarray, keys, batch: int = 32, n_models: Optional[int]
         empty = [b for b in range(n_models) if not members[b]]
         if empty:
             raise ValueError(f"models {empty[:8]} receive no keys: use fewer models or n_models=None")
+    return [np.flatnonzero(model_of_row == b) for b in range(len(members))], members
+
+
+def rings_by_key(raw: np.ndarray, keys, batch: int = 32, n_models: Optional[int] = None):
+    """Route a keyed stream to per-model rings: ``(rings [M, R, D] float32, members)``.
+
+    ``n_models=None``: one model per distinct key (``members[b] = [key]``, keys in order
+    of first appearance -- e.g. one anomaly model per car of the reference's
+    ``testdata/car-sensor-data.csv``).  Otherwise key -> model ``fnv1a(key) % n_models``
+    (the same stable hash as ``parallel.dp.shard_by_key`` for ``str`` keys; other keys
+    are hashed as ``str(key)``), so a key always lands on the same model across restarts
+    and hosts.  Each model's rows keep stream order; a ring is the longest group rounded
+    up to a multiple of ``batch``, and shorter groups are repeated cyclically to fill it,
+    so every model takes the same number of steps per pass.  Memory is therefore
+    ``M x longest group`` and small groups are replayed (oversampled) -- use
+    :func:`ragged_rings_by_key` + ``AEFleet.attach_ragged`` when group sizes differ a lot.
+    """
+    raw = np.asarray(raw, dtype=np.float32)
+    keys = np.asarray(keys)
+    if raw.ndim != 2 or len(keys) != raw.shape[0]:
+        raise ValueError("raw must be [n, D] with one key per row")
+    groups, members = _groups_by_key(keys, n_models)
     M = len(members)
-    groups = [np.flatnonzero(model_of_row == b) for b in range(M)]
     R = -(-max(len(g) for g in groups) // batch) * batch
     rings = np.empty((M, R, raw.shape[1]), np.float32)
     for b, g in enumerate(groups):
         rings[b] = raw[np.resize(g, R)]          # cyclic repeat of the group's rows
     return rings, members
+
+
+def ragged_rings_by_key(raw: np.ndarray, keys, batch: int = 32, n_models: Optional[int] = None):
+    """Like :func:`rings_by_key`, without padding every model to the largest group:
+    ``(flat [sum R_b, D] float32, table [M, 2] int64 {first row, ring rows R_b}, members)``.
+    ``R_b`` is model b's row count rounded up to a multiple of ``batch`` (at most
+    ``batch - 1`` rows repeated), so memory is the stream's size and one epoch of model b
+    is ``R_b / batch`` steps -- no model replays its rows more often than another."""
+    raw = np.asarray(raw, dtype=np.float32)
+    if raw.ndim != 2 or len(np.asarray(keys)) != raw.shape[0]:
+        raise ValueError("raw must be [n, D] with one key per row")
+    groups, members = _groups_by_key(keys, n_models)
+    lens = [-(-len(g) // batch) * batch for g in groups]
+    table = np.zeros((len(groups), 2), np.int64)
+    table[:, 1] = lens
+    table[1:, 0] = np.cumsum(lens)[:-1]
+    flat = np.empty((int(sum(lens)), raw.shape[1]), np.float32)
+    for b, g in enumerate(groups):
+        flat[table[b, 0]:table[b, 0] + lens[b]] = raw[np.resize(g, lens[b])]
+    return flat, table, members
 
 
 class AEFleet:
@@ -126,6 +153,7 @@ class AEFleet:
             self.shift = torch.as_tensor(np.asarray(shift, dtype=np.float32), device=dev)
         self.ring: Optional[torch.Tensor] = None
         self.ring_batch = 0
+        self.ragged: Optional[torch.Tensor] = None
 
     @classmethod
     def from_seeds(cls, spec: AESpec, seeds: Sequence[int], device, **kw) -> "AEFleet":
@@ -154,7 +182,40 @@ class AEFleet:
         if offs.shape != (M,) or (offs % batch).any() or (offs < 0).any() or (offs >= n).any():
             raise ValueError("offsets must be [M] multiples of the batch inside the ring")
         self.ring, self.ring_batch = rings, int(batch)
+        self.ragged = None
         self.cursor.copy_(torch.from_numpy(offs))
+
+    def attach_ragged(self, flat: torch.Tensor, batch: int, table) -> None:
+        """Models of different sizes in one flat row array (:func:`ragged_rings_by_key`):
+        model b's ring is ``flat[table[b, 0] : table[b, 0] + table[b, 1]]``."""
+        M = self.n_models
+        table = np.asarray(table, dtype=np.int64)
+        if table.shape != (M, 2) or (table[:, 1] % batch).any() or (table[:, 1] < batch).any():
+            raise ValueError(f"table must be [{M}, 2] {{first row, ring rows (multiple of the batch)}}")
+        if flat.dim() != 2 or table[:, 0].min() < 0 or (table[:, 0] + table[:, 1]).max() > flat.size(0):
+            raise ValueError("table rows outside the flat array")
+        if batch <= 0 or batch > self.C.ae_minibatch_max_batch():
+            raise ValueError(f"batch must be in [1, {self.C.ae_minibatch_max_batch()}]")
+        self.ring, self.ring_batch = flat, int(batch)
+        self._ragged_table = table
+        self.ragged = torch.zeros((M, 3), dtype=torch.int64, device=self.device)
+        self.cursor.zero_()
+
+    def epoch_steps(self) -> np.ndarray:
+        """Steps of one pass over each model's own rows (ragged) or the shared ring length."""
+        if self.ragged is not None:
+            return self._ragged_table[:, 1] // self.ring_batch
+        return np.full(self.n_models, self.ring.size(-2) // self.ring_batch)
+
+    def train_epoch(self, epochs: int = 1) -> None:
+        """Every model passes ``epochs`` times over its OWN rows (ragged: own step count)."""
+        steps = self.epoch_steps() * int(epochs)
+        if self.ragged is None:
+            self.train_minibatches(int(steps[0]))
+            return
+        t = np.concatenate([self._ragged_table, steps[:, None]], axis=1)
+        self.ragged.copy_(torch.from_numpy(np.ascontiguousarray(t)))
+        self._launch(max(int(steps.max()), 1), ragged=self.ragged)
 
     # -- training ----------------------------------------------------------------------
     def train_minibatches(self, nsteps: int, dp=None) -> None:
@@ -174,13 +235,26 @@ class AEFleet:
             it0 = int(self.iter[0].item())
             kw = dp.kernel_args(it0)
             gscale = 1.0 / (B * dp.world)
-        self.C.ae_train_minibatches(self.ring, self.cursor, self.scale, self.shift, self.params, self.m, self.v,
-                                    self.iter, self.metrics, B, int(nsteps), self.spec.dims, self.spec.act_codes,
-                                    float(self.spec.activity_l1), self.lr, self.beta_1, self.beta_2, self.epsilon,
-                                    gscale, bool(self.want_acc), None, self.lrs, **kw)
+        if self.ragged is not None:
+            if dp is not None:
+                raise ValueError("ragged fleets are independent models (no data parallelism)")
+            t = self._ragged_table
+            self.ragged.copy_(torch.from_numpy(np.concatenate(
+                [t, np.full((self.n_models, 1), int(nsteps), np.int64)], axis=1)))
+            self._launch(int(nsteps), ragged=self.ragged)
+            return
+        self._launch(int(nsteps), gscale=gscale, **kw)
         if dp is not None:
             dp.note_iter(it0 + int(nsteps) - 1)
             dp.check()
+
+    def _launch(self, nsteps: int, gscale: Optional[float] = None, ragged=None, **kw) -> None:
+        B = self.ring_batch
+        self.C.ae_train_minibatches(self.ring, self.cursor, self.scale, self.shift, self.params, self.m, self.v,
+                                    self.iter, self.metrics, B, int(nsteps), self.spec.dims, self.spec.act_codes,
+                                    float(self.spec.activity_l1), self.lr, self.beta_1, self.beta_2, self.epsilon,
+                                    1.0 / B if gscale is None else gscale, bool(self.want_acc), None, self.lrs,
+                                    ragged=ragged, **kw)
 
     # -- state -------------------------------------------------------------------------
     def get_weights(self, i: int) -> List[np.ndarray]:

@@ -54,3 +54,35 @@ def test_fleet_cli_args_and_names():
     assert ns.models == 64 and ns.epochs == 2 and ns.batch == 32
     assert model_name([["car/1"], ["a", "b"]], 0) == "car_1"
     assert model_name([["car/1"], ["a", "b"]], 1) == "model00001"
+
+
+def test_fleet_trains_on_normal_rows_only():
+    """failure rows must never reach a per-car anomaly model's ring."""
+    from streamml.cli.fleet import parse_args, training_rows
+    from streamml.data.cardata import SyntheticCarSource
+    ns = parse_args(["synthetic", "--synthetic-rows", "20000", "--synthetic-devices", "50", "--seed", "3"])
+    raw, keys = training_rows(ns)
+    all_raw, fail, _, _ = SyntheticCarSource(seed=3, n_devices=50).generate(20000)
+    assert fail.any() and len(raw) == int((~fail).sum()) == len(keys)
+    np.testing.assert_array_equal(raw, all_raw[~fail])
+
+
+def test_fleet_model_names_never_collide():
+    from streamml.cli.fleet import model_name
+    members = [["car/1"], ["car_1"], ["model00003"], ["a", "b"], ["car:1"]]
+    used = set()
+    names = [model_name(members, i, used) for i in range(len(members))]
+    assert len(set(names)) == len(names)
+    assert names[0] == "car_1" and names[1] == "car_1-1" and names[3] == "model00003-3"
+
+
+def test_ragged_rings_no_padding_to_the_largest_group():
+    from streamml.ops.ae_fleet import ragged_rings_by_key
+    raw = np.arange(10 * 2, dtype=np.float32).reshape(10, 2)
+    keys = np.array(["a"] * 7 + ["b"] * 3)
+    flat, table, members = ragged_rings_by_key(raw, keys, batch=4)
+    assert members == [["a"], ["b"]]
+    np.testing.assert_array_equal(table, [[0, 8], [8, 4]])   # 7 -> 8 rows, 3 -> 4 rows
+    np.testing.assert_array_equal(flat[:7], raw[:7])
+    np.testing.assert_array_equal(flat[7], raw[0])            # one cyclic pad row
+    np.testing.assert_array_equal(flat[8:11], raw[7:])

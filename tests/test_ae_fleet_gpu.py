@@ -150,3 +150,33 @@ def test_fleet_cli_one_model_per_car(cuda_device, tmp_path):
         assert rec["keys"] == [name] and np.isfinite(rec["loss"])
     m = load_model(str(out / index[cars[0]]["file"]), device="cpu")
     assert len(m.get_weights()) == 8
+
+
+def test_ragged_fleet_each_model_its_own_epoch(cuda_device):
+    """Ragged rings: models of different sizes in one flat array, each taking
+    its own number of steps per epoch -- model b equals a lone FusedAE on its own rows."""
+    from streamml.data.cardata import normalize_affine
+    from streamml.models.reference import init_dense_weights
+    from streamml.ops.ae import AESpec, FusedAE
+    from streamml.ops.ae_fleet import AEFleet, ragged_rings_by_key
+    spec = AESpec()
+    sc, sh = normalize_affine()
+    rng = np.random.default_rng(0)
+    sizes = [32 * 3, 32 * 10 + 5, 40]
+    keys = np.concatenate([[f"car{i}"] * n for i, n in enumerate(sizes)])
+    raw = rng.uniform(0, 40, (len(keys), 18)).astype(np.float32)
+    flat, table, members = ragged_rings_by_key(raw, keys, batch=32)
+    fleet = AEFleet.from_seeds(spec, [7, 8, 9], cuda_device, scale=sc, shift=sh)
+    fleet.attach_ragged(torch.from_numpy(flat).to(cuda_device), 32, table)
+    fleet.train_epoch(2)
+    torch.cuda.synchronize()
+    steps = fleet.epoch_steps() * 2
+    np.testing.assert_array_equal(fleet.iter.cpu().numpy(), steps)
+    for b in range(3):
+        ring = torch.from_numpy(flat[table[b, 0]:table[b, 0] + table[b, 1]]).to(cuda_device)
+        one = FusedAE(spec, init_dense_weights(spec.layer_sizes, seed=7 + b), cuda_device, scale=sc, shift=sh)
+        one.attach_ring(ring, 32)
+        one.train_minibatches(int(steps[b]))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(fleet.params[b].cpu().numpy(), one.params.cpu().numpy())
+        assert fleet.read_metrics()[b]["rows"] == steps[b] * 32
