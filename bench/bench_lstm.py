@@ -18,15 +18,21 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=65536)
-    ap.add_argument("--seq-len", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=None, help="default 65536 (two_layer) / 1 (reference)")
+    ap.add_argument("--seq-len", type=int, default=None, help="default 50 (two_layer) / 1 (reference)")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--stack", default="two_layer", choices=["two_layer", "reference"])
+    ap.add_argument("--materialize", action="store_true", help="copy every window ([n, T, F]) instead of views")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay each train step (fwd + bwd + Adam) as a captured HIP graph "
                          "(measured: 54.1 vs 55.1 M windows/s eager -- the step is GPU-bound, not launch-bound)")
     args = ap.parse_args()
+    ref = args.stack == "reference"
+    args.batch = args.batch or (1 if ref else 65536)
+    args.seq_len = args.seq_len or (1 if ref else 50)
+    if ref and args.seq_len == 1 and args.batch <= 32:
+        return bench_reference(args)
     import numpy as np
     import torch
     from streamml.data.cardata import normalize_affine, synthetic_device_tensor
@@ -39,11 +45,13 @@ def main():
     sc, sh = normalize_affine()
     raw = synthetic_device_tensor(B * 4 + T + 1, dev, seed=0)
     xn = raw * torch.tensor(sc, dtype=torch.float32, device=dev) + torch.tensor(sh, dtype=torch.float32, device=dev)
-    # sliding windows [n, T, 18] -> next row targets
+    # sliding windows [n, T, 18] -> next row targets, read IN PLACE from the event rows
+    # (strided views; cardata-v2.py:199-206's window(look_back, shift=1) + skip(look_back))
+    from streamml.data.stream import sliding_windows
     n = B * 4
-    idx = torch.arange(n, device=dev)[:, None] + torch.arange(T, device=dev)[None, :]
-    X = xn[idx].contiguous()
-    Y = xn[torch.arange(n, device=dev) + T].contiguous()
+    X, Y = sliding_windows(xn[:n + T].contiguous(), T)
+    if args.materialize:   # the round-1 layout: every window copied (T x the input bytes)
+        X, Y = X.contiguous(), Y.contiguous()
     for s in range(args.warmup):
         i = s % 4
         m.train_step(X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B])
@@ -62,7 +70,56 @@ def main():
     print(json.dumps({"metric": "LSTM train windows/s (seq_len=%d, %s)" % (T, args.stack), "value": wps,
                       "unit": "windows/s", "events_per_s": wps * T, "ms_per_step": dt / args.steps * 1e3,
                       "batch": B, "seq_len": T, "params": m.count_params(), "dtype": "bf16",
-                      "final_loss": float(loss), "n_gpus": 1, "data": "synthetic", "hip_graph": bool(args.graph)}))
+                      "final_loss": float(loss), "n_gpus": 1, "data": "synthetic", "hip_graph": bool(args.graph),
+                      "windows": "materialized" if args.materialize else "in-place strided views"}))
+
+
+def bench_reference(args, epochs: int = 5, steps_per_epoch: int = 1000):
+    """cardata-v2.py:172-209 as the reference runs it: look_back 1, batch 1, 1 000 steps x
+    5 epochs, one Adam update per event.  Persistent kernel (one launch per epoch) vs the
+    per-step autograd path (fused LSTM kernels, ~10 launches per step)."""
+    import numpy as np
+    import torch
+    from streamml.data.cardata import normalize_affine, synthetic_device_tensor
+    from streamml.data.stream import sliding_windows
+    from streamml.models.lstm import LSTMPredictor
+    from streamml.ops import lstm_persistent as lp
+
+    dev = torch.device("cuda", 0)
+    B = args.batch
+    n = steps_per_epoch * B
+    sc, sh = normalize_affine()
+    raw = synthetic_device_tensor(n + 1, dev, seed=0)
+    xn = (raw * torch.tensor(sc, dtype=torch.float32, device=dev)
+          + torch.tensor(sh, dtype=torch.float32, device=dev)).contiguous()
+    X, Y = sliding_windows(xn, 1)
+    m = LSTMPredictor.reference(look_back=1, device=dev)
+    lp.train_steps(m, X, Y, B, 50)          # warm-up (module load, LDS opt-in)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e in range(epochs):                  # one launch per epoch, as fit() does
+        out = lp.train_steps(m, X, Y, B, steps_per_epoch)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    steps = epochs * steps_per_epoch
+    # the same steps through the autograd path (per-step launches), fewer of them
+    ma = LSTMPredictor.reference(look_back=1, device=dev)
+    for i in range(20):
+        ma.train_step(X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B])
+    torch.cuda.synchronize()
+    na = 300
+    t1 = time.perf_counter()
+    for i in range(na):
+        ma.train_step(X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B])
+    torch.cuda.synchronize()
+    da = time.perf_counter() - t1
+    print(json.dumps({"metric": "LSTM reference stack Keras step time (look_back=1, batch=%d)" % B,
+                      "value": dt / steps * 1e6, "unit": "us/step", "higher_is_better": False,
+                      "steps_per_s": steps / dt, "events_per_s": steps * B / dt, "steps": steps,
+                      "epochs": epochs, "steps_per_epoch": steps_per_epoch, "launches": epochs,
+                      "autograd_us_per_step": da / na * 1e6, "speedup_vs_autograd": (da / na) / (dt / steps),
+                      "final_loss": float(out[-1, 0]), "params": m.count_params(), "dtype": "fp32",
+                      "n_gpus": 1, "data": "synthetic", "engine": "persistent (lstm_ref_train.hip)"}))
 
 
 if __name__ == "__main__":

@@ -64,11 +64,18 @@ int lstm_fused_slabs(int64_t B);  // one weight-gradient slab per workgroup
 // x: fp32 or bf16 (x_bf16); h and dh are bf16 (lstm_fused.hip header), dx has x's dtype
 hipError_t lstm_fused_fwd_launch(const void* x, bool x_bf16, const float* W, const float* Uw, const float* b,
                                  const float* h0, const float* c0, void* hseq_bf16, void* cseq_bf16, int64_t B, int T,
-                                 int IN, int U, int act, hipStream_t stream);
+                                 int IN, int U, int act, int64_t x_seq, hipStream_t stream);
 hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, const void* hseq_bf16, const void* x,
                                  bool x_bf16, const float* h0, const float* c0, const float* W, const float* Uw,
                                  const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,
-                                 int IN, int U, int act, int dh_last_only, hipStream_t stream);
+                                 int IN, int U, int act, int dh_last_only, int64_t x_seq, hipStream_t stream);
+
+// ---- persistent Keras-step trainer for the reference LSTM stack (lstm_ref_train.hip) ----
+int lstm_ref_train_params();
+hipError_t lstm_ref_train_launch(float* flat, float* m, float* v, int64_t* iter, const float* x, int64_t ldx,
+                                 const float* y, int64_t ldy, const int32_t* order, int64_t nrows, int64_t row0, int B,
+                                 int nsteps, int act, float lr, float beta1, float beta2, float eps, float* out,
+                                 hipStream_t stream);
 
 // ---- persistent per-event scorer (ae_serve.hip); structures live in host-mapped memory ----
 struct alignas(128) ServeCtl {

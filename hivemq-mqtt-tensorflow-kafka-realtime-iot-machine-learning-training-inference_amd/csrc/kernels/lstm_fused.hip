@@ -72,6 +72,7 @@ struct FusedBwdArgs {
   int64_t B;
   int T, IN, act;
   int dh_last_only;    // return_sequences=False: only h_T received a gradient (no [B, T, U] zeros read)
+  int64_t x_seq;       // elements between consecutive sequences of x (T*IN contiguous, IN sliding windows)
 };
 
 template <int U, int KT, int XV, typename XT, int ACT>
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     const __bf16* dhp = a.dh_last_only ? a.dh + sq * U : a.dh + (sq * T + t) * (int64_t)U;
 #pragma unroll
     for (int b = 0; b < UB; ++b) st.dho[b] = ld_bf16x4(dhp + 16 * b + 4 * g);
-    const XT* p = static_cast<const XT*>(a.x) + (sq * T + t) * (int64_t)IN;
+    const XT* p = static_cast<const XT*>(a.x) + sq * a.x_seq + (int64_t)t * IN;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) st.xt[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN);
   };
@@ -419,9 +420,9 @@ int lstm_fused_slabs(int64_t B) { return (int)((B + 16 * WAVES - 1) / (16 * WAVE
 hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, const void* hseq_bf16, const void* x,
                                  bool x_bf16, const float* h0, const float* c0, const float* W, const float* Uw,
                                  const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,
-                                 int IN, int U, int act, int dh_last_only, hipStream_t stream) {
+                                 int IN, int U, int act, int dh_last_only, int64_t x_seq, hipStream_t stream) {
   FusedBwdArgs a{(const __bf16*)dh_bf16, (const __bf16*)cseq_bf16, (const __bf16*)hseq_bf16, x, h0, c0, W, Uw, b, dx,
-                 dh0, dc0, partials, B, T, IN, act, dh_last_only};
+                 dh0, dc0, partials, B, T, IN, act, dh_last_only, x_seq > 0 ? x_seq : (int64_t)T * IN};
   return dispatch(U, IN, row_vec(x, IN, x_bf16 ? 2 : 4), x_bf16, [&](auto u, auto k, auto v, auto xt) {
     using XT = std::remove_const_t<std::remove_pointer_t<decltype(xt)>>;
     return launch_bwd<decltype(u)::value, decltype(k)::value, decltype(v)::value, XT>(a, stream);

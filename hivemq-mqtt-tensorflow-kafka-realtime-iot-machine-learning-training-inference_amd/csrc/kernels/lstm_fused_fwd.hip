@@ -8,7 +8,9 @@ using namespace sml_lstm;
 namespace {
 
 struct FusedFwdArgs {
-  const void* x;       // [B, T, IN] fp32 (model input) or bf16 (a lower LSTM layer's h)
+  const void* x;       // [B, T, IN] fp32 (model input) or bf16 (a lower LSTM layer's h); sequence b
+                       // starts x_seq elements after sequence b-1 (T*IN: contiguous; IN: the
+                       // sliding windows of cardata-v2.py:199-206 read in place from the base rows)
   const float* W;      // [IN, 4U]
   const float* Uw;     // [U, 4U]
   const float* b;      // [4U]
@@ -20,6 +22,7 @@ struct FusedFwdArgs {
   __bf16* cseq;        // [B/16, T, U/16, 64, 4]   cell state, bf16, fragment-native (backward only)
   int64_t B;
   int T, IN, act;
+  int64_t x_seq;
 };
 
 template <int U, int KT, int XV, typename XT, int ACT>
@@ -72,7 +75,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
     hb[b] = pack4(h[b]);
   }
   // x_t^T as B operand: B[k = feature 16kt + 4g + j][n = sequence c]
-  const XT* xrow = static_cast<const XT*>(a.x) + sq * (int64_t)T * IN;
+  const XT* xrow = static_cast<const XT*>(a.x) + sq * a.x_seq;
   auto load_x = [&](int t, XR* v) {
     const XT* p = xrow + (int64_t)t * IN;
 #pragma unroll
@@ -149,8 +152,9 @@ namespace sml {
 
 hipError_t lstm_fused_fwd_launch(const void* x, bool x_bf16, const float* W, const float* Uw, const float* b,
                                  const float* h0, const float* c0, void* hseq_bf16, void* cseq_bf16, int64_t B, int T,
-                                 int IN, int U, int act, hipStream_t stream) {
-  FusedFwdArgs a{x, W, Uw, b, h0, c0, (__bf16*)hseq_bf16, (__bf16*)cseq_bf16, B, T, IN, act};
+                                 int IN, int U, int act, int64_t x_seq, hipStream_t stream) {
+  FusedFwdArgs a{x, W, Uw, b, h0, c0, (__bf16*)hseq_bf16, (__bf16*)cseq_bf16, B, T, IN, act,
+                 x_seq > 0 ? x_seq : (int64_t)T * IN};
   return dispatch(U, IN, row_vec(x, IN, x_bf16 ? 2 : 4), x_bf16, [&](auto u, auto k, auto v, auto xt) {
     using XT = std::remove_const_t<std::remove_pointer_t<decltype(xt)>>;
     return launch_fwd<decltype(u)::value, decltype(k)::value, decltype(v)::value, XT>(a, stream);

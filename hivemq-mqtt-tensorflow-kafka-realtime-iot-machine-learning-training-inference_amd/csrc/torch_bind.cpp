@@ -433,8 +433,12 @@ std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W,
   check_dev(W, "W", at::kFloat);
   check_dev(Uw, "U", at::kFloat);
   check_dev(b, "b", at::kFloat);
-  TORCH_CHECK(x.dim() == 3 && x.is_contiguous(), "x must be contiguous [B, T, IN]");
+  // x: contiguous [B, T, IN], or a strided view whose steps are consecutive rows --
+  // sliding windows base.as_strided((B, T, IN), (shift*IN, IN, 1)) read in place
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1 && x.stride(1) == x.size(2) && x.stride(0) >= 0,
+              "x must be [B, T, IN] with consecutive rows per step (contiguous or sliding windows)");
   const int64_t B = x.size(0), T = x.size(1), IN = x.size(2), U = Uw.size(0);
+  const int64_t x_seq = B > 1 ? x.stride(0) : T * IN;
   TORCH_CHECK(W.is_contiguous() && W.size(0) == IN && W.size(1) == 4 * U, "W must be [IN, 4U]");
   TORCH_CHECK(Uw.is_contiguous() && Uw.size(1) == 4 * U, "U must be [U, 4U]");
   TORCH_CHECK(b.is_contiguous() && b.numel() == 4 * U, "b must be [4U]");
@@ -454,7 +458,7 @@ std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W,
   SML_CHECK_HIP(sml::lstm_fused_fwd_launch(x.data_ptr(), x.scalar_type() == at::kBFloat16, W.data_ptr<float>(),
                                            Uw.data_ptr<float>(), b.data_ptr<float>(), opt_ptr(h0), opt_ptr(c0),
                                            h.data_ptr(), c.data_ptr(), B, (int)T, (int)IN, (int)U, (int)act,
-                                           cur_stream(x)));
+                                           x_seq, cur_stream(x)));
   return {h.narrow(0, 0, B), c};
 }
 
@@ -474,8 +478,10 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
   check_dev(Uw, "U", at::kFloat);
   check_dev(b, "b", at::kFloat);
   const int64_t B = x.size(0), T = x.size(1), IN = x.size(2), U = Uw.size(0);
-  TORCH_CHECK(dh.is_contiguous() && cseq.is_contiguous() && hseq.is_contiguous() && x.is_contiguous(),
-              "inputs must be contiguous");
+  TORCH_CHECK(dh.is_contiguous() && cseq.is_contiguous() && hseq.is_contiguous(), "inputs must be contiguous");
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1 && x.stride(1) == IN && x.stride(0) >= 0,
+              "x must be [B, T, IN] with consecutive rows per step (contiguous or sliding windows)");
+  const int64_t x_seq = B > 1 ? x.stride(0) : T * IN;
   const int64_t Bp = (B + 15) / 16 * 16;
   TORCH_CHECK(hseq.size(0) == B && hseq.size(1) == T && hseq.size(2) == U, "h shape mismatch");
   TORCH_CHECK(cseq.dim() == 3 && cseq.size(0) == Bp && cseq.size(1) == T && cseq.size(2) == U,
@@ -508,7 +514,7 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
       opt_ptr(c0), W.data_ptr<float>(), Uw.data_ptr<float>(), b.data_ptr<float>(),
       want_dx ? dx_pad.data_ptr() : nullptr, want_state_grads ? dh0.data_ptr<float>() : nullptr,
       want_state_grads ? dc0.data_ptr<float>() : nullptr, partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U,
-      (int)act, dh_last_only ? 1 : 0, st));
+      (int)act, dh_last_only ? 1 : 0, x_seq, st));
   SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
                                      out.data_ptr<float>(), st));
   const int64_t G4 = 4 * U, LDW = (S / G4) - U - 1;
@@ -520,6 +526,39 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
     if (dx_pad.size(2) != IN) dx = dx.narrow(2, 0, IN).contiguous();
   }
   return {dx, dW, dU, db, dh0, dc0};
+}
+
+// N consecutive Keras steps of the reference LSTM stack (look_back 1) in one launch.
+at::Tensor lstm_ref_train(const at::Tensor& flat, const at::Tensor& m, const at::Tensor& v, const at::Tensor& iter,
+                          const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Tensor>& order,
+                          int64_t row0, int64_t B, int64_t nsteps, int64_t act, double lr, double beta1, double beta2,
+                          double eps) {
+  check_dev(flat, "flat", at::kFloat);
+  check_dev(m, "m", at::kFloat);
+  check_dev(v, "v", at::kFloat);
+  check_dev(x, "x", at::kFloat);
+  check_dev(y, "y", at::kFloat);
+  TORCH_CHECK(iter.is_cuda() && iter.scalar_type() == at::kLong && iter.numel() == 1, "iter must be a device int64[1]");
+  const int64_t P = sml::lstm_ref_train_params();
+  TORCH_CHECK(flat.is_contiguous() && m.is_contiguous() && v.is_contiguous() && flat.numel() >= P &&
+                  m.numel() >= P && v.numel() >= P, "flat / m / v must hold the reference stack's ", P, " parameters");
+  TORCH_CHECK(x.dim() == 2 && y.dim() == 2 && x.size(1) == 18 && y.size(1) == 18 && x.stride(1) == 1 &&
+                  y.stride(1) == 1 && x.size(0) == y.size(0), "x / y must be [n, 18] row views");
+  const int64_t n = x.size(0);
+  if (order.has_value()) {
+    TORCH_CHECK(order->is_cuda() && order->scalar_type() == at::kInt && order->is_contiguous() && order->numel() == n,
+                "order must be a device int32 permutation of the n samples");
+  }
+  TORCH_CHECK(B >= 1 && B <= 32 && nsteps >= 1 && row0 >= 0 && row0 < n, "bad B / nsteps / row0");
+  c10::hip::HIPGuard guard(x.device().index());
+  auto out = at::zeros({nsteps, 2}, flat.options());
+  SML_CHECK_HIP(sml::lstm_ref_train_launch(flat.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                                           iter.data_ptr<int64_t>(), x.data_ptr<float>(), x.stride(0),
+                                           y.data_ptr<float>(), y.stride(0),
+                                           order.has_value() ? order->data_ptr<int32_t>() : nullptr, n, row0, (int)B,
+                                           (int)nsteps, (int)act, (float)lr, (float)beta1, (float)beta2, (float)eps,
+                                           out.data_ptr<float>(), cur_stream(x)));
+  return out;
 }
 
 // K3 + K6: (y_pred - y) * gscale -> grad, [sum sq err, #correct rows] += into acc.
@@ -771,6 +810,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("c"), py::arg("h"), py::arg("x"), py::arg("h0") = py::none(), py::arg("c0") = py::none(),
         py::arg("W"), py::arg("U"), py::arg("b"), py::arg("act") = 1, py::arg("want_dx") = true,
         py::arg("want_state_grads") = false, py::arg("dh_last_only") = false);
+  m.def("lstm_ref_train", &lstm_ref_train,
+        "persistent trainer: nsteps Keras Adam steps of the reference LSTM stack (look_back 1) in one launch",
+        py::arg("flat"), py::arg("m"), py::arg("v"), py::arg("iter"), py::arg("x"), py::arg("y"),
+        py::arg("order") = py::none(), py::arg("row0") = 0, py::arg("B") = 1, py::arg("nsteps") = 1,
+        py::arg("act") = 1, py::arg("lr") = 1e-3, py::arg("beta1") = 0.9, py::arg("beta2") = 0.999,
+        py::arg("eps") = 1e-7);
+  m.def("lstm_ref_train_params", &sml::lstm_ref_train_params);
   m.def("lstm_fused_supported", &sml::lstm_fused_supported, "whether (U, IN) has a fused LSTM kernel", py::arg("U"),
         py::arg("IN"));
   py::class_<ServePy>(m, "AEServe", "persistent per-event autoencoder scorer over host-mapped rings")

@@ -176,6 +176,25 @@ class WindowStream:
             carry = rows[-need:] if need > 0 else rows[:0]
 
 
+def sliding_windows(rows, look_back: int, horizon: int = 1):
+    """Device-side ``window(look_back, shift=1)`` + ``skip(look_back)`` targets
+    (LSTM-TensorFlow-IO-Kafka/cardata-v2.py:199-206) WITHOUT materialising the windows:
+    ``X[b] = rows[b : b + look_back]`` is a strided view ``[n, T, F]`` with sequence
+    stride F (one row), ``Y[b] = rows[b + look_back + horizon - 1]``.  The fused LSTM
+    kernels read X in place (each base row is fetched once per window that contains it,
+    from L2 / Infinity Cache, not T copies in HBM)."""
+    T, h = int(look_back), int(horizon)
+    if rows.dim() != 2 or not rows.is_contiguous():
+        raise ValueError("rows must be a contiguous [N, F] tensor")
+    n = rows.size(0) - T - h + 1
+    if n <= 0:
+        raise ValueError("fewer rows than look_back + horizon")
+    F = rows.size(1)
+    X = rows.as_strided((n, T, F), (F, F, 1), rows.storage_offset())
+    Y = rows[T + h - 1:T + h - 1 + n]
+    return X, Y
+
+
 # ---------------------------------------------------------------------------
 # sources
 # ---------------------------------------------------------------------------

@@ -112,6 +112,7 @@ class LSTMPredictor:
         self.opt = FlatAdam(self.fp, **self.hp)
         self._acc = np.zeros(4)   # loss*n, correct, n, batches
         self.stop_training = False
+        self.last_fit_engine = None
 
     @classmethod
     def reference(cls, look_back: int = 1, **kw) -> "LSTMPredictor":
@@ -157,8 +158,13 @@ class LSTMPredictor:
     # ------------------------------------------------------------------ training
     def fit(self, x, y=None, epochs: int = 1, batch_size: int = 1, verbose: int = 1, take: Optional[int] = None,
             callbacks: Optional[Sequence[Callback]] = None, shuffle: bool = False, normalize: bool = True,
-            initial_epoch: int = 0, seed: int = 0):
-        """``x``: windows [n, T, F] + ``y`` next rows [n, F], or a Stream (windows built here)."""
+            initial_epoch: int = 0, seed: int = 0, engine: str = "auto"):
+        """``x``: windows [n, T, F] + ``y`` next rows [n, F], or a Stream (windows built here).
+
+        ``engine``: ``"persistent"`` runs each epoch as ONE launch of the Keras-step kernel
+        (``ops/lstm_persistent.py``; the reference stack at look_back 1, batch <= 32,
+        one replica), ``"autograd"`` one fused-kernel train_step per batch, ``"auto"``
+        the persistent kernel whenever it applies."""
         from ..data.stream import Stream
         from ..parallel.dp import allreduce_sum_
         import torch.distributed as dist
@@ -171,21 +177,52 @@ class LSTMPredictor:
             cb.set_model(self)
         if isinstance(x, Stream):
             st = x.normalize() if normalize else x
-            wins = [w for w in st.windows(self.look_back)]
-            xs = np.concatenate([w[0] for w in wins]) if wins else np.zeros((0, self.look_back, self.features))
-            ys = np.concatenate([w[1] for w in wins]) if wins else np.zeros((0, self.features))
+            if self.device.type == "cuda":
+                # the event rows go to the device once; windows are strided views over them
+                # (sliding_windows), read in place by the fused LSTM kernels
+                from ..data.stream import sliding_windows
+                rows = st.collect().x
+                if world > 1:   # contiguous row shard per replica (+ the look_back overlap)
+                    from ..parallel.dp import shard_range
+                    nw = max(len(rows) - self.look_back, 0)
+                    s0, s1 = shard_range(nw, dist.get_rank(), world)
+                    rows = rows[s0:s1 + self.look_back]
+                base = torch.as_tensor(np.ascontiguousarray(rows, np.float32), device=self.device)
+                xd, yd = sliding_windows(base, self.look_back)
+                world_sharded = True
+            else:
+                wins = [w for w in st.windows(self.look_back)]
+                xs = np.concatenate([w[0] for w in wins]) if wins else np.zeros((0, self.look_back, self.features))
+                ys = np.concatenate([w[1] for w in wins]) if wins else np.zeros((0, self.features))
+                world_sharded = False
         else:
             xs, ys = np.asarray(x, np.float32), np.asarray(y, np.float32)
-        if world > 1:   # each replica trains on its contiguous shard (same contract as Autoencoder.fit)
-            from ..parallel.dp import shard_range
-            s0, s1 = shard_range(len(xs), dist.get_rank(), world)
-            xs, ys = xs[s0:s1], ys[s0:s1]
-        xd = torch.as_tensor(xs, dtype=torch.float32, device=self.device)
-        yd = torch.as_tensor(ys, dtype=torch.float32, device=self.device)
+            world_sharded = False
+        if not isinstance(x, Stream) or self.device.type != "cuda":
+            if world > 1 and not world_sharded:   # contiguous shard per replica (as Autoencoder.fit)
+                from ..parallel.dp import shard_range
+                s0, s1 = shard_range(len(xs), dist.get_rank(), world)
+                xs, ys = xs[s0:s1], ys[s0:s1]
+            xd = torch.as_tensor(xs, dtype=torch.float32, device=self.device)
+            yd = torch.as_tensor(ys, dtype=torch.float32, device=self.device)
         n = len(xd)
         nb = math.ceil(n / batch_size)
         if take is not None:
             nb = min(nb, take)
+        from ..ops import lstm_persistent as lp
+        persistent = engine == "persistent" or (
+            engine == "auto" and world == 1 and lp.supported(self) and batch_size <= lp.MAX_BATCH and n > 0)
+        if persistent:
+            if not (lp.supported(self) and world == 1 and batch_size <= lp.MAX_BATCH):
+                raise ValueError("engine='persistent' needs the reference stack at look_back 1, batch <= "
+                                 f"{lp.MAX_BATCH}, one replica")
+            if not lp.check_inactive(self):
+                raise RuntimeError("recurrent / forget-gate Adam moments are non-zero: the look_back-1 kernel "
+                                   "would not reproduce their Keras updates (use engine='autograd')")
+            self.last_fit_engine = "persistent"
+            return self._fit_persistent(xd, yd, n, nb, epochs, batch_size, verbose, cbs, hist, shuffle, seed,
+                                        initial_epoch)
+        self.last_fit_engine = "autograd"
         from ..parallel.fault import maybe_inject
         rank = dist.get_rank() if world > 1 else 0
         gstep = 0
@@ -208,6 +245,30 @@ class LSTMPredictor:
                 tot_corr += corr
                 rows += len(xb)
             logs = {"loss": float(tot_loss) / max(rows, 1), "accuracy": float(tot_corr) / max(rows, 1),
+                    "_seconds": time.perf_counter() - t0, "_rows": rows}
+            if verbose:
+                print(f"Epoch {epoch + 1}/{epochs} - {nb} steps - loss: {logs['loss']:.4f} - "
+                      f"accuracy: {logs['accuracy']:.4f}", flush=True)
+            for cb in cbs:
+                cb.on_epoch_end(epoch, logs)
+            if self.stop_training:
+                break
+        return hist
+
+    def _fit_persistent(self, xd, yd, n, nb, epochs, batch_size, verbose, cbs, hist, shuffle, seed, initial_epoch):
+        from ..ops import lstm_persistent as lp
+        for epoch in range(initial_epoch, epochs):
+            t0 = time.perf_counter()
+            order = None
+            if shuffle:
+                order = torch.as_tensor(np.random.default_rng([seed, 0, epoch]).permutation(n).astype(np.int32),
+                                        device=self.device)
+            out = lp.train_steps(self, xd, yd, batch_size, nb, 0, order)
+            rows = min(n, nb * batch_size)
+            sizes = torch.full((nb,), float(batch_size), device=self.device)
+            sizes[-1] = float(rows - (nb - 1) * batch_size)
+            tot = torch.stack([(out[:, 0] * sizes).sum(), out[:, 1].sum()]).cpu()
+            logs = {"loss": float(tot[0]) / max(rows, 1), "accuracy": float(tot[1]) / max(rows, 1),
                     "_seconds": time.perf_counter() - t0, "_rows": rows}
             if verbose:
                 print(f"Epoch {epoch + 1}/{epochs} - {nb} steps - loss: {logs['loss']:.4f} - "

@@ -139,9 +139,12 @@ def lstm(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor, act
     ``return_sequences=False`` returns h_T [B, U] (Keras semantics)."""
     if x.is_cuda:
         if fused and fused_supported(U.shape[0], x.shape[-1]):
-            xc = x.contiguous()
+            # sliding windows (consecutive rows per step, any sequence stride) are read
+            # in place by the fused kernels: no [B, T, F] materialisation
+            windowed = x.dim() == 3 and x.stride(2) == 1 and x.stride(1) == x.shape[2] and x.stride(0) >= 0
+            xc = x if windowed else x.contiguous()
             if xc.dtype not in (torch.float32, torch.bfloat16):
-                xc = xc.float()
+                xc = xc.float().contiguous()
             return FusedLSTMFunction.apply(xc, W, U, b, ACT[activation], not return_sequences)
         hs = LSTMFunction.apply(x.contiguous().float(), W, U, b, ACT[activation])
     else:

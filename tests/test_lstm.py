@@ -70,3 +70,19 @@ def test_save_load_roundtrip(tmp_path):
     ck = load_keras_h5(p)
     assert [n for n, _ in ck.weights["lstm"]] == ["lstm/kernel:0", "lstm/recurrent_kernel:0", "lstm/bias:0"]
     assert ck.model_config["class_name"] == "Sequential"
+
+
+def test_persistent_trainer_skips_exactly_the_zero_gradient_parameters():
+    """look_back 1: U and the forget-gate columns get zero gradient; the persistent kernel
+    carries the other 6 450 of the 18 642 parameters."""
+    from streamml.ops import lstm_persistent as lp
+    m = LSTMPredictor.reference(look_back=1, device="cpu", seed=0)
+    assert m.count_params() == 18642
+    assert int((~lp._inactive_mask(m))[:m.fp.n].sum()) == 6450
+    assert not lp.supported(m)              # CPU model: the autograd path
+    x = torch.randn(5, 1, 18)
+    y = torch.randn(5, 18)
+    m.train_step(x, y)
+    g = m.fp.grad[lp._inactive_mask(m)]
+    assert float(g.abs().max()) == 0.0
+    assert lp.check_inactive(m)

@@ -119,3 +119,43 @@ def test_graph_replayed_train_steps_match_eager(cuda_device):
     torch.cuda.synchronize()
     torch.testing.assert_close(graphed.fp.flat, eager.fp.flat, rtol=0, atol=0)
     torch.testing.assert_close(loss_g, loss_e, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("stack", ["two_layer", "reference"])
+def test_in_place_windows_match_materialized(cuda_device, stack):
+    """Sliding windows read in place (strided [n, T, F] views over the event rows, sequence
+    stride one row) give bit-identical forward outputs, gradients and Adam updates to the
+    same windows copied out ([n, T, F] contiguous) -- the fused kernels read x[start + t]."""
+    from streamml.data.stream import sliding_windows
+    T = 12 if stack == "two_layer" else 1
+    ctor = LSTMPredictor.two_layer if stack == "two_layer" else LSTMPredictor.reference
+    rows = torch.tensor(np.random.default_rng(5).uniform(-1, 1, (300 + T, 18)), dtype=torch.float32,
+                        device=cuda_device)
+    Xv, Yv = sliding_windows(rows, T)
+    assert Xv.data_ptr() == rows.data_ptr() and not Xv.is_contiguous() or T == 1
+    Xc, Yc = Xv.contiguous(), Yv.contiguous()
+    a = ctor(look_back=T, device=cuda_device, seed=2)
+    b = ctor(look_back=T, device=cuda_device, seed=2)
+    torch.testing.assert_close(a.forward(Xv), b.forward(Xc), rtol=0, atol=0)
+    for s in range(3):
+        sl = slice(s * 100, (s + 1) * 100)
+        la, _ = a.train_step(Xv[sl], Yv[sl])
+        lb, _ = b.train_step(Xc[sl], Yc[sl])
+        torch.testing.assert_close(la, lb, rtol=0, atol=0)
+    torch.testing.assert_close(a.fp.flat, b.fp.flat, rtol=0, atol=0)
+
+
+def test_fit_stream_uses_in_place_windows(cuda_device):
+    """LSTMPredictor.fit(Stream) on the GPU builds device windows as views; same history as
+    fit on the host-materialised window arrays."""
+    from streamml.data import stream as S
+    x = np.random.default_rng(9).uniform(0, 50, (600, 18)).astype(np.float32)
+    st = S.from_arrays(x, chunk=128)
+    wins = list(st.normalize().windows(8))
+    xs, ys = np.concatenate([w[0] for w in wins]), np.concatenate([w[1] for w in wins])
+    a = LSTMPredictor.two_layer(look_back=8, device=cuda_device, seed=4)
+    b = LSTMPredictor.two_layer(look_back=8, device=cuda_device, seed=4)
+    ha = a.fit(st, epochs=2, batch_size=64, verbose=0)
+    hb = b.fit(xs, ys, epochs=2, batch_size=64, verbose=0)
+    assert ha.history["loss"] == hb.history["loss"]
+    torch.testing.assert_close(a.fp.flat, b.fp.flat, rtol=0, atol=0)

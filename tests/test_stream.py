@@ -2,6 +2,7 @@
 import os
 
 import numpy as np
+import pytest
 
 from streamml.data import stream as S
 from streamml.data.cardata import FEATURES, normalize_np
@@ -56,6 +57,20 @@ def test_windows_cross_chunk_boundaries():
     for i in range(50 - T):
         np.testing.assert_array_equal(xs[i], x[i:i + T])
         np.testing.assert_array_equal(ys[i], x[i + T])
+
+
+@pytest.mark.parametrize("T,h", [(4, 1), (1, 1), (5, 3)])
+def test_sliding_windows_are_views_equal_to_window_stream(T, h):
+    import torch
+    x = np.random.default_rng(T).standard_normal((40, 18)).astype(np.float32)
+    wins = list(S.from_arrays(x, chunk=9).windows(T, h))
+    xs = np.concatenate([w[0] for w in wins])
+    ys = np.concatenate([w[1] for w in wins])
+    base = torch.from_numpy(x)
+    X, Y = S.sliding_windows(base, T, h)
+    assert X.data_ptr() == base.data_ptr() and X.stride() == (18, 18, 1)   # no copy
+    np.testing.assert_array_equal(X.numpy(), xs)
+    np.testing.assert_array_equal(Y.numpy(), ys)
 
 
 def test_label_codes():
