@@ -19,6 +19,53 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100):
+    """Append -> visible latency through the real serving path: a paced C++ producer
+    appends Confluent-Avro car events (one produce request each, keyed by car) to an
+    in-process broker at ``qps``; the ``serve --low-latency`` loop (long-poll fetch,
+    C++ decode, persistent GPU scorer, C++ JSON records, produce acks=1) runs in its own
+    thread.  Latency of an event = its result's produce ack minus the moment the
+    producer started sending it (same steady clock)."""
+    import threading
+
+    import numpy as np
+    from streamml.data.avro import AvroCodec
+    from streamml.data.produce import encode_chunk
+    from streamml.kafka import fake_broker
+    from streamml.kafka.scoreloop import LowLatencyScorer, paced_produce
+    from streamml.ops.serve import ScoringServer
+
+    n = events + warm
+    name = f"bench-e2e-{os.getpid()}-{rank}"
+    b = fake_broker(name)
+    b.create_topic("SENSOR_DATA_S_AVRO", 1)
+    b.create_topic("model-predictions", 1)
+    buf, offs = encode_chunk(AvroCodec("cardata-v1"), np.ascontiguousarray(ev[:n], np.float32),
+                             np.zeros(n, np.uint8))
+    keys = [f"car{i % 1000}" for i in range(n)]
+    out = {}
+    with ScoringServer(m, threshold=threshold, slots=4096) as srv:
+        loop = LowLatencyScorer(f"fake://{name}", "SENSOR_DATA_S_AVRO", "model-predictions", [0], srv, starts=[0],
+                                max_wait_ms=100, record_latency=True)
+        th = threading.Thread(target=lambda: out.update(loop.run(max_events=n, idle_timeout_s=10.0)))
+        th.start()
+        sent = paced_produce(f"fake://{name}", "SENSOR_DATA_S_AVRO", 0, bytes(buf), offs, keys=keys, qps=qps)
+        th.join(120)
+    lat = loop.latency_records()
+    vis = lat[np.argsort(lat[:, 1]), 2]
+    d = (vis[warm:] - sent[warm:]) / 1e3
+    st = out
+    ev_n = max(st.get("events", 1), 1)
+    return {"p50_us": float(np.percentile(d, 50)), "p99_us": float(np.percentile(d, 99)),
+            "max_us": float(d.max()), "events": int(len(d)), "offered_qps": qps,
+            "results": int(b.end_offset("model-predictions", 0)),
+            "batches": st.get("batches"), "events_per_batch": ev_n / max(st.get("batches", 1), 1),
+            "per_event_us": {k[:-2]: st[k] / ev_n * 1e6 for k in ("fetch_s", "decode_s", "score_s", "format_s",
+                                                                 "produce_s", "commit_s") if k in st},
+            "path": "paced producer -> broker (long-poll) -> C++ decode -> persistent GPU scorer -> "
+                    "C++ JSON -> produce acks=1"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default=None, help=".h5 to load (default: save a fresh 18-dim AE first)")
@@ -74,6 +121,8 @@ def main():
         for k in range(20):
             srv.score(ev[:4096])
         srv_eps = 20 * 4096 / (time.perf_counter() - t0)
+    # Kafka append -> result record visible (serve --low-latency: C++ loop + persistent scorer)
+    e2e = kafka_e2e(m, ev, args.qps, args.threshold, args.events, env.rank)
     # batched throughput
     big = synthetic_device_tensor(args.batch * 8, dev, seed=1)
     for _ in range(3):
@@ -107,7 +156,9 @@ def main():
                           "persistent_device_compute_p50_us": float(np.percentile(pcomp, 50)),
                           "persistent_relaunches": relaunches,
                           "offered_qps": args.qps, "events": args.events, "n_gpus": env.world_size,
-                          "batched_events_per_s": eps_all, "batch": args.batch, "data": "synthetic"}))
+                          "batched_events_per_s": eps_all, "batch": args.batch, "data": "synthetic",
+                          "kafka_e2e_p50_us": e2e["p50_us"], "kafka_e2e_p99_us": e2e["p99_us"],
+                          "kafka_e2e": e2e}))
     dp.shutdown()
 
 

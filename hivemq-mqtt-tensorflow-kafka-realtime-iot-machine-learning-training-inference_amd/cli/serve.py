@@ -16,6 +16,11 @@ only (cardata-v3.py:46) and writes reconstructions (cardata-v3.py:243-249). Here
   topic keyed by car: ``{"car", "partition", "offset", "score", "anomaly"}``, plus the
   reconstruction with ``--emit both`` (what the reference streams).
 
+``--low-latency``: the whole per-event path runs in one C++ thread per replica
+(:class:`streamml.kafka.scoreloop.LowLatencyScorer`): long-poll fetch -> Avro decode ->
+the persistent GPU scorer (:class:`streamml.ops.serve.ScoringServer`, no launch per
+event) -> the same result records formatted in C++ -> one produce per fetch -> commit.
+
 Replica identity comes from ``--replica-index/--replicas``, else torchrun's
 ``RANK/WORLD_SIZE``, else ``REPLICA_INDEX/REPLICAS`` (a StatefulSet ordinal), else 0/1.
 """
@@ -28,6 +33,7 @@ from typing import List, Sequence, Tuple
 
 import numpy as np
 
+from ..ops._ext import load_io
 from . import common
 
 USAGE = ("python -m streamml.cli serve <servers> <topic> <result_topic> <model-file> "
@@ -65,6 +71,37 @@ def _flags(p) -> None:
     p.add_argument("--synthetic-partitions", type=int, default=8)
     p.add_argument("--metrics-port", type=int, default=0)
     p.add_argument("--schema", default="cardata-v1")
+    p.add_argument("--low-latency", action="store_true",
+                   help="C++ fetch/decode/score/format/produce loop on the persistent GPU scorer")
+    p.add_argument("--max-wait-ms", type=int, default=100, help="long-poll bound of the low-latency loop")
+
+
+def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary) -> int:
+    from ..kafka.scoreloop import LowLatencyScorer
+    from ..obs.metrics import ENGINE
+    from ..ops.serve import ScoringServer
+
+    if model.device.type != "cuda":
+        raise SystemExit("--low-latency needs a ROCm device (the persistent scorer)")
+    with ScoringServer(model, threshold=ns.threshold) as srv:
+        starts = None
+        if ns.from_beginning:
+            from ..kafka import KafkaClient
+            c = KafkaClient(servers, cfg)
+            starts = [c.earliest(ns.topic, p) for p in mine]
+        loop = LowLatencyScorer(servers, ns.topic, ns.result_topic, mine, srv, schema=ns.schema, group=ns.group,
+                                starts=starts, result_partitions=[p % result_parts for p in mine],
+                                emit_recon=ns.emit == "both", config=cfg, max_batch=min(ns.max_batch, 4096),
+                                max_wait_ms=ns.max_wait_ms)
+        st = loop.run(max_events=ns.max_events, idle_timeout_s=ns.idle_timeout)
+    ENGINE.infer_rows.inc(st["events"], model=model.name)
+    ENGINE.anomaly_events.inc(st["anomalies"], model=model.name)
+    summary.update(events=st["events"], anomalies=st["anomalies"], skipped=st["skipped"],
+                   events_per_s=st["events"] / st["wall_s"] if st["wall_s"] > 0 else 0.0, low_latency=True,
+                   stages_s={k: st[k] for k in ("fetch_s", "decode_s", "score_s", "format_s", "produce_s",
+                                                 "commit_s")})
+    print(json.dumps(summary), flush=True)
+    return 0
 
 
 def main(argv: Sequence[str]) -> int:
@@ -109,6 +146,8 @@ def main(argv: Sequence[str]) -> int:
         print(json.dumps(summary), flush=True)
         return 0
 
+    if ns.low_latency:
+        return _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary)
     start = -2 if ns.from_beginning else 0
     topics = [f"{ns.topic}:{p}:{start}" for p in mine]
     stream = kafka(servers, topics, schema=ns.schema, group=ns.group, eof=False, config=cfg, commit=True,
@@ -121,7 +160,8 @@ def main(argv: Sequence[str]) -> int:
         if sink is None:   # results keep the source partition: a car's scores stay ordered
             sink = sinks[part] = KafkaOutputSequence(ns.result_topic, servers, cfg, partition=part % result_parts)
             next_index[part] = 0
-        ok = chunk.label != LABEL_MISSING          # undecodable records are skipped, not scored
+        ok = chunk.meta.get("ok")                  # undecodable records are skipped, not scored
+        ok = (chunk.label != LABEL_MISSING) if ok is None else ok.astype(bool)
         if not ok.all():
             chunk = chunk.select(ok)
         if len(chunk) == 0:
@@ -136,12 +176,11 @@ def main(argv: Sequence[str]) -> int:
         dt_us = (time.perf_counter() - t_batch) * 1e6 / len(chunk)
         keys = chunk.keys or [None] * len(chunk)
         offs = chunk.offsets if chunk.offsets is not None else np.arange(len(chunk))
+        # json.dumps({car, partition, offset, score, anomaly[, reconstruction]}) per event, in C++
+        recs = load_io().score_records(list(keys), part, np.asarray(offs, np.int64), np.asarray(scores, np.float32),
+                                       np.asarray(flags, np.uint8), recon)
         for i in range(len(chunk)):
-            rec = {"car": keys[i], "partition": part, "offset": int(offs[i]), "score": float(scores[i]),
-                   "anomaly": bool(flags[i])}
-            if recon is not None:
-                rec["reconstruction"] = np.array2string(recon[i])
-            sink.setitem(next_index[part], json.dumps(rec), key=keys[i])
+            sink.setitem(next_index[part], recs[i], key=keys[i])
             next_index[part] += 1
         sink.flush()   # produced before the dataset commits this batch's offsets (at-least-once)
         n_flag = int(flags.sum())

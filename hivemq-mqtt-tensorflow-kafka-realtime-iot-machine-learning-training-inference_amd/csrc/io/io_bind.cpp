@@ -8,6 +8,8 @@
 
 #include "avro.h"
 #include "feed.h"
+#include "format.h"
+#include "scoreloop.h"
 #include "h5.h"
 #include "kafka.h"
 #include "mqtt.h"
@@ -382,6 +384,188 @@ PYBIND11_MODULE(_io, m) {
       .def_property_readonly("bytes_received", &kafka::Client::bytes_received);
 
   // native ingest feed: worker threads decode Kafka records straight into caller slabs
+  // ---- low-latency streaming scorer (scoreloop.h) ----
+  struct EchoScorer {   // CPU stand-in for the GPU scorer (tests): score = mean(x^2), recon = x / 2
+    SmlScorerApi api{};
+    float thr;
+    static int infer(void* ctx, const float* rows, int k, float* scores, uint32_t* flags, float* recon, double) {
+      auto* self = static_cast<EchoScorer*>(ctx);
+      const int D = self->api.dim;
+      for (int i = 0; i < k; ++i) {
+        float s = 0.0f;
+        for (int j = 0; j < D; ++j) {
+          const float x = rows[(size_t)i * D + j];
+          s += x * x;
+          if (recon) recon[(size_t)i * D + j] = 0.5f * x;
+        }
+        scores[i] = s / (float)D;
+        flags[i] = scores[i] > self->thr ? 1u : 0u;
+      }
+      return 0;
+    }
+  };
+  py::class_<EchoScorer>(m, "EchoScorer")
+      .def(py::init([](int dim, float threshold) {
+             auto* e = new EchoScorer();
+             e->api.version = SML_SCORER_API_VERSION;
+             e->api.dim = dim;
+             e->api.ctx = e;
+             e->api.infer = &EchoScorer::infer;
+             e->api.last_error = nullptr;
+             e->thr = threshold;
+             return e;
+           }),
+           py::arg("dim"), py::arg("threshold") = 5.0f)
+      .def("c_api", [](EchoScorer& e) { return reinterpret_cast<uintptr_t>(&e.api); });
+  py::class_<serve::ScoreLoop>(m, "ScoreLoop")
+      .def(py::init([](const std::string& bootstrap, const std::string& client_id, const std::string& mech,
+                       const std::string& user, const std::string& pw, int timeout_ms, const py::list& fields,
+                       const std::string& topic, const std::string& result_topic, const std::string& group,
+                       std::vector<int> partitions, std::vector<int64_t> starts, std::vector<int> result_partitions,
+                       std::vector<int> feature_fields, bool framing, bool emit_recon, int max_batch,
+                       int32_t max_bytes, int32_t max_wait_ms, double commit_interval_s, bool record_latency,
+                       uintptr_t api) {
+             kafka::ClientConfig c;
+             c.client_id = client_id;
+             c.sasl_mechanism = mech;
+             c.sasl_username = user;
+             c.sasl_password = pw;
+             c.timeout_ms = timeout_ms;
+             serve::LoopConfig lc;
+             lc.topic = topic;
+             lc.result_topic = result_topic;
+             lc.group = group;
+             lc.partitions = std::move(partitions);
+             lc.starts = std::move(starts);
+             lc.result_partitions = std::move(result_partitions);
+             lc.feature_fields = std::move(feature_fields);
+             lc.framing = framing;
+             lc.emit_recon = emit_recon;
+             lc.max_batch = max_batch;
+             lc.max_bytes = max_bytes;
+             lc.max_wait_ms = max_wait_ms;
+             lc.commit_interval_s = commit_interval_s;
+             lc.record_latency = record_latency;
+             return new serve::ScoreLoop(bootstrap, c, fields_from_py(fields), lc,
+                                         reinterpret_cast<const SmlScorerApi*>(api));
+           }),
+           py::arg("bootstrap"), py::arg("client_id"), py::arg("sasl_mechanism"), py::arg("sasl_username"),
+           py::arg("sasl_password"), py::arg("timeout_ms"), py::arg("fields"), py::arg("topic"),
+           py::arg("result_topic"), py::arg("group"), py::arg("partitions"), py::arg("starts"),
+           py::arg("result_partitions"), py::arg("feature_fields"), py::arg("framing"), py::arg("emit_recon"),
+           py::arg("max_batch"), py::arg("max_bytes"), py::arg("max_wait_ms"), py::arg("commit_interval_s"),
+           py::arg("record_latency"), py::arg("scorer_api"))
+      .def("run",
+           [](serve::ScoreLoop& l, int64_t max_events, double idle_timeout_s) {
+             serve::LoopStats st;
+             {
+               py::gil_scoped_release nogil;
+               st = l.run(max_events, idle_timeout_s);
+             }
+             py::dict d;
+             d["events"] = st.events;
+             d["anomalies"] = st.anomalies;
+             d["skipped"] = st.skipped;
+             d["batches"] = st.batches;
+             d["fetches"] = st.fetches;
+             d["empty_fetches"] = st.empty_fetches;
+             d["commits"] = st.commits;
+             d["fetch_s"] = st.fetch_s;
+             d["decode_s"] = st.decode_s;
+             d["score_s"] = st.score_s;
+             d["format_s"] = st.format_s;
+             d["produce_s"] = st.produce_s;
+             d["commit_s"] = st.commit_s;
+             d["wall_s"] = st.wall_s;
+             return d;
+           },
+           py::arg("max_events") = 0, py::arg("idle_timeout_s") = -1.0)
+      .def("stop", &serve::ScoreLoop::stop)
+      .def("positions", &serve::ScoreLoop::positions)
+      .def("latency_records", [](serve::ScoreLoop& l) {
+        const auto& v = l.latency_records();
+        py::array_t<int64_t> a(std::vector<ssize_t>{(ssize_t)(v.size() / 3), 3});
+        std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(int64_t));
+        return a;
+      });
+  m.def("paced_produce",
+        [](const std::string& bootstrap, const std::string& topic, int partition, const py::bytes& values,
+           std::vector<int64_t> offs, py::object keys, double qps) {
+          std::string vals = values;
+          std::vector<std::string> ks;
+          if (!keys.is_none())
+            for (auto h : keys.cast<py::list>()) ks.push_back(py::isinstance<py::bytes>(h) ? h.cast<std::string>()
+                                                                                     : py::str(h).cast<std::string>());
+          std::vector<int64_t> sent;
+          {
+            py::gil_scoped_release nogil;
+            sent = serve::paced_produce(bootstrap, kafka::ClientConfig(), topic, partition, vals, offs, ks, qps);
+          }
+          return py::array_t<int64_t>((ssize_t)sent.size(), sent.data());
+        },
+        py::arg("bootstrap"), py::arg("topic"), py::arg("partition"), py::arg("values"), py::arg("offsets"),
+        py::arg("keys") = py::none(), py::arg("qps") = 10000.0,
+        "append records one produce request each at `qps`; -> steady-clock send time (ns) per record");
+  m.def("steady_ns", &serve::steady_ns);
+
+  // ---- result-record formatting (format.h) ----
+  m.def("array2string_f32",
+        [](py::array_t<float, py::array::c_style | py::array::forcecast> a) {
+          std::string out;
+          fmt::array2string_f32(a.data(), (int)a.size(), out);
+          return out;
+        },
+        "numpy.array2string of a 1-D float32 array (default options), in C++");
+  m.def("json_float", [](double v) {
+    std::string out;
+    fmt::py_float_repr(v, out);
+    return out;
+  });
+  m.def("score_records",
+        [](py::object keys, int partition, py::array_t<int64_t, py::array::c_style | py::array::forcecast> offsets,
+           py::array_t<float, py::array::c_style | py::array::forcecast> scores,
+           py::array_t<uint8_t, py::array::c_style | py::array::forcecast> flags, py::object recon) {
+          const int64_t k = scores.size();
+          if (offsets.size() != k || flags.size() != k) throw std::invalid_argument("score_records: length mismatch");
+          std::vector<std::string> ks;
+          std::vector<char> knull((size_t)k, 1);
+          if (!keys.is_none()) {
+            py::list kl = keys;
+            if ((int64_t)kl.size() != k) throw std::invalid_argument("score_records: keys length mismatch");
+            ks.resize((size_t)k);
+            for (int64_t i = 0; i < k; ++i) {
+              py::handle h = kl[(size_t)i];
+              if (h.is_none()) continue;
+              knull[(size_t)i] = 0;
+              if (py::isinstance<py::bytes>(h)) ks[(size_t)i] = h.cast<std::string>();
+              else ks[(size_t)i] = py::str(h).cast<std::string>();
+            }
+          }
+          py::array_t<float, py::array::c_style | py::array::forcecast> rec;
+          int D = 0;
+          if (!recon.is_none()) {
+            rec = recon.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+            if (rec.ndim() != 2 || rec.shape(0) != k) throw std::invalid_argument("score_records: recon must be [k, D]");
+            D = (int)rec.shape(1);
+          }
+          std::vector<std::string> out((size_t)k);
+          {
+            py::gil_scoped_release nogil;
+            for (int64_t i = 0; i < k; ++i) {
+              const bool kn = ks.empty() || knull[(size_t)i];
+              fmt::score_record_json(kn ? nullptr : reinterpret_cast<const uint8_t*>(ks[(size_t)i].data()),
+                                     kn ? -1 : (int64_t)ks[(size_t)i].size(), partition, offsets.data()[i],
+                                     scores.data()[i], flags.data()[i] != 0, D ? rec.data() + i * D : nullptr, D,
+                                     out[(size_t)i]);
+            }
+          }
+          py::list res;
+          for (auto& r : out) res.append(py::bytes(r));
+          return res;
+        },
+        py::arg("keys"), py::arg("partition"), py::arg("offsets"), py::arg("scores"), py::arg("flags"),
+        py::arg("recon") = py::none(),
+        "the serve result records (json.dumps of {car, partition, offset, score, anomaly[, reconstruction]}) in C++");
   m.def("label_code", [](const py::bytes& b) {
     std::string_view s = b;
     return (int)feed::label_code(reinterpret_cast<const uint8_t*>(s.data()), s.size());

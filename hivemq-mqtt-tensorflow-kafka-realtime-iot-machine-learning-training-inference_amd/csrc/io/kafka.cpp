@@ -788,6 +788,10 @@ Broker::~Broker() { stop(); }
 
 void Broker::stop() {
   if (!running_.exchange(false)) return;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    data_cv_.notify_all();
+  }
   ::shutdown(listen_fd_, SHUT_RDWR);
   ::close(listen_fd_);
   if (accept_thread_.joinable()) accept_thread_.join();
@@ -843,6 +847,7 @@ int64_t Broker::append_locked(Partition& p, const Record* recs, size_t n) {
     if (drop) p.segs.erase(p.segs.begin(), p.segs.begin() + (std::ptrdiff_t)drop);
   }
   p.start = p.segs.empty() ? p.end : p.segs.front().base;
+  data_cv_.notify_all();   // wake long-polling fetches
   return base;
 }
 
@@ -900,9 +905,9 @@ size_t Broker::FetchReply::total() const {
 Broker::FetchReply Broker::handle_fetch(const uint8_t* body, size_t n) {
   R r{body, n};
   const uint64_t nth = ++fetches_;
-  r.i32();
-  r.i32();   // max wait: the log is local, every fetch answers at once
-  r.i32();
+  r.i32();                              // replica id
+  const int32_t max_wait_ms = r.i32();  // long poll: an empty fetch waits up to this long
+  const int32_t min_bytes = r.i32();    //   for at least one byte of new records
   r.i32();
   r.i8();
   struct Want {
@@ -928,34 +933,54 @@ Broker::FetchReply Broker::handle_fetch(const uint8_t* body, size_t n) {
     }
   }
   {
-    std::lock_guard<std::mutex> g(mu_);   // only to pick the segments: the copy runs unlocked
+    // only to pick the segments: the copy runs unlocked.  Kafka's fetch.min.bytes /
+    // fetch.max.wait.ms: when nothing is available yet the request parks on data_cv_
+    // (signalled by every append) instead of returning empty, so a consumer sees a new
+    // record one wake-up after it is appended, without polling.
+    std::unique_lock<std::mutex> g(mu_);
     const int fe = fail_every_.load();
-    for (auto& tp : req)
-      for (Want& wt : tp.second) {
-        auto it = topics_.find(wt.topic);
-        if (fe > 0 && nth % (uint64_t)fe == 0) {
-          ++failures_;
-          wt.err = E_NOT_LEADER;
-          continue;
+    const bool fail = fe > 0 && nth % (uint64_t)fe == 0;
+    auto pick = [&]() {   // -> (any bytes, any error)
+      bool avail = false, errs = false;
+      for (auto& tp : req)
+        for (Want& wt : tp.second) {
+          wt.err = E_NONE;
+          wt.segs.clear();
+          auto it = topics_.find(wt.topic);
+          if (fail) {
+            wt.err = E_NOT_LEADER;
+          } else if (it == topics_.end() || wt.partition < 0 || wt.partition >= (int32_t)it->second.size()) {
+            wt.err = E_UNKNOWN_TOPIC;
+          } else {
+            const Partition& part = it->second[(size_t)wt.partition];
+            wt.hwm = part.end;
+            if (wt.off < part.start || wt.off > part.end) {
+              wt.err = E_OFFSET_OUT_OF_RANGE;
+            } else {
+              auto sg = std::upper_bound(part.segs.begin(), part.segs.end(), wt.off,
+                                         [](int64_t o, const Segment& s_) { return o < s_.base + s_.count; });
+              size_t bytes = 0;
+              for (; sg != part.segs.end() && (bytes == 0 || bytes < (size_t)std::max(wt.pmax, 0)); ++sg) {
+                wt.segs.push_back(sg->bytes);
+                bytes += sg->bytes->size();
+              }
+              avail |= bytes > 0;
+            }
+          }
+          errs |= wt.err != E_NONE;
         }
-        if (it == topics_.end() || wt.partition < 0 || wt.partition >= (int32_t)it->second.size()) {
-          wt.err = E_UNKNOWN_TOPIC;
-          continue;
-        }
-        const Partition& part = it->second[(size_t)wt.partition];
-        wt.hwm = part.end;
-        if (wt.off < part.start || wt.off > part.end) {
-          wt.err = E_OFFSET_OUT_OF_RANGE;
-          continue;
-        }
-        auto sg = std::upper_bound(part.segs.begin(), part.segs.end(), wt.off,
-                                   [](int64_t o, const Segment& s_) { return o < s_.base + s_.count; });
-        size_t bytes = 0;
-        for (; sg != part.segs.end() && (bytes == 0 || bytes < (size_t)std::max(wt.pmax, 0)); ++sg) {
-          wt.segs.push_back(sg->bytes);
-          bytes += sg->bytes->size();
-        }
+      return std::make_pair(avail, errs);
+    };
+    auto st = pick();
+    if (fail) ++failures_;
+    if (!st.first && !st.second && min_bytes > 0 && max_wait_ms > 0) {
+      const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(max_wait_ms);
+      while (running_ && !st.first && !st.second) {
+        const bool timed_out = data_cv_.wait_until(g, deadline) == std::cv_status::timeout;
+        st = pick();
+        if (timed_out) break;
       }
+    }
   }
   FetchReply out;
   W w;

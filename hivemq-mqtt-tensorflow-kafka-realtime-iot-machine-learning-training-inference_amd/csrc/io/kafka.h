@@ -18,6 +18,7 @@
 // (SURVEY.md 5.3).
 #pragma once
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -206,6 +207,7 @@ class Broker {
   std::vector<int> client_fds_;
   std::mutex mu_;
   std::map<std::string, std::vector<Partition>> topics_;
+  std::condition_variable data_cv_;   // appends -> long-polling fetches
   std::map<std::string, int64_t> group_offsets_;  // "group/topic/partition" -> offset
   std::atomic<int> fail_every_{0}, delay_ms_{0};
   std::atomic<uint64_t> fetches_{0}, failures_{0};

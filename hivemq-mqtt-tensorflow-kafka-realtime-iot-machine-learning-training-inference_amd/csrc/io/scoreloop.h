@@ -1,0 +1,91 @@
+// Low-latency streaming scorer: Kafka -> Avro decode -> GPU score -> result records ->
+// Kafka, all in one C++ thread (`serve --low-latency`).
+//
+// The reference's inference job (AUTOENCODER-TensorFlow-IO-Kafka/cardata-v3.py:235-279)
+// is a bounded Keras predict over a KafkaDataset with a per-batch output callback:
+// events wait for a whole batch, every output is formatted in Python
+// (np.array2string) and produced through KafkaOutputSequence.  Here each fetch is
+// scored as soon as it arrives:
+//
+//   * long-poll fetch (fetch.min.bytes = 1, fetch.max.wait.ms): the broker answers the
+//     moment a record is appended, no polling interval;
+//   * records are walked in place (RecordSetCursor) and decoded straight into a row
+//     buffer (feed::Feed's compiled Avro plan);
+//   * the rows go to the persistent GPU scorer through the SmlScorerApi table
+//     (host-mapped request ring, no launch, no hipMemcpy -- runtime/serve.h);
+//   * result records ({car, partition, offset, score, anomaly[, reconstruction]}, byte
+//     for byte what cli/serve.py writes with json.dumps / np.array2string) are
+//     formatted here (format.h) and produced as ONE record batch per fetch (acks = 1);
+//   * offsets are committed to the consumer group after the produce (at-least-once).
+//
+// With `record_latency`, the steady-clock time at which each event's result became
+// visible (produce acknowledged) is kept per input offset, for the append -> visible
+// latency bench (bench/bench_infer.py).
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "avro.h"
+#include "feed.h"
+#include "kafka.h"
+#include "sml_scorer_api.h"
+
+namespace sml {
+namespace serve {
+
+struct LoopConfig {
+  std::string topic, result_topic, group;   // group "" = no offset commits
+  std::vector<int> partitions;              // owned source partitions
+  std::vector<int64_t> starts;              // start offset per owned partition
+  std::vector<int> result_partitions;       // result partition per owned partition
+  std::vector<int> feature_fields;          // schema field of each model feature
+  bool framing = true;
+  bool emit_recon = false;                  // add "reconstruction": np.array2string(recon)
+  int max_batch = 4096;                     // rows per scorer call
+  int32_t max_bytes = 1 << 20;
+  int32_t max_wait_ms = 100;                // long-poll bound
+  double commit_interval_s = 0.0;           // 0: commit after every produced batch
+  bool record_latency = false;
+};
+
+struct LoopStats {
+  uint64_t events = 0, anomalies = 0, skipped = 0, batches = 0, fetches = 0, empty_fetches = 0, commits = 0;
+  double fetch_s = 0, decode_s = 0, score_s = 0, format_s = 0, produce_s = 0, commit_s = 0, wall_s = 0;
+};
+
+class ScoreLoop {
+ public:
+  ScoreLoop(std::string bootstrap, kafka::ClientConfig ccfg, std::vector<avro::Field> fields, LoopConfig cfg,
+            const SmlScorerApi* api);
+  // Blocking: runs until stop(), `max_events` scored events (0 = unbounded) or
+  // `idle_timeout_s` without records (< 0 = unbounded).
+  LoopStats run(int64_t max_events, double idle_timeout_s);
+  void stop() { stop_ = true; }
+  std::vector<int64_t> positions() const;   // next offset per owned partition
+  // (partition, offset, visible_ns) per scored event when record_latency
+  const std::vector<int64_t>& latency_records() const { return lat_; }
+
+ private:
+  std::string bootstrap_;
+  kafka::ClientConfig ccfg_;
+  LoopConfig cfg_;
+  const SmlScorerApi* api_;
+  feed::Feed decoder_;   // only its compiled decode plan is used (never started)
+  std::vector<int64_t> pos_;
+  std::vector<int64_t> lat_;
+  std::atomic<bool> stop_{false};
+};
+
+// Producer side of the latency bench: append records (value i = values[offs[i],
+// offs[i+1]), key i) one produce request per record, paced at `qps`; returns the
+// steady-clock ns just before each request was sent.
+std::vector<int64_t> paced_produce(const std::string& bootstrap, kafka::ClientConfig ccfg, const std::string& topic,
+                                   int partition, const std::string& values, const std::vector<int64_t>& offs,
+                                   const std::vector<std::string>& keys, double qps);
+
+int64_t steady_ns();
+
+}  // namespace serve
+}  // namespace sml

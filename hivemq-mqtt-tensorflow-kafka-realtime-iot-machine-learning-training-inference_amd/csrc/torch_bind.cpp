@@ -11,6 +11,7 @@
 #include "sml_ops.h"
 #include "../runtime/p2p.h"
 #include "sml_p2p.h"
+#include "sml_scorer_api.h"
 #include "../runtime/ring.h"
 #include "../runtime/serve.h"
 
@@ -675,6 +676,29 @@ struct RingPy {
 // the host thread spins on the completion counter.
 struct ServePy {
   std::unique_ptr<sml::AEServe> s;
+  // C ABI for the host-only streaming loop in _io (sml_scorer_api.h)
+  SmlScorerApi api{};
+  std::string err;
+  static int api_infer(void* ctx, const float* rows, int k, float* scores, uint32_t* flags, float* recon,
+                       double timeout_s) {
+    auto* self = static_cast<ServePy*>(ctx);
+    try {
+      self->s->infer(rows, k, scores, flags, recon, timeout_s);
+      return 0;
+    } catch (const std::exception& e) {
+      self->err = e.what();
+      return 1;
+    }
+  }
+  static const char* api_error(void* ctx) { return static_cast<ServePy*>(ctx)->err.c_str(); }
+  uintptr_t c_api() {
+    api.version = SML_SCORER_API_VERSION;
+    api.dim = s->D();
+    api.ctx = this;
+    api.infer = &ServePy::api_infer;
+    api.last_error = &ServePy::api_error;
+    return reinterpret_cast<uintptr_t>(&api);
+  }
   ServePy(int device, int nslots, py::array_t<float, py::array::c_style | py::array::forcecast> weights,
           std::vector<int> dims, std::vector<int> acts, py::object scale, py::object shift, double threshold,
           double idle_seconds) {
@@ -828,6 +852,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("infer", &ServePy::infer, py::arg("rows"), py::arg("want_recon") = false, py::arg("timeout_s") = 10.0)
       .def("latency_run", &ServePy::latency_run, py::arg("rows"), py::arg("gap_ns") = 0)
       .def("stop", [](ServePy& p) { p.s->stop(); })
+      .def("c_api", &ServePy::c_api, "address of the SmlScorerApi table (for _io.ScoreLoop)")
       .def_property_readonly("launches", [](ServePy& p) { return p.s->launches(); });
   m.def("mse_acc", &mse_acc, "fused MSE fwd/bwd + categorical accuracy (K3 + K6)", py::arg("y_pred"), py::arg("y"),
         py::arg("bcast") = 1, py::arg("gscale") = 1.0, py::arg("grad") = py::none(), py::arg("acc") = py::none());

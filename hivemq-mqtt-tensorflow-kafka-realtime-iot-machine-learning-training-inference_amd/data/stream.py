@@ -312,5 +312,6 @@ def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optio
             lab[~ok] = LABEL_MISSING
             keys = b["keys"]
             yield Chunk(np.ascontiguousarray(x), lab, keys, b["offsets"],
-                        meta={"topic": b["topic"], "partition": b["partition"], "errors": int(b["n_errors"])})
+                        meta={"topic": b["topic"], "partition": b["partition"], "errors": int(b["n_errors"]),
+                              "ok": ok})
     return Stream(gen)

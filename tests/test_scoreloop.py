@@ -1,0 +1,121 @@
+"""Low-latency streaming scorer loop (csrc/io/scoreloop.cpp) + C++ result formatting
+(csrc/io/format.cpp), on CPU: the GPU scorer is replaced by _io.EchoScorer (score =
+mean(x^2), recon = x / 2) through the same SmlScorerApi table."""
+import json
+import threading
+
+import numpy as np
+import pytest
+
+from streamml.data import stream as S
+from streamml.data.avro import AvroCodec
+from streamml.data.produce import encode_chunk
+from streamml.kafka import KafkaClient, fake_broker
+from streamml.kafka.scoreloop import LowLatencyScorer, paced_produce
+from streamml.ops._ext import load_io
+
+
+def _records(n, seed=0):
+    c = next(iter(S.synthetic(n, chunk=n, seed=seed, failure_rate=0.1)))
+    buf, offs = encode_chunk(AvroCodec("cardata-v1"), c.x, c.label)
+    offs = np.asarray(offs)
+    return c.x.astype(np.float32), [bytes(buf[offs[i]:offs[i + 1]]) for i in range(n)], buf, offs
+
+
+def _expected_score(x):
+    s = np.float32(0)
+    for v in x:
+        s = np.float32(s + np.float32(v) * np.float32(v))
+    return np.float32(s / np.float32(len(x)))
+
+
+def test_array2string_and_json_match_python_exactly():
+    io = load_io()
+    rng = np.random.default_rng(0)
+    for t in range(3000):
+        a = (rng.standard_normal(rng.integers(1, 25)) * 10.0 ** rng.integers(-7, 10)).astype(np.float32)
+        if t % 7 == 0:
+            a[0] = 0
+        if t % 11 == 0:
+            a = np.round(a, 2).astype(np.float32)
+        assert io.array2string_f32(a) == np.array2string(a)
+    for a in (np.array([np.nan, -np.inf, 1.0], np.float32), np.zeros(18, np.float32), np.array([], np.float32)):
+        assert io.array2string_f32(a) == np.array2string(a)
+    for v in [0.0, -0.0, 1e16, 1e15, 1e-4, 1e-5, float("nan"), float("inf"), 0.1, 2.5e-7] + \
+            list(rng.standard_normal(500) * 10.0 ** rng.integers(-30, 30, 500)):
+        assert io.json_float(float(v)) == json.dumps(float(v))
+
+
+def test_score_records_match_json_dumps():
+    io = load_io()
+    rng = np.random.default_rng(1)
+    k = 50
+    keys = [f"car-{i}" for i in range(k)]
+    keys[3], keys[4], keys[5] = None, 'quo"te\\\n\x01', "ünï-\U0001F697"
+    offs = np.arange(100, 100 + k, dtype=np.int64)
+    scores = (rng.standard_normal(k) ** 2 * 3).astype(np.float32)
+    flags = (scores > 5).astype(np.uint8)
+    recon = rng.standard_normal((k, 18)).astype(np.float32)
+    got = io.score_records(keys, 7, offs, scores, flags, recon)
+    for i in range(k):
+        ref = json.dumps({"car": keys[i], "partition": 7, "offset": int(offs[i]), "score": float(scores[i]),
+                          "anomaly": bool(flags[i]), "reconstruction": np.array2string(recon[i])})
+        assert got[i] == ref.encode()
+
+
+def test_loop_scores_every_event_and_commits(tmp_path):
+    name = "scoreloop-basic"
+    b = fake_broker(name)
+    b.create_topic("SENSOR", 2)
+    b.create_topic("RESULTS", 2)
+    x, vals, _, _ = _records(300)
+    cli = KafkaClient(f"fake://{name}")
+    keys = [f"car{i % 13}" for i in range(300)]
+    cli.produce("SENSOR", 0, vals[:200], keys=[k.encode() for k in keys[:200]])
+    cli.produce("SENSOR", 1, vals[200:] + [b"\x00garbage"], keys=[k.encode() for k in keys[200:]] + [None])
+    echo = load_io().EchoScorer(18, 2.0)
+    loop = LowLatencyScorer(f"fake://{name}", "SENSOR", "RESULTS", [0, 1], echo, group="g1", emit_recon=True,
+                            max_batch=64, max_wait_ms=5)
+    st = loop.run(idle_timeout_s=0.2)
+    assert st["events"] == 300 and st["skipped"] == 1
+    assert loop.positions() == [200, 101]
+    assert cli.committed("g1", "SENSOR", 0) == 200 and cli.committed("g1", "SENSOR", 1) == 101
+    res = b.read("RESULTS", 0, 0) + b.read("RESULTS", 1, 0)
+    assert len(res) == 300
+    seen = {}
+    for r in res:
+        d = json.loads(r[2])
+        seen[(d["partition"], d["offset"])] = d
+    for i in range(300):
+        p, o = (0, i) if i < 200 else (1, i - 200)
+        d = seen[(p, o)]
+        assert d["car"] == keys[i]
+        assert np.float32(d["score"]) == _expected_score(x[i])
+        assert d["anomaly"] == bool(_expected_score(x[i]) > 2.0)
+        assert d["reconstruction"] == np.array2string(x[i] * np.float32(0.5))
+    assert st["anomalies"] == sum(1 for d in seen.values() if d["anomaly"])
+
+
+def test_long_poll_delivers_paced_events_promptly():
+    """Events appended at 2 000/s while the loop long-polls: each result is visible a
+    few ms at most after its append (CPU box, loopback sockets)."""
+    name = "scoreloop-latency"
+    b = fake_broker(name)
+    b.create_topic("SENSOR", 1)
+    b.create_topic("RESULTS", 1)
+    _, _, buf, offs = _records(400, seed=2)
+    echo = load_io().EchoScorer(18, 5.0)
+    loop = LowLatencyScorer(f"fake://{name}", "SENSOR", "RESULTS", [0], echo, starts=[0], max_wait_ms=50,
+                            record_latency=True)
+    out = {}
+    th = threading.Thread(target=lambda: out.update(loop.run(max_events=400, idle_timeout_s=5.0)))
+    th.start()
+    sent = paced_produce(f"fake://{name}", "SENSOR", 0, bytes(buf), offs, qps=2000.0)
+    th.join(30)
+    assert not th.is_alive() and out["events"] == 400
+    lat = loop.latency_records()
+    assert lat.shape == (400, 3)
+    d = (lat[np.argsort(lat[:, 1]), 2] - sent) / 1e3
+    assert (d > 0).all()
+    assert np.percentile(d, 50) < 5000, np.percentile(d, 50)   # us; ~100 us typical
+    assert out["empty_fetches"] < 400   # long-poll, not a busy poll

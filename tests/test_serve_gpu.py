@@ -50,3 +50,50 @@ def test_matches_fused_forward_kernel(cuda_device):
         s, _ = srv.score(x)
     # the fused kernel computes in bf16 MFMA, the server in fp32 VALU
     np.testing.assert_allclose(s, fused, rtol=3e-2, atol=1e-4)
+
+
+def test_low_latency_loop_end_to_end(cuda_device):
+    """serve --low-latency path: Kafka -> C++ decode -> persistent GPU scorer -> C++ JSON
+    records -> Kafka.  Every record's score equals the scorer's own result for that row
+    and the record text is byte-identical to the Python serve formatting."""
+    import json
+    import threading
+
+    from streamml.data import stream as S
+    from streamml.data.avro import AvroCodec
+    from streamml.data.produce import encode_chunk
+    from streamml.kafka import fake_broker
+    from streamml.kafka.scoreloop import LowLatencyScorer, paced_produce
+    from streamml.ops.serve import ScoringServer
+
+    name = "gpu-lowlat"
+    b = fake_broker(name)
+    b.create_topic("SENSOR", 1)
+    b.create_topic("RESULTS", 1)
+    c = next(iter(S.synthetic(600, chunk=600, seed=5, failure_rate=0.05)))
+    buf, offs = encode_chunk(AvroCodec("cardata-v1"), c.x, c.label)
+    keys = [f"car{i % 17}" for i in range(600)]
+    m = _model(cuda_device)
+    with ScoringServer(m, threshold=0.5, slots=256) as srv:
+        ref_s, ref_f, ref_r = srv.infer(c.x)
+        loop = LowLatencyScorer(f"fake://{name}", "SENSOR", "RESULTS", [0], srv, starts=[0], emit_recon=True,
+                                max_wait_ms=50, record_latency=True)
+        out = {}
+        th = threading.Thread(target=lambda: out.update(loop.run(max_events=600, idle_timeout_s=10.0)))
+        th.start()
+        sent = paced_produce(f"fake://{name}", "SENSOR", 0, bytes(buf), offs, keys=keys, qps=5000.0)
+        th.join(60)
+    assert not th.is_alive() and out["events"] == 600
+    res = b.read("RESULTS", 0, 0)
+    assert len(res) == 600
+    for off, key, val in res:
+        d = json.loads(val)
+        i = d["offset"]
+        assert key.decode() == keys[i] == d["car"]
+        assert np.float32(d["score"]) == ref_s[i]
+        ref = json.dumps({"car": keys[i], "partition": 0, "offset": i, "score": float(ref_s[i]),
+                          "anomaly": bool(ref_f[i]), "reconstruction": np.array2string(ref_r[i])})
+        assert val == ref.encode()
+    lat = loop.latency_records()
+    d_us = (lat[np.argsort(lat[:, 1]), 2] - sent) / 1e3
+    assert np.percentile(d_us, 50) < 2000
