@@ -974,7 +974,9 @@ Broker::FetchReply Broker::handle_fetch(const uint8_t* body, size_t n) {
     auto st = pick();
     if (fail) ++failures_;
     if (!st.first && !st.second && min_bytes > 0 && max_wait_ms > 0) {
-      const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(max_wait_ms);
+      // system_clock deadline: pthread_cond_timedwait (the steady_clock form maps to
+      // pthread_cond_clockwait, which the ThreadSanitizer runtime here does not model)
+      const auto deadline = std::chrono::system_clock::now() + std::chrono::milliseconds(max_wait_ms);
       while (running_ && !st.first && !st.second) {
         const bool timed_out = data_cv_.wait_until(g, deadline) == std::cv_status::timeout;
         st = pick();
