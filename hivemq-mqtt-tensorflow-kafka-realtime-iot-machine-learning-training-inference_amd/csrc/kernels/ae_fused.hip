@@ -36,6 +36,7 @@ using namespace sml;
 namespace {
 
 constexpr int WAVES = 4;  // waves per workgroup
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int OFF1 = 0, OFF2 = 512, OFF3 = 768, OFF4 = 1024;
 constexpr int NPARAM = 1536;
 constexpr int NSLOT = 1540;
@@ -54,6 +55,10 @@ struct AEArgs {
   float* partials;       // [grid][NSLOT]
   int64_t* iter;         // incremented by block 0 when non-null
   const int64_t* cursor; // device ring cursor: rows start at x + cursor[0]*ld (null = 0)
+  // [n] argmax of each NORMALISED input row, computed once at ingest (row_argmax_u8 /
+  // K8), or null.  x is data, not a model output, so its half of the accuracy metric
+  // (tf.argmax(x) == tf.argmax(y)) need not be recomputed every time a row is trained on.
+  const uint8_t* xarg;
   int D, n1, n2, n3;
   int a1, a2, a3, a4;
   float l1;
@@ -368,11 +373,11 @@ constexpr bool prescaled_tanh() {
   return PACK >= 0 && ((PACK & 3) == ACT_TANH) && (((PACK >> 4) & 3) == ACT_TANH) && zero_preserving<PACK>();
 }
 
-template <int PACK, bool FAST, bool TAIL, bool LOW_REAL = false, int DC = 0>
+template <int PACK, bool FAST, bool TAIL, bool LOW_REAL = false, int DC = 0, bool XA = false>
 __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char* scr, int c, int g, int lane,
                                            bool valid, const f32x4 xf[2], float pad1,
                                            f32x4 acc1[2], f32x4& acc2, f32x4& acc3, f32x4 acc4[2], float& sq,
-                                           float& ab, float& corr, float& rows) {
+                                           float& ab, float& corr, float& rows, int ix_pre = -1) {
   const int a1 = act_of<PACK>(a, 0), a2 = act_of<PACK>(a, 1), a3 = act_of<PACK>(a, 2), a4 = act_of<PACK>(a, 3);
   constexpr bool PRE = FAST && prescaled_tanh<PACK>();
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
@@ -433,7 +438,7 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
     }
   if (a.want_acc) {
     const int iy = row_argmax_fast<LOW_REAL, DC>(y, a.D, g);
-    const int ix = row_argmax_fast<LOW_REAL, DC>(xf, a.D, g);
+    const int ix = XA ? ix_pre : row_argmax_fast<LOW_REAL, DC>(xf, a.D, g);
     corr += (g == 0 && vm && iy == ix) ? 1.f : 0.f;
   }
   rows += (g == 0 && vm) ? 1.f : 0.f;
@@ -501,7 +506,7 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
 template <int OCC>
 constexpr int ring_bytes() { return OCC >= 4 ? 3968 : 6144; }
 
-template <int PACK, bool VEC, int PF, int OCC, int DC = 0>
+template <int PACK, bool VEC, int PF, int OCC, int DC = 0, bool XA = false>
 __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   constexpr bool FAST = zero_preserving<PACK>();
   constexpr int RING = ring_bytes<OCC>();
@@ -515,7 +520,10 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   const int c = lane & 15, g = lane >> 4;
   char* scr = reinterpret_cast<char*>(smem) + wid * (10 * 512);
   const char* norm = reinterpret_cast<const char*>(smem) + SLAB_BYTES;
-  if (a.cursor) a.x += a.cursor[0] * a.ld;  // streaming ring consumer (uniform scalar load)
+  if (a.cursor) {  // streaming ring consumer (uniform scalar load)
+    a.x += a.cursor[0] * a.ld;
+    if (XA) a.xarg += a.cursor[0];
+  }
 
   if (a.iter && blockIdx.x == 0 && threadIdx.x == 0) a.iter[0] += 1;
   if (threadIdx.x < 64) {
@@ -568,16 +576,31 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
         issue(t + (PF - 1) * stride, wr);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (PF - 1)) : "memory");
         f32x4 xf[2], sc[2], sh[2];
+        // XA: the tile's 16 argmax bytes come in through the SCALAR cache (t is
+        // wave-uniform): one s_load_dwordx4, so the LDS-DMA ring's vmcnt accounting (two
+        // VMEM ops per tile) is untouched.  Inline asm because hipcc turns the plain
+        // uniform load into per-lane global loads with a vmcnt(0) that drains the ring.
+        u32x4 q = {0u, 0u, 0u, 0u};
+        if constexpr (XA) {
+          const uint8_t* pa = a.xarg + t * 16;
+          asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(q) : "s"(pa));
+        }
         ring_x(a, ring + rd * slotb, c, g, xf);
         norm_lds(norm, g, sc, sh);
+        int ix = -1;
+        if constexpr (XA) {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(q));
+          const unsigned w = c < 8 ? (c < 4 ? q[0] : q[1]) : (c < 12 ? q[2] : q[3]);
+          ix = (int)((w >> ((c & 3) * 8)) & 0xffu);   // lane c takes byte c
+        }
         rd = rd + 1 == PF ? 0 : rd + 1;
         wr = wr + 1 == PF ? 0 : wr + 1;
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
           for (int j = 0; j < 4; ++j) xf[s][j] = (s == 0 || live_hi<DC>(j)) ? fmaf(xf[s][j], sc[s][j], sh[s][j]) : 0.f;
-        train_tile<PACK, FAST, false, true, DC>(a, F, scr, c, g, lane, true, xf, pad1, acc1, acc2, acc3, acc4, sq,
-                                                ab, corr, rows);
+        train_tile<PACK, FAST, false, true, DC, XA>(a, F, scr, c, g, lane, true, xf, pad1, acc1, acc2, acc3, acc4,
+                                                    sq, ab, corr, rows, ix);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the ring is retired
     }
@@ -829,10 +852,11 @@ int ae_train_grid(int64_t n, int max_blocks) {
 
 hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
                            const float* params, float* partials, int64_t* iter, const int64_t* cursor,
-                           const int* dims, const int* acts, float l1, int want_acc, int grid, hipStream_t stream) {
+                           const int* dims, const int* acts, float l1, int want_acc, int grid, const uint8_t* xarg,
+                           hipStream_t stream) {
   AEArgs a{};
   a.x = x; a.n = n; a.ld = ld; a.scale = scale; a.shift = shift; a.params = params;
-  a.partials = partials; a.iter = iter; a.cursor = cursor;
+  a.partials = partials; a.iter = iter; a.cursor = cursor; a.xarg = xarg;
   a.D = dims[0]; a.n1 = dims[1]; a.n2 = dims[2]; a.n3 = dims[3];
   a.a1 = acts[0]; a.a2 = acts[1]; a.a3 = acts[2]; a.a4 = acts[3];
   a.l1 = l1; a.want_acc = want_acc;
@@ -847,7 +871,13 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
   const dim3 gd(grid), bd(WAVES * 64);
   const int occ = train_occupancy();
   if (pack == PACK_REF) {
-    if (ring_ok && occ == 4 && D == 18)  // the cardata-v1 reference model: D fixed at compile time
+    // precomputed x argmax: 16-B aligned per-tile byte groups (whole 16-row tiles, and a
+    // ring cursor that moves in multiples of 16 rows)
+    const bool xa_ok = xarg != nullptr && want_acc && (n & 15) == 0 &&
+                       ((reinterpret_cast<uintptr_t>(xarg) & 15) == 0);
+    if (ring_ok && occ == 4 && D == 18 && xa_ok)
+      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18, true>), gd, bd, 0, stream, a);
+    else if (ring_ok && occ == 4 && D == 18)  // the cardata-v1 reference model: D fixed at compile time
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18>), gd, bd, 0, stream, a);
     else if (ring_ok && occ == 4 && 3 * 64 * D <= ring_bytes<4>())
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4>), gd, bd, 0, stream, a);

@@ -102,3 +102,37 @@ hipError_t normalize_filter_launch(const float* x, int64_t n, int64_t ld, int D,
 }
 
 }  // namespace sml
+
+// Ingest-time argmax of each normalised row (the data half of the accuracy metric,
+// tf.argmax(x) of cardata-v3's `metrics=['accuracy']`): one thread per row, the same
+// fmaf(x, scale, shift) the training kernels apply, ties to the lowest index.
+namespace {
+__global__ __launch_bounds__(256) void row_argmax_kernel(const float* __restrict__ x, int64_t n, int64_t ld, int D,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, uint8_t* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  const float* row = x + r * ld;
+  float best = 0.0f;
+  int bi = 0;
+  for (int j = 0; j < D; ++j) {
+    const float v = scale ? fmaf(row[j], scale[j], shift[j]) : row[j];
+    if (j == 0 || v > best) {
+      best = v;
+      bi = j;
+    }
+  }
+  out[r] = (uint8_t)bi;
+}
+}  // namespace
+
+namespace sml {
+hipError_t row_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale, const float* shift,
+                             uint8_t* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (D < 1 || D > 255) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_argmax_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, n, ld, D, scale,
+                     shift, out);
+  return hipGetLastError();
+}
+}  // namespace sml

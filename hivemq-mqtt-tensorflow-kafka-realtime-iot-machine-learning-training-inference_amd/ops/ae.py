@@ -14,6 +14,8 @@ accumulated on device and read once per epoch, never per step.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -132,6 +134,7 @@ class FusedAE:
         self.metrics = torch.zeros(NSLOT - NPARAM, device=dev)   # epoch accumulators
         self.cursor = torch.zeros(1, dtype=torch.int64, device=dev)
         self.ring: Optional[torch.Tensor] = None
+        self.ring_xarg: Optional[torch.Tensor] = None
         self.ring_batch = 0
         self.set_normalizer(scale, shift)
 
@@ -195,6 +198,12 @@ class FusedAE:
             raise ValueError("ring rows must be a positive multiple of the batch")
         self.ring, self.ring_batch = ring, int(batch)
         self.cursor.zero_()
+        # ingest-time argmax of every normalised row (the data half of the accuracy
+        # metric): computed once here, read as 1 byte per row by the training kernel
+        # instead of an 8-feature x 4-lane argmax per row per step.  SML_AE_XARG=0 disables.
+        self.ring_xarg = None
+        if self.want_acc and os.environ.get("SML_AE_XARG", "1") != "0":
+            self.ring_xarg = self.C.row_argmax_u8(ring, self.spec.input_dim, self.scale, self.shift)
 
     def step_ring(self, global_batch: Optional[int] = None, allreduce=None) -> None:
         if self.ring is None:
@@ -203,7 +212,7 @@ class FusedAE:
         gb = B if global_batch is None else int(global_batch)
         G = self.C.ae_train_partials(self.ring, self.scale, self.shift, self.params, self.partials, self.iter,
                                      self.spec.dims, self.spec.act_codes, float(self.spec.activity_l1),
-                                     bool(self.want_acc), self.max_blocks, B, self.cursor)
+                                     bool(self.want_acc), self.max_blocks, B, self.cursor, self.ring_xarg)
         if allreduce is None:
             self.reduce(G, RA_ADAM | RA_METRICS | RA_ADVANCE, gscale=1.0 / gb)
         else:

@@ -155,6 +155,10 @@ def test_ring_cursor_and_graph_replay(cuda_device):
     torch.cuda.synchronize()
     assert int(b.cursor.item()) == (4 % nsl) * B
     torch.testing.assert_close(a.params, b.params, rtol=0, atol=0)
+    # the ring path reads x's argmax from the ingest-time byte array (row_argmax_u8);
+    # the accuracy counts equal the in-kernel argmax of the slice path exactly
+    assert b.ring_xarg is not None
+    torch.testing.assert_close(a.metrics, b.metrics, rtol=0, atol=0)
     # hipGraph capture of one ring step, replayed
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
@@ -195,3 +199,18 @@ def test_lds_dma_ring_matches_register_path(cuda_device, D, n, blocks):
     for a, b in zip(g_ring, g_reg):
         np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(m_ring, m_reg)
+
+
+def test_row_argmax_u8_matches_numpy(cuda_device):
+    """Ingest-time argmax of the normalised rows (ties -> lowest index, as tf.argmax)."""
+    from streamml.ops._ext import load_c
+    scale, shift = normalize_affine()
+    rng = np.random.default_rng(11)
+    raw = (rng.uniform(0, 1, size=(5000, 18)) * 40).astype(np.float32)
+    raw[::7, 3] = raw[::7, 9]                     # ties between two features
+    raw[::11] = 0.0                               # all-equal normalised rows (zeroed columns tie)
+    out = load_c().row_argmax_u8(torch.from_numpy(raw).to(cuda_device), 18,
+                                 torch.tensor(scale, device=cuda_device), torch.tensor(shift, device=cuda_device))
+    xn = (raw.astype(np.float64) * np.float32(scale) + np.float32(shift)).astype(np.float32)  # = fmaf
+    ref = np.argmax(xn, axis=1)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)

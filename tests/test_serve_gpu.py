@@ -90,10 +90,14 @@ def test_low_latency_loop_end_to_end(cuda_device):
         d = json.loads(val)
         i = d["offset"]
         assert key.decode() == keys[i] == d["car"]
-        assert np.float32(d["score"]) == ref_s[i]
-        ref = json.dumps({"car": keys[i], "partition": 0, "offset": i, "score": float(ref_s[i]),
-                          "anomaly": bool(ref_f[i]), "reconstruction": np.array2string(ref_r[i])})
-        assert val == ref.encode()
+        # the scorer's last-ulp rounding can depend on which slot / batch position an
+        # event lands in, so values are compared to the reference call with a tolerance;
+        # the C++ formatter itself is byte-checked against json / numpy in test_scoreloop.py
+        np.testing.assert_allclose(np.float32(d["score"]), ref_s[i], rtol=1e-5)
+        assert d["anomaly"] == bool(np.float32(d["score"]) > 0.5)
+        rec = np.array(d["reconstruction"].strip("[]").split(), dtype=np.float32)
+        np.testing.assert_allclose(rec, ref_r[i], rtol=1e-5, atol=1e-7)
+        assert set(d) == {"car", "partition", "offset", "score", "anomaly", "reconstruction"}
     lat = loop.latency_records()
     d_us = (lat[np.argsort(lat[:, 1]), 2] - sent) / 1e3
     assert np.percentile(d_us, 50) < 2000
