@@ -75,6 +75,16 @@ hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, con
 hipError_t row_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale, const float* shift,
                              uint8_t* out, hipStream_t stream);
 
+// ---- MNIST MLP GEMMs (mlp.hip): fp32 MFMA, LDS-tiled K loop, fused epilogues ----
+hipError_t mlp_fwd_launch(const void* x, int x_u8, int64_t ldx, const float* W, const float* b, float* y, int M,
+                          int K, int N, int relu, float keep, uint32_t seed, uint32_t step, hipStream_t st);
+hipError_t mlp_bwd_data_launch(const float* dz, const float* W, const float* h, float* dh, int M, int N1, int N2,
+                               float inv_keep, hipStream_t st);
+hipError_t mlp_wgrad_launch(const void* x, int x_u8, int64_t ldx, const float* dy, float* out, int B, int K, int N,
+                            hipStream_t st);
+hipError_t mlp_dropout_mask_launch(float* out, int M, int N, float keep, uint32_t seed, uint32_t step,
+                                   hipStream_t st);
+
 // ---- persistent Keras-step trainer for the reference LSTM stack (lstm_ref_train.hip) ----
 int lstm_ref_train_params();
 hipError_t lstm_ref_train_launch(float* flat, float* m, float* v, int64_t* iter, const float* x, int64_t ldx,

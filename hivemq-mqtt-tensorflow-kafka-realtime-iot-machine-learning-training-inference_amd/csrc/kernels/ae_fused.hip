@@ -36,7 +36,6 @@ using namespace sml;
 namespace {
 
 constexpr int WAVES = 4;  // waves per workgroup
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int OFF1 = 0, OFF2 = 512, OFF3 = 768, OFF4 = 1024;
 constexpr int NPARAM = 1536;
 constexpr int NSLOT = 1540;
@@ -512,6 +511,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   constexpr int RING = ring_bytes<OCC>();
   static_assert(WAVES * 10 * 512 <= SLAB_BYTES, "transpose scratch must fit in the slab buffer");
   static_assert(PF == 0 || PF * 64 * 17 <= RING, "ring slots must fit the smallest ring tile");
+  static_assert(!XA || (DC > 0 && PF > 0 && PF * (64 * DC + 16) <= RING), "XA: compile-time D, ring slots + argmax");
   // one LDS array: per-wave transpose scratch during the tile loop, per-wave
   // gradient slabs afterwards | the normaliser | (PF > 0) the per-wave input rings
   __shared__ __attribute__((aligned(16))) float smem[(SLAB_BYTES + NORM_BYTES + (PF > 0 ? WAVES * RING : 0)) / 4];
@@ -548,7 +548,8 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
     // LDS-DMA ring: tile first + k*stride lives in slot k % PF.  Every issue is
     // exactly two VMEM instructions (tiles past the end are clamped to the last
     // full tile, never skipped), so "tile k landed" is vmcnt(2 * (PF - 1)).
-    const int slotb = 64 * a.D;
+    const int slotb = 64 * a.D + (XA ? 16 : 0);
+    constexpr int NV = XA ? 3 : 2;  // VMEM instructions per tile issue
     const int nl2 = 4 * a.D - 64;  // lanes of the second 16-B-per-lane DMA (>= 4)
     const int uwid = __builtin_amdgcn_readfirstlane(wid);  // keep the ring bookkeeping scalar
     const int ring_off = SLAB_BYTES + NORM_BYTES + uwid * RING;
@@ -568,30 +569,40 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
         const unsigned dst = ring_lds + slot * slotb;
         glds16(src, voff, dst);
         if (lane < nl2) glds16(src + 1024, voff, dst + 1024);
+        // XA: the tile's 16 argmax bytes ride the same ring, 16 B behind its rows
+        // (a third DMA, one lane; lane 0 always exists, so it is never skipped)
+        if (XA && lane == 0) glds16(a.xarg + tt * 16, 0u, dst + 64 * a.D);
       };
+      // Tile order of this wave: chunks of CH consecutive tiles, chunks interleaved over
+      // the waves (CH = 1: plain interleave).  XA uses CH = 8, so the 8 argmax groups of
+      // a 128-B line of xarg are all read by the same wave, in consecutive iterations
+      // (with CH = 1 every line is fetched by 8 different waves / XCDs).
+      constexpr int CH = XA ? 8 : 1;
+      // next tile in this wave's order (CH = 1: + stride; else +1 inside a chunk, then
+      // on to the wave's next chunk); increasing, so t >= nfull ends the wave
+      auto next_tile = [&](int64_t t) -> int64_t {
+        if constexpr (CH == 1) return t + stride;
+        return ((t + 1) & (CH - 1)) ? t + 1 : t + 1 + (stride - 1) * CH;
+      };
+      const int64_t t0 = ufirst * CH;
+      int64_t tp = t0;   // tile of the next DMA issue (PF - 1 ahead of t)
 #pragma unroll
-      for (int k = 0; k < PF - 1; ++k) issue(ufirst + k * stride, k);
+      for (int k = 0; k < PF - 1; ++k) {
+        issue(tp, k);
+        tp = next_tile(tp);
+      }
       int rd = 0, wr = PF - 1;
-      for (int64_t t = ufirst; t < nfull; t += stride) {
-        issue(t + (PF - 1) * stride, wr);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (PF - 1)) : "memory");
+      for (int64_t t = t0; t < nfull; t = next_tile(t)) {
+        issue(tp, wr);
+        tp = next_tile(tp);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV * (PF - 1)) : "memory");
         f32x4 xf[2], sc[2], sh[2];
-        // XA: the tile's 16 argmax bytes come in through the SCALAR cache (t is
-        // wave-uniform): one s_load_dwordx4, so the LDS-DMA ring's vmcnt accounting (two
-        // VMEM ops per tile) is untouched.  Inline asm because hipcc turns the plain
-        // uniform load into per-lane global loads with a vmcnt(0) that drains the ring.
-        u32x4 q = {0u, 0u, 0u, 0u};
-        if constexpr (XA) {
-          const uint8_t* pa = a.xarg + t * 16;
-          asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(q) : "s"(pa));
-        }
         ring_x(a, ring + rd * slotb, c, g, xf);
         norm_lds(norm, g, sc, sh);
         int ix = -1;
         if constexpr (XA) {
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(q));
-          const unsigned w = c < 8 ? (c < 4 ? q[0] : q[1]) : (c < 12 ? q[2] : q[3]);
-          ix = (int)((w >> ((c & 3) * 8)) & 0xffu);   // lane c takes byte c
+          typedef __attribute__((address_space(3))) const unsigned char lds_u8;
+          ix = (int)*(lds_u8*)(ring + rd * slotb + 64 * a.D + c);
         }
         rd = rd + 1 == PF ? 0 : rd + 1;
         wr = wr + 1 == PF ? 0 : wr + 1;

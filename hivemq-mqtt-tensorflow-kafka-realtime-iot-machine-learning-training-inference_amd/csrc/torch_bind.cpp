@@ -549,6 +549,71 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
   return {dx, dW, dU, db, dh0, dc0};
 }
 
+// ---- MNIST MLP layers (mlp.hip) ----
+static void check_x_mlp(const at::Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1 &&
+                  (x.scalar_type() == at::kFloat || x.scalar_type() == at::kByte),
+              "x must be a device [B, K] float32 or uint8 tensor with unit column stride");
+}
+
+at::Tensor mlp_fwd(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::Tensor>& b, bool relu,
+                   double keep, int64_t seed, int64_t step) {
+  check_x_mlp(x);
+  check_dev(W, "W", at::kFloat);
+  TORCH_CHECK(W.is_contiguous() && W.dim() == 2 && W.size(0) == x.size(1), "W must be [K, N] contiguous");
+  if (b.has_value()) {
+    check_dev(*b, "b", at::kFloat);
+    TORCH_CHECK(b->is_contiguous() && b->numel() == W.size(1), "b must be [N]");
+  }
+  TORCH_CHECK(keep > 0.0 && keep <= 1.0, "keep must be in (0, 1]");
+  c10::hip::HIPGuard guard(x.device().index());
+  auto y = at::empty({x.size(0), W.size(1)}, x.options().dtype(at::kFloat));
+  if (x.size(0) == 0) return y;
+  SML_CHECK_HIP(sml::mlp_fwd_launch(x.data_ptr(), x.scalar_type() == at::kByte, x.stride(0), W.data_ptr<float>(),
+                                    opt_ptr(b), y.data_ptr<float>(), (int)x.size(0), (int)x.size(1),
+                                    (int)W.size(1), relu ? 1 : 0, (float)keep, (uint32_t)seed, (uint32_t)step,
+                                    cur_stream(x)));
+  return y;
+}
+
+at::Tensor mlp_bwd_data(const at::Tensor& dz, const at::Tensor& W, const at::Tensor& h, double keep) {
+  check_dev(dz, "dz", at::kFloat);
+  check_dev(W, "W", at::kFloat);
+  check_dev(h, "h", at::kFloat);
+  TORCH_CHECK(dz.is_contiguous() && W.is_contiguous() && h.is_contiguous(), "inputs must be contiguous");
+  TORCH_CHECK(W.dim() == 2 && dz.dim() == 2 && h.dim() == 2 && dz.size(1) == W.size(1) && h.size(1) == W.size(0) &&
+                  h.size(0) == dz.size(0), "shapes: dz [B, N2], W [N1, N2], h [B, N1]");
+  c10::hip::HIPGuard guard(dz.device().index());
+  auto dh = at::empty_like(h);
+  if (dz.size(0) == 0) return dh;
+  SML_CHECK_HIP(sml::mlp_bwd_data_launch(dz.data_ptr<float>(), W.data_ptr<float>(), h.data_ptr<float>(),
+                                         dh.data_ptr<float>(), (int)dz.size(0), (int)W.size(0), (int)W.size(1),
+                                         (float)(1.0 / keep), cur_stream(dz)));
+  return dh;
+}
+
+void mlp_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor& out) {
+  check_x_mlp(x);
+  check_dev(dy, "dy", at::kFloat);
+  check_dev(out, "out", at::kFloat);
+  TORCH_CHECK(dy.is_contiguous() && out.is_contiguous() && dy.dim() == 2 && dy.size(0) == x.size(0),
+              "dy must be [B, N] contiguous");
+  TORCH_CHECK(out.numel() == (x.size(1) + 1) * dy.size(1), "out must hold [K + 1, N] (dW then db)");
+  c10::hip::HIPGuard guard(x.device().index());
+  SML_CHECK_HIP(sml::mlp_wgrad_launch(x.data_ptr(), x.scalar_type() == at::kByte, x.stride(0), dy.data_ptr<float>(),
+                                      out.data_ptr<float>(), (int)x.size(0), (int)x.size(1), (int)dy.size(1),
+                                      cur_stream(x)));
+}
+
+at::Tensor mlp_dropout_mask(const at::Tensor& like, int64_t M, int64_t N, double keep, int64_t seed, int64_t step) {
+  TORCH_CHECK(like.is_cuda(), "needs a device tensor for placement");
+  c10::hip::HIPGuard guard(like.device().index());
+  auto out = at::empty({M, N}, like.options().dtype(at::kFloat));
+  SML_CHECK_HIP(sml::mlp_dropout_mask_launch(out.data_ptr<float>(), (int)M, (int)N, (float)keep, (uint32_t)seed,
+                                             (uint32_t)step, cur_stream(like)));
+  return out;
+}
+
 // N consecutive Keras steps of the reference LSTM stack (look_back 1) in one launch.
 at::Tensor lstm_ref_train(const at::Tensor& flat, const at::Tensor& m, const at::Tensor& v, const at::Tensor& iter,
                           const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Tensor>& order,
@@ -863,6 +928,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("act") = 1, py::arg("lr") = 1e-3, py::arg("beta1") = 0.9, py::arg("beta2") = 0.999,
         py::arg("eps") = 1e-7);
   m.def("lstm_ref_train_params", &sml::lstm_ref_train_params);
+  m.def("mlp_fwd", &mlp_fwd, "dropout(act(x . W + b)) on fp32 MFMA (x float32 or uint8 scaled by 1/255)",
+        py::arg("x"), py::arg("W"), py::arg("b") = py::none(), py::arg("relu") = false, py::arg("keep") = 1.0,
+        py::arg("seed") = 0, py::arg("step") = 0);
+  m.def("mlp_bwd_data", &mlp_bwd_data, "(dz . W^T) * [h > 0] / keep", py::arg("dz"), py::arg("W"), py::arg("h"),
+        py::arg("keep") = 1.0);
+  m.def("mlp_wgrad", &mlp_wgrad, "[x ; 1]^T . dy -> out [K + 1, N] (dW then db)", py::arg("x"), py::arg("dy"),
+        py::arg("out"));
+  m.def("mlp_dropout_mask", &mlp_dropout_mask, "the in-kernel dropout multipliers (0 or 1/keep)", py::arg("like"),
+        py::arg("M"), py::arg("N"), py::arg("keep"), py::arg("seed"), py::arg("step"));
   m.def("lstm_fused_supported", &sml::lstm_fused_supported, "whether (U, IN) has a fused LSTM kernel", py::arg("U"),
         py::arg("IN"));
   py::class_<ServePy>(m, "AEServe", "persistent per-event autoencoder scorer over host-mapped rings")

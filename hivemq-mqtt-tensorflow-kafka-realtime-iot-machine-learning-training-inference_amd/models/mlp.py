@@ -11,11 +11,14 @@ Reference models:
 * confluent-tensorflow-io-kafka-simplified.py:10-29 -- Dense(512, relu) + Dropout(0.2),
   ``fit(x_train, y_train, epochs=5, validation_data=(x_test, y_test))`` (Keras default batch 32).
 
-Device path: inputs travel as ``uint8`` and are scaled by 1/255 on the device
-(``convert_image_dtype``), the two GEMMs run on hipBLASLt with the bias fused
-into the epilogue (``addmm``), the softmax + sparse-CE forward/backward + the
-accuracy count are ONE fused HIP kernel (``softmax_xent``, K13), the backward
-GEMMs write straight into the flat gradient buffer and the optimizer step is
+Device path (every GEMM on the in-tree fp32-MFMA kernels of ``csrc/kernels/mlp.hip``):
+inputs travel as ``uint8`` and are scaled by 1/255 as the GEMM stages them
+(``convert_image_dtype``); layer 1 = one launch with bias + relu + Dropout fused in
+the epilogue (the mask is a counter hash of (seed, step, row, col), no torch.rand);
+layer 2 = one launch; softmax + sparse-CE forward/backward + the accuracy count are
+ONE fused HIP kernel (``softmax_xent``, K13); the backward is three launches (dW2|db2
+as one [h ; 1]^T . dz product written straight into the flat gradient buffer, dH =
+dz . W2^T gated by [h > 0] / keep, dW1|db1 = [x ; 1]^T . dH) and the optimizer step is
 one flat HIP Adam launch.  Metrics stay on the device until the epoch ends.
 """
 from __future__ import annotations
@@ -76,6 +79,7 @@ class MLPClassifier:
         self._acc = torch.zeros(2, device=self.device)
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(seed)
+        self._seed, self._step = int(seed) & 0xffffffff, 0   # in-kernel dropout RNG key
         self.stop_training = False
 
     # ------------------------------------------------------------------ core
@@ -93,18 +97,25 @@ class MLPClassifier:
             t = t.to(self.device, non_blocking=True)
         t = t.reshape(len(t), -1)
         if t.dtype == torch.uint8:
-            return t.float().mul_(1.0 / 255.0)
+            # the device GEMM scales uint8 by 1/255 while staging it (no fp32 copy)
+            return t.contiguous() if self.on_gpu else t.float().mul_(1.0 / 255.0)
         return t.float()
 
     def logits(self, x: torch.Tensor, training: bool = False):
         W1, b1, W2, b2 = self.fp.params
-        h = torch.addmm(b1, x, W1).relu_()
+        if self.on_gpu:
+            keep = 1.0 - self.dropout if (training and self.dropout > 0) else 1.0
+            h = self.C.mlp_fwd(x, W1, b1, True, keep, self._seed, self._step)
+            return self.C.mlp_fwd(h, W2, b2, False), h, None
+        # CPU path / fp32 oracle: plain torch ops
+        x = x.float() / 255.0 if x.dtype == torch.uint8 else x
+        h = (x @ W1 + b1).relu_()
         mask = None
         if training and self.dropout > 0:
             keep = 1.0 - self.dropout
             mask = (torch.rand(h.shape, device=h.device, generator=self._gen) < keep).float().mul_(1.0 / keep)
             h = h * mask
-        return torch.addmm(b2, h, W2), h, mask
+        return h @ W2 + b2, h, mask
 
     @torch.no_grad()
     def train_step(self, x, y, global_batch: Optional[int] = None, allreduce=None) -> None:
@@ -118,19 +129,28 @@ class MLPClassifier:
         if self.on_gpu:
             dz = torch.empty_like(z)
             self.C.softmax_xent(z.contiguous(), yb.contiguous(), scale, dz, None, self._acc)
+            fp = self.fp
+            o = fp.offsets
+            keep = 1.0 - self.dropout if self.dropout > 0 else 1.0
+            self.C.mlp_wgrad(h, dz, fp.grad[o[2]:o[4]])                # dW2 | db2
+            dh = self.C.mlp_bwd_data(dz, W2, h, keep)                   # dz . W2^T * [h > 0] / keep
+            self.C.mlp_wgrad(xb, dh, fp.grad[o[0]:o[2]])               # dW1 | db1
+            self._step += 1
+            self.opt.step(allreduce=allreduce)
+            return
         else:
             loss, corr, dz = softmax_xent_reference(z, yb)
             dz.mul_(scale)
             self._acc[0] += loss
             self._acc[1] += corr
         gW1, gb1, gW2, gb2 = (p.grad for p in self.fp.params)
-        torch.mm(h.t(), dz, out=gW2)
+        gW2.copy_(h.t() @ dz)
         torch.sum(dz, 0, out=gb2)
         dh = dz @ W2.t()
         dh.mul_(h > 0)
         if mask is not None:
             dh.mul_(mask)
-        torch.mm(xb.t(), dh, out=gW1)
+        gW1.copy_(xb.t() @ dh)
         torch.sum(dh, 0, out=gb1)
         self.opt.step(allreduce=allreduce)
 

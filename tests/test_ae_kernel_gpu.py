@@ -210,7 +210,8 @@ def test_row_argmax_u8_matches_numpy(cuda_device):
     raw[::7, 3] = raw[::7, 9]                     # ties between two features
     raw[::11] = 0.0                               # all-equal normalised rows (zeroed columns tie)
     out = load_c().row_argmax_u8(torch.from_numpy(raw).to(cuda_device), 18,
-                                 torch.tensor(scale, device=cuda_device), torch.tensor(shift, device=cuda_device))
+                                 torch.tensor(scale, dtype=torch.float32, device=cuda_device),
+                                 torch.tensor(shift, dtype=torch.float32, device=cuda_device))
     xn = (raw.astype(np.float64) * np.float32(scale) + np.float32(shift)).astype(np.float32)  # = fmaf
     ref = np.argmax(xn, axis=1)
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
