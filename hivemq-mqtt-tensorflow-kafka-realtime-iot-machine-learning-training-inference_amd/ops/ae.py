@@ -198,11 +198,14 @@ class FusedAE:
             raise ValueError("ring rows must be a positive multiple of the batch")
         self.ring, self.ring_batch = ring, int(batch)
         self.cursor.zero_()
-        # ingest-time argmax of every normalised row (the data half of the accuracy
-        # metric): computed once here, read as 1 byte per row by the training kernel
-        # instead of an 8-feature x 4-lane argmax per row per step.  SML_AE_XARG=0 disables.
+        # Optional (SML_AE_XARG=1): ingest-time argmax of every normalised row (the data
+        # half of the accuracy metric), read as 1 byte per row by the training kernel
+        # instead of an 8-feature x 4-lane argmax per tile.  It removes 30 of ~217 VALU
+        # instructions per 16-row tile, but measured 1-2 % SLOWER on MI355X (32.7 vs 33.3
+        # G rows/s, profiles/r02/SUMMARY.md): the removed argmax work sat in MFMA-latency
+        # gaps, while the extra per-tile DMA is not free.  Off by default.
         self.ring_xarg = None
-        if self.want_acc and os.environ.get("SML_AE_XARG", "1") != "0":
+        if self.want_acc and os.environ.get("SML_AE_XARG", "0") == "1":
             self.ring_xarg = self.C.row_argmax_u8(ring, self.spec.input_dim, self.scale, self.shift)
 
     def step_ring(self, global_batch: Optional[int] = None, allreduce=None) -> None:

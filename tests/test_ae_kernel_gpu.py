@@ -137,8 +137,11 @@ def test_accuracy_metric_exact(cuda_device):
     assert abs(metr[2] - ref.sum()) <= (~clear).sum()
 
 
-def test_ring_cursor_and_graph_replay(cuda_device):
-    """Device-cursor ring steps == explicit-slice steps; a captured graph replays them."""
+@pytest.mark.parametrize("xarg", ["0", "1"])
+def test_ring_cursor_and_graph_replay(cuda_device, xarg, monkeypatch):
+    """Device-cursor ring steps == explicit-slice steps; a captured graph replays them.
+    xarg=1: the ring variant that reads x's argmax from the ingest-time byte array."""
+    monkeypatch.setenv("SML_AE_XARG", xarg)
     spec = AESpec()
     w = _weights(spec, seed=5)
     scale, shift = normalize_affine()
@@ -154,11 +157,15 @@ def test_ring_cursor_and_graph_replay(cuda_device):
         b.step_ring()
     torch.cuda.synchronize()
     assert int(b.cursor.item()) == (4 % nsl) * B
-    torch.testing.assert_close(a.params, b.params, rtol=0, atol=0)
+    # the ring path walks its tiles in 8-tile chunks per wave (ingest-time argmax bytes, one
+    # 128-B line per chunk), so its fp32 gradient sums differ from the slice path's only in
+    # summation order
+    torch.testing.assert_close(a.params, b.params, rtol=1e-5, atol=1e-7)
     # the ring path reads x's argmax from the ingest-time byte array (row_argmax_u8);
     # the accuracy counts equal the in-kernel argmax of the slice path exactly
-    assert b.ring_xarg is not None
-    torch.testing.assert_close(a.metrics, b.metrics, rtol=0, atol=0)
+    assert (b.ring_xarg is not None) == (xarg == "1")
+    torch.testing.assert_close(a.metrics[2:4], b.metrics[2:4], rtol=0, atol=0)   # correct rows, rows
+    torch.testing.assert_close(a.metrics[:2], b.metrics[:2], rtol=1e-5, atol=0)   # fp32 sums (order)
     # hipGraph capture of one ring step, replayed
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
@@ -175,7 +182,7 @@ def test_ring_cursor_and_graph_replay(cuda_device):
         i = s % nsl
         a.step(raw[i * B:(i + 1) * B])
     torch.cuda.synchronize()
-    torch.testing.assert_close(a.params, b.params, rtol=0, atol=0)
+    torch.testing.assert_close(a.params, b.params, rtol=1e-5, atol=1e-7)
     assert int(b.iter.item()) == int(a.iter.item()) == 7
 
 
