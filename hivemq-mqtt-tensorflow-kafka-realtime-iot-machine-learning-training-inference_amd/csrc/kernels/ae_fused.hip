@@ -54,10 +54,12 @@ struct AEArgs {
   float* partials;       // [grid][NSLOT]
   int64_t* iter;         // incremented by block 0 when non-null
   const int64_t* cursor; // device ring cursor: rows start at x + cursor[0]*ld (null = 0)
-  // [n] argmax of each NORMALISED input row, computed once at ingest (row_argmax_u8 /
-  // K8), or null.  x is data, not a model output, so its half of the accuracy metric
-  // (tf.argmax(x) == tf.argmax(y)) need not be recomputed every time a row is trained on.
-  const uint8_t* xarg;
+  // tile-packed ring (XM 1): per 16-row tile the 64*D bytes of rows, then the 16 bytes of
+  // argmax(normalised x) computed once at ingest (pack_tiles_argmax) -- one 64*D + 16 byte
+  // block, so the tile's two DMAs carry the argmax too.  x is data, not a model output, so
+  // its half of the accuracy metric (tf.argmax(x) == tf.argmax(y)) need not be recomputed
+  // every time a row is trained on.
+  const uint8_t* xpack;
   int D, n1, n2, n3;
   int a1, a2, a3, a4;
   float l1;
@@ -505,13 +507,18 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
 template <int OCC>
 constexpr int ring_bytes() { return OCC >= 4 ? 3968 : 6144; }
 
-template <int PACK, bool VEC, int PF, int OCC, int DC = 0, bool XA = false>
+template <int PACK, bool VEC, int PF, int OCC, int DC = 0, int XM = 0>
 __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   constexpr bool FAST = zero_preserving<PACK>();
   constexpr int RING = ring_bytes<OCC>();
   static_assert(WAVES * 10 * 512 <= SLAB_BYTES, "transpose scratch must fit in the slab buffer");
   static_assert(PF == 0 || PF * 64 * 17 <= RING, "ring slots must fit the smallest ring tile");
-  static_assert(!XA || (DC > 0 && PF > 0 && PF * (64 * DC + 16) <= RING), "XA: compile-time D, ring slots + argmax");
+  // XM: x-argmax mode. 0 in-kernel argmax; 1 tile-packed ring (rows + ingest-time argmax
+  // bytes per tile, pack_tiles_argmax); 2 / 3 A/B probes that skip the argmax of x entirely (wrong accuracy, timing
+  // only: 2 with the plain tile order, 3 with the chunked order) -- they separate the VALU
+  // saving from the cost of delivering the bytes (profiles/r02/SUMMARY.md)
+  constexpr bool XA = XM != 0;
+  static_assert(XM != 1 || (DC > 0 && PF > 0 && PF * (64 * DC + 16) <= RING), "XA: compile-time D, ring slots + argmax");
   // one LDS array: per-wave transpose scratch during the tile loop, per-wave
   // gradient slabs afterwards | the normaliser | (PF > 0) the per-wave input rings
   __shared__ __attribute__((aligned(16))) float smem[(SLAB_BYTES + NORM_BYTES + (PF > 0 ? WAVES * RING : 0)) / 4];
@@ -522,7 +529,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   const char* norm = reinterpret_cast<const char*>(smem) + SLAB_BYTES;
   if (a.cursor) {  // streaming ring consumer (uniform scalar load)
     a.x += a.cursor[0] * a.ld;
-    if (XA) a.xarg += a.cursor[0];
+    if (XM == 1) a.xpack += (a.cursor[0] >> 4) * (int64_t)(64 * a.D + 16);
   }
 
   if (a.iter && blockIdx.x == 0 && threadIdx.x == 0) a.iter[0] += 1;
@@ -548,9 +555,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
     // LDS-DMA ring: tile first + k*stride lives in slot k % PF.  Every issue is
     // exactly two VMEM instructions (tiles past the end are clamped to the last
     // full tile, never skipped), so "tile k landed" is vmcnt(2 * (PF - 1)).
-    const int slotb = 64 * a.D + (XA ? 16 : 0);
-    constexpr int NV = XA ? 3 : 2;  // VMEM instructions per tile issue
-    const int nl2 = 4 * a.D - 64;  // lanes of the second 16-B-per-lane DMA (>= 4)
+    const int slotb = 64 * a.D + (XM == 1 ? 16 : 0);
+    constexpr int NV = 2;  // VMEM instructions per tile issue
+    const int nl2 = (slotb - 1024) >> 4;  // lanes of the second 16-B-per-lane DMA (>= 4)
     const int uwid = __builtin_amdgcn_readfirstlane(wid);  // keep the ring bookkeeping scalar
     const int ring_off = SLAB_BYTES + NORM_BYTES + uwid * RING;
     const unsigned ring_lds =
@@ -565,19 +572,15 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
     if (nfull > 0) {
       auto issue = [&](int64_t tt, int slot) {
         tt = tt < nfull ? tt : nfull - 1;
-        const char* src = reinterpret_cast<const char*>(a.x + tt * 16 * a.ld);
+        const char* src = XM == 1 ? reinterpret_cast<const char*>(a.xpack) + tt * slotb
+                                  : reinterpret_cast<const char*>(a.x + tt * 16 * a.ld);
         const unsigned dst = ring_lds + slot * slotb;
         glds16(src, voff, dst);
         if (lane < nl2) glds16(src + 1024, voff, dst + 1024);
-        // XA: the tile's 16 argmax bytes ride the same ring, 16 B behind its rows
-        // (a third DMA, one lane; lane 0 always exists, so it is never skipped)
-        if (XA && lane == 0) glds16(a.xarg + tt * 16, 0u, dst + 64 * a.D);
       };
       // Tile order of this wave: chunks of CH consecutive tiles, chunks interleaved over
-      // the waves (CH = 1: plain interleave).  XA uses CH = 8, so the 8 argmax groups of
-      // a 128-B line of xarg are all read by the same wave, in consecutive iterations
-      // (with CH = 1 every line is fetched by 8 different waves / XCDs).
-      constexpr int CH = XA ? 8 : 1;
+      // the waves (CH = 1: plain interleave; CH = 8 only in the XM 3 timing probe).
+      constexpr int CH = XM == 3 ? 8 : 1;
       // next tile in this wave's order (CH = 1: + stride; else +1 inside a chunk, then
       // on to the wave's next chunk); increasing, so t >= nfull ends the wave
       auto next_tile = [&](int64_t t) -> int64_t {
@@ -600,9 +603,11 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
         ring_x(a, ring + rd * slotb, c, g, xf);
         norm_lds(norm, g, sc, sh);
         int ix = -1;
-        if constexpr (XA) {
+        if constexpr (XM == 1) {
           typedef __attribute__((address_space(3))) const unsigned char lds_u8;
           ix = (int)*(lds_u8*)(ring + rd * slotb + 64 * a.D + c);
+        } else if constexpr (XA) {
+          ix = 0;
         }
         rd = rd + 1 == PF ? 0 : rd + 1;
         wr = wr + 1 == PF ? 0 : wr + 1;
@@ -863,11 +868,11 @@ int ae_train_grid(int64_t n, int max_blocks) {
 
 hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
                            const float* params, float* partials, int64_t* iter, const int64_t* cursor,
-                           const int* dims, const int* acts, float l1, int want_acc, int grid, const uint8_t* xarg,
+                           const int* dims, const int* acts, float l1, int want_acc, int grid, const uint8_t* xpack,
                            hipStream_t stream) {
   AEArgs a{};
   a.x = x; a.n = n; a.ld = ld; a.scale = scale; a.shift = shift; a.params = params;
-  a.partials = partials; a.iter = iter; a.cursor = cursor; a.xarg = xarg;
+  a.partials = partials; a.iter = iter; a.cursor = cursor; a.xpack = xpack;
   a.D = dims[0]; a.n1 = dims[1]; a.n2 = dims[2]; a.n3 = dims[3];
   a.a1 = acts[0]; a.a2 = acts[1]; a.a3 = acts[2]; a.a4 = acts[3];
   a.l1 = l1; a.want_acc = want_acc;
@@ -882,12 +887,19 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
   const dim3 gd(grid), bd(WAVES * 64);
   const int occ = train_occupancy();
   if (pack == PACK_REF) {
-    // precomputed x argmax: 16-B aligned per-tile byte groups (whole 16-row tiles, and a
-    // ring cursor that moves in multiples of 16 rows)
-    const bool xa_ok = xarg != nullptr && want_acc && (n & 15) == 0 &&
-                       ((reinterpret_cast<uintptr_t>(xarg) & 15) == 0);
-    if (ring_ok && occ == 4 && D == 18 && xa_ok)
-      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18, true>), gd, bd, 0, stream, a);
+    // tile-packed ring with ingest-time x argmax (pack_tiles_argmax): whole 16-row tiles
+    const bool xa_ok = xpack != nullptr && want_acc && (n & 15) == 0 &&
+                       ((reinterpret_cast<uintptr_t>(xpack) & 15) == 0);
+    static const int probe = [] {
+      const char* e = std::getenv("SML_AE_XPROBE");
+      return e ? std::atoi(e) : 0;
+    }();
+    if (ring_ok && occ == 4 && D == 18 && want_acc && probe == 2)
+      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18, 2>), gd, bd, 0, stream, a);
+    else if (ring_ok && occ == 4 && D == 18 && want_acc && probe == 3)
+      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18, 3>), gd, bd, 0, stream, a);
+    else if (ring_ok && occ == 4 && D == 18 && xa_ok)
+      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18, 1>), gd, bd, 0, stream, a);
     else if (ring_ok && occ == 4 && D == 18)  // the cardata-v1 reference model: D fixed at compile time
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18>), gd, bd, 0, stream, a);
     else if (ring_ok && occ == 4 && 3 * 64 * D <= ring_bytes<4>())

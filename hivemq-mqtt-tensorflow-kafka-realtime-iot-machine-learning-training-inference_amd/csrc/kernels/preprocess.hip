@@ -124,9 +124,43 @@ __global__ __launch_bounds__(256) void row_argmax_kernel(const float* __restrict
   }
   out[r] = (uint8_t)bi;
 }
+__device__ __forceinline__ int argmax_norm(const float* row, int D, const float* scale, const float* shift) {
+  float best = 0.0f;
+  int bi = 0;
+  for (int j = 0; j < D; ++j) {
+    const float v = scale ? fmaf(row[j], scale[j], shift[j]) : row[j];
+    if (j == 0 || v > best) {
+      best = v;
+      bi = j;
+    }
+  }
+  return bi;
+}
+
+__global__ __launch_bounds__(256) void pack_tiles_kernel(const float* __restrict__ x, int64_t n, int64_t ld, int D,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, uint8_t* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  const float* row = x + r * ld;
+  const int64_t tile_bytes = 64 * (int64_t)D + 16;
+  uint8_t* t = out + (r >> 4) * tile_bytes;
+  float* dst = reinterpret_cast<float*>(t) + (r & 15) * D;
+  for (int j = 0; j < D; ++j) dst[j] = row[j];
+  t[64 * D + (r & 15)] = (uint8_t)argmax_norm(row, D, scale, shift);
+}
 }  // namespace
 
 namespace sml {
+hipError_t pack_tiles_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale,
+                                    const float* shift, uint8_t* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if ((n & 15) || D < 1 || D > 255) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_tiles_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, n, ld, D, scale,
+                     shift, out);
+  return hipGetLastError();
+}
+
 hipError_t row_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale, const float* shift,
                              uint8_t* out, hipStream_t stream) {
   if (n <= 0) return hipSuccess;

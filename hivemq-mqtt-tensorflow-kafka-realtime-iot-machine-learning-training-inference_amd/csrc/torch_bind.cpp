@@ -69,7 +69,7 @@ int64_t ae_train_partials(const at::Tensor& x, const c10::optional<at::Tensor>& 
                           const c10::optional<at::Tensor>& shift, const at::Tensor& params, at::Tensor& partials,
                           const c10::optional<at::Tensor>& iter, std::vector<int64_t> dims, std::vector<int64_t> acts,
                           double l1, bool want_acc, int64_t max_blocks, int64_t n_rows,
-                          const c10::optional<at::Tensor>& cursor, const c10::optional<at::Tensor>& xarg) {
+                          const c10::optional<at::Tensor>& cursor, const c10::optional<at::Tensor>& xpack) {
   check_ae_dims(dims, acts);
   check_dev(x, "x", at::kFloat);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [n, ld] with unit column stride");
@@ -98,11 +98,12 @@ int64_t ae_train_partials(const at::Tensor& x, const c10::optional<at::Tensor>& 
   } else {
     TORCH_CHECK(n <= x.size(0), "n_rows larger than x");
   }
-  const uint8_t* xarg_ptr = nullptr;
-  if (xarg.has_value() && xarg->defined()) {
-    TORCH_CHECK(xarg->is_cuda() && xarg->scalar_type() == at::kByte && xarg->is_contiguous() &&
-                    xarg->numel() == x.size(0), "xarg must be a contiguous device uint8 [rows of x]");
-    xarg_ptr = xarg->data_ptr<uint8_t>();
+  const uint8_t* xpack_ptr = nullptr;
+  if (xpack.has_value() && xpack->defined()) {
+    TORCH_CHECK(xpack->is_cuda() && xpack->scalar_type() == at::kByte && xpack->is_contiguous() &&
+                    x.size(0) % 16 == 0 && xpack->numel() == x.size(0) / 16 * (64 * dims[0] + 16),
+                "xpack must be the tile-packed ring of x (pack_tiles_argmax)");
+    xpack_ptr = xpack->data_ptr<uint8_t>();
   }
   const int grid = sml::ae_train_grid(n, (int)max_blocks);
   TORCH_CHECK(partials.numel() >= (int64_t)grid * sml::ae_nslot(), "partials buffer too small for grid ", grid);
@@ -112,8 +113,22 @@ int64_t ae_train_partials(const at::Tensor& x, const c10::optional<at::Tensor>& 
   SML_CHECK_HIP(sml::ae_train_launch(x.data_ptr<float>(), n, x.stride(0), opt_ptr(scale), opt_ptr(shift),
                                      params.data_ptr<float>(), partials.data_ptr<float>(), iter_ptr, cur_ptr, d, a,
                                      (float)l1,
-                                     want_acc ? 1 : 0, grid, xarg_ptr, cur_stream(x)));
+                                     want_acc ? 1 : 0, grid, xpack_ptr, cur_stream(x)));
   return grid;
+}
+
+// ingest-time tile-packed ring: per 16-row tile the rows then the 16 argmax bytes
+at::Tensor pack_tiles_argmax(const at::Tensor& x, int64_t D, const c10::optional<at::Tensor>& scale,
+                             const c10::optional<at::Tensor>& shift) {
+  check_dev(x, "x", at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(1) >= D && D >= 1 && D <= 255 && x.size(0) % 16 == 0,
+              "x must be [n, >=D] with n a multiple of 16");
+  TORCH_CHECK(scale.has_value() == shift.has_value(), "scale and shift go together");
+  c10::hip::HIPGuard guard(x.device().index());
+  auto out = at::empty({x.size(0) / 16 * (64 * D + 16)}, x.options().dtype(at::kByte));
+  SML_CHECK_HIP(sml::pack_tiles_argmax_launch(x.data_ptr<float>(), x.size(0), x.stride(0), (int)D, opt_ptr(scale),
+                                              opt_ptr(shift), out.data_ptr<uint8_t>(), cur_stream(x)));
+  return out;
 }
 
 // ingest-time argmax of every normalised row -> uint8 [n]
@@ -848,7 +863,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ae_train_partials", &ae_train_partials, "fused AE fwd+bwd -> per-workgroup gradient slabs",
         py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("partials"), py::arg("iter"),
         py::arg("dims"), py::arg("acts"), py::arg("l1"), py::arg("want_acc"), py::arg("max_blocks"),
-        py::arg("n_rows") = -1, py::arg("cursor") = py::none(), py::arg("xarg") = py::none());
+        py::arg("n_rows") = -1, py::arg("cursor") = py::none(), py::arg("xpack") = py::none());
+  m.def("pack_tiles_argmax", &pack_tiles_argmax, "tile-packed training ring (rows + ingest-time argmax per tile)",
+        py::arg("x"), py::arg("D"), py::arg("scale") = py::none(), py::arg("shift") = py::none());
   m.def("row_argmax_u8", &row_argmax_u8, "ingest-time argmax of each normalised row (uint8)", py::arg("x"),
         py::arg("D"), py::arg("scale") = py::none(), py::arg("shift") = py::none());
   m.def("ae_minibatch_max_batch", &sml::ae_minibatch_max_batch, "largest batch the persistent small-batch trainer takes");

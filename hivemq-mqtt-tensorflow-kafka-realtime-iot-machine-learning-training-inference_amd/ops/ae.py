@@ -134,7 +134,7 @@ class FusedAE:
         self.metrics = torch.zeros(NSLOT - NPARAM, device=dev)   # epoch accumulators
         self.cursor = torch.zeros(1, dtype=torch.int64, device=dev)
         self.ring: Optional[torch.Tensor] = None
-        self.ring_xarg: Optional[torch.Tensor] = None
+        self.ring_xpack: Optional[torch.Tensor] = None
         self.ring_batch = 0
         self.set_normalizer(scale, shift)
 
@@ -198,15 +198,14 @@ class FusedAE:
             raise ValueError("ring rows must be a positive multiple of the batch")
         self.ring, self.ring_batch = ring, int(batch)
         self.cursor.zero_()
-        # Optional (SML_AE_XARG=1): ingest-time argmax of every normalised row (the data
-        # half of the accuracy metric), read as 1 byte per row by the training kernel
-        # instead of an 8-feature x 4-lane argmax per tile.  It removes 30 of ~217 VALU
-        # instructions per 16-row tile, but measured 1-2 % SLOWER on MI355X (32.7 vs 33.3
-        # G rows/s, profiles/r02/SUMMARY.md): the removed argmax work sat in MFMA-latency
-        # gaps, while the extra per-tile DMA is not free.  Off by default.
-        self.ring_xarg = None
-        if self.want_acc and os.environ.get("SML_AE_XARG", "0") == "1":
-            self.ring_xarg = self.C.row_argmax_u8(ring, self.spec.input_dim, self.scale, self.shift)
+        # Ingest-time tile packing (SML_AE_XPACK=0 disables): a copy of the ring laid out
+        # per 16-row tile as [rows | 16 argmax(normalised x) bytes], so the training kernel
+        # gets x's half of the accuracy metric with the tile's own two DMAs and skips the
+        # 8-feature x 4-lane argmax of x per tile (profiles/r02/SUMMARY.md).
+        self.ring_xpack = None
+        if (self.want_acc and os.environ.get("SML_AE_XPACK", "1") != "0" and ring.size(0) % 16 == 0
+                and batch % 16 == 0 and ring.size(1) == self.spec.input_dim):
+            self.ring_xpack = self.C.pack_tiles_argmax(ring, self.spec.input_dim, self.scale, self.shift)
 
     def step_ring(self, global_batch: Optional[int] = None, allreduce=None) -> None:
         if self.ring is None:
@@ -215,7 +214,7 @@ class FusedAE:
         gb = B if global_batch is None else int(global_batch)
         G = self.C.ae_train_partials(self.ring, self.scale, self.shift, self.params, self.partials, self.iter,
                                      self.spec.dims, self.spec.act_codes, float(self.spec.activity_l1),
-                                     bool(self.want_acc), self.max_blocks, B, self.cursor, self.ring_xarg)
+                                     bool(self.want_acc), self.max_blocks, B, self.cursor, self.ring_xpack)
         if allreduce is None:
             self.reduce(G, RA_ADAM | RA_METRICS | RA_ADVANCE, gscale=1.0 / gb)
         else:

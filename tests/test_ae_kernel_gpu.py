@@ -137,11 +137,11 @@ def test_accuracy_metric_exact(cuda_device):
     assert abs(metr[2] - ref.sum()) <= (~clear).sum()
 
 
-@pytest.mark.parametrize("xarg", ["0", "1"])
-def test_ring_cursor_and_graph_replay(cuda_device, xarg, monkeypatch):
+@pytest.mark.parametrize("xpack", ["0", "1"])
+def test_ring_cursor_and_graph_replay(cuda_device, xpack, monkeypatch):
     """Device-cursor ring steps == explicit-slice steps; a captured graph replays them.
-    xarg=1: the ring variant that reads x's argmax from the ingest-time byte array."""
-    monkeypatch.setenv("SML_AE_XARG", xarg)
+    xpack=1: the tile-packed ring (rows + ingest-time argmax bytes per 16-row tile)."""
+    monkeypatch.setenv("SML_AE_XPACK", xpack)
     spec = AESpec()
     w = _weights(spec, seed=5)
     scale, shift = normalize_affine()
@@ -157,15 +157,11 @@ def test_ring_cursor_and_graph_replay(cuda_device, xarg, monkeypatch):
         b.step_ring()
     torch.cuda.synchronize()
     assert int(b.cursor.item()) == (4 % nsl) * B
-    # the ring path walks its tiles in 8-tile chunks per wave (ingest-time argmax bytes, one
-    # 128-B line per chunk), so its fp32 gradient sums differ from the slice path's only in
-    # summation order
-    torch.testing.assert_close(a.params, b.params, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(a.params, b.params, rtol=0, atol=0)
     # the ring path reads x's argmax from the ingest-time byte array (row_argmax_u8);
     # the accuracy counts equal the in-kernel argmax of the slice path exactly
-    assert (b.ring_xarg is not None) == (xarg == "1")
-    torch.testing.assert_close(a.metrics[2:4], b.metrics[2:4], rtol=0, atol=0)   # correct rows, rows
-    torch.testing.assert_close(a.metrics[:2], b.metrics[:2], rtol=1e-5, atol=0)   # fp32 sums (order)
+    assert (b.ring_xpack is not None) == (xpack == "1")
+    torch.testing.assert_close(a.metrics, b.metrics, rtol=0, atol=0)
     # hipGraph capture of one ring step, replayed
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
@@ -182,7 +178,7 @@ def test_ring_cursor_and_graph_replay(cuda_device, xarg, monkeypatch):
         i = s % nsl
         a.step(raw[i * B:(i + 1) * B])
     torch.cuda.synchronize()
-    torch.testing.assert_close(a.params, b.params, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(a.params, b.params, rtol=0, atol=0)
     assert int(b.iter.item()) == int(a.iter.item()) == 7
 
 
@@ -222,3 +218,19 @@ def test_row_argmax_u8_matches_numpy(cuda_device):
     xn = (raw.astype(np.float64) * np.float32(scale) + np.float32(shift)).astype(np.float32)  # = fmaf
     ref = np.argmax(xn, axis=1)
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+def test_pack_tiles_argmax_layout(cuda_device):
+    """Tile-packed ring: per 16-row tile the raw rows then argmax(normalised row) bytes."""
+    from streamml.ops._ext import load_c
+    scale, shift = normalize_affine()
+    rng = np.random.default_rng(12)
+    raw = (rng.uniform(0, 1, size=(64, 18)) * 40).astype(np.float32)
+    sc = torch.tensor(scale, dtype=torch.float32, device=cuda_device)
+    sh = torch.tensor(shift, dtype=torch.float32, device=cuda_device)
+    p = load_c().pack_tiles_argmax(torch.from_numpy(raw).to(cuda_device), 18, sc, sh).cpu().numpy()
+    tiles = p.reshape(4, 64 * 18 + 16)
+    rows = tiles[:, :64 * 18].copy().view(np.float32).reshape(64, 18)
+    np.testing.assert_array_equal(rows, raw)
+    xn = (raw.astype(np.float64) * np.float32(scale) + np.float32(shift)).astype(np.float32)
+    np.testing.assert_array_equal(tiles[:, 64 * 18:].reshape(64), np.argmax(xn, axis=1))
