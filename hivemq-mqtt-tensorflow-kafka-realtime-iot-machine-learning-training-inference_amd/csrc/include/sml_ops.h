@@ -71,8 +71,8 @@ hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, con
                                  const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,
                                  int IN, int U, int act, int dh_last_only, int64_t x_seq, hipStream_t stream);
 
-// tile-packed training ring: per 16-row tile the rows (64*D bytes) then the 16 argmax bytes
-// of the normalised rows; out holds n/16 * (64*D + 16) bytes (n % 16 == 0)
+// tile-packed training ring: per 16-row tile the normalised rows (x * scale + shift, 64*D
+// bytes) then their 16 argmax bytes; out holds n/16 * (64*D + 16) bytes (n % 16 == 0)
 hipError_t pack_tiles_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale,
                                     const float* shift, uint8_t* out, hipStream_t stream);
 // argmax (lowest index on ties) of each normalised row x * scale + shift over D features

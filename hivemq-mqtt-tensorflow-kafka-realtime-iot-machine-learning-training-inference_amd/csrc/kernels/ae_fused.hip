@@ -54,8 +54,9 @@ struct AEArgs {
   float* partials;       // [grid][NSLOT]
   int64_t* iter;         // incremented by block 0 when non-null
   const int64_t* cursor; // device ring cursor: rows start at x + cursor[0]*ld (null = 0)
-  // tile-packed ring (XM 1): per 16-row tile the 64*D bytes of rows, then the 16 bytes of
-  // argmax(normalised x) computed once at ingest (pack_tiles_argmax) -- one 64*D + 16 byte
+  // tile-packed ring (XM 1): per 16-row tile the 64*D bytes of NORMALISED rows, then the
+  // 16 bytes of argmax(normalised x), both computed once at ingest (pack_tiles_argmax:
+  // normalize_fn, cardata-v3.py:78-168, applied where the event enters, like K8) -- one 64*D + 16 byte
   // block, so the tile's two DMAs carry the argmax too.  x is data, not a model output, so
   // its half of the accuracy metric (tf.argmax(x) == tf.argmax(y)) need not be recomputed
   // every time a row is trained on.
@@ -601,7 +602,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV * (PF - 1)) : "memory");
         f32x4 xf[2], sc[2], sh[2];
         ring_x(a, ring + rd * slotb, c, g, xf);
-        norm_lds(norm, g, sc, sh);
+        if constexpr (XM != 1) norm_lds(norm, g, sc, sh);
         int ix = -1;
         if constexpr (XM == 1) {
           typedef __attribute__((address_space(3))) const unsigned char lds_u8;
@@ -611,10 +612,18 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
         }
         rd = rd + 1 == PF ? 0 : rd + 1;
         wr = wr + 1 == PF ? 0 : wr + 1;
+        if constexpr (XM == 1) {
+          // packed rows are already normalised at ingest: only the features past D
+          // (clamped duplicates from ring_x) are zeroed
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+          for (int j = 0; j < 4; ++j) xf[1][j] = (live_hi<DC>(j) && 16 + 4 * g + j < DC) ? xf[1][j] : 0.f;
+        } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) xf[s][j] = (s == 0 || live_hi<DC>(j)) ? fmaf(xf[s][j], sc[s][j], sh[s][j]) : 0.f;
+          for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              xf[s][j] = (s == 0 || live_hi<DC>(j)) ? fmaf(xf[s][j], sc[s][j], sh[s][j]) : 0.f;
+        }
         train_tile<PACK, FAST, false, true, DC, XA>(a, F, scr, c, g, lane, true, xf, pad1, acc1, acc2, acc3, acc4,
                                                     sq, ab, corr, rows, ix);
       }

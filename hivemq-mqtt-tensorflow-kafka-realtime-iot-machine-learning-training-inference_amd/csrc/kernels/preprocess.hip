@@ -146,7 +146,8 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(const float* __restrict
   const int64_t tile_bytes = 64 * (int64_t)D + 16;
   uint8_t* t = out + (r >> 4) * tile_bytes;
   float* dst = reinterpret_cast<float*>(t) + (r & 15) * D;
-  for (int j = 0; j < D; ++j) dst[j] = row[j];
+  // normalize_fn once per event + the argmax of the normalised row
+  for (int j = 0; j < D; ++j) dst[j] = scale ? fmaf(row[j], scale[j], shift[j]) : row[j];
   t[64 * D + (r & 15)] = (uint8_t)argmax_norm(row, D, scale, shift);
 }
 }  // namespace

@@ -221,7 +221,7 @@ def test_row_argmax_u8_matches_numpy(cuda_device):
 
 
 def test_pack_tiles_argmax_layout(cuda_device):
-    """Tile-packed ring: per 16-row tile the raw rows then argmax(normalised row) bytes."""
+    """Tile-packed ring: per 16-row tile the normalised rows then their argmax bytes."""
     from streamml.ops._ext import load_c
     scale, shift = normalize_affine()
     rng = np.random.default_rng(12)
@@ -231,6 +231,6 @@ def test_pack_tiles_argmax_layout(cuda_device):
     p = load_c().pack_tiles_argmax(torch.from_numpy(raw).to(cuda_device), 18, sc, sh).cpu().numpy()
     tiles = p.reshape(4, 64 * 18 + 16)
     rows = tiles[:, :64 * 18].copy().view(np.float32).reshape(64, 18)
-    np.testing.assert_array_equal(rows, raw)
-    xn = (raw.astype(np.float64) * np.float32(scale) + np.float32(shift)).astype(np.float32)
+    xn = (raw.astype(np.float64) * np.float32(scale) + np.float32(shift)).astype(np.float32)   # = fmaf
+    np.testing.assert_array_equal(rows, xn)
     np.testing.assert_array_equal(tiles[:, 64 * 18:].reshape(64), np.argmax(xn, axis=1))
