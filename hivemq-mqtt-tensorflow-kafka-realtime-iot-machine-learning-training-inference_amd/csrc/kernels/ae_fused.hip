@@ -139,7 +139,9 @@ __device__ __forceinline__ void load_frags(const AEArgs& a, int c, int g, Frags&
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int out = 16 * s + k;
-        F.w4[s][j] = bfbits(ldsel(P, c < a.n3 && out < a.D, OFF4 + c * 32 + out));
+        // the MSE gradient's 2/D rides in the backward W4 operand (dz4 is left unscaled;
+        // the W4 weight-gradient slab is scaled once at the end of the launch)
+        F.w4[s][j] = bfbits((2.0f / (float)a.D) * ldsel(P, c < a.n3 && out < a.D, OFF4 + c * 32 + out));
       }
       F.w3[j] = bfbits(ldsel(P, c < a.n2 && k < a.n3, OFF3 + c * 16 + k));
       F.w2[j] = bfbits(ldsel(P, c < a.n1 && k < a.n2, OFF2 + c * 16 + k));
@@ -325,7 +327,7 @@ __device__ __forceinline__ constexpr bool live_hi(int i) { return DC == 0 || 16 
 __device__ __forceinline__ float bfly_max(float m) {
   const unsigned u = __float_as_uint(m);
   const auto r16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-  m = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  m = max3f(__uint_as_float(r16[0]), __uint_as_float(r16[1]), __uint_as_float(r16[1]));   // no canonicalising v_max
   const unsigned v = __float_as_uint(m);
   const auto r32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
   return max3f(__uint_as_float(r32[0]), __uint_as_float(r32[1]), __uint_as_float(r32[1]));
@@ -361,6 +363,44 @@ __device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], int D, int g) {
   return bfly_min(idx);
 }
 
+// Argmax of a row of NON-NEGATIVE values (a relu output) as one integer max: each live
+// feature f becomes the key (bits(v) & 0x7fffffc0) | (63 - f) -- a non-negative float's
+// bits order like the float (the sign bit is cleared, so a -0 from med3 counts as 0),
+// and the low 6 bits break ties toward the lowest index (tf.argmax).  Masked features
+// are key 0, below every live key.  Exact except when the two largest values agree in
+// all but the last 6 of 23 mantissa bits (relative gap < 2^-17, far below the bf16
+// noise of the values), where the lower index wins.  ~16 VALU instead of ~35.
+__device__ __forceinline__ unsigned umax3(unsigned a, unsigned b, unsigned c) {
+  unsigned r;
+  asm("v_max3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// (bits & 0x7fffffc0) | lo in ONE v_bfi_b32 (hipcc otherwise emits an and + sub pair)
+__device__ __forceinline__ unsigned bfi_key(unsigned bits, unsigned lo) {
+  unsigned r;
+  asm("v_bfi_b32 %0, 0x7fffffc0, %1, %2" : "=v"(r) : "v"(bits), "v"(lo));
+  return r;
+}
+template <int DC>
+__device__ __forceinline__ int row_argmax_nonneg(const f32x4 v[2], int D, int g) {
+  unsigned k[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int t = q >> 2, i = q & 3;
+    const int f = 16 * t + 4 * g + i;
+    const bool live = t == 0 || (live_hi<DC>(i) && f < D);
+    k[q] = live ? bfi_key(__float_as_uint(v[t][i]), (unsigned)(63 - f)) : 0u;
+  }
+  unsigned m = umax3(umax3(k[0], k[1], k[2]), k[3], live_hi<DC>(0) ? k[4] : k[3]);
+  if (live_hi<DC>(1) || live_hi<DC>(2)) m = umax3(m, live_hi<DC>(1) ? k[5] : m, live_hi<DC>(2) ? k[6] : m);
+  if (live_hi<DC>(3)) m = umax3(m, k[7], m);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
+  m = umax3(r16[0], r16[1], r16[1]);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+  m = umax3(r32[0], r32[1], r32[1]);
+  return 63 - (int)(m & 63u);
+}
+
 // One 16-row tile: forward, loss, metrics, backward, weight-gradient MFMAs.
 // FAST (zero-preserving activations): no per-feature masks -- padded features
 // stay exactly 0 because their weights are 0 and act(0) = 0; only the bias slot
@@ -383,7 +423,6 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
   const int a1 = act_of<PACK>(a, 0), a2 = act_of<PACK>(a, 1), a3 = act_of<PACK>(a, 2), a4 = act_of<PACK>(a, 3);
   constexpr bool PRE = FAST && prescaled_tanh<PACK>();
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  const float two_over_d = 2.0f / (float)a.D;
   const bool pad_lane = (g == 3);
   const bool vm = !TAIL || valid;
 
@@ -436,10 +475,15 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
       if constexpr (!FAST) e = (16 * t + 4 * g + i) < a.D ? e : 0.f;
       if constexpr (TAIL) e = vm ? e : 0.f;
       sq = fmaf(e, e, sq);
-      dz4[t][i] = act_grad(a4, y[t][i], two_over_d * e);
+      dz4[t][i] = act_grad(a4, y[t][i], e);   // x 2/D folded into F.w4 / the acc4 slab
     }
   if (a.want_acc) {
-    const int iy = row_argmax_fast<LOW_REAL, DC>(y, a.D, g);
+    // relu output layer (the reference model): integer-key argmax of the non-negative y
+    int iy;
+    if constexpr (PACK >= 0 && ((PACK >> 6) & 3) == ACT_RELU && LOW_REAL)
+      iy = row_argmax_nonneg<DC>(y, a.D, g);
+    else
+      iy = row_argmax_fast<LOW_REAL, DC>(y, a.D, g);
     const int ix = XA ? ix_pre : row_argmax_fast<LOW_REAL, DC>(xf, a.D, g);
     corr += (g == 0 && vm && iy == ix) ? 1.f : 0.f;
   }
@@ -668,8 +712,8 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
     my[OFF1 + (16 + m) * 16 + c] = acc1[1][i];
     my[OFF2 + m * 16 + c] = acc2[i];
     my[OFF3 + m * 16 + c] = acc3[i];
-    my[OFF4 + m * 32 + c] = acc4[0][i];
-    my[OFF4 + m * 32 + 16 + c] = acc4[1][i];
+    my[OFF4 + m * 32 + c] = acc4[0][i] * (2.0f / (float)a.D);
+    my[OFF4 + m * 32 + 16 + c] = acc4[1][i] * (2.0f / (float)a.D);
   }
   sq = wave_sum(sq);
   ab = wave_sum(ab);
