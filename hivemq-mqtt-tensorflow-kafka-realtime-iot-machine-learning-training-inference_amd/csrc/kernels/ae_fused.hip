@@ -378,7 +378,7 @@ __device__ __forceinline__ unsigned umax3(unsigned a, unsigned b, unsigned c) {
 // (bits & 0x7fffffc0) | lo in ONE v_bfi_b32 (hipcc otherwise emits an and + sub pair)
 __device__ __forceinline__ unsigned bfi_key(unsigned bits, unsigned lo) {
   unsigned r;
-  asm("v_bfi_b32 %0, 0x7fffffc0, %1, %2" : "=v"(r) : "v"(bits), "v"(lo));
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x7fffffc0u), "v"(bits), "v"(lo));   // mask from an SGPR
   return r;
 }
 template <int DC>

@@ -234,3 +234,20 @@ def test_pack_tiles_argmax_layout(cuda_device):
     xn = (raw.astype(np.float64) * np.float32(scale) + np.float32(shift)).astype(np.float32)   # = fmaf
     np.testing.assert_array_equal(rows, xn)
     np.testing.assert_array_equal(tiles[:, 64 * 18:].reshape(64), np.argmax(xn, axis=1))
+
+
+@pytest.mark.parametrize("D,n", [(18, 1000), (18, 4096), (30, 777)])
+def test_gradients_vs_bf16_rounded_reference(cuda_device, D, n):
+    """The fused AE step against a torch reference with the kernel's bf16 rounding points
+    (tests/helpers/bf16_ref.py): every gradient and the loss sum to <= 1e-3 relative."""
+    from helpers.bf16_ref import ae_bf16_reference, relerr
+    spec = AESpec(input_dim=D)
+    w = _weights(spec)
+    x = np.random.default_rng(5).uniform(-1, 1, size=(n, D)).astype(np.float32)
+    fused = FusedAE(spec, w, cuda_device, max_blocks=64)
+    g_fused, metr = fused.gradients(torch.from_numpy(x).to(cuda_device))
+    g_ref, (sq, ab) = ae_bf16_reference(torch.from_numpy(x), w, spec.activity_l1)
+    for i, (gf, gr) in enumerate(zip(g_fused, g_ref)):
+        assert relerr(gf, gr) < 1e-3, i
+    assert abs(metr[0] - sq) / sq < 1e-4
+    assert abs(metr[1] - ab) / ab < 1e-4

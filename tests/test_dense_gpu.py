@@ -82,3 +82,23 @@ def test_dense_autograd(cuda_device):
         outs.append([t.detach().cpu() for t in (y, xx.grad, WW.grad, bb.grad)])
     for a, r in zip(outs[1], outs[0]):
         assert (a - r).abs().max().item() < 3e-2 * (r.abs().max().item() + 1e-3) + 0.05
+
+
+@pytest.mark.parametrize("M,K,N", [(1000, 18, 128), (40961, 32, 64), (777, 7, 18), (5000, 128, 18)])
+@pytest.mark.parametrize("act", ["linear", "relu", "tanh", "sigmoid"])
+def test_rowgemm_wgrad_vs_bf16_rounded_reference(cuda_device, M, K, N, act):
+    """K1 / K2 against references that round the MFMA operands to bf16 (fp64 elsewhere):
+    <= 1e-3 relative, where the fp32-oracle tests above need the bf16 floor."""
+    from helpers.bf16_ref import bf, relerr
+    from streamml.ops import dense as dn
+    g = torch.Generator().manual_seed(M * 3 + K + N)
+    x = torch.randn(M, K, generator=g)
+    W = torch.randn(K, N, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    dy = torch.randn(M, N, generator=g)
+    out = dn.rowgemm(x.to(cuda_device), W.to(cuda_device), b.to(cuda_device), act).cpu()
+    ref = dn._act_torch(act, bf(x) @ bf(W) + b.double())
+    assert relerr(out, ref) < 1e-3
+    dW, db = dn.wgrad(x.to(cuda_device), dy.to(cuda_device))
+    assert relerr(dW.cpu(), bf(x).t() @ bf(dy)) < 1e-3
+    assert relerr(db.cpu(), dy.double().sum(0)) < 1e-5

@@ -159,3 +159,31 @@ def test_fit_stream_uses_in_place_windows(cuda_device):
     hb = b.fit(xs, ys, epochs=2, batch_size=64, verbose=0)
     assert ha.history["loss"] == hb.history["loss"]
     torch.testing.assert_close(a.fp.flat, b.fp.flat, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("last_only", [False, True])
+@pytest.mark.parametrize("u,act,B,T,inp", [(32, "relu", 100, 7, 18), (16, "tanh", 37, 50, 18),
+                                           (32, "tanh", 64, 50, 32), (64, "relu", 20, 4, 18),
+                                           (16, "relu", 130, 9, 32), (16, "relu", 16, 3, 64)])
+def test_fused_lstm_vs_bf16_rounded_reference(cuda_device, u, act, B, T, inp, last_only):
+    """The correctness claim for the fused kernels: against a torch reference that rounds to
+    bf16 at the kernels' own points (tests/helpers/bf16_ref.py) every output and gradient
+    agrees to <= 1e-3 relative -- the fp32-oracle test above only bounds the bf16 floor."""
+    from helpers.bf16_ref import lstm_fused_bf16_reference, relerr
+    if not fused_supported(u, inp):
+        pytest.skip("no fused instance for this shape")
+    rng = np.random.default_rng(u * T + B)
+    x = torch.tensor(rng.uniform(-1, 1, (B, T, inp)), dtype=torch.float32)
+    W = torch.tensor(rng.standard_normal((inp, 4 * u)) * 0.25, dtype=torch.float32)
+    U = torch.tensor(rng.standard_normal((u, 4 * u)) * 0.25, dtype=torch.float32)
+    b = torch.tensor(rng.standard_normal(4 * u) * 0.1, dtype=torch.float32)
+    gy = torch.tensor(rng.standard_normal((B, u) if last_only else (B, T, u)), dtype=torch.float32)
+    dev = [t.to(cuda_device).requires_grad_(True) for t in (x, W, U, b)]
+    y = FusedLSTMFunction.apply(*dev, 1 if act == "relu" else 2, last_only)
+    (y.float() * gy.to(cuda_device)).sum().backward()
+    hseq, dx, dW, dU, db = lstm_fused_bf16_reference(x, W, U, b, act, dh=gy, last_only=last_only)
+    yref = hseq[:, -1] if last_only else hseq
+    assert relerr(y.detach().cpu(), yref) < 1e-3
+    for name, d, r in (("dx", dev[0].grad, dx), ("dW", dev[1].grad, dW), ("dU", dev[2].grad, dU),
+                       ("db", dev[3].grad, db)):
+        assert relerr(d.cpu(), r) < 1e-3, name
