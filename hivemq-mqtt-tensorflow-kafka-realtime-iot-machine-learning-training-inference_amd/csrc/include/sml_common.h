@@ -46,6 +46,19 @@ __device__ __forceinline__ f32x4 mfma16(bf16x4 a, bf16x4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
 
+// Two consecutive K=16 tiles in ONE gfx950 v_mfma_f32_16x16x32_bf16: lane (c, g) holds
+// k = 4g..4g+3 of tile 0 and of tile 1, i.e. hardware k 8g..8g+7 is the logical
+// {16*0 + 4g + e, 16*1 + 4g + e}.  A and B are permuted alike, so the contraction is the
+// same sum as mfma16(a0, b0) + mfma16(a1, b1), in half the MFMA issues.
+__device__ __forceinline__ f32x4 mfma32(bf16x4 a0, bf16x4 a1, bf16x4 b0, bf16x4 b1, f32x4 c) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 a = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+  const s16x8 b = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+
 __device__ __forceinline__ unsigned pack2(float lo, float hi) {
   f32x2_t v = {lo, hi};
   bf16x2_t b = __builtin_convertvector(v, bf16x2_t);

@@ -249,10 +249,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       z[mt] = *reinterpret_cast<const f32x4*>(sbias + 16 * mt + (ol >> 4) * 4);
+      constexpr int NK = KT + UB;   // K-tiles in pairs on 16x16x32, exactly as the forward
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt) z[mt] = mfma16(wfwd[(mt * (KT + UB) + kt) * 64 + ol], xb[kt], z[mt]);
-#pragma unroll
-      for (int s = 0; s < UB; ++s) z[mt] = mfma16(wfwd[(mt * (KT + UB) + KT + s) * 64 + ol], hb[s], z[mt]);
+      for (int k = 0; k + 1 < NK; k += 2)
+        z[mt] = mfma32(wfwd[(mt * NK + k) * 64 + ol], wfwd[(mt * NK + k + 1) * 64 + ol], k < KT ? xb[k] : hb[k - KT],
+                       k + 1 < KT ? xb[k + 1] : hb[k + 1 - KT], z[mt]);
+      if constexpr (NK & 1)   // as the forward: never a 16x16x16 on a 16x16x32 result
+        z[mt] = mfma32(wfwd[(mt * NK + NK - 1) * 64 + ol], bf16x4{0, 0, 0, 0}, hb[UB - 1], bf16x4{0, 0, 0, 0}, z[mt]);
     }
     wgrad();                                    // step t+1's weight gradients (zeros on the first step)
     f32x4 cp[UB], dhi[UB];                      // c_{t-1}, incoming dh_t
@@ -292,16 +295,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       dzb[mt] = pack4(dzt[mt]);
       accb[mt] += dzt[mt];
     }
-    // critical path: recurrent gradient for step t-1, as two half-depth MFMA chains
+    // critical path: recurrent gradient for step t-1 -- the 4U gate tiles in pairs on
+    // 16x16x32 (MT/2 dependent MFMAs, half the issues of two 16x16x16 half-chains)
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
-      f32x4 acc0 = zero4, acc1 = zero4;
+      f32x4 acc = zero4;
 #pragma unroll
-      for (int kt = 0; kt < MT; kt += 2) {
-        acc0 = mfma16(ufl[(b * MT + kt) * 64 + ol], dzb[kt], acc0);
-        acc1 = mfma16(ufl[(b * MT + kt + 1) * 64 + ol], dzb[kt + 1], acc1);
-      }
-      dhr[b] = acc0 + acc1;
+      for (int kt = 0; kt < MT; kt += 2)
+        acc = mfma32(ufl[(b * MT + kt) * 64 + ol], ufl[(b * MT + kt + 1) * 64 + ol], dzb[kt], dzb[kt + 1], acc);
+      dhr[b] = acc;
     }
     // input gradient dX_t^T = W . dz_t^T
     if (want_dx) {
@@ -309,7 +311,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       for (int kt = 0; kt < KT; ++kt) {
         f32x4 acc = zero4;
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc = mfma16(wfl[(kt * MT + mt) * 64 + ol], dzb[mt], acc);
+        for (int mt = 0; mt < MT; mt += 2)
+          acc = mfma32(wfl[(kt * MT + mt) * 64 + ol], wfl[(kt * MT + mt + 1) * 64 + ol], dzb[mt], dzb[mt + 1], acc);
         // dx is [B16, T, 16*KT]: every lane stores its whole piece, unmasked
         const int64_t o = (seq * T + t) * (int64_t)(16 * KT) + 16 * kt + 4 * g;
         if constexpr (std::is_same_v<XT, float>) *reinterpret_cast<f32x4*>(static_cast<float*>(a.dx) + o) = acc;

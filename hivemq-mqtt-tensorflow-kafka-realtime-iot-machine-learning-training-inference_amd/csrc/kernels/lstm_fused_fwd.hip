@@ -98,11 +98,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
     f32x4 z[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
+      // z = b + [W ; U]^T . [x_t ; h_{t-1}]^T: the KT + UB K-tiles taken in pairs on the
+      // 16x16x32 MFMA (the backward's gate recompute uses the identical pairing)
       z[mt] = bias[mt];
+      constexpr int NK = KT + UB;
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt) z[mt] = mfma16(wt[mt][kt], xb[kt], z[mt]);
-#pragma unroll
-      for (int s = 0; s < UB; ++s) z[mt] = mfma16(ut[mt][s], hb[s], z[mt]);
+      for (int k = 0; k + 1 < NK; k += 2)
+        z[mt] = mfma32(k < KT ? wt[mt][k] : ut[mt][k - KT], k + 1 < KT ? wt[mt][k + 1] : ut[mt][k + 1 - KT],
+                       k < KT ? xb[k] : hb[k - KT], k + 1 < KT ? xb[k + 1] : hb[k + 1 - KT], z[mt]);
+      // odd tile count: the last tile against a zero tile, still on 16x16x32 -- a 16x16x16
+      // whose SrcC is a 16x16x32 result miscomputed here (ROCm 7.2, gfx950; measured)
+      if constexpr (NK & 1) z[mt] = mfma32(ut[mt][UB - 1], bf16x4{0, 0, 0, 0}, hb[UB - 1], bf16x4{0, 0, 0, 0}, z[mt]);
     }
     // hseq and cseq are padded to whole waves: padding lanes write their own rows,
     // so no store sits under a lane mask (a masked store makes the number of
