@@ -36,13 +36,15 @@
 namespace sml {
 namespace {
 
-constexpr int NT = 256;            // 4 waves
+constexpr int NT = 512;            // 8 waves: ~19 owned parameters per thread
 constexpr int MAXB = 32;           // rows per Keras step (reference: 1)
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__device__ __forceinline__ float sigm(float z) { return 1.0f / (1.0f + expf(-z)); }
-__device__ __forceinline__ float actf(int a, float z) { return a == 2 ? tanhf(z) : fmaxf(z, 0.0f); }
+// hardware exp / rcp (~1 ulp): the step is latency-bound and libm's accurate forms cost
+// several times as many instructions on the serial phase chain
+__device__ __forceinline__ float sigm(float z) { return sigmoid_fast(z); }
+__device__ __forceinline__ float actf(int a, float z) { return a == 2 ? tanh_fast(z) : fmaxf(z, 0.0f); }
 // derivative of the activation, from its OUTPUT value (relu: out > 0; tanh: 1 - out^2)
 __device__ __forceinline__ float actd(int a, float out) { return a == 2 ? 1.0f - out * out : (out > 0.0f ? 1.0f : 0.0f); }
 
@@ -192,7 +194,7 @@ __device__ __forceinline__ void own_block(float (&p)[R], float (&mo)[R], float (
         const float vv = a.beta2 * vo[R0 + r] + (1.0f - a.beta2) * gr * gr;
         mo[R0 + r] = mm;
         vo[R0 + r] = vv;
-        p[R0 + r] -= lr_t * mm / (sqrtf(vv) + a.eps);
+        p[R0 + r] -= lr_t * mm * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv) + a.eps);   // v_sqrt / v_rcp
         *lp = p[R0 + r];
       }
     }
