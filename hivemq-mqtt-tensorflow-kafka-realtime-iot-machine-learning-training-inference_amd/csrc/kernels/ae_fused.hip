@@ -435,8 +435,8 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
     x1[3] += pad1;
     xb0 = pack4(xf[0]);
     xb1 = pack4(x1);
-    f32x4 z1 = mfma16(F.w1t[0], xb0, zero4);
-    z1 = mfma16(F.w1t[1], xb1, z1);
+    // the 32 input features (18 real + bias slot) in ONE 16x16x32 MFMA
+    const f32x4 z1 = mfma32(F.w1t[0], F.w1t[1], xb0, xb1, zero4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) h1[i] = PRE ? tanh_exp2(z1[i]) : act_fwd(a1, z1[i]);
     h1[3] += pad1;
@@ -491,8 +491,7 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
 
   // backward through the layers (feature-major, in registers)
   const bf16x4 dz4b0 = pack4(dz4[0]), dz4b1 = pack4(dz4[1]);
-  f32x4 dh3 = mfma16(F.w4[0], dz4b0, zero4);
-  dh3 = mfma16(F.w4[1], dz4b1, dh3);
+  const f32x4 dh3 = mfma32(F.w4[0], F.w4[1], dz4b0, dz4b1, zero4);   // K = 32 outputs in one MFMA
   f32x4 dz3, dz2, dz1;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
