@@ -89,3 +89,35 @@ def test_serve_on_gpu_matches_cpu_scores(tmp_path, capsys, cuda_device):
         got = np.array([r["score"] for r in recs])
         np.testing.assert_allclose(got, cpu.score(src.x), rtol=3e-2, atol=1e-3)   # bf16 MFMA vs fp32
         assert all("reconstruction" in r for r in recs)
+
+
+@pytest.mark.gpu
+def test_serve_low_latency_cli(tmp_path, capsys, cuda_device):
+    """``serve --low-latency``: the C++ loop on the persistent scorer, two replicas over
+    four partitions, every event scored once, keyed and ordered, offsets committed (a
+    restarted replica has nothing left)."""
+    from streamml.data.stream import kafka
+    from streamml.models.autoencoder import Autoencoder, load_model
+    model_file = tmp_path / "model1.h5"
+    Autoencoder(device="cpu", seed=7).save(str(model_file))
+    n, parts = 3000, 4
+    common = ["serve", "synthetic://%d" % n, "SENSOR_LL", "preds-ll", "model1.h5", "--workdir", str(tmp_path),
+              "--device", str(cuda_device), "--synthetic-partitions", str(parts), "--idle-timeout", "0.3",
+              "--low-latency", "--max-wait-ms", "20", "--replicas", "2"]
+    summaries = []
+    for r in (0, 1):
+        assert cli_main(common + ["--replica-index", str(r)]) == 0
+        summaries.append(json.loads(capsys.readouterr().out.strip().splitlines()[-1]))
+    assert all(s_["low_latency"] for s_ in summaries)
+    assert summaries[0]["events"] + summaries[1]["events"] == n
+    servers = "fake://synthetic-SENSOR_LL"
+    res = _read_topic(servers, "preds-ll", parts)
+    assert sum(len(v) for v in res.values()) == n
+    cpu = load_model(str(model_file), device="cpu", input_normalizer="cardata")
+    for p, recs in res.items():
+        assert [r["offset"] for r in recs] == list(range(len(recs)))
+        src = next(iter(kafka(servers, [f"SENSOR_LL:{p}:0"]).batch(1 << 20)))
+        assert [r["car"] for r in recs] == list(src.keys)
+        np.testing.assert_allclose([r["score"] for r in recs], cpu.score(src.x), rtol=3e-2, atol=1e-3)
+    assert cli_main(common + ["--replica-index", "0"]) == 0
+    assert json.loads(capsys.readouterr().out.strip().splitlines()[-1])["events"] == 0
