@@ -64,8 +64,15 @@ def _build(ns):
 
 def _train(ns, rows, model):
     T = ns.look_back
-    x = _windows(rows, T)[:len(rows) - T]          # zip(dataset_x, dataset.skip(T)) drops the last window
-    y = rows[T:]
+    if model.device.type == "cuda":
+        # windows as strided views over the device-resident rows, read in place by the
+        # fused LSTM kernels (no [n, T, F] materialisation)
+        import torch
+        from ..data.stream import sliding_windows
+        x, y = sliding_windows(torch.as_tensor(np.ascontiguousarray(rows, np.float32), device=model.device), T)
+    else:
+        x = _windows(rows, T)[:len(rows) - T]      # zip(dataset_x, dataset.skip(T)) drops the last window
+        y = rows[T:]
     print("DATASET: ", f"windows={len(x)} look_back={T} batch={ns.batch_size} take={ns.take}", flush=True)
     t0 = time.perf_counter()
     model.fit(x, y, epochs=ns.epochs, batch_size=ns.batch_size, take=ns.take, verbose=2)

@@ -195,10 +195,21 @@ class LSTMPredictor:
                 xs = np.concatenate([w[0] for w in wins]) if wins else np.zeros((0, self.look_back, self.features))
                 ys = np.concatenate([w[1] for w in wins]) if wins else np.zeros((0, self.features))
                 world_sharded = False
+        elif isinstance(x, torch.Tensor) and x.device == self.device:
+            # device tensors (e.g. data.stream.sliding_windows views) are used as they are
+            xd = x if x.dtype == torch.float32 else x.float()
+            yd = torch.as_tensor(y, device=self.device).float()
+            if world > 1:
+                from ..parallel.dp import shard_range
+                s0, s1 = shard_range(len(xd), dist.get_rank(), world)
+                xd, yd = xd[s0:s1], yd[s0:s1]
+            world_sharded = True
         else:
             xs, ys = np.asarray(x, np.float32), np.asarray(y, np.float32)
             world_sharded = False
-        if not isinstance(x, Stream) or self.device.type != "cuda":
+        device_input = (isinstance(x, Stream) and self.device.type == "cuda") or (
+            isinstance(x, torch.Tensor) and x.device == self.device)
+        if not device_input:
             if world > 1 and not world_sharded:   # contiguous shard per replica (as Autoencoder.fit)
                 from ..parallel.dp import shard_range
                 s0, s1 = shard_range(len(xs), dist.get_rank(), world)

@@ -98,3 +98,27 @@ def test_multiprocess_pipeline_over_tcp_with_sasl(tmp_path):
     finally:
         broker.terminate()
         broker.wait(timeout=30)
+
+
+@pytest.mark.gpu
+def test_lstm_v2_train_on_gpu_uses_persistent_trainer(tmp_path, monkeypatch, capsys, cuda_device):
+    """cardata-v2's job on the GPU: device window views -> LSTMPredictor.fit -> the persistent
+    reference-stack kernel (look_back 1, batch 1); the two-layer stack trains on the fused
+    kernels with in-place windows; mnist trains on the mlp.hip GEMMs."""
+    from streamml.models import lstm as lstm_mod
+    engines = []
+    orig = lstm_mod.LSTMPredictor.fit
+
+    def spy(self, *a, **kw):
+        h = orig(self, *a, **kw)
+        engines.append(self.last_fit_engine)
+        return h
+    monkeypatch.setattr(lstm_mod.LSTMPredictor, "fit", spy)
+    monkeypatch.setenv("SML_MODEL_STORE", str(tmp_path / "store"))
+    base = ["synthetic://2500", "LSTMGPU", "0", "lstm-gpu-out"]
+    common = ["--device", str(cuda_device), "--workdir", str(tmp_path), "--epochs", "2", "--take", "200"]
+    assert cli(["lstm-v2", *base, "train", "lstm.h5", *common]) == 0
+    assert engines == ["persistent"]
+    assert cli(["lstm-v2", *base, "predict", "lstm.h5", *common]) == 0
+    assert cli(["mnist", "--device", str(cuda_device), "--epochs", "1", "--steps-per-epoch", "100",
+                "--rows", "1200"]) == 0

@@ -187,3 +187,17 @@ def test_fused_lstm_vs_bf16_rounded_reference(cuda_device, u, act, B, T, inp, la
     for name, d, r in (("dx", dev[0].grad, dx), ("dW", dev[1].grad, dW), ("dU", dev[2].grad, dU),
                        ("db", dev[3].grad, db)):
         assert relerr(d.cpu(), r) < 1e-3, name
+
+
+def test_fit_accepts_device_window_views(cuda_device):
+    """fit(x, y) with device tensors (sliding_windows views, as the lstm CLIs pass them)
+    trains exactly like fit on the host-materialised arrays."""
+    from streamml.data.stream import sliding_windows
+    rows = np.random.default_rng(3).uniform(-1, 1, (400, 18)).astype(np.float32)
+    X, Y = sliding_windows(torch.from_numpy(rows).to(cuda_device), 6)
+    a = LSTMPredictor.two_layer(look_back=6, device=cuda_device, seed=8)
+    b = LSTMPredictor.two_layer(look_back=6, device=cuda_device, seed=8)
+    ha = a.fit(X, Y, epochs=2, batch_size=50, verbose=0)
+    hb = b.fit(X.cpu().numpy(), Y.cpu().numpy(), epochs=2, batch_size=50, verbose=0)
+    assert ha.history["loss"] == hb.history["loss"]
+    torch.testing.assert_close(a.fp.flat, b.fp.flat, rtol=0, atol=0)
