@@ -68,7 +68,17 @@ class P2PGroup:
         ok, err, g = 1, None, None
         C = load_c()
         dev = torch.device(device)
+        # every rank must reach every other rank's GPU directly (xGMI peer access);
+        # ranks that share a GPU (tests) need no peer mapping
+        my_idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        idxs = [None] * dist.get_world_size(group)
+        dist.all_gather_object(idxs, int(my_idx), group=group)
+        for j in set(idxs):
+            if j != my_idx and not torch.cuda.can_device_access_peer(my_idx, j):
+                ok, err = 0, RuntimeError(f"GPU {my_idx} has no peer access to GPU {j}")
         try:
+            if not ok:
+                raise err
             x = C.P2PExchange(dev.index if dev.index is not None else torch.cuda.current_device(),
                               dist.get_rank(group), dist.get_world_size(group), int(slots))
             h = bytes(x.handle())
@@ -88,6 +98,19 @@ class P2PGroup:
         g.timeout_s, g._last_iter, g.x = float(timeout_s), -1, x
         g.rank, g.world, g.group, g.in_launch = dist.get_rank(group), dist.get_world_size(group), group, False
         dist.barrier(group=group)
+        # self-test before any persistent kernel relies on the exchange: one small all-reduce
+        # of exact integers (bounded device-side polls; a failure disables P2P on every rank)
+        try:
+            t = torch.arange(64, dtype=torch.float32, device=g.device) + float(g.rank)
+            g.allreduce_(t)
+            g.check()
+            want = torch.arange(64, dtype=torch.float32, device=g.device) * g.world + float(sum(range(g.world)))
+            ok = int(bool(torch.equal(t, want)))
+            err = None if ok else RuntimeError("P2P self-test sum mismatch")
+        except Exception as e:  # noqa: BLE001 - agreed on below
+            ok, err = 0, e
+        if not agree([ok], dev)[0]:
+            return None, err or RuntimeError("P2P self-test failed on a peer")
         return g, None
 
     @classmethod
