@@ -42,6 +42,8 @@
 #include "sml_common.h"
 #include "sml_p2p.h"
 
+#include <type_traits>
+
 using namespace sml;
 
 namespace {
@@ -208,8 +210,10 @@ __device__ __forceinline__ f32x4 layer16(const float* frag, const float* bias, i
 // KD: compiled input width class (<= 18 -> 6 K-steps, 32 -> 8); TB: batch (0 = runtime);
 // PACK: activation codes (-1 = runtime); WPE: minimum waves per SIMD the register
 // allocation must allow (2 = one workgroup per CU, the latency-optimal single-model
-// build; 4 = <= 128 VGPRs, two fleet models per CU); MB: LDS capacity class (rows)
-template <int KD, int TB, int PACK, int WPE = 2, int MB = MB_SMALL>
+// build; 4 = <= 128 VGPRs, two fleet models per CU); MB: LDS capacity class (rows);
+// DPX: compiled with the in-kernel gradient exchange (a runtime-gated exchange in the
+// single-replica build cost 0.4-0.5 us per batch-32 step, profiles/r02)
+template <int KD, int TB, int PACK, int WPE = 2, int MB = MB_SMALL, bool DPX = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void ae_minibatch_kernel(MBArgs a0) {
   static_assert(TB <= MB, "compiled batch exceeds the LDS capacity class");
   static_assert(KD <= 32, "input width <= 32");
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     S.one[0] = 1.f;
     S.abort = 0;
   }
-  const bool dp = a.dp_ranks > 1;
+  const bool dp = DPX && a.dp_ranks > 1;
   const int dp_rank = a.dp_rank0 + (int)blockIdx.x;
 
   // ---- phase-A input operands: lane (c, g) of wave w holds row 16w + c, features f(s, g) ----
@@ -586,21 +590,29 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
   const bool ref = acts[0] == ACT_TANH && acts[1] == ACT_RELU && acts[2] == ACT_TANH && acts[3] == ACT_RELU;
   void (*k)(MBArgs) = nullptr;
   size_t lds = 0;
-  if (B <= MB_SMALL) {
-    lds = sizeof(Smem<MB_SMALL>);
-    k = ae_minibatch_kernel<32, 0, -1>;   // any shape / activations
-    if (ref && dims[0] <= 18) k = B == 32 ? ae_minibatch_kernel<18, 32, PACK_REF> : ae_minibatch_kernel<18, 0, PACK_REF>;
-    else if (ref) k = B == 32 ? ae_minibatch_kernel<32, 32, PACK_REF> : ae_minibatch_kernel<32, 0, PACK_REF>;
-    // (a 128-VGPR two-models-per-CU build measured no faster for fleets beyond the CU count:
-    // 3.92 vs 3.96 G rows/s at 1024 / 256 models, profiles/r02)
-  } else {
-    // cardata-v3's fit(batch_size=100) and anything up to 128 rows: one workgroup per CU
-    lds = sizeof(Smem<MB_LARGE>);
-    k = ae_minibatch_kernel<32, 0, -1, 2, MB_LARGE>;
-    if (ref && dims[0] <= 18)
-      k = B == 100 ? ae_minibatch_kernel<18, 100, PACK_REF, 2, MB_LARGE> : ae_minibatch_kernel<18, 0, PACK_REF, 2, MB_LARGE>;
-    else if (ref) k = ae_minibatch_kernel<32, 0, PACK_REF, 2, MB_LARGE>;
-  }
+  auto pick = [&](auto dpx) {
+    constexpr bool X = decltype(dpx)::value;
+    if (B <= MB_SMALL) {
+      lds = sizeof(Smem<MB_SMALL>);
+      k = ae_minibatch_kernel<32, 0, -1, 2, MB_SMALL, X>;   // any shape / activations
+      if (ref && dims[0] <= 18)
+        k = B == 32 ? ae_minibatch_kernel<18, 32, PACK_REF, 2, MB_SMALL, X> : ae_minibatch_kernel<18, 0, PACK_REF, 2, MB_SMALL, X>;
+      else if (ref)
+        k = B == 32 ? ae_minibatch_kernel<32, 32, PACK_REF, 2, MB_SMALL, X> : ae_minibatch_kernel<32, 0, PACK_REF, 2, MB_SMALL, X>;
+      // (a 128-VGPR two-models-per-CU build measured no faster for fleets beyond the CU count:
+      // 3.92 vs 3.96 G rows/s at 1024 / 256 models, profiles/r02)
+    } else {
+      // cardata-v3's fit(batch_size=100) and anything up to 128 rows: one workgroup per CU
+      lds = sizeof(Smem<MB_LARGE>);
+      k = ae_minibatch_kernel<32, 0, -1, 2, MB_LARGE, X>;
+      if (ref && dims[0] <= 18)
+        k = B == 100 ? ae_minibatch_kernel<18, 100, PACK_REF, 2, MB_LARGE, X>
+                     : ae_minibatch_kernel<18, 0, PACK_REF, 2, MB_LARGE, X>;
+      else if (ref) k = ae_minibatch_kernel<32, 0, PACK_REF, 2, MB_LARGE, X>;
+    }
+  };
+  if (dp_ranks > 1) pick(std::true_type{});
+  else pick(std::false_type{});
   if (lds > 65536) {   // > 64 KB of dynamic LDS must be opted into per kernel
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
