@@ -208,7 +208,7 @@ class Autoencoder:
                 arr = arr[s0:s1]
             # device arrays stay on the device (no host round trip)
             xd = self._to_device(arr) if self.device.type == "cuda" else self._cpu_x(arr)
-        from ..parallel.fault import maybe_inject
+        from ..parallel.fault import maybe_inject, maybe_inject_range
         persistent = self._use_persistent(engine, batch_size, world, dp)
         exch, local_k = None, 0
         if persistent and world > 1:
@@ -241,8 +241,7 @@ class Autoencoder:
                 if steps_per_epoch is not None:
                     nb = min(nb, steps_per_epoch)
                 xs = xd[self._device_perm(n, seed, rank, epoch)] if shuffle else xd
-                for s in range(gstep, gstep + nb):   # injection points, before the epoch's launches
-                    maybe_inject(s, rank)
+                maybe_inject_range(gstep, gstep + nb, rank)   # injection points, before the epoch's launches
                 if world > 1:
                     steps = self._dp_train(xs[:nb * batch_size], batch_size, exch, local_k)
                 else:
@@ -415,7 +414,7 @@ class Autoencoder:
         ``train_rows`` (hundreds of Keras steps per launch); the < B rows left at a chunk
         boundary are carried to the next chunk, so the batches are exactly the
         reference's ``batch(B)`` over the (filtered) stream; ``max_steps`` = ``take(n)``."""
-        from ..parallel.fault import maybe_inject
+        from ..parallel.fault import maybe_inject, maybe_inject_range
         be = self.backend
         D = self.spec.input_dim
         carry = torch.empty((B, D), dtype=torch.float32, device=self.device)
@@ -443,8 +442,7 @@ class Autoencoder:
             if max_steps is not None:
                 nfull = min(nfull, max_steps - steps)
             if nfull:
-                for s in range(gstep + steps, gstep + steps + nfull):
-                    maybe_inject(s, rank)
+                maybe_inject_range(gstep + steps, gstep + steps + nfull, rank)
                 s, _ = be.train_rows(xd[pos:pos + nfull * B], B)
                 steps += s
                 pos += nfull * B

@@ -40,3 +40,13 @@ def maybe_inject(step: int, rank: int) -> None:
     if mode == "hang":
         time.sleep(float(os.environ.get("SML_FAULT_HANG_S", "3600")))
     os._exit(17)
+
+
+def maybe_inject_range(start: int, stop: int, rank: int) -> None:
+    """``maybe_inject`` for every step in ``[start, stop)`` -- the injection points of a
+    whole persistent-kernel launch -- at O(1) cost (an epoch is ~10^4-10^5 steps)."""
+    fs = os.environ.get("SML_FAULT_STEP")
+    if fs is None or os.environ.get("SML_FAULT_RANK") is None:
+        return
+    if start <= int(fs) < stop:
+        maybe_inject(int(fs), rank)
