@@ -50,9 +50,13 @@ int dense_wgrad_slab(int K, int N);
 int dense_wgrad_grid(int64_t M, int max_blocks);
 int slab_sum_scratch(int G, int S);
 int slab_sum_level_launch(const float* in, int G, int S, float* out, hipStream_t stream);
-hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, float* out, hipStream_t stream);
+// map (optional, S ints): the final level writes element s to out[map[s]] (< 0: dropped)
+hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, float* out, hipStream_t stream,
+                           const int* map = nullptr);
+// w_t: W is the row-major [N, K] weight used transposed (Y = X . W^T)
 hipError_t rowgemm_launch(const void* X, int x_bf16, int64_t M, int K, int64_t ldx, const float* W, const float* bias,
-                          int N, int act, void* Y, int y_bf16, int64_t ldy, int max_blocks, hipStream_t stream);
+                          int N, int act, void* Y, int y_bf16, int64_t ldy, int max_blocks, hipStream_t stream,
+                          int w_t = 0);
 hipError_t wgrad_launch(const void* X, int x_bf16, int64_t M, int K, int64_t ldx, int shift_T, const void* DY,
                         int dy_bf16, int N, int64_t ldy, int want_db, float* partials, int grid, hipStream_t stream);
 

@@ -96,13 +96,16 @@ __device__ __forceinline__ void store4<__bf16>(__bf16* row, int n0, int N, f32x4
 // into registers while the current tile's MFMAs and stores run.
 template <int KT, int NT, typename TX, typename TY>
 __global__ __launch_bounds__(kThreads) void rowgemm_kernel(const TX* __restrict__ X, int64_t M, int K, int64_t ldx,
-                                                            const float* __restrict__ W, const float* __restrict__ bias,
-                                                            int N, int act, TY* __restrict__ Y, int64_t ldy) {
+                                                            const float* __restrict__ W, int wsk, int wsn,
+                                                            const float* __restrict__ bias, int N, int act,
+                                                            TY* __restrict__ Y, int64_t ldy) {
   __shared__ float ws[16 * KT][16 * NT];
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  // W element (k, n) at W[k * wsk + n * wsn]: a row-major [K, N] weight, or (wsk = 1,
+  // wsn = K) the transpose of a row-major [N, K] one -- dX = dY . W^T without a copy of W^T
   for (int i = threadIdx.x; i < 16 * KT * 16 * NT; i += kThreads) {
     const int k = i / (16 * NT), n = i % (16 * NT);
-    ws[k][n] = (k < K && n < N) ? W[(int64_t)k * N + n] : 0.0f;
+    ws[k][n] = (k < K && n < N) ? W[(int64_t)k * wsk + (int64_t)n * wsn] : 0.0f;
   }
   __syncthreads();
   // W^T fragments: A[m = out feature 16nt + c][k = in feature 16kt + 4g + j] = W[k][m]
@@ -299,8 +302,11 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(const TX* __restrict__ 
 // LDS in fixed order.  Applied level by level until one slab remains.
 constexpr int kSlabChunk = 32;
 
+// MAP (final level only): element s goes to out[map[s]] (map[s] < 0: dropped) -- the
+// slab layout scattered straight into a flat gradient buffer (transposes included)
+template <bool MAP = false>
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ in, int G, int S,
-                                                       float* __restrict__ out) {
+                                                       float* __restrict__ out, const int* __restrict__ map = nullptr) {
   __shared__ f32x4 red[4][64];
   const int q = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int quad = blockIdx.x * 64 + q;
@@ -320,7 +326,15 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
   __syncthreads();
   if (grp == 0 && quad * 4 < S) {
     const f32x4 t = red[0][q] + red[1][q] + red[2][q] + red[3][q];
-    *reinterpret_cast<f32x4*>(out + (int64_t)blockIdx.y * S + quad * 4) = t;
+    if constexpr (MAP) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = map[quad * 4 + j];
+        if (d >= 0) out[d] = t[j];
+      }
+    } else {
+      *reinterpret_cast<f32x4*>(out + (int64_t)blockIdx.y * S + quad * 4) = t;
+    }
   }
 }
 
@@ -381,7 +395,8 @@ int slab_sum_scratch(int G, int S) {
 
 // sum G slabs of S floats (S % 4 == 0) into out[S]; intermediate levels go to
 // consecutive regions of scratch (slab_sum_scratch(G, S) floats)
-hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, float* out, hipStream_t stream) {
+hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, float* out, hipStream_t stream,
+                           const int* map) {
   if (S % 4 != 0 || G < 1) return hipErrorInvalidValue;
   const float* src = partials;
   float* buf = scratch;
@@ -389,7 +404,11 @@ hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, 
   while (true) {
     const int gy = (g + kSlabChunk - 1) / kSlabChunk;
     float* dst = gy == 1 ? out : buf;
-    hipLaunchKernelGGL(slab_sum_kernel, dim3((S / 4 + 63) / 64, gy), dim3(256), 0, stream, src, g, S, dst);
+    if (gy == 1 && map)
+      hipLaunchKernelGGL(slab_sum_kernel<true>, dim3((S / 4 + 63) / 64, 1), dim3(256), 0, stream, src, g, S, dst, map);
+    else
+      hipLaunchKernelGGL(slab_sum_kernel<false>, dim3((S / 4 + 63) / 64, gy), dim3(256), 0, stream, src, g, S, dst,
+                         nullptr);
     if (gy == 1) break;
     src = dst;
     buf = dst + (int64_t)gy * S;
@@ -402,7 +421,7 @@ hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, 
 int slab_sum_level_launch(const float* in, int G, int S, float* out, hipStream_t stream) {
   if (S % 4 != 0 || G < 1) return -1;
   const int gy = (G + kSlabChunk - 1) / kSlabChunk;
-  hipLaunchKernelGGL(slab_sum_kernel, dim3((S / 4 + 63) / 64, gy), dim3(256), 0, stream, in, G, S, out);
+  hipLaunchKernelGGL(slab_sum_kernel<false>, dim3((S / 4 + 63) / 64, gy), dim3(256), 0, stream, in, G, S, out, nullptr);
   return gy;
 }
 
@@ -412,25 +431,27 @@ bool dense_supported(int K, int N) {
 }
 
 hipError_t rowgemm_launch(const void* X, int x_bf16, int64_t M, int K, int64_t ldx, const float* W, const float* bias,
-                          int N, int act, void* Y, int y_bf16, int64_t ldy, int max_blocks, hipStream_t stream) {
+                          int N, int act, void* Y, int y_bf16, int64_t ldy, int max_blocks, hipStream_t stream,
+                          int w_t) {
   if (M <= 0) return hipSuccess;
   if (!dense_supported(K, N)) return hipErrorInvalidValue;
   const int KT = round_tiles(K), NT = round_tiles(N);
   const int grid = grid_for(M, max_blocks);
+  const int wsk = w_t ? 1 : N, wsn = w_t ? K : 1;
   bool ok = dispatch_kn(KT, NT, [&](auto kt, auto nt) {
     constexpr int A = decltype(kt)::value, B = decltype(nt)::value;
     if (x_bf16 && y_bf16)
       hipLaunchKernelGGL((rowgemm_kernel<A, B, __bf16, __bf16>), dim3(grid), dim3(kThreads), 0, stream,
-                         (const __bf16*)X, M, K, ldx, W, bias, N, act, (__bf16*)Y, ldy);
+                         (const __bf16*)X, M, K, ldx, W, wsk, wsn, bias, N, act, (__bf16*)Y, ldy);
     else if (x_bf16)
       hipLaunchKernelGGL((rowgemm_kernel<A, B, __bf16, float>), dim3(grid), dim3(kThreads), 0, stream,
-                         (const __bf16*)X, M, K, ldx, W, bias, N, act, (float*)Y, ldy);
+                         (const __bf16*)X, M, K, ldx, W, wsk, wsn, bias, N, act, (float*)Y, ldy);
     else if (y_bf16)
       hipLaunchKernelGGL((rowgemm_kernel<A, B, float, __bf16>), dim3(grid), dim3(kThreads), 0, stream,
-                         (const float*)X, M, K, ldx, W, bias, N, act, (__bf16*)Y, ldy);
+                         (const float*)X, M, K, ldx, W, wsk, wsn, bias, N, act, (__bf16*)Y, ldy);
     else
       hipLaunchKernelGGL((rowgemm_kernel<A, B, float, float>), dim3(grid), dim3(kThreads), 0, stream,
-                         (const float*)X, M, K, ldx, W, bias, N, act, (float*)Y, ldy);
+                         (const float*)X, M, K, ldx, W, wsk, wsn, bias, N, act, (float*)Y, ldy);
   });
   if (!ok) return hipErrorInvalidValue;
   return hipGetLastError();

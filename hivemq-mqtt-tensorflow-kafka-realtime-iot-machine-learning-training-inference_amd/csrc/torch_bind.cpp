@@ -406,14 +406,16 @@ void softmax_xent(const at::Tensor& logits, const at::Tensor& labels, double gsc
 }
 
 // K1: Y = act(X . W + b) for tall-skinny X [M, K] (fp32 or bf16), W [K, N] fp32.
+// w_t: W is a contiguous [N, K] weight applied transposed (dX = dY . W^T, no W^T copy).
 at::Tensor dense_fwd(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::Tensor>& bias, int64_t act,
-                     bool out_bf16, int64_t max_blocks) {
+                     bool out_bf16, int64_t max_blocks, bool w_t) {
   TORCH_CHECK(x.is_cuda() && W.is_cuda(), "dense_fwd needs ROCm device tensors");
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be fp32 or bf16");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [M, K] with unit inner stride");
   check_dev(W, "W", at::kFloat);
-  TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.size(0) == x.size(1), "W must be contiguous [K, N]");
-  const int64_t M = x.size(0), K = x.size(1), N = W.size(1);
+  TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.size(w_t ? 1 : 0) == x.size(1),
+              w_t ? "W must be contiguous [N, K]" : "W must be contiguous [K, N]");
+  const int64_t M = x.size(0), K = x.size(1), N = W.size(w_t ? 0 : 1);
   TORCH_CHECK(sml::dense_supported((int)K, (int)N), "dense_fwd: K=", K, " N=", N, " exceeds the register tile");
   if (bias.has_value()) {
     check_dev(*bias, "bias", at::kFloat);
@@ -424,14 +426,29 @@ at::Tensor dense_fwd(const at::Tensor& x, const at::Tensor& W, const c10::option
   auto y = at::empty({M, N}, x.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
   SML_CHECK_HIP(sml::rowgemm_launch(x.data_ptr(), x.scalar_type() == at::kBFloat16, M, (int)K, x.stride(0),
                                     W.data_ptr<float>(), opt_ptr(bias), (int)N, (int)act, y.data_ptr(), out_bf16, N,
-                                    (int)max_blocks, cur_stream(x)));
+                                    (int)max_blocks, cur_stream(x), w_t ? 1 : 0));
   return y;
+}
+
+// Optional (grad, map) pair of the weight-gradient bindings: the final slab reduction
+// writes slab element s straight to grad[map[s]] (the parameter's place in a flat
+// gradient buffer, transposes included; map[s] < 0 drops padding), so a train step
+// needs no copy / transpose / accumulate kernels between the backward and Adam.
+static const int* grad_map(const c10::optional<at::Tensor>& grad, const c10::optional<at::Tensor>& map, int S) {
+  TORCH_CHECK(grad.has_value() == map.has_value(), "grad and map go together");
+  if (!grad.has_value()) return nullptr;
+  check_dev(*grad, "grad", at::kFloat);
+  TORCH_CHECK(grad->is_contiguous(), "grad must be contiguous");
+  TORCH_CHECK(map->is_cuda() && map->scalar_type() == at::kInt && map->is_contiguous() && map->numel() == S,
+              "map must be a device int32 tensor of the slab size ", S);
+  return map->data_ptr<int>();
 }
 
 // K2 (weight half): dW = X^T . dY, db = colsum(dY) over M rows (split-row MFMA + slab reduce).
 // shift_T > 0: X row r is read as X[r - 1] (zero when r % shift_T == 0).
 std::vector<at::Tensor> dense_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t shift_T, bool want_db,
-                                    int64_t max_blocks) {
+                                    int64_t max_blocks, const c10::optional<at::Tensor>& grad,
+                                    const c10::optional<at::Tensor>& map) {
   TORCH_CHECK(x.is_cuda() && dy.is_cuda(), "dense_wgrad needs ROCm device tensors");
   for (const auto* t : {&x, &dy}) {
     TORCH_CHECK(t->scalar_type() == at::kFloat || t->scalar_type() == at::kBFloat16, "inputs must be fp32 or bf16");
@@ -444,15 +461,17 @@ std::vector<at::Tensor> dense_wgrad(const at::Tensor& x, const at::Tensor& dy, i
   const int S = sml::dense_wgrad_slab((int)K, (int)N);
   const int G = sml::dense_wgrad_grid(M, (int)max_blocks);
   auto opts = x.options().dtype(at::kFloat);
+  const int* mp = grad_map(grad, map, S);
   auto partials = at::empty({G, S}, opts);
-  auto out = at::empty({S}, opts);
+  auto out = mp ? *grad : at::empty({S}, opts);
   auto scratch = at::empty({std::max(1, sml::slab_sum_scratch(G, S))}, opts);
   auto st = cur_stream(x);
   SML_CHECK_HIP(sml::wgrad_launch(x.data_ptr(), x.scalar_type() == at::kBFloat16, M, (int)K, x.stride(0),
                                   (int)shift_T, dy.data_ptr(), dy.scalar_type() == at::kBFloat16, (int)N,
                                   dy.stride(0), want_db ? 1 : 0, partials.data_ptr<float>(), G, st));
   SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
-                                     out.data_ptr<float>(), st));
+                                     out.data_ptr<float>(), st, mp));
+  if (mp) return {at::Tensor(), at::Tensor()};
   const int64_t KP = 16 * sml::dense_tiles((int)K), NP = 16 * sml::dense_tiles((int)N);
   auto dW = out.narrow(0, 0, KP * NP).view({KP, NP}).narrow(0, 0, K).narrow(1, 0, N);
   auto db = out.narrow(0, KP * NP, N);
@@ -504,7 +523,8 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
                                        const at::Tensor& x, const c10::optional<at::Tensor>& h0,
                                        const c10::optional<at::Tensor>& c0, const at::Tensor& W, const at::Tensor& Uw,
                                        const at::Tensor& b, int64_t act, bool want_dx, bool want_state_grads,
-                                       bool dh_last_only) {
+                                       bool dh_last_only, const c10::optional<at::Tensor>& grad,
+                                       const c10::optional<at::Tensor>& map) {
   check_dev(dh, "dh", at::kBFloat16);
   check_dev(cseq, "c", at::kBFloat16);
   check_dev(hseq, "h", at::kBFloat16);
@@ -541,8 +561,9 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
   }
   const int S = sml::lstm_fused_slab((int)U, (int)IN);
   const int G = sml::lstm_fused_slabs(B);
+  const int* mp = grad_map(grad, map, S);
   auto partials = at::empty({G, S}, opts);   // every workgroup writes its slab (idle waves add nothing)
-  auto out = at::empty({S}, opts);
+  auto out = mp ? *grad : at::empty({S}, opts);
   auto scratch = at::empty({std::max(1, sml::slab_sum_scratch(G, S))}, opts);
   auto st = cur_stream(x);
   SML_CHECK_HIP(sml::lstm_fused_bwd_launch(
@@ -552,11 +573,14 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
       want_state_grads ? dc0.data_ptr<float>() : nullptr, partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U,
       (int)act, dh_last_only ? 1 : 0, x_seq, st));
   SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
-                                     out.data_ptr<float>(), st));
+                                     out.data_ptr<float>(), st, mp));
   const int64_t G4 = 4 * U, LDW = (S / G4) - U - 1;
-  auto dW = out.narrow(0, 0, G4 * LDW).view({G4, LDW}).narrow(1, 0, IN).t().contiguous();
-  auto dU = out.narrow(0, G4 * LDW, G4 * U).view({G4, U}).t().contiguous();
-  auto db = out.narrow(0, G4 * LDW + G4 * U, G4);
+  at::Tensor dW, dU, db;
+  if (!mp) {
+    dW = out.narrow(0, 0, G4 * LDW).view({G4, LDW}).narrow(1, 0, IN).t().contiguous();
+    dU = out.narrow(0, G4 * LDW, G4 * U).view({G4, U}).t().contiguous();
+    db = out.narrow(0, G4 * LDW + G4 * U, G4);
+  }
   if (want_dx) {
     dx = dx_pad.narrow(0, 0, B);
     if (dx_pad.size(2) != IN) dx = dx.narrow(2, 0, IN).contiguous();
@@ -925,9 +949,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("labels"), py::arg("gscale"), py::arg("dlogits") = py::none(), py::arg("probs") = py::none(),
         py::arg("acc") = py::none());
   m.def("dense_fwd", &dense_fwd, "K1 tall-skinny dense forward act(X.W + b) on MFMA", py::arg("x"), py::arg("W"),
-        py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("out_bf16") = false, py::arg("max_blocks") = 1024);
+        py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("out_bf16") = false, py::arg("max_blocks") = 1024,
+        py::arg("w_t") = false);
   m.def("dense_wgrad", &dense_wgrad, "K2 weight gradient X^T.dY (+ colsum dY) over rows", py::arg("x"),
-        py::arg("dy"), py::arg("shift_T") = 0, py::arg("want_db") = true, py::arg("max_blocks") = 1024);
+        py::arg("dy"), py::arg("shift_T") = 0, py::arg("want_db") = true, py::arg("max_blocks") = 1024,
+        py::arg("grad") = py::none(), py::arg("map") = py::none());
+  m.def("dense_wgrad_slab", &sml::dense_wgrad_slab, "floats per dense_wgrad slab", py::arg("K"), py::arg("N"));
+  m.def("dense_tiles", &sml::dense_tiles, "16-wide tiles a dense dimension is padded to", py::arg("d"));
+  m.def("lstm_fused_slab", &sml::lstm_fused_slab, "floats per fused-LSTM weight-gradient slab", py::arg("U"),
+        py::arg("IN"));
+  m.def("lstm_fused_dx_ld", &sml::lstm_fused_dx_ld, "padded feature stride of the fused-LSTM slab / dx",
+        py::arg("IN"));
   m.def("dense_supported", &sml::dense_supported, "whether (K, N) fits the register-resident tile", py::arg("K"),
         py::arg("N"));
   m.def("lstm_fused_fwd", &lstm_fused_fwd, "fully fused LSTM layer forward (x.W + recurrence in one kernel)",
@@ -937,7 +969,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "fully fused LSTM layer backward (gate recompute + BPTT + dW/dU/db + dX in one kernel)", py::arg("dh"),
         py::arg("c"), py::arg("h"), py::arg("x"), py::arg("h0") = py::none(), py::arg("c0") = py::none(),
         py::arg("W"), py::arg("U"), py::arg("b"), py::arg("act") = 1, py::arg("want_dx") = true,
-        py::arg("want_state_grads") = false, py::arg("dh_last_only") = false);
+        py::arg("want_state_grads") = false, py::arg("dh_last_only") = false, py::arg("grad") = py::none(),
+        py::arg("map") = py::none());
   m.def("lstm_ref_train", &lstm_ref_train,
         "persistent trainer: nsteps Keras Adam steps of the reference LSTM stack (look_back 1) in one launch",
         py::arg("flat"), py::arg("m"), py::arg("v"), py::arg("iter"), py::arg("x"), py::arg("y"),

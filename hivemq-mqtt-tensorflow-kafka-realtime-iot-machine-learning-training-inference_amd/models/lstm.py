@@ -147,6 +147,9 @@ class LSTMPredictor:
 
     def train_step(self, x: torch.Tensor, y: torch.Tensor, global_batch: Optional[int] = None, allreduce=None):
         n = x.shape[0]
+        plan = self._fused_plan()
+        if plan is not None and x.is_cuda and x.dim() == 3 and y.dim() == 2 and n > 0:
+            return self._fused_step(plan, x, y, global_batch, allreduce)
         self.fp.zero_grad()
         y_pred = self.forward(x)
         loss, correct = self._loss(y_pred, y)
@@ -154,6 +157,101 @@ class LSTMPredictor:
         (loss * scale).backward()
         self.opt.step(allreduce=allreduce)
         return loss.detach(), correct.detach()
+
+    def _fused_plan(self):
+        """Whether a train step can run as explicit kernel calls (no autograd graph): fused
+        LSTM layers (the last one ``return_sequences=False``) and one Dense head, e.g.
+        :meth:`two_layer`.  Builds, once, the int32 maps that scatter each layer's
+        weight-gradient slab straight into the flat gradient buffer."""
+        if getattr(self, "_plan_built", False):
+            return self._plan
+        self._plan_built, self._plan = True, None
+        if self.device.type != "cuda":
+            return None
+        from ..ops.dense import supported as dense_ok
+        from ..ops.loss import supported as mse_ok
+        from ..ops.lstm import fused_supported
+        lstms, head = self.layers[:-1], self.layers[-1]
+        if (not lstms or head["kind"] != "dense" or head["td"] or not mse_ok(head["units"])
+                or not dense_ok(head["in_dim"], head["units"])):
+            return None
+        for i, L in enumerate(lstms):
+            if (L["kind"] != "lstm" or L["return_sequences"] != (i < len(lstms) - 1)
+                    or not fused_supported(L["units"], L["in_dim"])):
+                return None
+        from ..ops._ext import load_c
+        C = load_c()
+        off = self.fp.offsets
+        maps = []
+        for L in lstms:
+            u, IN = L["units"], L["in_dim"]
+            G4, ldw = 4 * u, C.lstm_fused_dx_ld(IN)
+            S = C.lstm_fused_slab(u, IN)
+            mp = np.full(S, -1, np.int64)
+            oW, oU, ob = (int(off[L["params"] + k]) for k in range(3))
+            m, f = np.meshgrid(np.arange(G4), np.arange(ldw), indexing="ij")   # slab [G4][ldw] = dW^T
+            mp[:G4 * ldw] = np.where(f < IN, oW + f * G4 + m, -1).ravel()
+            m, uu = np.meshgrid(np.arange(G4), np.arange(u), indexing="ij")   # [G4][u] = dU^T
+            mp[G4 * ldw:G4 * (ldw + u)] = (oU + uu * G4 + m).ravel()
+            mp[G4 * (ldw + u):] = ob + np.arange(G4)
+            assert G4 * (ldw + u + 1) == S
+            maps.append(torch.as_tensor(mp.astype(np.int32), device=self.device))
+        K, N = head["in_dim"], head["units"]
+        KP, NP = 16 * C.dense_tiles(K), 16 * C.dense_tiles(N)
+        S = C.dense_wgrad_slab(K, N)
+        mp = np.full(S, -1, np.int64)
+        oK, ob = int(off[head["params"]]), int(off[head["params"] + 1])
+        k, nn = np.meshgrid(np.arange(KP), np.arange(NP), indexing="ij")
+        mp[:KP * NP] = np.where((k < K) & (nn < N), oK + k * N + nn, -1).ravel()
+        mp[KP * NP:KP * NP + NP] = np.where(np.arange(NP) < N, ob + np.arange(NP), -1)
+        head_map = torch.as_tensor(mp.astype(np.int32), device=self.device)
+        self._plan = dict(lstms=lstms, head=head, maps=maps, head_map=head_map,
+                          acc=torch.zeros(2, device=self.device))
+        return self._plan
+
+    def _fused_step(self, plan, x, y, global_batch, allreduce):
+        """One train step as explicit kernel calls on the flat buffers: per LSTM layer one
+        fused forward and one fused backward (weight-gradient slabs reduced straight into
+        the flat gradient through ``plan['maps']``), the Dense head on K1/K2 reading h_T in
+        place, the fused MSE + accuracy kernel, one Adam launch.  Same kernels and
+        rounding points as the autograd path, ~20 fewer small launches per step."""
+        from ..ops._ext import load_c
+        from ..ops.lstm import ACT
+        C = load_c()
+        P, grad = self.fp.params, self.fp.grad
+        n = x.shape[0]
+        if not (x.stride(2) == 1 and x.stride(1) == x.shape[2] and x.stride(0) >= 0):
+            x = x.contiguous()
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        saved = []
+        h = x
+        for L in plan["lstms"]:
+            W, Uw, b = P[L["params"]:L["params"] + 3]
+            hs, c = C.lstm_fused_fwd(h, W.detach(), Uw.detach(), b.detach(), None, None, ACT[L["activation"]])
+            saved.append((h, hs, c))
+            h = hs
+        hT = h[:, -1]                                  # bf16 [n, U] view, read in place
+        hd = plan["head"]
+        K, bh = (t.detach() for t in P[hd["params"]:hd["params"] + 2])
+        y_pred = C.dense_fwd(hT, K, bh, 0, False, 1024, False)
+        yt = y.to(device=self.device, dtype=torch.float32).contiguous()
+        acc = plan["acc"]
+        acc.zero_()
+        dy = torch.empty_like(y_pred)
+        scale = n / float(global_batch or n)           # mean over the global batch under DP
+        C.mse_acc(y_pred, yt, 1, 2.0 / y_pred.numel() * scale, dy, acc)
+        C.dense_wgrad(hT, dy, 0, True, 1024, grad, plan["head_map"])
+        dh = C.dense_fwd(dy, K, None, 0, True, 1024, True)   # dh_T = dy . K^T, bf16
+        for i in range(len(plan["lstms"]) - 1, -1, -1):
+            L = plan["lstms"][i]
+            xin, hs, c = saved[i]
+            W, Uw, b = (t.detach() for t in P[L["params"]:L["params"] + 3])
+            out = C.lstm_fused_bwd(dh, c, hs, xin, None, None, W, Uw, b, ACT[L["activation"]], i > 0, False,
+                                   i == len(plan["lstms"]) - 1, grad, plan["maps"][i])
+            dh = out[0]
+        self.opt.step(allreduce=allreduce)
+        return acc[0] / y_pred.numel(), acc[1]
 
     # ------------------------------------------------------------------ training
     def fit(self, x, y=None, epochs: int = 1, batch_size: int = 1, verbose: int = 1, take: Optional[int] = None,

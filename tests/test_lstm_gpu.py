@@ -121,6 +121,30 @@ def test_graph_replayed_train_steps_match_eager(cuda_device):
     torch.testing.assert_close(loss_g, loss_e, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("B,T", [(256, 20), (100, 7), (33, 50)])
+def test_fused_step_matches_autograd_step(cuda_device, B, T):
+    """LSTMPredictor._fused_step (explicit kernel calls, weight-gradient slabs scattered
+    straight into the flat gradient, dh_T = dy . K^T from the transposed-weight K1) gives
+    the same gradients, Adam updates and losses as the autograd step over the same
+    kernels, on in-place sliding windows."""
+    from streamml.data.stream import sliding_windows
+    rows = torch.tensor(np.random.default_rng(B + T).uniform(-1, 1, (3 * B + T, 18)), dtype=torch.float32,
+                        device=cuda_device)
+    X, Y = sliding_windows(rows, T)
+    fused = LSTMPredictor.two_layer(look_back=T, device=cuda_device, seed=6)
+    auto = LSTMPredictor.two_layer(look_back=T, device=cuda_device, seed=6)
+    assert fused._fused_plan() is not None
+    auto._plan_built, auto._plan = True, None          # force the autograd path
+    for s in range(3):
+        sl = slice(s * B, (s + 1) * B)
+        lf, cf = fused.train_step(X[sl], Y[sl])
+        la, ca = auto.train_step(X[sl], Y[sl])
+        torch.testing.assert_close(fused.fp.grad, auto.fp.grad, rtol=1e-6, atol=1e-9)
+        torch.testing.assert_close(lf, la, rtol=1e-6, atol=0)
+        assert float(cf) == float(ca)
+    torch.testing.assert_close(fused.fp.flat, auto.fp.flat, rtol=1e-6, atol=1e-8)
+
+
 @pytest.mark.parametrize("stack", ["two_layer", "reference"])
 def test_in_place_windows_match_materialized(cuda_device, stack):
     """Sliding windows read in place (strided [n, T, F] views over the event rows, sequence
