@@ -75,7 +75,11 @@ struct FusedBwdArgs {
   int64_t x_seq;       // elements between consecutive sequences of x (T*IN contiguous, IN sliding windows)
 };
 
-template <int U, int KT, int XV, typename XT, int ACT>
+// DX: the input gradient is wanted (compile-time: the first layer of a stack needs none).
+// RF: weight A fragments kept in registers for the whole launch instead of re-read from
+// LDS every step (bits: 1 the recurrent U fragments of the dh chain, 2 the gate
+// recompute's [W^T | U^T], 4 the dX fragments W) -- where the registers exist, see launch_bwd.
+template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdArgs a) {
   using XR = typename RowRaw<XT>::type;
   constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
@@ -85,8 +89,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   __shared__ __attribute__((aligned(16))) char scratch[WAVES][NTR * 512];
   __shared__ __attribute__((aligned(16))) float slab[S];   // the workgroup's combined weight-gradient slab
   // Weight A fragments, shared by the 4 waves, [tile][lane] bf16x4 (conflict-free
-  // ds_read_b64), read in the loop through an opaque lane offset so the compiler cannot
-  // hoist all of them into registers (that costs ~130 registers and spills):
+  // ds_read_b64).  RF selects which stay in registers for the launch; the rest are read
+  // in the loop through an opaque lane offset so the compiler cannot hoist them (all
+  // three sets together, with dX, would not fit next to the accumulators):
   //   wfwd: W^T / U^T (forward orientation, gate recompute), ufl: U (dh), wfl: W (dX)
   __shared__ __attribute__((aligned(16))) bf16x4 wfwd[MT * (KT + UB) * 64];
   __shared__ __attribute__((aligned(16))) bf16x4 ufl[UB * MT * 64];
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   }
 
   // A fragments: U[m = unit 16b + c][k = gate 16kt + 4g + j] (for dh), W[m = feature][k = gate] (for dX)
-  const bool want_dx = a.dx != nullptr;
+  const bool want_dx = DX && a.dx != nullptr;
   for (int tile = w; tile < UB * MT; tile += WAVES) {
     const int b = tile / MT, kt = tile % MT;
     f32x4 t4;
@@ -141,6 +146,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   __syncthreads();   // weight fragments / sbias visible
 
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  constexpr int NKT = KT + UB;
+  constexpr bool RFU = RF & 1, RFW = RF & 2, RFX = DX && (RF & 4);
+  bf16x4 rfw[RFW ? MT * NKT : 1], rfu[RFU ? UB * MT : 1], rfx[RFX ? KT * MT : 1];
+  if constexpr (RFW) {
+#pragma unroll
+    for (int i = 0; i < MT * NKT; ++i) rfw[i] = wfwd[i * 64 + lane];
+  }
+  if constexpr (RFU) {
+#pragma unroll
+    for (int i = 0; i < UB * MT; ++i) rfu[i] = ufl[i * 64 + lane];
+  }
+  if constexpr (RFX) {
+#pragma unroll
+    for (int i = 0; i < KT * MT; ++i) rfx[i] = wfl[i * 64 + lane];
+  }
   f32x4 accW[MT][KT], accU[MT][UB];
   f32x4 accb[MT];   // db in exact fp32: per lane (sequence c) over time, folded across lanes at the end
 #pragma unroll
@@ -237,6 +257,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 
   auto step = [&](int t, const Step& cur) {
     const int ol = opaque_lane(lane);   // re-materialised per step: fragment reads stay in the loop
+    auto fw = [&](int i) { if constexpr (RFW) return rfw[i]; else return wfwd[i * 64 + ol]; };
+    auto fu = [&](int i) { if constexpr (RFU) return rfu[i]; else return ufl[i * 64 + ol]; };
+    auto fx = [&](int i) { if constexpr (RFX) return rfx[i]; else return wfl[i * 64 + ol]; };
     // gate recompute: z^T = b + W^T . x_t^T + U^T . h_{t-1}^T, the forward's exact
     // operands and accumulation order (bit-identical pre-activations)
     bf16x4 xb[KT], hb[UB];
@@ -252,10 +275,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       constexpr int NK = KT + UB;   // K-tiles in pairs on 16x16x32, exactly as the forward
 #pragma unroll
       for (int k = 0; k + 1 < NK; k += 2)
-        z[mt] = mfma32(wfwd[(mt * NK + k) * 64 + ol], wfwd[(mt * NK + k + 1) * 64 + ol], k < KT ? xb[k] : hb[k - KT],
+        z[mt] = mfma32(fw(mt * NK + k), fw(mt * NK + k + 1), k < KT ? xb[k] : hb[k - KT],
                        k + 1 < KT ? xb[k + 1] : hb[k + 1 - KT], z[mt]);
       if constexpr (NK & 1)   // as the forward: never a 16x16x16 on a 16x16x32 result
-        z[mt] = mfma32(wfwd[(mt * NK + NK - 1) * 64 + ol], bf16x4{0, 0, 0, 0}, hb[UB - 1], bf16x4{0, 0, 0, 0}, z[mt]);
+        z[mt] = mfma32(fw(mt * NK + NK - 1), bf16x4{0, 0, 0, 0}, hb[UB - 1], bf16x4{0, 0, 0, 0}, z[mt]);
     }
     wgrad();                                    // step t+1's weight gradients (zeros on the first step)
     f32x4 cp[UB], dhi[UB];                      // c_{t-1}, incoming dh_t
@@ -302,17 +325,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       f32x4 acc = zero4;
 #pragma unroll
       for (int kt = 0; kt < MT; kt += 2)
-        acc = mfma32(ufl[(b * MT + kt) * 64 + ol], ufl[(b * MT + kt + 1) * 64 + ol], dzb[kt], dzb[kt + 1], acc);
+        acc = mfma32(fu(b * MT + kt), fu(b * MT + kt + 1), dzb[kt], dzb[kt + 1], acc);
       dhr[b] = acc;
     }
     // input gradient dX_t^T = W . dz_t^T
-    if (want_dx) {
+    if (DX && want_dx) {
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) {
         f32x4 acc = zero4;
 #pragma unroll
         for (int mt = 0; mt < MT; mt += 2)
-          acc = mfma32(wfl[(kt * MT + mt) * 64 + ol], wfl[(kt * MT + mt + 1) * 64 + ol], dzb[mt], dzb[mt + 1], acc);
+          acc = mfma32(fx(kt * MT + mt), fx(kt * MT + mt + 1), dzb[mt], dzb[mt + 1], acc);
         // dx is [B16, T, 16*KT]: every lane stores its whole piece, unmasked
         const int64_t o = (seq * T + t) * (int64_t)(16 * KT) + 16 * kt + 4 * g;
         if constexpr (std::is_same_v<XT, float>) *reinterpret_cast<f32x4*>(static_cast<float*>(a.dx) + o) = acc;
@@ -388,10 +411,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 template <int U, int KT, int XV, typename XT>
 hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
   const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
-  if (a.act == ACT_RELU)
-    hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU>), dim3(grid), dim3(WAVES * 64), 0, st, a);
-  else
-    hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  // Without dX (the first layer of a stack, U = 32 at one wave per SIMD) every weight
+  // fragment fits in registers next to the AGPR accumulators: the per-step LDS fragment
+  // reads were exposed latency there (SQ_WAIT_ANY 41 % of wave cycles) and the kernel
+  // runs 17 % faster (bench_lstm 62.3 -> 68.1 M windows/s, profiles/r02).  With dX, at
+  // two waves per SIMD, register fragments measured the same as LDS reads (67.8 vs 67.9).
+  auto go = [&](auto dx, auto rf) {
+    constexpr bool DX = decltype(dx)::value;
+    constexpr int RF = decltype(rf)::value;
+    if (a.act == ACT_RELU)
+      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+    else
+      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  };
+  if (a.dx) go(std::true_type{}, std::integral_constant<int, 0>{});
+  else go(std::false_type{}, std::integral_constant<int, 3>{});
   return hipGetLastError();
 }
 
