@@ -11,28 +11,57 @@
 // rows (a [n, T, F] TimeDistributed output against [n, F] next-event targets,
 // LSTM-TensorFlow-IO-Kafka/cardata-v2.py:183-206).
 //
-// One row per lane (F <= 64 values in registers), 256-thread blocks, per-block
-// partial sums reduced with shuffles + LDS and ONE atomic per block into acc
-// [loss_sum, correct]; torch-side this replaces ~10 elementwise / reduction
-// kernels per training step.
+// One row per lane, rows staged through LDS: a block's RPB rows of y_pred (and of y when
+// bcast = 1) are contiguous, so they come in and the gradient goes out as coalesced
+// 16-byte accesses (a lane walking its own 72-byte row issued F scalar loads and stores
+// per lane, 4-5x slower at F = 18).  Per-block partial sums are reduced with shuffles +
+// LDS and ONE atomic per block into acc [loss_sum, correct]; torch-side this replaces
+// ~10 elementwise / reduction kernels per training step.
 #include "sml_common.h"
 #include "sml_ops.h"
 
 namespace sml {
 namespace {
 
-constexpr int kThreads = 256;
+template <int F>
+constexpr int rows_per_block() { return F <= 16 ? 256 : (F <= 32 ? 128 : 64); }
 
 template <int F>
-__global__ __launch_bounds__(kThreads) void mse_acc_kernel(const float* __restrict__ yp, const float* __restrict__ y,
-                                                            int64_t rows, int bcast, float gscale,
-                                                            float* __restrict__ grad, float* __restrict__ acc) {
-  __shared__ float red[2][kThreads / 64];
-  const int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+__global__ __launch_bounds__(rows_per_block<F>()) void mse_acc_kernel(const float* __restrict__ yp,
+                                                                      const float* __restrict__ y, int64_t rows,
+                                                                      int bcast, float gscale,
+                                                                      float* __restrict__ grad,
+                                                                      float* __restrict__ acc) {
+  constexpr int RPB = rows_per_block<F>(), NW = RPB / 64;
+  __shared__ __attribute__((aligned(16))) float sp[RPB * F];
+  __shared__ __attribute__((aligned(16))) float st[RPB * F];
+  __shared__ float red[2][NW];
+  const int64_t r0 = (int64_t)blockIdx.x * RPB;
+  const int nr = (int)(rows - r0 < RPB ? rows - r0 : RPB);
+  const int n = nr * F;
+  const float* pb = yp + r0 * F;
+  const float* tb = y + r0 * F;
+  const bool vec = ((n & 3) == 0) && ((reinterpret_cast<uintptr_t>(pb) & 15) == 0) &&
+                   (bcast != 1 || (reinterpret_cast<uintptr_t>(tb) & 15) == 0) &&
+                   (!grad || (reinterpret_cast<uintptr_t>(grad + r0 * F) & 15) == 0);
+  if (vec) {
+    for (int i = threadIdx.x; i < n / 4; i += RPB) {
+      reinterpret_cast<f32x4*>(sp)[i] = reinterpret_cast<const f32x4*>(pb)[i];
+      if (bcast == 1) reinterpret_cast<f32x4*>(st)[i] = reinterpret_cast<const f32x4*>(tb)[i];
+    }
+  } else {
+    for (int i = threadIdx.x; i < n; i += RPB) {
+      sp[i] = pb[i];
+      if (bcast == 1) st[i] = tb[i];
+    }
+  }
+  __syncthreads();
   float se = 0.f, correct = 0.f;
-  if (r < rows) {
-    const float* p = yp + r * F;
-    const float* t = y + (r / bcast) * F;
+  const int rl = threadIdx.x;
+  if (rl < nr) {
+    const int64_t r = r0 + rl;
+    float* p = sp + rl * F;
+    const float* t = bcast == 1 ? st + rl * F : y + (r / bcast) * F;
     float mp = -INFINITY, mt = -INFINITY;
     int ip = 0, it = 0;
 #pragma unroll
@@ -40,11 +69,20 @@ __global__ __launch_bounds__(kThreads) void mse_acc_kernel(const float* __restri
       const float a = p[j], b = t[j];
       const float d = a - b;
       se = fmaf(d, d, se);
-      if (grad) grad[r * F + j] = d * gscale;
+      p[j] = d * gscale;                      // the gradient, written back in place
       if (a > mp) { mp = a; ip = j; }
       if (b > mt) { mt = b; it = j; }
     }
     correct = ip == it ? 1.f : 0.f;
+  }
+  if (grad) {
+    __syncthreads();
+    float* gb = grad + r0 * F;
+    if (vec) {
+      for (int i = threadIdx.x; i < n / 4; i += RPB) reinterpret_cast<f32x4*>(gb)[i] = reinterpret_cast<const f32x4*>(sp)[i];
+    } else {
+      for (int i = threadIdx.x; i < n; i += RPB) gb[i] = sp[i];
+    }
   }
   if (acc) {
     se = wave_sum(se);
@@ -58,7 +96,7 @@ __global__ __launch_bounds__(kThreads) void mse_acc_kernel(const float* __restri
     if (threadIdx.x == 0) {
       float a = 0.f, b = 0.f;
 #pragma unroll
-      for (int i = 0; i < kThreads / 64; ++i) {
+      for (int i = 0; i < NW; ++i) {
         a += red[0][i];
         b += red[1][i];
       }
@@ -74,11 +112,13 @@ hipError_t mse_acc_launch(const float* yp, const float* y, int64_t rows, int F, 
                           float* acc, hipStream_t stream) {
   if (rows <= 0) return hipSuccess;
   if (bcast < 1) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)((rows + kThreads - 1) / kThreads));
-#define SML_F(n)                                                                                               \
-  case n:                                                                                                     \
-    hipLaunchKernelGGL(mse_acc_kernel<n>, grid, dim3(kThreads), 0, stream, yp, y, rows, bcast, gscale, grad, acc); \
-    break;
+#define SML_F(n)                                                                                              \
+  case n: {                                                                                                  \
+    constexpr int R = rows_per_block<n>();                                                                   \
+    hipLaunchKernelGGL(mse_acc_kernel<n>, dim3((unsigned)((rows + R - 1) / R)), dim3(R), 0, stream, yp, y, rows, \
+                       bcast, gscale, grad, acc);                                                            \
+    break;                                                                                                   \
+  }
   switch (F) {
     SML_F(1) SML_F(2) SML_F(4) SML_F(8) SML_F(10) SML_F(16) SML_F(18) SML_F(30) SML_F(32) SML_F(64)
     default: return hipErrorInvalidValue;

@@ -8,7 +8,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("shape,tshape", [((1000, 18), (1000, 18)), ((77, 5, 18), (77, 18)), ((4097, 10), (4097, 10)),
-                                          ((33, 1, 30), (33, 30))])
+                                          ((33, 1, 30), (33, 30)), ((65537, 18), (65537, 18)),
+                                          ((300, 64), (300, 64)), ((129, 4, 16), (129, 16))])
 def test_mse_accuracy_matches_torch(cuda_device, shape, tshape):
     g = torch.Generator().manual_seed(sum(shape))
     yp = torch.randn(*shape, generator=g)
