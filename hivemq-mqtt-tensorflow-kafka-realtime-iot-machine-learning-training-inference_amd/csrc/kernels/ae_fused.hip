@@ -112,7 +112,14 @@ __device__ __forceinline__ float ldsel(const float* P, bool cond, int idx) {
 // tanh(z) = 1 - 2 / (2^(2 log2(e) z) + 1) (one v_mul per activation saved).
 constexpr float kTanhExp2 = 2.8853900817779268f;
 
-template <bool FOLD, bool PRE = false>
+// INJ (with FOLD + PRE, layer 2 relu / linear): the constant-1 bias slot 15 of each hidden
+// layer is produced by the forward MFMA itself instead of a v_add after the activation:
+// the fragment entry [in = bias slot][out = 15] is set to a value whose activation is
+// exactly 1 -- 256 for the prescaled tanh layers (exp2(256) = inf, so 1 - 2 / (inf + 1)
+// = 1), 1.0 for layer 2.  Fragments only: the parameter image keeps 0 there, and its
+// gradient is 0 (dz at an output of exactly 1 is (1 - 1*1) * ... = 0 for tanh; layer 2's
+// backward never reads its bias row).  Needs n1, n2, n3 <= 15 (as FOLD does).
+template <bool FOLD, bool PRE = false, bool INJ = false>
 __device__ __forceinline__ void load_frags(const AEArgs& a, int c, int g, Frags& F, bool bwd) {
   const float* P = a.params;
   const float k1 = PRE ? kTanhExp2 : 1.0f;
@@ -157,6 +164,13 @@ __device__ __forceinline__ void load_frags(const AEArgs& a, int c, int g, Frags&
     for (int t = 0; t < 2; ++t) {
       const int ft = 16 * t + f;
       F.b4[t][i] = ldsel(P, !FOLD && ft < a.D, OFF4 + 15 * 32 + ft);
+    }
+  }
+  if constexpr (INJ) {
+    if (c == 15 && g == 3) {   // A[m = out 15][k = in 4g + 3 = bias slot]
+      F.w1t[1][3] = bfbits(256.0f);
+      F.w2t[3] = bfbits(1.0f);
+      F.w3t[3] = bfbits(256.0f);
     }
   }
 }
@@ -415,6 +429,12 @@ constexpr bool prescaled_tanh() {
   return PACK >= 0 && ((PACK & 3) == ACT_TANH) && (((PACK >> 4) & 3) == ACT_TANH) && zero_preserving<PACK>();
 }
 
+// bias slots made by the forward MFMAs (load_frags<., ., true>)
+template <int PACK>
+constexpr bool inject_bias_slots() {
+  return prescaled_tanh<PACK>() && (((PACK >> 2) & 3) == ACT_RELU || ((PACK >> 2) & 3) == ACT_LINEAR);
+}
+
 template <int PACK, bool FAST, bool TAIL, bool LOW_REAL = false, int DC = 0, bool XA = false>
 __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char* scr, int c, int g, int lane,
                                            bool valid, const f32x4 xf[2], float pad1,
@@ -422,6 +442,7 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
                                            float& ab, float& corr, float& rows, int ix_pre = -1) {
   const int a1 = act_of<PACK>(a, 0), a2 = act_of<PACK>(a, 1), a3 = act_of<PACK>(a, 2), a4 = act_of<PACK>(a, 3);
   constexpr bool PRE = FAST && prescaled_tanh<PACK>();
+  constexpr bool INJ = FAST && inject_bias_slots<PACK>();
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const bool pad_lane = (g == 3);
   const bool vm = !TAIL || valid;
@@ -439,17 +460,17 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
     const f32x4 z1 = mfma32(F.w1t[0], F.w1t[1], xb0, xb1, zero4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) h1[i] = PRE ? tanh_exp2(z1[i]) : act_fwd(a1, z1[i]);
-    h1[3] += pad1;
+    if constexpr (!INJ) h1[3] += pad1;
     h1b = pack4(h1);
     const f32x4 z2 = mfma16(F.w2t, h1b, zero4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) h2[i] = act_fwd(a2, z2[i]);
-    h2[3] += pad1;
+    if constexpr (!INJ) h2[3] += pad1;
     h2b = pack4(h2);
     const f32x4 z3 = mfma16(F.w3t, h2b, zero4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) h3[i] = PRE ? tanh_exp2(z3[i]) : act_fwd(a3, z3[i]);
-    h3[3] += pad1;
+    if constexpr (!INJ) h3[3] += pad1;
     h3b = pack4(h3);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -514,8 +535,16 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
     const bool use = real && vm;
     ab += use ? fabsf(hv) : 0.f;
     // Keras L1 activity regulariser gradient: l1 * sign(h1) (sign(0) = 0)
-    const float sgn = (use && hv != 0.f) ? __builtin_copysignf(1.0f, hv) : 0.f;
-    float d = act_grad(a1, hv, fmaf(a.l1, sgn, dh1[i]));
+    float d;
+    if constexpr (PRE && !TAIL) {
+      // one v_med3: clamp(h, -l1, l1) = l1 * sign(h) for |h| >= l1 (and 0 at h = 0); it
+      // differs only for 0 < |h1| < l1 = 1e-7, by less than l1.  The bias slot (h = 1)
+      // needs no mask: the tanh derivative 1 - h*h is exactly 0 there.
+      d = act_grad(a1, hv, dh1[i] + __builtin_amdgcn_fmed3f(hv, -a.l1, a.l1));
+    } else {
+      const float sgn = (use && hv != 0.f) ? __builtin_copysignf(1.0f, hv) : 0.f;
+      d = act_grad(a1, hv, fmaf(a.l1, sgn, dh1[i]));
+    }
     if constexpr (!FAST) d = real ? d : 0.f;
     dz1[i] = d;
   }
@@ -583,7 +612,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   }
 
   Frags F;
-  load_frags<FAST, FAST && prescaled_tanh<PACK>()>(a, c, g, F, true);
+  load_frags<FAST, FAST && prescaled_tanh<PACK>(), FAST && inject_bias_slots<PACK>()>(a, c, g, F, true);
   const float pad1 = (g == 3) ? 1.0f : 0.0f;
   __syncthreads();  // normaliser visible (before any LDS-DMA is in flight)
 
