@@ -55,6 +55,8 @@ def parse():
                    help="write this rank's final parameter image to <path>.rank<R>.npy (replica checks)")
     p.add_argument("--graph", action="store_true",
                    help="replay one captured hipGraph step (replay floor ~10 us; eager is faster at these sizes)")
+    p.add_argument("--collective-iters", type=int, default=300,
+                   help="N > 1: back-to-back 6 KB all-reduces timed, RCCL vs the xGMI P2P one-launch path (0 = skip)")
     p.add_argument("--dp-steps", type=int, default=20000,
                    help="Keras batch-32 steps per launch of the multi-GPU in-kernel P2P DP measurement (0 = skip)")
     p.add_argument("--fit-rows", type=int, default=2_000_000,
@@ -127,7 +129,39 @@ def measure_batch32(spec, data, device, steps, scale, shift, seed, launches=5):
             "final_loss": ae.read_metrics()["loss"]}
 
 
-def measure_batch_dp(spec, data, device, steps, scale, shift, seed, world, batch=32, launches=3):
+def measure_collectives(device, world, group=None, iters=300, floats=1536):
+    """Small-bucket all-reduce latency at the AE's bucket size (1536 floats = 6 KB, the
+    padded gradient image): the process group's ``all_reduce`` (RCCL) vs the one-launch xGMI P2P all-reduce
+    (``P2PGroup.allreduce_``).  Back-to-back calls on one stream,
+    mean us per call, max over ranks.  Collective: every rank calls it."""
+    import torch
+    import torch.distributed as dist
+
+    from streamml.parallel import dp as dpm
+
+    out = {"bucket_bytes": floats * 4, "iters": iters}
+    t = torch.zeros(floats, device=device)
+
+    def timed(fn):
+        for _ in range(20):
+            fn()
+        torch.cuda.synchronize()
+        dpm.barrier(device)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        return dpm.allreduce_max(time.perf_counter() - t0, device) / iters * 1e6
+
+    out["backend"] = dist.get_backend()          # "nccl" is RCCL on ROCm
+    out["backend_allreduce_us"] = timed(lambda: dist.all_reduce(t))
+    if group is not None:
+        out["p2p_allreduce_us"] = timed(lambda: group.allreduce_(t))
+        group.check()
+    return out
+
+
+def measure_batch_dp(spec, data, device, steps, scale, shift, seed, world, batch=32, launches=3, group=None):
     """Keras batch-32 training with data parallelism at optimizer granularity: every step's
     gradient tile is pushed to every peer over xGMI and summed in rank order INSIDE the
     persistent kernel (parallel/p2p.py) -- no launch, no RCCL call per step.  Collective:
@@ -139,7 +173,9 @@ def measure_batch_dp(spec, data, device, steps, scale, shift, seed, world, batch
     from streamml.parallel import dp as dpm
     from streamml.parallel.p2p import P2PGroup
 
-    group, err = P2PGroup.try_create(device)
+    err = None
+    if group is None:
+        group, err = P2PGroup.try_create(device)
     if group is None:
         return {"error": f"P2P exchange unavailable: {err!r}"}
     ae = FusedAE(spec, init_dense_weights(spec.layer_sizes, seed=seed), device, scale=scale, shift=shift)
@@ -312,8 +348,17 @@ def main():
             b32["fleet"] = guarded(measure_batch32_fleet, spec, data, device, max(args.batch32_steps // 10, 1),
                                    scale, shift, args.fleet_models)
     b32_dp = {"skipped": "single GPU (no peers)"}
-    if world > 1 and args.dp_steps > 0:
-        b32_dp = guarded(measure_batch_dp, spec, data, device, args.dp_steps, scale, shift, args.seed, world)
+    coll = {"skipped": "single GPU (no peers)"}
+    if world > 1 and (args.dp_steps > 0 or args.collective_iters > 0):
+        from streamml.parallel.p2p import P2PGroup
+        p2p, p2p_err = P2PGroup.try_create(device)   # collective: every rank gets a group, or none
+        if args.collective_iters > 0:
+            coll = guarded(measure_collectives, device, world, p2p, args.collective_iters)
+            if p2p is None:
+                coll["p2p_error"] = repr(p2p_err)[:200]
+        if args.dp_steps > 0:
+            b32_dp = (guarded(measure_batch_dp, spec, data, device, args.dp_steps, scale, shift, args.seed, world,
+                              group=p2p) if p2p is not None else {"error": f"P2P exchange unavailable: {p2p_err!r}"})
     fit100 = stream = None
     if rank == 0 and args.fit_rows > 0:
         fit100 = guarded(measure_fit, device, args.fit_rows)
@@ -354,6 +399,7 @@ def main():
             "final_accuracy": metrics["accuracy"],
             "keras_batch32": b32,
             "keras_batch32_dp": b32_dp,
+            "small_allreduce": coll,
             "fit_batch100_rows_per_s": None if not fit100 or "error" in fit100 else fit100["rows_per_s"],
             "fit_batch100": fit100,
             "stream_e2e_rows_per_s": None if not stream or "error" in stream else stream["rows_per_s"],

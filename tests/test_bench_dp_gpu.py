@@ -41,6 +41,9 @@ def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
     assert out["n_gpus"] == 2 and out["steps"] == 4 and out["warmup"] == 2
     assert out["config"]["global_batch"] == 2 * 65536 and out["config"]["parallelism"] == "dp2"
     assert out["value"] > 0 and np.isfinite(out["final_epoch_loss"])
+    coll = out["small_allreduce"]
+    assert coll["bucket_bytes"] == 6144 and coll["backend_allreduce_us"] > 0 and coll["p2p_allreduce_us"] > 0, coll
+    assert out["keras_batch32_dp"]["replicas_identical"] is True, out["keras_batch32_dp"]
     p0 = np.load(dump + ".rank0.npy")
     p1 = np.load(dump + ".rank1.npy")
     np.testing.assert_array_equal(p0, p1)
