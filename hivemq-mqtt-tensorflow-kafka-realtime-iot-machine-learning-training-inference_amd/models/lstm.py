@@ -148,7 +148,8 @@ class LSTMPredictor:
     def train_step(self, x: torch.Tensor, y: torch.Tensor, global_batch: Optional[int] = None, allreduce=None):
         n = x.shape[0]
         plan = self._fused_plan()
-        if plan is not None and x.is_cuda and x.dim() == 3 and y.dim() == 2 and n > 0:
+        if (plan is not None and isinstance(x, torch.Tensor) and isinstance(y, torch.Tensor) and x.is_cuda
+                and x.dim() == 3 and y.dim() == 2 and n > 0):
             return self._fused_step(plan, x, y, global_batch, allreduce)
         self.fp.zero_grad()
         y_pred = self.forward(x)
