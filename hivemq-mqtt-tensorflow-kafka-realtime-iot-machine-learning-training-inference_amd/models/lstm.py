@@ -252,7 +252,7 @@ class LSTMPredictor:
                                    i == len(plan["lstms"]) - 1, grad, plan["maps"][i])
             dh = out[0]
         self.opt.step(allreduce=allreduce)
-        return acc[0] / y_pred.numel(), acc[1]
+        return acc[0] / y_pred.numel(), acc[1].clone()   # acc is re-zeroed by the next step
 
     # ------------------------------------------------------------------ training
     def fit(self, x, y=None, epochs: int = 1, batch_size: int = 1, verbose: int = 1, take: Optional[int] = None,
