@@ -206,6 +206,8 @@ class LSTMPredictor:
         mp[:KP * NP] = np.where((k < K) & (nn < N), oK + k * N + nn, -1).ravel()
         mp[KP * NP:KP * NP + NP] = np.where(np.arange(NP) < N, ob + np.arange(NP), -1)
         head_map = torch.as_tensor(mp.astype(np.int32), device=self.device)
+        for m_ in maps + [head_map]:   # the kernels scatter through these unchecked
+            assert int(m_.max()) < self.fp.n_pad and int(m_.min()) >= -1
         self._plan = dict(lstms=lstms, head=head, maps=maps, head_map=head_map,
                           acc=torch.zeros(2, device=self.device))
         return self._plan
