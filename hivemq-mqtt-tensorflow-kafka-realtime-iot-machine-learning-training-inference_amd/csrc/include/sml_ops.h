@@ -7,14 +7,14 @@ namespace sml {
 
 // ---- dense autoencoder (ae_fused.hip) ----
 int ae_nslot();
-int ae_train_blocks_per_cu();  // resident 256-thread workgroups per CU of the selected variant
+int ae_train_blocks_per_cu();  // most resident 256-thread workgroups per CU of any train variant (4)
 int ae_nparam();
 int ae_waves_per_block();
 int ae_train_grid(int64_t n, int max_blocks);
 hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
                            const float* params, float* partials, int64_t* iter, const int64_t* cursor,
                            const int* dims, const int* acts, float l1, int want_acc, int grid, const uint8_t* xpack,
-                           hipStream_t stream);
+                           hipStream_t stream, int* grid_used);  // grid_used <= grid: slabs written
 hipError_t ae_forward_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
                              const float* params, float* recon, float* score, uint8_t* flag, float threshold,
                              const int* dims, const int* acts, int max_blocks, hipStream_t stream);

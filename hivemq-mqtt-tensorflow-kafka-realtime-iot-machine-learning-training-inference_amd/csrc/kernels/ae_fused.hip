@@ -570,6 +570,411 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
   acc4[1] = mfma16(h3r, dz4r1, acc4[1]);
 }
 
+// U (1 or 2) whole tiles of one wave in ONE interleaved instruction stream (ILP variant of
+// train_tile for the headline configuration: zero-preserving, prescaled tanh, bias slots
+// from the MFMAs, ingest-time argmax of x, compile-time D).  Every stage is written as a
+// loop over the U tiles, so the two tiles' dependent MFMA -> activation -> MFMA chains
+// are independent instruction sequences the scheduler can pair: while one tile waits on
+// an MFMA result the other's VALU issues (profiles/r02: 43 % of wave cycles were issue
+// stalls on the one-tile chain at 4 waves / SIMD).  The weight-gradient contraction of
+// the pair is one v_mfma_f32_16x16x32_bf16 per weight block (K = 2 x 16 rows) instead of
+// two 16x16x16s.  U = 1 pads the second K half with zeros, so every accumulator is only
+// ever fed by 16x16x32 MFMAs (a 16x16x16 taking a 16x16x32 result as SrcC miscomputed on
+// this toolchain, see the LSTM notes in profiles/r02).  The tiles share the wave's
+// transpose scratch: LDS ops of one wave execute in order, so tile 1's write of a slot
+// cannot overtake tile 0's transposed read of it.
+template <int PACK, int DC, int U>
+__device__ __forceinline__ void train_tiles_ilp(const AEArgs& a, const Frags& F, char* scr, int c, int g,
+                                                const f32x4 (&xf)[U][2], const int (&ix)[U], float pad1,
+                                                f32x4 acc1[2], f32x4& acc2, f32x4& acc3, f32x4 acc4[2], float& sq,
+                                                float& ab, float& corr, float& rows) {
+  static_assert(zero_preserving<PACK>() && inject_bias_slots<PACK>() && DC > 16, "headline configuration only");
+  static_assert(U == 1 || U == 2, "one or two tiles");
+  const int a2 = act_of<PACK>(a, 1), a3 = act_of<PACK>(a, 2), a4 = act_of<PACK>(a, 3);
+  const int a1 = act_of<PACK>(a, 0);
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const bf16x4 zb = {0, 0, 0, 0};
+  const bool pad_lane = (g == 3);
+
+  bf16x4 xb0[U], xb1[U], h1b[U], h2b[U], h3b[U];
+  f32x4 h1[U], h2[U], h3[U], y[U][2];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    f32x4 x1 = xf[u][1];
+    x1[3] += pad1;
+    xb0[u] = pack4(xf[u][0]);
+    xb1[u] = pack4(x1);
+  }
+  f32x4 z[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) z[u] = mfma32(F.w1t[0], F.w1t[1], xb0[u], xb1[u], zero4);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h1[u][i] = tanh_exp2(z[u][i]);
+    h1b[u] = pack4(h1[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) z[u] = mfma16(F.w2t, h1b[u], zero4);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h2[u][i] = act_fwd(a2, z[u][i]);
+    h2b[u] = pack4(h2[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) z[u] = mfma16(F.w3t, h2b[u], zero4);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h3[u][i] = tanh_exp2(z[u][i]);
+    h3b[u] = pack4(h3[u]);
+  }
+  f32x4 z4[U][2];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) z4[u][t] = mfma16(F.w4t[t], h3b[u], zero4);
+  f32x4 dz4[U][2];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (t == 1 && !live_hi<DC>(i)) {
+          y[u][t][i] = 0.f;
+          dz4[u][t][i] = 0.f;
+          continue;
+        }
+        y[u][t][i] = act_fwd(a4, z4[u][t][i]);
+        const float e = y[u][t][i] - xf[u][t][i];
+        sq = fmaf(e, e, sq);
+        dz4[u][t][i] = act_grad(a4, y[u][t][i], e);   // x 2/D folded into F.w4 / the acc4 slab
+      }
+  if (a.want_acc) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int iy;
+      if constexpr (((PACK >> 6) & 3) == ACT_RELU)
+        iy = row_argmax_nonneg<DC>(y[u], a.D, g);
+      else
+        iy = row_argmax_fast<true, DC>(y[u], a.D, g);
+      corr += (g == 0 && iy == ix[u]) ? 1.f : 0.f;
+    }
+  }
+  rows += (g == 0) ? (float)U : 0.f;
+
+  bf16x4 dz4b0[U], dz4b1[U], dz3b[U], dz2b[U], dz1b[U];
+  f32x4 d[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    dz4b0[u] = pack4(dz4[u][0]);
+    dz4b1[u] = pack4(dz4[u][1]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) d[u] = mfma32(F.w4[0], F.w4[1], dz4b0[u], dz4b1[u], zero4);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    f32x4 dz3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dz3[i] = act_grad(a3, h3[u][i], d[u][i]);
+    dz3b[u] = pack4(dz3);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) d[u] = mfma16(F.w3, dz3b[u], zero4);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    f32x4 dz2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dz2[i] = act_grad(a2, h2[u][i], d[u][i]);
+    dz2b[u] = pack4(dz2);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) d[u] = mfma16(F.w2, dz2b[u], zero4);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    f32x4 dz1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float hv = h1[u][i];
+      ab += (i == 3 && pad_lane) ? 0.f : fabsf(hv);
+      // Keras L1 activity regulariser gradient as one v_med3 (see train_tile)
+      dz1[i] = act_grad(a1, hv, d[u][i] + __builtin_amdgcn_fmed3f(hv, -a.l1, a.l1));
+    }
+    dz1b[u] = pack4(dz1);
+  }
+
+  // weight gradients: rows-on-K operands through the LDS transpose, both tiles per MFMA
+  bf16x4 xr0[2], xr1[2], dz1r[2], h1r[2], dz2r[2], h2r[2], dz3r[2], h3r[2], dz4r0[2], dz4r1[2];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    xr0[u] = lds_transpose(xb0[u], scr + 0 * 512, c, g);
+    xr1[u] = lds_transpose(xb1[u], scr + 1 * 512, c, g);
+    dz1r[u] = lds_transpose(dz1b[u], scr + 2 * 512, c, g);
+    h1r[u] = lds_transpose(h1b[u], scr + 3 * 512, c, g);
+    dz2r[u] = lds_transpose(dz2b[u], scr + 4 * 512, c, g);
+    h2r[u] = lds_transpose(h2b[u], scr + 5 * 512, c, g);
+    dz3r[u] = lds_transpose(dz3b[u], scr + 6 * 512, c, g);
+    h3r[u] = lds_transpose(h3b[u], scr + 7 * 512, c, g);
+    dz4r0[u] = lds_transpose(dz4b0[u], scr + 8 * 512, c, g);
+    dz4r1[u] = lds_transpose(dz4b1[u], scr + 9 * 512, c, g);
+  }
+  if constexpr (U == 1) {
+    xr0[1] = xr1[1] = dz1r[1] = h1r[1] = dz2r[1] = h2r[1] = dz3r[1] = h3r[1] = dz4r0[1] = dz4r1[1] = zb;
+  }
+  acc1[0] = mfma32(xr0[0], xr0[1], dz1r[0], dz1r[1], acc1[0]);
+  acc1[1] = mfma32(xr1[0], xr1[1], dz1r[0], dz1r[1], acc1[1]);
+  acc2 = mfma32(h1r[0], h1r[1], dz2r[0], dz2r[1], acc2);
+  acc3 = mfma32(h2r[0], h2r[1], dz3r[0], dz3r[1], acc3);
+  acc4[0] = mfma32(h3r[0], h3r[1], dz4r0[0], dz4r0[1], acc4[0]);
+  acc4[1] = mfma32(h3r[0], h3r[1], dz4r1[0], dz4r1[1], acc4[1]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Packed tile pairs (ILP 3).  Layers 2 and 3 of the reference model are 7 wide (+ the bias
+// slot = 8), so in the 16-feature fragment of one tile half the lanes' elementwise work is
+// padding.  Two tiles share ONE fragment there: packed feature p < 8 is feature p of tile 0,
+// p >= 8 feature p - 8 of tile 1 (packed 7 / 15 = the tiles' constant-1 bias slots, image
+// row 15).  The weights become block-diagonal (or one block beside zeros) so every layer
+// is still one MFMA; the relu / tanh / derivative work of layers 2-3 and four of the ten
+// LDS transposes are done once per PAIR.  Layer 1 and the output layer stay per tile.
+//   forward  L2: z2p = [W2^T 0; 0 W2^T] . [h1_0; h1_1]          (one 16x16x32)
+//            L3: z3p = blockdiag(W3^T, W3^T) . h2p              (one 16x16x16)
+//            L4: z4_u = [W4^T 0] / [0 W4^T] . h3p              (per tile, per 16-output half)
+//   backward dh3p = [W4 0; 0 W4] . [dz4_0; dz4_1]              (two chained 16x16x32)
+//            dh2p = blockdiag(W3, W3) . dz3p;  dh1_u = [W2 0] / [0 W2] . dz2p
+//   weight gradients: dW2 / dW4 contract one tile against a lane-masked copy of the packed
+//   operand (the other tile's half zeroed); dW3 is the diagonal blocks of ONE contraction.
+//   The accumulators hold both tiles' halves side by side and are folded into the parameter
+//   image once per launch (packed_fold_src).  Needs n2, n3 <= 7.
+struct FragsP {
+  bf16x4 w1t[2];      // L1 forward (as Frags: prescaled, bias slot 15 injected)
+  bf16x4 w2t[2];      // L2 forward, K halves = tile 0 / tile 1 inputs
+  bf16x4 w3t;         // L3 forward, block-diagonal (prescaled, packed bias slots injected)
+  bf16x4 w4t[2][2];   // L4 forward [tile][output half]
+  bf16x4 w4b[2][2];   // L4 backward [tile][K half = output half] (x 2/D)
+  bf16x4 w3b;         // L3 backward, block-diagonal
+  bf16x4 w2b[2];      // L2 backward [tile]
+};
+
+__device__ __forceinline__ int img_row_of_packed(int i) { return i == 7 ? 15 : i; }   // i = packed % 8
+
+__device__ __forceinline__ void load_frags_packed(const AEArgs& a, int c, int g, FragsP& F) {
+  const float* P = a.params;
+  const float k1 = kTanhExp2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = 4 * g + j;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int in = 16 * s + k;
+      const bool row_ok = in < a.D || in == 31;
+      F.w1t[s][j] = bfbits(k1 * ldsel(P, row_ok && c < a.n1, OFF1 + in * 16 + c));
+    }
+    // L2 forward: A[m = packed out c][k = in (of tile h)]
+    const int o2 = c & 7;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bool ok = (c >> 3) == h && o2 < a.n2 && (k < a.n1 || k == 15);
+      float v = ldsel(P, ok, OFF2 + k * 16 + o2);
+      if ((c >> 3) == h && o2 == 7 && k == 15) v = 1.0f;   // packed bias slot: relu(1) = 1
+      F.w2t[h][j] = bfbits(v);
+    }
+    // L3 forward: A[m = packed out c][k = packed in k], same tile only
+    {
+      const int o = c & 7, i = k & 7;
+      const bool same = (c >> 3) == (k >> 3);
+      float v = k1 * ldsel(P, same && o < a.n3 && (i < a.n2 || i == 7), OFF3 + img_row_of_packed(i) * 16 + o);
+      if (same && o == 7 && i == 7) v = 256.0f;   // tanh_exp2(256) = 1 exactly
+      F.w3t[j] = bfbits(v);
+    }
+    // L4 forward: A[m = out 16t + c][k = packed in of tile u]
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int out = 16 * t + c, i = k & 7;
+        const bool ok = (k >> 3) == u && out < a.D && (i < a.n3 || i == 7);
+        F.w4t[u][t][j] = bfbits(ldsel(P, ok, OFF4 + img_row_of_packed(i) * 32 + out));
+      }
+    // L4 backward: A[m = packed in c (tile u)][k = out 16s + k]; bias rows carry no gradient
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int out = 16 * s + k, i = c & 7;
+        const bool ok = (c >> 3) == u && i < a.n3 && out < a.D;
+        F.w4b[u][s][j] = bfbits((2.0f / (float)a.D) * ldsel(P, ok, OFF4 + i * 32 + out));
+      }
+    // L3 backward: A[m = packed in c][k = packed out k], same tile
+    {
+      const int i = c & 7, o = k & 7;
+      const bool ok = (c >> 3) == (k >> 3) && i < a.n2 && o < a.n3;
+      F.w3b[j] = bfbits(ldsel(P, ok, OFF3 + i * 16 + o));
+    }
+    // L2 backward: A[m = in c][k = packed out of tile u]
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int o = k & 7;
+      const bool ok = (k >> 3) == u && c < a.n1 && o < a.n2;
+      F.w2b[u][j] = bfbits(ldsel(P, ok, OFF2 + c * 16 + o));
+    }
+  }
+  if (c == 15 && g == 3) F.w1t[1][3] = bfbits(256.0f);   // L1 bias slot 15 (as load_frags INJ)
+}
+
+// Image slot s -> the packed-accumulator slab slots whose sum it is (-1: none, gradient 0).
+__device__ __forceinline__ void packed_fold_src(int s, int& s1, int& s2) {
+  s1 = s;
+  s2 = -1;
+  if (s < OFF2 || s >= NPARAM) return;   // layer 1 and the metric sums are not packed
+  if (s < OFF3) {
+    const int in = (s - OFF2) >> 4, out = (s - OFF2) & 15;
+    if (out < 7) s2 = s + 8;
+    else s1 = -1;
+    return;
+  }
+  const bool l3 = s < OFF4;
+  const int base = l3 ? OFF3 : OFF4, w = l3 ? 16 : 32;
+  const int in = (s - base) / w, out = (s - base) % w;
+  const int pin = in < 7 ? in : (in == 15 ? 7 : -1);
+  if (pin < 0 || (l3 && out >= 7)) {
+    s1 = -1;
+    return;
+  }
+  s1 = base + pin * w + out;
+  s2 = base + (pin + 8) * w + out + (l3 ? 8 : 0);
+}
+
+// One packed pair.  TP: the pair's second tile is a stand-in (a wave's odd last tile) whose
+// loss, metrics and gradients are all masked to zero.
+template <int PACK, int DC, bool TP>
+__device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP& F, char* scr, int c, int g,
+                                                  const f32x4 (&xf)[2][2], const int (&ix)[2], float pad1,
+                                                  f32x4 acc1[2], f32x4& acc2, f32x4& acc3, f32x4 acc4[2],
+                                                  float& sq, float& ab, float& corr, float& rows) {
+  static_assert(PACK == PACK_REF && DC > 16, "reference model, compile-time D");
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const bf16x4 zb = {0, 0, 0, 0};
+  const bool pad_lane = (g == 3);
+  const bool lo = c < 8;   // lanes holding tile 0's half of a packed operand (as n or m = c)
+
+  bf16x4 xb0[2], xb1[2], h1b[2];
+  f32x4 h1[2], y[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    f32x4 x1 = xf[u][1];
+    x1[3] += pad1;
+    xb0[u] = pack4(xf[u][0]);
+    xb1[u] = pack4(x1);
+  }
+  f32x4 z1[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) z1[u] = mfma32(F.w1t[0], F.w1t[1], xb0[u], xb1[u], zero4);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h1[u][i] = tanh_exp2(z1[u][i]);
+    h1b[u] = pack4(h1[u]);
+  }
+  const f32x4 z2 = mfma32(F.w2t[0], F.w2t[1], h1b[0], h1b[1], zero4);
+  f32x4 h2, h3;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) h2[i] = relu_fast(z2[i]);
+  const bf16x4 h2b = pack4(h2);
+  const f32x4 z3 = mfma16(F.w3t, h2b, zero4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) h3[i] = tanh_exp2(z3[i]);
+  const bf16x4 h3b = pack4(h3);
+  f32x4 dz4[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const f32x4 z4 = mfma16(F.w4t[u][t], h3b, zero4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (t == 1 && !live_hi<DC>(i)) {
+          y[u][t][i] = 0.f;
+          dz4[u][t][i] = 0.f;
+          continue;
+        }
+        y[u][t][i] = relu_fast(z4[i]);
+        float e = y[u][t][i] - xf[u][t][i];
+        if (TP && u == 1) e = 0.f;
+        sq = fmaf(e, e, sq);
+        dz4[u][t][i] = y[u][t][i] > 0.f ? e : 0.f;   // relu'; x 2/D folded into F.w4b / the acc4 slab
+      }
+    }
+  if (a.want_acc) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (TP && u == 1) continue;
+      const int iy = row_argmax_nonneg<DC>(y[u], a.D, g);
+      corr += (g == 0 && iy == ix[u]) ? 1.f : 0.f;
+    }
+  }
+  rows += (g == 0) ? (TP ? 1.f : 2.f) : 0.f;
+
+  bf16x4 dz4b0[2], dz4b1[2], dz1b[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    dz4b0[u] = pack4(dz4[u][0]);
+    dz4b1[u] = pack4(dz4[u][1]);
+  }
+  f32x4 d3 = mfma32(F.w4b[0][0], F.w4b[0][1], dz4b0[0], dz4b1[0], zero4);
+  d3 = mfma32(F.w4b[1][0], F.w4b[1][1], dz4b0[1], dz4b1[1], d3);
+  f32x4 dz3, dz2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dz3[i] = d3[i] * fmaf(-h3[i], h3[i], 1.0f);   // 0 at the bias slots (h = 1)
+  const bf16x4 dz3b = pack4(dz3);
+  const f32x4 d2 = mfma16(F.w3b, dz3b, zero4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dz2[i] = h2[i] > 0.f ? d2[i] : 0.f;
+  const bf16x4 dz2b = pack4(dz2);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const f32x4 d1 = mfma16(F.w2b[u], dz2b, zero4);
+    f32x4 dz1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float hv = h1[u][i];
+      if (TP && u == 1) {
+        dz1[i] = 0.f;
+        continue;
+      }
+      ab += (i == 3 && pad_lane) ? 0.f : fabsf(hv);
+      // Keras L1 activity regulariser gradient as one v_med3 (see train_tile)
+      dz1[i] = (d1[i] + __builtin_amdgcn_fmed3f(hv, -a.l1, a.l1)) * fmaf(-hv, hv, 1.0f);
+    }
+    dz1b[u] = pack4(dz1);
+  }
+
+  // weight gradients (rows on K through the LDS transpose)
+  bf16x4 xr0[2], xr1[2], dz1r[2], h1r[2], dz4r0[2], dz4r1[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    xr0[u] = lds_transpose(xb0[u], scr + 0 * 512, c, g);
+    xr1[u] = lds_transpose(xb1[u], scr + 1 * 512, c, g);
+    dz1r[u] = lds_transpose(dz1b[u], scr + 2 * 512, c, g);
+    h1r[u] = lds_transpose(h1b[u], scr + 3 * 512, c, g);
+    dz4r0[u] = lds_transpose(dz4b0[u], scr + 8 * 512, c, g);
+    dz4r1[u] = lds_transpose(dz4b1[u], scr + 9 * 512, c, g);
+  }
+  const bf16x4 dz2r = lds_transpose(dz2b, scr + 4 * 512, c, g);
+  const bf16x4 h2r = lds_transpose(h2b, scr + 5 * 512, c, g);
+  const bf16x4 dz3r = lds_transpose(dz3b, scr + 6 * 512, c, g);
+  const bf16x4 h3r = lds_transpose(h3b, scr + 7 * 512, c, g);
+  acc1[0] = mfma32(xr0[0], xr0[1], dz1r[0], dz1r[1], acc1[0]);
+  acc1[1] = mfma32(xr1[0], xr1[1], dz1r[0], dz1r[1], acc1[1]);
+  acc2 = mfma32(h1r[0], h1r[1], lo ? dz2r : zb, lo ? zb : dz2r, acc2);   // n < 8: tile 0, n >= 8: tile 1
+  acc3 = mfma32(h2r, zb, dz3r, zb, acc3);                               // diagonal blocks
+  const bf16x4 h3r0 = lo ? h3r : zb, h3r1 = lo ? zb : h3r;               // m < 8: tile 0, m >= 8: tile 1
+  acc4[0] = mfma32(h3r0, h3r1, dz4r0[0], dz4r0[1], acc4[0]);
+  acc4[1] = mfma32(h3r0, h3r1, dz4r1[0], dz4r1[1], acc4[1]);
+}
+
 // 3 waves/SIMD: caps the allocation at 168 VGPRs (no spills); 171 would drop to 2.
 // PF > 0: the input rows stream through a per-wave LDS ring PF tiles deep, filled
 // by LDS-DMA (no VGPRs held for the prefetch, PF-1 tiles in flight per wave);
@@ -577,13 +982,15 @@ __device__ __forceinline__ void train_tile(const AEArgs& a, const Frags& F, char
 // of register prefetch (any ld / D).
 // OCC = waves per SIMD the variant is built for: 3 (168-VGPR budget, 6 KB ring per
 // wave) or 4 (128-VGPR budget, 3968-B ring per wave so four workgroups fit in LDS).
-template <int OCC>
-constexpr int ring_bytes() { return OCC >= 4 ? 3968 : 6144; }
+// ILP 2 (tile pairs, 3 waves/SIMD): 7008 B = six 1168-B packed tiles per wave; with the
+// slab area and the normaliser 52928 B per workgroup, three workgroups per CU.
+template <int OCC, int ILP = 1>
+constexpr int ring_bytes() { return OCC >= 4 ? 3968 : (ILP >= 2 ? 7008 : 6144); }
 
-template <int PACK, bool VEC, int PF, int OCC, int DC = 0, int XM = 0>
+template <int PACK, bool VEC, int PF, int OCC, int DC = 0, int XM = 0, int ILP = 1>
 __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   constexpr bool FAST = zero_preserving<PACK>();
-  constexpr int RING = ring_bytes<OCC>();
+  constexpr int RING = ring_bytes<OCC, ILP>();
   static_assert(WAVES * 10 * 512 <= SLAB_BYTES, "transpose scratch must fit in the slab buffer");
   static_assert(PF == 0 || PF * 64 * 17 <= RING, "ring slots must fit the smallest ring tile");
   // XM: x-argmax mode. 0 in-kernel argmax; 1 tile-packed ring (rows + ingest-time argmax
@@ -612,7 +1019,11 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   }
 
   Frags F;
-  load_frags<FAST, FAST && prescaled_tanh<PACK>(), FAST && inject_bias_slots<PACK>()>(a, c, g, F, true);
+  FragsP FP;   // ILP 3 (packed pairs) only
+  if constexpr (ILP == 3)
+    load_frags_packed(a, c, g, FP);
+  else
+    load_frags<FAST, FAST && prescaled_tanh<PACK>(), FAST && inject_bias_slots<PACK>()>(a, c, g, F, true);
   const float pad1 = (g == 3) ? 1.0f : 0.0f;
   __syncthreads();  // normaliser visible (before any LDS-DMA is in flight)
 
@@ -661,6 +1072,63 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
         return ((t + 1) & (CH - 1)) ? t + 1 : t + 1 + (stride - 1) * CH;
       };
       const int64_t t0 = ufirst * CH;
+      if constexpr (ILP >= 2) {
+        // tile pairs (t, t + stride): two issues per iteration, the pair's two tiles landed
+        // = vmcnt(NV * (PF - 2)); a last unpaired tile runs alone (ILP 2: U = 1; ILP 3: a
+        // packed pair whose second tile is a masked stand-in)
+        static_assert(XM == 1 && CH == 1 && PF >= 3, "tile pairs: tile-packed ring, plain order");
+        auto ring_tile = [&](int slot, f32x4 xf[2], int& ix) {
+          typedef __attribute__((address_space(3))) const unsigned char lds_u8;
+          ring_x(a, ring + slot * slotb, c, g, xf);
+          ix = (int)*(lds_u8*)(ring + slot * slotb + 64 * a.D + c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xf[1][j] = (live_hi<DC>(j) && 16 + 4 * g + j < DC) ? xf[1][j] : 0.f;
+        };
+        int64_t tp = t0;
+#pragma unroll
+        for (int k = 0; k < PF - 2; ++k) {
+          issue(tp, k);
+          tp += stride;
+        }
+        int rd = 0, wr = PF - 2;
+        int64_t t = t0;
+        for (; t + stride < nfull; t += 2 * stride) {
+          issue(tp, wr);
+          issue(tp + stride, wr + 1 == PF ? 0 : wr + 1);
+          tp += 2 * stride;
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV * (PF - 2)) : "memory");
+          f32x4 xf[2][2];
+          int ix[2];
+          ring_tile(rd, xf[0], ix[0]);
+          ring_tile(rd + 1 == PF ? 0 : rd + 1, xf[1], ix[1]);
+          rd = rd + 2 >= PF ? rd + 2 - PF : rd + 2;
+          wr = wr + 2 >= PF ? wr + 2 - PF : wr + 2;
+          if constexpr (ILP == 3)
+            train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr,
+                                               rows);
+          else
+            train_tiles_ilp<PACK, DC, 2>(a, F, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
+        }
+        if (t < nfull) {   // already issued: the oldest of the PF - 2 tiles in flight
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV * (PF - 3)) : "memory");
+          if constexpr (ILP == 3) {
+            f32x4 xf[2][2];
+            int ix[2];
+            ring_tile(rd, xf[0], ix[0]);
+            xf[1][0] = xf[0][0];
+            xf[1][1] = xf[0][1];
+            ix[1] = ix[0];
+            train_pair_packed<PACK, DC, true>(a, FP, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr,
+                                              rows);
+          } else {
+            f32x4 xf[1][2];
+            int ix[1];
+            ring_tile(rd, xf[0], ix[0]);
+            train_tiles_ilp<PACK, DC, 1>(a, F, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the ring is retired
+      } else {
       int64_t tp = t0;   // tile of the next DMA issue (PF - 1 ahead of t)
 #pragma unroll
       for (int k = 0; k < PF - 1; ++k) {
@@ -700,6 +1168,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
                                                     sq, ab, corr, rows, ix);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the ring is retired
+      }
     }
   } else {
     f32x4 xnext[2];
@@ -716,8 +1185,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
                                     rows);
     }
   }
-  // ragged last tile: handled by the wave that would own tile index nfull
-  if ((a.n & 15) && first == nfull % stride) {
+  // ragged last tile: handled by the wave that would own tile index nfull (never with packed
+  // pairs: that variant runs on whole tiles only)
+  if (ILP != 3 && (a.n & 15) && first == nfull % stride) {
     const int64_t r = nfull * 16 + c;
     const bool valid = r < a.n;
     f32x4 xf[2], sc[2], sh[2];
@@ -756,10 +1226,22 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   __syncthreads();
   float* out = a.partials + (int64_t)blockIdx.x * NSLOT;
   for (int s = threadIdx.x; s < NSLOT; s += WAVES * 64) {
-    float v = smem[s];
+    if constexpr (ILP == 3) {   // packed accumulators -> parameter-image slots
+      int s1, s2;
+      packed_fold_src(s, s1, s2);
+      float v = 0.f;
 #pragma unroll
-    for (int w = 1; w < WAVES; ++w) v += smem[w * NSLOT + s];
-    out[s] = v;
+      for (int w = 0; w < WAVES; ++w) {
+        if (s1 >= 0) v += smem[w * NSLOT + s1];
+        if (s2 >= 0) v += smem[w * NSLOT + s2];
+      }
+      out[s] = v;
+    } else {
+      float v = smem[s];
+#pragma unroll
+      for (int w = 1; w < WAVES; ++w) v += smem[w * NSLOT + s];
+      out[s] = v;
+    }
   }
 }
 
@@ -926,14 +1408,32 @@ static bool ring_pf_enabled() {
 // SML_AE_OCC=3|4 picks the waves-per-SIMD variant of the ring kernel.  Default 4:
 // 128 VGPRs, 4 workgroups/CU; on MI355X 27.1 vs 25.7 G rows/s at B = 8M
 // (profiles/r01_v4/sweep_occ*.log).
-static int train_occupancy() {
-  static const int occ = [] {
-    const char* e = getenv("SML_AE_OCC");
-    return (e && e[0] == '3') ? 3 : 4;
-  }();
-  return occ;
+// SML_AE_ILP=1|2 picks the one-tile or the tile-pair (train_tiles_ilp, 3 waves/SIMD) loop of
+// the headline variant (reference model, D = 18, tile-packed ring).
+// Both are read at every launch (one getenv per ~1 ms step), so a test can A/B them in one process.
+// Default 3 (packed pairs: 40.4 vs 36.9 G rows/s for the one-tile loop, profiles/r02/ilp);
+// the pair variants always run at 3 waves/SIMD, SML_AE_OCC only picks the one-tile variants'.
+static int train_ilp() {
+  const char* e = getenv("SML_AE_ILP");
+  return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 3;
 }
-int ae_train_blocks_per_cu() { return train_occupancy(); }
+static int train_occupancy() {
+  const char* e = getenv("SML_AE_OCC");
+  return (e && e[0] == '3') ? 3 : 4;
+}
+// The host sizes its partials buffer for the largest variant (4 resident workgroups per CU);
+// the launcher trims the grid to two rounds of the launched variant's residency.
+int ae_train_blocks_per_cu() { return 4; }
+static int device_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      return 256;
+    return n;
+  }();
+  return cus;
+}
 
 int ae_nslot() { return NSLOT; }
 int ae_nparam() { return NPARAM; }
@@ -950,7 +1450,7 @@ int ae_train_grid(int64_t n, int max_blocks) {
 hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
                            const float* params, float* partials, int64_t* iter, const int64_t* cursor,
                            const int* dims, const int* acts, float l1, int want_acc, int grid, const uint8_t* xpack,
-                           hipStream_t stream) {
+                           hipStream_t stream, int* grid_used) {
   AEArgs a{};
   a.x = x; a.n = n; a.ld = ld; a.scale = scale; a.shift = shift; a.params = params;
   a.partials = partials; a.iter = iter; a.cursor = cursor; a.xpack = xpack;
@@ -965,8 +1465,16 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
   const bool ring_ok = vec && ld == D && D >= 17 && D <= 31 && ((reinterpret_cast<uintptr_t>(x) & 15) == 0) &&
                        (cursor == nullptr || ((n * ld) & 3) == 0) && ring_pf_enabled();
   const int pack = acts[0] | (acts[1] << 2) | (acts[2] << 4) | (acts[3] << 6);
-  const dim3 gd(grid), bd(WAVES * 64);
+  const dim3 bd(WAVES * 64);
   const int occ = train_occupancy();
+  *grid_used = grid;
+  dim3 gd(grid);
+  // the pair variants hold 3 workgroups per CU: two rounds of that, not of the host's 4
+  auto pair_grid = [&] {
+    const int g3 = 2 * 3 * device_cus();
+    if (grid > g3) *grid_used = grid = g3;
+    gd = dim3(grid);
+  };
   if (pack == PACK_REF) {
     // tile-packed ring with ingest-time x argmax (pack_tiles_argmax): whole 16-row tiles
     const bool xa_ok = xpack != nullptr && want_acc && (n & 15) == 0 &&
@@ -979,6 +1487,13 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18, 2>), gd, bd, 0, stream, a);
     else if (ring_ok && occ == 4 && D == 18 && want_acc && probe == 3)
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18, 3>), gd, bd, 0, stream, a);
+    else if (ring_ok && D == 18 && xa_ok && train_ilp() == 2) {
+      pair_grid();
+      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 1, 2>), gd, bd, 0, stream, a);
+    } else if (ring_ok && D == 18 && xa_ok && train_ilp() == 3 && dims[1] <= 15 && dims[2] <= 7 && dims[3] <= 7) {
+      pair_grid();
+      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 1, 3>), gd, bd, 0, stream, a);
+    }
     else if (ring_ok && occ == 4 && D == 18 && xa_ok)
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18, 1>), gd, bd, 0, stream, a);
     else if (ring_ok && occ == 4 && D == 18)  // the cardata-v1 reference model: D fixed at compile time

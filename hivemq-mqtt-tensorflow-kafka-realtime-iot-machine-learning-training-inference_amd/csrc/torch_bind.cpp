@@ -107,14 +107,15 @@ int64_t ae_train_partials(const at::Tensor& x, const c10::optional<at::Tensor>& 
   }
   const int grid = sml::ae_train_grid(n, (int)max_blocks);
   TORCH_CHECK(partials.numel() >= (int64_t)grid * sml::ae_nslot(), "partials buffer too small for grid ", grid);
+  int used = grid;   // the launcher may trim it (pair variants: 3 resident workgroups per CU)
   c10::hip::HIPGuard guard(x.device().index());
   int d[4] = {(int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3]};
   int a[4] = {(int)acts[0], (int)acts[1], (int)acts[2], (int)acts[3]};
   SML_CHECK_HIP(sml::ae_train_launch(x.data_ptr<float>(), n, x.stride(0), opt_ptr(scale), opt_ptr(shift),
                                      params.data_ptr<float>(), partials.data_ptr<float>(), iter_ptr, cur_ptr, d, a,
                                      (float)l1,
-                                     want_acc ? 1 : 0, grid, xpack_ptr, cur_stream(x)));
-  return grid;
+                                     want_acc ? 1 : 0, grid, xpack_ptr, cur_stream(x), &used));
+  return used;
 }
 
 // ingest-time tile-packed ring: per 16-row tile the rows then the 16 argmax bytes

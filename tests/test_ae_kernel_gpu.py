@@ -142,6 +142,9 @@ def test_ring_cursor_and_graph_replay(cuda_device, xpack, monkeypatch):
     """Device-cursor ring steps == explicit-slice steps; a captured graph replays them.
     xpack=1: the tile-packed ring (rows + ingest-time argmax bytes per 16-row tile)."""
     monkeypatch.setenv("SML_AE_XPACK", xpack)
+    # the one-tile loop, so the packed ring's steps are bit-comparable with the slice path
+    # (the default packed-pair loop is checked against it in test_tile_pair_loop_matches_one_tile_loop)
+    monkeypatch.setenv("SML_AE_ILP", "1")
     spec = AESpec()
     w = _weights(spec, seed=5)
     scale, shift = normalize_affine()
@@ -251,3 +254,46 @@ def test_gradients_vs_bf16_rounded_reference(cuda_device, D, n):
         assert relerr(gf, gr) < 1e-3, i
     assert abs(metr[0] - sq) / sq < 1e-4
     assert abs(metr[1] - ab) / ab < 1e-4
+
+
+@pytest.mark.parametrize("ilp", ["2", "3"])
+@pytest.mark.parametrize("ntiles,blocks", [(64 * 5, 16), (64 * 4, 16), (100, 16), (30, 16), (4096, 48)])
+def test_tile_pair_loop_matches_one_tile_loop(cuda_device, monkeypatch, ntiles, blocks, ilp):
+    """SML_AE_ILP=2 (two tiles per wave interleaved, K = 32-row weight-gradient MFMAs) and
+    SML_AE_ILP=3 (two tiles packed into one fragment in the 7-wide layers, block-diagonal
+    weights, accumulators folded into the image per launch) against the one-tile loop on the
+    headline ring (tile-packed, D = 18).  On the same grid every wave visits the same tiles in
+    the same order: ILP 2's metric sums are bit-identical, ILP 3's differ only where the
+    packed MFMAs sum the same products in another K order.  Tile counts per wave cover odd
+    (a last unpaired tile), even, one and zero."""
+    from streamml.ops.ae import NPARAM
+    spec = AESpec()
+    w = _weights(spec, seed=7)
+    scale, shift = normalize_affine()
+    B = 16 * ntiles
+    rng = np.random.default_rng(17)
+    raw = torch.from_numpy((rng.uniform(0, 1, size=(2 * B, 18)) * 40).astype(np.float32)).to(cuda_device)
+    out = {}
+    for v in ("1", ilp):
+        monkeypatch.setenv("SML_AE_ILP", v)
+        f = FusedAE(spec, w, cuda_device, max_blocks=blocks, scale=scale, shift=shift)
+        f.attach_ring(raw, B)
+        assert f.ring_xpack is not None
+        imgs = []
+        for _ in range(3):
+            f.step_ring(allreduce=lambda g: imgs.append(g.detach().cpu().numpy().copy()))
+        torch.cuda.synchronize()
+        out[v] = (imgs, f.params.detach().cpu().numpy())
+    one, two = out["1"][0], out[ilp][0]
+    if ilp == "2":
+        np.testing.assert_array_equal(one[0][NPARAM:], two[0][NPARAM:])   # sq, |h1|, correct, rows
+    else:
+        np.testing.assert_allclose(two[0][NPARAM:NPARAM + 2], one[0][NPARAM:NPARAM + 2], rtol=1e-5)
+        assert abs(two[0][NPARAM + 2] - one[0][NPARAM + 2]) <= max(2, 1e-3 * B)   # argmax near-ties
+        assert two[0][NPARAM + 3] == one[0][NPARAM + 3]
+    assert one[0][NPARAM + 3] == B
+    assert _relerr(two[0][:NPARAM], one[0][:NPARAM]) < (1e-5 if ilp == "2" else 1e-3)
+    for a, b in zip(one[1:], two[1:]):
+        assert _relerr(b[:NPARAM], a[:NPARAM]) < (1e-4 if ilp == "2" else 2e-3)
+        assert abs(a[NPARAM] - b[NPARAM]) <= 1e-4 * abs(a[NPARAM])
+    assert _relerr(out[ilp][1], out["1"][1]) < (1e-4 if ilp == "2" else 1e-3)

@@ -48,6 +48,13 @@ for s in $STEPS; do
       step cli_lstm 600 python -m streamml.cli lstm-v1 synthetic://5000 SENSOR_DATA_S_AVRO 0 out --epochs 1 --take 300 &&
       step cli_mnist 600 python -m streamml.cli mnist --epochs 1 --steps-per-epoch 3000 --rows 20000 &&
       step cli_creditcard 600 python -m streamml.cli creditcard --evaluate --rows 100000 --epochs 3 ;;
+    ilpab)   # headline-only A/B of the one-tile vs tile-pair train loop, alternated
+      for r in 1 2; do
+        for v in ${ILPS:-1 2}; do
+          step "ilp${v}_run$r" 300 env SML_AE_ILP=$v python bench.py --infer-events 0 --fleet-models 0 --batch32-steps 0 \
+              --fit-rows 0 --stream-rows 0 || true
+        done
+      done ;;
     sweep) step ae_sweep 600 python tools/ae_sweep.py ${SWEEP_ARGS:-} ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc)
