@@ -380,8 +380,11 @@ __device__ __forceinline__ int row_argmax_fast(const f32x4 v[2], int D, int g) {
 // Argmax of a row of NON-NEGATIVE values (a relu output) as one integer max: each live
 // feature f becomes the key (bits(v) & 0x7fffffc0) | (63 - f) -- a non-negative float's
 // bits order like the float (the sign bit is cleared, so a -0 from med3 counts as 0),
-// and the low 6 bits break ties toward the lowest index (tf.argmax).  Masked features
-// are key 0, below every live key.  Exact except when the two largest values agree in
+// and the low 6 bits break ties toward the lowest index (tf.argmax).  Only compile-time
+// padding is masked (key 0): the callers' padded features f >= D hold exactly 0 (zero
+// weights, relu(0)), so their keys 63 - f lose to every real feature's -- a real 0 has the
+// lower index, anything larger has value bits >= 0x40 -- and need no per-lane mask (a
+// lane-dependent select around the asm key became four divergent branches).  Exact except when the two largest values agree in
 // all but the last 6 of 23 mantissa bits (relative gap < 2^-17, far below the bf16
 // noise of the values), where the lower index wins.  ~16 VALU instead of ~35.
 __device__ __forceinline__ unsigned umax3(unsigned a, unsigned b, unsigned c) {
@@ -396,20 +399,39 @@ __device__ __forceinline__ unsigned bfi_key(unsigned bits, unsigned lo) {
   return r;
 }
 template <int DC>
-__device__ __forceinline__ int row_argmax_nonneg(const f32x4 v[2], int D, int g) {
+__device__ __forceinline__ unsigned nonneg_key_max(const f32x4 v[2], int D, int g) {   // the lane's 8 features
   unsigned k[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int t = q >> 2, i = q & 3;
     const int f = 16 * t + 4 * g + i;
-    const bool live = t == 0 || (live_hi<DC>(i) && f < D);
+    const bool live = t == 0 || live_hi<DC>(i);
+    (void)D;
     k[q] = live ? bfi_key(__float_as_uint(v[t][i]), (unsigned)(63 - f)) : 0u;
   }
   unsigned m = umax3(umax3(k[0], k[1], k[2]), k[3], live_hi<DC>(0) ? k[4] : k[3]);
   if (live_hi<DC>(1) || live_hi<DC>(2)) m = umax3(m, live_hi<DC>(1) ? k[5] : m, live_hi<DC>(2) ? k[6] : m);
   if (live_hi<DC>(3)) m = umax3(m, k[7], m);
+  return m;
+}
+template <int DC>
+__device__ __forceinline__ int row_argmax_nonneg(const f32x4 v[2], int D, int g) {
+  unsigned m = nonneg_key_max<DC>(v, D, g);
   const auto r16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
   m = umax3(r16[0], r16[1], r16[1]);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+  m = umax3(r32[0], r32[1], r32[1]);
+  return 63 - (int)(m & 63u);
+}
+// Two tiles' row argmaxes with ONE butterfly: permlane16_swap(m0, m1) moves tile 1's even
+// rows next to tile 0's odd rows, so after its max rows 0 / 2 hold tile 0's pairwise maxima
+// and rows 1 / 3 tile 1's; the permlane32 step then completes both.  Lane group g gets the
+// argmax of row c of tile (g & 1).
+template <int DC>
+__device__ __forceinline__ int row_argmax_nonneg_pair(const f32x4 v0[2], const f32x4 v1[2], int D, int g) {
+  const unsigned m0 = nonneg_key_max<DC>(v0, D, g), m1 = nonneg_key_max<DC>(v1, D, g);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(m0, m1, false, false);
+  unsigned m = r16[0] > r16[1] ? r16[0] : r16[1];
   const auto r32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
   m = umax3(r32[0], r32[1], r32[1]);
   return 63 - (int)(m & 63u);
@@ -869,7 +891,7 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
     xb0[u] = pack4(xf[u][0]);
     xb1[u] = pack4(x1);
   }
-  f32x4 z1[2];
+  f32x4 z1[2], l1s[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) z1[u] = mfma32(F.w1t[0], F.w1t[1], xb0[u], xb1[u], zero4);
 #pragma unroll
@@ -878,6 +900,12 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
     for (int i = 0; i < 4; ++i) h1[u][i] = tanh_exp2(z1[u][i]);
     h1b[u] = pack4(h1[u]);
   }
+  // Keras L1 activity-regulariser gradient l1 * sign(h1) as one v_med3 (see train_tile), computed
+  // off the critical path and fed to the dh1 MFMA as its accumulator input
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) l1s[u][i] = (TP && u == 1) ? 0.f : __builtin_amdgcn_fmed3f(h1[u][i], -a.l1, a.l1);
   const f32x4 z2 = mfma32(F.w2t[0], F.w2t[1], h1b[0], h1b[1], zero4);
   f32x4 h2, h3;
 #pragma unroll
@@ -907,13 +935,11 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
         dz4[u][t][i] = y[u][t][i] > 0.f ? e : 0.f;   // relu'; x 2/D folded into F.w4b / the acc4 slab
       }
     }
-  if (a.want_acc) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (TP && u == 1) continue;
-      const int iy = row_argmax_nonneg<DC>(y[u], a.D, g);
-      corr += (g == 0 && iy == ix[u]) ? 1.f : 0.f;
-    }
+  if (a.want_acc) {   // lane group 0 counts row c of tile 0, group 1 row c of tile 1
+    const int iy = row_argmax_nonneg_pair<DC>(y[0], y[1], a.D, g);
+    const int sel = -(g & 1);   // bit-select: a ?: on the pair becomes a scratch array indexed by g
+    const int ixs = (ix[0] & ~sel) | (ix[1] & sel);
+    corr += ((TP ? g == 0 : g < 2) && iy == ixs) ? 1.f : 0.f;
   }
   rows += (g == 0) ? (TP ? 1.f : 2.f) : 0.f;
 
@@ -935,7 +961,7 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   const bf16x4 dz2b = pack4(dz2);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const f32x4 d1 = mfma16(F.w2b[u], dz2b, zero4);
+    const f32x4 d1 = mfma16(F.w2b[u], dz2b, l1s[u]);   // dh1 + l1 * sign(h1)
     f32x4 dz1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -945,8 +971,7 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
         continue;
       }
       ab += (i == 3 && pad_lane) ? 0.f : fabsf(hv);
-      // Keras L1 activity regulariser gradient as one v_med3 (see train_tile)
-      dz1[i] = (d1[i] + __builtin_amdgcn_fmed3f(hv, -a.l1, a.l1)) * fmaf(-hv, hv, 1.0f);
+      dz1[i] = d1[i] * fmaf(-hv, hv, 1.0f);
     }
     dz1b[u] = pack4(dz1);
   }
@@ -969,7 +994,7 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   acc1[0] = mfma32(xr0[0], xr0[1], dz1r[0], dz1r[1], acc1[0]);
   acc1[1] = mfma32(xr1[0], xr1[1], dz1r[0], dz1r[1], acc1[1]);
   acc2 = mfma32(h1r[0], h1r[1], lo ? dz2r : zb, lo ? zb : dz2r, acc2);   // n < 8: tile 0, n >= 8: tile 1
-  acc3 = mfma32(h2r, zb, dz3r, zb, acc3);                               // diagonal blocks
+  acc3 = mfma16(h2r, dz3r, acc3);   // diagonal blocks; acc3's chain is 16x16x16 only in this variant
   const bf16x4 h3r0 = lo ? h3r : zb, h3r1 = lo ? zb : h3r;               // m < 8: tile 0, m >= 8: tile 1
   acc4[0] = mfma32(h3r0, h3r1, dz4r0[0], dz4r0[1], acc4[0]);
   acc4[1] = mfma32(h3r0, h3r1, dz4r1[0], dz4r1[1], acc4[1]);
