@@ -436,6 +436,26 @@ __device__ __forceinline__ int row_argmax_nonneg_pair(const f32x4 v0[2], const f
   m = umax3(r32[0], r32[1], r32[1]);
   return 63 - (int)(m & 63u);
 }
+// The same for the packed-pair output layout: outputs 0..15 of tile u in lo[u] (lane (c, g)
+// features 4g..4g+3 of row c), outputs 16 / 17 of both tiles in ONE register `up` (lane group
+// g holds output 16 + (g & 1) of tile g >> 1).  D = 18.
+__device__ __forceinline__ int row_argmax_up_pair(const f32x4 lo0, const f32x4 lo1, float up, int g) {
+  unsigned k0[4], k1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    k0[i] = bfi_key(__float_as_uint(lo0[i]), (unsigned)(63 - 4 * g - i));
+    k1[i] = bfi_key(__float_as_uint(lo1[i]), (unsigned)(63 - 4 * g - i));
+  }
+  const unsigned ku = bfi_key(__float_as_uint(up), (unsigned)(63 - 16 - (g & 1)));
+  const unsigned own0 = g < 2 ? ~0u : 0u;   // which tile's row this lane's `up` belongs to
+  const unsigned m0 = umax3(umax3(k0[0], k0[1], k0[2]), k0[3], ku & own0);
+  const unsigned m1 = umax3(umax3(k1[0], k1[1], k1[2]), k1[3], ku & ~own0);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(m0, m1, false, false);
+  unsigned m = r16[0] > r16[1] ? r16[0] : r16[1];
+  const auto r32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+  m = umax3(r32[0], r32[1], r32[1]);
+  return 63 - (int)(m & 63u);
+}
 
 // One 16-row tile: forward, loss, metrics, backward, weight-gradient MFMAs.
 // FAST (zero-preserving activations): no per-feature masks -- padded features
@@ -774,8 +794,10 @@ struct FragsP {
   bf16x4 w1t[2];      // L1 forward (as Frags: prescaled, bias slot 15 injected)
   bf16x4 w2t[2];      // L2 forward, K halves = tile 0 / tile 1 inputs
   bf16x4 w3t;         // L3 forward, block-diagonal (prescaled, packed bias slots injected)
-  bf16x4 w4t[2][2];   // L4 forward [tile][output half]
-  bf16x4 w4b[2][2];   // L4 backward [tile][K half = output half] (x 2/D)
+  bf16x4 w4t[2];      // L4 forward, outputs 0..15 [tile]
+  bf16x4 w4u;         // L4 forward, outputs 16, 17 of both tiles into one register (see UP below)
+  bf16x4 w4b[2];      // L4 backward from outputs 0..15 [tile] (x 2/D)
+  bf16x4 w4bu;        // L4 backward from the packed outputs 16, 17 (x 2/D)
   bf16x4 w3b;         // L3 backward, block-diagonal
   bf16x4 w2b[2];      // L2 backward [tile]
 };
@@ -811,24 +833,32 @@ __device__ __forceinline__ void load_frags_packed(const AEArgs& a, int c, int g,
       if (same && o == 7 && i == 7) v = 256.0f;   // tanh_exp2(256) = 1 exactly
       F.w3t[j] = bfbits(v);
     }
-    // L4 forward: A[m = out 16t + c][k = packed in of tile u]
+    // L4 forward, outputs 0..15: A[m = out c][k = packed in of tile u]
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u) {
+      const int i = k & 7;
+      const bool ok = (k >> 3) == u && c < a.D && (i < a.n3 || i == 7);
+      F.w4t[u][j] = bfbits(ldsel(P, ok, OFF4 + img_row_of_packed(i) * 32 + c));
+    }
+    // L4 forward, outputs 16 / 17: A[m = 4q (UP slot q: tile q >> 1, output 16 + (q & 1))][k = packed in]
+    {
+      const int q = c >> 2, i = k & 7, out = 16 + (q & 1);
+      const bool ok = (c & 3) == 0 && (k >> 3) == (q >> 1) && out < a.D && (i < a.n3 || i == 7);
+      F.w4u[j] = bfbits(ldsel(P, ok, OFF4 + img_row_of_packed(i) * 32 + out));
+    }
+    // L4 backward from outputs 0..15: A[m = packed in c (tile u)][k = out k]; bias rows carry no gradient
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int out = 16 * t + c, i = k & 7;
-        const bool ok = (k >> 3) == u && out < a.D && (i < a.n3 || i == 7);
-        F.w4t[u][t][j] = bfbits(ldsel(P, ok, OFF4 + img_row_of_packed(i) * 32 + out));
-      }
-    // L4 backward: A[m = packed in c (tile u)][k = out 16s + k]; bias rows carry no gradient
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int out = 16 * s + k, i = c & 7;
-        const bool ok = (c >> 3) == u && i < a.n3 && out < a.D;
-        F.w4b[u][s][j] = bfbits((2.0f / (float)a.D) * ldsel(P, ok, OFF4 + i * 32 + out));
-      }
+    for (int u = 0; u < 2; ++u) {
+      const int i = c & 7;
+      const bool ok = (c >> 3) == u && i < a.n3 && k < a.D;
+      F.w4b[u][j] = bfbits((2.0f / (float)a.D) * ldsel(P, ok, OFF4 + i * 32 + k));
+    }
+    // L4 backward from UP: A[m = packed in c][k = 4q + j], only j = 0 and q's tile = c's tile
+    {
+      const int i = c & 7, q = g, out = 16 + (q & 1);
+      const bool ok = j == 0 && (q >> 1) == (c >> 3) && i < a.n3 && out < a.D;
+      F.w4bu[j] = bfbits((2.0f / (float)a.D) * ldsel(P, ok, OFF4 + i * 32 + out));
+    }
     // L3 backward: A[m = packed in c][k = packed out k], same tile
     {
       const int i = c & 7, o = k & 7;
@@ -865,6 +895,15 @@ __device__ __forceinline__ void packed_fold_src(int s, int& s1, int& s2) {
     s1 = -1;
     return;
   }
+  if (!l3 && out >= 16) {   // outputs 16 / 17 live in the UP columns 4q: tile 0 q = 0, 1; tile 1 q = 2, 3
+    if (out >= 18) {
+      s1 = -1;
+      return;
+    }
+    s1 = base + pin * w + 16 + 4 * (out - 16);
+    s2 = base + (pin + 8) * w + 16 + 8 + 4 * (out - 16);
+    return;
+  }
   s1 = base + pin * w + out;
   s2 = base + (pin + 8) * w + out + (l3 ? 8 : 0);
 }
@@ -873,17 +912,18 @@ __device__ __forceinline__ void packed_fold_src(int s, int& s1, int& s2) {
 // loss, metrics and gradients are all masked to zero.
 template <int PACK, int DC, bool TP>
 __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP& F, char* scr, int c, int g,
-                                                  const f32x4 (&xf)[2][2], const int (&ix)[2], float pad1,
-                                                  f32x4 acc1[2], f32x4& acc2, f32x4& acc3, f32x4 acc4[2],
-                                                  float& sq, float& ab, float& corr, float& rows) {
-  static_assert(PACK == PACK_REF && DC > 16, "reference model, compile-time D");
+                                                  const f32x4 (&xf)[2][2], float xup, const int (&ix)[2],
+                                                  float pad1, f32x4 acc1[2], f32x4& acc2, f32x4& acc3,
+                                                  f32x4 acc4[2], float& sq, float& ab, float& corr, float& rows) {
+  // xup: the UP-layout copy of inputs 16 / 17 (lane group g: input 16 + (g & 1) of tile g >> 1)
+  static_assert(PACK == PACK_REF && DC == 18, "reference model, D = 18 (outputs 16, 17 packed as UP)");
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const bf16x4 zb = {0, 0, 0, 0};
   const bool pad_lane = (g == 3);
   const bool lo = c < 8;   // lanes holding tile 0's half of a packed operand (as n or m = c)
 
   bf16x4 xb0[2], xb1[2], h1b[2];
-  f32x4 h1[2], y[2][2];
+  f32x4 h1[2], y[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     f32x4 x1 = xf[u][1];
@@ -915,42 +955,41 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
 #pragma unroll
   for (int i = 0; i < 4; ++i) h3[i] = tanh_exp2(z3[i]);
   const bf16x4 h3b = pack4(h3);
-  f32x4 dz4[2][2];
+  // output layer: outputs 0..15 per tile, outputs 16 / 17 of BOTH tiles in one register (UP:
+  // lane group g = output 16 + (g & 1) of tile g >> 1; w4u's rows m = 4q, so only C entry 0 is used)
+  f32x4 dz4[2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < 2; ++u) {
+    const f32x4 z4 = mfma16(F.w4t[u], h3b, zero4);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const f32x4 z4 = mfma16(F.w4t[u][t], h3b, zero4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (t == 1 && !live_hi<DC>(i)) {
-          y[u][t][i] = 0.f;
-          dz4[u][t][i] = 0.f;
-          continue;
-        }
-        y[u][t][i] = relu_fast(z4[i]);
-        float e = y[u][t][i] - xf[u][t][i];
-        if (TP && u == 1) e = 0.f;
-        sq = fmaf(e, e, sq);
-        dz4[u][t][i] = y[u][t][i] > 0.f ? e : 0.f;   // relu'; x 2/D folded into F.w4b / the acc4 slab
-      }
+    for (int i = 0; i < 4; ++i) {
+      y[u][i] = relu_fast(z4[i]);
+      float e = y[u][i] - xf[u][0][i];
+      if (TP && u == 1) e = 0.f;
+      sq = fmaf(e, e, sq);
+      dz4[u][i] = y[u][i] > 0.f ? e : 0.f;   // relu'; x 2/D folded into F.w4b / the acc4 slab
     }
+  }
+  const f32x4 z4u = mfma16(F.w4u, h3b, zero4);
+  const float yup = relu_fast(z4u[0]);
+  float eup = yup - xup;
+  if (TP) eup = g < 2 ? eup : 0.f;
+  sq = fmaf(eup, eup, sq);
+  const float dz4up = yup > 0.f ? eup : 0.f;
   if (a.want_acc) {   // lane group 0 counts row c of tile 0, group 1 row c of tile 1
-    const int iy = row_argmax_nonneg_pair<DC>(y[0], y[1], a.D, g);
+    const int iy = row_argmax_up_pair(y[0], y[1], yup, g);
     const int sel = -(g & 1);   // bit-select: a ?: on the pair becomes a scratch array indexed by g
     const int ixs = (ix[0] & ~sel) | (ix[1] & sel);
     corr += ((TP ? g == 0 : g < 2) && iy == ixs) ? 1.f : 0.f;
   }
   rows += (g == 0) ? (TP ? 1.f : 2.f) : 0.f;
 
-  bf16x4 dz4b0[2], dz4b1[2], dz1b[2];
+  bf16x4 dz4b[2], dz1b[2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    dz4b0[u] = pack4(dz4[u][0]);
-    dz4b1[u] = pack4(dz4[u][1]);
-  }
-  f32x4 d3 = mfma32(F.w4b[0][0], F.w4b[0][1], dz4b0[0], dz4b1[0], zero4);
-  d3 = mfma32(F.w4b[1][0], F.w4b[1][1], dz4b0[1], dz4b1[1], d3);
+  for (int u = 0; u < 2; ++u) dz4b[u] = pack4(dz4[u]);
+  const bf16x4 dz4bu = pack4(f32x4{dz4up, 0.f, 0.f, 0.f});
+  f32x4 d3 = mfma32(F.w4b[0], F.w4b[1], dz4b[0], dz4b[1], zero4);   // K halves: tile 0 / tile 1 outputs 0..15
+  d3 = mfma32(F.w4bu, zb, dz4bu, zb, d3);                          // + outputs 16 / 17 (one shape per chain)
   f32x4 dz3, dz2;
 #pragma unroll
   for (int i = 0; i < 4; ++i) dz3[i] = d3[i] * fmaf(-h3[i], h3[i], 1.0f);   // 0 at the bias slots (h = 1)
@@ -977,16 +1016,16 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   }
 
   // weight gradients (rows on K through the LDS transpose)
-  bf16x4 xr0[2], xr1[2], dz1r[2], h1r[2], dz4r0[2], dz4r1[2];
+  bf16x4 xr0[2], xr1[2], dz1r[2], h1r[2], dz4r[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     xr0[u] = lds_transpose(xb0[u], scr + 0 * 512, c, g);
     xr1[u] = lds_transpose(xb1[u], scr + 1 * 512, c, g);
     dz1r[u] = lds_transpose(dz1b[u], scr + 2 * 512, c, g);
     h1r[u] = lds_transpose(h1b[u], scr + 3 * 512, c, g);
-    dz4r0[u] = lds_transpose(dz4b0[u], scr + 8 * 512, c, g);
-    dz4r1[u] = lds_transpose(dz4b1[u], scr + 9 * 512, c, g);
+    dz4r[u] = lds_transpose(dz4b[u], scr + 8 * 512, c, g);
   }
+  const bf16x4 dz4ru = lds_transpose(dz4bu, scr + 9 * 512, c, g);
   const bf16x4 dz2r = lds_transpose(dz2b, scr + 4 * 512, c, g);
   const bf16x4 h2r = lds_transpose(h2b, scr + 5 * 512, c, g);
   const bf16x4 dz3r = lds_transpose(dz3b, scr + 6 * 512, c, g);
@@ -996,8 +1035,10 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   acc2 = mfma32(h1r[0], h1r[1], lo ? dz2r : zb, lo ? zb : dz2r, acc2);   // n < 8: tile 0, n >= 8: tile 1
   acc3 = mfma16(h2r, dz3r, acc3);   // diagonal blocks; acc3's chain is 16x16x16 only in this variant
   const bf16x4 h3r0 = lo ? h3r : zb, h3r1 = lo ? zb : h3r;               // m < 8: tile 0, m >= 8: tile 1
-  acc4[0] = mfma32(h3r0, h3r1, dz4r0[0], dz4r0[1], acc4[0]);
-  acc4[1] = mfma32(h3r0, h3r1, dz4r1[0], dz4r1[1], acc4[1]);
+  acc4[0] = mfma32(h3r0, h3r1, dz4r[0], dz4r[1], acc4[0]);
+  // outputs 16 / 17: UP columns 4q pair with their own tile's rows m by construction (the
+  // other tile's blocks are never folded), so h3r needs no mask; acc4[1]'s chain is 16x16x16
+  acc4[1] = mfma16(h3r, dz4ru, acc4[1]);
 }
 
 // 3 waves/SIMD: caps the allocation at 168 VGPRs (no spills); 171 would drop to 2.
@@ -1109,6 +1150,12 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) xf[1][j] = (live_hi<DC>(j) && 16 + 4 * g + j < DC) ? xf[1][j] : 0.f;
         };
+        // packed pairs' UP copy of inputs 16 / 17: lane group g reads input 16 + (g & 1) of row c
+        // of the tile in `slot` (the caller passes tile g >> 1's slot)
+        auto ring_up = [&](int slot) -> float {
+          typedef __attribute__((address_space(3))) const float lds_f;
+          return *(lds_f*)(ring + slot * slotb + c * 4 * a.D + 4 * (16 + (g & 1)));
+        };
         int64_t tp = t0;
 #pragma unroll
         for (int k = 0; k < PF - 2; ++k) {
@@ -1124,13 +1171,16 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV * (PF - 2)) : "memory");
           f32x4 xf[2][2];
           int ix[2];
+          const int rd1 = rd + 1 == PF ? 0 : rd + 1;
           ring_tile(rd, xf[0], ix[0]);
-          ring_tile(rd + 1 == PF ? 0 : rd + 1, xf[1], ix[1]);
+          ring_tile(rd1, xf[1], ix[1]);
+          float xup = 0.f;
+          if constexpr (ILP == 3) xup = ring_up(g < 2 ? rd : rd1);
           rd = rd + 2 >= PF ? rd + 2 - PF : rd + 2;
           wr = wr + 2 >= PF ? wr + 2 - PF : wr + 2;
           if constexpr (ILP == 3)
-            train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr,
-                                               rows);
+            train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, xup, ix, pad1, acc1, acc2, acc3, acc4, sq, ab,
+                                               corr, rows);
           else
             train_tiles_ilp<PACK, DC, 2>(a, F, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
         }
@@ -1143,8 +1193,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
             xf[1][0] = xf[0][0];
             xf[1][1] = xf[0][1];
             ix[1] = ix[0];
-            train_pair_packed<PACK, DC, true>(a, FP, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr,
-                                              rows);
+            const float xup = ring_up(rd);
+            train_pair_packed<PACK, DC, true>(a, FP, scr, c, g, xf, xup, ix, pad1, acc1, acc2, acc3, acc4, sq, ab,
+                                              corr, rows);
           } else {
             f32x4 xf[1][2];
             int ix[1];
