@@ -213,15 +213,17 @@ def _bench_fit_module():
 
 def measure_fit(device, rows, batch=100, seed=0):
     """The reference's own job on the real entry point: Autoencoder.fit(batch_size=100)
-    (cardata-v3.py:176-177, 212-222) on an array -- every Keras step on the persistent kernel."""
-    return _bench_fit_module().fit_array(device, rows=rows, batch=batch, seed=seed)
+    (cardata-v3.py:176-177, 212-222) on an array -- every Keras step on the persistent kernel.
+    Rank 0 alone (dp="none": no collective while the other ranks have moved on)."""
+    return _bench_fit_module().fit_array(device, rows=rows, batch=batch, seed=seed, dp="none")
 
 
 def measure_stream_e2e(device, rows, batch=100):
     """In-process Kafka (16 partitions of Confluent Avro) -> native C++ feed (decode-time
     label filter, pinned slabs, H2D in flight) -> fit(batch_size=100): events/s end to end,
     with the rate of each stage alone."""
-    return _bench_fit_module().stream_e2e(device, rows=rows, batch=batch, partitions=16, workers=8, native=True)
+    return _bench_fit_module().stream_e2e(device, rows=rows, batch=batch, partitions=16, workers=8, native=True,
+                                          dp="none")   # rank 0 alone, as measure_fit
 
 
 def measure_batch32_fleet(spec, data, device, steps, scale, shift, n_models=1024, launches=3):

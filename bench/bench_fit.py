@@ -25,7 +25,8 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def fit_array(device, rows: int = 2_000_000, batch: int = 100, engine: str = "auto", seed: int = 0) -> dict:
+def fit_array(device, rows: int = 2_000_000, batch: int = 100, engine: str = "auto", seed: int = 0,
+              dp: str = "auto") -> dict:
     import numpy as np
     import torch
 
@@ -36,10 +37,10 @@ def fit_array(device, rows: int = 2_000_000, batch: int = 100, engine: str = "au
     m = Autoencoder(device=device, input_normalizer="cardata", seed=seed)
     m.compile()
     x = torch.as_tensor(np.ascontiguousarray(raw, np.float32), device=device)
-    m.fit(x[:batch * 200], epochs=1, batch_size=batch, verbose=0, engine=engine)   # warm-up
+    m.fit(x[:batch * 200], epochs=1, batch_size=batch, verbose=0, engine=engine, dp=dp)   # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    h = m.fit(x, epochs=1, batch_size=batch, verbose=0, engine=engine)
+    h = m.fit(x, epochs=1, batch_size=batch, verbose=0, engine=engine, dp=dp)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     steps = -(-rows // batch)
@@ -48,7 +49,7 @@ def fit_array(device, rows: int = 2_000_000, batch: int = 100, engine: str = "au
 
 
 def stream_e2e(device, rows: int = 2_000_000, batch: int = 100, partitions: int = 8, workers: int = 8,
-               fetch_bytes: int = 4 << 20, failure_rate: float = 0.01, native: bool = True) -> dict:
+               fetch_bytes: int = 4 << 20, failure_rate: float = 0.01, native: bool = True, dp: str = "auto") -> dict:
     import torch
 
     from streamml.data import stream as S
@@ -93,12 +94,12 @@ def stream_e2e(device, rows: int = 2_000_000, batch: int = 100, partitions: int 
         out["per_worker_fetch_rows_per_s"] = st["records"] / max(st["fetch_s"] / w, 1e-9) / w
         out["per_worker_decode_rows_per_s"] = st["records"] / max(st["decode_s"] / w, 1e-9) / w
     # stage 3: the training kernel alone on the same number of rows (device resident)
-    out["train_only"] = fit_array(device, rows=max(kept, batch * 300), batch=batch)
+    out["train_only"] = fit_array(device, rows=max(kept, batch * 300), batch=batch, dp=dp)
     # end to end
-    m.fit(training, epochs=1, batch_size=batch, verbose=0, steps_per_epoch=50)   # warm-up
+    m.fit(training, epochs=1, batch_size=batch, verbose=0, steps_per_epoch=50, dp=dp)   # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    h = m.fit(training, epochs=1, batch_size=batch, verbose=0)
+    h = m.fit(training, epochs=1, batch_size=batch, verbose=0, dp=dp)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out.update({"rows_per_s": n / dt, "kept_rows": kept, "trained_rows_per_s": kept / dt,

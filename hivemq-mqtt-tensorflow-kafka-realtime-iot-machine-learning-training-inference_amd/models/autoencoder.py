@@ -178,7 +178,9 @@ class Autoencoder:
         * ``"local_sgd:K"`` -- documented semantics change: K
           independent persistent-kernel steps per rank, then the parameters are averaged;
         * ``"auto"`` -- ``p2p`` when the persistent kernel applies and the IPC exchange can
-          be set up on every rank, else ``rccl``.
+          be set up on every rank, else ``rccl``;
+        * ``"none"`` -- this process trains alone on all of ``x`` even inside a process group
+          (no collective is called: e.g. a measurement on one rank while the others idle).
         """
         from ..data.stream import Stream
         from ..parallel.dp import allreduce_sum_
@@ -187,7 +189,7 @@ class Autoencoder:
             self.compile()
         if y is not None and y is not x:
             raise ValueError("autoencoder fit expects y == x (or y=None)")
-        rank, world = self._dist()
+        rank, world = (0, 1) if dp == "none" else self._dist()
         allreduce = allreduce_sum_ if world > 1 else None
         hist = History()
         cbs = [hist] + list(callbacks or [])
@@ -317,8 +319,8 @@ class Autoencoder:
     def _use_persistent(self, engine: str, batch_size: int, world: int, dp: str = "auto") -> bool:
         if engine not in ("auto", "persistent", "launch"):
             raise ValueError(f"engine must be auto / persistent / launch, got {engine!r}")
-        if not (dp in ("auto", "p2p", "rccl") or dp.startswith("local_sgd:")):
-            raise ValueError(f"dp must be auto / p2p / rccl / local_sgd:K, got {dp!r}")
+        if not (dp in ("auto", "p2p", "rccl", "none") or dp.startswith("local_sgd:")):
+            raise ValueError(f"dp must be auto / p2p / rccl / local_sgd:K / none, got {dp!r}")
         if engine == "launch" or self.device.type != "cuda":
             if engine == "persistent" and self.device.type != "cuda":
                 raise ValueError("engine='persistent' needs a ROCm device")

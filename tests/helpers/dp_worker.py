@@ -35,6 +35,12 @@ def main(out_dir: str) -> None:
     mlp = MLPClassifier(hidden=32, device="cpu", seed=5)
     mlp.fit(xi, yi, epochs=1, batch_size=16, shuffle=False, verbose=0)
     np.savez(os.path.join(out_dir, f"mlp_{rank}.npz"), *mlp.fp.get())
+    # --- a one-rank measurement inside the group (bench.py's fit side fields): rank 0 fits
+    # alone with dp="none" while rank 1 has already left -- no collective may be called
+    if rank == 0:
+        solo = Autoencoder(device="cpu", seed=4)
+        hs = solo.fit(x, epochs=1, batch_size=32, shuffle=False, verbose=0, dp="none")
+        np.savez(os.path.join(out_dir, "ae_solo.npz"), *solo.get_weights(), loss=np.array(hs.history["loss"]))
     shutdown()
 
 

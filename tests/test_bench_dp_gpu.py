@@ -44,6 +44,11 @@ def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
     coll = out["small_allreduce"]
     assert coll["bucket_bytes"] == 6144 and coll["backend_allreduce_us"] > 0 and coll["p2p_allreduce_us"] > 0, coll
     assert out["keras_batch32_dp"]["replicas_identical"] is True, out["keras_batch32_dp"]
+    # rank 0's single-replica side measurements must not call a collective (dp="none"): the
+    # other rank has already shut its process group down
+    for k in ("fit_batch100", "stream_e2e"):
+        assert out[k] and "error" not in out[k], out[k]
+        assert out[k]["engine"] == "persistent", out[k]
     p0 = np.load(dump + ".rank0.npy")
     p1 = np.load(dump + ".rank1.npy")
     np.testing.assert_array_equal(p0, p1)

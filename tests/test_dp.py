@@ -64,3 +64,17 @@ def test_ae_dp_equals_single_process(dp_run):
     for u, v in zip(w, ae.get_weights()):
         np.testing.assert_allclose(u, v, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(z["loss"], h.history["loss"], rtol=1e-5)
+
+
+@pytest.mark.dist
+def test_fit_dp_none_is_single_replica_inside_a_group(dp_run):
+    """fit(dp="none") on rank 0 alone (its peer already shut down) trains on all of x like a
+    process with no group: bench.py's rank-0 side measurements at N > 1 rely on it."""
+    from streamml.models.autoencoder import Autoencoder
+    x = np.random.default_rng(0).uniform(-1, 1, size=(256, 18)).astype(np.float32)
+    ae = Autoencoder(device="cpu", seed=4)
+    h = ae.fit(x, epochs=1, batch_size=32, shuffle=False, verbose=0)
+    w, z = _load(dp_run / "ae_solo.npz")
+    for u, v in zip(w, ae.get_weights()):   # CPU torch thread counts differ: summation order only
+        np.testing.assert_allclose(u, v, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(z["loss"], h.history["loss"], rtol=1e-5)
