@@ -791,7 +791,8 @@ __device__ __forceinline__ void train_tiles_ilp(const AEArgs& a, const Frags& F,
 //   The accumulators hold both tiles' halves side by side and are folded into the parameter
 //   image once per launch (packed_fold_src).  Needs n2, n3 <= 7.
 struct FragsP {
-  bf16x4 w1t[2];      // L1 forward (as Frags: prescaled, bias slot 15 injected)
+  bf16x4 w1t;         // L1 forward from inputs 0..15 (prescaled)
+  bf16x4 w1u[2];      // L1 forward [tile] from the UP inputs 16 / 17 and the constant-1 bias input
   bf16x4 w2t[2];      // L2 forward, K halves = tile 0 / tile 1 inputs
   bf16x4 w3t;         // L3 forward, block-diagonal (prescaled, packed bias slots injected)
   bf16x4 w4t[2];      // L4 forward, outputs 0..15 [tile]
@@ -810,11 +811,16 @@ __device__ __forceinline__ void load_frags_packed(const AEArgs& a, int c, int g,
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int k = 4 * g + j;
+    F.w1t[j] = bfbits(k1 * ldsel(P, k < a.D && c < a.n1, OFF1 + k * 16 + c));
+    // L1 from UP: B row k = 4q (j = 0) is input 16 + (q & 1) of tile q >> 1, k = 1 (g = 0, j = 1)
+    // the constant 1 of the bias; bias slot 15's output is injected there (tanh_exp2(256) = 1)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int in = 16 * s + k;
-      const bool row_ok = in < a.D || in == 31;
-      F.w1t[s][j] = bfbits(k1 * ldsel(P, row_ok && c < a.n1, OFF1 + in * 16 + c));
+    for (int u = 0; u < 2; ++u) {
+      const int in = 16 + (g & 1);
+      float v = 0.f;
+      if (j == 0 && (g >> 1) == u) v = k1 * ldsel(P, in < a.D && c < a.n1, OFF1 + in * 16 + c);
+      if (j == 1 && g == 0) v = c == 15 ? 256.0f : k1 * ldsel(P, c < a.n1, OFF1 + 31 * 16 + c);
+      F.w1u[u][j] = bfbits(v);
     }
     // L2 forward: A[m = packed out c][k = in (of tile h)]
     const int o2 = c & 7;
@@ -873,14 +879,25 @@ __device__ __forceinline__ void load_frags_packed(const AEArgs& a, int c, int g,
       F.w2b[u][j] = bfbits(ldsel(P, ok, OFF2 + c * 16 + o));
     }
   }
-  if (c == 15 && g == 3) F.w1t[1][3] = bfbits(256.0f);   // L1 bias slot 15 (as load_frags INJ)
 }
 
 // Image slot s -> the packed-accumulator slab slots whose sum it is (-1: none, gradient 0).
 __device__ __forceinline__ void packed_fold_src(int s, int& s1, int& s2) {
   s1 = s;
   s2 = -1;
-  if (s < OFF2 || s >= NPARAM) return;   // layer 1 and the metric sums are not packed
+  if (s >= OFF1 + 16 * 16 && s < OFF2) {   // layer-1 rows 16..31: UP rows 16 + m of the slab
+    const int in = (s - OFF1) >> 4, out = (s - OFF1) & 15;
+    if (in == 16 || in == 17) {
+      s1 = OFF1 + (16 + 4 * (in - 16)) * 16 + out;        // tile 0: m = 4q
+      s2 = OFF1 + (16 + 8 + 4 * (in - 16)) * 16 + out;    // tile 1: m = 8 + 4q
+    } else if (in == 31) {
+      s1 = OFF1 + (16 + 1) * 16 + out;                     // the bias input, m = 1 (both tiles)
+    } else {
+      s1 = -1;
+    }
+    return;
+  }
+  if (s < OFF2 || s >= NPARAM) return;   // layer-1 rows 0..15 and the metric sums are not packed
   if (s < OFF3) {
     const int in = (s - OFF2) >> 4, out = (s - OFF2) & 15;
     if (out < 7) s2 = s + 8;
@@ -922,18 +939,17 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   const bool pad_lane = (g == 3);
   const bool lo = c < 8;   // lanes holding tile 0's half of a packed operand (as n or m = c)
 
-  bf16x4 xb0[2], xb1[2], h1b[2];
+  bf16x4 xb0[2], h1b[2];
   f32x4 h1[2], y[2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    f32x4 x1 = xf[u][1];
-    x1[3] += pad1;
-    xb0[u] = pack4(xf[u][0]);
-    xb1[u] = pack4(x1);
-  }
+  for (int u = 0; u < 2; ++u) xb0[u] = pack4(xf[u][0]);
+  // inputs 16 / 17 of both tiles (UP) and the constant-1 bias input (k = 1, lane group 0) in
+  // one B operand; layer 1 is one 16x16x32 per tile: [inputs 0..15 | UP + bias]
+  (void)pad1;
+  const bf16x4 xub = pack4(f32x4{xup, g == 0 ? 1.0f : 0.0f, 0.f, 0.f});
   f32x4 z1[2], l1s[2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) z1[u] = mfma32(F.w1t[0], F.w1t[1], xb0[u], xb1[u], zero4);
+  for (int u = 0; u < 2; ++u) z1[u] = mfma32(F.w1t, F.w1u[u], xb0[u], xub, zero4);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -1016,11 +1032,11 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   }
 
   // weight gradients (rows on K through the LDS transpose)
-  bf16x4 xr0[2], xr1[2], dz1r[2], h1r[2], dz4r[2];
+  bf16x4 xr0[2], dz1r[2], h1r[2], dz4r[2];
+  const bf16x4 xur = lds_transpose(xub, scr + 1 * 512, c, g);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     xr0[u] = lds_transpose(xb0[u], scr + 0 * 512, c, g);
-    xr1[u] = lds_transpose(xb1[u], scr + 1 * 512, c, g);
     dz1r[u] = lds_transpose(dz1b[u], scr + 2 * 512, c, g);
     h1r[u] = lds_transpose(h1b[u], scr + 3 * 512, c, g);
     dz4r[u] = lds_transpose(dz4b[u], scr + 8 * 512, c, g);
@@ -1031,7 +1047,8 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   const bf16x4 dz3r = lds_transpose(dz3b, scr + 6 * 512, c, g);
   const bf16x4 h3r = lds_transpose(h3b, scr + 7 * 512, c, g);
   acc1[0] = mfma32(xr0[0], xr0[1], dz1r[0], dz1r[1], acc1[0]);
-  acc1[1] = mfma32(xr1[0], xr1[1], dz1r[0], dz1r[1], acc1[1]);
+  // rows 16 + m: m = 0 / 4 tile 0's inputs 16 / 17, m = 8 / 12 tile 1's, m = 1 the bias (both)
+  acc1[1] = mfma32(lo ? xur : zb, (!lo || c == 1) ? xur : zb, dz1r[0], dz1r[1], acc1[1]);
   acc2 = mfma32(h1r[0], h1r[1], lo ? dz2r : zb, lo ? zb : dz2r, acc2);   // n < 8: tile 0, n >= 8: tile 1
   acc3 = mfma16(h2r, dz3r, acc3);   // diagonal blocks; acc3's chain is 16x16x16 only in this variant
   const bf16x4 h3r0 = lo ? h3r : zb, h3r1 = lo ? zb : h3r;               // m < 8: tile 0, m >= 8: tile 1
@@ -1145,8 +1162,16 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
         static_assert(XM == 1 && CH == 1 && PF >= 3, "tile pairs: tile-packed ring, plain order");
         auto ring_tile = [&](int slot, f32x4 xf[2], int& ix) {
           typedef __attribute__((address_space(3))) const unsigned char lds_u8;
-          ring_x(a, ring + slot * slotb, c, g, xf);
           ix = (int)*(lds_u8*)(ring + slot * slotb + 64 * a.D + c);
+          if constexpr (ILP == 3) {   // inputs 0..15 only (16 / 17 come as UP, ring_up)
+            typedef __attribute__((address_space(3))) const f32x2_t lds_f2;
+            const char* row = ring + slot * slotb + c * 4 * a.D + 16 * g;
+            const f32x2_t v0 = *(lds_f2*)row, v1 = *(lds_f2*)(row + 8);
+            xf[0] = f32x4{v0[0], v0[1], v1[0], v1[1]};
+            xf[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            return;
+          }
+          ring_x(a, ring + slot * slotb, c, g, xf);
 #pragma unroll
           for (int j = 0; j < 4; ++j) xf[1][j] = (live_hi<DC>(j) && 16 + 4 * g + j < DC) ? xf[1][j] : 0.f;
         };
