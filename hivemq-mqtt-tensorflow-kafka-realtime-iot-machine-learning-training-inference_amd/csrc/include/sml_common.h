@@ -59,6 +59,17 @@ __device__ __forceinline__ f32x4 mfma32(bf16x4 a0, bf16x4 a1, bf16x4 b0, bf16x4 
                                                  0, 0);
 }
 
+// The same with the A operand already concatenated (static fragments kept as one 8-short
+// vector: no register copies to make the two K halves adjacent at every use).
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ s16x8 cat8(bf16x4 a0, bf16x4 a1) { return __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7); }
+__device__ __forceinline__ f32x4 mfma32a(s16x8 a, bf16x4 b0, bf16x4 b1, f32x4 c) {
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 b = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+
 __device__ __forceinline__ unsigned pack2(float lo, float hi) {
   f32x2_t v = {lo, hi};
   bf16x2_t b = __builtin_convertvector(v, bf16x2_t);

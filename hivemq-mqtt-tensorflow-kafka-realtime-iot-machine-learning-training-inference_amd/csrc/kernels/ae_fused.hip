@@ -801,6 +801,9 @@ struct FragsP {
   bf16x4 w4bu;        // L4 backward from the packed outputs 16, 17 (x 2/D)
   bf16x4 w3b;         // L3 backward, block-diagonal
   bf16x4 w2b[2];      // L2 backward [tile]
+  // the 16x16x32 A operands, concatenated once per launch: tile 1's layer 1 takes its K halves
+  // in the order [UP | inputs 0..15] so the shared UP B operand can sit between the tiles' own
+  s16x8 w1a[2], w2a, w4ba, w4bua;
 };
 
 __device__ __forceinline__ int img_row_of_packed(int i) { return i == 7 ? 15 : i; }   // i = packed % 8
@@ -879,6 +882,12 @@ __device__ __forceinline__ void load_frags_packed(const AEArgs& a, int c, int g,
       F.w2b[u][j] = bfbits(ldsel(P, ok, OFF2 + c * 16 + o));
     }
   }
+  const bf16x4 zb = {0, 0, 0, 0};
+  F.w1a[0] = cat8(F.w1t, F.w1u[0]);
+  F.w1a[1] = cat8(F.w1u[1], F.w1t);
+  F.w2a = cat8(F.w2t[0], F.w2t[1]);
+  F.w4ba = cat8(F.w4b[0], F.w4b[1]);
+  F.w4bua = cat8(F.w4bu, zb);
 }
 
 // Image slot s -> the packed-accumulator slab slots whose sum it is (-1: none, gradient 0).
@@ -948,8 +957,8 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   (void)pad1;
   const bf16x4 xub = pack4(f32x4{xup, g == 0 ? 1.0f : 0.0f, 0.f, 0.f});
   f32x4 z1[2], l1s[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) z1[u] = mfma32(F.w1t, F.w1u[u], xb0[u], xub, zero4);
+  z1[0] = mfma32a(F.w1a[0], xb0[0], xub, zero4);
+  z1[1] = mfma32a(F.w1a[1], xub, xb0[1], zero4);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -962,7 +971,7 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int i = 0; i < 4; ++i) l1s[u][i] = (TP && u == 1) ? 0.f : __builtin_amdgcn_fmed3f(h1[u][i], -a.l1, a.l1);
-  const f32x4 z2 = mfma32(F.w2t[0], F.w2t[1], h1b[0], h1b[1], zero4);
+  const f32x4 z2 = mfma32a(F.w2a, h1b[0], h1b[1], zero4);
   f32x4 h2, h3;
 #pragma unroll
   for (int i = 0; i < 4; ++i) h2[i] = relu_fast(z2[i]);
@@ -1004,8 +1013,8 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
 #pragma unroll
   for (int u = 0; u < 2; ++u) dz4b[u] = pack4(dz4[u]);
   const bf16x4 dz4bu = pack4(f32x4{dz4up, 0.f, 0.f, 0.f});
-  f32x4 d3 = mfma32(F.w4b[0], F.w4b[1], dz4b[0], dz4b[1], zero4);   // K halves: tile 0 / tile 1 outputs 0..15
-  d3 = mfma32(F.w4bu, zb, dz4bu, zb, d3);                          // + outputs 16 / 17 (one shape per chain)
+  f32x4 d3 = mfma32a(F.w4ba, dz4b[0], dz4b[1], zero4);   // K halves: tile 0 / tile 1 outputs 0..15
+  d3 = mfma32a(F.w4bua, dz4bu, zb, d3);                  // + outputs 16 / 17 (one shape per chain)
   f32x4 dz3, dz2;
 #pragma unroll
   for (int i = 0; i < 4; ++i) dz3[i] = d3[i] * fmaf(-h3[i], h3[i], 1.0f);   // 0 at the bias slots (h = 1)
@@ -1122,7 +1131,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
     // LDS-DMA ring: tile first + k*stride lives in slot k % PF.  Every issue is
     // exactly two VMEM instructions (tiles past the end are clamped to the last
     // full tile, never skipped), so "tile k landed" is vmcnt(2 * (PF - 1)).
-    const int slotb = 64 * a.D + (XM == 1 ? 16 : 0);
+    const int slotb = 64 * (DC > 0 ? DC : a.D) + (XM == 1 ? 16 : 0);   // compile-time with DC: immediate offsets
     constexpr int NV = 2;  // VMEM instructions per tile issue
     const int nl2 = (slotb - 1024) >> 4;  // lanes of the second 16-B-per-lane DMA (>= 4)
     const int uwid = __builtin_amdgcn_readfirstlane(wid);  // keep the ring bookkeeping scalar
@@ -1177,9 +1186,13 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
         };
         // packed pairs' UP copy of inputs 16 / 17: lane group g reads input 16 + (g & 1) of row c
         // of the tile in `slot` (the caller passes tile g >> 1's slot)
-        auto ring_up = [&](int slot) -> float {
+        // tile 1 of a pair sits in the next slot (pairs start on even slots, PF even), so one
+        // loop-invariant lane offset covers both tiles
+        static_assert(ILP != 3 || PF % 2 == 0, "pairs start on even ring slots");
+        const int up_off = c * 4 * DC + 4 * (16 + (g & 1)) + (g >= 2 ? slotb : 0);
+        auto ring_up = [&](int slot, bool same) -> float {
           typedef __attribute__((address_space(3))) const float lds_f;
-          return *(lds_f*)(ring + slot * slotb + c * 4 * a.D + 4 * (16 + (g & 1)));
+          return *(lds_f*)(ring + slot * slotb + (same ? up_off - (g >= 2 ? slotb : 0) : up_off));
         };
         int64_t tp = t0;
 #pragma unroll
@@ -1196,11 +1209,11 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV * (PF - 2)) : "memory");
           f32x4 xf[2][2];
           int ix[2];
-          const int rd1 = rd + 1 == PF ? 0 : rd + 1;
+          const int rd1 = ILP == 3 ? rd + 1 : (rd + 1 == PF ? 0 : rd + 1);
           ring_tile(rd, xf[0], ix[0]);
           ring_tile(rd1, xf[1], ix[1]);
           float xup = 0.f;
-          if constexpr (ILP == 3) xup = ring_up(g < 2 ? rd : rd1);
+          if constexpr (ILP == 3) xup = ring_up(rd, false);
           rd = rd + 2 >= PF ? rd + 2 - PF : rd + 2;
           wr = wr + 2 >= PF ? wr + 2 - PF : wr + 2;
           if constexpr (ILP == 3)
@@ -1218,7 +1231,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
             xf[1][0] = xf[0][0];
             xf[1][1] = xf[0][1];
             ix[1] = ix[0];
-            const float xup = ring_up(rd);
+            const float xup = ring_up(rd, true);
             train_pair_packed<PACK, DC, true>(a, FP, scr, c, g, xf, xup, ix, pad1, acc1, acc2, acc3, acc4, sq, ab,
                                               corr, rows);
           } else {
