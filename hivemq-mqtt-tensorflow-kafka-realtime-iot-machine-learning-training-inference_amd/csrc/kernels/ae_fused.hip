@@ -940,7 +940,8 @@ template <int PACK, int DC, bool TP>
 __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP& F, char* scr, int c, int g,
                                                   const f32x4 (&xf)[2][2], float xup, const int (&ix)[2],
                                                   float pad1, f32x4 acc1[2], f32x4& acc2, f32x4& acc3,
-                                                  f32x4 acc4[2], float& sq, float& ab, float& corr, float& rows) {
+                                                  f32x4 acc4[2], f32x4& acc2b, f32x4& acc4b, float& sq, float& ab,
+                                                  float& corr, float& rows) {
   // xup: the UP-layout copy of inputs 16 / 17 (lane group g: input 16 + (g & 1) of tile g >> 1)
   static_assert(PACK == PACK_REF && DC == 18, "reference model, D = 18 (outputs 16, 17 packed as UP)");
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
@@ -1058,10 +1059,14 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   acc1[0] = mfma32(xr0[0], xr0[1], dz1r[0], dz1r[1], acc1[0]);
   // rows 16 + m: m = 0 / 4 tile 0's inputs 16 / 17, m = 8 / 12 tile 1's, m = 1 the bias (both)
   acc1[1] = mfma32(lo ? xur : zb, (!lo || c == 1) ? xur : zb, dz1r[0], dz1r[1], acc1[1]);
-  acc2 = mfma32(h1r[0], h1r[1], lo ? dz2r : zb, lo ? zb : dz2r, acc2);   // n < 8: tile 0, n >= 8: tile 1
+  // dW2 / dW4 (outputs 0..15): each tile against the whole packed operand, in an accumulator
+  // of its own (only its half -- n < 8 / m < 8 for tile 0 -- is kept when the slab is written):
+  // two 16x16x16 instead of a 16x16x32 on lane-masked copies (no per-pair selects)
+  acc2 = mfma16(h1r[0], dz2r, acc2);
+  acc2b = mfma16(h1r[1], dz2r, acc2b);
   acc3 = mfma16(h2r, dz3r, acc3);   // diagonal blocks; acc3's chain is 16x16x16 only in this variant
-  const bf16x4 h3r0 = lo ? h3r : zb, h3r1 = lo ? zb : h3r;               // m < 8: tile 0, m >= 8: tile 1
-  acc4[0] = mfma32(h3r0, h3r1, dz4r[0], dz4r[1], acc4[0]);
+  acc4[0] = mfma16(h3r, dz4r[0], acc4[0]);
+  acc4b = mfma16(h3r, dz4r[1], acc4b);
   // outputs 16 / 17: UP columns 4q pair with their own tile's rows m by construction (the
   // other tile's blocks are never folded), so h3r needs no mask; acc4[1]'s chain is 16x16x16
   acc4[1] = mfma16(h3r, dz4ru, acc4[1]);
@@ -1119,9 +1124,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   const float pad1 = (g == 3) ? 1.0f : 0.0f;
   __syncthreads();  // normaliser visible (before any LDS-DMA is in flight)
 
-  f32x4 acc1[2], acc2, acc3, acc4[2];
+  f32x4 acc1[2], acc2, acc3, acc4[2], acc2b, acc4b;   // acc2b / acc4b: packed pairs' tile-1 halves
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  acc1[0] = acc1[1] = acc2 = acc3 = acc4[0] = acc4[1] = zero4;
+  acc1[0] = acc1[1] = acc2 = acc3 = acc4[0] = acc4[1] = acc2b = acc4b = zero4;
   float sq = 0.f, ab = 0.f, corr = 0.f, rows = 0.f;
 
   const int64_t nfull = a.n >> 4;
@@ -1217,8 +1222,8 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
           rd = rd + 2 >= PF ? rd + 2 - PF : rd + 2;
           wr = wr + 2 >= PF ? wr + 2 - PF : wr + 2;
           if constexpr (ILP == 3)
-            train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, xup, ix, pad1, acc1, acc2, acc3, acc4, sq, ab,
-                                               corr, rows);
+            train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, xup, ix, pad1, acc1, acc2, acc3, acc4, acc2b,
+                                               acc4b, sq, ab, corr, rows);
           else
             train_tiles_ilp<PACK, DC, 2>(a, F, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
         }
@@ -1232,8 +1237,8 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
             xf[1][1] = xf[0][1];
             ix[1] = ix[0];
             const float xup = ring_up(rd, true);
-            train_pair_packed<PACK, DC, true>(a, FP, scr, c, g, xf, xup, ix, pad1, acc1, acc2, acc3, acc4, sq, ab,
-                                              corr, rows);
+            train_pair_packed<PACK, DC, true>(a, FP, scr, c, g, xf, xup, ix, pad1, acc1, acc2, acc3, acc4, acc2b,
+                                              acc4b, sq, ab, corr, rows);
           } else {
             f32x4 xf[1][2];
             int ix[1];
@@ -1317,6 +1322,10 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   // per-wave slab in LDS (every slot written exactly once per wave)
   __syncthreads();  // all waves done with their transpose scratch
   float* my = smem + wid * NSLOT;
+  if constexpr (ILP == 3) {   // tile 1's halves: dW2 columns n >= 8, dW4 rows m >= 8 (lane groups 2, 3)
+    acc2 = c < 8 ? acc2 : acc2b;
+    acc4[0] = g < 2 ? acc4[0] : acc4b;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = 4 * g + i;
