@@ -939,7 +939,7 @@ __device__ __forceinline__ void packed_fold_src(int s, int& s1, int& s2) {
 template <int PACK, int DC, bool TP>
 __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP& F, char* scr, int c, int g,
                                                   const f32x4 (&xf)[2][2], float xup, const int (&ix)[2],
-                                                  float pad1, f32x4 acc1[2], f32x4& acc2, f32x4& acc3,
+                                                  f32x4 acc1[2], f32x4& acc2, f32x4& acc3,
                                                   f32x4 acc4[2], f32x4& acc2b, f32x4& acc4b, float& sq, float& ab,
                                                   float& corr, float& rows) {
   // xup: the UP-layout copy of inputs 16 / 17 (lane group g: input 16 + (g & 1) of tile g >> 1)
@@ -955,7 +955,6 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   for (int u = 0; u < 2; ++u) xb0[u] = pack4(xf[u][0]);
   // inputs 16 / 17 of both tiles (UP) and the constant-1 bias input (k = 1, lane group 0) in
   // one B operand; layer 1 is one 16x16x32 per tile: [inputs 0..15 | UP + bias]
-  (void)pad1;
   const bf16x4 xub = pack4(f32x4{xup, g == 0 ? 1.0f : 0.0f, 0.f, 0.f});
   f32x4 z1[2], l1s[2];
   z1[0] = mfma32a(F.w1a[0], xb0[0], xub, zero4);
@@ -1222,7 +1221,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
           rd = rd + 2 >= PF ? rd + 2 - PF : rd + 2;
           wr = wr + 2 >= PF ? wr + 2 - PF : wr + 2;
           if constexpr (ILP == 3)
-            train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, xup, ix, pad1, acc1, acc2, acc3, acc4, acc2b,
+            train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3, acc4, acc2b,
                                                acc4b, sq, ab, corr, rows);
           else
             train_tiles_ilp<PACK, DC, 2>(a, F, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
@@ -1237,7 +1236,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
             xf[1][1] = xf[0][1];
             ix[1] = ix[0];
             const float xup = ring_up(rd, true);
-            train_pair_packed<PACK, DC, true>(a, FP, scr, c, g, xf, xup, ix, pad1, acc1, acc2, acc3, acc4, acc2b,
+            train_pair_packed<PACK, DC, true>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3, acc4, acc2b,
                                               acc4b, sq, ab, corr, rows);
           } else {
             f32x4 xf[1][2];
