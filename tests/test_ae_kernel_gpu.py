@@ -288,12 +288,14 @@ def test_tile_pair_loop_matches_one_tile_loop(cuda_device, monkeypatch, ntiles, 
     if ilp == "2":
         np.testing.assert_array_equal(one[0][NPARAM:], two[0][NPARAM:])   # sq, |h1|, correct, rows
     else:
-        np.testing.assert_allclose(two[0][NPARAM:NPARAM + 2], one[0][NPARAM:NPARAM + 2], rtol=1e-5)
+        np.testing.assert_allclose(two[0][NPARAM:NPARAM + 2], one[0][NPARAM:NPARAM + 2], rtol=1e-6)
         assert abs(two[0][NPARAM + 2] - one[0][NPARAM + 2]) <= max(2, 1e-3 * B)   # argmax near-ties
         assert two[0][NPARAM + 3] == one[0][NPARAM + 3]
     assert one[0][NPARAM + 3] == B
-    assert _relerr(two[0][:NPARAM], one[0][:NPARAM]) < (1e-5 if ilp == "2" else 1e-3)
+    # measured: ~5e-8 for ILP 3 (tools/ilp_err_probe.py) -- a fold that dropped or misplaced any
+    # accumulator entry would be off by orders of magnitude more
+    assert _relerr(two[0][:NPARAM], one[0][:NPARAM]) < 1e-6
     for a, b in zip(one[1:], two[1:]):
-        assert _relerr(b[:NPARAM], a[:NPARAM]) < (1e-4 if ilp == "2" else 2e-3)
+        assert _relerr(b[:NPARAM], a[:NPARAM]) < 1e-4
         assert abs(a[NPARAM] - b[NPARAM]) <= 1e-4 * abs(a[NPARAM])
-    assert _relerr(out[ilp][1], out["1"][1]) < (1e-4 if ilp == "2" else 1e-3)
+    assert _relerr(out[ilp][1], out["1"][1]) < 1e-4
