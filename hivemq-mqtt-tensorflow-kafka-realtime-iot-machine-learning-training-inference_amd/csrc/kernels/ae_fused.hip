@@ -1543,9 +1543,10 @@ static int train_occupancy() {
   const char* e = getenv("SML_AE_OCC");
   return (e && e[0] == '3') ? 3 : 4;
 }
-// The host sizes its partials buffer for the largest variant (4 resident workgroups per CU);
-// the launcher trims the grid to two rounds of the launched variant's residency.
-int ae_train_blocks_per_cu() { return 4; }
+// The host sizes its partials buffer for 2 x this many workgroups per CU (the largest grid
+// of any variant: the pair variants' 3 rounds x 3 resident = 9 <= 10); the launcher trims
+// the grid to the launched variant's own rounds x residency.
+int ae_train_blocks_per_cu() { return 5; }
 static int device_cus() {
   static const int cus = [] {
     int dev = 0, n = 0;
@@ -1589,13 +1590,23 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
   const int pack = acts[0] | (acts[1] << 2) | (acts[2] << 4) | (acts[3] << 6);
   const dim3 bd(WAVES * 64);
   const int occ = train_occupancy();
-  *grid_used = grid;
+  const int grid_in = grid;
   dim3 gd(grid);
-  // the pair variants hold 3 workgroups per CU: two rounds of that, not of the host's 4
-  auto pair_grid = [&] {
-    const int g3 = 2 * 3 * device_cus();
-    if (grid > g3) *grid_used = grid = g3;
+  auto set_grid = [&](int cap) {
+    grid = grid_in < cap ? grid_in : cap;
+    *grid_used = grid;
     gd = dim3(grid);
+  };
+  set_grid(2 * occ * device_cus());   // one-tile variants: two rounds of their residency
+  // the pair variants hold 3 workgroups per CU.  SML_AE_ROUNDS: residency rounds of their grid;
+  // default 3: 47.05 vs 46.86 (2), 46.17 (1), 46.86 (4) G rows/s (profiles/r02/ilp/rounds)
+  auto pair_grid = [&] {
+    static const int rounds = [] {
+      const char* e = std::getenv("SML_AE_ROUNDS");
+      const int r = e ? std::atoi(e) : 3;
+      return r >= 1 && r <= 8 ? r : 3;
+    }();
+    set_grid(rounds * 3 * device_cus());
   };
   if (pack == PACK_REF) {
     // tile-packed ring with ingest-time x argmax (pack_tiles_argmax): whole 16-row tiles

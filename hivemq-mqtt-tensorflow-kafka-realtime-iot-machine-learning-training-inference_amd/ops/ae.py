@@ -38,7 +38,9 @@ RA_WRITE_GRAD, RA_ADAM, RA_METRICS, RA_ADVANCE = 1, 2, 4, 8
 
 
 def default_train_blocks(device) -> int:
-    """Two rounds of the resident capacity: each workgroup's share halves, so CUs that
+    """Host partials capacity: 2 x ae_train_blocks_per_cu() (5) workgroups per CU; the launcher
+    trims each launch to its variant's own rounds x residency (one-tile: 2 x 4, packed pairs:
+    3 x 3).  Two rounds of the resident capacity: each workgroup's share halves, so CUs that
     finish early pick up second-round workgroups (B = 8M rows: 2048 blocks 304 us vs
     1024 blocks 310 us at 4/CU; profiles/r01_v4/sweep_occ4.log)."""
     try:

@@ -55,6 +55,13 @@ for s in $STEPS; do
               --fit-rows 0 --stream-rows 0 || true
         done
       done ;;
+    rounds)   # pair-grid residency rounds A/B (headline only)
+      for r in 1 2; do
+        for v in ${ROUNDS:-1 2 3}; do
+          step "rounds${v}_run$r" 300 env SML_AE_ROUNDS=$v python bench.py --max-blocks 8192 --infer-events 0 \
+              --fleet-models 0 --batch32-steps 0 --fit-rows 0 --stream-rows 0 || true
+        done
+      done ;;
     sweep) step ae_sweep 600 python tools/ae_sweep.py ${SWEEP_ARGS:-} ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc)
