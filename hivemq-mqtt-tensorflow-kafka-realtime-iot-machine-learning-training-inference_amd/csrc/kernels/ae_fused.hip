@@ -1198,6 +1198,46 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
           typedef __attribute__((address_space(3))) const float lds_f;
           return *(lds_f*)(ring + slot * slotb + (same ? up_off - (g >= 2 ? slotb : 0) : up_off));
         };
+        if constexpr (ILP == 3) {
+          // Packed pairs take CONTIGUOUS tiles (2p, 2p + 1): one pair is one 2 x 1168-B block of
+          // the tile-packed ring, moved by three LDS-DMAs (64 + 64 + 18 lanes x 16 B) instead of
+          // two per tile; pairs are interleaved over the waves.  The launcher guarantees an even
+          // tile count (no half pair).  Ring: PF / 2 pair slots, one pair in flight per slot.
+          constexpr int PS = PF / 2, NVP = 3;
+          const int pairb = 2 * slotb;
+          const int nl3 = (pairb - 2048) >> 4;   // lanes of the third DMA
+          const int64_t npairs = nfull >> 1;
+          auto issue_pair = [&](int64_t pi, int ps) {
+            pi = pi < npairs ? pi : npairs - 1;   // prefetch past the end re-reads the last pair
+            const char* src = reinterpret_cast<const char*>(a.xpack) + pi * pairb;
+            const unsigned dst = ring_lds + ps * pairb;
+            glds16(src, voff, dst);
+            glds16(src + 1024, voff, dst + 1024);
+            if (lane < nl3) glds16(src + 2048, voff, dst + 2048);
+          };
+          int64_t pp = ufirst;
+#pragma unroll
+          for (int k = 0; k < PS - 1; ++k) {
+            issue_pair(pp, k);
+            pp += stride;
+          }
+          int rs = 0, ws = PS - 1;
+          for (int64_t pi = ufirst; pi < npairs; pi += stride) {
+            issue_pair(pp, ws);
+            pp += stride;
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NVP * (PS - 1)) : "memory");
+            f32x4 xf[2][2];
+            int ix[2];
+            ring_tile(2 * rs, xf[0], ix[0]);
+            ring_tile(2 * rs + 1, xf[1], ix[1]);
+            const float xup = ring_up(2 * rs, false);
+            rs = rs + 1 == PS ? 0 : rs + 1;
+            ws = ws + 1 == PS ? 0 : ws + 1;
+            train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3, acc4, acc2b,
+                                               acc4b, sq, ab, corr, rows);
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the ring is retired
+        } else {
         int64_t tp = t0;
 #pragma unroll
         for (int k = 0; k < PF - 2; ++k) {
@@ -1246,6 +1286,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
           }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the ring is retired
+        }
       } else {
       int64_t tp = t0;   // tile of the next DMA issue (PF - 1 ahead of t)
 #pragma unroll
@@ -1623,7 +1664,8 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
     else if (ring_ok && D == 18 && xa_ok && train_ilp() == 2) {
       pair_grid();
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 1, 2>), gd, bd, 0, stream, a);
-    } else if (ring_ok && D == 18 && xa_ok && train_ilp() == 3 && dims[1] <= 15 && dims[2] <= 7 && dims[3] <= 7) {
+    } else if (ring_ok && D == 18 && xa_ok && ((n >> 4) & 1) == 0 && train_ilp() == 3 && dims[1] <= 15 &&
+               dims[2] <= 7 && dims[3] <= 7) {   // packed pairs: an even number of whole tiles
       pair_grid();
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 1, 3>), gd, bd, 0, stream, a);
     }

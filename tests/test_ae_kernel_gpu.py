@@ -257,7 +257,7 @@ def test_gradients_vs_bf16_rounded_reference(cuda_device, D, n):
 
 
 @pytest.mark.parametrize("ilp", ["2", "3"])
-@pytest.mark.parametrize("ntiles,blocks", [(64 * 5, 16), (64 * 4, 16), (100, 16), (30, 16), (4096, 48)])
+@pytest.mark.parametrize("ntiles,blocks", [(64 * 5, 16), (64 * 4, 16), (100, 16), (30, 16), (4096, 48), (101, 16)])
 def test_tile_pair_loop_matches_one_tile_loop(cuda_device, monkeypatch, ntiles, blocks, ilp):
     """SML_AE_ILP=2 (two tiles per wave interleaved, K = 32-row weight-gradient MFMAs) and
     SML_AE_ILP=3 (two tiles packed into one fragment in the 7-wide layers, block-diagonal
@@ -265,7 +265,8 @@ def test_tile_pair_loop_matches_one_tile_loop(cuda_device, monkeypatch, ntiles, 
     headline ring (tile-packed, D = 18).  On the same grid every wave visits the same tiles in
     the same order: ILP 2's metric sums are bit-identical, ILP 3's differ only where the
     packed MFMAs sum the same products in another K order.  Tile counts per wave cover odd
-    (a last unpaired tile), even, one and zero."""
+    (a last unpaired tile), even, one and zero; ILP 3 pairs contiguous tiles, so an odd total
+    (101 tiles) takes the one-tile loop."""
     from streamml.ops.ae import NPARAM
     spec = AESpec()
     w = _weights(spec, seed=7)
