@@ -1432,8 +1432,12 @@ __global__ __launch_bounds__(WAVES * 64) void ae_forward_kernel(FwdArgs fa) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
+  // the reference model takes the train kernel's FAST forward: biases folded into the MFMAs,
+  // hidden bias slots injected, prescaled tanh (padded features stay exactly 0)
+  constexpr bool FASTF = inject_bias_slots<PACK>();
   Frags F;
-  load_frags<false>(a, c, g, F, false);
+  load_frags<FASTF, FASTF, FASTF>(a, c, g, F, false);
+  const float pad1 = (g == 3) ? 1.0f : 0.0f;
   f32x4 nsc[2], nsh[2];
   norm_regs(a, g, nsc, nsh);
   const int64_t ntiles = (a.n + 15) >> 4;
@@ -1450,7 +1454,33 @@ __global__ __launch_bounds__(WAVES * 64) void ae_forward_kernel(FwdArgs fa) {
       for (int j = 0; j < 4; ++j) xf[s][j] = fmaf(xf[s][j], nsc[s][j], nsh[s][j]);
     bf16x4 xb0, xb1, h1b, h2b, h3b;
     f32x4 h1, h2, h3, y[2];
-    forward_tile<PACK>(a, F, g, xf, xb0, xb1, h1, h2, h3, h1b, h2b, h3b, y);
+    if constexpr (FASTF) {
+      const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+      f32x4 x1 = xf[1];
+      x1[3] += pad1;   // input 31: the constant-1 bias slot (features >= D read 0: scale / shift 0)
+      xb0 = pack4(xf[0]);
+      xb1 = pack4(x1);
+      const f32x4 z1 = mfma32(F.w1t[0], F.w1t[1], xb0, xb1, zero4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h1[i] = tanh_exp2(z1[i]);
+      h1b = pack4(h1);
+      const f32x4 z2 = mfma16(F.w2t, h1b, zero4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h2[i] = act_fwd(act_of<PACK>(a, 1), z2[i]);
+      h2b = pack4(h2);
+      const f32x4 z3 = mfma16(F.w3t, h2b, zero4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h3[i] = tanh_exp2(z3[i]);
+      h3b = pack4(h3);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f32x4 z4 = mfma16(F.w4t[t], h3b, zero4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[t][i] = act_fwd(act_of<PACK>(a, 3), z4[i]);   // 0 past D
+      }
+    } else {
+      forward_tile<PACK>(a, F, g, xf, xb0, xb1, h1, h2, h3, h1b, h2b, h3b, y);
+    }
     float se = 0.f;
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
