@@ -934,8 +934,9 @@ __device__ __forceinline__ void packed_fold_src(int s, int& s1, int& s2) {
   s2 = base + (pin + 8) * w + out + (l3 ? 8 : 0);
 }
 
-// One packed pair.  TP: the pair's second tile is a stand-in (a wave's odd last tile) whose
-// loss, metrics and gradients are all masked to zero.
+// One packed pair of whole tiles.  TP: the pair's second tile is a stand-in whose loss,
+// metrics and gradients are all masked to zero (kept for an odd last tile; the kernel's
+// contiguous-pair loop takes even tile counts only and instantiates TP = false).
 template <int PACK, int DC, bool TP>
 __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP& F, char* scr, int c, int g,
                                                   const f32x4 (&xf)[2][2], float xup, const int (&ix)[2],
@@ -1169,9 +1170,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
       };
       const int64_t t0 = ufirst * CH;
       if constexpr (ILP >= 2) {
-        // tile pairs (t, t + stride): two issues per iteration, the pair's two tiles landed
-        // = vmcnt(NV * (PF - 2)); a last unpaired tile runs alone (ILP 2: U = 1; ILP 3: a
-        // packed pair whose second tile is a masked stand-in)
+        // ILP 2: tile pairs (t, t + stride), two issues per iteration, the pair's two tiles
+        // landed = vmcnt(NV * (PF - 2)); a last unpaired tile runs alone (U = 1).  ILP 3:
+        // contiguous tile pairs (below).
         static_assert(XM == 1 && CH == 1 && PF >= 3, "tile pairs: tile-packed ring, plain order");
         auto ring_tile = [&](int slot, f32x4 xf[2], int& ix) {
           typedef __attribute__((address_space(3))) const unsigned char lds_u8;
@@ -1194,9 +1195,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
         // loop-invariant lane offset covers both tiles
         static_assert(ILP != 3 || PF % 2 == 0, "pairs start on even ring slots");
         const int up_off = c * 4 * DC + 4 * (16 + (g & 1)) + (g >= 2 ? slotb : 0);
-        auto ring_up = [&](int slot, bool same) -> float {
+        auto ring_up = [&](int slot) -> float {   // slot: the pair's first tile
           typedef __attribute__((address_space(3))) const float lds_f;
-          return *(lds_f*)(ring + slot * slotb + (same ? up_off - (g >= 2 ? slotb : 0) : up_off));
+          return *(lds_f*)(ring + slot * slotb + up_off);
         };
         if constexpr (ILP == 3) {
           // Packed pairs take CONTIGUOUS tiles (2p, 2p + 1): one pair is one 2 x 1168-B block of
@@ -1230,7 +1231,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
             int ix[2];
             ring_tile(2 * rs, xf[0], ix[0]);
             ring_tile(2 * rs + 1, xf[1], ix[1]);
-            const float xup = ring_up(2 * rs, false);
+            const float xup = ring_up(2 * rs);
             rs = rs + 1 == PS ? 0 : rs + 1;
             ws = ws + 1 == PS ? 0 : ws + 1;
             train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3, acc4, acc2b,
@@ -1253,37 +1254,18 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV * (PF - 2)) : "memory");
           f32x4 xf[2][2];
           int ix[2];
-          const int rd1 = ILP == 3 ? rd + 1 : (rd + 1 == PF ? 0 : rd + 1);
           ring_tile(rd, xf[0], ix[0]);
-          ring_tile(rd1, xf[1], ix[1]);
-          float xup = 0.f;
-          if constexpr (ILP == 3) xup = ring_up(rd, false);
+          ring_tile(rd + 1 == PF ? 0 : rd + 1, xf[1], ix[1]);
           rd = rd + 2 >= PF ? rd + 2 - PF : rd + 2;
           wr = wr + 2 >= PF ? wr + 2 - PF : wr + 2;
-          if constexpr (ILP == 3)
-            train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3, acc4, acc2b,
-                                               acc4b, sq, ab, corr, rows);
-          else
-            train_tiles_ilp<PACK, DC, 2>(a, F, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
+          train_tiles_ilp<PACK, DC, 2>(a, F, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
         }
         if (t < nfull) {   // already issued: the oldest of the PF - 2 tiles in flight
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV * (PF - 3)) : "memory");
-          if constexpr (ILP == 3) {
-            f32x4 xf[2][2];
-            int ix[2];
-            ring_tile(rd, xf[0], ix[0]);
-            xf[1][0] = xf[0][0];
-            xf[1][1] = xf[0][1];
-            ix[1] = ix[0];
-            const float xup = ring_up(rd, true);
-            train_pair_packed<PACK, DC, true>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3, acc4, acc2b,
-                                              acc4b, sq, ab, corr, rows);
-          } else {
-            f32x4 xf[1][2];
-            int ix[1];
-            ring_tile(rd, xf[0], ix[0]);
-            train_tiles_ilp<PACK, DC, 1>(a, F, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
-          }
+          f32x4 xf[1][2];
+          int ix[1];
+          ring_tile(rd, xf[0], ix[0]);
+          train_tiles_ilp<PACK, DC, 1>(a, F, scr, c, g, xf, ix, pad1, acc1, acc2, acc3, acc4, sq, ab, corr, rows);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the ring is retired
         }
