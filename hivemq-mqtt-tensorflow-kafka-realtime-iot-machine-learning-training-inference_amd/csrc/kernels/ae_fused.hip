@@ -20,6 +20,14 @@
 //    fp32 slab is written once per launch (deterministic, no float atomics);
 //  * a second small kernel reduces the slabs and applies Adam (Keras semantics:
 //    bias-corrected lr_t, epsilon 1e-7) elementwise on the padded image.
+//  * the reference model's default loop (SML_AE_ILP=3, train_pair_packed) takes two
+//    contiguous tiles per iteration and packs them into ONE fragment wherever a layer is
+//    narrower than 16: the 7-wide layers 2-3 (+ bias slots), inputs 16-17 + the bias input
+//    of layer 1 and outputs 16-17 of layer 4.  The weights become block-diagonal / masked
+//    copies built once per launch, so every layer is still one MFMA, and the packed
+//    accumulators are folded into the image when the slab is written (packed_fold_src).
+//    The loop is issue-bound: this cut VALU 27 %, LDS 31 %, SALU 40 % per row against
+//    the one-tile loop (SML_AE_ILP=1), 37 -> 47 G rows/s (profiles/r02/ilp).
 //
 // Padded parameter image (fp32, 1536 floats), row-major [in][out]:
 //   L1 [32][16] @0    (bias = row 31)     requires D  <= 31, n1 <= 15
