@@ -95,8 +95,10 @@ def build_c(verbose: bool = False, force: bool = False, checked: bool = False) -
             # interleave VALU with MFMA opt out of SLP packing
             if "sml-build: no-slp" in head:
                 vgpr_form = vgpr_form + ["-fno-slp-vectorize"]
+            # SML_HIPCC_EXTRA: extra device-compile flags for A/B builds (e.g. a scheduler strategy)
+            extra = os.environ.get("SML_HIPCC_EXTRA", "").split()
             jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
-                         f"-I{inc}", "-Wno-unused-result", "-munsafe-fp-atomics", *vgpr_form, *dflags])
+                         f"-I{inc}", "-Wno-unused-result", "-munsafe-fp-atomics", *vgpr_form, *dflags, *extra])
     # host runtime pieces that use the HIP runtime API (no device code, no torch)
     for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
         obj = os.path.join(BUILD, "rt_" + os.path.basename(src) + ".o")
