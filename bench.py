@@ -45,7 +45,15 @@ def parse():
     p.add_argument("--batch-per-gpu", type=int, default=1 << 25)
     p.add_argument("--dataset-rows", type=int, default=1 << 26, help="rows resident per GPU (ring of batches)")
     p.add_argument("--max-blocks", type=int, default=0, help="0 = two rounds of the resident capacity")
-    p.add_argument("--infer-events", type=int, default=1000)
+    p.add_argument("--infer-events", type=int, default=20000,
+                   help="events per latency repeat of the persistent scorer, on every replica (0 = skip)")
+    p.add_argument("--infer-repeats", type=int, default=3)
+    p.add_argument("--qps", type=float, default=10000.0,
+                   help="offered events/s per replica (scenario.xml: 100 000 cars x 1 msg / 10 s)")
+    p.add_argument("--e2e-events", type=int, default=20000,
+                   help="events of the Kafka append -> scored result latency run on rank 0 (0 = skip)")
+    p.add_argument("--lstm-steps", type=int, default=20,
+                   help="timed steps of the seq-50 LSTM side measurement, BASELINE config 3 (0 = skip)")
     p.add_argument("--fleet-models", type=int, default=1024,
                    help="side measurement: batch-32 training of this many independent models at once (0 = skip)")
     p.add_argument("--batch32-steps", type=int, default=20000,
@@ -66,43 +74,52 @@ def parse():
     return p.parse_args()
 
 
-def measure_infer_p50(fused, device, n_events: int, model=None, qps: float = 10000.0):
-    """Per-event latency (us): event in pinned host memory -> score on the host.
+def gather_all(obj, device):
+    """Every rank's ``obj`` (a list indexed by rank; [obj] without a process group)."""
+    from streamml.parallel import dp as dpm
+    if not dpm._pg_active():
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
 
-    Primary path: the persistent scorer (one resident wave polling a host-mapped
-    request ring, ``ops.serve.ScoringServer``), events offered one at a time at
-    ``qps``.  Falls back to launch-per-event (H2D + fused forward + D2H) when no
-    Autoencoder object is given.
-    """
+
+def measure_infer(model, device, n_events: int, repeats: int = 3, qps: float = 10000.0, rank: int = 0):
+    """BASELINE config 5 per replica: per-event latency (us) of the persistent scorer (one
+    resident wave polling a host-mapped request ring, ``ops.serve.ScoringServer``) -- event
+    in pinned host memory -> score + flag back on the host -- events offered one at a time at
+    ``qps`` from this replica's own car-key shard.  ``repeats`` runs of ``n_events``; p50 is
+    the median of the runs' p50s, p99 the worst run's, with the device-side breakdown."""
     import numpy as np
-    import torch
 
-    if n_events <= 0:
-        return None, None
-    rng = np.random.default_rng(1)
-    events = rng.uniform(0, 40, size=(n_events + 100, 18)).astype(np.float32)
-    if model is not None:
-        from streamml.ops.serve import ScoringServer
-        with ScoringServer(model, slots=4096) as srv:
-            srv.latency_us(events[:100], qps=qps)
-            lat = srv.latency_us(events[100:], qps=qps)
-        return float(np.percentile(lat, 50)), float(np.percentile(lat, 99))
-    host = torch.empty((1, 18), dtype=torch.float32).pin_memory()
-    out = torch.empty(1, dtype=torch.float32).pin_memory()
-    dev = torch.empty((1, 18), dtype=torch.float32, device=device)
-    lat = []
-    for i in range(n_events + 50):
-        host.copy_(torch.from_numpy(events[i:i + 1]))
-        t0 = time.perf_counter()
-        dev.copy_(host, non_blocking=True)
-        _, s, _ = fused.forward(dev, recon=False, score=True)
-        out.copy_(s, non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        t1 = time.perf_counter()
-        if i >= 50:
-            lat.append((t1 - t0) * 1e6)
-    lat = np.asarray(lat)
-    return float(np.percentile(lat, 50)), float(np.percentile(lat, 99))
+    from streamml.data.cardata import synthetic_device_tensor
+    from streamml.ops.serve import ScoringServer
+
+    ev = synthetic_device_tensor(n_events + 1000, device, seed=100 + rank).cpu().numpy()
+    runs = []
+    with ScoringServer(model, slots=4096) as srv:
+        srv.latency_us(ev[:1000], qps=qps)            # warm: resident wave, clocks, caches
+        for _ in range(repeats):
+            host, devt, load, comp = srv.latency_us(ev[1000:], qps=qps, device_breakdown=True)
+            runs.append({"p50_us": float(np.percentile(host, 50)), "p99_us": float(np.percentile(host, 99)),
+                         "device_p50_us": float(np.percentile(devt, 50)),
+                         "device_load_p50_us": float(np.percentile(load, 50)),
+                         "device_compute_p50_us": float(np.percentile(comp, 50))})
+        relaunches = srv.launches
+    p50s = [r["p50_us"] for r in runs]
+    return {"p50_us": float(np.median(p50s)), "p99_us": max(r["p99_us"] for r in runs),
+            "p50_spread_us": [min(p50s), max(p50s)], "runs": runs, "events_per_run": n_events,
+            "offered_qps": qps, "kernel_launches": relaunches,
+            "host_overhead_p50_us": float(np.median(p50s)) - float(np.median([r["device_p50_us"] for r in runs]))}
+
+
+def measure_kafka_e2e(model, device, n_events: int, qps: float = 10000.0):
+    """Kafka append -> scored result record acknowledged, through ``serve --low-latency``
+    (bench/bench_infer.py:kafka_e2e): p50/p99 and the per-stage breakdown."""
+    from streamml.data.cardata import synthetic_device_tensor
+    ev = synthetic_device_tensor(n_events + 200, device, seed=7).cpu().numpy()
+    return _bench_module("bench_infer").kafka_e2e(model, ev, qps, 5.0, n_events, warm=200)
 
 
 def measure_batch32(spec, data, device, steps, scale, shift, seed, launches=5):
@@ -202,13 +219,17 @@ def measure_batch_dp(spec, data, device, steps, scale, shift, seed, world, batch
             "path": f"persistent kernel, in-kernel P2P gradient exchange over xGMI, dp{world}"}
 
 
-def _bench_fit_module():
-    """bench/bench_fit.py by path (``bench`` the package name is shadowed by this file)."""
+def _bench_module(name: str):
+    """bench/<name>.py by path (``bench`` the package name is shadowed by this file)."""
     import importlib.util
-    spec = importlib.util.spec_from_file_location("sml_bench_fit", os.path.join(ROOT, "bench", "bench_fit.py"))
+    spec = importlib.util.spec_from_file_location(f"sml_{name}", os.path.join(ROOT, "bench", f"{name}.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
+
+
+def _bench_fit_module():
+    return _bench_module("bench_fit")
 
 
 def measure_fit(device, rows, batch=100, seed=0):
@@ -250,8 +271,35 @@ def measure_batch32_fleet(spec, data, device, steps, scale, shift, n_models=1024
             "path": "fleet mode of ae_minibatch.hip (one workgroup per independent model), 1 GPU"}
 
 
+def self_launch(args) -> int | None:
+    """``--gpus N > 1`` without a launcher: run N ranks under ``torch.distributed.run`` as a
+    CHILD process (never an exec, and before anything touches the GPU), relay its output
+    -- rank 0 prints the JSON line to the inherited stdout -- and return its exit code.
+    Returns None when this process is already a rank (torchrun set WORLD_SIZE) or N == 1."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+
+    shared = os.environ.get("SML_SHARE_GPU0") == "1"
+    if not shared:
+        import torch   # device_count() enumerates without initialising HIP on this image
+        visible = torch.cuda.device_count()
+        if visible < args.gpus:
+            print(f"[bench] --gpus {args.gpus} but only {visible} GPU(s) visible; refusing to measure fewer "
+                  f"(SML_SHARE_GPU0=1 rehearses N ranks on GPU 0)", file=sys.stderr, flush=True)
+            return 2
+    from streamml.parallel.dp import free_port
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] self-launch: {' '.join(cmd[2:6])} ... ({args.gpus} ranks)", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     import numpy as np
     import torch
 
@@ -264,7 +312,10 @@ def main():
     world, rank, device = env.world_size, env.rank, env.device
     if args.gpus != world:
         if rank == 0:
-            print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+            print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing a mislabelled measurement",
+                  file=sys.stderr, flush=True)
+        dp.shutdown()
+        sys.exit(2)
 
     B = int(args.batch_per_gpu)
     rows = max(B, (int(args.dataset_rows) // B) * B)
@@ -275,10 +326,15 @@ def main():
     data = synthetic_device_tensor(rows, device, seed=args.seed, n_devices=100_000, shard=rank, n_shards=world)
     fused = FusedAE(spec, weights, device, max_blocks=args.max_blocks, scale=scale, shift=shift)
     dp.broadcast_(fused.params)
-    allreduce = dp.allreduce_sum_ if world > 1 else None
+    # SML_FORCE_PG=1 runs this DP path (RCCL all-reduce per step) even at world 1
+    allreduce = dp.allreduce_sum_ if env.is_dist else None
     gb = B * world
 
-    fused.attach_ring(data, B)
+    torch.cuda.synchronize()
+    tp = time.perf_counter()
+    fused.attach_ring(data, B)      # ingest transform: normalize_fn + argmax(x) + tile packing
+    torch.cuda.synchronize()
+    pack_ms = (time.perf_counter() - tp) * 1e3
 
     def eager_step():
         fused.step_ring(global_batch=gb, allreduce=allreduce)
@@ -323,26 +379,34 @@ def main():
     metrics = fused.read_metrics()
     if args.dump_params:
         np.save(f"{args.dump_params}.rank{rank}.npy", fused.params.detach().cpu().numpy())
-    p50 = p99 = None
-    infer_path = None
-    if rank == 0 and args.infer_events > 0:
-        try:   # persistent scorer loaded with the weights just trained
-            from streamml.models.autoencoder import Autoencoder
-            am = Autoencoder(device=device, input_normalizer="cardata")
-            am.set_weights(fused.get_weights())
-            am.compile()
-            p50, p99 = measure_infer_p50(fused, device, args.infer_events, model=am)
-            infer_path = "persistent-kernel"
-        except Exception as e:  # noqa: BLE001 - report, then measure the launch path
-            print(f"[bench] persistent scorer unavailable ({e!r}); launch-per-event path", file=sys.stderr)
-            p50, p99 = measure_infer_p50(fused, device, args.infer_events)
-            infer_path = "launch-per-event"
+    # per-rank timed-region spread (the headline uses the max)
+    spread = gather_all([t1 - t0], device)
+    step_ms = [v[0] / args.steps * 1e3 for v in spread]
+
     def guarded(fn, *a, **kw):   # a side measurement never takes the headline down
         try:
             return fn(*a, **kw)
         except Exception as e:  # noqa: BLE001
             return {"error": repr(e)[:400]}
 
+    # -- BASELINE config 5: per-event scoring on every replica at once (shard-by-key) ----------
+    am = None
+    infer = {"skipped": "--infer-events 0"}
+    if args.infer_events > 0:
+        try:   # the model just trained, loaded into the persistent scorer
+            from streamml.models.autoencoder import Autoencoder
+            am = Autoencoder(device=device, input_normalizer="cardata")
+            am.set_weights(fused.get_weights())
+            am.compile()
+        except Exception as e:  # noqa: BLE001
+            infer = {"error": repr(e)[:400]}
+        if am is not None:
+            dp.barrier(device)
+            infer = guarded(measure_infer, am, device, args.infer_events, args.infer_repeats, args.qps, rank)
+    per_rank_infer = gather_all(infer, device)
+    e2e = None
+    if rank == 0 and am is not None and args.e2e_events > 0:
+        e2e = guarded(measure_kafka_e2e, am, device, args.e2e_events, args.qps)
     b32 = None
     if rank == 0 and args.batch32_steps > 0:
         b32 = guarded(measure_batch32, spec, data, device, args.batch32_steps, scale, shift, args.seed)
@@ -351,7 +415,7 @@ def main():
                                    scale, shift, args.fleet_models)
     b32_dp = {"skipped": "single GPU (no peers)"}
     coll = {"skipped": "single GPU (no peers)"}
-    if world > 1 and (args.dp_steps > 0 or args.collective_iters > 0):
+    if env.is_dist and (args.dp_steps > 0 or args.collective_iters > 0):
         from streamml.parallel.p2p import P2PGroup
         p2p, p2p_err = P2PGroup.try_create(device)   # collective: every rank gets a group, or none
         if args.collective_iters > 0:
@@ -366,9 +430,17 @@ def main():
         fit100 = guarded(measure_fit, device, args.fit_rows)
     if rank == 0 and args.stream_rows > 0:
         stream = guarded(measure_stream_e2e, device, args.stream_rows)
-    del nslices
+    # -- BASELINE config 3: LSTM (rank 0; the LSTM trains single-replica here) --------------------
+    lstm = lstm_ref = None
+    if rank == 0 and args.lstm_steps > 0:
+        from_b = _bench_module("bench_lstm")
+        lstm = guarded(from_b.measure_seq, batch=65536, seq_len=50, steps=args.lstm_steps, warmup=3, device=device)
+        lstm_ref = guarded(from_b.measure_reference, batch=1, epochs=5, steps_per_epoch=1000, autograd_steps=100,
+                           device=device)
     rows_per_s = gb * args.steps / elapsed
     if rank == 0:
+        p50s = [r.get("p50_us") for r in per_rank_infer if isinstance(r, dict)]
+        p50s = [v for v in p50s if v is not None]
         out = {
             "metric": METRIC,
             "value": rows_per_s,
@@ -393,9 +465,17 @@ def main():
                 "parallelism": f"dp{world}",
                 "micro_batch_per_gpu": B,
             },
-            "p50_infer_us": p50,
-            "p99_infer_us": p99,
-            "infer_path": infer_path,
+            "backend": env.backend,
+            "per_rank_ms_per_step": {"min": min(step_ms), "max": max(step_ms), "ranks": step_ms},
+            "pack_ms": pack_ms,
+            "p50_infer_us": max(p50s) if p50s else None,   # worst replica (conservative)
+            "p99_infer_us": max((r.get("p99_us") or 0.0) for r in per_rank_infer if isinstance(r, dict)) or None,
+            "infer_path": "persistent-kernel (ae_serve.hip), host-mapped request ring",
+            "infer": per_rank_infer[0],
+            "infer_per_replica_p50_us": p50s,
+            "kafka_e2e_p50_us": None if not e2e or "error" in e2e else e2e["p50_us"],
+            "kafka_e2e_p99_us": None if not e2e or "error" in e2e else e2e["p99_us"],
+            "kafka_e2e": e2e,
             "hip_graph": graph is not None,
             "final_epoch_loss": metrics["loss"],
             "final_accuracy": metrics["accuracy"],
@@ -406,8 +486,13 @@ def main():
             "fit_batch100": fit100,
             "stream_e2e_rows_per_s": None if not stream or "error" in stream else stream["rows_per_s"],
             "stream_e2e": stream,
+            "lstm_seq50_windows_per_s": None if not lstm or "error" in lstm else lstm["value"],
+            "lstm_seq50": lstm,
+            "lstm_ref_us_per_step": None if not lstm_ref or "error" in lstm_ref else lstm_ref["value"],
+            "lstm_ref": lstm_ref,
         }
         print(json.dumps(out), flush=True)
+    dp.barrier(device)   # every rank leaves together (rank 0's side measurements run alone)
     dp.shutdown()
 
 

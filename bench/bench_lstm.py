@@ -32,15 +32,22 @@ def main():
     args.batch = args.batch or (1 if ref else 65536)
     args.seq_len = args.seq_len or (1 if ref else 50)
     if ref and args.seq_len == 1 and args.batch <= 32:
-        return bench_reference(args)
-    import numpy as np
+        print(json.dumps(measure_reference(batch=args.batch)))
+        return
+    print(json.dumps(measure_seq(batch=args.batch, seq_len=args.seq_len, steps=args.steps, warmup=args.warmup,
+                                 stack=args.stack, materialize=args.materialize, graph=bool(args.graph))))
+
+
+def measure_seq(batch: int = 65536, seq_len: int = 50, steps: int = 30, warmup: int = 5, stack: str = "two_layer",
+                materialize: bool = False, graph: bool = False, device=None) -> dict:
+    """Train windows/s of an LSTM stack on sliding windows of synthetic car events."""
     import torch
     from streamml.data.cardata import normalize_affine, synthetic_device_tensor
     from streamml.models.lstm import LSTMPredictor
 
-    dev = torch.device("cuda", 0)
-    T, B = args.seq_len, args.batch
-    ctor = LSTMPredictor.two_layer if args.stack == "two_layer" else LSTMPredictor.reference
+    dev = torch.device(device) if device is not None else torch.device("cuda", 0)
+    T, B = seq_len, batch
+    ctor = LSTMPredictor.two_layer if stack == "two_layer" else LSTMPredictor.reference
     m = ctor(look_back=T, device=dev)
     sc, sh = normalize_affine()
     raw = synthetic_device_tensor(B * 4 + T + 1, dev, seed=0)
@@ -50,31 +57,32 @@ def main():
     from streamml.data.stream import sliding_windows
     n = B * 4
     X, Y = sliding_windows(xn[:n + T].contiguous(), T)
-    if args.materialize:   # the round-1 layout: every window copied (T x the input bytes)
+    if materialize:   # the round-1 layout: every window copied (T x the input bytes)
         X, Y = X.contiguous(), Y.contiguous()
-    for s in range(args.warmup):
+    for s in range(warmup):
         i = s % 4
         m.train_step(X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B])
     torch.cuda.synchronize()
     step = lambda s: m.train_step(X[(s % 4) * B:(s % 4 + 1) * B], Y[(s % 4) * B:(s % 4 + 1) * B])
-    if args.graph:
+    if graph:
         from streamml.utils.graphs import capture_steps
         step = capture_steps([lambda i=i: m.train_step(X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B])
                               for i in range(4)])
     t0 = time.perf_counter()
-    for s in range(args.steps):
+    for s in range(steps):
         loss, _ = step(s)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    wps = B * args.steps / dt
-    print(json.dumps({"metric": "LSTM train windows/s (seq_len=%d, %s)" % (T, args.stack), "value": wps,
-                      "unit": "windows/s", "events_per_s": wps * T, "ms_per_step": dt / args.steps * 1e3,
-                      "batch": B, "seq_len": T, "params": m.count_params(), "dtype": "bf16",
-                      "final_loss": float(loss), "n_gpus": 1, "data": "synthetic", "hip_graph": bool(args.graph),
-                      "windows": "materialized" if args.materialize else "in-place strided views"}))
+    wps = B * steps / dt
+    return {"metric": "LSTM train windows/s (seq_len=%d, %s)" % (T, stack), "value": wps,
+            "unit": "windows/s", "events_per_s": wps * T, "ms_per_step": dt / steps * 1e3,
+            "batch": B, "seq_len": T, "steps": steps, "params": m.count_params(), "dtype": "bf16",
+            "final_loss": float(loss), "n_gpus": 1, "data": "synthetic", "hip_graph": bool(graph),
+            "windows": "materialized" if materialize else "in-place strided views"}
 
 
-def bench_reference(args, epochs: int = 5, steps_per_epoch: int = 1000):
+def measure_reference(batch: int = 1, epochs: int = 5, steps_per_epoch: int = 1000, autograd_steps: int = 300,
+                      device=None) -> dict:
     """cardata-v2.py:172-209 as the reference runs it: look_back 1, batch 1, 1 000 steps x
     5 epochs, one Adam update per event.  Persistent kernel (one launch per epoch) vs the
     per-step autograd path (fused LSTM kernels, ~10 launches per step)."""
@@ -85,9 +93,9 @@ def bench_reference(args, epochs: int = 5, steps_per_epoch: int = 1000):
     from streamml.models.lstm import LSTMPredictor
     from streamml.ops import lstm_persistent as lp
 
-    dev = torch.device("cuda", 0)
-    B = args.batch
-    n = steps_per_epoch * B
+    dev = torch.device(device) if device is not None else torch.device("cuda", 0)
+    B = batch
+    n = max(steps_per_epoch, autograd_steps + 20) * B
     sc, sh = normalize_affine()
     raw = synthetic_device_tensor(n + 1, dev, seed=0)
     xn = (raw * torch.tensor(sc, dtype=torch.float32, device=dev)
@@ -107,19 +115,19 @@ def bench_reference(args, epochs: int = 5, steps_per_epoch: int = 1000):
     for i in range(20):
         ma.train_step(X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B])
     torch.cuda.synchronize()
-    na = 300
+    na = autograd_steps
     t1 = time.perf_counter()
     for i in range(na):
         ma.train_step(X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B])
     torch.cuda.synchronize()
     da = time.perf_counter() - t1
-    print(json.dumps({"metric": "LSTM reference stack Keras step time (look_back=1, batch=%d)" % B,
-                      "value": dt / steps * 1e6, "unit": "us/step", "higher_is_better": False,
-                      "steps_per_s": steps / dt, "events_per_s": steps * B / dt, "steps": steps,
-                      "epochs": epochs, "steps_per_epoch": steps_per_epoch, "launches": epochs,
-                      "autograd_us_per_step": da / na * 1e6, "speedup_vs_autograd": (da / na) / (dt / steps),
-                      "final_loss": float(out[-1, 0]), "params": m.count_params(), "dtype": "fp32",
-                      "n_gpus": 1, "data": "synthetic", "engine": "persistent (lstm_ref_train.hip)"}))
+    return {"metric": "LSTM reference stack Keras step time (look_back=1, batch=%d)" % B,
+            "value": dt / steps * 1e6, "unit": "us/step", "higher_is_better": False,
+            "steps_per_s": steps / dt, "events_per_s": steps * B / dt, "steps": steps,
+            "epochs": epochs, "steps_per_epoch": steps_per_epoch, "launches": epochs,
+            "autograd_us_per_step": da / na * 1e6, "speedup_vs_autograd": (da / na) / (dt / steps),
+            "final_loss": float(out[-1, 0]), "params": m.count_params(), "dtype": "fp32",
+            "n_gpus": 1, "data": "synthetic", "engine": "persistent (lstm_ref_train.hip)"}
 
 
 if __name__ == "__main__":

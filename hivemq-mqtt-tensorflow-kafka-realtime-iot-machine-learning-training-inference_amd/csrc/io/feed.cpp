@@ -76,6 +76,7 @@ void Feed::start(const std::vector<uintptr_t>& slabs, int64_t cap_rows) {
   if (!workers_.empty()) throw std::logic_error("feed: already started");
   if (slabs.empty() || cap_rows <= 0) throw std::invalid_argument("feed: need slabs of > 0 rows");
   slabs_ = slabs;
+  marks_.assign(slabs_.size(), {});
   cap_ = cap_rows;
   for (size_t i = 0; i < slabs_.size(); ++i) free_.push_back((int)i);
   const int nw = std::max(1, std::min(cfg_.workers, (int)parts_.size()));
@@ -146,13 +147,22 @@ int Feed::take_free(double& waited) {
   return s;
 }
 
-void Feed::publish(int slab, int64_t rows) {
+std::vector<std::pair<int, int64_t>> Feed::slab_marks(int slab) const {
+  if (slab < 0 || slab >= (int)slabs_.size()) throw std::out_of_range("feed: bad slab");
+  std::lock_guard<std::mutex> g(mu_);
+  return marks_[(size_t)slab];
+}
+
+void Feed::publish(int w, int slab, int64_t rows) {
   // labels were staged after the slab's `cap` rows; move them right behind the `rows` rows
   char* base = reinterpret_cast<char*>(slabs_[(size_t)slab]);
   const size_t F = cfg_.feature_fields.size();
   std::memmove(base + (size_t)rows * F * 4, base + (size_t)cap_ * F * 4, (size_t)rows);
   {
     std::lock_guard<std::mutex> g(mu_);
+    auto& mk = marks_[(size_t)slab];
+    mk.clear();
+    for (int pi : workers_[(size_t)w].parts) mk.emplace_back(pi, parts_[(size_t)pi]->pos.load());
     ready_.emplace_back(slab, rows);
     ++stats_.slabs;
   }
@@ -268,6 +278,10 @@ void Feed::run(int w) {
     loc = Stats();
   };
   std::unique_ptr<kafka::Client> cl;
+  // long-poll policy (as scoreloop.cpp): a worker that owns several partitions fetches with
+  // wait 0 while any of them made progress in the last round; only after an empty round does
+  // it long-poll, and then on one partition, so an idle partition never stalls busy ones
+  bool prev_progress = true;
   try {
     cl = std::make_unique<kafka::Client>(bootstrap_, ccfg_);   // one broker connection per worker
     for (;;) {
@@ -290,7 +304,8 @@ void Feed::run(int w) {
           }
           const auto t0 = Clock::now();
           size_t off = 0, len = 0;
-          cl->fetch_raw(P.spec.topic, P.spec.partition, pos, cfg_.max_bytes, cfg_.max_wait_ms, S.resp, off, len);
+          const int wait = (mine.size() == 1 || (!prev_progress && q == 0)) ? cfg_.max_wait_ms : 0;
+          cl->fetch_raw(P.spec.topic, P.spec.partition, pos, cfg_.max_bytes, wait, S.resp, off, len);
           loc.fetch_s += secs(t0, Clock::now());
           ++loc.fetches;
           if (len == 0) continue;
@@ -336,7 +351,7 @@ void Feed::run(int w) {
           ++loc.rows;
           progressed = true;
           if (n == cap_) {
-            publish(slab, n);
+            publish(w, slab, n);
             slab = -1;
             flush_stats();
           }
@@ -344,6 +359,7 @@ void Feed::run(int w) {
         loc.decode_s += secs(t1, Clock::now());
       }
       ++rr;
+      prev_progress = progressed;
       if (all_done) break;
       if (progressed) {
         last_data = Clock::now();
@@ -351,7 +367,7 @@ void Feed::run(int w) {
         // nothing new on any of this worker's partitions (a followed, unbounded log):
         // hand over what is buffered, and give up after the idle timeout
         if (slab >= 0 && n > 0) {
-          publish(slab, n);
+          publish(w, slab, n);
           slab = -1;
         }
         if (cfg_.idle_timeout_s >= 0 && secs(last_data, Clock::now()) > cfg_.idle_timeout_s) break;
@@ -363,7 +379,7 @@ void Feed::run(int w) {
 out:
   if (slab >= 0) {
     if (n > 0) {
-      publish(slab, n);
+      publish(w, slab, n);
     } else {
       std::lock_guard<std::mutex> g(mu_);
       free_.push_back(slab);

@@ -76,6 +76,10 @@ class Feed {
   void stop();
   Stats stats() const;
   std::vector<int64_t> positions() const;   // next offset to read, per PartSpec
+  // commit marks of a popped slab: (PartSpec index, next offset) of the publishing worker's
+  // partitions at publish time -- every record before them is in this slab, an earlier slab
+  // of the same worker, or was dropped by the label filter (at-least-once commit points)
+  std::vector<std::pair<int, int64_t>> slab_marks(int slab) const;
   int features() const { return (int)cfg_.feature_fields.size(); }
   // decode one (framed) Avro value into a projected row + label code; false = malformed
   bool decode_row(const uint8_t* p, size_t n, float* out_row, uint8_t* label) const;
@@ -119,7 +123,8 @@ class Feed {
 
   void run(int w);
   int take_free(double& waited);
-  void publish(int slab, int64_t rows);
+  void publish(int w, int slab, int64_t rows);
+  std::vector<std::vector<std::pair<int, int64_t>>> marks_;   // per slab, see slab_marks()
 };
 
 }  // namespace feed

@@ -624,6 +624,7 @@ PYBIND11_MODULE(_io, m) {
              f.stop();
            })
       .def("positions", &feed::Feed::positions)
+      .def("slab_marks", &feed::Feed::slab_marks, py::arg("slab"))
       .def_property_readonly("features", &feed::Feed::features)
       .def("stats", [](const feed::Feed& f) {
         const feed::Stats s = f.stats();

@@ -327,7 +327,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const float l1r = row_ok ? a.l1 : 0.f;
   auto fm = [&](bool keep, float v) { return FMASK ? (keep ? v : 0.f) : v; };
 
+  const int64_t cur0 = cur;
+  int done = a.nsteps;   // optimizer steps applied (fewer only when a DP exchange gave up)
+  // DP: a step whose gradient exchange timed out is rolled back on EVERY wave (some waves'
+  // granules may have arrived): these hold the state from before the step's update
+  float wp[4] = {0.f, 0.f, 0.f, 0.f}, mp[4] = {0.f, 0.f, 0.f, 0.f}, vp[4] = {0.f, 0.f, 0.f, 0.f};
+  float sq0 = 0.f, ab0 = 0.f, corr0 = 0.f;
   for (int step = 0; step < a.nsteps; ++step) {
+    if (DPX) {
+      sq0 = sq;
+      ab0 = ab;
+      corr0 = corr;
+    }
     // ================= phase A: forward + activation gradients of this wave's 16 rows =================
     if (has_rows) {
       float xv[8];
@@ -492,6 +503,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         acc = sum;
         if (failed && lane == 0) S.abort = 1;
       }
+      if (DPX) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          wp[i] = wo[i];
+          mp[i] = mo[i];
+          vp[i] = vo[i];
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float gr = acc[i] * a.gscale;
@@ -524,7 +543,24 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     mark(2);
     lds_barrier();
     mark(3);
-    if (dp && S.abort) break;   // read after the barrier: every wave leaves together
+    if (dp && S.abort) {   // read after the barrier: every wave leaves together
+      // roll the failed step back everywhere: its update, metrics and cursor never happened,
+      // so the replica stays in the state it had after `step` completed steps (the host
+      // raises P2PTimeout and can resync / retry from there)
+      if (has_tile) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          wo[i] = wp[i];
+          mo[i] = mp[i];
+          vo[i] = vp[i];
+        }
+      }
+      sq = sq0;
+      ab = ab0;
+      corr = corr0;
+      done = step;
+      break;
+    }
   }
 
   // ---- write back: the whole image (padding slots keep zero gradients), moments, metrics ----
@@ -558,10 +594,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         for (int w = 0; w < NT / 64; ++w) s += S.red[k][w];
         a.metrics[k] += s;
       }
-      a.metrics[3] += (float)B * (float)a.nsteps;
+      a.metrics[3] += (float)B * (float)done;
     }
-    a.iter[0] = it0 + a.nsteps;
-    if (a.cursor) a.cursor[0] = a.nsteps > 0 ? nxt : cur;
+    a.iter[0] = it0 + done;
+    if (a.cursor) a.cursor[0] = done == a.nsteps ? nxt : (cur0 + (int64_t)done * B) % a.ring;
     if (dp && S.abort) __hip_atomic_store(a.dp_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }

@@ -95,14 +95,30 @@ class NativeFeed:
                                 -1.0 if self.idle_timeout_s is None else float(self.idle_timeout_s), parts)
         return f, client, parts
 
-    def _finish(self, f, client, parts, t0: float) -> None:
+    @staticmethod
+    def _consumed(f, slab: int, marks: dict) -> None:
+        """The consumer asked for the next slab: everything this one carried has been used."""
+        for pi, pos in f.slab_marks(int(slab)):
+            marks[int(pi)] = max(marks.get(int(pi), -1), int(pos))
+
+    def _finish(self, f, client, parts, t0: float, marks: dict, exhausted: bool) -> None:
+        """Commit (``commit=True``) at-least-once positions: the decode positions of the
+        workers when the stream was drained to its end (``exhausted``), otherwise -- early
+        stop, ``take``, an exception in the consumer -- only the publish-time marks of the
+        slabs the consumer came back from (rows decoded ahead into queued or in-flight
+        slabs are re-read by a resumed run, never skipped)."""
         st = dict(f.stats())
         st["wall_s"] = time.perf_counter() - t0
         st["workers"] = min(self.workers, max(len(parts), 1))
+        st["committed"] = "end" if exhausted else "consumed-slabs"
         self.last_stats = st
-        if self.commit:
-            for (topic, partition, _, _), pos in zip(parts, f.positions()):
-                client.commit(self.group, topic, partition, int(pos))
+        if not self.commit:
+            return
+        final = f.positions() if exhausted else None
+        for pi, (topic, partition, start, _) in enumerate(parts):
+            pos = int(final[pi]) if final is not None else marks.get(pi, -1)
+            if pos > start or (final is not None and pos >= start):
+                client.commit(self.group, topic, partition, pos)
 
     # ------------------------------------------------------------------ host
     def host_chunks(self, keep_label: Optional[int] = None, slab_rows: int = 65536,
@@ -114,21 +130,27 @@ class NativeFeed:
         bufs = [np.empty(slab_rows * (F * 4 + 1), np.uint8) for _ in range(nslots)]
         t0 = time.perf_counter()
         f.start([int(b.ctypes.data) for b in bufs], int(slab_rows))
+        marks: dict = {}
+        exhausted = False
         try:
             while True:
                 code, slab, n = f.pop(1000)
                 if code < 0:
+                    exhausted = True
                     break
                 if code == 0:
                     continue
                 b = bufs[slab]
                 rows = b[:n * F * 4].view(np.float32).reshape(n, F).copy()
                 labs = b[n * F * 4:n * F * 4 + n].copy()
+                mk = f.slab_marks(slab)
                 f.recycle(slab)
                 yield rows, labs
+                for pi, pos in mk:
+                    marks[int(pi)] = max(marks.get(int(pi), -1), int(pos))
         finally:
             f.stop()
-            self._finish(f, client, parts, t0)
+            self._finish(f, client, parts, t0, marks, exhausted)
 
     def count_rows(self, keep_label: Optional[int] = None) -> int:
         return sum(len(r) for r, _ in self.host_chunks(keep_label))
@@ -158,6 +180,8 @@ class NativeFeed:
         f.start([int(ring.host_ptr(i)) for i in range(nslots)], int(slab_rows))
         pending: collections.deque = collections.deque()
         done = False
+        exhausted = False
+        marks: dict = {}
         h2d_bytes = 0
         try:
             while pending or not done:
@@ -179,14 +203,16 @@ class NativeFeed:
                 slab, n = pending.popleft()
                 ring.wait(slab)
                 yield bufs[slab][:n * F * 4].view(torch.float32).view(n, F)
+                self._consumed(f, slab, marks)
                 ring.release(slab)          # the consumer's kernels for this slab are enqueued
                 ring.host_ptr(slab)         # its H2D copy has landed: the host slab is free
                 f.recycle(slab)
+            exhausted = True
         finally:
             f.stop()
             while pending:                  # drain copies that were submitted but not consumed
                 slab, _ = pending.popleft()
                 ring.wait(slab)
                 ring.release(slab)
-            self._finish(f, client, parts, t0)
+            self._finish(f, client, parts, t0, marks, exhausted)
             self.last_stats["h2d_bytes"] = h2d_bytes

@@ -34,7 +34,7 @@ class DistEnv:
 
     @property
     def is_dist(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.backend is not None
 
     @property
     def is_main(self) -> bool:
@@ -44,7 +44,9 @@ class DistEnv:
 def init_from_env(device_type: Optional[str] = None, timeout_s: Optional[int] = None) -> DistEnv:
     """Initialise the process group from torchrun's RANK/WORLD_SIZE/LOCAL_RANK.
 
-    Single-process runs (no WORLD_SIZE or WORLD_SIZE=1) do not create a group.
+    Single-process runs (no WORLD_SIZE or WORLD_SIZE=1) do not create a group, unless
+    ``SML_FORCE_PG=1`` asks for one at world 1 (TCP rendezvous on MASTER_ADDR/PORT,
+    defaulting to 127.0.0.1 and a free port).
     ``device_type`` defaults to ``cuda`` (ROCm) when available, else ``cpu``.
     """
     if timeout_s is None:   # collective watchdog: a dead / hung peer raises instead of hanging
@@ -65,8 +67,11 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: Optional[int] = 
     else:
         device = torch.device("cpu")
         backend = "gloo"
-    if world > 1 and not dist.is_initialized():
+    force = os.environ.get("SML_FORCE_PG") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(free_port())
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
         if restart is not None and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
@@ -79,12 +84,27 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: Optional[int] = 
             kw["device_id"] = device
         dist.init_process_group(**kw)
     return DistEnv(rank=rank, world_size=world, local_rank=local, device=device,
-                   backend=backend if world > 1 else None)
+                   backend=backend if (world > 1 or force) else None)
+
+
+def free_port() -> int:
+    """An unused TCP port on 127.0.0.1 (rendezvous for a self-launched or forced group)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def _pg_active() -> bool:
+    """A process group exists: torchrun with WORLD_SIZE > 1, or one forced at world 1
+    (``SML_FORCE_PG=1``: the whole DP path -- RCCL communicator, collectives, P2P
+    exchange -- on a single GPU, so it is exercised even where only one device exists)."""
+    return dist.is_available() and dist.is_initialized()
 
 
 def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
     """In-place SUM all-reduce of one flat bucket (no-op without a process group)."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _pg_active():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         ENGINE.allreduce_calls.inc()
         ENGINE.allreduce_bytes.inc(t.numel() * t.element_size())
@@ -92,14 +112,14 @@ def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
 
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _pg_active():
         dist.broadcast(t, src=src)
     return t
 
 
 def sync_model_from_rank0(model) -> None:
     """Broadcast rank 0's parameters AND optimizer state to every replica (after init / load)."""
-    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+    if not (_pg_active()):
         return
     fp = getattr(model, "fp", None)
     if fp is not None and getattr(model, "_fused", None) is None:
@@ -139,7 +159,7 @@ def agree(values, device: torch.device, ops=None):
     """Element-wise collective agreement on small ints (default MIN): every rank returns the
     same list.  One all-reduce (no-op without a process group)."""
     vals = [int(v) for v in values]
-    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+    if not (_pg_active()):
         return vals
     ops = ops or ["min"] * len(vals)
     out = []
@@ -153,7 +173,7 @@ def agree(values, device: torch.device, ops=None):
 
 
 def allreduce_max(value: float, device: torch.device) -> float:
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _pg_active():
         t = torch.tensor([value], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
@@ -162,7 +182,7 @@ def allreduce_max(value: float, device: torch.device) -> float:
 
 def reduce_metrics(metrics: dict, device: torch.device, weight_key: str = "rows") -> dict:
     """Row-weighted average of per-replica epoch metrics (one small all-reduce per epoch)."""
-    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+    if not (_pg_active()):
         return dict(metrics)
     keys = [k for k in metrics if k != weight_key]
     w = float(metrics.get(weight_key, 1.0))
@@ -175,7 +195,7 @@ def reduce_metrics(metrics: dict, device: torch.device, weight_key: str = "rows"
 
 
 def barrier(device: Optional[torch.device] = None) -> None:
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _pg_active():
         if device is not None and device.type == "cuda" and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[device.index])
         else:

@@ -125,6 +125,10 @@ class P2PGroup:
         restart from an older iteration (new model, restored checkpoint) re-zeroes the
         receive buffers first, behind a barrier on both sides, so no stale granule of the
         earlier run can match a new tag."""
+        from ..ops.ae import NPARAM
+        if int(self.x.slots) < NPARAM:   # the trainer strides peer buffers by NPARAM floats
+            raise ValueError(f"P2P exchange built with {int(self.x.slots)} slots; the persistent trainer needs "
+                             f">= {NPARAM}")
         if start_iter <= self._last_iter:
             self._reset()
         return dict(dp_peers=int(self.x.peers_ptr), dp_ranks=self.world, dp_rank0=0 if self.in_launch else self.rank,

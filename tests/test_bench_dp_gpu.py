@@ -1,6 +1,8 @@
-"""bench.py's multi-rank path on the GPU box (one GPU): two torchrun ranks share
-GPU 0 and all-reduce over gloo (``SML_SHARE_GPU0=1``; RCCL refuses two ranks on
-one device).  Exercises exactly the code the driver's 2/4/8-GPU scaling run
+"""bench.py's multi-rank path on the GPU box (one GPU).
+
+``test_bench_two_ranks_shared_gpu``: the driver's plain ``python3 bench.py --gpus 2``
+self-launches two torchrun ranks as a child process; they share GPU 0 and all-reduce
+over gloo (``SML_SHARE_GPU0=1``; RCCL refuses two ranks on one device).  Exercises exactly the code the driver's 2/4/8-GPU scaling run
 executes -- shard-by-key data, broadcast, per-step flat-bucket all-reduce,
 barrier-bracketed timing, max-over-ranks -- and checks that the replicas end
 bit-identical and rank 0 prints one well-formed JSON line.
@@ -29,10 +31,11 @@ def _free_port():
 def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
     env = dict(os.environ, SML_SHARE_GPU0="1", OMP_NUM_THREADS="2")
     dump = str(tmp_path / "params")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+    # no torchrun prefix: bench.py must launch its own ranks (the driver runs it this way)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "4", "--warmup", "2", "--batch-per-gpu", "65536",
-           "--dataset-rows", "262144", "--infer-events", "0", "--dump-params", dump]
+           "--dataset-rows", "262144", "--infer-events", "2000", "--infer-repeats", "1", "--e2e-events", "0",
+           "--lstm-steps", "0", "--batch32-steps", "2000", "--dump-params", dump]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -41,6 +44,9 @@ def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
     assert out["n_gpus"] == 2 and out["steps"] == 4 and out["warmup"] == 2
     assert out["config"]["global_batch"] == 2 * 65536 and out["config"]["parallelism"] == "dp2"
     assert out["value"] > 0 and np.isfinite(out["final_epoch_loss"])
+    assert out["backend"] == "gloo" and len(out["per_rank_ms_per_step"]["ranks"]) == 2
+    # config 5 per replica: both ranks scored their own shard
+    assert len(out["infer_per_replica_p50_us"]) == 2 and all(v > 0 for v in out["infer_per_replica_p50_us"])
     coll = out["small_allreduce"]
     assert coll["bucket_bytes"] == 6144 and coll["backend_allreduce_us"] > 0 and coll["p2p_allreduce_us"] > 0, coll
     assert out["keras_batch32_dp"]["replicas_identical"] is True, out["keras_batch32_dp"]
@@ -52,3 +58,35 @@ def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
     p0 = np.load(dump + ".rank0.npy")
     p1 = np.load(dump + ".rank1.npy")
     np.testing.assert_array_equal(p0, p1)
+
+
+@pytest.mark.gpu
+def test_bench_force_pg_rccl_world1(cuda_device):
+    """The whole DP bench path on ONE RCCL rank (SML_FORCE_PG=1): nccl communicator,
+    per-step all-reduce in the timed loop, P2P exchange + in-kernel DP, collectives."""
+    env = dict(os.environ, SML_FORCE_PG="1", OMP_NUM_THREADS="2")
+    env.pop("SML_SHARE_GPU0", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "4", "--warmup", "2",
+           "--batch-per-gpu", "65536", "--dataset-rows", "262144", "--infer-events", "1000", "--infer-repeats", "1",
+           "--e2e-events", "0", "--lstm-steps", "0", "--batch32-steps", "2000", "--fit-rows", "0",
+           "--stream-rows", "0", "--dp-steps", "2000", "--collective-iters", "50"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["n_gpus"] == 1 and out["backend"] == "nccl", out
+    assert out["small_allreduce"]["backend"] == "nccl" and out["small_allreduce"]["backend_allreduce_us"] > 0
+    assert out["small_allreduce"]["p2p_allreduce_us"] > 0, out["small_allreduce"]
+    assert out["keras_batch32_dp"]["replicas_identical"] is True, out["keras_batch32_dp"]
+
+
+def test_bench_refuses_missing_gpus():
+    """--gpus N with fewer visible GPUs (none here) exits non-zero instead of measuring fewer."""
+    env = dict(os.environ)
+    for k in ("SML_SHARE_GPU0", "WORLD_SIZE"):
+        env.pop(k, None)
+    import torch
+    n = torch.cuda.device_count()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(max(n + 1, 2)), "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode == 2, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "visible" in r.stderr and not r.stdout.strip()

@@ -96,6 +96,31 @@ def test_feed_commits_positions():
     assert cl.committed("g1", "C", 0) == 600 and cl.committed("g1", "C", 1) == 600
 
 
+def test_feed_early_stop_commits_only_consumed_slabs():
+    """At-least-once: stopping after the first slab commits that slab's publish-time
+    position, never the workers' decode-ahead positions; a resumed run reads the rest."""
+    from streamml.kafka.feed import NativeFeed
+    b = fake_broker("feed-early")
+    b.create_topic("E", 1)
+    codec = AvroCodec("cardata-v1")
+    c = next(iter(S.synthetic(5000, chunk=5000, seed=5)))
+    buf, offs = encode_chunk(codec, c.x, c.label)
+    b.append_buffer("E", 0, buf, offs)
+    feed = NativeFeed("fake://feed-early", ["E:0:0"], codec, list(range(18)), group="g", commit=True,
+                      resume=True)
+    it = feed.host_chunks(slab_rows=1000, slots=4)
+    first, _ = next(it)          # the workers decode ahead into the other slots meanwhile
+    next(it)                     # coming back for slab 1 marks slab 0 consumed
+    it.close()                   # the consumer stops while slab 1 is in its hands
+    cl = KafkaClient("fake://feed-early")
+    assert cl.committed("g", "E", 0) == 1000, cl.committed("g", "E", 0)
+    assert feed.last_stats["committed"] == "consumed-slabs"
+    rest = sum(len(r) for r, _ in feed.host_chunks(slab_rows=1000))   # resumes at the commit
+    assert rest == 4000 and feed.last_stats["committed"] == "end"
+    assert cl.committed("g", "E", 0) == 5000
+    np.testing.assert_array_equal(first, c.x[:1000].astype(np.float32))
+
+
 def test_feed_malformed_records_become_nan_missing():
     b = fake_broker("feed-bad")
     b.create_topic("M", 1)
