@@ -52,6 +52,10 @@ def parse():
                    help="offered events/s per replica (scenario.xml: 100 000 cars x 1 msg / 10 s)")
     p.add_argument("--e2e-events", type=int, default=20000,
                    help="events of the Kafka append -> scored result latency run on rank 0 (0 = skip)")
+    p.add_argument("--fit-epochs", type=int, default=10,
+                   help="epochs of the Autoencoder.fit(engine='throughput') measurement at the headline batch (0 = skip)")
+    p.add_argument("--fresh-steps", type=int, default=10,
+                   help="steps of the fresh-rows measurement: pack B new raw rows + train them, per step (0 = skip)")
     p.add_argument("--lstm-steps", type=int, default=20,
                    help="timed steps of the seq-50 LSTM side measurement, BASELINE config 3 (0 = skip)")
     p.add_argument("--fleet-models", type=int, default=1024,
@@ -247,6 +251,61 @@ def measure_stream_e2e(device, rows, batch=100):
                                           dp="none")   # rank 0 alone, as measure_fit
 
 
+def measure_fit_large_batch(data, device, batch, epochs=10, shuffle=False, seed=0):
+    """The throughput engine through the real entry point: ``Autoencoder.fit(x, batch_size=B,
+    engine="throughput")`` on the HBM-resident rows (each epoch tile-packed once -- a fused
+    gather + pack when shuffled -- then every batch on the headline kernel).  Rank 0 alone."""
+    import torch
+
+    from streamml.models.autoencoder import Autoencoder
+    m = Autoencoder(device=device, input_normalizer="cardata", seed=seed)
+    m.compile()
+    m.fit(data, epochs=1, batch_size=batch, shuffle=shuffle, verbose=0, engine="throughput", dp="none")  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    h = m.fit(data, epochs=epochs, batch_size=batch, shuffle=shuffle, verbose=0, engine="throughput", dp="none",
+              initial_epoch=0)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    rows = (data.size(0) // batch) * batch * epochs
+    return {"rows_per_s": rows / dt, "epochs": epochs, "batch": batch, "rows_per_epoch": data.size(0),
+            "shuffle": shuffle, "engine": m.last_fit_engine, "loss": h.history["loss"][-1], "dtype": "bf16",
+            "ms_per_step": dt / (rows // batch) * 1e3}
+
+
+def measure_fresh_rows(spec, data, device, batch, steps, scale, shift, seed=0):
+    """Every step trains rows never seen before: K8 packs the step's B raw rows (normalize_fn +
+    argmax + tile layout) and the headline kernel trains them -- the per-row cost of fresh
+    ingest on the device, against the headline's multi-epoch replay of a packed ring."""
+    import torch
+
+    from streamml.models.reference import init_dense_weights
+    from streamml.ops.ae import FusedAE
+    ae = FusedAE(spec, init_dense_weights(spec.layer_sizes, seed=seed), device, scale=scale, shift=shift)
+    nsl = data.size(0) // batch
+
+    def one(k):
+        ae.pack_ring(data[(k % nsl) * batch:(k % nsl + 1) * batch], batch)
+        ae.step_ring()
+
+    for k in range(2):
+        one(k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        one(k)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # the pack alone, same slices
+    t1 = time.perf_counter()
+    for k in range(steps):
+        ae.pack_ring(data[(k % nsl) * batch:(k % nsl + 1) * batch], batch)
+    torch.cuda.synchronize()
+    dp_ = time.perf_counter() - t1
+    return {"rows_per_s": batch * steps / dt, "ms_per_step": dt / steps * 1e3, "pack_ms_per_step": dp_ / steps * 1e3,
+            "pack_tb_s": batch * (72 + 73) / (dp_ / steps) / 1e12, "steps": steps, "batch": batch}
+
+
 def measure_batch32_fleet(spec, data, device, steps, scale, shift, n_models=1024, launches=3):
     """The same Keras batch-32 semantics for a fleet of independent models (one per car /
     device group), one workgroup each (ops/ae_fleet.py): aggregate rows/s over the fleet."""
@@ -425,6 +484,13 @@ def main():
         if args.dp_steps > 0:
             b32_dp = (guarded(measure_batch_dp, spec, data, device, args.dp_steps, scale, shift, args.seed, world,
                               group=p2p) if p2p is not None else {"error": f"P2P exchange unavailable: {p2p_err!r}"})
+    fit_large = fresh = None
+    if rank == 0 and args.fit_epochs > 0:
+        fit_large = guarded(measure_fit_large_batch, data, device, B, epochs=args.fit_epochs)
+        fit_large["shuffled"] = guarded(measure_fit_large_batch, data, device, B, epochs=max(args.fit_epochs // 2, 1),
+                                        shuffle=True)
+    if rank == 0 and args.fresh_steps > 0:
+        fresh = guarded(measure_fresh_rows, spec, data, device, B, args.fresh_steps, scale, shift)
     fit100 = stream = None
     if rank == 0 and args.fit_rows > 0:
         fit100 = guarded(measure_fit, device, args.fit_rows)
@@ -482,6 +548,10 @@ def main():
             "keras_batch32": b32,
             "keras_batch32_dp": b32_dp,
             "small_allreduce": coll,
+            "fit_large_batch_rows_per_s": None if not fit_large or "error" in fit_large else fit_large["rows_per_s"],
+            "fit_large_batch": fit_large,
+            "fresh_rows_per_s": None if not fresh or "error" in fresh else fresh["rows_per_s"],
+            "fresh_rows": fresh,
             "fit_batch100_rows_per_s": None if not fit100 or "error" in fit100 else fit100["rows_per_s"],
             "fit_batch100": fit100,
             "stream_e2e_rows_per_s": None if not stream or "error" in stream else stream["rows_per_s"],

@@ -76,9 +76,11 @@ hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, con
                                  int IN, int U, int act, int dh_last_only, int64_t x_seq, hipStream_t stream);
 
 // tile-packed training ring: per 16-row tile the normalised rows (x * scale + shift, 64*D
-// bytes) then their 16 argmax bytes; out holds n/16 * (64*D + 16) bytes (n % 16 == 0)
+// bytes) then their 16 argmax bytes; out holds n/16 * (64*D + 16) bytes (n % 16 == 0).
+// index (optional, n int64): packed row r is x[index[r]] (a shuffle fused into the pack)
 hipError_t pack_tiles_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale,
-                                    const float* shift, uint8_t* out, hipStream_t stream);
+                                    const float* shift, uint8_t* out, hipStream_t stream,
+                                    const int64_t* index = nullptr);
 // argmax (lowest index on ties) of each normalised row x * scale + shift over D features
 hipError_t row_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale, const float* shift,
                              uint8_t* out, hipStream_t stream);
@@ -133,6 +135,39 @@ struct ServeResult {
 hipError_t ae_serve_launch(ServeCtl* ctl, const ServeReq* req, ServeResult* res, int nslots, const float* wts,
                            const float* scale, const float* shift, const int* dims, const int* acts, float threshold,
                            double idle_seconds, hipStream_t stream);
+
+// ---- persistent per-event LSTM scorer (lstm_serve.hip): same rings as ae_serve ----
+// request word 31 carries the car key (uint32 payload); result words [0, D) the forecast of
+// the key's next event, kServeScore the MSE of this event against the key's previous
+// forecast, kServeFlag 0 normal / 1 anomaly / 2 no forecast yet (fewer than T + 1 events)
+enum : int { LS_LSTM = 0, LS_REPEAT = 1, LS_DENSE = 2, LS_MAXLAYERS = 8 };
+struct LstmServeLayer {
+  int kind;            // LS_*
+  int in, u;           // input width, units (Dense: output width)
+  int act, ret, n;     // LSTM activation code, return_sequences; RepeatVector n
+  int woff, uoff, boff;   // float offsets of kernel / recurrent kernel / bias in the weights
+};
+struct LstmServeArgs {
+  ServeCtl* ctl;
+  const ServeReq* req;
+  ServeResult* res;
+  int nslots;
+  const float* wts;
+  int nw;
+  int nl;
+  LstmServeLayer L[LS_MAXLAYERS];
+  const float* scale;
+  const float* shift;
+  int D, T;
+  float* hist;         // [nkeys][T][D] per-key window ring (device)
+  int* hcount;         // [nkeys] events seen per key
+  float* lastpred;     // [nkeys][D] the key's latest forecast
+  int nkeys;
+  float threshold;
+  uint64_t idle_ticks;
+};
+size_t lstm_serve_lds_bytes(int nw);
+hipError_t lstm_serve_launch(const LstmServeArgs& args, hipStream_t stream);
 
 // ---- fused MSE + categorical accuracy (loss.hip) ----
 bool mse_acc_supported(int F);

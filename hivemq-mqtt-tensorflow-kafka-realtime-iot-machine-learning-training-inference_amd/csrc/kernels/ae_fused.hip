@@ -1677,6 +1677,13 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
       const char* e = std::getenv("SML_AE_XPROBE");
       return e ? std::atoi(e) : 0;
     }();
+    // A caller that passes a tile-packed ring may have packed it from rows other than x's (an
+    // epoch's shuffle fused into the pack: FusedAE.pack_ring); only the XM 1 variants read it,
+    // so refuse to silently train on x when none of them applies.
+    const bool xpack_used = xa_ok && ring_ok && D == 18 &&
+                            (train_ilp() == 2 || (((n >> 4) & 1) == 0 && train_ilp() == 3 && dims[1] <= 15 &&
+                                                  dims[2] <= 7 && dims[3] <= 7) || occ == 4);
+    if (xpack != nullptr && !xpack_used && probe < 2) return hipErrorInvalidValue;
     if (ring_ok && occ == 4 && D == 18 && want_acc && probe == 2)
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18, 2>), gd, bd, 0, stream, a);
     else if (ring_ok && occ == 4 && D == 18 && want_acc && probe == 3)

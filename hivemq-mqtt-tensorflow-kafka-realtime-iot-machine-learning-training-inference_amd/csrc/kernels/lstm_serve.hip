@@ -1,0 +1,318 @@
+// Persistent per-event LSTM scorer (BASELINE config 3 model, served like config 5).
+//
+// The reference LSTM job predicts each next car event from a window of the last
+// `look_back` events and streams the predictions through a Python OutputCallback
+// (LSTM-TensorFlow-IO-Kafka/cardata-v2.py:220-273).  Here one resident workgroup polls
+// the host-mapped request ring exactly like the autoencoder scorer (ae_serve.hip: LL
+// framed slots, no launch and no hipMemcpy per event) and keeps, on the device, the last
+// T normalised events of every car key (a per-key ring in HBM: 100 000 cars x 50 x 18
+// floats = 360 MB of 288 GB) plus the key's previous prediction.  Per event:
+//   1. append the event to its key's window;
+//   2. score it: mean squared error against the prediction made at the key's previous
+//      event (the LSTM's own anomaly signal: how far the car moved from its forecast);
+//   3. once T events are known, run the whole stack (LSTM layers, RepeatVector, Dense /
+//      TimeDistributed head) over the window from zero state -- Keras' stateless
+//      semantics, as the model was trained -- and emit the forecast of the next event.
+//
+// Execution: 4 waves.  An LSTM step is z = [x_t ; h] . [W ; U] + b for 4u <= 128 gates:
+// wave w owns gates 32w..32w+31, lane half k (lane >> 5) one 32-long half of the
+// concatenated input, with its 32 weights in registers (every layer's, loaded once at
+// launch); the two halves meet through a permlane32 swap, the gates through LDS, and
+// threads t < u update unit t's cell state in a register.  Two workgroup barriers per
+// step.  Weights, biases, the window and the activations live in LDS.
+//
+// Exit conditions every wave reaches: the host's stop flag or `idle` without a request
+// (decided by wave 0, broadcast through LDS at the next barrier).
+#include "sml_common.h"
+#include "sml_ops.h"
+#include "sml_serve_dev.h"
+
+namespace sml {
+namespace {
+
+using namespace serve_dev;
+
+constexpr int NT = 256;
+constexpr int MAXW = 32;       // widest layer input / output
+constexpr int MAXT = 64;       // longest window
+constexpr int MAXLSTM = 4;     // LSTM layers with register-resident weights
+constexpr int KEY_WORD = 31;   // request word carrying the car key
+
+__device__ __forceinline__ float sigm(float z) { return 1.0f / (1.0f + __expf(-z)); }
+__device__ __forceinline__ float act_lstm(int a, float z) { return a == ACT_RELU ? fmaxf(z, 0.f) : tanhf(z); }
+
+struct Smem {
+  float* w;       // all parameters, Keras order
+  float* seqa;    // [MAXT][MAXW]
+  float* seqb;    // [MAXT][MAXW]
+  float* v;       // [64]: [x_t ; h]
+  float* z;       // [128] gate pre-activations
+  float* pred;    // [MAXW]
+  float* xrow;    // [MAXW]
+  float* sc;      // [MAXW]
+  float* sh;      // [MAXW]
+  int* ctl;       // [4]: quit, key, count
+};
+
+__global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem_f[];
+  Smem S;
+  S.w = smem_f;
+  const int nwp = (a.nw + 3) & ~3;
+  S.seqa = S.w + nwp;
+  S.seqb = S.seqa + MAXT * MAXW;
+  S.v = S.seqb + MAXT * MAXW;
+  S.z = S.v + 64;
+  S.pred = S.z + 128;
+  S.xrow = S.pred + MAXW;
+  S.sc = S.xrow + MAXW;
+  S.sh = S.sc + MAXW;
+  S.ctl = reinterpret_cast<int*>(S.sh + MAXW);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int half = lane >> 5;
+  const int gate = wid * 32 + (lane & 31);
+  const int D = a.D, T = a.T;
+  for (int i = tid; i < a.nw; i += NT) S.w[i] = a.wts[i];
+  for (int i = tid; i < MAXW; i += NT) {
+    S.sc[i] = (i < D && a.scale) ? a.scale[i] : 1.f;
+    S.sh[i] = (i < D && a.shift) ? a.shift[i] : 0.f;
+  }
+  __syncthreads();
+  // register-resident weight halves of every LSTM layer: k = 32 * half + i of [W ; U]
+  float wr[MAXLSTM][32], br[MAXLSTM];
+  {
+    int li = 0;
+    for (int l = 0; l < a.nl; ++l) {
+      const LstmServeLayer& L = a.L[l];
+      if (L.kind != LS_LSTM) continue;
+#pragma unroll
+      for (int q = 0; q < MAXLSTM; ++q) {
+        if (q != li) continue;
+        const int G = 4 * L.u;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          const int k = 32 * half + i;
+          float wv = 0.f;
+          if (gate < G) {
+            if (k < L.in) wv = S.w[L.woff + k * G + gate];
+            else if (k - L.in < L.u) wv = S.w[L.uoff + (k - L.in) * G + gate];
+          }
+          wr[q][i] = wv;
+        }
+        br[q] = gate < G ? S.w[L.boff + gate] : 0.f;
+      }
+      ++li;
+    }
+  }
+
+  uint64_t tail = ld_sys(&a.ctl->done);
+  uint64_t last = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0) st_sys32(&a.ctl->alive, 1u);
+  for (;;) {
+    // ---------------- wave 0 polls the next request slot (ae_serve.hip's pipelined poll)
+    const int slot = (int)(tail % (uint64_t)a.nslots);
+    const uint32_t want = (uint32_t)(tail + 1);
+    uint64_t t_seen = 0;
+    if (wid == 0) {
+      const uint64_t* wp = &a.req[slot].w[lane & 31];
+      const uint64_t* hp = &a.ctl->head;
+      uint64_t w0, h0, w1, h1, w2, h2, wv = 0;
+      poll_issue(w0, h0, wp, hp);
+      __builtin_amdgcn_s_sleep(8);
+      poll_issue(w1, h1, wp, hp);
+      __builtin_amdgcn_s_sleep(8);
+      poll_issue(w2, h2, wp, hp);
+      auto ready = [&](uint64_t w) {
+        const bool ok = (lane >= D && lane != KEY_WORD) || lane >= 32 || (uint32_t)(w >> 32) == want;
+        return __ballot(ok) == ~0ull;
+      };
+      int quit = 0;
+      for (uint32_t it = 0;; ++it) {
+        asm volatile("s_waitcnt vmcnt(4)" : "+v"(w0), "+v"(h0)::"memory");
+        if (ready(w0)) { wv = w0; break; }
+        poll_issue(w0, h0, wp, hp);
+        asm volatile("s_waitcnt vmcnt(4)" : "+v"(w1), "+v"(h1)::"memory");
+        if (ready(w1)) { wv = w1; break; }
+        poll_issue(w1, h1, wp, hp);
+        asm volatile("s_waitcnt vmcnt(4)" : "+v"(w2), "+v"(h2)::"memory");
+        if (ready(w2)) { wv = w2; break; }
+        poll_issue(w2, h2, wp, hp);
+        if ((it & 63) == 63) {
+          if (ld_sys32(&a.ctl->stop) || __builtin_amdgcn_s_memrealtime() - last > a.idle_ticks) {
+            quit = 1;
+            break;
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(w0), "+v"(h0), "+v"(w1), "+v"(h1), "+v"(w2), "+v"(h2)::"memory");
+      t_seen = __builtin_amdgcn_s_memrealtime();
+      if (lane < D) S.xrow[lane] = fmaf(__uint_as_float((uint32_t)wv), S.sc[lane], S.sh[lane]);
+      if (lane == KEY_WORD) S.ctl[1] = (int)(uint32_t)wv;
+      if (lane == 0) S.ctl[0] = quit;
+    }
+    __syncthreads();
+    if (S.ctl[0]) break;
+    int key = S.ctl[1];
+    key = key < 0 ? 0 : (key >= a.nkeys ? a.nkeys - 1 : key);   // the host validates; never leave the table
+    float* hist = a.hist + (int64_t)key * T * D;
+    float* lastp = a.lastpred + (int64_t)key * D;
+    const int cnt = a.hcount[key];   // events of this key before this one
+    // ---------------- append the event, score it against the previous forecast
+    float err = 0.f;
+    if (tid < D) {
+      const float xn = S.xrow[tid];
+      hist[(cnt % T) * D + tid] = xn;
+      if (cnt >= T) {
+        const float d = xn - lastp[tid];
+        err = d * d;
+      }
+    }
+    if (wid == 0) err = wave_sum(err);
+    const bool full = cnt + 1 >= T;
+    __syncthreads();   // hist row written (workgroup-scope global visibility)
+    // ---------------- the window, oldest first, into seqa [t][k]
+    if (full) {
+      for (int e = tid; e < T * D; e += NT) {
+        const int t = e / D, k = e - t * D;
+        S.seqa[t * MAXW + k] = hist[((cnt + 1 - T + t) % T) * D + k];
+      }
+    }
+    __syncthreads();
+    if (full) {
+      float* cur = S.seqa;
+      float* nxt = S.seqb;
+      int tcur = T, dim = D, li = 0;
+      for (int l = 0; l < a.nl; ++l) {
+        const LstmServeLayer& L = a.L[l];
+        if (L.kind == LS_LSTM) {
+          const int I = L.in, u = L.u, G = 4 * u;
+          float c = 0.f, h = 0.f;
+          if (tid < u) S.v[I + tid] = 0.f;
+          for (int t = 0; t < tcur; ++t) {
+            if (tid < I) S.v[tid] = cur[t * MAXW + tid];
+            __syncthreads();
+            float s = 0.f;
+#pragma unroll
+            for (int q = 0; q < MAXLSTM; ++q) {
+              if (q != li) continue;
+              const float4* v4 = reinterpret_cast<const float4*>(S.v + 32 * half);
+#pragma unroll
+              for (int i4 = 0; i4 < 8; ++i4) {
+                const float4 vv = v4[i4];
+                s = fmaf(vv.x, wr[q][4 * i4 + 0], s);
+                s = fmaf(vv.y, wr[q][4 * i4 + 1], s);
+                s = fmaf(vv.z, wr[q][4 * i4 + 2], s);
+                s = fmaf(vv.w, wr[q][4 * i4 + 3], s);
+              }
+              s += xor32(s, lane) + br[q];
+            }
+            if (half == 0 && gate < G) S.z[gate] = s;
+            __syncthreads();
+            if (tid < u) {
+              const float ig = sigm(S.z[tid]), fg = sigm(S.z[u + tid]);
+              const float gg = act_lstm(L.act, S.z[2 * u + tid]), og = sigm(S.z[3 * u + tid]);
+              c = fmaf(fg, c, ig * gg);
+              h = og * act_lstm(L.act, c);
+              S.v[I + tid] = h;
+              if (L.ret) nxt[t * MAXW + tid] = h;
+            }
+          }
+          if (!L.ret && tid < u) nxt[tid] = h;
+          tcur = L.ret ? tcur : 1;
+          dim = u;
+          ++li;
+        } else if (L.kind == LS_REPEAT) {
+          for (int e = tid; e < L.n * dim; e += NT) {
+            const int t = e / dim, k = e - t * dim;
+            nxt[t * MAXW + k] = cur[k];   // cur holds one vector (the previous layer's h_T)
+          }
+          tcur = L.n;
+        } else {   // dense / TimeDistributed(Dense): only the last step is the forecast
+          const int U = L.u;
+          if (tid < U) {
+            float acc = S.w[L.boff + tid];
+            const float* xin = cur + (tcur - 1) * MAXW;
+            for (int k = 0; k < dim; ++k) acc = fmaf(xin[k], S.w[L.woff + k * U + tid], acc);
+            nxt[(tcur - 1) * MAXW + tid] = acc;
+            if (l == a.nl - 1) S.pred[tid] = acc;
+          }
+          dim = U;
+        }
+        __syncthreads();
+        float* tmp = cur;
+        cur = nxt;
+        nxt = tmp;
+      }
+    }
+    const uint64_t t_comp = __builtin_amdgcn_s_memrealtime();
+    // ---------------- results (wave 0), the key's state, completion counter
+    if (wid == 0) {
+      ServeResult* r = a.res + slot;
+      const float p = (full && lane < D) ? S.pred[lane] : 0.f;
+      if (lane < D) {
+        st_sys(&r->w[lane], tagged(want, p));
+        if (full) lastp[lane] = p;
+      }
+      if (lane == 0) {
+        const float score = cnt >= T ? err / (float)D : __builtin_nanf("");
+        const uint32_t flag = cnt >= T ? (score > a.threshold ? 1u : 0u) : 2u;
+        a.hcount[key] = cnt + 1;
+        st_sys(&r->w[kServeScore], tagged(want, score));
+        st_sys(&r->w[kServeFlag], tagged_u(want, flag));
+        st_sys(&r->w[kServeTLoad], tagged_u(want, 0u));
+        st_sys(&r->w[kServeTComp], tagged_u(want, (uint32_t)(t_comp - t_seen)));
+        st_sys(&r->w[kServeTDone], tagged_u(want, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seen)));
+        st_sys(&a.ctl->done, tail + 1);
+      }
+    }
+    tail += 1;
+    last = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();   // key state stored before the next event may read it
+  }
+  __syncthreads();
+  wait_stores();
+  if (tid == 0) st_sys32(&a.ctl->alive, 0u);
+}
+
+}  // namespace
+
+size_t lstm_serve_lds_bytes(int nw) {
+  const int nwp = (nw + 3) & ~3;
+  return (size_t)(nwp + 2 * MAXT * MAXW + 64 + 128 + 4 * MAXW) * sizeof(float) + 4 * sizeof(int);
+}
+
+hipError_t lstm_serve_launch(const LstmServeArgs& args, hipStream_t stream) {
+  // shape contract of the kernel (also checked by the host class): every layer fits
+  if (args.D < 1 || args.D > 31 || args.T < 1 || args.T > MAXT || args.nl < 1 || args.nl > LS_MAXLAYERS ||
+      args.nslots < 64 || args.nkeys < 1)
+    return hipErrorInvalidValue;
+  int nlstm = 0, dim = args.D, tlen = args.T;
+  for (int l = 0; l < args.nl; ++l) {
+    const LstmServeLayer& L = args.L[l];
+    if (L.kind == LS_LSTM) {
+      if (L.in != dim || L.u < 1 || L.u > 32 || L.in > 32 || ++nlstm > MAXLSTM) return hipErrorInvalidValue;
+      dim = L.u;
+      tlen = L.ret ? tlen : 1;
+    } else if (L.kind == LS_REPEAT) {
+      if (tlen != 1 || L.n < 1 || L.n > MAXT) return hipErrorInvalidValue;
+      tlen = L.n;
+    } else if (L.kind == LS_DENSE) {
+      if (L.in != dim || L.u < 1 || L.u > MAXW) return hipErrorInvalidValue;
+      dim = L.u;
+    } else {
+      return hipErrorInvalidValue;
+    }
+  }
+  if (args.L[args.nl - 1].kind != LS_DENSE || dim != args.D) return hipErrorInvalidValue;
+  const size_t lds = lstm_serve_lds_bytes(args.nw);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_serve_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(lstm_serve_kernel, dim3(1), dim3(NT), lds, stream, args);
+  return hipGetLastError();
+}
+
+}  // namespace sml

@@ -67,10 +67,14 @@ __device__ __forceinline__ int argmax_row(const float* row, int Drt) {
 // Stage rows [r0, r0 + nrows) of x (row stride ld) into LDS as normalised fp32, flat [row][D].
 // CONTIG (ld == D, x 16-byte aligned, r0 * D a multiple of 4): float4 loads; the per-position
 // scale table has 4 * ceil(...) entries indexed by the flat position modulo the table period.
+// Generic path (strided rows, or rows gathered through `index`: row r of the group is
+// x[index[r0 + r]], e.g. an epoch's shuffle permutation fused into the pack): one element per
+// lane, consecutive lanes on consecutive columns of a row.
 template <int DT, bool CONTIG>
 __device__ __forceinline__ void stage_rows(const float* __restrict__ x, int64_t r0, int nrows, int64_t ld, int Drt,
                                            const float* s_sc, const float* s_sh, int period, float* stage, int lane,
-                                           float* __restrict__ out_stream, int64_t out_chunk0, int tile_chunks) {
+                                           float* __restrict__ out_stream, int64_t out_chunk0, int tile_chunks,
+                                           const int64_t* __restrict__ index = nullptr) {
   const int D = DT > 0 ? DT : Drt;
   const int nflt = nrows * D;
   if (CONTIG) {
@@ -98,7 +102,8 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ x, int64_t 
   } else {
     for (int e = lane; e < nflt; e += 64) {
       const int r = e / D, col = e - r * D;
-      stage[e] = fmaf(x[(r0 + r) * ld + col], s_sc[col], s_sh[col]);
+      const int64_t src = index ? index[r0 + r] : r0 + r;
+      stage[e] = fmaf(x[src * ld + col], s_sc[col], s_sh[col]);
     }
     if (out_stream) {
       wave_lds_sync();
@@ -128,7 +133,8 @@ template <int DT, bool CONTIG, int MODE>
 __global__ __launch_bounds__(kThreads) void rows_group_kernel(const float* __restrict__ x, int64_t n, int64_t ld,
                                                               int Drt, const float* __restrict__ scale,
                                                               const float* __restrict__ shift,
-                                                              uint8_t* __restrict__ out) {
+                                                              uint8_t* __restrict__ out,
+                                                              const int64_t* __restrict__ index) {
   const int D = DT > 0 ? DT : Drt;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int period = 4 * D;
@@ -146,7 +152,7 @@ __global__ __launch_bounds__(kThreads) void rows_group_kernel(const float* __res
     const int nrows = (int)imin64(kRowsPerGroup, n - r0);
     float* ostream = MODE == 0 ? reinterpret_cast<float*>(out) : nullptr;
     stage_rows<DT, CONTIG>(x, r0, nrows, ld, D, s_sc, s_sh, period, stage, lane, ostream,
-                           (r0 >> 4) * (int64_t)(tile_chunks + 1), tile_chunks);
+                           (r0 >> 4) * (int64_t)(tile_chunks + 1), tile_chunks, index);
     wave_lds_sync();
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -182,18 +188,24 @@ int stream_grid(int64_t groups_of_waves) {
 
 template <int MODE>
 hipError_t launch_rows_group(const float* x, int64_t n, int64_t ld, int D, const float* scale, const float* shift,
-                             uint8_t* out, hipStream_t stream) {
-  const bool contig = ld == D && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+                             uint8_t* out, hipStream_t stream, const int64_t* index = nullptr) {
+  const bool contig = index == nullptr && ld == D && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   const int64_t groups = (n + kRowsPerGroup - 1) / kRowsPerGroup;
   const dim3 grid(stream_grid(groups)), block(kThreads);
   const size_t lds = rows_group_lds(D);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (D == 18 && contig)
-    hipLaunchKernelGGL((rows_group_kernel<18, true, MODE>), grid, block, lds, stream, x, n, ld, D, scale, shift, out);
+    hipLaunchKernelGGL((rows_group_kernel<18, true, MODE>), grid, block, lds, stream, x, n, ld, D, scale, shift, out,
+                       index);
   else if (contig)
-    hipLaunchKernelGGL((rows_group_kernel<0, true, MODE>), grid, block, lds, stream, x, n, ld, D, scale, shift, out);
+    hipLaunchKernelGGL((rows_group_kernel<0, true, MODE>), grid, block, lds, stream, x, n, ld, D, scale, shift, out,
+                       index);
+  else if (D == 18)
+    hipLaunchKernelGGL((rows_group_kernel<18, false, MODE>), grid, block, lds, stream, x, n, ld, D, scale, shift, out,
+                       index);
   else
-    hipLaunchKernelGGL((rows_group_kernel<0, false, MODE>), grid, block, lds, stream, x, n, ld, D, scale, shift, out);
+    hipLaunchKernelGGL((rows_group_kernel<0, false, MODE>), grid, block, lds, stream, x, n, ld, D, scale, shift, out,
+                       index);
   return hipGetLastError();
 }
 
@@ -349,11 +361,11 @@ hipError_t normalize_filter_launch(const float* x, int64_t n, int64_t ld, int D,
 }
 
 hipError_t pack_tiles_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale,
-                                    const float* shift, uint8_t* out, hipStream_t stream) {
+                                    const float* shift, uint8_t* out, hipStream_t stream, const int64_t* index) {
   if (n <= 0) return hipSuccess;
   if ((n & 15) || D < 1 || D > 64) return hipErrorInvalidValue;
   if (reinterpret_cast<uintptr_t>(out) & 15) return hipErrorInvalidValue;
-  return launch_rows_group<0>(x, n, ld, D, scale, shift, out, stream);
+  return launch_rows_group<0>(x, n, ld, D, scale, shift, out, stream, index);
 }
 
 hipError_t row_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale, const float* shift,

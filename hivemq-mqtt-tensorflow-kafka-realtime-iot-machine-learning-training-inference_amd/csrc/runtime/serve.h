@@ -19,16 +19,18 @@
 
 namespace sml {
 
-class AEServe {
+// The host-mapped request / result rings and the relaunch-on-demand protocol shared by the
+// persistent scorers; a subclass supplies the kernel launch.
+class ServeRing {
  public:
-  AEServe(int device, int nslots, const std::vector<float>& weights, const int dims[3], const int acts[4],
-          const std::vector<float>& scale, const std::vector<float>& shift, float threshold, double idle_seconds);
-  ~AEServe();
-  AEServe(const AEServe&) = delete;
-  AEServe& operator=(const AEServe&) = delete;
+  ServeRing(int device, int nslots, int D, double idle_seconds);
+  virtual ~ServeRing();
+  ServeRing(const ServeRing&) = delete;
+  ServeRing& operator=(const ServeRing&) = delete;
 
-  // Publish k rows of D floats; returns the sequence number of the first one.
-  uint64_t submit(const float* rows, int k);
+  // Publish k rows of D floats (keys: optional per-row uint32 in request word 31);
+  // returns the sequence number of the first one.
+  uint64_t submit(const float* rows, int k, const uint32_t* keys = nullptr);
   // Block until the results of the events in [seq_end - nslots, seq_end) have landed
   // (throws after timeout_s).
   void wait(uint64_t seq_end, double timeout_s);
@@ -39,21 +41,22 @@ class AEServe {
   uint32_t word(uint64_t seq, int i) const;
   float score(uint64_t seq) const;
   // submit + wait + copy scores / flags (/ recon) for k rows.
-  void infer(const float* rows, int k, float* scores, uint32_t* flags, float* recon, double timeout_s);
+  void infer(const float* rows, int k, float* scores, uint32_t* flags, float* recon, double timeout_s,
+             const uint32_t* keys = nullptr);
   // Per-event latency (ns) of n events submitted one at a time, spaced by gap_ns.
   // Also fills dev_ns[i] (device pick-up -> stores issued, if non-null) and counts relaunches.
-  std::vector<int64_t> latency_run(const float* rows, int n, int64_t gap_ns, std::vector<int64_t>* dev_ns = nullptr);
+  std::vector<int64_t> latency_run(const float* rows, int n, int64_t gap_ns, std::vector<int64_t>* dev_ns = nullptr,
+                                   const uint32_t* keys = nullptr);
   void stop();
   int D() const { return D_; }
   uint64_t launches() const { return launches_; }
 
- private:
+ protected:
+  virtual hipError_t launch_kernel() = 0;
   void launch();
   // back-pressure: block until the device consumed every event < n (its request slot is free)
   void wait_done(uint64_t n, double timeout_s);
   int device_, nslots_, D_;
-  int dims_[3], acts_[4];
-  float threshold_;
   double idle_s_;
   ServeCtl* ctl_ = nullptr;
   ServeReq* req_ = nullptr;
@@ -61,13 +64,52 @@ class AEServe {
   ServeCtl* ctl_d_ = nullptr;
   ServeReq* req_d_ = nullptr;
   ServeResult* res_d_ = nullptr;
-  float* wts_d_ = nullptr;
-  float* scale_d_ = nullptr;
-  float* shift_d_ = nullptr;
   hipStream_t stream_ = nullptr;
   uint64_t head_ = 0;
   uint64_t launches_ = 0;
   uint64_t complete_ = 0;   // events known complete (prefix)
+  const char* name_ = "serve";
+};
+
+// Dense autoencoder scorer (ae_serve.hip): reconstruction + MSE anomaly score per event.
+class AEServe : public ServeRing {
+ public:
+  AEServe(int device, int nslots, const std::vector<float>& weights, const int dims[3], const int acts[4],
+          const std::vector<float>& scale, const std::vector<float>& shift, float threshold, double idle_seconds);
+  ~AEServe() override;
+
+ protected:
+  hipError_t launch_kernel() override;
+
+ private:
+  int dims_[3], acts_[4];
+  float threshold_;
+  float* wts_d_ = nullptr;
+  float* scale_d_ = nullptr;
+  float* shift_d_ = nullptr;
+};
+
+// LSTM forecaster (lstm_serve.hip): per car key, the last T events stay on the device; each
+// event is scored against the key's previous forecast and a new forecast is emitted.
+class LSTMServe : public ServeRing {
+ public:
+  // layers: LstmServeLayer descriptors (offsets into weights); keys in [0, nkeys)
+  LSTMServe(int device, int nslots, const std::vector<float>& weights, const std::vector<LstmServeLayer>& layers,
+            int D, int T, int nkeys, const std::vector<float>& scale, const std::vector<float>& shift, float threshold,
+            double idle_seconds);
+  ~LSTMServe() override;
+  int nkeys() const { return args_.nkeys; }
+  // forget every key's window and forecast (device memset; the kernel must be idle or stopped)
+  void reset_keys();
+
+ protected:
+  hipError_t launch_kernel() override;
+
+ private:
+  LstmServeArgs args_{};
+  float* wts_d_ = nullptr;
+  float* scale_d_ = nullptr;
+  float* shift_d_ = nullptr;
 };
 
 }  // namespace sml

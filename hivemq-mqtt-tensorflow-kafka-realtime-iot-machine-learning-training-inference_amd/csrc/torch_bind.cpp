@@ -119,16 +119,44 @@ int64_t ae_train_partials(const at::Tensor& x, const c10::optional<at::Tensor>& 
 }
 
 // ingest-time tile-packed ring: per 16-row tile the rows then the 16 argmax bytes
+// index (optional int64 [m]): pack rows x[index[0..m)] instead of x[0..n); out (optional): an
+// existing byte buffer of at least the packed size (e.g. a slice of a ring being refilled)
 at::Tensor pack_tiles_argmax(const at::Tensor& x, int64_t D, const c10::optional<at::Tensor>& scale,
-                             const c10::optional<at::Tensor>& shift) {
+                             const c10::optional<at::Tensor>& shift, const c10::optional<at::Tensor>& index,
+                             const c10::optional<at::Tensor>& out_opt) {
   check_dev(x, "x", at::kFloat);
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(1) >= D && D >= 1 && D <= 255 && x.size(0) % 16 == 0,
-              "x must be [n, >=D] with n a multiple of 16");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(1) >= D && D >= 1 && D <= 64,
+              "x must be [n, >=D] with D <= 64");
   TORCH_CHECK(scale.has_value() == shift.has_value(), "scale and shift go together");
+  if (scale.has_value()) TORCH_CHECK(scale->numel() >= D && shift->numel() >= D, "scale/shift too short");
+  int64_t n = x.size(0);
+  const int64_t* idx = nullptr;
+  if (index.has_value() && index->defined()) {
+    TORCH_CHECK(index->is_cuda() && index->device() == x.device() && index->scalar_type() == at::kLong &&
+                    index->dim() == 1 && index->is_contiguous(), "index must be a contiguous int64 device vector");
+    n = index->numel();
+    // the kernel trusts the indices: bounds-check on the device before launching it
+    if (n > 0) {
+      const auto mm = at::aminmax(*index);
+      TORCH_CHECK(std::get<0>(mm).item<int64_t>() >= 0 && std::get<1>(mm).item<int64_t>() < x.size(0),
+                  "index out of range for x");
+    }
+    idx = index->data_ptr<int64_t>();
+  }
+  TORCH_CHECK(n % 16 == 0, "packed rows must be a multiple of 16");
+  const int64_t bytes = n / 16 * (64 * D + 16);
   c10::hip::HIPGuard guard(x.device().index());
-  auto out = at::empty({x.size(0) / 16 * (64 * D + 16)}, x.options().dtype(at::kByte));
-  SML_CHECK_HIP(sml::pack_tiles_argmax_launch(x.data_ptr<float>(), x.size(0), x.stride(0), (int)D, opt_ptr(scale),
-                                              opt_ptr(shift), out.data_ptr<uint8_t>(), cur_stream(x)));
+  at::Tensor out;
+  if (out_opt.has_value() && out_opt->defined()) {
+    out = *out_opt;
+    TORCH_CHECK(out.is_cuda() && out.device() == x.device() && out.scalar_type() == at::kByte && out.is_contiguous() &&
+                    out.numel() >= bytes && (reinterpret_cast<uintptr_t>(out.data_ptr()) & 15) == 0,
+                "out must be a contiguous, 16-byte aligned uint8 device buffer of >= the packed size");
+  } else {
+    out = at::empty({bytes}, x.options().dtype(at::kByte));
+  }
+  SML_CHECK_HIP(sml::pack_tiles_argmax_launch(x.data_ptr<float>(), n, x.stride(0), (int)D, opt_ptr(scale),
+                                              opt_ptr(shift), out.data_ptr<uint8_t>(), cur_stream(x), idx));
   return out;
 }
 
@@ -800,13 +828,18 @@ struct RingPy {
 // Python face of the persistent scorer: numpy in / numpy out, GIL released while
 // the host thread spins on the completion counter.
 struct ServePy {
-  std::unique_ptr<sml::AEServe> s;
+  std::unique_ptr<sml::ServeRing> s;
+  ServePy() = default;
   // C ABI for the host-only streaming loop in _io (sml_scorer_api.h)
   SmlScorerApi api{};
   std::string err;
   static int api_infer(void* ctx, const float* rows, int k, float* scores, uint32_t* flags, float* recon,
                        double timeout_s) {
     auto* self = static_cast<ServePy*>(ctx);
+    if (self->nkeys() > 0) {   // the C loop carries no car keys
+      self->err = "a keyed (LSTM) scorer cannot serve the key-less C scoring loop";
+      return 1;
+    }
     try {
       self->s->infer(rows, k, scores, flags, recon, timeout_s);
       return 0;
@@ -840,10 +873,30 @@ struct ServePy {
     s = std::make_unique<sml::AEServe>(device, nslots, w, dims.data(), acts.data(), sc, sh, (float)threshold,
                                        idle_seconds);
   }
+  // optional per-row uint32 keys (the LSTM scorer's car keys), validated against nkeys
+  static std::vector<uint32_t> keys_of(const py::object& keys, ssize_t n, int64_t nkeys) {
+    std::vector<uint32_t> out;
+    if (keys.is_none()) {
+      if (nkeys > 0) throw std::invalid_argument("this scorer needs one key per row");
+      return out;
+    }
+    auto k = keys.cast<py::array_t<int64_t, py::array::c_style | py::array::forcecast>>();
+    if (k.ndim() != 1 || k.shape(0) != n) throw std::invalid_argument("keys must be [k] integers, one per row");
+    out.resize((size_t)n);
+    for (ssize_t i = 0; i < n; ++i) {
+      const int64_t v = k.data()[i];
+      if (v < 0 || (nkeys > 0 && v >= nkeys) || v > 0xffffffffLL) throw std::out_of_range("key outside [0, nkeys)");
+      out[(size_t)i] = (uint32_t)v;
+    }
+    return out;
+  }
+  virtual int64_t nkeys() const { return 0; }
+  virtual ~ServePy() = default;
   py::tuple infer(py::array_t<float, py::array::c_style | py::array::forcecast> rows, bool want_recon,
-                  double timeout_s) {
+                  double timeout_s, py::object keys) {
     if (rows.ndim() != 2 || rows.shape(1) != s->D()) throw std::invalid_argument("rows must be [k, D]");
     const int k = (int)rows.shape(0);
+    const std::vector<uint32_t> kv = keys_of(keys, k, nkeys());
     py::array_t<float> scores(k);
     py::array_t<uint32_t> flags(k);
     py::array_t<float> recon(want_recon ? std::vector<ssize_t>{k, s->D()} : std::vector<ssize_t>{0});
@@ -853,18 +906,19 @@ struct ServePy {
     float* pr = want_recon ? recon.mutable_data() : nullptr;
     {
       py::gil_scoped_release rel;
-      s->infer(src, k, ps, pf, pr, timeout_s);
+      s->infer(src, k, ps, pf, pr, timeout_s, kv.empty() ? nullptr : kv.data());
     }
     return py::make_tuple(scores, flags, recon);
   }
   // -> int64 [n, 2]: host round-trip ns, device processing ns
   py::array_t<int64_t> latency_run(py::array_t<float, py::array::c_style | py::array::forcecast> rows,
-                                   int64_t gap_ns) {
+                                   int64_t gap_ns, py::object keys) {
     if (rows.ndim() != 2 || rows.shape(1) != s->D()) throw std::invalid_argument("rows must be [n, D]");
+    const std::vector<uint32_t> kv = keys_of(keys, rows.shape(0), nkeys());
     std::vector<int64_t> lat, dev;
     {
       py::gil_scoped_release rel;
-      lat = s->latency_run(rows.data(), (int)rows.shape(0), gap_ns, &dev);
+      lat = s->latency_run(rows.data(), (int)rows.shape(0), gap_ns, &dev, kv.empty() ? nullptr : kv.data());
     }
     // columns: host round trip, device total, device load, device compute (ns)
     py::array_t<int64_t> out(std::vector<ssize_t>{(ssize_t)lat.size(), 4});
@@ -879,6 +933,32 @@ struct ServePy {
   }
 };
 
+// layers: list of (kind, in, u, act, ret, n, woff, uoff, boff) tuples (sml::LstmServeLayer)
+struct LSTMServePy : ServePy {
+  int64_t nk = 0;
+  LSTMServePy(int device, int nslots, py::array_t<float, py::array::c_style | py::array::forcecast> weights,
+              std::vector<std::vector<int>> layers, int D, int T, int nkeys, py::object scale, py::object shift,
+              double threshold, double idle_seconds) {
+    std::vector<float> w(weights.data(), weights.data() + weights.size());
+    std::vector<sml::LstmServeLayer> L;
+    for (const auto& t : layers) {
+      if (t.size() != 9) throw std::invalid_argument("layer descriptor: (kind, in, u, act, ret, n, woff, uoff, boff)");
+      L.push_back(sml::LstmServeLayer{t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7], t[8]});
+    }
+    std::vector<float> sc, sh;
+    if (!scale.is_none()) {
+      auto a = scale.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+      auto b = shift.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+      sc.assign(a.data(), a.data() + a.size());
+      sh.assign(b.data(), b.data() + b.size());
+    }
+    c10::hip::HIPGuard guard(device);
+    s = std::make_unique<sml::LSTMServe>(device, nslots, w, L, D, T, nkeys, sc, sh, (float)threshold, idle_seconds);
+    nk = nkeys;
+  }
+  int64_t nkeys() const override { return nk; }
+};
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -890,7 +970,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dims"), py::arg("acts"), py::arg("l1"), py::arg("want_acc"), py::arg("max_blocks"),
         py::arg("n_rows") = -1, py::arg("cursor") = py::none(), py::arg("xpack") = py::none());
   m.def("pack_tiles_argmax", &pack_tiles_argmax, "tile-packed training ring (rows + ingest-time argmax per tile)",
-        py::arg("x"), py::arg("D"), py::arg("scale") = py::none(), py::arg("shift") = py::none());
+        py::arg("x"), py::arg("D"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
+        py::arg("index") = py::none(), py::arg("out") = py::none());
   m.def("row_argmax_u8", &row_argmax_u8, "ingest-time argmax of each normalised row (uint8)", py::arg("x"),
         py::arg("D"), py::arg("scale") = py::none(), py::arg("shift") = py::none());
   m.def("ae_minibatch_max_batch", &sml::ae_minibatch_max_batch, "largest batch the persistent small-batch trainer takes");
@@ -996,11 +1077,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("device"), py::arg("nslots"), py::arg("weights"), py::arg("dims"), py::arg("acts"),
            py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("threshold") = 5.0,
            py::arg("idle_seconds") = 2.0)
-      .def("infer", &ServePy::infer, py::arg("rows"), py::arg("want_recon") = false, py::arg("timeout_s") = 10.0)
-      .def("latency_run", &ServePy::latency_run, py::arg("rows"), py::arg("gap_ns") = 0)
+      .def("infer", &ServePy::infer, py::arg("rows"), py::arg("want_recon") = false, py::arg("timeout_s") = 10.0,
+           py::arg("keys") = py::none())
+      .def("latency_run", &ServePy::latency_run, py::arg("rows"), py::arg("gap_ns") = 0, py::arg("keys") = py::none())
       .def("stop", [](ServePy& p) { p.s->stop(); })
       .def("c_api", &ServePy::c_api, "address of the SmlScorerApi table (for _io.ScoreLoop)")
       .def_property_readonly("launches", [](ServePy& p) { return p.s->launches(); });
+  py::class_<LSTMServePy, ServePy>(m, "LSTMServe",
+                                   "persistent per-event LSTM forecaster: per-key windows on the device")
+      .def(py::init<int, int, py::array_t<float, py::array::c_style | py::array::forcecast>,
+                    std::vector<std::vector<int>>, int, int, int, py::object, py::object, double, double>(),
+           py::arg("device"), py::arg("nslots"), py::arg("weights"), py::arg("layers"), py::arg("D"), py::arg("T"),
+           py::arg("nkeys"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
+           py::arg("threshold") = 5.0, py::arg("idle_seconds") = 2.0)
+      .def("reset_keys", [](LSTMServePy& p) {
+        p.s->stop();   // the kernel must not run while its state is cleared
+        static_cast<sml::LSTMServe*>(p.s.get())->reset_keys();
+      })
+      .def_property_readonly("nkeys", [](LSTMServePy& p) { return p.nk; });
   m.def("mse_acc", &mse_acc, "fused MSE fwd/bwd + categorical accuracy (K3 + K6)", py::arg("y_pred"), py::arg("y"),
         py::arg("bcast") = 1, py::arg("gscale") = 1.0, py::arg("grad") = py::none(), py::arg("acc") = py::none());
   m.def("mse_acc_supported", &sml::mse_acc_supported, "feature counts with a fused MSE kernel", py::arg("F"));

@@ -163,9 +163,13 @@ class Autoencoder:
         ``engine``: ``"persistent"`` runs every Keras step of an epoch on the persistent
         small-batch kernel (``ae_minibatch.hip``: one launch per up to 16k steps, fp32,
         batch <= 128 -- the reference's batch 32 and cardata-v3's batch 100,
-        cardata-v3.py:176-177, 212-222); ``"launch"`` issues the two-launch fused step
-        (bf16 MFMA train kernel + slab-reduce/Adam) per batch, for any batch size;
-        ``"auto"`` picks ``persistent`` on a single ROCm replica when the batch fits.
+        cardata-v3.py:176-177, 212-222); ``"throughput"`` is the large-batch mode (SURVEY.md
+        7.3 step 7): each epoch's rows -- shuffled by a device permutation fused into the
+        pack -- are tile-packed once (K8: normalize_fn + argmax(x)) and every full batch runs
+        the headline kernel (packed-pair bf16 MFMA train + slab-reduce/Adam, ``step_ring``),
+        the short last batch the plain fused step; ``"launch"`` issues the two-launch fused
+        step per batch with in-kernel normalisation, for any batch size; ``"auto"`` picks
+        ``persistent`` on a single ROCm replica when the batch fits, else ``throughput``.
 
         Under ``torch.distributed`` every rank trains on its own shard: arrays are split
         contiguously by rank, Streams are expected to be rank-sharded already; the global
@@ -212,12 +216,14 @@ class Autoencoder:
             xd = self._to_device(arr) if self.device.type == "cuda" else self._cpu_x(arr)
         from ..parallel.fault import maybe_inject, maybe_inject_range
         persistent = self._use_persistent(engine, batch_size, world, dp)
+        throughput = not persistent and self._use_throughput(engine, batch_size)
         exch, local_k = None, 0
         if persistent and world > 1:
             exch, local_k = self._dp_setup(dp)
             if exch is None and not local_k:
                 persistent = False   # p2p unavailable on some rank: RCCL launch path
-        self.last_fit_engine = "persistent" if persistent else ("launch" if self.device.type == "cuda" else "torch-cpu")
+        self.last_fit_engine = ("persistent" if persistent else "throughput" if throughput else
+                                ("launch" if self.device.type == "cuda" else "torch-cpu"))
         if persistent and world > 1:
             self.last_fit_engine += "+p2p" if exch is not None else f"+local_sgd:{local_k}"
         gstep = int(getattr(self, "_global_step", 0))
@@ -248,6 +254,13 @@ class Autoencoder:
                     steps = self._dp_train(xs[:nb * batch_size], batch_size, exch, local_k)
                 else:
                     steps, _ = be.train_rows(xs[:min(n, nb * batch_size)], batch_size)
+                gstep += steps
+            elif throughput and is_stream:
+                steps = self._fit_stream_throughput(x, batch_size, steps_per_epoch, world, allreduce, gstep, rank)
+                gstep += steps
+            elif throughput:
+                steps = self._fit_array_throughput(xd, batch_size, steps_per_epoch, shuffle, seed, rank, epoch, world,
+                                                   allreduce, gstep)
                 gstep += steps
             elif is_stream:
                 for xb in self._stream_batches(x, batch_size):
@@ -316,9 +329,107 @@ class Autoencoder:
         g.manual_seed((int(seed) * 1_000_003 + int(rank) * 7_919 + int(epoch)) & 0x7FFFFFFFFFFF)
         return torch.randperm(n, generator=g, device=self.device)
 
+    def _use_throughput(self, engine: str, batch_size: int) -> bool:
+        if self.device.type != "cuda":
+            if engine == "throughput":
+                raise ValueError("engine='throughput' needs a ROCm device")
+            return False
+        if engine == "throughput":
+            return True
+        return engine == "auto" and batch_size > self.backend.max_minibatch()
+
+    def _fit_array_throughput(self, xd: torch.Tensor, B: int, steps_per_epoch: Optional[int], shuffle: bool,
+                              seed: int, rank: int, epoch: int, world: int, allreduce, gstep: int) -> int:
+        """One epoch of the throughput engine over a device array: every full batch on the
+        headline kernel from the epoch's tile-packed ring; the last short batch (Keras) on
+        the plain fused step.  Unshuffled epochs reuse the packed ring of the previous one."""
+        from ..parallel.fault import maybe_inject_range
+        be = self.backend
+        n = xd.size(0)
+        nfull = n // B
+        if world > 1:   # every rank runs the same number of full batches; no short batch
+            from ..parallel.dp import agree
+            nfull = agree([nfull], self.device)[0]
+        if steps_per_epoch is not None:
+            nfull = min(nfull, steps_per_epoch)
+        perm = self._device_perm(n, seed, rank, epoch) if shuffle else None
+        maybe_inject_range(gstep, gstep + nfull + 1, rank)
+        steps = 0
+        if nfull:
+            key = (xd.data_ptr(), n, B, nfull)
+            if perm is not None or getattr(self, "_tp_key", None) != key or be.ring_xpack is None:
+                be.pack_ring(xd, B, index=perm[:nfull * B] if perm is not None else None)
+                self._tp_key = None if perm is not None else key
+            else:
+                be.cursor.zero_()
+            for _ in range(nfull):
+                be.step_ring(global_batch=B * world, allreduce=allreduce)
+            steps = nfull
+        rem = n - nfull * B
+        if rem and world == 1 and (steps_per_epoch is None or steps < steps_per_epoch) and n // B == nfull:
+            tail = xd[perm[nfull * B:]] if perm is not None else xd[nfull * B:]
+            be.step(tail.contiguous())
+            steps += 1
+        return steps
+
+    def _fit_stream_throughput(self, stream, B: int, max_steps: Optional[int], world: int, allreduce,
+                               gstep: int, rank: int, pack_batches: int = 8) -> int:
+        """A streaming epoch on the throughput engine: device chunks fill a staging buffer of
+        ``pack_batches`` batches; each round packs the buffer's full batches (K8) and trains
+        them on the headline kernel, carrying the < B leftover rows to the next round, so the
+        batches are exactly ``batch(B)`` over the stream; the final partial batch runs the
+        plain fused step.  Under DP the ranks agree per round on the batch count, and the
+        epoch ends for everyone when any rank's stream is exhausted."""
+        from ..parallel.dp import agree
+        be = self.backend
+        D = self.spec.input_dim
+        cap = B * max(1, int(pack_batches))
+        stage = torch.empty((cap, D), dtype=torch.float32, device=self.device)
+        have, steps = 0, 0
+        it = iter(self._stream_device_chunks(stream))
+        pend, ppos, exhausted = None, 0, False
+        while True:
+            while have < cap:
+                if pend is None or ppos >= pend.size(0):
+                    if exhausted:
+                        break
+                    try:
+                        pend, ppos = next(it), 0
+                    except StopIteration:
+                        pend, exhausted = None, True
+                        break
+                t = min(cap - have, pend.size(0) - ppos)
+                stage[have:have + t].copy_(pend[ppos:ppos + t])
+                have += t
+                ppos += t
+            drained = exhausted and (pend is None or ppos >= pend.size(0))
+            nb = have // B
+            if world > 1:
+                nb, any_done = agree([nb, int(drained)], self.device, ["min", "max"])
+                drained = bool(any_done)
+            if max_steps is not None:
+                nb = min(nb, max_steps - steps)
+            if nb > 0:
+                be.pack_ring(stage[:nb * B], B)
+                for _ in range(nb):
+                    be.step_ring(global_batch=B * world, allreduce=allreduce)
+                steps += nb
+            rest = have - nb * B
+            if rest and nb:
+                stage[:rest].copy_(stage[nb * B:have].clone())
+            have = rest
+            if drained or (max_steps is not None and steps >= max_steps):
+                break
+        if have and world == 1 and (max_steps is None or steps < max_steps):
+            be.step(stage[:have].contiguous())   # Keras' short final batch
+            steps += 1
+        return steps
+
     def _use_persistent(self, engine: str, batch_size: int, world: int, dp: str = "auto") -> bool:
-        if engine not in ("auto", "persistent", "launch"):
-            raise ValueError(f"engine must be auto / persistent / launch, got {engine!r}")
+        if engine not in ("auto", "persistent", "launch", "throughput"):
+            raise ValueError(f"engine must be auto / persistent / throughput / launch, got {engine!r}")
+        if engine == "throughput":
+            return False
         if not (dp in ("auto", "p2p", "rccl", "none") or dp.startswith("local_sgd:")):
             raise ValueError(f"dp must be auto / p2p / rccl / local_sgd:K / none, got {dp!r}")
         if engine == "launch" or self.device.type != "cuda":

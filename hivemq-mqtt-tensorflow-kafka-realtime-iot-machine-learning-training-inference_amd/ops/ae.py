@@ -205,9 +205,48 @@ class FusedAE:
         # gets x's half of the accuracy metric with the tile's own two DMAs and skips the
         # 8-feature x 4-lane argmax of x per tile (profiles/r02/SUMMARY.md).
         self.ring_xpack = None
-        if (self.want_acc and os.environ.get("SML_AE_XPACK", "1") != "0" and ring.size(0) % 16 == 0
-                and batch % 16 == 0 and ring.size(1) == self.spec.input_dim):
+        if self._xpack_ok(ring.size(0), batch) and ring.size(1) == self.spec.input_dim:
             self.ring_xpack = self.C.pack_tiles_argmax(ring, self.spec.input_dim, self.scale, self.shift)
+
+    def _xpack_ok(self, rows: int, batch: int) -> bool:
+        """The tile-packed ring applies: the reference model (D = 18, reference activations,
+        accuracy metric) and whole 16-row tiles -- the train kernels that read it."""
+        return (self.want_acc and os.environ.get("SML_AE_XPACK", "1") != "0" and rows % 16 == 0
+                and batch % 16 == 0 and self.spec.input_dim == 18
+                and tuple(self.spec.activations) == ("tanh", "relu", "tanh", "relu"))
+
+    def pack_ring(self, x: torch.Tensor, batch: int, index: Optional[torch.Tensor] = None,
+                  reuse: bool = True) -> int:
+        """Throughput-mode ring for ``step_ring``: the rows ``x[index]`` (or ``x``), cut to
+        whole batches, packed ONCE into the tile layout (normalize_fn + argmax(x), K8) --
+        the shuffle gather fused into the pack, so an epoch's permutation costs one pass over
+        the rows instead of a gather copy plus a pack.  Returns the number of ring rows
+        (full batches); the caller trains ``rows // batch`` steps with ``step_ring`` and the
+        remainder (Keras' short last batch) with ``step``.  Buffers are reused across epochs."""
+        self._check_x(x)
+        B = int(batch)
+        n = int(index.numel()) if index is not None else int(x.size(0))
+        rows = (n // B) * B
+        if rows == 0:
+            raise ValueError(f"fewer rows ({n}) than one batch ({B})")
+        if not (self._xpack_ok(rows, B) and x.size(1) == self.spec.input_dim):
+            # no packed kernel for this model: materialise the epoch's rows, plain ring
+            src = x[index[:rows]] if index is not None else x[:rows]
+            self.attach_ring(src.contiguous(), B)
+            return rows
+        nbytes = rows // 16 * (64 * self.spec.input_dim + 16)
+        buf = getattr(self, "_pack_buf", None)
+        if not reuse or buf is None or buf.numel() < nbytes:
+            buf = self._pack_buf = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        idx = index[:rows].contiguous() if index is not None else None
+        self.C.pack_tiles_argmax(x if idx is not None else x[:rows], self.spec.input_dim, self.scale, self.shift,
+                                 idx, buf)
+        # the ring tensor only carries the geometry (rows, stride): with a packed ring the
+        # launcher reads the rows from the pack alone and refuses any variant that would not
+        self.ring, self.ring_batch = x[:rows], B
+        self.ring_xpack = buf[:nbytes]
+        self.cursor.zero_()
+        return rows
 
     def step_ring(self, global_batch: Optional[int] = None, allreduce=None) -> None:
         if self.ring is None:

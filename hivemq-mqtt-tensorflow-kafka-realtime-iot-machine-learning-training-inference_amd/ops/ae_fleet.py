@@ -232,6 +232,14 @@ class AEFleet:
         if dp is not None:
             if not dp.in_launch or dp.world != self.n_models:
                 raise ValueError("in-launch data parallelism needs P2PGroup.local(device, n_models)")
+            # the replicas spin-wait for each other inside ONE launch: every workgroup must be
+            # resident at once, or the resident ones wait for ones that never start.  One
+            # workgroup per CU is always resident (the kernel's LDS/VGPR budget admits >= 1),
+            # so cap the replicas at the CU count rather than trusting the occupancy query.
+            cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+            if dp.world > cus:
+                raise ValueError(f"in-launch DP with {dp.world} replicas > {cus} CUs: not all replicas can be "
+                                 "resident at once (use one process per GPU for more ranks)")
             it0 = int(self.iter[0].item())
             kw = dp.kernel_args(it0)
             gscale = 1.0 / (B * dp.world)

@@ -1,0 +1,108 @@
+"""``Autoencoder.fit(engine="throughput")``: the large-batch mode on the headline kernel.
+
+Each epoch's rows are tile-packed once (K8, the epoch's shuffle fused into the pack) and
+every full batch runs the packed-pair bf16 MFMA train kernel + slab-reduce/Adam
+(``FusedAE.step_ring``); Keras' short last batch runs the plain fused step.  The oracle is
+``tests/helpers/bf16_ref.py`` -- gradients with the kernels' bf16 rounding points, Keras
+Adam (eps 1e-7) in float64 -- so the whole epoch's parameter trajectory is checked at
+1e-3 relative (reference job: AUTOENCODER-TensorFlow-IO-Kafka/cardata-v3.py:212-222)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from streamml.data import stream as S
+from streamml.data.cardata import normalize_affine
+from streamml.models.autoencoder import Autoencoder
+
+pytestmark = pytest.mark.gpu
+
+
+def _adam_oracle(w0, xn, batches, lr=1e-3, b1=0.9, b2=0.999, eps=1e-7):
+    """Keras Adam over the given row-index batches of the normalised rows xn (float64)."""
+    from helpers.bf16_ref import ae_bf16_reference
+    w = [torch.as_tensor(a).double() for a in w0]
+    m = [torch.zeros_like(a) for a in w]
+    v = [torch.zeros_like(a) for a in w]
+    sq = ab = rows = 0.0
+    for t, idx in enumerate(batches, start=1):
+        g, (s, a) = ae_bf16_reference(torch.from_numpy(xn[idx]), [x.float().numpy() for x in w])
+        sq, ab, rows = sq + s, ab + a, rows + len(idx)
+        lr_t = lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+        for i in range(len(w)):
+            gi = torch.as_tensor(g[i]).double()
+            m[i] = b1 * m[i] + (1 - b1) * gi
+            v[i] = b2 * v[i] + (1 - b2) * gi * gi
+            w[i] = w[i] - lr_t * m[i] / (v[i].sqrt() + eps)
+    return [a.numpy() for a in w], (sq / 18 + 1e-7 * ab) / rows
+
+
+def _relerr(got, want):
+    a = np.concatenate([np.ravel(x) for x in got]).astype(np.float64)
+    b = np.concatenate([np.ravel(x) for x in want]).astype(np.float64)
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+def _data(n, seed):
+    raw = np.random.default_rng(seed).uniform(0, 40, size=(n, 18)).astype(np.float32)
+    sc, sh = normalize_affine()
+    xn = (raw.astype(np.float64) * np.float32(sc) + np.float32(sh)).astype(np.float32)   # = the kernels' fmaf
+    return raw, xn
+
+
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_fit_throughput_epoch_vs_bf16_reference(cuda_device, shuffle):
+    B, n = 4096, 4096 * 6 + 1000      # 6 packed batches + Keras' short last batch
+    raw, xn = _data(n, 3)
+    m = Autoencoder(device=cuda_device, input_normalizer="cardata", seed=2)
+    w0 = m.get_weights()
+    m.compile()
+    xd = torch.from_numpy(raw).to(cuda_device)
+    h = m.fit(xd, epochs=1, batch_size=B, shuffle=shuffle, seed=9, verbose=0, engine="throughput")
+    assert m.last_fit_engine == "throughput" and m.iterations == 7
+    order = (m._device_perm(n, 9, 0, 0).cpu().numpy() if shuffle else np.arange(n))
+    batches = [order[i:i + B] for i in range(0, n, B)]
+    want, loss = _adam_oracle(w0, xn, batches)
+    assert _relerr(m.get_weights(), want) < 1e-3
+    assert abs(h.history["loss"][-1] - loss) <= 1e-3 * loss
+
+
+def test_fit_throughput_reuses_pack_across_unshuffled_epochs(cuda_device):
+    B, n = 2048, 2048 * 4
+    raw, xn = _data(n, 4)
+    m = Autoencoder(device=cuda_device, input_normalizer="cardata", seed=5)
+    w0 = m.get_weights()
+    m.compile()
+    xd = torch.from_numpy(raw).to(cuda_device)
+    m.fit(xd, epochs=3, batch_size=B, shuffle=False, verbose=0, engine="throughput")
+    assert m.iterations == 12
+    want, _ = _adam_oracle(w0, xn, [np.arange(i, i + B) for _ in range(3) for i in range(0, n, B)])
+    assert _relerr(m.get_weights(), want) < 1e-3
+
+
+def test_fit_throughput_stream_vs_bf16_reference(cuda_device):
+    """A stream whose chunks straddle batches and pack rounds: batch(B) exactly."""
+    B = 1024
+    src = S.synthetic(1024 * 20 + 300, chunk=3001, seed=6)
+    raw = np.concatenate([c.x for c in src])
+    sc, sh = normalize_affine()
+    xn = (raw.astype(np.float64) * np.float32(sc) + np.float32(sh)).astype(np.float32)
+    m = Autoencoder(device=cuda_device, input_normalizer="cardata", seed=7)
+    w0 = m.get_weights()
+    m.compile()
+    m.fit(src, epochs=1, batch_size=B, verbose=0, engine="throughput")
+    n = len(raw)
+    assert m.iterations == -(-n // B)
+    want, _ = _adam_oracle(w0, xn, [np.arange(i, min(i + B, n)) for i in range(0, n, B)])
+    assert _relerr(m.get_weights(), want) < 1e-3
+
+
+def test_fit_auto_picks_throughput_for_large_batches(cuda_device):
+    raw, _ = _data(4096, 8)
+    m = Autoencoder(device=cuda_device, input_normalizer="cardata")
+    m.compile()
+    m.fit(raw, epochs=1, batch_size=1024, verbose=0)
+    assert m.last_fit_engine == "throughput"
+    m.fit(raw, epochs=1, batch_size=100, verbose=0)
+    assert m.last_fit_engine == "persistent"

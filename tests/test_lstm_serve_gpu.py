@@ -1,0 +1,97 @@
+"""Persistent per-event LSTM scorer (csrc/kernels/lstm_serve.hip) vs a float64 torch oracle.
+
+Events of several car keys arrive interleaved; per key the device keeps the last
+``look_back`` normalised events and its latest forecast.  For every event the oracle
+recomputes the key's window from scratch (Keras stateless LSTM semantics, gate order
+i, f, c, o, sigmoid recurrent activation) and checks the forecast, the score against
+the key's previous forecast and the flag (reference: LSTM-TensorFlow-IO-Kafka/
+cardata-v2.py:220-273 streams one prediction per event)."""
+import numpy as np
+import pytest
+import torch
+
+from streamml.data.cardata import normalize_affine
+from streamml.models.lstm import LSTMPredictor
+
+pytestmark = pytest.mark.gpu
+
+
+def _forward64(model, window):
+    """[T, F] normalised window -> forecast [F] (float64 torch, CPU)."""
+    P = [torch.as_tensor(a).double() for a in model.fp.get()]
+    h = torch.as_tensor(window).double()[None]
+    for L in model.layers:
+        if L["kind"] == "lstm":
+            W, U, b = P[L["params"]:L["params"] + 3]
+            u = L["units"]
+            hh = torch.zeros(1, u, dtype=torch.float64)
+            c = torch.zeros(1, u, dtype=torch.float64)
+            act = torch.relu if L["activation"] == "relu" else torch.tanh
+            outs = []
+            for t in range(h.shape[1]):
+                z = h[:, t] @ W + hh @ U + b
+                i, f, g, o = z.split(u, dim=1)
+                c = torch.sigmoid(f) * c + torch.sigmoid(i) * act(g)
+                hh = torch.sigmoid(o) * act(c)
+                outs.append(hh)
+            h = torch.stack(outs, 1) if L["return_sequences"] else hh
+        elif L["kind"] == "repeat":
+            h = h[:, None].expand(1, L["n"], h.shape[-1])
+        else:
+            K, b = P[L["params"]:L["params"] + 2]
+            h = h @ K + b
+    return (h[0, -1] if h.dim() == 3 else h[0]).numpy()
+
+
+@pytest.mark.parametrize("stack,T", [("two_layer", 5), ("reference", 1), ("two_layer", 50), ("reference", 3)])
+def test_lstm_serve_matches_oracle(cuda_device, stack, T):
+    from streamml.ops.serve import LSTMScoringServer
+    ctor = LSTMPredictor.two_layer if stack == "two_layer" else LSTMPredictor.reference
+    m = ctor(look_back=T, device=cuda_device, seed=4)
+    rng = np.random.default_rng(T)
+    nkeys = 7 if T < 10 else 2
+    n = (T + 12) * nkeys + 5
+    keys = rng.integers(0, nkeys, size=n)
+    raw = rng.uniform(0, 40, size=(n, 18)).astype(np.float32)
+    sc, sh = normalize_affine()
+    xn = (raw.astype(np.float64) * np.float32(sc) + np.float32(sh)).astype(np.float32)
+    thr = 0.05
+    with LSTMScoringServer(m, nkeys=nkeys, threshold=thr) as srv:
+        pred, score, flag = srv.forecast(raw, keys)
+    hist = {k: [] for k in range(nkeys)}
+    last = {}
+    checked = 0
+    for i in range(n):
+        k = int(keys[i])
+        cnt = len(hist[k])
+        if cnt >= T:
+            want = float(np.mean((xn[i].astype(np.float64) - last[k]) ** 2))
+            assert abs(score[i] - want) <= 2e-3 * max(want, 1e-3), (i, score[i], want)
+            assert flag[i] == (1 if want > thr else 0) or abs(want - thr) < 1e-5
+        else:
+            assert flag[i] == 2 and np.isnan(score[i])
+        hist[k].append(xn[i])
+        if len(hist[k]) >= T:
+            f = _forward64(m, np.stack(hist[k][-T:]))
+            np.testing.assert_allclose(pred[i], f, rtol=2e-4, atol=2e-5)
+            last[k] = f
+            checked += 1
+        else:
+            assert not pred[i].any()
+    assert checked >= 5 * nkeys
+
+
+def test_lstm_serve_latency_and_reset(cuda_device):
+    from streamml.ops.serve import LSTMScoringServer
+    m = LSTMPredictor.two_layer(look_back=50, device=cuda_device)
+    rng = np.random.default_rng(1)
+    rows = rng.uniform(0, 40, size=(600, 18)).astype(np.float32)
+    keys = np.zeros(600, np.int64)
+    with LSTMScoringServer(m, nkeys=10) as srv:
+        lat = srv.latency_us(rows, keys, qps=20000)
+        assert lat.shape == (600,) and np.all(lat > 0)
+        srv.reset()
+        _, s, f = srv.forecast(rows[:3], keys[:3])
+        assert np.all(f == 2)
+        with pytest.raises(Exception):
+            srv.forecast(rows[:1], np.array([10]))   # keys are validated on the host
