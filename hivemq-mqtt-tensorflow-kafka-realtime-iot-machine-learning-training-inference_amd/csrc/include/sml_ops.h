@@ -77,10 +77,15 @@ hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, con
 
 // tile-packed training ring: per 16-row tile the normalised rows (x * scale + shift, 64*D
 // bytes) then their 16 argmax bytes; out holds n/16 * (64*D + 16) bytes (n % 16 == 0).
-// index (optional, n int64): packed row r is x[index[r]] (a shuffle fused into the pack)
+// index (optional, n int64): packed row r is x[index[r]]; perm_n > 0: packed row r is
+// x[perm_row(r, perm_n, perm_key)], a keyed bijection of [0, perm_n) (an epoch's shuffle
+// fused into the pack with no permutation array)
 hipError_t pack_tiles_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale,
                                     const float* shift, uint8_t* out, hipStream_t stream,
-                                    const int64_t* index = nullptr);
+                                    const int64_t* index = nullptr, uint64_t perm_key = 0, int64_t perm_n = 0);
+// out[i] = perm_row(start + i, n, key): the same bijection, materialised (short batches, tests)
+hipError_t perm_indices_launch(int64_t* out, int64_t start, int64_t count, int64_t n, uint64_t key,
+                               hipStream_t stream);
 // argmax (lowest index on ties) of each normalised row x * scale + shift over D features
 hipError_t row_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale, const float* shift,
                              uint8_t* out, hipStream_t stream);

@@ -46,6 +46,60 @@ __device__ __forceinline__ int64_t imax64(int64_t a, int64_t b) { return a > b ?
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+}  // namespace
+
+namespace sml {
+// Keyed pseudo-random bijection of [0, n) (a balanced 4-round Feistel network over the
+// smallest even-bit domain >= n, cycle-walked back into range): an epoch's shuffle as a
+// function of the row number, so a packed epoch needs no permutation array, no sort and no
+// index reads.  The same function serves the host (FusedAE.perm_indices) and the kernels.
+__host__ __device__ __forceinline__ uint64_t perm_mix(uint64_t z) {   // splitmix64 finaliser
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t perm_apply(uint64_t v, uint64_t key, int half) {
+  const uint64_t mask = (1ull << half) - 1ull;
+  uint64_t L = v >> half, R = v & mask;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t F = perm_mix(R ^ (key + 0x9E3779B97F4A7C15ull * (uint64_t)(i + 1))) & mask;
+    const uint64_t t = L ^ F;
+    L = R;
+    R = t;
+  }
+  return (L << half) | R;
+}
+__host__ __device__ __forceinline__ int64_t perm_row(int64_t r, int64_t n, uint64_t key, int half) {
+  uint64_t v = perm_apply((uint64_t)r, key, half);
+  while (v >= (uint64_t)n) v = perm_apply(v, key, half);   // cycle walk: a bijection on [0, n)
+  return (int64_t)v;
+}
+int perm_half_bits(int64_t n) {
+  int b = 2;
+  while (b < 62 && (1ll << b) < n) b += 2;
+  return b / 2;
+}
+}  // namespace sml
+
+namespace {
+
+// Where packed row r comes from: r itself, index[r], or the keyed bijection perm_row(r).
+struct RowSource {
+  const int64_t* index;
+  uint64_t key;
+  int64_t pn;
+  int half;   // > 0: permutation
+  __device__ __forceinline__ bool gather() const { return index != nullptr || half > 0; }
+  __device__ __forceinline__ int64_t operator()(int64_t r) const {
+    if (index) return index[r];
+    if (half > 0) return sml::perm_row(r, pn, key, half);
+    return r;
+  }
+};
+
 // argmax over D normalised values of one LDS-resident row: ties to the lowest index, NaN
 // never wins (the same comparison order as the training kernels' metric)
 template <int DT>
@@ -74,7 +128,8 @@ template <int DT, bool CONTIG>
 __device__ __forceinline__ void stage_rows(const float* __restrict__ x, int64_t r0, int nrows, int64_t ld, int Drt,
                                            const float* s_sc, const float* s_sh, int period, float* stage, int lane,
                                            float* __restrict__ out_stream, int64_t out_chunk0, int tile_chunks,
-                                           const int64_t* __restrict__ index = nullptr) {
+                                           const RowSource& src = RowSource{nullptr, 0, 0, 0},
+                                           int64_t* s_src = nullptr, bool vec2 = false) {
   const int D = DT > 0 ? DT : Drt;
   const int nflt = nrows * D;
   if (CONTIG) {
@@ -100,10 +155,34 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ x, int64_t 
       stage[e] = fmaf(src[e], s_sc[col], s_sh[col]);
     }
   } else {
-    for (int e = lane; e < nflt; e += 64) {
-      const int r = e / D, col = e - r * D;
-      const int64_t src = index ? index[r0 + r] : r0 + r;
-      stage[e] = fmaf(x[src * ld + col], s_sc[col], s_sh[col]);
+    if (src.gather()) {
+      // source rows first (index reads / bijection once per row, into LDS), then the row
+      // loads all independent: many in flight per lane
+      for (int r = lane; r < nrows; r += 64) s_src[r] = src(r0 + r);
+      wave_lds_sync();
+      if (DT > 0 && (DT & 1) == 0 && vec2) {   // 8-byte aligned rows: D / 2 float2 loads each
+        constexpr int H = DT / 2;
+        const int nv = nrows * H;
+#pragma unroll 4
+        for (int c = lane; c < nv; c += 64) {
+          const int r = c / H, seg = c - r * H;
+          const float2 v = *reinterpret_cast<const float2*>(x + s_src[r] * ld + 2 * seg);
+          const int col = 2 * seg;
+          *reinterpret_cast<float2*>(stage + r * D + col) =
+              make_float2(fmaf(v.x, s_sc[col], s_sh[col]), fmaf(v.y, s_sc[col + 1], s_sh[col + 1]));
+        }
+      } else {
+#pragma unroll 4
+        for (int e = lane; e < nflt; e += 64) {
+          const int r = e / D, col = e - r * D;
+          stage[e] = fmaf(x[s_src[r] * ld + col], s_sc[col], s_sh[col]);
+        }
+      }
+    } else {
+      for (int e = lane; e < nflt; e += 64) {
+        const int r = e / D, col = e - r * D;
+        stage[e] = fmaf(x[(r0 + r) * ld + col], s_sc[col], s_sh[col]);
+      }
     }
     if (out_stream) {
       wave_lds_sync();
@@ -133,16 +212,19 @@ template <int DT, bool CONTIG, int MODE>
 __global__ __launch_bounds__(kThreads) void rows_group_kernel(const float* __restrict__ x, int64_t n, int64_t ld,
                                                               int Drt, const float* __restrict__ scale,
                                                               const float* __restrict__ shift,
-                                                              uint8_t* __restrict__ out,
-                                                              const int64_t* __restrict__ index) {
+                                                              uint8_t* __restrict__ out, RowSource src,
+                                                              int vec2) {
   const int D = DT > 0 ? DT : Drt;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int period = 4 * D;
   float* s_sc = reinterpret_cast<float*>(smem);
   float* s_sh = s_sc + period;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float* stage = s_sh + period + wid * (kRowsPerGroup * D + 32);   // + 128 argmax bytes
+  // per wave: the staged rows | 128 argmax bytes | 128 source-row indices
+  const int srcw = src.gather() ? 2 * kRowsPerGroup : 0;   // contiguous packs keep 4 blocks per CU
+  float* stage = s_sh + period + wid * (kRowsPerGroup * D + 32 + srcw);
   uint8_t* s_arg = reinterpret_cast<uint8_t*>(stage + kRowsPerGroup * D);
+  int64_t* s_src = reinterpret_cast<int64_t*>(stage + kRowsPerGroup * D + 32);
   load_tables(s_sc, s_sh, period, D, scale, shift);
   __syncthreads();
   const int tile_chunks = 4 * D;   // float4s of one 16-row tile
@@ -152,7 +234,7 @@ __global__ __launch_bounds__(kThreads) void rows_group_kernel(const float* __res
     const int nrows = (int)imin64(kRowsPerGroup, n - r0);
     float* ostream = MODE == 0 ? reinterpret_cast<float*>(out) : nullptr;
     stage_rows<DT, CONTIG>(x, r0, nrows, ld, D, s_sc, s_sh, period, stage, lane, ostream,
-                           (r0 >> 4) * (int64_t)(tile_chunks + 1), tile_chunks, index);
+                           (r0 >> 4) * (int64_t)(tile_chunks + 1), tile_chunks, src, s_src, vec2 != 0);
     wave_lds_sync();
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -178,7 +260,9 @@ __global__ __launch_bounds__(kThreads) void rows_group_kernel(const float* __res
   }
 }
 
-size_t rows_group_lds(int D) { return (size_t)(8 * D + kWaves * (kRowsPerGroup * D + 32)) * sizeof(float); }
+size_t rows_group_lds(int D, bool gather) {
+  return (size_t)(8 * D + kWaves * (kRowsPerGroup * D + 32 + (gather ? 2 * kRowsPerGroup : 0))) * sizeof(float);
+}
 
 int stream_grid(int64_t groups_of_waves) {
   // enough waves for every CU to keep ~8 groups in flight; grid-stride beyond that
@@ -188,25 +272,49 @@ int stream_grid(int64_t groups_of_waves) {
 
 template <int MODE>
 hipError_t launch_rows_group(const float* x, int64_t n, int64_t ld, int D, const float* scale, const float* shift,
-                             uint8_t* out, hipStream_t stream, const int64_t* index = nullptr) {
-  const bool contig = index == nullptr && ld == D && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+                             uint8_t* out, hipStream_t stream, RowSource src = RowSource{nullptr, 0, 0, 0}) {
+  const bool gather = src.index != nullptr || src.half > 0;
+  const bool contig = !gather && ld == D && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  const int vec2 = (ld & 1) == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0;
   const int64_t groups = (n + kRowsPerGroup - 1) / kRowsPerGroup;
   const dim3 grid(stream_grid(groups)), block(kThreads);
-  const size_t lds = rows_group_lds(D);
+  const size_t lds = rows_group_lds(D, gather);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 65536) {
+    hipError_t e = hipSuccess;
+    if (D == 18 && contig)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(rows_group_kernel<18, true, MODE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    else if (contig)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(rows_group_kernel<0, true, MODE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    else if (D == 18)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(rows_group_kernel<18, false, MODE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    else
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(rows_group_kernel<0, false, MODE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   if (D == 18 && contig)
     hipLaunchKernelGGL((rows_group_kernel<18, true, MODE>), grid, block, lds, stream, x, n, ld, D, scale, shift, out,
-                       index);
+                       src, vec2);
   else if (contig)
     hipLaunchKernelGGL((rows_group_kernel<0, true, MODE>), grid, block, lds, stream, x, n, ld, D, scale, shift, out,
-                       index);
+                       src, vec2);
   else if (D == 18)
     hipLaunchKernelGGL((rows_group_kernel<18, false, MODE>), grid, block, lds, stream, x, n, ld, D, scale, shift, out,
-                       index);
+                       src, vec2);
   else
     hipLaunchKernelGGL((rows_group_kernel<0, false, MODE>), grid, block, lds, stream, x, n, ld, D, scale, shift, out,
-                       index);
+                       src, vec2);
   return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void perm_indices_kernel(int64_t* __restrict__ out, int64_t start, int64_t count,
+                                                           int64_t n, uint64_t key, int half) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < count) out[i] = sml::perm_row(start + i, n, key, half);
 }
 
 // ---------------------------------------------------------------- normalize + filter
@@ -361,11 +469,23 @@ hipError_t normalize_filter_launch(const float* x, int64_t n, int64_t ld, int D,
 }
 
 hipError_t pack_tiles_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale,
-                                    const float* shift, uint8_t* out, hipStream_t stream, const int64_t* index) {
+                                    const float* shift, uint8_t* out, hipStream_t stream, const int64_t* index,
+                                    uint64_t perm_key, int64_t perm_n) {
   if (n <= 0) return hipSuccess;
   if ((n & 15) || D < 1 || D > 64) return hipErrorInvalidValue;
   if (reinterpret_cast<uintptr_t>(out) & 15) return hipErrorInvalidValue;
-  return launch_rows_group<0>(x, n, ld, D, scale, shift, out, stream, index);
+  if (perm_n > 0 && (index != nullptr || n > perm_n)) return hipErrorInvalidValue;
+  const RowSource src{index, perm_key, perm_n, perm_n > 0 ? perm_half_bits(perm_n) : 0};
+  return launch_rows_group<0>(x, n, ld, D, scale, shift, out, stream, src);
+}
+
+hipError_t perm_indices_launch(int64_t* out, int64_t start, int64_t count, int64_t n, uint64_t key,
+                               hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  if (n <= 0 || start < 0 || start + count > n) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(perm_indices_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, out, start,
+                     count, n, key, perm_half_bits(n));
+  return hipGetLastError();
 }
 
 hipError_t row_argmax_launch(const float* x, int64_t n, int64_t ld, int D, const float* scale, const float* shift,

@@ -121,9 +121,12 @@ int64_t ae_train_partials(const at::Tensor& x, const c10::optional<at::Tensor>& 
 // ingest-time tile-packed ring: per 16-row tile the rows then the 16 argmax bytes
 // index (optional int64 [m]): pack rows x[index[0..m)] instead of x[0..n); out (optional): an
 // existing byte buffer of at least the packed size (e.g. a slice of a ring being refilled)
+// perm_n > 0: pack rows x[perm_row(r, perm_n, perm_key)] for r < n_rows (default perm_n): an
+// epoch's shuffle as a keyed bijection evaluated in the kernel
 at::Tensor pack_tiles_argmax(const at::Tensor& x, int64_t D, const c10::optional<at::Tensor>& scale,
                              const c10::optional<at::Tensor>& shift, const c10::optional<at::Tensor>& index,
-                             const c10::optional<at::Tensor>& out_opt) {
+                             const c10::optional<at::Tensor>& out_opt, uint64_t perm_key, int64_t perm_n,
+                             int64_t n_rows) {
   check_dev(x, "x", at::kFloat);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(1) >= D && D >= 1 && D <= 64,
               "x must be [n, >=D] with D <= 64");
@@ -143,6 +146,15 @@ at::Tensor pack_tiles_argmax(const at::Tensor& x, int64_t D, const c10::optional
     }
     idx = index->data_ptr<int64_t>();
   }
+  if (perm_n > 0) {
+    TORCH_CHECK(idx == nullptr, "index and perm are exclusive");
+    TORCH_CHECK(perm_n <= x.size(0), "perm_n larger than x");
+    n = n_rows >= 0 ? n_rows : perm_n;
+    TORCH_CHECK(n <= perm_n, "more packed rows than the permuted domain");
+  } else if (n_rows >= 0) {
+    TORCH_CHECK(n_rows <= n, "n_rows larger than the source");
+    n = n_rows;
+  }
   TORCH_CHECK(n % 16 == 0, "packed rows must be a multiple of 16");
   const int64_t bytes = n / 16 * (64 * D + 16);
   c10::hip::HIPGuard guard(x.device().index());
@@ -156,7 +168,19 @@ at::Tensor pack_tiles_argmax(const at::Tensor& x, int64_t D, const c10::optional
     out = at::empty({bytes}, x.options().dtype(at::kByte));
   }
   SML_CHECK_HIP(sml::pack_tiles_argmax_launch(x.data_ptr<float>(), n, x.stride(0), (int)D, opt_ptr(scale),
-                                              opt_ptr(shift), out.data_ptr<uint8_t>(), cur_stream(x), idx));
+                                              opt_ptr(shift), out.data_ptr<uint8_t>(), cur_stream(x), idx, perm_key,
+                                              perm_n));
+  return out;
+}
+
+// the pack's keyed bijection, materialised: int64 [count] = perm_row(start + i, n, key)
+at::Tensor perm_indices(const at::Tensor& like, int64_t n, uint64_t key, int64_t start, int64_t count) {
+  TORCH_CHECK(like.is_cuda(), "like must be a device tensor");
+  if (count < 0) count = n - start;
+  TORCH_CHECK(n > 0 && start >= 0 && count >= 0 && start + count <= n, "need 0 <= start, start + count <= n");
+  c10::hip::HIPGuard guard(like.device().index());
+  auto out = at::empty({count}, like.options().dtype(at::kLong));
+  SML_CHECK_HIP(sml::perm_indices_launch(out.data_ptr<int64_t>(), start, count, n, key, cur_stream(like)));
   return out;
 }
 
@@ -971,7 +995,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("n_rows") = -1, py::arg("cursor") = py::none(), py::arg("xpack") = py::none());
   m.def("pack_tiles_argmax", &pack_tiles_argmax, "tile-packed training ring (rows + ingest-time argmax per tile)",
         py::arg("x"), py::arg("D"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
-        py::arg("index") = py::none(), py::arg("out") = py::none());
+        py::arg("index") = py::none(), py::arg("out") = py::none(), py::arg("perm_key") = 0,
+        py::arg("perm_n") = 0, py::arg("n_rows") = -1);
+  m.def("perm_indices", &perm_indices, "the pack's keyed row bijection of [0, n), materialised", py::arg("like"),
+        py::arg("n"), py::arg("key"), py::arg("start") = 0, py::arg("count") = -1);
   m.def("row_argmax_u8", &row_argmax_u8, "ingest-time argmax of each normalised row (uint8)", py::arg("x"),
         py::arg("D"), py::arg("scale") = py::none(), py::arg("shift") = py::none());
   m.def("ae_minibatch_max_batch", &sml::ae_minibatch_max_batch, "largest batch the persistent small-batch trainer takes");

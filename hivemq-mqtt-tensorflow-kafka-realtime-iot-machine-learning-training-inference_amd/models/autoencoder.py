@@ -352,14 +352,18 @@ class Autoencoder:
             nfull = agree([nfull], self.device)[0]
         if steps_per_epoch is not None:
             nfull = min(nfull, steps_per_epoch)
-        perm = self._device_perm(n, seed, rank, epoch) if shuffle else None
+        pkey = self.shuffle_key(seed, rank, epoch) if shuffle else None
         maybe_inject_range(gstep, gstep + nfull + 1, rank)
         steps = 0
         if nfull:
             key = (xd.data_ptr(), n, B, nfull)
-            if perm is not None or getattr(self, "_tp_key", None) != key or be.ring_xpack is None:
-                be.pack_ring(xd, B, index=perm[:nfull * B] if perm is not None else None)
-                self._tp_key = None if perm is not None else key
+            if pkey is not None or getattr(self, "_tp_key", None) != key or be.ring_xpack is None:
+                if pkey is not None:   # the epoch's shuffle evaluated inside the pack kernel
+                    be.pack_ring(xd, B, perm_key=pkey) if nfull * B == (n // B) * B else \
+                        be.pack_ring(xd, B, index=be.perm_indices(n, pkey, 0, nfull * B))
+                else:
+                    be.pack_ring(xd[:nfull * B], B)
+                self._tp_key = None if pkey is not None else key
             else:
                 be.cursor.zero_()
             for _ in range(nfull):
@@ -367,10 +371,18 @@ class Autoencoder:
             steps = nfull
         rem = n - nfull * B
         if rem and world == 1 and (steps_per_epoch is None or steps < steps_per_epoch) and n // B == nfull:
-            tail = xd[perm[nfull * B:]] if perm is not None else xd[nfull * B:]
+            tail = xd[be.perm_indices(n, pkey, nfull * B, rem)] if pkey is not None else xd[nfull * B:]
             be.step(tail.contiguous())
             steps += 1
         return steps
+
+    @staticmethod
+    def shuffle_key(seed: int, rank: int, epoch: int) -> int:
+        """64-bit key of an epoch's throughput-mode shuffle (a keyed bijection evaluated in the
+        pack kernel; deterministic in (seed, rank, epoch), so a resumed run reshuffles alike)."""
+        import hashlib
+        h = hashlib.blake2b(f"{int(seed)}:{int(rank)}:{int(epoch)}".encode(), digest_size=8).digest()
+        return int.from_bytes(h, "little")
 
     def _fit_stream_throughput(self, stream, B: int, max_steps: Optional[int], world: int, allreduce,
                                gstep: int, rank: int, pack_batches: int = 8) -> int:

@@ -216,13 +216,14 @@ class FusedAE:
                 and tuple(self.spec.activations) == ("tanh", "relu", "tanh", "relu"))
 
     def pack_ring(self, x: torch.Tensor, batch: int, index: Optional[torch.Tensor] = None,
-                  reuse: bool = True) -> int:
-        """Throughput-mode ring for ``step_ring``: the rows ``x[index]`` (or ``x``), cut to
-        whole batches, packed ONCE into the tile layout (normalize_fn + argmax(x), K8) --
-        the shuffle gather fused into the pack, so an epoch's permutation costs one pass over
-        the rows instead of a gather copy plus a pack.  Returns the number of ring rows
-        (full batches); the caller trains ``rows // batch`` steps with ``step_ring`` and the
-        remainder (Keras' short last batch) with ``step``.  Buffers are reused across epochs."""
+                  perm_key: Optional[int] = None, reuse: bool = True) -> int:
+        """Throughput-mode ring for ``step_ring``: the rows of ``x`` -- in order, through an
+        explicit ``index``, or shuffled by the keyed bijection ``perm_key`` over all of ``x``
+        (:meth:`perm_indices`) -- cut to whole batches and packed ONCE into the tile layout
+        (normalize_fn + argmax(x), K8).  The shuffle is evaluated inside the pack kernel, so a
+        shuffled epoch costs one gather pass over the rows: no permutation array, no copy.
+        Returns the number of ring rows (full batches); the caller trains ``rows // batch``
+        steps with ``step_ring`` and Keras' short last batch with ``step``."""
         self._check_x(x)
         B = int(batch)
         n = int(index.numel()) if index is not None else int(x.size(0))
@@ -231,6 +232,8 @@ class FusedAE:
             raise ValueError(f"fewer rows ({n}) than one batch ({B})")
         if not (self._xpack_ok(rows, B) and x.size(1) == self.spec.input_dim):
             # no packed kernel for this model: materialise the epoch's rows, plain ring
+            if perm_key is not None:
+                index = self.perm_indices(int(x.size(0)), perm_key)
             src = x[index[:rows]] if index is not None else x[:rows]
             self.attach_ring(src.contiguous(), B)
             return rows
@@ -238,15 +241,25 @@ class FusedAE:
         buf = getattr(self, "_pack_buf", None)
         if not reuse or buf is None or buf.numel() < nbytes:
             buf = self._pack_buf = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-        idx = index[:rows].contiguous() if index is not None else None
-        self.C.pack_tiles_argmax(x if idx is not None else x[:rows], self.spec.input_dim, self.scale, self.shift,
-                                 idx, buf)
+        if perm_key is not None:
+            self.C.pack_tiles_argmax(x, self.spec.input_dim, self.scale, self.shift, None, buf,
+                                     perm_key=int(perm_key) & ((1 << 64) - 1), perm_n=int(x.size(0)), n_rows=rows)
+        else:
+            idx = index[:rows].contiguous() if index is not None else None
+            self.C.pack_tiles_argmax(x if idx is not None else x[:rows], self.spec.input_dim, self.scale, self.shift,
+                                     idx, buf)
         # the ring tensor only carries the geometry (rows, stride): with a packed ring the
         # launcher reads the rows from the pack alone and refuses any variant that would not
         self.ring, self.ring_batch = x[:rows], B
         self.ring_xpack = buf[:nbytes]
         self.cursor.zero_()
         return rows
+
+    def perm_indices(self, n: int, perm_key: int, start: int = 0, count: Optional[int] = None) -> torch.Tensor:
+        """Rows ``start .. start + count`` of the keyed shuffle of [0, n) that ``pack_ring``
+        evaluates in-kernel (int64 device tensor)."""
+        return self.C.perm_indices(self.params, int(n), int(perm_key) & ((1 << 64) - 1), int(start),
+                                   -1 if count is None else int(count))
 
     def step_ring(self, global_batch: Optional[int] = None, allreduce=None) -> None:
         if self.ring is None:

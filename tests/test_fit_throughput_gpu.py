@@ -61,7 +61,7 @@ def test_fit_throughput_epoch_vs_bf16_reference(cuda_device, shuffle):
     xd = torch.from_numpy(raw).to(cuda_device)
     h = m.fit(xd, epochs=1, batch_size=B, shuffle=shuffle, seed=9, verbose=0, engine="throughput")
     assert m.last_fit_engine == "throughput" and m.iterations == 7
-    order = (m._device_perm(n, 9, 0, 0).cpu().numpy() if shuffle else np.arange(n))
+    order = (m.backend.perm_indices(n, Autoencoder.shuffle_key(9, 0, 0)).cpu().numpy() if shuffle else np.arange(n))
     batches = [order[i:i + B] for i in range(0, n, B)]
     want, loss = _adam_oracle(w0, xn, batches)
     assert _relerr(m.get_weights(), want) < 1e-3
@@ -106,3 +106,31 @@ def test_fit_auto_picks_throughput_for_large_batches(cuda_device):
     assert m.last_fit_engine == "throughput"
     m.fit(raw, epochs=1, batch_size=100, verbose=0)
     assert m.last_fit_engine == "persistent"
+
+
+@pytest.mark.parametrize("n", [1, 2, 17, 4096, 1_000_003])
+def test_pack_shuffle_is_a_bijection(cuda_device, n):
+    """The in-kernel epoch shuffle (keyed Feistel bijection, cycle-walked into [0, n))."""
+    m = Autoencoder(device=cuda_device, input_normalizer="cardata")
+    m.compile()
+    idx = m.backend.perm_indices(n, 12345).cpu().numpy()
+    assert np.array_equal(np.sort(idx), np.arange(n))
+    if n > 1000:   # and it actually shuffles: few fixed points, low correlation with the identity
+        assert (idx == np.arange(n)).mean() < 0.01
+        assert abs(np.corrcoef(idx, np.arange(n))[0, 1]) < 0.05
+    other = m.backend.perm_indices(n, 54321).cpu().numpy()
+    assert n < 17 or not np.array_equal(idx, other)
+
+
+def test_pack_with_perm_key_equals_indexed_pack(cuda_device):
+    from streamml.ops._ext import load_c
+    C = load_c()
+    raw, _ = _data(4096 + 37, 11)
+    x = torch.from_numpy(raw).to(cuda_device)
+    sc, sh = (torch.tensor(a, dtype=torch.float32, device=cuda_device) for a in normalize_affine())
+    idx = C.perm_indices(x, x.size(0), 777, 0, 4096)
+    a = C.pack_tiles_argmax(x, 18, sc, sh, idx, None)
+    b = C.pack_tiles_argmax(x, 18, sc, sh, None, None, perm_key=777, perm_n=x.size(0), n_rows=4096)
+    assert torch.equal(a, b)
+    c = C.pack_tiles_argmax(x[idx].contiguous(), 18, sc, sh)
+    assert torch.equal(a, c)
