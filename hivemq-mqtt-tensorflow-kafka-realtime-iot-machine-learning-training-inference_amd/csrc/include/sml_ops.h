@@ -15,9 +15,11 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
                            const float* params, float* partials, int64_t* iter, const int64_t* cursor,
                            const int* dims, const int* acts, float l1, int want_acc, int grid, const uint8_t* xpack,
                            hipStream_t stream, int* grid_used);  // grid_used <= grid: slabs written
+// metrics (optional, 4 floats): += (sum sq err, sum |h1|, correct argmax, rows) -- evaluate()
 hipError_t ae_forward_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
                              const float* params, float* recon, float* score, uint8_t* flag, float threshold,
-                             const int* dims, const int* acts, int max_blocks, hipStream_t stream);
+                             const int* dims, const int* acts, int max_blocks, hipStream_t stream,
+                             float* metrics = nullptr);
 hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, float* grad_out, float* params,
                               float* m, float* v, const int64_t* iter, float lr, float beta1, float beta2, float eps,
                               float gscale, float* metrics_acc, int flags, int64_t* cursor, int64_t cursor_step,

@@ -1411,6 +1411,7 @@ struct FwdArgs {
   float threshold;
   int D, n1, n2, n3;
   int a1, a2, a3, a4;
+  float* metrics;        // [4] += (sum sq err, sum |h1|, correct argmax, rows), or null (evaluate)
 };
 
 template <int PACK, bool VEC>
@@ -1433,6 +1434,7 @@ __global__ __launch_bounds__(WAVES * 64) void ae_forward_kernel(FwdArgs fa) {
   const int64_t ntiles = (a.n + 15) >> 4;
   const int64_t stride = (int64_t)gridDim.x * WAVES;
   const float inv_d = 1.0f / (float)a.D;
+  float m_sq = 0.f, m_ab = 0.f, m_corr = 0.f, m_rows = 0.f;
   for (int64_t t = (int64_t)blockIdx.x * WAVES + wid; t < ntiles; t += stride) {
     const int64_t r = t * 16 + c;
     const bool valid = r < a.n;
@@ -1490,6 +1492,20 @@ __global__ __launch_bounds__(WAVES * 64) void ae_forward_kernel(FwdArgs fa) {
       if (fa.score) fa.score[r] = sc;
       if (fa.flag) fa.flag[r] = sc > fa.threshold ? 1 : 0;
     }
+    if (fa.metrics) {   // Keras evaluate(): the train step's loss terms + accuracy, no backward
+      m_sq += (g == 0 && valid) ? se : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) m_ab += (valid && 4 * g + i < a.n1) ? fabsf(h1[i]) : 0.f;
+      const int iy = row_argmax_fast<false>(y, a.D, g), ix = row_argmax_fast<false>(xf, a.D, g);
+      m_corr += (g == 0 && valid && iy == ix) ? 1.f : 0.f;
+      m_rows += (g == 0 && valid) ? 1.f : 0.f;
+    }
+  }
+  if (fa.metrics) {   // one float atomic per wave and metric (evaluation only: order-insensitive sums)
+    const float vals[4] = {wave_sum(m_sq), wave_sum(m_ab), wave_sum(m_corr), wave_sum(m_rows)};
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) atomicAdd(fa.metrics + k, vals[k]);
   }
 }
 
@@ -1717,8 +1733,9 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
 
 hipError_t ae_forward_launch(const float* x, int64_t n, int64_t ld, const float* scale, const float* shift,
                              const float* params, float* recon, float* score, uint8_t* flag, float threshold,
-                             const int* dims, const int* acts, int max_blocks, hipStream_t stream) {
+                             const int* dims, const int* acts, int max_blocks, hipStream_t stream, float* metrics) {
   FwdArgs a{};
+  a.metrics = metrics;
   a.x = x; a.n = n; a.ld = ld; a.scale = scale; a.shift = shift; a.params = params;
   a.recon = recon; a.score = score; a.flag = flag; a.threshold = threshold;
   a.D = dims[0]; a.n1 = dims[1]; a.n2 = dims[2]; a.n3 = dims[3];

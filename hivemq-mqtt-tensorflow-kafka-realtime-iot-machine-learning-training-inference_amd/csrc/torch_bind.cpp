@@ -356,8 +356,12 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
 void ae_forward(const at::Tensor& x, const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift,
                 const at::Tensor& params, const c10::optional<at::Tensor>& recon,
                 const c10::optional<at::Tensor>& score, const c10::optional<at::Tensor>& flag, double threshold,
-                std::vector<int64_t> dims, std::vector<int64_t> acts, int64_t max_blocks) {
+                std::vector<int64_t> dims, std::vector<int64_t> acts, int64_t max_blocks,
+                const c10::optional<at::Tensor>& metrics) {
   check_ae_dims(dims, acts);
+  if (metrics.has_value() && metrics->defined())
+    TORCH_CHECK(metrics->is_cuda() && metrics->scalar_type() == at::kFloat && metrics->numel() >= 4 &&
+                    metrics->is_contiguous(), "metrics must be a float32 device tensor of >= 4 sums");
   check_dev(x, "x", at::kFloat);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [n, ld]");
   TORCH_CHECK(x.size(1) >= dims[0], "x has fewer columns than the model input dim");
@@ -377,7 +381,7 @@ void ae_forward(const at::Tensor& x, const c10::optional<at::Tensor>& scale, con
   int a[4] = {(int)acts[0], (int)acts[1], (int)acts[2], (int)acts[3]};
   SML_CHECK_HIP(sml::ae_forward_launch(x.data_ptr<float>(), n, x.stride(0), opt_ptr(scale), opt_ptr(shift),
                                        params.data_ptr<float>(), opt_mut(recon), opt_mut(score), flag_ptr,
-                                       (float)threshold, d, a, (int)max_blocks, cur_stream(x)));
+                                       (float)threshold, d, a, (int)max_blocks, cur_stream(x), opt_mut(metrics)));
 }
 
 std::vector<at::Tensor> lstm_fwd(const at::Tensor& zx, const at::Tensor& Uw, const c10::optional<at::Tensor>& h0,
@@ -1128,5 +1132,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),
         py::arg("scale"), py::arg("shift"), py::arg("params"), py::arg("recon"), py::arg("score"), py::arg("flag"),
-        py::arg("threshold"), py::arg("dims"), py::arg("acts"), py::arg("max_blocks"));
+        py::arg("threshold"), py::arg("dims"), py::arg("acts"), py::arg("max_blocks"), py::arg("metrics") = py::none());
 }

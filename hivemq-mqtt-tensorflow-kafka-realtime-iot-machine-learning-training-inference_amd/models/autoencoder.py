@@ -604,16 +604,30 @@ class Autoencoder:
 
     # ------------------------------------------------------------------ inference
     def _forward_batches(self, x, batch_size: int):
+        """(first row, reconstruction, score) per batch: device tensors on ROCm (the input
+        goes to the device once, outputs stay there), numpy on CPU."""
+        if self.device.type == "cuda":
+            xd = self._to_device(x)
+            for s in range(0, xd.size(0), batch_size):
+                r, sc, _ = self.backend.forward(xd[s:s + batch_size])
+                yield s, r, sc
+            return
         arr = x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x, np.float32)
         for s in range(0, len(arr), batch_size):
-            xb = arr[s:s + batch_size]
-            if self.device.type == "cuda":
-                r, sc, _ = self.backend.forward(self._to_device(xb))
-                yield xb, r.cpu().numpy(), sc.cpu().numpy()
-            else:
-                xn = self._cpu_x(xb)
-                y = self.backend.forward(xn)
-                yield xb, y.numpy(), ((y - xn) ** 2).mean(dim=1).numpy()
+            xn = self._cpu_x(arr[s:s + batch_size])
+            y = self.backend.forward(xn)
+            yield s, y.numpy(), ((y - xn) ** 2).mean(dim=1).numpy()
+
+    @staticmethod
+    def _np(t):
+        return t.cpu().numpy() if isinstance(t, torch.Tensor) else t
+
+    def _collect(self, parts):
+        if not parts:
+            return None
+        if isinstance(parts[0], torch.Tensor):
+            return torch.cat(parts).cpu().numpy()   # one device -> host copy
+        return np.concatenate(parts)
 
     def predict(self, x, batch_size: int = 32, callbacks: Optional[Sequence[Callback]] = None,
                 verbose: int = 0) -> np.ndarray:
@@ -626,32 +640,33 @@ class Autoencoder:
             cb.set_model(self)
         outs = []
         if isinstance(x, Stream):
-            batches = ((c.x,) for c in x.batch(batch_size))
-            it = (self._forward_batches(b[0], batch_size) for b in batches)
-            gen = (r for g in it for r in g)
+            gen = (r for c in x.batch(batch_size) for r in self._forward_batches(c.x, batch_size))
         else:
-            gen = self._forward_batches(x, batch_size)
+            gen = self._forward_batches(x, batch_size if cbs else max(batch_size, 1 << 20))
         for bi, (_, rec, sc) in enumerate(gen):
             outs.append(rec)
             ENGINE.infer_rows.inc(len(rec), model=self.name)
-            for cb in cbs:
-                cb.on_predict_batch_end(bi, {"outputs": rec, "scores": sc})
+            if cbs:   # the callbacks see host arrays per batch, as Keras' on_predict_batch_end
+                logs = {"outputs": self._np(rec), "scores": self._np(sc)}
+                for cb in cbs:
+                    cb.on_predict_batch_end(bi, logs)
         for cb in cbs:
             cb.on_predict_end()
-        return np.concatenate(outs) if outs else np.zeros((0, self.spec.input_dim), np.float32)
+        out = self._collect(outs)
+        return out if out is not None else np.zeros((0, self.spec.input_dim), np.float32)
 
     def score(self, x, batch_size: int = 1 << 20) -> np.ndarray:
         """Per-row reconstruction MSE = anomaly score (notebook ...ipynb:1014-1015)."""
         if not self.compiled:
             self.compile()
-        return np.concatenate([sc for _, _, sc in self._forward_batches(x, batch_size)])
+        return self._collect([sc for _, _, sc in self._forward_batches(x, batch_size)])
 
     def reconstruct_and_score(self, x, batch_size: int = 1 << 20) -> Tuple[np.ndarray, np.ndarray]:
         """Reconstructions and anomaly scores from one device pass (K12)."""
         if not self.compiled:
             self.compile()
         parts = list(self._forward_batches(x, batch_size))
-        return np.concatenate([r for _, r, _ in parts]), np.concatenate([sc for _, _, sc in parts])
+        return self._collect([r for _, r, _ in parts]), self._collect([sc for _, _, sc in parts])
 
     def detect(self, x, threshold: float = 5.0, batch_size: int = 1 << 20) -> np.ndarray:
         """Anomaly flags with the notebook's fixed threshold (``threshold_fixed = 5``)."""
@@ -663,16 +678,13 @@ class Autoencoder:
         """Keras ``evaluate``: (loss, accuracy) without updating weights."""
         if not self.compiled:
             self.compile()
-        arr = x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x, np.float32)
         D = self.spec.input_dim
         if self.device.type == "cuda":
-            tot = np.zeros(4)
-            for s in range(0, len(arr), batch_size):
-                _, metr = self.backend.gradients(self._to_device(arr[s:s + batch_size]))
-                tot += metr
-            sq, ab, corr, rows = tot
+            # forward kernel with on-device metric sums: no backward, one host read
+            sq, ab, corr, rows = self.backend.evaluate_sums(self._to_device(x), max(int(batch_size), 1))
             rows = max(rows, 1.0)
             return float((sq / D + self.spec.activity_l1 * ab) / rows), float(corr / rows)
+        arr = x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x, np.float32)
         from .reference import ae_loss_torch
         xn = self._cpu_x(arr)
         with torch.no_grad():

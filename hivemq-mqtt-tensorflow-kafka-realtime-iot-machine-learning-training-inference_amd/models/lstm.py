@@ -54,12 +54,6 @@ def _glorot(fi: int, fo: int, rng) -> np.ndarray:
     return rng.uniform(-lim, lim, size=(fi, fo)).astype(np.float32)
 
 
-def _bf16_mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    if a.is_cuda:
-        return (a.to(torch.bfloat16) @ b.to(torch.bfloat16)).float()
-    return a @ b
-
-
 class LSTMPredictor:
     def __init__(self, look_back: int = 1, features: int = 18, stack=None, device="auto", seed: int = 0,
                  name: str = "sequential", lr: float = 1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7):

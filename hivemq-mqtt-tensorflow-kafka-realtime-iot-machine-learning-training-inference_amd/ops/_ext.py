@@ -7,6 +7,7 @@ PyTorch eager ops on the GPU path); on CPU-only machines callers can ask
 """
 from __future__ import annotations
 
+import collections
 import importlib
 import os
 import threading
@@ -26,6 +27,18 @@ def _try_build(which: str) -> None:
         _build.build_c(checked=kernel_checks())
     else:
         _build.build_io()
+
+
+# Calls that left the in-tree HIP kernels for a vendor library (hipBLASLt GEMMs for shapes
+# beyond the tall-skinny register tiles).  The reference models never should: the tests
+# assert this stays empty, and SML_STRICT_KERNELS=1 turns any such call into an error.
+FALLBACKS: "collections.Counter[str]" = collections.Counter()
+
+
+def note_fallback(what: str) -> None:
+    FALLBACKS[what] += 1
+    if os.environ.get("SML_STRICT_KERNELS") == "1":
+        raise RuntimeError(f"vendor-library fallback '{what}' with SML_STRICT_KERNELS=1")
 
 
 def kernel_checks() -> bool:

@@ -396,8 +396,10 @@ class FusedAE:
         return {"loss": loss, "mse": sq / (D * rows), "accuracy": corr / rows, "rows": rows}
 
     def forward(self, x: torch.Tensor, recon: bool = True, score: bool = True,
-                threshold: Optional[float] = None):
-        """Inference: reconstruction [n, D], per-row MSE score [n], anomaly flag [n]."""
+                threshold: Optional[float] = None, metrics: Optional[torch.Tensor] = None):
+        """Inference: reconstruction [n, D], per-row MSE score [n], anomaly flag [n].
+        ``metrics`` (float32 [4] on the device): += (sum squared error, sum |h1|, correct
+        argmax, rows) -- Keras ``evaluate`` from the forward pass alone."""
         self._check_x(x)
         n = x.size(0)
         D = self.spec.input_dim
@@ -406,5 +408,12 @@ class FusedAE:
         f = torch.empty(n, dtype=torch.uint8, device=self.device) if threshold is not None else None
         self.C.ae_forward(x, self.scale, self.shift, self.params, r, s, f,
                           float(threshold if threshold is not None else 0.0), self.spec.dims,
-                          self.spec.act_codes, self.max_blocks)
+                          self.spec.act_codes, self.max_blocks, metrics)
         return r, s, f
+
+    def evaluate_sums(self, x: torch.Tensor, batch: int = 1 << 22) -> np.ndarray:
+        """(sum squared error, sum |h1|, correct, rows) over x: forward kernel only."""
+        acc = torch.zeros(4, device=self.device)
+        for s0 in range(0, x.size(0), batch):
+            self.forward(x[s0:s0 + batch], recon=False, score=False, metrics=acc)
+        return acc.double().cpu().numpy()

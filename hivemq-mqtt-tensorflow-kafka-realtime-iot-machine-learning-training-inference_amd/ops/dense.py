@@ -89,6 +89,8 @@ def dense(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None, ac
             x2 = x2.contiguous()
         return DenseFunction.apply(x2, W, b, act).reshape(*lead, N)
     if x.is_cuda:   # large layers: hipBLASLt (bias fused into the GEMM epilogue)
+        from ._ext import note_fallback
+        note_fallback(f"dense[{K}x{N}]")
         z = torch.addmm(b, x.reshape(-1, K), W) if b is not None else x.reshape(-1, K) @ W
         return _act_torch(act, z).reshape(*lead, N)
     z = x @ W

@@ -53,6 +53,8 @@ def lstm_reference(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.T
 
 def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """bf16 MFMA GEMM via hipBLASLt, fp32 result (shapes beyond the K1/K2 register tile)."""
+    from ._ext import note_fallback
+    note_fallback(f"lstm_mm[{tuple(a.shape)}x{tuple(b.shape)}]")
     return (a.to(torch.bfloat16) @ b.to(torch.bfloat16)).float()
 
 

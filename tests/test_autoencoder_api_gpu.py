@@ -44,3 +44,54 @@ def test_reference_model_on_gpu(cuda_device):
     mc = load_model(os.path.join(FIX, "autoencoder_sensor_anomaly_detection.h5"), device="cpu")
     x = np.random.default_rng(0).standard_normal((4096, 30)).astype(np.float32)
     np.testing.assert_allclose(m.score(x), mc.score(x), rtol=3e-2, atol=3e-3)
+
+
+def test_evaluate_forward_only_matches_train_kernel_metrics(cuda_device):
+    """evaluate() runs the forward kernel with on-device metric sums (no backward); its loss
+    and accuracy equal the train kernel's metric sums on the same rows (gradients(), which
+    computes the same forward) and the fp32 torch oracle."""
+    from streamml.models.reference import ae_loss_torch
+    x = S.csv(os.path.join(FIX, "car-sensor-data.csv")).collect().x[:9000]
+    m = Autoencoder(device=cuda_device, input_normalizer="cardata", seed=3)
+    m.compile()
+    loss, acc = m.evaluate(x, batch_size=4096)
+    _, metr = m.backend.gradients(torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(cuda_device))
+    sq, ab, corr, rows = metr
+    want_loss = (sq / 18 + 1e-7 * ab) / rows
+    assert abs(loss - want_loss) <= 1e-5 * want_loss
+    assert abs(acc - corr / rows) <= 2.0 / rows          # argmax near-ties may differ by a row
+    mc = Autoencoder(device="cpu", input_normalizer="cardata", seed=3)
+    mc.compile()
+    lc, ac = mc.evaluate(x)
+    assert abs(loss - lc) <= 2e-2 * lc                   # bf16 MFMA vs fp32 torch
+    assert abs(acc - ac) <= 0.02
+
+
+def test_predict_and_score_stay_on_device_until_the_end(cuda_device):
+    """Device inputs: one forward pass per batch on the device, one copy back at the end;
+    identical to per-batch host round trips."""
+    rng = np.random.default_rng(5)
+    x = rng.uniform(0, 40, size=(10_000, 18)).astype(np.float32)
+    m = Autoencoder(device=cuda_device, input_normalizer="cardata", seed=1)
+    m.compile()
+    xd = torch.from_numpy(x).to(cuda_device)
+    p_dev = m.predict(xd, batch_size=1000)
+    p_host = m.predict(x, batch_size=1000)
+    np.testing.assert_array_equal(p_dev, p_host)
+    r, s = m.reconstruct_and_score(xd, batch_size=3000)
+    np.testing.assert_array_equal(r, p_host)
+    np.testing.assert_allclose(s, m.score(x), rtol=0, atol=0)
+    seen = []
+
+    class CB:
+        def set_model(self, model):
+            pass
+
+        def on_predict_batch_end(self, b, logs):
+            seen.append(logs["outputs"].shape)
+
+        def on_predict_end(self):
+            pass
+
+    m.predict(xd, batch_size=4096, callbacks=[CB()])
+    assert seen == [(4096, 18), (4096, 18), (1808, 18)]
