@@ -73,7 +73,7 @@ def parse():
                    help="Keras batch-32 steps per launch of the multi-GPU in-kernel P2P DP measurement (0 = skip)")
     p.add_argument("--fit-rows", type=int, default=2_000_000,
                    help="rows of the Autoencoder.fit(batch_size=100) measurement (0 = skip)")
-    p.add_argument("--stream-rows", type=int, default=2_000_000,
+    p.add_argument("--stream-rows", type=int, default=20_000_000,
                    help="events of the Kafka -> native feed -> fit end-to-end measurement (0 = skip)")
     return p.parse_args()
 

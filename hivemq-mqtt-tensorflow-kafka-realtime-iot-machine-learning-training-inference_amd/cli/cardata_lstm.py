@@ -37,6 +37,9 @@ def _flags(p):
     p.add_argument("--stack", choices=["reference", "two-layer"], default="reference")
     p.add_argument("--schema", default="cardata-v1")
     p.add_argument("--group", default="cardata-v1")
+    p.add_argument("--predict-engine", choices=["auto", "persistent", "batch"], default="auto",
+                   help="persistent: events one at a time through the resident GPU forecaster "
+                        "(lstm_serve.hip); batch: model.predict over the windows; auto: persistent on ROCm")
 
 
 def _rows(ns, servers, cfg) -> np.ndarray:
@@ -79,12 +82,40 @@ def _train(ns, rows, model):
     print(f"Training complete ({time.perf_counter() - t0:.2f}s)", flush=True)
 
 
+def _predict_persistent(model, rows: np.ndarray, first: int, count: int) -> np.ndarray:
+    """Forecasts of windows [first, first + count) by streaming the events one at a time
+    through the resident forecaster: the window ending at event i is window i - T + 1, so
+    events 0 .. first + count + T - 2 are fed (one key: the reference windows the partition's
+    event sequence, not per car) and the forecasts at the matching events returned."""
+    from ..ops.serve import LSTMScoringServer
+    T = model.look_back
+    end = min(len(rows), first + count + T - 1)
+    if end < first + T:
+        return np.zeros((0, model.features), np.float32)
+    with LSTMScoringServer(model, nkeys=1, normalizer=None) as srv:   # rows are normalised already
+        pred, _, _ = srv.forecast(rows[:end], np.zeros(end, np.int64))
+    return pred[first + T - 1:end]
+
+
 def _predict(ns, servers, cfg, rows, model, result_topic):
     from ..nn.callbacks import KafkaPredictionSink
     xw = _windows(rows, ns.look_back)
     b0 = ns.skip * ns.batch_size
     xw = xw[b0:b0 + ns.predict_take * ns.batch_size]
     cbs = [KafkaPredictionSink(ns.batch_size, result_topic, servers, cfg)] if result_topic else []
+    engine = ns.predict_engine
+    if engine == "auto":
+        engine = "persistent" if model.device.type == "cuda" else "batch"
+    if engine == "persistent":
+        out = _predict_persistent(model, rows, b0, len(xw))
+        for cb in cbs:   # the reference OutputCallback, per batch_size forecasts
+            cb.set_model(model)
+            for bi, s0 in enumerate(range(0, len(out), ns.batch_size)):
+                cb.on_predict_batch_end(bi, {"outputs": out[s0:s0 + ns.batch_size]})
+            cb.on_predict_end()
+        print(f"predict {len(out)} windows (persistent forecaster) -> {result_topic}", flush=True)
+        print("Predict complete", flush=True)
+        return out
     out = model.predict(xw, batch_size=ns.batch_size, callbacks=cbs)
     print(f"predict {len(xw)} windows -> {result_topic}", flush=True)
     print("Predict complete", flush=True)

@@ -74,6 +74,10 @@ def _flags(p) -> None:
     p.add_argument("--low-latency", action="store_true",
                    help="C++ fetch/decode/score/format/produce loop on the persistent GPU scorer")
     p.add_argument("--max-wait-ms", type=int, default=100, help="long-poll bound of the low-latency loop")
+    p.add_argument("--model", choices=["autoencoder", "lstm"], default="autoencoder",
+                   help="lstm: per-car forecaster (look_back events per car on the device, each event "
+                        "scored against the car's previous forecast; lstm_serve.hip)")
+    p.add_argument("--max-keys", type=int, default=200_000, help="--model lstm: car keys held on the device")
 
 
 def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary) -> int:
@@ -124,8 +128,16 @@ def main(argv: Sequence[str]) -> int:
 
     path = common.model_path(ns.workdir, ns.model_file)
     if not os.path.exists(path):
-        autoencoder_store(ns.project, ns.store).download("/" + ns.model_file, path)
-    model = load_model(path, device=device, input_normalizer="cardata")
+        if ns.model == "lstm":
+            from ..utils.model_store import lstm_store
+            lstm_store(ns.store).download(ns.model_file, path)
+        else:
+            autoencoder_store(ns.project, ns.store).download("/" + ns.model_file, path)
+    if ns.model == "lstm":
+        from ..models.lstm import LSTMPredictor
+        model = LSTMPredictor.load(path, device=device)
+    else:
+        model = load_model(path, device=device, input_normalizer="cardata")
     if ns.metrics_port and rank == 0:
         REGISTRY.serve(ns.metrics_port, addr="0.0.0.0")
 
@@ -146,8 +158,16 @@ def main(argv: Sequence[str]) -> int:
         print(json.dumps(summary), flush=True)
         return 0
 
+    if ns.low_latency and ns.model == "lstm":
+        raise SystemExit("--low-latency serves the autoencoder; --model lstm runs its own persistent forecaster")
     if ns.low_latency:
         return _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary)
+    forecaster, key_ids = None, {}
+    if ns.model == "lstm":
+        if model.device.type != "cuda":
+            raise SystemExit("--model lstm serving needs a ROCm device (the persistent forecaster)")
+        from ..ops.serve import LSTMScoringServer
+        forecaster = LSTMScoringServer(model, nkeys=ns.max_keys, threshold=ns.threshold)
     start = -2 if ns.from_beginning else 0
     topics = [f"{ns.topic}:{p}:{start}" for p in mine]
     stream = kafka(servers, topics, schema=ns.schema, group=ns.group, eof=False, config=cfg, commit=True,
@@ -168,11 +188,26 @@ def main(argv: Sequence[str]) -> int:
             continue
         t_batch = time.perf_counter()
         recon = None
-        if ns.emit == "both":
+        if forecaster is not None:
+            # car key -> device slot (first come, first served; the table holds --max-keys cars)
+            ids = np.empty(len(chunk), np.int64)
+            for i, k in enumerate(chunk.keys or [None] * len(chunk)):
+                kid = key_ids.get(k)
+                if kid is None:
+                    if len(key_ids) >= ns.max_keys:
+                        raise SystemExit(f"more than --max-keys {ns.max_keys} cars on this replica")
+                    kid = key_ids[k] = len(key_ids)
+                ids[i] = kid
+            pred, scores, fl = forecaster.forecast(chunk.x, ids)
+            flags = fl == 1               # 2 = the car has no forecast yet (score NaN)
+            if ns.emit == "both":
+                recon = pred
+        elif ns.emit == "both":
             recon, scores = model.reconstruct_and_score(chunk.x, batch_size=ns.max_batch)
+            flags = scores > ns.threshold
         else:
             scores = model.score(chunk.x, batch_size=ns.max_batch)
-        flags = scores > ns.threshold
+            flags = scores > ns.threshold
         dt_us = (time.perf_counter() - t_batch) * 1e6 / len(chunk)
         keys = chunk.keys or [None] * len(chunk)
         offs = chunk.offsets if chunk.offsets is not None else np.arange(len(chunk))
@@ -193,6 +228,10 @@ def main(argv: Sequence[str]) -> int:
             break
     for sink in sinks.values():
         sink.flush()
+    if forecaster is not None:
+        forecaster.close()
+        summary["model"] = "lstm"
+        summary["keys"] = len(key_ids)
     wall = time.perf_counter() - t0
     summary["events_per_s"] = summary["events"] / wall if wall > 0 else 0.0
     print(json.dumps(summary), flush=True)

@@ -496,23 +496,34 @@ class Autoencoder:
         when any rank's stream is exhausted (its leftover rows and the others' are dropped)."""
         from ..parallel.dp import agree
         D = self.spec.input_dim
-        stage = torch.empty((0, D), dtype=torch.float32, device=self.device)
+        stage = torch.empty((max(4 * B, 1 << 16), D), dtype=torch.float32, device=self.device)
+        have = 0   # rows staged (a preallocated buffer: no per-chunk concatenation)
         it = iter(self._stream_device_chunks(stream))
         steps, exhausted = 0, False
         while True:
             if not exhausted:
                 try:
                     xd = next(it)
-                    stage = torch.cat([stage, xd]) if stage.size(0) else xd.clone()
+                    k = xd.size(0)
+                    if have + k > stage.size(0):   # grow geometrically; rare after the first chunks
+                        bigger = torch.empty((max(2 * stage.size(0), have + k), D), dtype=torch.float32,
+                                             device=self.device)
+                        bigger[:have].copy_(stage[:have])
+                        stage = bigger
+                    stage[have:have + k].copy_(xd)
+                    have += k
                 except StopIteration:
                     exhausted = True
-            avail = stage.size(0) // B
+            avail = have // B
             if max_steps is not None:
                 avail = min(avail, max_steps - steps)
             mn, any_done = agree([avail, int(exhausted)], self.device, ["min", "max"])
             if mn > 0:
                 steps += self._dp_train(stage[:mn * B], B, exch, local_k)
-                stage = stage[mn * B:].clone()
+                rest = have - mn * B
+                if rest:
+                    stage[:rest].copy_(stage[mn * B:have].clone())
+                have = rest
             if any_done or (max_steps is not None and steps >= max_steps):
                 return steps
 

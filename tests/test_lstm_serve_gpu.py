@@ -95,3 +95,20 @@ def test_lstm_serve_latency_and_reset(cuda_device):
         assert np.all(f == 2)
         with pytest.raises(Exception):
             srv.forecast(rows[:1], np.array([10]))   # keys are validated on the host
+
+
+@pytest.mark.parametrize("stack,T", [("reference", 1), ("two_layer", 8)])
+def test_cli_persistent_predict_matches_window_predict(cuda_device, stack, T):
+    """``cardata-lstm ... predict`` on ROCm streams the events through the forecaster; its
+    forecasts for windows [skip, skip + take) equal model.predict on those windows (the
+    batched path runs bf16 MFMA kernels, the forecaster fp32: bf16-level agreement)."""
+    from streamml.cli.cardata_lstm import _predict_persistent, _windows
+    ctor = LSTMPredictor.two_layer if stack == "two_layer" else LSTMPredictor.reference
+    m = ctor(look_back=T, device=cuda_device, seed=2)
+    rows = np.random.default_rng(3).uniform(-1, 1, size=(300, 18)).astype(np.float32)
+    skip, take = 40, 100
+    got = _predict_persistent(m, rows, skip, take)
+    want = m.predict(_windows(rows, T)[skip:skip + take])
+    want = want.reshape(len(want), -1, 18)[:, -1]
+    assert got.shape == want.shape == (take, 18)
+    np.testing.assert_allclose(got, want, rtol=0, atol=3e-2)
