@@ -74,6 +74,8 @@ def _flags(p) -> None:
     p.add_argument("--low-latency", action="store_true",
                    help="C++ fetch/decode/score/format/produce loop on the persistent GPU scorer")
     p.add_argument("--max-wait-ms", type=int, default=100, help="long-poll bound of the low-latency loop")
+    p.add_argument("--spin-us", type=int, default=0,
+                   help="low-latency loop: busy-poll each broker response this long before blocking")
     p.add_argument("--model", choices=["autoencoder", "lstm"], default="autoencoder",
                    help="lstm: per-car forecaster (look_back events per car on the device, each event "
                         "scored against the car's previous forecast; lstm_serve.hip)")
@@ -96,7 +98,7 @@ def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary) -> 
         loop = LowLatencyScorer(servers, ns.topic, ns.result_topic, mine, srv, schema=ns.schema, group=ns.group,
                                 starts=starts, result_partitions=[p % result_parts for p in mine],
                                 emit_recon=ns.emit == "both", config=cfg, max_batch=min(ns.max_batch, 4096),
-                                max_wait_ms=ns.max_wait_ms)
+                                max_wait_ms=ns.max_wait_ms, spin_us=ns.spin_us)
         st = loop.run(max_events=ns.max_events, idle_timeout_s=ns.idle_timeout)
     ENGINE.infer_rows.inc(st["events"], model=model.name)
     ENGINE.anomaly_events.inc(st["anomalies"], model=model.name)

@@ -424,13 +424,14 @@ PYBIND11_MODULE(_io, m) {
                        std::vector<int> partitions, std::vector<int64_t> starts, std::vector<int> result_partitions,
                        std::vector<int> feature_fields, bool framing, bool emit_recon, int max_batch,
                        int32_t max_bytes, int32_t max_wait_ms, double commit_interval_s, bool record_latency,
-                       uintptr_t api) {
+                       uintptr_t api, int spin_us) {
              kafka::ClientConfig c;
              c.client_id = client_id;
              c.sasl_mechanism = mech;
              c.sasl_username = user;
              c.sasl_password = pw;
              c.timeout_ms = timeout_ms;
+             c.spin_us = spin_us;
              serve::LoopConfig lc;
              lc.topic = topic;
              lc.result_topic = result_topic;
@@ -454,7 +455,7 @@ PYBIND11_MODULE(_io, m) {
            py::arg("result_topic"), py::arg("group"), py::arg("partitions"), py::arg("starts"),
            py::arg("result_partitions"), py::arg("feature_fields"), py::arg("framing"), py::arg("emit_recon"),
            py::arg("max_batch"), py::arg("max_bytes"), py::arg("max_wait_ms"), py::arg("commit_interval_s"),
-           py::arg("record_latency"), py::arg("scorer_api"))
+           py::arg("record_latency"), py::arg("scorer_api"), py::arg("spin_us") = 0)
       .def("run",
            [](serve::ScoreLoop& l, int64_t max_events, double idle_timeout_s) {
              serve::LoopStats st;
@@ -490,7 +491,7 @@ PYBIND11_MODULE(_io, m) {
       });
   m.def("paced_produce",
         [](const std::string& bootstrap, const std::string& topic, int partition, const py::bytes& values,
-           std::vector<int64_t> offs, py::object keys, double qps) {
+           std::vector<int64_t> offs, py::object keys, double qps, int spin_us) {
           std::string vals = values;
           std::vector<std::string> ks;
           if (!keys.is_none())
@@ -499,12 +500,14 @@ PYBIND11_MODULE(_io, m) {
           std::vector<int64_t> sent;
           {
             py::gil_scoped_release nogil;
-            sent = serve::paced_produce(bootstrap, kafka::ClientConfig(), topic, partition, vals, offs, ks, qps);
+            kafka::ClientConfig c;
+            c.spin_us = spin_us;
+            sent = serve::paced_produce(bootstrap, c, topic, partition, vals, offs, ks, qps);
           }
           return py::array_t<int64_t>((ssize_t)sent.size(), sent.data());
         },
         py::arg("bootstrap"), py::arg("topic"), py::arg("partition"), py::arg("values"), py::arg("offsets"),
-        py::arg("keys") = py::none(), py::arg("qps") = 10000.0,
+        py::arg("keys") = py::none(), py::arg("qps") = 10000.0, py::arg("spin_us") = 0,
         "append records one produce request each at `qps`; -> steady-clock send time (ns) per record");
   m.def("steady_ns", &serve::steady_ns);
 
@@ -683,6 +686,16 @@ PYBIND11_MODULE(_io, m) {
              return out;
            })
       .def("set_faults", &kafka::Broker::set_faults, py::arg("fail_every") = 0, py::arg("delay_ms") = 0)
+      .def("set_spin_us", &kafka::Broker::set_spin_us, py::arg("us"),
+           "low-latency mode: connection threads and empty long polls busy-wait this long first")
+      .def("record_append_times", &kafka::Broker::record_append_times, py::arg("on") = true)
+      .def("append_times",
+           [](kafka::Broker& b, const std::string& t, int p, int64_t start, int64_t count) {
+             const auto v = b.append_times(t, p, start, count);
+             return py::array_t<int64_t>((ssize_t)v.size(), v.data());
+           },
+           py::arg("topic"), py::arg("partition"), py::arg("start"), py::arg("count"),
+           "steady-clock append time (ns) per offset, -1 where not recorded")
       .def_property_readonly("fetch_count", &kafka::Broker::fetch_count)
       .def_property_readonly("injected_failures", &kafka::Broker::injected_failures)
       .def("stop", [](kafka::Broker& b) {

@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <chrono>
 #include <cstring>
 #include <sstream>
@@ -375,16 +376,34 @@ class Connection {
   }
   void recv_all(char* p, size_t n) {
     size_t off = 0;
+    if (spin_us_ > 0) {   // busy-poll first: the response usually lands within microseconds
+      const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
+      while (off < n) {
+        const ssize_t k = ::recv(fd_, p + off, n - off, MSG_DONTWAIT);
+        if (k > 0) {
+          off += (size_t)k;
+          continue;
+        }
+        if (k == 0) throw Error("kafka: connection closed");
+        if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) throw Error("kafka: recv failed");
+        if (std::chrono::steady_clock::now() >= t_end) break;
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
+    }
     while (off < n) {
       const ssize_t k = ::recv(fd_, p + off, n - off, 0);
       if (k <= 0) throw Error("kafka: connection closed / timed out");
       off += (size_t)k;
     }
   }
+  void set_spin_us(int us) { spin_us_ = us; }
   bool authed = false;
 
  private:
   int fd_ = -1;
+  int spin_us_ = 0;
 };
 
 // ---------------------------------------------------------------------------
@@ -406,6 +425,7 @@ Client::~Client() = default;
 
 std::unique_ptr<Connection> Client::open(const BrokerAddr& a) {
   auto c = std::make_unique<Connection>(a.host, a.port, cfg_.timeout_ms);
+  c->set_spin_us(cfg_.spin_us);
   if (!cfg_.sasl_mechanism.empty()) {
     W hs;
     hs.str(cfg_.sasl_mechanism);
@@ -827,8 +847,28 @@ void Broker::create_topic(const std::string& name, int partitions) {
   if ((int)t.size() < partitions) t.resize((size_t)partitions);
 }
 
+void Broker::record_append_times(bool on) { record_times_ = on; }
+
+std::vector<int64_t> Broker::append_times(const std::string& topic, int partition, int64_t start, int64_t count) {
+  std::lock_guard<std::mutex> g(mu_);
+  const Partition& p = topics_.at(topic).at((size_t)partition);
+  std::vector<int64_t> out((size_t)std::max<int64_t>(count, 0), -1);
+  for (int64_t i = 0; i < count; ++i) {
+    const int64_t k = start + i - p.tbase;
+    if (p.tbase >= 0 && k >= 0 && k < (int64_t)p.tappend.size()) out[(size_t)i] = p.tappend[(size_t)k];
+  }
+  return out;
+}
+
 int64_t Broker::append_locked(Partition& p, const Record* recs, size_t n) {
   const int64_t base = p.end;
+  if (record_times_.load(std::memory_order_relaxed)) {
+    const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::steady_clock::now().time_since_epoch()).count();
+    if (p.tbase < 0) p.tbase = base;
+    p.tappend.resize((size_t)(base - p.tbase), -1);   // offsets appended while recording was off
+    p.tappend.insert(p.tappend.end(), n, now);
+  }
   for (size_t k = 0; k < n; k += kSegmentRecords) {
     const size_t m = std::min(kSegmentRecords, n - k);
     Segment sg;
@@ -847,6 +887,7 @@ int64_t Broker::append_locked(Partition& p, const Record* recs, size_t n) {
     if (drop) p.segs.erase(p.segs.begin(), p.segs.begin() + (std::ptrdiff_t)drop);
   }
   p.start = p.segs.empty() ? p.end : p.segs.front().base;
+  append_seq_.fetch_add(1, std::memory_order_release);
   data_cv_.notify_all();   // wake long-polling fetches
   return base;
 }
@@ -973,6 +1014,20 @@ Broker::FetchReply Broker::handle_fetch(const uint8_t* body, size_t n) {
     };
     auto st = pick();
     if (fail) ++failures_;
+    const int spin = spin_us_.load();
+    if (!st.first && !st.second && min_bytes > 0 && max_wait_ms > 0 && spin > 0) {
+      // low-latency mode: watch the append counter without the lock before parking
+      const uint64_t seq0 = append_seq_.load(std::memory_order_acquire);
+      g.unlock();
+      const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(std::min(spin, max_wait_ms * 1000));
+      while (running_ && append_seq_.load(std::memory_order_acquire) == seq0 && std::chrono::steady_clock::now() < t_end) {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
+      g.lock();
+      st = pick();
+    }
     if (!st.first && !st.second && min_bytes > 0 && max_wait_ms > 0) {
       // system_clock deadline: pthread_cond_timedwait (the steady_clock form maps to
       // pthread_cond_clockwait, which the ThreadSanitizer runtime here does not model)
@@ -1020,6 +1075,23 @@ void Broker::serve(int fd) {
   while (running_) {
     uint8_t hdr[4];
     size_t got = 0;
+    if (const int spin = spin_us_.load(); spin > 0) {
+      // low-latency mode: the next request on a serving connection usually follows within
+      // microseconds; busy-poll it instead of paying a blocked recv's thread wake-up
+      const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin);
+      while (got < 4 && running_) {
+        const ssize_t k = ::recv(fd, hdr + got, 4 - got, MSG_DONTWAIT);
+        if (k > 0) {
+          got += (size_t)k;
+          continue;
+        }
+        if (k == 0 || (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)) goto done;
+        if (std::chrono::steady_clock::now() >= t_end) break;
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
+    }
     while (got < 4) {
       const ssize_t k = ::recv(fd, hdr + got, 4 - got, 0);
       if (k <= 0) goto done;

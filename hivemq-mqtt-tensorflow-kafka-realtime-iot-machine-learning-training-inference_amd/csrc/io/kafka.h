@@ -95,6 +95,9 @@ struct ClientConfig {
   std::string sasl_username, sasl_password;
   int timeout_ms = 30000;
   int max_retries = 5;
+  // > 0: busy-poll (non-blocking recv) a response this many microseconds before blocking --
+  // the low-latency serving loop's socket policy (a blocked recv costs a thread wake-up)
+  int spin_us = 0;
 };
 
 class Connection;
@@ -150,6 +153,7 @@ struct BrokerConfig {
   std::string sasl_username, sasl_password;  // empty = no auth
   int64_t retention_records = -1;           // -1 = unbounded
   bool auto_create_topics = true;            // Kafka's auto.create.topics.enable default
+  int spin_us = 0;                           // > 0: connection threads / long polls busy-wait this long first
 };
 
 class Broker {
@@ -169,6 +173,14 @@ class Broker {
     delay_ms_ = delay_ms;
   }
   uint64_t fetch_count() const { return fetches_; }
+  // Low-latency mode: each connection thread busy-polls its socket, and an empty long-poll
+  // fetch watches the append counter, for `us` microseconds before blocking (0 = off).
+  void set_spin_us(int us) { spin_us_ = us; }
+  // Record the steady-clock time (ns, the process's std::chrono::steady_clock) at which
+  // every record is appended from now on -- Kafka's LogAppendTime, for latency accounting.
+  void record_append_times(bool on);
+  // Append times of offsets [start, start + count) of a partition (-1 where not recorded).
+  std::vector<int64_t> append_times(const std::string& topic, int partition, int64_t start, int64_t count);
   uint64_t injected_failures() const { return failures_; }
   void stop();
 
@@ -187,6 +199,8 @@ class Broker {
     std::vector<Segment> segs;
     int64_t start = 0;  // offset of the first retained record
     int64_t end = 0;    // next offset to assign
+    int64_t tbase = -1;              // first offset with a recorded append time
+    std::vector<int64_t> tappend;    // append times (ns) of offsets tbase, tbase + 1, ...
   };
   int64_t append_locked(Partition& p, const Record* recs, size_t n);
   // A fetch reply: the response framing in `meta`, with the (shared, immutable) segment
@@ -209,7 +223,9 @@ class Broker {
   std::map<std::string, std::vector<Partition>> topics_;
   std::condition_variable data_cv_;   // appends -> long-polling fetches
   std::map<std::string, int64_t> group_offsets_;  // "group/topic/partition" -> offset
-  std::atomic<int> fail_every_{0}, delay_ms_{0};
+  std::atomic<int> fail_every_{0}, delay_ms_{0}, spin_us_{0};
+  std::atomic<bool> record_times_{false};
+  std::atomic<uint64_t> append_seq_{0};   // bumped by every append: lock-free wake-up check for spinning polls
   std::atomic<uint64_t> fetches_{0}, failures_{0};
 
   void accept_loop();

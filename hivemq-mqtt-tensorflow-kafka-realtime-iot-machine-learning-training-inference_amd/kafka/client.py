@@ -73,6 +73,18 @@ class FakeBroker:
     def set_faults(self, fail_every: int = 0, delay_ms: int = 0) -> None:
         self._b.set_faults(fail_every, delay_ms)
 
+    def set_spin_us(self, us: int) -> None:
+        """Low-latency mode: connection threads and empty long polls busy-wait ``us`` first."""
+        self._b.set_spin_us(int(us))
+
+    def record_append_times(self, on: bool = True) -> None:
+        """Record each appended record's steady-clock time (LogAppendTime, ns)."""
+        self._b.record_append_times(bool(on))
+
+    def append_times(self, topic: str, partition: int, start: int, count: int):
+        """int64 [count]: append time (ns, the process steady clock) of each offset (-1 = none)."""
+        return self._b.append_times(topic, int(partition), int(start), int(count))
+
     @property
     def fetch_count(self) -> int:
         return self._b.fetch_count

@@ -36,14 +36,15 @@ def feature_fields(schema: str = "cardata-v1"):
 class LowLatencyScorer:
     """``scorer``: a :class:`~streamml.ops.serve.ScoringServer` (or anything with a
     ``c_api()`` returning an ``SmlScorerApi`` table address, e.g. ``_io.EchoScorer`` in
-    CPU tests).  Keep the scorer alive while the loop runs."""
+    CPU tests).  Keep the scorer alive while the loop runs.  ``spin_us`` > 0 busy-polls each
+    broker response that long before blocking (a blocked recv costs a thread wake-up)."""
 
     def __init__(self, servers: str, topic: str, result_topic: str, partitions: Sequence[int], scorer,
                  schema: str = "cardata-v1", group: Optional[str] = None, starts: Optional[Sequence[int]] = None,
                  result_partitions: Optional[Sequence[int]] = None, emit_recon: bool = False,
                  config: Optional[Sequence[str]] = None, max_batch: int = 4096, max_bytes: int = 1 << 20,
                  max_wait_ms: int = 100, commit_interval_s: float = 0.0, record_latency: bool = False,
-                 framing: bool = True):
+                 framing: bool = True, spin_us: int = 0):
         client = KafkaClient(servers, config)
         self.partitions = [int(p) for p in partitions]
         if starts is None:   # committed offset of the group, else the log start
@@ -63,7 +64,7 @@ class LowLatencyScorer:
                                          self.partitions, [int(s) for s in starts],
                                          [int(r) for r in result_partitions], fields, framing, bool(emit_recon),
                                          int(max_batch), int(max_bytes), int(max_wait_ms), float(commit_interval_s),
-                                         bool(record_latency), int(api))
+                                         bool(record_latency), int(api), int(spin_us))
 
     def run(self, max_events: int = 0, idle_timeout_s: Optional[float] = None) -> dict:
         """Blocking (GIL released): until ``stop()``, ``max_events`` or ``idle_timeout_s``
@@ -82,9 +83,9 @@ class LowLatencyScorer:
 
 
 def paced_produce(servers: str, topic: str, partition: int, values: bytes, offsets, keys=None,
-                  qps: float = 10000.0) -> np.ndarray:
+                  qps: float = 10000.0, spin_us: int = 0) -> np.ndarray:
     """Append records one produce request each at ``qps`` (C++, GIL released); returns
     the steady-clock send time (ns) of every record (same clock as latency_records)."""
     from .client import resolve_servers
     return load_io().paced_produce(resolve_servers(servers), topic, int(partition), values,
-                                   [int(o) for o in offsets], keys, float(qps))
+                                   [int(o) for o in offsets], keys, float(qps), int(spin_us))

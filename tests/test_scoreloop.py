@@ -119,3 +119,32 @@ def test_long_poll_delivers_paced_events_promptly():
     assert (d > 0).all()
     assert np.percentile(d, 50) < 5000, np.percentile(d, 50)   # us; ~100 us typical
     assert out["empty_fetches"] < 400   # long-poll, not a busy poll
+
+
+def test_spin_mode_and_broker_append_times():
+    """Low-latency socket policy (busy-poll before blocking, broker and client) keeps every
+    result, in order; the broker's recorded append times give the append -> result latency."""
+    n = 400
+    x, vals, buf, offs = _records(n, seed=3)
+    b = fake_broker("spin-unit")
+    b.create_topic("S", 1)
+    b.create_topic("R", 1)
+    b.record_append_times(True)
+    b.set_spin_us(100)
+    echo = load_io().EchoScorer(18, 5.0)
+    loop = LowLatencyScorer("fake://spin-unit", "S", "R", [0], echo, starts=[0], max_wait_ms=50,
+                            record_latency=True, spin_us=100)
+    out = {}
+    th = threading.Thread(target=lambda: out.update(loop.run(max_events=n, idle_timeout_s=5.0)))
+    th.start()
+    paced_produce("fake://spin-unit", "S", 0, bytes(buf), offs, qps=20000, spin_us=100)
+    th.join(60)
+    b.set_spin_us(0)
+    assert out["events"] == n and b.end_offset("R", 0) == n
+    t_in = b.append_times("S", 0, 0, n)
+    t_res = b.append_times("R", 0, 0, n)
+    assert (t_in > 0).all() and (t_res > 0).all()
+    assert (np.diff(t_in) >= 0).all() and (t_res > t_in).all()
+    assert (b.append_times("S", 0, n, 3) == -1).all()     # not appended yet
+    recs = b.read("R", 0, 0, n)
+    assert [json.loads(v)["offset"] for _, _, v in recs] == list(range(n))
