@@ -39,6 +39,18 @@ constexpr int MAXLSTM = 4;     // LSTM layers with register-resident weights
 constexpr int KEY_WORD = 31;   // request word carrying the car key
 
 __device__ __forceinline__ float sigm(float z) { return 1.0f / (1.0f + __expf(-z)); }
+
+// The per-key state (window ring, count, forecast) is written by one wave and read by the
+// others in later events: agent-scope relaxed atomics go around the per-CU L1, so no wave
+// can hit a stale line of an older event.
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ float act_lstm(int a, float z) { return a == ACT_RELU ? fmaxf(z, 0.f) : tanhf(z); }
 
 struct Smem {
@@ -77,6 +89,7 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
     S.sc[i] = (i < D && a.scale) ? a.scale[i] : 1.f;
     S.sh[i] = (i < D && a.shift) ? a.shift[i] : 0.f;
   }
+  if (tid < 64) S.v[tid] = 0.f;   // [x ; h] past I + u stays 0 (its weights are 0: no 0 * garbage)
   __syncthreads();
   // register-resident weight halves of every LSTM layer: k = 32 * half + i of [W ; U]
   float wr[MAXLSTM][32], br[MAXLSTM];
@@ -156,25 +169,28 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
     key = key < 0 ? 0 : (key >= a.nkeys ? a.nkeys - 1 : key);   // the host validates; never leave the table
     float* hist = a.hist + (int64_t)key * T * D;
     float* lastp = a.lastpred + (int64_t)key * D;
-    const int cnt = a.hcount[key];   // events of this key before this one
+    // events of this key before this one: read once, broadcast, so every wave takes the same
+    // branches (the stack below has barriers)
+    if (tid == 0) S.ctl[2] = ld_agent(&a.hcount[key]);
+    __syncthreads();
+    const int cnt = S.ctl[2];
+    const bool full = cnt + 1 >= T;
     // ---------------- append the event, score it against the previous forecast
     float err = 0.f;
     if (tid < D) {
       const float xn = S.xrow[tid];
-      hist[(cnt % T) * D + tid] = xn;
+      st_agent(&hist[(cnt % T) * D + tid], xn);
       if (cnt >= T) {
-        const float d = xn - lastp[tid];
+        const float d = xn - ld_agent(&lastp[tid]);
         err = d * d;
       }
     }
     if (wid == 0) err = wave_sum(err);
-    const bool full = cnt + 1 >= T;
-    __syncthreads();   // hist row written (workgroup-scope global visibility)
-    // ---------------- the window, oldest first, into seqa [t][k]
+    // ---------------- the window, oldest first, into seqa [t][k] (the newest row from LDS)
     if (full) {
       for (int e = tid; e < T * D; e += NT) {
         const int t = e / D, k = e - t * D;
-        S.seqa[t * MAXW + k] = hist[((cnt + 1 - T + t) % T) * D + k];
+        S.seqa[t * MAXW + k] = t == T - 1 ? S.xrow[k] : ld_agent(&hist[((cnt + 1 - T + t) % T) * D + k]);
       }
     }
     __syncthreads();
@@ -251,12 +267,12 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
       const float p = (full && lane < D) ? S.pred[lane] : 0.f;
       if (lane < D) {
         st_sys(&r->w[lane], tagged(want, p));
-        if (full) lastp[lane] = p;
+        if (full) st_agent(&lastp[lane], p);
       }
       if (lane == 0) {
         const float score = cnt >= T ? err / (float)D : __builtin_nanf("");
         const uint32_t flag = cnt >= T ? (score > a.threshold ? 1u : 0u) : 2u;
-        a.hcount[key] = cnt + 1;
+        st_agent(&a.hcount[key], cnt + 1);
         st_sys(&r->w[kServeScore], tagged(want, score));
         st_sys(&r->w[kServeFlag], tagged_u(want, flag));
         st_sys(&r->w[kServeTLoad], tagged_u(want, 0u));
