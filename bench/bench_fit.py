@@ -49,7 +49,8 @@ def fit_array(device, rows: int = 2_000_000, batch: int = 100, engine: str = "au
 
 
 def stream_e2e(device, rows: int = 2_000_000, batch: int = 100, partitions: int = 8, workers: int = 8,
-               fetch_bytes: int = 4 << 20, failure_rate: float = 0.01, native: bool = True, dp: str = "auto") -> dict:
+               fetch_bytes: int = 4 << 20, failure_rate: float = 0.01, native: bool = True, dp: str = "auto",
+               compare_chunks: bool = False) -> dict:
     import torch
 
     from streamml.data import stream as S
@@ -116,7 +117,18 @@ def stream_e2e(device, rows: int = 2_000_000, batch: int = 100, partitions: int 
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out.update({"rows_per_s": n / dt, "kept_rows": kept, "trained_rows_per_s": kept / dt,
-                "engine": m.last_fit_engine, "loss": h.history["loss"][-1]})
+                "engine": m.last_fit_engine, "loss": h.history["loss"][-1],
+                "epoch_launch": "doorbell" if os.environ.get("SML_STREAM_DOORBELL", "1") != "0" else "per-chunk"})
+    if compare_chunks:   # the launch-per-chunk streaming epoch on the same log
+        os.environ["SML_STREAM_DOORBELL"] = "0"
+        try:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            m.fit(training, epochs=1, batch_size=batch, verbose=0, dp=dp)
+            torch.cuda.synchronize()
+            out["per_chunk_rows_per_s"] = n / (time.perf_counter() - t0)
+        finally:
+            os.environ.pop("SML_STREAM_DOORBELL", None)
     return out
 
 
@@ -128,6 +140,7 @@ def main():
     ap.add_argument("--workers", default="8", help="comma-separated feed worker counts to sweep")
     ap.add_argument("--python-feed", action="store_true", help="chunk-by-chunk Python Kafka path")
     ap.add_argument("--skip-stream", action="store_true")
+    ap.add_argument("--compare-chunks", action="store_true", help="also time the launch-per-chunk stream epoch")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
@@ -136,7 +149,7 @@ def main():
     res["fit_launch_batch100"] = fit_array(dev, args.rows // 10, args.batch, engine="launch")
     if not args.skip_stream:
         res["stream_e2e"] = [stream_e2e(dev, args.rows, args.batch, args.partitions, int(w),
-                                        native=not args.python_feed) for w in str(args.workers).split(",")]
+                                        native=not args.python_feed, compare_chunks=args.compare_chunks) for w in str(args.workers).split(",")]
     print(json.dumps(res))
 
 

@@ -27,13 +27,21 @@ hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, f
 
 // ---- persistent small-batch AE trainer (ae_minibatch.hip): nsteps Keras steps in one launch ----
 int ae_minibatch_max_batch();
+// streaming epoch counters (host-mapped device pointers, runtime/stream_ring.h)
+struct MBStream {
+  const int64_t* avail;      // rows in the ring so far (absolute)
+  const int64_t* total;      // -1 until the stream ended, then the row count
+  int64_t* consumed;         // rows the kernel no longer needs
+  int* status;               // 1 = timed out waiting for rows
+  long long timeout_ticks;   // s_memrealtime (100 MHz)
+};
 hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t* cursor, const float* scale,
                                const float* shift, float* params, float* m, float* v, int64_t* iter, float* metrics,
                                int B, int nsteps, const int* dims, const int* acts, float l1, float lr, float beta1,
                                float beta2, float eps, float gscale, int want_acc, unsigned long long* prof,
                                int nmodels, int64_t xmodel, const float* lrs, const int64_t* ragged,
                                uint64_t* const* dp_peers, int dp_ranks, int dp_rank0, int* dp_status,
-                               long long dp_timeout, hipStream_t stream);
+                               long long dp_timeout, hipStream_t stream, const MBStream* sr = nullptr);
 
 // ---- LSTM recurrence (lstm.hip) ----
 hipError_t lstm_fwd_launch(const float* zx, const float* Uw, const float* h0, const float* c0, float* hseq,

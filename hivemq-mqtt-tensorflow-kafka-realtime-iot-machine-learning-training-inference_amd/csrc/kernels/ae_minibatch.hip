@@ -40,6 +40,7 @@
 // digital-twin models, ensembles, learning-rate sweeps), one per workgroup, each with
 // its own parameters, optimizer state, ring cursor and metrics.
 #include "sml_common.h"
+#include "sml_ops.h"
 #include "sml_p2p.h"
 
 #include <type_traits>
@@ -99,6 +100,18 @@ struct MBArgs {
   int dp_ranks, dp_rank0;
   int* dp_status;           // set to 1 when a peer's gradient never arrived (timeout)
   long long dp_timeout;     // s_memrealtime ticks (100 MHz)
+  // Streaming epoch (runtime/stream_ring.h): rows are still arriving while the kernel runs.
+  // The host publishes the rows copied into the ring so far (sr_avail: absolute count,
+  // host-mapped, written by the copy stream after each copy) and, once the stream has
+  // ended, the total (sr_total, -1 before).  The kernel waits for each next batch, stops
+  // when the next full batch would pass the total, and reports the rows it no longer needs
+  // (sr_consumed: back-pressure).  Ring memory is uncached (a copy on another engine must
+  // never be shadowed by a stale line of the previous lap).  Null: a resident ring.
+  const int64_t* sr_avail;
+  const int64_t* sr_total;
+  int64_t* sr_consumed;
+  int* sr_status;           // 1 = no rows arrived within sr_timeout
+  long long sr_timeout;
 };
 
 template <int MB>
@@ -112,6 +125,7 @@ struct Smem {   // MB 48: ~47 KB, MB 128: ~108 KB
   float one[4];                         // constant 1 (bias-row activation), dummy store slot
   float red[3][NT / 64];
   int abort;                            // DP: a gradient exchange timed out (all waves stop)
+  int stream_end;                       // streaming: no further full batch (all waves stop)
 };
 
 // logical feature of K-step s for lane group g (the C/D register order of the producer)
@@ -178,6 +192,27 @@ __device__ __forceinline__ Tile make_tile(int id, int c, int g, const SM& S, con
   T.slot0 = img + (row0 + 4 * g) * istride + col0 + c;
   T.sst = istride;
   return T;
+}
+
+// Streaming epoch: wait until rows [0, need) are in the ring.  1 = they are, 0 = the stream
+// ended before `need`, -1 = nothing arrived within the timeout.  Wave-uniform.
+__device__ __forceinline__ int64_t ld_host64(const int64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ int stream_wait(const MBArgs& a, int64_t need, int64_t& avail) {
+  if (avail >= need) return 1;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    avail = ld_host64(a.sr_avail);   // same address in every lane: a wave-uniform value
+    if (avail >= need) return 1;
+    const int64_t total = ld_host64(a.sr_total);
+    if (total >= 0) {   // the host writes the final avail before the total
+      avail = ld_host64(a.sr_avail);
+      return avail >= need ? 1 : 0;
+    }
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.sr_timeout) return -1;
+    __builtin_amdgcn_s_sleep(2);
+  }
 }
 
 // LDS-only barrier: the next batch's global prefetch stays in flight across it
@@ -270,6 +305,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   if (t == 0) {
     S.one[0] = 1.f;
     S.abort = 0;
+    S.stream_end = 0;
   }
   const bool dp = DPX && a.dp_ranks > 1;
   const int dp_rank = a.dp_rank0 + (int)blockIdx.x;
@@ -296,7 +332,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
     for (int s = 0; s < KSX; ++s) xr[s] = __builtin_nontemporal_load(rp + (fok[s] ? feat(s, g) : 0));
   };
-  if (has_rows) fetch(cur);
+  const bool stream = a.sr_avail != nullptr;
+  int64_t avail = 0;   // streaming: rows known to be in the ring (cached; re-polled only when short)
+  int first_ok = 1;
+  if (stream) {
+    first_ok = stream_wait(a, (int64_t)B, avail);
+    if (first_ok < 0 && t == 0) __hip_atomic_store(a.sr_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (has_rows && first_ok == 1) fetch(cur);
   int64_t nxt = advance(cur);
 
   float sq = 0.f, ab = 0.f, corr = 0.f;
@@ -333,7 +376,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   // granules may have arrived): these hold the state from before the step's update
   float wp[4] = {0.f, 0.f, 0.f, 0.f}, mp[4] = {0.f, 0.f, 0.f, 0.f}, vp[4] = {0.f, 0.f, 0.f, 0.f};
   float sq0 = 0.f, ab0 = 0.f, corr0 = 0.f;
-  for (int step = 0; step < a.nsteps; ++step) {
+  if (stream && first_ok != 1) done = 0;
+  for (int step = 0; step < a.nsteps && first_ok == 1; ++step) {
     if (DPX) {
       sq0 = sq;
       ab0 = ab;
@@ -347,9 +391,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
       for (int s = 0; s < KSX; ++s) xv[s] = (row_ok && fok[s]) ? fmaf(xr[s], sc[s], sh[s]) : 0.f;
       if (step + 1 < a.nsteps) {   // next step's rows: in flight across phase B
-        fetch(nxt);
-        cur = nxt;
-        nxt = advance(cur);
+        int more = 1;
+        if (stream) {   // the next batch must have landed in the ring (or the stream ends here)
+          more = stream_wait(a, (int64_t)(step + 2) * B, avail);
+          if (more != 1 && lane == 0) {
+            S.stream_end = 1;
+            if (more < 0) __hip_atomic_store(a.sr_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
+        if (more == 1) {
+          fetch(nxt);
+          cur = nxt;
+          nxt = advance(cur);
+        }
       }
       // L1: h1^T = act1(W1^T x^T + b1)
       f32x4 z1 = ld4(S.w + BB1 + 4 * g);
@@ -543,6 +597,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     mark(2);
     lds_barrier();
     mark(3);
+    if (stream) {   // read after the barrier: every wave sees the same decision
+      if (t == 0 && (step & 7) == 7)   // rows of steps <= step are no longer needed (back-pressure)
+        __hip_atomic_store(a.sr_consumed, (int64_t)(step + 1) * B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (S.stream_end) {
+        done = step + 1;
+        break;
+      }
+    }
     if (dp && S.abort) {   // read after the barrier: every wave leaves together
       // roll the failed step back everywhere: its update, metrics and cursor never happened,
       // so the replica stays in the state it had after `step` completed steps (the host
@@ -598,6 +660,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
     a.iter[0] = it0 + done;
     if (a.cursor) a.cursor[0] = done == a.nsteps ? nxt : (cur0 + (int64_t)done * B) % a.ring;
+    if (stream) __hip_atomic_store(a.sr_consumed, (int64_t)done * B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (dp && S.abort) __hip_atomic_store(a.dp_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -614,15 +677,19 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
                                float beta2, float eps, float gscale, int want_acc, unsigned long long* prof,
                                int nmodels, int64_t xmodel, const float* lrs, const int64_t* ragged,
                                uint64_t* const* dp_peers, int dp_ranks, int dp_rank0, int* dp_status,
-                               long long dp_timeout, hipStream_t stream) {
+                               long long dp_timeout, hipStream_t stream, const MBStream* sr) {
   // ragged: per-model ring / steps were validated on the host (torch_bind.cpp)
+  if (sr && (nmodels != 1 || ragged || dp_ranks > 1 || !sr->avail || !sr->total || !sr->consumed || !sr->status))
+    return hipErrorInvalidValue;   // streaming: one model, one replica
   if (B < 1 || B > MAXB || nsteps < 1 || (!ragged && (ring < B || ring % B))) return hipErrorInvalidValue;
   if (dims[0] > 31 || nmodels < 1 || nmodels > (1 << 20) || xmodel < 0) return hipErrorInvalidValue;
   if (dp_ranks > 1 && (!dp_peers || !dp_status || dp_rank0 < 0 || dp_rank0 + nmodels > dp_ranks))
     return hipErrorInvalidValue;
   MBArgs a{x, ld, ring, cursor, scale, shift, params, m, v, iter, metrics, B, nsteps, dims[0], dims[1], dims[2],
            dims[3], acts[0], acts[1], acts[2], acts[3], l1, lr, beta1, beta2, eps, gscale, want_acc, prof,
-           xmodel, lrs, ragged, dp_peers, dp_ranks, dp_rank0, dp_status, dp_timeout};
+           xmodel, lrs, ragged, dp_peers, dp_ranks, dp_rank0, dp_status, dp_timeout,
+           sr ? sr->avail : nullptr, sr ? sr->total : nullptr, sr ? sr->consumed : nullptr,
+           sr ? sr->status : nullptr, sr ? sr->timeout_ticks : 0};
   const bool ref = acts[0] == ACT_TANH && acts[1] == ACT_RELU && acts[2] == ACT_TANH && acts[3] == ACT_RELU;
   void (*k)(MBArgs) = nullptr;
   size_t lds = 0;

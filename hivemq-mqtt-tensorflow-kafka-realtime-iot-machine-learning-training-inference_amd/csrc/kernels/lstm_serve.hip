@@ -63,7 +63,7 @@ struct Smem {
   float* xrow;    // [MAXW]
   float* sc;      // [MAXW]
   float* sh;      // [MAXW]
-  int* ctl;       // [4]: quit, key, count
+  int* ctl;       // [8]: quit, key, count, seen sequence, t_seen lo / hi
 };
 
 __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
@@ -90,6 +90,7 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
     S.sh[i] = (i < D && a.shift) ? a.shift[i] : 0.f;
   }
   if (tid < 64) S.v[tid] = 0.f;   // [x ; h] past I + u stays 0 (its weights are 0: no 0 * garbage)
+  if (tid < 8) S.ctl[tid] = 0;
   __syncthreads();
   // register-resident weight halves of every LSTM layer: k = 32 * half + i of [W ; U]
   float wr[MAXLSTM][32], br[MAXLSTM];
@@ -122,46 +123,45 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
   uint64_t last = __builtin_amdgcn_s_memrealtime();
   if (tid == 0) st_sys32(&a.ctl->alive, 1u);
   for (;;) {
-    // ---------------- wave 0 polls the next request slot (ae_serve.hip's pipelined poll)
+    // ---------------- all four waves poll the next request slot, staggered by a quarter
+    // of a PCIe round trip so their samples interleave.  Each poll is one synchronous
+    // cache-bypassing load whose wait the compiler places (no load result is ever in flight
+    // across statements: an asm-issued pipelined poll let the compiler copy a destination
+    // register before its data landed).  The first wave that sees the whole request
+    // publishes the row and key to LDS, then its sequence number; the others see that.
     const int slot = (int)(tail % (uint64_t)a.nslots);
     const uint32_t want = (uint32_t)(tail + 1);
-    uint64_t t_seen = 0;
-    if (wid == 0) {
+    {
+      volatile int* seen = &S.ctl[3];
+      volatile int* quit_f = &S.ctl[0];
       const uint64_t* wp = &a.req[slot].w[lane & 31];
-      const uint64_t* hp = &a.ctl->head;
-      uint64_t w0, h0, w1, h1, w2, h2, wv = 0;
-      poll_issue(w0, h0, wp, hp);
-      __builtin_amdgcn_s_sleep(8);
-      poll_issue(w1, h1, wp, hp);
-      __builtin_amdgcn_s_sleep(8);
-      poll_issue(w2, h2, wp, hp);
-      auto ready = [&](uint64_t w) {
-        const bool ok = (lane >= D && lane != KEY_WORD) || lane >= 32 || (uint32_t)(w >> 32) == want;
-        return __ballot(ok) == ~0ull;
-      };
-      int quit = 0;
+      // ~0.25 / 0.5 / 0.75 us: s_sleep takes an immediate
+      if (wid == 1) __builtin_amdgcn_s_sleep(10);
+      else if (wid == 2) __builtin_amdgcn_s_sleep(20);
+      else if (wid == 3) __builtin_amdgcn_s_sleep(30);
       for (uint32_t it = 0;; ++it) {
-        asm volatile("s_waitcnt vmcnt(4)" : "+v"(w0), "+v"(h0)::"memory");
-        if (ready(w0)) { wv = w0; break; }
-        poll_issue(w0, h0, wp, hp);
-        asm volatile("s_waitcnt vmcnt(4)" : "+v"(w1), "+v"(h1)::"memory");
-        if (ready(w1)) { wv = w1; break; }
-        poll_issue(w1, h1, wp, hp);
-        asm volatile("s_waitcnt vmcnt(4)" : "+v"(w2), "+v"(h2)::"memory");
-        if (ready(w2)) { wv = w2; break; }
-        poll_issue(w2, h2, wp, hp);
-        if ((it & 63) == 63) {
+        if (*seen == (int)want || *quit_f) break;
+        const uint64_t w = ld_sys(wp);
+        const bool ok = (lane >= D && lane != KEY_WORD) || lane >= 32 || (uint32_t)(w >> 32) == want;
+        if (__ballot(ok) == ~0ull) {
+          if (lane < D) S.xrow[lane] = fmaf(__uint_as_float((uint32_t)w), S.sc[lane], S.sh[lane]);
+          if (lane == KEY_WORD) S.ctl[1] = (int)(uint32_t)w;
+          if (lane == 0) {
+            const uint64_t ts = __builtin_amdgcn_s_memrealtime();
+            S.ctl[4] = (int)(uint32_t)ts;
+            S.ctl[5] = (int)(uint32_t)(ts >> 32);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // row and key before the sequence
+          if (lane == 0) *seen = (int)want;
+          break;
+        }
+        if ((it & 63) == 63 && wid == 0) {   // exit conditions every wave reaches
           if (ld_sys32(&a.ctl->stop) || __builtin_amdgcn_s_memrealtime() - last > a.idle_ticks) {
-            quit = 1;
+            if (lane == 0) *quit_f = 1;
             break;
           }
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(w0), "+v"(h0), "+v"(w1), "+v"(h1), "+v"(w2), "+v"(h2)::"memory");
-      t_seen = __builtin_amdgcn_s_memrealtime();
-      if (lane < D) S.xrow[lane] = fmaf(__uint_as_float((uint32_t)wv), S.sc[lane], S.sh[lane]);
-      if (lane == KEY_WORD) S.ctl[1] = (int)(uint32_t)wv;
-      if (lane == 0) S.ctl[0] = quit;
     }
     __syncthreads();
     if (S.ctl[0]) break;
@@ -261,6 +261,7 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
       }
     }
     const uint64_t t_comp = __builtin_amdgcn_s_memrealtime();
+    const uint64_t t_seen = (uint64_t)(uint32_t)S.ctl[4] | ((uint64_t)(uint32_t)S.ctl[5] << 32);
     // ---------------- results (wave 0), the key's state, completion counter
     if (wid == 0) {
       ServeResult* r = a.res + slot;
@@ -294,7 +295,7 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
 
 size_t lstm_serve_lds_bytes(int nw) {
   const int nwp = (nw + 3) & ~3;
-  return (size_t)(nwp + 2 * MAXT * MAXW + 64 + 128 + 4 * MAXW) * sizeof(float) + 4 * sizeof(int);
+  return (size_t)(nwp + 2 * MAXT * MAXW + 64 + 128 + 4 * MAXW) * sizeof(float) + 8 * sizeof(int);
 }
 
 hipError_t lstm_serve_launch(const LstmServeArgs& args, hipStream_t stream) {

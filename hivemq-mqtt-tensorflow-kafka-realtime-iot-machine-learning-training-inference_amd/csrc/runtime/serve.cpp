@@ -1,4 +1,5 @@
 #include "serve.h"
+#include "queues.h"
 
 #include <chrono>
 #include <cstring>
@@ -40,7 +41,7 @@ ServeRing::ServeRing(int device, int nslots, int D, double idle_seconds)
   ck(hipHostGetDevicePointer((void**)&ctl_d_, ctl_, 0), "device ptr ctl");
   ck(hipHostGetDevicePointer((void**)&req_d_, req_, 0), "device ptr req");
   ck(hipHostGetDevicePointer((void**)&res_d_, res_, 0), "device ptr res");
-  ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
+  ck(create_persistent_stream(&stream_), "stream");
 }
 
 ServeRing::~ServeRing() {

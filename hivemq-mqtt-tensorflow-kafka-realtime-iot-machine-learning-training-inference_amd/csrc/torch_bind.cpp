@@ -14,6 +14,8 @@
 #include "sml_scorer_api.h"
 #include "../runtime/ring.h"
 #include "../runtime/serve.h"
+#include "../runtime/stream_ring.h"
+#include "../runtime/queues.h"
 
 #include <pybind11/numpy.h>
 #include <cstdlib>
@@ -270,14 +272,15 @@ void reduce_adam(const at::Tensor& partials, int64_t G, int64_t S, int64_t npara
                                         cursor_step, cursor_ring, cur_stream(partials)));
 }
 
-void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c10::optional<at::Tensor>& scale,
-                          const c10::optional<at::Tensor>& shift, const at::Tensor& params, const at::Tensor& m,
-                          const at::Tensor& v, const at::Tensor& iter, const c10::optional<at::Tensor>& metrics,
-                          int64_t batch, int64_t nsteps, std::vector<int64_t> dims, std::vector<int64_t> acts,
-                          double l1, double lr, double beta1, double beta2, double eps, double gscale, bool want_acc,
-                          const c10::optional<at::Tensor>& prof, const c10::optional<at::Tensor>& lrs,
-                          uint64_t dp_peers, int64_t dp_ranks, int64_t dp_rank0, uint64_t dp_status,
-                          int64_t dp_timeout_ticks, const c10::optional<at::Tensor>& ragged) {
+void train_minibatches_impl(const at::Tensor& x, const at::Tensor& cursor, const c10::optional<at::Tensor>& scale,
+                            const c10::optional<at::Tensor>& shift, const at::Tensor& params, const at::Tensor& m,
+                            const at::Tensor& v, const at::Tensor& iter, const c10::optional<at::Tensor>& metrics,
+                            int64_t batch, int64_t nsteps, std::vector<int64_t> dims, std::vector<int64_t> acts,
+                            double l1, double lr, double beta1, double beta2, double eps, double gscale,
+                            bool want_acc, const c10::optional<at::Tensor>& prof,
+                            const c10::optional<at::Tensor>& lrs, uint64_t dp_peers, int64_t dp_ranks,
+                            int64_t dp_rank0, uint64_t dp_status, int64_t dp_timeout_ticks,
+                            const c10::optional<at::Tensor>& ragged, const sml::MBStream* sr, hipStream_t st) {
   // One model: params/m/v [1536], cursor/iter [1], x [ring, ld].  Fleet of M models:
   // params/m/v [M, 1536], cursor/iter [M], metrics [M, 4], x [ring, ld] (shared) or [M, ring, ld].
   check_ae_dims(dims, acts);
@@ -350,8 +353,106 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
                                          prof_ptr, (int)M, x.dim() == 3 ? x.stride(0) : 0, lrs_ptr, ragged_ptr,
                                          reinterpret_cast<uint64_t* const*>(dp_peers), (int)dp_ranks, (int)dp_rank0,
                                          reinterpret_cast<int*>(dp_status), (long long)dp_timeout_ticks,
-                                         cur_stream(x)));
+                                         st, sr));
 }
+
+void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c10::optional<at::Tensor>& scale,
+                          const c10::optional<at::Tensor>& shift, const at::Tensor& params, const at::Tensor& m,
+                          const at::Tensor& v, const at::Tensor& iter, const c10::optional<at::Tensor>& metrics,
+                          int64_t batch, int64_t nsteps, std::vector<int64_t> dims, std::vector<int64_t> acts,
+                          double l1, double lr, double beta1, double beta2, double eps, double gscale, bool want_acc,
+                          const c10::optional<at::Tensor>& prof, const c10::optional<at::Tensor>& lrs,
+                          uint64_t dp_peers, int64_t dp_ranks, int64_t dp_rank0, uint64_t dp_status,
+                          int64_t dp_timeout_ticks, const c10::optional<at::Tensor>& ragged) {
+  train_minibatches_impl(x, cursor, scale, shift, params, m, v, iter, metrics, batch, nsteps, std::move(dims),
+                         std::move(acts), l1, lr, beta1, beta2, eps, gscale, want_acc, prof, lrs, dp_peers, dp_ranks,
+                         dp_rank0, dp_status, dp_timeout_ticks, ragged, nullptr, cur_stream(x));
+}
+
+// A streaming epoch on ONE persistent ae_minibatch launch (runtime/stream_ring.h): the
+// kernel runs on the ring's own train stream and takes its batches from the device ring
+// as push() lands them (doorbell = host-mapped row count written by the copy stream).
+// Deadlock rule: the producer of pushed rows must not be the train stream, so train()
+// never makes the caller's stream wait for the kernel -- join() does, after finish().
+class StreamRingPy {
+ public:
+  StreamRingPy(int64_t device, int64_t rows, int64_t features)
+      : dev_(device), ring_((int)device, rows, (int)features) {
+    c10::hip::HIPGuard guard((int)device);
+    SML_CHECK_HIP(sml::create_persistent_stream(&train_));
+    SML_CHECK_HIP(hipEventCreateWithFlags(&before_, hipEventDisableTiming));
+    SML_CHECK_HIP(hipEventCreateWithFlags(&after_, hipEventDisableTiming));
+  }
+  ~StreamRingPy() {
+    if (running_) (void)hipStreamSynchronize(train_);
+    (void)hipEventDestroy(before_);
+    (void)hipEventDestroy(after_);
+    (void)hipStreamDestroy(train_);
+  }
+  at::Tensor ring() const {
+    auto opts = at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, (int)dev_);
+    return torch::from_blob(ring_.ring(), {ring_.rows(), (int64_t)ring_.features()}, opts);
+  }
+  void reset() {
+    TORCH_CHECK(!running_, "StreamRing.reset: join() the running epoch first");
+    ring_.reset();
+  }
+  void train(const at::Tensor& cursor, const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift,
+             const at::Tensor& params, const at::Tensor& m, const at::Tensor& v, const at::Tensor& iter,
+             const c10::optional<at::Tensor>& metrics, int64_t batch, int64_t max_steps, std::vector<int64_t> dims,
+             std::vector<int64_t> acts, double l1, double lr, double beta1, double beta2, double eps, double gscale,
+             bool want_acc, double timeout_s) {
+    TORCH_CHECK(!running_, "StreamRing.train: an epoch is already running");
+    TORCH_CHECK(ring_.pushed() == 0 && ring_.consumed() == 0, "StreamRing.train: reset() the ring first");
+    TORCH_CHECK(ring_.rows() % batch == 0, "StreamRing: ring rows must be a multiple of the batch");
+    TORCH_CHECK(params.numel() == sml::ae_nparam(), "StreamRing.train: one model");
+    TORCH_CHECK(params.device().index() == dev_, "StreamRing.train: parameters on another device");
+    c10::hip::HIPGuard guard((int)dev_);
+    // the kernel sees everything queued before it on the caller's stream (params, cursor)
+    SML_CHECK_HIP(hipEventRecord(before_, cur_stream(params)));
+    SML_CHECK_HIP(hipStreamWaitEvent(train_, before_, 0));
+    const sml::MBStream sr = ring_.counters(timeout_s);
+    train_minibatches_impl(ring(), cursor, scale, shift, params, m, v, iter, metrics, batch, max_steps,
+                           std::move(dims), std::move(acts), l1, lr, beta1, beta2, eps, gscale, want_acc,
+                           c10::nullopt, c10::nullopt, 0, 1, 0, 0, 0, c10::nullopt, &sr, train_);
+    SML_CHECK_HIP(hipEventRecord(after_, train_));
+    running_ = true;
+  }
+  void push(const at::Tensor& x, double timeout_s) {
+    check_dev(x, "rows", at::kFloat);
+    TORCH_CHECK(x.dim() == 2 && x.size(1) >= ring_.features() && x.stride(1) == 1, "rows must be [n, >= features]");
+    TORCH_CHECK(x.device().index() == dev_, "rows on another device");
+    if (x.size(0) == 0) return;
+    py::gil_scoped_release nogil;   // may block on back-pressure while the kernel trains
+    ring_.push(x.data_ptr<float>(), x.size(0), x.stride(0), cur_stream(x), timeout_s);
+  }
+  void finish() { ring_.finish(); }
+  // the caller's stream waits for the epoch's kernel; returns the kernel's status
+  int join() {
+    if (running_) {
+      c10::hip::HIPGuard guard((int)dev_);
+      SML_CHECK_HIP(hipStreamWaitEvent(c10::hip::getCurrentHIPStream((int)dev_).stream(), after_, 0));
+      running_ = false;
+    }
+    return ring_.status();
+  }
+  // wait on the host for the kernel (used before reading counters)
+  void synchronize() {
+    py::gil_scoped_release nogil;
+    SML_CHECK_HIP(hipEventSynchronize(after_));
+  }
+  int64_t pushed() const { return ring_.pushed(); }
+  int64_t consumed() const { return ring_.consumed(); }
+  int status() const { return ring_.status(); }
+  int64_t rows() const { return ring_.rows(); }
+
+ private:
+  int64_t dev_;
+  sml::StreamRing ring_;
+  hipStream_t train_ = nullptr;
+  hipEvent_t before_ = nullptr, after_ = nullptr;
+  bool running_ = false;
+};
 
 void ae_forward(const at::Tensor& x, const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift,
                 const at::Tensor& params, const c10::optional<at::Tensor>& recon,
@@ -1044,6 +1145,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("status_ptr", [](const P2PPy& p) { return reinterpret_cast<uint64_t>(p.x->status_dev()); });
   m.def("p2p_allreduce", &p2p_allreduce, "in-place sum over the P2P exchange's ranks (one launch, one xGMI hop)",
         py::arg("x"), py::arg("exchange"), py::arg("timeout_s") = 10.0);
+  py::class_<StreamRingPy>(m, "StreamRing")
+      .def(py::init<int64_t, int64_t, int64_t>(), py::arg("device"), py::arg("rows"), py::arg("features"))
+      .def("ring", &StreamRingPy::ring)
+      .def("reset", &StreamRingPy::reset)
+      .def("train", &StreamRingPy::train, py::arg("cursor"), py::arg("scale"), py::arg("shift"), py::arg("params"),
+           py::arg("m"), py::arg("v"), py::arg("iter"), py::arg("metrics"), py::arg("batch"), py::arg("max_steps"),
+           py::arg("dims"), py::arg("acts"), py::arg("l1"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"),
+           py::arg("eps"), py::arg("gscale"), py::arg("want_acc"), py::arg("timeout_s") = 30.0)
+      .def("push", &StreamRingPy::push, py::arg("rows"), py::arg("timeout_s") = 30.0)
+      .def("finish", &StreamRingPy::finish)
+      .def("join", &StreamRingPy::join)
+      .def("synchronize", &StreamRingPy::synchronize)
+      .def_property_readonly("pushed", &StreamRingPy::pushed)
+      .def_property_readonly("consumed", &StreamRingPy::consumed)
+      .def_property_readonly("status", &StreamRingPy::status)
+      .def_property_readonly("rows", &StreamRingPy::rows);
   py::class_<RingPy>(m, "PinnedRing")
       .def(py::init<int, int64_t, int>(), py::arg("slots"), py::arg("slot_bytes"), py::arg("device"))
       .def("fill", &RingPy::fill, py::arg("slot"), py::arg("array"), py::arg("offset") = 0)

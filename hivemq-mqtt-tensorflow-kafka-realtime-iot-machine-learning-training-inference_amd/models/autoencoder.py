@@ -16,6 +16,7 @@ reference ``normalize_fn`` inside the kernel's first load.
 from __future__ import annotations
 
 import math
+import os
 import sys
 import time
 from typing import List, Optional, Sequence, Tuple, Union
@@ -546,12 +547,20 @@ class Autoencoder:
         yield from DeviceLoader(stream, self.device, max_rows=chunk_rows, features=self.spec.input_dim).chunks()
 
     def _fit_stream_persistent(self, stream, B: int, max_steps: Optional[int], gstep: int, rank: int) -> int:
-        """One streaming epoch on the persistent kernel: whole device chunks go to
-        ``train_rows`` (hundreds of Keras steps per launch); the < B rows left at a chunk
-        boundary are carried to the next chunk, so the batches are exactly the
-        reference's ``batch(B)`` over the (filtered) stream; ``max_steps`` = ``take(n)``."""
+        """One streaming epoch on the persistent kernel.  Default: ONE launch for the whole
+        epoch fed through the device ring's doorbell (``FusedAE.train_stream``: batches
+        straddle chunk boundaries inside the ring, no carry copy, no launch per chunk).
+        With fault injection armed (SML_FAULT_STEP) or SML_STREAM_DOORBELL=0, whole device
+        chunks go to ``train_rows`` instead and the < B rows left at a chunk boundary are
+        carried to the next chunk (injection needs a host point between steps).  Both give
+        exactly the reference's ``batch(B)`` over the (filtered) stream; ``max_steps`` =
+        ``take(n)``."""
         from ..parallel.fault import maybe_inject, maybe_inject_range
         be = self.backend
+        if os.environ.get("SML_FAULT_STEP") is None and os.environ.get("SML_STREAM_DOORBELL", "1") != "0":
+            maybe_inject(gstep, rank)
+            steps, _ = be.train_stream(self._stream_device_chunks(stream), B, max_steps)
+            return steps
         D = self.spec.input_dim
         carry = torch.empty((B, D), dtype=torch.float32, device=self.device)
         have, steps = 0, 0

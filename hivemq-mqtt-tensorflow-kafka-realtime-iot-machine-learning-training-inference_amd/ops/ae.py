@@ -343,6 +343,72 @@ class FusedAE:
             steps += 1
         return steps, nfull * B + rem
 
+    def train_stream(self, chunks, batch: int, max_steps: Optional[int] = None, ring_rows: Optional[int] = None,
+                     timeout_s: float = 60.0) -> Tuple[int, int]:
+        """Keras ``fit`` over a stream of device row chunks on ONE persistent-kernel launch.
+
+        The kernel (``ae_minibatch.hip`` streaming mode) starts before the first chunk and
+        stays resident for the whole epoch; ``push`` copies each chunk into a device ring
+        and rings a doorbell (a host-mapped row count written by the copy stream after the
+        copy), the kernel waits only when its next batch has not landed yet, and reports the
+        rows it no longer needs (back-pressure).  Batches straddle chunk boundaries inside
+        the ring, so there is no carry copy and no launch per chunk.  The stream's last
+        ``n % batch`` rows are Keras' short final batch (one plain launch).  Returns
+        ``(steps, rows)``; ``max_steps`` = the reference's ``take(n)`` (cardata-v3.py:218).
+        """
+        B = int(batch)
+        if not 1 <= B <= self.max_minibatch():
+            raise ValueError(f"batch {B} outside [1, {self.max_minibatch()}]")
+        D = self.spec.input_dim
+        if ring_rows is None:
+            ring_rows = 1 << 20
+        rows = max(B, (int(ring_rows) // B) * B)
+        sr = getattr(self, "_sring", None)
+        if sr is None or sr.rows != rows or getattr(self, "_sring_b", None) != B:
+            sr = self.C.StreamRing(self.device.index or 0, rows, D)
+            self._sring, self._sring_b = sr, B
+        if not hasattr(self, "_tcur"):
+            self._tcur = torch.zeros(1, dtype=torch.int64, device=self.device)
+        sr.reset()
+        self._tcur.zero_()
+        it0 = int(self.iter.item())
+        nmax = (1 << 30) if max_steps is None else int(max_steps)
+        if nmax <= 0:
+            return 0, 0
+        limit = None if max_steps is None else nmax * B
+        sr.train(self._tcur, self.scale, self.shift, self.params, self.m, self.v, self.iter, self.metrics, B, nmax,
+                 self.spec.dims, self.spec.act_codes, float(self.spec.activity_l1), self.lr, self.beta_1,
+                 self.beta_2, self.epsilon, 1.0 / B, bool(self.want_acc), float(timeout_s))
+        pushed = 0
+        try:
+            for xd in chunks:
+                if limit is not None and pushed >= limit:
+                    break
+                if xd.dim() != 2 or xd.size(1) < D:
+                    raise ValueError(f"stream chunks must be [n, >= {D}] rows")
+                if limit is not None and pushed + xd.size(0) > limit:
+                    xd = xd[:limit - pushed]
+                sr.push(xd, float(timeout_s))
+                pushed += int(xd.size(0))
+        finally:
+            sr.finish()
+            sr.join()
+            sr.synchronize()
+        if sr.status:
+            raise RuntimeError(f"streaming fit: the training kernel waited {timeout_s:.0f} s for rows")
+        steps = int(self.iter.item()) - it0
+        rem = pushed - steps * B
+        if steps < pushed // B:
+            raise RuntimeError(f"streaming fit: kernel trained {steps} of {pushed // B} full batches")
+        if 0 < rem < B and steps < nmax:
+            start = (steps * B) % rows      # a multiple of B: the short batch never wraps
+            self._tcur.zero_()
+            self._launch_minibatch(sr.ring()[start:start + rem], self._tcur, rem, 1)
+            steps += 1
+        else:
+            rem = 0
+        return steps, (steps - (1 if rem else 0)) * B + rem
+
     def _launch_minibatch(self, ring: torch.Tensor, cursor: torch.Tensor, B: int, nsteps: int,
                           prof: Optional[torch.Tensor] = None, dp=None) -> None:
         kw, gscale = {}, 1.0 / B
