@@ -63,6 +63,9 @@ def parse():
     p.add_argument("--batch32-steps", type=int, default=20000,
                    help="steps per launch of the Keras batch-32 side measurement (0 = skip)")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--settle-ms", type=float, default=0.0,
+                   help="untimed steps before the warm-up until this much GPU time has passed (DPM clock settle)")
+    p.add_argument("--headline-only", action="store_true", help="skip every side measurement")
     p.add_argument("--dump-params", default=None,
                    help="write this rank's final parameter image to <path>.rank<R>.npy (replica checks)")
     p.add_argument("--graph", action="store_true",
@@ -425,6 +428,13 @@ def main():
             else:
                 eager_step()
 
+    settle_steps = 0
+    if args.settle_ms > 0:
+        ts = time.perf_counter()
+        while (time.perf_counter() - ts) * 1e3 < args.settle_ms:
+            run(4, 0)
+            torch.cuda.synchronize()
+            settle_steps += 4
     run(args.warmup, 0)
     dp.barrier(device)
     torch.cuda.synchronize()
@@ -441,6 +451,11 @@ def main():
     # per-rank timed-region spread (the headline uses the max)
     spread = gather_all([t1 - t0], device)
     step_ms = [v[0] / args.steps * 1e3 for v in spread]
+
+    if args.headline_only:
+        for k in ("infer_events", "e2e_events", "batch32_steps", "dp_steps", "collective_iters", "fit_epochs",
+                  "fresh_steps", "fit_rows", "stream_rows", "lstm_steps"):
+            setattr(args, k, 0)
 
     def guarded(fn, *a, **kw):   # a side measurement never takes the headline down
         try:
@@ -533,6 +548,7 @@ def main():
             },
             "backend": env.backend,
             "per_rank_ms_per_step": {"min": min(step_ms), "max": max(step_ms), "ranks": step_ms},
+            "clock_settle": {"ms": args.settle_ms, "steps": settle_steps},
             "pack_ms": pack_ms,
             "p50_infer_us": max(p50s) if p50s else None,   # worst replica (conservative)
             "p99_infer_us": max((r.get("p99_us") or 0.0) for r in per_rank_infer if isinstance(r, dict)) or None,

@@ -24,14 +24,15 @@
 //            stored in fragment order (one contiguous 256-byte block per K-step: no
 //            bank conflicts).  Bias = the accumulator's initial value.  Loss and the L1
 //            activity term are lane-local.  The wave then stores its activations /
-//            gradients / reconstructions [row][feature] to LDS.
+//            gradients [row][feature] to LDS (column-swizzled, see swz()), and takes
+//            the categorical accuracy of its rows in registers (lane-local argmax over
+//            its 8 features + two cross-lane steps).
 //   barrier
 //   phase B  waves 0-5 each own one 16x16 tile of the padded parameter image: weight
 //            gradient act^T . dz over the B rows (fp32 MFMA, K = 4 rows per
 //            instruction, bias rows read a constant 1), then Keras Adam on the 4
 //            parameters per lane they hold in registers for the whole launch, and
-//            write the new values into the forward / backward weight fragments;
-//            waves 6-7 take the argmax accuracy of one row per lane meanwhile.
+//            write the new values into the forward / backward weight fragments.
 //   barrier
 // Two barriers per step (the round-1 version had eight, one per layer phase, and did
 // every dot product on the VALU: 12 us per batch-100 step).
@@ -57,6 +58,13 @@ constexpr int MB_SMALL = 48, MB_LARGE = 128, MAXB = MB_LARGE;
 // reads of rows r and r+1 by the two 16-lane halves of a ds_read_b32 group never share a bank
 constexpr int XS = 48;   // x / dz4 rows (<= 32 features)
 constexpr int HS = 16;   // hidden rows (<= 16 features)
+// Column swizzle of those rows: feature f of row r lives at column f ^ swz(r).  A phase-A
+// ds_write_b128 is serviced in 8-lane groups (rows 16w + 0..7 of one column block, bank =
+// dword mod 32): unswizzled, rows r and r + 2 hit the same 16-byte bank slot (4-way
+// conflict, ~60 % of the kernel's SQ_LDS_BANK_CONFLICT, profiles/r03); swizzled, the 8 rows
+// cover 8 distinct slots.  The phase-B ds_read_b32 groups read rows 4 s4 + {0, 1} (or
+// {2, 3}) -- one swz value per group -- so they stay conflict-free.
+__device__ __forceinline__ int swz(int r) { return 4 * ((r >> 1) & 3); }
 // padded parameter image (ae_fused.hip / ops/ae.py LAYOUT): L1 [32][16] @0 (bias row 31),
 // L2 [16][16] @512, L3 @768 (bias row 15), L4 [16][32] @1024 (bias row 15)
 constexpr int IMG2 = 512, IMG3 = 768, IMG4 = 1024, NPARAM = 1536;
@@ -115,13 +123,12 @@ struct MBArgs {
 };
 
 template <int MB>
-struct Smem {   // MB 48: ~47 KB, MB 128: ~108 KB
+struct Smem {   // MB 48: ~38 KB, MB 128: ~84 KB
   float w[W_END];
   float x[MB * XS];                     // normalised inputs (phase-B activation of L1)
   float h1[MB * HS], h2[MB * HS], h3[MB * HS];
   float dz4[MB * XS];
   float dz3[MB * HS], dz2[MB * HS], dz1[MB * HS];
-  float y[MB * XS];                     // reconstructions (phase-B argmax accuracy)
   float one[4];                         // constant 1 (bias-row activation), dummy store slot
   float red[3][NT / 64];
   int abort;                            // DP: a gradient exchange timed out (all waves stop)
@@ -159,9 +166,9 @@ __device__ __forceinline__ void lds_slots(int p, int& fw, int& bw, int none) {
 // MFMAs (K = 4 batch rows per instruction).  Tiles: 0/1 = L1 rows 0-15 / 16-31, 2 = L2,
 // 3 = L3, 4/5 = L4 cols 0-15 / 16-31; wave w < 6 owns tile w.
 struct Tile {
-  int act, as;      // activation base (float offset into Smem) + this lane's column, row stride;
+  int act, as, am;  // activation base (float offset into Smem), row stride, this lane's column;
                     // a bias-row lane reads the constant-1 word with stride 0 (branch-free)
-  int dz, ds;       // upstream-gradient base + this lane's column, row stride
+  int dz, ds, dc;   // upstream-gradient base, row stride, this lane's column
   int slot0, sst;   // image slots of C[4g+i][c]: slot0 + i * sst (consecutive image rows)
   __device__ __forceinline__ int slot(int i) const { return slot0 + i * sst; }
 };
@@ -182,13 +189,12 @@ __device__ __forceinline__ Tile make_tile(int id, int c, int g, const SM& S, con
     T.act = (int)(S.h3 - sbase); T.as = HS; T.dz = (int)(S.dz4 - sbase); T.ds = XS;
   }
   const int m = row0 + c;
+  T.am = m;
   if (m == bias_row) {
     T.act = (int)(S.one - sbase);
     T.as = 0;
-  } else {
-    T.act += m;
   }
-  T.dz += col0 + c;
+  T.dc = col0 + c;
   T.slot0 = img + (row0 + 4 * g) * istride + col0 + c;
   T.sst = istride;
   return T;
@@ -462,21 +468,49 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const float sgn = h != 0.f ? __builtin_copysignf(1.0f, h) : 0.f;
         dz1[i] = fm(4 * g + i < n1, act_grad(a1, h, fmaf(l1r, sgn, acc1[i])));
       }
-      // rows -> LDS [row][feature] for the weight-gradient contraction and the accuracy (16-byte stores)
+      // rows -> LDS [row][feature ^ swz(row)] for the weight-gradient contraction (16-byte stores)
       const int r = row_l;
-      st4(S.x + r * XS + 4 * g, f32x4{xv[0], xv[1], xv[2], xv[3]});
-      st4(S.x + r * XS + 16 + 4 * g, f32x4{xv[4], xv[5], xv[6], xv[7]});
-      st4(S.h1 + r * HS + 4 * g, h1);
-      st4(S.h2 + r * HS + 4 * g, h2);
-      st4(S.h3 + r * HS + 4 * g, h3);
-      st4(S.dz4 + r * XS + 4 * g, dz4[0]);
-      st4(S.dz4 + r * XS + 16 + 4 * g, dz4[1]);
-      st4(S.dz3 + r * HS + 4 * g, dz3);
-      st4(S.dz2 + r * HS + 4 * g, dz2);
-      st4(S.dz1 + r * HS + 4 * g, dz1);
+      const int cw = (4 * g) ^ swz(r);
+      st4(S.x + r * XS + cw, f32x4{xv[0], xv[1], xv[2], xv[3]});
+      st4(S.x + r * XS + 16 + cw, f32x4{xv[4], xv[5], xv[6], xv[7]});
+      st4(S.h1 + r * HS + cw, h1);
+      st4(S.h2 + r * HS + cw, h2);
+      st4(S.h3 + r * HS + cw, h3);
+      st4(S.dz4 + r * XS + cw, dz4[0]);
+      st4(S.dz4 + r * XS + 16 + cw, dz4[1]);
+      st4(S.dz3 + r * HS + cw, dz3);
+      st4(S.dz2 + r * HS + cw, dz2);
+      st4(S.dz1 + r * HS + cw, dz1);
       if (a.want_acc) {
-        st4(S.y + r * XS + 4 * g, y[0]);
-        st4(S.y + r * XS + 16 + 4 * g, y[1]);
+        // Keras categorical accuracy, argmax(y) == argmax(x) with ties to the lowest feature:
+        // lane (c, g) holds features 16 t4 + 4 g + i of row c (increasing in (t4, i)), so a
+        // strict lane-local argmax, then the row's four lane groups combine (xor 16, 32).
+        float by = -__builtin_inff(), bx = -__builtin_inff();
+        int iy = 64, ix = 64;
+#pragma unroll
+        for (int t4 = 0; t4 < 2; ++t4) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int f = 16 * t4 + 4 * g + i;
+            const float yy = y[t4][i], xx = xv[4 * t4 + i];
+            const bool gy = f < D && yy > by, gx = f < D && xx > bx;
+            by = gy ? yy : by;
+            iy = gy ? f : iy;
+            bx = gx ? xx : bx;
+            ix = gx ? f : ix;
+          }
+        }
+#pragma unroll
+        for (int off = 16; off <= 32; off <<= 1) {
+          const float oy = __shfl_xor(by, off, 64), ox = __shfl_xor(bx, off, 64);
+          const int jy = __shfl_xor(iy, off, 64), jx = __shfl_xor(ix, off, 64);
+          const bool ty = oy > by || (oy == by && jy < iy), tx = ox > bx || (ox == bx && jx < ix);
+          by = ty ? oy : by;
+          iy = ty ? jy : iy;
+          bx = tx ? ox : bx;
+          ix = tx ? jx : ix;
+        }
+        corr += (g == 0 && row_ok && iy == ix) ? 1.f : 0.f;
       }
     }
     mark(0);
@@ -489,6 +523,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       const float lr_t = a.lr * __builtin_amdgcn_sqrtf((float)(1.0 - b2t)) * __builtin_amdgcn_rcpf((float)(1.0 - b1t));
       const float* av = sbase + T.act;
       const float* dv = sbase + T.dz;
+      // row r = 4 s4 + g has swz(r) = 4 ((2 s4 + (g >> 1)) & 3): one column per lane for even
+      // s4 (E) and one for odd s4 (O); the bias-row lane reads the constant word unswizzled
+      const int X0 = 4 * (g >> 1), X1 = 4 * (2 + (g >> 1));
+      const int aE = T.as ? (T.am ^ X0) : 0, aO = T.as ? (T.am ^ X1) : 0;
+      const int dE = T.dc ^ X0, dO = T.dc ^ X1;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if constexpr (TB > 0) {
         constexpr int NS = (TB + 3) / 4;
@@ -499,7 +538,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
         for (int s4 = 0; s4 < NS; ++s4) {
           const int r = 4 * s4 + g;   // rows in [B, 4*NS) hold zero gradients
-          part[s4 % CH] = mfma4(av[r * T.as], dv[r * T.ds], part[s4 % CH]);
+          part[s4 % CH] = mfma4(av[r * T.as + ((s4 & 1) ? aO : aE)], dv[r * T.ds + ((s4 & 1) ? dO : dE)],
+                                part[s4 % CH]);
         }
 #pragma unroll
         for (int c4 = 0; c4 < CH; ++c4) acc += part[c4];
@@ -508,13 +548,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const int ns = (B + 3) / 4;
         int s4 = 0;
         for (; s4 + 1 < ns; s4 += 2) {
-          const int r = 4 * s4 + g;
-          acc = mfma4(av[r * T.as], dv[r * T.ds], acc);
-          acc2 = mfma4(av[(r + 4) * T.as], dv[(r + 4) * T.ds], acc2);
+          const int r = 4 * s4 + g;   // s4 even, s4 + 1 odd
+          acc = mfma4(av[r * T.as + aE], dv[r * T.ds + dE], acc);
+          acc2 = mfma4(av[(r + 4) * T.as + aO], dv[(r + 4) * T.ds + dO], acc2);
         }
         if (s4 < ns) {
           const int r = 4 * s4 + g;
-          acc = mfma4(av[r * T.as], dv[r * T.ds], acc);
+          acc = mfma4(av[r * T.as + aE], dv[r * T.ds + dE], acc);
         }
         acc += acc2;
       }
@@ -576,23 +616,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         S.w[fpos[i]] = wo[i];
         S.w[bpos[i]] = wo[i];
       }
-    } else if (a.want_acc && t - 6 * 64 < B) {
-      // categorical accuracy (waves 6-7, one row per lane): argmax of y and x, ties -> lowest index
-      const int r = t - 6 * 64;
-      const float* yr = S.y + r * XS;
-      const float* xq = S.x + r * XS;
-      float by = yr[0], bx = xq[0];
-      int iy = 0, ix = 0;
-#pragma unroll
-      for (int f = 1; f < KD; ++f) {   // branch-free selects
-        const float yv = yr[f], xw = xq[f];
-        const bool gy = f < D && yv > by, gx = f < D && xw > bx;
-        by = gy ? yv : by;
-        iy = gy ? f : iy;
-        bx = gx ? xw : bx;
-        ix = gx ? f : ix;
-      }
-      corr += iy == ix ? 1.f : 0.f;
     }
     mark(2);
     lds_barrier();

@@ -94,4 +94,18 @@ void PinnedRing::release(int slot, hipStream_t stream) {
   state_[(size_t)slot] = SlotState::kIdle;
 }
 
+void PinnedRing::reset() {
+  for (size_t i = 0; i < host_.size(); ++i) {
+    bool pending;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      pending = pending_copy_[i] != 0;
+    }
+    if (pending) RING_CHECK(hipEventSynchronize(copied_[i]));
+    std::lock_guard<std::mutex> g(mu_);
+    pending_copy_[i] = 0;
+    state_[i] = SlotState::kIdle;
+  }
+}
+
 }  // namespace sml

@@ -36,6 +36,10 @@ class PinnedRing {
   void wait(int slot, hipStream_t stream);
   // Consumer is done with the device buffer of `slot` once `stream` reaches here.
   void release(int slot, hipStream_t stream);
+  // Back to all-IDLE for a new owner (a pooled ring, data/loader.py): copies submitted but
+  // never consumed are waited for on the host; pending releases stay pending (the next
+  // submit of that slot still waits for the old consumer's release event).
+  void reset();
   //
   // Ordering contract, asserted on every call (every H2D copy records an
   // event that the compute stream waits on), per slot:

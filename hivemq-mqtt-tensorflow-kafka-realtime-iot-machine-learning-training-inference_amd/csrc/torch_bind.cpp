@@ -1168,6 +1168,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("submit", &RingPy::submit, py::arg("slot"), py::arg("dst"), py::arg("bytes"))
       .def("wait", &RingPy::wait, py::arg("slot"))
       .def("release", &RingPy::release, py::arg("slot"))
+      .def("reset", [](RingPy& r) {
+        py::gil_scoped_release rel;
+        r.r->reset();
+      })
       .def_property_readonly("slots", [](const RingPy& r) { return r.r->slots(); })
       .def_property_readonly("slot_bytes", [](const RingPy& r) { return (int64_t)r.r->slot_bytes(); })
       .def_property_readonly("bytes_copied", [](const RingPy& r) { return (uint64_t)r.r->bytes_copied(); });

@@ -18,9 +18,15 @@ Pipeline (all stages overlap; up to ``slots - 1`` H2D copies in flight):
 ``chunks()`` yields whole device chunks (the persistent-kernel ``fit`` path consumes
 many Keras batches per launch); iterating the loader yields ``(rows, chunk)`` per
 ring slot, or exact ``batch_rows``-row batches in device-filter mode.
+
+Pinned rings come from a process-wide pool (:func:`pinned_ring`): allocating page-locked
+memory is slow, and FREEING it (hipHostFree) synchronises the whole device -- which would
+stall for as long as a persistent kernel that waits for this very stream's rows (the
+one-launch streaming epoch, ``FusedAE.train_stream``) is running.
 """
 from __future__ import annotations
 
+import contextlib
 import queue
 import threading
 import time
@@ -34,6 +40,28 @@ from ..ops._ext import load_c
 from .stream import Chunk, Stream
 
 _END = object()
+
+_RING_POOL: dict = {}
+_POOL_LOCK = threading.Lock()
+
+
+@contextlib.contextmanager
+def pinned_ring(slots: int, slot_bytes: int, device_index: int):
+    """A ``PinnedRing`` of this exact shape from the process-wide pool (allocated on first
+    use), reset to all-idle and returned to the pool on exit -- never freed while the
+    process runs (see the module docstring)."""
+    key = (int(slots), int(slot_bytes), int(device_index))
+    with _POOL_LOCK:
+        free = _RING_POOL.setdefault(key, [])
+        ring = free.pop() if free else None
+    if ring is None:
+        ring = load_c().PinnedRing(*key)
+    try:
+        yield ring
+    finally:
+        ring.reset()   # copies submitted but never consumed land before the next owner
+        with _POOL_LOCK:
+            _RING_POOL[key].append(ring)
 
 
 class DeviceLoader:
@@ -59,8 +87,7 @@ class DeviceLoader:
         self.row_bytes = self.features * 4
         # slot layout: n rows [n, F] float32, then n label bytes right behind them
         self.slot_bytes = self.max_rows * (self.row_bytes + 1)
-        C = load_c()
-        self.ring = C.PinnedRing(self.slots, self.slot_bytes, self.device.index)
+        self.ring = None   # a pooled PinnedRing while iterating (pinned_ring)
         self.bufs = [torch.empty(self.slot_bytes, dtype=torch.uint8, device=self.device) for _ in range(self.slots)]
         self.rows = 0
         self.keep_label = keep_label
@@ -112,6 +139,14 @@ class DeviceLoader:
     def _slots(self) -> Iterator[Tuple[int, int, Chunk]]:
         """Ring slots in order, copy waited for on the consumer's stream; the slot is
         released (and handed back to the producer) when the consumer asks for the next."""
+        with pinned_ring(self.slots, self.slot_bytes, self.device.index) as ring:
+            self.ring = ring
+            try:
+                yield from self._slots_on_ring()
+            finally:
+                self.ring = None
+
+    def _slots_on_ring(self) -> Iterator[Tuple[int, int, Chunk]]:
         q: "queue.Queue" = queue.Queue()
         stop = threading.Event()
         free = threading.Semaphore(self.slots)

@@ -165,7 +165,7 @@ class NativeFeed:
         slabs are submitted to the copy engine ahead of the one being consumed."""
         import torch
 
-        from ..ops._ext import load_c
+        from ..data.loader import pinned_ring
         dev = torch.device(device)
         if dev.index is None:
             dev = torch.device("cuda", torch.cuda.current_device())
@@ -173,7 +173,12 @@ class NativeFeed:
         nslots = int(slots or 2 * self.workers + 6)
         depth = int(inflight or max(2, nslots - self.workers - 1))
         slab_bytes = slab_rows * (F * 4 + 1)
-        ring = load_c().PinnedRing(nslots, slab_bytes, dev.index)
+        with pinned_ring(nslots, slab_bytes, dev.index) as ring:   # pooled: never freed mid-stream
+            yield from self._device_chunks_on(ring, dev, keep_label, slab_rows, nslots, depth, slab_bytes)
+
+    def _device_chunks_on(self, ring, dev, keep_label, slab_rows, nslots, depth, slab_bytes):
+        import torch
+        F = self.features
         bufs = [torch.empty(slab_bytes, dtype=torch.uint8, device=dev) for _ in range(nslots)]
         f, client, parts = self._make(keep_label)
         t0 = time.perf_counter()

@@ -362,7 +362,9 @@ class FusedAE:
         D = self.spec.input_dim
         if ring_rows is None:
             ring_rows = 1 << 20
-        rows = max(B, (int(ring_rows) // B) * B)
+        # the kernel reports consumed rows every 8 steps and prefetches one batch ahead, so
+        # back-pressure needs room for >= 10 batches beyond the consumed mark
+        rows = max(32 * B, (int(ring_rows) // B) * B)
         sr = getattr(self, "_sring", None)
         if sr is None or sr.rows != rows or getattr(self, "_sring_b", None) != B:
             sr = self.C.StreamRing(self.device.index or 0, rows, D)
@@ -376,24 +378,31 @@ class FusedAE:
         if nmax <= 0:
             return 0, 0
         limit = None if max_steps is None else nmax * B
+        # Set the producer up BEFORE the kernel starts: building a loader allocates pinned
+        # memory and starts threads, and no runtime call that may synchronise the device may
+        # run while the resident kernel waits for the rows it produces.
+        it = iter(chunks)
+        xd = next(it, None)
         sr.train(self._tcur, self.scale, self.shift, self.params, self.m, self.v, self.iter, self.metrics, B, nmax,
                  self.spec.dims, self.spec.act_codes, float(self.spec.activity_l1), self.lr, self.beta_1,
                  self.beta_2, self.epsilon, 1.0 / B, bool(self.want_acc), float(timeout_s))
         pushed = 0
         try:
-            for xd in chunks:
-                if limit is not None and pushed >= limit:
-                    break
+            while xd is not None and (limit is None or pushed < limit):
                 if xd.dim() != 2 or xd.size(1) < D:
                     raise ValueError(f"stream chunks must be [n, >= {D}] rows")
                 if limit is not None and pushed + xd.size(0) > limit:
                     xd = xd[:limit - pushed]
                 sr.push(xd, float(timeout_s))
                 pushed += int(xd.size(0))
+                xd = next(it, None)
         finally:
             sr.finish()
             sr.join()
             sr.synchronize()
+            close = getattr(it, "close", None)
+            if close is not None:   # a partly consumed producer cleans up now, not mid next epoch
+                close()
         if sr.status:
             raise RuntimeError(f"streaming fit: the training kernel waited {timeout_s:.0f} s for rows")
         steps = int(self.iter.item()) - it0

@@ -29,8 +29,14 @@ def main():
         data = synthetic_device_tensor(B * 32768, dev, seed=0)
         ae = FusedAE(spec, init_dense_weights(spec.layer_sizes, seed=0), dev, scale=sc, shift=sh)
         ae.attach_ring(data, B)
-        for _ in range(4):
+        for _ in range(3):
             ae.train_minibatches(a.steps)
+        import time
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ae.train_minibatches(a.steps)
+        torch.cuda.synchronize()
+        print(f"{a.mode}: {(time.perf_counter() - t0) / a.steps * 1e6:.3f} us/step", flush=True)
     else:
         from streamml.data.stream import sliding_windows
         from streamml.models.lstm import LSTMPredictor

@@ -3,7 +3,9 @@
 //           across PCIe (the current ae_serve.hip design);
 //   vram -- fine-grained device memory that the CPU writes through the PCIe BAR
 //           (HSA pool allocation + hsa_amd_agents_allow_access for the CPU agent): the
-//           host's store is a posted write, the GPU polls its own memory.
+//           host's store is a posted write, the GPU polls its own memory;
+//   *_sfence -- the same with a store fence after each host store (the BAR mapping is
+//           write-combining: round 3's first probe saw 8.7 ms p50 without it).
 // One resident wave echoes each tagged request word into a host-memory result word; the
 // host measures store -> echo seen.  Every device spin is bounded (s_memrealtime).
 #include <hip/hip_runtime.h>
@@ -77,7 +79,7 @@ static hsa_status_t agent_cb(hsa_agent_t a, void* data) {
 }
 
 static int run(const char* name, uint64_t* req_host_view, const uint64_t* req_dev_view, uint64_t* res_host,
-               uint64_t* res_dev, int* status_d, int n, std::vector<double>& lat) {
+               uint64_t* res_dev, int* status_d, int n, std::vector<double>& lat, bool fence = false) {
   *reinterpret_cast<volatile uint64_t*>(res_host) = 0;
   *reinterpret_cast<volatile uint64_t*>(req_host_view) = 0;
   hipStream_t s;
@@ -89,6 +91,9 @@ static int run(const char* name, uint64_t* req_host_view, const uint64_t* req_de
     const uint64_t w = ((uint64_t)(uint32_t)(i + 1) << 32) | 0x3f800000u;
     auto t0 = std::chrono::steady_clock::now();
     __atomic_store_n(req_host_view, w, __ATOMIC_RELEASE);
+    // a BAR mapping is write-combining: without a store fence the word can sit in the
+    // core's WC buffer until it is evicted (milliseconds)
+    if (fence) __builtin_ia32_sfence();
     uint64_t spins = 0;
     while (__atomic_load_n(res_host, __ATOMIC_ACQUIRE) != w) {
       if (++spins > 2000000000ull) {
@@ -143,6 +148,8 @@ int main(int argc, char** argv) {
     return 0;
   }
   if (run("vram", (uint64_t*)vr, (const uint64_t*)vr, res_host, res_dev, status_d, n, lat)) return 1;
+  if (run("vram_sfence", (uint64_t*)vr, (const uint64_t*)vr, res_host, res_dev, status_d, n, lat, true)) return 1;
+  if (run("host_sfence", req_h, req_hd, res_host, res_dev, status_d, n, lat, true)) return 1;
   int st = 0;
   CK(hipMemcpy(&st, status_d, sizeof(int), hipMemcpyDeviceToHost));
   std::printf("{\"device_timeouts\": %d}\n", st);
