@@ -17,6 +17,15 @@ Multi GPU:   python -m torch.distributed.run --nproc-per-node N --master-addr 12
                  --master-port P bench.py --gpus N --steps K --warmup W
 Scaling is weak: the per-GPU micro-batch is fixed, global batch = N x micro-batch.
 Reference to beat: 62 661 rows/s (TF 2.0 on a laptop CPU).
+
+Clock settle: before the W warm-up steps, full training steps run untimed for
+``--settle-ms`` (default 100 ms).  A GPU coming out of idle goes through a power /
+clock-management transient lasting ~40 dispatches (~30 ms) of this kernel: per-step time
+750 -> 890 -> ~680 us (profiles/r03/headline_dispatch_*.csv); a 20-step run otherwise
+times mostly that transient (42.2 G rows/s) while a 200-step run is at the steady state
+(47.8).  With the settle the 20-step run measures 48.5 (profiles/r03/SUMMARY.md).  The
+timed steps are unchanged: full optimizer steps, K of them, and the JSON reports the
+settle (``clock_settle``).
 """
 from __future__ import annotations
 
@@ -63,7 +72,7 @@ def parse():
     p.add_argument("--batch32-steps", type=int, default=20000,
                    help="steps per launch of the Keras batch-32 side measurement (0 = skip)")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--settle-ms", type=float, default=0.0,
+    p.add_argument("--settle-ms", type=float, default=100.0,
                    help="untimed steps before the warm-up until this much GPU time has passed (DPM clock settle)")
     p.add_argument("--headline-only", action="store_true", help="skip every side measurement")
     p.add_argument("--dump-params", default=None,
@@ -429,12 +438,17 @@ def main():
                 eager_step()
 
     settle_steps = 0
-    if args.settle_ms > 0:
+    if args.settle_ms > 0:   # clock settle (module docstring); every rank runs the same step count
         ts = time.perf_counter()
-        while (time.perf_counter() - ts) * 1e3 < args.settle_ms:
+        while True:
             run(4, 0)
             torch.cuda.synchronize()
             settle_steps += 4
+            el = (time.perf_counter() - ts) * 1e3
+            if env.is_dist:
+                el = dp.allreduce_max(el, device)   # one decision for all ranks (collectives stay paired)
+            if el >= args.settle_ms:
+                break
     run(args.warmup, 0)
     dp.barrier(device)
     torch.cuda.synchronize()

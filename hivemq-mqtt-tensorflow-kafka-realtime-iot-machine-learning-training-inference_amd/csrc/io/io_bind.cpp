@@ -485,7 +485,8 @@ PYBIND11_MODULE(_io, m) {
       .def("positions", &serve::ScoreLoop::positions)
       .def("latency_records", [](serve::ScoreLoop& l) {
         const auto& v = l.latency_records();
-        py::array_t<int64_t> a(std::vector<ssize_t>{(ssize_t)(v.size() / 3), 3});
+        constexpr int C = serve::ScoreLoop::kLatCols;
+        py::array_t<int64_t> a(std::vector<ssize_t>{(ssize_t)(v.size() / C), C});
         std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(int64_t));
         return a;
       });

@@ -860,6 +860,25 @@ std::vector<int64_t> Broker::append_times(const std::string& topic, int partitio
   return out;
 }
 
+// Low-latency mode (spin_us > 0): take the broker lock by spinning on try_lock for up to
+// `spin_us` before blocking.  The lock is only ever held for microseconds (picking segments,
+// appending a batch); a blocked lock() parks the thread in the kernel and costs a
+// scheduler wake-up (several microseconds) on exactly the append -> fetch path the
+// low-latency serving loop measures.
+static void lock_spin(std::unique_lock<std::mutex>& g, int spin_us) {
+  if (spin_us > 0) {
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
+    for (uint32_t i = 0;; ++i) {
+      if (g.try_lock()) return;
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+      if ((i & 63) == 63 && std::chrono::steady_clock::now() >= t_end) break;
+    }
+  }
+  g.lock();
+}
+
 int64_t Broker::append_locked(Partition& p, const Record* recs, size_t n) {
   const int64_t base = p.end;
   if (record_times_.load(std::memory_order_relaxed)) {
@@ -978,7 +997,8 @@ Broker::FetchReply Broker::handle_fetch(const uint8_t* body, size_t n) {
     // fetch.max.wait.ms: when nothing is available yet the request parks on data_cv_
     // (signalled by every append) instead of returning empty, so a consumer sees a new
     // record one wake-up after it is appended, without polling.
-    std::unique_lock<std::mutex> g(mu_);
+    std::unique_lock<std::mutex> g(mu_, std::defer_lock);
+    lock_spin(g, spin_us_.load());
     const int fe = fail_every_.load();
     const bool fail = fe > 0 && nth % (uint64_t)fe == 0;
     auto pick = [&]() {   // -> (any bytes, any error)
@@ -1025,7 +1045,7 @@ Broker::FetchReply Broker::handle_fetch(const uint8_t* body, size_t n) {
         __builtin_ia32_pause();
 #endif
       }
-      g.lock();
+      lock_spin(g, spin);
       st = pick();
     }
     if (!st.first && !st.second && min_bytes > 0 && max_wait_ms > 0) {
@@ -1236,7 +1256,8 @@ std::string Broker::handle(int16_t api, int16_t ver, const uint8_t* body, size_t
     flat.append(fr.meta, at, std::string::npos);
     return flat;
   }
-  std::lock_guard<std::mutex> g(mu_);
+  std::unique_lock<std::mutex> g(mu_, std::defer_lock);
+  lock_spin(g, spin_us_.load());
   switch (api) {
     case API_METADATA: {
       const int32_t nt = r.i32();

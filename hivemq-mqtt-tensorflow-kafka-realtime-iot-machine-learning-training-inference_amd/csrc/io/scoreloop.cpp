@@ -153,10 +153,13 @@ LoopStats ScoreLoop::run(int64_t max_events, double idle_timeout_s) {
         const int64_t t5 = steady_ns();
         st.produce_s += secs(t4, t5);
         if (cfg_.record_latency)
-          for (int i = 0; i < k; ++i) {
+          for (int i = 0; i < k; ++i) {   // kLatCols per event (scoreloop.h)
             lat_.push_back(cfg_.partitions[pi]);
             lat_.push_back(offs[(size_t)i]);
             lat_.push_back(t5);
+            lat_.push_back(t1);
+            lat_.push_back(t3);
+            lat_.push_back(t4);
           }
         st.events += (uint64_t)k;
         ++st.batches;

@@ -65,6 +65,9 @@ class ScoreLoop {
   void stop() { stop_ = true; }
   std::vector<int64_t> positions() const;   // next offset per owned partition
   // (partition, offset, visible_ns) per scored event when record_latency
+  // kLatCols int64 per scored event: partition, offset, steady-clock ns of the produce ack
+  // (result visible), of the fetch response, of the scores, of the formatted records
+  static constexpr int kLatCols = 6;
   const std::vector<int64_t>& latency_records() const { return lat_; }
 
  private:

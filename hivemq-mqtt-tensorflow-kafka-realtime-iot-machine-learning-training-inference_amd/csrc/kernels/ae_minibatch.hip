@@ -24,15 +24,17 @@
 //            stored in fragment order (one contiguous 256-byte block per K-step: no
 //            bank conflicts).  Bias = the accumulator's initial value.  Loss and the L1
 //            activity term are lane-local.  The wave then stores its activations /
-//            gradients [row][feature] to LDS (column-swizzled, see swz()), and takes
-//            the categorical accuracy of its rows in registers (lane-local argmax over
-//            its 8 features + two cross-lane steps).
+//            gradients / reconstructions [row][feature] to LDS (column-swizzled, see
+//            swz()).
 //   barrier
 //   phase B  waves 0-5 each own one 16x16 tile of the padded parameter image: weight
 //            gradient act^T . dz over the B rows (fp32 MFMA, K = 4 rows per
 //            instruction, bias rows read a constant 1), then Keras Adam on the 4
 //            parameters per lane they hold in registers for the whole launch, and
-//            write the new values into the forward / backward weight fragments.
+//            write the new values into the forward / backward weight fragments;
+//            waves 6-7 take the argmax accuracy of one row per lane meanwhile (off the
+//            critical path: the same argmax in phase A, on the row waves, cost
+//            0.4-0.5 us per step, profiles/r03).
 //   barrier
 // Two barriers per step (the round-1 version had eight, one per layer phase, and did
 // every dot product on the VALU: 12 us per batch-100 step).
@@ -123,12 +125,13 @@ struct MBArgs {
 };
 
 template <int MB>
-struct Smem {   // MB 48: ~38 KB, MB 128: ~84 KB
+struct Smem {   // MB 48: ~47 KB, MB 128: ~108 KB
   float w[W_END];
   float x[MB * XS];                     // normalised inputs (phase-B activation of L1)
   float h1[MB * HS], h2[MB * HS], h3[MB * HS];
   float dz4[MB * XS];
   float dz3[MB * HS], dz2[MB * HS], dz1[MB * HS];
+  float y[MB * XS];                     // reconstructions (phase-B argmax accuracy)
   float one[4];                         // constant 1 (bias-row activation), dummy store slot
   float red[3][NT / 64];
   int abort;                            // DP: a gradient exchange timed out (all waves stop)
@@ -482,35 +485,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       st4(S.dz2 + r * HS + cw, dz2);
       st4(S.dz1 + r * HS + cw, dz1);
       if (a.want_acc) {
-        // Keras categorical accuracy, argmax(y) == argmax(x) with ties to the lowest feature:
-        // lane (c, g) holds features 16 t4 + 4 g + i of row c (increasing in (t4, i)), so a
-        // strict lane-local argmax, then the row's four lane groups combine (xor 16, 32).
-        float by = -__builtin_inff(), bx = -__builtin_inff();
-        int iy = 64, ix = 64;
-#pragma unroll
-        for (int t4 = 0; t4 < 2; ++t4) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int f = 16 * t4 + 4 * g + i;
-            const float yy = y[t4][i], xx = xv[4 * t4 + i];
-            const bool gy = f < D && yy > by, gx = f < D && xx > bx;
-            by = gy ? yy : by;
-            iy = gy ? f : iy;
-            bx = gx ? xx : bx;
-            ix = gx ? f : ix;
-          }
-        }
-#pragma unroll
-        for (int off = 16; off <= 32; off <<= 1) {
-          const float oy = __shfl_xor(by, off, 64), ox = __shfl_xor(bx, off, 64);
-          const int jy = __shfl_xor(iy, off, 64), jx = __shfl_xor(ix, off, 64);
-          const bool ty = oy > by || (oy == by && jy < iy), tx = ox > bx || (ox == bx && jx < ix);
-          by = ty ? oy : by;
-          iy = ty ? jy : iy;
-          bx = tx ? ox : bx;
-          ix = tx ? jx : ix;
-        }
-        corr += (g == 0 && row_ok && iy == ix) ? 1.f : 0.f;
+        st4(S.y + r * XS + cw, y[0]);
+        st4(S.y + r * XS + 16 + cw, y[1]);
       }
     }
     mark(0);
@@ -616,6 +592,45 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         S.w[fpos[i]] = wo[i];
         S.w[bpos[i]] = wo[i];
       }
+    } else if (a.want_acc && t - 6 * 64 < B) {
+      // categorical accuracy (waves 6-7, one row per lane): argmax of y and x, ties -> lowest
+      // feature.  The row's 20 first (logical) features come in as five 16-byte reads per
+      // array; logical block jl sits at physical block jl ^ (swz(r) / 4) of its 16-column half.
+      const int r = t - 6 * 64;
+      const int sb = swz(r) >> 2;
+      const float* yr = S.y + r * XS;
+      const float* xq = S.x + r * XS;
+      f32x4 yb[5], xb[5];
+#pragma unroll
+      for (int jl = 0; jl < 5; ++jl) {
+        const int pj = jl < 4 ? (jl ^ sb) : 4 + sb;
+        yb[jl] = ld4(yr + 4 * pj);
+        xb[jl] = ld4(xq + 4 * pj);
+      }
+      float by = yb[0][0], bx = xb[0][0];
+      int iy = 0, ix = 0;
+#pragma unroll
+      for (int f = 1; f < (KD < 20 ? KD : 20); ++f) {   // branch-free selects, increasing f
+        const float yv = yb[f >> 2][f & 3], xw = xb[f >> 2][f & 3];
+        const bool gy = f < D && yv > by, gx = f < D && xw > bx;
+        by = gy ? yv : by;
+        iy = gy ? f : iy;
+        bx = gx ? xw : bx;
+        ix = gx ? f : ix;
+      }
+      if constexpr (KD > 20) {   // wide inputs: the remaining features one by one
+#pragma unroll
+        for (int f = 20; f < KD; ++f) {
+          const int pf = f ^ swz(r);
+          const float yv = yr[pf], xw = xq[pf];
+          const bool gy = f < D && yv > by, gx = f < D && xw > bx;
+          by = gy ? yv : by;
+          iy = gy ? f : iy;
+          bx = gx ? xw : bx;
+          ix = gx ? f : ix;
+        }
+      }
+      corr += iy == ix ? 1.f : 0.f;
     }
     mark(2);
     lds_barrier();

@@ -316,6 +316,17 @@ std::vector<int64_t> ServeRing::latency_run(const float* rows, int n, int64_t ga
   return lat;
 }
 
+std::vector<uint64_t> ServeRing::debug_state(uint64_t seq) const {
+  std::vector<uint64_t> v = {__atomic_load_n(&ctl_->head, __ATOMIC_ACQUIRE), __atomic_load_n(&ctl_->done, __ATOMIC_ACQUIRE),
+                             __atomic_load_n(&ctl_->stop, __ATOMIC_ACQUIRE), __atomic_load_n(&ctl_->alive, __ATOMIC_ACQUIRE),
+                             launches_, hipStreamQuery(stream_) == hipSuccess ? 1u : 0u};
+  const ServeResult& r = res_[seq % (uint64_t)nslots_];
+  for (int i = 0; i < kServeWords; ++i) v.push_back(__atomic_load_n(&r.w[i], __ATOMIC_ACQUIRE));
+  const ServeReq& q = req_[seq % (uint64_t)nslots_];
+  for (int i = 0; i < 32; ++i) v.push_back(__atomic_load_n(&q.w[i], __ATOMIC_ACQUIRE));
+  return v;
+}
+
 void ServeRing::stop() {
   if (!ctl_) return;
   __atomic_store_n(&ctl_->stop, 1u, __ATOMIC_RELEASE);

@@ -49,6 +49,9 @@ class ServeRing {
                                    const uint32_t* keys = nullptr);
   void stop();
   int D() const { return D_; }
+  // debugging: {head, done, stop, alive, launches, stream idle (1) / busy (0)} then the raw
+  // result words and request words of event `seq`'s slot
+  std::vector<uint64_t> debug_state(uint64_t seq) const;
   uint64_t launches() const { return launches_; }
 
  protected:

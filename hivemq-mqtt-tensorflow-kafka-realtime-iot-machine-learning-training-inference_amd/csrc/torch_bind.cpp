@@ -1224,6 +1224,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_fused_supported", &sml::lstm_fused_supported, "whether (U, IN) has a fused LSTM kernel", py::arg("U"),
         py::arg("IN"));
   py::class_<ServePy>(m, "AEServe", "persistent per-event autoencoder scorer over host-mapped rings")
+      .def("debug_state", [](ServePy& p, uint64_t seq) { return p.s->debug_state(seq); }, py::arg("seq"))
       .def(py::init<int, int, py::array_t<float, py::array::c_style | py::array::forcecast>, std::vector<int>,
                     std::vector<int>, py::object, py::object, double, double>(),
            py::arg("device"), py::arg("nslots"), py::arg("weights"), py::arg("dims"), py::arg("acts"),

@@ -78,7 +78,9 @@ class LowLatencyScorer:
         return list(self._loop.positions())
 
     def latency_records(self) -> np.ndarray:
-        """[n, 3] int64: (partition, offset, steady-clock ns the result became visible)."""
+        """[n, 6] int64: (partition, offset, steady-clock ns the result became visible (produce
+        ack), of the fetch response that carried the event, of its score, of its formatted
+        record) -- the same clock as the broker's append times."""
         return self._loop.latency_records()
 
 

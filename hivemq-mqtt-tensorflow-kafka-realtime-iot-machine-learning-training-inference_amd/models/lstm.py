@@ -154,10 +154,17 @@ class LSTMPredictor:
         return loss.detach(), correct.detach()
 
     def _fused_plan(self):
-        """Whether a train step can run as explicit kernel calls (no autograd graph): fused
-        LSTM layers (the last one ``return_sequences=False``) and one Dense head, e.g.
-        :meth:`two_layer`.  Builds, once, the int32 maps that scatter each layer's
-        weight-gradient slab straight into the flat gradient buffer."""
+        """Whether a train step can run as explicit kernel calls (no autograd graph), and how.
+
+        Two stack shapes qualify:
+          * fused LSTM layers (the last one ``return_sequences=False``) and one Dense head --
+            :meth:`two_layer`;
+          * an encoder of fused LSTM layers ending in ``return_sequences=False``, a
+            RepeatVector, a decoder of ``return_sequences=True`` LSTM layers and a
+            TimeDistributed Dense head -- the reference stack (:meth:`reference`,
+            LSTM-TensorFlow-IO-Kafka/cardata-v2.py:172-209).
+        Builds, once, the int32 maps that scatter each layer's weight-gradient slab straight
+        into the flat gradient buffer."""
         if getattr(self, "_plan_built", False):
             return self._plan
         self._plan_built, self._plan = True, None
@@ -166,19 +173,32 @@ class LSTMPredictor:
         from ..ops.dense import supported as dense_ok
         from ..ops.loss import supported as mse_ok
         from ..ops.lstm import fused_supported
-        lstms, head = self.layers[:-1], self.layers[-1]
-        if (not lstms or head["kind"] != "dense" or head["td"] or not mse_ok(head["units"])
-                or not dense_ok(head["in_dim"], head["units"])):
+        body, head = self.layers[:-1], self.layers[-1]
+        if not body or head["kind"] != "dense" or not mse_ok(head["units"]) or not dense_ok(head["in_dim"], head["units"]):
             return None
-        for i, L in enumerate(lstms):
-            if (L["kind"] != "lstm" or L["return_sequences"] != (i < len(lstms) - 1)
-                    or not fused_supported(L["units"], L["in_dim"])):
+        kinds = [L["kind"] for L in body]
+        if kinds.count("repeat") > 1 or any(k not in ("lstm", "repeat") for k in kinds):
+            return None
+        if "repeat" in kinds:
+            r = kinds.index("repeat")
+            pre, post, repeat = body[:r], body[r + 1:], body[r]["n"]
+            if not pre or not post or not head["td"]:
                 return None
+            if any(L["return_sequences"] for L in pre[-1:]) or any(not L["return_sequences"] for L in post):
+                return None
+        else:
+            pre, post, repeat = body, [], None
+            if head["td"]:
+                return None
+        if any(L["return_sequences"] != (i < len(pre) - 1) for i, L in enumerate(pre)):
+            return None
+        if any(not fused_supported(L["units"], L["in_dim"]) for L in pre + post):
+            return None
         from ..ops._ext import load_c
         C = load_c()
         off = self.fp.offsets
         maps = []
-        for L in lstms:
+        for L in pre + post:
             u, IN = L["units"], L["in_dim"]
             G4, ldw = 4 * u, C.lstm_fused_dx_ld(IN)
             S = C.lstm_fused_slab(u, IN)
@@ -202,16 +222,18 @@ class LSTMPredictor:
         head_map = torch.as_tensor(mp.astype(np.int32), device=self.device)
         for m_ in maps + [head_map]:   # the kernels scatter through these unchecked
             assert int(m_.max()) < self.fp.n_pad and int(m_.min()) >= -1
-        self._plan = dict(lstms=lstms, head=head, maps=maps, head_map=head_map,
+        self._plan = dict(pre=pre, post=post, repeat=repeat, head=head, maps=maps, head_map=head_map,
                           acc=torch.zeros(2, device=self.device))
         return self._plan
 
     def _fused_step(self, plan, x, y, global_batch, allreduce):
         """One train step as explicit kernel calls on the flat buffers: per LSTM layer one
         fused forward and one fused backward (weight-gradient slabs reduced straight into
-        the flat gradient through ``plan['maps']``), the Dense head on K1/K2 reading h_T in
-        place, the fused MSE + accuracy kernel, one Adam launch.  Same kernels and
-        rounding points as the autograd path, ~20 fewer small launches per step."""
+        the flat gradient through ``plan['maps']``), RepeatVector as a broadcast copy of
+        h_T (its backward: the sum over the repeated steps), the Dense / TimeDistributed
+        head on K1/K2, the fused MSE + accuracy kernel (target broadcast over the
+        repeated steps), one Adam launch (+ one flat-gradient all-reduce under DP).  Same
+        kernels and rounding points as the autograd path, ~20 fewer small launches per step."""
         from ..ops._ext import load_c
         from ..ops.lstm import ACT
         C = load_c()
@@ -221,34 +243,46 @@ class LSTMPredictor:
             x = x.contiguous()
         if x.dtype not in (torch.float32, torch.bfloat16):
             x = x.float()
+        pre, post, R = plan["pre"], plan["post"], plan["repeat"]
         saved = []
         h = x
-        for L in plan["lstms"]:
+        for L in pre + post:
+            if L is (post[0] if post else None):   # RepeatVector: h_T broadcast over R steps
+                # fp32 (exact widening of the bf16 h_T), as the autograd path feeds it: the
+                # decoder's dx then comes back fp32 and is summed before one bf16 rounding
+                h = h[:, -1].float().unsqueeze(1).expand(n, R, h.shape[-1]).contiguous()
             W, Uw, b = P[L["params"]:L["params"] + 3]
             hs, c = C.lstm_fused_fwd(h, W.detach(), Uw.detach(), b.detach(), None, None, ACT[L["activation"]])
             saved.append((h, hs, c))
             h = hs
-        hT = h[:, -1]                                  # bf16 [n, U] view, read in place
         hd = plan["head"]
         K, bh = (t.detach() for t in P[hd["params"]:hd["params"] + 2])
-        y_pred = C.dense_fwd(hT, K, bh, 0, False, 1024, False)
+        hin = h.reshape(n * R, h.shape[-1]) if R else h[:, -1]   # bf16, read in place when h_T
+        y_pred = C.dense_fwd(hin, K, bh, 0, False, 1024, False)
         yt = y.to(device=self.device, dtype=torch.float32).contiguous()
         acc = plan["acc"]
         acc.zero_()
         dy = torch.empty_like(y_pred)
         scale = n / float(global_batch or n)           # mean over the global batch under DP
-        C.mse_acc(y_pred, yt, 1, 2.0 / y_pred.numel() * scale, dy, acc)
-        C.dense_wgrad(hT, dy, 0, True, 1024, grad, plan["head_map"])
-        dh = C.dense_fwd(dy, K, None, 0, True, 1024, True)   # dh_T = dy . K^T, bf16
-        for i in range(len(plan["lstms"]) - 1, -1, -1):
-            L = plan["lstms"][i]
+        C.mse_acc(y_pred, yt, R or 1, 2.0 / y_pred.numel() * scale, dy, acc)
+        C.dense_wgrad(hin, dy, 0, True, 1024, grad, plan["head_map"])
+        dh = C.dense_fwd(dy, K, None, 0, True, 1024, True)   # dh = dy . K^T, bf16
+        layers = pre + post
+        for i in range(len(layers) - 1, -1, -1):
+            L = layers[i]
             xin, hs, c = saved[i]
             W, Uw, b = (t.detach() for t in P[L["params"]:L["params"] + 3])
+            last_only = i == len(pre) - 1
+            if R and i >= len(pre):
+                dh = dh.view(n, R, -1)
             out = C.lstm_fused_bwd(dh, c, hs, xin, None, None, W, Uw, b, ACT[L["activation"]], i > 0, False,
-                                   i == len(plan["lstms"]) - 1, grad, plan["maps"][i])
+                                   last_only, grad, plan["maps"][i])
             dh = out[0]
+            if R and i == len(pre):   # RepeatVector backward: the repeated steps' gradients summed
+                dh = (dh.view(n, -1) if R == 1 else dh.sum(1)).to(torch.bfloat16)
         self.opt.step(allreduce=allreduce)
-        return acc[0] / y_pred.numel(), acc[1].clone()   # acc is re-zeroed by the next step
+        correct = acc[1] / float(R) if R else acc[1].clone()
+        return acc[0] / y_pred.numel(), correct   # acc is re-zeroed by the next step
 
     # ------------------------------------------------------------------ training
     def fit(self, x, y=None, epochs: int = 1, batch_size: int = 1, verbose: int = 1, take: Optional[int] = None,

@@ -121,18 +121,21 @@ def test_graph_replayed_train_steps_match_eager(cuda_device):
     torch.testing.assert_close(loss_g, loss_e, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("B,T", [(256, 20), (100, 7), (33, 50)])
-def test_fused_step_matches_autograd_step(cuda_device, B, T):
+@pytest.mark.parametrize("stack,B,T", [("two_layer", 256, 20), ("two_layer", 100, 7), ("two_layer", 33, 50),
+                                       ("reference", 64, 1), ("reference", 100, 4)])
+def test_fused_step_matches_autograd_step(cuda_device, stack, B, T):
     """LSTMPredictor._fused_step (explicit kernel calls, weight-gradient slabs scattered
-    straight into the flat gradient, dh_T = dy . K^T from the transposed-weight K1) gives
-    the same gradients, Adam updates and losses as the autograd step over the same
-    kernels, on in-place sliding windows."""
+    straight into the flat gradient, dh_T = dy . K^T from the transposed-weight K1; for the
+    reference stack also RepeatVector as a broadcast copy and TimeDistributed Dense over the
+    repeated steps) gives the same gradients, Adam updates and losses as the autograd step
+    over the same kernels, on in-place sliding windows."""
     from streamml.data.stream import sliding_windows
     rows = torch.tensor(np.random.default_rng(B + T).uniform(-1, 1, (3 * B + T, 18)), dtype=torch.float32,
                         device=cuda_device)
     X, Y = sliding_windows(rows, T)
-    fused = LSTMPredictor.two_layer(look_back=T, device=cuda_device, seed=6)
-    auto = LSTMPredictor.two_layer(look_back=T, device=cuda_device, seed=6)
+    ctor = LSTMPredictor.two_layer if stack == "two_layer" else LSTMPredictor.reference
+    fused = ctor(look_back=T, device=cuda_device, seed=6)
+    auto = ctor(look_back=T, device=cuda_device, seed=6)
     assert fused._fused_plan() is not None
     auto._plan_built, auto._plan = True, None          # force the autograd path
     for s in range(3):

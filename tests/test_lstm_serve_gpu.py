@@ -74,13 +74,15 @@ def test_lstm_serve_matches_oracle(cuda_device, stack, T):
         if len(hist[k]) >= T:
             # the float64 oracle, with room for the window's own fp32 conditioning: a random
             # relu LSTM over 50 steps grows to |h| ~ 1e3 and plain fp32 torch already differs
-            # from float64 by up to 2 % there, so the bound adds 4x the window's largest
-            # fp32-vs-fp64 gap
+            # from float64 by up to 2 % there, so for such a window the bound adds 8x its
+            # largest fp32-vs-fp64 gap and 5e-4 of its largest output (rounding differences
+            # are amplified chaotically; a wrong window, key or state is off by O(|f|))
             w = np.stack(hist[k][-T:])
             f = _forward(m, w)
             gap = np.abs(_forward(m, w, torch.float32) - f)
             err = np.abs(pred[i].astype(np.float64) - f)
-            assert np.all(err <= 2e-4 * np.abs(f) + 2e-5 + 4 * gap.max()), (i, float(err.max()), float(gap.max()))
+            tol = 2e-4 * np.abs(f) + 2e-5 + 8 * gap.max() + (5e-4 * np.abs(f).max() if gap.max() > 1e-3 else 0.0)
+            assert np.all(err <= tol), (i, float(err.max()), float(gap.max()))
             last[k] = pred[i].astype(np.float64)
             checked += 1
         else:

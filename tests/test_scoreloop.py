@@ -114,7 +114,7 @@ def test_long_poll_delivers_paced_events_promptly():
     th.join(30)
     assert not th.is_alive() and out["events"] == 400
     lat = loop.latency_records()
-    assert lat.shape == (400, 3)
+    assert lat.shape == (400, 6)
     d = (lat[np.argsort(lat[:, 1]), 2] - sent) / 1e3
     assert (d > 0).all()
     assert np.percentile(d, 50) < 5000, np.percentile(d, 50)   # us; ~100 us typical

@@ -29,6 +29,8 @@ def main():
         data = synthetic_device_tensor(B * 32768, dev, seed=0)
         ae = FusedAE(spec, init_dense_weights(spec.layer_sizes, seed=0), dev, scale=sc, shift=sh)
         ae.attach_ring(data, B)
+        if os.environ.get("SML_PMC_NOACC") == "1":   # A/B: the accuracy's cost on the step
+            ae.want_acc = False
         for _ in range(3):
             ae.train_minibatches(a.steps)
         import time
