@@ -60,17 +60,24 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200):
         th.join(120)
     b.set_spin_us(0)
     lat = loop.latency_records()
-    vis = lat[np.argsort(lat[:, 1]), 2]
+    lat = lat[np.argsort(lat[:, 1])]
+    vis = lat[:, 2]
     d_ack = (vis[warm:] - sent[warm:]) / 1e3
     t_in = b.append_times("SENSOR_DATA_S_AVRO", 0, 0, n)
     t_res = b.append_times("model-predictions", 0, 0, n)
     d = (t_res[warm:] - t_in[warm:]) / 1e3
+    lw, ti, tr = lat[warm:], t_in[warm:], t_res[warm:]
+    med = lambda a: float(np.median(a)) / 1e3   # noqa: E731
+    legs = {"append_to_fetched": med(lw[:, 3] - ti), "fetched_to_scored": med(lw[:, 4] - lw[:, 3]),
+            "scored_to_formatted": med(lw[:, 5] - lw[:, 4]), "formatted_to_result_append": med(tr - lw[:, 5]),
+            "result_append_to_ack": med(lw[:, 2] - tr)}
     st = out
     ev_n = max(st.get("events", 1), 1)
     return {"p50_us": float(np.percentile(d, 50)), "p99_us": float(np.percentile(d, 99)),
             "max_us": float(d.max()), "events": int(len(d)), "offered_qps": qps, "spin_us": spin_us,
             "latency": "broker append time of the event -> broker append time of its result record",
             "send_to_ack_p50_us": float(np.percentile(d_ack, 50)), "send_to_ack_p99_us": float(np.percentile(d_ack, 99)),
+            "legs_p50_us": legs,
             "results": int(b.end_offset("model-predictions", 0)),
             "batches": st.get("batches"), "events_per_batch": ev_n / max(st.get("batches", 1), 1),
             "per_event_us": {k[:-2]: st[k] / ev_n * 1e6 for k in ("decode_s", "score_s", "format_s",

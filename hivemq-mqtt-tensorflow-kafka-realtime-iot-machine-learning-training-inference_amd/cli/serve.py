@@ -216,9 +216,8 @@ def main(argv: Sequence[str]) -> int:
         # json.dumps({car, partition, offset, score, anomaly[, reconstruction]}) per event, in C++
         recs = load_io().score_records(list(keys), part, np.asarray(offs, np.int64), np.asarray(scores, np.float32),
                                        np.asarray(flags, np.uint8), recon)
-        for i in range(len(chunk)):
-            sink.setitem(next_index[part], recs[i], key=keys[i])
-            next_index[part] += 1
+        sink.extend(next_index[part], recs, keys)   # one bulk append, no per-event Python loop
+        next_index[part] += len(chunk)
         sink.flush()   # produced before the dataset commits this batch's offsets (at-least-once)
         n_flag = int(flags.sum())
         ENGINE.infer_rows.inc(len(chunk), model=model.name)

@@ -27,75 +27,12 @@ __device__ __forceinline__ void st_sys32(uint32_t* p, uint32_t v) {
 }
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Pipelined poll of the next request slot, entirely inside ONE asm statement.
-// Three polls (this lane's tagged word + the host's head counter) are kept in flight,
-// spaced ~1/3 of a PCIe round trip, and each one consumed is re-issued at once, so an
-// event is seen ~RTT/3 after its row lands.  Why one statement: with the loads issued by
-// one asm and waited by another, the compiler is free to copy a load's destination
-// register in between (a loop-carried phi copy) -- reading the register before the data
-// landed.  Here the in-flight loads target fixed clobbered registers v[240:251] that no
-// compiler code touches, and every load has landed (vmcnt 0) when the statement ends.
-// Returns 1: all lanes not in `dontcare` see tag == want (row in `w`, head in `hd`);
-// 2: head > lim (backlog); 0: `rounds` rounds without either (caller checks stop/idle).
-__device__ __forceinline__ uint32_t poll_ready(const uint64_t* wp, const uint64_t* hp, uint32_t want, uint64_t lim,
-                                               uint64_t dontcare, uint32_t rounds, uint64_t& w, uint64_t& hd) {
-  uint32_t st, n;
-#define SML_POLL_ISSUE(W, H) \
-  "global_load_dwordx2 v[" #W "], %[wp], off sc0 sc1\n" \
-  "global_load_dwordx2 v[" #H "], %[hp], off sc0 sc1\n"
-#define SML_POLL_CHECK(W_HI, H, K) \
-  "s_waitcnt vmcnt(4)\n" \
-  "v_cmp_lt_u64 vcc, %[lim], v[" #H "]\n" \
-  "s_cmp_lg_u64 vcc, 0\n" \
-  "s_cbranch_scc1 .Lsml_poll_b" #K "_%=\n" \
-  "v_cmp_eq_u32 vcc, %[want], v" #W_HI "\n" \
-  "s_or_b64 vcc, vcc, %[dc]\n" \
-  "s_cmp_eq_u64 vcc, -1\n" \
-  "s_cbranch_scc1 .Lsml_poll_r" #K "_%=\n"
-#define SML_POLL_OUT(K, W, H, S) \
-  ".Lsml_poll_r" #K "_%=:\n" \
-  "s_mov_b32 %[st], 1\n" \
-  "s_branch .Lsml_poll_m" #K "_%=\n" \
-  ".Lsml_poll_b" #K "_%=:\n" \
-  "s_mov_b32 %[st], 2\n" \
-  ".Lsml_poll_m" #K "_%=:\n" \
-  "v_mov_b64 %[w], v[" #W "]\n" \
-  "v_mov_b64 %[hd], v[" #H "]\n" \
-  "s_branch .Lsml_poll_e_%=\n"
-  asm volatile(
-      "s_mov_b32 %[n], %[rounds]\n"
-      SML_POLL_ISSUE(240:241, 242:243)
-      "s_sleep 8\n"
-      SML_POLL_ISSUE(244:245, 246:247)
-      "s_sleep 8\n"
-      SML_POLL_ISSUE(248:249, 250:251)
-      ".Lsml_poll_l_%=:\n"
-      SML_POLL_CHECK(241, 242:243, 0)
-      SML_POLL_ISSUE(240:241, 242:243)
-      SML_POLL_CHECK(245, 246:247, 1)
-      SML_POLL_ISSUE(244:245, 246:247)
-      SML_POLL_CHECK(249, 250:251, 2)
-      SML_POLL_ISSUE(248:249, 250:251)
-      "s_sub_u32 %[n], %[n], 1\n"
-      "s_cmp_lg_u32 %[n], 0\n"
-      "s_cbranch_scc1 .Lsml_poll_l_%=\n"
-      "s_mov_b32 %[st], 0\n"
-      "v_mov_b64 %[w], 0\n"
-      "v_mov_b64 %[hd], 0\n"
-      "s_branch .Lsml_poll_e_%=\n"
-      SML_POLL_OUT(0, 240:241, 242:243, 0)
-      SML_POLL_OUT(1, 244:245, 246:247, 1)
-      SML_POLL_OUT(2, 248:249, 250:251, 2)
-      ".Lsml_poll_e_%=:\n"
-      "s_waitcnt vmcnt(0)\n"
-      : [st] "=&s"(st), [n] "=&s"(n), [w] "=&v"(w), [hd] "=&v"(hd)
-      : [wp] "v"(wp), [hp] "v"(hp), [want] "v"(want), [lim] "v"(lim), [dc] "s"(dontcare), [rounds] "s"(rounds)
-      : "memory", "vcc", "scc", "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249",
-        "v250", "v251");
-#undef SML_POLL_ISSUE
-#undef SML_POLL_CHECK
-#undef SML_POLL_OUT
-  return st;
+// One poll: this lane's tagged word of the next request slot and the host's head
+// counter, as cache-bypassing loads issued without a wait (the caller waits with a
+// counted s_waitcnt tied to the outputs, so several polls can be in flight).
+__device__ __forceinline__ void poll_issue(uint64_t& w, uint64_t& hd, const uint64_t* wp, const uint64_t* hp) {
+  asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1" : "=v"(w) : "v"(wp) : "memory");
+  asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1" : "=v"(hd) : "v"(hp) : "memory");
 }
 
 // One request slot's first 32 tagged words (16 x 16-byte cache-bypassing loads from one

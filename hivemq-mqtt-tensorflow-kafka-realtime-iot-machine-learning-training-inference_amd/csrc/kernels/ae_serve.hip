@@ -100,22 +100,47 @@ __global__ __launch_bounds__(64) void ae_serve_kernel(ServeCtl* ctl, const Serve
   if (lane == 0) st_sys32(&ctl->alive, 1u);
   bool quit = false;
   while (!quit) {
-    // Pipelined polling (sml_serve_dev.h poll_ready): three polls of the next slot in
-    // flight, ~1/3 of a PCIe round trip apart, so an event is seen ~RTT/3 after its row
-    // lands instead of up to a whole round trip later.
+    // Pipelined polling: three polls of the next slot (word `lane` + the head counter)
+    // in flight, spaced about a third of a PCIe round trip apart, so an event is seen
+    // ~RTT/3 after its row lands instead of up to a whole round trip later.  Each
+    // consumed poll is re-issued at once, which keeps the spacing.  The polls are issued
+    // and waited for by separate asm statements, so the compiler may copy a poll register
+    // before its data lands (a loop phi copy; lstm_serve.hip was bitten by it): that is
+    // harmless here because the tag and the payload are the SAME 8-byte word -- a stale
+    // copy can only fail the tag test (the wave polls again), never pair a new tag with
+    // old data -- and the row used afterwards is exactly the word that passed the test.
     const int slot0 = (int)(tail % (uint64_t)nslots);
     SML_DCHECK(slot0 >= 0 && slot0 < nslots);
     const uint32_t want = (uint32_t)(tail + 1);
     const uint64_t* wp = &req[slot0].w[lane & (MAXD - 1)];
-    const uint64_t dontcare = D >= 64 ? 0ull : ~((1ull << D) - 1ull);   // lanes >= D
+    const uint64_t* hp = &ctl->head;
+    uint64_t w0, h0, w1, h1, w2, h2;
+    poll_issue(w0, h0, wp, hp);
+    __builtin_amdgcn_s_sleep(8);
+    poll_issue(w1, h1, wp, hp);
+    __builtin_amdgcn_s_sleep(8);
+    poll_issue(w2, h2, wp, hp);
     uint64_t wv = 0, head = 0;
-    uint32_t st;
-    for (;;) {
-      st = poll_ready(wp, &ctl->head, want, tail + 4, dontcare, 64, wv, head);
-      if (st != 0) break;
-      // exit conditions every wave reaches
-      if (ld_sys32(&ctl->stop) || __builtin_amdgcn_s_memrealtime() - last > idle_ticks) { quit = true; break; }
+    auto ready = [&](uint64_t w, uint64_t hd) {
+      const bool ok = lane >= D || (uint32_t)(w >> 32) == want;
+      return __ballot(ok) == ~0ull || hd > tail + 4;
+    };
+    for (uint32_t it = 0;; ++it) {
+      asm volatile("s_waitcnt vmcnt(4)" : "+v"(w0), "+v"(h0)::"memory");
+      if (ready(w0, h0)) { wv = w0; head = h0; break; }
+      poll_issue(w0, h0, wp, hp);
+      asm volatile("s_waitcnt vmcnt(4)" : "+v"(w1), "+v"(h1)::"memory");
+      if (ready(w1, h1)) { wv = w1; head = h1; break; }
+      poll_issue(w1, h1, wp, hp);
+      asm volatile("s_waitcnt vmcnt(4)" : "+v"(w2), "+v"(h2)::"memory");
+      if (ready(w2, h2)) { wv = w2; head = h2; break; }
+      poll_issue(w2, h2, wp, hp);
+      if ((it & 63) == 63) {   // exit conditions every wave reaches
+        if (ld_sys32(&ctl->stop) || __builtin_amdgcn_s_memrealtime() - last > idle_ticks) { quit = true; break; }
+      }
     }
+    // the polls still in flight must land before their registers are reused
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(w0), "+v"(h0), "+v"(w1), "+v"(h1), "+v"(w2), "+v"(h2)::"memory");
     if (quit) break;
     const bool ok = lane >= D || (uint32_t)(wv >> 32) == want;
     if (__ballot(ok) == ~0ull && head <= tail + 4) {

@@ -7,10 +7,6 @@
 #include <string>
 #include <thread>
 #include <algorithm>
-#include <cstdlib>
-#if defined(__x86_64__)
-#include <immintrin.h>
-#endif
 
 namespace sml {
 namespace {
@@ -46,8 +42,6 @@ ServeRing::ServeRing(int device, int nslots, int D, double idle_seconds)
   ck(hipHostGetDevicePointer((void**)&req_d_, req_, 0), "device ptr req");
   ck(hipHostGetDevicePointer((void**)&res_d_, res_, 0), "device ptr res");
   ck(create_persistent_stream(&stream_), "stream");
-  const char* st = std::getenv("SML_SERVE_STORES");
-  nt_ = st && std::strcmp(st, "nt") == 0;
 }
 
 ServeRing::~ServeRing() {
@@ -186,28 +180,14 @@ uint64_t ServeRing::submit(const float* rows, int k, const uint32_t* keys) {
     ServeReq& dst = req_[ev % (uint64_t)nslots_];
     const uint64_t tag = (uint64_t)(uint32_t)(ev + 1) << 32;
     const float* row = rows + (size_t)i * D_;
-    for (int j = 0; j < D_; ++j) {   // aligned 8-byte stores: a word is never seen half-written
+    for (int j = 0; j < D_; ++j) {   // 8-byte atomic stores: a word is never seen half-written
       uint32_t bits;
       std::memcpy(&bits, &row[j], 4);
-#if defined(__x86_64__)
-      if (nt_) {
-        _mm_stream_si64(reinterpret_cast<long long*>(&dst.w[j]), (long long)(tag | bits));
-        continue;
-      }
-#endif
       __atomic_store_n(&dst.w[j], tag | bits, __ATOMIC_RELAXED);
     }
     if (keys) __atomic_store_n(&dst.w[31], tag | keys[i], __ATOMIC_RELAXED);
   }
   head_ += k;
-#if defined(__x86_64__)
-  if (nt_) {   // rows out of the write-combining buffers before head (the backlog path trusts rows below it)
-    _mm_sfence();
-    _mm_stream_si64(reinterpret_cast<long long*>(&ctl_->head), (long long)head_);
-    _mm_sfence();
-    return first;
-  }
-#endif
   store_rel(&ctl_->head, head_);   // after the rows: the backlog path trusts rows below head
   return first;
 }
@@ -321,7 +301,7 @@ std::vector<uint64_t> ServeRing::debug_state(uint64_t seq) const {
                              __atomic_load_n(&ctl_->stop, __ATOMIC_ACQUIRE), __atomic_load_n(&ctl_->alive, __ATOMIC_ACQUIRE),
                              launches_, hipStreamQuery(stream_) == hipSuccess ? 1u : 0u};
   const ServeResult& r = res_[seq % (uint64_t)nslots_];
-  for (int i = 0; i < kServeWords; ++i) v.push_back(__atomic_load_n(&r.w[i], __ATOMIC_ACQUIRE));
+  for (size_t i = 0; i < sizeof(ServeResult) / 8; ++i) v.push_back(__atomic_load_n(&r.w[i], __ATOMIC_ACQUIRE));
   const ServeReq& q = req_[seq % (uint64_t)nslots_];
   for (int i = 0; i < 32; ++i) v.push_back(__atomic_load_n(&q.w[i], __ATOMIC_ACQUIRE));
   return v;

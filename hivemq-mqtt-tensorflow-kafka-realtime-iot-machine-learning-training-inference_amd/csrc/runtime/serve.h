@@ -68,10 +68,6 @@ class ServeRing {
   ServeReq* req_d_ = nullptr;
   ServeResult* res_d_ = nullptr;
   hipStream_t stream_ = nullptr;
-  // SML_SERVE_STORES=nt: request words and the head counter go out as non-temporal
-  // stores + one store fence, so the GPU's PCIe read finds them in memory instead of
-  // probing a modified line out of a core's cache (A/B in bench/bench_infer.py)
-  bool nt_ = false;
   uint64_t head_ = 0;
   uint64_t launches_ = 0;
   uint64_t complete_ = 0;   // events known complete (prefix)

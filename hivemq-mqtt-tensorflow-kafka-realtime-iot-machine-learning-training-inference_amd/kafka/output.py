@@ -43,6 +43,32 @@ class KafkaOutputSequence:
         if len(self._ready) >= self.batch_records:
             self._send()
 
+    def extend(self, index: int, messages: Sequence[Union[str, bytes]],
+               keys: Optional[Sequence[Optional[Union[str, bytes]]]] = None) -> None:
+        """``setitem(index + i, messages[i], keys[i])`` for a contiguous run, in bulk: when the
+        run starts at the next index to produce (the serving loop's case) the records go
+        straight to the produce batch (list operations, no per-record Python bookkeeping)."""
+        n = len(messages)
+        if keys is not None and len(keys) != n:
+            raise ValueError("keys and messages differ in length")
+        if n == 0:
+            return
+        if index != self._next or self._pending:
+            for i in range(n):
+                self.setitem(index + i, messages[i], None if keys is None else keys[i])
+            return
+        self._ready.extend(m.encode() if isinstance(m, str) else m for m in messages)
+        if keys is None:
+            self._ready_keys.extend([None] * n)
+        else:
+            self._ready_keys.extend(k.encode() if isinstance(k, str) else k for k in keys)
+        self._next += n
+        while len(self._ready) >= self.batch_records:   # produce requests of batch_records, as setitem
+            rest, rest_keys = self._ready[self.batch_records:], self._ready_keys[self.batch_records:]
+            del self._ready[self.batch_records:], self._ready_keys[self.batch_records:]
+            self._send()
+            self._ready, self._ready_keys = rest, rest_keys
+
     def _send(self) -> None:
         if not self._ready:
             return
