@@ -298,8 +298,11 @@ class LSTMPredictor:
         from ..parallel.dp import allreduce_sum_
         import torch.distributed as dist
 
-        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
-        allreduce = allreduce_sum_ if world > 1 else None
+        pg = dist.is_available() and dist.is_initialized()
+        world = dist.get_world_size() if pg else 1
+        # any process group (also a 1-rank one, SML_FORCE_PG=1) takes the data-parallel path:
+        # fused no-autograd steps + one flat-gradient RCCL all-reduce per step
+        allreduce = allreduce_sum_ if pg else None
         hist = History()
         cbs = [hist] + list(callbacks or [])
         for cb in cbs:
@@ -351,9 +354,9 @@ class LSTMPredictor:
             nb = min(nb, take)
         from ..ops import lstm_persistent as lp
         persistent = engine == "persistent" or (
-            engine == "auto" and world == 1 and lp.supported(self) and batch_size <= lp.MAX_BATCH and n > 0)
+            engine == "auto" and not pg and lp.supported(self) and batch_size <= lp.MAX_BATCH and n > 0)
         if persistent:
-            if not (lp.supported(self) and world == 1 and batch_size <= lp.MAX_BATCH):
+            if not (lp.supported(self) and not pg and batch_size <= lp.MAX_BATCH):
                 raise ValueError("engine='persistent' needs the reference stack at look_back 1, batch <= "
                                  f"{lp.MAX_BATCH}, one replica")
             if not lp.check_inactive(self):
@@ -362,7 +365,8 @@ class LSTMPredictor:
             self.last_fit_engine = "persistent"
             return self._fit_persistent(xd, yd, n, nb, epochs, batch_size, verbose, cbs, hist, shuffle, seed,
                                         initial_epoch)
-        self.last_fit_engine = "autograd"
+        plan = self._fused_plan()
+        self.last_fit_engine = ("fused" if plan is not None else "autograd") + ("+allreduce" if pg else "")
         from ..parallel.fault import maybe_inject
         rank = dist.get_rank() if world > 1 else 0
         gstep = 0

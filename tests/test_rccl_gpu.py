@@ -4,8 +4,9 @@ Every multi-rank test on the one-GPU box shares GPU 0 over gloo (RCCL refuses tw
 on one device), so this is the test that opens an RCCL communicator: ``SML_FORCE_PG=1``
 makes ``dp.init_from_env`` create the group at world 1, and the script exercises
 ``init_process_group(device_id=...)``, ``all_reduce``, ``barrier(device_ids=...)``,
-``all_gather_object``, ``P2PGroup.try_create`` and one ``step_ring`` whose gradient bucket
-goes through the RCCL all-reduce -- compared bit-for-bit with the same step without it.
+``all_gather_object``, ``P2PGroup.try_create``, one ``step_ring`` whose gradient bucket
+goes through the RCCL all-reduce -- compared bit-for-bit with the same step without it --
+and a reference-stack LSTM epoch on the fused DP step (flat-gradient all-reduce per step).
 Runs in a child process so the group never outlives the test.
 """
 import json
@@ -59,6 +60,19 @@ if g is not None:
     a.attach_ring(data, 32)
     a.train_minibatches(100, dp=g)
     res["p2p_steps_ok"] = bool(torch.isfinite(a.params).all())
+# the reference LSTM stack under the group: fused no-autograd steps + the RCCL all-reduce
+from streamml.models.lstm import LSTMPredictor
+from streamml.data.stream import sliding_windows
+rows = torch.tensor(np.random.default_rng(1).uniform(-1, 1, (257, 18)), dtype=torch.float32, device=dev)
+X, Y = sliding_windows(rows, 1)
+la = LSTMPredictor.reference(look_back=1, device=dev, seed=2)
+lb = LSTMPredictor.reference(look_back=1, device=dev, seed=2)
+la.fit(X, Y, epochs=1, batch_size=64, verbose=0)
+res["lstm_engine"] = la.last_fit_engine
+for s in range(0, 256, 64):
+    lb.train_step(X[s:s + 64], Y[s:s + 64])
+torch.cuda.synchronize()
+res["lstm_equal"] = bool(torch.equal(la.fp.flat, lb.fp.flat))
 dp.shutdown()
 print("RESULT " + json.dumps(res))
 '''
@@ -78,3 +92,4 @@ def test_dp_path_on_one_rccl_rank(cuda_device):
     assert res["p2p"], res
     assert res["p2p_steps_ok"], res
     assert res["step_equal"] and res["step_changed"], res
+    assert res["lstm_engine"] == "fused+allreduce" and res["lstm_equal"], res
