@@ -10,6 +10,7 @@ With torchrun, every rank serves its own car-key shard (shard-by-key) and rank
 0 reports the aggregate.  The reference publishes no latency number.
 """
 import argparse
+import itertools
 import json
 import os
 import sys
@@ -19,7 +20,32 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200):
+_E2E_RUNS = itertools.count()
+
+
+def _serving_cpus(k: int):
+    """``k`` CPUs of this process's affinity set for the spinning serving threads, one per
+    physical core where the topology says which CPUs are SMT siblings (None: too few)."""
+    cpus = sorted(os.sched_getaffinity(0))
+    if len(cpus) < k + 2:   # leave room for the broker's connection threads
+        return None
+    picked, seen = [], set()
+    for c in reversed(cpus):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                core = f.read().strip()
+        except OSError:
+            core = str(c)
+        if core in seen:
+            continue
+        seen.add(core)
+        picked.append(c)
+        if len(picked) == k:
+            return picked
+    return None
+
+
+def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=False):
     """Kafka append -> result append latency through the real serving path: a paced C++
     producer appends Confluent-Avro car events (one produce request each, keyed by car) to
     an in-process broker at ``qps``; the ``serve --low-latency`` loop (long-poll fetch, C++
@@ -29,7 +55,9 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200):
     event's result record minus that of the event itself -- Kafka-append -> result
     visible to consumers.  Also reported: producer-send -> result-produce-ack (both client
     legs included).  ``spin_us``: the low-latency socket policy (broker connection threads,
-    long polls and the loop's client busy-poll this long before blocking)."""
+    long polls and the loop's client busy-poll this long before blocking).  ``pin``: the
+    scoring loop and the producer run on two CPUs of their own (distinct physical cores); off
+    by default -- on the MI355X boxes it changed nothing measurable (profiles/r03)."""
     import threading
 
     import numpy as np
@@ -40,7 +68,7 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200):
     from streamml.ops.serve import ScoringServer
 
     n = events + warm
-    name = f"bench-e2e-{os.getpid()}-{rank}-{spin_us}"
+    name = f"bench-e2e-{os.getpid()}-{rank}-{spin_us}-{next(_E2E_RUNS)}"   # a fresh broker per call
     b = fake_broker(name)
     b.create_topic("SENSOR_DATA_S_AVRO", 1)
     b.create_topic("model-predictions", 1)
@@ -53,10 +81,23 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200):
     with ScoringServer(m, threshold=threshold, slots=4096) as srv:
         loop = LowLatencyScorer(f"fake://{name}", "SENSOR_DATA_S_AVRO", "model-predictions", [0], srv, starts=[0],
                                 max_wait_ms=100, record_latency=True, spin_us=spin_us)
-        th = threading.Thread(target=lambda: out.update(loop.run(max_events=n, idle_timeout_s=10.0)))
+        cpus = _serving_cpus(2) if pin else None
+
+        def serve():
+            if cpus:
+                os.sched_setaffinity(0, {cpus[0]})   # this thread only (Linux: pid 0 = calling thread)
+            out.update(loop.run(max_events=n, idle_timeout_s=10.0))
+
+        th = threading.Thread(target=serve)
         th.start()
-        sent = paced_produce(f"fake://{name}", "SENSOR_DATA_S_AVRO", 0, bytes(buf), offs, keys=keys, qps=qps,
-                             spin_us=spin_us)
+        main_mask = os.sched_getaffinity(0)
+        if cpus:
+            os.sched_setaffinity(0, {cpus[1]})
+        try:
+            sent = paced_produce(f"fake://{name}", "SENSOR_DATA_S_AVRO", 0, bytes(buf), offs, keys=keys, qps=qps,
+                                 spin_us=spin_us)
+        finally:
+            os.sched_setaffinity(0, main_mask)
         th.join(120)
     b.set_spin_us(0)
     lat = loop.latency_records()
@@ -77,7 +118,7 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200):
             "max_us": float(d.max()), "events": int(len(d)), "offered_qps": qps, "spin_us": spin_us,
             "latency": "broker append time of the event -> broker append time of its result record",
             "send_to_ack_p50_us": float(np.percentile(d_ack, 50)), "send_to_ack_p99_us": float(np.percentile(d_ack, 99)),
-            "legs_p50_us": legs,
+            "legs_p50_us": legs, "pinned_cpus": cpus,
             "results": int(b.end_offset("model-predictions", 0)),
             "batches": st.get("batches"), "events_per_batch": ev_n / max(st.get("batches", 1), 1),
             "per_event_us": {k[:-2]: st[k] / ev_n * 1e6 for k in ("decode_s", "score_s", "format_s",
