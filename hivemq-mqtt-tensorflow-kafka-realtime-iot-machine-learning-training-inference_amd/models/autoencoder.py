@@ -261,7 +261,7 @@ class Autoencoder:
                 gstep += steps
             elif throughput:
                 steps = self._fit_array_throughput(xd, batch_size, steps_per_epoch, shuffle, seed, rank, epoch, world,
-                                                   allreduce, gstep)
+                                                   allreduce, gstep, epochs_left=epochs - epoch)
                 gstep += steps
             elif is_stream:
                 for xb in self._stream_batches(x, batch_size):
@@ -339,11 +339,20 @@ class Autoencoder:
             return True
         return engine == "auto" and batch_size > self.backend.max_minibatch()
 
+    # rows trained once: the direct fused step (normalize_fn + argmax inside the unpacked
+    # kernel) takes 0.97 ms per 33.5 M rows against 1.03 (K8 pack) + 0.69 (packed-pair
+    # kernel) -- the pack pays off from the 3rd pass over the same rows (profiles/r03)
+    PACK_MIN_PASSES = 3
+
     def _fit_array_throughput(self, xd: torch.Tensor, B: int, steps_per_epoch: Optional[int], shuffle: bool,
-                              seed: int, rank: int, epoch: int, world: int, allreduce, gstep: int) -> int:
+                              seed: int, rank: int, epoch: int, world: int, allreduce, gstep: int,
+                              epochs_left: int = 1) -> int:
         """One epoch of the throughput engine over a device array: every full batch on the
-        headline kernel from the epoch's tile-packed ring; the last short batch (Keras) on
-        the plain fused step.  Unshuffled epochs reuse the packed ring of the previous one."""
+        headline kernel from the epoch's tile-packed ring (shuffled epochs: the permutation
+        is evaluated inside the pack kernel; unshuffled epochs reuse the packed ring of the
+        previous one), or -- unshuffled, fewer than PACK_MIN_PASSES epochs left and no packed
+        ring yet -- on the direct fused step over the rows in place; the last short batch
+        (Keras) on the plain fused step."""
         from ..parallel.fault import maybe_inject_range
         be = self.backend
         n = xd.size(0)
@@ -358,17 +367,22 @@ class Autoencoder:
         steps = 0
         if nfull:
             key = (xd.data_ptr(), n, B, nfull)
-            if pkey is not None or getattr(self, "_tp_key", None) != key or be.ring_xpack is None:
+            packed = pkey is None and getattr(self, "_tp_key", None) == key and be.ring_xpack is not None
+            if pkey is None and not packed and epochs_left < self.PACK_MIN_PASSES:
+                for i in range(nfull):   # rows in place, normalised inside the kernel
+                    be.step(xd[i * B:(i + 1) * B], global_batch=B * world, allreduce=allreduce)
+            else:
                 if pkey is not None:   # the epoch's shuffle evaluated inside the pack kernel
                     be.pack_ring(xd, B, perm_key=pkey) if nfull * B == (n // B) * B else \
                         be.pack_ring(xd, B, index=be.perm_indices(n, pkey, 0, nfull * B))
-                else:
+                    self._tp_key = None
+                elif not packed:
                     be.pack_ring(xd[:nfull * B], B)
-                self._tp_key = None if pkey is not None else key
-            else:
-                be.cursor.zero_()
-            for _ in range(nfull):
-                be.step_ring(global_batch=B * world, allreduce=allreduce)
+                    self._tp_key = key
+                else:
+                    be.cursor.zero_()
+                for _ in range(nfull):
+                    be.step_ring(global_batch=B * world, allreduce=allreduce)
             steps = nfull
         rem = n - nfull * B
         if rem and world == 1 and (steps_per_epoch is None or steps < steps_per_epoch) and n // B == nfull:
@@ -386,19 +400,58 @@ class Autoencoder:
         return int.from_bytes(h, "little")
 
     def _fit_stream_throughput(self, stream, B: int, max_steps: Optional[int], world: int, allreduce,
-                               gstep: int, rank: int, pack_batches: int = 8) -> int:
-        """A streaming epoch on the throughput engine: device chunks fill a staging buffer of
-        ``pack_batches`` batches; each round packs the buffer's full batches (K8) and trains
-        them on the headline kernel, carrying the < B leftover rows to the next round, so the
-        batches are exactly ``batch(B)`` over the stream; the final partial batch runs the
-        plain fused step.  Under DP the ranks agree per round on the batch count, and the
-        epoch ends for everyone when any rank's stream is exhausted."""
+                               gstep: int, rank: int, round_batches: int = 8) -> int:
+        """A streaming epoch on the throughput engine.  Streamed rows are trained once, so
+        every batch runs the direct fused step (normalize_fn + argmax inside the unpacked
+        kernel: faster than K8 pack + packed kernel for single-pass rows, PACK_MIN_PASSES).
+        One replica: a batch that lies inside one device chunk is trained in place; only a
+        batch straddling chunks is assembled in a B-row carry buffer.  Under DP the ranks
+        agree, per round of ``round_batches`` staged batches, on how many to train, and the
+        epoch ends for everyone when any rank's stream is exhausted.  Batches are exactly
+        ``batch(B)`` over the stream; the final partial batch is Keras' short batch."""
         from ..parallel.dp import agree
         be = self.backend
         D = self.spec.input_dim
-        cap = B * max(1, int(pack_batches))
+        steps = 0
+
+        def left():
+            return None if max_steps is None else max_steps - steps
+
+        if world == 1:
+            carry = torch.empty((B, D), dtype=torch.float32, device=self.device)
+            have = 0
+            for xd in self._stream_device_chunks(stream):
+                if max_steps is not None and steps >= max_steps:
+                    break
+                k, pos = xd.size(0), 0
+                if have:   # complete the batch straddling the previous chunk
+                    t = min(B - have, k)
+                    carry[have:have + t].copy_(xd[:t])
+                    have += t
+                    pos = t
+                    if have < B:
+                        continue
+                    be.step(carry, global_batch=B)
+                    steps += 1
+                    have = 0
+                nfull = (k - pos) // B
+                if left() is not None:
+                    nfull = min(nfull, left())
+                for i in range(nfull):
+                    be.step(xd[pos + i * B:pos + (i + 1) * B], global_batch=B)
+                steps += nfull
+                pos += nfull * B
+                if k > pos and (max_steps is None or steps < max_steps):
+                    carry[:k - pos].copy_(xd[pos:])
+                    have = k - pos
+            if have and (max_steps is None or steps < max_steps):
+                be.step(carry[:have].contiguous())   # Keras' short final batch
+                steps += 1
+            return steps
+
+        cap = B * max(1, int(round_batches))
         stage = torch.empty((cap, D), dtype=torch.float32, device=self.device)
-        have, steps = 0, 0
+        have = 0
         it = iter(self._stream_device_chunks(stream))
         pend, ppos, exhausted = None, 0, False
         while True:
@@ -416,26 +469,19 @@ class Autoencoder:
                 have += t
                 ppos += t
             drained = exhausted and (pend is None or ppos >= pend.size(0))
-            nb = have // B
-            if world > 1:
-                nb, any_done = agree([nb, int(drained)], self.device, ["min", "max"])
-                drained = bool(any_done)
+            nb, any_done = agree([have // B, int(drained)], self.device, ["min", "max"])
+            drained = bool(any_done)
             if max_steps is not None:
                 nb = min(nb, max_steps - steps)
-            if nb > 0:
-                be.pack_ring(stage[:nb * B], B)
-                for _ in range(nb):
-                    be.step_ring(global_batch=B * world, allreduce=allreduce)
-                steps += nb
-            rest = have - nb * B
-            if rest and nb:
+            for i in range(nb):
+                be.step(stage[i * B:(i + 1) * B], global_batch=B * world, allreduce=allreduce)
+            steps += max(nb, 0)
+            rest = have - max(nb, 0) * B
+            if rest and nb > 0:
                 stage[:rest].copy_(stage[nb * B:have].clone())
             have = rest
             if drained or (max_steps is not None and steps >= max_steps):
                 break
-        if have and world == 1 and (max_steps is None or steps < max_steps):
-            be.step(stage[:have].contiguous())   # Keras' short final batch
-            steps += 1
         return steps
 
     def _use_persistent(self, engine: str, batch_size: int, world: int, dp: str = "auto") -> bool:

@@ -1,8 +1,10 @@
 """``Autoencoder.fit(engine="throughput")``: the large-batch mode on the headline kernel.
 
-Each epoch's rows are tile-packed once (K8, the epoch's shuffle fused into the pack) and
-every full batch runs the packed-pair bf16 MFMA train kernel + slab-reduce/Adam
-(``FusedAE.step_ring``); Keras' short last batch runs the plain fused step.  The oracle is
+A shuffled epoch's rows are tile-packed (K8, the shuffle fused into the pack) and every
+full batch runs the packed-pair bf16 MFMA train kernel + slab-reduce/Adam
+(``FusedAE.step_ring``); unshuffled rows are packed once when they will be replayed
+(>= Autoencoder.PACK_MIN_PASSES epochs) and otherwise trained in place by the direct fused
+step; Keras' short last batch runs the plain fused step.  The oracle is
 ``tests/helpers/bf16_ref.py`` -- gradients with the kernels' bf16 rounding points, Keras
 Adam (eps 1e-7) in float64 -- so the whole epoch's parameter trajectory is checked at
 1e-3 relative (reference job: AUTOENCODER-TensorFlow-IO-Kafka/cardata-v3.py:212-222)."""
