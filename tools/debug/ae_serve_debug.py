@@ -15,7 +15,7 @@ def dump(srv, seq, tag):
     print(tag, "head/done/stop/alive/launches/idle:", v[:6], flush=True)
     res = v[6:6 + 40]
     req = v[6 + 40:]
-    print("  trace words 34..39 (poll word, head, ballot, exec before, exec after, dontcare):",
+    print("  result words 34..39 (timing fields, padding):",
           [hex(w) for w in res[34:40]], flush=True)
     print("  res tags:", [w >> 32 for w in res], flush=True)
     print("  req tags:", [w >> 32 for w in req], flush=True)
