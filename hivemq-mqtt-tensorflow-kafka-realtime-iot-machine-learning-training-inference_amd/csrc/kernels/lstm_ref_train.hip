@@ -8,7 +8,12 @@
 // each per step.  Here ONE workgroup runs N consecutive Keras steps in one launch
 // (the ae_minibatch.hip pattern): the live parameters sit in LDS for the whole launch,
 // every thread owns a fixed set of (parameter, Adam m, Adam v) in registers and is the
-// only writer of those parameters, and each step is 10 barrier-separated phases:
+// only writer of those parameters.
+//
+// Two kernels share that ownership scheme.  At batch 1 (the reference's setting,
+// `lstm_ref_train_b1_kernel`, further down) the chain of nine layers runs on ONE wave with
+// no workgroup barrier inside it, and a step has two barriers.  For batches 2..32
+// (`lstm_ref_train_kernel`) each step is 10 barrier-separated phases:
 //     F1-F4   LSTM layer forward  (task = (row, unit): three gate dot products, gate
 //             math, c, h; i, g~, o, c saved for backward)
 //     D0      head + loss          (wave per row: Dense(18), MSE gradient, loss and
@@ -351,6 +356,230 @@ __global__ __launch_bounds__(NT) void lstm_ref_train_kernel(RefArgs a) {
   if (threadIdx.x == 0) *a.iter = it0 + s;
 }
 
+// ===================================================================================
+// Batch-1 path (the reference's setting).  At B = 1 no phase of the chain has more than
+// 32 (unit) tasks, so the whole forward + backward chain runs on wave 0 alone with
+// lane-split dot products (lane = j + U * part, the P = 64 / U parts each take every
+// P-th input and meet through permlane swaps) and NO workgroup barrier between its nine
+// layers: a wave's LDS operations complete in order, so a value one lane writes is seen
+// by every lane of the same wave that reads it afterwards.  The gates each lane saves
+// in the forward pass stay in its registers for the backward pass (same j mapping).
+// Per step there are two barriers: chain -> Adam on all 8 waves -> next step.
+// Off the critical path, while wave 0 runs the chain:
+//   * wave 1 computes the Adam step size lr_t and the loss / argmax accuracy of the
+//     PREVIOUS step (from its saved prediction row);
+//   * the sample rows arrive 32 steps ahead: every 32nd step the workgroup writes the
+//     block it prefetched into registers 32 steps earlier to LDS and issues the loads of
+//     the block after it, so no step waits on a global load.
+// ===================================================================================
+constexpr int NB = MAXB;          // steps per prefetched row block (reuses the two row buffers)
+
+__device__ __forceinline__ void wave_order() { asm volatile("" ::: "memory"); }
+
+// sum of a lane value over the P = 64 / U lane groups of lane = j + U * part
+template <int U>
+__device__ __forceinline__ float part_sum(float v, int lane) {
+  static_assert(U == 16 || U == 32, "chain layouts");
+  if (U == 16) v += xor16(v, lane);
+  return v + xor32(v, lane);
+}
+
+// forward of one LSTM layer for one row on one wave: h[j] = o * act(i * g~)
+template <int K, int U>
+__device__ __forceinline__ void chain_fwd(const float* __restrict__ W, const float* __restrict__ bias, int S,
+                                          const float* in, float* h, int act, int lane, float& ig, float& gt,
+                                          float& og, float& ac) {
+  constexpr int P = 64 / U;
+  const int j = lane % U, part = lane / U;
+  float zi = 0.0f, zg = 0.0f, zo = 0.0f;
+#pragma unroll
+  for (int k0 = 0; k0 < K; k0 += P) {
+    const int k = k0 + part;
+    if (K % P == 0 || k < K) {
+      const float xv = in[k];
+      const float* w = W + k * S + j;
+      zi = fmaf(xv, w[0], zi);
+      zg = fmaf(xv, w[U], zg);
+      zo = fmaf(xv, w[2 * U], zo);
+    }
+  }
+  zi = part_sum<U>(zi, lane) + bias[j];
+  zg = part_sum<U>(zg, lane) + bias[U + j];
+  zo = part_sum<U>(zo, lane) + bias[2 * U + j];
+  ig = sigm(zi);
+  gt = actf(act, zg);
+  og = sigm(zo);
+  ac = actf(act, ig * gt);
+  if (part == 0) h[j] = og * ac;
+  wave_order();
+}
+
+// backward of one LSTM layer for one row: dh[j] = up . Wup[j], then dz (i | g | o)
+template <int U, int KN>
+__device__ __forceinline__ void chain_bwd(const float* up, const float* __restrict__ Wup, int WS, float ig, float gt,
+                                          float og, float ac, float* dz, int act, int lane) {
+  constexpr int P = 64 / U;
+  const int j = lane % U, part = lane / U;
+  const float* wr = Wup + j * WS;
+  float d0 = 0.0f, d1 = 0.0f;
+#pragma unroll
+  for (int n0 = 0; n0 < KN; n0 += 2 * P) {
+    const int n = n0 + part;
+    if (KN % P == 0 || n < KN) d0 = fmaf(up[n], wr[n], d0);
+    if (n + P < KN) d1 = fmaf(up[n + P], wr[n + P], d1);
+  }
+  const float dh = part_sum<U>(d0 + d1, lane);
+  const float dc = dh * og * actd(act, ac);
+  if (part == 0) dz[j] = dc * gt * ig * (1.0f - ig);
+  if (part == (P > 2 ? 1 : 0)) dz[U + j] = dc * ig * actd(act, gt);
+  if (part == (P > 2 ? 2 : 1)) dz[2 * U + j] = dh * ac * og * (1.0f - og);
+  wave_order();
+}
+
+// the whole chain of one Keras step at B = 1 (wave 0)
+template <typename G>
+__device__ __forceinline__ void chain_step(float* L, const float* xb, const float* yb, float* yp_out, int act,
+                                           int lane) {
+  float i1, g1, o1, a1, i2, g2, o2, a2, i3, g3, o3, a3, i4, g4, o4, a4;
+  chain_fwd<G::F, G::U1>(L + G::lW1, L + G::lb1, G::S1, xb, L + G::oH1, act, lane, i1, g1, o1, a1);
+  chain_fwd<G::U1, G::U2>(L + G::lW2, L + G::lb2, G::S2, L + G::oH1, L + G::oH2, act, lane, i2, g2, o2, a2);
+  chain_fwd<G::U2, G::U3>(L + G::lW3, L + G::lb3, G::S3, L + G::oH2, L + G::oH3, act, lane, i3, g3, o3, a3);
+  chain_fwd<G::U3, G::U4>(L + G::lW4, L + G::lb4, G::S4, L + G::oH3, L + G::oH4, act, lane, i4, g4, o4, a4);
+  {  // TimeDistributed(Dense(F)) + the MSE gradient: lane = f + 32 * part, k split in halves
+    const int f = lane & 31, part = lane >> 5;
+    float acc = 0.0f;
+    if (f < G::F) {
+#pragma unroll
+      for (int k0 = 0; k0 < G::U4; k0 += 2) acc = fmaf(L[G::oH4 + k0 + part], L[G::lK + (k0 + part) * G::SK + f], acc);
+    }
+    acc += xor32(acc, lane);
+    if (f < G::F) {
+      const float yp = acc + L[G::lkb + f];
+      if (part == 0) L[G::oDY + f] = (2.0f / (float)G::F) * (yp - yb[f]);   // Keras MSE: mean over features
+      else yp_out[f] = yp;
+    }
+    wave_order();
+  }
+  chain_bwd<G::U4, G::F>(L + G::oDY, L + G::lK, G::SK, i4, g4, o4, a4, L + G::oZ4, act, lane);
+  chain_bwd<G::U3, 3 * G::U4>(L + G::oZ4, L + G::lW4, G::S4, i3, g3, o3, a3, L + G::oZ3, act, lane);
+  chain_bwd<G::U2, 3 * G::U3>(L + G::oZ3, L + G::lW3, G::S3, i2, g2, o2, a2, L + G::oZ2, act, lane);
+  chain_bwd<G::U1, 3 * G::U2>(L + G::oZ2, L + G::lW2, G::S2, i1, g1, o1, a1, L + G::oZ1, act, lane);
+}
+
+// loss and argmax accuracy of one step from its saved prediction and target rows (one wave)
+template <typename G>
+__device__ __forceinline__ void step_stats(const float* yp, const float* yt, float* out, int lane) {
+  float vp = -3.402823466e38f, vt = -3.402823466e38f, d2 = 0.0f;
+  int ip = lane < G::F ? lane : 1 << 20, it = ip;
+  if (lane < G::F) {
+    vp = yp[lane];
+    vt = yt[lane];
+    const float d = vp - vt;
+    d2 = d * d;
+  }
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) {   // F <= 32: the first half-wave holds every feature
+    const float op = __shfl_xor(vp, o), ot = __shfl_xor(vt, o);
+    const int jp = __shfl_xor(ip, o), jt = __shfl_xor(it, o);
+    if (op > vp || (op == vp && jp < ip)) { vp = op; ip = jp; }
+    if (ot > vt || (ot == vt && jt < it)) { vt = ot; it = jt; }
+    d2 += __shfl_xor(d2, o);
+  }
+  if (lane == 0) {
+    out[0] = d2 / (float)G::F;
+    out[1] = ip == it ? 1.0f : 0.0f;
+  }
+}
+
+// Block `blk` of NB sample rows into LDS buffer blk & 1 by asynchronous global -> LDS
+// copies (global_load_lds_dword: LDS destination = M0 + 4 * lane, no registers held
+// while the rows are in flight).  Buffer layout: NB x rows of F floats, then NB y rows.
+// Issued from inline asm, so the compiler does not wait on it: the caller orders it with
+// an explicit `s_waitcnt vmcnt(0)` and a barrier before the block is read.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is deliberately clobbered (no other user here)
+__device__ __forceinline__ void glds4(const float* src, unsigned lds_addr) {
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(lds_addr), "v"(src) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <typename G>
+__device__ __forceinline__ float* row_block(float* L, int par) { return L + G::oX + par * 2 * NB * G::F; }
+
+template <typename G>
+__device__ __forceinline__ void block_load(const RefArgs& a, float* L, int64_t blk) {
+  static_assert(2 * 2 * NB * G::F <= 4 * MAXB * G::XS, "two row blocks fit the batch path's row buffers");
+  static_assert((2 * NB * G::F) % 64 == 0, "whole wave chunks");
+  constexpr int CHUNKS = 2 * NB * G::F / 64;
+  const int lane = threadIdx.x & 63;
+  float* buf = row_block<G>(L, (int)(blk & 1));
+  for (int c = threadIdx.x >> 6; c < CHUNKS; c += NT / 64) {
+    const int e = c * 64 + lane;
+    const bool yrow = e >= NB * G::F;
+    const int rem = yrow ? e - NB * G::F : e;
+    const int st = rem / G::F, f = rem - st * G::F;
+    const int64_t i = a.row0 + blk * NB + st;
+    const unsigned dst = (unsigned)(uintptr_t)((__attribute__((address_space(3))) float*)(buf + c * 64));
+    if (i < a.nrows) {
+      const int64_t src = a.order ? (int64_t)a.order[i] : i;
+      glds4(yrow ? a.y + src * a.ldy + f : a.x + src * a.ldx + f, __builtin_amdgcn_readfirstlane(dst));
+    }
+  }
+}
+
+template <typename G>
+__global__ __launch_bounds__(NT) void lstm_ref_train_b1_kernel(RefArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float L[];
+  constexpr int R = own_regs<G>();
+  static_assert(G::U1 <= 32 && G::U2 <= 32 && G::U3 <= 32 && G::U4 <= 32 && G::F <= 32, "one-wave chain");
+  float p[R], mo[R], vo[R];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t it0 = *a.iter;
+  own_all<OWN_LOAD, G>(p, mo, vo, a, L, nullptr, 0, 0.0f);
+  const int64_t avail = a.nrows - a.row0;
+  const int total = (int)(avail < a.nsteps ? avail : a.nsteps);
+  block_load<G>(a, L, 0);
+  wait_vm();
+  if (total > NB) block_load<G>(a, L, 1);
+  double b1t = pow((double)a.beta1, (double)it0), b2t = pow((double)a.beta2, (double)it0);
+  float* const yp_buf = L + G::oG1;   // [2][F] prediction rows (the batch path's gate saves are unused here)
+  float* const lr_slot = L + G::oST;
+  lds_barrier();
+  for (int s = 0; s < total; ++s) {
+    const int slot = s % NB, par = (s / NB) & 1;
+    const float* xb = row_block<G>(L, par) + slot * G::F;
+    const float* yb = xb + NB * G::F;
+    b1t *= (double)a.beta1;
+    b2t *= (double)a.beta2;
+    if (wave == 0) {
+      chain_step<G>(L, xb, yb, yp_buf + (s & 1) * G::F, a.act, lane);
+    } else if (wave == 1) {
+      if (lane == 0) *lr_slot = (float)((double)a.lr * sqrt(1.0 - b2t) / (1.0 - b1t));
+      if (s > 0) {
+        const int sp = s - 1;
+        step_stats<G>(yp_buf + (sp & 1) * G::F, row_block<G>(L, (sp / NB) & 1) + (NB + sp % NB) * G::F,
+                      a.out + 2 * sp, lane);
+      }
+    }
+    lds_barrier();
+    own_all<OWN_STEP, G>(p, mo, vo, a, L, xb, 1, *lr_slot);
+    // block b + 1 was requested 32 steps ago: land it before the barrier that ends block b.
+    // Block b + 2 reuses block b's buffer once the stats of b's last step are out (slot 0).
+    if (slot == NB - 1) wait_vm();
+    if (slot == 0 && s > 0 && (s / NB + 1) * NB < total) block_load<G>(a, L, s / NB + 1);
+    lds_barrier();
+  }
+  if (total > 0 && wave == 1) {
+    const int sp = total - 1;
+    step_stats<G>(yp_buf + (sp & 1) * G::F, row_block<G>(L, (sp / NB) & 1) + (NB + sp % NB) * G::F, a.out + 2 * sp,
+                  lane);
+  }
+  wait_vm();   // no copy may still target LDS when the workgroup ends
+  own_all<OWN_STORE, G>(p, mo, vo, a, L, nullptr, 0, 0.0f);
+  if (threadIdx.x == 0) *a.iter = it0 + (total > 0 ? total : 0);
+}
+
 }  // namespace
 
 int lstm_ref_train_params() { return Ref::NPARAM; }
@@ -361,7 +590,7 @@ hipError_t lstm_ref_train_launch(float* flat, float* m, float* v, int64_t* iter,
                                  hipStream_t stream) {
   if (B < 1 || B > MAXB || nsteps < 1 || row0 < 0 || row0 >= nrows) return hipErrorInvalidValue;
   RefArgs a{flat, m, v, iter, x, y, ldx, ldy, order, nrows, row0, B, nsteps, act, lr, beta1, beta2, eps, out};
-  auto k = lstm_ref_train_kernel<Ref>;
+  auto k = B == 1 ? lstm_ref_train_b1_kernel<Ref> : lstm_ref_train_kernel<Ref>;
   const size_t lds = sizeof(float) * Ref::LDS_FLOATS;
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
