@@ -357,22 +357,74 @@ __global__ __launch_bounds__(NT) void lstm_ref_train_kernel(RefArgs a) {
 }
 
 // ===================================================================================
-// Batch-1 path (the reference's setting).  At B = 1 no phase of the chain has more than
-// 32 (unit) tasks, so the whole forward + backward chain runs on wave 0 alone with
-// lane-split dot products (lane = j + U * part, the P = 64 / U parts each take every
-// P-th input and meet through permlane swaps) and NO workgroup barrier between its nine
-// layers: a wave's LDS operations complete in order, so a value one lane writes is seen
-// by every lane of the same wave that reads it afterwards.  The gates each lane saves
-// in the forward pass stay in its registers for the backward pass (same j mapping).
-// Per step there are two barriers: chain -> Adam on all 8 waves -> next step.
+// Batch-1 path (the reference's setting, `lstm_ref_train_b1_kernel`).
+//
+// Chain.  At B = 1 no layer has more than 32 unit tasks, so the whole forward + backward
+// chain of a step runs on wave 0 alone, with NO workgroup barrier inside it.  Lane
+// l = j + U * part works on unit j of a U-unit layer and on every P-th input (P = 64 / U);
+// the P partial dot products meet through permlane swaps.  A wave's LDS operations
+// complete in order, so a value one lane writes is seen by every lane of the same wave
+// that reads it afterwards.  The gates a lane computes in the forward pass stay in its
+// registers for the backward pass of the same layer (same j mapping).
+//   * Weights come from per-lane IMAGES: for every layer each lane finds exactly the
+//     weights it multiplies, slot-major (slot s of lane l at s * 64 + l: conflict-free,
+//     paired into ds_read2st64).  A weight has a forward image (the lane that uses it in
+//     its layer's dot product) and, for W2..W4 and the head kernel, a backward image (the
+//     lane that uses it in dh of the layer below).  A layer's image is requested one
+//     layer ahead, so its latency hides under the current layer's math.
+//   * Activations pass between layers through LDS, each written twice: in natural order
+//     (the weight gradients read it) and part-major for the consuming layer (each part's
+//     inputs contiguous: 16-byte reads).
+// Adam.  All 8 waves, between the step's two barriers.  Thread t owns column n = t % NA
+// of a weight block and rows k = t / NA + R * i, with R a multiple of the forward split
+// P, so every image address is a per-block base plus a compile-time offset.  It keeps
+// (p, m, v) in registers and writes the new value into both images.
 // Off the critical path, while wave 0 runs the chain:
 //   * wave 1 computes the Adam step size lr_t and the loss / argmax accuracy of the
 //     PREVIOUS step (from its saved prediction row);
-//   * the sample rows arrive 32 steps ahead: every 32nd step the workgroup writes the
-//     block it prefetched into registers 32 steps earlier to LDS and issues the loads of
-//     the block after it, so no step waits on a global load.
+//   * the sample rows arrive 32 steps ahead by asynchronous global -> LDS copies.
 // ===================================================================================
-constexpr int NB = MAXB;          // steps per prefetched row block (reuses the two row buffers)
+constexpr int NB = MAXB;          // steps per prefetched row block
+
+constexpr int c4(int v) { return (v + 3) & ~3; }
+
+template <typename G>
+struct B1 {
+  static constexpr int F = G::F, U1 = G::U1, U2 = G::U2, U3 = G::U3, U4 = G::U4;
+  static constexpr int P1 = 64 / U1, P2 = 64 / U2, P3 = 64 / U3, P4 = 64 / U4, PH = 2;
+  // inputs per lane (per part) of each chain layer
+  static constexpr int KF1 = F / P1, KF2 = U1 / P2, KF3 = U2 / P3, KF4 = U3 / P4, KHD = U4 / PH;
+  static constexpr int KB4 = F / P4, KB3 = 3 * U4 / P3, KB2 = 3 * U3 / P2, KB1 = 3 * U2 / P1;
+  static_assert(F % P1 == 0 && U1 % P2 == 0 && U2 % P3 == 0 && U3 % P4 == 0 && U4 % PH == 0 && F % P4 == 0 &&
+                    (3 * U4) % P3 == 0 && (3 * U3) % P2 == 0 && (3 * U2) % P1 == 0 && F <= 32,
+                "even lane splits");
+  // image segments (slots per lane): forward = 3 gates x inputs + 3 bias slots (part 0 only)
+  static constexpr int sF1 = 0, sF2 = sF1 + 3 * KF1 + 3, sF3 = sF2 + 3 * KF2 + 3, sF4 = sF3 + 3 * KF3 + 3;
+  static constexpr int sHD = sF4 + 3 * KF4 + 3, sB4 = sHD + KHD + 1, sB3 = sB4 + KB4, sB2 = sB3 + KB3;
+  static constexpr int sB1 = sB2 + KB2, NSLOT = sB1 + KB1;
+  // LDS map (floats)
+  static constexpr int oROW = NSLOT * 64;                        // 2 blocks x [NB x rows | NB y rows]
+  static constexpr int oH1 = oROW + 4 * NB * F, oH2 = oH1 + U1, oH3 = oH2 + U2, oH4 = oH3 + U3;   // natural order
+  static constexpr int oZ1 = oH4 + U4, oZ2 = oZ1 + 3 * U1, oZ3 = oZ2 + 3 * U2, oZ4 = oZ3 + 3 * U3;
+  static constexpr int oDY = oZ4 + 3 * U4;
+  // part-major copies for the consuming layer (each part's run 16-byte aligned)
+  static constexpr int qH1 = c4(oDY + F), qH2 = qH1 + P2 * c4(KF2), qH3 = qH2 + P3 * c4(KF3);
+  static constexpr int qH4 = qH3 + P4 * c4(KF4), qDY = qH4 + PH * c4(KHD), qZ4 = qDY + P4 * c4(KB4);
+  static constexpr int qZ3 = qZ4 + P3 * c4(KB3), qZ2 = qZ3 + P2 * c4(KB2);
+  static constexpr int oYP = qZ2 + P1 * c4(KB1);                 // [2][F] predictions (stats of the previous step)
+  static constexpr int oLR = oYP + 2 * F;                         // Adam step size of the current step
+  static constexpr int oSINK = c4(oLR + 1);                       // per-lane sink for writes a lane must not make
+  static constexpr int LDS_FLOATS = oSINK + 64;
+  // Adam ownership: rows per pass R (a multiple of the forward split), items per thread
+  static constexpr int rpass(int na, int p) { return (NT / na) / p * p; }
+  static constexpr int R1 = rpass(3 * U1, P1), R2 = rpass(3 * U2, P2), R3 = rpass(3 * U3, P3);
+  static constexpr int R4 = rpass(3 * U4, P4), RK = rpass(F, PH);
+  static constexpr int N1 = (F + R1 - 1) / R1, N2 = (U1 + R2 - 1) / R2, N3 = (U2 + R3 - 1) / R3;
+  static constexpr int N4 = (U3 + R4 - 1) / R4, NK = (U4 + RK - 1) / RK;
+  static constexpr int NBIAS = 3 * (U1 + U2 + U3 + U4) + F;
+  static_assert(NBIAS <= NT, "one bias per thread");
+  static constexpr int NOWN = N1 + N2 + N3 + N4 + NK + 1;
+};
 
 __device__ __forceinline__ void wave_order() { asm volatile("" ::: "memory"); }
 
@@ -384,86 +436,167 @@ __device__ __forceinline__ float part_sum(float v, int lane) {
   return v + xor32(v, lane);
 }
 
-// forward of one LSTM layer for one row on one wave: h[j] = o * act(i * g~)
-template <int K, int U>
-__device__ __forceinline__ void chain_fwd(const float* __restrict__ W, const float* __restrict__ bias, int S,
-                                          const float* in, float* h, int act, int lane, float& ig, float& gt,
-                                          float& og, float& ac) {
-  constexpr int P = 64 / U;
-  const int j = lane % U, part = lane / U;
-  float zi = 0.0f, zg = 0.0f, zo = 0.0f;
+// N consecutive image slots of this lane from slot s0 (slot-major: stride 64 floats)
+template <int N>
+__device__ __forceinline__ void img_rd(const float* L, int s0, int lane, float (&w)[N]) {
+  const float* b = L + s0 * 64 + lane;
 #pragma unroll
-  for (int k0 = 0; k0 < K; k0 += P) {
-    const int k = k0 + part;
-    if (K % P == 0 || k < K) {
-      const float xv = in[k];
-      const float* w = W + k * S + j;
-      zi = fmaf(xv, w[0], zi);
-      zg = fmaf(xv, w[U], zg);
-      zo = fmaf(xv, w[2 * U], zo);
-    }
+  for (int i = 0; i < N; ++i) w[i] = b[i * 64];
+}
+// N floats (N % 4 == 0) of a 16-byte aligned LDS run
+template <int N>
+__device__ __forceinline__ void vec_rd(const float* v, float (&o)[N]) {
+  static_assert(N % 4 == 0, "whole 16-byte reads");
+#pragma unroll
+  for (int i = 0; i < N; i += 4) {
+    const float4 t = *reinterpret_cast<const float4*>(v + i);
+    o[i] = t.x;
+    o[i + 1] = t.y;
+    o[i + 2] = t.z;
+    o[i + 3] = t.w;
   }
-  zi = part_sum<U>(zi, lane) + bias[j];
-  zg = part_sum<U>(zg, lane) + bias[U + j];
-  zo = part_sum<U>(zo, lane) + bias[2 * U + j];
+}
+
+// position of element e of a vector in its consumer's part-major copy (PC parts of KPC)
+template <int PC, int KPC>
+__device__ __forceinline__ int qpos(int e) { return (e % PC) * c4(KPC) + e / PC; }
+
+// forward of one LSTM unit from this lane's image (3 gates x KP inputs + bias slots)
+template <int KP, int U, int NW, int NI>
+__device__ __forceinline__ float fwd_unit(const float (&w)[NW], const float (&in)[NI], int act, int lane, float& ig,
+                                          float& gt, float& og, float& ac) {
+  static_assert(NW == 3 * KP + 3 && NI >= KP, "image / input shapes");
+  float zi = w[3 * KP], zg = w[3 * KP + 1], zo = w[3 * KP + 2];
+#pragma unroll
+  for (int i = 0; i < KP; ++i) {
+    zi = fmaf(in[i], w[3 * i], zi);
+    zg = fmaf(in[i], w[3 * i + 1], zg);
+    zo = fmaf(in[i], w[3 * i + 2], zo);
+  }
+  zi = part_sum<U>(zi, lane);
+  zg = part_sum<U>(zg, lane);
+  zo = part_sum<U>(zo, lane);
   ig = sigm(zi);
   gt = actf(act, zg);
   og = sigm(zo);
   ac = actf(act, ig * gt);
-  if (part == 0) h[j] = og * ac;
+  return og * ac;
+}
+
+// dh of one unit: this lane's image row . its inputs from the layer above
+template <int KP, int U, int NI>
+__device__ __forceinline__ float bwd_dh(const float (&w)[KP], const float (&up)[NI], int lane) {
+  static_assert(NI >= KP, "input shape");
+  float d0 = 0.0f, d1 = 0.0f;
+#pragma unroll
+  for (int i = 0; i + 1 < KP; i += 2) {
+    d0 = fmaf(up[i], w[i], d0);
+    d1 = fmaf(up[i + 1], w[i + 1], d1);
+  }
+  if (KP & 1) d0 = fmaf(up[KP - 1], w[KP - 1], d0);
+  return part_sum<U>(d0 + d1, lane);
+}
+
+// h of a forward layer: part 0 -> natural order, part 1 -> the consumer's copy, rest -> sink
+template <typename Bq, int PC, int KPC>
+__device__ __forceinline__ void put_h(float* L, int nat, int q, int j, int part, int lane, float h) {
+  L[part == 0 ? nat + j : (part == 1 ? q + qpos<PC, KPC>(j) : Bq::oSINK + lane)] = h;
   wave_order();
 }
 
-// backward of one LSTM layer for one row: dh[j] = up . Wup[j], then dz (i | g | o)
-template <int U, int KN>
-__device__ __forceinline__ void chain_bwd(const float* up, const float* __restrict__ Wup, int WS, float ig, float gt,
-                                          float og, float ac, float* dz, int act, int lane) {
-  constexpr int P = 64 / U;
-  const int j = lane % U, part = lane / U;
-  const float* wr = Wup + j * WS;
-  float d0 = 0.0f, d1 = 0.0f;
-#pragma unroll
-  for (int n0 = 0; n0 < KN; n0 += 2 * P) {
-    const int n = n0 + part;
-    if (KN % P == 0 || n < KN) d0 = fmaf(up[n], wr[n], d0);
-    if (n + P < KN) d1 = fmaf(up[n + P], wr[n + P], d1);
-  }
-  const float dh = part_sum<U>(d0 + d1, lane);
-  const float dc = dh * og * actd(act, ac);
-  if (part == 0) dz[j] = dc * gt * ig * (1.0f - ig);
-  if (part == (P > 2 ? 1 : 0)) dz[U + j] = dc * ig * actd(act, gt);
-  if (part == (P > 2 ? 2 : 1)) dz[2 * U + j] = dh * ac * og * (1.0f - og);
+// dz (i | g | o) of unit j: part 0 -> natural, part 1 -> the consumer's copy (QZ), rest -> sink
+template <typename Bq, int U, int PC, int KPC, bool QZ>
+__device__ __forceinline__ void put_dz(float* L, int nat, int q, int j, int part, int lane, float zi, float zg,
+                                       float zo) {
+  const int sink = Bq::oSINK + lane;
+  L[part == 0 ? nat + j : (part == 1 && QZ ? q + qpos<PC, KPC>(j) : sink)] = zi;
+  L[part == 0 ? nat + U + j : (part == 1 && QZ ? q + qpos<PC, KPC>(U + j) : sink)] = zg;
+  L[part == 0 ? nat + 2 * U + j : (part == 1 && QZ ? q + qpos<PC, KPC>(2 * U + j) : sink)] = zo;
   wave_order();
+}
+
+// gate gradients of one unit from dh and the saved forward gates
+__device__ __forceinline__ void dz_unit(float dh, float ig, float gt, float og, float ac, int act, float& zi,
+                                        float& zg, float& zo) {
+  const float dc = dh * og * actd(act, ac);
+  zi = dc * gt * ig * (1.0f - ig);
+  zg = dc * ig * actd(act, gt);
+  zo = dh * ac * og * (1.0f - og);
 }
 
 // the whole chain of one Keras step at B = 1 (wave 0)
 template <typename G>
 __device__ __forceinline__ void chain_step(float* L, const float* xb, const float* yb, float* yp_out, int act,
                                            int lane) {
-  float i1, g1, o1, a1, i2, g2, o2, a2, i3, g3, o3, a3, i4, g4, o4, a4;
-  chain_fwd<G::F, G::U1>(L + G::lW1, L + G::lb1, G::S1, xb, L + G::oH1, act, lane, i1, g1, o1, a1);
-  chain_fwd<G::U1, G::U2>(L + G::lW2, L + G::lb2, G::S2, L + G::oH1, L + G::oH2, act, lane, i2, g2, o2, a2);
-  chain_fwd<G::U2, G::U3>(L + G::lW3, L + G::lb3, G::S3, L + G::oH2, L + G::oH3, act, lane, i3, g3, o3, a3);
-  chain_fwd<G::U3, G::U4>(L + G::lW4, L + G::lb4, G::S4, L + G::oH3, L + G::oH4, act, lane, i4, g4, o4, a4);
-  {  // TimeDistributed(Dense(F)) + the MSE gradient: lane = f + 32 * part, k split in halves
-    const int f = lane & 31, part = lane >> 5;
-    float acc = 0.0f;
-    if (f < G::F) {
+  using Q = B1<G>;
+  const int j1 = lane % G::U1, p1 = lane / G::U1, j2 = lane % G::U2, p2 = lane / G::U2;
+  const int j3 = lane % G::U3, p3 = lane / G::U3, j4 = lane % G::U4, p4 = lane / G::U4;
+  float i1, g1, o1, a1, i2, g2, o2, a2, i3, g3, o3, a3, i4, g4, o4, a4, h;
+  float x[Q::KF1];
 #pragma unroll
-      for (int k0 = 0; k0 < G::U4; k0 += 2) acc = fmaf(L[G::oH4 + k0 + part], L[G::lK + (k0 + part) * G::SK + f], acc);
-    }
-    acc += xor32(acc, lane);
-    if (f < G::F) {
-      const float yp = acc + L[G::lkb + f];
-      if (part == 0) L[G::oDY + f] = (2.0f / (float)G::F) * (yp - yb[f]);   // Keras MSE: mean over features
-      else yp_out[f] = yp;
-    }
+  for (int i = 0; i < Q::KF1; ++i) x[i] = xb[p1 + Q::P1 * i];
+  float w1[3 * Q::KF1 + 3], w2[3 * Q::KF2 + 3];
+  img_rd(L, Q::sF1, lane, w1);
+  img_rd(L, Q::sF2, lane, w2);
+  h = fwd_unit<Q::KF1, G::U1>(w1, x, act, lane, i1, g1, o1, a1);
+  put_h<Q, Q::P2, Q::KF2>(L, Q::oH1, Q::qH1, j1, p1, lane, h);
+
+  float w3[3 * Q::KF3 + 3], in2[c4(Q::KF2)];
+  img_rd(L, Q::sF3, lane, w3);
+  vec_rd(L + Q::qH1 + p2 * c4(Q::KF2), in2);
+  h = fwd_unit<Q::KF2, G::U2>(w2, in2, act, lane, i2, g2, o2, a2);
+  put_h<Q, Q::P3, Q::KF3>(L, Q::oH2, Q::qH2, j2, p2, lane, h);
+
+  float w4[3 * Q::KF4 + 3], in3[c4(Q::KF3)];
+  img_rd(L, Q::sF4, lane, w4);
+  vec_rd(L + Q::qH2 + p3 * c4(Q::KF3), in3);
+  h = fwd_unit<Q::KF3, G::U3>(w3, in3, act, lane, i3, g3, o3, a3);
+  put_h<Q, Q::P4, Q::KF4>(L, Q::oH3, Q::qH3, j3, p3, lane, h);
+
+  float wh[Q::KHD + 1], in4[c4(Q::KF4)];
+  img_rd(L, Q::sHD, lane, wh);
+  vec_rd(L + Q::qH3 + p4 * c4(Q::KF4), in4);
+  h = fwd_unit<Q::KF4, G::U4>(w4, in4, act, lane, i4, g4, o4, a4);
+  put_h<Q, Q::PH, Q::KHD>(L, Q::oH4, Q::qH4, j4, p4, lane, h);
+
+  float wb4[Q::KB4];
+  img_rd(L, Q::sB4, lane, wb4);
+  {  // TimeDistributed(Dense(F)) + the MSE gradient: lane = f + 32 * part
+    const int f = lane & 31, ph = lane >> 5, fc = f < G::F ? f : G::F - 1;
+    float inh[c4(Q::KHD)];
+    vec_rd(L + Q::qH4 + ph * c4(Q::KHD), inh);
+    float acc = wh[Q::KHD];
+#pragma unroll
+    for (int i = 0; i < Q::KHD; ++i) acc = fmaf(inh[i], wh[i], acc);
+    const float yp = acc + xor32(acc, lane);
+    const float dy = (2.0f / (float)G::F) * (yp - yb[fc]);   // Keras MSE: mean over features
+    const int sink = Q::oSINK + lane;
+    L[f >= G::F ? sink : (ph == 0 ? Q::oDY + f : Q::qDY + qpos<Q::P4, Q::KB4>(f))] = dy;
+    yp_out[f < G::F && ph == 0 ? f : sink - (int)(yp_out - L)] = yp;
     wave_order();
   }
-  chain_bwd<G::U4, G::F>(L + G::oDY, L + G::lK, G::SK, i4, g4, o4, a4, L + G::oZ4, act, lane);
-  chain_bwd<G::U3, 3 * G::U4>(L + G::oZ4, L + G::lW4, G::S4, i3, g3, o3, a3, L + G::oZ3, act, lane);
-  chain_bwd<G::U2, 3 * G::U3>(L + G::oZ3, L + G::lW3, G::S3, i2, g2, o2, a2, L + G::oZ2, act, lane);
-  chain_bwd<G::U1, 3 * G::U2>(L + G::oZ2, L + G::lW2, G::S2, i1, g1, o1, a1, L + G::oZ1, act, lane);
+  float wb3[Q::KB3], up4[c4(Q::KB4)], zi, zg, zo;
+  img_rd(L, Q::sB3, lane, wb3);
+  vec_rd(L + Q::qDY + p4 * c4(Q::KB4), up4);
+  dz_unit(bwd_dh<Q::KB4, G::U4>(wb4, up4, lane), i4, g4, o4, a4, act, zi, zg, zo);
+  put_dz<Q, G::U4, Q::P3, Q::KB3, true>(L, Q::oZ4, Q::qZ4, j4, p4, lane, zi, zg, zo);
+
+  float wb2[Q::KB2], up3[c4(Q::KB3)];
+  img_rd(L, Q::sB2, lane, wb2);
+  vec_rd(L + Q::qZ4 + p3 * c4(Q::KB3), up3);
+  dz_unit(bwd_dh<Q::KB3, G::U3>(wb3, up3, lane), i3, g3, o3, a3, act, zi, zg, zo);
+  put_dz<Q, G::U3, Q::P2, Q::KB2, true>(L, Q::oZ3, Q::qZ3, j3, p3, lane, zi, zg, zo);
+
+  float wb1[Q::KB1], up2[c4(Q::KB2)];
+  img_rd(L, Q::sB1, lane, wb1);
+  vec_rd(L + Q::qZ3 + p2 * c4(Q::KB2), up2);
+  dz_unit(bwd_dh<Q::KB2, G::U2>(wb2, up2, lane), i2, g2, o2, a2, act, zi, zg, zo);
+  put_dz<Q, G::U2, Q::P1, Q::KB1, true>(L, Q::oZ2, Q::qZ2, j2, p2, lane, zi, zg, zo);
+
+  float up1[c4(Q::KB1)];
+  vec_rd(L + Q::qZ2 + p1 * c4(Q::KB1), up1);
+  dz_unit(bwd_dh<Q::KB1, G::U1>(wb1, up1, lane), i1, g1, o1, a1, act, zi, zg, zo);
+  put_dz<Q, G::U1, 1, 1, false>(L, Q::oZ1, 0, j1, p1, lane, zi, zg, zo);
 }
 
 // loss and argmax accuracy of one step from its saved prediction and target rows (one wave)
@@ -491,7 +624,120 @@ __device__ __forceinline__ void step_stats(const float* yp, const float* yt, flo
   }
 }
 
-// Block `blk` of NB sample rows into LDS buffer blk & 1 by asynchronous global -> LDS
+// ---- Adam ownership of the batch-1 kernel ----
+// One weight block: rows K, columns NA, forward split P (rows per pass R).  Thread t owns
+// column n = t % NA and rows k0 + R * i (k0 = t / NA).  fwd(k0, n) / bwd(k0, n) give the
+// image addresses of row k0; row k0 + R * i sits FSTEP * i / BSTEP * i floats further.
+enum { B1_LOAD = 0, B1_STEP = 1, B1_STORE = 2 };
+
+struct AdamK {
+  float b1, b2, c1, c2, eps, lr_t;
+};
+__device__ __forceinline__ void adam_item(float& p, float& m, float& v, float g, const AdamK& k) {
+  m = k.b1 * m + k.c1 * g;
+  v = k.b2 * v + k.c2 * g * g;
+  p -= k.lr_t * m * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v) + k.eps);   // v_sqrt / v_rcp
+}
+
+template <int MODE, int K, int NA, int R, int NI, int R0, int NR, bool BWD>
+__device__ __forceinline__ void own_w(float (&p)[NR], float (&mo)[NR], float (&vo)[NR], const RefArgs& a, float* L,
+                                      int t, int64_t gbase, int gstride, int gcol, int fwd, int fstep, int bwd,
+                                      int bstep, int in, int dz, const AdamK& ak) {
+  static_assert(R0 + NI <= NR, "ownership register budget");
+  if (t >= R * NA) return;
+  const int k0 = t / NA;
+  float dzn = 0.0f;
+  if (MODE == B1_STEP) dzn = L[dz];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int k = k0 + R * i;
+    if ((K % R == 0 || i + 1 < NI) || k < K) {
+      const int64_t g = gbase + (int64_t)k * gstride + gcol;
+      if (MODE == B1_LOAD) {
+        p[R0 + i] = a.flat[g];
+        mo[R0 + i] = a.m[g];
+        vo[R0 + i] = a.v[g];
+      } else if (MODE == B1_STORE) {
+        a.flat[g] = p[R0 + i];
+        a.m[g] = mo[R0 + i];
+        a.v[g] = vo[R0 + i];
+      } else {
+        adam_item(p[R0 + i], mo[R0 + i], vo[R0 + i], L[in + R * i] * dzn, ak);
+      }
+      if (MODE != B1_STORE) {
+        L[fwd + fstep * i] = p[R0 + i];
+        if (BWD) L[bwd + bstep * i] = p[R0 + i];
+      }
+    }
+  }
+}
+
+template <int MODE, typename G, int NR>
+__device__ __forceinline__ void own_b1(float (&p)[NR], float (&mo)[NR], float (&vo)[NR], const RefArgs& a, float* L,
+                                       const float* xb, const AdamK& ak) {
+  using Q = B1<G>;
+  const int t = threadIdx.x;
+  const int x_in = (int)(xb - L);
+  // W_L[k][n], n = gate * U + j (active columns i | g | o); Keras column col(n) of the 4U-wide kernel
+  // forward image: lane j + U * (k % P), slot sF + 3 * (k / P) + gate
+  // backward image (consumer: the layer below, U' = K units, P' = 64 / K): lane k + K * (n % P'), slot sB + n / P'
+#define SML_W_BLOCK(K_, U_, P_, R_, N_, R0_, SF, BW, SB, GW, IN, DZ)                                                 \
+  {                                                                                                                  \
+    constexpr int NA = 3 * U_, PB = 64 / K_;                                                                         \
+    const int n = t % NA, k0 = t / NA, gate = n / U_, j = n % U_;                                                    \
+    const int fwd = (SF + 3 * (k0 / P_) + gate) * 64 + j + U_ * (k0 % P_);                                           \
+    const int bwd = BW ? (SB + n / PB) * 64 + k0 + K_ * (n % PB) : 0;                                                \
+    own_w<MODE, K_, NA, R_, N_, R0_, NR, BW>(p, mo, vo, a, L, t, GW, 4 * U_, n < U_ ? n : n + U_, fwd,               \
+                                             3 * (R_ / P_) * 64, bwd, R_, (IN) + k0, DZ + n, ak);                     \
+  }
+  constexpr int r1 = 0, r2 = r1 + Q::N1, r3 = r2 + Q::N2, r4 = r3 + Q::N3, rk = r4 + Q::N4, rb = rk + Q::NK;
+  SML_W_BLOCK(G::F, G::U1, Q::P1, Q::R1, Q::N1, r1, Q::sF1, false, 0, G::gW1, x_in, Q::oZ1)
+  SML_W_BLOCK(G::U1, G::U2, Q::P2, Q::R2, Q::N2, r2, Q::sF2, true, Q::sB1, G::gW2, Q::oH1, Q::oZ2)
+  SML_W_BLOCK(G::U2, G::U3, Q::P3, Q::R3, Q::N3, r3, Q::sF3, true, Q::sB2, G::gW3, Q::oH2, Q::oZ3)
+  SML_W_BLOCK(G::U3, G::U4, Q::P4, Q::R4, Q::N4, r4, Q::sF4, true, Q::sB3, G::gW4, Q::oH3, Q::oZ4)
+#undef SML_W_BLOCK
+  {  // head kernel K[k][f]: forward lane f + 32 * (k % 2), slot sHD + k / 2; backward (D4) lane k + 32 * (f % 2), slot sB4 + f / 2
+    const int f = t % G::F, k0 = t / G::F;
+    const int fwd = (Q::sHD + k0 / 2) * 64 + f + 32 * (k0 % 2);
+    const int bwd = (Q::sB4 + f / Q::P4) * 64 + k0 + G::U4 * (f % Q::P4);
+    own_w<MODE, G::U4, G::F, Q::RK, Q::NK, rk, NR, true>(p, mo, vo, a, L, t, G::gK, G::F, f, fwd, (Q::RK / 2) * 64,
+                                                         bwd, Q::RK, Q::oH4 + k0, Q::oDY + f, ak);
+  }
+  if (t < Q::NBIAS) {   // one bias per thread: b1 | b2 | b3 | b4 | head bias
+    int gofs, img, dz;
+    auto pick = [&](int e, int U, int sF, int KP, int gb, int oz) {
+      const int gate = e / U, j = e % U;
+      gofs = gb + (e < U ? e : e + U);
+      img = (sF + 3 * KP + gate) * 64 + j;
+      dz = oz + e;
+    };
+    constexpr int e1 = 3 * G::U1, e2 = e1 + 3 * G::U2, e3 = e2 + 3 * G::U3, e4 = e3 + 3 * G::U4;
+    if (t < e1) pick(t, G::U1, Q::sF1, Q::KF1, G::gb1, Q::oZ1);
+    else if (t < e2) pick(t - e1, G::U2, Q::sF2, Q::KF2, G::gb2, Q::oZ2);
+    else if (t < e3) pick(t - e2, G::U3, Q::sF3, Q::KF3, G::gb3, Q::oZ3);
+    else if (t < e4) pick(t - e3, G::U4, Q::sF4, Q::KF4, G::gb4, Q::oZ4);
+    else {
+      const int f = t - e4;
+      gofs = G::gkb + f;
+      img = (Q::sHD + Q::KHD) * 64 + f;
+      dz = Q::oDY + f;
+    }
+    if (MODE == B1_LOAD) {
+      p[rb] = a.flat[gofs];
+      mo[rb] = a.m[gofs];
+      vo[rb] = a.v[gofs];
+    } else if (MODE == B1_STORE) {
+      a.flat[gofs] = p[rb];
+      a.m[gofs] = mo[rb];
+      a.v[gofs] = vo[rb];
+    } else {
+      adam_item(p[rb], mo[rb], vo[rb], L[dz], ak);
+    }
+    if (MODE != B1_STORE) L[img] = p[rb];
+  }
+}
+
+// Block `blk` of NB sample rows into row buffer blk & 1 by asynchronous global -> LDS
 // copies (global_load_lds_dword: LDS destination = M0 + 4 * lane, no registers held
 // while the rows are in flight).  Buffer layout: NB x rows of F floats, then NB y rows.
 // Issued from inline asm, so the compiler does not wait on it: the caller orders it with
@@ -505,11 +751,10 @@ __device__ __forceinline__ void glds4(const float* src, unsigned lds_addr) {
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 template <typename G>
-__device__ __forceinline__ float* row_block(float* L, int par) { return L + G::oX + par * 2 * NB * G::F; }
+__device__ __forceinline__ float* row_block(float* L, int par) { return L + B1<G>::oROW + par * 2 * NB * G::F; }
 
 template <typename G>
 __device__ __forceinline__ void block_load(const RefArgs& a, float* L, int64_t blk) {
-  static_assert(2 * 2 * NB * G::F <= 4 * MAXB * G::XS, "two row blocks fit the batch path's row buffers");
   static_assert((2 * NB * G::F) % 64 == 0, "whole wave chunks");
   constexpr int CHUNKS = 2 * NB * G::F / 64;
   const int lane = threadIdx.x & 63;
@@ -528,24 +773,38 @@ __device__ __forceinline__ void block_load(const RefArgs& a, float* L, int64_t b
   }
 }
 
+#ifdef SML_LREF_PROBE
+// Phase probe (tools/lref_probe): shader-clock cycles summed over the steps of a launch,
+// measured by wave 0: [0] chain, [1] chain end -> past barrier 1, [2] Adam, [3] -> past
+// barrier 2, [4] steps.  Built only into the probe binary.
+__device__ unsigned long long g_lref_probe[8];
+#endif
+
 template <typename G>
 __global__ __launch_bounds__(NT) void lstm_ref_train_b1_kernel(RefArgs a) {
   extern __shared__ __attribute__((aligned(16))) float L[];
-  constexpr int R = own_regs<G>();
-  static_assert(G::U1 <= 32 && G::U2 <= 32 && G::U3 <= 32 && G::U4 <= 32 && G::F <= 32, "one-wave chain");
-  float p[R], mo[R], vo[R];
+  using Q = B1<G>;
+  float p[Q::NOWN], mo[Q::NOWN], vo[Q::NOWN];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t it0 = *a.iter;
-  own_all<OWN_LOAD, G>(p, mo, vo, a, L, nullptr, 0, 0.0f);
+  for (int i = threadIdx.x; i < Q::NSLOT * 64; i += NT) L[i] = 0.0f;   // unused image slots stay 0
+  lds_barrier();
+  AdamK ak{a.beta1, a.beta2, 1.0f - a.beta1, 1.0f - a.beta2, a.eps, 0.0f};
+  own_b1<B1_LOAD, G>(p, mo, vo, a, L, row_block<G>(L, 0), ak);
   const int64_t avail = a.nrows - a.row0;
   const int total = (int)(avail < a.nsteps ? avail : a.nsteps);
   block_load<G>(a, L, 0);
   wait_vm();
   if (total > NB) block_load<G>(a, L, 1);
   double b1t = pow((double)a.beta1, (double)it0), b2t = pow((double)a.beta2, (double)it0);
-  float* const yp_buf = L + G::oG1;   // [2][F] prediction rows (the batch path's gate saves are unused here)
-  float* const lr_slot = L + G::oST;
+  float* const yp_buf = L + Q::oYP;
   lds_barrier();
+#ifdef SML_LREF_PROBE
+  unsigned long long pc[4] = {0, 0, 0, 0}, tq = clock64(), tn;
+#define SML_PROBE_MARK(i) (tn = clock64(), pc[i] += tn - tq, tq = tn)
+#else
+#define SML_PROBE_MARK(i) ((void)0)
+#endif
   for (int s = 0; s < total; ++s) {
     const int slot = s % NB, par = (s / NB) & 1;
     const float* xb = row_block<G>(L, par) + slot * G::F;
@@ -554,8 +813,9 @@ __global__ __launch_bounds__(NT) void lstm_ref_train_b1_kernel(RefArgs a) {
     b2t *= (double)a.beta2;
     if (wave == 0) {
       chain_step<G>(L, xb, yb, yp_buf + (s & 1) * G::F, a.act, lane);
+      SML_PROBE_MARK(0);
     } else if (wave == 1) {
-      if (lane == 0) *lr_slot = (float)((double)a.lr * sqrt(1.0 - b2t) / (1.0 - b1t));
+      if (lane == 0) L[Q::oLR] = (float)((double)a.lr * sqrt(1.0 - b2t) / (1.0 - b1t));
       if (s > 0) {
         const int sp = s - 1;
         step_stats<G>(yp_buf + (sp & 1) * G::F, row_block<G>(L, (sp / NB) & 1) + (NB + sp % NB) * G::F,
@@ -563,26 +823,48 @@ __global__ __launch_bounds__(NT) void lstm_ref_train_b1_kernel(RefArgs a) {
       }
     }
     lds_barrier();
-    own_all<OWN_STEP, G>(p, mo, vo, a, L, xb, 1, *lr_slot);
+    SML_PROBE_MARK(1);
+    ak.lr_t = L[Q::oLR];
+    own_b1<B1_STEP, G>(p, mo, vo, a, L, xb, ak);
+    SML_PROBE_MARK(2);
     // block b + 1 was requested 32 steps ago: land it before the barrier that ends block b.
     // Block b + 2 reuses block b's buffer once the stats of b's last step are out (slot 0).
     if (slot == NB - 1) wait_vm();
     if (slot == 0 && s > 0 && (s / NB + 1) * NB < total) block_load<G>(a, L, s / NB + 1);
     lds_barrier();
+    SML_PROBE_MARK(3);
   }
+#ifdef SML_LREF_PROBE
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < 4; ++i) atomicAdd(&g_lref_probe[i], pc[i]);
+    atomicAdd(&g_lref_probe[4], (unsigned long long)total);
+  }
+#endif
+#undef SML_PROBE_MARK
   if (total > 0 && wave == 1) {
     const int sp = total - 1;
     step_stats<G>(yp_buf + (sp & 1) * G::F, row_block<G>(L, (sp / NB) & 1) + (NB + sp % NB) * G::F, a.out + 2 * sp,
                   lane);
   }
   wait_vm();   // no copy may still target LDS when the workgroup ends
-  own_all<OWN_STORE, G>(p, mo, vo, a, L, nullptr, 0, 0.0f);
+  own_b1<B1_STORE, G>(p, mo, vo, a, L, nullptr, ak);
   if (threadIdx.x == 0) *a.iter = it0 + (total > 0 ? total : 0);
 }
 
 }  // namespace
 
 int lstm_ref_train_params() { return Ref::NPARAM; }
+
+#ifdef SML_LREF_PROBE
+hipError_t lstm_ref_probe_read(unsigned long long* host8, bool reset) {
+  hipError_t e = hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_lref_probe), 8 * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[8] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_lref_probe), z, sizeof z);
+  }
+  return e;
+}
+#endif
 
 hipError_t lstm_ref_train_launch(float* flat, float* m, float* v, int64_t* iter, const float* x, int64_t ldx,
                                  const float* y, int64_t ldy, const int32_t* order, int64_t nrows, int64_t row0, int B,
@@ -591,7 +873,7 @@ hipError_t lstm_ref_train_launch(float* flat, float* m, float* v, int64_t* iter,
   if (B < 1 || B > MAXB || nsteps < 1 || row0 < 0 || row0 >= nrows) return hipErrorInvalidValue;
   RefArgs a{flat, m, v, iter, x, y, ldx, ldy, order, nrows, row0, B, nsteps, act, lr, beta1, beta2, eps, out};
   auto k = B == 1 ? lstm_ref_train_b1_kernel<Ref> : lstm_ref_train_kernel<Ref>;
-  const size_t lds = sizeof(float) * Ref::LDS_FLOATS;
+  const size_t lds = sizeof(float) * (B == 1 ? B1<Ref>::LDS_FLOATS : Ref::LDS_FLOATS);
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
