@@ -375,16 +375,29 @@ __global__ __launch_bounds__(NT) void lstm_ref_train_kernel(RefArgs a) {
 //   * Activations pass between layers through LDS, each written twice: in natural order
 //     (the weight gradients read it) and part-major for the consuming layer (each part's
 //     inputs contiguous: 16-byte reads).
-// Adam.  All 8 waves, between the step's two barriers.  Thread t owns column n = t % NA
-// of a weight block and rows k = t / NA + R * i, with R a multiple of the forward split
-// P, so every image address is a per-block base plus a compile-time offset.  It keeps
-// (p, m, v) in registers and writes the new value into both images.
-// Off the critical path, while wave 0 runs the chain:
-//   * wave 1 computes the Adam step size lr_t and the loss / argmax accuracy of the
-//     PREVIOUS step (from its saved prediction row);
-//   * the sample rows arrive 32 steps ahead by asynchronous global -> LDS copies.
+// Adam, pipelined against the next step's chain.  Wave 0 runs only the chain; waves 1..7
+// run Adam.  Thread t' = t - 64 owns column n = t' % NA of a weight block and rows
+// k = t' / NA + R * i, with R a multiple of the forward split P, so every image address
+// is a per-block base plus a compile-time offset; (p, m, v) stay in its registers and the
+// new value goes into both images.  The chain counts its stages in an LDS counter (head,
+// D4, D3, D2, D1 of every step), and the Adam waves take the blocks in REVERSE order,
+// each as soon as its gradient exists and the chain has read that block's old backward
+// image: head after the head layer, W4 after D4, W3 after D3, W2 after D2, W1 after D1.
+// So Adam of step s runs under the backward half of the chain of step s, and only W1's
+// update sits between the end of one chain and the start of the next (the chain waits on
+// a counter of finished W1 blocks before it reads any image).  No workgroup barrier
+// remains in the loop.  The activations Adam reads (natural-order h, dz) are double-
+// buffered by step
+// parity.  A wave's LDS operations complete in order, so "write the images, then bump
+// the counter" needs no fence beyond keeping the compiler from reordering them.
+// Off the critical path:
+//   * the lightest Adam wave computes the loss / argmax accuracy of the step it just
+//     updated (from its saved prediction row);
+//   * the sample rows arrive 32 steps ahead by asynchronous global -> LDS copies that
+//     wave 0 issues and waits for.
 // ===================================================================================
 constexpr int NB = MAXB;          // steps per prefetched row block
+constexpr int NADAM = NT - 64;    // Adam threads (waves 1..7)
 
 constexpr int c4(int v) { return (v + 3) & ~3; }
 
@@ -402,31 +415,52 @@ struct B1 {
   static constexpr int sF1 = 0, sF2 = sF1 + 3 * KF1 + 3, sF3 = sF2 + 3 * KF2 + 3, sF4 = sF3 + 3 * KF3 + 3;
   static constexpr int sHD = sF4 + 3 * KF4 + 3, sB4 = sHD + KHD + 1, sB3 = sB4 + KB4, sB2 = sB3 + KB3;
   static constexpr int sB1 = sB2 + KB2, NSLOT = sB1 + KB1;
+  // natural-order activations of one step (Adam's inputs), double-buffered by step parity
+  static constexpr int nH1 = 0, nH2 = nH1 + U1, nH3 = nH2 + U2, nH4 = nH3 + U3;
+  static constexpr int nZ1 = nH4 + U4, nZ2 = nZ1 + 3 * U1, nZ3 = nZ2 + 3 * U2, nZ4 = nZ3 + 3 * U3;
+  static constexpr int nDY = nZ4 + 3 * U4, NATS = c4(nDY + F);
   // LDS map (floats)
   static constexpr int oROW = NSLOT * 64;                        // 2 blocks x [NB x rows | NB y rows]
-  static constexpr int oH1 = oROW + 4 * NB * F, oH2 = oH1 + U1, oH3 = oH2 + U2, oH4 = oH3 + U3;   // natural order
-  static constexpr int oZ1 = oH4 + U4, oZ2 = oZ1 + 3 * U1, oZ3 = oZ2 + 3 * U2, oZ4 = oZ3 + 3 * U3;
-  static constexpr int oDY = oZ4 + 3 * U4;
+  static constexpr int oNAT = oROW + 4 * NB * F;                 // 2 x NATS
   // part-major copies for the consuming layer (each part's run 16-byte aligned)
-  static constexpr int qH1 = c4(oDY + F), qH2 = qH1 + P2 * c4(KF2), qH3 = qH2 + P3 * c4(KF3);
+  static constexpr int qH1 = oNAT + 2 * NATS, qH2 = qH1 + P2 * c4(KF2), qH3 = qH2 + P3 * c4(KF3);
   static constexpr int qH4 = qH3 + P4 * c4(KF4), qDY = qH4 + PH * c4(KHD), qZ4 = qDY + P4 * c4(KB4);
   static constexpr int qZ3 = qZ4 + P3 * c4(KB3), qZ2 = qZ3 + P2 * c4(KB2);
-  static constexpr int oYP = qZ2 + P1 * c4(KB1);                 // [2][F] predictions (stats of the previous step)
-  static constexpr int oLR = oYP + 2 * F;                         // Adam step size of the current step
-  static constexpr int oSINK = c4(oLR + 1);                       // per-lane sink for writes a lane must not make
+  static constexpr int oYP = qZ2 + P1 * c4(KB1);                 // [2][F] predictions
+  static constexpr int oCNT = c4(oYP + 2 * F);                    // counters: [0..4] Adam blocks, [5] chain
+  static constexpr int oSINK = oCNT + 8;                          // per-lane sink for writes a lane must not make
   static constexpr int LDS_FLOATS = oSINK + 64;
-  // Adam ownership: rows per pass R (a multiple of the forward split), items per thread
-  static constexpr int rpass(int na, int p) { return (NT / na) / p * p; }
+  // Adam ownership over the NADAM threads of waves 1..7: rows per pass R (a multiple of the
+  // forward split), items per thread N; register pairs per block from r*
+  static constexpr int rpass(int na, int p) { return (NADAM / na) / p * p; }
   static constexpr int R1 = rpass(3 * U1, P1), R2 = rpass(3 * U2, P2), R3 = rpass(3 * U3, P3);
   static constexpr int R4 = rpass(3 * U4, P4), RK = rpass(F, PH);
   static constexpr int N1 = (F + R1 - 1) / R1, N2 = (U1 + R2 - 1) / R2, N3 = (U2 + R3 - 1) / R3;
   static constexpr int N4 = (U3 + R4 - 1) / R4, NK = (U4 + RK - 1) / RK;
-  static constexpr int NBIAS = 3 * (U1 + U2 + U3 + U4) + F;
-  static_assert(NBIAS <= NT, "one bias per thread");
-  static constexpr int NOWN = N1 + N2 + N3 + N4 + NK + 1;
+  static constexpr int r1 = 0, r2 = r1 + (N1 + 1) / 2, r3 = r2 + (N2 + 1) / 2, r4 = r3 + (N3 + 1) / 2;
+  static constexpr int rK = r4 + (N4 + 1) / 2, NOWN2 = rK + (NK + 1) / 2;
+  static_assert(R1 > 0 && R2 > 0 && R3 > 0 && R4 > 0 && RK > 0, "ownership split");
+  static_assert(3 * (U1 + U2 + U3 + U4) + F <= NADAM, "one bias per thread");
+  // the W blocks keep R * 3U = 384 of the 448 threads busy; rotated so the idle wave is
+  // wave 4, which shares a SIMD with the chain wave under round-robin placement
+  static constexpr int WROT = 3 * 64;
 };
 
 __device__ __forceinline__ void wave_order() { asm volatile("" ::: "memory"); }
+
+// LDS counters between the chain wave and the Adam waves
+__device__ __forceinline__ unsigned cnt_ld(const float* L, int i) {
+  return __hip_atomic_load(reinterpret_cast<const unsigned*>(L) + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void cnt_wait(const float* L, int i, unsigned target) {
+  while (cnt_ld(L, i) < target) __builtin_amdgcn_s_sleep(0);
+}
+// one lane bumps the counter after the wave's LDS writes (in-order LDS: no fence needed)
+__device__ __forceinline__ void cnt_bump(float* L, int i, int lane) {
+  wave_order();
+  if (lane == 0)
+    __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(L) + i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // sum of a lane value over the P = 64 / U lane groups of lane = j + U * part
 template <int U>
@@ -461,10 +495,15 @@ __device__ __forceinline__ void vec_rd(const float* v, float (&o)[N]) {
 template <int PC, int KPC>
 __device__ __forceinline__ int qpos(int e) { return (e % PC) * c4(KPC) + e / PC; }
 
+template <int ACT>
+__device__ __forceinline__ float act_f(float z) { return ACT == 2 ? tanh_fast(z) : fmaxf(z, 0.0f); }
+template <int ACT>
+__device__ __forceinline__ float act_d(float out) { return ACT == 2 ? 1.0f - out * out : (out > 0.0f ? 1.0f : 0.0f); }
+
 // forward of one LSTM unit from this lane's image (3 gates x KP inputs + bias slots)
-template <int KP, int U, int NW, int NI>
-__device__ __forceinline__ float fwd_unit(const float (&w)[NW], const float (&in)[NI], int act, int lane, float& ig,
-                                          float& gt, float& og, float& ac) {
+template <int KP, int U, int ACT, int NW, int NI>
+__device__ __forceinline__ float fwd_unit(const float (&w)[NW], const float (&in)[NI], int lane, float& ig, float& gt,
+                                          float& og, float& ac) {
   static_assert(NW == 3 * KP + 3 && NI >= KP, "image / input shapes");
   float zi = w[3 * KP], zg = w[3 * KP + 1], zo = w[3 * KP + 2];
 #pragma unroll
@@ -477,9 +516,9 @@ __device__ __forceinline__ float fwd_unit(const float (&w)[NW], const float (&in
   zg = part_sum<U>(zg, lane);
   zo = part_sum<U>(zo, lane);
   ig = sigm(zi);
-  gt = actf(act, zg);
+  gt = act_f<ACT>(zg);
   og = sigm(zo);
-  ac = actf(act, ig * gt);
+  ac = act_f<ACT>(ig * gt);
   return og * ac;
 }
 
@@ -516,18 +555,30 @@ __device__ __forceinline__ void put_dz(float* L, int nat, int q, int j, int part
 }
 
 // gate gradients of one unit from dh and the saved forward gates
-__device__ __forceinline__ void dz_unit(float dh, float ig, float gt, float og, float ac, int act, float& zi,
-                                        float& zg, float& zo) {
-  const float dc = dh * og * actd(act, ac);
+template <int ACT>
+__device__ __forceinline__ void dz_unit(float dh, float ig, float gt, float og, float ac, float& zi, float& zg,
+                                        float& zo) {
+  const float dc = dh * og * act_d<ACT>(ac);
   zi = dc * gt * ig * (1.0f - ig);
-  zg = dc * ig * actd(act, gt);
+  zg = dc * ig * act_d<ACT>(gt);
   zo = dh * ac * og * (1.0f - og);
 }
 
-// the whole chain of one Keras step at B = 1 (wave 0)
-template <typename G>
-__device__ __forceinline__ void chain_step(float* L, const float* xb, const float* yb, float* yp_out, int act,
-                                           int lane) {
+#ifdef SML_LREF_PROBE
+// the phase probe's clock marks (the kernel and the chain share pc / tq / tn)
+#define SML_PROBE_MARK(i) (tn = clock64(), pc[i] += tn - tq, tq = tn)
+#define SML_PROBE_ARGS , unsigned long long (&pc)[4], unsigned long long &tq, unsigned long long &tn
+#define SML_PROBE_PASS , pc, tq, tn
+#else
+#define SML_PROBE_MARK(i) ((void)0)
+#define SML_PROBE_ARGS
+#define SML_PROBE_PASS
+#endif
+
+// the whole chain of Keras step s at B = 1 (wave 0)
+template <typename G, int ACT>
+__device__ __forceinline__ void chain_step(float* L, const float* xb, const float* yb, int nat, float* yp_out,
+                                           unsigned step, int lane SML_PROBE_ARGS) {
   using Q = B1<G>;
   const int j1 = lane % G::U1, p1 = lane / G::U1, j2 = lane % G::U2, p2 = lane / G::U2;
   const int j3 = lane % G::U3, p3 = lane / G::U3, j4 = lane % G::U4, p4 = lane / G::U4;
@@ -536,28 +587,30 @@ __device__ __forceinline__ void chain_step(float* L, const float* xb, const floa
 #pragma unroll
   for (int i = 0; i < Q::KF1; ++i) x[i] = xb[p1 + Q::P1 * i];
   float w1[3 * Q::KF1 + 3], w2[3 * Q::KF2 + 3];
+  cnt_wait(L, Q::oCNT + 0, 7u * step);   // every Adam wave has applied step s - 1 (W1 is its last block)
+  SML_PROBE_MARK(1);
   img_rd(L, Q::sF1, lane, w1);
   img_rd(L, Q::sF2, lane, w2);
-  h = fwd_unit<Q::KF1, G::U1>(w1, x, act, lane, i1, g1, o1, a1);
-  put_h<Q, Q::P2, Q::KF2>(L, Q::oH1, Q::qH1, j1, p1, lane, h);
+  h = fwd_unit<Q::KF1, G::U1, ACT>(w1, x, lane, i1, g1, o1, a1);
+  put_h<Q, Q::P2, Q::KF2>(L, nat + Q::nH1, Q::qH1, j1, p1, lane, h);
 
   float w3[3 * Q::KF3 + 3], in2[c4(Q::KF2)];
   img_rd(L, Q::sF3, lane, w3);
   vec_rd(L + Q::qH1 + p2 * c4(Q::KF2), in2);
-  h = fwd_unit<Q::KF2, G::U2>(w2, in2, act, lane, i2, g2, o2, a2);
-  put_h<Q, Q::P3, Q::KF3>(L, Q::oH2, Q::qH2, j2, p2, lane, h);
+  h = fwd_unit<Q::KF2, G::U2, ACT>(w2, in2, lane, i2, g2, o2, a2);
+  put_h<Q, Q::P3, Q::KF3>(L, nat + Q::nH2, Q::qH2, j2, p2, lane, h);
 
   float w4[3 * Q::KF4 + 3], in3[c4(Q::KF3)];
   img_rd(L, Q::sF4, lane, w4);
   vec_rd(L + Q::qH2 + p3 * c4(Q::KF3), in3);
-  h = fwd_unit<Q::KF3, G::U3>(w3, in3, act, lane, i3, g3, o3, a3);
-  put_h<Q, Q::P4, Q::KF4>(L, Q::oH3, Q::qH3, j3, p3, lane, h);
+  h = fwd_unit<Q::KF3, G::U3, ACT>(w3, in3, lane, i3, g3, o3, a3);
+  put_h<Q, Q::P4, Q::KF4>(L, nat + Q::nH3, Q::qH3, j3, p3, lane, h);
 
   float wh[Q::KHD + 1], in4[c4(Q::KF4)];
   img_rd(L, Q::sHD, lane, wh);
   vec_rd(L + Q::qH3 + p4 * c4(Q::KF4), in4);
-  h = fwd_unit<Q::KF4, G::U4>(w4, in4, act, lane, i4, g4, o4, a4);
-  put_h<Q, Q::PH, Q::KHD>(L, Q::oH4, Q::qH4, j4, p4, lane, h);
+  h = fwd_unit<Q::KF4, G::U4, ACT>(w4, in4, lane, i4, g4, o4, a4);
+  put_h<Q, Q::PH, Q::KHD>(L, nat + Q::nH4, Q::qH4, j4, p4, lane, h);
 
   float wb4[Q::KB4];
   img_rd(L, Q::sB4, lane, wb4);
@@ -571,32 +624,38 @@ __device__ __forceinline__ void chain_step(float* L, const float* xb, const floa
     const float yp = acc + xor32(acc, lane);
     const float dy = (2.0f / (float)G::F) * (yp - yb[fc]);   // Keras MSE: mean over features
     const int sink = Q::oSINK + lane;
-    L[f >= G::F ? sink : (ph == 0 ? Q::oDY + f : Q::qDY + qpos<Q::P4, Q::KB4>(f))] = dy;
-    yp_out[f < G::F && ph == 0 ? f : sink - (int)(yp_out - L)] = yp;
+    L[f >= G::F ? sink : (ph == 0 ? nat + Q::nDY + f : Q::qDY + qpos<Q::P4, Q::KB4>(f))] = dy;
+    L[f < G::F && ph == 0 ? (int)(yp_out - L) + f : sink] = yp;
     wave_order();
   }
+  // stage 1: dY, h4 and the prediction are out and the head's backward image is read (wb4)
+  cnt_bump(L, Q::oCNT + 5, lane);
   float wb3[Q::KB3], up4[c4(Q::KB4)], zi, zg, zo;
   img_rd(L, Q::sB3, lane, wb3);
   vec_rd(L + Q::qDY + p4 * c4(Q::KB4), up4);
-  dz_unit(bwd_dh<Q::KB4, G::U4>(wb4, up4, lane), i4, g4, o4, a4, act, zi, zg, zo);
-  put_dz<Q, G::U4, Q::P3, Q::KB3, true>(L, Q::oZ4, Q::qZ4, j4, p4, lane, zi, zg, zo);
+  dz_unit<ACT>(bwd_dh<Q::KB4, G::U4>(wb4, up4, lane), i4, g4, o4, a4, zi, zg, zo);
+  put_dz<Q, G::U4, Q::P3, Q::KB3, true>(L, nat + Q::nZ4, Q::qZ4, j4, p4, lane, zi, zg, zo);
+  cnt_bump(L, Q::oCNT + 5, lane);   // stage: dz and the next layer's backward image read
 
   float wb2[Q::KB2], up3[c4(Q::KB3)];
   img_rd(L, Q::sB2, lane, wb2);
   vec_rd(L + Q::qZ4 + p3 * c4(Q::KB3), up3);
-  dz_unit(bwd_dh<Q::KB3, G::U3>(wb3, up3, lane), i3, g3, o3, a3, act, zi, zg, zo);
-  put_dz<Q, G::U3, Q::P2, Q::KB2, true>(L, Q::oZ3, Q::qZ3, j3, p3, lane, zi, zg, zo);
+  dz_unit<ACT>(bwd_dh<Q::KB3, G::U3>(wb3, up3, lane), i3, g3, o3, a3, zi, zg, zo);
+  put_dz<Q, G::U3, Q::P2, Q::KB2, true>(L, nat + Q::nZ3, Q::qZ3, j3, p3, lane, zi, zg, zo);
+  cnt_bump(L, Q::oCNT + 5, lane);   // stage: dz and the next layer's backward image read
 
   float wb1[Q::KB1], up2[c4(Q::KB2)];
   img_rd(L, Q::sB1, lane, wb1);
   vec_rd(L + Q::qZ3 + p2 * c4(Q::KB2), up2);
-  dz_unit(bwd_dh<Q::KB2, G::U2>(wb2, up2, lane), i2, g2, o2, a2, act, zi, zg, zo);
-  put_dz<Q, G::U2, Q::P1, Q::KB1, true>(L, Q::oZ2, Q::qZ2, j2, p2, lane, zi, zg, zo);
+  dz_unit<ACT>(bwd_dh<Q::KB2, G::U2>(wb2, up2, lane), i2, g2, o2, a2, zi, zg, zo);
+  put_dz<Q, G::U2, Q::P1, Q::KB1, true>(L, nat + Q::nZ2, Q::qZ2, j2, p2, lane, zi, zg, zo);
+  cnt_bump(L, Q::oCNT + 5, lane);   // stage: dz and the next layer's backward image read
 
   float up1[c4(Q::KB1)];
   vec_rd(L + Q::qZ2 + p1 * c4(Q::KB1), up1);
-  dz_unit(bwd_dh<Q::KB1, G::U1>(wb1, up1, lane), i1, g1, o1, a1, act, zi, zg, zo);
-  put_dz<Q, G::U1, 1, 1, false>(L, Q::oZ1, 0, j1, p1, lane, zi, zg, zo);
+  dz_unit<ACT>(bwd_dh<Q::KB1, G::U1>(wb1, up1, lane), i1, g1, o1, a1, zi, zg, zo);
+  put_dz<Q, G::U1, 1, 1, false>(L, nat + Q::nZ1, 0, j1, p1, lane, zi, zg, zo);
+  cnt_bump(L, Q::oCNT + 5, lane);   // stage 5: the chain of this step is complete
 }
 
 // loss and argmax accuracy of one step from its saved prediction and target rows (one wave)
@@ -625,123 +684,165 @@ __device__ __forceinline__ void step_stats(const float* yp, const float* yt, flo
 }
 
 // ---- Adam ownership of the batch-1 kernel ----
-// One weight block: rows K, columns NA, forward split P (rows per pass R).  Thread t owns
-// column n = t % NA and rows k0 + R * i (k0 = t / NA).  fwd(k0, n) / bwd(k0, n) give the
-// image addresses of row k0; row k0 + R * i sits FSTEP * i / BSTEP * i floats further.
 enum { B1_LOAD = 0, B1_STEP = 1, B1_STORE = 2 };
 
 struct AdamK {
   float b1, b2, c1, c2, eps, lr_t;
 };
-__device__ __forceinline__ void adam_item(float& p, float& m, float& v, float g, const AdamK& k) {
+__device__ __forceinline__ void adam_item(float& p, float& m, float& v, float g, const AdamK k) {
   m = k.b1 * m + k.c1 * g;
   v = k.b2 * v + k.c2 * g * g;
   p -= k.lr_t * m * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v) + k.eps);   // v_sqrt / v_rcp
 }
+// the same on a register pair (v_pk_mul / v_pk_fma / v_pk_add: two parameters per VALU op)
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void adam_pair(f2& p, f2& m, f2& v, f2 g, const AdamK k) {
+  m = k.b1 * m + k.c1 * g;
+  v = k.b2 * v + (k.c2 * g) * g;
+  f2 d = {__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
+  d += k.eps;
+  const f2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  p -= (k.lr_t * m) * r;
+}
 
+// one parameter (a bias): global offset, image slot, gradient
+__device__ __forceinline__ void own_one(int mode, float& p, float& m, float& v, const RefArgs& a, float* L,
+                                        int64_t gofs, int img, int dz, const AdamK ak) {
+  if (mode == B1_LOAD) {
+    p = a.flat[gofs];
+    m = a.m[gofs];
+    v = a.v[gofs];
+  } else if (mode == B1_STORE) {
+    a.flat[gofs] = p;
+    a.m[gofs] = m;
+    a.v[gofs] = v;
+  } else {
+    adam_item(p, m, v, L[dz], ak);
+  }
+  if (mode != B1_STORE) L[img] = p;
+}
+
+// One weight block: rows K, columns NA, rows per pass R.  Thread u owns column n = u % NA
+// and rows k0 + R * i (k0 = u / NA), i < NI, held as register pairs R0 .. R0 + (NI + 1) / 2;
+// fwd / bwd are the image addresses of row k0, row k0 + R * i sits fstep * i / bstep * i
+// floats further; `in` indexes input k0 (natural order).
 template <int MODE, int K, int NA, int R, int NI, int R0, int NR, bool BWD>
-__device__ __forceinline__ void own_w(float (&p)[NR], float (&mo)[NR], float (&vo)[NR], const RefArgs& a, float* L,
-                                      int t, int64_t gbase, int gstride, int gcol, int fwd, int fstep, int bwd,
-                                      int bstep, int in, int dz, const AdamK& ak) {
-  static_assert(R0 + NI <= NR, "ownership register budget");
-  if (t >= R * NA) return;
-  const int k0 = t / NA;
-  float dzn = 0.0f;
-  if (MODE == B1_STEP) dzn = L[dz];
+__device__ __forceinline__ void own_w(f2 (&p)[NR], f2 (&mo)[NR], f2 (&vo)[NR], const RefArgs& a, float* L, int u,
+                                      int64_t gbase, int gstride, int gcol, int fwd, int fstep, int bwd, int bstep,
+                                      int in, int dz, const AdamK ak) {
+  constexpr int NP = (NI + 1) / 2;
+  static_assert(R0 + NP <= NR, "ownership register budget");
+  if (u >= R * NA) return;
+  const int k0 = u / NA;
+  auto valid = [&](int i) { return i < NI && (K % R == 0 || i + 1 < NI || k0 + R * i < K); };
+  if (MODE == B1_STEP) {
+    // every LDS read of the block first: the image writes below may alias them as far as
+    // the compiler knows, and reads issued after a write would each pay a full round trip
+    const float dzn = L[dz];
+    float inv[2 * NP];
+#pragma unroll
+    for (int i = 0; i < 2 * NP; ++i) inv[i] = L[in + R * (valid(i) ? i : 0)];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const f2 g = {inv[2 * q] * dzn, inv[2 * q + 1] * dzn};
+      adam_pair(p[R0 + q], mo[R0 + q], vo[R0 + q], g, ak);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int k = k0 + R * i;
-    if ((K % R == 0 || i + 1 < NI) || k < K) {
-      const int64_t g = gbase + (int64_t)k * gstride + gcol;
+    if (valid(i)) {
+      const int64_t g = gbase + (int64_t)(k0 + R * i) * gstride + gcol;
+      f2 &pp = p[R0 + i / 2], &mm = mo[R0 + i / 2], &vv = vo[R0 + i / 2];
       if (MODE == B1_LOAD) {
-        p[R0 + i] = a.flat[g];
-        mo[R0 + i] = a.m[g];
-        vo[R0 + i] = a.v[g];
+        pp[i & 1] = a.flat[g];
+        mm[i & 1] = a.m[g];
+        vv[i & 1] = a.v[g];
       } else if (MODE == B1_STORE) {
-        a.flat[g] = p[R0 + i];
-        a.m[g] = mo[R0 + i];
-        a.v[g] = vo[R0 + i];
-      } else {
-        adam_item(p[R0 + i], mo[R0 + i], vo[R0 + i], L[in + R * i] * dzn, ak);
+        a.flat[g] = pp[i & 1];
+        a.m[g] = mm[i & 1];
+        a.v[g] = vv[i & 1];
       }
       if (MODE != B1_STORE) {
-        L[fwd + fstep * i] = p[R0 + i];
-        if (BWD) L[bwd + bstep * i] = p[R0 + i];
+        L[fwd + fstep * i] = pp[i & 1];
+        if (BWD) L[bwd + bstep * i] = pp[i & 1];
       }
     }
   }
 }
 
-template <int MODE, typename G, int NR>
-__device__ __forceinline__ void own_b1(float (&p)[NR], float (&mo)[NR], float (&vo)[NR], const RefArgs& a, float* L,
-                                       const float* xb, const AdamK& ak) {
+// Adam (or load / store) of the parameters a thread of waves 1..7 (t = thread - 64) owns in
+// block BLK (0..3: W1..W4 with their biases, 4: the head kernel and bias).
+// `x_in` / `nat`: LDS offsets of this step's input row and natural-order activations.
+template <int MODE, int BLK, typename G, int NR>
+__device__ __forceinline__ void own_blk(f2 (&p)[NR], f2 (&mo)[NR], f2 (&vo)[NR], float& pb, float& mb, float& vb,
+                                        const RefArgs& a, float* L, int x_in, int nat, const AdamK ak) {
   using Q = B1<G>;
-  const int t = threadIdx.x;
-  const int x_in = (int)(xb - L);
-  // W_L[k][n], n = gate * U + j (active columns i | g | o); Keras column col(n) of the 4U-wide kernel
+  const int t = (int)threadIdx.x - 64;
+  const int u = (t + Q::WROT) % NADAM;
+  // W_L[k][n], n = gate * U + j (active columns i | g | o); Keras column col(n) of the 4U-wide kernel.
   // forward image: lane j + U * (k % P), slot sF + 3 * (k / P) + gate
   // backward image (consumer: the layer below, U' = K units, P' = 64 / K): lane k + K * (n % P'), slot sB + n / P'
-#define SML_W_BLOCK(K_, U_, P_, R_, N_, R0_, SF, BW, SB, GW, IN, DZ)                                                 \
+  // bias b_L[n]: forward image lane j (part 0), slot sF + 3 * KP + gate; owned by thread t = BO + n of the
+  // group (the ranges within a group do not overlap: one register slot)
+#define SML_W_BLOCK(K_, U_, P_, KP_, R_, N_, R0_, SF, BW, SB, GW, GB_, BO, IN, DZ)                                    \
   {                                                                                                                  \
     constexpr int NA = 3 * U_, PB = 64 / K_;                                                                         \
-    const int n = t % NA, k0 = t / NA, gate = n / U_, j = n % U_;                                                    \
+    const int n = u % NA, k0 = u / NA, gate = n / U_, j = n % U_;                                                    \
     const int fwd = (SF + 3 * (k0 / P_) + gate) * 64 + j + U_ * (k0 % P_);                                           \
     const int bwd = BW ? (SB + n / PB) * 64 + k0 + K_ * (n % PB) : 0;                                                \
-    own_w<MODE, K_, NA, R_, N_, R0_, NR, BW>(p, mo, vo, a, L, t, GW, 4 * U_, n < U_ ? n : n + U_, fwd,               \
-                                             3 * (R_ / P_) * 64, bwd, R_, (IN) + k0, DZ + n, ak);                     \
+    own_w<MODE, K_, NA, R_, N_, R0_, NR, BW>(p, mo, vo, a, L, u, GW, 4 * U_, n < U_ ? n : n + U_, fwd,               \
+                                             3 * (R_ / P_) * 64, bwd, R_, (IN) + k0, nat + (DZ) + n, ak);             \
+    if (t >= BO && t < BO + NA) {                                                                                    \
+      const int e = t - BO, bg = e / U_, bj = e % U_;                                                                \
+      own_one(MODE, pb, mb, vb, a, L, GB_ + (e < U_ ? e : e + U_), (SF + 3 * KP_ + bg) * 64 + bj, nat + (DZ) + e,    \
+              ak);                                                                                                   \
+    }                                                                                                                \
   }
-  constexpr int r1 = 0, r2 = r1 + Q::N1, r3 = r2 + Q::N2, r4 = r3 + Q::N3, rk = r4 + Q::N4, rb = rk + Q::NK;
-  SML_W_BLOCK(G::F, G::U1, Q::P1, Q::R1, Q::N1, r1, Q::sF1, false, 0, G::gW1, x_in, Q::oZ1)
-  SML_W_BLOCK(G::U1, G::U2, Q::P2, Q::R2, Q::N2, r2, Q::sF2, true, Q::sB1, G::gW2, Q::oH1, Q::oZ2)
-  SML_W_BLOCK(G::U2, G::U3, Q::P3, Q::R3, Q::N3, r3, Q::sF3, true, Q::sB2, G::gW3, Q::oH2, Q::oZ3)
-  SML_W_BLOCK(G::U3, G::U4, Q::P4, Q::R4, Q::N4, r4, Q::sF4, true, Q::sB3, G::gW4, Q::oH3, Q::oZ4)
-#undef SML_W_BLOCK
-  {  // head kernel K[k][f]: forward lane f + 32 * (k % 2), slot sHD + k / 2; backward (D4) lane k + 32 * (f % 2), slot sB4 + f / 2
+  constexpr int bo1 = 0, bo2 = bo1 + 3 * G::U1, bo3 = bo2 + 3 * G::U2, bo4 = bo3 + 3 * G::U3, bok = bo4 + 3 * G::U4;
+  if constexpr (BLK == 0) {
+    SML_W_BLOCK(G::F, G::U1, Q::P1, Q::KF1, Q::R1, Q::N1, Q::r1, Q::sF1, false, 0, G::gW1, G::gb1, bo1, x_in, Q::nZ1)
+  } else if constexpr (BLK == 1) {
+    SML_W_BLOCK(G::U1, G::U2, Q::P2, Q::KF2, Q::R2, Q::N2, Q::r2, Q::sF2, true, Q::sB1, G::gW2, G::gb2, bo2,
+                nat + Q::nH1, Q::nZ2)
+  } else if constexpr (BLK == 2) {
+    SML_W_BLOCK(G::U2, G::U3, Q::P3, Q::KF3, Q::R3, Q::N3, Q::r3, Q::sF3, true, Q::sB2, G::gW3, G::gb3, bo3,
+                nat + Q::nH2, Q::nZ3)
+  } else if constexpr (BLK == 3) {
+    SML_W_BLOCK(G::U3, G::U4, Q::P4, Q::KF4, Q::R4, Q::N4, Q::r4, Q::sF4, true, Q::sB3, G::gW4, G::gb4, bo4,
+                nat + Q::nH3, Q::nZ4)
+  } else {
+    // head kernel K[k][f]: forward lane f + 32 * (k % 2), slot sHD + k / 2; backward (D4) lane k + 32 * (f % 2),
+    // slot sB4 + f / 2; head bias: forward lane f, slot sHD + KHD
     const int f = t % G::F, k0 = t / G::F;
     const int fwd = (Q::sHD + k0 / 2) * 64 + f + 32 * (k0 % 2);
     const int bwd = (Q::sB4 + f / Q::P4) * 64 + k0 + G::U4 * (f % Q::P4);
-    own_w<MODE, G::U4, G::F, Q::RK, Q::NK, rk, NR, true>(p, mo, vo, a, L, t, G::gK, G::F, f, fwd, (Q::RK / 2) * 64,
-                                                         bwd, Q::RK, Q::oH4 + k0, Q::oDY + f, ak);
+    own_w<MODE, G::U4, G::F, Q::RK, Q::NK, Q::rK, NR, true>(p, mo, vo, a, L, t, G::gK, G::F, f, fwd,
+                                                            (Q::RK / 2) * 64, bwd, Q::RK, nat + Q::nH4 + k0,
+                                                            nat + Q::nDY + f, ak);
+    if (t >= bok && t < bok + G::F)
+      own_one(MODE, pb, mb, vb, a, L, G::gkb + (t - bok), (Q::sHD + Q::KHD) * 64 + (t - bok), nat + Q::nDY + (t - bok),
+              ak);
   }
-  if (t < Q::NBIAS) {   // one bias per thread: b1 | b2 | b3 | b4 | head bias
-    int gofs, img, dz;
-    auto pick = [&](int e, int U, int sF, int KP, int gb, int oz) {
-      const int gate = e / U, j = e % U;
-      gofs = gb + (e < U ? e : e + U);
-      img = (sF + 3 * KP + gate) * 64 + j;
-      dz = oz + e;
-    };
-    constexpr int e1 = 3 * G::U1, e2 = e1 + 3 * G::U2, e3 = e2 + 3 * G::U3, e4 = e3 + 3 * G::U4;
-    if (t < e1) pick(t, G::U1, Q::sF1, Q::KF1, G::gb1, Q::oZ1);
-    else if (t < e2) pick(t - e1, G::U2, Q::sF2, Q::KF2, G::gb2, Q::oZ2);
-    else if (t < e3) pick(t - e2, G::U3, Q::sF3, Q::KF3, G::gb3, Q::oZ3);
-    else if (t < e4) pick(t - e3, G::U4, Q::sF4, Q::KF4, G::gb4, Q::oZ4);
-    else {
-      const int f = t - e4;
-      gofs = G::gkb + f;
-      img = (Q::sHD + Q::KHD) * 64 + f;
-      dz = Q::oDY + f;
-    }
-    if (MODE == B1_LOAD) {
-      p[rb] = a.flat[gofs];
-      mo[rb] = a.m[gofs];
-      vo[rb] = a.v[gofs];
-    } else if (MODE == B1_STORE) {
-      a.flat[gofs] = p[rb];
-      a.m[gofs] = mo[rb];
-      a.v[gofs] = vo[rb];
-    } else {
-      adam_item(p[rb], mo[rb], vo[rb], L[dz], ak);
-    }
-    if (MODE != B1_STORE) L[img] = p[rb];
-  }
+#undef SML_W_BLOCK
+}
+
+// load / store every owned parameter
+template <int MODE, typename G, int NR>
+__device__ __forceinline__ void own_all_b1(f2 (&p)[NR], f2 (&mo)[NR], f2 (&vo)[NR], float& pb, float& mb, float& vb,
+                                           const RefArgs& a, float* L, const AdamK ak) {
+  own_blk<MODE, 0, G>(p, mo, vo, pb, mb, vb, a, L, 0, 0, ak);
+  own_blk<MODE, 1, G>(p, mo, vo, pb, mb, vb, a, L, 0, 0, ak);
+  own_blk<MODE, 2, G>(p, mo, vo, pb, mb, vb, a, L, 0, 0, ak);
+  own_blk<MODE, 3, G>(p, mo, vo, pb, mb, vb, a, L, 0, 0, ak);
+  own_blk<MODE, 4, G>(p, mo, vo, pb, mb, vb, a, L, 0, 0, ak);
 }
 
 // Block `blk` of NB sample rows into row buffer blk & 1 by asynchronous global -> LDS
 // copies (global_load_lds_dword: LDS destination = M0 + 4 * lane, no registers held
 // while the rows are in flight).  Buffer layout: NB x rows of F floats, then NB y rows.
-// Issued from inline asm, so the compiler does not wait on it: the caller orders it with
-// an explicit `s_waitcnt vmcnt(0)` and a barrier before the block is read.
+// Issued from inline asm, so the compiler does not wait on it: the issuing wave orders it
+// with an explicit `s_waitcnt vmcnt(0)` before the block is read.  `w0 / wstep`: the waves
+// that share the chunks (all 8 for the first block, wave 0 alone afterwards).
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"  // m0 is deliberately clobbered (no other user here)
 __device__ __forceinline__ void glds4(const float* src, unsigned lds_addr) {
@@ -754,12 +855,12 @@ template <typename G>
 __device__ __forceinline__ float* row_block(float* L, int par) { return L + B1<G>::oROW + par * 2 * NB * G::F; }
 
 template <typename G>
-__device__ __forceinline__ void block_load(const RefArgs& a, float* L, int64_t blk) {
+__device__ __forceinline__ void block_load(const RefArgs& a, float* L, int64_t blk, int w0, int wstep) {
   static_assert((2 * NB * G::F) % 64 == 0, "whole wave chunks");
   constexpr int CHUNKS = 2 * NB * G::F / 64;
   const int lane = threadIdx.x & 63;
   float* buf = row_block<G>(L, (int)(blk & 1));
-  for (int c = threadIdx.x >> 6; c < CHUNKS; c += NT / 64) {
+  for (int c = w0; c < CHUNKS; c += wstep) {
     const int e = c * 64 + lane;
     const bool yrow = e >= NB * G::F;
     const int rem = yrow ? e - NB * G::F : e;
@@ -774,80 +875,102 @@ __device__ __forceinline__ void block_load(const RefArgs& a, float* L, int64_t b
 }
 
 #ifdef SML_LREF_PROBE
-// Phase probe (tools/lref_probe): shader-clock cycles summed over the steps of a launch,
-// measured by wave 0: [0] chain, [1] chain end -> past barrier 1, [2] Adam, [3] -> past
-// barrier 2, [4] steps.  Built only into the probe binary.
+// Phase probe (tools/lref_probe): shader-clock cycles summed over a launch.  Wave 0:
+// [0] chain compute, [1] chain waiting for the previous step's Adam; wave 1: [2] Adam busy,
+// [3] Adam waiting on the chain; [4] steps.  Built only into the probe binary.
 __device__ unsigned long long g_lref_probe[8];
 #endif
 
-template <typename G>
+template <typename G, int ACT>
 __global__ __launch_bounds__(NT) void lstm_ref_train_b1_kernel(RefArgs a) {
   extern __shared__ __attribute__((aligned(16))) float L[];
   using Q = B1<G>;
-  float p[Q::NOWN], mo[Q::NOWN], vo[Q::NOWN];
+  f2 p[Q::NOWN2], mo[Q::NOWN2], vo[Q::NOWN2];
+  float pb = 0.0f, mb = 0.0f, vb = 0.0f;   // the thread's bias (if any)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t it0 = *a.iter;
   for (int i = threadIdx.x; i < Q::NSLOT * 64; i += NT) L[i] = 0.0f;   // unused image slots stay 0
-  lds_barrier();
-  AdamK ak{a.beta1, a.beta2, 1.0f - a.beta1, 1.0f - a.beta2, a.eps, 0.0f};
-  own_b1<B1_LOAD, G>(p, mo, vo, a, L, row_block<G>(L, 0), ak);
+  if (threadIdx.x < 8) reinterpret_cast<unsigned*>(L)[Q::oCNT + threadIdx.x] = 0u;
   const int64_t avail = a.nrows - a.row0;
   const int total = (int)(avail < a.nsteps ? avail : a.nsteps);
-  block_load<G>(a, L, 0);
+  block_load<G>(a, L, 0, wave, NT / 64);
   wait_vm();
-  if (total > NB) block_load<G>(a, L, 1);
-  double b1t = pow((double)a.beta1, (double)it0), b2t = pow((double)a.beta2, (double)it0);
-  float* const yp_buf = L + Q::oYP;
+  lds_barrier();
+  const AdamK ak0{a.beta1, a.beta2, 1.0f - a.beta1, 1.0f - a.beta2, a.eps, 0.0f};
+  if (wave > 0) {
+#pragma unroll
+    for (int i = 0; i < Q::NOWN2; ++i) p[i] = mo[i] = vo[i] = f2{0.0f, 0.0f};
+    own_all_b1<B1_LOAD, G>(p, mo, vo, pb, mb, vb, a, L, ak0);
+  }
   lds_barrier();
 #ifdef SML_LREF_PROBE
   unsigned long long pc[4] = {0, 0, 0, 0}, tq = clock64(), tn;
-#define SML_PROBE_MARK(i) (tn = clock64(), pc[i] += tn - tq, tq = tn)
-#else
-#define SML_PROBE_MARK(i) ((void)0)
 #endif
-  for (int s = 0; s < total; ++s) {
-    const int slot = s % NB, par = (s / NB) & 1;
-    const float* xb = row_block<G>(L, par) + slot * G::F;
-    const float* yb = xb + NB * G::F;
-    b1t *= (double)a.beta1;
-    b2t *= (double)a.beta2;
-    if (wave == 0) {
-      chain_step<G>(L, xb, yb, yp_buf + (s & 1) * G::F, a.act, lane);
+  if (wave == 0) {
+    // ---- the chain ----
+    if (total > NB) block_load<G>(a, L, 1, 0, 1);
+    for (int s = 0; s < total; ++s) {
+      const int slot = s % NB, blk = s / NB;
+      if (slot == 0 && s > 0) wait_vm();   // this block was requested ~30 steps ago
+      const float* xb = row_block<G>(L, blk & 1) + slot * G::F;
+      chain_step<G, ACT>(L, xb, xb + NB * G::F, Q::oNAT + (s & 1) * Q::NATS, L + Q::oYP + (s & 1) * G::F,
+                         (unsigned)s, lane SML_PROBE_PASS);
+      // block b + 1 reuses block b - 1's buffer: by the end of step b * NB + 1 the chain's
+      // wait has seen every Adam wave finish step b * NB (so also step b * NB - 1, the
+      // buffer's last reader, and the stats of that step)
+      if (slot == 1 && blk > 0 && (blk + 1) * NB < total) block_load<G>(a, L, blk + 1, 0, 1);
       SML_PROBE_MARK(0);
-    } else if (wave == 1) {
-      if (lane == 0) L[Q::oLR] = (float)((double)a.lr * sqrt(1.0 - b2t) / (1.0 - b1t));
-      if (s > 0) {
-        const int sp = s - 1;
-        step_stats<G>(yp_buf + (sp & 1) * G::F, row_block<G>(L, (sp / NB) & 1) + (NB + sp % NB) * G::F,
-                      a.out + 2 * sp, lane);
-      }
     }
-    lds_barrier();
-    SML_PROBE_MARK(1);
-    ak.lr_t = L[Q::oLR];
-    own_b1<B1_STEP, G>(p, mo, vo, a, L, xb, ak);
-    SML_PROBE_MARK(2);
-    // block b + 1 was requested 32 steps ago: land it before the barrier that ends block b.
-    // Block b + 2 reuses block b's buffer once the stats of b's last step are out (slot 0).
-    if (slot == NB - 1) wait_vm();
-    if (slot == 0 && s > 0 && (s / NB + 1) * NB < total) block_load<G>(a, L, s / NB + 1);
-    lds_barrier();
-    SML_PROBE_MARK(3);
+  } else {
+    // ---- Adam, one step behind the chain ----
+    // Keras' lr_t = lr * sqrt(1 - beta2^t) / (1 - beta1^t), t = it0 + s + 1, in f32 closed form
+    // (no loop-carried power: a launch split in two computes the same values)
+    const float lg1 = __log2f(a.beta1), lg2 = __log2f(a.beta2);
+    for (int s = 0; s < total; ++s) {
+      const float t = (float)(it0 + s + 1);
+      const AdamK ak{ak0.b1, ak0.b2, ak0.c1, ak0.c2, ak0.eps,
+                     a.lr * __builtin_amdgcn_sqrtf(1.0f - exp2f(t * lg2)) / (1.0f - exp2f(t * lg1))};
+      const int slot = s % NB, blk = s / NB;
+      const float* xb = row_block<G>(L, blk & 1) + slot * G::F;
+      const int nat = Q::oNAT + (s & 1) * Q::NATS, xin = (int)(xb - L);
+      const unsigned st0 = 5u * (unsigned)s;   // the chain's stage count when step s starts
+      // each block as soon as the chain has produced its gradient (and read its old backward
+      // image); each finished block is counted for the next chain (oCNT + block)
+      SML_PROBE_MARK(2);
+      cnt_wait(L, Q::oCNT + 5, st0 + 1u);   // head done
+      SML_PROBE_MARK(3);
+      if (wave == 4) step_stats<G>(L + Q::oYP + (s & 1) * G::F, xb + NB * G::F, a.out + 2 * s, lane);
+      own_blk<B1_STEP, 4, G>(p, mo, vo, pb, mb, vb, a, L, xin, nat, ak);
+      SML_PROBE_MARK(2);
+      cnt_wait(L, Q::oCNT + 5, st0 + 2u);   // D4 done
+      SML_PROBE_MARK(3);
+      own_blk<B1_STEP, 3, G>(p, mo, vo, pb, mb, vb, a, L, xin, nat, ak);
+      SML_PROBE_MARK(2);
+      cnt_wait(L, Q::oCNT + 5, st0 + 3u);   // D3 done
+      SML_PROBE_MARK(3);
+      own_blk<B1_STEP, 2, G>(p, mo, vo, pb, mb, vb, a, L, xin, nat, ak);
+      SML_PROBE_MARK(2);
+      cnt_wait(L, Q::oCNT + 5, st0 + 4u);   // D2 done
+      SML_PROBE_MARK(3);
+      own_blk<B1_STEP, 1, G>(p, mo, vo, pb, mb, vb, a, L, xin, nat, ak);
+      SML_PROBE_MARK(2);
+      cnt_wait(L, Q::oCNT + 5, st0 + 5u);   // D1 done: the chain of step s is complete
+      SML_PROBE_MARK(3);
+      own_blk<B1_STEP, 0, G>(p, mo, vo, pb, mb, vb, a, L, xin, nat, ak);
+      cnt_bump(L, Q::oCNT + 0, lane);       // step s fully applied (W1 is every wave's last block)
+      SML_PROBE_MARK(2);
+    }
   }
+  SML_PROBE_MARK(wave == 0 ? 0 : 2);
 #ifdef SML_LREF_PROBE
-  if (threadIdx.x == 0) {
+  if (lane == 0 && wave <= 1) {
     for (int i = 0; i < 4; ++i) atomicAdd(&g_lref_probe[i], pc[i]);
-    atomicAdd(&g_lref_probe[4], (unsigned long long)total);
+    if (wave == 0) atomicAdd(&g_lref_probe[4], (unsigned long long)total);
   }
 #endif
-#undef SML_PROBE_MARK
-  if (total > 0 && wave == 1) {
-    const int sp = total - 1;
-    step_stats<G>(yp_buf + (sp & 1) * G::F, row_block<G>(L, (sp / NB) & 1) + (NB + sp % NB) * G::F, a.out + 2 * sp,
-                  lane);
-  }
   wait_vm();   // no copy may still target LDS when the workgroup ends
-  own_b1<B1_STORE, G>(p, mo, vo, a, L, nullptr, ak);
+  lds_barrier();
+  if (wave > 0) own_all_b1<B1_STORE, G>(p, mo, vo, pb, mb, vb, a, L, ak0);
   if (threadIdx.x == 0) *a.iter = it0 + (total > 0 ? total : 0);
 }
 
@@ -872,7 +995,7 @@ hipError_t lstm_ref_train_launch(float* flat, float* m, float* v, int64_t* iter,
                                  hipStream_t stream) {
   if (B < 1 || B > MAXB || nsteps < 1 || row0 < 0 || row0 >= nrows) return hipErrorInvalidValue;
   RefArgs a{flat, m, v, iter, x, y, ldx, ldy, order, nrows, row0, B, nsteps, act, lr, beta1, beta2, eps, out};
-  auto k = B == 1 ? lstm_ref_train_b1_kernel<Ref> : lstm_ref_train_kernel<Ref>;
+  auto k = B > 1 ? lstm_ref_train_kernel<Ref> : act == 2 ? lstm_ref_train_b1_kernel<Ref, 2> : lstm_ref_train_b1_kernel<Ref, 1>;
   const size_t lds = sizeof(float) * (B == 1 ? B1<Ref>::LDS_FLOATS : Ref::LDS_FLOATS);
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),

@@ -68,7 +68,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost));
   const double n = pr[4] ? (double)pr[4] : 1.0, tot = (double)(pr[0] + pr[1] + pr[2] + pr[3]);
   std::printf("{\"us_per_step\": %.4f, \"steps\": %d, \"launches\": %d, \"cycles_per_step\": %.1f, "
-              "\"chain\": %.1f, \"barrier1\": %.1f, \"adam\": %.1f, \"barrier2\": %.1f, \"last_loss\": %.6f}\n",
+              "\"chain_busy\": %.1f, \"chain_wait\": %.1f, \"adam_busy\": %.1f, \"adam_wait\": %.1f, \"last_loss\": %.6f}\n",
               ms * 1e3 / (steps * launches), steps, launches, tot / n, pr[0] / n, pr[1] / n, pr[2] / n, pr[3] / n,
               out[2 * (steps - 1)]);
   return 0;
