@@ -23,6 +23,8 @@
 //
 // Exit conditions every wave reaches: the host's stop flag or `idle` without a request
 // (decided by wave 0, broadcast through LDS at the next barrier).
+#include <cstdlib>
+
 #include "sml_common.h"
 #include "sml_ops.h"
 #include "sml_serve_dev.h"
@@ -170,8 +172,12 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
     float* hist = a.hist + (int64_t)key * T * D;
     float* lastp = a.lastpred + (int64_t)key * D;
     // events of this key before this one: read once, broadcast, so every wave takes the same
-    // branches (the stack below has barriers)
+    // branches (the stack below has barriers).  The key's previous forecast is read in the
+    // same round trip (used only once the key has T events), not after the count.
+    float prev = 0.f;
     if (tid == 0) S.ctl[2] = ld_agent(&a.hcount[key]);
+    if (tid >= 64 && tid < 64 + D) prev = ld_agent(&lastp[tid - 64]);
+    if (tid >= 64 && tid < 64 + D) S.pred[tid - 64] = prev;   // parked until the count is known
     __syncthreads();
     const int cnt = S.ctl[2];
     const bool full = cnt + 1 >= T;
@@ -181,7 +187,7 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
       const float xn = S.xrow[tid];
       st_agent(&hist[(cnt % T) * D + tid], xn);
       if (cnt >= T) {
-        const float d = xn - ld_agent(&lastp[tid]);
+        const float d = xn - S.pred[tid];
         err = d * d;
       }
     }
@@ -248,7 +254,10 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
           if (tid < U) {
             float acc = S.w[L.boff + tid];
             const float* xin = cur + (tcur - 1) * MAXW;
-            for (int k = 0; k < dim; ++k) acc = fmaf(xin[k], S.w[L.woff + k * U + tid], acc);
+            // unrolled to the widest input: every LDS read is issued before the FMA chain
+#pragma unroll
+            for (int k = 0; k < MAXW; ++k)
+              if (k < dim) acc = fmaf(xin[k], S.w[L.woff + k * U + tid], acc);
             nxt[(tcur - 1) * MAXW + tid] = acc;
             if (l == a.nl - 1) S.pred[tid] = acc;
           }
@@ -291,6 +300,207 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
   if (tid == 0) st_sys32(&a.ctl->alive, 0u);
 }
 
+
+// ===================================================================================
+// The reference stack at look_back 1 (LSTM-TensorFlow-IO-Kafka/cardata-v2.py:172-209:
+// LSTM 32 -> LSTM 16 -> RepeatVector(1) -> LSTM 16 -> LSTM 32 -> TimeDistributed(Dense 18)).
+// With a one-event window every LSTM runs one step from h0 = c0 = 0, so only the i, g~, o
+// columns of each kernel matter and the whole forecast is a nine-stage chain of small dot
+// products.  ONE wave does all of it, with every weight it multiplies held in registers
+// for the kernel's life: lane l = j + U * part owns unit j of a U-unit layer and every
+// P-th input (P = 64 / U); the partial sums meet through permlane swaps, and a layer's
+// output passes to the next through LDS (one wave: no barrier, LDS operations complete in
+// order), written part-major so the consumer's inputs are 16-byte reads.  The key's event
+// count and previous forecast are requested right after the request is picked up and are
+// first needed after the chain, so their global round trip hides under it.
+// ===================================================================================
+constexpr int R1F = 18, R1U1 = 32, R1U2 = 16, R1U3 = 16, R1U4 = 32;
+
+template <int U>
+__device__ __forceinline__ float r1_part_sum(float v, int lane) {
+  if (U == 16) v += xor16(v, lane);
+  return v + xor32(v, lane);
+}
+template <int RELU>
+__device__ __forceinline__ float r1_act(float z) { return RELU ? fmaxf(z, 0.f) : tanh_fast(z); }
+
+// this lane's weights of one LSTM layer (K inputs, U units): w[3i + g] = W[k = part + P i][gate g],
+// gates i | g~ | o (Keras columns 0, 2U, 3U), then the 3 biases (part 0; 0 elsewhere)
+template <int K, int U, int NW>
+__device__ __forceinline__ void r1_load_lstm(const float* wts, const LstmServeLayer& L, int lane, float (&w)[NW]) {
+  constexpr int P = 64 / U, KP = K / P;
+  static_assert(NW == 3 * KP + 3 && K % P == 0, "image shape");
+  const int j = lane % U, part = lane / U;
+#pragma unroll
+  for (int i = 0; i < KP; ++i) {
+    const int k = part + P * i;
+    w[3 * i + 0] = wts[L.woff + k * 4 * U + j];
+    w[3 * i + 1] = wts[L.woff + k * 4 * U + 2 * U + j];
+    w[3 * i + 2] = wts[L.woff + k * 4 * U + 3 * U + j];
+  }
+  w[3 * KP + 0] = part == 0 ? wts[L.boff + j] : 0.f;
+  w[3 * KP + 1] = part == 0 ? wts[L.boff + 2 * U + j] : 0.f;
+  w[3 * KP + 2] = part == 0 ? wts[L.boff + 3 * U + j] : 0.f;
+}
+
+template <int KP, int U, int RELU, int NW, int NI>
+__device__ __forceinline__ float r1_unit(const float (&w)[NW], const float (&in)[NI], int lane) {
+  float zi = w[3 * KP], zg = w[3 * KP + 1], zo = w[3 * KP + 2];
+#pragma unroll
+  for (int i = 0; i < KP; ++i) {
+    zi = fmaf(in[i], w[3 * i], zi);
+    zg = fmaf(in[i], w[3 * i + 1], zg);
+    zo = fmaf(in[i], w[3 * i + 2], zo);
+  }
+  zi = r1_part_sum<U>(zi, lane);
+  zg = r1_part_sum<U>(zg, lane);
+  zo = r1_part_sum<U>(zo, lane);
+  return sigm(zo) * r1_act<RELU>(sigm(zi) * r1_act<RELU>(zg));   // c = i * g~ (c0 = 0), h = o * act(c)
+}
+
+// h[j] of part-0 lanes into the consumer's part-major copy (PC parts of KPC), others to the sink
+template <int PC, int KPC>
+__device__ __forceinline__ void r1_put(float* q, float* sink, int j, int part, int lane, float h) {
+  constexpr int RUN = (KPC + 3) & ~3;
+  float* dst = part == 0 ? q + (j % PC) * RUN + j / PC : sink + lane;
+  *dst = h;
+  asm volatile("" ::: "memory");
+}
+template <int N>
+__device__ __forceinline__ void r1_vec(const float* v, float (&o)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; i += 4) {
+    const float4 t = *reinterpret_cast<const float4*>(v + i);
+    o[i] = t.x;
+    o[i + 1] = t.y;
+    o[i + 2] = t.z;
+    o[i + 3] = t.w;
+  }
+}
+
+template <int RELU>
+__global__ __launch_bounds__(64) void lstm_serve_ref1_kernel(LstmServeArgs a) {
+  constexpr int P1 = 64 / R1U1, P2 = 64 / R1U2, P3 = 64 / R1U3, P4 = 64 / R1U4;
+  constexpr int K1 = R1F / P1, K2 = R1U1 / P2, K3 = R1U2 / P3, K4 = R1U3 / P4, KH = R1U4 / 2;
+  __shared__ __attribute__((aligned(16))) float xrow[32], q1[64], q2[64], q3[64], q4[64], sink[64], sc[32], sh[32];
+  const int lane = threadIdx.x;
+  const int D = a.D;
+  sc[lane & 31] = ((lane & 31) < D && a.scale) ? a.scale[lane & 31] : 1.f;
+  sh[lane & 31] = ((lane & 31) < D && a.shift) ? a.shift[lane & 31] : 0.f;
+  // every weight this lane multiplies, for the kernel's life (~120 registers)
+  float w1[3 * K1 + 3], w2[3 * K2 + 3], w3[3 * K3 + 3], w4[3 * K4 + 3], wh[KH + 1];
+  r1_load_lstm<R1F, R1U1>(a.wts, a.L[0], lane, w1);
+  r1_load_lstm<R1U1, R1U2>(a.wts, a.L[1], lane, w2);
+  r1_load_lstm<R1U2, R1U3>(a.wts, a.L[3], lane, w3);
+  r1_load_lstm<R1U3, R1U4>(a.wts, a.L[4], lane, w4);
+  {  // head: lane f + 32 * part, k = part + 2 i
+    const int f = lane & 31, part = lane >> 5;
+    const LstmServeLayer& H = a.L[5];
+#pragma unroll
+    for (int i = 0; i < KH; ++i) wh[i] = f < R1F ? a.wts[H.woff + (part + 2 * i) * R1F + f] : 0.f;
+    wh[KH] = (f < R1F && part == 0) ? a.wts[H.boff + f] : 0.f;
+  }
+  const int j1 = lane % R1U1, p1 = lane / R1U1, j2 = lane % R1U2, p2 = lane / R1U2;
+  const int j3 = lane % R1U3, p3 = lane / R1U3, j4 = lane % R1U4, p4 = lane / R1U4;
+  __syncthreads();
+
+  uint64_t tail = ld_sys(&a.ctl->done);
+  uint64_t last = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) st_sys32(&a.ctl->alive, 1u);
+  for (;;) {
+    const int slot = (int)(tail % (uint64_t)a.nslots);
+    const uint32_t want = (uint32_t)(tail + 1);
+    bool quit = false;
+    uint32_t keyw = 0;
+    uint64_t t_seen = 0;
+    {
+      const uint64_t* wp = &a.req[slot].w[lane & 31];
+      for (uint32_t it = 0;; ++it) {
+        const uint64_t w = ld_sys(wp);
+        const bool ok = (lane >= D && lane != KEY_WORD) || lane >= 32 || (uint32_t)(w >> 32) == want;
+        if (__ballot(ok) == ~0ull) {
+          t_seen = __builtin_amdgcn_s_memrealtime();
+          if (lane < D) xrow[lane] = fmaf(__uint_as_float((uint32_t)w), sc[lane], sh[lane]);
+          keyw = (uint32_t)__shfl((int)(uint32_t)w, KEY_WORD);
+          break;
+        }
+        if ((it & 63) == 63 &&
+            (ld_sys32(&a.ctl->stop) || __builtin_amdgcn_s_memrealtime() - last > a.idle_ticks)) {
+          quit = true;
+          break;
+        }
+      }
+    }
+    if (quit) break;
+    int key = (int)keyw;
+    key = key < 0 ? 0 : (key >= a.nkeys ? a.nkeys - 1 : key);   // the host validates; never leave the table
+    // the key's state: requested now, first used after the chain
+    const int cnt = ld_agent(&a.hcount[key]);
+    const float prev = lane < D ? ld_agent(&a.lastpred[(int64_t)key * D + lane]) : 0.f;
+    asm volatile("" ::: "memory");
+    // ---------------- the chain
+    float x[K1];
+#pragma unroll
+    for (int i = 0; i < K1; ++i) x[i] = xrow[p1 + P1 * i];
+    r1_put<P2, K2>(q1, sink, j1, p1, lane, r1_unit<K1, R1U1, RELU>(w1, x, lane));
+    float in2[(K2 + 3) & ~3];
+    r1_vec(q1 + p2 * ((K2 + 3) & ~3), in2);
+    r1_put<P3, K3>(q2, sink, j2, p2, lane, r1_unit<K2, R1U2, RELU>(w2, in2, lane));
+    float in3[(K3 + 3) & ~3];
+    r1_vec(q2 + p3 * ((K3 + 3) & ~3), in3);
+    r1_put<P4, K4>(q3, sink, j3, p3, lane, r1_unit<K3, R1U3, RELU>(w3, in3, lane));
+    float in4[(K4 + 3) & ~3];
+    r1_vec(q3 + p4 * ((K4 + 3) & ~3), in4);
+    r1_put<2, KH>(q4, sink, j4, p4, lane, r1_unit<K4, R1U4, RELU>(w4, in4, lane));
+    float inh[KH];
+    r1_vec(q4 + (lane >> 5) * ((KH + 3) & ~3), inh);
+    float acc = wh[KH];
+#pragma unroll
+    for (int i = 0; i < KH; ++i) acc = fmaf(inh[i], wh[i], acc);
+    const float pred = acc + xor32(acc, lane);   // lanes f < D (either half) hold forecast f
+    const uint64_t t_comp = __builtin_amdgcn_s_memrealtime();
+    // ---------------- score against the previous forecast, results, the key's state
+    float err = 0.f;
+    if (lane < D && cnt >= 1) {
+      const float d = xrow[lane] - prev;
+      err = d * d;
+    }
+    err = wave_sum(err);
+    ServeResult* r = a.res + slot;
+    if (lane < D) {
+      st_sys(&r->w[lane], tagged(want, pred));
+      st_agent(&a.lastpred[(int64_t)key * D + lane], pred);
+      st_agent(&a.hist[(int64_t)key * a.T * D + lane], xrow[lane]);
+    }
+    if (lane == 0) {
+      const float score = cnt >= 1 ? err / (float)D : __builtin_nanf("");
+      const uint32_t flag = cnt >= 1 ? (score > a.threshold ? 1u : 0u) : 2u;
+      st_agent(&a.hcount[key], cnt + 1);
+      st_sys(&r->w[kServeScore], tagged(want, score));
+      st_sys(&r->w[kServeFlag], tagged_u(want, flag));
+      st_sys(&r->w[kServeTLoad], tagged_u(want, 0u));
+      st_sys(&r->w[kServeTComp], tagged_u(want, (uint32_t)(t_comp - t_seen)));
+      st_sys(&r->w[kServeTDone], tagged_u(want, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seen)));
+      st_sys(&a.ctl->done, tail + 1);
+    }
+    tail += 1;
+    last = __builtin_amdgcn_s_memrealtime();
+  }
+  wait_stores();
+  if (lane == 0) st_sys32(&a.ctl->alive, 0u);
+}
+
+// the launch arguments describe exactly the reference stack at look_back 1
+bool lstm_serve_is_ref1(const LstmServeArgs& x) {
+  if (x.T != 1 || x.D != R1F || x.nl != 6) return false;
+  const LstmServeLayer* L = x.L;
+  const bool shape = L[0].kind == LS_LSTM && L[0].in == R1F && L[0].u == R1U1 && L[1].kind == LS_LSTM &&
+                     L[1].in == R1U1 && L[1].u == R1U2 && L[1].ret == 0 && L[2].kind == LS_REPEAT && L[2].n == 1 &&
+                     L[3].kind == LS_LSTM && L[3].in == R1U2 && L[3].u == R1U3 && L[4].kind == LS_LSTM &&
+                     L[4].in == R1U3 && L[4].u == R1U4 && L[5].kind == LS_DENSE && L[5].in == R1U4 && L[5].u == R1F;
+  const int act = L[0].act;
+  return shape && (act == ACT_RELU || act == ACT_TANH) && L[1].act == act && L[3].act == act && L[4].act == act;
+}
 }  // namespace
 
 size_t lstm_serve_lds_bytes(int nw) {
@@ -321,6 +531,14 @@ hipError_t lstm_serve_launch(const LstmServeArgs& args, hipStream_t stream) {
     }
   }
   if (args.L[args.nl - 1].kind != LS_DENSE || dim != args.D) return hipErrorInvalidValue;
+  // the reference stack at look_back 1 takes the one-wave register-resident path, unless
+  // SML_LSTM_SERVE_GENERIC=1 asks for the general kernel (A/B and cross-checks)
+  const char* gen = getenv("SML_LSTM_SERVE_GENERIC");
+  if (lstm_serve_is_ref1(args) && !(gen && gen[0] == '1')) {
+    auto k = args.L[0].act == ACT_RELU ? lstm_serve_ref1_kernel<1> : lstm_serve_ref1_kernel<0>;
+    hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, stream, args);
+    return hipGetLastError();
+  }
   const size_t lds = lstm_serve_lds_bytes(args.nw);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 65536) {
