@@ -130,6 +130,35 @@ def measure_infer(model, device, n_events: int, repeats: int = 3, qps: float = 1
             "host_overhead_p50_us": float(np.median(p50s)) - float(np.median([r["device_p50_us"] for r in runs]))}
 
 
+def measure_lstm_infer(device, n_events: int, repeats: int = 3, qps: float = 10000.0, nkeys: int = 100):
+    """Per-event forecast latency (us) of the persistent LSTM forecaster on the reference stack
+    at look_back 1 (LSTM-TensorFlow-IO-Kafka/cardata-v2.py:220-273 streams one prediction per
+    event): each event of a car key -> its next-event forecast, the score against the key's
+    previous forecast and the flag back on the host, offered one at a time at ``qps``."""
+    import numpy as np
+
+    from streamml.data.cardata import synthetic_device_tensor
+    from streamml.models.lstm import LSTMPredictor
+    from streamml.ops.serve import LSTMScoringServer
+
+    ev = synthetic_device_tensor(n_events + 1000, device, seed=7).cpu().numpy()
+    keys = np.arange(n_events + 1000) % nkeys
+    model = LSTMPredictor.reference(look_back=1, device=device)
+    runs = []
+    with LSTMScoringServer(model, nkeys=nkeys) as srv:
+        srv.latency_us(ev[:1000], keys[:1000], qps=qps)
+        for _ in range(repeats):
+            host, done, comp = srv.latency_us(ev[1000:], keys[1000:], qps=qps, device_breakdown=True)
+            runs.append({"p50_us": float(np.percentile(host, 50)), "p99_us": float(np.percentile(host, 99)),
+                         "device_p50_us": float(np.percentile(done, 50)),
+                         "device_compute_p50_us": float(np.percentile(comp, 50))})
+    p50s = [r["p50_us"] for r in runs]
+    return {"p50_us": float(np.median(p50s)), "p99_us": max(r["p99_us"] for r in runs),
+            "p50_spread_us": [min(p50s), max(p50s)], "runs": runs, "events_per_run": n_events, "offered_qps": qps,
+            "keys": nkeys, "model": "reference LSTM stack, look_back 1",
+            "path": "persistent one-wave forecaster (lstm_serve.hip), host-mapped request ring"}
+
+
 def measure_kafka_e2e(model, device, n_events: int, qps: float = 10000.0):
     """Kafka append -> scored result record acknowledged, through ``serve --low-latency``
     (bench/bench_infer.py:kafka_e2e): p50/p99 and the per-stage breakdown."""
@@ -539,6 +568,9 @@ def main():
         lstm = guarded(from_b.measure_seq, batch=65536, seq_len=50, steps=args.lstm_steps, warmup=3, device=device)
         lstm_ref = guarded(from_b.measure_reference, batch=1, epochs=5, steps_per_epoch=1000, autograd_steps=100,
                            device=device)
+    lstm_infer = None
+    if rank == 0 and args.infer_events > 0 and args.lstm_steps > 0:
+        lstm_infer = guarded(measure_lstm_infer, device, args.infer_events, args.infer_repeats, args.qps)
     rows_per_s = gb * args.steps / elapsed
     if rank == 0:
         p50s = [r.get("p50_us") for r in per_rank_infer if isinstance(r, dict)]
@@ -597,6 +629,9 @@ def main():
             "lstm_seq50": lstm,
             "lstm_ref_us_per_step": None if not lstm_ref or "error" in lstm_ref else lstm_ref["value"],
             "lstm_ref": lstm_ref,
+            "lstm_infer_p50_us": None if not lstm_infer or "error" in lstm_infer else lstm_infer["p50_us"],
+            "lstm_infer_p99_us": None if not lstm_infer or "error" in lstm_infer else lstm_infer["p99_us"],
+            "lstm_infer": lstm_infer,
         }
         print(json.dumps(out), flush=True)
     dp.barrier(device)   # every rank leaves together (rank 0's side measurements run alone)
