@@ -10,10 +10,11 @@
 // every thread owns a fixed set of (parameter, Adam m, Adam v) in registers and is the
 // only writer of those parameters.
 //
-// Two kernels share that ownership scheme.  At batch 1 (the reference's setting,
-// `lstm_ref_train_b1_kernel`, further down) the chain of nine layers runs on ONE wave with
-// no workgroup barrier inside it, and a step has two barriers.  For batches 2..32
-// (`lstm_ref_train_kernel`) each step is 10 barrier-separated phases:
+// Two kernels.  At batch 1 (the reference's setting, `lstm_ref_train_b1_kernel`, further
+// down, with its own design note) wave 0 runs the chain of nine layers alone and waves
+// 1..7 run Adam under it, synchronised by LDS counters: no workgroup barrier in the step
+// loop.  For batches 2..32 (`lstm_ref_train_kernel`) each step is 10 barrier-separated
+// phases:
 //     F1-F4   LSTM layer forward  (task = (row, unit): three gate dot products, gate
 //             math, c, h; i, g~, o, c saved for backward)
 //     D0      head + loss          (wave per row: Dense(18), MSE gradient, loss and
