@@ -368,7 +368,8 @@ __global__ __launch_bounds__(NT) void lstm_ref_train_kernel(RefArgs a) {
 // that reads it afterwards.  The gates a lane computes in the forward pass stay in its
 // registers for the backward pass of the same layer (same j mapping).
 //   * Weights come from per-lane IMAGES: for every layer each lane finds exactly the
-//     weights it multiplies, slot-major (slot s of lane l at s * 64 + l: conflict-free,
+//     weights it multiplies, slot-major (slot s of lane l at s * 64 + l, backward slots in
+//     padded, shifted rows -- B1::img; conflict-free,
 //     paired into ds_read2st64).  A weight has a forward image (the lane that uses it in
 //     its layer's dot product) and, for W2..W4 and the head kernel, a backward image (the
 //     lane that uses it in dh of the layer below).  A layer's image is requested one
@@ -416,12 +417,24 @@ struct B1 {
   static constexpr int sF1 = 0, sF2 = sF1 + 3 * KF1 + 3, sF3 = sF2 + 3 * KF2 + 3, sF4 = sF3 + 3 * KF3 + 3;
   static constexpr int sHD = sF4 + 3 * KF4 + 3, sB4 = sHD + KHD + 1, sB3 = sB4 + KB4, sB2 = sB3 + KB3;
   static constexpr int sB1 = sB2 + KB2, NSLOT = sB1 + KB1;
+  // The backward images (slots sB4 .. NSLOT) are written by Adam threads whose lanes walk
+  // the OTHER index (lane' = k + K * (n % P') with n running across the wave): in a plain
+  // 64-float slot row those writes fall on 2-4 banks.  Each backward slot row is therefore
+  // BROW floats long and shifted by (slot & 31): a lane's address stays slot-affine (the
+  // chain's reads keep compile-time offsets), and Adam's writes spread over the banks.
+  static constexpr int BROW = 96;
+  static constexpr int NSLOTF = sB4;                               // forward slots, 64-float rows
+  static constexpr int IMG_FLOATS = NSLOTF * 64 + (NSLOT - NSLOTF) * BROW;
+  // float offset of (slot, lane) in the images
+  static constexpr __host__ __device__ int img(int slot, int lane) {
+    return slot < NSLOTF ? slot * 64 + lane : NSLOTF * 64 + (slot - NSLOTF) * BROW + ((slot - NSLOTF) & 31) + lane;
+  }
   // natural-order activations of one step (Adam's inputs), double-buffered by step parity
   static constexpr int nH1 = 0, nH2 = nH1 + U1, nH3 = nH2 + U2, nH4 = nH3 + U3;
   static constexpr int nZ1 = nH4 + U4, nZ2 = nZ1 + 3 * U1, nZ3 = nZ2 + 3 * U2, nZ4 = nZ3 + 3 * U3;
   static constexpr int nDY = nZ4 + 3 * U4, NATS = c4(nDY + F);
   // LDS map (floats)
-  static constexpr int oROW = NSLOT * 64;                        // 2 blocks x [NB x rows | NB y rows]
+  static constexpr int oROW = IMG_FLOATS;                        // 2 blocks x [NB x rows | NB y rows]
   static constexpr int oNAT = oROW + 4 * NB * F;                 // 2 x NATS
   // part-major copies for the consuming layer (each part's run 16-byte aligned)
   static constexpr int qH1 = oNAT + 2 * NATS, qH2 = qH1 + P2 * c4(KF2), qH3 = qH2 + P3 * c4(KF3);
@@ -471,12 +484,12 @@ __device__ __forceinline__ float part_sum(float v, int lane) {
   return v + xor32(v, lane);
 }
 
-// N consecutive image slots of this lane from slot s0 (slot-major: stride 64 floats)
-template <int N>
-__device__ __forceinline__ void img_rd(const float* L, int s0, int lane, float (&w)[N]) {
-  const float* b = L + s0 * 64 + lane;
+// N consecutive image slots of this lane from slot S0 (slot-major; Bq::img places them)
+template <typename Bq, int S0, int N>
+__device__ __forceinline__ void img_rd(const float* L, int lane, float (&w)[N]) {
+  const float* b = L + lane;
 #pragma unroll
-  for (int i = 0; i < N; ++i) w[i] = b[i * 64];
+  for (int i = 0; i < N; ++i) w[i] = b[Bq::img(S0 + i, 0)];
 }
 // N floats (N % 4 == 0) of a 16-byte aligned LDS run
 template <int N>
@@ -590,31 +603,31 @@ __device__ __forceinline__ void chain_step(float* L, const float* xb, const floa
   float w1[3 * Q::KF1 + 3], w2[3 * Q::KF2 + 3];
   cnt_wait(L, Q::oCNT + 0, 7u * step);   // every Adam wave has applied step s - 1 (W1 is its last block)
   SML_PROBE_MARK(1);
-  img_rd(L, Q::sF1, lane, w1);
-  img_rd(L, Q::sF2, lane, w2);
+  img_rd<Q, Q::sF1>(L, lane, w1);
+  img_rd<Q, Q::sF2>(L, lane, w2);
   h = fwd_unit<Q::KF1, G::U1, ACT>(w1, x, lane, i1, g1, o1, a1);
   put_h<Q, Q::P2, Q::KF2>(L, nat + Q::nH1, Q::qH1, j1, p1, lane, h);
 
   float w3[3 * Q::KF3 + 3], in2[c4(Q::KF2)];
-  img_rd(L, Q::sF3, lane, w3);
+  img_rd<Q, Q::sF3>(L, lane, w3);
   vec_rd(L + Q::qH1 + p2 * c4(Q::KF2), in2);
   h = fwd_unit<Q::KF2, G::U2, ACT>(w2, in2, lane, i2, g2, o2, a2);
   put_h<Q, Q::P3, Q::KF3>(L, nat + Q::nH2, Q::qH2, j2, p2, lane, h);
 
   float w4[3 * Q::KF4 + 3], in3[c4(Q::KF3)];
-  img_rd(L, Q::sF4, lane, w4);
+  img_rd<Q, Q::sF4>(L, lane, w4);
   vec_rd(L + Q::qH2 + p3 * c4(Q::KF3), in3);
   h = fwd_unit<Q::KF3, G::U3, ACT>(w3, in3, lane, i3, g3, o3, a3);
   put_h<Q, Q::P4, Q::KF4>(L, nat + Q::nH3, Q::qH3, j3, p3, lane, h);
 
   float wh[Q::KHD + 1], in4[c4(Q::KF4)];
-  img_rd(L, Q::sHD, lane, wh);
+  img_rd<Q, Q::sHD>(L, lane, wh);
   vec_rd(L + Q::qH3 + p4 * c4(Q::KF4), in4);
   h = fwd_unit<Q::KF4, G::U4, ACT>(w4, in4, lane, i4, g4, o4, a4);
   put_h<Q, Q::PH, Q::KHD>(L, nat + Q::nH4, Q::qH4, j4, p4, lane, h);
 
   float wb4[Q::KB4];
-  img_rd(L, Q::sB4, lane, wb4);
+  img_rd<Q, Q::sB4>(L, lane, wb4);
   {  // TimeDistributed(Dense(F)) + the MSE gradient: lane = f + 32 * part
     const int f = lane & 31, ph = lane >> 5, fc = f < G::F ? f : G::F - 1;
     float inh[c4(Q::KHD)];
@@ -632,21 +645,21 @@ __device__ __forceinline__ void chain_step(float* L, const float* xb, const floa
   // stage 1: dY, h4 and the prediction are out and the head's backward image is read (wb4)
   cnt_bump(L, Q::oCNT + 5, lane);
   float wb3[Q::KB3], up4[c4(Q::KB4)], zi, zg, zo;
-  img_rd(L, Q::sB3, lane, wb3);
+  img_rd<Q, Q::sB3>(L, lane, wb3);
   vec_rd(L + Q::qDY + p4 * c4(Q::KB4), up4);
   dz_unit<ACT>(bwd_dh<Q::KB4, G::U4>(wb4, up4, lane), i4, g4, o4, a4, zi, zg, zo);
   put_dz<Q, G::U4, Q::P3, Q::KB3, true>(L, nat + Q::nZ4, Q::qZ4, j4, p4, lane, zi, zg, zo);
   cnt_bump(L, Q::oCNT + 5, lane);   // stage: dz and the next layer's backward image read
 
   float wb2[Q::KB2], up3[c4(Q::KB3)];
-  img_rd(L, Q::sB2, lane, wb2);
+  img_rd<Q, Q::sB2>(L, lane, wb2);
   vec_rd(L + Q::qZ4 + p3 * c4(Q::KB3), up3);
   dz_unit<ACT>(bwd_dh<Q::KB3, G::U3>(wb3, up3, lane), i3, g3, o3, a3, zi, zg, zo);
   put_dz<Q, G::U3, Q::P2, Q::KB2, true>(L, nat + Q::nZ3, Q::qZ3, j3, p3, lane, zi, zg, zo);
   cnt_bump(L, Q::oCNT + 5, lane);   // stage: dz and the next layer's backward image read
 
   float wb1[Q::KB1], up2[c4(Q::KB2)];
-  img_rd(L, Q::sB1, lane, wb1);
+  img_rd<Q, Q::sB1>(L, lane, wb1);
   vec_rd(L + Q::qZ3 + p2 * c4(Q::KB2), up2);
   dz_unit<ACT>(bwd_dh<Q::KB2, G::U2>(wb2, up2, lane), i2, g2, o2, a2, zi, zg, zo);
   put_dz<Q, G::U2, Q::P1, Q::KB1, true>(L, nat + Q::nZ2, Q::qZ2, j2, p2, lane, zi, zg, zo);
@@ -790,7 +803,7 @@ __device__ __forceinline__ void own_blk(f2 (&p)[NR], f2 (&mo)[NR], f2 (&vo)[NR],
     constexpr int NA = 3 * U_, PB = 64 / K_;                                                                         \
     const int n = u % NA, k0 = u / NA, gate = n / U_, j = n % U_;                                                    \
     const int fwd = (SF + 3 * (k0 / P_) + gate) * 64 + j + U_ * (k0 % P_);                                           \
-    const int bwd = BW ? (SB + n / PB) * 64 + k0 + K_ * (n % PB) : 0;                                                \
+    const int bwd = BW ? Q::img(SB + n / PB, k0 + K_ * (n % PB)) : 0;                                              \
     own_w<MODE, K_, NA, R_, N_, R0_, NR, BW>(p, mo, vo, a, L, u, GW, 4 * U_, n < U_ ? n : n + U_, fwd,               \
                                              3 * (R_ / P_) * 64, bwd, R_, (IN) + k0, nat + (DZ) + n, ak);             \
     if (t >= BO && t < BO + NA) {                                                                                    \
@@ -816,7 +829,7 @@ __device__ __forceinline__ void own_blk(f2 (&p)[NR], f2 (&mo)[NR], f2 (&vo)[NR],
     // slot sB4 + f / 2; head bias: forward lane f, slot sHD + KHD
     const int f = t % G::F, k0 = t / G::F;
     const int fwd = (Q::sHD + k0 / 2) * 64 + f + 32 * (k0 % 2);
-    const int bwd = (Q::sB4 + f / Q::P4) * 64 + k0 + G::U4 * (f % Q::P4);
+    const int bwd = Q::img(Q::sB4 + f / Q::P4, k0 + G::U4 * (f % Q::P4));
     own_w<MODE, G::U4, G::F, Q::RK, Q::NK, Q::rK, NR, true>(p, mo, vo, a, L, t, G::gK, G::F, f, fwd,
                                                             (Q::RK / 2) * 64, bwd, Q::RK, nat + Q::nH4 + k0,
                                                             nat + Q::nDY + f, ak);
@@ -890,7 +903,7 @@ __global__ __launch_bounds__(NT) void lstm_ref_train_b1_kernel(RefArgs a) {
   float pb = 0.0f, mb = 0.0f, vb = 0.0f;   // the thread's bias (if any)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t it0 = *a.iter;
-  for (int i = threadIdx.x; i < Q::NSLOT * 64; i += NT) L[i] = 0.0f;   // unused image slots stay 0
+  for (int i = threadIdx.x; i < Q::IMG_FLOATS; i += NT) L[i] = 0.0f;   // unused image slots stay 0
   if (threadIdx.x < 8) reinterpret_cast<unsigned*>(L)[Q::oCNT + threadIdx.x] = 0u;
   const int64_t avail = a.nrows - a.row0;
   const int total = (int)(avail < a.nsteps ? avail : a.nsteps);
