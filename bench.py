@@ -292,7 +292,7 @@ def measure_stream_e2e(device, rows, batch=100):
                                           dp="none")   # rank 0 alone, as measure_fit
 
 
-def measure_fit_large_batch(data, device, batch, epochs=10, shuffle=False, seed=0):
+def measure_fit_large_batch(data, device, batch, epochs=10, shuffle=False, seed=0, settle_ms=100.0):
     """The throughput engine through the real entry point: ``Autoencoder.fit(x, batch_size=B,
     engine="throughput")`` on the HBM-resident rows, every batch on the headline kernel.
     Unshuffled, the tile-packed ring is built once per dataset and reused across epochs and
@@ -304,9 +304,16 @@ def measure_fit_large_batch(data, device, batch, epochs=10, shuffle=False, seed=
     from streamml.models.autoencoder import Autoencoder
     m = Autoencoder(device=device, input_normalizer="cardata", seed=seed)
     m.compile()
-    m.fit(data, epochs=Autoencoder.PACK_MIN_PASSES, batch_size=batch, shuffle=shuffle, verbose=0, engine="throughput",
-          dp="none")  # warm
-    torch.cuda.synchronize()
+    # warm: builds the packed ring, then keeps fitting until settle_ms of load have passed --
+    # the same clock settle the headline gets (a GPU that was just idle, e.g. after the
+    # latency measurements, runs its first ~40 train dispatches ~10 % slower; profiles/r03)
+    ts = time.perf_counter()
+    while True:
+        m.fit(data, epochs=Autoencoder.PACK_MIN_PASSES, batch_size=batch, shuffle=shuffle, verbose=0,
+              engine="throughput", dp="none")
+        torch.cuda.synchronize()
+        if (time.perf_counter() - ts) * 1e3 >= settle_ms:
+            break
     t0 = time.perf_counter()
     h = m.fit(data, epochs=epochs, batch_size=batch, shuffle=shuffle, verbose=0, engine="throughput", dp="none",
               initial_epoch=0)
@@ -551,7 +558,7 @@ def main():
                               group=p2p) if p2p is not None else {"error": f"P2P exchange unavailable: {p2p_err!r}"})
     fit_large = fresh = None
     if rank == 0 and args.fit_epochs > 0:
-        fit_large = guarded(measure_fit_large_batch, data, device, B, epochs=args.fit_epochs)
+        fit_large = guarded(measure_fit_large_batch, data, device, B, epochs=args.fit_epochs, settle_ms=args.settle_ms)
         fit_large["shuffled"] = guarded(measure_fit_large_batch, data, device, B, epochs=max(args.fit_epochs // 2, 1),
                                         shuffle=True)
     if rank == 0 and args.fresh_steps > 0:

@@ -464,7 +464,11 @@ class FusedAE:
 
     def read_metrics(self) -> dict:
         """Epoch metrics in Keras terms from the device accumulators (one host sync)."""
-        sq, ab, corr, rows = [float(v) for v in self.metrics.cpu().tolist()]
+        return self.metrics_from(self.metrics.cpu())
+
+    def metrics_from(self, acc) -> dict:
+        """Keras metrics from a host copy of the 4 accumulators (sum sq err, sum |h1|, correct, rows)."""
+        sq, ab, corr, rows = [float(v) for v in acc.tolist()]
         D = self.spec.input_dim
         rows = max(rows, 1.0)
         loss = (sq / D + self.spec.activity_l1 * ab) / rows
