@@ -121,3 +121,29 @@ def test_cli_persistent_predict_matches_window_predict(cuda_device, stack, T):
     want = want.reshape(len(want), -1, 18)[:, -1]
     assert got.shape == want.shape == (take, 18)
     np.testing.assert_allclose(got, want, rtol=0, atol=3e-2)
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh"])
+def test_ref1_kernel_matches_general_kernel(cuda_device, monkeypatch, act):
+    """The reference stack at look_back 1 runs on the one-wave register-resident kernel by
+    default; SML_LSTM_SERVE_GENERIC=1 forces the general 4-wave kernel.  Both must give the
+    same forecasts, scores and flags on the same interleaved event stream (fp32, different
+    summation orders)."""
+    from streamml.models.lstm import REFERENCE_STACK
+    from streamml.ops.serve import LSTMScoringServer
+    stack = [tuple(act if v == "relu" else v for v in layer) for layer in REFERENCE_STACK]
+    m = LSTMPredictor(look_back=1, stack=stack, device=cuda_device, seed=11)
+    rng = np.random.default_rng(5)
+    n, nkeys = 400, 9
+    keys = rng.integers(0, nkeys, size=n)
+    raw = rng.uniform(0, 40, size=(n, 18)).astype(np.float32)
+    out = {}
+    for generic in ("0", "1"):
+        monkeypatch.setenv("SML_LSTM_SERVE_GENERIC", generic)
+        with LSTMScoringServer(m, nkeys=nkeys, threshold=0.05) as srv:
+            out[generic] = srv.forecast(raw, keys)
+    (pa, sa, fa), (pb, sb, fb) = out["0"], out["1"]
+    np.testing.assert_allclose(pa, pb, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(sa, sb, rtol=1e-4, atol=1e-6, equal_nan=True)
+    agree = (fa == fb) | (np.abs(sa - 0.05) < 1e-4)   # a score within rounding of the threshold may flip
+    assert agree.all()
