@@ -37,7 +37,9 @@
 //            0.4-0.5 us per step, profiles/r03).
 //   barrier
 // Two barriers per step (the round-1 version had eight, one per layer phase, and did
-// every dot product on the VALU: 12 us per batch-100 step).
+// every dot product on the VALU: 12 us per batch-100 step).  At batch 32 (two row waves)
+// ae_minibatch_pipe_kernel below replaces the barriers with LDS stage counters and runs the
+// tile gradients + Adam of W2-W4 under the backward pass.
 //
 // Fleet mode: a grid of M workgroups trains M independent models at once (per-device
 // digital-twin models, ensembles, learning-rate sweeps), one per workgroup, each with
@@ -133,9 +135,12 @@ struct Smem {   // MB 48: ~47 KB, MB 128: ~108 KB
   float dz3[MB * HS], dz2[MB * HS], dz1[MB * HS];
   float y[MB * XS];                     // reconstructions (phase-B argmax accuracy)
   float one[4];                         // constant 1 (bias-row activation), dummy store slot
-  float red[3][NT / 64];
+  float red[3][16];                     // per-wave partial metrics (<= 16 waves)
   int abort;                            // DP: a gradient exchange timed out (all waves stop)
   int stream_end;                       // streaming: no further full batch (all waves stop)
+  unsigned cnt[8];                      // pipelined build: stage counters (CE1.., CU1..)
+  int stream_last;                      // pipelined build, streaming: index of the last step (INT_MAX: open)
+  int first_ok;                         // pipelined build, streaming: the first batch arrived (1)
 };
 
 // logical feature of K-step s for lane group g (the C/D register order of the producer)
@@ -249,6 +254,47 @@ __device__ __forceinline__ f32x4 layer16(const float* frag, const float* bias, i
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc = mfma4(frag[s * 64 + lane], h[s], acc);
   return acc;
+}
+
+// Categorical accuracy of row r: argmax of y and x, ties -> lowest feature (1 or 0).  The
+// row's 20 first (logical) features come in as five 16-byte reads per array; logical block
+// jl sits at physical block jl ^ (swz(r) / 4) of its 16-column half.
+template <int KD>
+__device__ __forceinline__ float row_correct(const float* y, const float* x, int r, int D) {
+  const int sb = swz(r) >> 2;
+  const float* yr = y + r * XS;
+  const float* xq = x + r * XS;
+  f32x4 yb[5], xb[5];
+#pragma unroll
+  for (int jl = 0; jl < 5; ++jl) {
+    const int pj = jl < 4 ? (jl ^ sb) : 4 + sb;
+    yb[jl] = ld4(yr + 4 * pj);
+    xb[jl] = ld4(xq + 4 * pj);
+  }
+  float by = yb[0][0], bx = xb[0][0];
+  int iy = 0, ix = 0;
+#pragma unroll
+  for (int f = 1; f < (KD < 20 ? KD : 20); ++f) {   // branch-free selects, increasing f
+    const float yv = yb[f >> 2][f & 3], xw = xb[f >> 2][f & 3];
+    const bool gy = f < D && yv > by, gx = f < D && xw > bx;
+    by = gy ? yv : by;
+    iy = gy ? f : iy;
+    bx = gx ? xw : bx;
+    ix = gx ? f : ix;
+  }
+  if constexpr (KD > 20) {   // wide inputs: the remaining features one by one
+#pragma unroll
+    for (int f = 20; f < KD; ++f) {
+      const int pf = f ^ swz(r);
+      const float yv = yr[pf], xw = xq[pf];
+      const bool gy = f < D && yv > by, gx = f < D && xw > bx;
+      by = gy ? yv : by;
+      iy = gy ? f : iy;
+      bx = gx ? xw : bx;
+      ix = gx ? f : ix;
+    }
+  }
+  return iy == ix ? 1.f : 0.f;
 }
 
 // KD: compiled input width class (<= 18 -> 6 K-steps, 32 -> 8); TB: batch (0 = runtime);
@@ -593,44 +639,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         S.w[bpos[i]] = wo[i];
       }
     } else if (a.want_acc && t - 6 * 64 < B) {
-      // categorical accuracy (waves 6-7, one row per lane): argmax of y and x, ties -> lowest
-      // feature.  The row's 20 first (logical) features come in as five 16-byte reads per
-      // array; logical block jl sits at physical block jl ^ (swz(r) / 4) of its 16-column half.
-      const int r = t - 6 * 64;
-      const int sb = swz(r) >> 2;
-      const float* yr = S.y + r * XS;
-      const float* xq = S.x + r * XS;
-      f32x4 yb[5], xb[5];
-#pragma unroll
-      for (int jl = 0; jl < 5; ++jl) {
-        const int pj = jl < 4 ? (jl ^ sb) : 4 + sb;
-        yb[jl] = ld4(yr + 4 * pj);
-        xb[jl] = ld4(xq + 4 * pj);
-      }
-      float by = yb[0][0], bx = xb[0][0];
-      int iy = 0, ix = 0;
-#pragma unroll
-      for (int f = 1; f < (KD < 20 ? KD : 20); ++f) {   // branch-free selects, increasing f
-        const float yv = yb[f >> 2][f & 3], xw = xb[f >> 2][f & 3];
-        const bool gy = f < D && yv > by, gx = f < D && xw > bx;
-        by = gy ? yv : by;
-        iy = gy ? f : iy;
-        bx = gx ? xw : bx;
-        ix = gx ? f : ix;
-      }
-      if constexpr (KD > 20) {   // wide inputs: the remaining features one by one
-#pragma unroll
-        for (int f = 20; f < KD; ++f) {
-          const int pf = f ^ swz(r);
-          const float yv = yr[pf], xw = xq[pf];
-          const bool gy = f < D && yv > by, gx = f < D && xw > bx;
-          by = gy ? yv : by;
-          iy = gy ? f : iy;
-          bx = gx ? xw : bx;
-          ix = gx ? f : ix;
-        }
-      }
-      corr += iy == ix ? 1.f : 0.f;
+      // categorical accuracy (waves 6-7, one row per lane)
+      corr += row_correct<KD>(S.y, S.x, t - 6 * 64, D);
     }
     mark(2);
     lds_barrier();
@@ -703,6 +713,352 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Pipelined Keras batch-32 build (reference activations, <= 18 inputs, one replica per
+// workgroup; resident ring or streaming epoch).  At batch 32 only waves 0-1 own rows, so the other six waves
+// own the six parameter tiles and the two barriers per step become LDS stage counters:
+//   row waves   forward, then the backward, bumping E_l as soon as layer l's activation and
+//               upstream gradient are stored and its backward fragment has been read (E4
+//               after dz3, E3 after dz2, E2 after dz1 is computed, E1 once dz1 is stored);
+//               before layer l's forward of the next step they wait for U_l.
+//   tile waves  wait for E_l, contract act^T . dz over the 32 rows, Adam, write the forward /
+//               backward fragments, bump U_l.
+// W4's, W3's and W2's gradients and updates run under the rest of the backward pass; only
+// W1's (its gradient is produced last and the next forward needs it first) stays between two
+// steps.  Every LDS buffer a row wave writes in step s+1 is written after its U waits, i.e.
+// after the tile waves of step s have read it.  Placement under round-robin wave -> SIMD
+// assignment: rows on waves 0-1 (SIMDs 0-1); W1's tiles on waves 4-5 (the same SIMDs: they
+// run while the row waves wait for them); the tiles that overlap the backward pass on waves
+// 2, 3, 6, 7 (SIMDs 2-3).  Wave 6 also takes the accuracy of the 32 rows before it bumps U4.
+// LDS operations of one wave complete in order, so a counter bump after a wave's stores (or
+// after the reads whose values it has consumed) needs no fence; only the compiler is fenced.
+enum { CE1 = 0, CE2, CE3, CE4, CU1, CU2, CU3, CU4 };
+// SLEEP: s_sleep argument of the poll loop -- 0 for the row waves (their waits are on the
+// critical path), 1 for the tile waves, whose polls would otherwise take issue slots and LDS
+// cycles from the row waves sharing their SIMDs
+template <int SLEEP = 0>
+__device__ __forceinline__ void pcnt_wait(const unsigned* p, unsigned target) {
+  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(SLEEP);
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void pcnt_bump(unsigned* p, int lane) {
+  asm volatile("" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wave -> parameter tile (-1: row wave): rows on waves 0-1, W1 on 4-5, W2 2, W3 3, W4 6-7;
+// tile -> layer (1-based)
+__device__ __forceinline__ int pipe_tile(int wave) { return wave < 2 ? -1 : wave < 4 ? wave : wave < 6 ? wave - 4 : wave - 2; }
+__device__ __forceinline__ int tile_layer(int tile) { return tile <= 1 ? 1 : tile <= 3 ? tile : 4; }
+
+// Batch 32 only.  The same scheme at cardata-v3's batch 100 (7 row waves + 6 tile waves in a
+// 13-wave workgroup) measured 23.3 vs 27.3 M rows/s for the two-barrier kernel (profiles/r03/s3):
+// there every SIMD already carries row waves, and the tile waves' work and polls slow the chain.
+template <int PACK, int TB>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae_minibatch_pipe_kernel(MBArgs a0) {
+  static_assert(TB == 32, "pipelined build: two row waves + six tile waves");
+  constexpr int KD = 18, KSX = 6, NS = TB / 4;
+  constexpr int NRW = 2, NWV = 8;
+  constexpr int MB = MB_SMALL;
+  static_assert(((PACK & 3) != ACT_SIGMOID) && (((PACK >> 2) & 3) != ACT_SIGMOID) &&
+                (((PACK >> 4) & 3) != ACT_SIGMOID) && (((PACK >> 6) & 3) != ACT_SIGMOID),
+                "act(0) == 0 keeps padded features zero (no masks in this build)");
+  using Smem = ::Smem<MB>;
+  extern __shared__ __attribute__((aligned(16))) float smem_raw[];
+  MBArgs a = a0;
+  {
+    const int mdl = blockIdx.x;
+    a.x += mdl * a.xmodel;
+    if (a.ragged) {
+      const int64_t* rg = a.ragged + 3 * mdl;
+      a.x += rg[0] * a.ld;
+      a.ring = rg[1];
+      a.nsteps = (int)rg[2];
+    }
+    a.params += mdl * NPARAM;
+    a.m += mdl * NPARAM;
+    a.v += mdl * NPARAM;
+    a.iter += mdl;
+    if (a.cursor) a.cursor += mdl;
+    if (a.metrics) a.metrics += 4 * mdl;
+    if (a.lrs) a.lr = a.lrs[mdl];
+  }
+  Smem& S = *reinterpret_cast<Smem*>(smem_raw);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  constexpr int B = TB;
+  const int D = a.D;
+  constexpr int a1 = PACK & 3, a2 = (PACK >> 2) & 3, a3 = (PACK >> 4) & 3, a4 = (PACK >> 6) & 3;
+  const float* sbase = smem_raw;
+
+  for (int e = t; e < W_END; e += 64 * NWV) S.w[e] = 0.f;
+  if (t < 8) S.cnt[t] = 0u;
+  __syncthreads();
+
+  const int tile = pipe_tile(wave);
+  const bool has_tile = tile >= 0;
+  const Tile T = make_tile(has_tile ? tile : 0, c, g, S, sbase);
+  float mo[4], vo[4], wo[4];
+  int fpos[4], bpos[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = T.slot(i);
+    mo[i] = has_tile ? a.m[p] : 0.f;
+    vo[i] = has_tile ? a.v[p] : 0.f;
+    wo[i] = has_tile ? a.params[p] : 0.f;
+    lds_slots(p, fpos[i], bpos[i], (int)(S.one + 1 - S.w));
+    if (has_tile) {
+      S.w[fpos[i]] = wo[i];
+      S.w[bpos[i]] = wo[i];
+    }
+  }
+  if (t == 0) S.one[0] = 1.f;
+
+  const bool has_rows = wave < NRW;
+  const int row_l = 16 * wave + c;
+  const bool row_ok = row_l < B;   // (always, at batch 32)
+  const float rowf = row_ok ? 1.f : 0.f, l1r = row_ok ? a.l1 : 0.f;
+  float sc[KSX], sh[KSX];
+  bool fok[KSX];
+#pragma unroll
+  for (int s = 0; s < KSX; ++s) {
+    const int f = feat(s, g);
+    fok[s] = f < D;
+    sc[s] = fok[s] ? (a.scale ? a.scale[f] : 1.f) : 0.f;
+    sh[s] = (fok[s] && a.scale) ? a.shift[f] : 0.f;
+  }
+  int64_t cur = a.cursor ? a.cursor[0] : 0;
+  auto advance = [&](int64_t c0) { c0 += B; return c0 >= a.ring ? c0 - a.ring : c0; };
+  float xr[KSX];
+  auto fetch = [&](int64_t c0) {
+    const float* rp = a.x + (c0 + (row_ok ? row_l : 0)) * a.ld;
+#pragma unroll
+    for (int s = 0; s < KSX; ++s) xr[s] = __builtin_nontemporal_load(rp + (fok[s] ? feat(s, g) : 0));
+  };
+  // Streaming epoch (see MBArgs): thread 0 decides whether the first batch arrived; each row
+  // wave then polls for the batch after next at the start of a step, and a wave that finds the
+  // stream over writes this step's index to stream_last before its E bumps of the step, so
+  // every wave reads it after the counter waits that follow those bumps (LDS operations are
+  // performed in one order per CU, each wave's in program order).
+  const bool stream = a.sr_avail != nullptr;
+  int64_t avail = 0;
+  if (t == 0) {
+    S.stream_last = 0x7fffffff;
+    S.first_ok = stream ? stream_wait(a, (int64_t)B, avail) : 1;
+    if (S.first_ok < 0) __hip_atomic_store(a.sr_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  const int nsteps = S.first_ok == 1 ? a.nsteps : 0;
+  if (has_rows && nsteps) fetch(cur);
+  int64_t nxt = advance(cur);
+  const int64_t cur0 = cur;
+  int done = nsteps;
+
+  float sq = 0.f, ab = 0.f, corr = 0.f;
+  const float two_over_d = 2.0f / (float)D;
+  const int64_t it0 = a.iter[0];
+  __syncthreads();
+
+  if (has_rows) {
+    for (int step = 0; step < nsteps; ++step) {
+      const unsigned st = (unsigned)step;
+      // W1 (two tiles) of the previous step is in the fragments.  A resident ring waits after
+      // issuing the next rows' loads; a stream must first learn whether this step exists.
+      if (stream && step) pcnt_wait(S.cnt + CU1, 2u * st);
+      if (stream) {
+        if (S.stream_last < step) {   // another row wave found the stream over last step
+          done = step;
+          break;
+        }
+        if (wave == 0 && lane == 0 && step && (step & 7) == 0)   // rows of steps < step are in registers
+          __hip_atomic_store(a.sr_consumed, (int64_t)step * B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      float xv[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) xv[s] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KSX; ++s) xv[s] = (row_ok && fok[s]) ? fmaf(xr[s], sc[s], sh[s]) : 0.f;
+      if (step + 1 < nsteps) {   // next step's rows: in flight across this step
+        int more = 1;
+        if (stream) {
+          more = stream_wait(a, (int64_t)(step + 2) * B, avail);
+          if (more != 1 && lane == 0) {
+            S.stream_last = step;
+            if (more < 0) __hip_atomic_store(a.sr_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
+        if (more == 1) {
+          fetch(nxt);
+          cur = nxt;
+          nxt = advance(cur);
+        } else {
+          done = step + 1;   // this step is the last
+        }
+      }
+      if (!stream && step) pcnt_wait(S.cnt + CU1, 2u * st);
+      f32x4 z1 = ld4(S.w + BB1 + 4 * g);
+#pragma unroll
+      for (int s = 0; s < KSX; ++s) z1 = mfma4(S.w[F1 + s * 64 + lane], xv[s], z1);
+      f32x4 h1, h2, h3;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        h1[i] = act_fwd(a1, z1[i]);
+        ab = fmaf(fabsf(h1[i]), rowf, ab);
+      }
+      if (step) pcnt_wait(S.cnt + CU2, st);
+      const f32x4 z2 = layer16(S.w + F2, S.w + BB2, lane, g, h1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h2[i] = act_fwd(a2, z2[i]);
+      if (step) pcnt_wait(S.cnt + CU3, st);
+      const f32x4 z3 = layer16(S.w + F3, S.w + BB3, lane, g, h2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h3[i] = act_fwd(a3, z3[i]);
+      if (step) pcnt_wait(S.cnt + CU4, 2u * st);   // also: the accuracy of the previous step is read
+      f32x4 y[2], dz4[2];
+#pragma unroll
+      for (int t4 = 0; t4 < 2; ++t4) {
+        f32x4 acc = ld4(S.w + BB4 + 16 * t4 + 4 * g);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma4(S.w[F4 + (4 * t4 + s) * 64 + lane], h3[s], acc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int f = 16 * t4 + 4 * g + i;
+          const float yy = act_fwd(a4, acc[i]);   // padded features: act(0) = 0
+          const float e = row_ok ? yy - xv[4 * t4 + i] : 0.f;
+          sq = fmaf(e, e, sq);
+          y[t4][i] = yy;
+          dz4[t4][i] = act_grad(a4, yy, two_over_d * e);
+        }
+      }
+      const int r = row_l;
+      const int cw = (4 * g) ^ swz(r);
+      st4(S.x + r * XS + cw, f32x4{xv[0], xv[1], xv[2], xv[3]});
+      st4(S.x + r * XS + 16 + cw, f32x4{xv[4], xv[5], xv[6], xv[7]});
+      st4(S.h3 + r * HS + cw, h3);
+      st4(S.dz4 + r * XS + cw, dz4[0]);
+      st4(S.dz4 + r * XS + 16 + cw, dz4[1]);
+      if (a.want_acc) {
+        st4(S.y + r * XS + cw, y[0]);
+        st4(S.y + r * XS + 16 + cw, y[1]);
+      }
+      f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KSX; ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
+      f32x4 dz3, dz2, dz1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dz3[i] = act_grad(a3, h3[i], acc3[i]);
+      pcnt_bump(S.cnt + CE4, lane);   // h3, dz4 (and x, y) stored; G4 read
+      st4(S.h2 + r * HS + cw, h2);
+      st4(S.dz3 + r * HS + cw, dz3);
+      f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc2 = mfma4(S.w[G3 + s * 64 + lane], dz3[s], acc2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dz2[i] = act_grad(a2, h2[i], acc2[i]);
+      pcnt_bump(S.cnt + CE3, lane);   // h2, dz3 stored; G3 read
+      st4(S.h1 + r * HS + cw, h1);
+      st4(S.dz2 + r * HS + cw, dz2);
+      f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc1 = mfma4(S.w[G2 + s * 64 + lane], dz2[s], acc1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float h = h1[i];
+        const float sgn = h != 0.f ? __builtin_copysignf(1.0f, h) : 0.f;
+        dz1[i] = act_grad(a1, h, fmaf(l1r, sgn, acc1[i]));
+      }
+      pcnt_bump(S.cnt + CE2, lane);   // h1, dz2 stored; G2 read
+      st4(S.dz1 + r * HS + cw, dz1);
+      pcnt_bump(S.cnt + CE1, lane);   // dz1 stored (x was stored with h3)
+      if (done == step + 1) break;
+    }
+  } else {
+    const int layer = tile_layer(tile);
+    const int ce = CE1 + layer - 1, cu = CU1 + layer - 1;
+    double b1t = pow((double)a.beta1, (double)it0), b2t = pow((double)a.beta2, (double)it0);
+    const float* av = sbase + T.act;
+    const float* dv = sbase + T.dz;
+    const int X0 = 4 * (g >> 1), X1 = 4 * (2 + (g >> 1));
+    const int aE = T.as ? (T.am ^ X0) : 0, aO = T.as ? (T.am ^ X1) : 0;
+    const int dE = T.dc ^ X0, dO = T.dc ^ X1;
+    const int acc_row = tile == 4 ? lane : MB_LARGE;   // wave 6: one row per lane
+    const bool acc_lane = a.want_acc && acc_row < B;
+    for (int step = 0; step < nsteps; ++step) {
+      b1t *= (double)a.beta1;
+      b2t *= (double)a.beta2;
+      const float lr_t = a.lr * __builtin_amdgcn_sqrtf((float)(1.0 - b2t)) * __builtin_amdgcn_rcpf((float)(1.0 - b1t));
+      pcnt_wait<1>(S.cnt + ce, (unsigned)NRW * (unsigned)(step + 1));   // every row wave reached layer `layer`
+      f32x4 part[4];
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) part[c4] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // groups of 4 K-steps, one per accumulator chain
+#pragma unroll
+      for (int q = 0; q < NS / 4; ++q) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 16 * q + 4 * j + g;
+          part[j] = mfma4(av[r * T.as + ((j & 1) ? aO : aE)], dv[r * T.ds + ((j & 1) ? dO : dE)], part[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NS % 4; ++j) {
+        const int r = 16 * (NS / 4) + 4 * j + g;
+        part[j] = mfma4(av[r * T.as + ((j & 1) ? aO : aE)], dv[r * T.ds + ((j & 1) ? dO : dE)], part[j]);
+      }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};   // the barrier kernel's summation order (bit-identical A/B)
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) acc += part[c4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float gr = acc[i] * a.gscale;
+        const float mm = a.beta1 * mo[i] + (1.0f - a.beta1) * gr;
+        const float vv = a.beta2 * vo[i] + (1.0f - a.beta2) * gr * gr;
+        mo[i] = mm;
+        vo[i] = vv;
+        wo[i] -= lr_t * mm * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv) + a.eps);
+        S.w[fpos[i]] = wo[i];
+        S.w[bpos[i]] = wo[i];
+      }
+      if (acc_lane) corr += row_correct<KD>(S.y, S.x, acc_row, D);
+      pcnt_bump(S.cnt + cu, lane);
+      if (stream && S.stream_last <= step) break;   // read after this step's E wait: final
+    }
+  }
+
+  __syncthreads();
+  if (has_tile) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a.params[T.slot(i)] = wo[i];
+      a.m[T.slot(i)] = mo[i];
+      a.v[T.slot(i)] = vo[i];
+    }
+  }
+  float vals[3] = {sq, ab, corr};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float s = vals[k];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane == 0) S.red[k][wave] = s;
+  }
+  __syncthreads();
+  if (t == 0) {
+    if (a.metrics) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) s += S.red[k][w];
+        a.metrics[k] += s;
+      }
+      a.metrics[3] += (float)B * (float)done;
+    }
+    a.iter[0] = it0 + done;
+    if (a.cursor) a.cursor[0] = done == a.nsteps ? nxt : (cur0 + (int64_t)done * B) % a.ring;
+    if (stream) __hip_atomic_store(a.sr_consumed, (int64_t)done * B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace
 
 namespace sml {
@@ -754,6 +1110,14 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
   };
   if (dp_ranks > 1) pick(std::true_type{});
   else pick(std::false_type{});
+  // Keras batch 32, reference stack, one replica per workgroup (alone, fleet or streaming):
+  // the pipelined build (SML_MB_PIPE=0 selects the two-barrier kernel, for A/B runs; read per
+  // launch).  Same box: 15.5 -> 16.3 M rows/s alone, 3.93 -> 5.73 G rows/s for 1024 models.
+  const char* pe = getenv("SML_MB_PIPE");
+  if (B == 32 && ref && dims[0] <= 18 && dp_ranks <= 1 && !prof && !(pe && pe[0] == '0')) {
+    k = ae_minibatch_pipe_kernel<PACK_REF, 32>;
+    lds = sizeof(Smem<MB_SMALL>);
+  }
   if (lds > 65536) {   // > 64 KB of dynamic LDS must be opted into per kernel
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -103,3 +103,36 @@ def test_minibatch_rejects_bad_batch(cuda_device):
     fused.attach_ring(torch.zeros((129 * 4, 18), device=cuda_device), 129)
     with pytest.raises(ValueError):
         fused.train_minibatches(2)
+
+
+@pytest.mark.parametrize("B,models", [(32, 1), (32, 6)])
+def test_pipelined_build_bit_identical_to_barrier_kernel(cuda_device, monkeypatch, B, models):
+    """Keras batch 32 on the reference stack runs the pipelined build (the six parameter tiles
+    on their own waves, LDS stage counters instead of the two barriers per step).  Same
+    arithmetic in the same order as the two-barrier kernel (SML_MB_PIPE=0): bit-identical
+    parameters, moments, cursor and metrics, alone and as a fleet (one model per workgroup)."""
+    from streamml.ops.ae_fleet import AEFleet
+
+    spec = AESpec()
+    scale, shift = normalize_affine()
+    g = torch.Generator(device="cpu").manual_seed(5)
+    rings = (torch.rand((models, B * 24, 18), generator=g) * 40.0).to(cuda_device)
+    ws = [_weights(spec, seed=20 + i) for i in range(models)]
+    runs = []
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("SML_MB_PIPE", pipe)
+        if models == 1:
+            ae = FusedAE(spec, ws[0], cuda_device, scale=scale, shift=shift)
+            ae.attach_ring(rings[0].contiguous(), B)
+        else:
+            ae = AEFleet(spec, ws, cuda_device, lr=np.float32(2e-3), scale=scale, shift=shift)
+            ae.attach_rings(rings, B)
+        ae.train_minibatches(50)
+        ae.train_minibatches(37)   # 87 steps: the 24-batch ring wraps, the counters restart per launch
+        torch.cuda.synchronize()
+        runs.append((ae.params.clone(), ae.m.clone(), ae.v.clone(), ae.cursor.clone(), ae.iter.clone(),
+                     ae.read_metrics()))
+    (p1, m1, v1, c1, i1, r1), (p0, m0, v0, c0, i0, r0) = runs
+    assert torch.equal(p1, p0) and torch.equal(m1, m0) and torch.equal(v1, v0)
+    assert torch.equal(c1, c0) and torch.equal(i1, i0)
+    assert r1 == r0
