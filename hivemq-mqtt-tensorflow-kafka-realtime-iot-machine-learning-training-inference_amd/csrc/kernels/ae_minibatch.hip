@@ -138,7 +138,7 @@ struct Smem {   // MB 48: ~47 KB, MB 128: ~108 KB
   float red[3][16];                     // per-wave partial metrics (<= 16 waves)
   int abort;                            // DP: a gradient exchange timed out (all waves stop)
   int stream_end;                       // streaming: no further full batch (all waves stop)
-  unsigned cnt[8];                      // pipelined build: stage counters (CE1.., CU1..)
+  alignas(16) unsigned cnt[8];          // pipelined build: stage counters (CE1.., CU1..)
   int stream_last;                      // pipelined build, streaming: index of the last step (INT_MAX: open)
   int first_ok;                         // pipelined build, streaming: the first batch arrived (1)
 };
@@ -720,12 +720,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 //   row waves   forward, then the backward, bumping E_l as soon as layer l's activation and
 //               upstream gradient are stored and its backward fragment has been read (E4
 //               after dz3, E3 after dz2, E2 after dz1 is computed, E1 once dz1 is stored);
-//               before layer l's forward of the next step they wait for U_l.
+//               the next step starts once every U_l has counted this step's updates.
 //   tile waves  wait for E_l, contract act^T . dz over the 32 rows, Adam, write the forward /
 //               backward fragments, bump U_l.
 // W4's, W3's and W2's gradients and updates run under the rest of the backward pass; only
 // W1's (its gradient is produced last and the next forward needs it first) stays between two
-// steps.  Every LDS buffer a row wave writes in step s+1 is written after its U waits, i.e.
+// steps.  Every LDS buffer a row wave writes in step s+1 is written after its U wait, i.e.
 // after the tile waves of step s have read it.  Placement under round-robin wave -> SIMD
 // assignment: rows on waves 0-1 (SIMDs 0-1); W1's tiles on waves 4-5 (the same SIMDs: they
 // run while the row waves wait for them); the tiles that overlap the backward pass on waves
@@ -745,6 +745,19 @@ __device__ __forceinline__ void pcnt_bump(unsigned* p, int lane) {
   asm volatile("" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// The row waves' wait at the start of step st (>= 1) for ALL of the previous step's updates
+// (U1 >= 2 st, U2, U3 >= st, U4 >= 2 st) in one 16-byte LDS read per poll: W1's update comes
+// last, so one round trip replaces four (one before each forward layer).
+__device__ __forceinline__ void pcnt_wait_updates(const unsigned* cnt, unsigned st) {
+  for (;;) {
+    const uint4 u = *reinterpret_cast<const uint4*>(cnt + CU1);   // ds_read_b128 (counters only grow)
+    if (u.x >= 2u * st && u.y >= st && u.z >= st && u.w >= 2u * st) break;
+    __builtin_amdgcn_s_sleep(0);
+    asm volatile("" ::: "memory");   // read again
+  }
+  asm volatile("" ::: "memory");
+}
+
 // wave -> parameter tile (-1: row wave): rows on waves 0-1, W1 on 4-5, W2 2, W3 3, W4 6-7;
 // tile -> layer (1-based)
 __device__ __forceinline__ int pipe_tile(int wave) { return wave < 2 ? -1 : wave < 4 ? wave : wave < 6 ? wave - 4 : wave - 2; }
@@ -861,9 +874,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
   if (has_rows) {
     for (int step = 0; step < nsteps; ++step) {
       const unsigned st = (unsigned)step;
-      // W1 (two tiles) of the previous step is in the fragments.  A resident ring waits after
+      // Every tile of the previous step is updated (and its LDS reads, incl. the accuracy wave's,
+      // are done), so all of this step's stores are safe too.  A resident ring waits after
       // issuing the next rows' loads; a stream must first learn whether this step exists.
-      if (stream && step) pcnt_wait(S.cnt + CU1, 2u * st);
+      if (stream && step) pcnt_wait_updates(S.cnt, st);
       if (stream) {
         if (S.stream_last < step) {   // another row wave found the stream over last step
           done = step;
@@ -894,7 +908,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
           done = step + 1;   // this step is the last
         }
       }
-      if (!stream && step) pcnt_wait(S.cnt + CU1, 2u * st);
+      if (!stream && step) pcnt_wait_updates(S.cnt, st);
       f32x4 z1 = ld4(S.w + BB1 + 4 * g);
 #pragma unroll
       for (int s = 0; s < KSX; ++s) z1 = mfma4(S.w[F1 + s * 64 + lane], xv[s], z1);
@@ -904,15 +918,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
         h1[i] = act_fwd(a1, z1[i]);
         ab = fmaf(fabsf(h1[i]), rowf, ab);
       }
-      if (step) pcnt_wait(S.cnt + CU2, st);
       const f32x4 z2 = layer16(S.w + F2, S.w + BB2, lane, g, h1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) h2[i] = act_fwd(a2, z2[i]);
-      if (step) pcnt_wait(S.cnt + CU3, st);
       const f32x4 z3 = layer16(S.w + F3, S.w + BB3, lane, g, h2);
 #pragma unroll
       for (int i = 0; i < 4; ++i) h3[i] = act_fwd(a3, z3[i]);
-      if (step) pcnt_wait(S.cnt + CU4, 2u * st);   // also: the accuracy of the previous step is read
       f32x4 y[2], dz4[2];
 #pragma unroll
       for (int t4 = 0; t4 < 2; ++t4) {
