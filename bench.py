@@ -38,6 +38,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+T_PROC = time.time()          # the budget clock starts with the process
 BASELINE_ROWS_PER_S = 62661.0
 METRIC = "sensor-rows/sec (autoencoder train) + p50 per-event inference µs at 1/2/4/8 MI355X"
 
@@ -75,6 +76,9 @@ def parse():
     p.add_argument("--settle-ms", type=float, default=100.0,
                    help="untimed steps before the warm-up until this much GPU time has passed (DPM clock settle)")
     p.add_argument("--headline-only", action="store_true", help="skip every side measurement")
+    p.add_argument("--budget-s", type=float, default=450.0,
+                   help="wall-clock budget of the whole run (from process start): a side measurement starts only "
+                        "if its estimate still fits; past budget + 60 s a watchdog prints the line and ends the job")
     p.add_argument("--dump-params", default=None,
                    help="write this rank's final parameter image to <path>.rank<R>.npy (replica checks)")
     p.add_argument("--graph", action="store_true",
@@ -514,13 +518,45 @@ def main():
                   "fresh_steps", "fit_rows", "stream_rows", "lstm_steps"):
             setattr(args, k, 0)
 
-    def guarded(fn, *a, **kw):   # a side measurement never takes the headline down
-        try:
-            return fn(*a, **kw)
-        except Exception as e:  # noqa: BLE001
-            return {"error": repr(e)[:400]}
+    rows_per_s = gb * args.steps / elapsed
+    out = {
+        "metric": METRIC,
+        "value": rows_per_s,
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": rows_per_s / BASELINE_ROWS_PER_S,
+        "dtype": "bf16",
+        "input_dtype": ("fp32 sensor rows, tile-packed at ingest: normalize_fn and argmax(x) applied once per "
+                        "event when the ring is built (outside the timed loop, as the streaming K8 ingest does); "
+                        "bf16 MFMA, fp32 accumulate" if fused.ring_xpack is not None else
+                        "fp32 raw sensor rows (normalize_fn fused into the kernel's load; bf16 MFMA, fp32 accumulate)"),
+        "data": "synthetic (raw car-sensor rows, 100k simulated devices, HBM-resident, random-init weights)",
+        "config": {
+            "model": "dense-autoencoder 18-14-7-7-18 (cardata-v1, tanh/relu/tanh/relu, L1 1e-7, MSE, Adam)",
+            "global_batch": gb,
+            "seq_len": 1,
+            "parallelism": f"dp{world}",
+            "micro_batch_per_gpu": B,
+        },
+        "backend": env.backend,
+        "per_rank_ms_per_step": {"min": min(step_ms), "max": max(step_ms), "ranks": step_ms},
+        "clock_settle": {"ms": args.settle_ms, "steps": settle_steps},
+        "pack_ms": pack_ms,
+        "hip_graph": graph is not None,
+        "final_epoch_loss": metrics["loss"],
+        "final_accuracy": metrics["accuracy"],
+    }
+    ph = Phases(args.budget_s, rank, world, device, out)
+    ph.phase_s["startup_to_headline"] = round(time.time() - T_PROC, 3)
+    ph.start_watchdog()        # rank 0: from here on the line cannot be lost (bench/_watchdog.py)
 
-    # -- BASELINE config 5: per-event scoring on every replica at once (shard-by-key) ----------
+    # ---- collective phases: every rank takes part, one agreed budget decision each ---------------
+    # BASELINE config 5: per-event scoring on every replica at once (shard-by-key)
     am = None
     infer = {"skipped": "--infer-events 0"}
     if args.infer_events > 0:
@@ -533,116 +569,207 @@ def main():
             infer = {"error": repr(e)[:400]}
         if am is not None:
             dp.barrier(device)
-            infer = guarded(measure_infer, am, device, args.infer_events, args.infer_repeats, args.qps, rank)
+            infer = ph.run("infer", 6 + 3e-4 * args.infer_events * args.infer_repeats, measure_infer, am, device,
+                           args.infer_events, args.infer_repeats, args.qps, rank, collective=True)
     per_rank_infer = gather_all(infer, device)
-    e2e = None
-    if rank == 0 and am is not None and args.e2e_events > 0:
-        e2e = guarded(measure_kafka_e2e, am, device, args.e2e_events, args.qps)
-    b32 = None
-    if rank == 0 and args.batch32_steps > 0:
-        b32 = guarded(measure_batch32, spec, data, device, args.batch32_steps, scale, shift, args.seed)
-        if args.fleet_models > 0:
-            b32["fleet"] = guarded(measure_batch32_fleet, spec, data, device, max(args.batch32_steps // 10, 1),
-                                   scale, shift, args.fleet_models)
+    p50s = [r.get("p50_us") for r in per_rank_infer if isinstance(r, dict)]
+    p50s = [v for v in p50s if v is not None]
+    out.update({
+        "p50_infer_us": max(p50s) if p50s else None,   # worst replica (conservative)
+        "p99_infer_us": max((r.get("p99_us") or 0.0) for r in per_rank_infer if isinstance(r, dict)) or None,
+        "infer_path": "persistent-kernel (ae_serve.hip), host-mapped request ring",
+        "infer": per_rank_infer[0],
+        "infer_per_replica_p50_us": p50s,
+    })
     b32_dp = {"skipped": "single GPU (no peers)"}
     coll = {"skipped": "single GPU (no peers)"}
     if env.is_dist and (args.dp_steps > 0 or args.collective_iters > 0):
         from streamml.parallel.p2p import P2PGroup
-        p2p, p2p_err = P2PGroup.try_create(device)   # collective: every rank gets a group, or none
+        p2p, p2p_err = ph.run("p2p_setup", 10, P2PGroup.try_create, device, collective=True, default=(None, None))
         if args.collective_iters > 0:
-            coll = guarded(measure_collectives, device, world, p2p, args.collective_iters)
+            coll = ph.run("small_allreduce", 5, measure_collectives, device, world, p2p, args.collective_iters,
+                          collective=True)
             if p2p is None:
                 coll["p2p_error"] = repr(p2p_err)[:200]
         if args.dp_steps > 0:
-            b32_dp = (guarded(measure_batch_dp, spec, data, device, args.dp_steps, scale, shift, args.seed, world,
-                              group=p2p) if p2p is not None else {"error": f"P2P exchange unavailable: {p2p_err!r}"})
-    fit_large = fresh = None
-    if rank == 0 and args.fit_epochs > 0:
-        fit_large = guarded(measure_fit_large_batch, data, device, B, epochs=args.fit_epochs, settle_ms=args.settle_ms)
-        fit_large["shuffled"] = guarded(measure_fit_large_batch, data, device, B, epochs=max(args.fit_epochs // 2, 1),
-                                        shuffle=True)
-    if rank == 0 and args.fresh_steps > 0:
-        fresh = guarded(measure_fresh_rows, spec, data, device, B, args.fresh_steps, scale, shift)
-    fit100 = stream = None
-    if rank == 0 and args.fit_rows > 0:
-        fit100 = guarded(measure_fit, device, args.fit_rows)
-    if rank == 0 and args.stream_rows > 0:
-        stream = guarded(measure_stream_e2e, device, args.stream_rows)
-    # -- BASELINE config 3: LSTM (rank 0; the LSTM trains single-replica here) --------------------
-    lstm = lstm_ref = None
-    if rank == 0 and args.lstm_steps > 0:
+            b32_dp = (ph.run("keras_batch32_dp", 5 + 4e-5 * args.dp_steps * world, measure_batch_dp, spec, data,
+                             device, args.dp_steps, scale, shift, args.seed, world, group=p2p, collective=True)
+                      if p2p is not None else {"error": f"P2P exchange unavailable: {p2p_err!r}"})
+    out.update({"keras_batch32_dp": b32_dp, "small_allreduce": coll})
+    ph.snapshot()
+
+    # ---- rank 0 alone: every other rank parks on the rendezvous store (no GPU, no collective) ----
+    if rank != 0:
+        ph.park()
+        dp.shutdown()
+        return
+    if am is not None and args.e2e_events > 0:
+        e2e = ph.run("kafka_e2e", 6 + 3e-4 * args.e2e_events, measure_kafka_e2e, am, device, args.e2e_events,
+                     args.qps)
+        out.update({"kafka_e2e_p50_us": None if "p50_us" not in e2e else e2e["p50_us"],
+                    "kafka_e2e_p99_us": None if "p99_us" not in e2e else e2e["p99_us"], "kafka_e2e": e2e})
+    if args.batch32_steps > 0:
+        b32 = ph.run("keras_batch32", 4 + 1.5e-5 * args.batch32_steps, measure_batch32, spec, data, device,
+                     args.batch32_steps, scale, shift, args.seed)
+        if args.fleet_models > 0 and "error" not in b32 and "skipped" not in b32:
+            b32["fleet"] = ph.run("keras_batch32_fleet", 6, measure_batch32_fleet, spec, data, device,
+                                  max(args.batch32_steps // 10, 1), scale, shift, args.fleet_models)
+        out["keras_batch32"] = b32
+    if args.fit_epochs > 0:
+        fit_large = ph.run("fit_large_batch", 8, measure_fit_large_batch, data, device, B, epochs=args.fit_epochs,
+                           settle_ms=args.settle_ms)
+        if "rows_per_s" in fit_large:
+            fit_large["shuffled"] = ph.run("fit_large_batch_shuffled", 6, measure_fit_large_batch, data, device, B,
+                                           epochs=max(args.fit_epochs // 2, 1), shuffle=True)
+        out.update({"fit_large_batch_rows_per_s": fit_large.get("rows_per_s"), "fit_large_batch": fit_large})
+    if args.fresh_steps > 0:
+        fresh = ph.run("fresh_rows", 5, measure_fresh_rows, spec, data, device, B, args.fresh_steps, scale, shift)
+        out.update({"fresh_rows_per_s": fresh.get("rows_per_s"), "fresh_rows": fresh})
+    if args.fit_rows > 0:
+        fit100 = ph.run("fit_batch100", 5 + 1e-6 * args.fit_rows, measure_fit, device, args.fit_rows)
+        out.update({"fit_batch100_rows_per_s": fit100.get("rows_per_s"), "fit_batch100": fit100})
+    if args.stream_rows > 0:
+        stream = ph.run("stream_e2e", 10 + 1.5e-6 * args.stream_rows, measure_stream_e2e, device, args.stream_rows)
+        out.update({"stream_e2e_rows_per_s": stream.get("rows_per_s"), "stream_e2e": stream})
+    # BASELINE config 3: LSTM (rank 0; the LSTM trains single-replica here)
+    if args.lstm_steps > 0:
         from_b = _bench_module("bench_lstm")
-        lstm = guarded(from_b.measure_seq, batch=65536, seq_len=50, steps=args.lstm_steps, warmup=3, device=device)
-        lstm_ref = guarded(from_b.measure_reference, batch=1, epochs=5, steps_per_epoch=1000, autograd_steps=100,
-                           device=device)
-    lstm_infer = None
-    if rank == 0 and args.infer_events > 0 and args.lstm_steps > 0:
-        lstm_infer = guarded(measure_lstm_infer, device, args.infer_events, args.infer_repeats, args.qps)
-    rows_per_s = gb * args.steps / elapsed
-    if rank == 0:
-        p50s = [r.get("p50_us") for r in per_rank_infer if isinstance(r, dict)]
-        p50s = [v for v in p50s if v is not None]
-        out = {
-            "metric": METRIC,
-            "value": rows_per_s,
-            "unit": "rows/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": rows_per_s / BASELINE_ROWS_PER_S,
-            "dtype": "bf16",
-            "input_dtype": ("fp32 sensor rows, tile-packed at ingest: normalize_fn and argmax(x) applied once per "
-                            "event when the ring is built (outside the timed loop, as the streaming K8 ingest does); "
-                            "bf16 MFMA, fp32 accumulate" if fused.ring_xpack is not None else
-                            "fp32 raw sensor rows (normalize_fn fused into the kernel's load; bf16 MFMA, fp32 accumulate)"),
-            "data": "synthetic (raw car-sensor rows, 100k simulated devices, HBM-resident, random-init weights)",
-            "config": {
-                "model": "dense-autoencoder 18-14-7-7-18 (cardata-v1, tanh/relu/tanh/relu, L1 1e-7, MSE, Adam)",
-                "global_batch": gb,
-                "seq_len": 1,
-                "parallelism": f"dp{world}",
-                "micro_batch_per_gpu": B,
-            },
-            "backend": env.backend,
-            "per_rank_ms_per_step": {"min": min(step_ms), "max": max(step_ms), "ranks": step_ms},
-            "clock_settle": {"ms": args.settle_ms, "steps": settle_steps},
-            "pack_ms": pack_ms,
-            "p50_infer_us": max(p50s) if p50s else None,   # worst replica (conservative)
-            "p99_infer_us": max((r.get("p99_us") or 0.0) for r in per_rank_infer if isinstance(r, dict)) or None,
-            "infer_path": "persistent-kernel (ae_serve.hip), host-mapped request ring",
-            "infer": per_rank_infer[0],
-            "infer_per_replica_p50_us": p50s,
-            "kafka_e2e_p50_us": None if not e2e or "error" in e2e else e2e["p50_us"],
-            "kafka_e2e_p99_us": None if not e2e or "error" in e2e else e2e["p99_us"],
-            "kafka_e2e": e2e,
-            "hip_graph": graph is not None,
-            "final_epoch_loss": metrics["loss"],
-            "final_accuracy": metrics["accuracy"],
-            "keras_batch32": b32,
-            "keras_batch32_dp": b32_dp,
-            "small_allreduce": coll,
-            "fit_large_batch_rows_per_s": None if not fit_large or "error" in fit_large else fit_large["rows_per_s"],
-            "fit_large_batch": fit_large,
-            "fresh_rows_per_s": None if not fresh or "error" in fresh else fresh["rows_per_s"],
-            "fresh_rows": fresh,
-            "fit_batch100_rows_per_s": None if not fit100 or "error" in fit100 else fit100["rows_per_s"],
-            "fit_batch100": fit100,
-            "stream_e2e_rows_per_s": None if not stream or "error" in stream else stream["rows_per_s"],
-            "stream_e2e": stream,
-            "lstm_seq50_windows_per_s": None if not lstm or "error" in lstm else lstm["value"],
-            "lstm_seq50": lstm,
-            "lstm_ref_us_per_step": None if not lstm_ref or "error" in lstm_ref else lstm_ref["value"],
-            "lstm_ref": lstm_ref,
-            "lstm_infer_p50_us": None if not lstm_infer or "error" in lstm_infer else lstm_infer["p50_us"],
-            "lstm_infer_p99_us": None if not lstm_infer or "error" in lstm_infer else lstm_infer["p99_us"],
-            "lstm_infer": lstm_infer,
-        }
-        print(json.dumps(out), flush=True)
-    dp.barrier(device)   # every rank leaves together (rank 0's side measurements run alone)
+        lstm = ph.run("lstm_seq50", 10, from_b.measure_seq, batch=65536, seq_len=50, steps=args.lstm_steps, warmup=3,
+                      device=device, settle_ms=args.settle_ms)
+        lstm_ref = ph.run("lstm_ref", 10, from_b.measure_reference, batch=1, epochs=5, steps_per_epoch=1000,
+                          autograd_steps=100, device=device)
+        out.update({"lstm_seq50_windows_per_s": lstm.get("value"), "lstm_seq50": lstm,
+                    "lstm_ref_us_per_step": lstm_ref.get("value"), "lstm_ref": lstm_ref})
+        if args.infer_events > 0:
+            lstm_infer = ph.run("lstm_infer", 6 + 3e-4 * args.infer_events * args.infer_repeats, measure_lstm_infer,
+                                device, args.infer_events, args.infer_repeats, args.qps)
+            out.update({"lstm_infer_p50_us": lstm_infer.get("p50_us"), "lstm_infer_p99_us": lstm_infer.get("p99_us"),
+                        "lstm_infer": lstm_infer})
+    ph.finish()          # prints the ONE line (unless the watchdog already had to), releases parked ranks
     dp.shutdown()
+
+
+class Phases:
+    """Per-measurement wall clock and the ``--budget-s`` guard of the side measurements.
+
+    * ``run(name, est_s, fn, ...)`` starts a phase only if ``est_s`` still fits in the budget
+      (for a ``collective`` phase every rank takes the SAME decision: the minimum time left over
+      the ranks), records its wall time in ``phase_s``, and turns an exception into
+      ``{"error": ...}``: a side measurement never takes the headline down.
+    * rank 0 streams a snapshot of the line to ``bench/_watchdog.py`` after every phase; if a
+      phase hangs inside a native call past ``budget_s + grace``, the watchdog prints that
+      snapshot and ends the job, so the headline line is printed whatever happens.
+    * ranks != 0 wait for rank 0's solo phases on the rendezvous store (a host wait, not a
+      collective that could hit the process-group timeout), bounded by the same deadline.
+    """
+
+    GRACE_S = 60.0
+
+    def __init__(self, budget_s, rank, world, device, out):
+        import tempfile
+        self.budget_s, self.rank, self.world, self.device, self.out = float(budget_s), rank, world, device, out
+        self.phase_s, self.skipped = {}, {}
+        self.watch = None
+        self.marker = os.path.join(tempfile.gettempdir(), f"sml_bench_line_{os.getpid()}_{int(T_PROC * 1e3)}")
+        out["phase_s"], out["budget"] = self.phase_s, {"budget_s": self.budget_s, "skipped": self.skipped}
+
+    def left(self) -> float:
+        return self.budget_s - (time.time() - T_PROC)
+
+    def deadline(self) -> float:
+        # never earlier than GRACE_S from now: a budget already spent before the headline
+        # skips every phase, and the line still needs its moment to print
+        return max(T_PROC + self.budget_s, time.time()) + self.GRACE_S
+
+    def start_watchdog(self):
+        if self.rank != 0:
+            return
+        import subprocess
+        try:
+            self.watch = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench", "_watchdog.py"),
+                                           repr(self.deadline()), self.marker, str(os.getpid())],
+                                          stdin=subprocess.PIPE, stdout=None, stderr=None)
+        except OSError as e:
+            print(f"[bench] watchdog unavailable: {e!r}", file=sys.stderr, flush=True)
+        self.snapshot()
+
+    def _send(self, payload: bytes):
+        if self.watch is None:
+            return
+        try:
+            self.watch.stdin.write(payload)
+            self.watch.stdin.flush()
+        except (BrokenPipeError, OSError):
+            self.watch = None
+
+    def snapshot(self):
+        if self.rank == 0:
+            self._send((json.dumps(self.out) + "\n").encode())
+
+    def run(self, name, est_s, fn, *a, collective=False, default=None, **kw):
+        from streamml.parallel import dp
+        left = self.left()
+        if collective:
+            left = -dp.allreduce_max(-left, self.device)
+        if left < est_s:
+            self.skipped[name] = f"{left:.0f} s of the {self.budget_s:.0f} s budget left, phase estimated {est_s:.0f} s"
+            return default if default is not None else {"skipped": self.skipped[name]}
+        self._send(f"PHASE {name}\n".encode())
+        t = time.perf_counter()
+        try:
+            r = fn(*a, **kw)
+        except Exception as e:  # noqa: BLE001 - a side measurement never takes the headline down
+            r = default if default is not None else {"error": repr(e)[:400]}
+        self.phase_s[name] = round(time.perf_counter() - t, 3)
+        self.snapshot()
+        return r
+
+    def _store(self):
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return None
+        try:
+            return dist.distributed_c10d._get_default_store()
+        except Exception:  # noqa: BLE001
+            return None
+
+    def park(self):
+        """ranks != 0: wait until rank 0 has printed (host-side store wait, bounded)."""
+        import datetime
+        st = self._store()
+        if st is None:
+            return
+        try:
+            st.wait(["sml_bench_done"], datetime.timedelta(seconds=max(self.deadline() - time.time(), 1.0) + 30))
+        except Exception as e:  # noqa: BLE001 - rank 0 died or hung: leave anyway
+            print(f"[bench] rank {self.rank}: rank 0 never finished ({e!r:.200}); leaving", file=sys.stderr, flush=True)
+
+    def finish(self):
+        self.out["phase_s"]["total_wall"] = round(time.time() - T_PROC, 3)
+        try:
+            os.close(os.open(self.marker, os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o600))
+            mine = True
+        except FileExistsError:   # the watchdog already printed (cannot happen unless the deadline raced)
+            mine = False
+        if mine:
+            print(json.dumps(self.out), flush=True)
+        self._send(b"DONE\n")
+        if self.watch is not None:
+            try:
+                self.watch.stdin.close()
+                self.watch.wait(timeout=5)
+            except Exception:  # noqa: BLE001
+                pass
+        try:
+            os.unlink(self.marker)
+        except OSError:
+            pass
+        st = self._store()
+        if st is not None and self.world > 1:
+            try:
+                st.set("sml_bench_done", "1")
+            except Exception:  # noqa: BLE001
+                pass
 
 
 if __name__ == "__main__":

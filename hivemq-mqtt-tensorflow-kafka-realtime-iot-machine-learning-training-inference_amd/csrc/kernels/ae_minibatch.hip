@@ -390,9 +390,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const bool stream = a.sr_avail != nullptr;
   int64_t avail = 0;   // streaming: rows known to be in the ring (cached; re-polled only when short)
   int first_ok = 1;
-  if (stream) {
-    first_ok = stream_wait(a, (int64_t)B, avail);
-    if (first_ok < 0 && t == 0) __hip_atomic_store(a.sr_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (stream) {   // ONE decision for the whole workgroup: waves that disagreed near the timeout
+                  // would split between the in-loop barrier and the final one and hang
+    if (t == 0) {
+      int64_t av = 0;
+      S.first_ok = stream_wait(a, (int64_t)B, av);
+      if (S.first_ok < 0) __hip_atomic_store(a.sr_status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+    first_ok = S.first_ok;
   }
   if (has_rows && first_ok == 1) fetch(cur);
   int64_t nxt = advance(cur);

@@ -26,10 +26,12 @@ inline void cpu_relax() {
 
 }  // namespace
 
-ServeRing::ServeRing(int device, int nslots, int D, double idle_seconds)
+ServeRing::ServeRing(int device, int nslots, int D, double idle_seconds, int max_D)
     : device_(device), nslots_(nslots), D_(D), idle_s_(idle_seconds) {
   if (nslots < 64) throw std::invalid_argument("serve: nslots must be >= 64");
-  if (D < 1 || D > 31) throw std::invalid_argument("serve: rows must have 1..31 features");
+  if (max_D > 32) max_D = 32;   // a request slot holds 32 words
+  if (D < 1 || D > max_D)
+    throw std::invalid_argument(std::string("serve: rows must have 1..") + std::to_string(max_D) + " features");
   ck(hipSetDevice(device), "hipSetDevice");
   const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
   ck(hipHostMalloc((void**)&ctl_, sizeof(ServeCtl), fl), "hipHostMalloc ctl");
@@ -61,7 +63,7 @@ void ServeRing::launch() {
 AEServe::AEServe(int device, int nslots, const std::vector<float>& weights, const int dims[3], const int acts[4],
                  const std::vector<float>& scale, const std::vector<float>& shift, float threshold,
                  double idle_seconds)
-    : ServeRing(device, nslots, dims[0], idle_seconds), threshold_(threshold) {
+    : ServeRing(device, nslots, dims[0], idle_seconds, 32), threshold_(threshold) {   // no key word: all 32
   name_ = "AEServe";
   for (int i = 0; i < 3; ++i) dims_[i] = dims[i];
   for (int i = 0; i < 4; ++i) acts_[i] = acts[i];
@@ -101,7 +103,7 @@ LSTMServe::LSTMServe(int device, int nslots, const std::vector<float>& weights,
                      const std::vector<LstmServeLayer>& layers, int D, int T, int nkeys,
                      const std::vector<float>& scale, const std::vector<float>& shift, float threshold,
                      double idle_seconds)
-    : ServeRing(device, nslots, D, idle_seconds) {
+    : ServeRing(device, nslots, D, idle_seconds, 31) {   // request word 31 carries the car key
   name_ = "LSTMServe";
   if (layers.empty() || layers.size() > (size_t)LS_MAXLAYERS) throw std::invalid_argument("LSTMServe: 1..8 layers");
   if (T < 1 || T > 64) throw std::invalid_argument("LSTMServe: look_back must be 1..64");
@@ -144,14 +146,17 @@ LSTMServe::LSTMServe(int device, int nslots, const std::vector<float>& weights,
   ck(hipMalloc((void**)&a.hist, (size_t)nkeys * T * D * sizeof(float)), "hipMalloc windows");
   ck(hipMalloc((void**)&a.hcount, (size_t)nkeys * sizeof(int)), "hipMalloc counts");
   ck(hipMalloc((void**)&a.lastpred, (size_t)nkeys * D * sizeof(float)), "hipMalloc forecasts");
-  reset_keys();
-  launch();
+  reset_keys();   // zeroes the key state and launches the resident kernel
 }
 
 void LSTMServe::reset_keys() {
+  // the resident kernel reads and writes the key state: stop it first (flag + drain the
+  // stream), so the memsets never queue behind a kernel that only leaves at its idle timeout
+  stop();
   ck(hipMemsetAsync(args_.hcount, 0, (size_t)args_.nkeys * sizeof(int), stream_), "memset counts");
   ck(hipMemsetAsync(args_.lastpred, 0, (size_t)args_.nkeys * args_.D * sizeof(float), stream_), "memset forecasts");
   ck(hipStreamSynchronize(stream_), "sync");
+  launch();
 }
 
 LSTMServe::~LSTMServe() {

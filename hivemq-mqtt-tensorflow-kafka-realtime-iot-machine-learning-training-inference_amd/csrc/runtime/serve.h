@@ -23,7 +23,9 @@ namespace sml {
 // persistent scorers; a subclass supplies the kernel launch.
 class ServeRing {
  public:
-  ServeRing(int device, int nslots, int D, double idle_seconds);
+  // max_D: widest row the subclass's kernel takes (<= 32 request words; 31 when word 31
+  // carries a key)
+  ServeRing(int device, int nslots, int D, double idle_seconds, int max_D);
   virtual ~ServeRing();
   ServeRing(const ServeRing&) = delete;
   ServeRing& operator=(const ServeRing&) = delete;
@@ -102,7 +104,8 @@ class LSTMServe : public ServeRing {
             double idle_seconds);
   ~LSTMServe() override;
   int nkeys() const { return args_.nkeys; }
-  // forget every key's window and forecast (device memset; the kernel must be idle or stopped)
+  // forget every key's window and forecast: stops the resident kernel, zeroes the key state
+  // on the device, relaunches (returns without waiting for the kernel's idle timeout)
   void reset_keys();
 
  protected:

@@ -390,7 +390,7 @@ class Autoencoder:
         maybe_inject_range(gstep, gstep + nfull + 1, rank)
         steps = 0
         if nfull:
-            key = (xd.data_ptr(), n, B, nfull)
+            key = self.pack_key(xd, B, nfull)
             packed = pkey is None and getattr(self, "_tp_key", None) == key and be.ring_xpack is not None
             if pkey is None and not packed and epochs_left < self.PACK_MIN_PASSES:
                 for i in range(nfull):   # rows in place, normalised inside the kernel
@@ -414,6 +414,13 @@ class Autoencoder:
             be.step(tail.contiguous())
             steps += 1
         return steps
+
+    @staticmethod
+    def pack_key(xd: torch.Tensor, B: int, nfull: int) -> tuple:
+        """Identity of the rows a tile-packed ring was built from: storage, extent, batch AND
+        the tensor's version counter, so an in-place update of the same device array between
+        two ``fit`` calls re-packs instead of training on the stale packed rows."""
+        return (xd.data_ptr(), int(xd.size(0)), int(B), int(nfull), int(xd._version))
 
     @staticmethod
     def shuffle_key(seed: int, rank: int, epoch: int) -> int:

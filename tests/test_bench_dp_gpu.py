@@ -61,6 +61,63 @@ def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [4, 8])
+def test_bench_n_ranks_rehearsal(tmp_path, cuda_device, n):
+    """The driver's 4- and 8-GPU scaling run rehearsed on one GPU: ``bench.py --gpus N``
+    self-launches N ranks (gloo, all on GPU 0) with EVERY side measurement on, at reduced
+    sizes.  The line must carry N replicas' scoring p50s, the small all-reduce, an in-kernel
+    P2P DP run with N peers whose replicas end bit-identical, every rank's parameters
+    identical, and the per-phase wall clock; the whole job must stay inside its budget."""
+    env = dict(os.environ, SML_SHARE_GPU0="1", OMP_NUM_THREADS="2")
+    dump = str(tmp_path / "params")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n), "--steps", "4", "--warmup", "2", "--batch-per-gpu", "65536",
+           "--dataset-rows", "262144", "--infer-events", "2000", "--infer-repeats", "1", "--e2e-events", "2000",
+           "--batch32-steps", "2000", "--fleet-models", "64", "--dp-steps", "500", "--collective-iters", "50",
+           "--fit-epochs", "2", "--fresh-steps", "2", "--fit-rows", "200000", "--stream-rows", "500000",
+           "--lstm-steps", "4", "--budget-s", "240", "--dump-params", dump]
+    t0 = __import__("time").time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    wall = __import__("time").time() - t0
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["config"]["parallelism"] == f"dp{n}"
+    assert out["config"]["global_batch"] == n * 65536 and len(out["per_rank_ms_per_step"]["ranks"]) == n
+    assert len(out["infer_per_replica_p50_us"]) == n and all(v > 0 for v in out["infer_per_replica_p50_us"])
+    coll = out["small_allreduce"]
+    assert coll.get("backend_allreduce_us", 0) > 0 and coll.get("p2p_allreduce_us", 0) > 0, coll
+    dpr = out["keras_batch32_dp"]
+    assert dpr.get("replicas_identical") is True and dpr["global_batch"] == 32 * n, dpr
+    ph = out["phase_s"]
+    for k in ("infer", "small_allreduce", "keras_batch32_dp", "kafka_e2e", "keras_batch32", "fit_large_batch",
+              "fresh_rows", "fit_batch100", "stream_e2e", "lstm_seq50", "lstm_ref", "lstm_infer", "total_wall"):
+        assert k in ph, (k, ph, out["budget"])
+    assert not out["budget"]["skipped"], out["budget"]
+    assert wall < 300
+    ps = [np.load(f"{dump}.rank{i}.npy") for i in range(n)]
+    for p in ps[1:]:
+        np.testing.assert_array_equal(ps[0], p)
+
+
+@pytest.mark.gpu
+def test_bench_budget_skips_and_still_prints(cuda_device):
+    """A budget too small for any side measurement: every phase is skipped and named, the
+    headline line still prints."""
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("SML_SHARE_GPU0", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--batch-per-gpu",
+           "65536", "--dataset-rows", "131072", "--budget-s", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["value"] > 0 and out["n_gpus"] == 1
+    sk = out["budget"]["skipped"]
+    assert "infer" in sk and "kafka_e2e" in sk and "lstm_seq50" in sk, sk
+
+
+@pytest.mark.gpu
 def test_bench_force_pg_rccl_world1(cuda_device):
     """The whole DP bench path on ONE RCCL rank (SML_FORCE_PG=1): nccl communicator,
     per-step all-reduce in the timed loop, P2P exchange + in-kernel DP, collectives."""

@@ -136,3 +136,24 @@ def test_pack_with_perm_key_equals_indexed_pack(cuda_device):
     assert torch.equal(a, b)
     c = C.pack_tiles_argmax(x[idx].contiguous(), 18, sc, sh)
     assert torch.equal(a, c)
+
+
+def test_fit_throughput_repacks_after_in_place_update(cuda_device):
+    """Two unshuffled fits on the same device array with an in-place update between them:
+    the second fit must train on the NEW rows (the pack key carries the version counter),
+    not on the ring packed from the old ones."""
+    B, n = 2048, 2048 * 4
+    raw1, xn1 = _data(n, 21)
+    raw2, xn2 = _data(n, 22)
+    m = Autoencoder(device=cuda_device, input_normalizer="cardata", seed=5)
+    w0 = m.get_weights()
+    m.compile()
+    xd = torch.from_numpy(raw1).to(cuda_device)
+    m.fit(xd, epochs=3, batch_size=B, shuffle=False, verbose=0, engine="throughput")
+    xd.copy_(torch.from_numpy(raw2))
+    m.fit(xd, epochs=3, batch_size=B, shuffle=False, verbose=0, engine="throughput")
+    b = [np.arange(i, i + B) for _ in range(3) for i in range(0, n, B)]
+    # one Adam trajectory over both fits (the optimizer state carries across fit calls)
+    xcat = np.concatenate([xn1, xn2])
+    want, _ = _adam_oracle(w0, xcat, b + [x + n for x in b])
+    assert _relerr(m.get_weights(), want) < 1e-3

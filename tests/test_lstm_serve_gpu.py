@@ -91,15 +91,19 @@ def test_lstm_serve_matches_oracle(cuda_device, stack, T):
 
 
 def test_lstm_serve_latency_and_reset(cuda_device):
+    import time
+
     from streamml.ops.serve import LSTMScoringServer
     m = LSTMPredictor.two_layer(look_back=50, device=cuda_device)
     rng = np.random.default_rng(1)
     rows = rng.uniform(0, 40, size=(600, 18)).astype(np.float32)
     keys = np.zeros(600, np.int64)
-    with LSTMScoringServer(m, nkeys=10) as srv:
+    with LSTMScoringServer(m, nkeys=10, idle_seconds=5.0) as srv:
         lat = srv.latency_us(rows, keys, qps=20000)
         assert lat.shape == (600,) and np.all(lat > 0)
-        srv.reset()
+        t0 = time.perf_counter()
+        srv.reset()             # stops the resident kernel first: no wait for its idle timeout
+        assert time.perf_counter() - t0 < 1.0
         _, s, f = srv.forecast(rows[:3], keys[:3])
         assert np.all(f == 2)
         with pytest.raises(Exception):

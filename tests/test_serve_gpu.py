@@ -41,6 +41,22 @@ def test_scores_match_reference(cuda_device):
         assert lat.shape == (200,) and np.all(lat > 0)
 
 
+def test_scorer_accepts_32_features(cuda_device):
+    """The AE scorer takes rows of up to 32 features (the LSTM forecaster's limit is 31: its
+    request word 31 carries the key) -- the D = 32 boundary of ADVICE r03."""
+    from streamml.models.autoencoder import Autoencoder
+    from streamml.models.reference import ae_forward_torch
+    from streamml.ops.serve import ScoringServer
+    m = Autoencoder(input_dim=32, device=cuda_device, seed=1)   # weights only: no training backend
+    x = np.random.default_rng(3).uniform(-1, 1, (100, 32)).astype(np.float32)
+    y, _ = ae_forward_torch(torch.from_numpy(x), [torch.as_tensor(a) for a in m.get_weights()],
+                            list(m.spec.activations))
+    ref = ((y - torch.from_numpy(x)) ** 2).mean(1).numpy()
+    with ScoringServer(m, slots=256) as srv:
+        s, _ = srv.score(x)
+    np.testing.assert_allclose(s, ref, rtol=1e-4, atol=1e-6)
+
+
 def test_matches_fused_forward_kernel(cuda_device):
     from streamml.ops.serve import ScoringServer
     m = _model(cuda_device, normalizer=None)
