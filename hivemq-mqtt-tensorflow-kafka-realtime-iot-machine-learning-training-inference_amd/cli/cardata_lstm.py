@@ -104,10 +104,17 @@ def _predict(ns, servers, cfg, rows, model, result_topic):
     xw = xw[b0:b0 + ns.predict_take * ns.batch_size]
     cbs = [KafkaPredictionSink(ns.batch_size, result_topic, servers, cfg)] if result_topic else []
     engine = ns.predict_engine
+    # the forecaster emits each window's LAST step only: it serves stacks whose output is one
+    # step per window (the reference at look_back 1); a sequence-output stack (RepeatVector(R)
+    # with R > 1) keeps the batch engine under "auto", so both engines return the same shape
+    shape = np.shape(model.predict(np.zeros((1, ns.look_back, model.features), np.float32)))[1:]
+    one_step = int(np.prod(shape)) == model.features
     if engine == "auto":
-        engine = "persistent" if model.device.type == "cuda" else "batch"
+        engine = "persistent" if model.device.type == "cuda" and one_step else "batch"
     if engine == "persistent":
         out = _predict_persistent(model, rows, b0, len(xw))
+        if one_step:
+            out = out.reshape((len(out),) + tuple(shape))
         for cb in cbs:   # the reference OutputCallback, per batch_size forecasts
             cb.set_model(model)
             for bi, s0 in enumerate(range(0, len(out), ns.batch_size)):

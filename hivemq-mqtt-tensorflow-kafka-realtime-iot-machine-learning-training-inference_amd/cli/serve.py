@@ -17,9 +17,11 @@ only (cardata-v3.py:46) and writes reconstructions (cardata-v3.py:243-249). Here
   reconstruction with ``--emit both`` (what the reference streams).
 
 ``--low-latency``: the whole per-event path runs in one C++ thread per replica
-(:class:`streamml.kafka.scoreloop.LowLatencyScorer`): long-poll fetch -> Avro decode ->
-the persistent GPU scorer (:class:`streamml.ops.serve.ScoringServer`, no launch per
-event) -> the same result records formatted in C++ -> one produce per fetch -> commit.
+(:class:`streamml.kafka.scoreloop.LowLatencyScorer`): long-poll fetch -> Avro decode (or,
+``--source-format json``, the bridge's JSON events) -> the persistent GPU scorer
+(:class:`streamml.ops.serve.ScoringServer`; ``--model lstm``: the per-car forecaster
+:class:`~streamml.ops.serve.LSTMScoringServer`, car key -> device slot in C++), no launch
+per event -> the same result records formatted in C++ -> one produce per fetch -> commit.
 
 Replica identity comes from ``--replica-index/--replicas``, else torchrun's
 ``RANK/WORLD_SIZE``, else ``REPLICA_INDEX/REPLICAS`` (a StatefulSet ordinal), else 0/1.
@@ -80,16 +82,24 @@ def _flags(p) -> None:
                    help="lstm: per-car forecaster (look_back events per car on the device, each event "
                         "scored against the car's previous forecast; lstm_serve.hip)")
     p.add_argument("--max-keys", type=int, default=200_000, help="--model lstm: car keys held on the device")
+    p.add_argument("--source-format", choices=["avro", "json"], default="avro",
+                   help="--low-latency: json follows the MQTT bridge's JSON events (sensor-data, KSQL "
+                        "SENSOR_DATA_S) directly instead of the Avro stream")
 
 
 def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary) -> int:
+    """One C++ loop per replica over the resident scorer: the autoencoder's, or -- ``--model
+    lstm`` -- the per-car forecaster, whose car key -> device slot map lives in the loop
+    (cardata-v2.py:220-273 streams one LSTM prediction per event)."""
     from ..kafka.scoreloop import LowLatencyScorer
     from ..obs.metrics import ENGINE
-    from ..ops.serve import ScoringServer
+    from ..ops.serve import LSTMScoringServer, ScoringServer
 
     if model.device.type != "cuda":
         raise SystemExit("--low-latency needs a ROCm device (the persistent scorer)")
-    with ScoringServer(model, threshold=ns.threshold) as srv:
+    scorer = (LSTMScoringServer(model, nkeys=ns.max_keys, threshold=ns.threshold) if ns.model == "lstm"
+              else ScoringServer(model, threshold=ns.threshold))
+    with scorer as srv:
         starts = None
         if ns.from_beginning:
             from ..kafka import KafkaClient
@@ -98,10 +108,12 @@ def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary) -> 
         loop = LowLatencyScorer(servers, ns.topic, ns.result_topic, mine, srv, schema=ns.schema, group=ns.group,
                                 starts=starts, result_partitions=[p % result_parts for p in mine],
                                 emit_recon=ns.emit == "both", config=cfg, max_batch=min(ns.max_batch, 4096),
-                                max_wait_ms=ns.max_wait_ms, spin_us=ns.spin_us)
+                                max_wait_ms=ns.max_wait_ms, spin_us=ns.spin_us, source_format=ns.source_format)
         st = loop.run(max_events=ns.max_events, idle_timeout_s=ns.idle_timeout)
     ENGINE.infer_rows.inc(st["events"], model=model.name)
     ENGINE.anomaly_events.inc(st["anomalies"], model=model.name)
+    if ns.model == "lstm":
+        summary.update(model="lstm", keys=st["keys"])
     summary.update(events=st["events"], anomalies=st["anomalies"], skipped=st["skipped"],
                    events_per_s=st["events"] / st["wall_s"] if st["wall_s"] > 0 else 0.0, low_latency=True,
                    stages_s={k: st[k] for k in ("fetch_s", "decode_s", "score_s", "format_s", "produce_s",
@@ -160,8 +172,8 @@ def main(argv: Sequence[str]) -> int:
         print(json.dumps(summary), flush=True)
         return 0
 
-    if ns.low_latency and ns.model == "lstm":
-        raise SystemExit("--low-latency serves the autoencoder; --model lstm runs its own persistent forecaster")
+    if ns.source_format == "json" and not ns.low_latency:
+        raise SystemExit("--source-format json needs --low-latency (the C++ loop decodes the JSON events)")
     if ns.low_latency:
         return _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary)
     forecaster, key_ids = None, {}

@@ -20,8 +20,14 @@ struct SmlScorerApi {
   int (*infer)(void* ctx, const float* rows, int k, float* scores, uint32_t* flags, float* recon,
                double timeout_s);
   const char* (*last_error)(void* ctx);
+  // v2: keyed scorers (the LSTM forecaster: per-key windows on the device).  nkeys > 0
+  // means every row needs a key in [0, nkeys) and infer_keyed must be used; recon then
+  // receives each key's next-event forecast, flags 2 = the key has no previous forecast.
+  int64_t nkeys;
+  int (*infer_keyed)(void* ctx, const float* rows, const uint32_t* keys, int k, float* scores, uint32_t* flags,
+                     float* recon, double timeout_s);
 };
 
 }  // extern "C"
 
-#define SML_SCORER_API_VERSION 1u
+#define SML_SCORER_API_VERSION 2u

@@ -9,6 +9,7 @@
 #include "avro.h"
 #include "feed.h"
 #include "format.h"
+#include "jsonrow.h"
 #include "scoreloop.h"
 #include "h5.h"
 #include "kafka.h"
@@ -386,8 +387,9 @@ PYBIND11_MODULE(_io, m) {
   // native ingest feed: worker threads decode Kafka records straight into caller slabs
   // ---- low-latency streaming scorer (scoreloop.h) ----
   struct EchoScorer {   // CPU stand-in for the GPU scorer (tests): score = mean(x^2), recon = x / 2
-    SmlScorerApi api{};
+    SmlScorerApi api{};  // keyed (nkeys > 0): score = the row's key slot, flag 2 on a slot's first event
     float thr;
+    std::vector<uint8_t> seen;
     static int infer(void* ctx, const float* rows, int k, float* scores, uint32_t* flags, float* recon, double) {
       auto* self = static_cast<EchoScorer*>(ctx);
       const int D = self->api.dim;
@@ -403,19 +405,34 @@ PYBIND11_MODULE(_io, m) {
       }
       return 0;
     }
+    static int infer_keyed(void* ctx, const float* rows, const uint32_t* keys, int k, float* scores,
+                           uint32_t* flags, float* recon, double t) {
+      auto* self = static_cast<EchoScorer*>(ctx);
+      infer(ctx, rows, k, scores, flags, recon, t);
+      for (int i = 0; i < k; ++i) {
+        if ((int64_t)keys[i] >= self->api.nkeys) return 1;
+        scores[i] = (float)keys[i];
+        flags[i] = self->seen[keys[i]] ? 0u : 2u;
+        self->seen[keys[i]] = 1;
+      }
+      return 0;
+    }
   };
   py::class_<EchoScorer>(m, "EchoScorer")
-      .def(py::init([](int dim, float threshold) {
+      .def(py::init([](int dim, float threshold, int64_t nkeys) {
              auto* e = new EchoScorer();
              e->api.version = SML_SCORER_API_VERSION;
              e->api.dim = dim;
              e->api.ctx = e;
              e->api.infer = &EchoScorer::infer;
              e->api.last_error = nullptr;
+             e->api.nkeys = nkeys;
+             e->api.infer_keyed = nkeys > 0 ? &EchoScorer::infer_keyed : nullptr;
+             e->seen.assign((size_t)std::max<int64_t>(nkeys, 0), 0);
              e->thr = threshold;
              return e;
            }),
-           py::arg("dim"), py::arg("threshold") = 5.0f)
+           py::arg("dim"), py::arg("threshold") = 5.0f, py::arg("nkeys") = 0)
       .def("c_api", [](EchoScorer& e) { return reinterpret_cast<uintptr_t>(&e.api); });
   py::class_<serve::ScoreLoop>(m, "ScoreLoop")
       .def(py::init([](const std::string& bootstrap, const std::string& client_id, const std::string& mech,
@@ -424,7 +441,8 @@ PYBIND11_MODULE(_io, m) {
                        std::vector<int> partitions, std::vector<int64_t> starts, std::vector<int> result_partitions,
                        std::vector<int> feature_fields, bool framing, bool emit_recon, int max_batch,
                        int32_t max_bytes, int32_t max_wait_ms, double commit_interval_s, bool record_latency,
-                       uintptr_t api, int spin_us) {
+                       uintptr_t api, int spin_us, std::vector<std::pair<std::string, int>> json_columns,
+                       const std::string& json_stamp) {
              kafka::ClientConfig c;
              c.client_id = client_id;
              c.sasl_mechanism = mech;
@@ -447,6 +465,8 @@ PYBIND11_MODULE(_io, m) {
              lc.max_wait_ms = max_wait_ms;
              lc.commit_interval_s = commit_interval_s;
              lc.record_latency = record_latency;
+             lc.json_columns = std::move(json_columns);
+             lc.json_stamp = json_stamp;
              return new serve::ScoreLoop(bootstrap, c, fields_from_py(fields), lc,
                                          reinterpret_cast<const SmlScorerApi*>(api));
            }),
@@ -455,7 +475,8 @@ PYBIND11_MODULE(_io, m) {
            py::arg("result_topic"), py::arg("group"), py::arg("partitions"), py::arg("starts"),
            py::arg("result_partitions"), py::arg("feature_fields"), py::arg("framing"), py::arg("emit_recon"),
            py::arg("max_batch"), py::arg("max_bytes"), py::arg("max_wait_ms"), py::arg("commit_interval_s"),
-           py::arg("record_latency"), py::arg("scorer_api"), py::arg("spin_us") = 0)
+           py::arg("record_latency"), py::arg("scorer_api"), py::arg("spin_us") = 0,
+           py::arg("json_columns") = std::vector<std::pair<std::string, int>>{}, py::arg("json_stamp") = "")
       .def("run",
            [](serve::ScoreLoop& l, int64_t max_events, double idle_timeout_s) {
              serve::LoopStats st;
@@ -478,6 +499,7 @@ PYBIND11_MODULE(_io, m) {
              d["produce_s"] = st.produce_s;
              d["commit_s"] = st.commit_s;
              d["wall_s"] = st.wall_s;
+             d["keys"] = st.keys;
              return d;
            },
            py::arg("max_events") = 0, py::arg("idle_timeout_s") = -1.0)
@@ -511,6 +533,39 @@ PYBIND11_MODULE(_io, m) {
         py::arg("keys") = py::none(), py::arg("qps") = 10000.0, py::arg("spin_us") = 0,
         "append records one produce request each at `qps`; -> steady-clock send time (ns) per record");
   m.def("steady_ns", &serve::steady_ns);
+
+  // ---- JSON car-event records (jsonrow.h): the bridge's sensor-data / KSQL SENSOR_DATA_S ----
+  m.def("json_canonical", &jsonrow::canonical, py::arg("key"));
+  m.def("json_rows",
+        [](const py::bytes& values, std::vector<int64_t> offs, std::vector<std::pair<std::string, int>> columns,
+           const std::string& label_key, const std::string& stamp_key) {
+          const jsonrow::Plan plan(columns, label_key, stamp_key);
+          std::string_view v(values);
+          const ssize_t n = offs.empty() ? 0 : (ssize_t)offs.size() - 1;
+          const int F = plan.width();
+          py::array_t<float> rows(std::vector<ssize_t>{n, F});
+          py::array_t<uint8_t> labels(n), ok(n);
+          py::array_t<int64_t> stamps(n);
+          float* pr = rows.mutable_data();
+          uint8_t* pl = labels.mutable_data();
+          uint8_t* po = ok.mutable_data();
+          int64_t* ps = stamps.mutable_data();
+          {
+            py::gil_scoped_release nogil;
+            for (ssize_t i = 0; i < n; ++i) {
+              const int64_t a = offs[(size_t)i], b = offs[(size_t)i + 1];
+              if (a < 0 || b < a || (size_t)b > v.size()) throw std::out_of_range("json_rows: bad offsets");
+              po[i] = plan.decode(reinterpret_cast<const uint8_t*>(v.data()) + a, (size_t)(b - a), pr + i * F,
+                                  pl + i, ps + i)
+                          ? 1
+                          : 0;
+            }
+          }
+          return py::make_tuple(rows, labels, stamps, ok);
+        },
+        py::arg("values"), py::arg("offsets"), py::arg("columns"), py::arg("label_key") = "",
+        py::arg("stamp_key") = "",
+        "JSON records values[offs[i]:offs[i+1]] -> (rows [n, F] float32 (NaN = missing), label codes, stamps, ok)");
 
   // ---- result-record formatting (format.h) ----
   m.def("array2string_f32",
@@ -887,6 +942,10 @@ PYBIND11_MODULE(_io, m) {
           if (d.contains("lo")) c.lo = d["lo"].cast<std::vector<double>>();
           if (d.contains("hi")) c.hi = d["hi"].cast<std::vector<double>>();
           if (d.contains("is_int")) c.is_int = d["is_int"].cast<std::vector<int>>();
+          if (d.contains("paced")) c.paced = d["paced"].cast<bool>();
+          if (d.contains("start_at_unix")) c.start_at_unix = d["start_at_unix"].cast<double>();
+          if (d.contains("stamp_ns")) c.stamp_ns = d["stamp_ns"].cast<bool>();
+          if (d.contains("source_ips")) c.source_ips = d["source_ips"].cast<std::vector<std::string>>();
           mqtt::SimStats st;
           {
             py::gil_scoped_release rel;
@@ -899,6 +958,10 @@ PYBIND11_MODULE(_io, m) {
           out["acked"] = st.acked;
           out["publish_failed"] = st.publish_failed;
           out["elapsed_s"] = st.elapsed_s;
+          out["connect_s"] = st.connect_s;
+          out["publish_s"] = st.publish_s;
+          out["max_lag_ms"] = st.max_lag_ms;
+          out["late_10ms"] = st.late_10ms;
           return out;
         },
         py::arg("config"));

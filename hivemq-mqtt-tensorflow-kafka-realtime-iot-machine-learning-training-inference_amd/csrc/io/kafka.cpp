@@ -713,6 +713,118 @@ int64_t Client::fetch_raw(const std::string& topic, int partition, int64_t offse
   }
 }
 
+bool Client::same_leader(const std::string& topic, const std::vector<int>& partitions) {
+  std::lock_guard<std::mutex> g(mu_);
+  Connection* first = nullptr;
+  for (int p : partitions) {
+    Connection* c = &conn_for(topic, p);
+    if (first && c != first) return false;
+    first = c;
+  }
+  return true;
+}
+
+void Client::fetch_multi_raw(const std::string& topic, const std::vector<std::pair<int, int64_t>>& want,
+                             int32_t max_bytes, int32_t max_wait_ms, std::string& resp, std::vector<PartSlice>& parts) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (want.empty()) throw Error("kafka: fetch_multi_raw with no partitions");
+  for (int attempt = 0;; ++attempt) {
+    W w;
+    w.i32(-1);
+    w.i32(max_wait_ms);
+    w.i32(1);
+    w.i32(max_bytes);
+    w.i8(0);
+    w.arr(1);
+    w.str(topic);
+    w.arr((int32_t)want.size());
+    for (const auto& pw : want) {
+      w.i32(pw.first);
+      w.i64(pw.second);
+      w.i32(max_bytes);
+    }
+    size_t used = 0;
+    try {
+      used = call_into(conn_for(topic, want[0].first), API_FETCH, 4, w.s, resp);
+    } catch (const Error& e) {
+      if (attempt >= cfg_.max_retries) throw;
+      conns_.clear();
+      any_.reset();
+      refresh_metadata();
+      continue;
+    }
+    R r{reinterpret_cast<const uint8_t*>(resp.data()), used};
+    r.i32();
+    const int32_t nt = r.arr();
+    parts.assign(want.size(), PartSlice{});
+    bool retry = false;
+    for (int32_t t = 0; t < nt; ++t) {
+      r.str();
+      const int32_t np = r.arr();
+      for (int32_t k = 0; k < np; ++k) {
+        const int32_t p = r.i32();
+        const int16_t ec = r.i16();
+        const int64_t hwm = r.i64();
+        r.i64();
+        const int32_t naborted = r.i32();
+        for (int32_t a = 0; a < naborted; ++a) {
+          r.i64();
+          r.i64();
+        }
+        auto rec = r.bytes();
+        if (ec == E_NOT_LEADER) {
+          retry = true;
+          continue;
+        }
+        if (ec != E_NONE) throw Error("kafka: Fetch error " + std::to_string(ec) + " on partition " + std::to_string(p), ec);
+        for (size_t i = 0; i < want.size(); ++i)
+          if (want[i].first == p) {
+            parts[i].hwm = hwm;
+            parts[i].rec_off = rec.first ? (size_t)(rec.first - reinterpret_cast<const uint8_t*>(resp.data())) : 0;
+            parts[i].rec_len = rec.second;
+          }
+      }
+    }
+    if (retry && attempt < cfg_.max_retries) {
+      refresh_metadata();
+      continue;
+    }
+    if (retry) throw Error("kafka: Fetch error: not leader", E_NOT_LEADER);
+    return;
+  }
+}
+
+void Client::commit_multi(const std::string& group, const std::string& topic,
+                          const std::vector<std::pair<int, int64_t>>& offsets) {
+  if (offsets.empty()) return;
+  std::lock_guard<std::mutex> g(mu_);
+  W w;
+  w.str(group);
+  w.i32(-1);
+  w.str("");
+  w.i64(-1);
+  w.arr(1);
+  w.str(topic);
+  w.arr((int32_t)offsets.size());
+  for (const auto& po : offsets) {
+    w.i32(po.first);
+    w.i64(po.second);
+    w.nullstr();
+  }
+  const std::string resp = call(any_conn(), API_OFFSET_COMMIT, 2, w.s);
+  R r{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
+  const int32_t nt = r.arr();
+  for (int32_t t = 0; t < nt; ++t) {
+    r.str();
+    const int32_t np = r.arr();
+    for (int32_t k = 0; k < np; ++k) {
+      r.i32();
+      const int16_t ec = r.i16();
+      if (ec != E_NONE) throw Error("kafka: OffsetCommit error " + std::to_string(ec), ec);
+    }
+  }
+}
+
 int64_t Client::produce(const std::string& topic, int partition, const std::vector<Record>& recs, int16_t acks) {
   std::lock_guard<std::mutex> g(mu_);
   W w;
@@ -735,6 +847,48 @@ int64_t Client::produce(const std::string& topic, int partition, const std::vect
   const int64_t base = r.i64();
   if (ec != E_NONE) throw Error("kafka: Produce error " + std::to_string(ec), ec);
   return base;
+}
+
+void Client::produce_multi(const std::string& topic, const std::vector<std::pair<int, std::vector<Record>>>& parts,
+                           int16_t acks) {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::pair<Connection*, std::vector<size_t>>> by_leader;
+  for (size_t i = 0; i < parts.size(); ++i) {
+    if (parts[i].second.empty()) continue;
+    Connection* c = &conn_for(topic, parts[i].first);
+    auto it = std::find_if(by_leader.begin(), by_leader.end(), [&](const auto& e) { return e.first == c; });
+    if (it == by_leader.end()) by_leader.push_back({c, {i}});
+    else it->second.push_back(i);
+  }
+  for (const auto& lead : by_leader) {
+    W w;
+    w.nullstr();  // transactional id
+    w.i16(acks);
+    w.i32(cfg_.timeout_ms);
+    w.arr(1);
+    w.str(topic);
+    w.arr((int32_t)lead.second.size());
+    for (size_t i : lead.second) {
+      w.i32(parts[i].first);
+      w.bytes(encode_record_batch(0, parts[i].second));
+    }
+    const std::string resp = call(*lead.first, API_PRODUCE, 3, w.s);
+    if (acks == 0) continue;
+    R r{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
+    const int32_t nt = r.arr();
+    for (int32_t t = 0; t < nt; ++t) {
+      r.str();
+      const int32_t np = r.arr();
+      for (int32_t k = 0; k < np; ++k) {
+        const int32_t p = r.i32();
+        const int16_t ec = r.i16();
+        r.i64();
+        r.i64();   // log append time (v2+)
+        if (ec != E_NONE)
+          throw Error("kafka: Produce error " + std::to_string(ec) + " on partition " + std::to_string(p), ec);
+      }
+    }
+  }
 }
 
 void Client::commit(const std::string& group, const std::string& topic, int partition, int64_t offset) {

@@ -117,6 +117,24 @@ class Client {
   int64_t fetch_raw(const std::string& topic, int partition, int64_t offset, int32_t max_bytes,
                     int32_t max_wait_ms, std::string& resp, size_t& rec_off, size_t& rec_len);
   int64_t produce(const std::string& topic, int partition, const std::vector<Record>& recs, int16_t acks = 1);
+  // Fetch several partitions of one topic in ONE request (they must share a leader:
+  // same_leader()); a long poll returns as soon as ANY of them has records.  On return
+  // `parts[i]` holds (record-set offset, record-set length, high watermark) inside `resp`
+  // for the i-th requested (partition, offset).
+  struct PartSlice {
+    size_t rec_off = 0, rec_len = 0;
+    int64_t hwm = -1;
+  };
+  void fetch_multi_raw(const std::string& topic, const std::vector<std::pair<int, int64_t>>& want, int32_t max_bytes,
+                       int32_t max_wait_ms, std::string& resp, std::vector<PartSlice>& parts);
+  bool same_leader(const std::string& topic, const std::vector<int>& partitions);
+  // commit several partitions' offsets in one OffsetCommit request
+  void commit_multi(const std::string& group, const std::string& topic,
+                    const std::vector<std::pair<int, int64_t>>& offsets);
+  // Several partitions of one topic: ONE Produce request per partition leader carrying all
+  // of that leader's partitions (one round trip instead of one per partition).
+  void produce_multi(const std::string& topic, const std::vector<std::pair<int, std::vector<Record>>>& parts,
+                     int16_t acks = 1);
   void commit(const std::string& group, const std::string& topic, int partition, int64_t offset);
   int64_t committed(const std::string& group, const std::string& topic, int partition);
   // topic empty: all topics (replaces the cache); else that topic only (merged; on

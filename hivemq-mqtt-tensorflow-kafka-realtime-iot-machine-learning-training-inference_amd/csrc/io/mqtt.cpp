@@ -823,7 +823,7 @@ void Broker::bridge_loop() {
         break;
       }
       if (bq_.empty()) continue;
-      if ((int)bq_.size() < cfg_.bridge_batch && running_) {  // linger for a fuller batch
+      if (cfg_.bridge_linger_ms > 0 && (int)bq_.size() < cfg_.bridge_batch && running_) {  // linger for a fuller batch
         g.unlock();
         std::this_thread::sleep_for(std::chrono::milliseconds(cfg_.bridge_linger_ms));
         g.lock();
@@ -857,13 +857,18 @@ void Broker::bridge_loop() {
         groups[gk].push_back(std::move(rec));
         gmap[gk] = br.mapping;
       }
+      // one Produce request per topic (per partition leader) with all its partitions
+      std::map<std::string, std::vector<std::pair<int, std::vector<kafka::Record>>>> per_topic;
+      std::map<std::string, std::vector<std::pair<int, size_t>>> per_topic_counts;   // (mapping, records)
       for (auto& gr : groups) {
-        for (size_t off = 0; off < gr.second.size(); off += (size_t)cfg_.bridge_batch) {
-          const size_t e = std::min(gr.second.size(), off + (size_t)cfg_.bridge_batch);
-          std::vector<kafka::Record> part(gr.second.begin() + (long)off, gr.second.begin() + (long)e);
-          kc->produce(gr.first.first, gr.first.second, part, 1);
-          kafka_sent_ += part.size();
-          map_counts_[(size_t)gmap[gr.first]]->fetch_add(part.size());
+        per_topic_counts[gr.first.first].emplace_back(gmap[gr.first], gr.second.size());
+        per_topic[gr.first.first].emplace_back(gr.first.second, std::move(gr.second));
+      }
+      for (auto& pt : per_topic) {
+        kc->produce_multi(pt.first, pt.second, 1);
+        for (const auto& mc : per_topic_counts[pt.first]) {
+          map_counts_[(size_t)mc.first]->fetch_add(mc.second);
+          kafka_sent_ += mc.second;
         }
       }
     } catch (const std::exception&) {
@@ -954,7 +959,7 @@ bool Client::read_packet(Packet& pk, int timeout_ms) {
 
 int Client::connect(const std::string& host, int port, const std::string& client_id, int version,
                     uint16_t keepalive, bool clean, const std::string& username, const std::string& password,
-                    int timeout_ms) {
+                    int timeout_ms, const std::string& source_ip) {
   if (version != 4 && version != 5) throw Error("mqtt: version must be 4 (3.1.1) or 5");
   if (fd_ >= 0) disconnect();
   addrinfo hints{}, *res = nullptr;
@@ -963,6 +968,24 @@ int Client::connect(const std::string& host, int port, const std::string& client
   if (::getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) != 0 || !res)
     throw Error("mqtt: cannot resolve " + host);
   fd_ = ::socket(res->ai_family, res->ai_socktype, 0);
+  if (fd_ < 0) {
+    ::freeaddrinfo(res);
+    throw Error("mqtt: socket() failed (descriptor limit?)");
+  }
+  if (!source_ip.empty()) {
+    int one = 1;   // port chosen at connect(): ports are then unique per 4-tuple, not per source
+    ::setsockopt(fd_, IPPROTO_IP, IP_BIND_ADDRESS_NO_PORT, &one, sizeof(one));
+    sockaddr_in src{};
+    src.sin_family = AF_INET;
+    src.sin_port = 0;
+    if (::inet_pton(AF_INET, source_ip.c_str(), &src.sin_addr) != 1 ||
+        ::bind(fd_, reinterpret_cast<sockaddr*>(&src), sizeof(src)) != 0) {
+      ::close(fd_);
+      fd_ = -1;
+      ::freeaddrinfo(res);
+      throw Error("mqtt: cannot bind source address " + source_ip);
+    }
+  }
   const int rc = ::connect(fd_, res->ai_addr, res->ai_addrlen);
   ::freeaddrinfo(res);
   if (rc != 0) {
@@ -1127,7 +1150,7 @@ std::string client_name(const SimConfig& c, uint64_t i) {
 }
 }  // namespace
 
-std::string car_payload_json(const SimConfig& cfg, uint64_t car, uint64_t seq, int64_t ts_ms) {
+std::string car_payload_json(const SimConfig& cfg, uint64_t car, uint64_t seq, int64_t ts_ms, int64_t sent_ns) {
   // each car has a stable operating point (seeded by car id) plus per-event noise
   uint64_t cst = cfg.seed * 0x100000001B3ull + car * 0x9E3779B97F4A7C15ull + 1;
   uint64_t est = cst ^ (seq * 0xD1B54A32D192ED03ull + 7);
@@ -1158,16 +1181,34 @@ std::string car_payload_json(const SimConfig& cfg, uint64_t car, uint64_t seq, i
   const bool fail = unif(est) < cfg.failure_rate;
   s += "\"failure_occurred\":\"";
   s += fail ? "true" : "false";
-  s += "\",\"timestamp\":" + std::to_string(ts_ms) + "}";
+  s += "\",\"timestamp\":" + std::to_string(ts_ms);
+  if (sent_ns >= 0) s += ",\"sent_ns\":" + std::to_string(sent_ns);
+  s += "}";
   return s;
 }
 
 SimStats simulate(const SimConfig& cfg, std::atomic<bool>* stop) {
   SimStats st;
-  std::atomic<uint64_t> connected{0}, cfail{0}, published{0}, acked{0}, pfail{0};
-  const auto t0 = std::chrono::steady_clock::now();
+  std::atomic<uint64_t> connected{0}, cfail{0}, published{0}, acked{0}, pfail{0}, late{0};
+  using Clock = std::chrono::steady_clock;
+  const auto t0 = Clock::now();
   const int T = std::max(1, std::min(cfg.threads, cfg.clients));
   std::vector<std::thread> th;
+  std::atomic<int> conn_done{0};
+  std::atomic<int64_t> conn_end_ns{0}, first_pub_ns{INT64_MAX}, last_pub_ns{0}, max_lag_ns{0};
+  auto ns_since = [&](Clock::time_point t) {
+    return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t - t0).count();
+  };
+  auto atomic_max = [](std::atomic<int64_t>& a, int64_t v) {
+    int64_t cur = a.load();
+    while (v > cur && !a.compare_exchange_weak(cur, v)) {
+    }
+  };
+  auto atomic_min = [](std::atomic<int64_t>& a, int64_t v) {
+    int64_t cur = a.load();
+    while (v < cur && !a.compare_exchange_weak(cur, v)) {
+    }
+  };
   for (int t = 0; t < T; ++t) {
     th.emplace_back([&, t] {
       const int lo = (int)((int64_t)cfg.clients * t / T), hi = (int)((int64_t)cfg.clients * (t + 1) / T);
@@ -1175,12 +1216,14 @@ SimStats simulate(const SimConfig& cfg, std::atomic<bool>* stop) {
       auto at = [&](double sec) { return t0 + std::chrono::microseconds((int64_t)(sec * 1e6)); };
       // connect stage: client i at ramp * i / clients
       for (int i = lo; i < hi; ++i) {
-        if (stop && *stop) return;
-        std::this_thread::sleep_until(at(cfg.ramp_s * i / std::max(1, cfg.clients)));
+        if (stop && *stop) break;
+        if (cfg.ramp_s > 0) std::this_thread::sleep_until(at(cfg.ramp_s * i / std::max(1, cfg.clients)));
         auto c = std::make_unique<Client>();
+        const std::string& src =
+            cfg.source_ips.empty() ? std::string() : cfg.source_ips[(size_t)i % cfg.source_ips.size()];
         try {
           if (c->connect(cfg.host, cfg.port, client_name(cfg, (uint64_t)i), cfg.version, 60, true, cfg.username,
-                         cfg.password) == 0) {
+                         cfg.password, 5000, src) == 0) {
             connected++;
             cl[(size_t)(i - lo)] = std::move(c);
             continue;
@@ -1189,20 +1232,47 @@ SimStats simulate(const SimConfig& cfg, std::atomic<bool>* stop) {
         }
         cfail++;
       }
-      // publish stage: message k of client i at ramp * i / clients + k * interval (+ connect ramp)
-      const double base = cfg.ramp_s;
+      atomic_max(conn_end_ns, ns_since(Clock::now()));
+      Clock::time_point pub0 = t0 + std::chrono::microseconds((int64_t)(cfg.ramp_s * 1e6));
+      if (cfg.paced) {   // every thread of this process connected, then one common start
+        conn_done++;
+        while (conn_done.load() < T && !(stop && *stop)) std::this_thread::sleep_for(std::chrono::microseconds(200));
+        pub0 = t0 + std::chrono::nanoseconds(conn_end_ns.load()) + std::chrono::milliseconds(20);
+        if (cfg.start_at_unix > 0) {
+          const double now_unix = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+          pub0 = std::max(pub0, Clock::now() + std::chrono::microseconds((int64_t)((cfg.start_at_unix - now_unix) * 1e6)));
+        }
+      }
+      // publish stage: message k of client i at its offset + k * interval
       for (int k = 0; k < cfg.messages_per_client; ++k) {
         for (int i = lo; i < hi; ++i) {
           if (stop && *stop) return;
           Client* c = cl[(size_t)(i - lo)].get();
           if (!c || !c->connected()) continue;
-          std::this_thread::sleep_until(at(base + cfg.ramp_s * i / std::max(1, cfg.clients) + k * cfg.interval_s));
+          const double off = cfg.paced ? cfg.interval_s * (i + 0.5) / std::max(1, cfg.clients)
+                                       : cfg.ramp_s * i / std::max(1, cfg.clients);
+          const auto due = pub0 + std::chrono::microseconds((int64_t)((off + k * cfg.interval_s) * 1e6));
+          std::this_thread::sleep_until(due);
+          const auto now = Clock::now();
+          if (cfg.paced) {
+            const int64_t lag = (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(now - due).count();
+            atomic_max(max_lag_ns, lag);
+            if (lag > 10000000) late++;
+          }
           const std::string name = client_name(cfg, (uint64_t)i);
+          const int64_t sent = cfg.stamp_ns
+                                   ? (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                         Clock::now().time_since_epoch())
+                                         .count()
+                                   : -1;
           try {
             c->publish(cfg.topic_prefix + name,
-                       car_payload_json(cfg, (uint64_t)(i + cfg.id_offset), (uint64_t)k, now_ms()), cfg.qos);
+                       car_payload_json(cfg, (uint64_t)(i + cfg.id_offset), (uint64_t)k, now_ms(), sent), cfg.qos);
             published++;
             if (cfg.qos > 0) acked++;
+            const int64_t tn = ns_since(Clock::now());
+            atomic_min(first_pub_ns, tn);
+            atomic_max(last_pub_ns, tn);
           } catch (const std::exception&) {
             pfail++;
           }
@@ -1221,7 +1291,11 @@ SimStats simulate(const SimConfig& cfg, std::atomic<bool>* stop) {
   st.published = published;
   st.acked = acked;
   st.publish_failed = pfail;
-  st.elapsed_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  st.elapsed_s = std::chrono::duration<double>(Clock::now() - t0).count();
+  st.connect_s = (double)conn_end_ns.load() * 1e-9;
+  st.publish_s = last_pub_ns.load() > first_pub_ns.load() ? (double)(last_pub_ns - first_pub_ns) * 1e-9 : 0.0;
+  st.max_lag_ms = (double)max_lag_ns.load() * 1e-6;
+  st.late_10ms = late;
   return st;
 }
 

@@ -179,9 +179,12 @@ class Client {
   Client() = default;
   ~Client();
   // returns the CONNACK reason / return code (0 = accepted); throws on transport errors
+  // source_ip: bind the socket to this local address first ("" = the kernel's choice); a
+  // fleet beyond the ~28k ephemeral ports of one (source, destination) pair spreads its
+  // connections over several loopback sources (127.0.0.x)
   int connect(const std::string& host, int port, const std::string& client_id, int version = 5,
               uint16_t keepalive = 60, bool clean = true, const std::string& username = "",
-              const std::string& password = "", int timeout_ms = 5000);
+              const std::string& password = "", int timeout_ms = 5000, const std::string& source_ip = "");
   // QoS 1/2 block until the handshake completes (PUBACK / PUBCOMP)
   void publish(const std::string& topic, const std::string& payload, int qos = 0, bool retain = false);
   std::vector<int> subscribe(const std::vector<std::pair<std::string, int>>& filters);
@@ -227,6 +230,15 @@ struct SimConfig {
   uint64_t seed = 0;
   double failure_rate = 0.01;  // P(failure_occurred = "true") per event
   std::string username, password;
+  // Paced mode (fleet benchmarks): every client connects first; publishing starts for all
+  // clients at once -- at start_at_unix (wall clock, shared by several simulator processes)
+  // or, if 0, when this process's last client is connected -- and client i's message k is
+  // due at start + interval * (i + 0.5) / clients + k * interval, so the fleet offers a
+  // steady clients / interval messages per second.
+  bool paced = false;
+  double start_at_unix = 0.0;
+  bool stamp_ns = false;             // add "sent_ns" (CLOCK_MONOTONIC ns at send) to each payload
+  std::vector<std::string> source_ips;   // client i binds source_ips[i % n] (empty: kernel's choice)
   // per-feature generator ranges (18 entries, SENSOR_DATA_S column order)
   std::vector<double> lo, hi;
   std::vector<int> is_int;
@@ -239,10 +251,14 @@ struct SimStats {
   uint64_t acked = 0;
   uint64_t publish_failed = 0;
   double elapsed_s = 0.0;
+  double connect_s = 0.0;            // first connect -> last client connected
+  double publish_s = 0.0;            // first publish -> last publish
+  double max_lag_ms = 0.0;           // paced: worst send delay behind schedule
+  uint64_t late_10ms = 0;            // paced: sends more than 10 ms behind schedule
 };
 
 SimStats simulate(const SimConfig& cfg, std::atomic<bool>* stop = nullptr);
-std::string car_payload_json(const SimConfig& cfg, uint64_t car, uint64_t seq, int64_t ts_ms);
+std::string car_payload_json(const SimConfig& cfg, uint64_t car, uint64_t seq, int64_t ts_ms, int64_t sent_ns = -1);
 
 }  // namespace mqtt
 }  // namespace sml

@@ -37,8 +37,13 @@ ScoreLoop::ScoreLoop(std::string bootstrap, kafka::ClientConfig ccfg, std::vecto
       decoder_(bootstrap, ccfg, std::move(fields), decoder_config(cfg_), {}) {
   if (!api_ || api_->version != SML_SCORER_API_VERSION || !api_->infer)
     throw std::invalid_argument("scoreloop: bad scorer API table");
-  if (api_->dim != decoder_.features())
+  if (api_->nkeys > 0 && !api_->infer_keyed) throw std::invalid_argument("scoreloop: keyed scorer without infer_keyed");
+  if (!cfg_.json_columns.empty()) {
+    json_ = std::make_unique<jsonrow::Plan>(cfg_.json_columns, "", cfg_.json_stamp);
+    if (json_->width() != api_->dim) throw std::invalid_argument("scoreloop: scorer dim != number of JSON columns");
+  } else if (api_->dim != decoder_.features()) {
     throw std::invalid_argument("scoreloop: scorer dim != number of feature fields");
+  }
   if (cfg_.partitions.empty() || cfg_.starts.size() != cfg_.partitions.size() ||
       cfg_.result_partitions.size() != cfg_.partitions.size())
     throw std::invalid_argument("scoreloop: partitions / starts / result_partitions mismatch");
@@ -53,45 +58,77 @@ LoopStats ScoreLoop::run(int64_t max_events, double idle_timeout_s) {
   kafka::Client cli(bootstrap_, ccfg_);
   const int D = api_->dim;
   const size_t np = cfg_.partitions.size();
+  // Owned partitions that share a leader are fetched in ONE request, whose long poll wakes
+  // on an append to any of them (and their results go out in one produce, their offsets in
+  // one commit); otherwise one partition per fetch, round robin, long-polling briefly only
+  // after a round that found nothing.
+  const bool multi = np > 1 && cli.same_leader(cfg_.topic, cfg_.partitions);
   LoopStats st;
   std::string resp;
-  size_t ro = 0, rl = 0;
+  std::vector<kafka::Client::PartSlice> slices;
+  std::vector<std::pair<int, int64_t>> want;
+  std::vector<size_t> grp;
   std::vector<float> rows, scores, recon;
-  std::vector<uint32_t> flags;
-  std::vector<int64_t> offs;
+  std::vector<uint32_t> flags, kids;
+  std::vector<int64_t> offs, stamps;
+  std::vector<int> src;   // owned-partition index of each decoded row
   std::vector<std::pair<const uint8_t*, int64_t>> keys;
-  std::vector<kafka::Record> out;
+  std::vector<std::pair<int, std::vector<kafka::Record>>> outp;
+  std::vector<int> res_slot(np, -1);
   std::vector<char> dirty(np, 0);
   const int64_t t_start = steady_ns();
   int64_t last_data = t_start, last_commit = t_start;
-  bool idle_round = false;
+  bool idle_round = false, round_any = false;
+  size_t rr = 0;
   auto commit_all = [&]() {
     if (cfg_.group.empty()) return;
     const int64_t t0 = steady_ns();
+    std::vector<std::pair<int, int64_t>> co;
     for (size_t i = 0; i < np; ++i)
       if (dirty[i]) {
-        cli.commit(cfg_.group, cfg_.topic, cfg_.partitions[i], pos_[i]);
+        co.emplace_back(cfg_.partitions[i], pos_[i]);
         dirty[i] = 0;
-        ++st.commits;
       }
+    if (!co.empty()) {
+      cli.commit_multi(cfg_.group, cfg_.topic, co);
+      st.commits += co.size();
+    }
     last_commit = steady_ns();
     st.commit_s += secs(t0, last_commit);
   };
   while (!stop_) {
-    bool any = false;
-    for (size_t pi = 0; pi < np && !stop_; ++pi) {
-      // one partition: always long-poll; several: long-poll (briefly) only after an empty round
-      const int32_t wait = np == 1 ? cfg_.max_wait_ms : (idle_round && pi == 0 ? std::min(cfg_.max_wait_ms, 2) : 0);
-      int64_t t0 = steady_ns();
-      cli.fetch_raw(cfg_.topic, cfg_.partitions[pi], pos_[pi], cfg_.max_bytes, wait, resp, ro, rl);
-      int64_t t1 = steady_ns();
-      st.fetch_s += secs(t0, t1);
-      ++st.fetches;
-      // decode every record at or past our position
-      rows.clear();
-      offs.clear();
-      keys.clear();
-      kafka::RecordSetCursor cur(reinterpret_cast<const uint8_t*>(resp.data()) + ro, rl);
+    grp.clear();
+    int32_t wait = cfg_.max_wait_ms;
+    if (multi || np == 1) {
+      for (size_t i = 0; i < np; ++i) grp.push_back(i);
+    } else {
+      grp.push_back(rr);
+      wait = idle_round && rr == 0 ? std::min(cfg_.max_wait_ms, 2) : 0;
+    }
+    want.clear();
+    for (size_t i : grp) want.emplace_back(cfg_.partitions[i], pos_[i]);
+    const int64_t t0 = steady_ns();
+    if (grp.size() == 1) {
+      slices.assign(1, kafka::Client::PartSlice{});
+      slices[0].hwm = cli.fetch_raw(cfg_.topic, want[0].first, want[0].second, cfg_.max_bytes, wait, resp,
+                                    slices[0].rec_off, slices[0].rec_len);
+    } else {
+      cli.fetch_multi_raw(cfg_.topic, want, cfg_.max_bytes, wait, resp, slices);
+    }
+    const int64_t t1 = steady_ns();
+    st.fetch_s += secs(t0, t1);
+    ++st.fetches;
+    // decode every record at or past our position, in partition order
+    rows.clear();
+    offs.clear();
+    keys.clear();
+    stamps.clear();
+    src.clear();
+    bool progress = false;
+    for (size_t gi = 0; gi < grp.size(); ++gi) {
+      const size_t pi = grp[gi];
+      kafka::RecordSetCursor cur(reinterpret_cast<const uint8_t*>(resp.data()) + slices[gi].rec_off,
+                                 slices[gi].rec_len);
       kafka::RecordView v;
       int64_t next = pos_[pi];
       while (cur.next(v)) {
@@ -99,78 +136,130 @@ LoopStats ScoreLoop::run(int64_t max_events, double idle_timeout_s) {
         next = v.offset + 1;
         rows.resize(rows.size() + (size_t)D);
         uint8_t lab = 0;
-        if (!decoder_.decode_row(v.value, (size_t)v.value_len, rows.data() + rows.size() - (size_t)D, &lab)) {
+        int64_t stamp = 0;
+        float* row = rows.data() + rows.size() - (size_t)D;
+        const bool ok = json_ ? json_->decode(v.value, (size_t)v.value_len, row, &lab, &stamp)
+                              : decoder_.decode_row(v.value, (size_t)v.value_len, row, &lab);
+        if (!ok) {
           rows.resize(rows.size() - (size_t)D);   // undecodable: skipped, not scored
           ++st.skipped;
           continue;
         }
+        stamps.push_back(stamp);
         offs.push_back(v.offset);
         keys.emplace_back(v.key, v.key_len);
+        src.push_back((int)pi);
       }
-      const int64_t t2 = steady_ns();
-      st.decode_s += secs(t1, t2);
-      if (next == pos_[pi]) {
-        ++st.empty_fetches;
-        continue;
+      if (next != pos_[pi]) {
+        pos_[pi] = next;
+        dirty[pi] = 1;
+        progress = true;
       }
-      any = true;
-      pos_[pi] = next;
-      dirty[pi] = 1;
-      const int k = (int)offs.size();
-      if (k > 0) {
-        scores.resize((size_t)k);
-        flags.resize((size_t)k);
-        if (cfg_.emit_recon) recon.resize((size_t)k * (size_t)D);
-        for (int b = 0; b < k; b += cfg_.max_batch) {
-          const int n = std::min(cfg_.max_batch, k - b);
-          if (api_->infer(api_->ctx, rows.data() + (size_t)b * D, n, scores.data() + b, flags.data() + b,
-                          cfg_.emit_recon ? recon.data() + (size_t)b * D : nullptr, 10.0) != 0)
-            throw std::runtime_error(std::string("scoreloop: scorer failed: ") +
-                                     (api_->last_error ? api_->last_error(api_->ctx) : "?"));
-        }
-        const int64_t t3 = steady_ns();
-        st.score_s += secs(t2, t3);
-        out.resize((size_t)k);
-        const int64_t now_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
-                                   std::chrono::system_clock::now().time_since_epoch())
-                                   .count();
+    }
+    const int64_t t2 = steady_ns();
+    st.decode_s += secs(t1, t2);
+    if (!progress) ++st.empty_fetches;
+    round_any |= progress;
+    const int k = (int)offs.size();
+    if (k > 0) {
+      scores.resize((size_t)k);
+      flags.resize((size_t)k);
+      if (cfg_.emit_recon) recon.resize((size_t)k * (size_t)D);
+      if (api_->nkeys > 0) {   // record key -> the key's device slot
+        kids.resize((size_t)k);
         for (int i = 0; i < k; ++i) {
-          kafka::Record& r = out[(size_t)i];
-          r.offset = i;
-          r.timestamp = now_ms;
-          r.key_null = keys[(size_t)i].second < 0;
-          if (r.key_null) r.key.clear();
-          else r.key.assign(reinterpret_cast<const char*>(keys[(size_t)i].first), (size_t)keys[(size_t)i].second);
-          r.value.clear();
-          fmt::score_record_json(keys[(size_t)i].first, keys[(size_t)i].second, cfg_.partitions[pi],
-                                 offs[(size_t)i], scores[(size_t)i], flags[(size_t)i] != 0,
-                                 cfg_.emit_recon ? recon.data() + (size_t)i * D : nullptr, D, r.value);
-          st.anomalies += flags[(size_t)i] != 0;
-        }
-        const int64_t t4 = steady_ns();
-        st.format_s += secs(t3, t4);
-        cli.produce(cfg_.result_topic, cfg_.result_partitions[pi], out, 1);
-        const int64_t t5 = steady_ns();
-        st.produce_s += secs(t4, t5);
-        if (cfg_.record_latency)
-          for (int i = 0; i < k; ++i) {   // kLatCols per event (scoreloop.h)
-            lat_.push_back(cfg_.partitions[pi]);
-            lat_.push_back(offs[(size_t)i]);
-            lat_.push_back(t5);
-            lat_.push_back(t1);
-            lat_.push_back(t3);
-            lat_.push_back(t4);
+          const auto& kv = keys[(size_t)i];
+          std::string key = kv.second < 0 ? std::string()
+                                          : std::string(reinterpret_cast<const char*>(kv.first), (size_t)kv.second);
+          auto it = key_ids_.find(key);
+          if (it == key_ids_.end()) {
+            if ((int64_t)key_ids_.size() >= api_->nkeys)
+              throw std::runtime_error("scoreloop: more distinct record keys than the scorer's " +
+                                       std::to_string(api_->nkeys) + " key slots");
+            it = key_ids_.emplace(std::move(key), (uint32_t)key_ids_.size()).first;
+            st.keys = key_ids_.size();
           }
-        st.events += (uint64_t)k;
-        ++st.batches;
+          kids[(size_t)i] = it->second;
+        }
       }
-      if (cfg_.commit_interval_s <= 0.0 || secs(last_commit, steady_ns()) >= cfg_.commit_interval_s) commit_all();
-      if (max_events > 0 && (int64_t)st.events >= max_events) stop_ = true;
+      for (int b = 0; b < k; b += cfg_.max_batch) {
+        const int n = std::min(cfg_.max_batch, k - b);
+        float* rc = cfg_.emit_recon ? recon.data() + (size_t)b * D : nullptr;
+        const int rc_err = api_->nkeys > 0
+                               ? api_->infer_keyed(api_->ctx, rows.data() + (size_t)b * D, kids.data() + b, n,
+                                                   scores.data() + b, flags.data() + b, rc, 10.0)
+                               : api_->infer(api_->ctx, rows.data() + (size_t)b * D, n, scores.data() + b,
+                                             flags.data() + b, rc, 10.0);
+        if (rc_err != 0)
+          throw std::runtime_error(std::string("scoreloop: scorer failed: ") +
+                                   (api_->last_error ? api_->last_error(api_->ctx) : "?"));
+      }
+      const int64_t t3 = steady_ns();
+      st.score_s += secs(t2, t3);
+      // result records, grouped by result partition (a source partition's order is kept)
+      for (auto& o : outp) o.second.clear();
+      const int64_t now_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                                 std::chrono::system_clock::now().time_since_epoch())
+                                 .count();
+      for (int i = 0; i < k; ++i) {
+        const int pi = src[(size_t)i];
+        if (res_slot[(size_t)pi] < 0) {   // first result for this source partition
+          const int rp = cfg_.result_partitions[(size_t)pi];
+          int slot = -1;
+          for (size_t q = 0; q < outp.size(); ++q)
+            if (outp[q].first == rp) slot = (int)q;
+          if (slot < 0) {
+            outp.emplace_back(rp, std::vector<kafka::Record>());
+            slot = (int)outp.size() - 1;
+          }
+          res_slot[(size_t)pi] = slot;
+        }
+        auto& vec = outp[(size_t)res_slot[(size_t)pi]].second;
+        vec.emplace_back();
+        kafka::Record& r = vec.back();
+        r.offset = (int64_t)vec.size() - 1;
+        r.timestamp = now_ms;
+        r.key_null = keys[(size_t)i].second < 0;
+        if (!r.key_null) r.key.assign(reinterpret_cast<const char*>(keys[(size_t)i].first), (size_t)keys[(size_t)i].second);
+        // flag 1 = anomaly; a keyed forecaster's flag 2 = no previous forecast (score NaN)
+        const bool anomaly = flags[(size_t)i] == 1;
+        fmt::score_record_json(keys[(size_t)i].first, keys[(size_t)i].second, cfg_.partitions[(size_t)pi],
+                               offs[(size_t)i], scores[(size_t)i], anomaly,
+                               cfg_.emit_recon ? recon.data() + (size_t)i * D : nullptr, D, r.value);
+        st.anomalies += anomaly;
+      }
+      const int64_t t4 = steady_ns();
+      st.format_s += secs(t3, t4);
+      if (outp.size() == 1) cli.produce(cfg_.result_topic, outp[0].first, outp[0].second, 1);
+      else cli.produce_multi(cfg_.result_topic, outp, 1);
+      const int64_t t5 = steady_ns();
+      st.produce_s += secs(t4, t5);
+      if (cfg_.record_latency)
+        for (int i = 0; i < k; ++i) {   // kLatCols per event (scoreloop.h)
+          lat_.push_back(cfg_.partitions[(size_t)src[(size_t)i]]);
+          lat_.push_back(offs[(size_t)i]);
+          lat_.push_back(t5);
+          lat_.push_back(t1);
+          lat_.push_back(t3);
+          lat_.push_back(t4);
+          lat_.push_back(stamps[(size_t)i]);
+        }
+      st.events += (uint64_t)k;
+      ++st.batches;
+    }
+    if (progress && (cfg_.commit_interval_s <= 0.0 || secs(last_commit, steady_ns()) >= cfg_.commit_interval_s))
+      commit_all();
+    if (max_events > 0 && (int64_t)st.events >= max_events) stop_ = true;
+    // end of a round: every owned partition fetched once
+    if (!multi && np > 1) {
+      rr = (rr + 1) % np;
+      if (rr != 0) continue;
     }
     const int64_t now = steady_ns();
-    if (any) last_data = now;
-    idle_round = !any;
-    if (!any && idle_timeout_s >= 0.0 && secs(last_data, now) >= idle_timeout_s) break;
+    if (round_any) last_data = now;
+    idle_round = !round_any;
+    round_any = false;
+    if (idle_round && idle_timeout_s >= 0.0 && secs(last_data, now) >= idle_timeout_s) break;
   }
   commit_all();
   st.wall_s = secs(t_start, steady_ns());

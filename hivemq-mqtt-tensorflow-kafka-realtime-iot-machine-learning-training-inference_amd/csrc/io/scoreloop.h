@@ -24,11 +24,15 @@
 #pragma once
 #include <atomic>
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "avro.h"
 #include "feed.h"
+#include "jsonrow.h"
 #include "kafka.h"
 #include "sml_scorer_api.h"
 
@@ -48,10 +52,16 @@ struct LoopConfig {
   int32_t max_wait_ms = 100;                // long-poll bound
   double commit_interval_s = 0.0;           // 0: commit after every produced batch
   bool record_latency = false;
+  // JSON source records (the MQTT bridge's `sensor-data`, KSQL SENSOR_DATA_S) instead of
+  // Avro: (key, model column) per feature, decoded by jsonrow::Plan; json_stamp names a
+  // numeric field copied into the latency records (the device simulator's send time)
+  std::vector<std::pair<std::string, int>> json_columns;
+  std::string json_stamp;
 };
 
 struct LoopStats {
   uint64_t events = 0, anomalies = 0, skipped = 0, batches = 0, fetches = 0, empty_fetches = 0, commits = 0;
+  uint64_t keys = 0;   // keyed (LSTM) scorer: distinct record keys given a device slot
   double fetch_s = 0, decode_s = 0, score_s = 0, format_s = 0, produce_s = 0, commit_s = 0, wall_s = 0;
 };
 
@@ -64,10 +74,10 @@ class ScoreLoop {
   LoopStats run(int64_t max_events, double idle_timeout_s);
   void stop() { stop_ = true; }
   std::vector<int64_t> positions() const;   // next offset per owned partition
-  // (partition, offset, visible_ns) per scored event when record_latency
-  // kLatCols int64 per scored event: partition, offset, steady-clock ns of the produce ack
-  // (result visible), of the fetch response, of the scores, of the formatted records
-  static constexpr int kLatCols = 6;
+  // kLatCols int64 per scored event when record_latency: partition, offset, steady-clock ns
+  // of the produce ack (result visible), of the fetch response, of the scores, of the
+  // formatted records, and the record's json_stamp field (0 without one)
+  static constexpr int kLatCols = 7;
   const std::vector<int64_t>& latency_records() const { return lat_; }
 
  private:
@@ -76,6 +86,10 @@ class ScoreLoop {
   LoopConfig cfg_;
   const SmlScorerApi* api_;
   feed::Feed decoder_;   // only its compiled decode plan is used (never started)
+  std::unique_ptr<jsonrow::Plan> json_;   // JSON source records
+  // keyed scorers: record key -> device slot, first come first served (the device keeps
+  // each slot's window); more distinct keys than the scorer's nkeys is an error
+  std::unordered_map<std::string, uint32_t> key_ids_;
   std::vector<int64_t> pos_;
   std::vector<int64_t> lat_;
   std::atomic<bool> stop_{false};

@@ -977,6 +977,27 @@ struct ServePy {
       return 1;
     }
   }
+  static int api_infer_keyed(void* ctx, const float* rows, const uint32_t* keys, int k, float* scores,
+                             uint32_t* flags, float* recon, double timeout_s) {
+    auto* self = static_cast<ServePy*>(ctx);
+    const int64_t nk = self->nkeys();
+    if (nk <= 0) {
+      self->err = "infer_keyed on a key-less scorer";
+      return 1;
+    }
+    for (int i = 0; i < k; ++i)
+      if ((int64_t)keys[i] >= nk) {
+        self->err = "key outside [0, nkeys)";
+        return 1;
+      }
+    try {
+      self->s->infer(rows, k, scores, flags, recon, timeout_s, keys);
+      return 0;
+    } catch (const std::exception& e) {
+      self->err = e.what();
+      return 1;
+    }
+  }
   static const char* api_error(void* ctx) { return static_cast<ServePy*>(ctx)->err.c_str(); }
   uintptr_t c_api() {
     api.version = SML_SCORER_API_VERSION;
@@ -984,6 +1005,8 @@ struct ServePy {
     api.ctx = this;
     api.infer = &ServePy::api_infer;
     api.last_error = &ServePy::api_error;
+    api.nkeys = nkeys();
+    api.infer_keyed = nkeys() > 0 ? &ServePy::api_infer_keyed : nullptr;
     return reinterpret_cast<uintptr_t>(&api);
   }
   ServePy(int device, int nslots, py::array_t<float, py::array::c_style | py::array::forcecast> weights,

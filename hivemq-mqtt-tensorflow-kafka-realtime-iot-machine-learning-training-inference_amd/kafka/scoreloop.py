@@ -33,18 +33,31 @@ def feature_fields(schema: str = "cardata-v1"):
     return codec, idx
 
 
+def json_columns():
+    """(key, model column) of every car feature for JSON source records (the C++ decoder
+    canonicalises keys: KSQL UPPERCASE, the simulator's snake_case and camelCase all match)."""
+    from ..data.cardata import FEATURES
+    return [(name, i) for i, name in enumerate(FEATURES)]
+
+
 class LowLatencyScorer:
-    """``scorer``: a :class:`~streamml.ops.serve.ScoringServer` (or anything with a
-    ``c_api()`` returning an ``SmlScorerApi`` table address, e.g. ``_io.EchoScorer`` in
-    CPU tests).  Keep the scorer alive while the loop runs.  ``spin_us`` > 0 busy-polls each
-    broker response that long before blocking (a blocked recv costs a thread wake-up)."""
+    """``scorer``: a :class:`~streamml.ops.serve.ScoringServer`, a
+    :class:`~streamml.ops.serve.LSTMScoringServer` (keyed: each record key -- the car -- gets
+    a device slot holding its window, mapped in C++ on first sight), or anything with a
+    ``c_api()`` returning an ``SmlScorerApi`` table address (``_io.EchoScorer`` in CPU
+    tests).  Keep the scorer alive while the loop runs.  ``spin_us`` > 0 busy-polls each
+    broker response that long before blocking (a blocked recv costs a thread wake-up).
+
+    ``source_format="json"`` follows JSON car events -- the MQTT bridge's ``sensor-data``
+    topic, KSQL's SENSOR_DATA_S -- instead of Confluent Avro; ``json_stamp`` names a numeric
+    field copied into the latency records (the device simulator's ``sent_ns``)."""
 
     def __init__(self, servers: str, topic: str, result_topic: str, partitions: Sequence[int], scorer,
                  schema: str = "cardata-v1", group: Optional[str] = None, starts: Optional[Sequence[int]] = None,
                  result_partitions: Optional[Sequence[int]] = None, emit_recon: bool = False,
                  config: Optional[Sequence[str]] = None, max_batch: int = 4096, max_bytes: int = 1 << 20,
                  max_wait_ms: int = 100, commit_interval_s: float = 0.0, record_latency: bool = False,
-                 framing: bool = True, spin_us: int = 0):
+                 framing: bool = True, spin_us: int = 0, source_format: str = "avro", json_stamp: str = ""):
         client = KafkaClient(servers, config)
         self.partitions = [int(p) for p in partitions]
         if starts is None:   # committed offset of the group, else the log start
@@ -52,6 +65,8 @@ class LowLatencyScorer:
             for p in self.partitions:
                 s = client.committed(group, topic, p) if group else -1
                 starts.append(s if s >= 0 else client.earliest(topic, p))
+        if source_format not in ("avro", "json"):
+            raise ValueError(f"source_format must be 'avro' or 'json', not {source_format!r}")
         if result_partitions is None:
             nres = max(1, client.partitions().get(result_topic, 1))
             result_partitions = [p % nres for p in self.partitions]
@@ -64,7 +79,8 @@ class LowLatencyScorer:
                                          self.partitions, [int(s) for s in starts],
                                          [int(r) for r in result_partitions], fields, framing, bool(emit_recon),
                                          int(max_batch), int(max_bytes), int(max_wait_ms), float(commit_interval_s),
-                                         bool(record_latency), int(api), int(spin_us))
+                                         bool(record_latency), int(api), int(spin_us),
+                                         json_columns() if source_format == "json" else [], str(json_stamp))
 
     def run(self, max_events: int = 0, idle_timeout_s: Optional[float] = None) -> dict:
         """Blocking (GIL released): until ``stop()``, ``max_events`` or ``idle_timeout_s``
@@ -78,9 +94,10 @@ class LowLatencyScorer:
         return list(self._loop.positions())
 
     def latency_records(self) -> np.ndarray:
-        """[n, 6] int64: (partition, offset, steady-clock ns the result became visible (produce
+        """[n, 7] int64: (partition, offset, steady-clock ns the result became visible (produce
         ack), of the fetch response that carried the event, of its score, of its formatted
-        record) -- the same clock as the broker's append times."""
+        record, the record's ``json_stamp`` field or 0) -- the same clock as the broker's
+        append times."""
         return self._loop.latency_records()
 
 

@@ -424,19 +424,29 @@ class LSTMPredictor:
         return hist
 
     @torch.no_grad()
-    def predict(self, x, batch_size: int = 1024, callbacks: Optional[Sequence[Callback]] = None) -> np.ndarray:
-        xs = np.asarray(x, np.float32)
+    def predict(self, x, batch_size: int = 1024, callbacks: Optional[Sequence[Callback]] = None):
+        """Forecasts of windows ``x`` [n, look_back, features].
+
+        A torch tensor already on the model's device stays there: batches are views of it and
+        the result is a device tensor (no host round trip).  Host input is copied to the
+        device once and the result comes back once, as numpy (Keras' return type).  Output
+        callbacks get each batch's last-step forecasts as numpy."""
+        on_dev = isinstance(x, torch.Tensor) and x.device == self.device
+        xs = x if on_dev else torch.as_tensor(np.asarray(x, np.float32), device=self.device)
         outs = []
         for bi, s in enumerate(range(0, len(xs), batch_size)):
-            xb = torch.as_tensor(xs[s:s + batch_size], device=self.device)
-            out = self.forward(xb).cpu().numpy()
+            out = self.forward(xs[s:s + batch_size])
             outs.append(out)
             for cb in callbacks or []:
                 cb.set_model(self)
-                cb.on_predict_batch_end(bi, {"outputs": out.reshape(len(out), -1, self.features)[:, -1]})
+                o = out.detach().float().cpu().numpy()
+                cb.on_predict_batch_end(bi, {"outputs": o.reshape(len(o), -1, self.features)[:, -1]})
         for cb in callbacks or []:
             cb.on_predict_end()
-        return np.concatenate(outs) if outs else np.zeros((0,), np.float32)
+        if not outs:
+            return torch.zeros((0,), device=self.device) if on_dev else np.zeros((0,), np.float32)
+        res = torch.cat(outs) if len(outs) > 1 else outs[0]
+        return res if on_dev else res.detach().cpu().numpy()
 
     # ------------------------------------------------------------------ persistence
     def weight_names(self) -> List[Tuple[str, List[str]]]:

@@ -327,17 +327,42 @@ class Scenario:
         return self.clients / self.interval_s
 
 
+def raise_nofile_limit() -> int:
+    """Raise this process's descriptor limit to its hard limit (a simulator agent or broker
+    node holds one socket per connected car); returns the new soft limit."""
+    import resource
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    if hard == resource.RLIM_INFINITY:
+        hard = 1 << 20
+    if soft < hard:
+        try:
+            resource.setrlimit(resource.RLIMIT_NOFILE, (hard, hard))
+            soft = hard
+        except (ValueError, OSError):
+            pass
+    return int(soft)
+
+
 def simulate(scenario: Scenario, host: Optional[str] = None, port: Optional[int] = None, threads: int = 4,
              seed: int = 0, failure_rate: float = 0.01, username: str = "", password: str = "",
-             id_offset: int = 0) -> Dict[str, float]:
+             id_offset: int = 0, paced: bool = False, start_at_unix: float = 0.0, stamp_ns: bool = False,
+             source_ips: Sequence[str] = ()) -> Dict[str, float]:
     """Run the fleet: connect every client, publish ``messages_per_client`` car payloads each.
 
     Payloads are JSON objects with the 18 sensor fields + ``failure_occurred`` of the KSQL
     stream ``SENSOR_DATA_S``; each car has a stable operating point plus per-event noise
     drawn inside the ranges of :data:`streamml.data.cardata.SYNTH_RANGES`.  ``id_offset``
     numbers this process's cars from there (several simulator agents share one fleet).
+
+    ``paced``: all clients connect first, then publish on a fixed schedule from one start
+    (``start_at_unix``, shared by several agent processes) so the fleet offers a steady
+    ``clients / interval_s`` msg/s; the stats report the connect time and how far sends fell
+    behind schedule.  ``stamp_ns`` adds the CLOCK_MONOTONIC send time (``sent_ns``) to each
+    payload for publish -> result latency.  ``source_ips`` spreads the clients' sockets over
+    several loopback source addresses (beyond ~28k connections to one broker port).
     """
     from ..data.cardata import FEATURES, INT_FEATURES, SYNTH_RANGES
+    raise_nofile_limit()
     cfg = {
         "host": host or scenario.broker[0], "port": int(port or scenario.broker[1]),
         "client_prefix": scenario.client_prefix, "id_digits": scenario.id_digits, "id_offset": int(id_offset),
@@ -347,6 +372,8 @@ def simulate(scenario: Scenario, host: Optional[str] = None, port: Optional[int]
         "seed": seed, "failure_rate": failure_rate, "username": username, "password": password,
         "lo": [float(SYNTH_RANGES[f][0]) for f in FEATURES], "hi": [float(SYNTH_RANGES[f][1]) for f in FEATURES],
         "is_int": [1 if f in INT_FEATURES else 0 for f in FEATURES],
+        "paced": bool(paced), "start_at_unix": float(start_at_unix), "stamp_ns": bool(stamp_ns),
+        "source_ips": [str(a) for a in source_ips],
     }
     st = _io().mqtt_simulate(cfg)
     # device-simulator agent counters (infrastructure/test-generator/devsim.json)

@@ -1,0 +1,170 @@
+"""End-to-end device-fleet run: MQTT cars -> broker nodes -> Kafka bridge -> GPU scorer -> Kafka.
+
+The reference's defining scale axis is "100000+ IoT connections" (``README.md:157``): the
+device simulator connects 100 000 MQTT 5 clients and publishes one car payload per client
+every 10 s (``infrastructure/test-generator/scenario.xml:13, 25, 48-49``: 10 000 msg/s) into
+a 5-node HiveMQ cluster whose Kafka extension forwards ``vehicles/sensor/data/#`` to the
+topic ``sensor-data`` (``infrastructure/hivemq/kafka-config.yaml:20-29``), from which the
+model scores each event (``python-scripts/.../cardata-v3.py:235-279``).
+
+:func:`run_fleet` stands the same pipeline up on one host:
+
+* ``brokers`` broker-node processes (:mod:`streamml.mqtt.node`; the C++ epoll broker +
+  bridge), each bridging into an in-process Kafka broker;
+* ``agents`` simulator processes, agent ``i`` connecting its share of the cars to node
+  ``i % brokers`` (each process has its own descriptor limit: 100 000 sockets on the
+  client side and 100 000 on the broker side never share one process);
+* in this process, one C++ scoring loop per scorer following ``sensor-data`` (the JSON
+  events, KSQL's SENSOR_DATA_S) with the persistent GPU scorer(s) -- the autoencoder, and
+  optionally the per-car LSTM forecaster -- writing a result record per event.
+
+Every payload carries its CLOCK_MONOTONIC send time (``sent_ns``); the loop records when
+each result became visible on the same clock, so the publish -> result latency is exact.
+Counts at every hop (published, broker incoming, bridged to Kafka, scored, results) show
+whether anything was dropped.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import threading
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _spawn(args: List[str], stdin=subprocess.DEVNULL) -> subprocess.Popen:
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    return subprocess.Popen([sys.executable, "-m", "streamml.mqtt.node"] + args, stdin=stdin,
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, cwd=ROOT, env=env, text=True)
+
+
+def _json_line(p: subprocess.Popen, timeout_s: float) -> dict:
+    """Next JSON line on a child's stdout (bounded wait)."""
+    box: Dict[str, object] = {}
+
+    def rd():
+        for ln in p.stdout:
+            if ln.startswith("{"):
+                box["d"] = json.loads(ln)
+                return
+
+    t = threading.Thread(target=rd, daemon=True)
+    t.start()
+    t.join(timeout_s)
+    if "d" not in box:
+        err = p.stderr.read() if p.poll() is not None else ""
+        raise RuntimeError(f"fleet child gave no JSON line within {timeout_s:.0f} s (rc={p.poll()}): {err[-800:]}")
+    return box["d"]   # type: ignore[return-value]
+
+
+def _pct(a: np.ndarray, q: float) -> Optional[float]:
+    return float(np.percentile(a, q)) if len(a) else None
+
+
+def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: int = 10, brokers: int = 2,
+              agents: int = 2, partitions: int = 10, threads: int = 4, qos: int = 0, lstm_scorer=None,
+              name: str = "fleet", start_delay_s: Optional[float] = None, sources_per_agent: int = 1,
+              max_wait_ms: int = 5, drain_timeout_s: float = 30.0) -> dict:
+    """Run ``clients`` cars x ``messages`` events at ``clients / interval_s`` msg/s end to end.
+
+    ``scorer``: a :class:`~streamml.ops.serve.ScoringServer` (or ``_io.EchoScorer`` on CPU);
+    ``lstm_scorer``: optionally a :class:`~streamml.ops.serve.LSTMScoringServer` scoring the
+    same events per car in a second loop.  Returns connections, connect time, offered and
+    achieved rates, per-hop counts, drops and publish -> result latency percentiles (us)."""
+    from ..kafka import fake_broker
+    from ..kafka.scoreloop import LowLatencyScorer
+
+    t_begin = time.time()
+    kb = fake_broker(name)
+    topic, results, lresults = "sensor-data", "model-predictions", "lstm-predictions"
+    for t in (topic, results) + ((lresults,) if lstm_scorer is not None else ()):
+        kb.create_topic(t, partitions)
+    total = clients * messages
+    nodes = [_spawn(["broker", "--kafka", f"127.0.0.1:{kb.port}"], stdin=subprocess.PIPE) for _ in range(brokers)]
+    agents_p: List[subprocess.Popen] = []
+    try:
+        ports = [_json_line(p, 60.0)["port"] for p in nodes]
+        loops, outs, ths = [], [], []
+        for sc, res in [(scorer, results)] + ([(lstm_scorer, lresults)] if lstm_scorer is not None else []):
+            lp = LowLatencyScorer(f"fake://{name}", topic, res, list(range(partitions)), sc, starts=[0] * partitions,
+                                  result_partitions=list(range(partitions)), max_wait_ms=max_wait_ms,
+                                  record_latency=True, source_format="json", json_stamp="sent_ns")
+            out: Dict[str, object] = {}
+            th = threading.Thread(target=lambda lp=lp, out=out: out.update(lp.run(max_events=total)), daemon=True)
+            th.start()
+            loops.append(lp)
+            outs.append(out)
+            ths.append(th)
+        per = [clients * i // agents for i in range(agents + 1)]
+        if start_delay_s is None:   # interpreter start + every agent's connects (~100 us each, serial per thread)
+            start_delay_s = 3.0 + 2.0 * (max(per[i + 1] - per[i] for i in range(agents)) / max(threads, 1)) * 150e-6
+        start_at = time.time() + start_delay_s
+        for i in range(agents):
+            n = per[i + 1] - per[i]
+            srcs = ",".join(f"127.0.{1 + i}.{1 + s}" for s in range(sources_per_agent)) if sources_per_agent > 1 else ""
+            agents_p.append(_spawn(["agent", "--port", str(ports[i % brokers]), "--clients", str(n), "--messages",
+                                    str(messages), "--interval", str(interval_s), "--qos", str(qos), "--threads",
+                                    str(threads), "--id-offset", str(per[i]), "--paced", "--start-at", repr(start_at),
+                                    "--stamp", "--source-ips", srcs, "--seed", "7"]))
+        run_s = start_delay_s + messages * interval_s + 120.0
+        sims = [_json_line(p, run_s) for p in agents_p]
+        for p in agents_p:
+            p.wait(30)
+        for p in nodes:       # stdin EOF: flush the bridge, print the node's counters
+            p.stdin.close()
+        nstats = [_json_line(p, 60.0) for p in nodes]
+        for p in nodes:
+            p.wait(30)
+        published = sum(int(s["published"]) for s in sims)
+        t_drain = time.time() + drain_timeout_s
+        while time.time() < t_drain and any(th.is_alive() for th in ths):
+            if all(int(o.get("events", 0) or 0) >= published for o in outs):
+                break
+            time.sleep(0.05)
+        for lp in loops:
+            lp.stop()
+        for th in ths:
+            th.join(10)
+    finally:
+        for p in agents_p + nodes:
+            if p.poll() is None:
+                p.kill()
+    connected = sum(int(s["connected"]) for s in sims)
+    out = {
+        "clients": clients, "connections": connected, "connect_failed": sum(int(s["connect_failed"]) for s in sims),
+        "brokers": brokers, "agents": agents, "kafka_partitions": partitions,
+        "connect_s": max(float(s["connect_s"]) for s in sims),
+        "offered_msgs_per_s": clients / interval_s, "messages_per_client": messages,
+        "published": published, "publish_failed": sum(int(s["publish_failed"]) for s in sims),
+        "publish_msgs_per_s": published / max(max(float(s["publish_s"]) for s in sims), 1e-9),
+        "max_send_lag_ms": max(float(s["max_lag_ms"]) for s in sims),
+        "sends_late_10ms": sum(int(s["late_10ms"]) for s in sims),
+        "broker_incoming": sum(int(s["incoming_publish"]) for s in nstats),
+        "bridged_to_kafka": sum(int(s["kafka_sent"]) for s in nstats),
+        "bridge_failed": sum(int(s["kafka_failed"]) for s in nstats),
+        "bridge_flushed": all(bool(s.get("flushed")) for s in nstats),
+        "wall_s": time.time() - t_begin,
+    }
+    for tag, lp, o in zip(("ae", "lstm"), loops, outs):
+        lat = lp.latency_records()
+        ok = lat[:, 6] > 0
+        us = (lat[ok, 2] - lat[ok, 6]) / 1e3
+        to_fetch = (lat[ok, 3] - lat[ok, 6]) / 1e3
+        vis = np.sort(lat[:, 2])
+        rate = (len(vis) - 1) / ((vis[-1] - vis[0]) * 1e-9) if len(vis) > 1 and vis[-1] > vis[0] else None
+        out[tag] = {"scored": int(o.get("events", 0) or 0), "skipped": int(o.get("skipped", 0) or 0),
+                    "keys": int(o.get("keys", 0) or 0), "anomalies": int(o.get("anomalies", 0) or 0),
+                    "results_msgs_per_s": rate,
+                    "publish_to_result_p50_us": _pct(us, 50), "publish_to_result_p99_us": _pct(us, 99),
+                    "publish_to_result_max_us": float(us.max()) if len(us) else None,
+                    "publish_to_fetched_p50_us": _pct(to_fetch, 50),
+                    "fetched_to_result_p50_us": _pct(us - to_fetch, 50)}
+    out["dropped"] = published - out["ae"]["scored"]
+    return out

@@ -151,3 +151,97 @@ def test_ref1_kernel_matches_general_kernel(cuda_device, monkeypatch, act):
     np.testing.assert_allclose(sa, sb, rtol=1e-4, atol=1e-6, equal_nan=True)
     agree = (fa == fb) | (np.abs(sa - 0.05) < 1e-4)   # a score within rounding of the threshold may flip
     assert agree.all()
+
+
+@pytest.mark.parametrize("T", [1, 3])
+def test_cli_predict_engines_return_the_same_shape(cuda_device, T):
+    """``--predict-engine auto`` picks the persistent forecaster only for one-step-output
+    stacks, and both engines return model.predict's shape."""
+    import types
+
+    from streamml.cli.cardata_lstm import _predict
+    m = LSTMPredictor.reference(look_back=T, device=cuda_device, seed=2)
+    rows = np.random.default_rng(5).uniform(-1, 1, size=(200, 18)).astype(np.float32)
+    outs = {}
+    for eng in ("auto", "batch", "persistent"):
+        ns = types.SimpleNamespace(look_back=T, skip=2, batch_size=10, predict_take=5, predict_engine=eng)
+        outs[eng] = _predict(ns, None, None, rows, m, None)
+    assert outs["auto"].shape == outs["batch"].shape
+    if T == 1:
+        assert outs["persistent"].shape == outs["batch"].shape == (50, 1, 18)
+        np.testing.assert_allclose(outs["persistent"], outs["batch"], rtol=0, atol=3e-2)
+
+
+def test_lstm_predict_keeps_device_input_on_device(cuda_device):
+    m = LSTMPredictor.two_layer(look_back=4, device=cuda_device, seed=1)
+    x = torch.rand(300, 4, 18, device=cuda_device)
+    out = m.predict(x, batch_size=128)
+    assert isinstance(out, torch.Tensor) and out.device == x.device
+    np.testing.assert_allclose(out.cpu().numpy(), m.predict(x.cpu().numpy(), batch_size=128), rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("stack,T", [("reference", 1), ("two_layer", 5)])
+def test_lstm_kafka_low_latency_path_matches_oracle(cuda_device, stack, T):
+    """``serve --model lstm --low-latency``'s path: Kafka (several cars interleaved over two
+    partitions) -> C++ loop (car key -> device slot) -> persistent forecaster -> result
+    records.  Every record's forecast (``reconstruction``) and score are checked against the
+    float64 oracle of that car's own window."""
+    import json
+
+    from streamml.data.avro import AvroCodec
+    from streamml.data.produce import encode_chunk
+    from streamml.kafka import KafkaClient, fake_broker
+    from streamml.kafka.scoreloop import LowLatencyScorer
+    from streamml.ops.serve import LSTMScoringServer
+
+    ctor = LSTMPredictor.two_layer if stack == "two_layer" else LSTMPredictor.reference
+    m = ctor(look_back=T, device=cuda_device, seed=6)
+    rng = np.random.default_rng(11 + T)
+    n, ncar = 240, 6
+    raw = rng.uniform(0, 40, size=(n, 18)).astype(np.float32)
+    cars = [f"vehicles/sensor/data/electric-vehicle-{int(c):05d}" for c in rng.integers(0, ncar, size=n)]
+    part = np.array([hash(c) % 2 for c in cars])        # a car's events stay in one partition
+    name = f"lstm-ll-{stack}-{T}"
+    b = fake_broker(name)
+    b.create_topic("S", 2)
+    b.create_topic("R", 2)
+    codec = AvroCodec("cardata-v1")
+    cli = KafkaClient(f"fake://{name}")
+    idx = {p: np.nonzero(part == p)[0] for p in (0, 1)}
+    for p in (0, 1):
+        buf, offs = encode_chunk(codec, raw[idx[p]].astype(np.float64), np.zeros(len(idx[p]), np.uint8))
+        cli.produce("S", p, [bytes(buf[offs[i]:offs[i + 1]]) for i in range(len(idx[p]))],
+                    keys=[cars[i].encode() for i in idx[p]])
+    thr = 0.05
+    with LSTMScoringServer(m, nkeys=16, threshold=thr) as srv:
+        loop = LowLatencyScorer(f"fake://{name}", "S", "R", [0, 1], srv, starts=[0, 0], emit_recon=True,
+                                max_wait_ms=5, max_batch=32)
+        st = loop.run(idle_timeout_s=0.3)
+    assert st["events"] == n and st["keys"] == len(set(cars))
+    sc, sh = normalize_affine()
+    xn = (raw.astype(np.float64) * np.float32(sc) + np.float32(sh)).astype(np.float32)
+    checked = 0
+    for p in (0, 1):
+        recs = [json.loads(r[2]) for r in b.read("R", p, 0)]
+        assert [r["offset"] for r in recs] == list(range(len(idx[p])))
+        hist, last = {}, {}
+        for r, i in zip(recs, idx[p]):
+            c = cars[i]
+            assert r["car"] == c
+            h = hist.setdefault(c, [])
+            if len(h) >= T:
+                want = float(np.mean((xn[i].astype(np.float64) - last[c]) ** 2))
+                assert abs(r["score"] - want) <= 2e-3 * max(want, 1e-3) + 1e-6, (r, want)
+                assert r["anomaly"] == (want > thr) or abs(want - thr) < 1e-5
+            else:
+                assert np.isnan(r["score"]) and r["anomaly"] is False
+            h.append(xn[i])
+            got = np.array(r["reconstruction"].strip("[]").split(), dtype=np.float64)
+            if len(h) >= T:
+                f = _forward(m, np.stack(h[-T:]))
+                assert np.all(np.abs(got - f) <= 2e-4 * np.abs(f) + 1e-4), (i, got, f)
+                last[c] = got   # the printed forecast (8 significant digits) is the next score's reference
+                checked += 1
+            else:
+                assert not got.any()
+    assert checked >= n - ncar * T

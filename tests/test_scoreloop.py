@@ -114,7 +114,7 @@ def test_long_poll_delivers_paced_events_promptly():
     th.join(30)
     assert not th.is_alive() and out["events"] == 400
     lat = loop.latency_records()
-    assert lat.shape == (400, 6)
+    assert lat.shape == (400, 7)
     d = (lat[np.argsort(lat[:, 1]), 2] - sent) / 1e3
     assert (d > 0).all()
     assert np.percentile(d, 50) < 5000, np.percentile(d, 50)   # us; ~100 us typical
@@ -148,3 +148,103 @@ def test_spin_mode_and_broker_append_times():
     assert (b.append_times("S", 0, n, 3) == -1).all()     # not appended yet
     recs = b.read("R", 0, 0, n)
     assert [json.loads(v)["offset"] for _, _, v in recs] == list(range(n))
+
+
+# ---- JSON source records (jsonrow.h) and keyed scorers --------------------------------------
+def _json_events(n, seed=0, stamp=False):
+    """Device-simulator payloads (the bridge's sensor-data records) + the float32 rows."""
+    from streamml.data.cardata import FEATURES
+    from streamml.mqtt import car_payload
+    vals, rows = [], []
+    for i in range(n):
+        v = car_payload(i % 17, i, 1000 + i, seed=seed)
+        d = json.loads(v)
+        if stamp:
+            d["sent_ns"] = 123456789012 + i
+            v = json.dumps(d).encode()
+        vals.append(v)
+        canon = {k.replace("_", "").lower(): x for k, x in d.items()}
+        rows.append([np.float32(canon[f.replace("_", "")]) for f in FEATURES])
+    return vals, np.asarray(rows, np.float32)
+
+
+def test_json_rows_matches_json_loads():
+    from streamml.kafka.scoreloop import json_columns
+    io = load_io()
+    vals, rows = _json_events(200, stamp=True)
+    # other spellings of the same columns, nulls, strings, nesting, junk
+    extra = [b'{"COOLANT_TEMP": "12.5", "tirePressure11": 31, "failure_occurred": "TRUE", "x": {"a": [1, {"b": 2}]}}',
+             b'{"speed": null, "FAILURE_OCCURRED": false, "s": "esc\\"aped", "sent_ns": 7}',
+             b'{}', b'not json', b'{"speed": 1,}', b'[1, 2]']
+    allv = vals + extra
+    offs = np.cumsum([0] + [len(v) for v in allv])
+    x, lab, st, ok = io.json_rows(b"".join(allv), offs.tolist(), json_columns(), "failure_occurred", "sent_ns")
+    assert ok.tolist() == [1] * 200 + [1, 1, 1, 0, 0, 0]
+    np.testing.assert_array_equal(x[:200], rows)
+    assert st[:200].tolist() == [123456789012 + i for i in range(200)]
+    want_lab = [{"false": 0, "true": 1}[json.loads(v)["failure_occurred"]] for v in vals]
+    assert lab[:200].tolist() == want_lab
+    a = x[200]
+    assert a[0] == np.float32(12.5) and a[9] == 31 and np.isnan(a[1]) and lab[200] == 1
+    assert np.isnan(x[201, 6]) and lab[201] == 0 and st[201] == 7
+    assert np.isnan(x[202]).all() and lab[202] == 2
+    assert io.json_canonical("Tire_Pressure_1_1") == "tirepressure11"
+
+
+def test_loop_follows_json_records_with_stamps():
+    name = "scoreloop-json"
+    b = fake_broker(name)
+    b.create_topic("sensor-data", 2)
+    b.create_topic("R", 2)
+    vals, rows = _json_events(120, stamp=True)
+    cli = KafkaClient(f"fake://{name}")
+    cli.produce("sensor-data", 0, vals[:70], keys=[f"vehicles/sensor/data/car{i % 5}".encode() for i in range(70)])
+    cli.produce("sensor-data", 1, vals[70:] + [b"{broken"], keys=None)
+    echo = load_io().EchoScorer(18, 1e9)
+    loop = LowLatencyScorer(f"fake://{name}", "sensor-data", "R", [0, 1], echo, starts=[0, 0], max_wait_ms=5,
+                            record_latency=True, source_format="json", json_stamp="sent_ns")
+    st = loop.run(idle_timeout_s=0.2)
+    assert st["events"] == 120 and st["skipped"] == 1
+    lat = loop.latency_records()
+    got = {(int(p), int(o)): int(s) for p, o, s in zip(lat[:, 0], lat[:, 1], lat[:, 6])}
+    assert got[(0, 5)] == 123456789012 + 5 and got[(1, 0)] == 123456789012 + 70
+    res = [json.loads(r[2]) for r in b.read("R", 0, 0) + b.read("R", 1, 0)]
+    by = {(d["partition"], d["offset"]): d for d in res}
+    for i in range(120):
+        p, o = (0, i) if i < 70 else (1, i - 70)
+        assert np.float32(by[(p, o)]["score"]) == _expected_score(rows[i])
+
+
+def test_keyed_scorer_maps_record_keys_to_stable_slots():
+    """A keyed scorer (the LSTM forecaster's API): each distinct record key gets one slot,
+    first come first served, stable across fetches and partitions; flag 2 (no previous
+    forecast) is not an anomaly; more keys than slots is an error."""
+    name = "scoreloop-keyed"
+    b = fake_broker(name)
+    b.create_topic("S", 2)
+    b.create_topic("R", 1)
+    _, vals, _, _ = _records(90, seed=4)
+    cli = KafkaClient(f"fake://{name}")
+    keys = [f"car{(i * 7) % 9}".encode() for i in range(90)]
+    cli.produce("S", 0, vals[:50], keys=keys[:50])
+    cli.produce("S", 1, vals[50:], keys=keys[50:])
+    echo = load_io().EchoScorer(18, 5.0, nkeys=9)   # score = the key's slot
+    loop = LowLatencyScorer(f"fake://{name}", "S", "R", [0, 1], echo, starts=[0, 0], result_partitions=[0, 0],
+                            max_wait_ms=5, max_batch=16)
+    st = loop.run(idle_timeout_s=0.2)
+    assert st["events"] == 90 and st["keys"] == 9 and st["anomalies"] == 0
+    res = [json.loads(r[2]) for r in b.read("R", 0, 0)]
+    slot = {}
+    for d in res:
+        slot.setdefault(d["car"], set()).add(d["score"])
+    assert all(len(v) == 1 for v in slot.values()) and len(slot) == 9
+    assert sorted(s.pop() for s in slot.values()) == list(range(9))
+    first = [d for d in res if d["partition"] == 0][:9]   # first sight of each key in partition 0
+    assert [d["score"] for d in first] == list(range(9))
+    # a tenth key does not fit
+    b.create_topic("S2", 1)
+    cli.produce("S2", 0, vals[:10], keys=[f"k{i}".encode() for i in range(10)])
+    loop2 = LowLatencyScorer(f"fake://{name}", "S2", "R", [0], load_io().EchoScorer(18, 5.0, nkeys=9), starts=[0],
+                             max_wait_ms=5)
+    with pytest.raises(Exception, match="key slots"):
+        loop2.run(idle_timeout_s=0.2)
