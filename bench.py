@@ -72,6 +72,12 @@ def parse():
                    help="side measurement: batch-32 training of this many independent models at once (0 = skip)")
     p.add_argument("--batch32-steps", type=int, default=20000,
                    help="steps per launch of the Keras batch-32 side measurement (0 = skip)")
+    p.add_argument("--mqtt-clients", type=int, default=100_000,
+                   help="side measurement: MQTT device fleet -> broker nodes -> Kafka -> GPU scorers, this many "
+                        "connected cars at one payload per car per --mqtt-interval (0 = skip)")
+    p.add_argument("--mqtt-interval", type=float, default=10.0, help="seconds between a car's payloads "
+                                                                      "(scenario.xml: 1/10s)")
+    p.add_argument("--mqtt-messages", type=int, default=2, help="payloads per car in the fleet measurement")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--settle-ms", type=float, default=100.0,
                    help="untimed steps before the warm-up until this much GPU time has passed (DPM clock settle)")
@@ -515,7 +521,7 @@ def main():
 
     if args.headline_only:
         for k in ("infer_events", "e2e_events", "batch32_steps", "dp_steps", "collective_iters", "fit_epochs",
-                  "fresh_steps", "fit_rows", "stream_rows", "lstm_steps"):
+                  "fresh_steps", "fit_rows", "stream_rows", "lstm_steps", "mqtt_clients"):
             setattr(args, k, 0)
 
     rows_per_s = gb * args.steps / elapsed
@@ -645,6 +651,17 @@ def main():
                                 device, args.infer_events, args.infer_repeats, args.qps)
             out.update({"lstm_infer_p50_us": lstm_infer.get("p50_us"), "lstm_infer_p99_us": lstm_infer.get("p99_us"),
                         "lstm_infer": lstm_infer})
+    # the reference's scale axis: 100 000 MQTT cars at 1 msg / 10 s -> broker nodes + Kafka
+    # bridge -> Kafka -> the persistent AE scorer and the per-car LSTM forecaster
+    if args.mqtt_clients > 0:
+        mq = ph.run("mqtt_e2e", 15 + args.mqtt_messages * args.mqtt_interval + 4e-5 * args.mqtt_clients,
+                    _bench_module("bench_mqtt").measure, device, clients=args.mqtt_clients,
+                    interval_s=args.mqtt_interval, messages=args.mqtt_messages, lstm=True)
+        out["mqtt_e2e"] = mq
+        if "ae" in mq:
+            out.update({"mqtt_connections": mq["connections"], "mqtt_dropped": mq["dropped"],
+                        "mqtt_publish_to_result_p50_us": mq["ae"]["publish_to_result_p50_us"],
+                        "mqtt_publish_to_result_p99_us": mq["ae"]["publish_to_result_p99_us"]})
     ph.finish()          # prints the ONE line (unless the watchdog already had to), releases parked ranks
     dp.shutdown()
 

@@ -19,7 +19,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def measure(device="cuda", clients=100_000, interval_s=10.0, messages=3, brokers=5, agents=6, partitions=10,
+def measure(device="cuda", clients=100_000, interval_s=10.0, messages=3, brokers=None, agents=None, partitions=10,
             threads=4, lstm=True, name="bench-fleet", sources_per_agent=1):
     """One fleet run; scorers built here (the AE at random init, the reference LSTM stack at
     look_back 1 -- cardata-v2.py:172-183 -- with one device slot per car)."""
@@ -58,8 +58,8 @@ def main():
     ap.add_argument("--clients", type=int, default=100_000)
     ap.add_argument("--interval", type=float, default=10.0)
     ap.add_argument("--messages", type=int, default=3)
-    ap.add_argument("--brokers", type=int, default=5)
-    ap.add_argument("--agents", type=int, default=6)
+    ap.add_argument("--brokers", type=int, default=None, help="default: as many as the descriptor limit needs")
+    ap.add_argument("--agents", type=int, default=None)
     ap.add_argument("--partitions", type=int, default=10)
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--sources-per-agent", type=int, default=1)

@@ -307,6 +307,7 @@ class LSTMPredictor:
         cbs = [hist] + list(callbacks or [])
         for cb in cbs:
             cb.set_model(self)
+            cb.on_train_begin()
         if isinstance(x, Stream):
             st = x.normalize() if normalize else x
             if self.device.type == "cuda":
@@ -397,6 +398,8 @@ class LSTMPredictor:
                 cb.on_epoch_end(epoch, logs)
             if self.stop_training:
                 break
+        for cb in cbs:
+            cb.on_train_end()
         return hist
 
     def _fit_persistent(self, xd, yd, n, nb, epochs, batch_size, verbose, cbs, hist, shuffle, seed, initial_epoch):
@@ -421,6 +424,8 @@ class LSTMPredictor:
                 cb.on_epoch_end(epoch, logs)
             if self.stop_training:
                 break
+        for cb in cbs:
+            cb.on_train_end()
         return hist
 
     @torch.no_grad()

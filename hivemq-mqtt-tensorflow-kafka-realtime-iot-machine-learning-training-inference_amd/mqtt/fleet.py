@@ -64,12 +64,23 @@ def _json_line(p: subprocess.Popen, timeout_s: float) -> dict:
     return box["d"]   # type: ignore[return-value]
 
 
+def plan_processes(clients: int, per_process_max: int = 20_000) -> int:
+    """Processes per side (broker nodes = simulator agents) for ``clients`` connections: each
+    process holds one socket per car, so its share must fit the descriptor hard limit (which
+    children inherit) and, per (source, broker port) pair, the ~28k loopback ephemeral ports."""
+    import resource
+    hard = resource.getrlimit(resource.RLIMIT_NOFILE)[1]
+    cap = per_process_max if hard == resource.RLIM_INFINITY else max(64, min(per_process_max, int(hard) - 256))
+    return max(1, -(-int(clients) // cap))
+
+
 def _pct(a: np.ndarray, q: float) -> Optional[float]:
     return float(np.percentile(a, q)) if len(a) else None
 
 
-def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: int = 10, brokers: int = 2,
-              agents: int = 2, partitions: int = 10, threads: int = 4, qos: int = 0, lstm_scorer=None,
+def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: int = 10,
+              brokers: Optional[int] = None, agents: Optional[int] = None, partitions: int = 10,
+              threads: int = 4, qos: int = 0, lstm_scorer=None,
               name: str = "fleet", start_delay_s: Optional[float] = None, sources_per_agent: int = 1,
               max_wait_ms: int = 5, drain_timeout_s: float = 30.0) -> dict:
     """Run ``clients`` cars x ``messages`` events at ``clients / interval_s`` msg/s end to end.
@@ -77,10 +88,15 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
     ``scorer``: a :class:`~streamml.ops.serve.ScoringServer` (or ``_io.EchoScorer`` on CPU);
     ``lstm_scorer``: optionally a :class:`~streamml.ops.serve.LSTMScoringServer` scoring the
     same events per car in a second loop.  Returns connections, connect time, offered and
-    achieved rates, per-hop counts, drops and publish -> result latency percentiles (us)."""
+    achieved rates, per-hop counts, drops and publish -> result latency percentiles (us).
+    ``brokers`` / ``agents`` default to (and are raised to) what the descriptor limit needs
+    (:func:`plan_processes`)."""
     from ..kafka import fake_broker
     from ..kafka.scoreloop import LowLatencyScorer
 
+    need = plan_processes(clients)
+    brokers = max(int(brokers or 0), need)
+    agents = max(int(agents or 0), brokers)
     t_begin = time.time()
     kb = fake_broker(name)
     topic, results, lresults = "sensor-data", "model-predictions", "lstm-predictions"

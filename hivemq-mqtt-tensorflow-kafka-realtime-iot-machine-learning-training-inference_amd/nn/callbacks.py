@@ -68,12 +68,42 @@ class ModelCheckpoint(Callback):
 
 
 class TensorBoard(Callback):
-    """Writes ``epoch_<metric>`` scalars to ``log_dir/train`` and ``log_dir/validation``
-    (the TF2 tag layout decoded from the reference logs)."""
+    """Keras ``TensorBoard`` (TF 2.0 semantics; Fraud-Detection-Autoencoder.ipynb:866,
+    confluent-tensorflow-io-kafka.py:54-55):
 
-    def __init__(self, log_dir: str = "./logs", **_ignored):
+    * ``epoch_<metric>`` scalars to ``log_dir/train`` and ``log_dir/validation`` (the TF2 tag
+      layout decoded from the reference logs, SURVEY.md 5.5);
+    * ``histogram_freq=k``: every k-th epoch, one histogram per weight, tagged as TF2 does
+      (``dense/kernel_0``: the weight name with ':' -> '_'), in ``train``;
+    * ``write_images``: with the histograms, each weight as a grayscale image
+      (``<weight>/image``; kernels [in, out], vectors one row);
+    * ``write_graph``: the ``keras`` model summary (the model-config JSON as a string tensor,
+      plugin ``graph_keras_model``), written once in ``train`` at step 0.  There is no
+      TensorFlow graph to serialise: the model runs as HIP kernels;
+    * ``update_freq`` other than ``'epoch'`` and a non-zero ``profile_batch`` are accepted
+      with a warning and not honoured: logs are epoch-level (metrics are read from the device
+      once per epoch), and kernels are profiled with rocprofv3 (``streamml.obs.profile``)."""
+
+    def __init__(self, log_dir: str = "./logs", histogram_freq: int = 0, write_graph: bool = True,
+                 write_images: bool = False, update_freq="epoch", profile_batch=None, embeddings_freq: int = 0,
+                 embeddings_metadata=None, **unknown):
+        import warnings
+        if unknown:
+            raise TypeError(f"TensorBoard: unexpected arguments {sorted(unknown)}")
         self.log_dir = log_dir
+        self.histogram_freq = int(histogram_freq or 0)
+        self.write_graph = bool(write_graph)
+        self.write_images = bool(write_images)
+        if update_freq != "epoch":
+            warnings.warn("TensorBoard(update_freq=...): logs are written per epoch (metrics are read from the "
+                          "device once per epoch)", stacklevel=2)
+        if profile_batch:   # TF's default (2) is left unset here: only an explicit request warns
+            warnings.warn("TensorBoard(profile_batch=...): not traced here; profile kernels with rocprofv3 "
+                          "(streamml.obs.profile)", stacklevel=2)
+        if embeddings_freq:
+            warnings.warn("TensorBoard(embeddings_freq=...): no embedding layers; ignored", stacklevel=2)
         self._w = {}
+        self._graph_written = False
 
     def _writer(self, split: str):
         from ..obs.tfevents import EventFileWriter
@@ -81,18 +111,46 @@ class TensorBoard(Callback):
             self._w[split] = EventFileWriter(os.path.join(self.log_dir, split))
         return self._w[split]
 
+    def on_train_begin(self, logs=None):
+        if self.write_graph and not self._graph_written and hasattr(self.model, "model_config"):
+            self._writer("train").text_tensor("keras", json.dumps(self.model.model_config()), 0,
+                                              plugin="graph_keras_model", content=b"1")
+            self._graph_written = True
+
     def on_epoch_end(self, epoch, logs=None):
         for k, v in (logs or {}).items():
             if k.startswith("val_"):
                 self._writer("validation").scalar("epoch_" + k[4:], v, epoch)
             elif not k.startswith("_"):
                 self._writer("train").scalar("epoch_" + k, v, epoch)
+        if self.histogram_freq and epoch % self.histogram_freq == 0:
+            w = self._writer("train")
+            for name, arr in named_weights(self.model):
+                tag = name.replace(":", "_")
+                w.histogram(tag, arr, epoch)
+                if self.write_images:
+                    a = np.asarray(arr)
+                    w.image(tag + "/image", a.reshape(1, -1) if a.ndim == 1 else a.reshape(a.shape[0], -1), epoch)
         for w in self._w.values():
             w.flush()
 
     def on_train_end(self, logs=None):
         for w in self._w.values():
             w.close()
+        self._w = {}
+
+
+def named_weights(model):
+    """[(Keras weight name, array)] of a model: 'dense/kernel:0', 'lstm/recurrent_kernel:0', ..."""
+    ws = [np.asarray(a) for a in (model.get_weights() if hasattr(model, "get_weights") else model.fp.get())]
+    names = getattr(model, "weight_names", None)
+    if callable(names):
+        names = [n for _, ns in names() for n in ns]
+    if names is None and hasattr(model, "_layer_names"):
+        names = [f"{ln}/{k}:0" for ln in model._layer_names() for k in ("kernel", "bias")]
+    if not names or len(names) != len(ws):
+        names = [f"weight_{i}:0" for i in range(len(ws))]
+    return list(zip(names, ws))
 
 
 class JSONLogger(Callback):

@@ -35,7 +35,7 @@ def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "4", "--warmup", "2", "--batch-per-gpu", "65536",
            "--dataset-rows", "262144", "--infer-events", "2000", "--infer-repeats", "1", "--e2e-events", "0",
-           "--lstm-steps", "0", "--batch32-steps", "2000", "--dump-params", dump]
+           "--lstm-steps", "0", "--batch32-steps", "2000", "--mqtt-clients", "0", "--dump-params", dump]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -75,7 +75,8 @@ def test_bench_n_ranks_rehearsal(tmp_path, cuda_device, n):
            "--dataset-rows", "262144", "--infer-events", "2000", "--infer-repeats", "1", "--e2e-events", "2000",
            "--batch32-steps", "2000", "--fleet-models", "64", "--dp-steps", "500", "--collective-iters", "50",
            "--fit-epochs", "2", "--fresh-steps", "2", "--fit-rows", "200000", "--stream-rows", "500000",
-           "--lstm-steps", "4", "--budget-s", "240", "--dump-params", dump]
+           "--lstm-steps", "4", "--mqtt-clients", "2000", "--mqtt-interval", "1", "--mqtt-messages", "2",
+           "--budget-s", "240", "--dump-params", dump]
     t0 = __import__("time").time()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     wall = __import__("time").time() - t0
@@ -92,9 +93,11 @@ def test_bench_n_ranks_rehearsal(tmp_path, cuda_device, n):
     assert dpr.get("replicas_identical") is True and dpr["global_batch"] == 32 * n, dpr
     ph = out["phase_s"]
     for k in ("infer", "small_allreduce", "keras_batch32_dp", "kafka_e2e", "keras_batch32", "fit_large_batch",
-              "fresh_rows", "fit_batch100", "stream_e2e", "lstm_seq50", "lstm_ref", "lstm_infer", "total_wall"):
+              "fresh_rows", "fit_batch100", "stream_e2e", "lstm_seq50", "lstm_ref", "lstm_infer", "mqtt_e2e",
+              "total_wall"):
         assert k in ph, (k, ph, out["budget"])
     assert not out["budget"]["skipped"], out["budget"]
+    assert out["mqtt_connections"] == 2000 and out["mqtt_dropped"] == 0, out["mqtt_e2e"]
     assert wall < 300
     ps = [np.load(f"{dump}.rank{i}.npy") for i in range(n)]
     for p in ps[1:]:
@@ -126,7 +129,7 @@ def test_bench_force_pg_rccl_world1(cuda_device):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "4", "--warmup", "2",
            "--batch-per-gpu", "65536", "--dataset-rows", "262144", "--infer-events", "1000", "--infer-repeats", "1",
            "--e2e-events", "0", "--lstm-steps", "0", "--batch32-steps", "2000", "--fit-rows", "0",
-           "--stream-rows", "0", "--dp-steps", "2000", "--collective-iters", "50"]
+           "--stream-rows", "0", "--dp-steps", "2000", "--collective-iters", "50", "--mqtt-clients", "0"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])

@@ -121,3 +121,44 @@ def test_grafana_dashboard_queries_exported_metrics():
     committed = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                             "deploy", "grafana", "streamml.json")))
     assert committed == dashboard.build()
+
+
+def test_tensorboard_histograms_images_and_keras_summary(tmp_path):
+    """TensorBoard(histogram_freq, write_images, write_graph) as TF2 writes them: per-weight
+    histograms tagged 'dense/kernel_0', weight images, the 'keras' model-config tensor
+    (plugin graph_keras_model, tensor before metadata as in the reference's own logs)."""
+    import json
+    import warnings
+
+    from streamml.models.autoencoder import Autoencoder
+    from streamml.nn.callbacks import TensorBoard
+    from streamml.obs.tfevents import read_values
+    m = Autoencoder(device="cpu", seed=1)
+    m.compile()
+    x = np.random.default_rng(0).uniform(-1, 1, (512, 18)).astype(np.float32)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")    # no profile_batch warning when it is 0
+        tb = TensorBoard(str(tmp_path), histogram_freq=2, write_images=True, profile_batch=0)
+    m.fit(x, epochs=3, batch_size=64, verbose=0, callbacks=[tb])
+    f = glob.glob(str(tmp_path / "train" / "events.out.tfevents.*"))[0]
+    vals = read_values(f)
+    keras = [p for _, t, k, p in vals if t == "keras"]
+    assert len(keras) == 1 and keras[0]["plugin"] == "graph_keras_model"
+    cfg = json.loads(keras[0]["strings"][0])
+    assert cfg["class_name"] == "Model" and [ly["name"] for ly in cfg["config"]["layers"]][1] == "dense"
+    hist = {(s, t): p for s, t, k, p in vals if k == "histo"}
+    assert {s for s, _ in hist} == {0, 2}                      # epochs 0 and 2 (freq 2)
+    assert {t for _, t in hist} == {"dense/kernel_0", "dense/bias_0", "dense_1/kernel_0", "dense_1/bias_0",
+                                    "dense_2/kernel_0", "dense_2/bias_0", "dense_3/kernel_0", "dense_3/bias_0"}
+    w = m.get_weights()
+    h = hist[(2, "dense/kernel_0")]
+    assert h["num"] == w[0].size and sum(h["bucket"]) == w[0].size
+    np.testing.assert_allclose([h["min"], h["max"], h["sum"]], [w[0].min(), w[0].max(), w[0].sum()], rtol=1e-5)
+    imgs = {t: p for s, t, k, p in vals if k == "image" and s == 2}
+    im = imgs["dense/kernel_0/image"]
+    assert im["height"] == 18 and im["width"] == 14 and im["png"].startswith(b"\x89PNG")
+    assert imgs["dense/bias_0/image"]["height"] == 1
+    with pytest.raises(TypeError):
+        TensorBoard(str(tmp_path), not_an_argument=1)
+    with pytest.warns(UserWarning):
+        TensorBoard(str(tmp_path), profile_batch=2)
