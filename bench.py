@@ -177,6 +177,21 @@ def measure_kafka_e2e(model, device, n_events: int, qps: float = 10000.0):
     return _bench_module("bench_infer").kafka_e2e(model, ev, qps, 5.0, n_events, warm=200)
 
 
+def measure_lstm_kafka_e2e(device, n_events: int, qps: float = 10000.0, nkeys: int = 1000):
+    """``serve --model lstm --low-latency``: Kafka append -> result append through the C++ loop
+    and the persistent per-car LSTM forecaster (reference stack, look_back 1; car key -> device
+    slot in C++; LSTM-TensorFlow-IO-Kafka/cardata-v2.py:220-273)."""
+    from streamml.data.cardata import synthetic_device_tensor
+    from streamml.models.lstm import LSTMPredictor
+    from streamml.ops.serve import LSTMScoringServer
+    ev = synthetic_device_tensor(n_events + 200, device, seed=8).cpu().numpy()
+    lm = LSTMPredictor.reference(look_back=1, device=device)
+    r = _bench_module("bench_infer").kafka_e2e(None, ev, qps, 5.0, n_events, warm=200,
+                                                make_scorer=lambda: LSTMScoringServer(lm, nkeys=nkeys, threshold=5.0))
+    r["model"] = "reference LSTM stack, look_back 1 (lstm_serve.hip), 1000 car keys"
+    return r
+
+
 def measure_batch32(spec, data, device, steps, scale, shift, seed, launches=5):
     """Side measurement at the reference's own optimizer granularity: one Adam step per
     32 rows (Keras fit(batch_size=32)), ``steps`` sequential steps per launch of the
@@ -614,6 +629,10 @@ def main():
                      args.qps)
         out.update({"kafka_e2e_p50_us": None if "p50_us" not in e2e else e2e["p50_us"],
                     "kafka_e2e_p99_us": None if "p99_us" not in e2e else e2e["p99_us"], "kafka_e2e": e2e})
+        le2e = ph.run("lstm_kafka_e2e", 6 + 3e-4 * args.e2e_events, measure_lstm_kafka_e2e, device, args.e2e_events,
+                      args.qps)
+        out.update({"lstm_kafka_e2e_p50_us": le2e.get("p50_us"), "lstm_kafka_e2e_p99_us": le2e.get("p99_us"),
+                    "lstm_kafka_e2e": le2e})
     if args.batch32_steps > 0:
         b32 = ph.run("keras_batch32", 4 + 1.5e-5 * args.batch32_steps, measure_batch32, spec, data, device,
                      args.batch32_steps, scale, shift, args.seed)

@@ -132,6 +132,86 @@ def stream_e2e(device, rows: int = 2_000_000, batch: int = 100, partitions: int 
     return out
 
 
+def _fill_topic(b, topic, rows, partitions, failure_rate=0.01, distinct=1_000_000):
+    """Append ``rows`` Confluent-framed Avro events round-robin over ``partitions`` (up to
+    ``distinct`` encoded once, then re-appended)."""
+    from streamml.data import stream as S
+    from streamml.data.avro import AvroCodec
+    from streamml.data.produce import encode_chunk
+    b.create_topic(topic, partitions)
+    codec = AvroCodec("cardata-v1")
+    chunk = min(rows, 250_000)
+    encoded = [encode_chunk(codec, c.x, c.label) + (len(c.x),)
+               for c in S.synthetic(min(rows, distinct), chunk=chunk, seed=0, failure_rate=failure_rate)]
+    left, i, nbytes = rows, 0, 0
+    while left > 0:
+        buf, offs, k = encoded[i % len(encoded)]
+        if k > left:
+            buf, offs = buf[:offs[left]], offs[:left + 1]
+            k = left
+        b.append_buffer(topic, i % partitions, buf, offs)
+        nbytes += int(offs[k])
+        left -= k
+        i += 1
+    return nbytes
+
+
+def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, batch: int = 1 << 20,
+                       workers=(1, 2, 4, 8, 16, 32), train_workers: int = 0) -> dict:
+    """Fresh rows at large batch: ``partitions`` partitions of Confluent
+    Avro -> native C++ feed (one worker per partition group, pinned slabs, H2D in flight) ->
+    ``fit(batch_size=batch, engine="throughput")`` over the stream, every epoch re-reading the
+    log like the reference (cardata-v3.py:44-75, python-scripts/README.md:116).
+
+    Reports the host fetch + decode rate against the number of feed workers (the slabs are
+    recycled uncopied: the decode alone) and the end-to-end trained rows/s at the best
+    worker count.  Each row is ~155 bytes on the wire, so 100 M rows/s is 15.5 GB/s of
+    loopback Kafka traffic."""
+    import torch
+
+    from streamml.data import stream as S
+    from streamml.kafka import fake_broker
+    from streamml.models.autoencoder import Autoencoder
+
+    name = f"bench-large-{rows}-{partitions}"
+    b = fake_broker(name)
+    topic = "SENSOR_DATA_S_AVRO"
+    t0 = time.perf_counter()
+    nbytes = _fill_topic(b, topic, rows, partitions)
+    out = {"rows": rows, "partitions": partitions, "batch": batch, "log_bytes": nbytes,
+           "bytes_per_row": nbytes / rows, "produce_s": time.perf_counter() - t0,
+           "cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0))}
+    specs = [f"{topic}:{p}:0" for p in range(partitions)]
+    curve = []
+    for w in workers:
+        src = S.kafka(f"fake://{name}", specs, max_bytes=8 << 20, workers=int(w), native=True)
+        t1 = time.perf_counter()
+        n = src.native_feed.count_rows()
+        dt = time.perf_counter() - t1
+        st = src.native_feed.last_stats
+        curve.append({"workers": int(w), "rows_per_s": n / dt, "gb_per_s": n * out["bytes_per_row"] / dt / 1e9,
+                      "fetch_s": st.get("fetch_s"), "decode_s": st.get("decode_s"),
+                      "wait_slab_s": st.get("wait_slab_s")})
+    out["decode_curve"] = curve
+    best = max(curve, key=lambda c: c["rows_per_s"])
+    tw = int(train_workers or best["workers"])
+    src = S.kafka(f"fake://{name}", specs, max_bytes=8 << 20, workers=tw, native=True)
+    training = src.filter_normal(device=True)
+    m = Autoencoder(device=device, input_normalizer="cardata")
+    m.compile()
+    m.fit(training, epochs=1, batch_size=batch, verbose=0, steps_per_epoch=4, engine="throughput", dp="none")
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    h = m.fit(training, epochs=1, batch_size=batch, verbose=0, engine="throughput", dp="none")
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t1
+    kept = int(h.history["_rows"][-1]) if "_rows" in h.history else None
+    out.update({"train_workers": tw, "rows_per_s": rows / dt, "trained_rows_per_s": (kept or 0) / dt,
+                "kept_rows": kept, "engine": m.last_fit_engine, "loss": h.history["loss"][-1],
+                "h2d_gb_per_s": src.native_feed.last_stats.get("h2d_bytes", 0) / dt / 1e9})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=2_000_000)
@@ -141,7 +221,12 @@ def main():
     ap.add_argument("--python-feed", action="store_true", help="chunk-by-chunk Python Kafka path")
     ap.add_argument("--skip-stream", action="store_true")
     ap.add_argument("--compare-chunks", action="store_true", help="also time the launch-per-chunk stream epoch")
+    ap.add_argument("--large-batch", action="store_true", help="only the large-batch streaming measurement")
     args = ap.parse_args()
+    if args.large_batch:
+        import torch
+        print(json.dumps(stream_large_batch(torch.device("cuda", 0), rows=args.rows)))
+        return
     import torch
     dev = torch.device("cuda", 0)
     res = {"fit_batch100": fit_array(dev, args.rows, args.batch)}

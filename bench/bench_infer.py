@@ -45,7 +45,7 @@ def _serving_cpus(k: int):
     return None
 
 
-def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=False):
+def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=False, make_scorer=None):
     """Kafka append -> result append latency through the real serving path: a paced C++
     producer appends Confluent-Avro car events (one produce request each, keyed by car) to
     an in-process broker at ``qps``; the ``serve --low-latency`` loop (long-poll fetch, C++
@@ -57,7 +57,10 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=
     legs included).  ``spin_us``: the low-latency socket policy (broker connection threads,
     long polls and the loop's client busy-poll this long before blocking).  ``pin``: the
     scoring loop and the producer run on two CPUs of their own (distinct physical cores); off
-    by default -- on the MI355X boxes it changed nothing measurable (profiles/r03)."""
+    by default -- on the MI355X boxes it changed nothing measurable (profiles/r03).
+    ``make_scorer``: the resident scorer to serve with (default the autoencoder's
+    ``ScoringServer``; e.g. an ``LSTMScoringServer``, whose car keys the loop maps to device
+    slots in C++)."""
     import threading
 
     import numpy as np
@@ -78,7 +81,7 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=
                              np.zeros(n, np.uint8))
     keys = [f"car{i % 1000}" for i in range(n)]
     out = {}
-    with ScoringServer(m, threshold=threshold, slots=4096) as srv:
+    with (make_scorer() if make_scorer is not None else ScoringServer(m, threshold=threshold, slots=4096)) as srv:
         loop = LowLatencyScorer(f"fake://{name}", "SENSOR_DATA_S_AVRO", "model-predictions", [0], srv, starts=[0],
                                 max_wait_ms=100, record_latency=True, spin_us=spin_us)
         cpus = _serving_cpus(2) if pin else None

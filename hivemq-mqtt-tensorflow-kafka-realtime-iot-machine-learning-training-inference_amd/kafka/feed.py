@@ -152,8 +152,29 @@ class NativeFeed:
             f.stop()
             self._finish(f, client, parts, t0, marks, exhausted)
 
-    def count_rows(self, keep_label: Optional[int] = None) -> int:
-        return sum(len(r) for r, _ in self.host_chunks(keep_label))
+    def count_rows(self, keep_label: Optional[int] = None, slab_rows: int = 65536) -> int:
+        """Fetch + decode the whole range and count the rows; slabs are recycled as they are
+        published, never copied (the host decode rate alone, for scaling measurements)."""
+        f, client, parts = self._make(keep_label)
+        F = self.features
+        nslots = 2 * self.workers + 2
+        bufs = [np.empty(slab_rows * (F * 4 + 1), np.uint8) for _ in range(nslots)]
+        t0 = time.perf_counter()
+        f.start([int(b.ctypes.data) for b in bufs], int(slab_rows))
+        total, exhausted = 0, False
+        try:
+            while True:
+                code, slab, n = f.pop(1000)
+                if code < 0:
+                    exhausted = True
+                    break
+                if code:
+                    total += int(n)
+                    f.recycle(slab)
+        finally:
+            f.stop()
+            self._finish(f, client, parts, t0, {}, exhausted)
+        return total
 
     # ------------------------------------------------------------------ device
     def device_chunks(self, device, keep_label: Optional[int] = None, slab_rows: int = 32768,

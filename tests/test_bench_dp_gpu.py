@@ -92,7 +92,8 @@ def test_bench_n_ranks_rehearsal(tmp_path, cuda_device, n):
     dpr = out["keras_batch32_dp"]
     assert dpr.get("replicas_identical") is True and dpr["global_batch"] == 32 * n, dpr
     ph = out["phase_s"]
-    for k in ("infer", "small_allreduce", "keras_batch32_dp", "kafka_e2e", "keras_batch32", "fit_large_batch",
+    for k in ("infer", "small_allreduce", "keras_batch32_dp", "kafka_e2e", "lstm_kafka_e2e", "keras_batch32",
+              "fit_large_batch",
               "fresh_rows", "fit_batch100", "stream_e2e", "lstm_seq50", "lstm_ref", "lstm_infer", "mqtt_e2e",
               "total_wall"):
         assert k in ph, (k, ph, out["budget"])

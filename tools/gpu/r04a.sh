@@ -26,7 +26,7 @@ for l in open("gpurun_out/r04a/bench.out"):
     if l.startswith("{"):
         d = json.loads(l)
         print({k: d.get(k) for k in ("value", "ms_per_step", "p50_infer_us", "kafka_e2e_p50_us", "lstm_seq50_windows_per_s",
-                                     "lstm_infer_p50_us", "mqtt_connections", "mqtt_dropped",
+                                     "lstm_infer_p50_us", "lstm_kafka_e2e_p50_us", "mqtt_connections", "mqtt_dropped",
                                      "mqtt_publish_to_result_p50_us")})
         print(d["phase_s"], d["budget"])
 PY
