@@ -59,7 +59,7 @@ def stream_e2e(device, rows: int = 2_000_000, batch: int = 100, partitions: int 
     from streamml.kafka import fake_broker
     from streamml.models.autoencoder import Autoencoder
 
-    name = f"bench-e2e-{rows}-{partitions}"
+    name = f"bench-e2e-{rows}-{partitions}-{time.time_ns()}"
     b = fake_broker(name)
     topic = "SENSOR_DATA_S_AVRO"
     b.create_topic(topic, partitions)
@@ -173,7 +173,7 @@ def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, bat
     from streamml.kafka import fake_broker
     from streamml.models.autoencoder import Autoencoder
 
-    name = f"bench-large-{rows}-{partitions}"
+    name = f"bench-large-{rows}-{partitions}-{time.time_ns()}"
     b = fake_broker(name)
     topic = "SENSOR_DATA_S_AVRO"
     t0 = time.perf_counter()

@@ -71,7 +71,9 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=
     from streamml.ops.serve import ScoringServer
 
     n = events + warm
-    name = f"bench-e2e-{os.getpid()}-{rank}-{spin_us}-{next(_E2E_RUNS)}"   # a fresh broker per call
+    # a fresh broker per call (bench.py re-executes this module per use: the counter alone
+    # would repeat, so the name also carries a nanosecond stamp)
+    name = f"bench-e2e-{os.getpid()}-{rank}-{spin_us}-{next(_E2E_RUNS)}-{time.time_ns()}"
     b = fake_broker(name)
     b.create_topic("SENSOR_DATA_S_AVRO", 1)
     b.create_topic("model-predictions", 1)

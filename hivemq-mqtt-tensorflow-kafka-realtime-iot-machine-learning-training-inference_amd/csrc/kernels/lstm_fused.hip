@@ -48,6 +48,8 @@
 // weight-gradient accumulators can live in AGPRs (launch_bounds(256, 1): 512
 // registers/lane); the forward is lstm_fused_fwd.hip (VGPR form), shared helpers
 // are in include/lstm_fused_impl.h.
+#include <cstdlib>
+
 #include "lstm_fused_impl.h"
 
 using namespace sml;
@@ -75,11 +77,15 @@ struct FusedBwdArgs {
   int64_t x_seq;       // elements between consecutive sequences of x (T*IN contiguous, IN sliding windows)
 };
 
+// DBX: the bias gradient comes out of the dW^T MFMA: the x operand carries a constant 1 in its
+// first padding column (IN < 16*KT), whose W^T / W fragment columns are zero, so column IN of
+// the dW^T accumulator is sum_t,seq dz = db -- no per-step db adds, at the price of
+// bf16-rounded dz in db (as in dW and dU).  Not the default: see launch_bwd.
 // DX: the input gradient is wanted (compile-time: the first layer of a stack needs none).
 // RF: weight A fragments kept in registers for the whole launch instead of re-read from
 // LDS every step (bits: 1 the recurrent U fragments of the dh chain, 2 the gate
 // recompute's [W^T | U^T], 4 the dX fragments W) -- where the registers exist, see launch_bwd.
-template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0>
+template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0, bool DBX = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdArgs a) {
   using XR = typename RowRaw<XT>::type;
   constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
@@ -174,6 +180,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   f32x4 dhr[UB], dcn[UB];
 #pragma unroll
   for (int b = 0; b < UB; ++b) dhr[b] = dcn[b] = zero4;
+  // DBX: the bf16 1.0 this lane ORs into its x operand (zero except at feature IN)
+  bf16x4 onex[KT];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) onex[kt][j] = (DBX && 16 * kt + 4 * g + j == IN) ? (short)0x3F80 : (short)0;
 
   // Per-step operands, all in C orientation (lane c = this lane's sequence): the
   // forward's inputs x_t and h_{t-1} (gates are recomputed from them instead of being
@@ -264,7 +276,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     // operands and accumulation order (bit-identical pre-activations)
     bf16x4 xb[KT], hb[UB];
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) xb[kt] = row_operand(cur.xt[kt], 16 * kt + 4 * g, IN);
+    for (int kt = 0; kt < KT; ++kt) {
+      xb[kt] = row_operand(cur.xt[kt], 16 * kt + 4 * g, IN);
+      if constexpr (DBX) xb[kt] |= onex[kt];   // column IN: 0 -> 1.0 (its weights are zero)
+    }
     const bool take_dh = valid && (!a.dh_last_only || t == T - 1);
 #pragma unroll
     for (int s = 0; s < UB; ++s) hb[s] = cur.hp[s];
@@ -298,13 +313,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
         const float dh = (take_dh ? dhi[b][i] : 0.f) + dhr[b][i];
         const float ct = ctc[b][i];
         const float ac = act_f(ACT, ct);
-        const float dc = dcn[b][i] + dh * go * act_d(ACT, ct, ac);
-        dzt[b][i] = dc * gc * gi * (1.f - gi);
-        dzt[UB + b][i] = dc * cp[b][i] * gf * (1.f - gf);
-        const float gcd = ACT == ACT_RELU ? (gc > 0.f ? 1.f : 0.f) : fmaf(-gc, gc, 1.f);
-        dzt[2 * UB + b][i] = dc * gi * gcd;
-        dzt[3 * UB + b][i] = dh * ac * go * (1.f - go);
-        dcn[b][i] = dc * gf;
+        // the gate derivatives with shared factors and s(1-s) = fma(-s, s, s); relu's
+        // derivative as selects: 16 VALU per element instead of ~25 (17 v_mul + 3 v_sub + ...)
+        const float dhgo = dh * go;
+        const float dc = ACT == ACT_RELU ? (ct > 0.f ? dcn[b][i] + dhgo : dcn[b][i])
+                                         : fmaf(dhgo, fmaf(-ac, ac, 1.f), dcn[b][i]);
+        const float di = dc * gi;
+        const float df = dc * gf;
+        dzt[b][i] = (dc * gc) * fmaf(-gi, gi, gi);                                   // dc g i(1-i)
+        dzt[UB + b][i] = fmaf(-df, gf, df) * cp[b][i];                               // dc f(1-f) c_{t-1}
+        dzt[2 * UB + b][i] = ACT == ACT_RELU ? (gc > 0.f ? di : 0.f) : di * fmaf(-gc, gc, 1.f);
+        dzt[3 * UB + b][i] = (dh * ac) * fmaf(-go, go, go);                          // dh act(c) o(1-o)
+        dcn[b][i] = df;
       }
       ctc[b] = cp[b];   // c_{t-1} is the next (earlier) step's c_t
     }
@@ -316,7 +336,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       dzb[mt] = pack4(dzt[mt]);
-      accb[mt] += dzt[mt];
+      if constexpr (!DBX) accb[mt] += dzt[mt];
     }
     // critical path: recurrent gradient for step t-1 -- the 4U gate tiles in pairs on
     // 16x16x32 (MT/2 dependent MFMAs, half the issues of two 16x16x16 half-chains)
@@ -372,6 +392,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     }
   }
   // db: sum the 16 sequence lanes c of each row group (butterfly within 16 lanes)
+  if constexpr (!DBX)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -397,11 +418,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
           for (int kt = 0; kt < KT; ++kt) slab[m * LDW + 16 * kt + c] += accW[mt][kt][i];
 #pragma unroll
           for (int kb = 0; kb < UB; ++kb) slab[G4 * LDW + m * U + 16 * kb + c] += accU[mt][kb][i];
-          if (c == 0) slab[G4 * LDW + G4 * U + m] += accb[mt][i];
+          if (!DBX && c == 0) slab[G4 * LDW + G4 * U + m] += accb[mt][i];
         }
     }
   }
   __syncthreads();
+  if constexpr (DBX) {   // db = column IN of dW^T (the constant-1 input); the column itself is padding
+    for (int m = threadIdx.x; m < G4; m += WAVES * 64) {
+      slab[G4 * LDW + G4 * U + m] = slab[m * LDW + IN];
+      slab[m * LDW + IN] = 0.f;
+    }
+    __syncthreads();
+  }
   float* out = a.partials + (int64_t)blockIdx.x * S;
   for (int i = threadIdx.x; i < S; i += WAVES * 64) out[i] = slab[i];
 }
@@ -416,16 +444,43 @@ hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
   // reads were exposed latency there (SQ_WAIT_ANY 41 % of wave cycles) and the kernel
   // runs 17 % faster (bench_lstm 62.3 -> 68.1 M windows/s, profiles/r02).  With dX, at
   // two waves per SIMD, register fragments measured the same as LDS reads (67.8 vs 67.9).
-  auto go = [&](auto dx, auto rf) {
+  auto go = [&](auto dx, auto rf, auto dbx) {
     constexpr bool DX = decltype(dx)::value;
     constexpr int RF = decltype(rf)::value;
+    constexpr bool DB = decltype(dbx)::value;
     if (a.act == ACT_RELU)
-      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF, DB>), dim3(grid), dim3(WAVES * 64), 0,
+                         st, a);
     else
-      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF, DB>), dim3(grid), dim3(WAVES * 64), 0,
+                         st, a);
   };
-  if (a.dx) go(std::true_type{}, std::integral_constant<int, 0>{});
-  else go(std::false_type{}, std::integral_constant<int, 3>{});
+  // the constant-1 column needs a padding column in x (IN < 16*KT).  Off by default: the
+  // compiler keeps the db adds in packed VGPR form, so it saves no instructions (loop count
+  // 403 vs 410 VALU + accumulator moves per step) and db loses its exact fp32 sum.
+  // SML_LSTM_DBX=1 selects it (A/B).
+  static const bool dbx_env = [] {
+    const char* e = std::getenv("SML_LSTM_DBX");
+    return e && e[0] == '1';
+  }();
+  const bool dbx = dbx_env && a.IN < 16 * KT;
+  if (a.dx) {
+    if (dbx) go(std::true_type{}, std::integral_constant<int, 0>{}, std::true_type{});
+    else go(std::true_type{}, std::integral_constant<int, 0>{}, std::false_type{});
+  } else {
+    // SML_LSTM_RF=0: weight fragments read from LDS (fewer registers, more waves per SIMD)
+    static const bool rf_lds = [] {
+      const char* e = std::getenv("SML_LSTM_RF");
+      return e && e[0] == '0';
+    }();
+    if (rf_lds) {
+      if (dbx) go(std::false_type{}, std::integral_constant<int, 0>{}, std::true_type{});
+      else go(std::false_type{}, std::integral_constant<int, 0>{}, std::false_type{});
+    } else {
+      if (dbx) go(std::false_type{}, std::integral_constant<int, 3>{}, std::true_type{});
+      else go(std::false_type{}, std::integral_constant<int, 3>{}, std::false_type{});
+    }
+  }
   return hipGetLastError();
 }
 

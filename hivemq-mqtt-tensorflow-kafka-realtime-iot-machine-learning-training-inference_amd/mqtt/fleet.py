@@ -98,6 +98,7 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
     brokers = max(int(brokers or 0), need)
     agents = max(int(agents or 0), brokers)
     t_begin = time.time()
+    name = f"{name}-{os.getpid()}-{time.time_ns()}"   # a fresh in-process Kafka per run
     kb = fake_broker(name)
     topic, results, lresults = "sensor-data", "model-predictions", "lstm-predictions"
     for t in (topic, results) + ((lresults,) if lstm_scorer is not None else ()):
@@ -166,7 +167,7 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
         "bridged_to_kafka": sum(int(s["kafka_sent"]) for s in nstats),
         "bridge_failed": sum(int(s["kafka_failed"]) for s in nstats),
         "bridge_flushed": all(bool(s.get("flushed")) for s in nstats),
-        "wall_s": time.time() - t_begin,
+        "wall_s": time.time() - t_begin, "kafka": f"fake://{name}",
     }
     for tag, lp, o in zip(("ae", "lstm"), loops, outs):
         lat = lp.latency_records()

@@ -199,6 +199,10 @@ def test_lstm_kafka_low_latency_path_matches_oracle(cuda_device, stack, T):
     rng = np.random.default_rng(11 + T)
     n, ncar = 240, 6
     raw = rng.uniform(0, 40, size=(n, 18)).astype(np.float32)
+    from streamml.data.cardata import FEATURES, INT_FEATURES
+    for j, f in enumerate(FEATURES):   # the Avro schema's int fields carry whole numbers
+        if f in INT_FEATURES:
+            raw[:, j] = np.round(raw[:, j])
     cars = [f"vehicles/sensor/data/electric-vehicle-{int(c):05d}" for c in rng.integers(0, ncar, size=n)]
     part = np.array([hash(c) % 2 for c in cars])        # a car's events stay in one partition
     name = f"lstm-ll-{stack}-{T}"

@@ -23,7 +23,7 @@ def test_fleet_small_scale_no_drops():
     assert r["dropped"] == 0 and r["ae"]["scored"] == 1200 and r["ae"]["skipped"] == 0
     assert r["lstm"]["scored"] == 1200 and r["lstm"]["keys"] == 300    # one slot per car
     assert 0 < r["ae"]["publish_to_result_p50_us"] < 2e6
-    c = KafkaClient("fake://fleet-cpu-test")
+    c = KafkaClient(r["kafka"])
     n = 0
     cars = set()
     for p in range(4):

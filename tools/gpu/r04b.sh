@@ -13,8 +13,15 @@ step() {
   echo "== $name rc=$rc"
   case $rc in 0) ;; *) tail -20 $O/$name.err; tail -30 $O/$name.out; exit $rc;; esac
 }
-step lstm 200 python bench/bench_lstm.py --steps 20 --warmup 3
-cat $O/lstm.out
+step tests_lstm 300 python -u -m pytest -x -v --timeout 150 --timeout-method thread -m gpu tests/test_lstm_gpu.py
+grep -E "passed|failed" $O/tests_lstm.out | tail -2
+# same-box A/B of the layer-1 backward variants (bias gradient via the constant-1 column; LDS fragments)
+for k in 1 2; do
+  step lstm_def_$k 200 python bench/bench_lstm.py --steps 20 --warmup 3
+  step lstm_dbx1x_$k 200 env SML_LSTM_DBX=1 python bench/bench_lstm.py --steps 20 --warmup 3
+  step lstm_rf0_$k 200 env SML_LSTM_RF=0 python bench/bench_lstm.py --steps 20 --warmup 3
+done
+for f in $O/lstm_*.out; do echo "$f $(python -c "import json,sys; d=json.load(open('$f')); print(round(d['value']/1e6,2), round(d['ms_per_step'],3))")"; done
 cd /tmp
 pass() {  # pass <name> <counters...>
   local name=$1; shift
@@ -28,6 +35,10 @@ timeout -k 10 150 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O
 echo "== trace rc=$?"
 pass issue SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES
 pass insts SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS
+export SML_LSTM_DBX=1
+pass insts_dbx1 SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS
+pass issue_dbx1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES
+unset SML_LSTM_DBX
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 echo ALLDONE
