@@ -4,6 +4,8 @@
 // keeps its gate accumulators in VGPRs, the backward its weight-gradient accumulators
 // in AGPRs -- see the build marker at the top of lstm_fused.hip).
 #pragma once
+#include <cstdlib>
+
 #include "sml_common.h"
 #include "sml_ops.h"
 
@@ -110,6 +112,54 @@ hipError_t dispatch(int U, int IN, int xv, bool x_bf16, F&& f) {
   SML_UK(32, 1) SML_UK(32, 2)
 #undef SML_UK
   return hipErrorInvalidValue;
+}
+
+// Bias modes of the fused kernels (BM), chosen per layer by bias_mode():
+//   BM_PLAIN 0: bias in registers (forward) / LDS (backward recompute); db summed per step.
+//   BM_BX    1 ("bias columns", needs IN + 2 <= 16*KT, e.g. the 18 car features in 32
+//            K-slots): the x MFMA operand carries a constant 1.0 in columns IN and IN + 1 and
+//            the W^T fragments carry the bias there, split as bf16 hi + lo (hi + lo equals the
+//            fp32 bias to 2^-16 relative).  The gate pre-activations come out of the MFMAs
+//            with the bias included -- no bias registers, no accumulator initialisation --
+//            and in the backward the same constant column makes dW^T column IN the bias
+//            gradient (no per-step db adds).  Forward and backward recompute use identical
+//            operands, so the recomputed pre-activations stay bit-identical.
+//   BM_DB    2 (needs IN + 1 <= 16*KT): only the backward changes -- a constant-1 x column
+//            with zero weights, whose dW^T column is db; the bias itself stays as in PLAIN.
+// In BX and DB db is the sum of bf16-rounded dz (the dW / dU precision) instead of fp32.
+// SML_LSTM_BIASCOL=0 / 1 / d selects PLAIN / BX / DB where the layer admits it (A/B;
+// default BX, else DB, else PLAIN).
+constexpr int BM_PLAIN = 0, BM_BX = 1, BM_DB = 2;
+inline int bias_mode(int IN, int KT) {
+  static const char m = [] {
+    const char* e = std::getenv("SML_LSTM_BIASCOL");
+    return e && e[0] ? e[0] : '1';
+  }();
+  if (m == '0') return BM_PLAIN;
+  if (m != 'd' && IN + 2 <= 16 * KT) return BM_BX;
+  return IN + 1 <= 16 * KT ? BM_DB : BM_PLAIN;
+}
+
+// lane (c, g)'s constant-1 bits for x tile kt (BX / DB): bf16 1.0 at columns IN, IN + 1
+// (in DB column IN + 1, if it exists, also has zero weights: one more padding column)
+__device__ __forceinline__ bf16x4 ones_at_bias(int kt, int g, int IN) {
+  bf16x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int f = 16 * kt + 4 * g + j;
+    r[j] = (f == IN || f == IN + 1) ? (short)0x3F80 : (short)0;
+  }
+  return r;
+}
+
+// W^T fragment element (gate m, feature f) in BX mode: the weight, or the bias hi / lo parts
+__device__ __forceinline__ float wt_elem_bx(const float* W, const float* b, int G4, int IN, int f, int m) {
+  if (f < IN) return W[(int64_t)f * G4 + m];
+  const float bv = b[m];
+  const float hi = bf16_to_f32((unsigned short)(pack2(bv, 0.f) & 0xFFFFu));   // RNE, as the fragment pack
+  if (f == IN) return hi;
+  if (f == IN + 1) return bv - hi;
+  return 0.f;
 }
 
 // widest row access (elements, up to 4) that IN and the base pointer's alignment allow

@@ -62,6 +62,28 @@ Feed::Feed(std::string bootstrap, kafka::ClientConfig ccfg, std::vector<avro::Fi
     plan_.push_back(Op{(uint8_t)f.kind, (int8_t)f.null_branch, (int8_t)col_of_[fi],
                        (uint8_t)((int)fi == cfg_.label_field), f.fixed_size});
   }
+  fast_ = true;
+  for (const Op& op : plan_) {
+    const bool num = op.kind == avro::K_FLOAT || op.kind == avro::K_INT || op.kind == avro::K_LONG ||
+                     op.kind == avro::K_DOUBLE;
+    if (op.null_branch > 1 || !(num || op.kind == avro::K_STRING || op.kind == avro::K_BYTES)) {
+      fast_ = false;
+      break;
+    }
+    const uint8_t k = op.kind == avro::K_LONG ? (uint8_t)avro::K_INT : op.kind;   // the same varint
+    const int16_t vb = op.null_branch < 0 ? -1 : (int16_t)(2 * (1 - op.null_branch));   // zig-zag branch index
+    if (!runs_.empty()) {
+      Run& r = runs_.back();
+      const bool same = r.kind == k && k != avro::K_STRING && k != avro::K_BYTES && !op.label && r.vb == vb &&
+                        r.n < 255 && ((r.col < 0 && op.col < 0) || (r.col >= 0 && op.col == r.col + r.n));
+      if (same) {
+        ++r.n;
+        continue;
+      }
+    }
+    runs_.push_back(Run{k, 1, op.col, op.label, vb});
+  }
+  if (!fast_) runs_.clear();
   for (auto& s : parts) {
     auto p = std::make_unique<Part>();
     p->spec = s;
@@ -169,7 +191,67 @@ void Feed::publish(int w, int slab, int64_t rows) {
   cv_ready_.notify_one();
 }
 
+int Feed::decode_fast(const uint8_t* p, size_t n, float* out_row, uint8_t* label) const {
+  const uint8_t* e = p + n;
+  if (cfg_.framing) {
+    if (n < 5 || p[0] != 0) return -1;
+    p += 5;
+  }
+  for (const Run& r : runs_) {
+    const int u = r.vb >= 0 ? 1 : 0;   // union branch byte before each value
+    switch (r.kind) {
+      case avro::K_FLOAT:
+      case avro::K_DOUBLE: {   // raw little-endian values (KSQL's DOUBLE columns narrowed)
+        const int w = r.kind == avro::K_FLOAT ? 4 : 8, stride = u + w;
+        if (e - p < (ptrdiff_t)stride * r.n) return -1;
+        for (int k = 0; k < r.n; ++k, p += stride) {
+          if (u && p[0] != (uint8_t)r.vb) return -1;
+          float x;
+          if (w == 4) {
+            std::memcpy(&x, p + u, 4);
+          } else {
+            double v;
+            std::memcpy(&v, p + u, 8);
+            x = (float)v;
+          }
+          if (r.col >= 0) out_row[r.col + k] = x;
+        }
+        break;
+      }
+      case avro::K_INT: {      // zig-zag varints (int and long)
+        for (int k = 0; k < r.n; ++k) {
+          if (u) {
+            if (p >= e || p[0] != (uint8_t)r.vb) return -1;
+            ++p;
+          }
+          int64_t x;
+          if (p < e && !(*p & 0x80)) {
+            const uint8_t b = *p++;
+            x = (int64_t)((b >> 1) ^ (~(b & 1) + 1));
+          } else if (!varlong(p, e, x)) {
+            return -1;
+          }
+          if (r.col >= 0) out_row[r.col + k] = (float)x;
+        }
+        break;
+      }
+      default: {               // string / bytes
+        if (u) {
+          if (p >= e || p[0] != (uint8_t)r.vb) return -1;
+          ++p;
+        }
+        int64_t len;
+        if (!varlong(p, e, len) || len < 0 || len > e - p) return -1;
+        if (r.label) *label = label_code(p, (size_t)len);
+        p += len;
+      }
+    }
+  }
+  return p == e ? 1 : -1;
+}
+
 bool Feed::decode_row(const uint8_t* p, size_t n, float* out_row, uint8_t* label) const {
+  if (fast_ && decode_fast(p, n, out_row, label) == 1) return true;
   const uint8_t* e = p + n;
   if (cfg_.framing) {
     if (n < 5 || p[0] != 0) return false;
@@ -310,7 +392,7 @@ void Feed::run(int w) {
           ++loc.fetches;
           if (len == 0) continue;
           loc.bytes += len;
-          S.cur = kafka::RecordSetCursor(reinterpret_cast<const uint8_t*>(S.resp.data()) + off, len);
+          S.cur = kafka::RecordSetCursor(reinterpret_cast<const uint8_t*>(S.resp.data()) + off, len, cfg_.check_crcs);
           S.have = true;
         }
         const auto t1 = Clock::now();

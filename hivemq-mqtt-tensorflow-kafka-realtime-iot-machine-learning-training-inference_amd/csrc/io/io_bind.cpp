@@ -634,7 +634,7 @@ PYBIND11_MODULE(_io, m) {
                        const std::string& user, const std::string& pw, int timeout_ms, const py::list& fields,
                        std::vector<int> feature_fields, int label_field, int keep_label, bool framing,
                        int32_t max_bytes, int32_t max_wait_ms, int workers, double idle_timeout_s,
-                       const std::vector<std::tuple<std::string, int, int64_t, int64_t>>& parts) {
+                       const std::vector<std::tuple<std::string, int, int64_t, int64_t>>& parts, bool check_crcs) {
              kafka::ClientConfig c;
              c.client_id = client_id;
              c.sasl_mechanism = mech;
@@ -650,6 +650,7 @@ PYBIND11_MODULE(_io, m) {
              fc.max_wait_ms = max_wait_ms;
              fc.workers = workers;
              fc.idle_timeout_s = idle_timeout_s;
+             fc.check_crcs = check_crcs;
              std::vector<feed::PartSpec> ps;
              for (const auto& t : parts) ps.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t)});
              return new feed::Feed(bootstrap, c, fields_from_py(fields), fc, ps);
@@ -657,7 +658,8 @@ PYBIND11_MODULE(_io, m) {
            py::arg("bootstrap"), py::arg("client_id"), py::arg("sasl_mechanism"), py::arg("sasl_username"),
            py::arg("sasl_password"), py::arg("timeout_ms"), py::arg("fields"), py::arg("feature_fields"),
            py::arg("label_field"), py::arg("keep_label"), py::arg("framing"), py::arg("max_bytes"),
-           py::arg("max_wait_ms"), py::arg("workers"), py::arg("idle_timeout_s"), py::arg("parts"))
+           py::arg("max_wait_ms"), py::arg("workers"), py::arg("idle_timeout_s"), py::arg("parts"),
+           py::arg("check_crcs") = false)
       .def("start",
            [](feed::Feed& f, const std::vector<uint64_t>& slabs, int64_t cap) {
              std::vector<uintptr_t> v(slabs.begin(), slabs.end());
@@ -682,6 +684,15 @@ PYBIND11_MODULE(_io, m) {
              py::gil_scoped_release rel;
              f.stop();
            })
+      .def("decode_row",   // one framed Avro value -> (ok, projected row, label code); tests / debugging
+           [](const feed::Feed& f, const py::bytes& value) {
+             const std::string v = value;
+             std::vector<float> row((size_t)f.features(), 0.f);
+             uint8_t lab = 0;
+             const bool ok = f.decode_row(reinterpret_cast<const uint8_t*>(v.data()), v.size(), row.data(), &lab);
+             return py::make_tuple(ok, row, (int)lab);
+           }, py::arg("value"))
+      .def_property_readonly("fast_plan", &feed::Feed::fast_plan)
       .def("positions", &feed::Feed::positions)
       .def("slab_marks", &feed::Feed::slab_marks, py::arg("slab"))
       .def_property_readonly("features", &feed::Feed::features)

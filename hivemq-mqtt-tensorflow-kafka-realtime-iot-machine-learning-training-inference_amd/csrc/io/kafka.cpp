@@ -312,7 +312,7 @@ bool RecordSetCursor::next(RecordView& out) {
     const int8_t magic = b.i8();
     if (magic != 2) throw Error("kafka: unsupported record batch magic " + std::to_string(magic));
     const uint32_t crc = (uint32_t)b.u(4);
-    if (crc != crc32c(p_ + pos_ + 12 + b.i, (size_t)blen - b.i)) throw Error("kafka: record batch CRC mismatch");
+    if (crc_ && crc != crc32c(p_ + pos_ + 12 + b.i, (size_t)blen - b.i)) throw Error("kafka: record batch CRC mismatch");
     const int16_t attrs = b.i16();
     if (attrs & 0x7) throw Error("kafka: compressed record batches are not supported");
     b.i32();

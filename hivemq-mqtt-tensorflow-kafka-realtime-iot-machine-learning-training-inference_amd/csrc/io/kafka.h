@@ -76,7 +76,9 @@ struct RecordView {
 class RecordSetCursor {
  public:
   RecordSetCursor() = default;
-  RecordSetCursor(const uint8_t* p, size_t n) : p_(p), n_(n) {}
+  // verify_crc: check each record batch's CRC-32C (consumers that trust the transport may
+  // skip it, as librdkafka does by default: check.crcs=false)
+  RecordSetCursor(const uint8_t* p, size_t n, bool verify_crc = true) : p_(p), n_(n), crc_(verify_crc) {}
   // next data record (control batches / records skipped); false at the end of the set
   bool next(RecordView& out);
  private:
@@ -87,6 +89,7 @@ class RecordSetCursor {
   int32_t left_ = 0;
   int64_t base_ = 0, first_ts_ = 0;
   bool control_ = false;
+  bool crc_ = true;
 };
 
 struct ClientConfig {

@@ -77,16 +77,19 @@ struct FusedBwdArgs {
   int64_t x_seq;       // elements between consecutive sequences of x (T*IN contiguous, IN sliding windows)
 };
 
-// DBX: the bias gradient comes out of the dW^T MFMA: the x operand carries a constant 1 in its
-// first padding column (IN < 16*KT), whose W^T / W fragment columns are zero, so column IN of
-// the dW^T accumulator is sum_t,seq dz = db -- no per-step db adds, at the price of
-// bf16-rounded dz in db (as in dW and dU).  Not the default: see launch_bwd.
+// BM: bias mode (lstm_fused_impl.h bias_mode).  BX: the x operand carries constant 1.0
+// columns at IN and IN + 1, the recompute's W^T fragments the bias there (bf16 hi + lo), so
+// the gate recompute needs no bias read; BX and DB: column IN of the dW^T accumulator is
+// sum_t,seq dz = db -- no per-step db adds (with them, the layer-1 kernel spent 13 % more
+// wave cycles, mostly in s_waitcnt: profiles/r04), at the price of bf16-rounded dz in db, as
+// in dW and dU.
 // DX: the input gradient is wanted (compile-time: the first layer of a stack needs none).
 // RF: weight A fragments kept in registers for the whole launch instead of re-read from
 // LDS every step (bits: 1 the recurrent U fragments of the dh chain, 2 the gate
 // recompute's [W^T | U^T], 4 the dX fragments W) -- where the registers exist, see launch_bwd.
-template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0, bool DBX = false>
+template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0, int BM = BM_PLAIN>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdArgs a) {
+  constexpr bool BX = BM == BM_BX, DB = BM != BM_PLAIN;   // bias in the MFMAs / db from the dW^T column
   using XR = typename RowRaw<XT>::type;
   constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
   constexpr int LDW = 16 * KT;
@@ -124,7 +127,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     for (int j = 0; j < 4; ++j) {
       if (k < KT) {
         const int f = 16 * k + 4 * g + j;
-        t4[j] = f < IN ? a.W[(int64_t)f * G4 + 16 * mt + c] : 0.f;
+        t4[j] = BX ? wt_elem_bx(a.W, a.bias, G4, IN, f, 16 * mt + c) : (f < IN ? a.W[(int64_t)f * G4 + 16 * mt + c] : 0.f);
       } else {
         t4[j] = a.Uw[(16 * (k - KT) + 4 * g + j) * G4 + 16 * mt + c];
       }
@@ -180,12 +183,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   f32x4 dhr[UB], dcn[UB];
 #pragma unroll
   for (int b = 0; b < UB; ++b) dhr[b] = dcn[b] = zero4;
-  // DBX: the bf16 1.0 this lane ORs into its x operand (zero except at feature IN)
+  // BX / DB: the bf16 1.0 bits this lane ORs into its x operand (features IN, IN + 1)
   bf16x4 onex[KT];
 #pragma unroll
-  for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) onex[kt][j] = (DBX && 16 * kt + 4 * g + j == IN) ? (short)0x3F80 : (short)0;
+  for (int kt = 0; kt < KT; ++kt) onex[kt] = DB ? ones_at_bias(kt, g, IN) : bf16x4{0, 0, 0, 0};
 
   // Per-step operands, all in C orientation (lane c = this lane's sequence): the
   // forward's inputs x_t and h_{t-1} (gates are recomputed from them instead of being
@@ -266,8 +267,38 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       for (int kb = 0; kb < UB; ++kb) accU[mt][kb] = mfma16(adz, hB[kb], accU[mt][kb]);
     }
   };
+  // Pair loop (RF != 0): each step transposes its own operands right after its dh chain
+  // (slot 0: the pair's first step, slot 1: the second) and the next pair's first step
+  // contracts both steps at once -- K = the 2 x 16 sequence-steps of one 16x16x32 per
+  // accumulator tile, so every accumulator is written once per trip (with one 16x16x16 per
+  // step the allocator rotated them through spare AGPRs: 96 v_accvgpr_mov per step).
+  constexpr bool PAIR = RF != 0 && DB;
+  bf16x4 tdz[2][PAIR ? MT : 1], txb[2][PAIR ? KT : 1], thb[2][PAIR ? UB : 1];
+  if constexpr (PAIR) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) tdz[q][mt] = pack4(zero4);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) txb[q][kt] = pack4(zero4);
+#pragma unroll
+      for (int s = 0; s < UB; ++s) thb[q][s] = pack4(zero4);
+    }
+  }
+  auto wgrad2 = [&]() {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) accW[mt][kt] = mfma32(tdz[0][mt], tdz[1][mt], txb[0][kt], txb[1][kt], accW[mt][kt]);
+#pragma unroll
+      for (int kb = 0; kb < UB; ++kb) accU[mt][kb] = mfma32(tdz[0][mt], tdz[1][mt], thb[0][kb], thb[1][kb], accU[mt][kb]);
+    }
+  };
 
-  auto step = [&](int t, const Step& cur) {
+  // mode 0: one-step loop (weight gradients one step behind through pdz / pxb / phb);
+  // 1 / 2: first / second step of a pair-loop trip (tdz / txb / thb slot 0 / 1)
+  auto step = [&](int t, const Step& cur, auto mode) {
+    constexpr int M = decltype(mode)::value;
     const int ol = opaque_lane(lane);   // re-materialised per step: fragment reads stay in the loop
     auto fw = [&](int i) { if constexpr (RFW) return rfw[i]; else return wfwd[i * 64 + ol]; };
     auto fu = [&](int i) { if constexpr (RFU) return rfu[i]; else return ufl[i * 64 + ol]; };
@@ -278,7 +309,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) {
       xb[kt] = row_operand(cur.xt[kt], 16 * kt + 4 * g, IN);
-      if constexpr (DBX) xb[kt] |= onex[kt];   // column IN: 0 -> 1.0 (its weights are zero)
+      if constexpr (DB) xb[kt] |= onex[kt];   // columns IN, IN + 1: 0 -> 1.0 (their weights: the bias / 0)
     }
     const bool take_dh = valid && (!a.dh_last_only || t == T - 1);
 #pragma unroll
@@ -286,7 +317,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     f32x4 z[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      z[mt] = *reinterpret_cast<const f32x4*>(sbias + 16 * mt + (ol >> 4) * 4);
+      z[mt] = BX ? zero4 : *reinterpret_cast<const f32x4*>(sbias + 16 * mt + (ol >> 4) * 4);
       constexpr int NK = KT + UB;   // K-tiles in pairs on 16x16x32, exactly as the forward
 #pragma unroll
       for (int k = 0; k + 1 < NK; k += 2)
@@ -295,7 +326,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       if constexpr (NK & 1)   // as the forward: never a 16x16x16 on a 16x16x32 result
         z[mt] = mfma32(fw(mt * NK + NK - 1), bf16x4{0, 0, 0, 0}, hb[UB - 1], bf16x4{0, 0, 0, 0}, z[mt]);
     }
-    wgrad();                                    // step t+1's weight gradients (zeros on the first step)
+    if constexpr (M == 0) wgrad();              // step t+1's weight gradients (zeros on the first step)
+    else if constexpr (M == 1) wgrad2();        // the previous trip's two steps (zeros on the first trip)
     f32x4 cp[UB], dhi[UB];                      // c_{t-1}, incoming dh_t
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
@@ -328,15 +360,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       }
       ctc[b] = cp[b];   // c_{t-1} is the next (earlier) step's c_t
     }
-    if (!valid) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) dzt[mt] = zero4;
-    }
+    // padding lanes (!valid) need no masking here: they never take dh (take_dh) and start
+    // from dcn = 0, and every dz term carries a factor dh or dc, so their dz stays exactly 0
+    // and they add nothing to the weight gradients
     bf16x4 dzb[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       dzb[mt] = pack4(dzt[mt]);
-      if constexpr (!DBX) accb[mt] += dzt[mt];
+      if constexpr (!DB) accb[mt] += dzt[mt];
     }
     // critical path: recurrent gradient for step t-1 -- the 4U gate tiles in pairs on
     // 16x16x32 (MT/2 dependent MFMAs, half the issues of two 16x16x16 half-chains)
@@ -362,24 +393,50 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
         else *reinterpret_cast<bf16x4*>(static_cast<__bf16*>(a.dx) + o) = pack4(acc);
       }
     }
-    // operands of this step's weight gradients, consumed one step later
+    if constexpr (M == 0) {   // operands of this step's weight gradients, consumed one step later
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) pdz[mt] = dzb[mt];
+      for (int mt = 0; mt < MT; ++mt) pdz[mt] = dzb[mt];
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) pxb[kt] = xb[kt];
+      for (int kt = 0; kt < KT; ++kt) pxb[kt] = xb[kt];
 #pragma unroll
-    for (int s = 0; s < UB; ++s) phb[s] = hb[s];
+      for (int s = 0; s < UB; ++s) phb[s] = hb[s];
+    } else {                  // transposed now, contracted by the next trip's first step
+      constexpr int q = M - 1;
+#pragma unroll
+      for (int kb = 0; kb < UB; ++kb) thb[q][kb] = lds_transpose(hb[kb], scr + (MT + KT + kb) * 512, c, g);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) txb[q][kt] = lds_transpose(xb[kt], scr + (MT + kt) * 512, c, g);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) tdz[q][mt] = lds_transpose(dzb[mt], scr + mt * 512, c, g);
+    }
   };
 
   // the next step's operands are in flight while the current one computes (a deeper,
-  // unrolled three-buffer prefetch measured slower for U = 32: 626 vs 525 us)
+  // unrolled three-buffer prefetch measured slower for U = 32: 626 vs 525 us).
+  // Register-fragment builds with the db column (PAIR: layer 1 of the stack, one wave per SIMD anyway) take
+  // two steps per trip with two fixed operand buffers, and only steps whose predecessor is
+  // a stored one (t - 2 >= 1): no buffer copies (the one-step loop moved ~70 registers per
+  // step) and no t = 0 branch splitting the loop body -- 418 -> 362 us for the U = 32 layer
+  // (profiles/r04).  The two-wave builds keep the one-step loop: the pair loop's registers
+  // pushed them past 256 (one wave per SIMD, 247 -> 326 us).
   if (active) {
-    Step cur, nxt;
+    Step nxt;
     load_any(T - 1, nxt);
-    for (int t = T - 1; t >= 0; --t) {
-      cur = nxt;
+    int t = T - 1;
+    if constexpr (PAIR) {   // (with per-step db adds, BM_PLAIN, the pair loop spills at U = 32)
+      Step sb;
+      for (; t >= 3; t -= 2) {
+        load_step(t - 1, sb);
+        step(t, nxt, std::integral_constant<int, 1>{});
+        load_step(t - 2, nxt);
+        step(t - 1, sb, std::integral_constant<int, 2>{});
+      }
+      wgrad2();                                 // the last trip's two steps
+    }
+    for (; t >= 0; --t) {
+      const Step cur = nxt;
       if (t >= 1) load_any(t - 1, nxt);
-      step(t, cur);
+      step(t, cur, std::integral_constant<int, 0>{});
     }
     wgrad();                                    // step 0's weight gradients
   }
@@ -392,7 +449,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     }
   }
   // db: sum the 16 sequence lanes c of each row group (butterfly within 16 lanes)
-  if constexpr (!DBX)
+  if constexpr (!DB)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -418,15 +475,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
           for (int kt = 0; kt < KT; ++kt) slab[m * LDW + 16 * kt + c] += accW[mt][kt][i];
 #pragma unroll
           for (int kb = 0; kb < UB; ++kb) slab[G4 * LDW + m * U + 16 * kb + c] += accU[mt][kb][i];
-          if (!DBX && c == 0) slab[G4 * LDW + G4 * U + m] += accb[mt][i];
+          if (!DB && c == 0) slab[G4 * LDW + G4 * U + m] += accb[mt][i];
         }
     }
   }
   __syncthreads();
-  if constexpr (DBX) {   // db = column IN of dW^T (the constant-1 input); the column itself is padding
+  if constexpr (DB) {   // db = column IN of dW^T (a constant-1 input); columns IN, IN + 1 are padding
     for (int m = threadIdx.x; m < G4; m += WAVES * 64) {
       slab[G4 * LDW + G4 * U + m] = slab[m * LDW + IN];
       slab[m * LDW + IN] = 0.f;
+      if (IN + 1 < LDW) slab[m * LDW + IN + 1] = 0.f;
     }
     __syncthreads();
   }
@@ -444,43 +502,26 @@ hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
   // reads were exposed latency there (SQ_WAIT_ANY 41 % of wave cycles) and the kernel
   // runs 17 % faster (bench_lstm 62.3 -> 68.1 M windows/s, profiles/r02).  With dX, at
   // two waves per SIMD, register fragments measured the same as LDS reads (67.8 vs 67.9).
-  auto go = [&](auto dx, auto rf, auto dbx) {
+  auto go = [&](auto dx, auto rf, auto bmc) {
     constexpr bool DX = decltype(dx)::value;
     constexpr int RF = decltype(rf)::value;
-    constexpr bool DB = decltype(dbx)::value;
+    constexpr int BM = decltype(bmc)::value;
     if (a.act == ACT_RELU)
-      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF, DB>), dim3(grid), dim3(WAVES * 64), 0,
+      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF, BM>), dim3(grid), dim3(WAVES * 64), 0,
                          st, a);
     else
-      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF, DB>), dim3(grid), dim3(WAVES * 64), 0,
+      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF, BM>), dim3(grid), dim3(WAVES * 64), 0,
                          st, a);
   };
-  // the constant-1 column needs a padding column in x (IN < 16*KT).  Off by default: the
-  // compiler keeps the db adds in packed VGPR form, so it saves no instructions (loop count
-  // 403 vs 410 VALU + accumulator moves per step) and db loses its exact fp32 sum.
-  // SML_LSTM_DBX=1 selects it (A/B).
-  static const bool dbx_env = [] {
-    const char* e = std::getenv("SML_LSTM_DBX");
-    return e && e[0] == '1';
-  }();
-  const bool dbx = dbx_env && a.IN < 16 * KT;
-  if (a.dx) {
-    if (dbx) go(std::true_type{}, std::integral_constant<int, 0>{}, std::true_type{});
-    else go(std::true_type{}, std::integral_constant<int, 0>{}, std::false_type{});
-  } else {
-    // SML_LSTM_RF=0: weight fragments read from LDS (fewer registers, more waves per SIMD)
-    static const bool rf_lds = [] {
-      const char* e = std::getenv("SML_LSTM_RF");
-      return e && e[0] == '0';
-    }();
-    if (rf_lds) {
-      if (dbx) go(std::false_type{}, std::integral_constant<int, 0>{}, std::true_type{});
-      else go(std::false_type{}, std::integral_constant<int, 0>{}, std::false_type{});
-    } else {
-      if (dbx) go(std::false_type{}, std::integral_constant<int, 3>{}, std::true_type{});
-      else go(std::false_type{}, std::integral_constant<int, 3>{}, std::false_type{});
+  auto with_bm = [&](auto dx, auto rf) {   // the same decision as the forward (lstm_fused_fwd.hip)
+    switch (bias_mode(a.IN, KT)) {
+      case BM_BX: go(dx, rf, std::integral_constant<int, BM_BX>{}); break;
+      case BM_DB: go(dx, rf, std::integral_constant<int, BM_DB>{}); break;
+      default: go(dx, rf, std::integral_constant<int, BM_PLAIN>{});
     }
-  }
+  };
+  if (a.dx) with_bm(std::true_type{}, std::integral_constant<int, 0>{});
+  else with_bm(std::false_type{}, std::integral_constant<int, 3>{});
   return hipGetLastError();
 }
 

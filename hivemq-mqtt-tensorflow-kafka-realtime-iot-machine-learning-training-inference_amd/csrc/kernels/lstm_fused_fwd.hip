@@ -25,7 +25,10 @@ struct FusedFwdArgs {
   int64_t x_seq;
 };
 
-template <int U, int KT, int XV, typename XT, int ACT>
+// BX: bias columns (lstm_fused_impl.h bias_mode BM_BX): the bias enters through constant-1 x columns
+// IN, IN + 1 and the W^T fragment, so no bias registers (32 VGPRs at U = 32) and no
+// accumulator initialisation -- identical operands to the backward's gate recompute.
+template <int U, int KT, int XV, typename XT, int ACT, bool BX = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdArgs a) {
   using XR = typename RowRaw<XT>::type;
   constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
@@ -48,7 +51,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int k = 16 * kt + 4 * g + j;
-        t4[j] = k < IN ? a.W[(int64_t)k * G4 + 16 * mt + c] : 0.f;
+        t4[j] = BX ? wt_elem_bx(a.W, a.b, G4, IN, k, 16 * mt + c) : (k < IN ? a.W[(int64_t)k * G4 + 16 * mt + c] : 0.f);
       }
       wt[mt][kt] = pack4(t4);
     }
@@ -60,8 +63,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
       ut[mt][s] = pack4(t4);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bias[mt][i] = a.b[16 * mt + 4 * g + i];
+    for (int i = 0; i < 4; ++i) bias[mt][i] = BX ? 0.f : a.b[16 * mt + 4 * g + i];
   }
+  bf16x4 onex[KT];   // BX: the constant-1 bits of x columns IN, IN + 1
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) onex[kt] = BX ? ones_at_bias(kt, g, IN) : bf16x4{0, 0, 0, 0};
   f32x4 h[UB], cs[UB];
   bf16x4 hb[UB];
 #pragma unroll
@@ -93,14 +99,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
   auto fwd_step = [&](int t, XR* xin) {
     bf16x4 xb[KT];
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) xb[kt] = row_operand(xin[kt], 16 * kt + 4 * g, IN);
+    for (int kt = 0; kt < KT; ++kt) {
+      xb[kt] = row_operand(xin[kt], 16 * kt + 4 * g, IN);
+      if constexpr (BX) xb[kt] |= onex[kt];
+    }
     load_x(t + PF < T ? t + PF : T - 1, xin);   // in flight for PF steps
     f32x4 z[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       // z = b + [W ; U]^T . [x_t ; h_{t-1}]^T: the KT + UB K-tiles taken in pairs on the
       // 16x16x32 MFMA (the backward's gate recompute uses the identical pairing)
-      z[mt] = bias[mt];
+      z[mt] = BX ? f32x4{0.f, 0.f, 0.f, 0.f} : bias[mt];
       constexpr int NK = KT + UB;
 #pragma unroll
       for (int k = 0; k + 1 < NK; k += 2)
@@ -145,10 +154,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
 template <int U, int KT, int XV, typename XT>
 hipError_t launch_fwd(const FusedFwdArgs& a, hipStream_t st) {
   const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
-  if (a.act == ACT_RELU)
-    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, XT, ACT_RELU>), dim3(grid), dim3(WAVES * 64), 0, st, a);
-  else
-    hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, XT, ACT_TANH>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  auto go = [&](auto bxc) {
+    constexpr bool BXV = decltype(bxc)::value;
+    if (a.act == ACT_RELU)
+      hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, XT, ACT_RELU, BXV>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+    else
+      hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, XT, ACT_TANH, BXV>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+  };
+  if (bias_mode(a.IN, KT) == BM_BX) go(std::true_type{});   // the same decision as the backward (lstm_fused.hip)
+  else go(std::false_type{});
   return hipGetLastError();
 }
 

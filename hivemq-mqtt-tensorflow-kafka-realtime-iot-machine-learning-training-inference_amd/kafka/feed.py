@@ -61,6 +61,8 @@ class NativeFeed:
         self.resume = resume and group is not None
         self.commit = commit and group is not None
         self.idle_timeout_s = idle_timeout_s
+        # librdkafka's check.crcs (default false): verify every record batch's CRC-32C
+        self.check_crcs = str(parse_config(self.config).get("check.crcs", "false")).lower() in ("true", "1")
         self.last_stats: dict = {}
 
     @property
@@ -92,7 +94,8 @@ class NativeFeed:
                                 [fs.as_tuple() for fs in self.codec.fields], self.feature_fields,
                                 self.label_field, -1 if keep_label is None else int(keep_label), self.framing,
                                 self.max_bytes, self.max_wait_ms, self.workers,
-                                -1.0 if self.idle_timeout_s is None else float(self.idle_timeout_s), parts)
+                                -1.0 if self.idle_timeout_s is None else float(self.idle_timeout_s), parts,
+                                check_crcs=self.check_crcs)
         return f, client, parts
 
     @staticmethod

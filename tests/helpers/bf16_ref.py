@@ -25,14 +25,16 @@ def _act_d(name, z, y):
     return (z > 0).double() if name == "relu" else 1.0 - y * y
 
 
-def lstm_fused_bf16_reference(x, W, U, b, act="relu", dh=None, last_only=False, want_dx=True):
+def lstm_fused_bf16_reference(x, W, U, b, act="relu", dh=None, last_only=False, want_dx=True, db_bf16=False):
     """lstm_fused_fwd.hip + lstm_fused.hip.
 
     Forward: z = b + bf16(x_t) . bf16(W) + bf16(h_{t-1}) . bf16(U); c in fp32, h and c
     stored bf16 (h feeds the next step as the stored bf16 value).
     Backward: gates recomputed from the same operands; the cell state read back as its
     bf16 copy; dh_t = bf16(dh_in) + U . bf16(dz_{t+1}); dz rounded to bf16 for every
-    MFMA consumer (dh recurrence, dx, dW, dU); db = fp32 column sums of dz.
+    MFMA consumer (dh recurrence, dx, dW, dU); db = fp32 column sums of dz, or with
+    ``db_bf16`` (the kernels' bias-column mode, lstm_fused_impl.h bias_in_x: db is the dW^T
+    column of a constant-1 input) of bf16(dz), as dW and dU.
     Returns (h_seq [B, T, u] (bf16 values), dx, dW, dU, db) in float64."""
     B, T, IN = x.shape
     u = U.shape[0]
@@ -79,7 +81,7 @@ def lstm_fused_bf16_reference(x, W, U, b, act="relu", dh=None, last_only=False, 
                         dc * gi * _act_d(act, zg, gc), dht * ac * go * (1 - go)], 1)
         dcn = dc * gf
         dzb = bf(dz)
-        db += dz.sum(0)
+        db += (dzb if db_bf16 else dz).sum(0)
         dhr = dzb @ Ub.t()
         if want_dx:
             dx[:, t] = dzb @ Wb.t()

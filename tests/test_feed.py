@@ -139,3 +139,41 @@ def test_feed_malformed_records_become_nan_missing():
 def test_label_code_matches_python():
     lc = load_io().label_code
     assert [lc(b"false"), lc(b" TRUE "), lc(b""), lc(b"maybe")] == [0, 1, 2, 2]
+
+
+def _bare_feed(codec, feature_idx, label_idx):
+    """A KafkaFeed that is never started: only its decode plan is exercised."""
+    return load_io().KafkaFeed("127.0.0.1:9", "t", "", "", "", 1000, [f.as_tuple() for f in codec.fields],
+                               feature_idx, label_idx, -1, True, 1 << 20, 100, 1, -1.0, [])
+
+
+def test_fast_decode_plan_matches_codec():
+    """The car schema compiles to 5 runs (9 doubles, 4 ints, 4 doubles, 1 int, the label)
+    and decodes every record exactly as the Avro codec; truncated / over-long values fail."""
+    codec = AvroCodec("cardata-v1")
+    names = [f.name for f in codec.fields]
+    feat = [names.index(n) for n in codec.numeric_fields]
+    f = _bare_feed(codec, feat, names.index(codec.text_fields[0]))
+    assert f.fast_plan == 5
+    c = next(iter(S.synthetic(500, chunk=500, seed=11, failure_rate=0.3)))
+    buf, offs = encode_chunk(codec, c.x, c.label)
+    for i in range(500):
+        ok, row, lab = f.decode_row(bytes(buf[offs[i]:offs[i + 1]]))
+        assert ok and lab == int(c.label[i])
+        np.testing.assert_array_equal(np.asarray(row, np.float32), c.x[i].astype(np.float32))
+    v = bytes(buf[offs[0]:offs[1]])
+    assert not f.decode_row(v[:-3])[0] and not f.decode_row(v + b"\x00")[0]
+    # a projection that skips / reorders fields leaves the fast plan's runs consistent
+    g = _bare_feed(codec, feat[::-1][:5], -1)
+    ok, row, _ = g.decode_row(v)
+    assert ok and np.asarray(row, np.float32).tolist() == c.x[0].astype(np.float32)[::-1][:5].tolist()
+
+
+def test_feed_check_crcs_config(topic):
+    """librdkafka's check.crcs=true turns on per-batch CRC-32C verification (default off)."""
+    servers, specs = topic
+    st = S.kafka(servers, specs[:1], native=True, config=["check.crcs=true"])
+    assert st.native_feed.check_crcs
+    ref = S.kafka(servers, specs[:1], native=True)
+    assert not ref.native_feed.check_crcs
+    np.testing.assert_array_equal(np.concatenate([c.x for c in st]), np.concatenate([c.x for c in ref]))

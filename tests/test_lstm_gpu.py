@@ -1,4 +1,6 @@
 """Fused HIP LSTM recurrence vs the plain PyTorch fp32 reference."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -188,6 +190,18 @@ def test_fit_stream_uses_in_place_windows(cuda_device):
     torch.testing.assert_close(a.fp.flat, b.fp.flat, rtol=0, atol=0)
 
 
+def bias_columns(inp: int) -> bool:
+    """lstm_fused_impl.h bias_mode: db comes out of the dW^T column of a constant-1 input
+    (bf16-rounded dz) when the input's K-tile bucket (16, 32 or 64 features) has a spare
+    column -- two for the default bias-column mode, one for SML_LSTM_BIASCOL=d."""
+    kt = (inp + 15) // 16
+    kt = 1 if kt <= 1 else (2 if kt <= 2 else 4)
+    mode = os.environ.get("SML_LSTM_BIASCOL", "1")[:1] or "1"
+    if mode == "0":
+        return False
+    return inp + (2 if mode != "d" else 1) <= 16 * kt or inp + 1 <= 16 * kt
+
+
 @pytest.mark.parametrize("last_only", [False, True])
 @pytest.mark.parametrize("u,act,B,T,inp", [(32, "relu", 100, 7, 18), (16, "tanh", 37, 50, 18),
                                            (32, "tanh", 64, 50, 32), (64, "relu", 20, 4, 18),
@@ -208,7 +222,8 @@ def test_fused_lstm_vs_bf16_rounded_reference(cuda_device, u, act, B, T, inp, la
     dev = [t.to(cuda_device).requires_grad_(True) for t in (x, W, U, b)]
     y = FusedLSTMFunction.apply(*dev, 1 if act == "relu" else 2, last_only)
     (y.float() * gy.to(cuda_device)).sum().backward()
-    hseq, dx, dW, dU, db = lstm_fused_bf16_reference(x, W, U, b, act, dh=gy, last_only=last_only)
+    hseq, dx, dW, dU, db = lstm_fused_bf16_reference(x, W, U, b, act, dh=gy, last_only=last_only,
+                                                     db_bf16=bias_columns(inp))
     yref = hseq[:, -1] if last_only else hseq
     assert relerr(y.detach().cpu(), yref) < 1e-3
     for name, d, r in (("dx", dev[0].grad, dx), ("dW", dev[1].grad, dW), ("dU", dev[2].grad, dU),
