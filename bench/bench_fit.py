@@ -156,6 +156,25 @@ def _fill_topic(b, topic, rows, partitions, failure_rate=0.01, distinct=1_000_00
     return nbytes
 
 
+def _cpu_quota():
+    """CPUs this process may keep busy (cgroup v2 cpu.max / v1 cfs quota), None if unlimited:
+    the feed workers AND the in-process broker's connection threads share it."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else round(q / per, 2)
+    except (OSError, ValueError):
+        return None
+
+
 def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, batch: int = 1 << 20,
                        workers=(1, 2, 4, 8, 16, 32), train_workers: int = 0) -> dict:
     """Fresh rows at large batch: ``partitions`` partitions of Confluent
@@ -180,7 +199,7 @@ def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, bat
     nbytes = _fill_topic(b, topic, rows, partitions)
     out = {"rows": rows, "partitions": partitions, "batch": batch, "log_bytes": nbytes,
            "bytes_per_row": nbytes / rows, "produce_s": time.perf_counter() - t0,
-           "cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0))}
+           "cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_quota": _cpu_quota()}
     specs = [f"{topic}:{p}:0" for p in range(partitions)]
     curve = []
     for w in workers:

@@ -272,7 +272,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   // contracts both steps at once -- K = the 2 x 16 sequence-steps of one 16x16x32 per
   // accumulator tile, so every accumulator is written once per trip (with one 16x16x16 per
   // step the allocator rotated them through spare AGPRs: 96 v_accvgpr_mov per step).
-  constexpr bool PAIR = RF != 0 && DB;
+  constexpr bool PAIR = RF != 0 && DB && !DX;
   bf16x4 tdz[2][PAIR ? MT : 1], txb[2][PAIR ? KT : 1], thb[2][PAIR ? UB : 1];
   if constexpr (PAIR) {
 #pragma unroll
@@ -432,6 +432,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
         step(t - 1, sb, std::integral_constant<int, 2>{});
       }
       wgrad2();                                 // the last trip's two steps
+    } else {
+      for (; t >= 2; --t) {   // one step per trip, no t = 0 branch in the body
+        const Step cur = nxt;
+        load_step(t - 1, nxt);
+        step(t, cur, std::integral_constant<int, 0>{});
+      }
     }
     for (; t >= 0; --t) {
       const Step cur = nxt;
@@ -520,8 +526,23 @@ hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
       default: go(dx, rf, std::integral_constant<int, BM_PLAIN>{});
     }
   };
-  if (a.dx) with_bm(std::true_type{}, std::integral_constant<int, 0>{});
-  else with_bm(std::false_type{}, std::integral_constant<int, 3>{});
+  // U = 16 with dX (layer 2 of the stack): every fragment set fits in registers at two waves
+  // per SIMD (174 VGPRs + 64 AGPRs); SML_LSTM_DXRF=0 reads them from LDS every step (A/B)
+  static const bool dxrf = [] {
+    const char* e = std::getenv("SML_LSTM_DXRF");
+    return !(e && e[0] == '0');
+  }();
+  if (a.dx) {
+    if constexpr (U == 16) {
+      if (dxrf) {
+        with_bm(std::true_type{}, std::integral_constant<int, 7>{});
+        return hipGetLastError();
+      }
+    }
+    with_bm(std::true_type{}, std::integral_constant<int, 0>{});
+  } else {
+    with_bm(std::false_type{}, std::integral_constant<int, 3>{});
+  }
   return hipGetLastError();
 }
 

@@ -28,7 +28,7 @@ struct FusedFwdArgs {
 // BX: bias columns (lstm_fused_impl.h bias_mode BM_BX): the bias enters through constant-1 x columns
 // IN, IN + 1 and the W^T fragment, so no bias registers (32 VGPRs at U = 32) and no
 // accumulator initialisation -- identical operands to the backward's gate recompute.
-template <int U, int KT, int XV, typename XT, int ACT, bool BX = false>
+template <int U, int KT, int XV, typename XT, int ACT, bool BX = false, int PF = 2>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdArgs a) {
   using XR = typename RowRaw<XT>::type;
   constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
@@ -91,8 +91,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
   SML_DCHECK(wv * 16 < a.B + 15 && seq < (a.B + 15) / 16 * 16);   // inside the padded h / c buffers
   __bf16* cw = a.cseq + wv * T * (int64_t)(UB * 256) + lane * 4;
   // x prefetch PF steps ahead in a register ring; the loop is unrolled by PF so every
-  // ring slot is a fixed register set (a rotating copy would wait for the newest load)
-  constexpr int PF = 2;
+  // ring slot is a fixed register set (a rotating copy would wait for the newest load).
+  // vmcnt also counts the h / c stores, in issue order: at PF = 2 the loop waited for
+  // vmcnt(0) -- every load and store of the previous two steps -- once per trip
+
   XR xr[PF][KT];
 #pragma unroll
   for (int p = 0; p < PF; ++p) load_x(p < T ? p : T - 1, xr[p]);
@@ -154,15 +156,28 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
 template <int U, int KT, int XV, typename XT>
 hipError_t launch_fwd(const FusedFwdArgs& a, hipStream_t st) {
   const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
-  auto go = [&](auto bxc) {
+  auto go = [&](auto bxc, auto pfc) {
     constexpr bool BXV = decltype(bxc)::value;
+    constexpr int PF = decltype(pfc)::value;
     if (a.act == ACT_RELU)
-      hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, XT, ACT_RELU, BXV>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+      hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, XT, ACT_RELU, BXV, PF>), dim3(grid), dim3(WAVES * 64), 0, st,
+                         a);
     else
-      hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, XT, ACT_TANH, BXV>), dim3(grid), dim3(WAVES * 64), 0, st, a);
+      hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, XT, ACT_TANH, BXV, PF>), dim3(grid), dim3(WAVES * 64), 0, st,
+                         a);
   };
-  if (bias_mode(a.IN, KT) == BM_BX) go(std::true_type{});   // the same decision as the backward (lstm_fused.hip)
-  else go(std::false_type{});
+  static const int pf = [] {   // SML_LSTM_FWD_PF=2 / 4: x prefetch distance (A/B)
+    const char* e = std::getenv("SML_LSTM_FWD_PF");
+    return e && e[0] == '2' ? 2 : 4;
+  }();
+  const bool bx = bias_mode(a.IN, KT) == BM_BX;   // the same decision as the backward (lstm_fused.hip)
+  if (pf == 2) {
+    if (bx) go(std::true_type{}, std::integral_constant<int, 2>{});
+    else go(std::false_type{}, std::integral_constant<int, 2>{});
+  } else {
+    if (bx) go(std::true_type{}, std::integral_constant<int, 4>{});
+    else go(std::false_type{}, std::integral_constant<int, 4>{});
+  }
   return hipGetLastError();
 }
 
