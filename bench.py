@@ -97,6 +97,9 @@ def parse():
                    help="rows of the Autoencoder.fit(batch_size=100) measurement (0 = skip)")
     p.add_argument("--stream-rows", type=int, default=20_000_000,
                    help="events of the Kafka -> native feed -> fit end-to-end measurement (0 = skip)")
+    p.add_argument("--large-stream-rows", type=int, default=16_000_000,
+                   help="events of the large-batch streaming measurement: decode rows/s vs feed workers, then "
+                        "fit(batch_size=1M) over the stream (0 = skip)")
     return p.parse_args()
 
 
@@ -536,7 +539,7 @@ def main():
 
     if args.headline_only:
         for k in ("infer_events", "e2e_events", "batch32_steps", "dp_steps", "collective_iters", "fit_epochs",
-                  "fresh_steps", "fit_rows", "stream_rows", "lstm_steps", "mqtt_clients"):
+                  "fresh_steps", "fit_rows", "stream_rows", "large_stream_rows", "lstm_steps", "mqtt_clients"):
             setattr(args, k, 0)
 
     rows_per_s = gb * args.steps / elapsed
@@ -656,6 +659,11 @@ def main():
     if args.stream_rows > 0:
         stream = ph.run("stream_e2e", 10 + 1.5e-6 * args.stream_rows, measure_stream_e2e, device, args.stream_rows)
         out.update({"stream_e2e_rows_per_s": stream.get("rows_per_s"), "stream_e2e": stream})
+    if args.large_stream_rows > 0:   # fresh rows at large batch: the host decode curve and the trained rate
+        big = ph.run("stream_large_batch", 12 + 1.2e-6 * args.large_stream_rows,
+                     _bench_module("bench_fit").stream_large_batch, device, rows=args.large_stream_rows,
+                     partitions=32, workers=(1, 2, 4, 8, 16))
+        out.update({"stream_large_batch_rows_per_s": big.get("trained_rows_per_s"), "stream_large_batch": big})
     # BASELINE config 3: LSTM (rank 0; the LSTM trains single-replica here)
     if args.lstm_steps > 0:
         from_b = _bench_module("bench_lstm")

@@ -75,7 +75,7 @@ bool lstm_fused_supported(int U, int IN);
 int lstm_fused_slab(int U, int IN);
 int lstm_fused_dx_ld(int IN);     // row stride of the padded dx buffer the backward kernel writes
 int lstm_fused_waves(int64_t B);
-int lstm_fused_slabs(int64_t B);  // one weight-gradient slab per workgroup
+int lstm_fused_slabs(int64_t B, int U, bool dx);  // backward workgroups = weight-gradient slabs (persistent grid)
 // x: fp32 or bf16 (x_bf16); h and dh are bf16 (lstm_fused.hip header), dx has x's dtype
 hipError_t lstm_fused_fwd_launch(const void* x, bool x_bf16, const float* W, const float* Uw, const float* b,
                                  const float* h0, const float* c0, void* hseq_bf16, void* cseq_bf16, int64_t B, int T,

@@ -141,8 +141,6 @@ struct Smem {   // MB 48: ~47 KB, MB 128: ~108 KB
   alignas(16) unsigned cnt[8];          // pipelined build: stage counters (CE1.., CU1..)
   int stream_last;                      // pipelined build, streaming: index of the last step (INT_MAX: open)
   int first_ok;                         // pipelined build, streaming: the first batch arrived (1)
-  alignas(16) float part[2][64 * 4];    // split phase B: helper waves 6 / 7's partial L4 tiles
-  int part_step[2];                     //   and the step they belong to (+1)
 };
 
 // logical feature of K-step s for lane group g (the C/D register order of the producer)
@@ -344,13 +342,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 
   // ---- phase-B tiles + their Adam moments (registers for the whole launch) ----
   const bool has_tile = wave < 6;
-  // Split phase B (compiled batch >= 64): waves w and w + 4 share a SIMD, so tiles 4 / 5 on
-  // waves 4 / 5 put two tile reductions on SIMDs 0 and 1 and one on SIMDs 2 and 3.  Waves 6
-  // / 7 (SIMDs 2 / 3) reduce the second half of the batch rows of tiles 4 / 5 and hand the
-  // partial to the owner through LDS: every SIMD then carries 1.5 tiles of MFMAs.
-  constexpr bool SPLIT = TB >= 64;
-  const bool helper = SPLIT && wave >= 6;
-  const Tile T = make_tile(has_tile ? wave : (helper ? wave - 2 : 0), c, g, S, sbase);
+  const Tile T = make_tile(has_tile ? wave : 0, c, g, S, sbase);
   float mo[4], vo[4], wo[4];   // Adam moments + the parameters themselves (sole writer)
   int fpos[4], bpos[4];
 #pragma unroll
@@ -369,7 +361,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     S.one[0] = 1.f;
     S.abort = 0;
     S.stream_end = 0;
-    S.part_step[0] = S.part_step[1] = 0;
   }
   const bool dp = DPX && a.dp_ranks > 1;
   const int dp_rank = a.dp_rank0 + (int)blockIdx.x;
@@ -556,29 +547,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // ================= phase B: weight gradients + Adam (waves 0-5) =================
     b1t *= (double)a.beta1;
     b2t *= (double)a.beta2;
-    if (helper) {   // second half of the rows of tile wave - 2 (4 or 5), handed over in LDS
-      if constexpr (SPLIT) {
-        const float* av = sbase + T.act;
-        const float* dv = sbase + T.dz;
-        const int X0 = 4 * (g >> 1), X1 = 4 * (2 + (g >> 1));
-        const int aE = T.as ? (T.am ^ X0) : 0, aO = T.as ? (T.am ^ X1) : 0;
-        const int dE = T.dc ^ X0, dO = T.dc ^ X1;
-        constexpr int NS = (TB + 3) / 4, NH = NS / 2;
-        f32x4 part[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-        for (int s4 = NH; s4 < NS; ++s4) {
-          const int r = 4 * s4 + g;
-          part[s4 & 1] = mfma4(av[r * T.as + ((s4 & 1) ? aO : aE)], dv[r * T.ds + ((s4 & 1) ? dO : dE)], part[s4 & 1]);
-        }
-        const int h = wave - 6;
-        st4(S.part[h] + 4 * lane, part[0] + part[1]);
-        // lgkmcnt(0) only: the partial is in LDS before the flag (a release fence would also
-        // drain vmcnt, i.e. the next batch's row prefetch)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(&S.part_step[h], step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      if (a.want_acc && t - 6 * 64 < B) corr += row_correct<KD>(S.y, S.x, t - 6 * 64, D);
-    }
     if (has_tile) {
       const float lr_t = a.lr * __builtin_amdgcn_sqrtf((float)(1.0 - b2t)) * __builtin_amdgcn_rcpf((float)(1.0 - b1t));
       const float* av = sbase + T.act;
@@ -595,35 +563,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         f32x4 part[CH];
 #pragma unroll
         for (int c4 = 0; c4 < CH; ++c4) part[c4] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const bool split_tile = SPLIT && wave >= 4;   // tiles 4 / 5: rows [0, NS/2) here
-        if (split_tile) {
-          if constexpr (SPLIT) {
 #pragma unroll
-            for (int s4 = 0; s4 < NS / 2; ++s4) {
-              const int r = 4 * s4 + g;
-              part[s4 % CH] = mfma4(av[r * T.as + ((s4 & 1) ? aO : aE)], dv[r * T.ds + ((s4 & 1) ? dO : dE)],
-                                    part[s4 % CH]);
-            }
-          }
-        } else {
-#pragma unroll
-          for (int s4 = 0; s4 < NS; ++s4) {
-            const int r = 4 * s4 + g;   // rows in [B, 4*NS) hold zero gradients
-            part[s4 % CH] = mfma4(av[r * T.as + ((s4 & 1) ? aO : aE)], dv[r * T.ds + ((s4 & 1) ? dO : dE)],
-                                  part[s4 % CH]);
-          }
+        for (int s4 = 0; s4 < NS; ++s4) {
+          const int r = 4 * s4 + g;   // rows in [B, 4*NS) hold zero gradients
+          part[s4 % CH] = mfma4(av[r * T.as + ((s4 & 1) ? aO : aE)], dv[r * T.ds + ((s4 & 1) ? dO : dE)],
+                                part[s4 % CH]);
         }
 #pragma unroll
         for (int c4 = 0; c4 < CH; ++c4) acc += part[c4];
-        if (split_tile) {   // + the helper's half (bounded wait: it runs right after the same barrier)
-          const int h = wave - 4;
-          for (int spin = 0; spin < (1 << 22); ++spin) {
-            if (__hip_atomic_load(&S.part_step[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == step + 1) break;
-            __builtin_amdgcn_s_sleep(1);
-          }
-          asm volatile("" ::: "memory");   // the partial is read after the flag (LDS ops stay in order)
-          acc += ld4(S.part[h] + 4 * lane);
-        }
       } else {
         f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
         const int ns = (B + 3) / 4;
@@ -697,7 +644,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         S.w[fpos[i]] = wo[i];
         S.w[bpos[i]] = wo[i];
       }
-    } else if (!helper && a.want_acc && t - 6 * 64 < B) {
+    } else if (a.want_acc && t - 6 * 64 < B) {
       // categorical accuracy (waves 6-7, one row per lane)
       corr += row_correct<KD>(S.y, S.x, t - 6 * 64, D);
     }

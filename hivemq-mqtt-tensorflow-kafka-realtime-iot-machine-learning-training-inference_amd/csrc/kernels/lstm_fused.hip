@@ -87,7 +87,7 @@ struct FusedBwdArgs {
 // RF: weight A fragments kept in registers for the whole launch instead of re-read from
 // LDS every step (bits: 1 the recurrent U fragments of the dh chain, 2 the gate
 // recompute's [W^T | U^T], 4 the dX fragments W) -- where the registers exist, see launch_bwd.
-template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0, int BM = BM_PLAIN>
+template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0, int BM = BM_PLAIN, bool NP = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdArgs a) {
   constexpr bool BX = BM == BM_BX, DB = BM != BM_PLAIN;   // bias in the MFMAs / db from the dW^T column
   using XR = typename RowRaw<XT>::type;
@@ -108,12 +108,19 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   __shared__ __attribute__((aligned(16))) float sbias[G4];
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int w = threadIdx.x >> 6;
-  const int64_t wave_id = (int64_t)blockIdx.x * WAVES + w;
-  const int64_t s0 = wave_id * 16;
-  const bool active = s0 < a.B;  // waves past B contribute zeros (they still join the block barriers)
-  const int64_t seq = s0 + c;
-  const bool valid = seq < a.B;
-  const int64_t sq = valid ? seq : a.B - 1;
+  // Persistent grid (lstm_fused_slabs): workgroup blockIdx.x takes 4-wave groups of 16-sequence
+  // tiles blockIdx.x, + gridDim.x, ... -- the weight fragments are staged once per workgroup
+  // and the weight gradients of all its tiles land in ONE slab (4x fewer slab bytes written
+  // and re-read by slab_sum at one workgroup per CU).  The per-tile values below are set by
+  // the tile loop; the lambdas read them by reference.
+  const int64_t nblk = (a.B + 16 * WAVES - 1) / (16 * WAVES);
+  int64_t wave_id = (int64_t)blockIdx.x * WAVES + w;
+  int64_t s0 = wave_id * 16;
+  bool active = s0 < a.B;  // waves past B contribute zeros (they still join the block barriers)
+  int64_t seq = s0 + c;
+  bool valid = seq < a.B;
+  int64_t sq = valid ? seq : a.B - 1;
+  bool any_active = false;
   const int IN = a.IN, T = a.T;
   char* scr = scratch[w];
   for (int i = threadIdx.x; i < S; i += WAVES * 64) slab[i] = 0.f;
@@ -233,10 +240,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     else load_step0(st);
   };
 
-  f32x4 ctc[UB];   // c_t
-#pragma unroll
-  for (int b = 0; b < UB; ++b)
-    ctc[b] = active ? unpack4(ld_bf16x4(cw + (int64_t)(T - 1) * (UB * 256) + b * 256)) : zero4;
+  f32x4 ctc[UB];   // c_t (loaded per tile)
 
   // Weight gradients, contracted over the wave's 16 sequences: dz_t^T as A operand and
   // x_t / h_{t-1} as B operands [k = sequence][n = feature | unit], each one LDS transpose
@@ -267,12 +271,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       for (int kb = 0; kb < UB; ++kb) accU[mt][kb] = mfma16(adz, hB[kb], accU[mt][kb]);
     }
   };
-  // Pair loop (RF != 0): each step transposes its own operands right after its dh chain
-  // (slot 0: the pair's first step, slot 1: the second) and the next pair's first step
-  // contracts both steps at once -- K = the 2 x 16 sequence-steps of one 16x16x32 per
-  // accumulator tile, so every accumulator is written once per trip (with one 16x16x16 per
-  // step the allocator rotated them through spare AGPRs: 96 v_accvgpr_mov per step).
-  constexpr bool PAIR = RF != 0 && DB && !DX;
+  // Pair loop (layer 1: register fragments, db column, no dX): each step transposes its own
+  // operands right after its dh chain (slot 0: the trip's first step, slot 1: the second)
+  // and the second step contracts two steps at once -- K = the 2 x 16 sequence-steps of
+  // one 16x16x32 per accumulator tile, so every accumulator is written once per trip (with
+  // one 16x16x16 per step the allocator rotated them through spare AGPRs: 96
+  // v_accvgpr_mov per step).
+  constexpr bool PAIR = RF != 0 && DB && !DX && !NP && XV != 1;   // (scalar-row x: the pair loop spilled)
   bf16x4 tdz[2][PAIR ? MT : 1], txb[2][PAIR ? KT : 1], thb[2][PAIR ? UB : 1];
   if constexpr (PAIR) {
 #pragma unroll
@@ -327,7 +332,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
         z[mt] = mfma32(fw(mt * NK + NK - 1), bf16x4{0, 0, 0, 0}, hb[UB - 1], bf16x4{0, 0, 0, 0}, z[mt]);
     }
     if constexpr (M == 0) wgrad();              // step t+1's weight gradients (zeros on the first step)
-    else if constexpr (M == 1) wgrad2();        // the previous trip's two steps (zeros on the first trip)
+    // (pair loop: the weight gradients are contracted at the end of the second step, below --
+    // placed after the z recompute of the first step the allocator rotated the accumulators
+    // through spare AGPRs: 112 v_accvgpr_mov per trip instead of 32)
+            // the previous trip's two steps (zeros on the first trip)
     f32x4 cp[UB], dhi[UB];                      // c_{t-1}, incoming dh_t
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
@@ -402,6 +410,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       for (int s = 0; s < UB; ++s) phb[s] = hb[s];
     } else {                  // transposed now, contracted by the next trip's first step
       constexpr int q = M - 1;
+      if constexpr (M == 2) wgrad2();         // slot 0: this trip's first step, slot 1: the previous
+                                              // trip's second step (zeros on the first trip)
 #pragma unroll
       for (int kb = 0; kb < UB; ++kb) thb[q][kb] = lds_transpose(hb[kb], scr + (MT + KT + kb) * 512, c, g);
 #pragma unroll
@@ -419,6 +429,38 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   // step) and no t = 0 branch splitting the loop body -- 418 -> 362 us for the U = 32 layer
   // (profiles/r04).  The two-wave builds keep the one-step loop: the pair loop's registers
   // pushed them past 256 (one wave per SIMD, 247 -> 326 us).
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {   // block-uniform trip count
+  wave_id = blk * WAVES + w;
+  s0 = wave_id * 16;
+  active = s0 < a.B;
+  seq = s0 + c;
+  valid = seq < a.B;
+  sq = valid ? seq : a.B - 1;
+  cw = a.cseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
+  any_active |= active;
+  // fresh recurrence and weight-gradient pipeline per tile (the accumulators carry on)
+#pragma unroll
+  for (int b = 0; b < UB; ++b) {
+    dhr[b] = dcn[b] = zero4;
+    ctc[b] = active ? unpack4(ld_bf16x4(cw + (int64_t)(T - 1) * (UB * 256) + b * 256)) : zero4;
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) pdz[mt] = pack4(zero4);
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) pxb[kt] = pack4(zero4);
+#pragma unroll
+  for (int s = 0; s < UB; ++s) phb[s] = pack4(zero4);
+  if constexpr (PAIR) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) tdz[q][mt] = pack4(zero4);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) txb[q][kt] = pack4(zero4);
+#pragma unroll
+      for (int s = 0; s < UB; ++s) thb[q][s] = pack4(zero4);
+    }
+  }
   if (active) {
     Step nxt;
     load_any(T - 1, nxt);
@@ -431,7 +473,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
         load_step(t - 2, nxt);
         step(t - 1, sb, std::integral_constant<int, 2>{});
       }
-      wgrad2();                                 // the last trip's two steps
+      // the second step of a trip contracts (this trip's first step, the previous trip's
+      // second step); left over: the last trip's second step (slot 1) alone
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) tdz[0][mt] = pack4(zero4);
+      wgrad2();
     } else {
       for (; t >= 2; --t) {   // one step per trip, no t = 0 branch in the body
         const Step cur = nxt;
@@ -454,6 +500,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       if (a.dc0) *reinterpret_cast<f32x4*>(a.dc0 + sq * U + off) = dcn[b];
     }
   }
+  }   // tile loop
   // db: sum the 16 sequence lanes c of each row group (butterfly within 16 lanes)
   if constexpr (!DB)
 #pragma unroll
@@ -471,7 +518,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   // column = lane c.
   for (int turn = 0; turn < WAVES; ++turn) {
     __syncthreads();
-    if (turn == w && active) {
+    if (turn == w && any_active) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -502,22 +549,36 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 // per step, which split the time loop into basic blocks the scheduler cannot overlap
 template <int U, int KT, int XV, typename XT>
 hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
-  const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
+  const int grid = lstm_fused_slabs(a.B, U, a.dx != nullptr);
   // Without dX (the first layer of a stack, U = 32 at one wave per SIMD) every weight
   // fragment fits in registers next to the AGPR accumulators: the per-step LDS fragment
   // reads were exposed latency there (SQ_WAIT_ANY 41 % of wave cycles) and the kernel
   // runs 17 % faster (bench_lstm 62.3 -> 68.1 M windows/s, profiles/r02).  With dX, at
   // two waves per SIMD, register fragments measured the same as LDS reads (67.8 vs 67.9).
+  static const bool nopair = [] {   // SML_LSTM_PAIR=0: the one-step loop for layer 1 too (A/B)
+    const char* e = std::getenv("SML_LSTM_PAIR");
+    return e && e[0] == '0';
+  }();
   auto go = [&](auto dx, auto rf, auto bmc) {
     constexpr bool DX = decltype(dx)::value;
     constexpr int RF = decltype(rf)::value;
     constexpr int BM = decltype(bmc)::value;
-    if (a.act == ACT_RELU)
-      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF, BM>), dim3(grid), dim3(WAVES * 64), 0,
-                         st, a);
-    else
-      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF, BM>), dim3(grid), dim3(WAVES * 64), 0,
-                         st, a);
+    auto launch = [&](auto npc) {
+      constexpr bool NP = decltype(npc)::value;
+      if (a.act == ACT_RELU)
+        hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF, BM, NP>), dim3(grid),
+                           dim3(WAVES * 64), 0, st, a);
+      else
+        hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF, BM, NP>), dim3(grid),
+                           dim3(WAVES * 64), 0, st, a);
+    };
+    if constexpr (!DX && RF != 0 && BM != BM_PLAIN) {
+      if (nopair) {
+        launch(std::true_type{});
+        return;
+      }
+    }
+    launch(std::false_type{});
   };
   auto with_bm = [&](auto dx, auto rf) {   // the same decision as the forward (lstm_fused_fwd.hip)
     switch (bias_mode(a.IN, KT)) {
@@ -569,7 +630,23 @@ int lstm_fused_dx_ld(int IN) {
 }
 
 int lstm_fused_waves(int64_t B) { return (int)(((B + 16 * WAVES - 1) / (16 * WAVES)) * WAVES); }
-int lstm_fused_slabs(int64_t B) { return (int)((B + 16 * WAVES - 1) / (16 * WAVES)); }
+int lstm_fused_slabs(int64_t B, int U, bool dx) {
+  const int64_t nblk = (B + 16 * WAVES - 1) / (16 * WAVES);
+  static const int cus = [] {
+    int d = 0, n = 0;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+      n = 0;
+    return n > 0 ? n : 256;
+  }();
+  // resident workgroups per CU: the U = 32 layer without dX runs one wave per SIMD (register
+  // fragments next to the AGPR accumulators), the other builds two
+  const int64_t per_cu = (U == 32 && !dx) ? 1 : 2;
+  static const bool persist = [] {   // SML_LSTM_PERSIST=0: one tile group per workgroup (A/B)
+    const char* e = std::getenv("SML_LSTM_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  return (int)(persist ? std::min<int64_t>(nblk, (int64_t)cus * per_cu) : nblk);
+}
 
 hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, const void* hseq_bf16, const void* x,
                                  bool x_bf16, const float* h0, const float* c0, const float* W, const float* Uw,

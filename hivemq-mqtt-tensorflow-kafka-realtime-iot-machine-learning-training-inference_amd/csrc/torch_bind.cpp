@@ -718,7 +718,7 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
     dc0 = at::empty({B, U}, opts);
   }
   const int S = sml::lstm_fused_slab((int)U, (int)IN);
-  const int G = sml::lstm_fused_slabs(B);
+  const int G = sml::lstm_fused_slabs(B, (int)U, want_dx);
   const int* mp = grad_map(grad, map, S);
   auto partials = at::empty({G, S}, opts);   // every workgroup writes its slab (idle waves add nothing)
   auto out = mp ? *grad : at::empty({S}, opts);

@@ -35,7 +35,8 @@ def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "4", "--warmup", "2", "--batch-per-gpu", "65536",
            "--dataset-rows", "262144", "--infer-events", "2000", "--infer-repeats", "1", "--e2e-events", "0",
-           "--lstm-steps", "0", "--batch32-steps", "2000", "--mqtt-clients", "0", "--dump-params", dump]
+           "--lstm-steps", "0", "--batch32-steps", "2000", "--mqtt-clients", "0", "--large-stream-rows", "400000",
+           "--dump-params", dump]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -55,6 +56,9 @@ def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
     for k in ("fit_batch100", "stream_e2e"):
         assert out[k] and "error" not in out[k], out[k]
         assert out[k]["engine"] == "persistent", out[k]
+    big = out["stream_large_batch"]
+    assert "error" not in big and big["engine"] == "throughput" and big["trained_rows_per_s"] > 0, big
+    assert [c["workers"] for c in big["decode_curve"]] == [1, 2, 4, 8, 16], big
     p0 = np.load(dump + ".rank0.npy")
     p1 = np.load(dump + ".rank1.npy")
     np.testing.assert_array_equal(p0, p1)
@@ -76,6 +80,7 @@ def test_bench_n_ranks_rehearsal(tmp_path, cuda_device, n):
            "--batch32-steps", "2000", "--fleet-models", "64", "--dp-steps", "500", "--collective-iters", "50",
            "--fit-epochs", "2", "--fresh-steps", "2", "--fit-rows", "200000", "--stream-rows", "500000",
            "--lstm-steps", "4", "--mqtt-clients", "2000", "--mqtt-interval", "1", "--mqtt-messages", "2",
+           "--large-stream-rows", "400000",
            "--budget-s", "240", "--dump-params", dump]
     t0 = __import__("time").time()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
@@ -94,7 +99,8 @@ def test_bench_n_ranks_rehearsal(tmp_path, cuda_device, n):
     ph = out["phase_s"]
     for k in ("infer", "small_allreduce", "keras_batch32_dp", "kafka_e2e", "lstm_kafka_e2e", "keras_batch32",
               "fit_large_batch",
-              "fresh_rows", "fit_batch100", "stream_e2e", "lstm_seq50", "lstm_ref", "lstm_infer", "mqtt_e2e",
+              "fresh_rows", "fit_batch100", "stream_e2e", "stream_large_batch", "lstm_seq50", "lstm_ref",
+              "lstm_infer", "mqtt_e2e",
               "total_wall"):
         assert k in ph, (k, ph, out["budget"])
     assert not out["budget"]["skipped"], out["budget"]
@@ -130,7 +136,8 @@ def test_bench_force_pg_rccl_world1(cuda_device):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "4", "--warmup", "2",
            "--batch-per-gpu", "65536", "--dataset-rows", "262144", "--infer-events", "1000", "--infer-repeats", "1",
            "--e2e-events", "0", "--lstm-steps", "0", "--batch32-steps", "2000", "--fit-rows", "0",
-           "--stream-rows", "0", "--dp-steps", "2000", "--collective-iters", "50", "--mqtt-clients", "0"]
+           "--stream-rows", "0", "--large-stream-rows", "0", "--dp-steps", "2000", "--collective-iters", "50",
+           "--mqtt-clients", "0"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
