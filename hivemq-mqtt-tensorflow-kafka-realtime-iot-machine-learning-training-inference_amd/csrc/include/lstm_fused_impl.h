@@ -129,16 +129,24 @@ hipError_t dispatch(int U, int IN, int xv, bool x_bf16, F&& f) {
 // In BX and DB db is the sum of bf16-rounded dz (the dW / dU precision) instead of fp32.
 // SML_LSTM_BIASCOL=0 / 1 / d selects PLAIN / BX / DB where the layer admits it (A/B;
 // default BX, else DB, else PLAIN).
+// SML_LSTM_BIASCOL=m (A/B): the backward in BX mode under a plain forward -- the recomputed
+// pre-activations then differ from the forward's by the bias's fp32 rounding (not bit-identical).
 constexpr int BM_PLAIN = 0, BM_BX = 1, BM_DB = 2;
-inline int bias_mode(int IN, int KT) {
+inline char bias_env() {
   static const char m = [] {
     const char* e = std::getenv("SML_LSTM_BIASCOL");
     return e && e[0] ? e[0] : '1';
   }();
+  return m;
+}
+inline int bias_mode(int IN, int KT) {
+  const char m = bias_env();
   if (m == '0') return BM_PLAIN;
   if (m != 'd' && IN + 2 <= 16 * KT) return BM_BX;
   return IN + 1 <= 16 * KT ? BM_DB : BM_PLAIN;
 }
+// the forward's bias mode: the backward's, except under SML_LSTM_BIASCOL=m
+inline int bias_mode_fwd(int IN, int KT) { return bias_env() == 'm' ? BM_PLAIN : bias_mode(IN, KT); }
 
 // lane (c, g)'s constant-1 bits for x tile kt (BX / DB): bf16 1.0 at columns IN, IN + 1
 // (in DB column IN + 1, if it exists, also has zero weights: one more padding column)

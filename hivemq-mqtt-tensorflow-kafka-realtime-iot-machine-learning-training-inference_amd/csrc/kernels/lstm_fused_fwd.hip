@@ -171,7 +171,7 @@ hipError_t launch_fwd(const FusedFwdArgs& a, hipStream_t st) {
     const char* e = std::getenv("SML_LSTM_FWD_PF");
     return e && e[0] == '4' ? 4 : 2;
   }();
-  const bool bx = bias_mode(a.IN, KT) == BM_BX;   // the same decision as the backward (lstm_fused.hip)
+  const bool bx = bias_mode_fwd(a.IN, KT) == BM_BX;   // the same decision as the backward (lstm_fused.hip)
   if (pf == 2) {
     if (bx) go(std::true_type{}, std::integral_constant<int, 2>{});
     else go(std::false_type{}, std::integral_constant<int, 2>{});

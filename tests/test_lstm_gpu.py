@@ -199,7 +199,7 @@ def bias_columns(inp: int) -> bool:
     mode = os.environ.get("SML_LSTM_BIASCOL", "1")[:1] or "1"
     if mode == "0":
         return False
-    return inp + (2 if mode != "d" else 1) <= 16 * kt or inp + 1 <= 16 * kt
+    return inp + 1 <= 16 * kt   # bias columns (2 spare) or, failing that, the db column (1 spare)
 
 
 @pytest.mark.parametrize("last_only", [False, True])
