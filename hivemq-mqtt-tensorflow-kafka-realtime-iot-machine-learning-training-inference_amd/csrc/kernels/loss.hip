@@ -15,7 +15,10 @@
 // bcast = 1) are contiguous, so they come in and the gradient goes out as coalesced
 // 16-byte accesses (a lane walking its own 72-byte row issued F scalar loads and stores
 // per lane, 4-5x slower at F = 18).  Per-block partial sums are reduced with shuffles +
-// LDS and ONE atomic per block into acc [loss_sum, correct]; torch-side this replaces
+// LDS into one partial per block; a one-block kernel then folds the partials into acc
+// [loss_sum, correct] in a fixed order (deterministic).  The earlier one-atomic-per-block
+// fold serialised ~1000 same-address float atomics: 17.4 vs 4.4 us for the kernel at
+// 65 536 x 18 (profiles/r04, tools/lstm_probe/head_probe.py).  Torch-side this replaces
 // ~10 elementwise / reduction kernels per training step.
 #include "sml_common.h"
 #include "sml_ops.h"
@@ -31,7 +34,7 @@ __global__ __launch_bounds__(rows_per_block<F>()) void mse_acc_kernel(const floa
                                                                       const float* __restrict__ y, int64_t rows,
                                                                       int bcast, float gscale,
                                                                       float* __restrict__ grad,
-                                                                      float* __restrict__ acc) {
+                                                                      float* __restrict__ part) {
   constexpr int RPB = rows_per_block<F>(), NW = RPB / 64;
   __shared__ __attribute__((aligned(16))) float sp[RPB * F];
   __shared__ __attribute__((aligned(16))) float st[RPB * F];
@@ -84,7 +87,7 @@ __global__ __launch_bounds__(rows_per_block<F>()) void mse_acc_kernel(const floa
       for (int i = threadIdx.x; i < n; i += RPB) gb[i] = sp[i];
     }
   }
-  if (acc) {
+  if (part) {
     se = wave_sum(se);
     correct = wave_sum(correct);
     const int w = threadIdx.x >> 6;
@@ -100,23 +103,54 @@ __global__ __launch_bounds__(rows_per_block<F>()) void mse_acc_kernel(const floa
         a += red[0][i];
         b += red[1][i];
       }
-      atomicAdd(acc, a);
-      atomicAdd(acc + 1, b);
+      part[2 * blockIdx.x] = a;
+      part[2 * blockIdx.x + 1] = b;
     }
+  }
+}
+
+// acc[k] (+)= sum over the n block partials part[2 i + k], in a fixed order
+__global__ __launch_bounds__(256) void acc_fold_kernel(const float* __restrict__ part, int n, float* __restrict__ acc,
+                                                       int reset) {
+  __shared__ float red[2][4];
+  float a = 0.f, b = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    a += part[2 * i];
+    b += part[2 * i + 1];
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = a;
+    red[1][w] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float sa = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    const float sb = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    acc[0] = reset ? sa : acc[0] + sa;
+    acc[1] = reset ? sb : acc[1] + sb;
   }
 }
 
 }  // namespace
 
+int mse_acc_blocks(int64_t rows, int F) {
+  const int R = F <= 16 ? 256 : (F <= 32 ? 128 : 64);   // rows_per_block<F>()
+  return (int)((rows + R - 1) / R);
+}
+
 hipError_t mse_acc_launch(const float* yp, const float* y, int64_t rows, int F, int bcast, float gscale, float* grad,
-                          float* acc, hipStream_t stream) {
+                          float* acc, float* part, int reset, hipStream_t stream) {
   if (rows <= 0) return hipSuccess;
-  if (bcast < 1) return hipErrorInvalidValue;
+  if (bcast < 1 || (acc && !part)) return hipErrorInvalidValue;
+  float* pp = acc ? part : nullptr;
 #define SML_F(n)                                                                                              \
   case n: {                                                                                                  \
     constexpr int R = rows_per_block<n>();                                                                   \
     hipLaunchKernelGGL(mse_acc_kernel<n>, dim3((unsigned)((rows + R - 1) / R)), dim3(R), 0, stream, yp, y, rows, \
-                       bcast, gscale, grad, acc);                                                            \
+                       bcast, gscale, grad, pp);                                                             \
     break;                                                                                                   \
   }
   switch (F) {
@@ -124,6 +158,7 @@ hipError_t mse_acc_launch(const float* yp, const float* y, int64_t rows, int F, 
     default: return hipErrorInvalidValue;
   }
 #undef SML_F
+  if (acc) hipLaunchKernelGGL(acc_fold_kernel, dim3(1), dim3(256), 0, stream, part, mse_acc_blocks(rows, F), acc, reset);
   return hipGetLastError();
 }
 

@@ -846,7 +846,7 @@ at::Tensor lstm_ref_train(const at::Tensor& flat, const at::Tensor& m, const at:
 
 // K3 + K6: (y_pred - y) * gscale -> grad, [sum sq err, #correct rows] += into acc.
 void mse_acc(const at::Tensor& yp, const at::Tensor& y, int64_t bcast, double gscale,
-             const c10::optional<at::Tensor>& grad, const c10::optional<at::Tensor>& acc) {
+             const c10::optional<at::Tensor>& grad, const c10::optional<at::Tensor>& acc, bool reset) {
   check_dev(yp, "y_pred", at::kFloat);
   check_dev(y, "y", at::kFloat);
   TORCH_CHECK(yp.is_contiguous() && y.is_contiguous(), "inputs must be contiguous");
@@ -863,8 +863,11 @@ void mse_acc(const at::Tensor& yp, const at::Tensor& y, int64_t bcast, double gs
     TORCH_CHECK(acc->numel() >= 2, "acc needs 2 floats");
   }
   c10::hip::HIPGuard guard(yp.device().index());
+  at::Tensor part;
+  if (acc.has_value()) part = at::empty({2 * (int64_t)sml::mse_acc_blocks(rows, (int)F)}, yp.options());
   SML_CHECK_HIP(sml::mse_acc_launch(yp.data_ptr<float>(), y.data_ptr<float>(), rows, (int)F, (int)bcast,
-                                    (float)gscale, opt_mut(grad), opt_mut(acc), cur_stream(yp)));
+                                    (float)gscale, opt_mut(grad), opt_mut(acc),
+                                    part.defined() ? part.data_ptr<float>() : nullptr, reset ? 1 : 0, cur_stream(yp)));
 }
 
 at::Tensor lane_xor_probe(const at::Tensor& like) {
@@ -1272,7 +1275,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       })
       .def_property_readonly("nkeys", [](LSTMServePy& p) { return p.nk; });
   m.def("mse_acc", &mse_acc, "fused MSE fwd/bwd + categorical accuracy (K3 + K6)", py::arg("y_pred"), py::arg("y"),
-        py::arg("bcast") = 1, py::arg("gscale") = 1.0, py::arg("grad") = py::none(), py::arg("acc") = py::none());
+        py::arg("bcast") = 1, py::arg("gscale") = 1.0, py::arg("grad") = py::none(), py::arg("acc") = py::none(),
+        py::arg("reset") = false);
   m.def("mse_acc_supported", &sml::mse_acc_supported, "feature counts with a fused MSE kernel", py::arg("F"));
   m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),

@@ -261,10 +261,9 @@ class LSTMPredictor:
         y_pred = C.dense_fwd(hin, K, bh, 0, False, 1024, False)
         yt = y.to(device=self.device, dtype=torch.float32).contiguous()
         acc = plan["acc"]
-        acc.zero_()
         dy = torch.empty_like(y_pred)
         scale = n / float(global_batch or n)           # mean over the global batch under DP
-        C.mse_acc(y_pred, yt, R or 1, 2.0 / y_pred.numel() * scale, dy, acc)
+        C.mse_acc(y_pred, yt, R or 1, 2.0 / y_pred.numel() * scale, dy, acc, reset=True)   # acc = this step's sums
         C.dense_wgrad(hin, dy, 0, True, 1024, grad, plan["head_map"])
         dh = C.dense_fwd(dy, K, None, 0, True, 1024, True)   # dh = dy . K^T, bf16
         layers = pre + post
@@ -282,7 +281,7 @@ class LSTMPredictor:
                 dh = (dh.view(n, -1) if R == 1 else dh.sum(1)).to(torch.bfloat16)
         self.opt.step(allreduce=allreduce)
         correct = acc[1] / float(R) if R else acc[1].clone()
-        return acc[0] / y_pred.numel(), correct   # acc is re-zeroed by the next step
+        return acc[0] / y_pred.numel(), correct   # acc is overwritten by the next step
 
     # ------------------------------------------------------------------ training
     def fit(self, x, y=None, epochs: int = 1, batch_size: int = 1, verbose: int = 1, take: Optional[int] = None,

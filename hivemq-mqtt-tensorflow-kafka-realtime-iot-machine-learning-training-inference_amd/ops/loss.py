@@ -19,8 +19,8 @@ class MSEAccuracy(torch.autograd.Function):
         yp = y_pred.contiguous()
         n = yp.numel()
         grad = torch.empty_like(yp)
-        acc = torch.zeros(2, device=yp.device)
-        load_c().mse_acc(yp, y.contiguous(), int(bcast), 2.0 / n, grad, acc)
+        acc = torch.empty(2, device=yp.device)
+        load_c().mse_acc(yp, y.contiguous(), int(bcast), 2.0 / n, grad, acc, reset=True)
         ctx.save_for_backward(grad)
         correct = acc[1] / float(bcast)
         ctx.mark_non_differentiable(correct)
