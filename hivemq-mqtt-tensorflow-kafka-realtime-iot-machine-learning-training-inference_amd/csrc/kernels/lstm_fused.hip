@@ -87,7 +87,7 @@ struct FusedBwdArgs {
 // RF: weight A fragments kept in registers for the whole launch instead of re-read from
 // LDS every step (bits: 1 the recurrent U fragments of the dh chain, 2 the gate
 // recompute's [W^T | U^T], 4 the dX fragments W) -- where the registers exist, see launch_bwd.
-template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0, int BM = BM_PLAIN, bool NP = false>
+template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0, int BM = BM_PLAIN>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdArgs a) {
   constexpr bool BX = BM == BM_BX, DB = BM != BM_PLAIN;   // bias in the MFMAs / db from the dW^T column
   using XR = typename RowRaw<XT>::type;
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   // one 16x16x32 per accumulator tile, so every accumulator is written once per trip (with
   // one 16x16x16 per step the allocator rotated them through spare AGPRs: 96
   // v_accvgpr_mov per step).
-  constexpr bool PAIR = RF != 0 && DB && !DX && !NP && XV != 1;   // (scalar-row x: the pair loop spilled)
+  constexpr bool PAIR = RF != 0 && DB && !DX && XV != 1;   // (scalar-row x: the pair loop spilled)
   bf16x4 tdz[2][PAIR ? MT : 1], txb[2][PAIR ? KT : 1], thb[2][PAIR ? UB : 1];
   if constexpr (PAIR) {
 #pragma unroll
@@ -555,30 +555,16 @@ hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
   // reads were exposed latency there (SQ_WAIT_ANY 41 % of wave cycles) and the kernel
   // runs 17 % faster (bench_lstm 62.3 -> 68.1 M windows/s, profiles/r02).  With dX, at
   // two waves per SIMD, register fragments measured the same as LDS reads (67.8 vs 67.9).
-  static const bool nopair = [] {   // SML_LSTM_PAIR=0: the one-step loop for layer 1 too (A/B)
-    const char* e = std::getenv("SML_LSTM_PAIR");
-    return e && e[0] == '0';
-  }();
   auto go = [&](auto dx, auto rf, auto bmc) {
     constexpr bool DX = decltype(dx)::value;
     constexpr int RF = decltype(rf)::value;
     constexpr int BM = decltype(bmc)::value;
-    auto launch = [&](auto npc) {
-      constexpr bool NP = decltype(npc)::value;
-      if (a.act == ACT_RELU)
-        hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF, BM, NP>), dim3(grid),
-                           dim3(WAVES * 64), 0, st, a);
-      else
-        hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF, BM, NP>), dim3(grid),
-                           dim3(WAVES * 64), 0, st, a);
-    };
-    if constexpr (!DX && RF != 0 && BM != BM_PLAIN) {
-      if (nopair) {
-        launch(std::true_type{});
-        return;
-      }
-    }
-    launch(std::false_type{});
+    if (a.act == ACT_RELU)
+      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF, BM>), dim3(grid), dim3(WAVES * 64), 0,
+                         st, a);
+    else
+      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF, BM>), dim3(grid), dim3(WAVES * 64), 0,
+                         st, a);
   };
   auto with_bm = [&](auto dx, auto rf) {   // the same decision as the forward (lstm_fused_fwd.hip)
     switch (bias_mode(a.IN, KT)) {
@@ -588,19 +574,10 @@ hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
     }
   };
   // U = 16 with dX (layer 2 of the stack): every fragment set fits in registers at two waves
-  // per SIMD (174 VGPRs + 64 AGPRs); SML_LSTM_DXRF=0 reads them from LDS every step (A/B)
-  static const bool dxrf = [] {
-    const char* e = std::getenv("SML_LSTM_DXRF");
-    return !(e && e[0] == '0');
-  }();
+  // per SIMD (174 VGPRs + 64 AGPRs); U = 32 with dX reads them from LDS every step
   if (a.dx) {
-    if constexpr (U == 16) {
-      if (dxrf) {
-        with_bm(std::true_type{}, std::integral_constant<int, 7>{});
-        return hipGetLastError();
-      }
-    }
-    with_bm(std::true_type{}, std::integral_constant<int, 0>{});
+    if constexpr (U == 16) with_bm(std::true_type{}, std::integral_constant<int, 7>{});
+    else with_bm(std::true_type{}, std::integral_constant<int, 0>{});
   } else {
     with_bm(std::false_type{}, std::integral_constant<int, 3>{});
   }

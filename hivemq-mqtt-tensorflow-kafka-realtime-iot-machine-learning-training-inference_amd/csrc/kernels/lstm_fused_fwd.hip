@@ -166,19 +166,9 @@ hipError_t launch_fwd(const FusedFwdArgs& a, hipStream_t st) {
       hipLaunchKernelGGL((lstm_fused_fwd_kernel<U, KT, XV, XT, ACT_TANH, BXV, PF>), dim3(grid), dim3(WAVES * 64), 0, st,
                          a);
   };
-  static const int pf = [] {   // SML_LSTM_FWD_PF=2 / 4: x prefetch distance (A/B; 2 measured best with
-                               // the bias columns, profiles/r04 r04g / r04h)
-    const char* e = std::getenv("SML_LSTM_FWD_PF");
-    return e && e[0] == '4' ? 4 : 2;
-  }();
-  const bool bx = bias_mode_fwd(a.IN, KT) == BM_BX;   // the same decision as the backward (lstm_fused.hip)
-  if (pf == 2) {
-    if (bx) go(std::true_type{}, std::integral_constant<int, 2>{});
-    else go(std::false_type{}, std::integral_constant<int, 2>{});
-  } else {
-    if (bx) go(std::true_type{}, std::integral_constant<int, 4>{});
-    else go(std::false_type{}, std::integral_constant<int, 4>{});
-  }
+  // x prefetch distance 2 (4 measured within noise and costs registers: profiles/r04)
+  if (bias_mode_fwd(a.IN, KT) == BM_BX) go(std::true_type{}, std::integral_constant<int, 2>{});   // as the backward
+  else go(std::false_type{}, std::integral_constant<int, 2>{});
   return hipGetLastError();
 }
 
