@@ -148,17 +148,6 @@ inline int bias_mode(int IN, int KT) {
 // the forward's bias mode: the backward's, except under SML_LSTM_BIASCOL=m
 inline int bias_mode_fwd(int IN, int KT) { return bias_env() == 'm' ? BM_PLAIN : bias_mode(IN, KT); }
 
-// Pre-scaled sigmoid gates: the W / U / bias entries of the i, f and o gates enter the MFMA
-// operands multiplied by -log2(e), so those pre-activations come out as z' = -log2(e) z and a
-// gate is rcp(1 + exp2(z')) -- one multiply per gate value less (24 per step of a 32-unit
-// layer, ~12 % of the forward's issue).  Both kernels build their recompute operands the same
-// way (the backward's pre-activations stay the forward's, bit for bit); the dh chain and dX
-// use the unscaled U and W.  (bf16 rounding of -log2(e) w instead of w: tests/helpers/bf16_ref.py.)
-constexpr float kNegLog2e = -1.4426950408889634f;
-// scale of gate row m (0..4U): i, f, o rows by -log2(e), the cell-candidate rows c by 1
-__device__ __forceinline__ float gate_scale(int m, int U) { return (m / U) == 2 ? 1.f : kNegLog2e; }
-__device__ __forceinline__ float sigmoid_pre(float zs) { return rcp_fast(1.0f + __builtin_amdgcn_exp2f(zs)); }
-
 // lane (c, g)'s constant-1 bits for x tile kt (BX / DB): bf16 1.0 at columns IN, IN + 1
 // (in DB column IN + 1, if it exists, also has zero weights: one more padding column)
 __device__ __forceinline__ bf16x4 ones_at_bias(int kt, int g, int IN) {
@@ -172,11 +161,9 @@ __device__ __forceinline__ bf16x4 ones_at_bias(int kt, int g, int IN) {
 }
 
 // W^T fragment element (gate m, feature f) in BX mode: the weight, or the bias hi / lo parts
-// (all times the gate row's scale)
 __device__ __forceinline__ float wt_elem_bx(const float* W, const float* b, int G4, int IN, int f, int m) {
-  const float sc = gate_scale(m, G4 / 4);
-  if (f < IN) return sc * W[(int64_t)f * G4 + m];
-  const float bv = sc * b[m];
+  if (f < IN) return W[(int64_t)f * G4 + m];
+  const float bv = b[m];
   const float hi = bf16_to_f32((unsigned short)(pack2(bv, 0.f) & 0xFFFFu));   // RNE, as the fragment pack
   if (f == IN) return hi;
   if (f == IN + 1) return bv - hi;

@@ -124,7 +124,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   const int IN = a.IN, T = a.T;
   char* scr = scratch[w];
   for (int i = threadIdx.x; i < S; i += WAVES * 64) slab[i] = 0.f;
-  for (int i = threadIdx.x; i < G4; i += WAVES * 64) sbias[i] = gate_scale(i, U) * a.bias[i];   // recompute operand
+  for (int i = threadIdx.x; i < G4; i += WAVES * 64) sbias[i] = a.bias[i];
   // tile (mt, k) of [W^T | U^T]: k < KT -> W^T[m = gate 16mt + c][feature 16k + 4g + j],
   //                              k >= KT -> U^T[m = gate][unit 16(k-KT) + 4g + j]
   for (int tile = w; tile < MT * (KT + UB); tile += WAVES) {
@@ -134,10 +134,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     for (int j = 0; j < 4; ++j) {
       if (k < KT) {
         const int f = 16 * k + 4 * g + j;
-        t4[j] = BX ? wt_elem_bx(a.W, a.bias, G4, IN, f, 16 * mt + c)
-                   : (f < IN ? gate_scale(16 * mt + c, U) * a.W[(int64_t)f * G4 + 16 * mt + c] : 0.f);
+        t4[j] = BX ? wt_elem_bx(a.W, a.bias, G4, IN, f, 16 * mt + c) : (f < IN ? a.W[(int64_t)f * G4 + 16 * mt + c] : 0.f);
       } else {
-        t4[j] = gate_scale(16 * mt + c, U) * a.Uw[(16 * (k - KT) + 4 * g + j) * G4 + 16 * mt + c];
+        t4[j] = a.Uw[(16 * (k - KT) + 4 * g + j) * G4 + 16 * mt + c];
       }
     }
     wfwd[tile * 64 + lane] = pack4(t4);
@@ -349,8 +348,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         // fp32 gates, exactly the values the forward used for c_t / h_t
-        const float gi = sigmoid_pre(z[b][i]), gf = sigmoid_pre(z[UB + b][i]);   // pre-scaled rows, as the forward
-        const float gc = act_f(ACT, z[2 * UB + b][i]), go = sigmoid_pre(z[3 * UB + b][i]);
+        const float gi = sigmoid_fast(z[b][i]), gf = sigmoid_fast(z[UB + b][i]);
+        const float gc = act_f(ACT, z[2 * UB + b][i]), go = sigmoid_fast(z[3 * UB + b][i]);
         const float dh = (take_dh ? dhi[b][i] : 0.f) + dhr[b][i];
         const float ct = ctc[b][i];
         const float ac = act_f(ACT, ct);

@@ -51,8 +51,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int k = 16 * kt + 4 * g + j;
-        t4[j] = BX ? wt_elem_bx(a.W, a.b, G4, IN, k, 16 * mt + c)
-                   : (k < IN ? gate_scale(16 * mt + c, U) * a.W[(int64_t)k * G4 + 16 * mt + c] : 0.f);
+        t4[j] = BX ? wt_elem_bx(a.W, a.b, G4, IN, k, 16 * mt + c) : (k < IN ? a.W[(int64_t)k * G4 + 16 * mt + c] : 0.f);
       }
       wt[mt][kt] = pack4(t4);
     }
@@ -60,11 +59,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
     for (int s = 0; s < UB; ++s) {
       f32x4 t4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) t4[j] = gate_scale(16 * mt + c, U) * a.Uw[(16 * s + 4 * g + j) * G4 + 16 * mt + c];
+      for (int j = 0; j < 4; ++j) t4[j] = a.Uw[(16 * s + 4 * g + j) * G4 + 16 * mt + c];
       ut[mt][s] = pack4(t4);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bias[mt][i] = BX ? 0.f : gate_scale(16 * mt + 4 * g + i, U) * a.b[16 * mt + 4 * g + i];
+    for (int i = 0; i < 4; ++i) bias[mt][i] = BX ? 0.f : a.b[16 * mt + 4 * g + i];
   }
   bf16x4 onex[KT];   // BX: the constant-1 bits of x columns IN, IN + 1
 #pragma unroll
@@ -132,10 +131,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
       f32x4 gi, gf, gc, go;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        gi[i] = sigmoid_pre(z[b][i]);   // i, f, o rows pre-scaled by -log2(e) (lstm_fused_impl.h)
-        gf[i] = sigmoid_pre(z[UB + b][i]);
+        gi[i] = sigmoid_fast(z[b][i]);
+        gf[i] = sigmoid_fast(z[UB + b][i]);
         gc[i] = act_f(ACT, z[2 * UB + b][i]);
-        go[i] = sigmoid_pre(z[3 * UB + b][i]);
+        go[i] = sigmoid_fast(z[3 * UB + b][i]);
         cs[b][i] = fmaf(gf[i], cs[b][i], gi[i] * gc[i]);
         h[b][i] = go[i] * act_f(ACT, cs[b][i]);
       }

@@ -264,9 +264,7 @@ class LSTMPredictor:
         dy = torch.empty_like(y_pred)
         scale = n / float(global_batch or n)           # mean over the global batch under DP
         C.mse_acc(y_pred, yt, R or 1, 2.0 / y_pred.numel() * scale, dy, acc, reset=True)   # acc = this step's sums
-        # 256 weight-gradient slabs (rows per block grow with n): the slab reduction, not the
-        # contraction, dominated the head's weight gradient at 1024 slabs (11.3 us, profiles/r04)
-        C.dense_wgrad(hin, dy, 0, True, 256, grad, plan["head_map"])
+        C.dense_wgrad(hin, dy, 0, True, 1024, grad, plan["head_map"])
         dh = C.dense_fwd(dy, K, None, 0, True, 1024, True)   # dh = dy . K^T, bf16
         layers = pre + post
         for i in range(len(layers) - 1, -1, -1):

@@ -28,8 +28,7 @@ def _act_d(name, z, y):
 def lstm_fused_bf16_reference(x, W, U, b, act="relu", dh=None, last_only=False, want_dx=True, db_bf16=False):
     """lstm_fused_fwd.hip + lstm_fused.hip.
 
-    Forward: z = b + bf16(x_t) . bf16(W) + bf16(h_{t-1}) . bf16(U) (i, f, o gate columns of W
-    and U rounded as bf16(-log2(e) w) / -log2(e): the kernels' pre-scaled operands); c in fp32, h and c
+    Forward: z = b + bf16(x_t) . bf16(W) + bf16(h_{t-1}) . bf16(U); c in fp32, h and c
     stored bf16 (h feeds the next step as the stored bf16 value).
     Backward: gates recomputed from the same operands; the cell state read back as its
     bf16 copy; dh_t = bf16(dh_in) + U . bf16(dz_{t+1}); dz rounded to bf16 for every
@@ -40,19 +39,12 @@ def lstm_fused_bf16_reference(x, W, U, b, act="relu", dh=None, last_only=False, 
     B, T, IN = x.shape
     u = U.shape[0]
     xb, Wb, Ub = bf(x), bf(W), bf(U)
-    # forward / recompute operands: the i, f, o gate columns enter the MFMAs pre-scaled by
-    # -log2(e) (lstm_fused_impl.h gate_scale), i.e. rounded to bf16 as -log2(e) w; the dh
-    # chain and dX use the plainly rounded weights
-    sc = torch.full((4 * u,), -1.4426950408889634, dtype=torch.float64)
-    sc[2 * u:3 * u] = 1.0
-    Wf = bf(W.double() * sc) / sc
-    Uf = bf(U.double() * sc) / sc
     bb = b.double()
     h = torch.zeros(B, u, dtype=torch.float64)
     c = torch.zeros(B, u, dtype=torch.float64)
     hs, cs = [], []
     for t in range(T):
-        z = bb + xb[:, t] @ Wf + bf(h) @ Uf
+        z = bb + xb[:, t] @ Wb + bf(h) @ Ub
         i, f, g, o = z.split(u, dim=1)
         i, f, o = torch.sigmoid(i), torch.sigmoid(f), torch.sigmoid(o)
         c = f * c + i * _act(act, g)
@@ -73,7 +65,7 @@ def lstm_fused_bf16_reference(x, W, U, b, act="relu", dh=None, last_only=False, 
     for t in range(T - 1, -1, -1):
         hp = hs[t - 1] if t > 0 else zero
         cp = cs[t - 1] if t > 0 else zero
-        z = bb + xb[:, t] @ Wf + hp @ Uf
+        z = bb + xb[:, t] @ Wb + hp @ Ub
         zi, zf, zg, zo = z.split(u, dim=1)
         gi, gf, go = torch.sigmoid(zi), torch.sigmoid(zf), torch.sigmoid(zo)
         gc = _act(act, zg)

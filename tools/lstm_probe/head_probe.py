@@ -45,7 +45,6 @@ def main():
         "mse_acc_us": timed(lambda: C.mse_acc(yp, y, 1, 1e-5, dy, acc)),
         "mse_noacc_us": timed(lambda: C.mse_acc(yp, y, 1, 1e-5, dy, None)),
         "dense_wgrad_us": timed(lambda: C.dense_wgrad(hin, dy, 0, True, 1024, m.fp.grad, plan["head_map"])),
-        "dense_wgrad256_us": timed(lambda: C.dense_wgrad(hin, dy, 0, True, 256, m.fp.grad, plan["head_map"])),
         "dense_dh_us": timed(lambda: C.dense_fwd(dy, K, None, 0, True, 1024, True)),
         "acc_zero_us": timed(lambda: acc.zero_()),
         "y_to_contig_us": timed(lambda: y[:, :].to(device=dev, dtype=torch.float32).contiguous()),
