@@ -26,6 +26,8 @@
 // Inputs may be fp32 or bf16; math is bf16 MFMA with fp32 accumulation.
 // Shapes: K <= 16*KT, N <= 16*NT with KT*NT <= 32 (weights <= 64 VGPRs); larger
 // layers (e.g. MNIST 784 x 128) stay on hipBLASLt where it is efficient.
+#include <cstdlib>
+
 #include "sml_common.h"
 #include "sml_ops.h"
 
@@ -395,9 +397,57 @@ int slab_sum_scratch(int G, int S) {
 
 // sum G slabs of S floats (S % 4 == 0) into out[S]; intermediate levels go to
 // consecutive regions of scratch (slab_sum_scratch(G, S) floats)
+// One-pass variant for up to a few thousand slabs: 256 threads = 16 column quads x 16 slab
+// groups; group j sums slabs j, j + 16, ... with four independent accumulators, the 16 groups
+// combine in LDS in fixed order (deterministic).  ONE launch instead of two or three levels:
+// each level of the multi-pass reduction cost ~5 us of launch and ramp at the LSTM's slab
+// counts (3 x 2 levels per seq-50 training step, profiles/r04).
+template <bool MAP>
+__global__ __launch_bounds__(256) void slab_sum1_kernel(const float* __restrict__ in, int G, int S,
+                                                        float* __restrict__ out, const int* __restrict__ map) {
+  __shared__ f32x4 red[16][16];
+  const int qi = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int quad = blockIdx.x * 16 + qi;
+  f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  if (quad * 4 < S) {
+    int g = grp, k = 0;
+    for (; g + 48 < G; g += 64, k = 0) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += *reinterpret_cast<const f32x4*>(in + (int64_t)(g + 16 * u) * S + quad * 4);
+    }
+    for (; g < G; g += 16, k = (k + 1) & 3) acc[k] += *reinterpret_cast<const f32x4*>(in + (int64_t)g * S + quad * 4);
+  }
+  red[grp][qi] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (grp == 0 && quad * 4 < S) {
+    f32x4 t = red[0][qi];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) t += red[j][qi];
+    if constexpr (MAP) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = map[quad * 4 + j];
+        if (d >= 0) out[d] = t[j];
+      }
+    } else {
+      *reinterpret_cast<f32x4*>(out + quad * 4) = t;
+    }
+  }
+}
+
 hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, float* out, hipStream_t stream,
                            const int* map) {
   if (S % 4 != 0 || G < 1) return hipErrorInvalidValue;
+  static const bool one_pass = [] {   // SML_SLAB_1P=0: the multi-level reduction (A/B)
+    const char* e = std::getenv("SML_SLAB_1P");
+    return !(e && e[0] == '0');
+  }();
+  if (one_pass && G <= 4096) {
+    const dim3 grid((S / 4 + 15) / 16);
+    if (map) hipLaunchKernelGGL(slab_sum1_kernel<true>, grid, dim3(256), 0, stream, partials, G, S, out, map);
+    else hipLaunchKernelGGL(slab_sum1_kernel<false>, grid, dim3(256), 0, stream, partials, G, S, out, nullptr);
+    return hipGetLastError();
+  }
   const float* src = partials;
   float* buf = scratch;
   int g = G;
