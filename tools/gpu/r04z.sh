@@ -3,7 +3,7 @@
 # and a kernel trace of the headline step
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r04z2
+O=gpurun_out/r04z3
 mkdir -p $O
 step() {
   local name=$1 t=$2; shift 2
@@ -19,7 +19,7 @@ grep -E "passed|failed" $O/tests_gpu.out | tail -1
 step bench 400 python bench.py
 python - <<'PY'
 import json
-d = json.load(open("gpurun_out/r04z2/bench.out"))
+d = json.load(open("gpurun_out/r04z3/bench.out"))
 keys = ["value", "ms_per_step", "vs_baseline", "keras_batch32", "fit_batch100_rows_per_s", "stream_e2e_rows_per_s",
         "stream_large_batch_rows_per_s", "lstm_seq50_windows_per_s", "lstm_ref_us_per_step", "p50_infer_us",
         "kafka_e2e_p50_us", "lstm_kafka_e2e_p50_us", "lstm_infer_p50_us", "mqtt_connections", "mqtt_dropped",
