@@ -45,7 +45,28 @@ def _serving_cpus(k: int):
     return None
 
 
-def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=False, make_scorer=None):
+def _l3_cpus(k: int, slot: int = 0):
+    """``k`` CPUs of this process's affinity set that share one L3 (one core complex), one per
+    physical core (None: topology unknown or no L3 domain with ``k`` allowed cores).  ``slot``
+    (a rank) picks among the qualifying domains round-robin, so replicas do not share one.  A loopback hop between core complexes costs microseconds: the append -> result
+    path's spinning threads (scoring loop, producer, broker connection threads) go here."""
+    allowed = sorted(os.sched_getaffinity(0))
+    groups = {}
+    for c in allowed:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") as f:
+                l3 = f.read().strip()
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                core = f.read().strip()
+        except OSError:
+            return None
+        g = groups.setdefault(l3, {})
+        g.setdefault(core, c)           # first allowed CPU of each physical core
+    ok = sorted((sorted(g.values()) for g in groups.values() if len(g) >= k), key=lambda c: c[0])
+    return ok[slot % len(ok)][:k] if ok else None
+
+
+def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=None, make_scorer=None):
     """Kafka append -> result append latency through the real serving path: a paced C++
     producer appends Confluent-Avro car events (one produce request each, keyed by car) to
     an in-process broker at ``qps``; the ``serve --low-latency`` loop (long-poll fetch, C++
@@ -55,9 +76,12 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=
     event's result record minus that of the event itself -- Kafka-append -> result
     visible to consumers.  Also reported: producer-send -> result-produce-ack (both client
     legs included).  ``spin_us``: the low-latency socket policy (broker connection threads,
-    long polls and the loop's client busy-poll this long before blocking).  ``pin``: the
-    scoring loop and the producer run on two CPUs of their own (distinct physical cores); off
-    by default -- on the MI355X boxes it changed nothing measurable (profiles/r03).
+    long polls and the loop's client busy-poll this long before blocking).  ``pin``: ``"l3"``
+    (the default where the topology is readable; ``SML_E2E_PIN=0`` turns it off) puts the
+    scoring loop, the producer and the broker's connection threads on distinct cores of ONE
+    L3 domain -- unpinned, each loopback hop took ~2.3 or ~4.7 us depending on where the
+    scheduler placed the threads (profiles/r04); ``"cores"`` pins only the loop and the
+    producer (distinct physical cores, any L3); ``False`` leaves placement to the scheduler.
     ``make_scorer``: the resident scorer to serve with (default the autoencoder's
     ``ScoringServer``; e.g. an ``LSTMScoringServer``, whose car keys the loop maps to device
     slots in C++)."""
@@ -79,6 +103,13 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=
     b.create_topic("model-predictions", 1)
     b.record_append_times(True)
     b.set_spin_us(spin_us)
+    if pin is None:
+        pin = "l3" if os.environ.get("SML_E2E_PIN", "1") != "0" else False
+    cpus = None
+    if pin == "l3":
+        cpus = _l3_cpus(5, rank)
+        if cpus:
+            b.set_thread_cpus(cpus[2:])   # before any client connects
     buf, offs = encode_chunk(AvroCodec("cardata-v1"), np.ascontiguousarray(ev[:n], np.float32),
                              np.zeros(n, np.uint8))
     keys = [f"car{i % 1000}" for i in range(n)]
@@ -86,7 +117,8 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=
     with (make_scorer() if make_scorer is not None else ScoringServer(m, threshold=threshold, slots=4096)) as srv:
         loop = LowLatencyScorer(f"fake://{name}", "SENSOR_DATA_S_AVRO", "model-predictions", [0], srv, starts=[0],
                                 max_wait_ms=100, record_latency=True, spin_us=spin_us)
-        cpus = _serving_cpus(2) if pin else None
+        if pin and pin != "l3":
+            cpus = _serving_cpus(2)
 
         def serve():
             if cpus:
@@ -123,7 +155,7 @@ def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=
             "max_us": float(d.max()), "events": int(len(d)), "offered_qps": qps, "spin_us": spin_us,
             "latency": "broker append time of the event -> broker append time of its result record",
             "send_to_ack_p50_us": float(np.percentile(d_ack, 50)), "send_to_ack_p99_us": float(np.percentile(d_ack, 99)),
-            "legs_p50_us": legs, "pinned_cpus": cpus,
+            "legs_p50_us": legs, "pinned_cpus": cpus, "pin": pin if cpus else False,
             "results": int(b.end_offset("model-predictions", 0)),
             "batches": st.get("batches"), "events_per_batch": ev_n / max(st.get("batches", 1), 1),
             "per_event_us": {k[:-2]: st[k] / ev_n * 1e6 for k in ("decode_s", "score_s", "format_s",

@@ -753,6 +753,8 @@ PYBIND11_MODULE(_io, m) {
              return out;
            })
       .def("set_faults", &kafka::Broker::set_faults, py::arg("fail_every") = 0, py::arg("delay_ms") = 0)
+      .def("set_thread_cpus", &kafka::Broker::set_thread_cpus, py::arg("cpus"),
+           "CPUs for connection threads accepted from now on (empty: unpinned)")
       .def("set_spin_us", &kafka::Broker::set_spin_us, py::arg("us"),
            "low-latency mode: connection threads and empty long polls busy-wait this long first")
       .def("record_append_times", &kafka::Broker::record_append_times, py::arg("on") = true)

@@ -1,6 +1,9 @@
 // Kafka wire protocol client + in-process broker (see kafka.h).
 #include "kafka.h"
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/in.h>
@@ -992,7 +995,19 @@ void Broker::accept_loop() {
     std::lock_guard<std::mutex> g(mu_);
     client_fds_.push_back(fd);
     workers_.emplace_back([this, fd] { serve(fd); });
+    if (!thread_cpus_.empty()) {
+      cpu_set_t set;
+      CPU_ZERO(&set);
+      for (int c : thread_cpus_)
+        if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
+      pthread_setaffinity_np(workers_.back().native_handle(), sizeof(set), &set);   // best effort
+    }
   }
+}
+
+void Broker::set_thread_cpus(const std::vector<int>& cpus) {
+  std::lock_guard<std::mutex> g(mu_);
+  thread_cpus_ = cpus;
 }
 
 void Broker::create_topic(const std::string& name, int partitions) {

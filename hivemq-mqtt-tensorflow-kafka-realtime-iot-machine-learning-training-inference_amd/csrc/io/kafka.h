@@ -197,6 +197,10 @@ class Broker {
   // Low-latency mode: each connection thread busy-polls its socket, and an empty long-poll
   // fetch watches the append counter, for `us` microseconds before blocking (0 = off).
   void set_spin_us(int us) { spin_us_ = us; }
+  // CPUs for the connection threads accepted from now on (empty: unpinned).  The latency
+  // bench keeps every spinning thread of the append -> result path on one L3 domain: a hop
+  // between core complexes costs microseconds on the loopback path.
+  void set_thread_cpus(const std::vector<int>& cpus);
   // Record the steady-clock time (ns, the process's std::chrono::steady_clock) at which
   // every record is appended from now on -- Kafka's LogAppendTime, for latency accounting.
   void record_append_times(bool on);
@@ -234,6 +238,7 @@ class Broker {
   };
   FetchReply handle_fetch(const uint8_t* body, size_t n);
   BrokerConfig cfg_;
+  std::vector<int> thread_cpus_;   // guarded by mu_
   int listen_fd_ = -1;
   int port_ = 0;
   std::atomic<bool> running_{false};

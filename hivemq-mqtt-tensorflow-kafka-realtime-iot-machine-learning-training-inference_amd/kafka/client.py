@@ -73,6 +73,10 @@ class FakeBroker:
     def set_faults(self, fail_every: int = 0, delay_ms: int = 0) -> None:
         self._b.set_faults(fail_every, delay_ms)
 
+    def set_thread_cpus(self, cpus) -> None:
+        """Pin the connection threads accepted from now on to ``cpus`` (empty: unpinned)."""
+        self._b.set_thread_cpus([int(c) for c in cpus])
+
     def set_spin_us(self, us: int) -> None:
         """Low-latency mode: connection threads and empty long polls busy-wait ``us`` first."""
         self._b.set_spin_us(int(us))

@@ -2,6 +2,7 @@
 (csrc/io/format.cpp), on CPU: the GPU scorer is replaced by _io.EchoScorer (score =
 mean(x^2), recon = x / 2) through the same SmlScorerApi table."""
 import json
+import os
 import threading
 
 import numpy as np
@@ -131,6 +132,8 @@ def test_spin_mode_and_broker_append_times():
     b.create_topic("R", 1)
     b.record_append_times(True)
     b.set_spin_us(100)
+    pin = min(os.sched_getaffinity(0))
+    b.set_thread_cpus([pin])   # connection threads start on this CPU only
     echo = load_io().EchoScorer(18, 5.0)
     loop = LowLatencyScorer("fake://spin-unit", "S", "R", [0], echo, starts=[0], max_wait_ms=50,
                             record_latency=True, spin_us=100)
@@ -140,6 +143,17 @@ def test_spin_mode_and_broker_append_times():
     paced_produce("fake://spin-unit", "S", 0, bytes(buf), offs, qps=20000, spin_us=100)
     th.join(60)
     b.set_spin_us(0)
+    if len(os.sched_getaffinity(0)) > 1:
+        c = KafkaClient("fake://spin-unit")   # a live connection: its broker thread is pinned
+        assert c.latest("R", 0) == n
+        masks = []
+        for t in os.listdir("/proc/self/task"):
+            try:
+                masks.append(os.sched_getaffinity(int(t)))
+            except OSError:   # the thread ended
+                pass
+        assert {pin} in masks, masks
+        del c
     assert out["events"] == n and b.end_offset("R", 0) == n
     t_in = b.append_times("S", 0, 0, n)
     t_res = b.append_times("R", 0, 0, n)
@@ -248,3 +262,27 @@ def test_keyed_scorer_maps_record_keys_to_stable_slots():
                              max_wait_ms=5)
     with pytest.raises(Exception, match="key slots"):
         loop2.run(idle_timeout_s=0.2)
+
+
+def test_l3_cpus_picks_distinct_cores_of_one_l3():
+    """bench_infer._l3_cpus: the e2e bench's placement for its spinning threads."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "bench_infer_l3", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench", "bench_infer.py"))
+    bi = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bi)
+    allowed = os.sched_getaffinity(0)
+    assert bi._l3_cpus(len(allowed) + 1) is None
+    c = bi._l3_cpus(1)
+    if c is None:   # no cache topology in sysfs
+        return
+    assert len(c) == 1 and c[0] in allowed
+    path = f"/sys/devices/system/cpu/cpu{c[0]}/cache/index3/shared_cpu_list"
+    for k in (2, 3):
+        cs = bi._l3_cpus(k)
+        if cs is None:
+            continue
+        assert len(set(cs)) == k and set(cs) <= allowed
+        l3 = {open(f"/sys/devices/system/cpu/cpu{x}/cache/index3/shared_cpu_list").read() for x in cs}
+        cores = {open(f"/sys/devices/system/cpu/cpu{x}/topology/thread_siblings_list").read() for x in cs}
+        assert len(l3) == 1 and len(cores) == k and os.path.exists(path)

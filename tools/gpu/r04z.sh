@@ -3,7 +3,7 @@
 # and a kernel trace of the headline step
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r04z3
+O=${O:-gpurun_out/r04z4}
 mkdir -p $O
 step() {
   local name=$1 t=$2; shift 2
@@ -17,9 +17,9 @@ cat $O/smoke.out
 step tests_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider
 grep -E "passed|failed" $O/tests_gpu.out | tail -1
 step bench 400 python bench.py
-python - <<'PY'
-import json
-d = json.load(open("gpurun_out/r04z3/bench.out"))
+O=$O python - <<'PY'
+import json, os
+d = json.load(open(os.environ["O"] + "/bench.out"))
 keys = ["value", "ms_per_step", "vs_baseline", "keras_batch32", "fit_batch100_rows_per_s", "stream_e2e_rows_per_s",
         "stream_large_batch_rows_per_s", "lstm_seq50_windows_per_s", "lstm_ref_us_per_step", "p50_infer_us",
         "kafka_e2e_p50_us", "lstm_kafka_e2e_p50_us", "lstm_infer_p50_us", "mqtt_connections", "mqtt_dropped",
@@ -33,9 +33,4 @@ echo "== trace rc=$?"
 cd "$GRAFT_REPO_ROOT"
 step head_probe 120 python tools/lstm_probe/head_probe.py
 cat $O/head_probe.out
-for k in 1 2; do
-  step lstm_def_$k 200 python bench/bench_lstm.py --steps 20 --warmup 3
-  step lstm_mix_$k 200 env SML_LSTM_BIASCOL=m python bench/bench_lstm.py --steps 20 --warmup 3
-done
-for f in $O/lstm_*_[12].out; do echo "$f $(python -c "import json,sys; d=json.load(open('$f')); print(round(d['value']/1e6,2), round(d['ms_per_step'],3))")"; done
 echo ALLDONE
