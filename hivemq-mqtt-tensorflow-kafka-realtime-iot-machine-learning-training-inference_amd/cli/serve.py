@@ -78,6 +78,9 @@ def _flags(p) -> None:
     p.add_argument("--max-wait-ms", type=int, default=100, help="long-poll bound of the low-latency loop")
     p.add_argument("--spin-us", type=int, default=0,
                    help="low-latency loop: busy-poll each broker response this long before blocking")
+    p.add_argument("--cpus", default=None,
+                   help="--low-latency: CPUs for the loop thread, e.g. '4' or '4-7,12' (one L3 domain near "
+                        "the GPU; a loopback hop across core complexes costs microseconds, profiles/r04 §7)")
     p.add_argument("--model", choices=["autoencoder", "lstm"], default="autoencoder",
                    help="lstm: per-car forecaster (look_back events per car on the device, each event "
                         "scored against the car's previous forecast; lstm_serve.hip)")
@@ -85,6 +88,23 @@ def _flags(p) -> None:
     p.add_argument("--source-format", choices=["avro", "json"], default="avro",
                    help="--low-latency: json follows the MQTT bridge's JSON events (sensor-data, KSQL "
                         "SENSOR_DATA_S) directly instead of the Avro stream")
+
+
+def parse_cpus(spec: str) -> set:
+    """'4', '4-7,12' -> {4, 5, 6, 7, 12} (taskset's list syntax)."""
+    out = set()
+    for part in spec.split(","):
+        part = part.strip()
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        lo_i, hi_i = int(lo), int(hi) if hi else int(lo)
+        if lo_i < 0 or hi_i < lo_i:
+            raise ValueError(f"bad CPU range {part!r}")
+        out.update(range(lo_i, hi_i + 1))
+    if not out:
+        raise ValueError(f"no CPUs in {spec!r}")
+    return out
 
 
 def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary) -> int:
@@ -109,7 +129,13 @@ def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary) -> 
                                 starts=starts, result_partitions=[p % result_parts for p in mine],
                                 emit_recon=ns.emit == "both", config=cfg, max_batch=min(ns.max_batch, 4096),
                                 max_wait_ms=ns.max_wait_ms, spin_us=ns.spin_us, source_format=ns.source_format)
-        st = loop.run(max_events=ns.max_events, idle_timeout_s=ns.idle_timeout)
+        mask = os.sched_getaffinity(0)
+        if ns.cpus:
+            os.sched_setaffinity(0, parse_cpus(ns.cpus))   # this (the loop's) thread
+        try:
+            st = loop.run(max_events=ns.max_events, idle_timeout_s=ns.idle_timeout)
+        finally:
+            os.sched_setaffinity(0, mask)
     ENGINE.infer_rows.inc(st["events"], model=model.name)
     ENGINE.anomaly_events.inc(st["anomalies"], model=model.name)
     if ns.model == "lstm":

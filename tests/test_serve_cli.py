@@ -34,6 +34,14 @@ def _read_topic(servers, topic, parts):
     return out
 
 
+def test_parse_cpus_taskset_syntax():
+    assert serve_cli.parse_cpus("4") == {4}
+    assert serve_cli.parse_cpus("4-7, 12") == {4, 5, 6, 7, 12}
+    for bad in ("", "7-4", "-1"):
+        with pytest.raises(ValueError):
+            serve_cli.parse_cpus(bad)
+
+
 def test_serve_replicas_score_every_event_once(tmp_path, capsys):
     from streamml.data.stream import kafka
     from streamml.models.autoencoder import Autoencoder, load_model
@@ -105,8 +113,12 @@ def test_serve_low_latency_cli(tmp_path, capsys, cuda_device):
               "--device", str(cuda_device), "--synthetic-partitions", str(parts), "--idle-timeout", "0.3",
               "--low-latency", "--max-wait-ms", "20", "--replicas", "2"]
     summaries = []
+    import os
+    mask = os.sched_getaffinity(0)
     for r in (0, 1):
-        assert cli_main(common + ["--replica-index", str(r)]) == 0
+        pin = ["--cpus", str(min(mask))] if r == 0 else []   # the loop thread on one CPU, restored after
+        assert cli_main(common + ["--replica-index", str(r)] + pin) == 0
+        assert os.sched_getaffinity(0) == mask
         summaries.append(json.loads(capsys.readouterr().out.strip().splitlines()[-1]))
     assert all(s_["low_latency"] for s_ in summaries)
     assert summaries[0]["events"] + summaries[1]["events"] == n
