@@ -256,6 +256,34 @@ __device__ __forceinline__ f32x4 layer16(const float* frag, const float* bias, i
   return acc;
 }
 
+// Sum over the 4 lanes of a row (l, l^16, l^32, l^48) with the gfx950 row swaps:
+// permlane16_swap of two copies leaves {rows 0,0,2,2} in one result and {rows 1,1,3,3} in the
+// other, permlane32_swap the same across halves; every lane ends with the same bits.
+__device__ __forceinline__ float rowsum4(float v) {
+  const unsigned u = __float_as_uint(v);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  const float s = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+  const unsigned w = __float_as_uint(s);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+}
+
+// Layer 4's padded tail on the VALU (inputs <= 18: the car-sensor schema).  With NO = KSX - 4
+// <= 2 real features past 16, 14 of the 16 outputs of layer 4's second tile are padding, and so
+// are three quarters of the backward's K-steps 4 .. 3 + NO.  Outputs 16 + o are a 4-term dot per
+// lane over its h3 features (W4[4g + i][16 + o]: one 16-byte read from the backward fragment
+// image), then the row's 4 lanes summed; the inputs x[16 + o] are summed over the row's lanes at
+// the top of the step (off the chain), so every lane computes the same dz and the backward's two
+// K-steps become 8 fmas.  6 of the 36 fp32 MFMAs per row tile go.  Same-box A/B (r04o2/o3,
+// profiles/r04 SUMMARY §6): batch 32 (pipelined build) +2 %, batch 100 +0.7 %; doing the same for
+// layer 1's inputs 16 + o (2 more MFMAs) measured slower at batch 100 and was dropped.
+// SML_MB_TAILV=0 compiles the MFMA forms back in.
+#ifndef SML_MB_TAILV
+#define SML_MB_TAILV 1
+#endif
+template <int KSX>
+constexpr bool tail_valu() { return SML_MB_TAILV && KSX > 4 && KSX <= 6; }
+
 // Categorical accuracy of row r: argmax of y and x, ties -> lowest feature (1 or 0).  The
 // row's 20 first (logical) features come in as five 16-byte reads per array; logical block
 // jl sits at physical block jl ^ (swz(r) / 4) of its 16-column half.
@@ -451,6 +479,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       for (int s = 0; s < 8; ++s) xv[s] = 0.f;
 #pragma unroll
       for (int s = 0; s < KSX; ++s) xv[s] = (row_ok && fok[s]) ? fmaf(xr[s], sc[s], sh[s]) : 0.f;
+      float xh[2];   // TV: inputs 16 + o of this lane's row (lane group 0's xv[4 + o]) in all 4 lanes
+#pragma unroll
+      for (int o = 0; o < 2; ++o) xh[o] = (tail_valu<KSX>() && 4 + o < KSX) ? rowsum4(xv[4 + o]) : 0.f;
       if (step + 1 < a.nsteps) {   // next step's rows: in flight across phase B
         int more = 1;
         if (stream) {   // the next batch must have landed in the ring (or the stream ends here)
@@ -485,9 +516,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
       for (int i = 0; i < 4; ++i) h3[i] = fm(4 * g + i < n3, act_fwd(a3, z3[i]));
       // L4 (two output tiles), MSE, dz4 = act4'(y) * 2 (y - x) / D   (1/B applied in Adam)
-      f32x4 y[2], dz4[2];
+      constexpr bool TV = tail_valu<KSX>();
+      f32x4 y[2], dz4[2], w4h[2];
 #pragma unroll
-      for (int t4 = 0; t4 < 2; ++t4) {
+      for (int t4 = 0; t4 < (TV ? 1 : 2); ++t4) {
         f32x4 acc = ld4(S.w + BB4 + 16 * t4 + 4 * g);
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc = mfma4(S.w[F4 + (4 * t4 + s) * 64 + lane], h3[s], acc);
@@ -501,11 +533,36 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           dz4[t4][i] = act_grad(a4, yy, two_over_d * e);
         }
       }
+      float dzh[2];   // TV: dz of outputs 16 + o, the same in all 4 lanes of a row
+      if constexpr (TV) {   // outputs 16 .. 15 + NO: lane group 0 holds them, as the MFMA tile did
+        y[1] = dz4[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int o = 0; o < KSX - 4; ++o) {
+          w4h[o] = ld4(S.w + G4 + (4 + o) * 64 + 4 * g);
+          float p = h3[0] * w4h[o][0];
+#pragma unroll
+          for (int i = 1; i < 4; ++i) p = fmaf(h3[i], w4h[o][i], p);
+          const float yy = fm(16 + o < D, act_fwd(a4, S.w[BB4 + 16 + o] + rowsum4(p)));
+          const float e = row_ok ? yy - xh[o] : 0.f;
+          dzh[o] = act_grad(a4, yy, two_over_d * e);
+          const bool g0 = g == 0;
+          const float em = g0 ? e : 0.f;
+          sq = fmaf(em, em, sq);
+          y[1][o] = g0 ? yy : 0.f;
+          dz4[1][o] = g0 ? dzh[o] : 0.f;
+        }
+      }
       // backward: dz3 = act3'(h3) * (W4 dz4^T), dz2 = act2'(h2) * (W3 dz3^T),
       //           dz1 = act1'(h1) * (W2 dz2^T + l1 sign(h1))   (Keras L1 activity regulariser)
       f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < KSX; ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
+      for (int s = 0; s < (TV ? 4 : KSX); ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
+      if constexpr (TV) {
+#pragma unroll
+        for (int o = 0; o < KSX - 4; ++o)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc3[i] = fmaf(w4h[o][i], dzh[o], acc3[i]);
+      }
       f32x4 dz3, dz2, dz1;
 #pragma unroll
       for (int i = 0; i < 4; ++i) dz3[i] = fm(4 * g + i < n3, act_grad(a3, h3[i], acc3[i]));
@@ -897,6 +954,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
       for (int s = 0; s < 8; ++s) xv[s] = 0.f;
 #pragma unroll
       for (int s = 0; s < KSX; ++s) xv[s] = (row_ok && fok[s]) ? fmaf(xr[s], sc[s], sh[s]) : 0.f;
+      float xh[2];
+#pragma unroll
+      for (int o = 0; o < 2; ++o) xh[o] = (tail_valu<KSX>() && 4 + o < KSX) ? rowsum4(xv[4 + o]) : 0.f;
       if (step + 1 < nsteps) {   // next step's rows: in flight across this step
         int more = 1;
         if (stream) {
@@ -930,9 +990,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
       const f32x4 z3 = layer16(S.w + F3, S.w + BB3, lane, g, h2);
 #pragma unroll
       for (int i = 0; i < 4; ++i) h3[i] = act_fwd(a3, z3[i]);
-      f32x4 y[2], dz4[2];
+      constexpr bool TV = tail_valu<KSX>();   // as ae_minibatch_kernel (bit-identical results)
+      f32x4 y[2], dz4[2], w4h[2];
 #pragma unroll
-      for (int t4 = 0; t4 < 2; ++t4) {
+      for (int t4 = 0; t4 < (TV ? 1 : 2); ++t4) {
         f32x4 acc = ld4(S.w + BB4 + 16 * t4 + 4 * g);
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc = mfma4(S.w[F4 + (4 * t4 + s) * 64 + lane], h3[s], acc);
@@ -944,6 +1005,25 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
           sq = fmaf(e, e, sq);
           y[t4][i] = yy;
           dz4[t4][i] = act_grad(a4, yy, two_over_d * e);
+        }
+      }
+      float dzh[2];
+      if constexpr (TV) {
+        y[1] = dz4[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int o = 0; o < KSX - 4; ++o) {
+          w4h[o] = ld4(S.w + G4 + (4 + o) * 64 + 4 * g);
+          float p = h3[0] * w4h[o][0];
+#pragma unroll
+          for (int i = 1; i < 4; ++i) p = fmaf(h3[i], w4h[o][i], p);
+          const float yy = act_fwd(a4, S.w[BB4 + 16 + o] + rowsum4(p));
+          const float e = row_ok ? yy - xh[o] : 0.f;
+          dzh[o] = act_grad(a4, yy, two_over_d * e);
+          const bool g0 = g == 0;
+          const float em = g0 ? e : 0.f;
+          sq = fmaf(em, em, sq);
+          y[1][o] = g0 ? yy : 0.f;
+          dz4[1][o] = g0 ? dzh[o] : 0.f;
         }
       }
       const int r = row_l;
@@ -959,7 +1039,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
       }
       f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < KSX; ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
+      for (int s = 0; s < (TV ? 4 : KSX); ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
+      if constexpr (TV) {
+#pragma unroll
+        for (int o = 0; o < KSX - 4; ++o)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc3[i] = fmaf(w4h[o][i], dzh[o], acc3[i]);
+      }
       f32x4 dz3, dz2, dz1;
 #pragma unroll
       for (int i = 0; i < 4; ++i) dz3[i] = act_grad(a3, h3[i], acc3[i]);
