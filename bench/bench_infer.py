@@ -46,24 +46,9 @@ def _serving_cpus(k: int):
 
 
 def _l3_cpus(k: int, slot: int = 0):
-    """``k`` CPUs of this process's affinity set that share one L3 (one core complex), one per
-    physical core (None: topology unknown or no L3 domain with ``k`` allowed cores).  ``slot``
-    (a rank) picks among the qualifying domains round-robin, so replicas do not share one.  A loopback hop between core complexes costs microseconds: the append -> result
-    path's spinning threads (scoring loop, producer, broker connection threads) go here."""
-    allowed = sorted(os.sched_getaffinity(0))
-    groups = {}
-    for c in allowed:
-        try:
-            with open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") as f:
-                l3 = f.read().strip()
-            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
-                core = f.read().strip()
-        except OSError:
-            return None
-        g = groups.setdefault(l3, {})
-        g.setdefault(core, c)           # first allowed CPU of each physical core
-    ok = sorted((sorted(g.values()) for g in groups.values() if len(g) >= k), key=lambda c: c[0])
-    return ok[slot % len(ok)][:k] if ok else None
+    """streamml.utils.affinity.l3_cpus: ``k`` distinct cores of one L3 domain (None: unknown)."""
+    from streamml.utils.affinity import l3_cpus
+    return l3_cpus(k, slot)
 
 
 def kafka_e2e(m, ev, qps, threshold, events, rank=0, warm=100, spin_us=200, pin=None, make_scorer=None):

@@ -36,6 +36,7 @@ from typing import List, Sequence, Tuple
 import numpy as np
 
 from ..ops._ext import load_io
+from ..utils.affinity import parse_cpus, resolve_cpus  # noqa: F401  (serve.parse_cpus)
 from . import common
 
 USAGE = ("python -m streamml.cli serve <servers> <topic> <result_topic> <model-file> "
@@ -79,8 +80,9 @@ def _flags(p) -> None:
     p.add_argument("--spin-us", type=int, default=0,
                    help="low-latency loop: busy-poll each broker response this long before blocking")
     p.add_argument("--cpus", default=None,
-                   help="--low-latency: CPUs for the loop thread, e.g. '4' or '4-7,12' (one L3 domain near "
-                        "the GPU; a loopback hop across core complexes costs microseconds, profiles/r04 §7)")
+                   help="--low-latency: CPUs for the loop thread, e.g. '4' or '4-7,12', or 'auto' (one core of "
+                        "an L3 domain, a different one per replica); a loopback hop across core "
+                        "complexes costs microseconds (profiles/r04 SUMMARY §7)")
     p.add_argument("--model", choices=["autoencoder", "lstm"], default="autoencoder",
                    help="lstm: per-car forecaster (look_back events per car on the device, each event "
                         "scored against the car's previous forecast; lstm_serve.hip)")
@@ -90,24 +92,7 @@ def _flags(p) -> None:
                         "SENSOR_DATA_S) directly instead of the Avro stream")
 
 
-def parse_cpus(spec: str) -> set:
-    """'4', '4-7,12' -> {4, 5, 6, 7, 12} (taskset's list syntax)."""
-    out = set()
-    for part in spec.split(","):
-        part = part.strip()
-        if not part:
-            continue
-        lo, _, hi = part.partition("-")
-        lo_i, hi_i = int(lo), int(hi) if hi else int(lo)
-        if lo_i < 0 or hi_i < lo_i:
-            raise ValueError(f"bad CPU range {part!r}")
-        out.update(range(lo_i, hi_i + 1))
-    if not out:
-        raise ValueError(f"no CPUs in {spec!r}")
-    return out
-
-
-def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary) -> int:
+def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary, rank: int = 0) -> int:
     """One C++ loop per replica over the resident scorer: the autoencoder's, or -- ``--model
     lstm`` -- the per-car forecaster, whose car key -> device slot map lives in the loop
     (cardata-v2.py:220-273 streams one LSTM prediction per event)."""
@@ -130,8 +115,9 @@ def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary) -> 
                                 emit_recon=ns.emit == "both", config=cfg, max_batch=min(ns.max_batch, 4096),
                                 max_wait_ms=ns.max_wait_ms, spin_us=ns.spin_us, source_format=ns.source_format)
         mask = os.sched_getaffinity(0)
-        if ns.cpus:
-            os.sched_setaffinity(0, parse_cpus(ns.cpus))   # this (the loop's) thread
+        cpus = resolve_cpus(ns.cpus, slot=rank)
+        if cpus:
+            os.sched_setaffinity(0, cpus)   # this (the loop's) thread
         try:
             st = loop.run(max_events=ns.max_events, idle_timeout_s=ns.idle_timeout)
         finally:
@@ -201,7 +187,7 @@ def main(argv: Sequence[str]) -> int:
     if ns.source_format == "json" and not ns.low_latency:
         raise SystemExit("--source-format json needs --low-latency (the C++ loop decodes the JSON events)")
     if ns.low_latency:
-        return _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary)
+        return _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary, rank)
     forecaster, key_ids = None, {}
     if ns.model == "lstm":
         if model.device.type != "cuda":

@@ -1,0 +1,61 @@
+"""CPU placement for the latency-critical host threads (the ``serve --low-latency`` loop, a
+paced producer, the in-process broker's connection threads).
+
+A loopback TCP hop between two threads costs ~2.3 us when both run in one core complex (one
+L3) and ~4.7 us across complexes; unpinned, the scheduler picks either, run to run
+(profiles/r04/SUMMARY.md §7).  ``l3_cpus`` returns distinct physical cores of one L3 domain
+from this process's affinity set; ``parse_cpus`` reads taskset's list syntax.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Set
+
+
+def parse_cpus(spec: str) -> Set[int]:
+    """'4', '4-7,12' -> {4, 5, 6, 7, 12} (taskset's list syntax)."""
+    out: Set[int] = set()
+    for part in spec.split(","):
+        part = part.strip()
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        lo_i, hi_i = int(lo), int(hi) if hi else int(lo)
+        if lo_i < 0 or hi_i < lo_i:
+            raise ValueError(f"bad CPU range {part!r}")
+        out.update(range(lo_i, hi_i + 1))
+    if not out:
+        raise ValueError(f"no CPUs in {spec!r}")
+    return out
+
+
+def _read(path: str) -> str:
+    with open(path) as f:
+        return f.read().strip()
+
+
+def l3_cpus(k: int, slot: int = 0) -> Optional[List[int]]:
+    """``k`` CPUs of this process's affinity set sharing one L3, one per physical core (None:
+    cache topology not readable, or no L3 domain with ``k`` allowed cores).  ``slot`` (e.g. a
+    replica's rank) picks among the qualifying domains round-robin, so replicas do not share one."""
+    groups = {}
+    for c in sorted(os.sched_getaffinity(0)):
+        try:
+            l3 = _read(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list")
+            core = _read(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list")
+        except OSError:
+            return None
+        groups.setdefault(l3, {}).setdefault(core, c)   # first allowed CPU of each core
+    ok = sorted((sorted(g.values()) for g in groups.values() if len(g) >= k), key=lambda cs: cs[0])
+    return ok[slot % len(ok)][:k] if ok else None
+
+
+def resolve_cpus(spec: Optional[str], slot: int = 0) -> Optional[Set[int]]:
+    """``--cpus`` value -> CPU set: None / '' = leave placement alone, 'auto' = one core of an L3
+    domain chosen by ``slot`` (None when the topology is unknown), else taskset syntax."""
+    if not spec:
+        return None
+    if spec == "auto":
+        cs = l3_cpus(1, slot)
+        return set(cs) if cs else None
+    return parse_cpus(spec)

@@ -265,24 +265,22 @@ def test_keyed_scorer_maps_record_keys_to_stable_slots():
 
 
 def test_l3_cpus_picks_distinct_cores_of_one_l3():
-    """bench_infer._l3_cpus: the e2e bench's placement for its spinning threads."""
-    import importlib.util
-    spec = importlib.util.spec_from_file_location(
-        "bench_infer_l3", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench", "bench_infer.py"))
-    bi = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(bi)
+    """utils.affinity: the placement of the e2e bench's spinning threads and ``serve --cpus auto``."""
+    from streamml.utils.affinity import l3_cpus, parse_cpus, resolve_cpus
     allowed = os.sched_getaffinity(0)
-    assert bi._l3_cpus(len(allowed) + 1) is None
-    c = bi._l3_cpus(1)
+    assert l3_cpus(len(allowed) + 1) is None
+    assert resolve_cpus(None) is None and resolve_cpus("") is None
+    assert resolve_cpus("0-2,5") == parse_cpus("0-2,5") == {0, 1, 2, 5}
+    c = l3_cpus(1)
     if c is None:   # no cache topology in sysfs
+        assert resolve_cpus("auto") is None
         return
-    assert len(c) == 1 and c[0] in allowed
-    path = f"/sys/devices/system/cpu/cpu{c[0]}/cache/index3/shared_cpu_list"
+    assert len(c) == 1 and c[0] in allowed and resolve_cpus("auto") == set(c)
     for k in (2, 3):
-        cs = bi._l3_cpus(k)
+        cs = l3_cpus(k)
         if cs is None:
             continue
         assert len(set(cs)) == k and set(cs) <= allowed
         l3 = {open(f"/sys/devices/system/cpu/cpu{x}/cache/index3/shared_cpu_list").read() for x in cs}
         cores = {open(f"/sys/devices/system/cpu/cpu{x}/topology/thread_siblings_list").read() for x in cs}
-        assert len(l3) == 1 and len(cores) == k and os.path.exists(path)
+        assert len(l3) == 1 and len(cores) == k

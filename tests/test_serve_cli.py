@@ -116,7 +116,8 @@ def test_serve_low_latency_cli(tmp_path, capsys, cuda_device):
     import os
     mask = os.sched_getaffinity(0)
     for r in (0, 1):
-        pin = ["--cpus", str(min(mask))] if r == 0 else []   # the loop thread on one CPU, restored after
+        # the loop thread on one CPU (explicit, or one core of an L3 domain), restored after
+        pin = ["--cpus", str(min(mask)) if r == 0 else "auto"]
         assert cli_main(common + ["--replica-index", str(r)] + pin) == 0
         assert os.sched_getaffinity(0) == mask
         summaries.append(json.loads(capsys.readouterr().out.strip().splitlines()[-1]))
