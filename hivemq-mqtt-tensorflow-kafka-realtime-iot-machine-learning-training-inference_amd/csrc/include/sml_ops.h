@@ -187,10 +187,13 @@ hipError_t lstm_serve_launch(const LstmServeArgs& args, hipStream_t stream);
 // ---- fused MSE + categorical accuracy (loss.hip) ----
 bool mse_acc_supported(int F);
 // acc != null needs part: 2 * mse_acc_blocks(rows, F) floats of scratch (the block partials,
-// folded into acc by a one-block kernel: acc = partials (reset) or acc += partials)
+// folded into acc by a one-block kernel: acc = partials (reset) or acc += partials); out
+// (optional, needs acc): out[k] = acc[k] / div_k after the fold; counter (optional, needs acc):
+// an int64 step count advanced by one in the same launch
 int mse_acc_blocks(int64_t rows, int F);
 hipError_t mse_acc_launch(const float* yp, const float* y, int64_t rows, int F, int bcast, float gscale, float* grad,
-                          float* acc, float* part, int reset, hipStream_t stream);
+                          float* acc, float* part, int reset, hipStream_t stream, float* out = nullptr,
+                          float div0 = 1.f, float div1 = 1.f, int64_t* counter = nullptr);
 
 // ---- utilities (util.hip) ----
 hipError_t lane_xor_probe_launch(float* out, hipStream_t stream);

@@ -109,9 +109,12 @@ __global__ __launch_bounds__(rows_per_block<F>()) void mse_acc_kernel(const floa
   }
 }
 
-// acc[k] (+)= sum over the n block partials part[2 i + k], in a fixed order
+// acc[k] (+)= sum over the n block partials part[2 i + k], in a fixed order; out (optional):
+// out[k] = acc[k] / div[k] -- a train step's loss and accuracy, normalised in this launch
+// instead of two torch ops (a division and a copy) on the stream after it
 __global__ __launch_bounds__(256) void acc_fold_kernel(const float* __restrict__ part, int n, float* __restrict__ acc,
-                                                       int reset) {
+                                                       int reset, float* __restrict__ out, float div0, float div1,
+                                                       int64_t* __restrict__ counter) {
   __shared__ float red[2][4];
   float a = 0.f, b = 0.f;
   for (int i = threadIdx.x; i < n; i += 256) {
@@ -129,8 +132,14 @@ __global__ __launch_bounds__(256) void acc_fold_kernel(const float* __restrict__
   if (threadIdx.x == 0) {
     const float sa = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
     const float sb = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-    acc[0] = reset ? sa : acc[0] + sa;
-    acc[1] = reset ? sb : acc[1] + sb;
+    const float a0 = reset ? sa : acc[0] + sa, a1 = reset ? sb : acc[1] + sb;
+    acc[0] = a0;
+    acc[1] = a1;
+    if (out) {
+      out[0] = a0 / div0;
+      out[1] = a1 / div1;
+    }
+    if (counter) counter[0] += 1;   // the optimizer's step count (read by the Adam launch after this)
   }
 }
 
@@ -142,7 +151,8 @@ int mse_acc_blocks(int64_t rows, int F) {
 }
 
 hipError_t mse_acc_launch(const float* yp, const float* y, int64_t rows, int F, int bcast, float gscale, float* grad,
-                          float* acc, float* part, int reset, hipStream_t stream) {
+                          float* acc, float* part, int reset, hipStream_t stream, float* out, float div0,
+                          float div1, int64_t* counter) {
   if (rows <= 0) return hipSuccess;
   if (bcast < 1 || (acc && !part)) return hipErrorInvalidValue;
   float* pp = acc ? part : nullptr;
@@ -158,7 +168,8 @@ hipError_t mse_acc_launch(const float* yp, const float* y, int64_t rows, int F, 
     default: return hipErrorInvalidValue;
   }
 #undef SML_F
-  if (acc) hipLaunchKernelGGL(acc_fold_kernel, dim3(1), dim3(256), 0, stream, part, mse_acc_blocks(rows, F), acc, reset);
+  if (acc) hipLaunchKernelGGL(acc_fold_kernel, dim3(1), dim3(256), 0, stream, part, mse_acc_blocks(rows, F), acc, reset,
+                               out, div0, div1, counter);
   return hipGetLastError();
 }
 

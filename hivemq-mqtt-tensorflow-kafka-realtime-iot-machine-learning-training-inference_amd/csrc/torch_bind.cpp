@@ -846,7 +846,9 @@ at::Tensor lstm_ref_train(const at::Tensor& flat, const at::Tensor& m, const at:
 
 // K3 + K6: (y_pred - y) * gscale -> grad, [sum sq err, #correct rows] += into acc.
 void mse_acc(const at::Tensor& yp, const at::Tensor& y, int64_t bcast, double gscale,
-             const c10::optional<at::Tensor>& grad, const c10::optional<at::Tensor>& acc, bool reset) {
+             const c10::optional<at::Tensor>& grad, const c10::optional<at::Tensor>& acc, bool reset,
+             const c10::optional<at::Tensor>& out, double div0, double div1,
+             const c10::optional<at::Tensor>& counter) {
   check_dev(yp, "y_pred", at::kFloat);
   check_dev(y, "y", at::kFloat);
   TORCH_CHECK(yp.is_contiguous() && y.is_contiguous(), "inputs must be contiguous");
@@ -862,12 +864,23 @@ void mse_acc(const at::Tensor& yp, const at::Tensor& y, int64_t bcast, double gs
     check_dev(*acc, "acc", at::kFloat);
     TORCH_CHECK(acc->numel() >= 2, "acc needs 2 floats");
   }
+  if (out.has_value()) {
+    TORCH_CHECK(acc.has_value(), "out needs acc");
+    check_dev(*out, "out", at::kFloat);
+    TORCH_CHECK(out->numel() >= 2 && out->is_contiguous(), "out needs 2 contiguous floats");
+  }
+  if (counter.has_value()) {
+    TORCH_CHECK(acc.has_value(), "counter needs acc");
+    check_dev(*counter, "counter", at::kLong);
+  }
   c10::hip::HIPGuard guard(yp.device().index());
   at::Tensor part;
   if (acc.has_value()) part = at::empty({2 * (int64_t)sml::mse_acc_blocks(rows, (int)F)}, yp.options());
   SML_CHECK_HIP(sml::mse_acc_launch(yp.data_ptr<float>(), y.data_ptr<float>(), rows, (int)F, (int)bcast,
                                     (float)gscale, opt_mut(grad), opt_mut(acc),
-                                    part.defined() ? part.data_ptr<float>() : nullptr, reset ? 1 : 0, cur_stream(yp)));
+                                    part.defined() ? part.data_ptr<float>() : nullptr, reset ? 1 : 0, cur_stream(yp),
+                                    opt_mut(out), (float)div0, (float)div1,
+                                    counter.has_value() ? counter->data_ptr<int64_t>() : nullptr));
 }
 
 at::Tensor lane_xor_probe(const at::Tensor& like) {
@@ -1276,7 +1289,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("nkeys", [](LSTMServePy& p) { return p.nk; });
   m.def("mse_acc", &mse_acc, "fused MSE fwd/bwd + categorical accuracy (K3 + K6)", py::arg("y_pred"), py::arg("y"),
         py::arg("bcast") = 1, py::arg("gscale") = 1.0, py::arg("grad") = py::none(), py::arg("acc") = py::none(),
-        py::arg("reset") = false);
+        py::arg("reset") = false, py::arg("out") = py::none(), py::arg("div0") = 1.0, py::arg("div1") = 1.0,
+        py::arg("counter") = py::none());
   m.def("mse_acc_supported", &sml::mse_acc_supported, "feature counts with a fused MSE kernel", py::arg("F"));
   m.def("lane_xor_probe", &lane_xor_probe, "self-test of the permlane lane-exchange helpers", py::arg("like"));
   m.def("ae_forward", &ae_forward, "fused AE inference: reconstruction + per-row MSE score", py::arg("x"),

@@ -22,6 +22,7 @@ optimizer step is one HIP Adam launch and DP is one RCCL all-reduce.
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -53,6 +54,8 @@ def _glorot(fi: int, fo: int, rng) -> np.ndarray:
     lim = math.sqrt(6.0 / (fi + fo))
     return rng.uniform(-lim, lim, size=(fi, fo)).astype(np.float32)
 
+
+_FOLD = os.environ.get("SML_LSTM_FOLD", "1") != "0"
 
 class LSTMPredictor:
     def __init__(self, look_back: int = 1, features: int = 18, stack=None, device="auto", seed: int = 0,
@@ -263,7 +266,12 @@ class LSTMPredictor:
         acc = plan["acc"]
         dy = torch.empty_like(y_pred)
         scale = n / float(global_batch or n)           # mean over the global batch under DP
-        C.mse_acc(y_pred, yt, R or 1, 2.0 / y_pred.numel() * scale, dy, acc, reset=True)   # acc = this step's sums
+        # this step's (loss, accuracy) and the Adam step count come out of the loss kernel's fold
+        # launch (SML_LSTM_FOLD=0: a division, a copy and a counter add on the stream instead)
+        fold = _FOLD
+        metrics = torch.empty(2, device=self.device) if fold else None
+        C.mse_acc(y_pred, yt, R or 1, 2.0 / y_pred.numel() * scale, dy, acc, reset=True,   # acc = this step's sums
+                  out=metrics, div0=float(y_pred.numel()), div1=float(R or 1), counter=self.fp.iter if fold else None)
         C.dense_wgrad(hin, dy, 0, True, 1024, grad, plan["head_map"])
         dh = C.dense_fwd(dy, K, None, 0, True, 1024, True)   # dh = dy . K^T, bf16
         layers = pre + post
@@ -279,9 +287,11 @@ class LSTMPredictor:
             dh = out[0]
             if R and i == len(pre):   # RepeatVector backward: the repeated steps' gradients summed
                 dh = (dh.view(n, -1) if R == 1 else dh.sum(1)).to(torch.bfloat16)
-        self.opt.step(allreduce=allreduce)
+        self.opt.step(allreduce=allreduce, counted=fold)
+        if fold:
+            return metrics[0], metrics[1]   # acc is overwritten by the next step, metrics is this step's own
         correct = acc[1] / float(R) if R else acc[1].clone()
-        return acc[0] / y_pred.numel(), correct   # acc is overwritten by the next step
+        return acc[0] / y_pred.numel(), correct
 
     # ------------------------------------------------------------------ training
     def fit(self, x, y=None, epochs: int = 1, batch_size: int = 1, verbose: int = 1, take: Optional[int] = None,

@@ -75,11 +75,14 @@ class FlatAdam:
         if self.on_gpu:
             self.C = load_c()
 
-    def step(self, grad_scale: float = 1.0, allreduce=None) -> None:
+    def step(self, grad_scale: float = 1.0, allreduce=None, counted: bool = False) -> None:
+        """``counted``: the step count was already advanced on the device this step (a fused
+        train step folds the increment into its loss kernel: one launch fewer)."""
         fp = self.fp
         if allreduce is not None:
             allreduce(fp.grad)
-        fp.iter.add_(1)
+        if not counted:
+            fp.iter.add_(1)
         if self.on_gpu:
             self.C.reduce_adam(fp.grad, 1, fp.n_pad, fp.n_pad, None, fp.flat, fp.m, fp.v, fp.iter, self.lr, self.b1,
                                self.b2, self.eps, float(grad_scale), None, RA_ADAM)

@@ -243,3 +243,25 @@ def test_fit_accepts_device_window_views(cuda_device):
     hb = b.fit(X.cpu().numpy(), Y.cpu().numpy(), epochs=2, batch_size=50, verbose=0)
     assert ha.history["loss"] == hb.history["loss"]
     torch.testing.assert_close(a.fp.flat, b.fp.flat, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ctor", ["two_layer", "reference"])
+def test_fused_step_folded_metrics_match_torch_ops(cuda_device, monkeypatch, ctor):
+    """The fused train step takes its (loss, accuracy) and the Adam step count from the loss
+    kernel's fold launch; the SML_LSTM_FOLD=0 path does the same with torch ops.  Both give
+    the same bits, the same parameters and a step count equal to the steps taken."""
+    import streamml.models.lstm as L
+    T = 10 if ctor == "two_layer" else 1
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(96, T, 18, generator=g).to(cuda_device)
+    y = torch.rand(96, 18, generator=g).to(cuda_device)
+    runs = []
+    for fold in (True, False):
+        monkeypatch.setattr(L, "_FOLD", fold)
+        m = getattr(LSTMPredictor, ctor)(look_back=T, device=cuda_device, seed=5)
+        vals = [tuple(float(v) for v in m.train_step(x, y)) for _ in range(3)]
+        runs.append((vals, m.fp.flat.detach().cpu().clone(), int(m.fp.iter.item())))
+    (v1, p1, it1), (v0, p0, it0) = runs
+    assert v1 == v0 and it1 == it0 == 3
+    assert torch.equal(p1, p0)
