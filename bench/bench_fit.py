@@ -231,6 +231,81 @@ def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, bat
     return out
 
 
+def stream_dp(device, rank: int, world: int, rows_per_rank: int = 4_000_000, partitions: int = 10,
+              batch: int = 1 << 20, workers: int = 4) -> dict:
+    """Data-parallel training from ONE partitioned topic (BASELINE config 4 with the reference's
+    ingestion path; SURVEY.md 2.4 stream / partition parallelism).  Collective: every rank calls it.
+
+    Rank 0 hosts the in-process Kafka broker (127.0.0.1, reached by every rank over TCP like a
+    broker of the cluster) and fills ``partitions`` partitions (the reference's sensor-data has
+    10, 01_installConfluentPlatform.sh:180) with ``rows_per_rank x world`` Confluent-Avro car
+    events.  Every rank streams its own share -- equal contiguous offset ranges of all
+    partitions (kafka/assign.py "split") -- through its native feed (``workers`` threads) into
+    ``fit(batch_size=batch, engine="throughput")``: one fused step + one flat RCCL all-reduce
+    per batch, every filtered row of every share trained exactly once.  Whole-job trained
+    rows/s over the slowest rank's epoch."""
+    import torch
+    import torch.distributed as dist
+
+    from streamml.data import stream as S
+    from streamml.models.autoencoder import Autoencoder
+    from streamml.parallel import dp as dpm
+
+    topic = "SENSOR_DATA_S_AVRO"
+    broker, info = None, [None]
+    if rank == 0:
+        try:   # a failure here reaches every rank through the broadcast (no rank left waiting)
+            from streamml.kafka import FakeBroker
+            broker = FakeBroker()
+            t0 = time.perf_counter()
+            nbytes = _fill_topic(broker, topic, rows_per_rank * world, partitions)
+            info = [{"addr": broker.address, "log_bytes": nbytes, "produce_s": time.perf_counter() - t0}]
+        except Exception as e:  # noqa: BLE001
+            info = [{"error": repr(e)[:300]}]
+    dist.broadcast_object_list(info, src=0)
+    info = info[0]
+    if "error" in info:
+        if broker is not None:
+            broker.stop()
+        raise RuntimeError(f"stream_dp setup on rank 0: {info['error']}")
+    try:
+        src = S.kafka(info["addr"], [f"{topic}:*:0"], shard="auto", assign="split", native=True,
+                      workers=workers, max_bytes=8 << 20)
+        training = src.filter_normal(device=True)
+        m = Autoencoder(device=device, input_normalizer="cardata")
+        m.compile()
+        dpm.sync_model_from_rank0(m)
+        m.fit(training, epochs=1, batch_size=batch, verbose=0, steps_per_epoch=2, engine="throughput", dp="rccl")
+        torch.cuda.synchronize()
+        dpm.barrier(device)
+        t1 = time.perf_counter()
+        h = m.fit(training, epochs=1, batch_size=batch, verbose=0, engine="throughput", dp="rccl")
+        torch.cuda.synchronize()
+        dpm.barrier(device)
+        dt = dpm.allreduce_max(time.perf_counter() - t1, device)
+        shares = [[s.partition, s.start, s.end] for s in src.plan.last]
+        st = dict(src.native_feed.last_stats)
+        chk = float(m.backend.params.double().sum())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"shares": shares, "rows_read": st.get("records"), "kept": st.get("rows"),
+                                          "iterations": m.iterations, "param_checksum": chk,
+                                          "fetch_s": st.get("fetch_s"), "decode_s": st.get("decode_s")})
+    finally:
+        dpm.barrier(device)
+        if broker is not None:
+            broker.stop()
+    trained = int(h.history["_rows"][-1])
+    return {"trained_rows_per_s": trained / dt, "rows_per_s": rows_per_rank * world / dt, "seconds": dt,
+            "rows": rows_per_rank * world, "trained_rows": trained, "partitions": partitions, "batch": batch,
+            "global_batch": batch * world, "world": world, "feed_workers_per_rank": workers,
+            "engine": m.last_fit_engine, "loss": h.history["loss"][-1], "assign": "split",
+            "partition_lists": [sorted({s[0] for s in r["shares"]}) for r in per_rank], "per_rank": per_rank,
+            "replicas_identical": len({r["param_checksum"] for r in per_rank}) == 1,
+            "steps_equal": len({r["iterations"] for r in per_rank}) == 1, "broker": info,
+            "path": "rank 0's in-process broker over TCP -> per-rank native feed (own offset ranges) -> "
+                    "fit(throughput) + RCCL all-reduce per step"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=2_000_000)

@@ -39,26 +39,51 @@ def _flags(p):
     p.add_argument("--schema", default="cardata-v1")
     p.add_argument("--with-score", action="store_true", help="also emit the per-event anomaly score")
     p.add_argument("--group", default="cardata-autoencoder")
+    p.add_argument("--partitions", default=None,
+                   help="partitions to read: '0' (the reference, cardata-v3.py:46), 'all', or a comma list; "
+                        "default 0, or all under torchrun (WORLD_SIZE > 1)")
+    p.add_argument("--assign", default="auto", choices=["auto", "split", "partitions"],
+                   help="under torchrun: each rank's share of the partitions (streamml.kafka.assign)")
+    p.add_argument("--native-feed", action="store_true", help="ROCm: the C++ partition-parallel feed")
+    p.add_argument("--feed-workers", type=int, default=4)
 
 
-def _stream(ns, servers, cfg):
+def _world() -> int:
+    import os
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def _stream(ns, servers, cfg, shard=None):
     from ..data import stream as st
-    return st.kafka(servers, [f"{ns.topic}:0:{int(ns.offset)}"], schema=ns.schema, group=ns.group, eof=True,
-                    config=cfg)
+    parts = ns.partitions or ("all" if _world() > 1 else "0")
+    specs = ([f"{ns.topic}:*:{int(ns.offset)}"] if parts == "all" else
+             [f"{ns.topic}:{int(p)}:{int(ns.offset)}" for p in parts.split(",") if p != ""])
+    native = bool(ns.native_feed) and shard is not None
+    return st.kafka(servers, specs, schema=ns.schema, group=ns.group, eof=True, config=cfg, shard=shard,
+                    assign=ns.assign, native=native, workers=ns.feed_workers)
 
 
 def _train(ns, servers, cfg, epochs, batch_size, out_path):
+    """Under torchrun every rank trains on its own share of the partitions (one process per
+    GPU, gradients all-reduced per step); rank 0 writes the model."""
     from ..models.autoencoder import Autoencoder
-    ae = Autoencoder(input_dim=18, encoding_dim=14, hidden_dim=7, input_normalizer="cardata", device=ns.device,
+    from ..parallel.dp import init_from_env, sync_model_from_rank0
+    env = init_from_env(None if ns.device == "auto" else ("cuda" if ns.device.startswith("cuda") else "cpu"))
+    device = ns.device if env.world_size == 1 else env.device
+    ae = Autoencoder(input_dim=18, encoding_dim=14, hidden_dim=7, input_normalizer="cardata", device=device,
                      seed=ns.seed)
     ae.compile(metrics=["accuracy"], loss="mean_squared_error", optimizer="adam")
-    ae.summary()
+    sync_model_from_rank0(ae)
+    if env.rank == 0:
+        ae.summary()
     # filter(y == "false") (cardata-v3.py:212): on a GPU the K8 kernel compacts on the device
-    training = _stream(ns, servers, cfg).filter_normal(device=True)
+    training = _stream(ns, servers, cfg, shard="auto" if env.world_size > 1 else None).filter_normal(device=True)
     t0 = time.perf_counter()
-    ae.fit(training, epochs=epochs, batch_size=batch_size, steps_per_epoch=ns.take, verbose=2)
-    print(f"Training complete ({time.perf_counter() - t0:.2f}s)", flush=True)
-    ae.save(out_path)
+    ae.fit(training, epochs=epochs, batch_size=batch_size, steps_per_epoch=ns.take, verbose=2 if env.rank == 0 else 0)
+    if env.rank == 0:
+        print(f"Training complete ({time.perf_counter() - t0:.2f}s)", flush=True)
+        ae.save(out_path)
+    ae.dist_rank = env.rank
     return ae
 
 
@@ -92,9 +117,12 @@ def main_v3(argv: Sequence[str]) -> int:
     path = common.model_path(ns.workdir, ns.model_file)
     batch_size = ns.batch_size or 100
     if mode == "train":
-        _train(ns, servers, cfg, ns.epochs or 20, batch_size, path)
-        url = store.upload(path, "/" + ns.model_file)
-        print("Model stored successfully", ns.model_file, url, flush=True)
+        ae = _train(ns, servers, cfg, ns.epochs or 20, batch_size, path)
+        if ae.dist_rank == 0:
+            url = store.upload(path, "/" + ns.model_file)
+            print("Model stored successfully", ns.model_file, url, flush=True)
+        from ..parallel.dp import shutdown
+        shutdown()
     else:
         print("Downloading model", ns.model_file, flush=True)
         store.download("/" + ns.model_file, path)
@@ -114,9 +142,12 @@ def main_v1(argv: Sequence[str]) -> int:
     cfg = common.kafka_config(ns.servers, ns.kafka_config)
     path = common.model_path(ns.workdir, "path_to_my_model.h5")
     batch_size = ns.batch_size or 32
-    _train(ns, servers, cfg, ns.epochs or 5, batch_size, path)
-    model = load_model(path, device=ns.device, input_normalizer="cardata")   # "recreate purely from the file"
-    _predict(ns, servers, cfg, model, batch_size, ns.result_topic)
+    ae = _train(ns, servers, cfg, ns.epochs or 5, batch_size, path)
+    from ..parallel.dp import shutdown
+    shutdown()
+    if ae.dist_rank == 0:   # predict runs once, on rank 0
+        model = load_model(path, device=ns.device, input_normalizer="cardata")   # "recreate purely from the file"
+        _predict(ns, servers, cfg, model, batch_size, ns.result_topic)
     return 0
 
 

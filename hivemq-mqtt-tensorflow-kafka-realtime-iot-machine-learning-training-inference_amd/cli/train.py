@@ -14,7 +14,9 @@ costs at most one epoch of work (see :mod:`streamml.parallel.fault`).
 
 Data: ``servers=synthetic://N`` (default) trains on N synthetic car events
 (deterministic, rank-sharded inside ``fit``); a Kafka bootstrap / ``fake://``
-source streams the topic.  Prints one JSON summary line on rank 0.
+source streams the topic (``partition=-1``: every partition), each rank its own share
+(``assign``: split | partitions, :mod:`streamml.kafka.assign`) through the native feed,
+with no collect.  Prints one JSON summary line on rank 0.
 """
 from __future__ import annotations
 
@@ -117,11 +119,16 @@ def main(argv: Sequence[str]) -> int:
         else:
             data = (x[chunk.label == 0],)
     else:
+        # every rank streams its own share of the topic's partitions (kafka/assign.py: equal
+        # contiguous offset ranges, resolved on one log snapshot per epoch) straight into fit --
+        # no rank reads another's records and nothing is collected first
         from ..data import stream as st
-        s = st.kafka(servers, [f"{cfg.topic}:{cfg.partition}:{cfg.offset}"], schema=cfg.schema, group=cfg.group,
-                     eof=True, config=cfg.kafka_config if not servers.startswith("fake://") else None)
-        c = s.collect()
-        data = (c.x[c.label == 0],)
+        part = "*" if cfg.partition < 0 else str(cfg.partition)
+        s = st.kafka(servers, [f"{cfg.topic}:{part}:{cfg.offset}"], schema=cfg.schema, group=cfg.group,
+                     eof=True, config=cfg.kafka_config if not servers.startswith("fake://") else None,
+                     shard="auto", assign=cfg.assign, native=cfg.native_feed and dev.type == "cuda",
+                     workers=cfg.feed_workers)
+        data = (s.filter_normal(device=True),) if cfg.model == "autoencoder" else (s, None)
 
     # ---------------------------------------------------------------- train
     from ..nn.callbacks import Callback

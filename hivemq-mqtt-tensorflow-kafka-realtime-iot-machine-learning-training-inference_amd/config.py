@@ -32,8 +32,11 @@ class Config:
     # --- source / sink -------------------------------------------------------
     servers: str = "synthetic://"          # kafka host:port list | fake:// | synthetic:// | csv:<path>
     topic: str = "SENSOR_DATA_S_AVRO"
-    partition: int = 0                      # reference hard-codes partition 0 (cardata-v3.py:46)
+    partition: int = 0                      # reference hard-codes partition 0 (cardata-v3.py:46); -1 = all
     offset: int = 0
+    assign: str = "auto"                    # DP share of the partitions: split | partitions | keys (kafka/assign.py)
+    native_feed: bool = True                # ROCm: the C++ partition-parallel feed (kafka/feed.py)
+    feed_workers: int = 4                   # its fetch + decode threads per rank
     result_topic: str = "model-predictions"
     group: str = "cardata-autoencoder"
     kafka_config: List[str] = field(default_factory=lambda: list(REFERENCE_KAFKA_CONFIG))

@@ -80,15 +80,23 @@ class Chunk:
 class Stream:
     """A lazy, re-iterable chain of chunk transforms (each ``iter`` restarts the source)."""
 
-    def __init__(self, factory: Callable[[], Iterator[Chunk]]):
+    # (rank, world) when this stream yields only one data-parallel rank's share of its
+    # source (``kafka(shard=...)``); transforms keep it, ``fit`` trains on it unsharded
+    shard = None
+
+    def __init__(self, factory: Callable[[], Iterator[Chunk]], shard=None):
         self._factory = factory
+        self.shard = shard
 
     def __iter__(self) -> Iterator[Chunk]:
         return self._factory()
 
+    def _derive(self, factory: Callable[[], Iterator[Chunk]]) -> "Stream":
+        return Stream(factory, self.shard)
+
     # --- transforms ---------------------------------------------------------
     def map(self, fn: Callable[[Chunk], Chunk]) -> "Stream":
-        return Stream(lambda: (fn(c) for c in self))
+        return self._derive(lambda: (fn(c) for c in self))
 
     def filter_label(self, keep: int = LABEL_FALSE, device: bool = False) -> "Stream":
         """``filter(lambda x, y: y == "false")`` (cardata-v3.py:212).
@@ -101,7 +109,7 @@ class Stream:
                 m = c.label == keep
                 if m.any():
                     yield c.select(m)
-        out = Stream(gen)
+        out = self._derive(gen)
         if device:
             out.device_filter = (self, int(keep))
         return out
@@ -130,7 +138,7 @@ class Stream:
                     buf, have = ([rest] if len(rest) else []), len(rest)
             if have and not drop_remainder:
                 yield Chunk.concat(buf)
-        return Stream(gen)
+        return self._derive(gen)
 
     def take(self, n: int) -> "Stream":
         def gen():
@@ -138,14 +146,14 @@ class Stream:
                 if i >= n:
                     return
                 yield c
-        return Stream(gen)
+        return self._derive(gen)
 
     def skip(self, n: int) -> "Stream":
         def gen():
             for i, c in enumerate(self):
                 if i >= n:
                     yield c
-        return Stream(gen)
+        return self._derive(gen)
 
     def windows(self, look_back: int, horizon: int = 1) -> "WindowStream":
         """Sliding windows for next-event prediction (LSTM-.../cardata-v2.py:199-206).
@@ -261,16 +269,45 @@ def json_lines(path: str, chunk: int = 65536) -> Stream:
 def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optional[str] = None,
           eof: bool = True, config: Optional[Sequence[str]] = None, max_bytes: int = 4 << 20,
           framing: bool = True, commit: bool = False, resume: bool = False,
-          idle_timeout_s: Optional[float] = None, workers: int = 1, native: bool = False) -> Stream:
+          idle_timeout_s: Optional[float] = None, workers: int = 1, native: bool = False,
+          shard=None, assign: str = "auto") -> Stream:
     """Kafka topic(s) of (Confluent-framed) Avro car records -> raw feature chunks.
+
+    ``topics``: ``"topic:partition:offset"`` specs; ``"topic:*:offset"`` is every partition.
 
     ``native=True``: the partition-parallel C++ feed (:mod:`streamml.kafka.feed`) decodes
     records straight into page-locked slabs; the Stream still iterates host chunks, and a
     GPU ``fit`` picks up ``stream.native_feed`` to stream slabs to the device with no
-    Python-side row handling (``filter_normal(device=True)`` becomes a decode-time filter)."""
+    Python-side row handling (``filter_normal(device=True)`` becomes a decode-time filter).
+
+    ``shard``: read only this rank's share of the listed partitions (:mod:`streamml.kafka.assign`)
+    -- ``"auto"`` (the ``torch.distributed`` rank / world, a no-op without a process group) or
+    ``(rank, world)``.  ``assign``: ``"split"`` (equal contiguous offset ranges; bounded reads),
+    ``"partitions"`` (whole partitions, ``p % world``), ``"keys"`` (key-hash shares, per-key
+    order; Python reader only), ``"auto"``: split when ``eof`` else partitions.  Under a process
+    group every rank resolves the same log snapshot (an all-reduce of the offsets), so starting
+    an iteration of a sharded stream is collective -- as every ``fit`` epoch is.  The stream
+    carries ``stream.shard = (rank, world)``; ``fit`` then trains each rank on its own rows."""
     from ..kafka import KafkaDataset
+    from ..kafka.client import parse_topic_spec
     from .avro import AvroCodec
 
+    plan = None
+    if shard is not None:
+        from ..kafka.assign import ShardPlan, torch_sync
+        if shard == "auto":
+            import torch.distributed as dist
+            pg = dist.is_available() and dist.is_initialized()
+            rank, world = (dist.get_rank(), dist.get_world_size()) if pg else (0, 1)
+            sync = torch_sync if pg else None
+        else:
+            rank, world = (int(v) for v in shard)
+            sync = None
+        mode = ("split" if eof else "partitions") if assign == "auto" else assign
+        if mode == "split" and (commit or resume):
+            raise ValueError("assign='split' cuts partitions between ranks: per-partition offset commits do not "
+                             "apply (checkpoint the position instead, or use assign='partitions')")
+        plan = ShardPlan([parse_topic_spec(t) for t in topics], rank, world, mode, sync)
     codec = AvroCodec(schema)
     cols = []
     for name in FEATURES:
@@ -287,21 +324,25 @@ def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optio
         label_idx = names.index(label_field) if label_field is not None else -1
         spec = NativeFeed(servers, topics, codec, feature_idx, label_idx, config=config, workers=workers,
                           max_bytes=max_bytes, eof=eof, framing=framing, group=group, resume=resume,
-                          commit=commit, idle_timeout_s=idle_timeout_s)
+                          commit=commit, idle_timeout_s=idle_timeout_s, plan=plan)
 
         def native_gen():
             for rows, labs in spec.host_chunks():
                 yield Chunk(rows, labs)
         out = Stream(native_gen)
         out.native_feed = spec
+        out.shard = None if plan is None else (plan.rank, plan.world)
+        out.plan = plan
         return out
 
     def gen():
         # label codes and str keys come straight from C++ (no per-record Python objects
         # for the text column, no second pass over the keys)
+        from ..kafka.assign import key_mask
         ds = KafkaDataset(topics, servers=servers, group=group, eof=eof, config_global=config, codec=codec,
                           max_bytes=max_bytes, framing=framing, commit=commit, resume=resume,
-                          idle_timeout_s=idle_timeout_s, with_text=False, str_keys=True, workers=workers)
+                          idle_timeout_s=idle_timeout_s, with_text=False, str_keys=True, workers=workers,
+                          plan=plan)
         for b in ds:
             ok = b["ok"].astype(bool)
             x = b["numeric"][:, cols]
@@ -311,7 +352,19 @@ def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optio
                 lab = np.zeros(len(x), np.uint8)
             lab[~ok] = LABEL_MISSING
             keys = b["keys"]
-            yield Chunk(np.ascontiguousarray(x), lab, keys, b["offsets"],
-                        meta={"topic": b["topic"], "partition": b["partition"], "errors": int(b["n_errors"]),
-                              "ok": ok})
-    return Stream(gen)
+            c = Chunk(np.ascontiguousarray(x), lab, keys, b["offsets"],
+                      meta={"topic": b["topic"], "partition": b["partition"], "errors": int(b["n_errors"]),
+                            "ok": ok})
+            hr = b.get("hash_range")
+            if hr is not None:   # keys share: the cars of this partition another replica owns are skipped
+                m = key_mask(keys, hr[0], hr[1])
+                if not m.all():
+                    c = c.select(m)
+                    c.meta["ok"] = ok[m]
+                if len(c) == 0:
+                    continue
+            yield c
+    out = Stream(gen)
+    out.shard = None if plan is None else (plan.rank, plan.world)
+    out.plan = plan
+    return out

@@ -27,10 +27,15 @@ def parse_config(config: Optional[Sequence[str]]) -> Dict[str, str]:
 
 
 def parse_topic_spec(spec: str) -> Tuple[str, int, int]:
-    """``"topic:partition:offset"`` (tfio convention) -> (topic, partition, offset)."""
+    """``"topic:partition:offset"`` (tfio convention) -> (topic, partition, offset).
+    ``"topic:*:offset"`` names every partition of the topic (partition -1, expanded from the
+    broker's metadata by :func:`streamml.kafka.assign.expand_specs`)."""
     parts = spec.split(":")
     topic = parts[0]
-    partition = int(parts[1]) if len(parts) > 1 and parts[1] != "" else 0
+    if len(parts) > 1 and parts[1] == "*":
+        partition = -1
+    else:
+        partition = int(parts[1]) if len(parts) > 1 and parts[1] != "" else 0
     offset = int(parts[2]) if len(parts) > 2 and parts[2] != "" else 0
     return topic, partition, offset
 

@@ -31,8 +31,9 @@ class KafkaDataset:
                  eof: bool = True, config_global: Optional[Sequence[str]] = None, codec=None,
                  max_bytes: int = 4 << 20, max_wait_ms: int = 100, framing: bool = True,
                  commit: bool = False, resume: bool = False, idle_timeout_s: Optional[float] = None,
-                 with_text: bool = True, str_keys: bool = False, workers: int = 1):
+                 with_text: bool = True, str_keys: bool = False, workers: int = 1, plan=None):
         self.specs = [parse_topic_spec(t) for t in topics]
+        self.plan = plan              # kafka.assign.ShardPlan: this rank's share of the partitions
         self.servers = servers
         self.group = group
         self.eof = eof
@@ -68,9 +69,9 @@ class KafkaDataset:
         return max(offset, c.earliest(topic, partition))
 
     def _step(self, c: KafkaClient, cur: List) -> Optional[dict]:
-        """One fetch(+decode) for a cursor ``[topic, partition, pos, end]``; advances it.
-        Returns the batch, ``None`` when nothing arrived, or ``False`` when the cursor is done."""
-        topic, partition, pos, end = cur
+        """One fetch(+decode) for a cursor ``[topic, partition, pos, end, hash_range]``; advances
+        it.  Returns the batch, ``None`` when nothing arrived, or ``False`` when the cursor is done."""
+        topic, partition, pos, end = cur[:4]
         if end is not None and pos >= end:
             return False
         t_fetch = time.perf_counter()
@@ -103,11 +104,18 @@ class KafkaDataset:
         ENGINE.ingest_bytes.inc(nbytes, topic=topic)
         ENGINE.decode_seconds.inc(time.perf_counter() - t_fetch, topic=topic)
         batch["topic"], batch["partition"] = topic, partition
+        batch["hash_range"] = cur[4] if len(cur) > 4 else None   # keys share: the consumer filters
         return batch
 
     def _cursors(self, c: KafkaClient) -> List[List]:
+        if self.plan is not None:   # this rank's share (kafka/assign.py), resolved per iteration
+            shares = self.plan.resolve(c, self._start_offset, self.eof)
+            return [[s.topic, s.partition, s.start, s.end if s.end >= 0 else None,
+                     None if s.whole_keys else (s.hash_lo, s.hash_hi)] for s in shares]
+        from .assign import expand_specs
+        specs = expand_specs(self.specs, c.partitions() if any(p == -1 for _, p, _ in self.specs) else {})
         cursors: List[List] = []
-        for topic, partition, offset in self.specs:
+        for topic, partition, offset in specs:
             start = self._start_offset(topic, partition, offset)
             end = c.latest(topic, partition) if self.eof else None
             cursors.append([topic, partition, start, end])

@@ -45,8 +45,9 @@ class NativeFeed:
                  label_field: int = -1, config: Optional[Sequence[str]] = None, workers: int = 1,
                  max_bytes: int = 4 << 20, max_wait_ms: int = 100, eof: bool = True, framing: bool = True,
                  group: Optional[str] = None, resume: bool = False, commit: bool = False,
-                 idle_timeout_s: Optional[float] = None):
+                 idle_timeout_s: Optional[float] = None, plan=None):
         self.servers = servers
+        self.plan = plan              # kafka.assign.ShardPlan: this rank's share, resolved per iteration
         self.specs = [parse_topic_spec(t) for t in topics]
         self.codec = codec
         self.feature_fields = [int(f) for f in feature_fields]
@@ -69,21 +70,33 @@ class NativeFeed:
     def features(self) -> int:
         return len(self.feature_fields)
 
+    def _start(self, client: KafkaClient, topic: str, partition: int, offset: int) -> int:
+        start = -1
+        if self.resume:
+            start = client.committed(self.group, topic, partition)
+        if start < 0:
+            if offset == -1:
+                start = client.latest(topic, partition)
+            elif offset == -2:
+                start = client.earliest(topic, partition)
+            else:
+                start = max(offset, client.earliest(topic, partition))
+        return int(start)
+
     def _parts(self, client: KafkaClient) -> List[Tuple[str, int, int, int]]:
+        if self.plan is not None:   # this rank's share of the partitions (kafka/assign.py)
+            shares = self.plan.resolve(client, lambda t, p, o: self._start(client, t, p, o), self.eof)
+            if any(not s.whole_keys for s in shares):
+                raise KafkaError("the native feed reads whole partitions or offset ranges; assign='keys' "
+                                 "needs the Python reader (native=False) or the serving loop")
+            return [s.as_part() for s in shares]
+        from .assign import expand_specs
+        specs = expand_specs(self.specs, client.partitions() if any(p == -1 for _, p, _ in self.specs) else {})
         parts = []
-        for topic, partition, offset in self.specs:
-            start = -1
-            if self.resume:
-                start = client.committed(self.group, topic, partition)
-            if start < 0:
-                if offset == -1:
-                    start = client.latest(topic, partition)
-                elif offset == -2:
-                    start = client.earliest(topic, partition)
-                else:
-                    start = max(offset, client.earliest(topic, partition))
+        for topic, partition, offset in specs:
+            start = self._start(client, topic, partition, offset)
             end = client.latest(topic, partition) if self.eof else -1
-            parts.append((topic, partition, int(start), int(end)))
+            parts.append((topic, partition, start, int(end)))
         return parts
 
     def _make(self, keep_label: Optional[int]):

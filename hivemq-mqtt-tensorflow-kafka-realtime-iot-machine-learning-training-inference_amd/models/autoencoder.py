@@ -33,6 +33,35 @@ from ..ops.ae import AESpec, FusedAE
 from .reference import TorchAE, init_dense_weights
 
 
+class _RowStage:
+    """Rows of a stream staged for whole batches: a preallocated [cap, D] buffer on the
+    training device (grown geometrically; no per-chunk concatenation), consumed from the
+    front."""
+
+    def __init__(self, D: int, device: torch.device, cap: int):
+        self.buf = torch.empty((int(cap), D), dtype=torch.float32, device=device)
+        self.n = 0
+
+    def push(self, x: torch.Tensor) -> None:
+        k = int(x.size(0))
+        if self.n + k > self.buf.size(0):
+            bigger = torch.empty((max(2 * self.buf.size(0), self.n + k), self.buf.size(1)), dtype=torch.float32,
+                                 device=self.buf.device)
+            bigger[:self.n].copy_(self.buf[:self.n])
+            self.buf = bigger
+        self.buf[self.n:self.n + k].copy_(x[:, :self.buf.size(1)])
+        self.n += k
+
+    def rows(self, k: int) -> torch.Tensor:
+        return self.buf[:k]
+
+    def drop(self, k: int) -> None:
+        rest = self.n - k
+        if rest > 0:
+            self.buf[:rest].copy_(self.buf[k:self.n].clone())
+        self.n = max(rest, 0)
+
+
 def _resolve_device(device) -> torch.device:
     if device in (None, "auto"):
         return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
@@ -173,8 +202,11 @@ class Autoencoder:
         ``persistent`` on a single ROCm replica when the batch fits, else ``throughput``.
 
         Under ``torch.distributed`` every rank trains on its own shard: arrays are split
-        contiguously by rank, Streams are expected to be rank-sharded already; the global
-        batch is ``batch_size * world_size``.  ``dp`` picks the gradient exchange:
+        contiguously by rank; a Stream must be rank-sharded already -- ``data.stream.kafka(...,
+        shard="auto")`` gives every rank its own offset ranges of the topic's partitions
+        (:mod:`streamml.kafka.assign`) -- and every row of every rank's share is trained exactly
+        once (:meth:`_fit_stream_dp`); the global batch is ``batch_size * world_size``.  ``dp``
+        picks the gradient exchange:
 
         * ``"p2p"`` -- inside the persistent kernel, every Keras step (xGMI push of the
           gradient tile to every peer + rank-order sum, :mod:`streamml.parallel.p2p`);
@@ -205,6 +237,10 @@ class Autoencoder:
         for cb in cbs:
             cb.on_train_begin()
         is_stream = isinstance(x, Stream)
+        if is_stream and world > 1 and x.shard is None:
+            import warnings
+            warnings.warn("fit(stream) under data parallelism with a stream that is not rank-sharded: every rank "
+                          "trains on the same records (build it with data.stream.kafka(..., shard='auto'))")
         if not is_stream:
             on_dev = isinstance(x, torch.Tensor) and x.device == self.device and self.device.type == "cuda"
             arr = x.detach() if on_dev else (x.detach().cpu().numpy() if isinstance(x, torch.Tensor)
@@ -242,11 +278,12 @@ class Autoencoder:
                 cb.on_epoch_begin(epoch)
             be.reset_metrics()
             steps = 0
-            if persistent and is_stream:
-                if world > 1:
-                    steps = self._fit_stream_dp(x, batch_size, steps_per_epoch, exch, local_k)
-                else:
-                    steps = self._fit_stream_persistent(x, batch_size, steps_per_epoch, gstep, rank)
+            if is_stream and world > 1:
+                steps = self._fit_stream_dp(x, batch_size, steps_per_epoch, exch, local_k, persistent=persistent,
+                                            world=world, allreduce=allreduce, gstep=gstep, rank=rank)
+                gstep += steps
+            elif persistent and is_stream:
+                steps = self._fit_stream_persistent(x, batch_size, steps_per_epoch, gstep, rank)
                 gstep += steps
             elif persistent:
                 n = len(xd)
@@ -440,7 +477,6 @@ class Autoencoder:
         agree, per round of ``round_batches`` staged batches, on how many to train, and the
         epoch ends for everyone when any rank's stream is exhausted.  Batches are exactly
         ``batch(B)`` over the stream; the final partial batch is Keras' short batch."""
-        from ..parallel.dp import agree
         be = self.backend
         D = self.spec.input_dim
         steps = 0
@@ -479,41 +515,9 @@ class Autoencoder:
                 be.step(carry[:have].contiguous())   # Keras' short final batch
                 steps += 1
             return steps
-
-        cap = B * max(1, int(round_batches))
-        stage = torch.empty((cap, D), dtype=torch.float32, device=self.device)
-        have = 0
-        it = iter(self._stream_device_chunks(stream))
-        pend, ppos, exhausted = None, 0, False
-        while True:
-            while have < cap:
-                if pend is None or ppos >= pend.size(0):
-                    if exhausted:
-                        break
-                    try:
-                        pend, ppos = next(it), 0
-                    except StopIteration:
-                        pend, exhausted = None, True
-                        break
-                t = min(cap - have, pend.size(0) - ppos)
-                stage[have:have + t].copy_(pend[ppos:ppos + t])
-                have += t
-                ppos += t
-            drained = exhausted and (pend is None or ppos >= pend.size(0))
-            nb, any_done = agree([have // B, int(drained)], self.device, ["min", "max"])
-            drained = bool(any_done)
-            if max_steps is not None:
-                nb = min(nb, max_steps - steps)
-            for i in range(nb):
-                be.step(stage[i * B:(i + 1) * B], global_batch=B * world, allreduce=allreduce)
-            steps += max(nb, 0)
-            rest = have - max(nb, 0) * B
-            if rest and nb > 0:
-                stage[:rest].copy_(stage[nb * B:have].clone())
-            have = rest
-            if drained or (max_steps is not None and steps >= max_steps):
-                break
-        return steps
+        # several replicas: the sharded epoch (every rank its own partitions' rows)
+        return self._fit_stream_dp(stream, B, max_steps, None, 0, persistent=False, world=world,
+                                   allreduce=allreduce, gstep=gstep, rank=rank, round_batches=round_batches)
 
     def _use_persistent(self, engine: str, batch_size: int, world: int, dp: str = "auto") -> bool:
         if engine not in ("auto", "persistent", "launch", "throughput"):
@@ -567,43 +571,97 @@ class Autoencoder:
             done += k
         return n
 
-    def _fit_stream_dp(self, stream, B: int, max_steps: Optional[int], exch, local_k: int) -> int:
-        """Streaming epoch under DP: ranks agree, per device chunk, on how many full batches
-        every rank can run (an all-reduce of two ints per chunk -- hundreds of steps);
-        rows a rank cannot use yet are kept for the next round; the epoch ends for everyone
-        when any rank's stream is exhausted (its leftover rows and the others' are dropped)."""
+    def _fit_stream_dp(self, stream, B: int, max_steps: Optional[int], exch, local_k: int, persistent: bool = True,
+                       world: int = 2, allreduce=None, gstep: int = 0, rank: int = 0,
+                       round_batches: int = 8) -> int:
+        """One streaming epoch under data parallelism, every rank on its own share of the
+        stream (``kafka(..., shard="auto")``: its own partitions' offset ranges).  Every row of
+        every share is trained exactly once and every rank runs the same number of optimizer
+        steps -- the contract a DP all-reduce needs, without dropping a rank's leftovers.
+
+        Phase 1 (lockstep): each rank stages rows from its stream; per round the ranks agree
+        (one all-reduce of two ints) on the full batches every rank can run, and run them --
+        on the persistent kernel with the in-kernel xGMI exchange (``persistent``:
+        ``_dp_train``), or one fused step + one flat all-reduce per batch (throughput /
+        launch engines, and the CPU path).  Global batch ``B x world``.
+
+        Phase 2 (tail, once any rank's stream is exhausted): the remaining rows, < B on the
+        exhausted ranks and whatever is left on the others, go in steps where each rank
+        contributes ``min(B, rows left)`` rows -- possibly none -- and the step's global batch
+        is the agreed sum, so the update is the mean over exactly the rows trained (Keras' short
+        final batch, spread over the ranks).  With ``assign="split"`` shares differ by at most a
+        record (plus the label filter), so the tail is a step or two.
+
+        ``max_steps`` (``take(n)``) caps the steps of the epoch on every rank alike."""
         from ..parallel.dp import agree
+        from ..parallel.fault import maybe_inject
+        be = self.backend
         D = self.spec.input_dim
-        stage = torch.empty((max(4 * B, 1 << 16), D), dtype=torch.float32, device=self.device)
-        have = 0   # rows staged (a preallocated buffer: no per-chunk concatenation)
-        it = iter(self._stream_device_chunks(stream))
-        steps, exhausted = 0, False
-        while True:
-            if not exhausted:
+        gb = B * world
+        cuda = self.device.type == "cuda"
+
+        def chunks():
+            if cuda:
+                yield from self._stream_device_chunks(stream)
+            else:   # CPU path: the host stream (filtered there), normalised as the CPU trainer expects
+                for c in stream:
+                    if len(c):
+                        yield self._cpu_x(c.x)
+
+        stage = _RowStage(D, self.device, max(round_batches * B, 1 << 16))
+        it = iter(chunks())
+        exhausted = False
+        steps = 0
+
+        def fill(target: int) -> None:
+            nonlocal exhausted
+            while not exhausted and stage.n < target:
                 try:
-                    xd = next(it)
-                    k = xd.size(0)
-                    if have + k > stage.size(0):   # grow geometrically; rare after the first chunks
-                        bigger = torch.empty((max(2 * stage.size(0), have + k), D), dtype=torch.float32,
-                                             device=self.device)
-                        bigger[:have].copy_(stage[:have])
-                        stage = bigger
-                    stage[have:have + k].copy_(xd)
-                    have += k
+                    stage.push(next(it))
                 except StopIteration:
                     exhausted = True
-            avail = have // B
-            if max_steps is not None:
-                avail = min(avail, max_steps - steps)
-            mn, any_done = agree([avail, int(exhausted)], self.device, ["min", "max"])
-            if mn > 0:
-                steps += self._dp_train(stage[:mn * B], B, exch, local_k)
-                rest = have - mn * B
-                if rest:
-                    stage[:rest].copy_(stage[mn * B:have].clone())
-                have = rest
-            if any_done or (max_steps is not None and steps >= max_steps):
-                return steps
+
+        def full(nb: int) -> None:   # nb full batches of B rows on every rank
+            rows = stage.rows(nb * B)
+            if persistent:
+                self._dp_train(rows, B, exch, local_k)
+                return
+            for i in range(nb):
+                maybe_inject(gstep + steps + i, rank)
+                be.step(rows[i * B:(i + 1) * B], global_batch=gb, allreduce=allreduce)
+
+        try:
+            while True:   # phase 1
+                fill(round_batches * B)
+                left = None if max_steps is None else max_steps - steps
+                # a rank whose stream has ended with < B rows staged can run no more full batches
+                nb, any_done = agree([stage.n // B, int(exhausted and stage.n < B)], self.device, ["min", "max"])
+                if left is not None:
+                    nb = min(nb, left)
+                if nb > 0:
+                    full(nb)
+                    stage.drop(nb * B)
+                    steps += nb
+                if any_done or (max_steps is not None and steps >= max_steps):
+                    break
+            while max_steps is None or steps < max_steps:   # phase 2: uneven tail
+                fill(B)
+                k = min(B, stage.n)
+                tot = agree([k], self.device, ["sum"])[0]
+                if tot == 0:
+                    break
+                maybe_inject(gstep + steps, rank)
+                if k:
+                    be.step(stage.rows(k), global_batch=tot, allreduce=allreduce)
+                    stage.drop(k)
+                else:
+                    be.step_empty(global_batch=tot, allreduce=allreduce)
+                steps += 1
+        finally:
+            close = getattr(it, "close", None)
+            if close is not None:
+                close()
+        return steps
 
     def _stream_device_chunks(self, stream, chunk_rows: int = 1 << 16):
         """Device chunks of raw rows from a Stream (no host re-batching): the pinned ring

@@ -324,7 +324,7 @@ class LSTMPredictor:
                 # (sliding_windows), read in place by the fused LSTM kernels
                 from ..data.stream import sliding_windows
                 rows = st.collect().x
-                if world > 1:   # contiguous row shard per replica (+ the look_back overlap)
+                if world > 1 and x.shard is None:   # contiguous row shard per replica (+ the look_back overlap)
                     from ..parallel.dp import shard_range
                     nw = max(len(rows) - self.look_back, 0)
                     s0, s1 = shard_range(nw, dist.get_rank(), world)
@@ -336,7 +336,7 @@ class LSTMPredictor:
                 wins = [w for w in st.windows(self.look_back)]
                 xs = np.concatenate([w[0] for w in wins]) if wins else np.zeros((0, self.look_back, self.features))
                 ys = np.concatenate([w[1] for w in wins]) if wins else np.zeros((0, self.features))
-                world_sharded = False
+                world_sharded = x.shard is not None   # kafka(shard=...): this rank's own partitions' windows
         elif isinstance(x, torch.Tensor) and x.device == self.device:
             # device tensors (e.g. data.stream.sliding_windows views) are used as they are
             xd = x if x.dtype == torch.float32 else x.float()
@@ -360,6 +360,11 @@ class LSTMPredictor:
             yd = torch.as_tensor(ys, dtype=torch.float32, device=self.device)
         n = len(xd)
         nb = math.ceil(n / batch_size)
+        if world > 1:
+            # one all-reduce per step: every rank must run the same step count (shards may
+            # differ by a few windows -- the rank with more drops its excess, as drop_last)
+            from ..parallel.dp import agree
+            nb = agree([nb])[0]
         if take is not None:
             nb = min(nb, take)
         from ..ops import lstm_persistent as lp

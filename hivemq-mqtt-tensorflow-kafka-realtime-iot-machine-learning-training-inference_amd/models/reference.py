@@ -118,6 +118,13 @@ class TorchAE:
         self._acc[2] += float(acc) * n
         self._acc[3] += n
 
+    def step_empty(self, global_batch: int, allreduce) -> None:
+        """This replica has no rows in a data-parallel step: contribute a zero gradient to the
+        all-reduce and apply the same Adam update as every other replica."""
+        flat = torch.zeros(sum(w.numel() for w in self.w), dtype=self.dtype, device=self.device)
+        allreduce(flat)
+        self.opt.apply([c.view_as(w) for c, w in zip(torch.split(flat, [w.numel() for w in self.w]), self.w)])
+
     def reset_metrics(self) -> None:
         self._acc = [0.0, 0.0, 0.0, 0.0]
 

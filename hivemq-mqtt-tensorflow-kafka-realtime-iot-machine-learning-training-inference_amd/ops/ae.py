@@ -451,6 +451,15 @@ class FusedAE:
             allreduce(self.grad)
             self.reduce(1, RA_ADAM | RA_METRICS, gscale=1.0 / gb, partials=self.grad)
 
+    def step_empty(self, global_batch: int, allreduce) -> None:
+        """This replica has no rows in a data-parallel step (the uneven tail of a sharded
+        streaming epoch): a zero gradient bucket into the all-reduce, then the same Adam
+        update (and iteration count) as every replica that had rows."""
+        self.grad.zero_()
+        self.iter.add_(1)   # what the train kernel's first workgroup does for a step with rows
+        allreduce(self.grad)
+        self.reduce(1, RA_ADAM | RA_METRICS, gscale=1.0 / int(global_batch), partials=self.grad)
+
     def gradients(self, x: torch.Tensor, global_batch: Optional[int] = None) -> Tuple[List[np.ndarray], np.ndarray]:
         """Mean-over-batch gradients (Keras weight order) + raw metric sums; no update."""
         G = self.grad_partials(x, bump_iter=False)

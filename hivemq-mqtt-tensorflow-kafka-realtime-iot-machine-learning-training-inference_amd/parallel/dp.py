@@ -155,18 +155,32 @@ def sync_model_from_rank0(model) -> None:
         be.set_optimizer_state(it2, mm, vv)
 
 
-def agree(values, device: torch.device, ops=None):
-    """Element-wise collective agreement on small ints (default MIN): every rank returns the
-    same list.  One all-reduce (no-op without a process group)."""
+_REDUCE_OPS = {"min": "MIN", "max": "MAX", "sum": "SUM"}
+
+
+def collective_device() -> torch.device:
+    """Where a small host-side collective's tensor must live: the current GPU under RCCL
+    (``nccl``), the CPU under gloo."""
+    if _pg_active() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def agree(values, device: Optional[torch.device] = None, ops=None):
+    """Element-wise collective agreement on small ints (``ops`` per element: ``"min"``
+    (default), ``"max"`` or ``"sum"``): every rank returns the same list.  One all-reduce
+    per distinct op (no-op without a process group)."""
     vals = [int(v) for v in values]
     if not (_pg_active()):
         return vals
     ops = ops or ["min"] * len(vals)
+    if device is None:
+        device = collective_device()
     out = []
     t = torch.tensor(vals, dtype=torch.int64, device=device)
     for op in sorted(set(ops)):
         u = t.clone()
-        dist.all_reduce(u, op=dist.ReduceOp.MIN if op == "min" else dist.ReduceOp.MAX)
+        dist.all_reduce(u, op=getattr(dist.ReduceOp, _REDUCE_OPS[op]))
         out.append((op, u.cpu().tolist()))
     res = dict(out)
     return [res[o][i] for i, o in enumerate(ops)]

@@ -27,6 +27,17 @@ def _free_port():
     return p
 
 
+def _check_stream_dp(out, n):
+    """The stream_dp phase: every rank trained on its own offset ranges of the 10-partition topic."""
+    sdp = out["stream_dp"]
+    assert "error" not in sdp and "skipped" not in sdp, sdp
+    assert sdp["world"] == n and len(sdp["partition_lists"]) == n and all(sdp["partition_lists"]), sdp
+    assert sdp["steps_equal"] and sdp["replicas_identical"], sdp
+    assert sum(r["rows_read"] for r in sdp["per_rank"]) == sdp["rows"], sdp
+    assert sdp["trained_rows"] == sum(r["kept"] for r in sdp["per_rank"]) and sdp["trained_rows_per_s"] > 0, sdp
+    assert out["stream_dp_rows_per_s"] == sdp["trained_rows_per_s"]
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
     env = dict(os.environ, SML_SHARE_GPU0="1", OMP_NUM_THREADS="2")
@@ -36,7 +47,7 @@ def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
            "--gpus", "2", "--steps", "4", "--warmup", "2", "--batch-per-gpu", "65536",
            "--dataset-rows", "262144", "--infer-events", "2000", "--infer-repeats", "1", "--e2e-events", "0",
            "--lstm-steps", "0", "--batch32-steps", "2000", "--mqtt-clients", "0", "--large-stream-rows", "400000",
-           "--dump-params", dump]
+           "--stream-dp-rows", "150000", "--stream-dp-batch", "16384", "--dump-params", dump]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -59,6 +70,7 @@ def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
     big = out["stream_large_batch"]
     assert "error" not in big and big["engine"] == "throughput" and big["trained_rows_per_s"] > 0, big
     assert [c["workers"] for c in big["decode_curve"]] == [1, 2, 4, 8, 16], big
+    _check_stream_dp(out, 2)
     p0 = np.load(dump + ".rank0.npy")
     p1 = np.load(dump + ".rank1.npy")
     np.testing.assert_array_equal(p0, p1)
@@ -80,7 +92,7 @@ def test_bench_n_ranks_rehearsal(tmp_path, cuda_device, n):
            "--batch32-steps", "2000", "--fleet-models", "64", "--dp-steps", "500", "--collective-iters", "50",
            "--fit-epochs", "2", "--fresh-steps", "2", "--fit-rows", "200000", "--stream-rows", "500000",
            "--lstm-steps", "4", "--mqtt-clients", "2000", "--mqtt-interval", "1", "--mqtt-messages", "2",
-           "--large-stream-rows", "400000",
+           "--large-stream-rows", "400000", "--stream-dp-rows", "100000", "--stream-dp-batch", "8192",
            "--budget-s", "240", "--dump-params", dump]
     t0 = __import__("time").time()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
@@ -100,11 +112,12 @@ def test_bench_n_ranks_rehearsal(tmp_path, cuda_device, n):
     for k in ("infer", "small_allreduce", "keras_batch32_dp", "kafka_e2e", "lstm_kafka_e2e", "keras_batch32",
               "fit_large_batch",
               "fresh_rows", "fit_batch100", "stream_e2e", "stream_large_batch", "lstm_seq50", "lstm_ref",
-              "lstm_infer", "mqtt_e2e",
+              "lstm_infer", "mqtt_e2e", "stream_dp",
               "total_wall"):
         assert k in ph, (k, ph, out["budget"])
     assert not out["budget"]["skipped"], out["budget"]
     assert out["mqtt_connections"] == 2000 and out["mqtt_dropped"] == 0, out["mqtt_e2e"]
+    _check_stream_dp(out, n)
     assert wall < 300
     ps = [np.load(f"{dump}.rank{i}.npy") for i in range(n)]
     for p in ps[1:]:

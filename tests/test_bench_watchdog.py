@@ -75,3 +75,24 @@ def test_deadline_prints_snapshot_and_ends_the_job(tmp_path):
     assert r.returncode == -9, (r.returncode, r.stderr)        # SIGKILLed instead of sleeping 60 s
     assert dt < 30
     assert len(ls) == 1 and ls[0]["budget"]["exceeded_in"] == "slow_side", r.stdout
+
+
+def test_line_order_ends_with_summary():
+    """bench.py's line: the contract's keys first, scalar secondaries next, detail objects, then
+    a compact ``summary`` LAST (a stored tail of a long line still carries the secondary metric)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("sml_bench_main", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    out = {"infer": {"runs": [1, 2]}, "metric": "m", "value": 48447797557.72098, "unit": "rows/s", "n_gpus": 1,
+           "p50_infer_us": 4.37612, "keras_batch32": {"rows_per_s": 16829151.4, "vs_baseline": 268.57},
+           "config": {"model": "ae"}, "steps": 20, "kafka_e2e_p50_us": 8.973}
+    line = bench.ordered_line(out)
+    keys = list(line)
+    assert keys[:3] == ["metric", "value", "unit"] and keys[-1] == "summary"
+    assert keys.index("p50_infer_us") < keys.index("infer")
+    s = line["summary"]
+    assert s["headline_rows_per_s"] == 4.845e10 and s["ae_infer_p50_us"] == 4.376
+    assert s["vs_baseline_same_batch32"] == 268.6 and s["ae_kafka_e2e_p50_us"] == 8.973
+    assert "lstm_seq50_windows_per_s" not in s
+    json.dumps(line)
