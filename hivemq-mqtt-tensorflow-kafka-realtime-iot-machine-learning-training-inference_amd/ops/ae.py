@@ -272,9 +272,12 @@ class FusedAE:
         if allreduce is None:
             self.reduce(G, RA_ADAM | RA_METRICS | RA_ADVANCE, gscale=1.0 / gb)
         else:
-            self.reduce(G, RA_WRITE_GRAD)
+            # this replica's metric sums are accumulated BEFORE the all-reduce: every replica
+            # keeps its own (``dp.reduce_metrics`` forms the global epoch values), as the
+            # persistent kernel's in-kernel exchange and the CPU trainer do
+            self.reduce(G, RA_WRITE_GRAD | RA_METRICS)
             allreduce(self.grad)
-            self.reduce(1, RA_ADAM | RA_METRICS | RA_ADVANCE, gscale=1.0 / gb, partials=self.grad)
+            self.reduce(1, RA_ADAM | RA_ADVANCE, gscale=1.0 / gb, partials=self.grad)
 
     def train_minibatches(self, nsteps: int, prof: Optional[torch.Tensor] = None, dp=None) -> None:
         """``nsteps`` sequential optimizer steps of ``ring_batch`` rows each, in ONE launch.
@@ -447,9 +450,9 @@ class FusedAE:
         if allreduce is None:
             self.reduce(G, RA_ADAM | RA_METRICS, gscale=1.0 / gb)
         else:
-            self.reduce(G, RA_WRITE_GRAD)
+            self.reduce(G, RA_WRITE_GRAD | RA_METRICS)   # local metric sums (see step_ring)
             allreduce(self.grad)
-            self.reduce(1, RA_ADAM | RA_METRICS, gscale=1.0 / gb, partials=self.grad)
+            self.reduce(1, RA_ADAM, gscale=1.0 / gb, partials=self.grad)
 
     def step_empty(self, global_batch: int, allreduce) -> None:
         """This replica has no rows in a data-parallel step (the uneven tail of a sharded
@@ -458,7 +461,7 @@ class FusedAE:
         self.grad.zero_()
         self.iter.add_(1)   # what the train kernel's first workgroup does for a step with rows
         allreduce(self.grad)
-        self.reduce(1, RA_ADAM | RA_METRICS, gscale=1.0 / int(global_batch), partials=self.grad)
+        self.reduce(1, RA_ADAM, gscale=1.0 / int(global_batch), partials=self.grad)
 
     def gradients(self, x: torch.Tensor, global_batch: Optional[int] = None) -> Tuple[List[np.ndarray], np.ndarray]:
         """Mean-over-batch gradients (Keras weight order) + raw metric sums; no update."""

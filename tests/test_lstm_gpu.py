@@ -231,6 +231,37 @@ def test_fused_lstm_vs_bf16_rounded_reference(cuda_device, u, act, B, T, inp, la
         assert relerr(d.cpu(), r) < 1e-3, name
 
 
+@pytest.mark.parametrize("u,inp,need_dx", [(32, 18, False), (16, 32, True)])
+def test_fused_lstm_persistent_tile_loop_vs_bf16_reference(cuda_device, u, inp, need_dx):
+    """B large enough that every workgroup of the persistent backward grid (CUs x 1-2
+    workgroups, lstm_fused.hip) loops over several 16-sequence tiles, with a ragged last tile:
+    the per-tile state reset, the weight-gradient accumulators carried across tiles and the
+    padding lanes' zero dz are all exercised (the other tests use B <= 130: one tile per
+    workgroup).  U=32 without dX (layer 1 of the bench stack), U=16 with dX (layer 2)."""
+    from helpers.bf16_ref import lstm_fused_bf16_reference, relerr
+    if not fused_supported(u, inp):
+        pytest.skip("no fused instance for this shape")
+    cus = torch.cuda.get_device_properties(cuda_device).multi_processor_count
+    B, T = 64 * cus * 2 + 37, 3
+    rng = np.random.default_rng(u + B)
+    x = torch.tensor(rng.uniform(-1, 1, (B, T, inp)), dtype=torch.float32)
+    W = torch.tensor(rng.standard_normal((inp, 4 * u)) * 0.25, dtype=torch.float32)
+    U = torch.tensor(rng.standard_normal((u, 4 * u)) * 0.25, dtype=torch.float32)
+    b = torch.tensor(rng.standard_normal(4 * u) * 0.1, dtype=torch.float32)
+    gy = torch.tensor(rng.standard_normal((B, T, u)), dtype=torch.float32)
+    dev = [t.to(cuda_device).requires_grad_(need_dx if i == 0 else True) for i, t in enumerate((x, W, U, b))]
+    y = FusedLSTMFunction.apply(*dev, 1, False)
+    (y.float() * gy.to(cuda_device)).sum().backward()
+    hseq, dx, dW, dU, db = lstm_fused_bf16_reference(x, W, U, b, "relu", dh=gy, last_only=False,
+                                                     db_bf16=bias_columns(inp))
+    assert relerr(y.detach().cpu(), hseq) < 1e-3
+    checks = [("dW", dev[1].grad, dW), ("dU", dev[2].grad, dU), ("db", dev[3].grad, db)]
+    if need_dx:
+        checks.append(("dx", dev[0].grad, dx))
+    for name, d, r in checks:
+        assert relerr(d.cpu(), r) < 1e-3, name
+
+
 def test_fit_accepts_device_window_views(cuda_device):
     """fit(x, y) with device tensors (sliding_windows views, as the lstm CLIs pass them)
     trains exactly like fit on the host-materialised arrays."""

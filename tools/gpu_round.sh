@@ -20,9 +20,9 @@ step() {
 STEPS=${STEPS:-"tests smoke bench pmc"}
 for s in $STEPS; do
   case $s in
-    tests) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    tests) step pytest_gpu ${TESTS_TIMEOUT:-600} python -u -m pytest ${TESTS:-tests -m gpu} -x -q -p no:cacheprovider --timeout ${TEST_TIMEOUT:-120} --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
-    bench) step bench 400 python bench.py ;;
+    bench) step bench 400 python bench.py ${BENCH_ARGS:-} ;;
     pmc) step pmc 300 bash tools/gpu_pmc_r02.sh ;;
   esac
 done
