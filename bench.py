@@ -386,7 +386,7 @@ def measure_fresh_rows(spec, data, device, batch, steps, scale, shift, seed=0):
     t_direct = timed(lambda k: ae.step(sl(k)))
     t_packed = timed(lambda k: (ae.pack_ring(sl(k), batch), ae.step_ring()))
     t_pack = timed(lambda k: ae.pack_ring(sl(k), batch))
-    return {"rows_per_s": batch / t_direct, "ms_per_step": t_direct * 1e3, "path": "direct fused step (rows in place)",
+    return {"rows_per_s": batch / t_direct, "ms_per_step": t_direct * 1e3, "path": "direct fused step: packed-pair kernel on the raw rows in place, normalize_fn + argmax(x) in registers",
             "pack_then_packed_kernel": {"rows_per_s": batch / t_packed, "ms_per_step": t_packed * 1e3},
             "pack_ms_per_step": t_pack * 1e3, "pack_tb_s": batch * (72 + 73) / t_pack / 1e12,
             "steps": steps, "batch": batch}

@@ -19,8 +19,14 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+SCENARIOS = {   # infrastructure/test-generator/scenario*.xml
+    "full": {"clients": 100_000, "interval_s": 10.0, "messages": 3000, "qos": 0},       # scenario.xml:13, 48-49
+    "evaluation": {"clients": 25, "interval_s": 5.0, "messages": 40, "qos": 1},         # scenario_evaluation.xml:13, 47-48
+}
+
+
 def measure(device="cuda", clients=100_000, interval_s=10.0, messages=3, brokers=None, agents=None, partitions=10,
-            threads=4, lstm=True, name="bench-fleet", sources_per_agent=1):
+            threads=4, lstm=True, name="bench-fleet", sources_per_agent=1, qos=0, window_s=None):
     """One fleet run; scorers built here (the AE at random init, the reference LSTM stack at
     look_back 1 -- cardata-v2.py:172-183 -- with one device slot per car)."""
     from streamml.mqtt.fleet import run_fleet
@@ -29,7 +35,7 @@ def measure(device="cuda", clients=100_000, interval_s=10.0, messages=3, brokers
         sc = load_io().EchoScorer(18, 5.0)
         lsc = load_io().EchoScorer(18, 5.0, nkeys=clients) if lstm else None
         return run_fleet(sc, clients, interval_s, messages, brokers, agents, partitions, threads, lstm_scorer=lsc,
-                         name=name, sources_per_agent=sources_per_agent)
+                         name=name, sources_per_agent=sources_per_agent, qos=qos, window_s=window_s)
     import torch
 
     from streamml.models.autoencoder import Autoencoder
@@ -41,12 +47,13 @@ def measure(device="cuda", clients=100_000, interval_s=10.0, messages=3, brokers
     with ScoringServer(ae, threshold=5.0) as srv:
         if not lstm:
             r = run_fleet(srv, clients, interval_s, messages, brokers, agents, partitions, threads, name=name,
-                          sources_per_agent=sources_per_agent)
+                          sources_per_agent=sources_per_agent, qos=qos, window_s=window_s)
         else:
             lm = LSTMPredictor.reference(look_back=1, device=dev)
             with LSTMScoringServer(lm, nkeys=clients, threshold=5.0) as lsrv:
                 r = run_fleet(srv, clients, interval_s, messages, brokers, agents, partitions, threads,
-                              lstm_scorer=lsrv, name=name, sources_per_agent=sources_per_agent)
+                              lstm_scorer=lsrv, name=name, sources_per_agent=sources_per_agent, qos=qos,
+                              window_s=window_s)
     r["scorers"] = ["autoencoder (ae_serve.hip)"] + (["LSTM reference stack, look_back 1 (lstm_serve.hip)"] if lstm
                                                      else [])
     return r
@@ -64,9 +71,32 @@ def main():
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--sources-per-agent", type=int, default=1)
     ap.add_argument("--no-lstm", action="store_true")
+    ap.add_argument("--qos", type=int, default=0)
+    ap.add_argument("--scenario", choices=sorted(SCENARIOS), default=None,
+                    help="the reference scenario's clients / interval / messages / QoS (--messages still caps the "
+                         "rounds if given)")
+    ap.add_argument("--window", type=float, default=None, help="timeline window (s); default the send interval")
+    ap.add_argument("--out", default=None, help="also write the JSON here")
     a = ap.parse_args()
-    print(json.dumps(measure(a.device, a.clients, a.interval, a.messages, a.brokers, a.agents, a.partitions,
-                             a.threads, not a.no_lstm, sources_per_agent=a.sources_per_agent)), flush=True)
+    clients, interval, messages, qos = a.clients, a.interval, a.messages, a.qos
+    if a.scenario:
+        sc = SCENARIOS[a.scenario]
+        clients, interval, qos = sc["clients"], sc["interval_s"], sc["qos"]
+        messages = min(a.messages, sc["messages"]) if "--messages" in sys.argv else sc["messages"]
+    r = measure(a.device, clients, interval, messages, a.brokers, a.agents, a.partitions, a.threads, not a.no_lstm,
+                sources_per_agent=a.sources_per_agent, qos=qos, window_s=a.window)
+    r["scenario"] = a.scenario
+    r["qos"] = qos
+    ae = r.get("timeline", {}).get("ae", [])
+    r["soak_summary"] = {
+        "windows": len(ae), "scored": r["ae"]["scored"], "published": r["published"], "dropped": r["dropped"],
+        "p99_us_per_window": [w["p99_us"] for w in ae], "max_us": r["ae"]["publish_to_result_max_us"],
+        "broker_rss_mb": r["broker_rss_mb"], "short_windows": sum(1 for w in ae[:-1] if w["scored"] < w["offered"])}
+    line = json.dumps(r)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(line + "\n")
+    print(line, flush=True)
 
 
 if __name__ == "__main__":

@@ -35,6 +35,7 @@ from typing import List, Sequence, Tuple
 
 import numpy as np
 
+from ..kafka.assign import HASH_SPACE
 from ..ops._ext import load_io
 from ..utils.affinity import parse_cpus, resolve_cpus  # noqa: F401  (serve.parse_cpus)
 from . import common
@@ -44,9 +45,19 @@ USAGE = ("python -m streamml.cli serve <servers> <topic> <result_topic> <model-f
 
 
 def shard_partitions(n_partitions: int, rank: int, world: int) -> List[int]:
-    """Partitions owned by replica ``rank`` of ``world`` (round-robin, so W > P leaves
-    replicas idle instead of splitting a partition and breaking per-key order)."""
+    """Whole partitions round-robin (``p % world == rank``): Kafka consumer-group semantics,
+    skewed when ``world`` does not divide the partition count (8 replicas over the reference's
+    10 partitions: 2 vs 1).  ``serve`` uses :func:`serve_shares` instead."""
     return [p for p in range(int(n_partitions)) if p % int(world) == int(rank)]
+
+
+def serve_shares(n_partitions: int, rank: int, world: int):
+    """Replica ``rank``'s ``(partition, hash_lo, hash_hi)`` key shares (kafka/assign.py "keys"):
+    the partitions laid on a line, each replica owning ``P / W`` of it; where a cut falls
+    inside a partition, its car keys are split by a 32-bit key hash.  Every car is scored by
+    exactly one replica, in order, and the replicas' loads are equal at any ``W``."""
+    from ..kafka.assign import key_shares
+    return key_shares(n_partitions, rank, world)
 
 
 def replica_identity(ns) -> Tuple[int, int]:
@@ -92,7 +103,8 @@ def _flags(p) -> None:
                         "SENSOR_DATA_S) directly instead of the Avro stream")
 
 
-def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary, rank: int = 0) -> int:
+def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary, rank: int = 0,
+                       hash_ranges=None) -> int:
     """One C++ loop per replica over the resident scorer: the autoencoder's, or -- ``--model
     lstm`` -- the per-car forecaster, whose car key -> device slot map lives in the loop
     (cardata-v2.py:220-273 streams one LSTM prediction per event)."""
@@ -113,7 +125,8 @@ def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary, ran
         loop = LowLatencyScorer(servers, ns.topic, ns.result_topic, mine, srv, schema=ns.schema, group=ns.group,
                                 starts=starts, result_partitions=[p % result_parts for p in mine],
                                 emit_recon=ns.emit == "both", config=cfg, max_batch=min(ns.max_batch, 4096),
-                                max_wait_ms=ns.max_wait_ms, spin_us=ns.spin_us, source_format=ns.source_format)
+                                max_wait_ms=ns.max_wait_ms, spin_us=ns.spin_us, source_format=ns.source_format,
+                                hash_ranges=hash_ranges)
         mask = os.sched_getaffinity(0)
         cpus = resolve_cpus(ns.cpus, slot=rank)
         if cpus:
@@ -126,7 +139,8 @@ def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary, ran
     ENGINE.anomaly_events.inc(st["anomalies"], model=model.name)
     if ns.model == "lstm":
         summary.update(model="lstm", keys=st["keys"])
-    summary.update(events=st["events"], anomalies=st["anomalies"], skipped=st["skipped"],
+    summary.update(events=st["events"], anomalies=st["anomalies"], skipped=st["skipped"], foreign=st["foreign"],
+                   keys_dropped=st["keys_dropped"],
                    events_per_s=st["events"] / st["wall_s"] if st["wall_s"] > 0 else 0.0, low_latency=True,
                    stages_s={k: st[k] for k in ("fetch_s", "decode_s", "score_s", "format_s", "produce_s",
                                                  "commit_s")})
@@ -177,9 +191,14 @@ def main(argv: Sequence[str]) -> int:
             pass   # another replica created it first
         meta = KafkaClient(servers, cfg).partitions()
     result_parts = max(1, meta.get(ns.result_topic, 1))
-    mine = shard_partitions(n_parts, rank, world)
+    shares = serve_shares(n_parts, rank, world)
+    mine = [p for p, _, _ in shares]
+    partial = any(not (lo == 0 and hi == HASH_SPACE) for _, lo, hi in shares)
+    if partial:   # a shared partition's position is per replica: its own consumer group
+        ns.group = f"{ns.group}.{rank}-of-{world}"
     print(f"replica {rank}/{world}: partitions {mine} of {n_parts} on {device}", flush=True)
-    summary = {"replica": rank, "replicas": world, "partitions": mine, "events": 0, "anomalies": 0}
+    summary = {"replica": rank, "replicas": world, "partitions": mine, "events": 0, "anomalies": 0,
+               "key_shares": [[p, lo / HASH_SPACE, hi / HASH_SPACE] for p, lo, hi in shares], "group": ns.group}
     if not mine:
         print(json.dumps(summary), flush=True)
         return 0
@@ -187,7 +206,8 @@ def main(argv: Sequence[str]) -> int:
     if ns.source_format == "json" and not ns.low_latency:
         raise SystemExit("--source-format json needs --low-latency (the C++ loop decodes the JSON events)")
     if ns.low_latency:
-        return _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary, rank)
+        return _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary, rank,
+                                  [(lo, hi) for _, lo, hi in shares])
     forecaster, key_ids = None, {}
     if ns.model == "lstm":
         if model.device.type != "cuda":
@@ -195,9 +215,11 @@ def main(argv: Sequence[str]) -> int:
         from ..ops.serve import LSTMScoringServer
         forecaster = LSTMScoringServer(model, nkeys=ns.max_keys, threshold=ns.threshold)
     start = -2 if ns.from_beginning else 0
-    topics = [f"{ns.topic}:{p}:{start}" for p in mine]
+    # every partition listed; the plan keeps this replica's key shares (records of a shared
+    # partition whose car another replica owns are dropped after decode)
+    topics = [f"{ns.topic}:{p}:{start}" for p in range(n_parts)]
     stream = kafka(servers, topics, schema=ns.schema, group=ns.group, eof=False, config=cfg, commit=True,
-                   resume=not ns.from_beginning, idle_timeout_s=ns.idle_timeout)
+                   resume=not ns.from_beginning, idle_timeout_s=ns.idle_timeout, shard=(rank, world), assign="keys")
     sinks, next_index = {}, {}
     t0 = time.perf_counter()
     for chunk in stream:

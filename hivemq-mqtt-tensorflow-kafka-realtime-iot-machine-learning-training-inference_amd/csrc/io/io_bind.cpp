@@ -434,6 +434,10 @@ PYBIND11_MODULE(_io, m) {
            }),
            py::arg("dim"), py::arg("threshold") = 5.0f, py::arg("nkeys") = 0)
       .def("c_api", [](EchoScorer& e) { return reinterpret_cast<uintptr_t>(&e.api); });
+  m.def("key_share_hash", [](py::bytes key) {
+    const std::string k = key;
+    return serve::key_share_hash(reinterpret_cast<const uint8_t*>(k.data()), (int64_t)k.size());
+  }, "FNV-1a 64 >> 32 of a record key (the serving loop's key-share hash; kafka/assign.py key_hash)");
   py::class_<serve::ScoreLoop>(m, "ScoreLoop")
       .def(py::init([](const std::string& bootstrap, const std::string& client_id, const std::string& mech,
                        const std::string& user, const std::string& pw, int timeout_ms, const py::list& fields,
@@ -442,7 +446,7 @@ PYBIND11_MODULE(_io, m) {
                        std::vector<int> feature_fields, bool framing, bool emit_recon, int max_batch,
                        int32_t max_bytes, int32_t max_wait_ms, double commit_interval_s, bool record_latency,
                        uintptr_t api, int spin_us, std::vector<std::pair<std::string, int>> json_columns,
-                       const std::string& json_stamp) {
+                       const std::string& json_stamp, std::vector<std::pair<uint64_t, uint64_t>> hash_ranges) {
              kafka::ClientConfig c;
              c.client_id = client_id;
              c.sasl_mechanism = mech;
@@ -467,6 +471,7 @@ PYBIND11_MODULE(_io, m) {
              lc.record_latency = record_latency;
              lc.json_columns = std::move(json_columns);
              lc.json_stamp = json_stamp;
+             lc.hash_ranges = std::move(hash_ranges);
              return new serve::ScoreLoop(bootstrap, c, fields_from_py(fields), lc,
                                          reinterpret_cast<const SmlScorerApi*>(api));
            }),
@@ -476,7 +481,8 @@ PYBIND11_MODULE(_io, m) {
            py::arg("result_partitions"), py::arg("feature_fields"), py::arg("framing"), py::arg("emit_recon"),
            py::arg("max_batch"), py::arg("max_bytes"), py::arg("max_wait_ms"), py::arg("commit_interval_s"),
            py::arg("record_latency"), py::arg("scorer_api"), py::arg("spin_us") = 0,
-           py::arg("json_columns") = std::vector<std::pair<std::string, int>>{}, py::arg("json_stamp") = "")
+           py::arg("json_columns") = std::vector<std::pair<std::string, int>>{}, py::arg("json_stamp") = "",
+           py::arg("hash_ranges") = std::vector<std::pair<uint64_t, uint64_t>>{})
       .def("run",
            [](serve::ScoreLoop& l, int64_t max_events, double idle_timeout_s) {
              serve::LoopStats st;
@@ -500,6 +506,8 @@ PYBIND11_MODULE(_io, m) {
              d["commit_s"] = st.commit_s;
              d["wall_s"] = st.wall_s;
              d["keys"] = st.keys;
+             d["foreign"] = st.foreign;
+             d["keys_dropped"] = st.keys_dropped;
              return d;
            },
            py::arg("max_events") = 0, py::arg("idle_timeout_s") = -1.0)
@@ -713,16 +721,18 @@ PYBIND11_MODULE(_io, m) {
       });
 
   py::class_<kafka::Broker>(m, "KafkaBroker")
-      .def(py::init([](int port, const std::string& user, const std::string& pw, int64_t retention) {
+      .def(py::init([](int port, const std::string& user, const std::string& pw, int64_t retention,
+                       int64_t message_max_bytes) {
              kafka::BrokerConfig c;
              c.port = port;
              c.sasl_username = user;
              c.sasl_password = pw;
              c.retention_records = retention;
+             c.message_max_bytes = message_max_bytes;
              return new kafka::Broker(c);
            }),
            py::arg("port") = 0, py::arg("sasl_username") = "", py::arg("sasl_password") = "",
-           py::arg("retention_records") = -1)
+           py::arg("retention_records") = -1, py::arg("message_max_bytes") = 1048588)
       .def_property_readonly("port", &kafka::Broker::port)
       .def("create_topic", &kafka::Broker::create_topic)
       .def("append",

@@ -162,7 +162,7 @@ enum Api : int16_t {
   API_SASL_AUTH = 36,
 };
 enum Err : int16_t {
-  E_NONE = 0, E_OFFSET_OUT_OF_RANGE = 1, E_UNKNOWN_TOPIC = 3, E_NOT_LEADER = 6,
+  E_NONE = 0, E_OFFSET_OUT_OF_RANGE = 1, E_UNKNOWN_TOPIC = 3, E_NOT_LEADER = 6, E_MESSAGE_TOO_LARGE = 10,
   E_ILLEGAL_SASL_STATE = 34, E_UNSUPPORTED_SASL = 33, E_SASL_AUTH_FAILED = 58,
 };
 }  // namespace
@@ -170,8 +170,41 @@ enum Err : int16_t {
 // ---------------------------------------------------------------------------
 // record batch v2
 // ---------------------------------------------------------------------------
+namespace {
+// largest record batch (baseOffset + batchLength + batchLength bytes) of a record set
+int64_t max_batch_size(const uint8_t* p, size_t n) {
+  int64_t best = 0;
+  size_t o = 0;
+  while (o + 12 <= n) {
+    const int32_t len = (int32_t)((uint32_t)p[o + 8] << 24 | (uint32_t)p[o + 9] << 16 | (uint32_t)p[o + 10] << 8 |
+                                  (uint32_t)p[o + 11]);
+    if (len < 0) break;
+    best = std::max<int64_t>(best, 12 + (int64_t)len);
+    o += 12 + (size_t)len;
+  }
+  return best;
+}
+}  // namespace
 std::string encode_record_batch(int64_t base_offset, const std::vector<Record>& recs) {
   return encode_record_batch(base_offset, recs.data(), recs.size());
+}
+
+std::string encode_record_set(const std::vector<Record>& recs, size_t max_batch_bytes) {
+  // a producer's record set: consecutive batches, each under the broker's message.max.bytes
+  std::string out;
+  size_t k = 0;
+  while (k < recs.size()) {
+    size_t bytes = 0, m = 0;
+    while (k + m < recs.size()) {
+      const size_t rb = recs[k + m].value.size() + recs[k + m].key.size() + 32;   // + varint framing
+      if (m > 0 && bytes + rb > max_batch_bytes) break;
+      bytes += rb;
+      ++m;
+    }
+    out += encode_record_batch(0, recs.data() + k, m);
+    k += m;
+  }
+  return out;
 }
 
 std::string encode_record_batch(int64_t base_offset, const Record* recs, size_t n) {
@@ -838,7 +871,7 @@ int64_t Client::produce(const std::string& topic, int partition, const std::vect
   w.str(topic);
   w.arr(1);
   w.i32(partition);
-  w.bytes(encode_record_batch(0, recs));
+  w.bytes(encode_record_set(recs));
   const std::string resp = call(conn_for(topic, partition), API_PRODUCE, 3, w.s);
   if (acks == 0) return -1;
   R r{reinterpret_cast<const uint8_t*>(resp.data()), resp.size()};
@@ -873,7 +906,7 @@ void Client::produce_multi(const std::string& topic, const std::vector<std::pair
     w.arr((int32_t)lead.second.size());
     for (size_t i : lead.second) {
       w.i32(parts[i].first);
-      w.bytes(encode_record_batch(0, parts[i].second));
+      w.bytes(encode_record_set(parts[i].second));
     }
     const std::string resp = call(*lead.first, API_PRODUCE, 3, w.s);
     if (acks == 0) continue;
@@ -1507,8 +1540,6 @@ std::string Broker::handle(int16_t api, int16_t ver, const uint8_t* body, size_t
         for (int32_t k = 0; k < np; ++k) {
           const int32_t p = r.i32();
           auto recs = r.bytes();
-          FetchResult tmp;
-          decode_record_batches(recs.first, recs.second, INT64_MIN, tmp);
           auto it = topics_.find(name);
           w.i32(p);
           if (it == topics_.end() || p < 0 || p >= (int32_t)it->second.size()) {
@@ -1517,6 +1548,14 @@ std::string Broker::handle(int16_t api, int16_t ver, const uint8_t* body, size_t
             w.i64(-1);
             continue;
           }
+          if (cfg_.message_max_bytes > 0 && max_batch_size(recs.first, recs.second) > cfg_.message_max_bytes) {
+            w.i16(E_MESSAGE_TOO_LARGE);   // a record batch over message.max.bytes: nothing appended
+            w.i64(-1);
+            w.i64(-1);
+            continue;
+          }
+          FetchResult tmp;
+          decode_record_batches(recs.first, recs.second, INT64_MIN, tmp);
           std::vector<Record> recs_in(tmp.size());
           for (size_t q = 0; q < tmp.size(); ++q) {
             Record& rec = recs_in[q];

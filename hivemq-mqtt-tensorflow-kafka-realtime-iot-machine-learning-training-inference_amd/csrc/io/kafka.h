@@ -62,6 +62,10 @@ struct FetchResult {
 // record batch v2 codec
 std::string encode_record_batch(int64_t base_offset, const std::vector<Record>& recs);
 std::string encode_record_batch(int64_t base_offset, const Record* recs, size_t n);
+// Record set of consecutive batches, each at most ~max_batch_bytes (a broker refuses a batch
+// over message.max.bytes: 1 048 588 by default)
+constexpr size_t kMaxBatchBytes = 900u * 1024u;
+std::string encode_record_set(const std::vector<Record>& recs, size_t max_batch_bytes = kMaxBatchBytes);
 void decode_record_batches(const uint8_t* p, size_t n, int64_t min_offset, FetchResult& out);
 
 // Zero-copy iteration over the records of a fetched record set (v2 batches, CRC
@@ -175,6 +179,7 @@ struct BrokerConfig {
   int64_t retention_records = -1;           // -1 = unbounded
   bool auto_create_topics = true;            // Kafka's auto.create.topics.enable default
   int spin_us = 0;                           // > 0: connection threads / long polls busy-wait this long first
+  int64_t message_max_bytes = 1048588;        // Kafka's message.max.bytes default (per record batch); <= 0 = no cap
 };
 
 class Broker {

@@ -833,7 +833,7 @@ void Broker::bridge_loop() {
       bq_.erase(bq_.begin(), bq_.begin() + (long)n);
     }
     bq_done_cv_.notify_all();
-    size_t failed = 0;
+    size_t failed = 0, sent = 0;
     try {
       if (!kc) kc.reset(new kafka::Client(cfg_.kafka_bootstrap, cfg_.kafka));
       // group by (kafka topic, partition), keep arrival order inside a group
@@ -857,24 +857,68 @@ void Broker::bridge_loop() {
         groups[gk].push_back(std::move(rec));
         gmap[gk] = br.mapping;
       }
-      // one Produce request per topic (per partition leader) with all its partitions
-      std::map<std::string, std::vector<std::pair<int, std::vector<kafka::Record>>>> per_topic;
-      std::map<std::string, std::vector<std::pair<int, size_t>>> per_topic_counts;   // (mapping, records)
+      // A partition's records go out in record batches of at most bridge_batch records and
+      // kBridgeBatchBytes bytes (a broker refuses a batch over message.max.bytes, 1 MB by
+      // default).  Request j of a topic carries batch j of each of its partitions: one
+      // Produce per topic per round, every partition in it.
+      using Round = std::vector<std::pair<int, std::vector<kafka::Record>>>;
+      std::map<std::string, std::vector<Round>> rounds;
+      std::map<std::string, std::vector<std::vector<std::pair<int, size_t>>>> round_counts;   // (mapping, records)
+      const size_t max_recs = (size_t)std::max(1, cfg_.bridge_batch);
       for (auto& gr : groups) {
-        per_topic_counts[gr.first.first].emplace_back(gmap[gr.first], gr.second.size());
-        per_topic[gr.first.first].emplace_back(gr.first.second, std::move(gr.second));
+        auto& rs = rounds[gr.first.first];
+        auto& rc = round_counts[gr.first.first];
+        size_t j = 0, bytes = 0;
+        std::vector<kafka::Record> cur;
+        auto close_chunk = [&]() {
+          if (cur.empty()) return;
+          if (rs.size() <= j) {
+            rs.emplace_back();
+            rc.emplace_back();
+          }
+          rc[j].emplace_back(gmap[gr.first], cur.size());
+          rs[j].emplace_back(gr.first.second, std::move(cur));
+          cur.clear();
+          bytes = 0;
+          ++j;
+        };
+        for (auto& r : gr.second) {
+          const size_t rb = r.value.size() + r.key.size() + 32;   // + record framing
+          if (!cur.empty() && (cur.size() >= max_recs || bytes + rb > kBridgeBatchBytes)) close_chunk();
+          bytes += rb;
+          cur.push_back(std::move(r));
+        }
+        close_chunk();
       }
-      for (auto& pt : per_topic) {
-        kc->produce_multi(pt.first, pt.second, 1);
-        for (const auto& mc : per_topic_counts[pt.first]) {
-          map_counts_[(size_t)mc.first]->fetch_add(mc.second);
-          kafka_sent_ += mc.second;
+      bool broken = false;   // a failed request: this connection's later requests are not tried
+      for (auto& tr : rounds) {
+        auto& counts = round_counts[tr.first];
+        for (size_t j = 0; j < tr.second.size(); ++j) {
+          size_t n = 0;
+          for (const auto& mc : counts[j]) n += mc.second;
+          if (!broken) {
+            try {
+              kc->produce_multi(tr.first, tr.second[j], 1);
+              for (const auto& mc : counts[j]) map_counts_[(size_t)mc.first]->fetch_add(mc.second);
+              kafka_sent_ += n;
+              sent += n;
+              continue;
+            } catch (const std::exception&) {
+              broken = true;
+            }
+          }
+          failed += n;
         }
       }
-    } catch (const std::exception&) {
-      failed = batch.size();
+      if (broken) {
+        kafka_failed_ += failed;
+        kc.reset();  // reconnect on the next batch
+        nparts.clear();
+      }
+    } catch (const std::exception&) {   // connect / metadata: nothing of the rest went out
+      failed = batch.size() - sent;
       kafka_failed_ += failed;
-      kc.reset();  // reconnect on the next batch
+      kc.reset();
       nparts.clear();
     }
     {

@@ -96,10 +96,13 @@ struct BrokerConfig {
   std::string kafka_bootstrap;       // "host:port" of the Kafka cluster; empty = no bridge
   kafka::ClientConfig kafka;
   std::vector<TopicMapping> mappings;
-  int bridge_batch = 1024;           // records per Produce request
+  int bridge_batch = 1024;           // records per partition record batch of a Produce request
   int bridge_linger_ms = 2;
   size_t bridge_queue_max = 1 << 20; // back-pressure bound (records)
 };
+
+// Byte cap of one bridged record batch: under a Kafka broker's default message.max.bytes (1 MB)
+constexpr size_t kBridgeBatchBytes = 900u * 1024u;
 
 struct BrokerStats {
   uint64_t incoming_publish = 0;     // com_hivemq_messages_incoming_publish_count

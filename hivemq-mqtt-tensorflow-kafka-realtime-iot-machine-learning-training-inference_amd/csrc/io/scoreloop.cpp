@@ -1,5 +1,6 @@
 #include "scoreloop.h"
 
+#include <algorithm>
 #include <chrono>
 #include <stdexcept>
 #include <thread>
@@ -28,6 +29,20 @@ double secs(int64_t a, int64_t b) { return (double)(b - a) * 1e-9; }
 
 }  // namespace
 
+uint32_t key_share_hash(const uint8_t* key, int64_t len) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  for (int64_t i = 0; i < len; ++i) {
+    h ^= key[i];
+    h *= 0x100000001B3ull;
+  }
+  h ^= h >> 33;   // fmix64: FNV-1a's top bits barely move for keys differing at the end
+  h *= 0xFF51AFD7ED558CCDull;
+  h ^= h >> 33;
+  h *= 0xC4CEB9FE1A85EC53ull;
+  h ^= h >> 33;
+  return (uint32_t)(h >> 32);
+}
+
 ScoreLoop::ScoreLoop(std::string bootstrap, kafka::ClientConfig ccfg, std::vector<avro::Field> fields, LoopConfig cfg,
                      const SmlScorerApi* api)
     : bootstrap_(bootstrap),
@@ -47,6 +62,8 @@ ScoreLoop::ScoreLoop(std::string bootstrap, kafka::ClientConfig ccfg, std::vecto
   if (cfg_.partitions.empty() || cfg_.starts.size() != cfg_.partitions.size() ||
       cfg_.result_partitions.size() != cfg_.partitions.size())
     throw std::invalid_argument("scoreloop: partitions / starts / result_partitions mismatch");
+  if (!cfg_.hash_ranges.empty() && cfg_.hash_ranges.size() != cfg_.partitions.size())
+    throw std::invalid_argument("scoreloop: one hash range per owned partition");
   if (cfg_.max_batch < 1) throw std::invalid_argument("scoreloop: max_batch >= 1");
   pos_ = cfg_.starts;
 }
@@ -105,6 +122,10 @@ LoopStats ScoreLoop::run(int64_t max_events, double idle_timeout_s) {
       grp.push_back(rr);
       wait = idle_round && rr == 0 ? std::min(cfg_.max_wait_ms, 2) : 0;
     }
+    if (grp.size() > 1) {   // rotate the request order: a broker fills the response in request
+      std::rotate(grp.begin(), grp.begin() + (long)(rot_ % grp.size()), grp.end());   // order up to
+      rot_ = (rot_ + 1) % grp.size();                                               // max_bytes
+    }
     want.clear();
     for (size_t i : grp) want.emplace_back(cfg_.partitions[i], pos_[i]);
     const int64_t t0 = steady_ns();
@@ -131,9 +152,18 @@ LoopStats ScoreLoop::run(int64_t max_events, double idle_timeout_s) {
                                  slices[gi].rec_len);
       kafka::RecordView v;
       int64_t next = pos_[pi];
+      const bool shared = !cfg_.hash_ranges.empty() &&
+                          !(cfg_.hash_ranges[pi].first == 0 && cfg_.hash_ranges[pi].second >= (1ull << 32));
       while (cur.next(v)) {
         if (v.offset < pos_[pi]) continue;
         next = v.offset + 1;
+        if (shared) {   // a car of this partition that another replica owns
+          const uint64_t kh = key_share_hash(v.key, v.key_len < 0 ? 0 : v.key_len);
+          if (kh < cfg_.hash_ranges[pi].first || kh >= cfg_.hash_ranges[pi].second) {
+            ++st.foreign;
+            continue;
+          }
+        }
         rows.resize(rows.size() + (size_t)D);
         uint8_t lab = 0;
         int64_t stamp = 0;
@@ -160,28 +190,43 @@ LoopStats ScoreLoop::run(int64_t max_events, double idle_timeout_s) {
     st.decode_s += secs(t1, t2);
     if (!progress) ++st.empty_fetches;
     round_any |= progress;
-    const int k = (int)offs.size();
+    int k = (int)offs.size();
+    if (k > 0 && api_->nkeys > 0) {   // record key -> the key's device slot
+      {
+        kids.resize((size_t)k);
+        int w = 0;   // rows kept: a null key or a key past the slot table is skipped, counted
+        for (int i = 0; i < k; ++i) {
+          const auto& kv = keys[(size_t)i];
+          if (kv.second < 0) {
+            ++st.keys_dropped;
+            continue;
+          }
+          std::string key(reinterpret_cast<const char*>(kv.first), (size_t)kv.second);
+          auto it = key_ids_.find(key);
+          if (it == key_ids_.end()) {
+            if ((int64_t)key_ids_.size() >= api_->nkeys) {
+              ++st.keys_dropped;
+              continue;
+            }
+            it = key_ids_.emplace(std::move(key), (uint32_t)key_ids_.size()).first;
+            st.keys = key_ids_.size();
+          }
+          if (w != i) {
+            std::copy(rows.begin() + (size_t)i * D, rows.begin() + (size_t)(i + 1) * D, rows.begin() + (size_t)w * D);
+            offs[(size_t)w] = offs[(size_t)i];
+            keys[(size_t)w] = keys[(size_t)i];
+            stamps[(size_t)w] = stamps[(size_t)i];
+            src[(size_t)w] = src[(size_t)i];
+          }
+          kids[(size_t)w++] = it->second;
+        }
+        k = w;
+      }
+    }
     if (k > 0) {
       scores.resize((size_t)k);
       flags.resize((size_t)k);
       if (cfg_.emit_recon) recon.resize((size_t)k * (size_t)D);
-      if (api_->nkeys > 0) {   // record key -> the key's device slot
-        kids.resize((size_t)k);
-        for (int i = 0; i < k; ++i) {
-          const auto& kv = keys[(size_t)i];
-          std::string key = kv.second < 0 ? std::string()
-                                          : std::string(reinterpret_cast<const char*>(kv.first), (size_t)kv.second);
-          auto it = key_ids_.find(key);
-          if (it == key_ids_.end()) {
-            if ((int64_t)key_ids_.size() >= api_->nkeys)
-              throw std::runtime_error("scoreloop: more distinct record keys than the scorer's " +
-                                       std::to_string(api_->nkeys) + " key slots");
-            it = key_ids_.emplace(std::move(key), (uint32_t)key_ids_.size()).first;
-            st.keys = key_ids_.size();
-          }
-          kids[(size_t)i] = it->second;
-        }
-      }
       for (int b = 0; b < k; b += cfg_.max_batch) {
         const int n = std::min(cfg_.max_batch, k - b);
         float* rc = cfg_.emit_recon ? recon.data() + (size_t)b * D : nullptr;

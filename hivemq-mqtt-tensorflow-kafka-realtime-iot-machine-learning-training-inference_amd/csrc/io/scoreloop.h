@@ -57,11 +57,18 @@ struct LoopConfig {
   // numeric field copied into the latency records (the device simulator's send time)
   std::vector<std::pair<std::string, int>> json_columns;
   std::string json_stamp;
+  // key-hash share per owned partition (kafka/assign.py "keys"): a record is scored only if
+  // the top 32 bits of fmix64(FNV-1a 64) of its key lie in [lo, hi); empty = every key of every
+  // owned partition.  Replicas sharing a partition split its cars this way, each car on
+  // exactly one replica, in order.
+  std::vector<std::pair<uint64_t, uint64_t>> hash_ranges;
 };
 
 struct LoopStats {
   uint64_t events = 0, anomalies = 0, skipped = 0, batches = 0, fetches = 0, empty_fetches = 0, commits = 0;
   uint64_t keys = 0;   // keyed (LSTM) scorer: distinct record keys given a device slot
+  uint64_t foreign = 0;        // records of a shared partition whose key another replica owns
+  uint64_t keys_dropped = 0;   // keyed scorer: records not scored (key table full, or a null key)
   double fetch_s = 0, decode_s = 0, score_s = 0, format_s = 0, produce_s = 0, commit_s = 0, wall_s = 0;
 };
 
@@ -88,10 +95,12 @@ class ScoreLoop {
   feed::Feed decoder_;   // only its compiled decode plan is used (never started)
   std::unique_ptr<jsonrow::Plan> json_;   // JSON source records
   // keyed scorers: record key -> device slot, first come first served (the device keeps
-  // each slot's window); more distinct keys than the scorer's nkeys is an error
+  // each slot's window); records of keys past the scorer's nkeys slots, and null-keyed
+  // records, are skipped and counted (LoopStats::keys_dropped), never scored into a shared slot
   std::unordered_map<std::string, uint32_t> key_ids_;
   std::vector<int64_t> pos_;
   std::vector<int64_t> lat_;
+  size_t rot_ = 0;   // first partition of the next multi-partition fetch (rotated, KIP-74)
   std::atomic<bool> stop_{false};
 };
 
@@ -103,6 +112,7 @@ std::vector<int64_t> paced_produce(const std::string& bootstrap, kafka::ClientCo
                                    const std::vector<std::string>& keys, double qps);
 
 int64_t steady_ns();
+uint32_t key_share_hash(const uint8_t* key, int64_t len);   // fmix64(FNV-1a 64) >> 32 (kafka/assign.py key_hash)
 
 }  // namespace serve
 }  // namespace sml

@@ -465,6 +465,41 @@ __device__ __forceinline__ int row_argmax_up_pair(const f32x4 lo0, const f32x4 l
   return 63 - (int)(m & 63u);
 }
 
+// The same argmax for values of ANY sign (normalised inputs, argmax(x) of the accuracy
+// metric): the float bits become a signed-int-ordered key (a negative value's magnitude bits
+// flipped: v_ashrrev + v_xor + v_bfi), then (key & ~63) | (63 - f) as above -- ties and gaps
+// below 2^-17 relative go to the lowest index.  Four VALU per feature, one butterfly per pair.
+__device__ __forceinline__ int imax3(int a, int b, int c) {
+  int r;
+  asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ int signed_key(float v, unsigned lo) {
+  const unsigned u = __float_as_uint(v);
+  const unsigned sx = u ^ (unsigned)((int)u >> 31);   // every bit flipped when negative
+  unsigned t, k;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(t) : "s"(0x7fffffffu), "v"(sx), "v"(u));   // keep the sign bit
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(k) : "s"(0xffffffc0u), "v"(t), "v"(lo));
+  return (int)k;
+}
+__device__ __forceinline__ int row_argmax_up_pair_signed(const f32x4 lo0, const f32x4 lo1, float up, int g) {
+  int k0[4], k1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    k0[i] = signed_key(lo0[i], (unsigned)(63 - 4 * g - i));
+    k1[i] = signed_key(lo1[i], (unsigned)(63 - 4 * g - i));
+  }
+  const int ku = signed_key(up, (unsigned)(63 - 16 - (g & 1)));
+  const bool own0 = g < 2;   // which tile's row this lane's `up` belongs to
+  const int m0 = imax3(imax3(k0[0], k0[1], k0[2]), k0[3], own0 ? ku : (-2147483647 - 1));
+  const int m1 = imax3(imax3(k1[0], k1[1], k1[2]), k1[3], own0 ? (-2147483647 - 1) : ku);
+  const auto r16 = __builtin_amdgcn_permlane16_swap((unsigned)m0, (unsigned)m1, false, false);
+  int m = max((int)r16[0], (int)r16[1]);
+  const auto r32 = __builtin_amdgcn_permlane32_swap((unsigned)m, (unsigned)m, false, false);
+  m = imax3((int)r32[0], (int)r32[1], (int)r32[1]);
+  return 63 - (m & 63);
+}
+
 // One 16-row tile: forward, loss, metrics, backward, weight-gradient MFMAs.
 // FAST (zero-preserving activations): no per-feature masks -- padded features
 // stay exactly 0 because their weights are 0 and act(0) = 0; only the bias slot
@@ -1181,10 +1216,11 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
         // ILP 2: tile pairs (t, t + stride), two issues per iteration, the pair's two tiles
         // landed = vmcnt(NV * (PF - 2)); a last unpaired tile runs alone (U = 1).  ILP 3:
         // contiguous tile pairs (below).
-        static_assert(XM == 1 && CH == 1 && PF >= 3, "tile pairs: tile-packed ring, plain order");
+        static_assert((XM == 1 || (XM == 0 && ILP == 3)) && CH == 1 && PF >= 3,
+                      "tile pairs: tile-packed ring (or raw rows, packed pairs), plain order");
         auto ring_tile = [&](int slot, f32x4 xf[2], int& ix) {
           typedef __attribute__((address_space(3))) const unsigned char lds_u8;
-          ix = (int)*(lds_u8*)(ring + slot * slotb + 64 * a.D + c);
+          if constexpr (XM == 1) ix = (int)*(lds_u8*)(ring + slot * slotb + 64 * a.D + c);
           if constexpr (ILP == 3) {   // inputs 0..15 only (16 / 17 come as UP, ring_up)
             typedef __attribute__((address_space(3))) const f32x2_t lds_f2;
             const char* row = ring + slot * slotb + c * 4 * a.D + 16 * g;
@@ -1218,7 +1254,10 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
           const int64_t npairs = nfull >> 1;
           auto issue_pair = [&](int64_t pi, int ps) {
             pi = pi < npairs ? pi : npairs - 1;   // prefetch past the end re-reads the last pair
-            const char* src = reinterpret_cast<const char*>(a.xpack) + pi * pairb;
+            // XM 1: the tile-packed ring; XM 0: the raw rows themselves (ld == D: a pair of
+            // whole tiles is 32 contiguous rows = pairb bytes)
+            const char* src = (XM == 1 ? reinterpret_cast<const char*>(a.xpack) : reinterpret_cast<const char*>(a.x)) +
+                              pi * pairb;
             const unsigned dst = ring_lds + ps * pairb;
             glds16(src, voff, dst);
             glds16(src + 1024, voff, dst + 1024);
@@ -1239,7 +1278,23 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
             int ix[2];
             ring_tile(2 * rs, xf[0], ix[0]);
             ring_tile(2 * rs + 1, xf[1], ix[1]);
-            const float xup = ring_up(2 * rs);
+            float xup = ring_up(2 * rs);
+            if constexpr (XM == 0) {
+              // raw rows (the direct step: rows trained once): normalize_fn on the lane's inputs
+              // 4g..4g+3 of both tiles and its UP input 16 + (g & 1), then argmax(x) of both
+              // tiles' rows with one butterfly -- what pack_tiles_argmax does at ingest for XM 1
+              typedef __attribute__((address_space(3))) const f32x4 lds_f4;
+              typedef __attribute__((address_space(3))) const float lds_f;
+              const f32x4 nsc = *(lds_f4*)(norm + 16 * g), nsh = *(lds_f4*)(norm + 128 + 16 * g);
+              const int fu = 4 * (16 + (g & 1));
+              const float usc = *(lds_f*)(norm + fu), ush = *(lds_f*)(norm + 128 + fu);
+#pragma unroll
+              for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) xf[u][0][j] = fmaf(xf[u][0][j], nsc[j], nsh[j]);
+              xup = fmaf(xup, usc, ush);
+              ix[0] = ix[1] = a.want_acc ? row_argmax_up_pair_signed(xf[0][0], xf[1][0], xup, g) : -1;
+            }
             rs = rs + 1 == PS ? 0 : rs + 1;
             ws = ws + 1 == PS ? 0 : ws + 1;
             train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3, acc4, acc2b,
@@ -1616,6 +1671,12 @@ static int train_ilp() {
   const char* e = getenv("SML_AE_ILP");
   return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 3;
 }
+// SML_AE_DIRECT_PAIRS=0: raw-row steps on the one-tile loop (in-kernel normalise + argmax)
+// instead of the packed-pair loop (A/B; read at every launch like SML_AE_ILP)
+static bool direct_pairs() {
+  const char* e = getenv("SML_AE_DIRECT_PAIRS");
+  return !(e && e[0] == '0');
+}
 static int train_occupancy() {
   const char* e = getenv("SML_AE_OCC");
   return (e && e[0] == '3') ? 3 : 4;
@@ -1714,6 +1775,13 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
     }
     else if (ring_ok && occ == 4 && D == 18 && xa_ok)
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18, 1>), gd, bd, 0, stream, a);
+    else if (ring_ok && D == 18 && xpack == nullptr && (n & 31) == 0 && train_ilp() == 3 && direct_pairs() &&
+             dims[1] <= 15 && dims[2] <= 7 && dims[3] <= 7) {
+      // rows trained once (fresh / streamed): packed pairs straight from the raw rows,
+      // normalize_fn + argmax(x) in registers (no K8 pack pass)
+      pair_grid();
+      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 0, 3>), gd, bd, 0, stream, a);
+    }
     else if (ring_ok && occ == 4 && D == 18)  // the cardata-v1 reference model: D fixed at compile time
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18>), gd, bd, 0, stream, a);
     else if (ring_ok && occ == 4 && 3 * 64 * D <= ring_bytes<4>())

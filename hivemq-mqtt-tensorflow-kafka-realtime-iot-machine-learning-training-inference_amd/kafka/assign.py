@@ -16,7 +16,7 @@ of a data-parallel job, or every serving replica, reads a disjoint share of ALL 
 * ``"keys"`` (serving, unbounded, per-key order) -- the key space balanced over the
   replicas: the partitions are laid on a line ``[0, P)`` and replica ``r`` owns
   ``[r P / W, (r + 1) P / W)``.  Where that cuts a partition, the replicas sharing it split
-  its car keys by a 32-bit key hash (FNV-1a, independent of the producer's murmur2
+  its car keys by a 32-bit key hash (FNV-1a + fmix64, independent of the producer's murmur2
   partitioner), so every car is scored by exactly one replica, in order, and each replica
   carries ``P / W`` partitions' worth of keys at any ``W``.
 
@@ -53,8 +53,8 @@ class Share:
 
 
 def key_hash(key) -> int:
-    """32-bit share hash of a record key: the top half of FNV-1a 64 (``scoreloop.cpp`` computes
-    the same).  ``None`` keys hash as the empty key."""
+    """32-bit share hash of a record key: the top half of fmix64(FNV-1a 64) (``scoreloop.cpp``
+    computes the same).  ``None`` keys hash as the empty key."""
     if key is None:
         b = b""
     elif isinstance(key, str):
@@ -65,6 +65,14 @@ def key_hash(key) -> int:
     for c in b:
         h ^= c
         h = (h * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    # FNV-1a alone leaves the top bits nearly constant for keys that differ in their last
+    # characters ("electric-vehicle-00017" / "-00018"): MurmurHash3's fmix64 finaliser first
+    M = 0xFFFFFFFFFFFFFFFF
+    h ^= h >> 33
+    h = (h * 0xFF51AFD7ED558CCD) & M
+    h ^= h >> 33
+    h = (h * 0xC4CEB9FE1A85EC53) & M
+    h ^= h >> 33
     return h >> 32
 
 

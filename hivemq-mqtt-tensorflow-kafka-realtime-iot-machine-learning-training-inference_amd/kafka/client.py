@@ -44,8 +44,10 @@ class FakeBroker:
     """In-process partitioned append-only log serving the Kafka protocol on 127.0.0.1."""
 
     def __init__(self, port: int = 0, sasl_username: str = "", sasl_password: str = "",
-                 retention_records: int = -1):
-        self._b = _io().KafkaBroker(port, sasl_username, sasl_password, retention_records)
+                 retention_records: int = -1, message_max_bytes: int = 1048588):
+        """``message_max_bytes``: a produced record batch over it is refused (MESSAGE_TOO_LARGE,
+        nothing appended), as a Kafka broker's ``message.max.bytes`` default; <= 0 = no cap."""
+        self._b = _io().KafkaBroker(port, sasl_username, sasl_password, retention_records, message_max_bytes)
 
     @property
     def port(self) -> int:

@@ -57,7 +57,11 @@ class LowLatencyScorer:
                  result_partitions: Optional[Sequence[int]] = None, emit_recon: bool = False,
                  config: Optional[Sequence[str]] = None, max_batch: int = 4096, max_bytes: int = 1 << 20,
                  max_wait_ms: int = 100, commit_interval_s: float = 0.0, record_latency: bool = False,
-                 framing: bool = True, spin_us: int = 0, source_format: str = "avro", json_stamp: str = ""):
+                 framing: bool = True, spin_us: int = 0, source_format: str = "avro", json_stamp: str = "",
+                 hash_ranges: Optional[Sequence] = None):
+        """``hash_ranges``: one ``(lo, hi)`` key-hash share per partition (kafka/assign.py
+        ``key_shares``); records whose key hashes outside it are another replica's cars
+        (skipped, counted as ``foreign``)."""
         client = KafkaClient(servers, config)
         self.partitions = [int(p) for p in partitions]
         if starts is None:   # committed offset of the group, else the log start
@@ -80,7 +84,8 @@ class LowLatencyScorer:
                                          [int(r) for r in result_partitions], fields, framing, bool(emit_recon),
                                          int(max_batch), int(max_bytes), int(max_wait_ms), float(commit_interval_s),
                                          bool(record_latency), int(api), int(spin_us),
-                                         json_columns() if source_format == "json" else [], str(json_stamp))
+                                         json_columns() if source_format == "json" else [], str(json_stamp),
+                                         [(int(lo), int(hi)) for lo, hi in (hash_ranges or [])])
 
     def run(self, max_events: int = 0, idle_timeout_s: Optional[float] = None) -> dict:
         """Blocking (GIL released): until ``stop()``, ``max_events`` or ``idle_timeout_s``

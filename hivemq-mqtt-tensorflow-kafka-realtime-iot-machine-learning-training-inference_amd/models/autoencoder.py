@@ -400,10 +400,12 @@ class Autoencoder:
             return True
         return engine == "auto" and batch_size > self.backend.max_minibatch()
 
-    # rows trained once: the direct fused step (normalize_fn + argmax inside the unpacked
-    # kernel) takes 0.97 ms per 33.5 M rows against 1.03 (K8 pack) + 0.69 (packed-pair
-    # kernel) -- the pack pays off from the 3rd pass over the same rows (profiles/r03)
-    PACK_MIN_PASSES = 3
+    # rows trained once: the direct fused step (packed pairs straight from the raw rows,
+    # normalize_fn + argmax(x) in registers) takes 0.75 ms per 33.5 M rows against 1.04 (K8
+    # pack) + 0.695 (packed-pair kernel on the packed ring) -- the pack pays off only from
+    # ~19 passes over the same rows (profiles/r05/SUMMARY.md; with r03's one-tile direct
+    # loop, 0.97 ms, it was 3)
+    PACK_MIN_PASSES = 18
 
     def _fit_array_throughput(self, xd: torch.Tensor, B: int, steps_per_epoch: Optional[int], shuffle: bool,
                               seed: int, rank: int, epoch: int, world: int, allreduce, gstep: int,

@@ -39,10 +39,29 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 
 def _spawn(args: List[str], stdin=subprocess.DEVNULL) -> subprocess.Popen:
+    """A node / agent child.  Its stderr goes to an unlinked temporary file, never a pipe: a
+    child writing more than a pipe buffer of warnings (per-connection errors over 20 000
+    sockets) would block on a pipe nobody reads until the run's timeouts."""
+    import tempfile
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
-    return subprocess.Popen([sys.executable, "-m", "streamml.mqtt.node"] + args, stdin=stdin,
-                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, cwd=ROOT, env=env, text=True)
+    err = tempfile.TemporaryFile(mode="w+")
+    p = subprocess.Popen([sys.executable, "-m", "streamml.mqtt.node"] + args, stdin=stdin,
+                         stdout=subprocess.PIPE, stderr=err, cwd=ROOT, env=env, text=True)
+    p.err_file = err   # type: ignore[attr-defined]
+    return p
+
+
+def _err_tail(p: subprocess.Popen, n: int = 800) -> str:
+    f = getattr(p, "err_file", None)
+    if f is None:
+        return ""
+    try:
+        f.flush()
+        f.seek(0)
+        return f.read()[-n:]
+    except (OSError, ValueError):
+        return ""
 
 
 def _json_line(p: subprocess.Popen, timeout_s: float) -> dict:
@@ -59,9 +78,19 @@ def _json_line(p: subprocess.Popen, timeout_s: float) -> dict:
     t.start()
     t.join(timeout_s)
     if "d" not in box:
-        err = p.stderr.read() if p.poll() is not None else ""
-        raise RuntimeError(f"fleet child gave no JSON line within {timeout_s:.0f} s (rc={p.poll()}): {err[-800:]}")
+        raise RuntimeError(f"fleet child gave no JSON line within {timeout_s:.0f} s (rc={p.poll()}): {_err_tail(p)}")
     return box["d"]   # type: ignore[return-value]
+
+
+def _rss_mb(pid: int) -> float:
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            for ln in f:
+                if ln.startswith("VmRSS:"):
+                    return int(ln.split()[1]) / 1024.0
+    except OSError:
+        pass
+    return 0.0
 
 
 def plan_processes(clients: int, per_process_max: int = 20_000) -> int:
@@ -78,11 +107,26 @@ def _pct(a: np.ndarray, q: float) -> Optional[float]:
     return float(np.percentile(a, q)) if len(a) else None
 
 
+def _windows(sent_ns: np.ndarray, us: np.ndarray, window_s: float, offered_per_s: float) -> List[dict]:
+    """Per window of send time: events scored vs offered, p50 / p99 / max publish -> result us."""
+    if not len(sent_ns):
+        return []
+    t = (sent_ns - sent_ns.min()) / 1e9
+    idx = (t // window_s).astype(np.int64)
+    out = []
+    for w in range(int(idx.max()) + 1):
+        u = us[idx == w]
+        out.append({"t_s": w * window_s, "scored": int(len(u)), "offered": int(round(offered_per_s * window_s)),
+                    "p50_us": _pct(u, 50), "p99_us": _pct(u, 99), "max_us": float(u.max()) if len(u) else None})
+    return out
+
+
 def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: int = 10,
               brokers: Optional[int] = None, agents: Optional[int] = None, partitions: int = 10,
               threads: int = 4, qos: int = 0, lstm_scorer=None,
               name: str = "fleet", start_delay_s: Optional[float] = None, sources_per_agent: int = 1,
-              max_wait_ms: int = 5, drain_timeout_s: float = 30.0) -> dict:
+              max_wait_ms: int = 5, drain_timeout_s: float = 30.0, sample_s: float = 5.0,
+              window_s: Optional[float] = None) -> dict:
     """Run ``clients`` cars x ``messages`` events at ``clients / interval_s`` msg/s end to end.
 
     ``scorer``: a :class:`~streamml.ops.serve.ScoringServer` (or ``_io.EchoScorer`` on CPU);
@@ -90,7 +134,12 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
     same events per car in a second loop.  Returns connections, connect time, offered and
     achieved rates, per-hop counts, drops and publish -> result latency percentiles (us).
     ``brokers`` / ``agents`` default to (and are raised to) what the descriptor limit needs
-    (:func:`plan_processes`)."""
+    (:func:`plan_processes`).
+
+    Over time (a sustained run): every ``sample_s`` the broker nodes', agents' and this
+    process's resident memory is sampled (``timeline.samples``), and the scored events are cut
+    into ``window_s`` windows of result time (default: the send interval) with each window's
+    count against the offered count and its p50 / p99 / max latency (``timeline.<scorer>``)."""
     from ..kafka import fake_broker
     from ..kafka.scoreloop import LowLatencyScorer
 
@@ -119,6 +168,20 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
             loops.append(lp)
             outs.append(out)
             ths.append(th)
+        samples: List[dict] = []
+        stop_sampler = threading.Event()
+
+        def sampler():
+            while True:
+                samples.append({"t_s": round(time.time() - t_begin, 2),
+                                "broker_rss_mb": round(sum(_rss_mb(p.pid) for p in nodes), 1),
+                                "agents_rss_mb": round(sum(_rss_mb(p.pid) for p in agents_p), 1),
+                                "scorer_rss_mb": round(_rss_mb(os.getpid()), 1)})
+                if stop_sampler.wait(sample_s):
+                    return
+
+        sth = threading.Thread(target=sampler, daemon=True)
+        sth.start()
         per = [clients * i // agents for i in range(agents + 1)]
         if start_delay_s is None:   # interpreter start + every agent's connects (~100 us each, serial per thread)
             start_delay_s = 3.0 + 2.0 * (max(per[i + 1] - per[i] for i in range(agents)) / max(threads, 1)) * 150e-6
@@ -149,6 +212,8 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
             lp.stop()
         for th in ths:
             th.join(10)
+        stop_sampler.set()
+        sth.join(10)
     finally:
         for p in agents_p + nodes:
             if p.poll() is None:
@@ -169,6 +234,10 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
         "bridge_flushed": all(bool(s.get("flushed")) for s in nstats),
         "wall_s": time.time() - t_begin, "kafka": f"fake://{name}",
     }
+    rss = [x["broker_rss_mb"] for x in samples if x["broker_rss_mb"] > 0]
+    out["broker_rss_mb"] = {"first": rss[0] if rss else None, "last": rss[-1] if rss else None,
+                            "max": max(rss) if rss else None}
+    out["timeline"] = {"samples": samples, "window_s": float(window_s or interval_s)}
     for tag, lp, o in zip(("ae", "lstm"), loops, outs):
         lat = lp.latency_records()
         ok = lat[:, 6] > 0
@@ -183,5 +252,6 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
                     "publish_to_result_max_us": float(us.max()) if len(us) else None,
                     "publish_to_fetched_p50_us": _pct(to_fetch, 50),
                     "fetched_to_result_p50_us": _pct(us - to_fetch, 50)}
+        out["timeline"][tag] = _windows(lat[ok, 6], us, float(window_s or interval_s), clients / interval_s)
     out["dropped"] = published - out["ae"]["scored"]
     return out

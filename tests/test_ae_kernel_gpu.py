@@ -186,11 +186,13 @@ def test_ring_cursor_and_graph_replay(cuda_device, xpack, monkeypatch):
 
 
 @pytest.mark.parametrize("D,n,blocks", [(18, 16 * 1000 + 5, 7), (18, 4096, 768), (30, 16 * 333, 5), (18, 40, 64)])
-def test_lds_dma_ring_matches_register_path(cuda_device, D, n, blocks):
+def test_lds_dma_ring_matches_register_path(cuda_device, monkeypatch, D, n, blocks):
     """The LDS-DMA input ring (contiguous rows) and the register-prefetch path
     (rows with a wider stride) run the same tile math in the same order: their
     gradient slabs must agree bit for bit, including ragged tails, waves with no
-    tiles and rings clamped past the last tile."""
+    tiles and rings clamped past the last tile.  (The one-tile ring loop: the direct
+    packed-pair loop is checked against it in test_direct_pair_loop_matches_one_tile_direct.)"""
+    monkeypatch.setenv("SML_AE_DIRECT_PAIRS", "0")
     spec = AESpec(input_dim=D)
     w = _weights(spec, seed=11)
     rng = np.random.default_rng(13)
@@ -254,6 +256,66 @@ def test_gradients_vs_bf16_rounded_reference(cuda_device, D, n):
         assert relerr(gf, gr) < 1e-3, i
     assert abs(metr[0] - sq) / sq < 1e-4
     assert abs(metr[1] - ab) / ab < 1e-4
+
+
+@pytest.mark.parametrize("ntiles,blocks", [(64 * 4, 16), (2 * 4096, 48), (30, 16), (2, 16), (64 * 2, 64)])
+def test_direct_pair_loop_matches_one_tile_direct(cuda_device, monkeypatch, ntiles, blocks):
+    """Rows trained once (the direct step, no tile-packed ring): the packed-pair loop on raw
+    rows -- normalize_fn and argmax(x) of BOTH tiles in registers (signed-key butterfly) --
+    against the one-tile direct loop (SML_AE_DIRECT_PAIRS=0), three steps on raw car-sensor
+    rows whose normalised values take both signs.  Same tiles per wave on the same grid: the
+    gradient image agrees to the packed MFMAs' K-order rounding, sq / |h1| / rows exactly as
+    before, the correct count up to argmax near-ties."""
+    from streamml.ops.ae import NPARAM
+    spec = AESpec()
+    w = _weights(spec, seed=9)
+    scale, shift = normalize_affine()
+    B = 16 * ntiles
+    rng = np.random.default_rng(23)
+    raw = torch.from_numpy((rng.uniform(-0.3, 1.2, size=(B, 18)) * 40).astype(np.float32)).to(cuda_device)
+    out = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("SML_AE_DIRECT_PAIRS", v)
+        f = FusedAE(spec, w, cuda_device, max_blocks=blocks, scale=scale, shift=shift)
+        imgs = []
+        for _ in range(3):
+            f.step(raw, allreduce=lambda g: imgs.append(g.detach().cpu().numpy().copy()))
+        torch.cuda.synchronize()
+        out[v] = (imgs, f.params.detach().cpu().numpy())
+    one, two = out["0"][0], out["1"][0]
+    for k in range(3):
+        np.testing.assert_allclose(two[k][NPARAM:NPARAM + 2], one[k][NPARAM:NPARAM + 2], rtol=1e-6)
+        assert abs(two[k][NPARAM + 2] - one[k][NPARAM + 2]) <= max(2, 1e-3 * B)
+        assert two[k][NPARAM + 3] == one[k][NPARAM + 3] == B
+        assert _relerr(two[k][:NPARAM], one[k][:NPARAM]) < 1e-6
+    assert _relerr(out["1"][1], out["0"][1]) < 1e-6
+
+
+def test_direct_pair_accuracy_vs_numpy_argmax(cuda_device, monkeypatch):
+    """argmax(x) of the direct pair loop (signed keys over normalised inputs of both signs)
+    against numpy on rows with a clear input argmax: the correct count matches exactly."""
+    monkeypatch.setenv("SML_AE_DIRECT_PAIRS", "1")
+    spec = AESpec()
+    w = _weights(spec, seed=21)
+    scale, shift = normalize_affine()
+    n = 16 * 64
+    rng = np.random.default_rng(31)
+    xn = rng.uniform(-1.5, 1.0, size=(n, 18)).astype(np.float32)
+    xn[:, [1, 8]] = -1.4     # zeroed / constant columns stay in the race as negatives
+    k = rng.integers(0, 18, n)
+    xn[np.arange(n), k] = 1.3 + rng.uniform(0, 0.5, n).astype(np.float32)   # clear winner per row
+    live = np.asarray(scale) != 0
+    raw = np.where(live, (xn - np.asarray(shift)) / np.where(live, scale, 1), 0).astype(np.float32)
+    fused = FusedAE(spec, w, cuda_device, max_blocks=16, scale=scale, shift=shift)
+    _, metr = fused.gradients(torch.from_numpy(raw).to(cuda_device))
+    xin = (raw * scale + shift).astype(np.float32)
+    y, _ = ae_forward_torch(torch.from_numpy(xin), [torch.from_numpy(a) for a in w], spec.activations)
+    y = y.numpy()
+    ys = np.sort(y, axis=1)
+    clear = (ys[:, -1] - ys[:, -2]) > 2e-2
+    ref = np.argmax(y, 1) == np.argmax(xin, 1)
+    assert abs(metr[2] - ref.sum()) <= (~clear).sum()
+    assert metr[3] == n
 
 
 @pytest.mark.parametrize("ilp", ["2", "3"])

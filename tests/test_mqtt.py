@@ -196,6 +196,43 @@ def test_bridge_to_kafka_keys_and_partitions():
     assert got == {t: i for i, t in enumerate(topics)}
 
 
+def test_bridge_batches_fit_message_max_bytes():
+    """A burst of ~600-byte car payloads to a one-partition topic (the auto-created default):
+    the bridge cuts each partition's share of a drained queue into record batches under the
+    broker's message.max.bytes (1 MB here, as Kafka's default) -- none refused, none dropped."""
+    from streamml.kafka import FakeBroker
+    kb = FakeBroker(message_max_bytes=1048588)
+    kb.create_topic("sensor-data", 1)
+    n = 6000
+    payload = b"x" * 600
+    with MqttBroker(kafka=kb.address) as b:
+        pub = _client(b, "burst")
+        for i in range(n):
+            pub.publish(f"vehicles/sensor/data/electric-vehicle-{i % 50:05d}", payload, qos=0)
+        assert b.flush(20.0)
+        st = b.stats()
+        assert st["kafka_failed"] == 0 and st["kafka_sent"] == n, st
+    assert kb.end_offset("sensor-data", 0) == n
+
+
+def test_broker_refuses_oversized_batches_client_splits():
+    """The in-process broker's message.max.bytes check (MESSAGE_TOO_LARGE, nothing appended),
+    and the client's record sets: one produce call of 1.8 MB goes out as several batches."""
+    from streamml.kafka import FakeBroker, KafkaClient
+    kb = FakeBroker(message_max_bytes=1048588)
+    kb.create_topic("t", 1)
+    c = KafkaClient(kb.address)
+    c.produce("t", 0, [b"v" * 600] * 3000)
+    assert kb.end_offset("t", 0) == 3000
+    small = FakeBroker(message_max_bytes=10_000)
+    small.create_topic("t", 1)
+    with pytest.raises(Exception, match="10"):
+        KafkaClient(small.address).produce("t", 0, [b"v" * 600] * 100)
+    assert small.end_offset("t", 0) == 0
+    kb.stop()
+    small.stop()
+
+
 # ---- simulator ---------------------------------------------------------------------
 def test_reference_scenarios_parse():
     full = Scenario.from_xml(_ref("test-generator/scenario.xml"))

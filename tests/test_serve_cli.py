@@ -78,6 +78,34 @@ def test_serve_replicas_score_every_event_once(tmp_path, capsys):
     assert again["events"] == 0
 
 
+def test_serve_eight_replicas_ten_partitions_balanced(tmp_path, capsys):
+    """BASELINE config 5 on the reference's topology (10 partitions) at 8 replicas: the key
+    shares give every car to exactly one replica, every event is scored once, and the
+    replicas' event counts are balanced (round-robin partitions would give 2:1)."""
+    from streamml.models.autoencoder import Autoencoder
+    model_file = tmp_path / "model1.h5"
+    Autoencoder(device="cpu", seed=3).save(str(model_file))
+    n, parts, W = 40000, 10, 8
+    common = ["synthetic://%d" % n, "SENSOR_SERVE8", "preds-serve8", "model1.h5", "--workdir", str(tmp_path),
+              "--device", "cpu", "--synthetic-partitions", str(parts), "--idle-timeout", "0.3", "--replicas", str(W)]
+    events = []
+    for r in range(W):
+        assert cli_main(["serve"] + common + ["--replica-index", str(r)]) == 0
+        s = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+        events.append(s["events"])
+        assert 1 <= len(s["partitions"]) <= 3
+    assert sum(events) == n
+    assert max(events) / min(events) <= 1.15, events
+    res = _read_topic("fake://synthetic-SENSOR_SERVE8", "preds-serve8", parts)
+    recs = [r for v in res.values() for r in v]
+    assert len(recs) == n and len({(r["partition"], r["offset"]) for r in recs}) == n
+    # a car's events come from one source partition -> ordered by offset in its result stream
+    by_car = {}
+    for r in recs:
+        by_car.setdefault(r["car"], set()).add(r["partition"])
+    assert all(len(v) == 1 for v in by_car.values())
+
+
 @pytest.mark.gpu
 def test_serve_on_gpu_matches_cpu_scores(tmp_path, capsys, cuda_device):
     from streamml.models.autoencoder import Autoencoder, load_model
