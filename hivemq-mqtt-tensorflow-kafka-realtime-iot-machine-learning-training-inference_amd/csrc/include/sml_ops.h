@@ -80,6 +80,12 @@ int lstm_fused_slabs(int64_t B, int U, bool dx);  // backward workgroups = weigh
 hipError_t lstm_fused_fwd_launch(const void* x, bool x_bf16, const float* W, const float* Uw, const float* b,
                                  const float* h0, const float* c0, void* hseq_bf16, void* cseq_bf16, int64_t B, int T,
                                  int IN, int U, int act, int64_t x_seq, hipStream_t stream);
+// two stacked layers in one forward (lstm_fused_fwd.hip): x fp32 [B, T, IN1] -> layer 1 (U1 32) ->
+// layer 2 (U2 16); saves both layers' h / c exactly as two lstm_fused_fwd_launch calls do
+bool lstm_fused_fwd2_supported(int IN1, int U1, int U2, int act1, int act2);
+hipError_t lstm_fused_fwd2_launch(const float* x, const float* W1, const float* U1, const float* b1, const float* W2,
+                                  const float* U2, const float* b2, void* hseq1, void* cseq1, void* hseq2, void* cseq2,
+                                  int64_t B, int T, int IN1, int act1, int act2, int64_t x_seq, hipStream_t stream);
 hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, const void* hseq_bf16, const void* x,
                                  bool x_bf16, const float* h0, const float* c0, const float* W, const float* Uw,
                                  const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,

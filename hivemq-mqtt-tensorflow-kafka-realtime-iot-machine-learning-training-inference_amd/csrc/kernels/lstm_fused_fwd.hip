@@ -172,9 +172,202 @@ hipError_t launch_fwd(const FusedFwdArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// Two stacked LSTM layers in ONE forward launch (the seq-50 two-layer stack of BASELINE
+// config 3: LSTM(32, relu, seq) -> LSTM(16, relu), LSTM-TensorFlow-IO-Kafka/cardata-v2.py:
+// 172-183 with look_back 50).  Each wave carries its 16 sequences through layer 1 AND layer 2
+// at every time step: layer 1's h_t leaves the step as the bf16 B operand of layer 2's x.W
+// MFMAs straight from registers -- the lane (c, g) holds units 16b + 4g + j of sequence c,
+// which IS the B layout of layer 2's K tile b -- so the second layer never re-reads layer 1's
+// h sequence from HBM (210 MB per 65 536-window step) and the two recurrences' dependency
+// chains interleave in one instruction stream (layer 2 alone issued 13 % of its cycles, 54 %
+// dependency stalls: profiles/r04/SUMMARY.md sec. 3).  Layer 1's h / c and layer 2's h / c are
+// still saved (bf16) for the backward, which recomputes the gates from them: every operand,
+// operand pairing and bias mode is the single-layer kernels', so the saved sequences are
+// bit-identical to two lstm_fused_fwd launches.
+struct FusedFwd2Args {
+  const float* x;                       // [B, T, IN1] fp32 (x_seq elements between sequences)
+  const float *W1, *U1, *b1, *W2, *U2, *b2;
+  __bf16 *hseq1, *cseq1, *hseq2, *cseq2;   // padded to whole 16-sequence waves
+  int64_t B;
+  int T, IN1, act1, act2;
+  int64_t x_seq;
+};
+
+template <int U, int KT, bool BX>
+__device__ __forceinline__ void load_layer_frags(const float* W, const float* Uw, const float* b, int IN, int c, int g,
+                                                 bf16x4 (&wt)[4 * U / 16][KT], bf16x4 (&ut)[4 * U / 16][U / 16],
+                                                 f32x4 (&bias)[4 * U / 16]) {
+  constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      f32x4 t4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 16 * kt + 4 * g + j;
+        t4[j] = BX ? wt_elem_bx(W, b, G4, IN, k, 16 * mt + c) : (k < IN ? W[(int64_t)k * G4 + 16 * mt + c] : 0.f);
+      }
+      wt[mt][kt] = pack4(t4);
+    }
+#pragma unroll
+    for (int s = 0; s < UB; ++s) {
+      f32x4 t4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t4[j] = Uw[(16 * s + 4 * g + j) * G4 + 16 * mt + c];
+      ut[mt][s] = pack4(t4);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[mt][i] = BX ? 0.f : b[16 * mt + 4 * g + i];
+  }
+}
+
+// z = b + [W ; U]^T . [x_t ; h_{t-1}]^T with the single-layer kernel's K-tile pairing
+template <int MT, int KT, int UB, bool BX>
+__device__ __forceinline__ void gate_preacts(const bf16x4 (&wt)[MT][KT], const bf16x4 (&ut)[MT][UB],
+                                             const f32x4 (&bias)[MT], const bf16x4 (&xb)[KT], const bf16x4 (&hb)[UB],
+                                             f32x4 (&z)[MT]) {
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    z[mt] = BX ? f32x4{0.f, 0.f, 0.f, 0.f} : bias[mt];
+    constexpr int NK = KT + UB;
+#pragma unroll
+    for (int k = 0; k + 1 < NK; k += 2)
+      z[mt] = mfma32(k < KT ? wt[mt][k] : ut[mt][k - KT], k + 1 < KT ? wt[mt][k + 1] : ut[mt][k + 1 - KT],
+                     k < KT ? xb[k] : hb[k - KT], k + 1 < KT ? xb[k + 1] : hb[k + 1 - KT], z[mt]);
+    if constexpr (NK & 1) z[mt] = mfma32(ut[mt][UB - 1], bf16x4{0, 0, 0, 0}, hb[UB - 1], bf16x4{0, 0, 0, 0}, z[mt]);
+  }
+}
+
+template <int U, int ACT>
+__device__ __forceinline__ void cell_update(const f32x4 (&z)[4 * U / 16], f32x4 (&h)[U / 16], f32x4 (&cs)[U / 16],
+                                            bf16x4 (&hb)[U / 16], __bf16* ht, __bf16* ct) {
+  constexpr int UB = U / 16;
+#pragma unroll
+  for (int b = 0; b < UB; ++b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float gi = sigmoid_fast(z[b][i]);
+      const float gf = sigmoid_fast(z[UB + b][i]);
+      const float gc = act_f(ACT, z[2 * UB + b][i]);
+      const float go = sigmoid_fast(z[3 * UB + b][i]);
+      cs[b][i] = fmaf(gf, cs[b][i], gi * gc);
+      h[b][i] = go * act_f(ACT, cs[b][i]);
+    }
+    hb[b] = pack4(h[b]);
+    *reinterpret_cast<bf16x4*>(ct + b * 256) = pack4(cs[b]);
+    *reinterpret_cast<bf16x4*>(ht + 16 * b) = hb[b];
+  }
+}
+
+template <int U1, int KT1, int XV, int ACT1, bool BX1, int U2, int ACT2, int PF = 2>
+__global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd2_kernel(FusedFwd2Args a) {
+  constexpr int MT1 = 4 * U1 / 16, UB1 = U1 / 16, MT2 = 4 * U2 / 16, UB2 = U2 / 16, KT2 = UB1;
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int64_t s0 = ((int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * 16;
+  if (s0 >= a.B) return;  // wave-uniform
+  const int64_t seq = s0 + c;
+  const int64_t sq = seq < a.B ? seq : a.B - 1;
+  const int IN1 = a.IN1, T = a.T;
+
+  bf16x4 wt1[MT1][KT1], ut1[MT1][UB1], wt2[MT2][KT2], ut2[MT2][UB2];
+  f32x4 bias1[MT1], bias2[MT2];
+  load_layer_frags<U1, KT1, BX1>(a.W1, a.U1, a.b1, IN1, c, g, wt1, ut1, bias1);
+  load_layer_frags<U2, KT2, false>(a.W2, a.U2, a.b2, U1, c, g, wt2, ut2, bias2);   // x = h1: no spare columns
+  bf16x4 onex[KT1];
+#pragma unroll
+  for (int kt = 0; kt < KT1; ++kt) onex[kt] = BX1 ? ones_at_bias(kt, g, IN1) : bf16x4{0, 0, 0, 0};
+  f32x4 h1[UB1], c1[UB1], h2[UB2], c2[UB2];
+  bf16x4 hb1[UB1], hb2[UB2];
+#pragma unroll
+  for (int b = 0; b < UB1; ++b) {
+    h1[b] = c1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    hb1[b] = bf16x4{0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int b = 0; b < UB2; ++b) {
+    h2[b] = c2[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    hb2[b] = bf16x4{0, 0, 0, 0};
+  }
+  const float* xrow = a.x + sq * a.x_seq;
+  auto load_x = [&](int t, f32x4* v) {
+    const float* p = xrow + (int64_t)t * IN1;
+#pragma unroll
+    for (int kt = 0; kt < KT1; ++kt) v[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN1);
+  };
+  const int64_t wv = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  SML_DCHECK(wv * 16 < a.B + 15 && seq < (a.B + 15) / 16 * 16);
+  __bf16* cw1 = a.cseq1 + wv * T * (int64_t)(UB1 * 256) + lane * 4;
+  __bf16* cw2 = a.cseq2 + wv * T * (int64_t)(UB2 * 256) + lane * 4;
+  f32x4 xr[PF][KT1];
+#pragma unroll
+  for (int p = 0; p < PF; ++p) load_x(p < T ? p : T - 1, xr[p]);
+  auto step = [&](int t, f32x4* xin) {
+    bf16x4 xb[KT1];
+#pragma unroll
+    for (int kt = 0; kt < KT1; ++kt) {
+      xb[kt] = row_operand(xin[kt], 16 * kt + 4 * g, IN1);
+      if constexpr (BX1) xb[kt] |= onex[kt];
+    }
+    load_x(t + PF < T ? t + PF : T - 1, xin);
+    f32x4 z1[MT1];
+    gate_preacts<MT1, KT1, UB1, BX1>(wt1, ut1, bias1, xb, hb1, z1);
+    cell_update<U1, ACT1>(z1, h1, c1, hb1, a.hseq1 + (seq * T + t) * (int64_t)U1 + 4 * g, cw1 + (int64_t)t * (UB1 * 256));
+    // layer 2: x_t = layer 1's h_t, already the B operand (hb1)
+    f32x4 z2[MT2];
+    gate_preacts<MT2, KT2, UB2, false>(wt2, ut2, bias2, hb1, hb2, z2);
+    cell_update<U2, ACT2>(z2, h2, c2, hb2, a.hseq2 + (seq * T + t) * (int64_t)U2 + 4 * g, cw2 + (int64_t)t * (UB2 * 256));
+  };
+  int t0 = 0;
+  for (; t0 + PF <= T; t0 += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) step(t0 + p, xr[p]);
+  }
+#pragma unroll
+  for (int p = 0; p < PF - 1; ++p)
+    if (t0 + p < T) step(t0 + p, xr[p]);
+}
+
+template <int XV>
+hipError_t launch_fwd2(const FusedFwd2Args& a, hipStream_t st) {
+  const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
+  const bool bx = bias_mode_fwd(a.IN1, 2) == BM_BX;
+  if (bias_mode_fwd(32, 2) == BM_BX) return hipErrorInvalidValue;   // layer 2 (IN 32) has no spare columns
+#define SML_F2(A1, A2, BXV)                                                                                  \
+  hipLaunchKernelGGL((lstm_fused_fwd2_kernel<32, 2, XV, A1, BXV, 16, A2>), dim3(grid), dim3(WAVES * 64), 0, st, a)
+  if (a.act1 == ACT_RELU && a.act2 == ACT_RELU) {
+    if (bx) SML_F2(ACT_RELU, ACT_RELU, true);
+    else SML_F2(ACT_RELU, ACT_RELU, false);
+  } else if (a.act1 == ACT_TANH && a.act2 == ACT_TANH) {
+    if (bx) SML_F2(ACT_TANH, ACT_TANH, true);
+    else SML_F2(ACT_TANH, ACT_TANH, false);
+  } else {
+    return hipErrorInvalidValue;   // mixed activations: two single-layer launches
+  }
+#undef SML_F2
+  return hipGetLastError();
+}
+
 }  // namespace
 
 namespace sml {
+
+bool lstm_fused_fwd2_supported(int IN1, int U1, int U2, int act1, int act2) {
+  return U1 == 32 && U2 == 16 && IN1 >= 1 && IN1 <= 32 && act1 == act2 && (act1 == ACT_RELU || act1 == ACT_TANH);
+}
+
+hipError_t lstm_fused_fwd2_launch(const float* x, const float* W1, const float* U1, const float* b1, const float* W2,
+                                  const float* U2, const float* b2, void* hseq1, void* cseq1, void* hseq2, void* cseq2,
+                                  int64_t B, int T, int IN1, int act1, int act2, int64_t x_seq, hipStream_t stream) {
+  FusedFwd2Args a{x, W1, U1, b1, W2, U2, b2, (__bf16*)hseq1, (__bf16*)cseq1, (__bf16*)hseq2, (__bf16*)cseq2,
+                  B, T, IN1, act1, act2, x_seq > 0 ? x_seq : (int64_t)T * IN1};
+  const int xv = row_vec(x, IN1, 4);
+  if (xv == 4) return launch_fwd2<4>(a, stream);
+  if (xv == 2) return launch_fwd2<2>(a, stream);
+  return launch_fwd2<1>(a, stream);
+}
+
 
 hipError_t lstm_fused_fwd_launch(const void* x, bool x_bf16, const float* W, const float* Uw, const float* b,
                                  const float* h0, const float* c0, void* hseq_bf16, void* cseq_bf16, int64_t B, int T,

@@ -675,6 +675,39 @@ std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W,
   return {h.narrow(0, 0, B), c};
 }
 
+// Two stacked fused LSTM layers in one forward launch -> [h1 [B,T,U1] bf16, c1 (padded, fragment
+// order), h2 [B,T,U2] bf16, c2] -- the same four tensors two lstm_fused_fwd calls return.
+std::vector<at::Tensor> lstm_fused_fwd2(const at::Tensor& x, const at::Tensor& W1, const at::Tensor& U1,
+                                        const at::Tensor& b1, const at::Tensor& W2, const at::Tensor& U2,
+                                        const at::Tensor& b2, int64_t act1, int64_t act2) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat, "x must be a float32 device tensor");
+  for (const auto* t : {&W1, &U1, &b1, &W2, &U2, &b2}) check_dev(*t, "weights", at::kFloat);
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1 && x.stride(1) == x.size(2) && x.stride(0) >= 0,
+              "x must be [B, T, IN] with consecutive rows per step (contiguous or sliding windows)");
+  const int64_t B = x.size(0), T = x.size(1), IN = x.size(2), Ua = U1.size(0), Ub = U2.size(0);
+  const int64_t x_seq = B > 1 ? x.stride(0) : T * IN;
+  TORCH_CHECK(W1.is_contiguous() && W1.size(0) == IN && W1.size(1) == 4 * Ua, "W1 must be [IN, 4U1]");
+  TORCH_CHECK(U1.is_contiguous() && U1.size(1) == 4 * Ua, "U1 must be [U1, 4U1]");
+  TORCH_CHECK(b1.is_contiguous() && b1.numel() == 4 * Ua, "b1 must be [4U1]");
+  TORCH_CHECK(W2.is_contiguous() && W2.size(0) == Ua && W2.size(1) == 4 * Ub, "W2 must be [U1, 4U2]");
+  TORCH_CHECK(U2.is_contiguous() && U2.size(1) == 4 * Ub, "U2 must be [U2, 4U2]");
+  TORCH_CHECK(b2.is_contiguous() && b2.numel() == 4 * Ub, "b2 must be [4U2]");
+  TORCH_CHECK(sml::lstm_fused_fwd2_supported((int)IN, (int)Ua, (int)Ub, (int)act1, (int)act2),
+              "fused two-layer LSTM forward: unsupported IN=", IN, " U1=", Ua, " U2=", Ub);
+  TORCH_CHECK(B >= 1 && T >= 1, "empty input");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t Bp = (B + 15) / 16 * 16;
+  auto bf = x.options().dtype(at::kBFloat16);
+  auto h1 = at::empty({Bp, T, Ua}, bf), c1 = at::empty({Bp, T, Ua}, bf);
+  auto h2 = at::empty({Bp, T, Ub}, bf), c2 = at::empty({Bp, T, Ub}, bf);
+  SML_CHECK_HIP(sml::lstm_fused_fwd2_launch(x.data_ptr<float>(), W1.data_ptr<float>(), U1.data_ptr<float>(),
+                                            b1.data_ptr<float>(), W2.data_ptr<float>(), U2.data_ptr<float>(),
+                                            b2.data_ptr<float>(), h1.data_ptr(), c1.data_ptr(), h2.data_ptr(),
+                                            c2.data_ptr(), B, (int)T, (int)IN, (int)act1, (int)act2, x_seq,
+                                            cur_stream(x)));
+  return {h1.narrow(0, 0, B), c1, h2.narrow(0, 0, B), c2};
+}
+
 // Fully fused LSTM layer backward -> [dx (x's dtype, or undefined), dW [IN,4U], dU [U,4U],
 // db [4U], dh0, dc0].  dh: bf16 [B, T, U], or [B, U] (h_T only) when dh_last_only.
 std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& cseq, const at::Tensor& hseq,
@@ -1235,6 +1268,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("IN"));
   m.def("dense_supported", &sml::dense_supported, "whether (K, N) fits the register-resident tile", py::arg("K"),
         py::arg("N"));
+  m.def("lstm_fused_fwd2", &lstm_fused_fwd2, "two stacked fused LSTM layers (U 32 -> 16) in one forward launch",
+        py::arg("x"), py::arg("W1"), py::arg("U1"), py::arg("b1"), py::arg("W2"), py::arg("U2"), py::arg("b2"),
+        py::arg("act1"), py::arg("act2"));
+  m.def("lstm_fused_fwd2_supported", &sml::lstm_fused_fwd2_supported);
   m.def("lstm_fused_fwd", &lstm_fused_fwd, "fully fused LSTM layer forward (x.W + recurrence in one kernel)",
         py::arg("x"), py::arg("W"), py::arg("U"), py::arg("b"), py::arg("h0") = py::none(),
         py::arg("c0") = py::none(), py::arg("act") = 1);

@@ -57,6 +57,13 @@ def _glorot(fi: int, fo: int, rng) -> np.ndarray:
 
 _FOLD = os.environ.get("SML_LSTM_FOLD", "1") != "0"
 
+
+def _fwd2() -> bool:
+    """SML_LSTM_FWD2=0: two single-layer forward launches instead of the stacked one (A/B;
+    read per step)."""
+    return os.environ.get("SML_LSTM_FWD2", "1") != "0"
+
+
 class LSTMPredictor:
     def __init__(self, look_back: int = 1, features: int = 18, stack=None, device="auto", seed: int = 0,
                  name: str = "sequential", lr: float = 1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
@@ -249,7 +256,20 @@ class LSTMPredictor:
         pre, post, R = plan["pre"], plan["post"], plan["repeat"]
         saved = []
         h = x
-        for L in pre + post:
+        stack = pre + post
+        first = 0
+        if _fwd2() and len(pre) >= 2 and x.dtype == torch.float32:
+            # the first two layers (U 32 -> 16) in ONE forward launch: layer 1's h feeds layer 2
+            # from registers (lstm_fused_fwd.hip fwd2); the same saved h / c as two launches
+            L1, L2 = pre[0], pre[1]
+            W1, U1, b1 = (t.detach() for t in P[L1["params"]:L1["params"] + 3])
+            W2, U2, b2 = (t.detach() for t in P[L2["params"]:L2["params"] + 3])
+            a1, a2 = ACT[L1["activation"]], ACT[L2["activation"]]
+            if C.lstm_fused_fwd2_supported(x.shape[2], U1.shape[0], U2.shape[0], a1, a2):
+                hs1, c1, hs2, c2 = C.lstm_fused_fwd2(x, W1, U1, b1, W2, U2, b2, a1, a2)
+                saved += [(x, hs1, c1), (hs1, hs2, c2)]
+                h, first = hs2, 2
+        for L in stack[first:]:
             if L is (post[0] if post else None):   # RepeatVector: h_T broadcast over R steps
                 # fp32 (exact widening of the bf16 h_T), as the autograd path feeds it: the
                 # decoder's dx then comes back fp32 and is summed before one bf16 rounding

@@ -231,6 +231,53 @@ def test_fused_lstm_vs_bf16_rounded_reference(cuda_device, u, act, B, T, inp, la
         assert relerr(d.cpu(), r) < 1e-3, name
 
 
+@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("B,T,windows", [(1000 + 7, 50, True), (64, 3, False), (16 * 4 * 5 + 1, 9, True)])
+def test_stacked_forward_equals_two_launches(cuda_device, act, B, T, windows):
+    """lstm_fused_fwd2 (two layers U 32 -> 16 in one launch, layer 1's h fed to layer 2 from
+    registers) saves exactly what two lstm_fused_fwd launches save: h1, c1, h2, c2 bit for bit
+    -- the backward recomputes the gates from them, so nothing downstream changes."""
+    from streamml.data.stream import sliding_windows
+    from streamml.ops import load_c
+    C = load_c()
+    rng = np.random.default_rng(B + T)
+    if windows:   # in-place sliding windows over base rows, as the seq-50 bench feeds them
+        base = torch.tensor(rng.uniform(-1, 1, (B + T, 18)), dtype=torch.float32, device=cuda_device)
+        x, _ = sliding_windows(base, T)
+        x = x[:B]
+    else:
+        x = torch.tensor(rng.uniform(-1, 1, (B, T, 18)), dtype=torch.float32, device=cuda_device)
+
+    def w(*shape, s=0.25):
+        return torch.tensor(rng.standard_normal(shape) * s, dtype=torch.float32, device=cuda_device)
+    W1, U1, b1 = w(18, 128), w(32, 128), w(128, s=0.1)
+    W2, U2, b2 = w(32, 64), w(16, 64), w(64, s=0.1)
+    assert C.lstm_fused_fwd2_supported(18, 32, 16, act, act)
+    h1, c1, h2, c2 = C.lstm_fused_fwd2(x, W1, U1, b1, W2, U2, b2, act, act)
+    r1, rc1 = C.lstm_fused_fwd(x, W1, U1, b1, None, None, act)
+    r2, rc2 = C.lstm_fused_fwd(r1, W2, U2, b2, None, None, act)
+    torch.cuda.synchronize()
+    for got, want in ((h1, r1), (c1, rc1), (h2, r2), (c2, rc2)):
+        assert got.shape == want.shape
+        torch.testing.assert_close(got.view(torch.int16), want.view(torch.int16), rtol=0, atol=0)
+
+
+def test_fused_step_stacked_forward_matches_two_launches(cuda_device, monkeypatch):
+    """The seq-50 two-layer train step with the stacked forward (default) and with two
+    single-layer launches (SML_LSTM_FWD2=0): identical losses, parameters and Adam state."""
+    from streamml.data.stream import sliding_windows
+    rows = torch.tensor(np.random.default_rng(4).uniform(-1, 1, (2000, 18)), dtype=torch.float32, device=cuda_device)
+    X, Y = sliding_windows(rows, 50)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SML_LSTM_FWD2", v)
+        m = LSTMPredictor.two_layer(look_back=50, device=cuda_device, seed=2)
+        losses = [float(m.train_step(X[i * 512:(i + 1) * 512], Y[i * 512:(i + 1) * 512])[0]) for i in range(3)]
+        out[v] = (losses, m.fp.flat.detach().cpu().clone(), m.fp.m.detach().cpu().clone())
+    assert out["1"][0] == out["0"][0]
+    assert torch.equal(out["1"][1], out["0"][1]) and torch.equal(out["1"][2], out["0"][2])
+
+
 @pytest.mark.parametrize("u,inp,need_dx", [(32, 18, False), (16, 32, True)])
 def test_fused_lstm_persistent_tile_loop_vs_bf16_reference(cuda_device, u, inp, need_dx):
     """B large enough that every workgroup of the persistent backward grid (CUs x 1-2
