@@ -175,6 +175,39 @@ def measure_lstm_infer(device, n_events: int, repeats: int = 3, qps: float = 100
             "path": "persistent one-wave forecaster (lstm_serve.hip), host-mapped request ring"}
 
 
+def measure_lstm_seq50_infer(device, n_events: int, repeats: int = 3, qps: float = 10000.0, nkeys: int = 100,
+                             seq_len: int = 50):
+    """Per-event forecast latency of the BASELINE config-3 model served per event: the
+    two-layer stack LSTM(32) -> LSTM(16) -> Dense(18) at look_back 50 in the persistent
+    forecaster (lstm_serve.hip) -- each event appended to its car's 50-event window on the
+    device, the whole stack run over the window from zero state (Keras' stateless predict,
+    cardata-v2.py:220-273 with look_back 50), the forecast and the score back on the host.
+    Every key's window is filled before the timed runs (seq_len events per key)."""
+    import numpy as np
+
+    from streamml.data.cardata import synthetic_device_tensor
+    from streamml.models.lstm import LSTMPredictor
+    from streamml.ops.serve import LSTMScoringServer
+
+    warm = seq_len * nkeys + 1000
+    ev = synthetic_device_tensor(n_events + warm, device, seed=9).cpu().numpy()
+    keys = np.arange(n_events + warm) % nkeys
+    model = LSTMPredictor.two_layer(look_back=seq_len, device=device)
+    runs = []
+    with LSTMScoringServer(model, nkeys=nkeys) as srv:
+        srv.latency_us(ev[:warm], keys[:warm], qps=0)          # fill every key's window
+        for _ in range(repeats):
+            host, done, comp = srv.latency_us(ev[warm:], keys[warm:], qps=qps, device_breakdown=True)
+            runs.append({"p50_us": float(np.percentile(host, 50)), "p99_us": float(np.percentile(host, 99)),
+                         "device_p50_us": float(np.percentile(done, 50)),
+                         "device_compute_p50_us": float(np.percentile(comp, 50))})
+    p50s = [r["p50_us"] for r in runs]
+    return {"p50_us": float(np.median(p50s)), "p99_us": max(r["p99_us"] for r in runs),
+            "p50_spread_us": [min(p50s), max(p50s)], "runs": runs, "events_per_run": n_events, "offered_qps": qps,
+            "keys": nkeys, "seq_len": seq_len, "model": "two-layer LSTM(32)->LSTM(16)->Dense(18), look_back 50",
+            "path": "persistent forecaster (lstm_serve.hip): per-key 50-event device window, full stack per event"}
+
+
 def measure_kafka_e2e(model, device, n_events: int, qps: float = 10000.0):
     """Kafka append -> scored result record acknowledged, through ``serve --low-latency``
     (bench/bench_infer.py:kafka_e2e): p50/p99 and the per-stage breakdown."""
@@ -689,6 +722,10 @@ def main():
                                 device, args.infer_events, args.infer_repeats, args.qps)
             out.update({"lstm_infer_p50_us": lstm_infer.get("p50_us"), "lstm_infer_p99_us": lstm_infer.get("p99_us"),
                         "lstm_infer": lstm_infer})
+            s50 = ph.run("lstm_seq50_infer", 10 + 3e-4 * args.infer_events * args.infer_repeats,
+                         measure_lstm_seq50_infer, device, args.infer_events, args.infer_repeats, args.qps)
+            out.update({"lstm_seq50_infer_p50_us": s50.get("p50_us"), "lstm_seq50_infer_p99_us": s50.get("p99_us"),
+                        "lstm_seq50_infer": s50})
     # the reference's scale axis: 100 000 MQTT cars at 1 msg / 10 s -> broker nodes + Kafka
     # bridge -> Kafka -> the persistent AE scorer and the per-car LSTM forecaster
     if args.mqtt_clients > 0:

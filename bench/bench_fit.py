@@ -132,9 +132,10 @@ def stream_e2e(device, rows: int = 2_000_000, batch: int = 100, partitions: int 
     return out
 
 
-def _fill_topic(b, topic, rows, partitions, failure_rate=0.01, distinct=1_000_000):
+def _fill_topic(b, topic, rows, partitions, failure_rate=0.01, distinct=1_000_000, staged=None):
     """Append ``rows`` Confluent-framed Avro events round-robin over ``partitions`` (up to
-    ``distinct`` encoded once, then re-appended)."""
+    ``distinct`` encoded once, then re-appended).  ``staged`` (a list): receives the encoded
+    (buffer, offsets, count) chunks -- the same values, pre-staged in memory."""
     from streamml.data import stream as S
     from streamml.data.avro import AvroCodec
     from streamml.data.produce import encode_chunk
@@ -143,6 +144,8 @@ def _fill_topic(b, topic, rows, partitions, failure_rate=0.01, distinct=1_000_00
     chunk = min(rows, 250_000)
     encoded = [encode_chunk(codec, c.x, c.label) + (len(c.x),)
                for c in S.synthetic(min(rows, distinct), chunk=chunk, seed=0, failure_rate=failure_rate)]
+    if staged is not None:
+        staged.extend(encoded)
     left, i, nbytes = rows, 0, 0
     while left > 0:
         buf, offs, k = encoded[i % len(encoded)]
@@ -192,15 +195,34 @@ def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, bat
     from streamml.kafka import fake_broker
     from streamml.models.autoencoder import Autoencoder
 
+    import numpy as np
+
     name = f"bench-large-{rows}-{partitions}-{time.time_ns()}"
     b = fake_broker(name)
     topic = "SENSOR_DATA_S_AVRO"
     t0 = time.perf_counter()
-    nbytes = _fill_topic(b, topic, rows, partitions)
+    staged = []
+    nbytes = _fill_topic(b, topic, rows, partitions, staged=staged)
+    quota = _cpu_quota()
     out = {"rows": rows, "partitions": partitions, "batch": batch, "log_bytes": nbytes,
            "bytes_per_row": nbytes / rows, "produce_s": time.perf_counter() - t0,
-           "cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_quota": _cpu_quota()}
+           "cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_quota": quota}
     specs = [f"{topic}:{p}:0" for p in range(partitions)]
+    # 1. the decoder alone: the same Avro values pre-staged in memory (as a fetch response holds
+    #    them), decoded by W threads into private slabs -- no broker, no socket, no ring
+    sizes = [int(s[1][s[2]]) for s in staged]
+    buf = np.concatenate([np.frombuffer(s[0], np.uint8)[:n] for s, n in zip(staged, sizes)])
+    bases = np.cumsum([0] + sizes[:-1])
+    offs = np.concatenate([np.zeros(1, np.int64)] + [np.asarray(s[1][1:s[2] + 1], np.int64) + int(base)
+                                                    for s, base in zip(staged, bases)])
+    probe = S.kafka(f"fake://{name}", specs[:1], native=True).native_feed
+    dcurve = []
+    for w in tuple(workers) + ((32,) if 32 not in workers else ()):
+        r, _ = probe.decode_only(buf, offs, int(w), repeats=2, keep_label=0)
+        dcurve.append({"workers": int(w), "rows_per_s": r})
+    out["decode_only_curve"] = dcurve
+    out["decode_only_rows"] = int(len(offs) - 1)
+    # 2. fetch + decode from the broker (its connection threads share this process's CPUs)
     curve = []
     for w in workers:
         src = S.kafka(f"fake://{name}", specs, max_bytes=8 << 20, workers=int(w), native=True)
@@ -225,9 +247,25 @@ def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, bat
     torch.cuda.synchronize()
     dt = time.perf_counter() - t1
     kept = int(h.history["_rows"][-1]) if "_rows" in h.history else None
+    st = src.native_feed.last_stats
     out.update({"train_workers": tw, "rows_per_s": rows / dt, "trained_rows_per_s": (kept or 0) / dt,
                 "kept_rows": kept, "engine": m.last_fit_engine, "loss": h.history["loss"][-1],
-                "h2d_gb_per_s": src.native_feed.last_stats.get("h2d_bytes", 0) / dt / 1e9})
+                "h2d_gb_per_s": st.get("h2d_bytes", 0) / dt / 1e9,
+                "train_stage_s": {"wall": dt, "fetch_sum": st.get("fetch_s"), "decode_sum": st.get("decode_s"),
+                                  "wait_slab_sum": st.get("wait_slab_s")}})
+    # what caps the curve: the decoder alone against the fetch + decode path, within the CPUs
+    # this job may keep busy (the feed workers, the broker's connection threads and the
+    # training loop all draw on that one quota)
+    dbest = max(dcurve, key=lambda c: c["rows_per_s"])
+    per_worker = dcurve[0]["rows_per_s"]
+    out["cap"] = {
+        "decode_only_best": dbest, "fetch_decode_best": best,
+        "decode_per_worker_rows_per_s": per_worker,
+        "quota_cpus": quota,
+        "decode_rows_per_s_at_quota": per_worker * quota if quota else None,
+        "resource": ("CPU quota" if quota and dbest["workers"] <= quota * 1.5 else "decoder scaling"),
+        "note": "fetch + decode needs ~2 CPUs per worker (decode thread + the broker's connection thread); "
+                "the decode-only curve shows the decoder's own scaling on the same CPUs"}
     return out
 
 

@@ -250,6 +250,37 @@ int Feed::decode_fast(const uint8_t* p, size_t n, float* out_row, uint8_t* label
   return p == e ? 1 : -1;
 }
 
+double Feed::decode_throughput(const uint8_t* buf, const int64_t* offs, int64_t n, int workers, int repeats,
+                               int64_t* rows_out) const {
+  if (workers < 1 || n < 1) throw std::invalid_argument("decode_throughput: workers >= 1, n >= 1");
+  const int F = features();
+  double best = 0.0;
+  for (int r = 0; r < repeats; ++r) {
+    std::vector<int64_t> kept((size_t)workers, 0);
+    std::vector<std::thread> th;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int w = 0; w < workers; ++w)
+      th.emplace_back([&, w] {
+        const int64_t a = n * w / workers, b = n * (w + 1) / workers;
+        std::vector<float> slab((size_t)(b - a + 1) * (size_t)F);   // the worker's own slab, written row by row
+        int64_t k = 0;
+        uint8_t lab = 0;
+        for (int64_t i = a; i < b; ++i)
+          if (decode_row(buf + offs[i], (size_t)(offs[i + 1] - offs[i]), slab.data() + (size_t)k * F, &lab) &&
+              (cfg_.keep_label < 0 || lab == cfg_.keep_label))
+            ++k;
+        kept[(size_t)w] = k;
+      });
+    for (auto& t : th) t.join();
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    int64_t tot = 0;
+    for (int64_t k : kept) tot += k;
+    if (rows_out) *rows_out = tot;
+    best = std::max(best, (double)n / dt);
+  }
+  return best;
+}
+
 bool Feed::decode_row(const uint8_t* p, size_t n, float* out_row, uint8_t* label) const {
   if (fast_ && decode_fast(p, n, out_row, label) == 1) return true;
   const uint8_t* e = p + n;

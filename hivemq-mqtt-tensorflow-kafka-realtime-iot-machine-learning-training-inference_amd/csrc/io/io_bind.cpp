@@ -692,6 +692,22 @@ PYBIND11_MODULE(_io, m) {
              py::gil_scoped_release rel;
              f.stop();
            })
+      .def("decode_throughput",   // pre-staged values -> (best rows/s, rows kept per pass); no broker
+           [](const feed::Feed& f, py::buffer buf, py::array_t<int64_t, py::array::c_style | py::array::forcecast> offs,
+              int workers, int repeats) {
+             py::buffer_info bi = buf.request();
+             const int64_t n = (int64_t)offs.size() - 1;
+             if (n < 1 || offs.at(n) > (int64_t)bi.size * (int64_t)bi.itemsize)
+               throw std::invalid_argument("decode_throughput: offsets past the buffer");
+             int64_t rows = 0;
+             double r;
+             {
+               py::gil_scoped_release rel;
+               r = f.decode_throughput(static_cast<const uint8_t*>(bi.ptr), offs.data(), n, workers, repeats, &rows);
+             }
+             return py::make_tuple(r, rows);
+           },
+           py::arg("buf"), py::arg("offsets"), py::arg("workers"), py::arg("repeats") = 3)
       .def("decode_row",   // one framed Avro value -> (ok, projected row, label code); tests / debugging
            [](const feed::Feed& f, const py::bytes& value) {
              const std::string v = value;
