@@ -86,6 +86,14 @@ bool lstm_fused_fwd2_supported(int IN1, int U1, int U2, int act1, int act2);
 hipError_t lstm_fused_fwd2_launch(const float* x, const float* W1, const float* U1, const float* b1, const float* W2,
                                   const float* U2, const float* b2, void* hseq1, void* cseq1, void* hseq2, void* cseq2,
                                   int64_t B, int T, int IN1, int act1, int act2, int64_t x_seq, hipStream_t stream);
+// two stacked layers' backward in one launch (lstm_fused_stack.hip): layer 2's dX feeds layer 1's
+// dh in registers; one slab per workgroup per layer (partials1 [grid, S1], partials2 [grid, S2])
+bool lstm_fused_bwd2_supported(int IN1, int U1, int U2, int act1, int act2);
+int lstm_fused_bwd2_grid(int64_t B);
+hipError_t lstm_fused_bwd2_launch(const float* x, int64_t x_seq, int IN1, const void* h1, const void* c1, const void* h2,
+                                  const void* c2, const void* dh2, int dh2_last_only, const float* W1, const float* U1,
+                                  const float* b1, const float* W2, const float* U2, const float* b2, float* partials1,
+                                  float* partials2, int64_t B, int T, int act, hipStream_t stream);
 hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, const void* hseq_bf16, const void* x,
                                  bool x_bf16, const float* h0, const float* c0, const float* W, const float* Uw,
                                  const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,

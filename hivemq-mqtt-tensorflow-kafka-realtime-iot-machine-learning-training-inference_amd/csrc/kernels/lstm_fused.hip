@@ -87,7 +87,8 @@ struct FusedBwdArgs {
 // RF: weight A fragments kept in registers for the whole launch instead of re-read from
 // LDS every step (bits: 1 the recurrent U fragments of the dh chain, 2 the gate
 // recompute's [W^T | U^T], 4 the dX fragments W) -- where the registers exist, see launch_bwd.
-template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0, int BM = BM_PLAIN>
+// PFD: operand prefetch distance of the one-step loop (steps in flight ahead of the one computing).
+template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0, int BM = BM_PLAIN, int PFD = 1>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdArgs a) {
   constexpr bool BX = BM == BM_BX, DB = BM != BM_PLAIN;   // bias in the MFMAs / db from the dW^T column
   using XR = typename RowRaw<XT>::type;
@@ -478,6 +479,24 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) tdz[0][mt] = pack4(zero4);
       wgrad2();
+    } else if constexpr (PFD == 2) {
+      // two steps in flight: the U = 16 layer with dX at two waves per SIMD does ~1 us of work per
+      // step, less than an HBM round trip under load -- with one step ahead its waves sat in
+      // s_waitcnt 53 % of their cycles (profiles/r05/lstm)
+      Step n2 = nxt;
+      if (T >= 2) load_any(T - 2, n2);
+      for (; t >= 3; --t) {
+        const Step cur = nxt;
+        nxt = n2;
+        load_step(t - 2, n2);
+        step(t, cur, std::integral_constant<int, 0>{});
+      }
+      for (; t >= 0; --t) {
+        const Step cur = nxt;
+        nxt = n2;
+        if (t >= 2) load_any(t - 2, n2);
+        step(t, cur, std::integral_constant<int, 0>{});
+      }
     } else {
       for (; t >= 2; --t) {   // one step per trip, no t = 0 branch in the body
         const Step cur = nxt;
@@ -555,16 +574,30 @@ hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
   // reads were exposed latency there (SQ_WAIT_ANY 41 % of wave cycles) and the kernel
   // runs 17 % faster (bench_lstm 62.3 -> 68.1 M windows/s, profiles/r02).  With dX, at
   // two waves per SIMD, register fragments measured the same as LDS reads (67.8 vs 67.9).
+  static const int pf_env = [] {   // SML_LSTM_BWD_PF=1|2|3: the U = 16 dX build's prefetch (A/B)
+    const char* e = std::getenv("SML_LSTM_BWD_PF");
+    return e ? std::atoi(e) : 0;
+  }();
   auto go = [&](auto dx, auto rf, auto bmc) {
     constexpr bool DX = decltype(dx)::value;
     constexpr int RF = decltype(rf)::value;
     constexpr int BM = decltype(bmc)::value;
-    if (a.act == ACT_RELU)
-      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF, BM>), dim3(grid), dim3(WAVES * 64), 0,
-                         st, a);
-    else
-      hipLaunchKernelGGL((lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF, BM>), dim3(grid), dim3(WAVES * 64), 0,
-                         st, a);
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVES * 64), 0, st, a); };
+    if constexpr (U == 16 && DX) {
+      if (pf_env == 1) {   // one step ahead, every fragment set in registers
+        if (a.act == ACT_RELU) launch(lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, 7, BM, 1>);
+        else launch(lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, 7, BM, 1>);
+        return;
+      }
+      if (pf_env == 3) {   // two steps ahead, every fragment set in registers
+        if (a.act == ACT_RELU) launch(lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, 7, BM, 2>);
+        else launch(lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, 7, BM, 2>);
+        return;
+      }
+    }
+    constexpr int PFD = (U == 16 && DX) ? 2 : 1;
+    if (a.act == ACT_RELU) launch(lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF, BM, PFD>);
+    else launch(lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF, BM, PFD>);
   };
   auto with_bm = [&](auto dx, auto rf) {   // the same decision as the forward (lstm_fused_fwd.hip)
     switch (bias_mode(a.IN, KT)) {
@@ -576,7 +609,7 @@ hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
   // U = 16 with dX (layer 2 of the stack): every fragment set fits in registers at two waves
   // per SIMD (174 VGPRs + 64 AGPRs); U = 32 with dX reads them from LDS every step
   if (a.dx) {
-    if constexpr (U == 16) with_bm(std::true_type{}, std::integral_constant<int, 7>{});
+    if constexpr (U == 16) with_bm(std::true_type{}, std::integral_constant<int, 3>{});   // two steps ahead
     else with_bm(std::true_type{}, std::integral_constant<int, 0>{});
   } else {
     with_bm(std::false_type{}, std::integral_constant<int, 3>{});

@@ -779,6 +779,64 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
   return {dx, dW, dU, db, dh0, dc0};
 }
 
+// Backward of two stacked fused LSTM layers (U 32 -> 16) in one launch.  Layer 1's x (fp32
+// model input), its saved h / c, layer 2's saved h / c and layer 2's incoming dh (bf16, [B, 16]
+// when dh2_last_only).  With grad + map1 + map2 the two weight-gradient slabs are reduced
+// straight into the flat gradient; otherwise returns [dW1, dU1, db1, dW2, dU2, db2].
+std::vector<at::Tensor> lstm_fused_bwd2(const at::Tensor& x, const at::Tensor& h1, const at::Tensor& c1,
+                                        const at::Tensor& h2, const at::Tensor& c2, const at::Tensor& dh2,
+                                        const at::Tensor& W1, const at::Tensor& U1, const at::Tensor& b1,
+                                        const at::Tensor& W2, const at::Tensor& U2, const at::Tensor& b2, int64_t act,
+                                        bool dh2_last_only, const c10::optional<at::Tensor>& grad,
+                                        const c10::optional<at::Tensor>& map1, const c10::optional<at::Tensor>& map2) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat, "x must be a float32 device tensor");
+  for (const auto* t : {&h1, &c1, &h2, &c2, &dh2}) check_dev(*t, "saved state", at::kBFloat16);
+  for (const auto* t : {&W1, &U1, &b1, &W2, &U2, &b2}) check_dev(*t, "weights", at::kFloat);
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1 && x.stride(1) == x.size(2) && x.stride(0) >= 0,
+              "x must be [B, T, IN] with consecutive rows per step (contiguous or sliding windows)");
+  const int64_t B = x.size(0), T = x.size(1), IN = x.size(2);
+  const int64_t x_seq = B > 1 ? x.stride(0) : T * IN, Bp = (B + 15) / 16 * 16;
+  TORCH_CHECK(h1.is_contiguous() && h1.size(0) == B && h1.size(1) == T && h1.size(2) == 32, "h1 must be [B, T, 32]");
+  TORCH_CHECK(h2.is_contiguous() && h2.size(0) == B && h2.size(1) == T && h2.size(2) == 16, "h2 must be [B, T, 16]");
+  TORCH_CHECK(c1.is_contiguous() && c1.size(0) == Bp && c1.size(2) == 32 && c2.is_contiguous() && c2.size(0) == Bp &&
+                  c2.size(2) == 16, "c1 / c2 must be the padded buffers the forward returned");
+  TORCH_CHECK(dh2.is_contiguous() && (dh2_last_only ? (dh2.dim() == 2 && dh2.size(0) == B && dh2.size(1) == 16)
+                                                    : dh2.sizes() == h2.sizes()), "dh2 shape mismatch");
+  TORCH_CHECK(W1.size(0) == IN && W1.size(1) == 128 && U1.size(0) == 32 && W2.size(0) == 32 && W2.size(1) == 64 &&
+                  U2.size(0) == 16 && b1.numel() == 128 && b2.numel() == 64, "weight shape mismatch");
+  TORCH_CHECK(sml::lstm_fused_bwd2_supported((int)IN, 32, 16, (int)act, (int)act), "stacked LSTM backward: unsupported");
+  c10::hip::HIPGuard guard(x.device().index());
+  auto opts = x.options().dtype(at::kFloat);
+  const int S1 = sml::lstm_fused_slab(32, (int)IN), S2 = sml::lstm_fused_slab(16, 32);
+  const int G = sml::lstm_fused_bwd2_grid(B);
+  TORCH_CHECK(map1.has_value() == map2.has_value(), "map1 and map2 go together");
+  const int* mp1 = grad_map(grad, map1, S1);
+  const int* mp2 = grad.has_value() ? grad_map(grad, map2, S2) : nullptr;
+  auto p1 = at::empty({G, S1}, opts), p2 = at::empty({G, S2}, opts);
+  auto o1 = mp1 ? *grad : at::empty({S1}, opts);
+  auto o2 = mp2 ? *grad : at::empty({S2}, opts);
+  auto scratch = at::empty({std::max(1, std::max(sml::slab_sum_scratch(G, S1), sml::slab_sum_scratch(G, S2)))}, opts);
+  auto st = cur_stream(x);
+  SML_CHECK_HIP(sml::lstm_fused_bwd2_launch(x.data_ptr<float>(), x_seq, (int)IN, h1.data_ptr(), c1.data_ptr(),
+                                            h2.data_ptr(), c2.data_ptr(), dh2.data_ptr(), dh2_last_only ? 1 : 0,
+                                            W1.data_ptr<float>(), U1.data_ptr<float>(), b1.data_ptr<float>(),
+                                            W2.data_ptr<float>(), U2.data_ptr<float>(), b2.data_ptr<float>(),
+                                            p1.data_ptr<float>(), p2.data_ptr<float>(), B, (int)T, (int)act, st));
+  SML_CHECK_HIP(sml::slab_sum_launch(p1.data_ptr<float>(), G, S1, scratch.data_ptr<float>(), o1.data_ptr<float>(), st,
+                                     mp1));
+  SML_CHECK_HIP(sml::slab_sum_launch(p2.data_ptr<float>(), G, S2, scratch.data_ptr<float>(), o2.data_ptr<float>(), st,
+                                     mp2));
+  if (mp1) return {};
+  auto unpack = [&](const at::Tensor& o, int64_t U, int64_t in, int S) {
+    const int64_t G4 = 4 * U, LDW = (S / G4) - U - 1;
+    return std::vector<at::Tensor>{o.narrow(0, 0, G4 * LDW).view({G4, LDW}).narrow(1, 0, in).t().contiguous(),
+                                   o.narrow(0, G4 * LDW, G4 * U).view({G4, U}).t().contiguous(),
+                                   o.narrow(0, G4 * LDW + G4 * U, G4)};
+  };
+  auto a1 = unpack(o1, 32, IN, S1), a2 = unpack(o2, 16, 32, S2);
+  return {a1[0], a1[1], a1[2], a2[0], a2[1], a2[2]};
+}
+
 // ---- MNIST MLP layers (mlp.hip) ----
 static void check_x_mlp(const at::Tensor& x) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1 &&
@@ -1272,6 +1330,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("W1"), py::arg("U1"), py::arg("b1"), py::arg("W2"), py::arg("U2"), py::arg("b2"),
         py::arg("act1"), py::arg("act2"));
   m.def("lstm_fused_fwd2_supported", &sml::lstm_fused_fwd2_supported);
+  m.def("lstm_fused_bwd2", &lstm_fused_bwd2, "two stacked fused LSTM layers' backward (U 32 -> 16) in one launch",
+        py::arg("x"), py::arg("h1"), py::arg("c1"), py::arg("h2"), py::arg("c2"), py::arg("dh2"), py::arg("W1"),
+        py::arg("U1"), py::arg("b1"), py::arg("W2"), py::arg("U2"), py::arg("b2"), py::arg("act"),
+        py::arg("dh2_last_only"), py::arg("grad") = py::none(), py::arg("map1") = py::none(),
+        py::arg("map2") = py::none());
+  m.def("lstm_fused_bwd2_supported", &sml::lstm_fused_bwd2_supported);
   m.def("lstm_fused_fwd", &lstm_fused_fwd, "fully fused LSTM layer forward (x.W + recurrence in one kernel)",
         py::arg("x"), py::arg("W"), py::arg("U"), py::arg("b"), py::arg("h0") = py::none(),
         py::arg("c0") = py::none(), py::arg("act") = 1);

@@ -64,6 +64,15 @@ def _fwd2() -> bool:
     return os.environ.get("SML_LSTM_FWD2", "1") != "0"
 
 
+def _bwd2() -> bool:
+    """SML_LSTM_BWD2=1: the bottom two layers' backward in ONE launch (lstm_fused_stack.hip)
+    instead of two (read per step).  Off by default: correct (bit-identical to two launches
+    up to fp32 summation order) but slower on MI355X -- one wave per SIMD carries both
+    layers' dependency chains, 501 us vs 243 + 236 us for the two launches at the seq-50
+    config, 88.8 vs 91.7 M windows/s (profiles/r05/lstm/ab_r05g_bwd2.txt)."""
+    return os.environ.get("SML_LSTM_BWD2", "0") == "1"
+
+
 class LSTMPredictor:
     def __init__(self, look_back: int = 1, features: int = 18, stack=None, device="auto", seed: int = 0,
                  name: str = "sequential", lr: float = 1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
@@ -302,6 +311,18 @@ class LSTMPredictor:
             last_only = i == len(pre) - 1
             if R and i >= len(pre):
                 dh = dh.view(n, R, -1)
+            if i == 1 and _bwd2() and saved[0][0].dtype == torch.float32:
+                # the bottom two layers' backward in ONE launch (lstm_fused_stack.hip): layer 2's
+                # dX reaches layer 1 in registers, h1 is read once
+                L0 = layers[0]
+                W0, U0, b0 = (t.detach() for t in P[L0["params"]:L0["params"] + 3])
+                x0, hs0, c0 = saved[0]
+                a0, a1 = ACT[L0["activation"]], ACT[L["activation"]]
+                if C.lstm_fused_bwd2_supported(x0.shape[2], U0.shape[0], Uw.shape[0], a0, a1) and \
+                        dh.dim() == (2 if last_only else 3):
+                    C.lstm_fused_bwd2(x0, hs0, c0, hs, c, dh, W0, U0, b0, W, Uw, b, a0, last_only, grad,
+                                      plan["maps"][0], plan["maps"][1])
+                    break
             out = C.lstm_fused_bwd(dh, c, hs, xin, None, None, W, Uw, b, ACT[L["activation"]], i > 0, False,
                                    last_only, grad, plan["maps"][i])
             dh = out[0]

@@ -125,12 +125,15 @@ def test_graph_replayed_train_steps_match_eager(cuda_device):
 
 @pytest.mark.parametrize("stack,B,T", [("two_layer", 256, 20), ("two_layer", 100, 7), ("two_layer", 33, 50),
                                        ("reference", 64, 1), ("reference", 100, 4)])
-def test_fused_step_matches_autograd_step(cuda_device, stack, B, T):
+def test_fused_step_matches_autograd_step(cuda_device, monkeypatch, stack, B, T):
     """LSTMPredictor._fused_step (explicit kernel calls, weight-gradient slabs scattered
     straight into the flat gradient, dh_T = dy . K^T from the transposed-weight K1; for the
     reference stack also RepeatVector as a broadcast copy and TimeDistributed Dense over the
     repeated steps) gives the same gradients, Adam updates and losses as the autograd step
-    over the same kernels, on in-place sliding windows."""
+    over the same kernels, on in-place sliding windows.  (Per-layer backward launches, as the
+    autograd path runs them; the stacked backward is checked against them in
+    test_stacked_backward_vs_two_launches.)"""
+    monkeypatch.setenv("SML_LSTM_BWD2", "0")
     from streamml.data.stream import sliding_windows
     rows = torch.tensor(np.random.default_rng(B + T).uniform(-1, 1, (3 * B + T, 18)), dtype=torch.float32,
                         device=cuda_device)
@@ -260,6 +263,60 @@ def test_stacked_forward_equals_two_launches(cuda_device, act, B, T, windows):
     for got, want in ((h1, r1), (c1, rc1), (h2, r2), (c2, rc2)):
         assert got.shape == want.shape
         torch.testing.assert_close(got.view(torch.int16), want.view(torch.int16), rtol=0, atol=0)
+
+
+def _relerr_t(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("B,T,tiles", [(1000 + 7, 50, 1), (64, 5, 1), (0, 4, 2)])
+def test_stacked_backward_vs_two_launches(cuda_device, act, B, T, tiles):
+    """lstm_fused_bwd2 (both layers' BPTT in one launch, layer 2's dX handed to layer 1 in
+    registers) against the two single-layer backward launches on the same saved state: every
+    weight gradient to summation-order rounding (the launches' workgroups own other tiles).
+    B = 0 here means 64 x CUs + 37: every workgroup of the persistent grid takes 2 tiles."""
+    from streamml.data.stream import sliding_windows
+    from streamml.ops import load_c
+    C = load_c()
+    if B == 0:
+        B = 64 * torch.cuda.get_device_properties(cuda_device).multi_processor_count * tiles + 37
+    rng = np.random.default_rng(B + T + act)
+    base = torch.tensor(rng.uniform(-1, 1, (B + T, 18)), dtype=torch.float32, device=cuda_device)
+    x, _ = sliding_windows(base, T)
+    x = x[:B]
+
+    def w(*shape, s=0.25):
+        return torch.tensor(rng.standard_normal(shape) * s, dtype=torch.float32, device=cuda_device)
+    W1, U1, b1 = w(18, 128), w(32, 128), w(128, s=0.1)
+    W2, U2, b2 = w(32, 64), w(16, 64), w(64, s=0.1)
+    h1, c1, h2, c2 = C.lstm_fused_fwd2(x, W1, U1, b1, W2, U2, b2, act, act)
+    dh2 = torch.tensor(rng.standard_normal((B, 16)), dtype=torch.float32, device=cuda_device).to(torch.bfloat16)
+    assert C.lstm_fused_bwd2_supported(18, 32, 16, act, act)
+    got = C.lstm_fused_bwd2(x, h1, c1, h2, c2, dh2, W1, U1, b1, W2, U2, b2, act, True)
+    dx2, dW2, dU2, db2, _, _ = C.lstm_fused_bwd(dh2, c2, h2, h1, None, None, W2, U2, b2, act, True, False, True)
+    _, dW1, dU1, db1, _, _ = C.lstm_fused_bwd(dx2, c1, h1, x, None, None, W1, U1, b1, act, False, False, False)
+    torch.cuda.synchronize()
+    for name, g, r in zip(("dW1", "dU1", "db1", "dW2", "dU2", "db2"), got, (dW1, dU1, db1, dW2, dU2, db2)):
+        assert g.shape == r.shape, name
+        assert _relerr_t(g, r) < 2e-5, (name, _relerr_t(g, r))
+
+
+def test_fused_step_stacked_backward_close_to_two_launches(cuda_device, monkeypatch):
+    """The seq-50 train step with the stacked backward (SML_LSTM_BWD2=1) vs two backward
+    launches (the default): the same losses to fp32 summation order over 5 steps."""
+    from streamml.data.stream import sliding_windows
+    rows = torch.tensor(np.random.default_rng(5).uniform(-1, 1, (3000, 18)), dtype=torch.float32, device=cuda_device)
+    X, Y = sliding_windows(rows, 50)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SML_LSTM_BWD2", v)
+        m = LSTMPredictor.two_layer(look_back=50, device=cuda_device, seed=2)
+        losses = [float(m.train_step(X[i * 512:(i + 1) * 512], Y[i * 512:(i + 1) * 512])[0]) for i in range(5)]
+        out[v] = (np.array(losses), m.fp.flat.detach().cpu().double())
+    np.testing.assert_allclose(out["1"][0], out["0"][0], rtol=1e-5)
+    assert _relerr_t(out["1"][1], out["0"][1]) < 1e-3   # Adam: near-zero gradients may flip sign
 
 
 def test_fused_step_stacked_forward_matches_two_launches(cuda_device, monkeypatch):

@@ -209,6 +209,9 @@ def test_bridge_batches_fit_message_max_bytes():
         pub = _client(b, "burst")
         for i in range(n):
             pub.publish(f"vehicles/sensor/data/electric-vehicle-{i % 50:05d}", payload, qos=0)
+        deadline = time.time() + 20.0   # QoS 0: flush() covers what the broker has received so far
+        while b.stats()["incoming_publish"] < n and time.time() < deadline:
+            time.sleep(0.01)
         assert b.flush(20.0)
         st = b.stats()
         assert st["kafka_failed"] == 0 and st["kafka_sent"] == n, st
