@@ -110,6 +110,7 @@ hipError_t dispatch(int U, int IN, int xv, bool x_bf16, F&& f) {
   }
   SML_UK(16, 1) SML_UK(16, 2) SML_UK(16, 4)
   SML_UK(32, 1) SML_UK(32, 2)
+  SML_UK(64, 1) SML_UK(64, 2)
 #undef SML_UK
   return hipErrorInvalidValue;
 }

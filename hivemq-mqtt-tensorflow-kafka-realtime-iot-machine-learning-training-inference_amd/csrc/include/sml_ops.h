@@ -75,6 +75,7 @@ bool lstm_fused_supported(int U, int IN);
 int lstm_fused_slab(int U, int IN);
 int lstm_fused_dx_ld(int IN);     // row stride of the padded dx buffer the backward kernel writes
 int lstm_fused_waves(int64_t B);
+int64_t lstm_fused_dz_bytes(int64_t B, int T, int U);   // dz scratch of the backward (U >= 64 layers), else 0
 int lstm_fused_slabs(int64_t B, int U, bool dx);  // backward workgroups = weight-gradient slabs (persistent grid)
 // x: fp32 or bf16 (x_bf16); h and dh are bf16 (lstm_fused.hip header), dx has x's dtype
 hipError_t lstm_fused_fwd_launch(const void* x, bool x_bf16, const float* W, const float* Uw, const float* b,
@@ -97,7 +98,8 @@ hipError_t lstm_fused_bwd2_launch(const float* x, int64_t x_seq, int IN1, const 
 hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, const void* hseq_bf16, const void* x,
                                  bool x_bf16, const float* h0, const float* c0, const float* W, const float* Uw,
                                  const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,
-                                 int IN, int U, int act, int dh_last_only, int64_t x_seq, hipStream_t stream);
+                                 int IN, int U, int act, int dh_last_only, int64_t x_seq, void* dz_scratch,
+                                 hipStream_t stream);
 
 // tile-packed training ring: per 16-row tile the normalised rows (x * scale + shift, 64*D
 // bytes) then their 16 argmax bytes; out holds n/16 * (64*D + 16) bytes (n % 16 == 0).

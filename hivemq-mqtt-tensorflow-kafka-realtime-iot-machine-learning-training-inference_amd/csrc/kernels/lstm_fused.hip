@@ -75,6 +75,8 @@ struct FusedBwdArgs {
   int T, IN, act;
   int dh_last_only;    // return_sequences=False: only h_T received a gradient (no [B, T, U] zeros read)
   int64_t x_seq;       // elements between consecutive sequences of x (T*IN contiguous, IN sliding windows)
+  __bf16* dzs;         // U >= 64 (DZS): dz_t stored fragment-native [B/16, T, 4U/16, 64, 4] bf16 for
+                       // lstm_dz_wgrad_kernel (the weight gradients do not fit one wave's registers)
 };
 
 // BM: bias mode (lstm_fused_impl.h bias_mode).  BX: the x operand carries constant 1.0
@@ -95,9 +97,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
   constexpr int LDW = 16 * KT;
   constexpr int S = G4 * (LDW + U + 1);
+  // DZS (U >= 64): dW^T | dU^T alone would take 4U x (16 KT + U) / 64 >= 320 accumulator registers per
+  // lane, more than a wave has -- this kernel runs the recurrence, dh, dX and (PLAIN) db and stores dz_t
+  // (bf16, the precision dW / dU consume anyway); lstm_dz_wgrad_kernel contracts it, split over gate groups
+  constexpr bool DZS = U >= 64;
   constexpr int NTR = MT + KT + UB;                 // LDS transposes per step: dz tiles, x tiles, h tiles
-  __shared__ __attribute__((aligned(16))) char scratch[WAVES][NTR * 512];
-  __shared__ __attribute__((aligned(16))) float slab[S];   // the workgroup's combined weight-gradient slab
+  __shared__ __attribute__((aligned(16))) char scratch[WAVES][DZS ? 16 : NTR * 512];
+  __shared__ __attribute__((aligned(16))) float slab[DZS ? (BM == BM_PLAIN ? G4 : 1) : S];   // the workgroup's combined weight-gradient slab
   // Weight A fragments, shared by the 4 waves, [tile][lane] bf16x4 (conflict-free
   // ds_read_b64).  RF selects which stay in registers for the launch; the rest are read
   // in the loop through an opaque lane offset so the compiler cannot hoist them (all
@@ -124,7 +130,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   bool any_active = false;
   const int IN = a.IN, T = a.T;
   char* scr = scratch[w];
-  for (int i = threadIdx.x; i < S; i += WAVES * 64) slab[i] = 0.f;
+  for (int i = threadIdx.x; i < (DZS ? (BM == BM_PLAIN ? G4 : 1) : S); i += WAVES * 64) slab[i] = 0.f;
   for (int i = threadIdx.x; i < G4; i += WAVES * 64) sbias[i] = a.bias[i];
   // tile (mt, k) of [W^T | U^T]: k < KT -> W^T[m = gate 16mt + c][feature 16k + 4g + j],
   //                              k >= KT -> U^T[m = gate][unit 16(k-KT) + 4g + j]
@@ -178,16 +184,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
     for (int i = 0; i < KT * MT; ++i) rfx[i] = wfl[i * 64 + lane];
   }
-  f32x4 accW[MT][KT], accU[MT][UB];
+  constexpr int MA = DZS ? 1 : MT;   // weight-gradient accumulator rows (none held under DZS)
+  f32x4 accW[MA][KT], accU[MA][UB];
   f32x4 accb[MT];   // db in exact fp32: per lane (sequence c) over time, folded across lanes at the end
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
+  for (int mt = 0; mt < MA; ++mt) {
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) accW[mt][kt] = zero4;
 #pragma unroll
     for (int kb = 0; kb < UB; ++kb) accU[mt][kb] = zero4;
-    accb[mt] = zero4;
   }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) accb[mt] = zero4;
   f32x4 dhr[UB], dcn[UB];
 #pragma unroll
   for (int b = 0; b < UB; ++b) dhr[b] = dcn[b] = zero4;
@@ -207,6 +215,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     XR xt[KT];         // x_t[sequence c][feature 16kt + 4g + j]
   };
   const __bf16* cw = a.cseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
+  __bf16* dzw = DZS ? a.dzs + wave_id * T * (int64_t)(MT * 256) + lane * 4 : nullptr;
   // Loads are unconditional from in-bounds addresses (padding lanes read row B-1),
   // with zeros selected afterwards: no exec-masked branches and no waits in the loop.
   auto load_common = [&](int t, Step& st) {   // raw values; masks are applied in step()
@@ -258,6 +267,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
   for (int s = 0; s < UB; ++s) phb[s] = pack4(zero4);
   auto wgrad = [&]() {
+    if constexpr (DZS) return;
+    else {
     bf16x4 hB[UB], xB[KT];
 #pragma unroll
     for (int kb = 0; kb < UB; ++kb) hB[kb] = lds_transpose(phb[kb], scr + (MT + KT + kb) * 512, c, g);
@@ -271,6 +282,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
       for (int kb = 0; kb < UB; ++kb) accU[mt][kb] = mfma16(adz, hB[kb], accU[mt][kb]);
     }
+    }
   };
   // Pair loop (layer 1: register fragments, db column, no dX): each step transposes its own
   // operands right after its dh chain (slot 0: the trip's first step, slot 1: the second)
@@ -278,7 +290,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   // one 16x16x32 per accumulator tile, so every accumulator is written once per trip (with
   // one 16x16x16 per step the allocator rotated them through spare AGPRs: 96
   // v_accvgpr_mov per step).
-  constexpr bool PAIR = RF != 0 && DB && !DX && XV != 1;   // (scalar-row x: the pair loop spilled)
+  constexpr bool PAIR = RF != 0 && DB && !DX && XV != 1 && !DZS;   // (scalar-row x: the pair loop spilled)
   bf16x4 tdz[2][PAIR ? MT : 1], txb[2][PAIR ? KT : 1], thb[2][PAIR ? UB : 1];
   if constexpr (PAIR) {
 #pragma unroll
@@ -293,7 +305,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   }
   auto wgrad2 = [&]() {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+    for (int mt = 0; mt < (PAIR ? MT : 0); ++mt) {
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) accW[mt][kt] = mfma32(tdz[0][mt], tdz[1][mt], txb[0][kt], txb[1][kt], accW[mt][kt]);
 #pragma unroll
@@ -378,6 +390,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       dzb[mt] = pack4(dzt[mt]);
       if constexpr (!DB) accb[mt] += dzt[mt];
     }
+    if constexpr (DZS) {   // one contiguous 512-byte store per gate tile (padding lanes store dz = 0)
+      __bf16* dzp = dzw + (int64_t)t * (MT * 256);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<bf16x4*>(dzp + mt * 256) = dzb[mt];
+    }
     // critical path: recurrent gradient for step t-1 -- the 4U gate tiles in pairs on
     // 16x16x32 (MT/2 dependent MFMAs, half the issues of two 16x16x16 half-chains)
 #pragma unroll
@@ -438,6 +455,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   valid = seq < a.B;
   sq = valid ? seq : a.B - 1;
   cw = a.cseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
+  if constexpr (DZS) dzw = a.dzs + wave_id * T * (int64_t)(MT * 256) + lane * 4;
   any_active |= active;
   // fresh recurrence and weight-gradient pipeline per tile (the accumulators carry on)
 #pragma unroll
@@ -531,6 +549,23 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
       for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
       accb[mt][i] = v;
     }
+  if constexpr (DZS) {   // only db (PLAIN), into the slab's db row; lstm_dz_wgrad_kernel writes the rest
+    if constexpr (!DB) {
+      for (int turn = 0; turn < WAVES; ++turn) {
+        __syncthreads();
+        if (turn == w && any_active && c == 0) {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) slab[16 * mt + 4 * g + i] += accb[mt][i];
+        }
+      }
+      __syncthreads();
+      float* out = a.partials + (int64_t)blockIdx.x * S + G4 * LDW + G4 * U;
+      for (int i = threadIdx.x; i < G4; i += WAVES * 64) out[i] = slab[i];
+    }
+    return;
+  } else {
   // the 4 waves add their accumulators into the workgroup slab in LDS in a fixed
   // order (deterministic), then the workgroup writes ONE slab (4x fewer bytes for
   // the slab reduction than a slab per wave).  C layout: row m = gate 16mt + 4g + i,
@@ -562,6 +597,113 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   }
   float* out = a.partials + (int64_t)blockIdx.x * S;
   for (int i = threadIdx.x; i < S; i += WAVES * 64) out[i] = slab[i];
+  }
+}
+
+// Weight gradients of a DZS layer (U >= 64) from the stored dz: workgroup (x, y) takes the
+// 16-sequence tiles of the persistent grid's workgroup x (the same tiles, so slab x gets the
+// same rows) and the gate rows of group y (MG gate tiles), and contracts over its sequences and
+// the T steps exactly as the fused kernel's wgrad(): dz_t^T as A operand, x_t (with the bias
+// columns of BX / DB) and h_{t-1} as B operands, each through one LDS transpose.  MG = 8: 8 x
+// (KT + U/16) accumulator tiles = 192 AGPRs at U = 64, KT = 2.  Writes the group's rows of
+// dW^T, dU^T and (BX / DB) db of slab x; PLAIN db comes from the recurrence kernel (fp32 dz).
+template <int U, int KT, int XV, typename XT, int BM, int MG>
+__global__ __launch_bounds__(WAVES * 64, 1) void lstm_dz_wgrad_kernel(FusedBwdArgs a) {
+  constexpr bool DB = BM != BM_PLAIN;
+  using XR = typename RowRaw<XT>::type;
+  constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16, LDW = 16 * KT;
+  constexpr int S = G4 * (LDW + U + 1);
+  constexpr int RW = 16 * MG;                       // gate rows of this group
+  __shared__ __attribute__((aligned(16))) char scratch[WAVES][(MG + KT + UB) * 512];
+  __shared__ __attribute__((aligned(16))) float slab[RW * (LDW + U)];
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int w = threadIdx.x >> 6;
+  const int mt0 = blockIdx.y * MG;
+  const int IN = a.IN, T = a.T;
+  char* scr = scratch[w];
+  for (int i = threadIdx.x; i < RW * (LDW + U); i += WAVES * 64) slab[i] = 0.f;
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 accW[MG][KT], accU[MG][UB];
+#pragma unroll
+  for (int m = 0; m < MG; ++m) {
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) accW[m][kt] = zero4;
+#pragma unroll
+    for (int kb = 0; kb < UB; ++kb) accU[m][kb] = zero4;
+  }
+  bf16x4 onex[KT];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) onex[kt] = DB ? ones_at_bias(kt, g, IN) : bf16x4{0, 0, 0, 0};
+  const int64_t nblk = (a.B + 16 * WAVES - 1) / (16 * WAVES);
+  bool any_active = false;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t wave_id = blk * WAVES + w;
+    const int64_t s0 = wave_id * 16;
+    if (s0 >= a.B) continue;   // wave-uniform; no block barrier inside the tile loop
+    any_active = true;
+    const int64_t seq = s0 + c;
+    const bool valid = seq < a.B;
+    const int64_t sq = valid ? seq : a.B - 1;
+    const __bf16* dzw = a.dzs + wave_id * T * (int64_t)(MT * 256) + lane * 4 + mt0 * 256;
+    const XT* xrow = static_cast<const XT*>(a.x) + sq * a.x_seq;
+    for (int t = 0; t < T; ++t) {
+      bf16x4 dz[MG], hb[UB], xb[KT];
+#pragma unroll
+      for (int m = 0; m < MG; ++m) dz[m] = ld_bf16x4(dzw + (int64_t)t * (MT * 256) + m * 256);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const XR raw = load_row4<XV>(xrow + (int64_t)t * IN, 16 * kt + 4 * g, IN);
+        xb[kt] = row_operand(raw, 16 * kt + 4 * g, IN);
+        if constexpr (DB) xb[kt] |= onex[kt];
+      }
+#pragma unroll
+      for (int b = 0; b < UB; ++b) {
+        const int off = 16 * b + 4 * g;
+        if (t > 0) hb[b] = ld_bf16x4(a.hseq + (sq * T + t - 1) * (int64_t)U + off);
+        else hb[b] = pack4(a.h0 ? *reinterpret_cast<const f32x4*>(a.h0 + sq * U + off) : zero4);
+      }
+      // padding lanes carry dz = 0 (the recurrence kernel's invariant): their rows add nothing
+      bf16x4 hB[UB], xB[KT];
+#pragma unroll
+      for (int kb = 0; kb < UB; ++kb) hB[kb] = lds_transpose(hb[kb], scr + (MG + KT + kb) * 512, c, g);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) xB[kt] = lds_transpose(xb[kt], scr + (MG + kt) * 512, c, g);
+#pragma unroll
+      for (int m = 0; m < MG; ++m) {
+        const bf16x4 adz = lds_transpose(dz[m], scr + m * 512, c, g);
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) accW[m][kt] = mfma16(adz, xB[kt], accW[m][kt]);
+#pragma unroll
+        for (int kb = 0; kb < UB; ++kb) accU[m][kb] = mfma16(adz, hB[kb], accU[m][kb]);
+      }
+    }
+  }
+  for (int turn = 0; turn < WAVES; ++turn) {   // fixed-order combine of the 4 waves (deterministic)
+    __syncthreads();
+    if (turn == w && any_active) {
+#pragma unroll
+      for (int m = 0; m < MG; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * m + 4 * g + i;
+#pragma unroll
+          for (int kt = 0; kt < KT; ++kt) slab[r * LDW + 16 * kt + c] += accW[m][kt][i];
+#pragma unroll
+          for (int kb = 0; kb < UB; ++kb) slab[RW * LDW + r * U + 16 * kb + c] += accU[m][kb][i];
+        }
+    }
+  }
+  __syncthreads();
+  float* out = a.partials + (int64_t)blockIdx.x * S;
+  const int r0 = 16 * mt0;
+  for (int i = threadIdx.x; i < RW * LDW; i += WAVES * 64) {
+    const int r = i / LDW, col = i % LDW;
+    float v = slab[i];
+    if (DB && col == IN) out[G4 * LDW + G4 * U + r0 + r] = v;   // db = column IN (a constant-1 input)
+    if (DB && (col == IN || col == IN + 1)) v = 0.f;
+    out[(r0 + r) * LDW + col] = v;
+  }
+  for (int i = threadIdx.x; i < RW * U; i += WAVES * 64) out[G4 * LDW + r0 * U + i] = slab[RW * LDW + i];
 }
 
 // activation as a template parameter: a runtime switch became ~40 scalar branches
@@ -606,15 +748,28 @@ hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
       default: go(dx, rf, std::integral_constant<int, BM_PLAIN>{});
     }
   };
-  // U = 16 with dX (layer 2 of the stack): every fragment set fits in registers at two waves
-  // per SIMD (174 VGPRs + 64 AGPRs); U = 32 with dX reads them from LDS every step
-  if (a.dx) {
-    if constexpr (U == 16) with_bm(std::true_type{}, std::integral_constant<int, 3>{});   // two steps ahead
-    else with_bm(std::true_type{}, std::integral_constant<int, 0>{});
+  if constexpr (U >= 64) {   // DZS: fragments from LDS, then the gate-group weight-gradient kernel
+    if (a.dx) with_bm(std::true_type{}, std::integral_constant<int, 0>{});
+    else with_bm(std::false_type{}, std::integral_constant<int, 0>{});
+    constexpr int MG = 8;
+    const dim3 wg(grid, (4 * U / 16) / MG);
+    switch (bias_mode(a.IN, KT)) {
+      case BM_BX: hipLaunchKernelGGL((lstm_dz_wgrad_kernel<U, KT, XV, XT, BM_BX, MG>), wg, dim3(WAVES * 64), 0, st, a); break;
+      case BM_DB: hipLaunchKernelGGL((lstm_dz_wgrad_kernel<U, KT, XV, XT, BM_DB, MG>), wg, dim3(WAVES * 64), 0, st, a); break;
+      default: hipLaunchKernelGGL((lstm_dz_wgrad_kernel<U, KT, XV, XT, BM_PLAIN, MG>), wg, dim3(WAVES * 64), 0, st, a);
+    }
+    return hipGetLastError();
   } else {
-    with_bm(std::false_type{}, std::integral_constant<int, 3>{});
+    // U = 16 with dX (layer 2 of the stack): every fragment set fits in registers at two waves
+    // per SIMD (174 VGPRs + 64 AGPRs); U = 32 with dX reads them from LDS every step
+    if (a.dx) {
+      if constexpr (U == 16) with_bm(std::true_type{}, std::integral_constant<int, 3>{});   // two steps ahead
+      else with_bm(std::true_type{}, std::integral_constant<int, 0>{});
+    } else {
+      with_bm(std::false_type{}, std::integral_constant<int, 3>{});
+    }
+    return hipGetLastError();
   }
-  return hipGetLastError();
 }
 
 }  // namespace
@@ -623,9 +778,9 @@ namespace sml {
 
 bool lstm_fused_supported(int U, int IN) {
   const int KT = (IN + 15) / 16;
-  // larger (U, IN) would spill the backward kernel's weight-gradient accumulators
-  // (U = 64 layers use the unfused recurrence + K1/K2 path)
-  return IN >= 1 && (U == 16 ? KT <= 4 : (U == 32 ? KT <= 2 : false));
+  // U = 64 (DZS): dz stored, weight gradients by lstm_dz_wgrad_kernel; larger U / IN use the
+  // unfused recurrence + K1/K2 path
+  return IN >= 1 && (U == 16 ? KT <= 4 : (U == 32 || U == 64 ? KT <= 2 : false));
 }
 
 int lstm_fused_slab(int U, int IN) {
@@ -639,6 +794,10 @@ int lstm_fused_dx_ld(int IN) {
   return 16 * (KT <= 1 ? 1 : (KT <= 2 ? 2 : 4));
 }
 
+int64_t lstm_fused_dz_bytes(int64_t B, int T, int U) {   // DZS layers: [B/16 padded, T, 4U] bf16
+  return U >= 64 ? (B + 15) / 16 * 16 * (int64_t)T * 4 * U * 2 : 0;
+}
+
 int lstm_fused_waves(int64_t B) { return (int)(((B + 16 * WAVES - 1) / (16 * WAVES)) * WAVES); }
 int lstm_fused_slabs(int64_t B, int U, bool dx) {
   const int64_t nblk = (B + 16 * WAVES - 1) / (16 * WAVES);
@@ -650,7 +809,7 @@ int lstm_fused_slabs(int64_t B, int U, bool dx) {
   }();
   // resident workgroups per CU: the U = 32 layer without dX runs one wave per SIMD (register
   // fragments next to the AGPR accumulators), the other builds two
-  const int64_t per_cu = (U == 32 && !dx) ? 1 : 2;
+  const int64_t per_cu = ((U == 32 && !dx) || U >= 64) ? 1 : 2;
   static const bool persist = [] {   // SML_LSTM_PERSIST=0: one tile group per workgroup (A/B)
     const char* e = std::getenv("SML_LSTM_PERSIST");
     return !(e && e[0] == '0');
@@ -661,9 +820,12 @@ int lstm_fused_slabs(int64_t B, int U, bool dx) {
 hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, const void* hseq_bf16, const void* x,
                                  bool x_bf16, const float* h0, const float* c0, const float* W, const float* Uw,
                                  const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,
-                                 int IN, int U, int act, int dh_last_only, int64_t x_seq, hipStream_t stream) {
+                                 int IN, int U, int act, int dh_last_only, int64_t x_seq, void* dz_scratch,
+                                 hipStream_t stream) {
+  if (U >= 64 && dz_scratch == nullptr) return hipErrorInvalidValue;   // lstm_fused_dz_bytes
   FusedBwdArgs a{(const __bf16*)dh_bf16, (const __bf16*)cseq_bf16, (const __bf16*)hseq_bf16, x, h0, c0, W, Uw, b, dx,
-                 dh0, dc0, partials, B, T, IN, act, dh_last_only, x_seq > 0 ? x_seq : (int64_t)T * IN};
+                 dh0, dc0, partials, B, T, IN, act, dh_last_only, x_seq > 0 ? x_seq : (int64_t)T * IN,
+                 (__bf16*)dz_scratch};
   return dispatch(U, IN, row_vec(x, IN, x_bf16 ? 2 : 4), x_bf16, [&](auto u, auto k, auto v, auto xt) {
     using XT = std::remove_const_t<std::remove_pointer_t<decltype(xt)>>;
     return launch_bwd<decltype(u)::value, decltype(k)::value, decltype(v)::value, XT>(a, stream);

@@ -756,13 +756,15 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
   auto partials = at::empty({G, S}, opts);   // every workgroup writes its slab (idle waves add nothing)
   auto out = mp ? *grad : at::empty({S}, opts);
   auto scratch = at::empty({std::max(1, sml::slab_sum_scratch(G, S))}, opts);
+  const int64_t dzb = sml::lstm_fused_dz_bytes(B, (int)T, (int)U);   // U >= 64: dz for the gate-group wgrad
+  at::Tensor dzs = dzb > 0 ? at::empty({dzb / 2}, x.options().dtype(at::kBFloat16)) : at::Tensor();
   auto st = cur_stream(x);
   SML_CHECK_HIP(sml::lstm_fused_bwd_launch(
       dh.data_ptr(), cseq.data_ptr(), hseq.data_ptr(), x.data_ptr(), x.scalar_type() == at::kBFloat16, opt_ptr(h0),
       opt_ptr(c0), W.data_ptr<float>(), Uw.data_ptr<float>(), b.data_ptr<float>(),
       want_dx ? dx_pad.data_ptr() : nullptr, want_state_grads ? dh0.data_ptr<float>() : nullptr,
       want_state_grads ? dc0.data_ptr<float>() : nullptr, partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U,
-      (int)act, dh_last_only ? 1 : 0, x_seq, st));
+      (int)act, dh_last_only ? 1 : 0, x_seq, dzb > 0 ? dzs.data_ptr() : nullptr, st));
   SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
                                      out.data_ptr<float>(), st, mp));
   const int64_t G4 = 4 * U, LDW = (S / G4) - U - 1;

@@ -2,7 +2,10 @@
 
 Default path (:class:`FusedLSTMFunction`, ``csrc/kernels/lstm_fused.hip``): one
 kernel for the forward pass (input projection, recurrence, bf16 gate save) and one
-for the backward pass (BPTT, weight gradients accumulated in registers, dX).
+for the backward pass (BPTT, weight gradients accumulated in registers, dX).  U = 64
+layers keep the one-launch forward; their backward stores dz (bf16) and a second
+hand-written kernel (``lstm_dz_wgrad_kernel``, split over gate groups) contracts it,
+since 4U x (16 KT + U) weight-gradient accumulators do not fit one wave's registers.
 Fallback for shapes without a fused instance (:class:`LSTMFunction`): K1/K2
 projection kernels + the recurrence-only kernels described below.
 

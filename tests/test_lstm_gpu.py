@@ -19,7 +19,8 @@ def _relerr(a, b):
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("u,act,B,T,inp", [(32, "relu", 100, 7, 18), (16, "tanh", 37, 50, 18),
                                            (32, "tanh", 64, 50, 32), (64, "relu", 20, 4, 18),
-                                           (16, "relu", 130, 9, 32), (16, "relu", 16, 3, 64)])
+                                           (64, "tanh", 70, 6, 32), (16, "relu", 130, 9, 32),
+                                           (16, "relu", 16, 3, 64)])
 def test_lstm_fwd_bwd_vs_reference(cuda_device, u, act, B, T, inp, fused):
     if fused and not fused_supported(u, inp):
         pytest.skip("no fused instance for this shape")
@@ -208,7 +209,8 @@ def bias_columns(inp: int) -> bool:
 @pytest.mark.parametrize("last_only", [False, True])
 @pytest.mark.parametrize("u,act,B,T,inp", [(32, "relu", 100, 7, 18), (16, "tanh", 37, 50, 18),
                                            (32, "tanh", 64, 50, 32), (64, "relu", 20, 4, 18),
-                                           (16, "relu", 130, 9, 32), (16, "relu", 16, 3, 64)])
+                                           (64, "tanh", 70, 6, 32), (16, "relu", 130, 9, 32),
+                                           (16, "relu", 16, 3, 64)])
 def test_fused_lstm_vs_bf16_rounded_reference(cuda_device, u, act, B, T, inp, last_only):
     """The correctness claim for the fused kernels: against a torch reference that rounds to
     bf16 at the kernels' own points (tests/helpers/bf16_ref.py) every output and gradient
@@ -335,13 +337,14 @@ def test_fused_step_stacked_forward_matches_two_launches(cuda_device, monkeypatc
     assert torch.equal(out["1"][1], out["0"][1]) and torch.equal(out["1"][2], out["0"][2])
 
 
-@pytest.mark.parametrize("u,inp,need_dx", [(32, 18, False), (16, 32, True)])
+@pytest.mark.parametrize("u,inp,need_dx", [(32, 18, False), (16, 32, True), (64, 18, True), (64, 32, False)])
 def test_fused_lstm_persistent_tile_loop_vs_bf16_reference(cuda_device, u, inp, need_dx):
     """B large enough that every workgroup of the persistent backward grid (CUs x 1-2
     workgroups, lstm_fused.hip) loops over several 16-sequence tiles, with a ragged last tile:
     the per-tile state reset, the weight-gradient accumulators carried across tiles and the
     padding lanes' zero dz are all exercised (the other tests use B <= 130: one tile per
-    workgroup).  U=32 without dX (layer 1 of the bench stack), U=16 with dX (layer 2)."""
+    workgroup).  U=32 without dX (layer 1 of the bench stack), U=16 with dX (layer 2); U=64 (dz
+    stored, gate-group weight-gradient kernel) with bias columns + dX and in the plain bias mode."""
     from helpers.bf16_ref import lstm_fused_bf16_reference, relerr
     if not fused_supported(u, inp):
         pytest.skip("no fused instance for this shape")
@@ -362,8 +365,13 @@ def test_fused_lstm_persistent_tile_loop_vs_bf16_reference(cuda_device, u, inp, 
     checks = [("dW", dev[1].grad, dW), ("dU", dev[2].grad, dU), ("db", dev[3].grad, db)]
     if need_dx:
         checks.append(("dx", dev[0].grad, dx))
+    # U=64 at this B: 3 of the 32 805 sequences' recurrences round one bf16 h differently in the kernel's fp32
+    # than in the oracle's fp64 and their relu / gate derivatives follow it (1.1-1.5e-3 over the whole
+    # tensor; tools/debug/lstm64_probe2.py lists them, identical with SML_LSTM_PERSIST=0 -- no tile-loop
+    # effect); every other U=64 test, and this one at B = 64 x CUs + 5, agrees to < 2e-4
+    tol = 2e-3 if u == 64 else 1e-3
     for name, d, r in checks:
-        assert relerr(d.cpu(), r) < 1e-3, name
+        assert relerr(d.cpu(), r) < tol, name
 
 
 def test_fit_accepts_device_window_views(cuda_device):
