@@ -110,7 +110,13 @@ hipError_t dispatch(int U, int IN, int xv, bool x_bf16, F&& f) {
   }
   SML_UK(16, 1) SML_UK(16, 2) SML_UK(16, 4)
   SML_UK(32, 1) SML_UK(32, 2)
-  SML_UK(64, 1) SML_UK(64, 2)
+  // U = 64: scalar row loads only (a third of the instances; the per-step x load is not what
+  // bounds a U = 64 layer)
+  if (U == 64 && KT <= 2) {
+    using UC = std::integral_constant<int, 64>;
+    if (KT <= 1) return with_t(UC{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+    return with_t(UC{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
+  }
 #undef SML_UK
   return hipErrorInvalidValue;
 }

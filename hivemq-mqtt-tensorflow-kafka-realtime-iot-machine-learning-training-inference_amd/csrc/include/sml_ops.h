@@ -84,9 +84,13 @@ hipError_t lstm_fused_fwd_launch(const void* x, bool x_bf16, const float* W, con
 // two stacked layers in one forward (lstm_fused_fwd.hip): x fp32 [B, T, IN1] -> layer 1 (U1 32) ->
 // layer 2 (U2 16); saves both layers' h / c exactly as two lstm_fused_fwd_launch calls do
 bool lstm_fused_fwd2_supported(int IN1, int U1, int U2, int act1, int act2);
+int lstm_fused_fwd2_rows(int64_t B);   // sequences the h / c buffers of lstm_fused_fwd2_launch must hold
+// hlast2 non-null: h1 / h2 stored fragment-native (the backward's fragment mode) and layer 2's h_T
+// as [B16, U2] bf16 rows into hlast2
 hipError_t lstm_fused_fwd2_launch(const float* x, const float* W1, const float* U1, const float* b1, const float* W2,
                                   const float* U2, const float* b2, void* hseq1, void* cseq1, void* hseq2, void* cseq2,
-                                  int64_t B, int T, int IN1, int act1, int act2, int64_t x_seq, hipStream_t stream);
+                                  void* hlast2, int64_t B, int T, int IN1, int act1, int act2, int64_t x_seq,
+                                  hipStream_t stream);
 // two stacked layers' backward in one launch (lstm_fused_stack.hip): layer 2's dX feeds layer 1's
 // dh in registers; one slab per workgroup per layer (partials1 [grid, S1], partials2 [grid, S2])
 bool lstm_fused_bwd2_supported(int IN1, int U1, int U2, int act1, int act2);
@@ -99,7 +103,10 @@ hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, con
                                  bool x_bf16, const float* h0, const float* c0, const float* W, const float* Uw,
                                  const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,
                                  int IN, int U, int act, int dh_last_only, int64_t x_seq, void* dz_scratch,
-                                 hipStream_t stream);
+                                 int frag, hipStream_t stream);
+// fragment mode (frag = 1): h, a bf16 x and dh (unless dh_last_only) read fragment-native, dx written so;
+// instances for the stacked model's two layers (U 32 without dX from fp32 x, U 16 with dX from bf16 x)
+bool lstm_fused_frag_supported(int U, int IN, bool x_bf16, bool want_dx);
 
 // tile-packed training ring: per 16-row tile the normalised rows (x * scale + shift, 64*D
 // bytes) then their 16 argmax bytes; out holds n/16 * (64*D + 16) bytes (n % 16 == 0).

@@ -77,6 +77,7 @@ struct FusedBwdArgs {
   int64_t x_seq;       // elements between consecutive sequences of x (T*IN contiguous, IN sliding windows)
   __bf16* dzs;         // U >= 64 (DZS): dz_t stored fragment-native [B/16, T, 4U/16, 64, 4] bf16 for
                        // lstm_dz_wgrad_kernel (the weight gradients do not fit one wave's registers)
+  int frag;            // fragment mode requested (the launch picks the FR instance)
 };
 
 // BM: bias mode (lstm_fused_impl.h bias_mode).  BX: the x operand carries constant 1.0
@@ -90,7 +91,12 @@ struct FusedBwdArgs {
 // LDS every step (bits: 1 the recurrent U fragments of the dh chain, 2 the gate
 // recompute's [W^T | U^T], 4 the dX fragments W) -- where the registers exist, see launch_bwd.
 // PFD: operand prefetch distance of the one-step loop (steps in flight ahead of the one computing).
-template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0, int BM = BM_PLAIN, int PFD = 1>
+// FR: fragment mode -- the h sequence, a bf16 x (a lower layer's h), dh (unless dh_last_only) and dx
+// are [B/16, T, U/16 | KT, 64 lanes, 4] bf16 (the layout of c): every per-step access of a wave is one
+// contiguous 512-byte piece per tile instead of 16 row pieces (the stacked model's layers, fed by
+// lstm_fused_fwd2's HF mode).
+template <int U, int KT, int XV, typename XT, int ACT, bool DX = true, int RF = 0, int BM = BM_PLAIN, int PFD = 1,
+          bool FR = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdArgs a) {
   constexpr bool BX = BM == BM_BX, DB = BM != BM_PLAIN;   // bias in the MFMAs / db from the dW^T column
   using XR = typename RowRaw<XT>::type;
@@ -216,15 +222,30 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   };
   const __bf16* cw = a.cseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
   __bf16* dzw = DZS ? a.dzs + wave_id * T * (int64_t)(MT * 256) + lane * 4 : nullptr;
+  constexpr bool XFR = FR && std::is_same_v<XT, __bf16>;   // x is a fragment-native h sequence
+  // fragment-mode bases of this tile (h / dh with UB tiles per step, x / dx with KT)
+  const __bf16* hfw = a.hseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
+  const __bf16* dhfw = a.dh + wave_id * T * (int64_t)(UB * 256) + lane * 4;
+  const __bf16* xfw = static_cast<const __bf16*>(a.x) + wave_id * T * (int64_t)(KT * 256) + lane * 4;
   // Loads are unconditional from in-bounds addresses (padding lanes read row B-1),
   // with zeros selected afterwards: no exec-masked branches and no waits in the loop.
   auto load_common = [&](int t, Step& st) {   // raw values; masks are applied in step()
-    const __bf16* dhp = a.dh_last_only ? a.dh + sq * U : a.dh + (sq * T + t) * (int64_t)U;
+    if (FR && !a.dh_last_only) {
 #pragma unroll
-    for (int b = 0; b < UB; ++b) st.dho[b] = ld_bf16x4(dhp + 16 * b + 4 * g);
-    const XT* p = static_cast<const XT*>(a.x) + sq * a.x_seq + (int64_t)t * IN;
+      for (int b = 0; b < UB; ++b) st.dho[b] = ld_bf16x4(dhfw + (int64_t)t * (UB * 256) + b * 256);
+    } else {
+      const __bf16* dhp = a.dh_last_only ? a.dh + sq * U : a.dh + (sq * T + t) * (int64_t)U;
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) st.xt[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN);
+      for (int b = 0; b < UB; ++b) st.dho[b] = ld_bf16x4(dhp + 16 * b + 4 * g);
+    }
+    if constexpr (XFR) {
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) st.xt[kt] = ld_bf16x4(xfw + (int64_t)t * (KT * 256) + kt * 256);
+    } else {
+      const XT* p = static_cast<const XT*>(a.x) + sq * a.x_seq + (int64_t)t * IN;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) st.xt[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN);
+    }
   };
   auto load_step = [&](int t, Step& st) {   // t >= 1
     const __bf16* cp = cw + (int64_t)(t - 1) * (UB * 256);
@@ -232,7 +253,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
       st.cprev[b] = ld_bf16x4(cp + b * 256);
-      st.hp[b] = ld_bf16x4(hrow + 16 * b + 4 * g);
+      st.hp[b] = FR ? ld_bf16x4(hfw + (int64_t)(t - 1) * (UB * 256) + b * 256) : ld_bf16x4(hrow + 16 * b + 4 * g);
     }
     load_common(t, st);
   };
@@ -413,8 +434,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
 #pragma unroll
         for (int mt = 0; mt < MT; mt += 2)
           acc = mfma32(fx(kt * MT + mt), fx(kt * MT + mt + 1), dzb[mt], dzb[mt + 1], acc);
-        // dx is [B16, T, 16*KT]: every lane stores its whole piece, unmasked
-        const int64_t o = (seq * T + t) * (int64_t)(16 * KT) + 16 * kt + 4 * g;
+        // dx is [B16, T, 16*KT] (FR: fragment-native): every lane stores its whole piece, unmasked
+        const int64_t o = FR ? (wave_id * T + t) * (int64_t)(KT * 256) + kt * 256 + lane * 4
+                             : (seq * T + t) * (int64_t)(16 * KT) + 16 * kt + 4 * g;
         if constexpr (std::is_same_v<XT, float>) *reinterpret_cast<f32x4*>(static_cast<float*>(a.dx) + o) = acc;
         else *reinterpret_cast<bf16x4*>(static_cast<__bf16*>(a.dx) + o) = pack4(acc);
       }
@@ -456,6 +478,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   sq = valid ? seq : a.B - 1;
   cw = a.cseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
   if constexpr (DZS) dzw = a.dzs + wave_id * T * (int64_t)(MT * 256) + lane * 4;
+  if constexpr (FR) {
+    hfw = a.hseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
+    dhfw = a.dh + wave_id * T * (int64_t)(UB * 256) + lane * 4;
+    xfw = static_cast<const __bf16*>(a.x) + wave_id * T * (int64_t)(KT * 256) + lane * 4;
+  }
   any_active |= active;
   // fresh recurrence and weight-gradient pipeline per tile (the accumulators carry on)
 #pragma unroll
@@ -706,6 +733,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_dz_wgrad_kernel(FusedBwdAr
   for (int i = threadIdx.x; i < RW * U; i += WAVES * 64) out[G4 * LDW + r0 * U + i] = slab[RW * LDW + i];
 }
 
+// the fragment-mode instances: the stacked model's layer 1 (U 32, fp32 x, no dX) and layer 2
+// (U 16, bf16 x = layer 1's h, dX)
+template <int U, int KT, typename XT, bool DX>
+constexpr bool frag_instance() {
+  return KT == 2 && ((U == 32 && !DX && std::is_same_v<XT, float>) || (U == 16 && DX && std::is_same_v<XT, __bf16>));
+}
+
 // activation as a template parameter: a runtime switch became ~40 scalar branches
 // per step, which split the time loop into basic blocks the scheduler cannot overlap
 template <int U, int KT, int XV, typename XT>
@@ -725,6 +759,14 @@ hipError_t launch_bwd(const FusedBwdArgs& a, hipStream_t st) {
     constexpr int RF = decltype(rf)::value;
     constexpr int BM = decltype(bmc)::value;
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVES * 64), 0, st, a); };
+    if constexpr (frag_instance<U, KT, XT, DX>()) {
+      if (a.frag) {
+        constexpr int PFD = (U == 16 && DX) ? 2 : 1;
+        if (a.act == ACT_RELU) launch(lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, RF, BM, PFD, true>);
+        else launch(lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_TANH, DX, RF, BM, PFD, true>);
+        return;
+      }
+    }
     if constexpr (U == 16 && DX) {
       if (pf_env == 1) {   // one step ahead, every fragment set in registers
         if (a.act == ACT_RELU) launch(lstm_fused_bwd_kernel<U, KT, XV, XT, ACT_RELU, DX, 7, BM, 1>);
@@ -794,6 +836,11 @@ int lstm_fused_dx_ld(int IN) {
   return 16 * (KT <= 1 ? 1 : (KT <= 2 ? 2 : 4));
 }
 
+bool lstm_fused_frag_supported(int U, int IN, bool x_bf16, bool want_dx) {
+  const int KT = (IN + 15) / 16;
+  return KT == 2 && ((U == 32 && !x_bf16 && !want_dx) || (U == 16 && x_bf16 && want_dx && IN == 32));
+}
+
 int64_t lstm_fused_dz_bytes(int64_t B, int T, int U) {   // DZS layers: [B/16 padded, T, 4U] bf16
   return U >= 64 ? (B + 15) / 16 * 16 * (int64_t)T * 4 * U * 2 : 0;
 }
@@ -821,11 +868,12 @@ hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, con
                                  bool x_bf16, const float* h0, const float* c0, const float* W, const float* Uw,
                                  const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,
                                  int IN, int U, int act, int dh_last_only, int64_t x_seq, void* dz_scratch,
-                                 hipStream_t stream) {
+                                 int frag, hipStream_t stream) {
+  if (frag && !lstm_fused_frag_supported(U, IN, x_bf16, dx != nullptr)) return hipErrorInvalidValue;
   if (U >= 64 && dz_scratch == nullptr) return hipErrorInvalidValue;   // lstm_fused_dz_bytes
   FusedBwdArgs a{(const __bf16*)dh_bf16, (const __bf16*)cseq_bf16, (const __bf16*)hseq_bf16, x, h0, c0, W, Uw, b, dx,
                  dh0, dc0, partials, B, T, IN, act, dh_last_only, x_seq > 0 ? x_seq : (int64_t)T * IN,
-                 (__bf16*)dz_scratch};
+                 (__bf16*)dz_scratch, frag};
   return dispatch(U, IN, row_vec(x, IN, x_bf16 ? 2 : 4), x_bf16, [&](auto u, auto k, auto v, auto xt) {
     using XT = std::remove_const_t<std::remove_pointer_t<decltype(xt)>>;
     return launch_bwd<decltype(u)::value, decltype(k)::value, decltype(v)::value, XT>(a, stream);

@@ -189,6 +189,7 @@ struct FusedFwd2Args {
   const float* x;                       // [B, T, IN1] fp32 (x_seq elements between sequences)
   const float *W1, *U1, *b1, *W2, *U2, *b2;
   __bf16 *hseq1, *cseq1, *hseq2, *cseq2;   // padded to whole 16-sequence waves
+  __bf16* hlast2;                          // HF: layer 2's h_T as [B16, U2] rows (the head's input)
   int64_t B;
   int T, IN1, act1, act2;
   int64_t x_seq;
@@ -240,6 +241,67 @@ __device__ __forceinline__ void gate_preacts(const bf16x4 (&wt)[MT][KT], const b
   }
 }
 
+// The same sum with the x-side K pair's A fragment (W^T tiles 0 and 1, concatenated) read from LDS
+// (fwd2 with two tiles per wave: the registers go to the second tile's state; the x-side MFMAs are
+// off the recurrence's critical path, so the read's latency is not).  KT must be 2.
+template <int MT, int UB, bool BX>
+__device__ __forceinline__ void gate_preacts_lx(const s16x8* lx, int ol, const bf16x4 (&ut)[MT][UB],
+                                                const f32x4 (&bias)[MT], const bf16x4 (&xb)[2], const bf16x4 (&hb)[UB],
+                                                f32x4 (&z)[MT]) {
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    z[mt] = BX ? f32x4{0.f, 0.f, 0.f, 0.f} : bias[mt];
+    z[mt] = mfma32a(lx[mt * 64 + ol], xb[0], xb[1], z[mt]);
+    constexpr int NK = 2 + UB;
+#pragma unroll
+    for (int k = 2; k + 1 < NK; k += 2) z[mt] = mfma32(ut[mt][k - 2], ut[mt][k - 1], hb[k - 2], hb[k - 1], z[mt]);
+    if constexpr (NK & 1) z[mt] = mfma32(ut[mt][UB - 1], bf16x4{0, 0, 0, 0}, hb[UB - 1], bf16x4{0, 0, 0, 0}, z[mt]);
+  }
+}
+
+// Timing probes of the stacked forward (SML_LSTM_FWD2_PROBE, A/B only -- bits 1 and 4 give WRONG
+// values and exist to price an instruction class): 1 = sigmoid without the -log2(e) multiply (what a
+// pre-scaled W^T would cost), 2 = the three sigmoids of a unit through ONE reciprocal (exact up to
+// rounding; z clamped at -20 so the product cannot overflow), 4 = x operand without the column mask /
+// bias-column OR; 8 = h stored fragment-native (512 contiguous bytes per wave and tile, as c) instead
+// of [B, T, U] rows; 16 / 32 = h / c not stored (upper bounds of the store cost).
+template <int U, int ACT, int PROBE>
+__device__ __forceinline__ void cell_update_p(const f32x4 (&z)[4 * U / 16], f32x4 (&h)[U / 16], f32x4 (&cs)[U / 16],
+                                              bf16x4 (&hb)[U / 16], __bf16* ht, __bf16* ct) {
+  constexpr int UB = U / 16;
+#pragma unroll
+  for (int b = 0; b < UB; ++b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float gi, gf, go;
+      if constexpr (PROBE & 2) {
+        const float A = 1.0f + __expf(-fmaxf(z[b][i], -20.f));
+        const float Bf = 1.0f + __expf(-fmaxf(z[UB + b][i], -20.f));
+        const float C = 1.0f + __expf(-fmaxf(z[3 * UB + b][i], -20.f));
+        const float AB = A * Bf;
+        const float r = rcp_fast(AB * C);
+        gi = r * (Bf * C);
+        gf = r * (A * C);
+        go = r * AB;
+      } else if constexpr (PROBE & 1) {
+        gi = rcp_fast(1.0f + __builtin_amdgcn_exp2f(-z[b][i]));
+        gf = rcp_fast(1.0f + __builtin_amdgcn_exp2f(-z[UB + b][i]));
+        go = rcp_fast(1.0f + __builtin_amdgcn_exp2f(-z[3 * UB + b][i]));
+      } else {
+        gi = sigmoid_fast(z[b][i]);
+        gf = sigmoid_fast(z[UB + b][i]);
+        go = sigmoid_fast(z[3 * UB + b][i]);
+      }
+      const float gc = act_f(ACT, z[2 * UB + b][i]);
+      cs[b][i] = fmaf(gf, cs[b][i], gi * gc);
+      h[b][i] = go * act_f(ACT, cs[b][i]);
+    }
+    hb[b] = pack4(h[b]);
+    if constexpr (!(PROBE & 32)) *reinterpret_cast<bf16x4*>(ct + b * 256) = pack4(cs[b]);
+    if constexpr (!(PROBE & 16)) *reinterpret_cast<bf16x4*>(ht + ((PROBE & 8) ? b * 256 : 16 * b)) = hb[b];
+  }
+}
+
 template <int U, int ACT>
 __device__ __forceinline__ void cell_update(const f32x4 (&z)[4 * U / 16], f32x4 (&h)[U / 16], f32x4 (&cs)[U / 16],
                                             bf16x4 (&hb)[U / 16], __bf16* ht, __bf16* ct) {
@@ -261,63 +323,123 @@ __device__ __forceinline__ void cell_update(const f32x4 (&z)[4 * U / 16], f32x4 
   }
 }
 
-template <int U1, int KT1, int XV, int ACT1, bool BX1, int U2, int ACT2, int PF = 2>
+// NT: 16-sequence tiles per wave (2: two independent recurrences interleaved in one instruction
+// stream, sharing the weight fragments -- 2 048 waves for the 4 096 tiles of B = 65 536, one residency
+// round at two waves per SIMD instead of two rounds of one-tile waves).  The saved layouts are the
+// one-tile kernel's (cseq indexed by 16-sequence tile), so the backward is unchanged.
+// HF: h1 / h2 stored fragment-native ([B/16, T, U/16, 64 lanes, 4], like c: one 512-byte store per
+// wave and tile instead of 16 row pieces 64 / 32 bytes long) for the backward kernels' fragment mode
+// (lstm_fused.hip FR), and layer 2's h_T once more as rows for the head.
+template <int U1, int KT1, int XV, int ACT1, bool BX1, int U2, int ACT2, int PF = 2, int NT = 1, int PROBE = 0,
+          bool HF = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd2_kernel(FusedFwd2Args a) {
   constexpr int MT1 = 4 * U1 / 16, UB1 = U1 / 16, MT2 = 4 * U2 / 16, UB2 = U2 / 16, KT2 = UB1;
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int64_t s0 = ((int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * 16;
-  if (s0 >= a.B) return;  // wave-uniform
-  const int64_t seq = s0 + c;
-  const int64_t sq = seq < a.B ? seq : a.B - 1;
+  const int64_t wv0 = ((int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * NT;   // first 16-sequence tile
   const int IN1 = a.IN1, T = a.T;
+  // NT = 2: the x-side A fragments of both layers live in LDS (shared by the workgroup's waves)
+  constexpr bool LX = NT > 1;
+  static_assert(!LX || (KT1 == 2 && KT2 == 2), "LDS x fragments: one K pair per layer");
+  __shared__ __attribute__((aligned(16))) s16x8 lx1[LX ? MT1 * 64 : 1], lx2[LX ? MT2 * 64 : 1];
 
   bf16x4 wt1[MT1][KT1], ut1[MT1][UB1], wt2[MT2][KT2], ut2[MT2][UB2];
   f32x4 bias1[MT1], bias2[MT2];
   load_layer_frags<U1, KT1, BX1>(a.W1, a.U1, a.b1, IN1, c, g, wt1, ut1, bias1);
   load_layer_frags<U2, KT2, false>(a.W2, a.U2, a.b2, U1, c, g, wt2, ut2, bias2);   // x = h1: no spare columns
+  if constexpr (LX) {
+    if (threadIdx.x < 64) {
+#pragma unroll
+      for (int mt = 0; mt < MT1; ++mt) lx1[mt * 64 + lane] = cat8(wt1[mt][0], wt1[mt][1]);
+#pragma unroll
+      for (int mt = 0; mt < MT2; ++mt) lx2[mt * 64 + lane] = cat8(wt2[mt][0], wt2[mt][1]);
+    }
+    __syncthreads();   // before any wave leaves
+  }
+  if (wv0 * 16 >= a.B) return;  // wave-uniform
   bf16x4 onex[KT1];
 #pragma unroll
   for (int kt = 0; kt < KT1; ++kt) onex[kt] = BX1 ? ones_at_bias(kt, g, IN1) : bf16x4{0, 0, 0, 0};
-  f32x4 h1[UB1], c1[UB1], h2[UB2], c2[UB2];
-  bf16x4 hb1[UB1], hb2[UB2];
+  f32x4 h1[NT][UB1], c1[NT][UB1], h2[NT][UB2], c2[NT][UB2];
+  bf16x4 hb1[NT][UB1], hb2[NT][UB2];
+  const float* xrow[NT];
+  __bf16 *hw1[NT], *hw2[NT], *cw1[NT], *cw2[NT], *hf1[NT], *hf2[NT];
 #pragma unroll
-  for (int b = 0; b < UB1; ++b) {
-    h1[b] = c1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-    hb1[b] = bf16x4{0, 0, 0, 0};
+  for (int k = 0; k < NT; ++k) {
+#pragma unroll
+    for (int b = 0; b < UB1; ++b) {
+      h1[k][b] = c1[k][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      hb1[k][b] = bf16x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int b = 0; b < UB2; ++b) {
+      h2[k][b] = c2[k][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      hb2[k][b] = bf16x4{0, 0, 0, 0};
+    }
+    // a tile past B (the last wave's second tile) runs on clamped rows and stores into the
+    // buffers' padding (allocated to whole waves of NT tiles)
+    const int64_t wv = wv0 + k;
+    const int64_t seq = wv * 16 + c;
+    const int64_t sq = seq < a.B ? seq : a.B - 1;
+    SML_DCHECK(seq < (a.B + 16 * NT - 1) / (16 * NT) * (16 * NT));
+    xrow[k] = a.x + sq * a.x_seq;
+    hw1[k] = a.hseq1 + seq * T * (int64_t)U1 + 4 * g;
+    hw2[k] = a.hseq2 + seq * T * (int64_t)U2 + 4 * g;
+    cw1[k] = a.cseq1 + wv * T * (int64_t)(UB1 * 256) + lane * 4;
+    cw2[k] = a.cseq2 + wv * T * (int64_t)(UB2 * 256) + lane * 4;
+    hf1[k] = a.hseq1 + wv * T * (int64_t)(UB1 * 256) + lane * 4;
+    hf2[k] = a.hseq2 + wv * T * (int64_t)(UB2 * 256) + lane * 4;
   }
+  auto load_x = [&](int t, f32x4 (*v)[KT1]) {
 #pragma unroll
-  for (int b = 0; b < UB2; ++b) {
-    h2[b] = c2[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-    hb2[b] = bf16x4{0, 0, 0, 0};
-  }
-  const float* xrow = a.x + sq * a.x_seq;
-  auto load_x = [&](int t, f32x4* v) {
-    const float* p = xrow + (int64_t)t * IN1;
+    for (int k = 0; k < NT; ++k) {
+      const float* p = xrow[k] + (int64_t)t * IN1;
 #pragma unroll
-    for (int kt = 0; kt < KT1; ++kt) v[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN1);
+      for (int kt = 0; kt < KT1; ++kt) v[k][kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN1);
+    }
   };
-  const int64_t wv = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
-  SML_DCHECK(wv * 16 < a.B + 15 && seq < (a.B + 15) / 16 * 16);
-  __bf16* cw1 = a.cseq1 + wv * T * (int64_t)(UB1 * 256) + lane * 4;
-  __bf16* cw2 = a.cseq2 + wv * T * (int64_t)(UB2 * 256) + lane * 4;
-  f32x4 xr[PF][KT1];
+  f32x4 xr[PF][NT][KT1];
 #pragma unroll
   for (int p = 0; p < PF; ++p) load_x(p < T ? p : T - 1, xr[p]);
-  auto step = [&](int t, f32x4* xin) {
-    bf16x4 xb[KT1];
+  auto step = [&](int t, f32x4 (*xin)[KT1]) {
+    bf16x4 xb[NT][KT1];
 #pragma unroll
-    for (int kt = 0; kt < KT1; ++kt) {
-      xb[kt] = row_operand(xin[kt], 16 * kt + 4 * g, IN1);
-      if constexpr (BX1) xb[kt] |= onex[kt];
-    }
+    for (int k = 0; k < NT; ++k)
+#pragma unroll
+      for (int kt = 0; kt < KT1; ++kt) {
+        if constexpr (PROBE & 4) {
+          xb[k][kt] = pack4(xin[k][kt]);
+        } else {
+          xb[k][kt] = row_operand(xin[k][kt], 16 * kt + 4 * g, IN1);
+          if constexpr (BX1) xb[k][kt] |= onex[kt];
+        }
+      }
     load_x(t + PF < T ? t + PF : T - 1, xin);
-    f32x4 z1[MT1];
-    gate_preacts<MT1, KT1, UB1, BX1>(wt1, ut1, bias1, xb, hb1, z1);
-    cell_update<U1, ACT1>(z1, h1, c1, hb1, a.hseq1 + (seq * T + t) * (int64_t)U1 + 4 * g, cw1 + (int64_t)t * (UB1 * 256));
+    const int ol = opaque_lane(lane);   // per step: the LDS fragment reads stay in the loop
+    f32x4 z1[NT][MT1];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      if constexpr (LX) gate_preacts_lx<MT1, UB1, BX1>(lx1, ol, ut1, bias1, xb[k], hb1[k], z1[k]);
+      else gate_preacts<MT1, KT1, UB1, BX1>(wt1, ut1, bias1, xb[k], hb1[k], z1[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NT; ++k)
+      cell_update_p<U1, ACT1, PROBE | (HF ? 8 : 0)>(
+          z1[k], h1[k], c1[k], hb1[k],
+          ((PROBE & 8) || HF) ? hf1[k] + (int64_t)t * (UB1 * 256) : hw1[k] + (int64_t)t * U1,
+          cw1[k] + (int64_t)t * (UB1 * 256));
     // layer 2: x_t = layer 1's h_t, already the B operand (hb1)
-    f32x4 z2[MT2];
-    gate_preacts<MT2, KT2, UB2, false>(wt2, ut2, bias2, hb1, hb2, z2);
-    cell_update<U2, ACT2>(z2, h2, c2, hb2, a.hseq2 + (seq * T + t) * (int64_t)U2 + 4 * g, cw2 + (int64_t)t * (UB2 * 256));
+    f32x4 z2[NT][MT2];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      if constexpr (LX) gate_preacts_lx<MT2, UB2, false>(lx2, ol, ut2, bias2, hb1[k], hb2[k], z2[k]);
+      else gate_preacts<MT2, KT2, UB2, false>(wt2, ut2, bias2, hb1[k], hb2[k], z2[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NT; ++k)
+      cell_update_p<U2, ACT2, PROBE | (HF ? 8 : 0)>(
+          z2[k], h2[k], c2[k], hb2[k],
+          ((PROBE & 8) || HF) ? hf2[k] + (int64_t)t * (UB2 * 256) : hw2[k] + (int64_t)t * U2,
+          cw2[k] + (int64_t)t * (UB2 * 256));
   };
   int t0 = 0;
   for (; t0 + PF <= T; t0 += PF) {
@@ -327,15 +449,61 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd2_kernel(FusedFwd
 #pragma unroll
   for (int p = 0; p < PF - 1; ++p)
     if (t0 + p < T) step(t0 + p, xr[p]);
+  if constexpr (HF) {   // h2 of the last step, as rows (the Dense head reads h_T)
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      const int64_t seq = (wv0 + k) * 16 + c;
+#pragma unroll
+      for (int b = 0; b < UB2; ++b) *reinterpret_cast<bf16x4*>(a.hlast2 + seq * U2 + 16 * b + 4 * g) = hb2[k][b];
+    }
+  }
+}
+
+inline int fwd2_tiles() {   // SML_LSTM_FWD2_NT=1|2: 16-sequence tiles per wave of the stacked forward
+  static const int v = [] {
+    const char* e = std::getenv("SML_LSTM_FWD2_NT");
+    return e && e[0] == '2' ? 2 : 1;   // 2 measured 0.4-0.9 % slower (profiles/r05/lstm/ab_fwd2_nt.txt)
+  }();
+  return v;
 }
 
 template <int XV>
 hipError_t launch_fwd2(const FusedFwd2Args& a, hipStream_t st) {
-  const int grid = (int)((a.B + 16 * WAVES - 1) / (16 * WAVES));
   const bool bx = bias_mode_fwd(a.IN1, 2) == BM_BX;
   if (bias_mode_fwd(32, 2) == BM_BX) return hipErrorInvalidValue;   // layer 2 (IN 32) has no spare columns
+  const int nt = fwd2_tiles();
+  const int grid = (int)((a.B + 16 * WAVES * nt - 1) / (16 * WAVES * nt));
+  static const int probe = [] {
+    const char* e = std::getenv("SML_LSTM_FWD2_PROBE");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (probe && nt == 1 && XV == 2 && bx && a.act1 == ACT_RELU && a.act2 == ACT_RELU && a.hlast2 == nullptr) {   // the bench shape only
+    auto go = [&](auto k) {
+      hipLaunchKernelGGL((lstm_fused_fwd2_kernel<32, 2, XV, ACT_RELU, true, 16, ACT_RELU, 2, 1, decltype(k)::value>),
+                         dim3(grid), dim3(WAVES * 64), 0, st, a);
+    };
+    if (probe == 1) go(std::integral_constant<int, 1>{});
+    else if (probe == 2) go(std::integral_constant<int, 2>{});
+    else if (probe == 4) go(std::integral_constant<int, 4>{});
+    else if (probe == 8) go(std::integral_constant<int, 8>{});
+    else if (probe == 16) go(std::integral_constant<int, 16>{});
+    else if (probe == 32) go(std::integral_constant<int, 32>{});
+    else if (probe == 48) go(std::integral_constant<int, 48>{});
+    else go(std::integral_constant<int, 5>{});
+    return hipGetLastError();
+  }
 #define SML_F2(A1, A2, BXV)                                                                                  \
-  hipLaunchKernelGGL((lstm_fused_fwd2_kernel<32, 2, XV, A1, BXV, 16, A2>), dim3(grid), dim3(WAVES * 64), 0, st, a)
+  do {                                                                                                       \
+    if (a.hlast2 != nullptr)                                                                                 \
+      hipLaunchKernelGGL((lstm_fused_fwd2_kernel<32, 2, XV, A1, BXV, 16, A2, 2, 1, 0, true>), dim3(grid),   \
+                         dim3(WAVES * 64), 0, st, a);                                                        \
+    else if (nt == 2)                                                                                        \
+      hipLaunchKernelGGL((lstm_fused_fwd2_kernel<32, 2, XV, A1, BXV, 16, A2, 1, 2>), dim3(grid), dim3(WAVES * 64), \
+                         0, st, a);                                                                          \
+    else                                                                                                     \
+      hipLaunchKernelGGL((lstm_fused_fwd2_kernel<32, 2, XV, A1, BXV, 16, A2, 2, 1>), dim3(grid), dim3(WAVES * 64), \
+                         0, st, a);                                                                          \
+  } while (0)
   if (a.act1 == ACT_RELU && a.act2 == ACT_RELU) {
     if (bx) SML_F2(ACT_RELU, ACT_RELU, true);
     else SML_F2(ACT_RELU, ACT_RELU, false);
@@ -353,15 +521,21 @@ hipError_t launch_fwd2(const FusedFwd2Args& a, hipStream_t st) {
 
 namespace sml {
 
+int lstm_fused_fwd2_rows(int64_t B) {   // sequences the h / c buffers of the stacked forward must hold
+  const int64_t per = 16 * fwd2_tiles();
+  return (int)((B + per - 1) / per * per);
+}
+
 bool lstm_fused_fwd2_supported(int IN1, int U1, int U2, int act1, int act2) {
   return U1 == 32 && U2 == 16 && IN1 >= 1 && IN1 <= 32 && act1 == act2 && (act1 == ACT_RELU || act1 == ACT_TANH);
 }
 
 hipError_t lstm_fused_fwd2_launch(const float* x, const float* W1, const float* U1, const float* b1, const float* W2,
                                   const float* U2, const float* b2, void* hseq1, void* cseq1, void* hseq2, void* cseq2,
-                                  int64_t B, int T, int IN1, int act1, int act2, int64_t x_seq, hipStream_t stream) {
+                                  void* hlast2, int64_t B, int T, int IN1, int act1, int act2, int64_t x_seq,
+                                  hipStream_t stream) {
   FusedFwd2Args a{x, W1, U1, b1, W2, U2, b2, (__bf16*)hseq1, (__bf16*)cseq1, (__bf16*)hseq2, (__bf16*)cseq2,
-                  B, T, IN1, act1, act2, x_seq > 0 ? x_seq : (int64_t)T * IN1};
+                  (__bf16*)hlast2, B, T, IN1, act1, act2, x_seq > 0 ? x_seq : (int64_t)T * IN1};
   const int xv = row_vec(x, IN1, 4);
   if (xv == 4) return launch_fwd2<4>(a, stream);
   if (xv == 2) return launch_fwd2<2>(a, stream);

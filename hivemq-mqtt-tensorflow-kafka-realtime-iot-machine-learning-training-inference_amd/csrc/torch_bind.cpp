@@ -679,7 +679,7 @@ std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W,
 // order), h2 [B,T,U2] bf16, c2] -- the same four tensors two lstm_fused_fwd calls return.
 std::vector<at::Tensor> lstm_fused_fwd2(const at::Tensor& x, const at::Tensor& W1, const at::Tensor& U1,
                                         const at::Tensor& b1, const at::Tensor& W2, const at::Tensor& U2,
-                                        const at::Tensor& b2, int64_t act1, int64_t act2) {
+                                        const at::Tensor& b2, int64_t act1, int64_t act2, bool hfrag) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat, "x must be a float32 device tensor");
   for (const auto* t : {&W1, &U1, &b1, &W2, &U2, &b2}) check_dev(*t, "weights", at::kFloat);
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1 && x.stride(1) == x.size(2) && x.stride(0) >= 0,
@@ -697,15 +697,21 @@ std::vector<at::Tensor> lstm_fused_fwd2(const at::Tensor& x, const at::Tensor& W
   TORCH_CHECK(B >= 1 && T >= 1, "empty input");
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t Bp = (B + 15) / 16 * 16;
+  const int64_t Bw = std::max<int64_t>(Bp, sml::lstm_fused_fwd2_rows(B));   // whole waves of the kernel's tiles
   auto bf = x.options().dtype(at::kBFloat16);
-  auto h1 = at::empty({Bp, T, Ua}, bf), c1 = at::empty({Bp, T, Ua}, bf);
-  auto h2 = at::empty({Bp, T, Ub}, bf), c2 = at::empty({Bp, T, Ub}, bf);
+  auto h1 = at::empty({Bw, T, Ua}, bf), c1 = at::empty({Bw, T, Ua}, bf);
+  auto h2 = at::empty({Bw, T, Ub}, bf), c2 = at::empty({Bw, T, Ub}, bf);
+  at::Tensor hl = hfrag ? at::empty({Bp, Ub}, bf) : at::Tensor();
   SML_CHECK_HIP(sml::lstm_fused_fwd2_launch(x.data_ptr<float>(), W1.data_ptr<float>(), U1.data_ptr<float>(),
                                             b1.data_ptr<float>(), W2.data_ptr<float>(), U2.data_ptr<float>(),
                                             b2.data_ptr<float>(), h1.data_ptr(), c1.data_ptr(), h2.data_ptr(),
-                                            c2.data_ptr(), B, (int)T, (int)IN, (int)act1, (int)act2, x_seq,
-                                            cur_stream(x)));
-  return {h1.narrow(0, 0, B), c1, h2.narrow(0, 0, B), c2};
+                                            c2.data_ptr(), hfrag ? hl.data_ptr() : nullptr, B, (int)T, (int)IN,
+                                            (int)act1, (int)act2, x_seq, cur_stream(x)));
+  // c: the 16-sequence-padded prefix the backward expects (contiguous).  hfrag: h1 / h2 hold the
+  // fragment-native sequences (views of B rows over the padded buffers, for lstm_fused_bwd frag=True)
+  // and the fifth tensor is layer 2's h_T [B, U2]
+  return {h1.narrow(0, 0, B), c1.narrow(0, 0, Bp), h2.narrow(0, 0, B), c2.narrow(0, 0, Bp),
+          hfrag ? hl.narrow(0, 0, B) : at::Tensor()};
 }
 
 // Fully fused LSTM layer backward -> [dx (x's dtype, or undefined), dW [IN,4U], dU [U,4U],
@@ -715,7 +721,7 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
                                        const c10::optional<at::Tensor>& c0, const at::Tensor& W, const at::Tensor& Uw,
                                        const at::Tensor& b, int64_t act, bool want_dx, bool want_state_grads,
                                        bool dh_last_only, const c10::optional<at::Tensor>& grad,
-                                       const c10::optional<at::Tensor>& map) {
+                                       const c10::optional<at::Tensor>& map, bool frag) {
   check_dev(dh, "dh", at::kBFloat16);
   check_dev(cseq, "c", at::kBFloat16);
   check_dev(hseq, "h", at::kBFloat16);
@@ -741,6 +747,11 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
     TORCH_CHECK(dh.sizes() == hseq.sizes(), "dh must be [B, T, U]");
   }
   TORCH_CHECK(sml::lstm_fused_supported((int)U, (int)IN), "fused LSTM: unsupported U=", U, " IN=", IN);
+  // frag: h (and a bf16 x, and dh unless dh_last_only) are fragment-native sequences as
+  // lstm_fused_fwd2(hfrag=True) / this function's frag dx produce them (B-row views over buffers
+  // padded to whole 16-sequence tiles); dx comes back fragment-native too
+  TORCH_CHECK(!frag || sml::lstm_fused_frag_supported((int)U, (int)IN, x.scalar_type() == at::kBFloat16, want_dx),
+              "fused LSTM: no fragment-mode instance for U=", U, " IN=", IN);
   c10::hip::HIPGuard guard(x.device().index());
   auto opts = x.options().dtype(at::kFloat);
   at::Tensor dx, dh0, dc0;
@@ -764,7 +775,7 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
       opt_ptr(c0), W.data_ptr<float>(), Uw.data_ptr<float>(), b.data_ptr<float>(),
       want_dx ? dx_pad.data_ptr() : nullptr, want_state_grads ? dh0.data_ptr<float>() : nullptr,
       want_state_grads ? dc0.data_ptr<float>() : nullptr, partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U,
-      (int)act, dh_last_only ? 1 : 0, x_seq, dzb > 0 ? dzs.data_ptr() : nullptr, st));
+      (int)act, dh_last_only ? 1 : 0, x_seq, dzb > 0 ? dzs.data_ptr() : nullptr, frag ? 1 : 0, st));
   SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
                                      out.data_ptr<float>(), st, mp));
   const int64_t G4 = 4 * U, LDW = (S / G4) - U - 1;
@@ -776,7 +787,7 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
   }
   if (want_dx) {
     dx = dx_pad.narrow(0, 0, B);
-    if (dx_pad.size(2) != IN) dx = dx.narrow(2, 0, IN).contiguous();
+    if (dx_pad.size(2) != IN && !frag) dx = dx.narrow(2, 0, IN).contiguous();
   }
   return {dx, dW, dU, db, dh0, dc0};
 }
@@ -1330,8 +1341,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"));
   m.def("lstm_fused_fwd2", &lstm_fused_fwd2, "two stacked fused LSTM layers (U 32 -> 16) in one forward launch",
         py::arg("x"), py::arg("W1"), py::arg("U1"), py::arg("b1"), py::arg("W2"), py::arg("U2"), py::arg("b2"),
-        py::arg("act1"), py::arg("act2"));
+        py::arg("act1"), py::arg("act2"), py::arg("hfrag") = false);
   m.def("lstm_fused_fwd2_supported", &sml::lstm_fused_fwd2_supported);
+  m.def("lstm_fused_frag_supported", &sml::lstm_fused_frag_supported,
+        "whether lstm_fused_bwd(frag=True) has an instance for this layer", py::arg("U"), py::arg("IN"),
+        py::arg("x_bf16"), py::arg("want_dx"));
   m.def("lstm_fused_bwd2", &lstm_fused_bwd2, "two stacked fused LSTM layers' backward (U 32 -> 16) in one launch",
         py::arg("x"), py::arg("h1"), py::arg("c1"), py::arg("h2"), py::arg("c2"), py::arg("dh2"), py::arg("W1"),
         py::arg("U1"), py::arg("b1"), py::arg("W2"), py::arg("U2"), py::arg("b2"), py::arg("act"),
@@ -1346,7 +1360,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("c"), py::arg("h"), py::arg("x"), py::arg("h0") = py::none(), py::arg("c0") = py::none(),
         py::arg("W"), py::arg("U"), py::arg("b"), py::arg("act") = 1, py::arg("want_dx") = true,
         py::arg("want_state_grads") = false, py::arg("dh_last_only") = false, py::arg("grad") = py::none(),
-        py::arg("map") = py::none());
+        py::arg("map") = py::none(), py::arg("frag") = false);
   m.def("lstm_ref_train", &lstm_ref_train,
         "persistent trainer: nsteps Keras Adam steps of the reference LSTM stack (look_back 1) in one launch",
         py::arg("flat"), py::arg("m"), py::arg("v"), py::arg("iter"), py::arg("x"), py::arg("y"),

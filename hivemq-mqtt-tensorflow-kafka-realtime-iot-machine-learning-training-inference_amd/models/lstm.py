@@ -64,6 +64,13 @@ def _fwd2() -> bool:
     return os.environ.get("SML_LSTM_FWD2", "1") != "0"
 
 
+def _frag() -> bool:
+    """SML_LSTM_FRAG=0: the stacked two-layer step keeps h1 / h2 / dX as [B, T, U] rows instead of the
+    fragment-native layout (A/B; read per step).  Fragment-native, every per-step h / dh / x access of
+    a wave is one contiguous 512-byte piece per 16-sequence tile (lstm_fused.hip FR)."""
+    return os.environ.get("SML_LSTM_FRAG", "1") != "0"
+
+
 def _bwd2() -> bool:
     """SML_LSTM_BWD2=1: the bottom two layers' backward in ONE launch (lstm_fused_stack.hip)
     instead of two (read per step).  Off by default: correct (bit-identical to two launches
@@ -267,6 +274,8 @@ class LSTMPredictor:
         h = x
         stack = pre + post
         first = 0
+        frag = False   # layers 1 and 2 exchange fragment-native sequences (only h_T leaves the pair)
+        hlast = None
         if _fwd2() and len(pre) >= 2 and x.dtype == torch.float32:
             # the first two layers (U 32 -> 16) in ONE forward launch: layer 1's h feeds layer 2
             # from registers (lstm_fused_fwd.hip fwd2); the same saved h / c as two launches
@@ -275,7 +284,10 @@ class LSTMPredictor:
             W2, U2, b2 = (t.detach() for t in P[L2["params"]:L2["params"] + 3])
             a1, a2 = ACT[L1["activation"]], ACT[L2["activation"]]
             if C.lstm_fused_fwd2_supported(x.shape[2], U1.shape[0], U2.shape[0], a1, a2):
-                hs1, c1, hs2, c2 = C.lstm_fused_fwd2(x, W1, U1, b1, W2, U2, b2, a1, a2)
+                frag = (_frag() and not _bwd2() and len(pre) == 2 and not post
+                        and C.lstm_fused_frag_supported(U1.shape[0], x.shape[2], False, False)
+                        and C.lstm_fused_frag_supported(U2.shape[0], U1.shape[0], True, True))
+                hs1, c1, hs2, c2, hlast = C.lstm_fused_fwd2(x, W1, U1, b1, W2, U2, b2, a1, a2, frag)
                 saved += [(x, hs1, c1), (hs1, hs2, c2)]
                 h, first = hs2, 2
         for L in stack[first:]:
@@ -289,7 +301,7 @@ class LSTMPredictor:
             h = hs
         hd = plan["head"]
         K, bh = (t.detach() for t in P[hd["params"]:hd["params"] + 2])
-        hin = h.reshape(n * R, h.shape[-1]) if R else h[:, -1]   # bf16, read in place when h_T
+        hin = h.reshape(n * R, h.shape[-1]) if R else (hlast if frag else h[:, -1])   # bf16, in place when h_T
         y_pred = C.dense_fwd(hin, K, bh, 0, False, 1024, False)
         yt = y.to(device=self.device, dtype=torch.float32).contiguous()
         acc = plan["acc"]
@@ -311,7 +323,7 @@ class LSTMPredictor:
             last_only = i == len(pre) - 1
             if R and i >= len(pre):
                 dh = dh.view(n, R, -1)
-            if i == 1 and _bwd2() and saved[0][0].dtype == torch.float32:
+            if i == 1 and not frag and _bwd2() and saved[0][0].dtype == torch.float32:
                 # the bottom two layers' backward in ONE launch (lstm_fused_stack.hip): layer 2's
                 # dX reaches layer 1 in registers, h1 is read once
                 L0 = layers[0]
@@ -324,7 +336,7 @@ class LSTMPredictor:
                                       plan["maps"][0], plan["maps"][1])
                     break
             out = C.lstm_fused_bwd(dh, c, hs, xin, None, None, W, Uw, b, ACT[L["activation"]], i > 0, False,
-                                   last_only, grad, plan["maps"][i])
+                                   last_only, grad, plan["maps"][i], frag and i < 2)
             dh = out[0]
             if R and i == len(pre):   # RepeatVector backward: the repeated steps' gradients summed
                 dh = (dh.view(n, -1) if R == 1 else dh.sum(1)).to(torch.bfloat16)

@@ -258,13 +258,67 @@ def test_stacked_forward_equals_two_launches(cuda_device, act, B, T, windows):
     W1, U1, b1 = w(18, 128), w(32, 128), w(128, s=0.1)
     W2, U2, b2 = w(32, 64), w(16, 64), w(64, s=0.1)
     assert C.lstm_fused_fwd2_supported(18, 32, 16, act, act)
-    h1, c1, h2, c2 = C.lstm_fused_fwd2(x, W1, U1, b1, W2, U2, b2, act, act)
+    h1, c1, h2, c2, _ = C.lstm_fused_fwd2(x, W1, U1, b1, W2, U2, b2, act, act)
     r1, rc1 = C.lstm_fused_fwd(x, W1, U1, b1, None, None, act)
     r2, rc2 = C.lstm_fused_fwd(r1, W2, U2, b2, None, None, act)
     torch.cuda.synchronize()
     for got, want in ((h1, r1), (c1, rc1), (h2, r2), (c2, rc2)):
         assert got.shape == want.shape
         torch.testing.assert_close(got.view(torch.int16), want.view(torch.int16), rtol=0, atol=0)
+
+
+def _frag_to_rows(t, B):
+    """A fragment-native sequence buffer ([B/16, T, U/16, 64 lanes, 4]: lane = 16 g + c holds
+    units 16 b + 4 g .. + 3 of sequence 16 tile + c) as [B, T, U] rows."""
+    _, T, U = t.shape
+    tiles = (B + 15) // 16
+    flat = torch.as_strided(t, (tiles * 16 * T * U,), (1,), t.storage_offset())
+    v = flat.view(tiles, T, U // 16, 4, 16, 4)            # tile, t, b, g, c, j
+    return v.permute(0, 4, 1, 2, 3, 5).reshape(tiles * 16, T, U)[:B]
+
+
+@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("B,T", [(1000 + 7, 50), (0, 4)])
+def test_fragment_mode_equals_row_mode(cuda_device, act, B, T):
+    """The stacked model's fragment mode (lstm_fused_fwd2 hfrag, lstm_fused_bwd frag): the saved h1 /
+    h2, layer 2's dX and every weight gradient are bit-identical to the row-layout path -- only the
+    addresses change.  B = 0: 64 x CUs x 2 + 37 (persistent backward grid, several tiles per
+    workgroup, ragged last tile)."""
+    from streamml.data.stream import sliding_windows
+    from streamml.ops import load_c
+    C = load_c()
+    if B == 0:
+        B = 64 * torch.cuda.get_device_properties(cuda_device).multi_processor_count * 2 + 37
+    rng = np.random.default_rng(B + T + 7 * act)
+    base = torch.tensor(rng.uniform(-1, 1, (B + T, 18)), dtype=torch.float32, device=cuda_device)
+    x, _ = sliding_windows(base, T)
+    x = x[:B]
+
+    def w(*shape, s=0.25):
+        return torch.tensor(rng.standard_normal(shape) * s, dtype=torch.float32, device=cuda_device)
+    W1, U1, b1 = w(18, 128), w(32, 128), w(128, s=0.1)
+    W2, U2, b2 = w(32, 64), w(16, 64), w(64, s=0.1)
+    assert C.lstm_fused_frag_supported(32, 18, False, False) and C.lstm_fused_frag_supported(16, 32, True, True)
+    h1, c1, h2, c2, _ = C.lstm_fused_fwd2(x, W1, U1, b1, W2, U2, b2, act, act, False)
+    f1, fc1, f2, fc2, hl = C.lstm_fused_fwd2(x, W1, U1, b1, W2, U2, b2, act, act, True)
+    bits = lambda t: t.contiguous().view(torch.int16)   # noqa: E731
+    torch.testing.assert_close(bits(_frag_to_rows(f1, B)), bits(h1), rtol=0, atol=0)
+    torch.testing.assert_close(bits(_frag_to_rows(f2, B)), bits(h2), rtol=0, atol=0)
+    torch.testing.assert_close(bits(hl), bits(h2[:, -1]), rtol=0, atol=0)
+    torch.testing.assert_close(bits(fc1), bits(c1), rtol=0, atol=0)
+    torch.testing.assert_close(bits(fc2), bits(c2), rtol=0, atol=0)
+    dh2 = torch.tensor(rng.standard_normal((B, 16)), dtype=torch.float32, device=cuda_device).to(torch.bfloat16)
+    dx2, dW2, dU2, db2, _, _ = C.lstm_fused_bwd(dh2, c2, h2, h1, None, None, W2, U2, b2, act, True, False, True)
+    _, dW1, dU1, db1, _, _ = C.lstm_fused_bwd(dx2, c1, h1, x, None, None, W1, U1, b1, act, False, False, False)
+    fx2, gW2, gU2, gb2, _, _ = C.lstm_fused_bwd(dh2, fc2, f2, f1, None, None, W2, U2, b2, act, True, False, True,
+                                                frag=True)
+    _, gW1, gU1, gb1, _, _ = C.lstm_fused_bwd(fx2, fc1, f1, x, None, None, W1, U1, b1, act, False, False, False,
+                                              frag=True)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(bits(_frag_to_rows(fx2, B)), bits(dx2), rtol=0, atol=0)
+    for name, g, r in (("dW1", gW1, dW1), ("dU1", gU1, dU1), ("db1", gb1, db1), ("dW2", gW2, dW2),
+                       ("dU2", gU2, dU2), ("db2", gb2, db2)):
+        assert torch.equal(g, r), name
 
 
 def _relerr_t(a, b):
@@ -293,7 +347,7 @@ def test_stacked_backward_vs_two_launches(cuda_device, act, B, T, tiles):
         return torch.tensor(rng.standard_normal(shape) * s, dtype=torch.float32, device=cuda_device)
     W1, U1, b1 = w(18, 128), w(32, 128), w(128, s=0.1)
     W2, U2, b2 = w(32, 64), w(16, 64), w(64, s=0.1)
-    h1, c1, h2, c2 = C.lstm_fused_fwd2(x, W1, U1, b1, W2, U2, b2, act, act)
+    h1, c1, h2, c2, _ = C.lstm_fused_fwd2(x, W1, U1, b1, W2, U2, b2, act, act)
     dh2 = torch.tensor(rng.standard_normal((B, 16)), dtype=torch.float32, device=cuda_device).to(torch.bfloat16)
     assert C.lstm_fused_bwd2_supported(18, 32, 16, act, act)
     got = C.lstm_fused_bwd2(x, h1, c1, h2, c2, dh2, W1, U1, b1, W2, U2, b2, act, True)
