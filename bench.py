@@ -704,7 +704,7 @@ def main():
         stream = ph.run("stream_e2e", 10 + 1.5e-6 * args.stream_rows, measure_stream_e2e, device, args.stream_rows)
         out.update({"stream_e2e_rows_per_s": stream.get("rows_per_s"), "stream_e2e": stream})
     if args.large_stream_rows > 0:   # fresh rows at large batch: the host decode curve and the trained rate
-        big = ph.run("stream_large_batch", 12 + 1.2e-6 * args.large_stream_rows,
+        big = ph.run("stream_large_batch", 16 + 1.2e-6 * args.large_stream_rows,
                      _bench_module("bench_fit").stream_large_batch, device, rows=args.large_stream_rows,
                      partitions=32, workers=(1, 2, 4, 8, 16))
         out.update({"stream_large_batch_rows_per_s": big.get("trained_rows_per_s"), "stream_large_batch": big})
@@ -764,6 +764,7 @@ SUMMARY_FIELDS = (
     ("lstm_ref_us_per_step", ("lstm_ref_us_per_step",)),
     ("stream_e2e_rows_per_s", ("stream_e2e_rows_per_s",)),
     ("stream_large_batch_rows_per_s", ("stream_large_batch_rows_per_s",)),
+    ("stream_staged_train_rows_per_s", ("stream_large_batch", "staged_train", "best_trained_rows_per_s")),
     ("stream_dp_rows_per_s", ("stream_dp_rows_per_s",)),
     ("mqtt_publish_to_result_p50_us", ("mqtt_publish_to_result_p50_us",)),
     ("mqtt_publish_to_result_p99_us", ("mqtt_publish_to_result_p99_us",)),

@@ -253,6 +253,34 @@ def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, bat
                 "h2d_gb_per_s": st.get("h2d_bytes", 0) / dt / 1e9,
                 "train_stage_s": {"wall": dt, "fetch_sum": st.get("fetch_s"), "decode_sum": st.get("decode_s"),
                                   "wait_slab_sum": st.get("wait_slab_s")}})
+    # 3. the consumer side alone: the same values pre-staged in memory (8 copies of the distinct set),
+    #    decoded by the feed workers straight into the pinned ring -> H2D -> fit(throughput); no broker
+    #    threads on the CPUs ("pre-stage fetched record batches")
+    reps = 8
+    sbuf = np.tile(buf, reps)
+    soffs = np.concatenate([offs[:-1] + k * len(buf) for k in range(reps)] + [np.array([reps * len(buf)], np.int64)])
+    staged_runs = []
+    for w in sorted({min(8, int(quota or 8)), max(1, min(16, int(quota or 16) - 2))}):
+        ssrc = S.kafka(f"fake://{name}", specs[:1], workers=int(w), native=True)
+        ssrc.native_feed.stage(sbuf, soffs)
+        st_train = ssrc.filter_normal(device=True)
+        ms = Autoencoder(device=device, input_normalizer="cardata")
+        ms.compile()
+        ms.fit(st_train, epochs=1, batch_size=batch, verbose=0, steps_per_epoch=2, engine="throughput", dp="none")
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        hs = ms.fit(st_train, epochs=2, batch_size=batch, verbose=0, engine="throughput", dp="none")
+        torch.cuda.synchronize()
+        dts = time.perf_counter() - t1
+        kept_s = int(sum(hs.history["_rows"])) if "_rows" in hs.history else 0
+        sst = ssrc.native_feed.last_stats
+        staged_runs.append({"workers": int(w), "values": int(len(soffs) - 1) * 2, "trained_rows_per_s": kept_s / dts,
+                            "decode_s_sum": sst.get("decode_s"), "wait_slab_s_sum": sst.get("wait_slab_s"),
+                            "h2d_gb_per_s": sst.get("h2d_bytes", 0) / dts / 1e9})
+    out["staged_train"] = {"runs": staged_runs, "best_trained_rows_per_s": max(r["trained_rows_per_s"]
+                                                                                for r in staged_runs),
+                           "path": "pre-staged record values -> feed workers decode into the pinned ring -> H2D -> "
+                                   "fit(batch_size=1 M, engine=throughput); no broker"}
     # what caps the curve: the decoder alone against the fetch + decode path, within the CPUs
     # this job may keep busy (the feed workers, the broker's connection threads and the
     # training loop all draw on that one quota)

@@ -112,6 +112,97 @@ void Feed::start(const std::vector<uintptr_t>& slabs, int64_t cap_rows) {
   for (int w = 0; w < nw; ++w) workers_[(size_t)w].th = std::thread([this, w] { run(w); });
 }
 
+void Feed::start_staged(const std::vector<uintptr_t>& slabs, int64_t cap_rows, const uint8_t* buf,
+                        const int64_t* offs, int64_t n, int workers) {
+  if (!workers_.empty()) throw std::logic_error("feed: already started");
+  if (slabs.empty() || cap_rows <= 0) throw std::invalid_argument("feed: need slabs of > 0 rows");
+  if (n < 0 || workers < 1) throw std::invalid_argument("feed: staged n >= 0, workers >= 1");
+  slabs_ = slabs;
+  marks_.assign(slabs_.size(), {});
+  cap_ = cap_rows;
+  for (size_t i = 0; i < slabs_.size(); ++i) free_.push_back((int)i);
+  const int nw = (int)std::max<int64_t>(1, std::min<int64_t>(workers, std::max<int64_t>(n, 1)));
+  workers_.resize((size_t)nw);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    live_workers_ = nw;
+  }
+  for (int w = 0; w < nw; ++w) {
+    const int64_t a = n * w / nw, b = n * (w + 1) / nw;
+    workers_[(size_t)w].th = std::thread([this, w, buf, offs, a, b] { run_staged(w, buf, offs, a, b); });
+  }
+}
+
+void Feed::run_staged(int w, const uint8_t* buf, const int64_t* offs, int64_t a, int64_t b) {
+  const size_t F = cfg_.feature_fields.size();
+  Stats loc;
+  int slab = -1;
+  int64_t n = 0;
+  float* rows = nullptr;
+  uint8_t* labs = nullptr;
+  std::string err;
+  try {
+    const auto t1 = Clock::now();
+    for (int64_t i = a; i < b; ++i) {
+      if (slab < 0) {
+        const auto tw = Clock::now();
+        slab = take_free(loc.wait_slab_s);
+        loc.decode_s -= secs(tw, Clock::now());   // the wait is not decode time
+        if (slab < 0) break;   // stopping
+        n = 0;
+        rows = reinterpret_cast<float*>(slabs_[(size_t)slab]);
+        labs = reinterpret_cast<uint8_t*>(slabs_[(size_t)slab]) + (size_t)cap_ * F * 4;
+      }
+      const size_t len = (size_t)(offs[i + 1] - offs[i]);
+      ++loc.records;
+      loc.bytes += len;
+      float* row = rows + (size_t)n * F;
+      uint8_t lab = cfg_.label_field >= 0 ? 2 : 0;
+      if (!decode_row(buf + offs[i], len, row, &lab)) {
+        ++loc.errors;
+        for (size_t k = 0; k < F; ++k) row[k] = NAN;
+        lab = 2;
+      }
+      if (cfg_.keep_label >= 0 && lab != (uint8_t)cfg_.keep_label) {
+        ++loc.dropped;
+        continue;
+      }
+      labs[n] = lab;
+      ++n;
+      ++loc.rows;
+      if (n == cap_) {
+        publish(w, slab, n);
+        slab = -1;
+      }
+    }
+    loc.decode_s += secs(t1, Clock::now());
+  } catch (const std::exception& e) {
+    err = e.what();
+  }
+  if (slab >= 0) {
+    if (n > 0) {
+      publish(w, slab, n);
+    } else {
+      std::lock_guard<std::mutex> g(mu_);
+      free_.push_back(slab);
+    }
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stats_.records += loc.records;
+    stats_.rows += loc.rows;
+    stats_.dropped += loc.dropped;
+    stats_.errors += loc.errors;
+    stats_.bytes += loc.bytes;
+    stats_.decode_s += loc.decode_s;
+    stats_.wait_slab_s += loc.wait_slab_s;
+    if (!err.empty() && error_.empty()) error_ = "feed worker " + std::to_string(w) + ": " + err;
+    --live_workers_;
+  }
+  cv_ready_.notify_all();
+  cv_free_.notify_all();
+}
+
 void Feed::stop() {
   {
     std::lock_guard<std::mutex> g(mu_);

@@ -73,6 +73,12 @@ class Feed {
   Feed& operator=(const Feed&) = delete;
 
   void start(const std::vector<uintptr_t>& slabs, int64_t cap_rows);
+  // Pre-staged source: the n record values of buf (value i = buf[offs[i], offs[i+1]), as fetched
+  // responses hold them) split into `workers` contiguous shares, each decoded by its own thread into
+  // the slabs and published like fetched rows -- the decode + ring + H2D path without the broker
+  // (buf / offs must outlive the stream).  No partitions, no commit marks.
+  void start_staged(const std::vector<uintptr_t>& slabs, int64_t cap_rows, const uint8_t* buf, const int64_t* offs,
+                    int64_t n, int workers);
   // 1 = got a slab, 0 = timed out, -1 = end of stream.  Rethrows a worker's error.
   int pop(int& slab, int64_t& rows, int timeout_ms);
   void recycle(int slab);
@@ -105,6 +111,7 @@ class Feed {
     std::thread th;
     std::vector<int> parts;
   };
+  void run_staged(int w, const uint8_t* buf, const int64_t* offs, int64_t a, int64_t b);
   std::string bootstrap_;
   kafka::ClientConfig ccfg_;
   std::vector<avro::Field> fields_;

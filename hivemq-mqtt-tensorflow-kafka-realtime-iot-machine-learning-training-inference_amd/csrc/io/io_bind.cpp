@@ -674,6 +674,17 @@ PYBIND11_MODULE(_io, m) {
              f.start(v, cap);
            },
            py::arg("slabs"), py::arg("cap_rows"))
+      .def("start_staged",   // pre-staged record values -> the slabs (the caller keeps buf / offsets alive)
+           [](feed::Feed& f, const std::vector<uint64_t>& slabs, int64_t cap, py::buffer buf,
+              py::array_t<int64_t, py::array::c_style> offs, int workers) {
+             py::buffer_info bi = buf.request();
+             const int64_t n = (int64_t)offs.size() - 1;
+             if (n < 0 || (n > 0 && offs.at(n) > (int64_t)bi.size * (int64_t)bi.itemsize))
+               throw std::invalid_argument("start_staged: offsets past the buffer");
+             std::vector<uintptr_t> v(slabs.begin(), slabs.end());
+             f.start_staged(v, cap, static_cast<const uint8_t*>(bi.ptr), offs.data(), n, workers);
+           },
+           py::arg("slabs"), py::arg("cap_rows"), py::arg("buf"), py::arg("offsets"), py::arg("workers"))
       .def("pop",
            [](feed::Feed& f, int timeout_ms) {
              int slab = -1;

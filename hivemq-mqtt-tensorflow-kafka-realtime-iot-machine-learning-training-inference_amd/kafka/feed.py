@@ -65,6 +65,17 @@ class NativeFeed:
         # librdkafka's check.crcs (default false): verify every record batch's CRC-32C
         self.check_crcs = str(parse_config(self.config).get("check.crcs", "false")).lower() in ("true", "1")
         self.last_stats: dict = {}
+        self.staged = None            # stage(): pre-fetched record values instead of the broker
+
+    def stage(self, buf, offsets) -> "NativeFeed":
+        """Serve every later iteration from ``len(offsets) - 1`` pre-staged record values (value i =
+        ``buf[offsets[i]:offsets[i+1]]``, as fetched responses hold them) instead of fetching: the
+        workers decode contiguous shares of them straight into the pinned ring, so the decode +
+        H2D + train path runs without the broker's socket threads sharing the CPUs (a bench mode
+        that measures the consumer side; no partitions, no commits)."""
+        arr = buf if isinstance(buf, np.ndarray) else np.frombuffer(buf, np.uint8)
+        self.staged = (np.ascontiguousarray(arr), np.ascontiguousarray(offsets, dtype=np.int64))
+        return self
 
     @property
     def features(self) -> int:
@@ -100,10 +111,11 @@ class NativeFeed:
         return parts
 
     def _make(self, keep_label: Optional[int]):
-        client = KafkaClient(self.servers, self.config)
-        parts = self._parts(client)
+        staged = self.staged is not None
+        client = None if staged else KafkaClient(self.servers, self.config)
+        parts = [] if staged else self._parts(client)
         cid, mech, user, pw, tmo = _auth(self.config)
-        f = load_io().KafkaFeed(client.servers, cid, mech, user, pw, tmo,
+        f = load_io().KafkaFeed("127.0.0.1:9" if staged else client.servers, cid, mech, user, pw, tmo,
                                 [fs.as_tuple() for fs in self.codec.fields], self.feature_fields,
                                 self.label_field, -1 if keep_label is None else int(keep_label), self.framing,
                                 self.max_bytes, self.max_wait_ms, self.workers,
@@ -123,6 +135,13 @@ class NativeFeed:
         rate, rows = f.decode_throughput(buf, np.ascontiguousarray(offsets, dtype=np.int64), int(workers), int(repeats))
         return float(rate), int(rows)
 
+    def _begin(self, f, ptrs, slab_rows: int) -> None:
+        if self.staged is not None:
+            buf, offs = self.staged
+            f.start_staged(ptrs, int(slab_rows), buf, offs, self.workers)
+        else:
+            f.start(ptrs, int(slab_rows))
+
     @staticmethod
     def _consumed(f, slab: int, marks: dict) -> None:
         """The consumer asked for the next slab: everything this one carried has been used."""
@@ -137,7 +156,9 @@ class NativeFeed:
         slabs are re-read by a resumed run, never skipped)."""
         st = dict(f.stats())
         st["wall_s"] = time.perf_counter() - t0
-        st["workers"] = min(self.workers, max(len(parts), 1))
+        st["workers"] = self.workers if self.staged is not None else min(self.workers, max(len(parts), 1))
+        if self.staged is not None:
+            st["source"] = "staged"
         st["committed"] = "end" if exhausted else "consumed-slabs"
         self.last_stats = st
         if not self.commit:
@@ -157,7 +178,7 @@ class NativeFeed:
         nslots = int(slots or 2 * self.workers + 2)
         bufs = [np.empty(slab_rows * (F * 4 + 1), np.uint8) for _ in range(nslots)]
         t0 = time.perf_counter()
-        f.start([int(b.ctypes.data) for b in bufs], int(slab_rows))
+        self._begin(f, [int(b.ctypes.data) for b in bufs], slab_rows)
         marks: dict = {}
         exhausted = False
         try:
@@ -188,7 +209,7 @@ class NativeFeed:
         nslots = 2 * self.workers + 2
         bufs = [np.empty(slab_rows * (F * 4 + 1), np.uint8) for _ in range(nslots)]
         t0 = time.perf_counter()
-        f.start([int(b.ctypes.data) for b in bufs], int(slab_rows))
+        self._begin(f, [int(b.ctypes.data) for b in bufs], slab_rows)
         total, exhausted = 0, False
         try:
             while True:
@@ -231,7 +252,7 @@ class NativeFeed:
         bufs = [torch.empty(slab_bytes, dtype=torch.uint8, device=dev) for _ in range(nslots)]
         f, client, parts = self._make(keep_label)
         t0 = time.perf_counter()
-        f.start([int(ring.host_ptr(i)) for i in range(nslots)], int(slab_rows))
+        self._begin(f, [int(ring.host_ptr(i)) for i in range(nslots)], slab_rows)
         pending: collections.deque = collections.deque()
         done = False
         exhausted = False

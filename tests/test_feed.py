@@ -177,3 +177,28 @@ def test_feed_check_crcs_config(topic):
     ref = S.kafka(servers, specs[:1], native=True)
     assert not ref.native_feed.check_crcs
     np.testing.assert_array_equal(np.concatenate([c.x for c in st]), np.concatenate([c.x for c in ref]))
+
+
+@pytest.mark.parametrize("workers", [1, 3])
+def test_feed_staged_values_match_fetched(topic, workers):
+    """NativeFeed.stage(): pre-staged record values decoded by the workers into the slabs give the
+    same rows (as a multiset: workers publish in any order) and the same decode-time filter as
+    fetching them from the broker; each later iteration re-reads the staged values."""
+    servers, specs = topic
+    codec = AvroCodec("cardata-v1")
+    bufs, offs, base = [], [np.zeros(1, np.int64)], 0
+    for c in S.synthetic(30_000, chunk=2_500, seed=7, failure_rate=0.1):
+        b, o = encode_chunk(codec, c.x, c.label)
+        bufs.append(np.frombuffer(b, np.uint8)[:int(o[-1])])
+        offs.append(np.asarray(o[1:], np.int64) + base)
+        base += int(o[-1])
+    buf, offs = np.concatenate(bufs), np.concatenate(offs)
+    feed = S.kafka(servers, specs, workers=workers, native=True).native_feed
+    feed.stage(buf, offs)
+    key = lambda x: x[np.lexsort(x.T[::-1])]   # noqa: E731
+    ref = np.concatenate([r for r, _ in S.kafka(servers, specs, native=True).native_feed.host_chunks(keep_label=0)])
+    for _ in range(2):
+        got = np.concatenate([r for r, labs in feed.host_chunks(keep_label=0) if np.all(labs == 0)])
+        np.testing.assert_array_equal(key(got), key(ref))
+        assert feed.last_stats["records"] == 30_000 and feed.last_stats["source"] == "staged"
+        assert feed.last_stats["dropped"] == 30_000 - len(ref)

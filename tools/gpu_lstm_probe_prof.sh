@@ -22,7 +22,7 @@ out = []
 for r in rows:
     n = r.get("Name", "")
     if "lstm" in n or "slab" in n or "adam" in n.lower():
-        out.append("%s:%.1f" % (n.split("(")[0].split("<")[0].replace("void ", ""), float(r["AverageNs"]) / 1e3))
+        out.append("%s:%.1f" % (n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:60], float(r["AverageNs"]) / 1e3))
 print(sys.argv[2], " ".join(out))
 PY
 done
