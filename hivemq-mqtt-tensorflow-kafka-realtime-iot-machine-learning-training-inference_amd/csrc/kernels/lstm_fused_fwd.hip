@@ -33,6 +33,30 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
   using XR = typename RowRaw<XT>::type;
   constexpr int G4 = 4 * U, MT = G4 / 16, UB = U / 16;
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  // LF (U >= 64): the MT x (KT + UB) weight fragments (160-192 registers) live in LDS, shared by the
+  // workgroup's waves and read per step through an opaque lane index; the registers held the scratch
+  // spills of the register-fragment build
+  constexpr bool LF = U >= 64;
+  constexpr int NK = KT + UB;
+  __shared__ __attribute__((aligned(16))) bf16x4 lfw[LF ? MT * NK * 64 : 1];
+  if constexpr (LF) {
+    const int w = threadIdx.x >> 6;
+    for (int tile = w; tile < MT * NK; tile += WAVES) {   // tile (mt, k): W^T (k < KT) | U^T
+      const int mt = tile / NK, k = tile % NK;
+      f32x4 t4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (k < KT) {
+          const int f = 16 * k + 4 * g + j;
+          t4[j] = BX ? wt_elem_bx(a.W, a.b, G4, a.IN, f, 16 * mt + c) : (f < a.IN ? a.W[(int64_t)f * G4 + 16 * mt + c] : 0.f);
+        } else {
+          t4[j] = a.Uw[(16 * (k - KT) + 4 * g + j) * G4 + 16 * mt + c];
+        }
+      }
+      lfw[tile * 64 + lane] = pack4(t4);
+    }
+    __syncthreads();   // before any wave leaves
+  }
   const int64_t s0 = ((int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * 16;
   if (s0 >= a.B) return;  // wave-uniform
   const int64_t seq = s0 + c;
@@ -41,10 +65,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
   const int IN = a.IN, T = a.T;
 
   // A fragments: W^T[m = gate][k = feature], U^T[m = gate][k = unit]
-  bf16x4 wt[MT][KT], ut[MT][UB];
+  constexpr int MR = LF ? 1 : MT;   // register fragments (none under LF)
+  bf16x4 wt[MR][KT], ut[MR][UB];
   f32x4 bias[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
+    if constexpr (LF) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bias[mt][i] = BX ? 0.f : a.b[16 * mt + 4 * g + i];
+      continue;
+    } else {
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) {
       f32x4 t4;
@@ -64,6 +94,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) bias[mt][i] = BX ? 0.f : a.b[16 * mt + 4 * g + i];
+    }
   }
   bf16x4 onex[KT];   // BX: the constant-1 bits of x columns IN, IN + 1
 #pragma unroll
@@ -106,20 +137,24 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd_kernel(FusedFwdA
       if constexpr (BX) xb[kt] |= onex[kt];
     }
     load_x(t + PF < T ? t + PF : T - 1, xin);   // in flight for PF steps
+    const int ol = opaque_lane(lane);   // LF: per step, so the fragment reads stay in the loop
+    auto fr = [&](int mt, int k) -> bf16x4 {   // A fragment of K tile k (x side k < KT, then h side)
+      if constexpr (LF) return lfw[(mt * NK + k) * 64 + ol];
+      else return k < KT ? wt[mt][k] : ut[mt][k - KT];
+    };
     f32x4 z[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       // z = b + [W ; U]^T . [x_t ; h_{t-1}]^T: the KT + UB K-tiles taken in pairs on the
       // 16x16x32 MFMA (the backward's gate recompute uses the identical pairing)
       z[mt] = BX ? f32x4{0.f, 0.f, 0.f, 0.f} : bias[mt];
-      constexpr int NK = KT + UB;
 #pragma unroll
       for (int k = 0; k + 1 < NK; k += 2)
-        z[mt] = mfma32(k < KT ? wt[mt][k] : ut[mt][k - KT], k + 1 < KT ? wt[mt][k + 1] : ut[mt][k + 1 - KT],
-                       k < KT ? xb[k] : hb[k - KT], k + 1 < KT ? xb[k + 1] : hb[k + 1 - KT], z[mt]);
+        z[mt] = mfma32(fr(mt, k), fr(mt, k + 1), k < KT ? xb[k] : hb[k - KT], k + 1 < KT ? xb[k + 1] : hb[k + 1 - KT],
+                       z[mt]);
       // odd tile count: the last tile against a zero tile, still on 16x16x32 -- a 16x16x16
       // whose SrcC is a 16x16x32 result miscomputed here (ROCm 7.2, gfx950; measured)
-      if constexpr (NK & 1) z[mt] = mfma32(ut[mt][UB - 1], bf16x4{0, 0, 0, 0}, hb[UB - 1], bf16x4{0, 0, 0, 0}, z[mt]);
+      if constexpr (NK & 1) z[mt] = mfma32(fr(mt, NK - 1), bf16x4{0, 0, 0, 0}, hb[UB - 1], bf16x4{0, 0, 0, 0}, z[mt]);
     }
     // hseq and cseq are padded to whole waves: padding lanes write their own rows,
     // so no store sits under a lane mask (a masked store makes the number of
