@@ -200,7 +200,8 @@ def measure_lstm_seq50_infer(device, n_events: int, repeats: int = 3, qps: float
             host, done, comp = srv.latency_us(ev[warm:], keys[warm:], qps=qps, device_breakdown=True)
             runs.append({"p50_us": float(np.percentile(host, 50)), "p99_us": float(np.percentile(host, 99)),
                          "device_p50_us": float(np.percentile(done, 50)),
-                         "device_compute_p50_us": float(np.percentile(comp, 50))})
+                         "device_window_p50_us": float(np.percentile(srv.last_device_load_us, 50)),
+                         "device_stack_p50_us": float(np.percentile(comp, 50))})
     p50s = [r["p50_us"] for r in runs]
     return {"p50_us": float(np.median(p50s)), "p99_us": max(r["p99_us"] for r in runs),
             "p50_spread_us": [min(p50s), max(p50s)], "runs": runs, "events_per_run": n_events, "offered_qps": qps,

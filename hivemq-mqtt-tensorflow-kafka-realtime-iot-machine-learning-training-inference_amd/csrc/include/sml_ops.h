@@ -70,6 +70,18 @@ hipError_t rowgemm_launch(const void* X, int x_bf16, int64_t M, int K, int64_t l
 hipError_t wgrad_launch(const void* X, int x_bf16, int64_t M, int K, int64_t ldx, int shift_T, const void* DY,
                         int dy_bf16, int N, int64_t ldy, int want_db, float* partials, int grid, hipStream_t stream);
 
+// ---- general LDS-tiled MFMA GEMM (gemm.hip) ----
+// C[M, N] = act(op(A)[M, K] . op(B)[K, N] + bias), operands fp32 or bf16:
+//   a_kc: A element (m, k) at A[m * lda + k] (else A[k * lda + m]);
+//   b_kc: B element (k, n) at B[n * ldb + k] (else B[k * ldb + n]).
+// splits > 1: split-K into `partials` ([splits, M, round4(N)] fp32; bias / act / C unused),
+// reduced by slab_sum_launch.
+hipError_t gemm_launch(const void* A, int a_bf16, int64_t lda, int a_kc, const void* B, int b_bf16, int64_t ldb,
+                       int b_kc, int64_t M, int64_t N, int64_t K, const float* bias, int act, void* C, int c_bf16,
+                       int64_t ldc, float* partials, int splits, hipStream_t stream);
+int gemm_auto_splits(int64_t M, int64_t N, int64_t K, int cus);
+
+
 // ---- fully fused LSTM layer (lstm_fused.hip) ----
 bool lstm_fused_supported(int U, int IN);
 int lstm_fused_slab(int U, int IN);

@@ -21,6 +21,18 @@
 // threads t < u update unit t's cell state in a register.  Two workgroup barriers per
 // step.  Weights, biases, the window and the activations live in LDS.
 //
+// Stacks of up to four LSTM layers (every one but the last returning sequences) under
+// one Dense head -- BASELINE config 3's LSTM(32) -> LSTM(16) -> Dense(18) at look_back 50
+// -- take the PIPELINED variant instead: wave l runs LSTM layer l over the window with no
+// workgroup barrier inside the recurrence.  Lane (p, j) = (lane >> 5, lane & 31) computes
+// two gates of unit j -- (i, g~) on p = 0, (f, o) on p = 1 -- as one packed-fp32 dot
+// product (v_pk_fma_f32) against its [W ; U] columns held in registers; the halves meet
+// through one permlane32 swap.  h_t goes to the layer's LDS sequence buffer, then a
+// release fence and the layer's step counter; layer l + 1 spins on that counter
+// (acquire) and consumes h_t while layer l computes step t + 1, so an event costs
+// ~T + L - 1 step latencies instead of L x T steps with two barriers each.  The last
+// layer's wave applies the Dense head to h_{T-1}.
+//
 // Exit conditions every wave reaches: the host's stop flag or `idle` without a request
 // (decided by wave 0, broadcast through LDS at the next barrier).
 #include <cstdlib>
@@ -56,6 +68,7 @@ __device__ __forceinline__ void st_agent(T* p, T v) {
 __device__ __forceinline__ float act_lstm(int a, float z) { return a == ACT_RELU ? fmaxf(z, 0.f) : tanhf(z); }
 
 struct Smem {
+  float* H;       // PIPE: [MAXLSTM][MAXT][MAXW] per-layer h sequences
   float* w;       // all parameters, Keras order
   float* seqa;    // [MAXT][MAXW]
   float* seqb;    // [MAXT][MAXW]
@@ -68,8 +81,29 @@ struct Smem {
   int* ctl;       // [8]: quit, key, count, seen sequence, t_seen lo / hi
 };
 
+// a.L is a pipelinable stack: n LSTM layers (u, in <= 32, n <= MAXLSTM, all but the last
+// returning sequences), then exactly one Dense head; returns n (0: not pipelinable)
+__host__ __device__ inline int pipe_layers(const LstmServeArgs& a) {
+  int n = 0;
+  while (n < a.nl && a.L[n].kind == LS_LSTM) ++n;
+  if (n < 1 || n > MAXLSTM || n + 1 != a.nl || a.L[n].kind != LS_DENSE || a.L[n].u > MAXW) return 0;
+  for (int l = 0; l < n; ++l)
+    if (a.L[l].u > 32 || a.L[l].in > 32 || (l + 1 < n && !a.L[l].ret)) return 0;
+  return n;
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 fma2(float x, f32x2 w, f32x2 acc) {
+  return __builtin_elementwise_fma(f32x2{x, x}, w, acc);
+}
+
+template <bool PIPE>
 __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem_f[];
+  // PIPE step counters and the zero h_{-1} row: static LDS, so volatile accesses stay ds_*
+  // operations (a generic pointer into the dynamic block made them flat system-scope ones)
+  __shared__ int s_rdy[MAXLSTM];
+  __shared__ __attribute__((aligned(16))) float s_zrow[MAXW];
   Smem S;
   S.w = smem_f;
   const int nwp = (a.nw + 3) & ~3;
@@ -82,6 +116,7 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
   S.sc = S.xrow + MAXW;
   S.sh = S.sc + MAXW;
   S.ctl = reinterpret_cast<int*>(S.sh + MAXW);
+  S.H = reinterpret_cast<float*>(S.ctl + 8);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int half = lane >> 5;
   const int gate = wid * 32 + (lane & 31);
@@ -93,10 +128,34 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
   }
   if (tid < 64) S.v[tid] = 0.f;   // [x ; h] past I + u stays 0 (its weights are 0: no 0 * garbage)
   if (tid < 8) S.ctl[tid] = 0;
+  if constexpr (PIPE) {
+    // padded columns (past a layer's width) are read against zero weights: keep them 0
+    for (int i = tid; i < MAXLSTM * MAXT * MAXW; i += NT) S.H[i] = 0.f;
+    for (int i = tid; i < MAXT * MAXW; i += NT) S.seqa[i] = 0.f;
+    if (tid < MAXW) s_zrow[tid] = 0.f;
+  }
   __syncthreads();
+  const int npipe = PIPE ? pipe_layers(a) : 0;
+  // PIPE: wave wid's layer, lane (p, j): wp[k] = ([W ; U][k][gate A], [W ; U][k][gate B]),
+  // k < 32 input rows, 32 + k recurrent rows; gates A | B = i | g~ (p = 0), f | o (p = 1)
+  f32x2 wp[64], bp = {0.f, 0.f};
+  if constexpr (PIPE) {
+    if (wid < npipe) {
+      const LstmServeLayer& L = a.L[wid];
+      const int G = 4 * L.u, j = lane & 31, p = lane >> 5;
+      const int ca = p * L.u + j, cb = (2 + p) * L.u + j;
+      const bool ok = j < L.u;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        wp[k] = (ok && k < L.in) ? f32x2{S.w[L.woff + k * G + ca], S.w[L.woff + k * G + cb]} : f32x2{0.f, 0.f};
+        wp[32 + k] = (ok && k < L.u) ? f32x2{S.w[L.uoff + k * G + ca], S.w[L.uoff + k * G + cb]} : f32x2{0.f, 0.f};
+      }
+      if (ok) bp = f32x2{S.w[L.boff + ca], S.w[L.boff + cb]};
+    }
+  }
   // register-resident weight halves of every LSTM layer: k = 32 * half + i of [W ; U]
   float wr[MAXLSTM][32], br[MAXLSTM];
-  {
+  if constexpr (!PIPE) {
     int li = 0;
     for (int l = 0; l < a.nl; ++l) {
       const LstmServeLayer& L = a.L[l];
@@ -134,8 +193,9 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
     const int slot = (int)(tail % (uint64_t)a.nslots);
     const uint32_t want = (uint32_t)(tail + 1);
     {
-      volatile int* seen = &S.ctl[3];
-      volatile int* quit_f = &S.ctl[0];
+      typedef __attribute__((address_space(3))) volatile int lds_vint;   // ds_* accesses, not flat
+      lds_vint* seen = (lds_vint*)&S.ctl[3];
+      lds_vint* quit_f = (lds_vint*)&S.ctl[0];
       const uint64_t* wp = &a.req[slot].w[lane & 31];
       // ~0.25 / 0.5 / 0.75 us: s_sleep takes an immediate
       if (wid == 1) __builtin_amdgcn_s_sleep(10);
@@ -192,6 +252,7 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
       }
     }
     if (wid == 0) err = wave_sum(err);
+    if (PIPE && tid < MAXLSTM) s_rdy[tid] = 0;
     // ---------------- the window, oldest first, into seqa [t][k] (the newest row from LDS)
     if (full) {
       for (int e = tid; e < T * D; e += NT) {
@@ -200,7 +261,88 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
       }
     }
     __syncthreads();
-    if (full) {
+    const uint64_t t_rec = __builtin_amdgcn_s_memrealtime();   // key state + window gathered
+    if (PIPE && full) {
+      // the wave's layer as a scalar: layer fields in SGPRs, uniform branches
+      const int lw = __builtin_amdgcn_readfirstlane(wid);
+      if (lw < npipe) {
+        const LstmServeLayer& L = a.L[lw];
+        const int u = L.u, relu = L.act == ACT_RELU;
+        const int nI4 = (L.in + 3) >> 2, nU4 = (u + 3) >> 2;
+        const float* xin = lw == 0 ? S.seqa : S.H + (lw - 1) * MAXT * MAXW;
+        float* hout = S.H + lw * MAXT * MAXW;
+        typedef __attribute__((address_space(3))) volatile int lds_vint;
+        lds_vint* rdy = (lds_vint*)s_rdy;   // ds_read / ds_write, never a flat access
+        float c = 0.f;
+        for (int t = 0; t < T; ++t) {
+          if (lw > 0) {   // the layer below has published h_t
+            while (rdy[lw - 1] <= t) {
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          }
+          // every 16-byte read first (padded columns are zero), then the FMAs under scalar
+          // branches: one LDS wait per step instead of one per read
+          const float4* x4 = reinterpret_cast<const float4*>(xin + t * MAXW);
+          const float4* h4 = reinterpret_cast<const float4*>(t > 0 ? hout + (t - 1) * MAXW : s_zrow);
+          float4 xv[8], hv[8];
+#pragma unroll
+          for (int k4 = 0; k4 < 8; ++k4) {
+            xv[k4] = x4[k4];
+            hv[k4] = h4[k4];
+          }
+          f32x2 acc[8];
+          acc[0] = bp;
+#pragma unroll
+          for (int q = 1; q < 8; ++q) acc[q] = f32x2{0.f, 0.f};
+#pragma unroll
+          for (int k4 = 0; k4 < 8; ++k4) {
+            if (k4 < nI4) {
+              acc[(2 * k4) & 7] = fma2(xv[k4].x, wp[4 * k4 + 0], acc[(2 * k4) & 7]);
+              acc[(2 * k4 + 1) & 7] = fma2(xv[k4].y, wp[4 * k4 + 1], acc[(2 * k4 + 1) & 7]);
+              acc[(2 * k4) & 7] = fma2(xv[k4].z, wp[4 * k4 + 2], acc[(2 * k4) & 7]);
+              acc[(2 * k4 + 1) & 7] = fma2(xv[k4].w, wp[4 * k4 + 3], acc[(2 * k4 + 1) & 7]);
+            }
+          }
+#pragma unroll
+          for (int k4 = 0; k4 < 8; ++k4) {
+            if (k4 < nU4) {
+              const int q0 = (2 * k4 + 4) & 7, q1 = (2 * k4 + 5) & 7;
+              acc[q0] = fma2(hv[k4].x, wp[32 + 4 * k4 + 0], acc[q0]);
+              acc[q1] = fma2(hv[k4].y, wp[32 + 4 * k4 + 1], acc[q1]);
+              acc[q0] = fma2(hv[k4].z, wp[32 + 4 * k4 + 2], acc[q0]);
+              acc[q1] = fma2(hv[k4].w, wp[32 + 4 * k4 + 3], acc[q1]);
+            }
+          }
+          const f32x2 z = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+          // p = 0 lanes: (i, g~) here, (f, o) from lane + 32
+          const float zf = xor32(z.x, lane), zo = xor32(z.y, lane);
+          const float ig = sigmoid_fast(z.x), fg = sigmoid_fast(zf), og = sigmoid_fast(zo);
+          float h;
+          if (relu) {
+            c = fmaf(fg, c, ig * fmaxf(z.y, 0.f));
+            h = og * fmaxf(c, 0.f);
+          } else {
+            c = fmaf(fg, c, ig * tanh_fast(z.y));
+            h = og * tanh_fast(c);
+          }
+          if (lane < u) hout[t * MAXW + lane] = h;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) rdy[lw] = t + 1;
+        }
+        if (lw == npipe - 1) {   // Dense head on h_{T-1}
+          const LstmServeLayer& Hd = a.L[npipe];
+          const float* hl = hout + (T - 1) * MAXW;
+          if (lane < Hd.u) {
+            float acc = S.w[Hd.boff + lane];
+#pragma unroll
+            for (int k = 0; k < 32; ++k)
+              if (k < Hd.in) acc = fmaf(hl[k], S.w[Hd.woff + k * Hd.u + lane], acc);
+            S.pred[lane] = acc;
+          }
+        }
+      }
+      __syncthreads();
+    } else if (full) {
       float* cur = S.seqa;
       float* nxt = S.seqb;
       int tcur = T, dim = D, li = 0;
@@ -285,7 +427,7 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
         st_agent(&a.hcount[key], cnt + 1);
         st_sys(&r->w[kServeScore], tagged(want, score));
         st_sys(&r->w[kServeFlag], tagged_u(want, flag));
-        st_sys(&r->w[kServeTLoad], tagged_u(want, 0u));
+        st_sys(&r->w[kServeTLoad], tagged_u(want, (uint32_t)(t_rec - t_seen)));
         st_sys(&r->w[kServeTComp], tagged_u(want, (uint32_t)(t_comp - t_seen)));
         st_sys(&r->w[kServeTDone], tagged_u(want, (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seen)));
         st_sys(&a.ctl->done, tail + 1);
@@ -505,7 +647,8 @@ bool lstm_serve_is_ref1(const LstmServeArgs& x) {
 
 size_t lstm_serve_lds_bytes(int nw) {
   const int nwp = (nw + 3) & ~3;
-  return (size_t)(nwp + 2 * MAXT * MAXW + 64 + 128 + 4 * MAXW) * sizeof(float) + 8 * sizeof(int);
+  return (size_t)(nwp + 2 * MAXT * MAXW + 64 + 128 + 4 * MAXW) * sizeof(float) + 8 * sizeof(int) +
+         (size_t)MAXLSTM * MAXT * MAXW * sizeof(float) + MAXLSTM * sizeof(int);   // PIPE sequences + counters
 }
 
 hipError_t lstm_serve_launch(const LstmServeArgs& args, hipStream_t stream) {
@@ -541,12 +684,16 @@ hipError_t lstm_serve_launch(const LstmServeArgs& args, hipStream_t stream) {
   }
   const size_t lds = lstm_serve_lds_bytes(args.nw);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
+  // stacks of LSTM layers under one Dense head: the pipelined variant (one wave per layer);
+  // SML_LSTM_SERVE_GENERIC=1 keeps the barrier-per-step kernel (A/B, cross-checks)
+  const bool pipe = pipe_layers(args) > 0 && !(gen && gen[0] == '1');
+  auto kern = pipe ? lstm_serve_kernel<true> : lstm_serve_kernel<false>;
   if (lds > 65536) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_serve_kernel),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(lstm_serve_kernel, dim3(1), dim3(NT), lds, stream, args);
+  hipLaunchKernelGGL(kern, dim3(1), dim3(NT), lds, stream, args);
   return hipGetLastError();
 }
 

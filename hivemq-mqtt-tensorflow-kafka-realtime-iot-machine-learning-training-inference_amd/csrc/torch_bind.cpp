@@ -636,6 +636,81 @@ std::vector<at::Tensor> dense_wgrad(const at::Tensor& x, const at::Tensor& dy, i
   return {dW, db};
 }
 
+// Orientation of one GEMM operand view: kc = 1 when the contraction dim has unit stride
+// (element (mn, k) at p[mn * ld + k]), kc = 0 when the mn dim has (p[k * ld + mn]); any
+// other strided view is made contiguous first.
+static at::Tensor gemm_operand(const at::Tensor& t, int mn_dim, int k_dim, int64_t& ld, int& kc) {
+  const int64_t smn = t.stride(mn_dim), sk = t.stride(k_dim), nmn = t.size(mn_dim), nk = t.size(k_dim);
+  if ((sk == 1 || nk <= 1) && (nmn <= 1 || smn >= nk)) {
+    kc = 1;
+    ld = nmn <= 1 ? std::max<int64_t>(nk, 1) : smn;
+    return t;
+  }
+  if ((smn == 1 || nmn <= 1) && (nk <= 1 || sk >= nmn)) {
+    kc = 0;
+    ld = nk <= 1 ? std::max<int64_t>(nmn, 1) : sk;
+    return t;
+  }
+  at::Tensor c = t.contiguous();
+  return gemm_operand(c, mn_dim, k_dim, ld, kc);
+}
+
+// General MFMA GEMM (gemm.hip): act(a . b + bias) for a [M, K], b [K, N] (fp32 or bf16,
+// either orientation -- transposed views need no copy).  splits: 1 = no split-K, > 1 =
+// that many K slices reduced deterministically, < 0 = choose from the shape (only when
+// there is no bias / activation and the output is fp32).
+at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias, int64_t act,
+                bool out_bf16, int64_t splits) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm needs ROCm device tensors");
+  for (const auto* t : {&a, &b})
+    TORCH_CHECK(t->dim() == 2 && (t->scalar_type() == at::kFloat || t->scalar_type() == at::kBFloat16),
+                "gemm operands must be 2-D fp32 or bf16");
+  TORCH_CHECK(a.size(1) == b.size(0), "gemm: inner dims differ (", a.size(1), " vs ", b.size(0), ")");
+  TORCH_CHECK(act >= 0 && act <= 3, "act must be 0..3");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(1);
+  if (bias.has_value()) {
+    check_dev(*bias, "bias", at::kFloat);
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "bias must be [N]");
+  }
+  c10::hip::HIPGuard guard(a.device().index());
+  int64_t lda = 0, ldb = 0;
+  int akc = 1, bkc = 1;
+  const at::Tensor A = gemm_operand(a, 0, 1, lda, akc);
+  const at::Tensor B = gemm_operand(b, 1, 0, ldb, bkc);
+  const int64_t Np = (N + 3) & ~int64_t(3);
+  const bool plain = !bias.has_value() && act == 0 && !out_bf16;
+  int s = 1;
+  if (plain && M * Np < (int64_t(1) << 31)) {
+    if (splits < 0) {
+      static const int cus = [] {
+        hipDeviceProp_t p;
+        return hipGetDeviceProperties(&p, 0) == hipSuccess ? p.multiProcessorCount : 256;
+      }();
+      s = sml::gemm_auto_splits(M, N, K, cus);
+    } else if (splits > 1) {
+      s = (int)std::min<int64_t>(splits, 4096);
+    }
+  }
+  auto st = cur_stream(a);
+  auto opts = a.options().dtype(at::kFloat);
+  if (s > 1) {
+    auto partials = at::empty({s, M * Np}, opts);
+    auto out = at::empty({M, Np}, opts);
+    auto scratch = at::empty({std::max(1, sml::slab_sum_scratch(s, (int)(M * Np)))}, opts);
+    SML_CHECK_HIP(sml::gemm_launch(A.data_ptr(), A.scalar_type() == at::kBFloat16, lda, akc, B.data_ptr(),
+                                   B.scalar_type() == at::kBFloat16, ldb, bkc, M, N, K, nullptr, 0, nullptr, 0, Np,
+                                   partials.data_ptr<float>(), s, st));
+    SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), s, (int)(M * Np), scratch.data_ptr<float>(),
+                                       out.data_ptr<float>(), st));
+    return Np == N ? out : out.narrow(1, 0, N);
+  }
+  auto c = at::empty({M, N}, a.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  SML_CHECK_HIP(sml::gemm_launch(A.data_ptr(), A.scalar_type() == at::kBFloat16, lda, akc, B.data_ptr(),
+                                 B.scalar_type() == at::kBFloat16, ldb, bkc, M, N, K, opt_ptr(bias), (int)act,
+                                 c.data_ptr(), out_bf16, N, nullptr, 1, st));
+  return c;
+}
+
 // Fully fused LSTM layer forward: x [B, T, IN] fp32 or bf16 -> (h [B,T,U] bf16, c: bf16
 // cell state for lstm_fused_bwd).
 std::vector<at::Tensor> lstm_fused_fwd(const at::Tensor& x, const at::Tensor& W, const at::Tensor& Uw,
@@ -1331,6 +1406,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dense_wgrad", &dense_wgrad, "K2 weight gradient X^T.dY (+ colsum dY) over rows", py::arg("x"),
         py::arg("dy"), py::arg("shift_T") = 0, py::arg("want_db") = true, py::arg("max_blocks") = 1024,
         py::arg("grad") = py::none(), py::arg("map") = py::none());
+  m.def("gemm", &gemm, "general LDS-tiled MFMA GEMM act(a . b + bias), any shape / orientation", py::arg("a"),
+        py::arg("b"), py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("out_bf16") = false,
+        py::arg("splits") = -1);
   m.def("dense_wgrad_slab", &sml::dense_wgrad_slab, "floats per dense_wgrad slab", py::arg("K"), py::arg("N"));
   m.def("dense_tiles", &sml::dense_tiles, "16-wide tiles a dense dimension is padded to", py::arg("d"));
   m.def("lstm_fused_slab", &sml::lstm_fused_slab, "floats per fused-LSTM weight-gradient slab", py::arg("U"),

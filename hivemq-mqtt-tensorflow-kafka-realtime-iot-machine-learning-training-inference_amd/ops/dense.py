@@ -5,8 +5,9 @@
 activation derivative, one ``dense_wgrad`` launch (dW and db in one pass over the
 rows) and one ``dense_fwd`` launch against W^T for dX.  Layers whose weight does
 not fit the register-resident tile (K or N beyond 128..256, e.g. MNIST's 784 x
-128) are routed to hipBLASLt, where those shapes are efficient; on CPU the
-reference torch ops run.
+128) run on the general LDS-tiled MFMA GEMM (``ops/gemm.py``, ``csrc/kernels/gemm.hip``):
+forward with bias + activation in its epilogue, dW = x^T . dz split over the rows,
+dX = dz . W^T from transposed views; on CPU the reference torch ops run.
 """
 from __future__ import annotations
 
@@ -14,6 +15,7 @@ from typing import Optional, Tuple
 
 import torch
 
+from . import gemm as gm
 from ._ext import load_c
 
 ACT = {"linear": 0, None: 0, "relu": 1, "tanh": 2, "sigmoid": 3}
@@ -77,6 +79,33 @@ class DenseFunction(torch.autograd.Function):
         return dx, dW, (db if ctx.has_b else None), None
 
 
+class GemmDenseFunction(torch.autograd.Function):
+    """Dense layer on the general MFMA GEMM (layers wider than the K1/K2 register tile)."""
+
+    @staticmethod
+    def forward(ctx, x2, W, b, act: str):
+        y = gm.matmul(x2, W, b, act)
+        ctx.save_for_backward(x2, W, y)
+        ctx.act = act
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, W, y = ctx.saved_tensors
+        dz = _act_grad(ctx.act, y, dy.contiguous()).contiguous()
+        dW = db = dx = None
+        if ctx.needs_input_grad[1]:
+            dW = gm.matmul(x2.t(), dz)           # split over the rows, deterministic
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = dz.sum(0)
+        if ctx.needs_input_grad[0]:
+            dx = gm.matmul(dz, W.t())            # W^T read in place
+            if x2.dtype != dx.dtype:
+                dx = dx.to(x2.dtype)
+        return dx, dW, db, None
+
+
 def dense(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None, act: str = "linear") -> torch.Tensor:
     """Dense layer over the last axis of ``x`` (any leading shape)."""
     K, N = W.shape
@@ -88,11 +117,11 @@ def dense(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None, ac
         if x2.stride(-1) != 1:
             x2 = x2.contiguous()
         return DenseFunction.apply(x2, W, b, act).reshape(*lead, N)
-    if x.is_cuda:   # large layers: hipBLASLt (bias fused into the GEMM epilogue)
-        from ._ext import note_fallback
-        note_fallback(f"dense[{K}x{N}]")
-        z = torch.addmm(b, x.reshape(-1, K), W) if b is not None else x.reshape(-1, K) @ W
-        return _act_torch(act, z).reshape(*lead, N)
+    if x.is_cuda:   # wider layers: general MFMA GEMM (bias + activation in its epilogue)
+        x2 = x.reshape(-1, K)
+        if x2.dtype not in (torch.float32, torch.bfloat16):
+            x2 = x2.float()
+        return GemmDenseFunction.apply(x2, W, b, act).reshape(*lead, N)
     z = x @ W
     if b is not None:
         z = z + b

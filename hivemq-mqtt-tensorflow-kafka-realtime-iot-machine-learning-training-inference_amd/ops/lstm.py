@@ -25,6 +25,7 @@ from __future__ import annotations
 import torch
 
 from . import dense as dn
+from . import gemm as gm
 from ._ext import load_c
 
 ACT = {"relu": 1, "tanh": 2}
@@ -55,15 +56,14 @@ def lstm_reference(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.T
 
 
 def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """bf16 MFMA GEMM via hipBLASLt, fp32 result (shapes beyond the K1/K2 register tile)."""
-    from ._ext import note_fallback
-    note_fallback(f"lstm_mm[{tuple(a.shape)}x{tuple(b.shape)}]")
-    return (a.to(torch.bfloat16) @ b.to(torch.bfloat16)).float()
+    """bf16 MFMA GEMM, fp32 result, on the general LDS-tiled kernel (``ops/gemm.py``) for
+    shapes beyond the K1/K2 register tile; transposed views are read in place."""
+    return gm.matmul(a, b)
 
 
 class LSTMFunction(torch.autograd.Function):
     """Input projection / weight gradients / dX on the K1/K2 tall-skinny kernels
-    (hipBLASLt when a layer is too wide for them), recurrence on lstm_fwd/lstm_bwd."""
+    (the general MFMA GEMM when a layer is too wide for them), recurrence on lstm_fwd/lstm_bwd."""
 
     @staticmethod
     def forward(ctx, x, W, U, b, act_code: int):
@@ -74,7 +74,7 @@ class LSTMFunction(torch.autograd.Function):
         if fast:
             zx = dn.rowgemm(x2, W, b).reshape(B, T, 4 * u)
         else:
-            zx = (_mm(x2, W) + b).reshape(B, T, 4 * u).contiguous()
+            zx = gm.matmul(x2, W, b).reshape(B, T, 4 * u)
         h, c, gates = load_c().lstm_fwd(zx, U.contiguous(), None, None, act_code)
         ctx.save_for_backward(x, W, U, h, c, gates)
         ctx.act = act_code

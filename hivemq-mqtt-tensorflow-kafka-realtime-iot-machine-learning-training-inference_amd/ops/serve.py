@@ -136,6 +136,9 @@ class LSTMScoringServer:
         gap = int(1e9 / qps) if qps > 0 else 0
         out = self._s.latency_run(np.ascontiguousarray(np.asarray(rows, np.float32)), gap,
                                   np.ascontiguousarray(np.asarray(keys, np.int64))) / 1e3
+        # device phases of the last run: pick-up -> key state and window gathered ("load"),
+        # then the stack over the window ("compute")
+        self.last_device_load_us = out[:, 2]
         if device_breakdown:
             return out[:, 0], out[:, 1], out[:, 3]
         return out[:, 0]

@@ -249,3 +249,38 @@ def test_lstm_kafka_low_latency_path_matches_oracle(cuda_device, stack, T):
             else:
                 assert not got.any()
     assert checked >= n - ncar * T
+
+
+@pytest.mark.parametrize("stack,T", [
+    ([("lstm", 32, True, "relu"), ("lstm", 16, False, "relu"), ("dense", 18, False)], 50),   # config 3
+    ([("lstm", 32, True, "tanh"), ("lstm", 24, True, "tanh"), ("lstm", 16, False, "tanh"), ("dense", 18, False)], 20),
+    ([("lstm", 20, True, "tanh"), ("lstm", 32, True, "tanh"), ("dense", 18, False)], 7),   # TimeDistributed head
+    ([("lstm", 8, False, "relu"), ("dense", 18, False)], 64),
+])
+def test_pipelined_stack_kernel_matches_general_kernel(cuda_device, monkeypatch, stack, T):
+    """LSTM stacks under one Dense head run on the pipelined variant (one wave per layer,
+    step counters in LDS instead of barriers); SML_LSTM_SERVE_GENERIC=1 forces the
+    barrier-per-step kernel.  Same forecasts / scores / flags on an interleaved stream."""
+    from streamml.ops.serve import LSTMScoringServer
+    m = LSTMPredictor(look_back=T, stack=stack, device=cuda_device, seed=13)
+    rng = np.random.default_rng(T)
+    nkeys = 3
+    n = (T + 10) * nkeys
+    keys = rng.integers(0, nkeys, size=n)
+    raw = rng.uniform(0, 40, size=(n, 18)).astype(np.float32)
+    out = {}
+    for generic in ("0", "1"):
+        monkeypatch.setenv("SML_LSTM_SERVE_GENERIC", generic)
+        with LSTMScoringServer(m, nkeys=nkeys, threshold=0.05) as srv:
+            out[generic] = srv.forecast(raw, keys)
+    (pa, sa, fa), (pb, sb, fb) = out["0"], out["1"]
+    assert np.abs(pb).max() > 0
+    scale = max(np.abs(pb).max(), 1.0)
+    # fp32 with different summation orders: a 50-step random relu stack grows to |h| ~ 1e2..1e3
+    # and amplifies rounding chaotically (see test_lstm_serve_matches_oracle), so relu stacks
+    # get 0.5 % of the largest output; a wrong window, key or state is off by O(|f|)
+    relu = any(layer[0] == "lstm" and layer[3] == "relu" for layer in stack)
+    np.testing.assert_allclose(pa, pb, rtol=2e-4, atol=(5e-3 if relu else 2e-5) * scale)
+    np.testing.assert_allclose(sa, sb, rtol=2e-2 if relu else 1e-3, atol=1e-6, equal_nan=True)
+    agree = (fa == fb) | (np.abs(sa - 0.05) < (2e-2 if relu else 1e-3))
+    assert agree.all()
