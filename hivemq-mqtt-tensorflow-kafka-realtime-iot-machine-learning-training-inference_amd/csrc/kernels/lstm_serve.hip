@@ -51,6 +51,7 @@ constexpr int MAXW = 32;       // widest layer input / output
 constexpr int MAXT = 64;       // longest window
 constexpr int MAXLSTM = 4;     // LSTM layers with register-resident weights
 constexpr int KEY_WORD = 31;   // request word carrying the car key
+constexpr int ZX_RING = 8;     // PIPE: steps of input projection buffered ahead of a recurrence
 
 __device__ __forceinline__ float sigm(float z) { return 1.0f / (1.0f + __expf(-z)); }
 
@@ -103,7 +104,9 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
   // PIPE step counters and the zero h_{-1} row: static LDS, so volatile accesses stay ds_*
   // operations (a generic pointer into the dynamic block made them flat system-scope ones)
   __shared__ int s_rdy[MAXLSTM];
+  __shared__ int s_prj[2];   // PIPE with projection waves: steps each layer's x-projection has published
   __shared__ __attribute__((aligned(16))) float s_zrow[MAXW];
+  __shared__ __attribute__((aligned(16))) f32x2 s_zx[2][ZX_RING][64];   // x . W + b per lane, ring of steps
   Smem S;
   S.w = smem_f;
   const int nwp = (a.nw + 3) & ~3;
@@ -136,21 +139,32 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
   }
   __syncthreads();
   const int npipe = PIPE ? pipe_layers(a) : 0;
-  // PIPE: wave wid's layer, lane (p, j): wp[k] = ([W ; U][k][gate A], [W ; U][k][gate B]),
-  // k < 32 input rows, 32 + k recurrent rows; gates A | B = i | g~ (p = 0), f | o (p = 1)
+  // PIPE roles.  Stacks of one or two LSTM layers split every layer over two waves: wave l
+  // runs layer l's recurrence (h_{t-1} . U + the gates), wave 2 + l its input projection
+  // x_t . W + b, published per step through a ring in LDS -- the recurrence's critical chain
+  // then holds only the u recurrent terms.  Deeper stacks: wave l does both for layer l.
+  const bool split = npipe <= 2;
+  const int role_layer = !PIPE ? -1 : wid < npipe ? wid : (split && wid >= 2 && wid - 2 < npipe) ? wid - 2 : -1;
+  const bool role_proj = PIPE && split && wid >= 2;
+  // PIPE: the role's layer, lane (p, j): wp[k] = ([W ; U][k][gate A], [W ; U][k][gate B]),
+  // k < 32 input rows, 32 + k recurrent rows; gates A | B = i | g~ (p = 0), f | o (p = 1).
+  // A split recurrence wave keeps only the U rows, a projection wave only the W rows and b.
   f32x2 wp[64], bp = {0.f, 0.f};
   if constexpr (PIPE) {
-    if (wid < npipe) {
-      const LstmServeLayer& L = a.L[wid];
+    if (role_layer >= 0) {
+      const LstmServeLayer& L = a.L[role_layer];
+      const bool want_w = !split || role_proj, want_u = !split || !role_proj;
       const int G = 4 * L.u, j = lane & 31, p = lane >> 5;
       const int ca = p * L.u + j, cb = (2 + p) * L.u + j;
       const bool ok = j < L.u;
 #pragma unroll
       for (int k = 0; k < 32; ++k) {
-        wp[k] = (ok && k < L.in) ? f32x2{S.w[L.woff + k * G + ca], S.w[L.woff + k * G + cb]} : f32x2{0.f, 0.f};
-        wp[32 + k] = (ok && k < L.u) ? f32x2{S.w[L.uoff + k * G + ca], S.w[L.uoff + k * G + cb]} : f32x2{0.f, 0.f};
+        wp[k] = (want_w && ok && k < L.in) ? f32x2{S.w[L.woff + k * G + ca], S.w[L.woff + k * G + cb]}
+                                           : f32x2{0.f, 0.f};
+        wp[32 + k] = (want_u && ok && k < L.u) ? f32x2{S.w[L.uoff + k * G + ca], S.w[L.uoff + k * G + cb]}
+                                               : f32x2{0.f, 0.f};
       }
-      if (ok) bp = f32x2{S.w[L.boff + ca], S.w[L.boff + cb]};
+      if (want_w && ok) bp = f32x2{S.w[L.boff + ca], S.w[L.boff + cb]};
     }
   }
   // register-resident weight halves of every LSTM layer: k = 32 * half + i of [W ; U]
@@ -253,6 +267,7 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
     }
     if (wid == 0) err = wave_sum(err);
     if (PIPE && tid < MAXLSTM) s_rdy[tid] = 0;
+    if (PIPE && tid < 2) s_prj[tid] = 0;
     // ---------------- the window, oldest first, into seqa [t][k] (the newest row from LDS)
     if (full) {
       for (int e = tid; e < T * D; e += NT) {
@@ -265,42 +280,84 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
     if (PIPE && full) {
       // the wave's layer as a scalar: layer fields in SGPRs, uniform branches
       const int lw = __builtin_amdgcn_readfirstlane(wid);
-      if (lw < npipe) {
+      typedef __attribute__((address_space(3))) volatile int lds_vint;
+      lds_vint* rdy = (lds_vint*)s_rdy;   // ds_read / ds_write, never a flat access
+      lds_vint* prj = (lds_vint*)s_prj;
+      if (split && lw >= 2 && lw - 2 < npipe) {
+        // ---- input projection of layer pl: zx_t = x_t . W + b into the ring
+        const int pl = lw - 2;
+        const LstmServeLayer& L = a.L[pl];
+        const int nI4 = (L.in + 3) >> 2;
+        const float* xin = pl == 0 ? S.seqa : S.H + (pl - 1) * MAXT * MAXW;
+        for (int t = 0; t < T; ++t) {
+          if (pl > 0)   // the layer below has published h_t
+            while (rdy[pl - 1] <= t) {
+            }
+          if (t >= ZX_RING)   // ring slot free: the recurrence has finished step t - ZX_RING
+            while (rdy[pl] <= t - ZX_RING) {
+            }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          const float4* x4 = reinterpret_cast<const float4*>(xin + t * MAXW);
+          float4 xv[8];
+#pragma unroll
+          for (int k4 = 0; k4 < 8; ++k4) xv[k4] = x4[k4];
+          f32x2 acc[4] = {bp, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+          for (int k4 = 0; k4 < 8; ++k4) {
+            if (k4 < nI4) {
+              acc[0] = fma2(xv[k4].x, wp[4 * k4 + 0], acc[0]);
+              acc[1] = fma2(xv[k4].y, wp[4 * k4 + 1], acc[1]);
+              acc[2] = fma2(xv[k4].z, wp[4 * k4 + 2], acc[2]);
+              acc[3] = fma2(xv[k4].w, wp[4 * k4 + 3], acc[3]);
+            }
+          }
+          s_zx[pl][t % ZX_RING][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) prj[pl] = t + 1;
+        }
+      } else if (lw < npipe) {
         const LstmServeLayer& L = a.L[lw];
         const int u = L.u, relu = L.act == ACT_RELU;
-        const int nI4 = (L.in + 3) >> 2, nU4 = (u + 3) >> 2;
+        const int nI4 = split ? 0 : (L.in + 3) >> 2, nU4 = (u + 3) >> 2;
         const float* xin = lw == 0 ? S.seqa : S.H + (lw - 1) * MAXT * MAXW;
         float* hout = S.H + lw * MAXT * MAXW;
-        typedef __attribute__((address_space(3))) volatile int lds_vint;
-        lds_vint* rdy = (lds_vint*)s_rdy;   // ds_read / ds_write, never a flat access
         float c = 0.f;
         for (int t = 0; t < T; ++t) {
-          if (lw > 0) {   // the layer below has published h_t
+          if (split) {   // this step's input projection is in the ring
+            while (prj[lw] <= t) {
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          } else if (lw > 0) {   // the layer below has published h_t
             while (rdy[lw - 1] <= t) {
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
           }
-          // every 16-byte read first (padded columns are zero), then the FMAs under scalar
+          // every LDS read first (padded columns are zero), then the FMAs under scalar
           // branches: one LDS wait per step instead of one per read
           const float4* x4 = reinterpret_cast<const float4*>(xin + t * MAXW);
           const float4* h4 = reinterpret_cast<const float4*>(t > 0 ? hout + (t - 1) * MAXW : s_zrow);
           float4 xv[8], hv[8];
-#pragma unroll
-          for (int k4 = 0; k4 < 8; ++k4) {
-            xv[k4] = x4[k4];
-            hv[k4] = h4[k4];
-          }
           f32x2 acc[8];
-          acc[0] = bp;
+          if (split) {
+            acc[0] = s_zx[lw][t % ZX_RING][lane];
+          } else {
+            acc[0] = bp;
+#pragma unroll
+            for (int k4 = 0; k4 < 8; ++k4) xv[k4] = x4[k4];
+          }
+#pragma unroll
+          for (int k4 = 0; k4 < 8; ++k4) hv[k4] = h4[k4];
 #pragma unroll
           for (int q = 1; q < 8; ++q) acc[q] = f32x2{0.f, 0.f};
+          if (!split) {
 #pragma unroll
-          for (int k4 = 0; k4 < 8; ++k4) {
-            if (k4 < nI4) {
-              acc[(2 * k4) & 7] = fma2(xv[k4].x, wp[4 * k4 + 0], acc[(2 * k4) & 7]);
-              acc[(2 * k4 + 1) & 7] = fma2(xv[k4].y, wp[4 * k4 + 1], acc[(2 * k4 + 1) & 7]);
-              acc[(2 * k4) & 7] = fma2(xv[k4].z, wp[4 * k4 + 2], acc[(2 * k4) & 7]);
-              acc[(2 * k4 + 1) & 7] = fma2(xv[k4].w, wp[4 * k4 + 3], acc[(2 * k4 + 1) & 7]);
+            for (int k4 = 0; k4 < 8; ++k4) {
+              if (k4 < nI4) {
+                acc[(2 * k4) & 7] = fma2(xv[k4].x, wp[4 * k4 + 0], acc[(2 * k4) & 7]);
+                acc[(2 * k4 + 1) & 7] = fma2(xv[k4].y, wp[4 * k4 + 1], acc[(2 * k4 + 1) & 7]);
+                acc[(2 * k4) & 7] = fma2(xv[k4].z, wp[4 * k4 + 2], acc[(2 * k4) & 7]);
+                acc[(2 * k4 + 1) & 7] = fma2(xv[k4].w, wp[4 * k4 + 3], acc[(2 * k4 + 1) & 7]);
+              }
             }
           }
 #pragma unroll
@@ -683,7 +740,7 @@ hipError_t lstm_serve_launch(const LstmServeArgs& args, hipStream_t stream) {
     return hipGetLastError();
   }
   const size_t lds = lstm_serve_lds_bytes(args.nw);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds + 9 * 1024 > 160 * 1024) return hipErrorInvalidValue;   // + the PIPE kernel's static LDS (8.2 KB)
   // stacks of LSTM layers under one Dense head: the pipelined variant (one wave per layer);
   // SML_LSTM_SERVE_GENERIC=1 keeps the barrier-per-step kernel (A/B, cross-checks)
   const bool pipe = pipe_layers(args) > 0 && !(gen && gen[0] == '1');
