@@ -235,6 +235,184 @@ __global__ __launch_bounds__(WAVES * 64) void lstm_bwd_kernel(LstmBwdArgs<U> a) 
   }
 }
 
+// ---------------------------------------------------------------------------
+// U = 128: the recurrent weight no longer fits one wave (4U x U bf16 = 256 VGPRs of
+// fragments), so FOUR waves share each 16-sequence tile.  Wave w owns units 32w..32w+31
+// (unit blocks 2w, 2w+1): the i / f / c~ / o gate tiles of those units (8 of the 32 gate
+// tiles) with their U^T fragments over all 8 unit k-steps in registers (128 VGPRs).  Per
+// step each wave computes its 8 gate tiles (64 MFMAs), updates its units' h / c, and
+// publishes its two bf16 h blocks through a double-buffered LDS image that every wave
+// reads back as the next step's B operand: one barrier per step.  The backward mirrors
+// it: each wave forms dz for its own gate tiles, the bf16 dz tiles meet in LDS, and
+// dh for the wave's units = U[units][all gates] . dz^T (64 MFMAs).
+// ---------------------------------------------------------------------------
+constexpr int SU = 128, SG4 = 4 * SU, SMT = SG4 / 16, SUB = SU / 16;
+
+__global__ __launch_bounds__(256) void lstm_fwd_split_kernel(LstmArgs<SU> a) {
+  __shared__ bf16x4 hbuf[2][SUB][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int64_t s0 = (int64_t)blockIdx.x * 16;   // block-uniform
+  const int64_t seq = s0 + c;
+  const bool valid = seq < a.B;
+  const int64_t sq = valid ? seq : a.B - 1;
+  // local tile li = 2q + j: gate q of unit block b = 2w + j, global gate tile q * SUB + b
+  bf16x4 ut[8][SUB];
+#pragma unroll
+  for (int li = 0; li < 8; ++li) {
+    const int mt = (li >> 1) * SUB + 2 * w + (li & 1);
+#pragma unroll
+    for (int s = 0; s < SUB; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        ut[li][s][j] = __builtin_bit_cast(short, (__bf16)a.Uw[(16 * s + 4 * g + j) * SG4 + 16 * mt + c]);
+  }
+  f32x4 h[2], cs[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = 16 * (2 * w + j) + 4 * g + i;
+      h[j][i] = a.h0 ? a.h0[sq * SU + u] : 0.f;
+      cs[j][i] = a.c0 ? a.c0[sq * SU + u] : 0.f;
+    }
+    hbuf[0][2 * w + j][lane] = pack4(h[j]);
+  }
+  const float* zrow = a.zx + sq * (int64_t)a.T * SG4;
+  f32x4 znext[8];
+#pragma unroll
+  for (int li = 0; li < 8; ++li) {
+    const int mt = (li >> 1) * SUB + 2 * w + (li & 1);
+    znext[li] = *reinterpret_cast<const f32x4*>(zrow + 16 * mt + 4 * g);
+  }
+  __syncthreads();
+  for (int t = 0; t < a.T; ++t) {
+    const int cur = t & 1;
+    f32x4 z[8];
+#pragma unroll
+    for (int li = 0; li < 8; ++li) z[li] = znext[li];
+    if (t + 1 < a.T) {
+#pragma unroll
+      for (int li = 0; li < 8; ++li) {
+        const int mt = (li >> 1) * SUB + 2 * w + (li & 1);
+        znext[li] = *reinterpret_cast<const f32x4*>(zrow + (int64_t)(t + 1) * SG4 + 16 * mt + 4 * g);
+      }
+    }
+    bf16x4 hb[SUB];
+#pragma unroll
+    for (int s = 0; s < SUB; ++s) hb[s] = hbuf[cur][s][lane];
+#pragma unroll
+    for (int li = 0; li < 8; ++li)
+#pragma unroll
+      for (int s = 0; s < SUB; ++s) z[li] = mfma16(ut[li][s], hb[s], z[li]);
+    const int64_t base_g = (sq * a.T + t) * (int64_t)SG4;
+    const int64_t base_u = (sq * a.T + t) * (int64_t)SU;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      f32x4 gi, gf, gc, go;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        gi[i] = sig(z[0 + j][i]);
+        gf[i] = sig(z[2 + j][i]);
+        gc[i] = act_f(a.act, z[4 + j][i]);
+        go[i] = sig(z[6 + j][i]);
+        cs[j][i] = fmaf(gf[i], cs[j][i], gi[i] * gc[i]);
+        h[j][i] = go[i] * act_f(a.act, cs[j][i]);
+      }
+      const int off = 16 * (2 * w + j) + 4 * g;
+      if (valid) {
+        *reinterpret_cast<f32x4*>(a.gates + base_g + off) = gi;
+        *reinterpret_cast<f32x4*>(a.gates + base_g + SU + off) = gf;
+        *reinterpret_cast<f32x4*>(a.gates + base_g + 2 * SU + off) = gc;
+        *reinterpret_cast<f32x4*>(a.gates + base_g + 3 * SU + off) = go;
+        *reinterpret_cast<f32x4*>(a.cseq + base_u + off) = cs[j];
+        *reinterpret_cast<f32x4*>(a.hseq + base_u + off) = h[j];
+      }
+      hbuf[cur ^ 1][2 * w + j][lane] = pack4(h[j]);   // read after this step's barrier
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void lstm_bwd_split_kernel(LstmBwdArgs<SU> a) {
+  __shared__ bf16x4 dzbuf[2][SMT][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int64_t s0 = (int64_t)blockIdx.x * 16;
+  const int64_t seq = s0 + c;
+  const bool valid = seq < a.B;
+  const int64_t sq = valid ? seq : a.B - 1;
+  // U fragments of the wave's two unit blocks over all gate k-tiles:
+  // A[m = unit 16b + c][k = gate 16kt + 4g + jj] = U[unit][gate]
+  bf16x4 uf[2][SMT];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int kt = 0; kt < SMT; ++kt)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        uf[j][kt][jj] = __builtin_bit_cast(short, (__bf16)a.Uw[(16 * (2 * w + j) + c) * SG4 + 16 * kt + 4 * g + jj]);
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 dhr[2] = {zero4, zero4}, dcn[2] = {zero4, zero4};
+  for (int t = a.T - 1; t >= 0; --t) {
+    const int cur = t & 1;
+    const int64_t bg = (sq * a.T + t) * (int64_t)SG4;
+    const int64_t bu = (sq * a.T + t) * (int64_t)SU;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int b = 2 * w + j;
+      const int off = 16 * b + 4 * g;
+      const f32x4 gi = *reinterpret_cast<const f32x4*>(a.gates + bg + off);
+      const f32x4 gf = *reinterpret_cast<const f32x4*>(a.gates + bg + SU + off);
+      const f32x4 gc = *reinterpret_cast<const f32x4*>(a.gates + bg + 2 * SU + off);
+      const f32x4 go = *reinterpret_cast<const f32x4*>(a.gates + bg + 3 * SU + off);
+      const f32x4 ct = *reinterpret_cast<const f32x4*>(a.cseq + bu + off);
+      f32x4 cp;
+      if (t > 0) cp = *reinterpret_cast<const f32x4*>(a.cseq + bu - SU + off);
+      else if (a.c0) cp = *reinterpret_cast<const f32x4*>(a.c0 + sq * SU + off);
+      else cp = zero4;
+      const f32x4 dho = valid ? *reinterpret_cast<const f32x4*>(a.dh + bu + off) : zero4;
+      f32x4 dzt[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float dh = dho[i] + dhr[j][i];
+        const float ac = act_f(a.act, ct[i]);
+        const float dc = dcn[j][i] + dh * go[i] * act_d(a.act, ct[i], ac);
+        dzt[0][i] = dc * gc[i] * gi[i] * (1.f - gi[i]);
+        dzt[1][i] = dc * cp[i] * gf[i] * (1.f - gf[i]);
+        const float gcd = a.act == ACT_RELU ? (gc[i] > 0.f ? 1.f : 0.f) : fmaf(-gc[i], gc[i], 1.f);
+        dzt[2][i] = dc * gi[i] * gcd;
+        dzt[3][i] = dh * ac * go[i] * (1.f - go[i]);
+        dcn[j][i] = dc * gf[i];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!valid) dzt[q] = zero4;
+        const int mt = q * SUB + b;
+        if (valid) *reinterpret_cast<f32x4*>(a.dz + bg + 16 * mt + 4 * g) = dzt[q];
+        dzbuf[cur][mt][lane] = pack4(dzt[q]);
+      }
+    }
+    __syncthreads();
+    // recurrent gradient for step t-1 of the wave's units: dh^T = U . dz^T over all gates
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      f32x4 acc = zero4;
+#pragma unroll
+      for (int kt = 0; kt < SMT; ++kt) acc = mfma16(uf[j][kt], dzbuf[cur][kt][lane], acc);
+      dhr[j] = acc;
+    }
+  }
+  if (valid) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int off = 16 * (2 * w + j) + 4 * g;
+      if (a.dh0) *reinterpret_cast<f32x4*>(a.dh0 + sq * SU + off) = dhr[j];
+      if (a.dc0) *reinterpret_cast<f32x4*>(a.dc0 + sq * SU + off) = dcn[j];
+    }
+  }
+}
+
 }  // namespace
 
 namespace sml {
@@ -251,6 +429,9 @@ hipError_t lstm_fwd_launch(const float* zx, const float* Uw, const float* h0, co
   } else if (U == 64) {
     LstmArgs<64> a{zx, Uw, h0, c0, hseq, cseq, gates, B, T, act};
     hipLaunchKernelGGL(lstm_fwd_kernel<64>, dim3(grid), dim3(WAVES * 64), 0, stream, a);
+  } else if (U == SU) {   // four waves per 16-sequence tile
+    LstmArgs<SU> a{zx, Uw, h0, c0, hseq, cseq, gates, B, T, act};
+    hipLaunchKernelGGL(lstm_fwd_split_kernel, dim3((unsigned)((B + 15) / 16)), dim3(256), 0, stream, a);
   } else {
     return hipErrorInvalidValue;
   }
@@ -269,6 +450,9 @@ hipError_t lstm_bwd_launch(const float* dh, const float* gates, const float* cse
   } else if (U == 64) {
     LstmBwdArgs<64> a{dh, gates, cseq, c0, Uw, dz, dh0, dc0, B, T, act};
     hipLaunchKernelGGL(lstm_bwd_kernel<64>, dim3(grid), dim3(WAVES * 64), 0, stream, a);
+  } else if (U == SU) {
+    LstmBwdArgs<SU> a{dh, gates, cseq, c0, Uw, dz, dh0, dc0, B, T, act};
+    hipLaunchKernelGGL(lstm_bwd_split_kernel, dim3((unsigned)((B + 15) / 16)), dim3(256), 0, stream, a);
   } else {
     return hipErrorInvalidValue;
   }

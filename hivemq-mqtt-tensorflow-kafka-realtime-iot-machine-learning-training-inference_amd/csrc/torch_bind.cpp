@@ -493,7 +493,8 @@ std::vector<at::Tensor> lstm_fwd(const at::Tensor& zx, const at::Tensor& Uw, con
   TORCH_CHECK(Uw.dim() == 2 && Uw.is_contiguous() && Uw.size(1) == 4 * Uw.size(0), "U must be [u, 4u]");
   const int64_t B = zx.size(0), T = zx.size(1), U = Uw.size(0);
   TORCH_CHECK(zx.size(2) == 4 * U, "zx last dim must be 4u");
-  TORCH_CHECK(U == 16 || U == 32 || U == 64, "LSTM units must be 16, 32 or 64");
+  TORCH_CHECK(U == 16 || U == 32 || U == 64 || U == 128,
+              "LSTM units must be 16, 32, 64 or 128 (ops/lstm.py zero-pads other widths up to one of them)");
   TORCH_CHECK(act == 1 || act == 2, "LSTM activation must be relu or tanh");
   TORCH_CHECK(T >= 1 && B >= 1, "empty input");
   if (h0.has_value()) TORCH_CHECK(h0->is_contiguous() && h0->numel() == B * U, "h0 must be [B, u]");
@@ -518,7 +519,8 @@ std::vector<at::Tensor> lstm_bwd(const at::Tensor& dh, const at::Tensor& gates, 
   const int64_t B = dh.size(0), T = dh.size(1), U = Uw.size(0);
   TORCH_CHECK(dh.is_contiguous() && gates.is_contiguous() && cseq.is_contiguous(), "inputs must be contiguous");
   TORCH_CHECK(dh.sizes() == cseq.sizes() && gates.size(2) == 4 * U && dh.size(2) == U, "shape mismatch");
-  TORCH_CHECK(U == 16 || U == 32 || U == 64, "LSTM units must be 16, 32 or 64");
+  TORCH_CHECK(U == 16 || U == 32 || U == 64 || U == 128,
+              "LSTM units must be 16, 32, 64 or 128 (ops/lstm.py zero-pads other widths up to one of them)");
   if (c0.has_value()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * U, "c0 must be [B, u]");
   c10::hip::HIPGuard guard(dh.device().index());
   auto dz = at::empty({B, T, 4 * U}, dh.options());

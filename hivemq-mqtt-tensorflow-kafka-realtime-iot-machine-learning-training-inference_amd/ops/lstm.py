@@ -7,7 +7,9 @@ layers keep the one-launch forward; their backward stores dz (bf16) and a second
 hand-written kernel (``lstm_dz_wgrad_kernel``, split over gate groups) contracts it,
 since 4U x (16 KT + U) weight-gradient accumulators do not fit one wave's registers.
 Fallback for shapes without a fused instance (:class:`LSTMFunction`): K1/K2
-projection kernels + the recurrence-only kernels described below.
+projection kernels (the general MFMA GEMM for wide layers) + the recurrence-only kernels
+described below (U = 128: four waves share each 16-sequence tile).  Widths other than
+16 / 32 / 64 / 128 are zero-padded to the next of them (:func:`pad_lstm_weights`: exact).
 
 Fallback forward: Zx = X.W + b over all B*T rows (K1 ``dense_fwd``), then the
 ``lstm_fwd`` kernel runs the recurrence (U.h MFMAs + gates + state update per
@@ -138,11 +140,48 @@ def fused_supported(units: int, in_features: int) -> bool:
     return bool(load_c().lstm_fused_supported(int(units), int(in_features)))
 
 
+KERNEL_UNITS = (16, 32, 64, 128)   # widths the recurrence kernels are built for
+
+
+def padded_units(units: int):
+    """Smallest kernel width >= ``units`` (None beyond 128)."""
+    for p in KERNEL_UNITS:
+        if units <= p:
+            return p
+    return None
+
+
+def _pad_gates(t: torch.Tensor, u: int, up: int) -> torch.Tensor:
+    """[..., 4u] Keras gate columns (i | f | c~ | o) -> [..., 4up], gate block k at
+    columns [k up, k up + u), zeros elsewhere (differentiable)."""
+    lead = t.shape[:-1]
+    return torch.nn.functional.pad(t.reshape(*lead, 4, u), (0, up - u)).reshape(*lead, 4 * up)
+
+
+def pad_lstm_weights(W: torch.Tensor, U: torch.Tensor, b: torch.Tensor, up: int):
+    """Zero-pad a u-unit layer to ``up`` units.  The padded units have zero weights and
+    bias, so from zero state their gates are i = f = o = 1/2, g~ = act(0) = 0: c and h
+    stay exactly 0 and feed nothing into the real units -- the real units' outputs and
+    gradients are those of the unpadded layer."""
+    u = U.shape[0]
+    Wp = _pad_gates(W, u, up)
+    Up = torch.nn.functional.pad(_pad_gates(U, u, up), (0, 0, 0, up - u))
+    return Wp, Up, _pad_gates(b, u, up)
+
+
 def lstm(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor, activation: str = "relu",
          fused: bool = True, return_sequences: bool = True) -> torch.Tensor:
     """Device-dispatching LSTM layer: fused HIP kernels on ROCm, torch reference on CPU.
     ``return_sequences=False`` returns h_T [B, U] (Keras semantics)."""
     if x.is_cuda:
+        u = U.shape[0]
+        if u not in KERNEL_UNITS:
+            up = padded_units(u)
+            if up is None:
+                raise ValueError(f"LSTM with {u} units: the ROCm kernels take up to 128 units")
+            Wp, Upad, bp = pad_lstm_weights(W, U, b, up)
+            hs = lstm(x, Wp, Upad, bp, activation, fused, return_sequences)
+            return hs[..., :u]
         if fused and fused_supported(U.shape[0], x.shape[-1]):
             # sliding windows (consecutive rows per step, any sequence stride) are read
             # in place by the fused kernels: no [B, T, F] materialisation

@@ -86,3 +86,28 @@ def test_persistent_trainer_skips_exactly_the_zero_gradient_parameters():
     g = m.fp.grad[lp._inactive_mask(m)]
     assert float(g.abs().max()) == 0.0
     assert lp.check_inactive(m)
+
+
+def test_zero_padded_lstm_weights_are_exact():
+    """ops.lstm.pad_lstm_weights: a u-unit layer padded to a kernel width gives the same h
+    (the padded units stay exactly 0) and the same weight gradients (float64, CPU oracle)."""
+    import numpy as np
+    import torch
+
+    from streamml.ops.lstm import lstm_reference, pad_lstm_weights, padded_units
+    assert [padded_units(u) for u in (1, 16, 17, 50, 64, 65, 128, 129)] == [16, 16, 32, 64, 64, 128, 128, None]
+    rng = np.random.default_rng(0)
+    for u, act in ((20, "relu"), (50, "tanh"), (100, "tanh")):
+        up = padded_units(u)
+        x = torch.tensor(rng.uniform(-1, 1, (4, 6, 18)))
+        W, U, b = (torch.tensor(rng.standard_normal(s) * 0.3, requires_grad=True)
+                   for s in ((18, 4 * u), (u, 4 * u), (4 * u,)))
+        h = lstm_reference(x, W, U, b, act)
+        g = torch.tensor(rng.standard_normal(h.shape))
+        gW, gU, gb = torch.autograd.grad((h * g).sum(), (W, U, b))
+        hp = lstm_reference(x, *pad_lstm_weights(W, U, b, up), act)
+        assert torch.equal(hp[..., u:], torch.zeros_like(hp[..., u:]))
+        assert torch.allclose(hp[..., :u], h, rtol=0, atol=1e-12)
+        pW, pU, pb = torch.autograd.grad((hp[..., :u] * g).sum(), (W, U, b))
+        for a_, b_ in ((pW, gW), (pU, gU), (pb, gb)):
+            assert torch.allclose(a_, b_, rtol=0, atol=1e-12)
