@@ -80,7 +80,8 @@ class AESpec:
     def check_fused(self) -> None:
         if not (1 <= self.input_dim <= 31 and 1 <= self.encoding_dim <= 15 and 1 <= self.hidden_dim <= 15):
             raise ValueError("fused AE kernel supports input_dim <= 31 and hidden sizes <= 15, got "
-                             f"{self.layer_sizes}")
+                             f"{self.layer_sizes}; wider autoencoders: streamml.nn.Sequential of Dense layers "
+                             "(layer-by-layer engine on the K1/K2 and general GEMM kernels)")
 
 
 def pack_image(weights: Sequence[np.ndarray]) -> np.ndarray:

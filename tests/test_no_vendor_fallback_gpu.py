@@ -54,3 +54,18 @@ def test_mlp_paths(cuda_device):
         m = MLPClassifier(hidden=hidden, dropout=drop, device=cuda_device)
         m.fit(x, y, epochs=1, batch_size=32, verbose=0)
         m.predict(x)
+
+
+def test_wide_dense_autoencoder_sequential(cuda_device):
+    """An autoencoder wider than the fused AE kernel (100 -> 64 -> 32 -> 64 -> 100) built with
+    nn.Sequential trains and predicts on the layer-by-layer engine: K1/K2 for the narrow
+    layers, the general MFMA GEMM for the wide ones -- no vendor fallback."""
+    from streamml import nn
+    rng = np.random.default_rng(3)
+    x = rng.uniform(-1, 1, size=(4096, 100)).astype(np.float32)
+    m = nn.Sequential([nn.Dense(64, activation="tanh", input_shape=(100,)), nn.Dense(32, activation="relu"),
+                       nn.Dense(64, activation="tanh"), nn.Dense(100)], device=cuda_device)
+    m.compile(optimizer="adam", loss="mean_squared_error")
+    h = m.fit(x, x, epochs=3, batch_size=256, verbose=0)
+    assert h.history["loss"][-1] < h.history["loss"][0]
+    assert m.predict(x[:300]).shape == (300, 100)
