@@ -256,6 +256,21 @@ def measure_batch32(spec, data, device, steps, scale, shift, seed, launches=5):
             "final_loss": ae.read_metrics()["loss"]}
 
 
+def measure_batch32_d30(device, steps, seed):
+    """keras_batch32 on the exact BASELINE model: the creditcard autoencoder (D = 30 -> 14 -> 7 ->
+    7 -> 30, tanh / relu / tanh / relu, L1 1e-7 activity regulariser, Adam) at batch 32, one Adam
+    step per 32 rows, on 2^20 synthetic standardised 30-feature rows resident on the device."""
+    import torch
+
+    from streamml.ops.ae import AESpec
+    g = torch.Generator(device=device).manual_seed(seed + 30)
+    data = torch.randn(1 << 20, 30, device=device, generator=g)
+    r = measure_batch32(AESpec(30, 14, 7), data, device, steps, None, None, seed)
+    r["model"] = "dense-autoencoder 30-14-7-7-30 (creditcard notebook, the BASELINE row)"
+    r["data"] = "synthetic standardised 30-feature rows"
+    return r
+
+
 def measure_collectives(device, world, group=None, iters=300, floats=1536):
     """Small-bucket all-reduce latency at the AE's bucket size (1536 floats = 6 KB, the
     padded gradient image): the process group's ``all_reduce`` (RCCL) vs the one-launch xGMI P2P all-reduce
@@ -687,6 +702,12 @@ def main():
         if args.fleet_models > 0 and "error" not in b32 and "skipped" not in b32:
             b32["fleet"] = ph.run("keras_batch32_fleet", 6, measure_batch32_fleet, spec, data, device,
                                   max(args.batch32_steps // 10, 1), scale, shift, args.fleet_models)
+        if "error" not in b32 and "skipped" not in b32:
+            # the BASELINE row itself: the creditcard autoencoder D = 30 -> 14 -> 7 -> 7 -> 30 at batch 32
+            # (Python-Tensorflow-2.0-Keras-Fraud-Detection-Autoencoder.ipynb:624-640, 62 661 rows/s on
+            # the reference's CPU); standardised synthetic features, no input normaliser
+            b32["d30"] = ph.run("keras_batch32_d30", 4 + 1.5e-5 * args.batch32_steps, measure_batch32_d30, device,
+                                args.batch32_steps, args.seed)
         out["keras_batch32"] = b32
     if args.fit_epochs > 0:
         fit_large = ph.run("fit_large_batch", 8, measure_fit_large_batch, data, device, B, epochs=args.fit_epochs,
@@ -751,6 +772,8 @@ SUMMARY_FIELDS = (
     ("fresh_rows_per_s", ("fresh_rows_per_s",)),
     ("keras_batch32_rows_per_s", ("keras_batch32", "rows_per_s")),
     ("vs_baseline_same_batch32", ("keras_batch32", "vs_baseline")),
+    ("keras_batch32_d30_rows_per_s", ("keras_batch32", "d30", "rows_per_s")),
+    ("vs_baseline_same_model_batch32", ("keras_batch32", "d30", "vs_baseline")),
     ("fit_batch100_rows_per_s", ("fit_batch100_rows_per_s",)),
     ("ae_infer_p50_us", ("p50_infer_us",)),
     ("ae_infer_p99_us", ("p99_infer_us",)),

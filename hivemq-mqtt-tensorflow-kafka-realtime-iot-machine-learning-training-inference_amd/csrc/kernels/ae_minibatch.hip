@@ -777,7 +777,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 }
 
 // ------------------------------------------------------------------------------------------
-// Pipelined Keras batch-32 build (reference activations, <= 18 inputs, one replica per
+// Pipelined Keras batch-32 build (reference activations, <= 18 inputs (KD = 18: cardata) or
+// <= 31 (KD = 32: the creditcard model D = 30 of the BASELINE row), one replica per
 // workgroup; resident ring or streaming epoch).  At batch 32 only waves 0-1 own rows, so the other six waves
 // own the six parameter tiles and the two barriers per step become LDS stage counters:
 //   row waves   forward, then the backward, bumping E_l as soon as layer l's activation and
@@ -829,10 +830,11 @@ __device__ __forceinline__ int tile_layer(int tile) { return tile <= 1 ? 1 : til
 // Batch 32 only.  The same scheme at cardata-v3's batch 100 (7 row waves + 6 tile waves in a
 // 13-wave workgroup) measured 23.3 vs 27.3 M rows/s for the two-barrier kernel (profiles/r03/s3):
 // there every SIMD already carries row waves, and the tile waves' work and polls slow the chain.
-template <int PACK, int TB>
+template <int PACK, int TB, int KD = 18>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae_minibatch_pipe_kernel(MBArgs a0) {
   static_assert(TB == 32, "pipelined build: two row waves + six tile waves");
-  constexpr int KD = 18, KSX = 6, NS = TB / 4;
+  static_assert(KD == 18 || KD == 32, "input width classes of the barrier kernel");
+  constexpr int KSX = KD <= 16 ? 4 : 4 + (KD - 16 < 4 ? KD - 16 : 4), NS = TB / 4;   // as ae_minibatch_kernel
   constexpr int NRW = 2, NWV = 8;
   constexpr int MB = MB_SMALL;
   static_assert(((PACK & 3) != ACT_SIGMOID) && (((PACK >> 2) & 3) != ACT_SIGMOID) &&
@@ -1217,8 +1219,8 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
   // the pipelined build (SML_MB_PIPE=0 selects the two-barrier kernel, for A/B runs; read per
   // launch).  Same box: 15.5 -> 16.3 M rows/s alone, 3.93 -> 5.73 G rows/s for 1024 models.
   const char* pe = getenv("SML_MB_PIPE");
-  if (B == 32 && ref && dims[0] <= 18 && dp_ranks <= 1 && !prof && !(pe && pe[0] == '0')) {
-    k = ae_minibatch_pipe_kernel<PACK_REF, 32>;
+  if (B == 32 && ref && dp_ranks <= 1 && !prof && !(pe && pe[0] == '0')) {
+    k = dims[0] <= 18 ? ae_minibatch_pipe_kernel<PACK_REF, 32, 18> : ae_minibatch_pipe_kernel<PACK_REF, 32, 32>;
     lds = sizeof(Smem<MB_SMALL>);
   }
   if (lds > 65536) {   // > 64 KB of dynamic LDS must be opted into per kernel

@@ -105,18 +105,19 @@ def test_minibatch_rejects_bad_batch(cuda_device):
         fused.train_minibatches(2)
 
 
-@pytest.mark.parametrize("B,models", [(32, 1), (32, 6)])
-def test_pipelined_build_bit_identical_to_barrier_kernel(cuda_device, monkeypatch, B, models):
+@pytest.mark.parametrize("B,models,D", [(32, 1, 18), (32, 6, 18), (32, 1, 30), (32, 3, 30)])
+def test_pipelined_build_bit_identical_to_barrier_kernel(cuda_device, monkeypatch, B, models, D):
     """Keras batch 32 on the reference stack runs the pipelined build (the six parameter tiles
     on their own waves, LDS stage counters instead of the two barriers per step).  Same
     arithmetic in the same order as the two-barrier kernel (SML_MB_PIPE=0): bit-identical
-    parameters, moments, cursor and metrics, alone and as a fleet (one model per workgroup)."""
+    parameters, moments, cursor and metrics, alone and as a fleet (one model per workgroup);
+    for the cardata model (D = 18) and the BASELINE row's creditcard model (D = 30)."""
     from streamml.ops.ae_fleet import AEFleet
 
-    spec = AESpec()
-    scale, shift = normalize_affine()
+    spec = AESpec(D, 14, 7)
+    scale, shift = normalize_affine() if D == 18 else (None, None)
     g = torch.Generator(device="cpu").manual_seed(5)
-    rings = (torch.rand((models, B * 24, 18), generator=g) * 40.0).to(cuda_device)
+    rings = (torch.rand((models, B * 24, D), generator=g) * (40.0 if D == 18 else 2.0)).to(cuda_device)
     ws = [_weights(spec, seed=20 + i) for i in range(models)]
     runs = []
     for pipe in ("1", "0"):
