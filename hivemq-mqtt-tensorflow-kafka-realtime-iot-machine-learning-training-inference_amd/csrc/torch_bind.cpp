@@ -668,11 +668,12 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
     TORCH_CHECK(t->dim() == 2 && (t->scalar_type() == at::kFloat || t->scalar_type() == at::kBFloat16),
                 "gemm operands must be 2-D fp32 or bf16");
   TORCH_CHECK(a.size(1) == b.size(0), "gemm: inner dims differ (", a.size(1), " vs ", b.size(0), ")");
+  TORCH_CHECK(a.device() == b.device(), "gemm operands must be on one device");
   TORCH_CHECK(act >= 0 && act <= 3, "act must be 0..3");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(1);
   if (bias.has_value()) {
     check_dev(*bias, "bias", at::kFloat);
-    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "bias must be [N]");
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous() && bias->device() == a.device(), "bias must be [N]");
   }
   c10::hip::HIPGuard guard(a.device().index());
   int64_t lda = 0, ldb = 0;
