@@ -177,8 +177,11 @@ def lstm(x: torch.Tensor, W: torch.Tensor, U: torch.Tensor, b: torch.Tensor, act
         u = U.shape[0]
         if u not in KERNEL_UNITS:
             up = padded_units(u)
-            if up is None:
-                raise ValueError(f"LSTM with {u} units: the ROCm kernels take up to 128 units")
+            if up is None:   # wider than any kernel: torch ops (counted; SML_STRICT_KERNELS=1 refuses)
+                from ._ext import note_fallback
+                note_fallback(f"lstm[{u} units]")
+                hs = lstm_reference(x.float(), W, U, b, activation)
+                return hs if return_sequences else hs[:, -1]
             Wp, Upad, bp = pad_lstm_weights(W, U, b, up)
             hs = lstm(x, Wp, Upad, bp, activation, fused, return_sequences)
             return hs[..., :u]
