@@ -364,6 +364,23 @@ def measure_fit(device, rows, batch=100, seed=0):
     return _bench_fit_module().fit_array(device, rows=rows, batch=batch, seed=seed, dp="none")
 
 
+def measure_fit_bf16(device, rows, batch=100, seed=0):
+    """measure_fit with the small-batch trainer's forward / activation-gradient contractions on
+    bf16 MFMAs (``Autoencoder.compile(minibatch_precision="bf16")``; fp32 weight gradients, master
+    weights and Adam)."""
+    old = os.environ.get("SML_MB_BF16")
+    os.environ["SML_MB_BF16"] = "1"
+    try:
+        r = measure_fit(device, rows, batch, seed)
+    finally:
+        if old is None:
+            os.environ.pop("SML_MB_BF16", None)
+        else:
+            os.environ["SML_MB_BF16"] = old
+    r["dtype"] = "bf16 MFMA contractions, fp32 weight gradients / master weights / Adam"
+    return r
+
+
 def measure_stream_e2e(device, rows, batch=100):
     """In-process Kafka (16 partitions of Confluent Avro) -> native C++ feed (decode-time
     label filter, pinned slabs, H2D in flight) -> fit(batch_size=100): events/s end to end,
@@ -722,6 +739,9 @@ def main():
     if args.fit_rows > 0:
         fit100 = ph.run("fit_batch100", 5 + 1e-6 * args.fit_rows, measure_fit, device, args.fit_rows)
         out.update({"fit_batch100_rows_per_s": fit100.get("rows_per_s"), "fit_batch100": fit100})
+        if "rows_per_s" in fit100:   # the same job with the small-batch trainer's bf16 contractions
+            fit100["bf16"] = ph.run("fit_batch100_bf16", 5 + 1e-6 * args.fit_rows, measure_fit_bf16, device,
+                                    args.fit_rows)
     if args.stream_rows > 0:
         stream = ph.run("stream_e2e", 10 + 1.5e-6 * args.stream_rows, measure_stream_e2e, device, args.stream_rows)
         out.update({"stream_e2e_rows_per_s": stream.get("rows_per_s"), "stream_e2e": stream})
@@ -775,6 +795,7 @@ SUMMARY_FIELDS = (
     ("keras_batch32_d30_rows_per_s", ("keras_batch32", "d30", "rows_per_s")),
     ("vs_baseline_same_model_batch32", ("keras_batch32", "d30", "vs_baseline")),
     ("fit_batch100_rows_per_s", ("fit_batch100_rows_per_s",)),
+    ("fit_batch100_bf16_rows_per_s", ("fit_batch100", "bf16", "rows_per_s")),
     ("ae_infer_p50_us", ("p50_infer_us",)),
     ("ae_infer_p99_us", ("p99_infer_us",)),
     ("ae_kafka_e2e_p50_us", ("kafka_e2e_p50_us",)),

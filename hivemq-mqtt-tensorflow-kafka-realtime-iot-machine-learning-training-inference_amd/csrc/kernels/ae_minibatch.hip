@@ -248,12 +248,27 @@ __device__ __forceinline__ int act_code(const MBArgs& a, int l) {
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
-// one hidden-width layer in registers: Z^T = W^T . H^T + b (4 K-steps over 16 features)
-__device__ __forceinline__ f32x4 layer16(const float* frag, const float* bias, int lane, int g, const f32x4& h) {
-  f32x4 acc = ld4(bias + 4 * g);
+// Four K-steps of a phase-A contraction: fp32 (four v_mfma_f32_16x16x4f32, K-step s = register s
+// of the B tile and fragment row s) or, with BF, ONE v_mfma_f32_16x16x16_bf16 over the same 16
+// features: lane (c, g)'s four fragment words W[4g + j][c] (rows j of the fp32 image) and its four
+// B registers H^T[4g + j][c] are exactly the bf16 A / B operands of that instruction, so the fp32
+// images serve both forms (phase B keeps updating only them).  fp32 accumulation either way.
+template <bool BF>
+__device__ __forceinline__ f32x4 kstep4(const float* frag, int lane, const f32x4& b, f32x4 acc) {
+  if constexpr (BF) {
+    const f32x4 a = {frag[lane], frag[64 + lane], frag[128 + lane], frag[192 + lane]};
+    return mfma16(pack4(a), pack4(b), acc);
+  } else {
 #pragma unroll
-  for (int s = 0; s < 4; ++s) acc = mfma4(frag[s * 64 + lane], h[s], acc);
-  return acc;
+    for (int s = 0; s < 4; ++s) acc = mfma4(frag[s * 64 + lane], b[s], acc);
+    return acc;
+  }
+}
+
+// one hidden-width layer in registers: Z^T = W^T . H^T + b (4 K-steps over 16 features)
+template <bool BF = false>
+__device__ __forceinline__ f32x4 layer16(const float* frag, const float* bias, int lane, int g, const f32x4& h) {
+  return kstep4<BF>(frag, lane, h, ld4(bias + 4 * g));
 }
 
 // Sum over the 4 lanes of a row (l, l^16, l^32, l^48) with the gfx950 row swaps:
@@ -331,7 +346,8 @@ __device__ __forceinline__ float row_correct(const float* y, const float* x, int
 // build; 4 = <= 128 VGPRs, two fleet models per CU); MB: LDS capacity class (rows);
 // DPX: compiled with the in-kernel gradient exchange (a runtime-gated exchange in the
 // single-replica build cost 0.4-0.5 us per batch-32 step, profiles/r02)
-template <int KD, int TB, int PACK, int WPE = 2, int MB = MB_SMALL, bool DPX = false>
+// BF: phase A's forward / activation-gradient contractions on bf16 MFMAs (kstep4), fp32 elsewhere
+template <int KD, int TB, int PACK, int WPE = 2, int MB = MB_SMALL, bool DPX = false, bool BF = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void ae_minibatch_kernel(MBArgs a0) {
   static_assert(TB <= MB, "compiled batch exceeds the LDS capacity class");
   static_assert(KD <= 32, "input width <= 32");
@@ -500,7 +516,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       // L1: h1^T = act1(W1^T x^T + b1)
       f32x4 z1 = ld4(S.w + BB1 + 4 * g);
 #pragma unroll
-      for (int s = 0; s < KSX; ++s) z1 = mfma4(S.w[F1 + s * 64 + lane], xv[s], z1);
+      for (int s4 = 0; s4 < KSX; s4 += 4) {
+        if constexpr (BF) {   // K-steps past KSX: zero inputs against zero padding rows
+          z1 = kstep4<BF>(S.w + F1 + s4 * 64, lane, f32x4{xv[s4], xv[s4 + 1], xv[s4 + 2], xv[s4 + 3]}, z1);
+        } else {
+#pragma unroll
+          for (int s = s4; s < (s4 + 4 < KSX ? s4 + 4 : KSX); ++s) z1 = mfma4(S.w[F1 + s * 64 + lane], xv[s], z1);
+        }
+      }
       f32x4 h1, h2, h3;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -509,10 +532,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         ab = fmaf(fabsf(h), rowf, ab);
       }
       // L2, L3
-      const f32x4 z2 = layer16(S.w + F2, S.w + BB2, lane, g, h1);
+      const f32x4 z2 = layer16<BF>(S.w + F2, S.w + BB2, lane, g, h1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) h2[i] = fm(4 * g + i < n2, act_fwd(a2, z2[i]));
-      const f32x4 z3 = layer16(S.w + F3, S.w + BB3, lane, g, h2);
+      const f32x4 z3 = layer16<BF>(S.w + F3, S.w + BB3, lane, g, h2);
 #pragma unroll
       for (int i = 0; i < 4; ++i) h3[i] = fm(4 * g + i < n3, act_fwd(a3, z3[i]));
       // L4 (two output tiles), MSE, dz4 = act4'(y) * 2 (y - x) / D   (1/B applied in Adam)
@@ -521,8 +544,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
       for (int t4 = 0; t4 < (TV ? 1 : 2); ++t4) {
         f32x4 acc = ld4(S.w + BB4 + 16 * t4 + 4 * g);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma4(S.w[F4 + (4 * t4 + s) * 64 + lane], h3[s], acc);
+        acc = kstep4<BF>(S.w + F4 + 4 * t4 * 64, lane, h3, acc);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int f = 16 * t4 + 4 * g + i;
@@ -555,8 +577,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       // backward: dz3 = act3'(h3) * (W4 dz4^T), dz2 = act2'(h2) * (W3 dz3^T),
       //           dz1 = act1'(h1) * (W2 dz2^T + l1 sign(h1))   (Keras L1 activity regulariser)
       f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (BF) {
 #pragma unroll
-      for (int s = 0; s < (TV ? 4 : KSX); ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
+        for (int s4 = 0; s4 < (TV ? 4 : KSX); s4 += 4) acc3 = kstep4<BF>(S.w + G4 + s4 * 64, lane, dz4[s4 >> 2], acc3);
+      } else {
+#pragma unroll
+        for (int s = 0; s < (TV ? 4 : KSX); ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
+      }
       if constexpr (TV) {
 #pragma unroll
         for (int o = 0; o < KSX - 4; ++o)
@@ -567,13 +594,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
       for (int i = 0; i < 4; ++i) dz3[i] = fm(4 * g + i < n3, act_grad(a3, h3[i], acc3[i]));
       f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc2 = mfma4(S.w[G3 + s * 64 + lane], dz3[s], acc2);
+      acc2 = kstep4<BF>(S.w + G3, lane, dz3, acc2);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dz2[i] = fm(4 * g + i < n2, act_grad(a2, h2[i], acc2[i]));
       f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc1 = mfma4(S.w[G2 + s * 64 + lane], dz2[s], acc1);
+      acc1 = kstep4<BF>(S.w + G2, lane, dz2, acc1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float h = h1[i];
@@ -830,7 +855,7 @@ __device__ __forceinline__ int tile_layer(int tile) { return tile <= 1 ? 1 : til
 // Batch 32 only.  The same scheme at cardata-v3's batch 100 (7 row waves + 6 tile waves in a
 // 13-wave workgroup) measured 23.3 vs 27.3 M rows/s for the two-barrier kernel (profiles/r03/s3):
 // there every SIMD already carries row waves, and the tile waves' work and polls slow the chain.
-template <int PACK, int TB, int KD = 18>
+template <int PACK, int TB, int KD = 18, bool BF = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae_minibatch_pipe_kernel(MBArgs a0) {
   static_assert(TB == 32, "pipelined build: two row waves + six tile waves");
   static_assert(KD == 18 || KD == 32, "input width classes of the barrier kernel");
@@ -979,17 +1004,24 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
       if (!stream && step) pcnt_wait_updates(S.cnt, st);
       f32x4 z1 = ld4(S.w + BB1 + 4 * g);
 #pragma unroll
-      for (int s = 0; s < KSX; ++s) z1 = mfma4(S.w[F1 + s * 64 + lane], xv[s], z1);
+      for (int s4 = 0; s4 < KSX; s4 += 4) {
+        if constexpr (BF) {   // K-steps past KSX: zero inputs against zero padding rows
+          z1 = kstep4<BF>(S.w + F1 + s4 * 64, lane, f32x4{xv[s4], xv[s4 + 1], xv[s4 + 2], xv[s4 + 3]}, z1);
+        } else {
+#pragma unroll
+          for (int s = s4; s < (s4 + 4 < KSX ? s4 + 4 : KSX); ++s) z1 = mfma4(S.w[F1 + s * 64 + lane], xv[s], z1);
+        }
+      }
       f32x4 h1, h2, h3;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         h1[i] = act_fwd(a1, z1[i]);
         ab = fmaf(fabsf(h1[i]), rowf, ab);
       }
-      const f32x4 z2 = layer16(S.w + F2, S.w + BB2, lane, g, h1);
+      const f32x4 z2 = layer16<BF>(S.w + F2, S.w + BB2, lane, g, h1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) h2[i] = act_fwd(a2, z2[i]);
-      const f32x4 z3 = layer16(S.w + F3, S.w + BB3, lane, g, h2);
+      const f32x4 z3 = layer16<BF>(S.w + F3, S.w + BB3, lane, g, h2);
 #pragma unroll
       for (int i = 0; i < 4; ++i) h3[i] = act_fwd(a3, z3[i]);
       constexpr bool TV = tail_valu<KSX>();   // as ae_minibatch_kernel (bit-identical results)
@@ -997,8 +1029,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
 #pragma unroll
       for (int t4 = 0; t4 < (TV ? 1 : 2); ++t4) {
         f32x4 acc = ld4(S.w + BB4 + 16 * t4 + 4 * g);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma4(S.w[F4 + (4 * t4 + s) * 64 + lane], h3[s], acc);
+        acc = kstep4<BF>(S.w + F4 + 4 * t4 * 64, lane, h3, acc);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int f = 16 * t4 + 4 * g + i;
@@ -1040,8 +1071,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
         st4(S.y + r * XS + 16 + cw, y[1]);
       }
       f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (BF) {
 #pragma unroll
-      for (int s = 0; s < (TV ? 4 : KSX); ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
+        for (int s4 = 0; s4 < (TV ? 4 : KSX); s4 += 4) acc3 = kstep4<BF>(S.w + G4 + s4 * 64, lane, dz4[s4 >> 2], acc3);
+      } else {
+#pragma unroll
+        for (int s = 0; s < (TV ? 4 : KSX); ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
+      }
       if constexpr (TV) {
 #pragma unroll
         for (int o = 0; o < KSX - 4; ++o)
@@ -1055,16 +1091,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
       st4(S.h2 + r * HS + cw, h2);
       st4(S.dz3 + r * HS + cw, dz3);
       f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc2 = mfma4(S.w[G3 + s * 64 + lane], dz3[s], acc2);
+      acc2 = kstep4<BF>(S.w + G3, lane, dz3, acc2);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dz2[i] = act_grad(a2, h2[i], acc2[i]);
       pcnt_bump(S.cnt + CE3, lane);   // h2, dz3 stored; G3 read
       st4(S.h1 + r * HS + cw, h1);
       st4(S.dz2 + r * HS + cw, dz2);
       f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc1 = mfma4(S.w[G2 + s * 64 + lane], dz2[s], acc1);
+      acc1 = kstep4<BF>(S.w + G2, lane, dz2, acc1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float h = h1[i];
@@ -1190,6 +1224,10 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
            sr ? sr->avail : nullptr, sr ? sr->total : nullptr, sr ? sr->consumed : nullptr,
            sr ? sr->status : nullptr, sr ? sr->timeout_ticks : 0};
   const bool ref = acts[0] == ACT_TANH && acts[1] == ACT_RELU && acts[2] == ACT_TANH && acts[3] == ACT_RELU;
+  // SML_MB_BF16=1 (read per launch): phase A's contractions on bf16 MFMAs (kstep4) for the
+  // reference-activation single-replica builds; fp32 (the Keras-exact path) otherwise
+  const char* bfe = getenv("SML_MB_BF16");
+  const bool bf = bfe && bfe[0] == '1' && ref && dp_ranks <= 1;
   void (*k)(MBArgs) = nullptr;
   size_t lds = 0;
   auto pick = [&](auto dpx) {
@@ -1201,6 +1239,12 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
         k = B == 32 ? ae_minibatch_kernel<18, 32, PACK_REF, 2, MB_SMALL, X> : ae_minibatch_kernel<18, 0, PACK_REF, 2, MB_SMALL, X>;
       else if (ref)
         k = B == 32 ? ae_minibatch_kernel<32, 32, PACK_REF, 2, MB_SMALL, X> : ae_minibatch_kernel<32, 0, PACK_REF, 2, MB_SMALL, X>;
+      if constexpr (!X) {
+        if (bf) k = dims[0] <= 18 ? (B == 32 ? ae_minibatch_kernel<18, 32, PACK_REF, 2, MB_SMALL, false, true>
+                                             : ae_minibatch_kernel<18, 0, PACK_REF, 2, MB_SMALL, false, true>)
+                                  : (B == 32 ? ae_minibatch_kernel<32, 32, PACK_REF, 2, MB_SMALL, false, true>
+                                             : ae_minibatch_kernel<32, 0, PACK_REF, 2, MB_SMALL, false, true>);
+      }
       // (a 128-VGPR two-models-per-CU build measured no faster for fleets beyond the CU count:
       // 3.92 vs 3.96 G rows/s at 1024 / 256 models, profiles/r02)
     } else {
@@ -1211,6 +1255,11 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
         k = B == 100 ? ae_minibatch_kernel<18, 100, PACK_REF, 2, MB_LARGE, X>
                      : ae_minibatch_kernel<18, 0, PACK_REF, 2, MB_LARGE, X>;
       else if (ref) k = ae_minibatch_kernel<32, 0, PACK_REF, 2, MB_LARGE, X>;
+      if constexpr (!X) {
+        if (bf) k = dims[0] <= 18 ? (B == 100 ? ae_minibatch_kernel<18, 100, PACK_REF, 2, MB_LARGE, false, true>
+                                              : ae_minibatch_kernel<18, 0, PACK_REF, 2, MB_LARGE, false, true>)
+                                  : ae_minibatch_kernel<32, 0, PACK_REF, 2, MB_LARGE, false, true>;
+      }
     }
   };
   if (dp_ranks > 1) pick(std::true_type{});
@@ -1220,7 +1269,8 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
   // launch).  Same box: 15.5 -> 16.3 M rows/s alone, 3.93 -> 5.73 G rows/s for 1024 models.
   const char* pe = getenv("SML_MB_PIPE");
   if (B == 32 && ref && dp_ranks <= 1 && !prof && !(pe && pe[0] == '0')) {
-    k = dims[0] <= 18 ? ae_minibatch_pipe_kernel<PACK_REF, 32, 18> : ae_minibatch_pipe_kernel<PACK_REF, 32, 32>;
+    if (bf) k = dims[0] <= 18 ? ae_minibatch_pipe_kernel<PACK_REF, 32, 18, true> : ae_minibatch_pipe_kernel<PACK_REF, 32, 32, true>;
+    else k = dims[0] <= 18 ? ae_minibatch_pipe_kernel<PACK_REF, 32, 18> : ae_minibatch_pipe_kernel<PACK_REF, 32, 32>;
     lds = sizeof(Smem<MB_SMALL>);
   }
   if (lds > 65536) {   // > 64 KB of dynamic LDS must be opted into per kernel

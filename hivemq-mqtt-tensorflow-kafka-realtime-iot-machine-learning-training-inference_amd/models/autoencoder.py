@@ -99,7 +99,13 @@ class Autoencoder:
         raise ValueError(f"unknown input_normalizer {self.input_normalizer!r}")
 
     def compile(self, optimizer="adam", loss="mean_squared_error", metrics=("accuracy",), learning_rate=None,
-                **adam_kw) -> "Autoencoder":
+                minibatch_precision: str = "fp32", **adam_kw) -> "Autoencoder":
+        """Keras ``compile``.  ``minibatch_precision`` picks the small-batch (Keras batch <= 128)
+        trainer's contraction precision: ``"fp32"`` (default, Keras-exact) or ``"bf16"`` (bf16
+        MFMA forward / activation gradients, fp32 weight gradients, master weights and Adam)."""
+        if minibatch_precision not in ("fp32", "bf16"):
+            raise ValueError("minibatch_precision must be 'fp32' or 'bf16'")
+        self.minibatch_precision = minibatch_precision
         if str(optimizer).lower() != "adam":
             raise ValueError("only the Adam optimizer is implemented (the reference uses 'adam')")
         if loss not in ("mean_squared_error", "mse"):
@@ -119,6 +125,7 @@ class Autoencoder:
         if self.device.type == "cuda":
             self._backend = FusedAE(self.spec, weights, self.device, max_blocks=self.max_blocks,
                                     want_acc="accuracy" in self.metrics, scale=sc, shift=sh, **self.hp)
+            self._backend.minibatch_bf16 = getattr(self, "minibatch_precision", "fp32") == "bf16"
         else:
             self._backend = TorchAE(self.spec.layer_sizes, self.spec.activations, self.spec.activity_l1, weights,
                                     device=self.device, **self.hp)

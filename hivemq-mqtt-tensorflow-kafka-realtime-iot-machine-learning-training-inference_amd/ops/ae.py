@@ -14,6 +14,8 @@ accumulated on device and read once per epoch, never per step.
 """
 from __future__ import annotations
 
+import contextlib
+
 import os
 
 from dataclasses import dataclass
@@ -387,9 +389,10 @@ class FusedAE:
         # run while the resident kernel waits for the rows it produces.
         it = iter(chunks)
         xd = next(it, None)
-        sr.train(self._tcur, self.scale, self.shift, self.params, self.m, self.v, self.iter, self.metrics, B, nmax,
-                 self.spec.dims, self.spec.act_codes, float(self.spec.activity_l1), self.lr, self.beta_1,
-                 self.beta_2, self.epsilon, 1.0 / B, bool(self.want_acc), float(timeout_s))
+        with self._minibatch_precision():
+            sr.train(self._tcur, self.scale, self.shift, self.params, self.m, self.v, self.iter, self.metrics, B,
+                     nmax, self.spec.dims, self.spec.act_codes, float(self.spec.activity_l1), self.lr, self.beta_1,
+                     self.beta_2, self.epsilon, 1.0 / B, bool(self.want_acc), float(timeout_s))
         pushed = 0
         try:
             while xd is not None and (limit is None or pushed < limit):
@@ -422,6 +425,29 @@ class FusedAE:
             rem = 0
         return steps, (steps - (1 if rem else 0)) * B + rem
 
+    # Small-batch trainer precision.  False: fp32 end to end (the Keras-exact path).  True: the
+    # forward / activation-gradient contractions of each step on bf16 MFMAs (fp32 accumulation,
+    # fp32 weight gradients, fp32 master weights and Adam): Autoencoder.fit(batch_size=100)
+    # 27.3 -> 33.3 M rows/s, parameters within 0.4-1.5 % of the fp32 run after 400 steps
+    # (profiles/r05 SUMMARY §9).  The launcher reads SML_MB_BF16 per launch; this flag sets it
+    # around this model's launches (the in-kernel DP exchange always runs fp32).
+    minibatch_bf16 = False
+
+    @contextlib.contextmanager
+    def _minibatch_precision(self):
+        if not self.minibatch_bf16:
+            yield
+            return
+        old = os.environ.get("SML_MB_BF16")
+        os.environ["SML_MB_BF16"] = "1"
+        try:
+            yield
+        finally:
+            if old is None:
+                os.environ.pop("SML_MB_BF16", None)
+            else:
+                os.environ["SML_MB_BF16"] = old
+
     def _launch_minibatch(self, ring: torch.Tensor, cursor: torch.Tensor, B: int, nsteps: int,
                           prof: Optional[torch.Tensor] = None, dp=None) -> None:
         kw, gscale = {}, 1.0 / B
@@ -431,10 +457,11 @@ class FusedAE:
             it0 = int(self.iter.item())
             kw = dp.kernel_args(it0)
             gscale = 1.0 / (B * dp.world)
-        self.C.ae_train_minibatches(ring, cursor, self.scale, self.shift, self.params, self.m, self.v,
-                                    self.iter, self.metrics, int(B), int(nsteps), self.spec.dims, self.spec.act_codes,
-                                    float(self.spec.activity_l1), self.lr, self.beta_1, self.beta_2, self.epsilon,
-                                    gscale, bool(self.want_acc), prof, None, **kw)
+        with self._minibatch_precision():
+            self.C.ae_train_minibatches(ring, cursor, self.scale, self.shift, self.params, self.m, self.v,
+                                        self.iter, self.metrics, int(B), int(nsteps), self.spec.dims,
+                                        self.spec.act_codes, float(self.spec.activity_l1), self.lr, self.beta_1,
+                                        self.beta_2, self.epsilon, gscale, bool(self.want_acc), prof, None, **kw)
         if dp is not None:
             dp.note_iter(it0 + int(nsteps) - 1)
             dp.check()

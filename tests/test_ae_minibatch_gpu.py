@@ -137,3 +137,69 @@ def test_pipelined_build_bit_identical_to_barrier_kernel(cuda_device, monkeypatc
     assert torch.equal(p1, p0) and torch.equal(m1, m0) and torch.equal(v1, v0)
     assert torch.equal(c1, c0) and torch.equal(i1, i0)
     assert r1 == r0
+
+
+@pytest.mark.parametrize("D,B", [(18, 100), (18, 32), (30, 32), (18, 7)])
+def test_bf16_phase_a_close_to_fp32(cuda_device, monkeypatch, D, B):
+    """SML_MB_BF16=1: phase A's forward / activation-gradient contractions on bf16 MFMAs
+    (fp32 accumulation, fp32 weight gradients and Adam).  400 steps from one init stay within
+    a few percent of the fp32 kernel's parameters and the same loss to 1e-3 -- and are NOT
+    bit-identical (the bf16 path really ran)."""
+    spec = AESpec(D, 14, 7)
+    if D == 18:
+        scale, shift = normalize_affine()
+        ring = (torch.rand((B * 40, D), generator=torch.Generator().manual_seed(2)) * 40.0).to(cuda_device)
+    else:
+        scale = shift = None
+        ring = torch.randn((B * 40, D), generator=torch.Generator().manual_seed(2)).to(cuda_device)
+    out = {}
+    for bf in ("0", "1"):
+        monkeypatch.setenv("SML_MB_BF16", bf)
+        ae = FusedAE(spec, _weights(spec, seed=3), cuda_device, scale=scale, shift=shift)
+        ae.attach_ring(ring, B)
+        ae.train_minibatches(400)
+        torch.cuda.synchronize()
+        out[bf] = (ae.params.clone(), ae.read_metrics())
+    (p0, m0), (p1, m1) = out["0"], out["1"]
+    assert not torch.equal(p0, p1)
+    assert ((p1 - p0).norm() / p0.norm()).item() < 3e-2
+    assert abs(m1["loss"] - m0["loss"]) <= 1e-3 * abs(m0["loss"]) + 1e-6
+
+
+def test_bf16_pipelined_build_bit_identical_to_barrier_kernel(cuda_device, monkeypatch):
+    """Under SML_MB_BF16=1 the batch-32 pipelined build and the barrier kernel run the same bf16
+    contractions in the same order: bit-identical parameters and metrics."""
+    spec = AESpec()
+    scale, shift = normalize_affine()
+    ring = (torch.rand((32 * 24, 18), generator=torch.Generator().manual_seed(5)) * 40.0).to(cuda_device)
+    monkeypatch.setenv("SML_MB_BF16", "1")
+    runs = []
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("SML_MB_PIPE", pipe)
+        ae = FusedAE(spec, _weights(spec, seed=21), cuda_device, scale=scale, shift=shift)
+        ae.attach_ring(ring, 32)
+        ae.train_minibatches(87)
+        torch.cuda.synchronize()
+        runs.append((ae.params.clone(), ae.m.clone(), ae.v.clone(), ae.read_metrics()))
+    (p1, m1, v1, r1), (p0, m0, v0, r0) = runs
+    assert torch.equal(p1, p0) and torch.equal(m1, m0) and torch.equal(v1, v0)
+    assert r1 == r0
+
+
+def test_autoencoder_minibatch_precision_option(cuda_device, monkeypatch):
+    """Autoencoder.compile(minibatch_precision="bf16") trains fit(batch_size=100) on the bf16
+    contractions (close to, not equal to, the fp32 model) and leaves the process default alone."""
+    from streamml.models.autoencoder import Autoencoder
+    monkeypatch.delenv("SML_MB_BF16", raising=False)
+    x = np.random.default_rng(0).uniform(-1, 1, size=(20000, 18)).astype(np.float32)
+    ws = {}
+    for prec in ("fp32", "bf16"):
+        m = Autoencoder(device=cuda_device, seed=4)
+        m.compile(minibatch_precision=prec)
+        h = m.fit(x, epochs=2, batch_size=100, verbose=0)
+        assert h.history["loss"][-1] < h.history["loss"][0]
+        ws[prec] = np.concatenate([w.ravel() for w in m.get_weights()])
+    import os
+    assert "SML_MB_BF16" not in os.environ
+    assert not np.array_equal(ws["fp32"], ws["bf16"])
+    assert np.linalg.norm(ws["bf16"] - ws["fp32"]) / np.linalg.norm(ws["fp32"]) < 3e-2

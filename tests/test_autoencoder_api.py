@@ -96,3 +96,12 @@ def test_stream_fit_and_kafka_prediction_sink(car_rows):
     recs = b.read("model-predictions", 0, 0)
     assert len(recs) == 250
     assert recs[7][2].decode() == np.array2string(out[7])
+
+
+def test_compile_rejects_unknown_minibatch_precision():
+    import pytest as _pt
+
+    from streamml.models.autoencoder import Autoencoder
+    with _pt.raises(ValueError):
+        Autoencoder(device="cpu").compile(minibatch_precision="fp8")
+    Autoencoder(device="cpu").compile(minibatch_precision="bf16")   # a no-op on the CPU backend
