@@ -232,16 +232,18 @@ def measure_lstm_kafka_e2e(device, n_events: int, qps: float = 10000.0, nkeys: i
     return r
 
 
-def measure_batch32(spec, data, device, steps, scale, shift, seed, launches=5):
+def measure_batch32(spec, data, device, steps, scale, shift, seed, launches=5, bf16=False):
     """Side measurement at the reference's own optimizer granularity: one Adam step per
     32 rows (Keras fit(batch_size=32)), ``steps`` sequential steps per launch of the
-    persistent small-batch kernel (csrc/kernels/ae_minibatch.hip, fp32)."""
+    persistent small-batch kernel (csrc/kernels/ae_minibatch.hip, fp32; ``bf16``: its bf16
+    MFMA contractions, fp32 master weights and Adam)."""
     import torch
 
     from streamml.models.reference import init_dense_weights
     from streamml.ops.ae import FusedAE
 
     ae = FusedAE(spec, init_dense_weights(spec.layer_sizes, seed=seed), device, scale=scale, shift=shift)
+    ae.minibatch_bf16 = bool(bf16)
     ae.attach_ring(data, 32)
     ae.train_minibatches(steps)
     torch.cuda.synchronize()
@@ -252,11 +254,12 @@ def measure_batch32(spec, data, device, steps, scale, shift, seed, launches=5):
     dt = time.perf_counter() - t0
     n = steps * launches
     return {"rows_per_s": n * 32 / dt, "us_per_step": dt / n * 1e6, "vs_baseline": n * 32 / dt / BASELINE_ROWS_PER_S,
-            "steps": n, "dtype": "fp32", "path": "persistent small-batch kernel (ae_minibatch.hip), 1 GPU",
+            "steps": n, "dtype": "bf16 MFMA contractions, fp32 master weights / Adam" if bf16 else "fp32",
+            "path": "persistent small-batch kernel (ae_minibatch.hip), 1 GPU",
             "final_loss": ae.read_metrics()["loss"]}
 
 
-def measure_batch32_d30(device, steps, seed):
+def measure_batch32_d30(device, steps, seed, bf16=False):
     """keras_batch32 on the exact BASELINE model: the creditcard autoencoder (D = 30 -> 14 -> 7 ->
     7 -> 30, tanh / relu / tanh / relu, L1 1e-7 activity regulariser, Adam) at batch 32, one Adam
     step per 32 rows, on 2^20 synthetic standardised 30-feature rows resident on the device."""
@@ -265,7 +268,7 @@ def measure_batch32_d30(device, steps, seed):
     from streamml.ops.ae import AESpec
     g = torch.Generator(device=device).manual_seed(seed + 30)
     data = torch.randn(1 << 20, 30, device=device, generator=g)
-    r = measure_batch32(AESpec(30, 14, 7), data, device, steps, None, None, seed)
+    r = measure_batch32(AESpec(30, 14, 7), data, device, steps, None, None, seed, bf16=bf16)
     r["model"] = "dense-autoencoder 30-14-7-7-30 (creditcard notebook, the BASELINE row)"
     r["data"] = "synthetic standardised 30-feature rows"
     return r
@@ -725,6 +728,13 @@ def main():
             # the reference's CPU); standardised synthetic features, no input normaliser
             b32["d30"] = ph.run("keras_batch32_d30", 4 + 1.5e-5 * args.batch32_steps, measure_batch32_d30, device,
                                 args.batch32_steps, args.seed)
+            # the same two with the small-batch trainer's bf16 contractions (the framework's compute
+            # dtype; fp32 master weights and Adam) next to the Keras-exact fp32 numbers
+            b32["bf16"] = ph.run("keras_batch32_bf16", 4 + 1.5e-5 * args.batch32_steps, measure_batch32, spec,
+                                 data, device, args.batch32_steps, scale, shift, args.seed, bf16=True)
+            if isinstance(b32["d30"], dict):
+                b32["d30"]["bf16"] = ph.run("keras_batch32_d30_bf16", 4 + 1.5e-5 * args.batch32_steps,
+                                            measure_batch32_d30, device, args.batch32_steps, args.seed, bf16=True)
         out["keras_batch32"] = b32
     if args.fit_epochs > 0:
         fit_large = ph.run("fit_large_batch", 8, measure_fit_large_batch, data, device, B, epochs=args.fit_epochs,
@@ -794,6 +804,9 @@ SUMMARY_FIELDS = (
     ("vs_baseline_same_batch32", ("keras_batch32", "vs_baseline")),
     ("keras_batch32_d30_rows_per_s", ("keras_batch32", "d30", "rows_per_s")),
     ("vs_baseline_same_model_batch32", ("keras_batch32", "d30", "vs_baseline")),
+    ("keras_batch32_bf16_rows_per_s", ("keras_batch32", "bf16", "rows_per_s")),
+    ("keras_batch32_d30_bf16_rows_per_s", ("keras_batch32", "d30", "bf16", "rows_per_s")),
+    ("vs_baseline_same_model_batch32_bf16", ("keras_batch32", "d30", "bf16", "vs_baseline")),
     ("fit_batch100_rows_per_s", ("fit_batch100_rows_per_s",)),
     ("fit_batch100_bf16_rows_per_s", ("fit_batch100", "bf16", "rows_per_s")),
     ("ae_infer_p50_us", ("p50_infer_us",)),

@@ -208,6 +208,26 @@ __device__ __forceinline__ Tile make_tile(int id, int c, int g, const SM& S, con
   return T;
 }
 
+// BF phase B: a tile's weight gradient act^T . dz over the batch rows, 16 rows per
+// v_mfma_f32_16x16x16_bf16 (lane (c, g) takes rows 16 q + 4 g + j of its activation column and
+// dz column; swizzled columns as phase A stored them; rows past the batch hold zero dz), two
+// accumulator chains.  The fp32 form contracts 4 rows per v_mfma_f32_16x16x4f32.
+__device__ __forceinline__ f32x4 wgrad_bf16(const float* av, const float* dv, const Tile& T, int nblk, int g) {
+  f32x4 part[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (int q = 0; q < nblk; ++q) {
+    f32x4 x, d;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 16 * q + 4 * g + j;
+      const int sw = swz(r);
+      x[j] = av[r * T.as + (T.as ? (T.am ^ sw) : 0)];
+      d[j] = dv[r * T.ds + (T.dc ^ sw)];
+    }
+    part[q & 1] = mfma16(pack4(x), pack4(d), part[q & 1]);
+  }
+  return part[0] + part[1];
+}
+
 // Streaming epoch: wait until rows [0, need) are in the ring.  1 = they are, 0 = the stream
 // ended before `need`, -1 = nothing arrived within the timeout.  Wave-uniform.
 __device__ __forceinline__ int64_t ld_host64(const int64_t* p) {
@@ -639,7 +659,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       const int aE = T.as ? (T.am ^ X0) : 0, aO = T.as ? (T.am ^ X1) : 0;
       const int dE = T.dc ^ X0, dO = T.dc ^ X1;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (TB > 0) {
+      if constexpr (BF) {
+        acc = wgrad_bf16(av, dv, T, (B + 15) / 16, g);
+      } else if constexpr (TB > 0) {
         constexpr int NS = (TB + 3) / 4;
         constexpr int CH = NS >= 4 ? 4 : NS;   // independent MFMA chains, summed at the end
         f32x4 part[CH];
@@ -1126,26 +1148,30 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
       b2t *= (double)a.beta2;
       const float lr_t = a.lr * __builtin_amdgcn_sqrtf((float)(1.0 - b2t)) * __builtin_amdgcn_rcpf((float)(1.0 - b1t));
       pcnt_wait<1>(S.cnt + ce, (unsigned)NRW * (unsigned)(step + 1));   // every row wave reached layer `layer`
-      f32x4 part[4];
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};   // the barrier kernel's summation order (bit-identical A/B)
+      if constexpr (BF) {
+        acc = wgrad_bf16(av, dv, T, (B + 15) / 16, g);
+      } else {
+        f32x4 part[4];
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) part[c4] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // groups of 4 K-steps, one per accumulator chain
+        for (int c4 = 0; c4 < 4; ++c4) part[c4] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // groups of 4 K-steps, one per accumulator chain
 #pragma unroll
-      for (int q = 0; q < NS / 4; ++q) {
+        for (int q = 0; q < NS / 4; ++q) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 16 * q + 4 * j + g;
+          for (int j = 0; j < 4; ++j) {
+            const int r = 16 * q + 4 * j + g;
+            part[j] = mfma4(av[r * T.as + ((j & 1) ? aO : aE)], dv[r * T.ds + ((j & 1) ? dO : dE)], part[j]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NS % 4; ++j) {
+          const int r = 16 * (NS / 4) + 4 * j + g;
           part[j] = mfma4(av[r * T.as + ((j & 1) ? aO : aE)], dv[r * T.ds + ((j & 1) ? dO : dE)], part[j]);
         }
-      }
 #pragma unroll
-      for (int j = 0; j < NS % 4; ++j) {
-        const int r = 16 * (NS / 4) + 4 * j + g;
-        part[j] = mfma4(av[r * T.as + ((j & 1) ? aO : aE)], dv[r * T.ds + ((j & 1) ? dO : dE)], part[j]);
+        for (int c4 = 0; c4 < 4; ++c4) acc += part[c4];
       }
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};   // the barrier kernel's summation order (bit-identical A/B)
-#pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) acc += part[c4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float gr = acc[i] * a.gscale;
