@@ -367,21 +367,26 @@ def measure_fit(device, rows, batch=100, seed=0):
     return _bench_fit_module().fit_array(device, rows=rows, batch=batch, seed=seed, dp="none")
 
 
-def measure_fit_bf16(device, rows, batch=100, seed=0):
-    """measure_fit with the small-batch trainer's forward / activation-gradient contractions on
-    bf16 MFMAs (``Autoencoder.compile(minibatch_precision="bf16")``; fp32 weight gradients, master
-    weights and Adam)."""
+def _with_mb_bf16(fn, *a, **kw):
+    """Run ``fn`` with the small-batch trainer's bf16 MFMA contractions (SML_MB_BF16=1, read per
+    launch; ``Autoencoder.compile(minibatch_precision="bf16")``): fp32 master weights and Adam."""
     old = os.environ.get("SML_MB_BF16")
     os.environ["SML_MB_BF16"] = "1"
     try:
-        r = measure_fit(device, rows, batch, seed)
+        r = fn(*a, **kw)
     finally:
         if old is None:
             os.environ.pop("SML_MB_BF16", None)
         else:
             os.environ["SML_MB_BF16"] = old
-    r["dtype"] = "bf16 MFMA contractions, fp32 weight gradients / master weights / Adam"
+    if isinstance(r, dict):
+        r["dtype"] = "bf16 MFMA contractions, fp32 master weights / Adam"
     return r
+
+
+def measure_fit_bf16(device, rows, batch=100, seed=0):
+    """measure_fit on the small-batch trainer's bf16 contractions."""
+    return _with_mb_bf16(measure_fit, device, rows, batch, seed)
 
 
 def measure_stream_e2e(device, rows, batch=100):
@@ -755,6 +760,9 @@ def main():
     if args.stream_rows > 0:
         stream = ph.run("stream_e2e", 10 + 1.5e-6 * args.stream_rows, measure_stream_e2e, device, args.stream_rows)
         out.update({"stream_e2e_rows_per_s": stream.get("rows_per_s"), "stream_e2e": stream})
+        if "rows_per_s" in stream:
+            stream["bf16"] = ph.run("stream_e2e_bf16", 10 + 1.5e-6 * args.stream_rows, _with_mb_bf16,
+                                    measure_stream_e2e, device, args.stream_rows)
     if args.large_stream_rows > 0:   # fresh rows at large batch: the host decode curve and the trained rate
         big = ph.run("stream_large_batch", 16 + 1.2e-6 * args.large_stream_rows,
                      _bench_module("bench_fit").stream_large_batch, device, rows=args.large_stream_rows,
@@ -821,6 +829,7 @@ SUMMARY_FIELDS = (
     ("lstm_seq50_infer_p99_us", ("lstm_seq50_infer_p99_us",)),
     ("lstm_ref_us_per_step", ("lstm_ref_us_per_step",)),
     ("stream_e2e_rows_per_s", ("stream_e2e_rows_per_s",)),
+    ("stream_e2e_bf16_rows_per_s", ("stream_e2e", "bf16", "rows_per_s")),
     ("stream_large_batch_rows_per_s", ("stream_large_batch_rows_per_s",)),
     ("stream_staged_train_rows_per_s", ("stream_large_batch", "staged_train", "best_trained_rows_per_s")),
     ("stream_dp_rows_per_s", ("stream_dp_rows_per_s",)),
