@@ -34,10 +34,42 @@ def _read(path: str) -> str:
         return f.read().strip()
 
 
-def l3_cpus(k: int, slot: int = 0) -> Optional[List[int]]:
+def cpu_busy(sample_s: float = 0.05) -> Optional[dict]:
+    """Per-CPU busy fraction over ``sample_s`` from /proc/stat (None where unreadable)."""
+    import time
+
+    def snap():
+        out = {}
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3:4].isdigit():
+                    v = line.split()
+                    t = [int(x) for x in v[1:]]
+                    idle = t[3] + (t[4] if len(t) > 4 else 0)
+                    out[int(v[0][3:])] = (sum(t), idle)
+        return out
+    try:
+        a = snap()
+        time.sleep(sample_s)
+        b = snap()
+    except (OSError, ValueError, IndexError):
+        return None
+    busy = {}
+    for c, (tot, idle) in b.items():
+        if c in a:
+            dt = tot - a[c][0]
+            busy[c] = 0.0 if dt <= 0 else 1.0 - (idle - a[c][1]) / dt
+    return busy
+
+
+def l3_cpus(k: int, slot: int = 0, avoid_busy: bool = True) -> Optional[List[int]]:
     """``k`` CPUs of this process's affinity set sharing one L3, one per physical core (None:
-    cache topology not readable, or no L3 domain with ``k`` allowed cores).  ``slot`` (e.g. a
-    replica's rank) picks among the qualifying domains round-robin, so replicas do not share one."""
+    cache topology not readable, or no L3 domain with ``k`` allowed cores).  Spinning
+    latency-critical threads lose whole scheduler slices (ms) to any other runnable thread on
+    their CPU, so with ``avoid_busy`` each domain keeps its ``k`` least-busy cores (a 50 ms
+    /proc/stat sample; CPU 0, which services most housekeeping, last) and the domains are
+    ordered by that load.  ``slot`` (e.g. a replica's rank) picks among the qualifying domains
+    round-robin, so replicas do not share one."""
     groups = {}
     for c in sorted(os.sched_getaffinity(0)):
         try:
@@ -46,8 +78,18 @@ def l3_cpus(k: int, slot: int = 0) -> Optional[List[int]]:
         except OSError:
             return None
         groups.setdefault(l3, {}).setdefault(core, c)   # first allowed CPU of each core
-    ok = sorted((sorted(g.values()) for g in groups.values() if len(g) >= k), key=lambda cs: cs[0])
-    return ok[slot % len(ok)][:k] if ok else None
+    cands = [sorted(g.values()) for g in groups.values() if len(g) >= k]
+    if not cands:
+        return None
+    busy = cpu_busy() if avoid_busy else None
+    if busy:
+        def load(c):
+            return busy.get(c, 0.0) + (0.5 if c == 0 else 0.0)
+        picked = [sorted(sorted(cs, key=lambda c: (load(c), c))[:k]) for cs in cands]
+        order = sorted(range(len(cands)), key=lambda i: (round(sum(load(c) for c in picked[i]), 2), cands[i][0]))
+        return picked[order[slot % len(order)]]
+    ok = sorted(cands, key=lambda cs: cs[0])
+    return ok[slot % len(ok)][:k]
 
 
 def resolve_cpus(spec: Optional[str], slot: int = 0) -> Optional[Set[int]]:
