@@ -679,7 +679,15 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
   int64_t lda = 0, ldb = 0;
   int akc = 1, bkc = 1;
   const at::Tensor A = gemm_operand(a, 0, 1, lda, akc);
-  const at::Tensor B = gemm_operand(b, 1, 0, ldb, bkc);
+  // A small fp32 B (a layer's weight) is re-read and re-converted by every one of the M / 128
+  // row tiles: convert it to bf16 once (one pass over <= 4 M elements) when there are many.
+  // SML_GEMM_BF16_B=0 keeps the in-kernel conversion (A/B).
+  static const bool pre_b = [] {
+    const char* e = std::getenv("SML_GEMM_BF16_B");
+    return !(e && e[0] == '0');
+  }();
+  const bool cast_b = pre_b && b.scalar_type() == at::kFloat && b.numel() <= (int64_t(1) << 22) && M >= 8 * 128;
+  const at::Tensor B = gemm_operand(cast_b ? b.to(at::kBFloat16) : b, 1, 0, ldb, bkc);
   const int64_t Np = (N + 3) & ~int64_t(3);
   const bool plain = !bias.has_value() && act == 0 && !out_bf16;
   int s = 1;
