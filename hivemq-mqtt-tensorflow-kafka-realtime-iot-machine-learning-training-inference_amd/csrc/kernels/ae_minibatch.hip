@@ -212,9 +212,14 @@ __device__ __forceinline__ Tile make_tile(int id, int c, int g, const SM& S, con
 // v_mfma_f32_16x16x16_bf16 (lane (c, g) takes rows 16 q + 4 g + j of its activation column and
 // dz column; swizzled columns as phase A stored them; rows past the batch hold zero dz), two
 // accumulator chains.  The fp32 form contracts 4 rows per v_mfma_f32_16x16x4f32.
+// NB > 0: the block count is compile-time (TB builds), the loop unrolls and every LDS read
+// is issued ahead of the MFMAs; NB = 0: nblk at run time.
+template <int NB = 0>
 __device__ __forceinline__ f32x4 wgrad_bf16(const float* av, const float* dv, const Tile& T, int nblk, int g) {
   f32x4 part[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  for (int q = 0; q < nblk; ++q) {
+  constexpr int NBU = NB > 0 ? NB : 1;
+#pragma unroll
+  for (int q = 0; q < (NB > 0 ? NBU : nblk); ++q) {
     f32x4 x, d;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -660,7 +665,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       const int dE = T.dc ^ X0, dO = T.dc ^ X1;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if constexpr (BF) {
-        acc = wgrad_bf16(av, dv, T, (B + 15) / 16, g);
+        acc = wgrad_bf16<(TB + 15) / 16>(av, dv, T, (B + 15) / 16, g);
       } else if constexpr (TB > 0) {
         constexpr int NS = (TB + 3) / 4;
         constexpr int CH = NS >= 4 ? 4 : NS;   // independent MFMA chains, summed at the end
@@ -1150,7 +1155,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
       pcnt_wait<1>(S.cnt + ce, (unsigned)NRW * (unsigned)(step + 1));   // every row wave reached layer `layer`
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};   // the barrier kernel's summation order (bit-identical A/B)
       if constexpr (BF) {
-        acc = wgrad_bf16(av, dv, T, (B + 15) / 16, g);
+        acc = wgrad_bf16<(TB + 15) / 16>(av, dv, T, (B + 15) / 16, g);
       } else {
         f32x4 part[4];
 #pragma unroll
