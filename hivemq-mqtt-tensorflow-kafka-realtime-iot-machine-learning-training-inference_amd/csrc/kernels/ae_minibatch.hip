@@ -522,7 +522,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       for (int s = 0; s < KSX; ++s) xv[s] = (row_ok && fok[s]) ? fmaf(xr[s], sc[s], sh[s]) : 0.f;
       float xh[2];   // TV: inputs 16 + o of this lane's row (lane group 0's xv[4 + o]) in all 4 lanes
 #pragma unroll
-      for (int o = 0; o < 2; ++o) xh[o] = (tail_valu<KSX>() && 4 + o < KSX) ? rowsum4(xv[4 + o]) : 0.f;
+      for (int o = 0; o < 2; ++o) xh[o] = (tail_valu<KSX>() && !BF && 4 + o < KSX) ? rowsum4(xv[4 + o]) : 0.f;
       if (step + 1 < a.nsteps) {   // next step's rows: in flight across phase B
         int more = 1;
         if (stream) {   // the next batch must have landed in the ring (or the stream ends here)
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
       for (int i = 0; i < 4; ++i) h3[i] = fm(4 * g + i < n3, act_fwd(a3, z3[i]));
       // L4 (two output tiles), MSE, dz4 = act4'(y) * 2 (y - x) / D   (1/B applied in Adam)
-      constexpr bool TV = tail_valu<KSX>();
+      constexpr bool TV = tail_valu<KSX>() && !BF;   // bf16: the tail tile is one more cheap MFMA
       f32x4 y[2], dz4[2], w4h[2];
 #pragma unroll
       for (int t4 = 0; t4 < (TV ? 1 : 2); ++t4) {
@@ -1010,7 +1010,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
       for (int s = 0; s < KSX; ++s) xv[s] = (row_ok && fok[s]) ? fmaf(xr[s], sc[s], sh[s]) : 0.f;
       float xh[2];
 #pragma unroll
-      for (int o = 0; o < 2; ++o) xh[o] = (tail_valu<KSX>() && 4 + o < KSX) ? rowsum4(xv[4 + o]) : 0.f;
+      for (int o = 0; o < 2; ++o) xh[o] = (tail_valu<KSX>() && !BF && 4 + o < KSX) ? rowsum4(xv[4 + o]) : 0.f;
       if (step + 1 < nsteps) {   // next step's rows: in flight across this step
         int more = 1;
         if (stream) {
@@ -1051,7 +1051,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
       const f32x4 z3 = layer16<BF>(S.w + F3, S.w + BB3, lane, g, h2);
 #pragma unroll
       for (int i = 0; i < 4; ++i) h3[i] = act_fwd(a3, z3[i]);
-      constexpr bool TV = tail_valu<KSX>();   // as ae_minibatch_kernel (bit-identical results)
+      constexpr bool TV = tail_valu<KSX>() && !BF;   // as ae_minibatch_kernel (bit-identical results)
       f32x4 y[2], dz4[2], w4h[2];
 #pragma unroll
       for (int t4 = 0; t4 < (TV ? 1 : 2); ++t4) {
