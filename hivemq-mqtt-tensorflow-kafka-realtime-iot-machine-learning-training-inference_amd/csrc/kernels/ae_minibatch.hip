@@ -1029,6 +1029,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
         }
       }
       if (!stream && step) pcnt_wait_updates(S.cnt, st);
+      // BF: the backward's fragments read here, off the chain (the E-counter bumps between the
+      // backward layers are compiler barriers, so those reads could not move up by themselves;
+      // every update of the previous step has landed, and this step's come after the bumps)
+      f32x4 pg4[2], pg3, pg2;
+      if constexpr (BF) {
+        auto frag4 = [&](int base) {
+          return f32x4{S.w[base + lane], S.w[base + 64 + lane], S.w[base + 128 + lane], S.w[base + 192 + lane]};
+        };
+        pg4[0] = frag4(G4);
+        pg4[1] = frag4(G4 + 256);
+        pg3 = frag4(G3);
+        pg2 = frag4(G2);
+      }
       f32x4 z1 = ld4(S.w + BB1 + 4 * g);
 #pragma unroll
       for (int s4 = 0; s4 < KSX; s4 += 4) {
@@ -1100,7 +1113,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
       f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
       if constexpr (BF) {
 #pragma unroll
-        for (int s4 = 0; s4 < (TV ? 4 : KSX); s4 += 4) acc3 = kstep4<BF>(S.w + G4 + s4 * 64, lane, dz4[s4 >> 2], acc3);
+        for (int s4 = 0; s4 < (TV ? 4 : KSX); s4 += 4) acc3 = mfma16(pack4(pg4[s4 >> 2]), pack4(dz4[s4 >> 2]), acc3);
       } else {
 #pragma unroll
         for (int s = 0; s < (TV ? 4 : KSX); ++s) acc3 = mfma4(S.w[G4 + s * 64 + lane], dz4[s >> 2][s & 3], acc3);
@@ -1118,14 +1131,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ae
       st4(S.h2 + r * HS + cw, h2);
       st4(S.dz3 + r * HS + cw, dz3);
       f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
-      acc2 = kstep4<BF>(S.w + G3, lane, dz3, acc2);
+      if constexpr (BF) acc2 = mfma16(pack4(pg3), pack4(dz3), acc2);
+      else acc2 = kstep4<BF>(S.w + G3, lane, dz3, acc2);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dz2[i] = act_grad(a2, h2[i], acc2[i]);
       pcnt_bump(S.cnt + CE3, lane);   // h2, dz3 stored; G3 read
       st4(S.h1 + r * HS + cw, h1);
       st4(S.dz2 + r * HS + cw, dz2);
       f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
-      acc1 = kstep4<BF>(S.w + G2, lane, dz2, acc1);
+      if constexpr (BF) acc1 = mfma16(pack4(pg2), pack4(dz2), acc1);
+      else acc1 = kstep4<BF>(S.w + G2, lane, dz2, acc1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float h = h1[i];
