@@ -536,6 +536,23 @@ def main():
         dp.shutdown()
         sys.exit(2)
 
+    # every rank's device identity: an N-GPU record must show N distinct devices (or say it is a
+    # one-GPU rehearsal, SML_SHARE_GPU0=1); otherwise refuse -- no JSON line, exit 3
+    rehearsal = os.environ.get("SML_SHARE_GPU0") == "1"
+    me = dp.device_identity(device)
+    idents = gather_all(me, device)
+    devcheck = dp.check_distinct_devices(idents, world, rehearsal)
+    if not devcheck["ok"]:
+        if rank == 0:
+            print(f"[bench] refusing a n_gpus={world} record: {devcheck['reason']}", file=sys.stderr, flush=True)
+        dp.shutdown()
+        sys.exit(3)
+    peers = gather_all(dp.peer_access(device, [i.get("index", 0) for i in idents if i.get("host") == me["host"]]),
+                       device)
+    devices = {"world_size": world, "backend": env.backend, "rccl_version": dp.rccl_version(),
+               "n_distinct_devices": devcheck["n_distinct_devices"], "rehearsal": rehearsal,
+               "per_rank": [dict(i, rank=r, peer_access=pa) for r, (i, pa) in enumerate(zip(idents, peers))]}
+
     B = int(args.batch_per_gpu)
     rows = max(B, (int(args.dataset_rows) // B) * B)
     nslices = rows // B
@@ -646,6 +663,9 @@ def main():
             "micro_batch_per_gpu": B,
         },
         "backend": env.backend,
+        "rehearsal": rehearsal,
+        "n_distinct_devices": devcheck["n_distinct_devices"],
+        "devices": devices,
         "per_rank_ms_per_step": {"min": min(step_ms), "max": max(step_ms), "ranks": step_ms},
         "clock_settle": {"ms": args.settle_ms, "steps": settle_steps},
         "pack_ms": pack_ms,

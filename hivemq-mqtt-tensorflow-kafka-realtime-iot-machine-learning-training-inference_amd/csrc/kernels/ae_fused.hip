@@ -930,7 +930,10 @@ __device__ __forceinline__ void load_frags_packed(const AEArgs& a, int c, int g,
   F.w1a[1] = cat8(F.w1u[1], F.w1t);
   F.w2a = cat8(F.w2t[0], F.w2t[1]);
   F.w4ba = cat8(F.w4b[0], F.w4b[1]);
-  F.w4bua = cat8(F.w4bu, zb);
+  // the second K half meets an all-zero B half (d3's UP MFMA), so it can be any finite fragment:
+  // w3b's registers serve as that half instead of two more persistent zero registers
+  F.w4bua = cat8(F.w4bu, F.w3b);
+  (void)zb;
 }
 
 // Image slot s -> the packed-accumulator slab slots whose sum it is (-1: none, gradient 0).
@@ -977,142 +980,285 @@ __device__ __forceinline__ void packed_fold_src(int s, int& s1, int& s2) {
   s2 = base + (pin + 8) * w + out + (l3 ? 8 : 0);
 }
 
-// One packed pair of whole tiles.  TP: the pair's second tile is a stand-in whose loss,
-// metrics and gradients are all masked to zero (kept for an odd last tile; the kernel's
-// contiguous-pair loop takes even tile counts only and instantiates TP = false).
-template <int PACK, int DC, bool TP>
+// The two halves of lds_transpose, for operands whose transposed copy is only needed at the end
+// of the step: write it to its own slot as soon as it exists (its registers die there), read the
+// transposed copy back right before the weight-gradient MFMA (EW variants).
+__device__ __forceinline__ void tr_write(bf16x4 v, char* slot, int c, int g) {
+  *(lds_bf16x4*)(slot + c * 32 + 8 * g) = v;
+}
+__device__ __forceinline__ bf16x4 tr_read(char* slot, int c, int g) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(slot + (4 * g + (c >> 2)) * 32 + 8 * (c & 3)));
+}
+
+// NP packed pairs of whole tiles in ONE interleaved instruction stream (NP = 1 or 2).  Every
+// stage is a loop over the NP pairs, so with NP = 2 the two pairs' dependent MFMA -> activation
+// -> MFMA chains are independent instruction sequences the compiler interleaves: one pair's
+// VALU issues while the other's MFMA result is in flight (the chain has ~13 dependent stages;
+// one pair per wave leaves most of a trip waiting on them, profiles/r06/SUMMARY.md §1).  The
+// pairs share the weight fragments and the gradient accumulators; each has TS transpose slots.
+// TP: the LAST pair's second tile is a stand-in whose loss, metrics and gradients are all masked
+// to zero (kept for an odd last tile; the kernel's contiguous-pair loop takes even tile counts
+// only and instantiates TP = false).
+// XP: how the weight-gradient operands reach the rows-on-K layout.  0: LDS transposes at the end
+// of the step; 1: the forward ones written to LDS as soon as they exist (EW), the tile halves of
+// dW2 / dW4 in one accumulator each (MA); 2: no LDS at all -- each operand is the A operand of one
+// 16x16x16 MFMA against the identity (C = A . I is the operand in the rows-on-K C layout, exact in
+// fp32, repacked to bf16 bit-exactly), plus MA.  The LDS-transpose loop spends half its issue
+// stalls waiting to issue LDS instructions (SQ_WAIT_INST_LDS, profiles/r06/SUMMARY.md §1).
+template <int PACK, int DC, bool TP, int TS = 10, int NP = 1, int XP = 0>
 __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP& F, char* scr, int c, int g,
-                                                  const f32x4 (&xf)[2][2], float xup, const int (&ix)[2],
-                                                  f32x4 acc1[2], f32x4& acc2, f32x4& acc3,
+                                                  const f32x4 (&xf)[NP][2][2], const float (&xup)[NP],
+                                                  const int (&ix)[NP][2], f32x4 acc1[2], f32x4& acc2, f32x4& acc3,
                                                   f32x4 acc4[2], f32x4& acc2b, f32x4& acc4b, float& sq, float& ab,
                                                   float& corr, float& rows) {
   // xup: the UP-layout copy of inputs 16 / 17 (lane group g: input 16 + (g & 1) of tile g >> 1)
   static_assert(PACK == PACK_REF && DC == 18, "reference model, D = 18 (outputs 16, 17 packed as UP)");
+  static_assert(NP == 1 || NP == 2, "one or two pairs per iteration");
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const bf16x4 zb = {0, 0, 0, 0};
   const bool pad_lane = (g == 3);
   const bool lo = c < 8;   // lanes holding tile 0's half of a packed operand (as n or m = c)
+  auto stand_in = [](int p, int u) { return TP && p == NP - 1 && u == 1; };
+  constexpr bool EW = XP == 1, MA = XP >= 1, TRM = XP == 2;
+  // identity B operand (lane (n = c, g) holds k = 4g..4g+3): 1 where k == n
+  bf16x4 ident;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ident[j] = bfbits(4 * g + j == c ? 1.0f : 0.0f);
+  auto mfma_tr = [&](bf16x4 v) -> bf16x4 { return pack4(mfma16(v, ident, zero4)); };
 
-  bf16x4 xb0[2], h1b[2];
-  f32x4 h1[2], y[2];
+  bf16x4 xb0[NP][2], h1b[NP][2], xub[NP];
+  f32x4 h1[NP][2], y[NP][2], z1[NP][2], l1s[NP][2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) xb0[u] = pack4(xf[u][0]);
-  // inputs 16 / 17 of both tiles (UP) and the constant-1 bias input (k = 1, lane group 0) in
-  // one B operand; layer 1 is one 16x16x32 per tile: [inputs 0..15 | UP + bias]
-  const bf16x4 xub = pack4(f32x4{xup, g == 0 ? 1.0f : 0.0f, 0.f, 0.f});
-  f32x4 z1[2], l1s[2];
-  z1[0] = mfma32a(F.w1a[0], xb0[0], xub, zero4);
-  z1[1] = mfma32a(F.w1a[1], xub, xb0[1], zero4);
+  for (int p = 0; p < NP; ++p) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) h1[u][i] = tanh_exp2(z1[u][i]);
-    h1b[u] = pack4(h1[u]);
+    for (int u = 0; u < 2; ++u) xb0[p][u] = pack4(xf[p][u][0]);
+    // inputs 16 / 17 of both tiles (UP) and the constant-1 bias input (k = 1, lane group 0) in
+    // one B operand; layer 1 is one 16x16x32 per tile: [inputs 0..15 | UP + bias]
+    xub[p] = pack4(f32x4{xup[p], g == 0 ? 1.0f : 0.0f, 0.f, 0.f});
+    if constexpr (EW) {   // slots 0..6 of the pair: the forward operands of the weight gradients
+      tr_write(xb0[p][0], scr + (p * 10 + 0) * 512, c, g);
+      tr_write(xb0[p][1], scr + (p * 10 + 1) * 512, c, g);
+      tr_write(xub[p], scr + (p * 10 + 2) * 512, c, g);
+    }
   }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    z1[p][0] = mfma32a(F.w1a[0], xb0[p][0], xub[p], zero4);
+    z1[p][1] = mfma32a(F.w1a[1], xub[p], xb0[p][1], zero4);
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h1[p][u][i] = tanh_exp2(z1[p][u][i]);
+      h1b[p][u] = pack4(h1[p][u]);
+      if constexpr (EW) tr_write(h1b[p][u], scr + (p * 10 + 3 + u) * 512, c, g);
+    }
   // Keras L1 activity-regulariser gradient l1 * sign(h1) as one v_med3 (see train_tile), computed
-  // off the critical path and fed to the dh1 MFMA as its accumulator input
+  // off the critical path and fed to the dh1 MFMA as its accumulator input (EW: right before it,
+  // so its registers are not live across the whole step)
+  auto l1_sign = [&] {
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+    for (int p = 0; p < NP; ++p)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) l1s[u][i] = (TP && u == 1) ? 0.f : __builtin_amdgcn_fmed3f(h1[u][i], -a.l1, a.l1);
-  const f32x4 z2 = mfma32a(F.w2a, h1b[0], h1b[1], zero4);
-  f32x4 h2, h3;
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) h2[i] = relu_fast(z2[i]);
-  const bf16x4 h2b = pack4(h2);
-  const f32x4 z3 = mfma16(F.w3t, h2b, zero4);
+        for (int i = 0; i < 4; ++i) l1s[p][u][i] = stand_in(p, u) ? 0.f : __builtin_amdgcn_fmed3f(h1[p][u][i], -a.l1, a.l1);
+  };
+  if constexpr (!MA) l1_sign();
+  f32x4 z2[NP], h2[NP], h3[NP], z3[NP];
+  bf16x4 h2b[NP], h3b[NP];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) h3[i] = tanh_exp2(z3[i]);
-  const bf16x4 h3b = pack4(h3);
+  for (int p = 0; p < NP; ++p) z2[p] = mfma32a(F.w2a, h1b[p][0], h1b[p][1], zero4);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h2[p][i] = relu_fast(z2[p][i]);
+    h2b[p] = pack4(h2[p]);
+    if constexpr (EW) tr_write(h2b[p], scr + (p * 10 + 5) * 512, c, g);
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) z3[p] = mfma16(F.w3t, h2b[p], zero4);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h3[p][i] = tanh_exp2(z3[p][i]);
+    h3b[p] = pack4(h3[p]);
+    if constexpr (EW) tr_write(h3b[p], scr + (p * 10 + 6) * 512, c, g);
+  }
   // output layer: outputs 0..15 per tile, outputs 16 / 17 of BOTH tiles in one register (UP:
   // lane group g = output 16 + (g & 1) of tile g >> 1; w4u's rows m = 4q, so only C entry 0 is used)
-  f32x4 dz4[2];
+  f32x4 dz4[NP][2], z4[NP][2], z4u[NP];
+  float dz4up[NP], yup[NP];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const f32x4 z4 = mfma16(F.w4t[u], h3b, zero4);
+  for (int p = 0; p < NP; ++p) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      y[u][i] = relu_fast(z4[i]);
-      float e = y[u][i] - xf[u][0][i];
-      if (TP && u == 1) e = 0.f;
-      sq = fmaf(e, e, sq);
-      dz4[u][i] = y[u][i] > 0.f ? e : 0.f;   // relu'; x 2/D folded into F.w4b / the acc4 slab
-    }
+    for (int u = 0; u < 2; ++u) z4[p][u] = mfma16(F.w4t[u], h3b[p], zero4);
+    z4u[p] = mfma16(F.w4u, h3b[p], zero4);
   }
-  const f32x4 z4u = mfma16(F.w4u, h3b, zero4);
-  const float yup = relu_fast(z4u[0]);
-  float eup = yup - xup;
-  if (TP) eup = g < 2 ? eup : 0.f;
-  sq = fmaf(eup, eup, sq);
-  const float dz4up = yup > 0.f ? eup : 0.f;
-  if (a.want_acc) {   // lane group 0 counts row c of tile 0, group 1 row c of tile 1
-    const int iy = row_argmax_up_pair(y[0], y[1], yup, g);
-    const int sel = -(g & 1);   // bit-select: a ?: on the pair becomes a scratch array indexed by g
-    const int ixs = (ix[0] & ~sel) | (ix[1] & sel);
-    corr += ((TP ? g == 0 : g < 2) && iy == ixs) ? 1.f : 0.f;
-  }
-  rows += (g == 0) ? (TP ? 1.f : 2.f) : 0.f;
-
-  bf16x4 dz4b[2], dz1b[2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) dz4b[u] = pack4(dz4[u]);
-  const bf16x4 dz4bu = pack4(f32x4{dz4up, 0.f, 0.f, 0.f});
-  f32x4 d3 = mfma32a(F.w4ba, dz4b[0], dz4b[1], zero4);   // K halves: tile 0 / tile 1 outputs 0..15
-  d3 = mfma32a(F.w4bua, dz4bu, zb, d3);                  // + outputs 16 / 17 (one shape per chain)
-  f32x4 dz3, dz2;
+  for (int p = 0; p < NP; ++p) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) dz3[i] = d3[i] * fmaf(-h3[i], h3[i], 1.0f);   // 0 at the bias slots (h = 1)
-  const bf16x4 dz3b = pack4(dz3);
-  const f32x4 d2 = mfma16(F.w3b, dz3b, zero4);
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) dz2[i] = h2[i] > 0.f ? d2[i] : 0.f;
-  const bf16x4 dz2b = pack4(dz2);
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const f32x4 d1 = mfma16(F.w2b[u], dz2b, l1s[u]);   // dh1 + l1 * sign(h1)
-    f32x4 dz1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float hv = h1[u][i];
-      if (TP && u == 1) {
-        dz1[i] = 0.f;
-        continue;
+      for (int i = 0; i < 4; ++i) {
+        y[p][u][i] = relu_fast(z4[p][u][i]);
+        float e = y[p][u][i] - xf[p][u][0][i];
+        if (stand_in(p, u)) e = 0.f;
+        sq = fmaf(e, e, sq);
+        dz4[p][u][i] = y[p][u][i] > 0.f ? e : 0.f;   // relu'; x 2/D folded into F.w4b / the acc4 slab
       }
-      ab += (i == 3 && pad_lane) ? 0.f : fabsf(hv);
-      dz1[i] = d1[i] * fmaf(-hv, hv, 1.0f);
-    }
-    dz1b[u] = pack4(dz1);
+    yup[p] = relu_fast(z4u[p][0]);
+    float eup = yup[p] - xup[p];
+    if (TP && p == NP - 1) eup = g < 2 ? eup : 0.f;
+    sq = fmaf(eup, eup, sq);
+    dz4up[p] = yup[p] > 0.f ? eup : 0.f;
   }
-
-  // weight gradients (rows on K through the LDS transpose)
-  bf16x4 xr0[2], dz1r[2], h1r[2], dz4r[2];
-  const bf16x4 xur = lds_transpose(xub, scr + 1 * 512, c, g);
+  if (a.want_acc) {   // lane group 0 counts row c of tile 0, group 1 row c of tile 1
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    xr0[u] = lds_transpose(xb0[u], scr + 0 * 512, c, g);
-    dz1r[u] = lds_transpose(dz1b[u], scr + 2 * 512, c, g);
-    h1r[u] = lds_transpose(h1b[u], scr + 3 * 512, c, g);
-    dz4r[u] = lds_transpose(dz4b[u], scr + 8 * 512, c, g);
+    for (int p = 0; p < NP; ++p) {
+      const int iy = row_argmax_up_pair(y[p][0], y[p][1], yup[p], g);
+      const int sel = -(g & 1);   // bit-select: a ?: on the pair becomes a scratch array indexed by g
+      const int ixs = (ix[p][0] & ~sel) | (ix[p][1] & sel);
+      corr += (((TP && p == NP - 1) ? g == 0 : g < 2) && iy == ixs) ? 1.f : 0.f;
+    }
   }
-  const bf16x4 dz4ru = lds_transpose(dz4bu, scr + 9 * 512, c, g);
-  const bf16x4 dz2r = lds_transpose(dz2b, scr + 4 * 512, c, g);
-  const bf16x4 h2r = lds_transpose(h2b, scr + 5 * 512, c, g);
-  const bf16x4 dz3r = lds_transpose(dz3b, scr + 6 * 512, c, g);
-  const bf16x4 h3r = lds_transpose(h3b, scr + 7 * 512, c, g);
-  acc1[0] = mfma32(xr0[0], xr0[1], dz1r[0], dz1r[1], acc1[0]);
-  // rows 16 + m: m = 0 / 4 tile 0's inputs 16 / 17, m = 8 / 12 tile 1's, m = 1 the bias (both)
-  acc1[1] = mfma32(lo ? xur : zb, (!lo || c == 1) ? xur : zb, dz1r[0], dz1r[1], acc1[1]);
-  // dW2 / dW4 (outputs 0..15): each tile against the whole packed operand, in an accumulator
-  // of its own (only its half -- n < 8 / m < 8 for tile 0 -- is kept when the slab is written):
-  // two 16x16x16 instead of a 16x16x32 on lane-masked copies (no per-pair selects)
-  acc2 = mfma16(h1r[0], dz2r, acc2);
-  acc2b = mfma16(h1r[1], dz2r, acc2b);
-  acc3 = mfma16(h2r, dz3r, acc3);   // diagonal blocks; acc3's chain is 16x16x16 only in this variant
-  acc4[0] = mfma16(h3r, dz4r[0], acc4[0]);
-  acc4b = mfma16(h3r, dz4r[1], acc4b);
-  // outputs 16 / 17: UP columns 4q pair with their own tile's rows m by construction (the
-  // other tile's blocks are never folded), so h3r needs no mask; acc4[1]'s chain is 16x16x16
-  acc4[1] = mfma16(h3r, dz4ru, acc4[1]);
+  rows += (g == 0) ? (TP ? 2.f * NP - 1.f : 2.f * NP) : 0.f;
+
+  bf16x4 dz4b[NP][2], dz1b[NP][2], dz4bu[NP], dz3b[NP], dz2b[NP];
+  f32x4 d3[NP], d2[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) dz4b[p][u] = pack4(dz4[p][u]);
+    dz4bu[p] = pack4(f32x4{dz4up[p], 0.f, 0.f, 0.f});
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    d3[p] = mfma32a(F.w4ba, dz4b[p][0], dz4b[p][1], zero4);   // K halves: tile 0 / tile 1 outputs 0..15
+    d3[p] = mfma32a(F.w4bua, dz4bu[p], zb, d3[p]);             // + outputs 16 / 17 (one shape per chain)
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    f32x4 dz3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dz3[i] = d3[p][i] * fmaf(-h3[p][i], h3[p][i], 1.0f);   // 0 at the bias slots (h = 1)
+    dz3b[p] = pack4(dz3);
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) d2[p] = mfma16(F.w3b, dz3b[p], zero4);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    f32x4 dz2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dz2[i] = h2[p][i] > 0.f ? d2[p][i] : 0.f;
+    dz2b[p] = pack4(dz2);
+  }
+  f32x4 d1[NP][2];
+  if constexpr (MA) l1_sign();
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) d1[p][u] = mfma16(F.w2b[u], dz2b[p], l1s[p][u]);   // dh1 + l1 * sign(h1)
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x4 dz1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float hv = h1[p][u][i];
+        if (stand_in(p, u)) {
+          dz1[i] = 0.f;
+          continue;
+        }
+        ab += (i == 3 && pad_lane) ? 0.f : fabsf(hv);
+        dz1[i] = d1[p][u][i] * fmaf(-hv, hv, 1.0f);
+      }
+      dz1b[p][u] = pack4(dz1);
+    }
+
+  // weight gradients (rows on K through the LDS transpose).  Pair p owns slots [p*TS, p*TS + TS);
+  // TS < 10: slots k and k + TS share 512 B of scratch -- a wave's LDS operations execute in order,
+  // so a later write cannot overtake an earlier transposed read of the same slot
+  // EW: slots 0..6 hold the forward operands written early, 7..9 take the backward ones in turn.
+  static_assert(TS >= 1 && TS <= 10 && (!EW || TS == 10), "transpose slots");
+  (void)mfma_tr;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    char* sp = scr + p * TS * 512;
+    bf16x4 xr0[2], dz1r[2], h1r[2], dz4r[2], xur, dz4ru, dz2r, h2r, dz3r, h3r;
+    if constexpr (TRM) {
+      xr0[0] = mfma_tr(xb0[p][0]);
+      xr0[1] = mfma_tr(xb0[p][1]);
+      xur = mfma_tr(xub[p]);
+      h1r[0] = mfma_tr(h1b[p][0]);
+      h1r[1] = mfma_tr(h1b[p][1]);
+      h2r = mfma_tr(h2b[p]);
+      h3r = mfma_tr(h3b[p]);
+      dz4r[0] = mfma_tr(dz4b[p][0]);
+      dz4r[1] = mfma_tr(dz4b[p][1]);
+      dz4ru = mfma_tr(dz4bu[p]);
+      dz3r = mfma_tr(dz3b[p]);
+      dz2r = mfma_tr(dz2b[p]);
+      dz1r[0] = mfma_tr(dz1b[p][0]);
+      dz1r[1] = mfma_tr(dz1b[p][1]);
+    } else if constexpr (EW) {
+      xr0[0] = tr_read(sp + 0 * 512, c, g);
+      xr0[1] = tr_read(sp + 1 * 512, c, g);
+      xur = tr_read(sp + 2 * 512, c, g);
+      h1r[0] = tr_read(sp + 3 * 512, c, g);
+      h1r[1] = tr_read(sp + 4 * 512, c, g);
+      h2r = tr_read(sp + 5 * 512, c, g);
+      h3r = tr_read(sp + 6 * 512, c, g);
+      dz4r[0] = lds_transpose(dz4b[p][0], sp + 7 * 512, c, g);
+      dz4r[1] = lds_transpose(dz4b[p][1], sp + 8 * 512, c, g);
+      dz4ru = lds_transpose(dz4bu[p], sp + 9 * 512, c, g);
+      dz3r = lds_transpose(dz3b[p], sp + 7 * 512, c, g);
+      dz2r = lds_transpose(dz2b[p], sp + 8 * 512, c, g);
+      dz1r[0] = lds_transpose(dz1b[p][0], sp + 9 * 512, c, g);
+      dz1r[1] = lds_transpose(dz1b[p][1], sp + 7 * 512, c, g);
+    } else {
+      xur = lds_transpose(xub[p], sp + (1 % TS) * 512, c, g);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        xr0[u] = lds_transpose(xb0[p][u], sp + (0 % TS) * 512, c, g);
+        dz1r[u] = lds_transpose(dz1b[p][u], sp + (2 % TS) * 512, c, g);
+        h1r[u] = lds_transpose(h1b[p][u], sp + (3 % TS) * 512, c, g);
+        dz4r[u] = lds_transpose(dz4b[p][u], sp + (8 % TS) * 512, c, g);
+      }
+      dz4ru = lds_transpose(dz4bu[p], sp + (9 % TS) * 512, c, g);
+      dz2r = lds_transpose(dz2b[p], sp + (4 % TS) * 512, c, g);
+      h2r = lds_transpose(h2b[p], sp + (5 % TS) * 512, c, g);
+      dz3r = lds_transpose(dz3b[p], sp + (6 % TS) * 512, c, g);
+      h3r = lds_transpose(h3b[p], sp + (7 % TS) * 512, c, g);
+    }
+    acc1[0] = mfma32(xr0[0], xr0[1], dz1r[0], dz1r[1], acc1[0]);
+    // rows 16 + m: m = 0 / 4 tile 0's inputs 16 / 17, m = 8 / 12 tile 1's, m = 1 the bias (both)
+    acc1[1] = mfma32(lo ? xur : zb, (!lo || c == 1) ? xur : zb, dz1r[0], dz1r[1], acc1[1]);
+    // dW2 / dW4 (outputs 0..15): each tile against the whole packed operand, in an accumulator
+    // of its own (only its half -- n < 8 / m < 8 for tile 0 -- is kept when the slab is written):
+    // two 16x16x16 instead of a 16x16x32 on lane-masked copies (no per-pair selects)
+    if constexpr (MA) {
+      // 8 fewer accumulator registers: each tile's contraction against its own half of the packed
+      // operand (the other half lane-masked to 0) in ONE 16x16x32 -- dW2 columns n < 8 / n >= 8
+      // (lane c) from tile 0 / 1, dW4 rows m < 8 / m >= 8 (lane c of the A operand) likewise; the
+      // masked products are exact zeros, acc2b / acc4b stay 0 and the slab fold keeps acc2 / acc4[0]
+      acc2 = mfma32(h1r[0], h1r[1], lo ? dz2r : zb, lo ? zb : dz2r, acc2);
+      acc3 = mfma16(h2r, dz3r, acc3);
+      acc4[0] = mfma32(lo ? h3r : zb, lo ? zb : h3r, dz4r[0], dz4r[1], acc4[0]);
+    } else {
+      acc2 = mfma16(h1r[0], dz2r, acc2);
+      acc2b = mfma16(h1r[1], dz2r, acc2b);
+      acc3 = mfma16(h2r, dz3r, acc3);   // diagonal blocks; acc3's chain is 16x16x16 only in this variant
+      acc4[0] = mfma16(h3r, dz4r[0], acc4[0]);
+      acc4b = mfma16(h3r, dz4r[1], acc4b);
+    }
+    // outputs 16 / 17: UP columns 4q pair with their own tile's rows m by construction (the
+    // other tile's blocks are never folded), so h3r needs no mask; acc4[1]'s chain is 16x16x16
+    acc4[1] = mfma16(h3r, dz4ru, acc4[1]);
+  }
 }
 
 // 3 waves/SIMD: caps the allocation at 168 VGPRs (no spills); 171 would drop to 2.
@@ -1124,14 +1270,39 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
 // wave) or 4 (128-VGPR budget, 3968-B ring per wave so four workgroups fit in LDS).
 // ILP 2 (tile pairs, 3 waves/SIMD): 7008 B = six 1168-B packed tiles per wave; with the
 // slab area and the normaliser 52928 B per workgroup, three workgroups per CU.
+// Packed pairs (ILP 3) at OCC >= 4: two pair slots (4 x 1168 B) per wave.
 template <int OCC, int ILP = 1>
-constexpr int ring_bytes() { return OCC >= 4 ? 3968 : (ILP >= 2 ? 7008 : 6144); }
+constexpr int ring_bytes() { return ILP == 3 ? (OCC >= 4 ? 4672 : 7008) : OCC >= 4 ? 3968 : (ILP >= 2 ? 7008 : 6144); }
+// packed pairs: PF tiles of 64 * 18 + 16 B (sized by the ring depth, not the occupancy)
+template <int OCC, int ILP, int PF>
+constexpr int ring_bytes_pf() { return ILP == 3 ? PF * 1168 : ring_bytes<OCC, ILP>(); }
 
-template <int PACK, bool VEC, int PF, int OCC, int DC = 0, int XM = 0, int ILP = 1>
+// LDS layout.  Default: [slab area = per-wave transpose scratch (10 x 512 B) | normaliser | rings].
+// Packed pairs (ILP 3): [TS x 512 B transpose scratch per wave | normaliser | rings], and the
+// per-wave gradient slabs written after the loop ALIAS that whole area (the rings are retired
+// with vmcnt(0) and a workgroup barrier first) -- so the loop's LDS is not charged for the slab:
+// OCC 4 (two pair slots, TS 10) is 39 424 B = four workgroups per CU.
+template <int PF, int OCC, int ILP, int TS, int NPW = 1>
+struct AELds {
+  static constexpr int SCR = (ILP == 3 ? NPW * TS : 10) * 512;      // per wave (0: MFMA transposes)
+  static constexpr int NORM_OFF = ILP == 3 ? WAVES * SCR : SLAB_BYTES;
+  static constexpr int RING_OFF = NORM_OFF + NORM_BYTES;
+  static constexpr int RING = ring_bytes_pf<OCC, ILP, PF>();
+  static constexpr int END = RING_OFF + (PF > 0 ? WAVES * RING : 0);
+  static constexpr int BYTES = END > SLAB_BYTES ? END : SLAB_BYTES;
+};
+
+// NPW (packed pairs only): pairs trained per loop iteration in one interleaved stream.
+// XP (packed pairs only): the weight-gradient operand path of train_pair_packed.
+template <int PACK, bool VEC, int PF, int OCC, int DC = 0, int XM = 0, int ILP = 1, int TS = 10, int NPW = 1,
+          int XP = 0>
 __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   constexpr bool FAST = zero_preserving<PACK>();
-  constexpr int RING = ring_bytes<OCC, ILP>();
+  using L = AELds<PF, OCC, ILP, (XP == 2 ? 0 : TS), NPW>;
+  static_assert(NPW == 1 || ILP == 3, "several pairs per iteration: packed pairs only");
+  constexpr int RING = L::RING;
   static_assert(WAVES * 10 * 512 <= SLAB_BYTES, "transpose scratch must fit in the slab buffer");
+  static_assert(ILP == 3 || TS == 10, "shared transpose slots: packed pairs only");
   static_assert(PF == 0 || PF * 64 * 17 <= RING, "ring slots must fit the smallest ring tile");
   // XM: x-argmax mode. 0 in-kernel argmax; 1 tile-packed ring (rows + ingest-time argmax
   // bytes per tile, pack_tiles_argmax); 2 / 3 A/B probes that skip the argmax of x entirely (wrong accuracy, timing
@@ -1141,12 +1312,12 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   static_assert(XM != 1 || (DC > 0 && PF > 0 && PF * (64 * DC + 16) <= RING), "XA: compile-time D, ring slots + argmax");
   // one LDS array: per-wave transpose scratch during the tile loop, per-wave
   // gradient slabs afterwards | the normaliser | (PF > 0) the per-wave input rings
-  __shared__ __attribute__((aligned(16))) float smem[(SLAB_BYTES + NORM_BYTES + (PF > 0 ? WAVES * RING : 0)) / 4];
+  __shared__ __attribute__((aligned(16))) float smem[L::BYTES / 4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
-  char* scr = reinterpret_cast<char*>(smem) + wid * (10 * 512);
-  const char* norm = reinterpret_cast<const char*>(smem) + SLAB_BYTES;
+  char* scr = reinterpret_cast<char*>(smem) + wid * L::SCR;
+  const char* norm = reinterpret_cast<const char*>(smem) + L::NORM_OFF;
   if (a.cursor) {  // streaming ring consumer (uniform scalar load)
     a.x += a.cursor[0] * a.ld;
     if (XM == 1) a.xpack += (a.cursor[0] >> 4) * (int64_t)(64 * a.D + 16);
@@ -1155,7 +1326,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   if (a.iter && blockIdx.x == 0 && threadIdx.x == 0) a.iter[0] += 1;
   if (threadIdx.x < 64) {
     const int f = threadIdx.x & 31;
-    smem[SLAB_BYTES / 4 + threadIdx.x] = threadIdx.x < 32 ? norm_scale(a, f) : norm_shift(a, f);
+    smem[L::NORM_OFF / 4 + threadIdx.x] = threadIdx.x < 32 ? norm_scale(a, f) : norm_shift(a, f);
   }
 
   Frags F;
@@ -1183,7 +1354,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
     constexpr int NV = 2;  // VMEM instructions per tile issue
     const int nl2 = (slotb - 1024) >> 4;  // lanes of the second 16-B-per-lane DMA (>= 4)
     const int uwid = __builtin_amdgcn_readfirstlane(wid);  // keep the ring bookkeeping scalar
-    const int ring_off = SLAB_BYTES + NORM_BYTES + uwid * RING;
+    const int ring_off = L::RING_OFF + uwid * RING;
     const unsigned ring_lds =
         (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem) + ring_off;
     const char* ring = reinterpret_cast<const char*>(smem) + ring_off;
@@ -1263,22 +1434,13 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
             glds16(src + 1024, voff, dst + 1024);
             if (lane < nl3) glds16(src + 2048, voff, dst + 2048);
           };
-          int64_t pp = ufirst;
-#pragma unroll
-          for (int k = 0; k < PS - 1; ++k) {
-            issue_pair(pp, k);
-            pp += stride;
-          }
-          int rs = 0, ws = PS - 1;
-          for (int64_t pi = ufirst; pi < npairs; pi += stride) {
-            issue_pair(pp, ws);
-            pp += stride;
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NVP * (PS - 1)) : "memory");
-            f32x4 xf[2][2];
-            int ix[2];
-            ring_tile(2 * rs, xf[0], ix[0]);
-            ring_tile(2 * rs + 1, xf[1], ix[1]);
-            float xup = ring_up(2 * rs);
+          // NPW pairs per iteration (pi, pi + stride, ...): the ring holds PS = PF / 2 pair slots, PS - NPW
+          // of them in flight while the NPW oldest are trained on.
+          static_assert(PS > NPW, "ring: at least one pair in flight");
+          auto load_pair = [&](int slot, f32x4 (&xf)[2][2], float& xup, int (&ix)[2]) {
+            ring_tile(2 * slot, xf[0], ix[0]);
+            ring_tile(2 * slot + 1, xf[1], ix[1]);
+            xup = ring_up(2 * slot);
             if constexpr (XM == 0) {
               // raw rows (the direct step: rows trained once): normalize_fn on the lane's inputs
               // 4g..4g+3 of both tiles and its UP input 16 + (g & 1), then argmax(x) of both
@@ -1295,10 +1457,43 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
               xup = fmaf(xup, usc, ush);
               ix[0] = ix[1] = a.want_acc ? row_argmax_up_pair_signed(xf[0][0], xf[1][0], xup, g) : -1;
             }
-            rs = rs + 1 == PS ? 0 : rs + 1;
-            ws = ws + 1 == PS ? 0 : ws + 1;
-            train_pair_packed<PACK, DC, false>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3, acc4, acc2b,
-                                               acc4b, sq, ab, corr, rows);
+          };
+          int64_t pp = ufirst;
+#pragma unroll
+          for (int k = 0; k < PS - NPW; ++k) {
+            issue_pair(pp, k);
+            pp += stride;
+          }
+          int rs = 0, ws = PS - NPW;
+          int64_t pi = ufirst;
+          for (; pi + (NPW - 1) * stride < npairs; pi += NPW * stride) {
+#pragma unroll
+            for (int k = 0; k < NPW; ++k) {
+              issue_pair(pp, ws);
+              pp += stride;
+              ws = ws + 1 == PS ? 0 : ws + 1;
+            }
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NVP * (PS - NPW)) : "memory");
+            f32x4 xf[NPW][2][2];
+            float xup[NPW];
+            int ix[NPW][2];
+#pragma unroll
+            for (int k = 0; k < NPW; ++k) {
+              load_pair(rs, xf[k], xup[k], ix[k]);
+              rs = rs + 1 == PS ? 0 : rs + 1;
+            }
+            train_pair_packed<PACK, DC, false, TS, NPW, XP>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3, acc4,
+                                                            acc2b, acc4b, sq, ab, corr, rows);
+          }
+          if (NPW == 2 && pi < npairs) {   // a last lone pair: the oldest of the PS - NPW in flight
+            static_assert(NPW == 1 || PS - NPW - 1 >= 0, "ring depth");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NVP * (PS - NPW - 1)) : "memory");
+            f32x4 xf[1][2][2];
+            float xup[1];
+            int ix[1][2];
+            load_pair(rs, xf[0], xup[0], ix[0]);
+            train_pair_packed<PACK, DC, false, TS, 1, XP>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3, acc4, acc2b,
+                                                          acc4b, sq, ab, corr, rows);
           }
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the ring is retired
         } else {
@@ -1408,8 +1603,10 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
   __syncthreads();  // all waves done with their transpose scratch
   float* my = smem + wid * NSLOT;
   if constexpr (ILP == 3) {   // tile 1's halves: dW2 columns n >= 8, dW4 rows m >= 8 (lane groups 2, 3)
-    acc2 = c < 8 ? acc2 : acc2b;
-    acc4[0] = g < 2 ? acc4[0] : acc4b;
+    if constexpr (XP == 0) {   // XP >= 1 (MA) holds both halves in acc2 / acc4[0]
+      acc2 = c < 8 ? acc2 : acc2b;
+      acc4[0] = g < 2 ? acc4[0] : acc4b;
+    }
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1677,6 +1874,18 @@ static bool direct_pairs() {
   const char* e = getenv("SML_AE_DIRECT_PAIRS");
   return !(e && e[0] == '0');
 }
+// SML_AE_PAIR_OCC=2|3|4: waves per SIMD (2: two packed pairs per loop iteration) of the packed-pair kernel on the tile-packed ring
+// (read at every launch, like SML_AE_ILP)
+static int pair_occ() {
+  const char* e = getenv("SML_AE_PAIR_OCC");
+  return (e && (e[0] == '2' || e[0] == '4')) ? e[0] - '0' : 3;
+}
+// SML_AE_PAIR_XP=0|1|2: the packed-pair weight-gradient operand path (train_pair_packed's XP;
+// 1 is implied at SML_AE_PAIR_OCC=4)
+static int pair_xp() {
+  const char* e = getenv("SML_AE_PAIR_XP");
+  return (e && e[0] == '2') ? 2 : 0;
+}
 static int train_occupancy() {
   const char* e = getenv("SML_AE_OCC");
   return (e && e[0] == '3') ? 3 : 4;
@@ -1684,7 +1893,7 @@ static int train_occupancy() {
 // The host sizes its partials buffer for 2 x this many workgroups per CU (the largest grid
 // of any variant: the pair variants' 3 rounds x 3 resident = 9 <= 10); the launcher trims
 // the grid to the launched variant's own rounds x residency.
-int ae_train_blocks_per_cu() { return 5; }
+int ae_train_blocks_per_cu() { return 8; }
 static int device_cus() {
   static const int cus = [] {
     int dev = 0, n = 0;
@@ -1738,13 +1947,13 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
   set_grid(2 * occ * device_cus());   // one-tile variants: two rounds of their residency
   // the pair variants hold 3 workgroups per CU.  SML_AE_ROUNDS: residency rounds of their grid;
   // default 3: 47.05 vs 46.86 (2), 46.17 (1), 46.86 (4) G rows/s (profiles/r02/ilp/rounds)
-  auto pair_grid = [&] {
+  auto pair_grid = [&](int occ_pairs = 3) {
     static const int rounds = [] {
       const char* e = std::getenv("SML_AE_ROUNDS");
       const int r = e ? std::atoi(e) : 3;
       return r >= 1 && r <= 8 ? r : 3;
     }();
-    set_grid(rounds * 3 * device_cus());
+    set_grid(rounds * occ_pairs * device_cus());
   };
   if (pack == PACK_REF) {
     // tile-packed ring with ingest-time x argmax (pack_tiles_argmax): whole 16-row tiles
@@ -1770,8 +1979,19 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 1, 2>), gd, bd, 0, stream, a);
     } else if (ring_ok && D == 18 && xa_ok && ((n >> 4) & 1) == 0 && train_ilp() == 3 && dims[1] <= 15 &&
                dims[2] <= 7 && dims[3] <= 7) {   // packed pairs: an even number of whole tiles
-      pair_grid();
-      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 1, 3>), gd, bd, 0, stream, a);
+      const int po = pair_occ();
+      pair_grid(po);
+      const int xp = pair_xp();
+      if (po == 2)   // two packed pairs per iteration, 2 waves / SIMD
+        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 8, 2, 18, 1, 3, 10, 2>), gd, bd, 0, stream, a);
+      else if (po == 4 && xp == 2)
+        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 4, 4, 18, 1, 3, 10, 1, 2>), gd, bd, 0, stream, a);
+      else if (po == 4)
+        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 4, 4, 18, 1, 3, 10, 1, 1>), gd, bd, 0, stream, a);
+      else if (xp == 2)
+        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 1, 3, 10, 1, 2>), gd, bd, 0, stream, a);
+      else
+        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 1, 3>), gd, bd, 0, stream, a);
     }
     else if (ring_ok && occ == 4 && D == 18 && xa_ok)
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18, 1>), gd, bd, 0, stream, a);

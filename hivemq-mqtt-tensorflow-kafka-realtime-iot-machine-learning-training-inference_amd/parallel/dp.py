@@ -216,6 +216,68 @@ def barrier(device: Optional[torch.device] = None) -> None:
             dist.barrier()
 
 
+def rccl_version() -> Optional[str]:
+    """The collective library's version as torch reports it (RCCL on ROCm), or None."""
+    try:
+        v = torch.cuda.nccl.version()
+    except Exception:  # noqa: BLE001 - no RCCL in this build / no GPU
+        return None
+    return ".".join(str(x) for x in v) if isinstance(v, (tuple, list)) else str(v)
+
+
+def device_identity(device: torch.device) -> dict:
+    """Who this rank is and which physical device it drives: host, pid, device index, PCI bus id,
+    UUID and name -- so a multi-GPU record can show that N distinct GPUs took part."""
+    import socket
+    ident = {"host": socket.gethostname(), "pid": os.getpid(), "device": str(device)}
+    if device.type == "cuda":
+        p = torch.cuda.get_device_properties(device)
+        ident.update(
+            name=p.name,
+            index=device.index if device.index is not None else torch.cuda.current_device(),
+            pci_bus_id="%04x:%02x:%02x.0" % (int(getattr(p, "pci_domain_id", 0)), int(getattr(p, "pci_bus_id", 0)),
+                                             int(getattr(p, "pci_device_id", 0))),
+            uuid=str(getattr(p, "uuid", "") or ""),
+            arch=str(getattr(p, "gcnArchName", "") or ""))
+    return ident
+
+
+def device_key(ident: dict) -> tuple:
+    """What makes two ranks' devices the same physical device: host + UUID (or PCI bus id)."""
+    return (ident.get("host"), ident.get("uuid") or ident.get("pci_bus_id") or ident.get("device"))
+
+
+def check_distinct_devices(idents, world: int, rehearsal: bool) -> dict:
+    """Decide whether a ``world``-rank measurement may be reported as ``n_gpus = world``: it needs
+    ``world`` distinct devices (by :func:`device_key`), unless it is a labelled rehearsal
+    (``SML_SHARE_GPU0=1``: every rank on GPU 0).  Returns ``{"ok", "n_distinct_devices",
+    "rehearsal", "reason"}``; a pure function, so the refusal logic is unit-tested on CPU."""
+    keys = [device_key(i) for i in idents]
+    n = len(set(keys))
+    ok = len(idents) == world and (n == world or rehearsal)
+    reason = ""
+    if len(idents) != world:
+        reason = f"{len(idents)} identities for world {world}"
+    elif n != world and not rehearsal:
+        reason = f"only {n} distinct device(s) among {world} ranks: {sorted(set(keys))}"
+    return {"ok": ok, "n_distinct_devices": n, "rehearsal": bool(rehearsal), "reason": reason}
+
+
+def peer_access(device: torch.device, peers) -> dict:
+    """``can_device_access_peer`` from this rank's device to each other local device index."""
+    out = {}
+    if device.type != "cuda":
+        return out
+    me = device.index if device.index is not None else torch.cuda.current_device()
+    for d in sorted(set(int(x) for x in peers)):
+        if d != me:
+            try:
+                out[str(d)] = bool(torch.cuda.can_device_access_peer(me, d))
+            except Exception as e:  # noqa: BLE001
+                out[str(d)] = repr(e)[:80]
+    return out
+
+
 def shutdown() -> None:
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()

@@ -362,3 +362,49 @@ def test_tile_pair_loop_matches_one_tile_loop(cuda_device, monkeypatch, ntiles, 
         assert _relerr(b[:NPARAM], a[:NPARAM]) < 1e-4
         assert abs(a[NPARAM] - b[NPARAM]) <= 1e-4 * abs(a[NPARAM])
     assert _relerr(out[ilp][1], out["1"][1]) < 1e-4
+
+
+@pytest.mark.parametrize("occ", ["2", "4", "3x2", "4x2"])
+@pytest.mark.parametrize("ntiles,blocks", [(64 * 5, 16), (64 * 4, 16), (4096, 48), (2 * 4096 + 6, 48), (2, 16)])
+def test_pair_occupancy_variants_bit_identical(cuda_device, monkeypatch, ntiles, blocks, occ):
+    """SML_AE_PAIR_OCC=2 (TWO packed pairs per loop iteration, one interleaved stream, 2 waves per
+    SIMD, a deeper ring) and =4 (one pair, 4 waves per SIMD, two ring pair slots, the gradient slabs
+    aliasing the loop's LDS, early transposed writes, merged tile-half accumulators) against the
+    default one-pair loop at 3 waves per SIMD, on the headline tile-packed ring.  The grid is capped
+    by max_blocks, so every wave trains the same pairs in the same order: occ 2 folds them into the
+    same accumulators (gradient image, metric sums and parameters after three steps bit-identical),
+    occ 4 sums the same products in another K order.  Pair counts per wave cover odd (a lone
+    last pair for the two-pair loop), even, one and zero."""
+    spec = AESpec()
+    w = _weights(spec, seed=5)
+    scale, shift = normalize_affine()
+    B = 16 * ntiles
+    rng = np.random.default_rng(29)
+    raw = torch.from_numpy((rng.uniform(0, 1, size=(2 * B, 18)) * 40).astype(np.float32)).to(cuda_device)
+    out = {}
+    for v in ("3", occ):
+        monkeypatch.setenv("SML_AE_PAIR_OCC", v[0])
+        monkeypatch.setenv("SML_AE_PAIR_XP", v[2:] or "0")   # "3x2": MFMA transposes (XP 2)
+        f = FusedAE(spec, w, cuda_device, max_blocks=blocks, scale=scale, shift=shift)
+        f.attach_ring(raw, B)
+        assert f.ring_xpack is not None
+        imgs = []
+        for _ in range(3):
+            f.step_ring(allreduce=lambda g: imgs.append(g.detach().cpu().numpy().copy()))
+        torch.cuda.synchronize()
+        out[v] = (imgs, f.params.detach().cpu().numpy())
+    from streamml.ops.ae import NPARAM
+    if occ == "2":
+        for a, b in zip(out["3"][0], out[occ][0]):
+            np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(out["3"][1], out[occ][1])
+        return
+    # occ 4 sums each tile's dW2 / dW4 half in one 16x16x32 against lane-masked operands (the
+    # other tile's products are exact zeros): the same sums in another K order
+    one, two = out["3"][0], out[occ][0]
+    np.testing.assert_array_equal(one[0][NPARAM + 2:], two[0][NPARAM + 2:])   # correct, rows
+    np.testing.assert_allclose(two[0][NPARAM:NPARAM + 2], one[0][NPARAM:NPARAM + 2], rtol=1e-6)
+    assert _relerr(two[0][:NPARAM], one[0][:NPARAM]) < 1e-6
+    for a, b in zip(one[1:], two[1:]):
+        assert _relerr(b[:NPARAM], a[:NPARAM]) < 1e-4
+    assert _relerr(out[occ][1], out["3"][1]) < 1e-4

@@ -57,6 +57,11 @@ def test_bench_two_ranks_shared_gpu(tmp_path, cuda_device):
     assert out["config"]["global_batch"] == 2 * 65536 and out["config"]["parallelism"] == "dp2"
     assert out["value"] > 0 and np.isfinite(out["final_epoch_loss"])
     assert out["backend"] == "gloo" and len(out["per_rank_ms_per_step"]["ranks"]) == 2
+    # the record says what it is: two ranks on ONE device, a labelled rehearsal
+    assert out["rehearsal"] is True and out["n_distinct_devices"] == 1, out["devices"]
+    devs = out["devices"]
+    assert devs["world_size"] == 2 and [d["rank"] for d in devs["per_rank"]] == [0, 1]
+    assert len({d["pci_bus_id"] for d in devs["per_rank"]}) == 1 and all(d["pid"] > 0 for d in devs["per_rank"])
     # config 5 per replica: both ranks scored their own shard
     assert len(out["infer_per_replica_p50_us"]) == 2 and all(v > 0 for v in out["infer_per_replica_p50_us"])
     coll = out["small_allreduce"]
