@@ -478,6 +478,7 @@ void Feed::run(int w) {
     stats_.fetches += loc.fetches;
     stats_.fetch_s += loc.fetch_s;
     stats_.decode_s += loc.decode_s;
+    stats_.reset_skipped += loc.reset_skipped;
     stats_.wait_slab_s += loc.wait_slab_s;
     loc = Stats();
   };
@@ -509,7 +510,16 @@ void Feed::run(int w) {
           const auto t0 = Clock::now();
           size_t off = 0, len = 0;
           const int wait = (mine.size() == 1 || (!prev_progress && q == 0)) ? cfg_.max_wait_ms : 0;
-          cl->fetch_raw(P.spec.topic, P.spec.partition, pos, cfg_.max_bytes, wait, S.resp, off, len);
+          try {
+            cl->fetch_raw(P.spec.topic, P.spec.partition, pos, cfg_.max_bytes, wait, S.resp, off, len);
+          } catch (const kafka::Error& e) {
+            if (e.code != 1 || cfg_.offset_reset == 2) throw;   // 1: OFFSET_OUT_OF_RANGE
+            int64_t np = cl->list_offset(P.spec.topic, P.spec.partition, cfg_.offset_reset == 1 ? -1 : -2);
+            if (P.spec.end >= 0) np = std::min(np, P.spec.end);
+            if (np > pos) loc.reset_skipped += (uint64_t)(np - pos);
+            P.pos.store(np, std::memory_order_relaxed);
+            continue;
+          }
           loc.fetch_s += secs(t0, Clock::now());
           ++loc.fetches;
           if (len == 0) continue;

@@ -54,10 +54,14 @@ struct FeedConfig {
   // librdkafka's check.crcs (default false there too): verify every record batch's CRC-32C.
   // The checksum is one dependent crc32 chain over every byte (~16 ns of a ~45 ns row decode)
   bool check_crcs = false;
+  // auto.offset.reset after OFFSET_OUT_OF_RANGE (the position was deleted by retention):
+  // 0 earliest, 1 latest, 2 none (the worker fails)
+  int offset_reset = 0;
 };
 
 struct Stats {
   uint64_t records = 0, rows = 0, dropped = 0, errors = 0, bytes = 0, fetches = 0, slabs = 0;
+  uint64_t reset_skipped = 0;   // records jumped over by auto.offset.reset
   double fetch_s = 0, decode_s = 0, wait_slab_s = 0;
 };
 

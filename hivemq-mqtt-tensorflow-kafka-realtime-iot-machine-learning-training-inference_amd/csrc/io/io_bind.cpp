@@ -228,7 +228,19 @@ PYBIND11_MODULE(_io, m) {
 
   py::register_exception<h5::Error>(m, "H5Error");
   py::register_exception<avro::Error>(m, "AvroError");
-  py::register_exception<kafka::Error>(m, "KafkaError");
+  // KafkaError carries the protocol error code as `.code` (1 = OFFSET_OUT_OF_RANGE: the consumer's
+  // position was deleted by retention -> auto.offset.reset)
+  static py::exception<kafka::Error> kafka_exc(m, "KafkaError");
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const kafka::Error& e) {
+      py::object cls = py::reinterpret_borrow<py::object>(kafka_exc.ptr());
+      py::object inst = cls(py::str(e.what()));
+      inst.attr("code") = e.code;
+      PyErr_SetObject(kafka_exc.ptr(), inst.ptr());
+    }
+  });
 
   // HDF5
   m.def("h5_read", [](const std::string& path) { return node_to_py(h5::read_file(path)); }, py::arg("path"));
@@ -446,7 +458,8 @@ PYBIND11_MODULE(_io, m) {
                        std::vector<int> feature_fields, bool framing, bool emit_recon, int max_batch,
                        int32_t max_bytes, int32_t max_wait_ms, double commit_interval_s, bool record_latency,
                        uintptr_t api, int spin_us, std::vector<std::pair<std::string, int>> json_columns,
-                       const std::string& json_stamp, std::vector<std::pair<uint64_t, uint64_t>> hash_ranges) {
+                       const std::string& json_stamp, std::vector<std::pair<uint64_t, uint64_t>> hash_ranges,
+                       int offset_reset) {
              kafka::ClientConfig c;
              c.client_id = client_id;
              c.sasl_mechanism = mech;
@@ -472,6 +485,7 @@ PYBIND11_MODULE(_io, m) {
              lc.json_columns = std::move(json_columns);
              lc.json_stamp = json_stamp;
              lc.hash_ranges = std::move(hash_ranges);
+             lc.offset_reset = offset_reset;
              return new serve::ScoreLoop(bootstrap, c, fields_from_py(fields), lc,
                                          reinterpret_cast<const SmlScorerApi*>(api));
            }),
@@ -482,7 +496,7 @@ PYBIND11_MODULE(_io, m) {
            py::arg("max_batch"), py::arg("max_bytes"), py::arg("max_wait_ms"), py::arg("commit_interval_s"),
            py::arg("record_latency"), py::arg("scorer_api"), py::arg("spin_us") = 0,
            py::arg("json_columns") = std::vector<std::pair<std::string, int>>{}, py::arg("json_stamp") = "",
-           py::arg("hash_ranges") = std::vector<std::pair<uint64_t, uint64_t>>{})
+           py::arg("hash_ranges") = std::vector<std::pair<uint64_t, uint64_t>>{}, py::arg("offset_reset") = 0)
       .def("run",
            [](serve::ScoreLoop& l, int64_t max_events, double idle_timeout_s) {
              serve::LoopStats st;
@@ -508,6 +522,7 @@ PYBIND11_MODULE(_io, m) {
              d["keys"] = st.keys;
              d["foreign"] = st.foreign;
              d["keys_dropped"] = st.keys_dropped;
+             d["reset_skipped"] = st.reset_skipped;
              return d;
            },
            py::arg("max_events") = 0, py::arg("idle_timeout_s") = -1.0)
@@ -642,7 +657,8 @@ PYBIND11_MODULE(_io, m) {
                        const std::string& user, const std::string& pw, int timeout_ms, const py::list& fields,
                        std::vector<int> feature_fields, int label_field, int keep_label, bool framing,
                        int32_t max_bytes, int32_t max_wait_ms, int workers, double idle_timeout_s,
-                       const std::vector<std::tuple<std::string, int, int64_t, int64_t>>& parts, bool check_crcs) {
+                       const std::vector<std::tuple<std::string, int, int64_t, int64_t>>& parts, bool check_crcs,
+                       int offset_reset) {
              kafka::ClientConfig c;
              c.client_id = client_id;
              c.sasl_mechanism = mech;
@@ -659,6 +675,7 @@ PYBIND11_MODULE(_io, m) {
              fc.workers = workers;
              fc.idle_timeout_s = idle_timeout_s;
              fc.check_crcs = check_crcs;
+             fc.offset_reset = offset_reset;
              std::vector<feed::PartSpec> ps;
              for (const auto& t : parts) ps.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t)});
              return new feed::Feed(bootstrap, c, fields_from_py(fields), fc, ps);
@@ -667,7 +684,7 @@ PYBIND11_MODULE(_io, m) {
            py::arg("sasl_password"), py::arg("timeout_ms"), py::arg("fields"), py::arg("feature_fields"),
            py::arg("label_field"), py::arg("keep_label"), py::arg("framing"), py::arg("max_bytes"),
            py::arg("max_wait_ms"), py::arg("workers"), py::arg("idle_timeout_s"), py::arg("parts"),
-           py::arg("check_crcs") = false)
+           py::arg("check_crcs") = false, py::arg("offset_reset") = 0)
       .def("start",
            [](feed::Feed& f, const std::vector<uint64_t>& slabs, int64_t cap) {
              std::vector<uintptr_t> v(slabs.begin(), slabs.end());
@@ -744,24 +761,39 @@ PYBIND11_MODULE(_io, m) {
         d["fetch_s"] = s.fetch_s;
         d["decode_s"] = s.decode_s;
         d["wait_slab_s"] = s.wait_slab_s;
+        d["reset_skipped"] = s.reset_skipped;
         return d;
       });
 
   py::class_<kafka::Broker>(m, "KafkaBroker")
       .def(py::init([](int port, const std::string& user, const std::string& pw, int64_t retention,
-                       int64_t message_max_bytes) {
+                       int64_t message_max_bytes, int64_t retention_ms, int64_t retention_bytes, int check_ms) {
              kafka::BrokerConfig c;
              c.port = port;
              c.sasl_username = user;
              c.sasl_password = pw;
              c.retention_records = retention;
              c.message_max_bytes = message_max_bytes;
+             c.retention_ms = retention_ms;
+             c.retention_bytes = retention_bytes;
+             c.retention_check_ms = check_ms;
              return new kafka::Broker(c);
            }),
            py::arg("port") = 0, py::arg("sasl_username") = "", py::arg("sasl_password") = "",
-           py::arg("retention_records") = -1, py::arg("message_max_bytes") = 1048588)
+           py::arg("retention_records") = -1, py::arg("message_max_bytes") = 1048588, py::arg("retention_ms") = -1,
+           py::arg("retention_bytes") = -1, py::arg("retention_check_ms") = 1000)
       .def_property_readonly("port", &kafka::Broker::port)
-      .def("create_topic", &kafka::Broker::create_topic)
+      .def("create_topic", &kafka::Broker::create_topic, py::arg("name"), py::arg("partitions"),
+           py::arg("retention_ms") = -2, py::arg("retention_bytes") = -2)
+      .def("enforce_retention",
+           [](kafka::Broker& b) {
+             py::gil_scoped_release rel;
+             return b.enforce_retention();
+           })
+      .def_property_readonly("deleted_segments", &kafka::Broker::deleted_segments)
+      .def_property_readonly("deleted_records", &kafka::Broker::deleted_records)
+      .def("log_bytes", &kafka::Broker::log_bytes)
+      .def("log_segments", &kafka::Broker::log_segments)
       .def("append",
            [](kafka::Broker& b, const std::string& t, int p, const py::list& values, py::object keys,
               py::object ts) { return b.append(t, p, records_from_py(values, keys, ts)); },

@@ -992,6 +992,88 @@ Broker::Broker(BrokerConfig cfg) : cfg_(std::move(cfg)) {
   port_ = ntohs(addr.sin_port);
   running_ = true;
   accept_thread_ = std::thread([this] { accept_loop(); });
+  retention_thread_ = std::thread([this] { retention_loop(); });
+}
+
+static int64_t steady_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+void Broker::retention_loop() {
+  std::unique_lock<std::mutex> g(mu_);
+  while (running_) {
+    retention_cv_.wait_for(g, std::chrono::milliseconds(std::max(cfg_.retention_check_ms, 10)));
+    if (!running_) break;
+    enforce_locked(steady_ms());
+  }
+}
+
+size_t Broker::enforce_retention() {
+  std::lock_guard<std::mutex> g(mu_);
+  return enforce_locked(steady_ms());
+}
+
+// Kafka's log cleaner in delete mode: per partition, whole segments oldest first -- while the
+// oldest is older than retention.ms (time), or while the log would still hold retention.bytes
+// without it (size; the newest segment is always kept).  A consumer positioned inside a deleted
+// range then gets OFFSET_OUT_OF_RANGE and follows its auto.offset.reset.  Segment bytes are
+// shared: a fetch still sending one keeps it alive until it is done.
+size_t Broker::enforce_locked(int64_t now_ms) {
+  size_t dropped_total = 0;
+  for (auto& tp : topics_) {
+    int64_t ms = cfg_.retention_ms, by = cfg_.retention_bytes;
+    auto rt = retention_.find(tp.first);
+    if (rt != retention_.end()) {
+      if (rt->second.ms != -2) ms = rt->second.ms;
+      if (rt->second.bytes != -2) by = rt->second.bytes;
+    }
+    if (ms < 0 && by < 0) continue;
+    for (Partition& p : tp.second) {
+      size_t drop = 0;
+      int64_t bytes = p.bytes, recs = 0;
+      while (drop < p.segs.size()) {
+        const Segment& sg = p.segs[drop];
+        const bool old = ms >= 0 && now_ms - sg.append_ms > ms;
+        const bool big = by >= 0 && drop + 1 < p.segs.size() && bytes - (int64_t)sg.bytes->size() >= by;
+        if (!old && !big) break;
+        bytes -= (int64_t)sg.bytes->size();
+        recs += sg.count;
+        ++drop;
+      }
+      if (!drop) continue;
+      p.segs.erase(p.segs.begin(), p.segs.begin() + (std::ptrdiff_t)drop);
+      if (p.segs.capacity() > 4 * p.segs.size() + 64) p.segs.shrink_to_fit();
+      p.bytes = bytes;
+      p.start = p.segs.empty() ? p.end : p.segs.front().base;
+      if (p.tbase >= 0 && p.tbase < p.start) {   // append times of deleted offsets go too
+        const int64_t k = std::min<int64_t>(p.start - p.tbase, (int64_t)p.tappend.size());
+        p.tappend.erase(p.tappend.begin(), p.tappend.begin() + (std::ptrdiff_t)k);
+        p.tbase += k;
+        if (p.tappend.capacity() > 4 * p.tappend.size() + 1024) p.tappend.shrink_to_fit();
+      }
+      deleted_segs_ += drop;
+      deleted_recs_ += (uint64_t)recs;
+      dropped_total += drop;
+    }
+  }
+  return dropped_total;
+}
+
+int64_t Broker::log_bytes() {
+  std::lock_guard<std::mutex> g(mu_);
+  int64_t t = 0;
+  for (auto& tp : topics_)
+    for (const Partition& p : tp.second) t += p.bytes;
+  return t;
+}
+
+size_t Broker::log_segments() {
+  std::lock_guard<std::mutex> g(mu_);
+  size_t t = 0;
+  for (auto& tp : topics_)
+    for (const Partition& p : tp.second) t += p.segs.size();
+  return t;
 }
 
 Broker::~Broker() { stop(); }
@@ -1002,6 +1084,11 @@ void Broker::stop() {
     std::lock_guard<std::mutex> g(mu_);
     data_cv_.notify_all();
   }
+  {
+    std::lock_guard<std::mutex> g(mu_);   // under the lock: the loop checks running_ while holding it
+    retention_cv_.notify_all();
+  }
+  if (retention_thread_.joinable()) retention_thread_.join();
   ::shutdown(listen_fd_, SHUT_RDWR);
   ::close(listen_fd_);
   if (accept_thread_.joinable()) accept_thread_.join();
@@ -1026,8 +1113,23 @@ void Broker::accept_loop() {
     int sz = 4 << 20;
     setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
     std::lock_guard<std::mutex> g(mu_);
+    // join the connection threads that have finished (serve closed its fd and took it off client_fds_)
+    for (size_t i = 0; i < workers_.size();) {
+      if (worker_done_[i]->load(std::memory_order_acquire)) {
+        workers_[i].join();
+        workers_.erase(workers_.begin() + (std::ptrdiff_t)i);
+        worker_done_.erase(worker_done_.begin() + (std::ptrdiff_t)i);   // (serve removed its own fd)
+      } else {
+        ++i;
+      }
+    }
     client_fds_.push_back(fd);
-    workers_.emplace_back([this, fd] { serve(fd); });
+    auto done = std::make_shared<std::atomic<bool>>(false);
+    worker_done_.push_back(done);
+    workers_.emplace_back([this, fd, done] {
+      serve(fd);
+      done->store(true, std::memory_order_release);
+    });
     if (!thread_cpus_.empty()) {
       cpu_set_t set;
       CPU_ZERO(&set);
@@ -1043,10 +1145,15 @@ void Broker::set_thread_cpus(const std::vector<int>& cpus) {
   thread_cpus_ = cpus;
 }
 
-void Broker::create_topic(const std::string& name, int partitions) {
+void Broker::create_topic(const std::string& name, int partitions, int64_t retention_ms, int64_t retention_bytes) {
   std::lock_guard<std::mutex> g(mu_);
   auto& t = topics_[name];
   if ((int)t.size() < partitions) t.resize((size_t)partitions);
+  if (retention_ms != -2 || retention_bytes != -2) {
+    TopicRetention& r = retention_[name];
+    if (retention_ms != -2) r.ms = retention_ms;
+    if (retention_bytes != -2) r.bytes = retention_bytes;
+  }
 }
 
 void Broker::record_append_times(bool on) { record_times_ = on; }
@@ -1090,22 +1197,33 @@ int64_t Broker::append_locked(Partition& p, const Record* recs, size_t n) {
     p.tappend.resize((size_t)(base - p.tbase), -1);   // offsets appended while recording was off
     p.tappend.insert(p.tappend.end(), n, now);
   }
+  const int64_t now_ms = steady_ms();
   for (size_t k = 0; k < n; k += kSegmentRecords) {
     const size_t m = std::min(kSegmentRecords, n - k);
     Segment sg;
     sg.base = p.end;
     sg.count = (int32_t)m;
+    sg.append_ms = now_ms;
     sg.bytes = std::make_shared<const std::string>(encode_record_batch(p.end, recs + k, m));
+    p.bytes += (int64_t)sg.bytes->size();
     p.segs.push_back(std::move(sg));
     p.end += (int64_t)m;
   }
-  // retention: whole segments, oldest first, while the rest still holds the limit (Kafka
-  // deletes log segments, not records)
+  // record-count retention: whole segments, oldest first, while the rest still holds the limit
+  // (Kafka deletes log segments, not records); time / size retention: retention_loop
   if (cfg_.retention_records > 0) {
     size_t drop = 0;
-    while (drop + 1 < p.segs.size() && p.end - (p.segs[drop].base + p.segs[drop].count) >= cfg_.retention_records)
+    int64_t recs_dropped = 0;
+    while (drop + 1 < p.segs.size() && p.end - (p.segs[drop].base + p.segs[drop].count) >= cfg_.retention_records) {
+      p.bytes -= (int64_t)p.segs[drop].bytes->size();
+      recs_dropped += p.segs[drop].count;
       ++drop;
-    if (drop) p.segs.erase(p.segs.begin(), p.segs.begin() + (std::ptrdiff_t)drop);
+    }
+    if (drop) {
+      p.segs.erase(p.segs.begin(), p.segs.begin() + (std::ptrdiff_t)drop);
+      deleted_segs_ += drop;
+      deleted_recs_ += (uint64_t)recs_dropped;
+    }
   }
   p.start = p.segs.empty() ? p.end : p.segs.front().base;
   append_seq_.fetch_add(1, std::memory_order_release);

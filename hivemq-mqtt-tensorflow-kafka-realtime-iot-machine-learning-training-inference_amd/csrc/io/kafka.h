@@ -177,6 +177,13 @@ struct BrokerConfig {
   int port = 0;  // 0 = ephemeral
   std::string sasl_username, sasl_password;  // empty = no auth
   int64_t retention_records = -1;           // -1 = unbounded
+  // Kafka's retention.ms / retention.bytes topic defaults (log.retention.*): -1 = unbounded.  The
+  // reference creates sensor-data and model-predictions with retention.ms=100000
+  // (infrastructure/confluent/01_installConfluentPlatform.sh:180, 183).  A background check every
+  // retention_check_ms (log.retention.check.interval.ms) deletes whole segments, oldest first.
+  int64_t retention_ms = -1;
+  int64_t retention_bytes = -1;
+  int retention_check_ms = 1000;
   bool auto_create_topics = true;            // Kafka's auto.create.topics.enable default
   int spin_us = 0;                           // > 0: connection threads / long polls busy-wait this long first
   int64_t message_max_bytes = 1048588;        // Kafka's message.max.bytes default (per record batch); <= 0 = no cap
@@ -187,7 +194,16 @@ class Broker {
   explicit Broker(BrokerConfig cfg);
   ~Broker();
   int port() const { return port_; }
-  void create_topic(const std::string& name, int partitions);
+  // retention_ms / retention_bytes: the topic's retention.ms / retention.bytes (-2 = the broker
+  // default, -1 = unbounded)
+  void create_topic(const std::string& name, int partitions, int64_t retention_ms = -2, int64_t retention_bytes = -2);
+  // One retention pass now (the background check runs the same): returns segments deleted.
+  size_t enforce_retention();
+  uint64_t deleted_segments() const { return deleted_segs_; }
+  uint64_t deleted_records() const { return deleted_recs_; }
+  // bytes / segments held by the log (all topics)
+  int64_t log_bytes();
+  size_t log_segments();
   int64_t append(const std::string& topic, int partition, const std::vector<Record>& recs);
   int64_t end_offset(const std::string& topic, int partition);
   int64_t start_offset(const std::string& topic, int partition);
@@ -223,12 +239,14 @@ class Broker {
   struct Segment {
     int64_t base = 0;
     int32_t count = 0;
+    int64_t append_ms = 0;   // steady-clock ms of the append (the segment's newest record)
     std::shared_ptr<const std::string> bytes;
   };
   struct Partition {
-    std::vector<Segment> segs;
+    std::vector<Segment> segs;   // a deque in effect: retention erases from the front in bulk
     int64_t start = 0;  // offset of the first retained record
     int64_t end = 0;    // next offset to assign
+    int64_t bytes = 0;  // encoded bytes of segs
     int64_t tbase = -1;              // first offset with a recorded append time
     std::vector<int64_t> tappend;    // append times (ns) of offsets tbase, tbase + 1, ...
   };
@@ -252,6 +270,17 @@ class Broker {
   std::vector<int> client_fds_;
   std::mutex mu_;
   std::map<std::string, std::vector<Partition>> topics_;
+  struct TopicRetention {
+    int64_t ms = -2, bytes = -2;   // -2: the broker default
+  };
+  std::map<std::string, TopicRetention> retention_;   // guarded by mu_
+  std::thread retention_thread_;
+  std::condition_variable retention_cv_;
+  std::atomic<uint64_t> deleted_segs_{0}, deleted_recs_{0};
+  void retention_loop();
+  size_t enforce_locked(int64_t now_ms);
+  // finished connection threads, joined by the accept loop (a long soak opens many connections)
+  std::vector<std::shared_ptr<std::atomic<bool>>> worker_done_;
   std::condition_variable data_cv_;   // appends -> long-polling fetches
   std::map<std::string, int64_t> group_offsets_;  // "group/topic/partition" -> offset
   std::atomic<int> fail_every_{0}, delay_ms_{0}, spin_us_{0};

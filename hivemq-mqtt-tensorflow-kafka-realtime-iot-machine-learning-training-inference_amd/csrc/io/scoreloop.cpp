@@ -129,12 +129,28 @@ LoopStats ScoreLoop::run(int64_t max_events, double idle_timeout_s) {
     want.clear();
     for (size_t i : grp) want.emplace_back(cfg_.partitions[i], pos_[i]);
     const int64_t t0 = steady_ns();
-    if (grp.size() == 1) {
-      slices.assign(1, kafka::Client::PartSlice{});
-      slices[0].hwm = cli.fetch_raw(cfg_.topic, want[0].first, want[0].second, cfg_.max_bytes, wait, resp,
-                                    slices[0].rec_off, slices[0].rec_len);
-    } else {
-      cli.fetch_multi_raw(cfg_.topic, want, cfg_.max_bytes, wait, resp, slices);
+    try {
+      if (grp.size() == 1) {
+        slices.assign(1, kafka::Client::PartSlice{});
+        slices[0].hwm = cli.fetch_raw(cfg_.topic, want[0].first, want[0].second, cfg_.max_bytes, wait, resp,
+                                      slices[0].rec_off, slices[0].rec_len);
+      } else {
+        cli.fetch_multi_raw(cfg_.topic, want, cfg_.max_bytes, wait, resp, slices);
+      }
+    } catch (const kafka::Error& e) {
+      // OFFSET_OUT_OF_RANGE: a position was deleted by the topic's retention -> auto.offset.reset
+      // for every requested partition below its log start (or past its end)
+      if (e.code != 1 || cfg_.offset_reset == 2) throw;
+      for (size_t i : grp) {
+        const int64_t lo = cli.list_offset(cfg_.topic, cfg_.partitions[i], -2);
+        const int64_t hi = cli.list_offset(cfg_.topic, cfg_.partitions[i], -1);
+        if (pos_[i] >= lo && pos_[i] <= hi) continue;
+        const int64_t np = cfg_.offset_reset == 1 ? hi : lo;
+        if (np > pos_[i]) st.reset_skipped += (uint64_t)(np - pos_[i]);
+        pos_[i] = np;
+        dirty[i] = 1;
+      }
+      continue;
     }
     const int64_t t1 = steady_ns();
     st.fetch_s += secs(t0, t1);

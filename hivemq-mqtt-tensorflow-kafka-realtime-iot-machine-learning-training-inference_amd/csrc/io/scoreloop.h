@@ -50,6 +50,7 @@ struct LoopConfig {
   int max_batch = 4096;                     // rows per scorer call
   int32_t max_bytes = 1 << 20;
   int32_t max_wait_ms = 100;                // long-poll bound
+  int offset_reset = 0;                     // auto.offset.reset: 0 earliest, 1 latest, 2 none (raise)
   double commit_interval_s = 0.0;           // 0: commit after every produced batch
   bool record_latency = false;
   // JSON source records (the MQTT bridge's `sensor-data`, KSQL SENSOR_DATA_S) instead of
@@ -68,6 +69,7 @@ struct LoopStats {
   uint64_t events = 0, anomalies = 0, skipped = 0, batches = 0, fetches = 0, empty_fetches = 0, commits = 0;
   uint64_t keys = 0;   // keyed (LSTM) scorer: distinct record keys given a device slot
   uint64_t foreign = 0;        // records of a shared partition whose key another replica owns
+  uint64_t reset_skipped = 0;  // records jumped over after OFFSET_OUT_OF_RANGE (retention)
   uint64_t keys_dropped = 0;   // keyed scorer: records not scored (key table full, or a null key)
   double fetch_s = 0, decode_s = 0, score_s = 0, format_s = 0, produce_s = 0, commit_s = 0, wall_s = 0;
 };

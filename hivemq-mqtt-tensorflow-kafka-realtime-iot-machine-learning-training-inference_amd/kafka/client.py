@@ -15,6 +15,28 @@ class KafkaError(RuntimeError):
     pass
 
 
+OFFSET_OUT_OF_RANGE = 1   # Kafka protocol error code
+
+
+def error_code(exc: BaseException) -> int:
+    """The Kafka protocol error code a native client error carries (``-1`` when none)."""
+    return int(getattr(exc, "code", -1))
+
+
+def offset_reset_policy(config) -> str:
+    """``auto.offset.reset`` from librdkafka-style config: ``earliest`` (default here: a consumer
+    whose position was deleted by retention loses the fewest records), ``latest``, or ``none``
+    (raise).  librdkafka's aliases smallest / beginning / largest / end / error are accepted."""
+    cfg = config if isinstance(config, dict) else parse_config(config)
+    v = cfg.get("auto.offset.reset", "earliest").lower()
+    alias = {"smallest": "earliest", "beginning": "earliest", "largest": "latest", "end": "latest",
+             "error": "none"}
+    v = alias.get(v, v)
+    if v not in ("earliest", "latest", "none"):
+        raise ValueError(f"bad auto.offset.reset {v!r}")
+    return v
+
+
 def parse_config(config: Optional[Sequence[str]]) -> Dict[str, str]:
     """librdkafka ``key=value`` strings (cardata-v3.py:7-15) -> dict."""
     out: Dict[str, str] = {}
@@ -44,10 +66,15 @@ class FakeBroker:
     """In-process partitioned append-only log serving the Kafka protocol on 127.0.0.1."""
 
     def __init__(self, port: int = 0, sasl_username: str = "", sasl_password: str = "",
-                 retention_records: int = -1, message_max_bytes: int = 1048588):
+                 retention_records: int = -1, message_max_bytes: int = 1048588, retention_ms: int = -1,
+                 retention_bytes: int = -1, retention_check_ms: int = 1000):
         """``message_max_bytes``: a produced record batch over it is refused (MESSAGE_TOO_LARGE,
-        nothing appended), as a Kafka broker's ``message.max.bytes`` default; <= 0 = no cap."""
-        self._b = _io().KafkaBroker(port, sasl_username, sasl_password, retention_records, message_max_bytes)
+        nothing appended), as a Kafka broker's ``message.max.bytes`` default; <= 0 = no cap.
+        ``retention_ms`` / ``retention_bytes``: the topics' default retention.ms / retention.bytes
+        (-1 = unbounded), enforced every ``retention_check_ms`` by deleting whole log segments
+        (the reference's topics: retention.ms=100000, 01_installConfluentPlatform.sh:180, 183)."""
+        self._b = _io().KafkaBroker(port, sasl_username, sasl_password, retention_records, message_max_bytes,
+                                    retention_ms, retention_bytes, retention_check_ms)
 
     @property
     def port(self) -> int:
@@ -57,8 +84,31 @@ class FakeBroker:
     def address(self) -> str:
         return f"127.0.0.1:{self.port}"
 
-    def create_topic(self, name: str, partitions: int = 1) -> None:
-        self._b.create_topic(name, partitions)
+    def create_topic(self, name: str, partitions: int = 1, retention_ms: Optional[int] = None,
+                     retention_bytes: Optional[int] = None) -> None:
+        """``kafka-topics --create --partitions N [--config retention.ms=..]``: None keeps the
+        broker default, -1 = unbounded."""
+        self._b.create_topic(name, partitions, -2 if retention_ms is None else int(retention_ms),
+                             -2 if retention_bytes is None else int(retention_bytes))
+
+    def enforce_retention(self) -> int:
+        """Run one retention pass now (the background check does the same); segments deleted."""
+        return self._b.enforce_retention()
+
+    @property
+    def deleted_segments(self) -> int:
+        return self._b.deleted_segments
+
+    @property
+    def deleted_records(self) -> int:
+        return self._b.deleted_records
+
+    def log_bytes(self) -> int:
+        """Encoded bytes the log holds over all topics."""
+        return self._b.log_bytes()
+
+    def log_segments(self) -> int:
+        return self._b.log_segments()
 
     def append(self, topic: str, partition: int, values: Sequence[bytes], keys=None, timestamps=None) -> int:
         return self._b.append(topic, partition, list(values), None if keys is None else list(keys),

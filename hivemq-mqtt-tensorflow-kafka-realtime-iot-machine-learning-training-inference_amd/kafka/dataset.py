@@ -23,7 +23,7 @@ from typing import Iterator, List, Optional, Sequence
 import numpy as np
 
 from ..obs.metrics import ENGINE
-from .client import KafkaClient, parse_topic_spec
+from .client import OFFSET_OUT_OF_RANGE, KafkaClient, error_code, offset_reset_policy, parse_topic_spec
 
 
 class KafkaDataset:
@@ -51,6 +51,10 @@ class KafkaDataset:
         self._client: Optional[KafkaClient] = None
         self.records_read = 0
         self.bytes_read = 0
+        # auto.offset.reset (config_global): where a cursor goes when its position was deleted by
+        # the topic's retention (OFFSET_OUT_OF_RANGE); records_skipped counts what it jumped over
+        self.offset_reset = offset_reset_policy(self.config)
+        self.records_skipped = 0
 
     @property
     def client(self) -> KafkaClient:
@@ -63,10 +67,20 @@ class KafkaDataset:
         if self.resume:
             got = c.committed(self.group, topic, partition)
             if got >= 0:
-                return got
+                offset = got
         if offset < 0:  # -1 latest, -2 earliest (librdkafka convention)
             return c.latest(topic, partition) if offset == -1 else c.earliest(topic, partition)
-        return max(offset, c.earliest(topic, partition))
+        first = c.earliest(topic, partition)
+        if offset < first:   # the position was deleted by retention: auto.offset.reset
+            if self.offset_reset == "none":
+                from .client import KafkaError
+                raise KafkaError(f"{topic}:{partition}: offset {offset} below the log start {first} "
+                                 f"(auto.offset.reset=none)")
+            new = first if self.offset_reset == "earliest" else c.latest(topic, partition)
+            self.records_skipped += new - offset
+            ENGINE.ingest_skipped.inc(new - offset, topic=topic)
+            return new
+        return offset
 
     def _step(self, c: KafkaClient, cur: List) -> Optional[dict]:
         """One fetch(+decode) for a cursor ``[topic, partition, pos, end, hash_range]``; advances
@@ -75,9 +89,19 @@ class KafkaDataset:
         if end is not None and pos >= end:
             return False
         t_fetch = time.perf_counter()
+        try:
+            batch = self._fetch(c, topic, partition, pos)
+        except Exception as e:  # noqa: BLE001 - only OFFSET_OUT_OF_RANGE is handled here
+            if error_code(e) != OFFSET_OUT_OF_RANGE or self.offset_reset == "none":
+                raise
+            new = c.earliest(topic, partition) if self.offset_reset == "earliest" else c.latest(topic, partition)
+            if new > pos:
+                skipped = (min(new, end) if end is not None else new) - pos
+                self.records_skipped += skipped
+                ENGINE.ingest_skipped.inc(skipped, topic=topic)
+            cur[2] = new
+            return False if end is not None and new >= end else None
         if self.codec is not None:
-            batch = c.fetch_decode(self.codec, topic, partition, pos, self.max_bytes, self.max_wait_ms,
-                                   self.framing, self.with_text, self.str_keys)
             nbytes = int(batch["bytes"])
             if int(batch.get("n_errors", 0)):
                 ENGINE.decode_errors.inc(int(batch["n_errors"]), topic=topic)
@@ -85,7 +109,6 @@ class KafkaDataset:
             batch["text_null"] = dict(zip(self.codec.text_fields, batch["text_null"]))
             batch["text_codes"] = dict(zip(self.codec.text_fields, batch["text_codes"]))
         else:
-            batch = c.fetch(topic, partition, pos, self.max_bytes, self.max_wait_ms)
             nbytes = len(batch["values"])
         offs = batch["offsets"]
         self.bytes_read += nbytes
@@ -106,6 +129,12 @@ class KafkaDataset:
         batch["topic"], batch["partition"] = topic, partition
         batch["hash_range"] = cur[4] if len(cur) > 4 else None   # keys share: the consumer filters
         return batch
+
+    def _fetch(self, c: KafkaClient, topic: str, partition: int, pos: int) -> dict:
+        if self.codec is not None:
+            return c.fetch_decode(self.codec, topic, partition, pos, self.max_bytes, self.max_wait_ms,
+                                  self.framing, self.with_text, self.str_keys)
+        return c.fetch(topic, partition, pos, self.max_bytes, self.max_wait_ms)
 
     def _cursors(self, c: KafkaClient) -> List[List]:
         if self.plan is not None:   # this rank's share (kafka/assign.py), resolved per iteration

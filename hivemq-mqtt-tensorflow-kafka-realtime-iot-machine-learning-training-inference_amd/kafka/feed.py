@@ -20,7 +20,7 @@ from typing import Iterator, List, Optional, Sequence, Tuple
 import numpy as np
 
 from ..ops._ext import load_io
-from .client import KafkaClient, KafkaError, parse_config, parse_topic_spec
+from .client import KafkaClient, KafkaError, offset_reset_policy, parse_config, parse_topic_spec
 
 
 def _auth(config) -> Tuple[str, str, str, str, int]:
@@ -91,7 +91,14 @@ class NativeFeed:
             elif offset == -2:
                 start = client.earliest(topic, partition)
             else:
-                start = max(offset, client.earliest(topic, partition))
+                start = offset
+        first = client.earliest(topic, partition)
+        if start < first:   # deleted by retention (or a stale commit): auto.offset.reset
+            policy = offset_reset_policy(self.config)
+            if policy == "none":
+                raise KafkaError(f"{topic}:{partition}: offset {start} below the log start {first} "
+                                 f"(auto.offset.reset=none)")
+            start = first if policy == "earliest" else client.latest(topic, partition)
         return int(start)
 
     def _parts(self, client: KafkaClient) -> List[Tuple[str, int, int, int]]:
@@ -120,7 +127,8 @@ class NativeFeed:
                                 self.label_field, -1 if keep_label is None else int(keep_label), self.framing,
                                 self.max_bytes, self.max_wait_ms, self.workers,
                                 -1.0 if self.idle_timeout_s is None else float(self.idle_timeout_s), parts,
-                                check_crcs=self.check_crcs)
+                                check_crcs=self.check_crcs,
+                                offset_reset={"earliest": 0, "latest": 1, "none": 2}[offset_reset_policy(self.config)])
         return f, client, parts
 
     def decode_only(self, buf, offsets, workers: int, repeats: int = 3, keep_label: Optional[int] = None):

@@ -78,6 +78,10 @@ class LowLatencyScorer:
         self._scorer = scorer
         cid, mech, user, pw, tmo = _auth(config)
         api = scorer.c_api() if hasattr(scorer, "c_api") else scorer._s.c_api()
+        from .client import offset_reset_policy
+        # auto.offset.reset for a position deleted by retention while the loop runs (the
+        # result's reset_skipped counts the records jumped over)
+        reset = {"earliest": 0, "latest": 1, "none": 2}[offset_reset_policy(config)]
         self._loop = load_io().ScoreLoop(client.servers, cid, mech, user, pw, tmo,
                                          [fs.as_tuple() for fs in codec.fields], topic, result_topic, group or "",
                                          self.partitions, [int(s) for s in starts],
@@ -85,7 +89,7 @@ class LowLatencyScorer:
                                          int(max_batch), int(max_bytes), int(max_wait_ms), float(commit_interval_s),
                                          bool(record_latency), int(api), int(spin_us),
                                          json_columns() if source_format == "json" else [], str(json_stamp),
-                                         [(int(lo), int(hi)) for lo, hi in (hash_ranges or [])])
+                                         [(int(lo), int(hi)) for lo, hi in (hash_ranges or [])], reset)
 
     def run(self, max_events: int = 0, idle_timeout_s: Optional[float] = None) -> dict:
         """Blocking (GIL released): until ``stop()``, ``max_events`` or ``idle_timeout_s``

@@ -201,6 +201,9 @@ class EngineMetrics:
     def __init__(self, reg: Registry):
         self.ingest_records = reg.counter("ingest_records_total", "records fetched from Kafka", ("topic",))
         self.ingest_bytes = reg.counter("ingest_bytes_total", "record bytes fetched from Kafka", ("topic",))
+        self.ingest_skipped = reg.counter("ingest_skipped_records_total",
+                                          "records a consumer jumped over after OFFSET_OUT_OF_RANGE "
+                                          "(deleted by retention; auto.offset.reset)", ("topic",))
         self.decode_seconds = reg.counter("decode_seconds_total", "host time in fetch + Avro decode", ("topic",))
         self.decode_errors = reg.counter("decode_errors_total", "records that failed Avro decoding", ("topic",))
         self.h2d_bytes = reg.counter("h2d_bytes_total", "bytes staged host->device through the pinned ring")
