@@ -17,6 +17,16 @@ Data: ``servers=synthetic://N`` (default) trains on N synthetic car events
 source streams the topic (``partition=-1``: every partition), each rank its own share
 (``assign``: split | partitions, :mod:`streamml.kafka.assign`) through the native feed,
 with no collect.  Prints one JSON summary line on rank 0.
+
+Continuous training (``segment_rows=N``, autoencoder): the job follows the topic instead of
+re-reading a bounded snapshot per epoch.  Each of ``epochs`` segments trains, on every rank, the
+next <= N records of each partition it owns (``p % world == rank``), from the positions of the
+last checkpoint (:class:`streamml.kafka.assign.SegmentPlan`); after the segment the positions
+advance, and every ``ckpt_every`` segments the checkpoint's sidecar stores every partition's
+position next to the model (committed to the consumer group too).  A restart -- e.g. by
+``torchrun --max-restarts`` after a crashed rank -- resumes from those positions: every record is
+trained exactly once, in the same step boundaries as an uninterrupted run
+(tests/test_stream_resume.py).
 """
 from __future__ import annotations
 
@@ -27,7 +37,8 @@ import time
 from typing import Sequence
 
 
-JOB_KEYS = {"ckpt_dir": None, "ckpt_every": 1, "rows": 200000, "stack": "two_layer", "metrics_port": 0}
+JOB_KEYS = {"ckpt_dir": None, "ckpt_every": 1, "rows": 200000, "stack": "two_layer", "metrics_port": 0,
+            "segment_rows": 0}
 
 
 def _split(argv):
@@ -105,6 +116,7 @@ def main(argv: Sequence[str]) -> int:
 
     # ---------------------------------------------------------------- data
     servers = cfg.servers
+    plan = None
     if servers.startswith("synthetic://"):
         from ..data.stream import synthetic
         n = int(servers[len("synthetic://"):] or job["rows"])
@@ -124,10 +136,23 @@ def main(argv: Sequence[str]) -> int:
         # no rank reads another's records and nothing is collected first
         from ..data import stream as st
         part = "*" if cfg.partition < 0 else str(cfg.partition)
+        if int(job["segment_rows"]) > 0:
+            if cfg.model != "autoencoder":
+                raise ValueError("train: segment_rows (continuous training) supports the autoencoder")
+            from ..kafka.assign import SegmentPlan
+            from ..kafka.client import parse_topic_spec
+            # positions of every partition from the checkpoint (any world size: the map is per
+            # partition), else the configured offset / the log start
+            plan = SegmentPlan([parse_topic_spec(f"{cfg.topic}:{part}:{cfg.offset}")], rank, world,
+                               int(job["segment_rows"]), (state or {}).get("offsets"))
+        # continuous mode reads with the ORDERED parallel reader (fetch + decode threads, batches in
+        # cursor order): the row order -- and so a replay after a restart -- is deterministic; the
+        # native feed hands slabs over in completion order
         s = st.kafka(servers, [f"{cfg.topic}:{part}:{cfg.offset}"], schema=cfg.schema, group=cfg.group,
                      eof=True, config=cfg.kafka_config if not servers.startswith("fake://") else None,
-                     shard="auto", assign=cfg.assign, native=cfg.native_feed and dev.type == "cuda",
-                     workers=cfg.feed_workers)
+                     shard="auto", assign=cfg.assign,
+                     native=cfg.native_feed and dev.type == "cuda" and plan is None,
+                     workers=cfg.feed_workers, plan=plan, ordered=plan is not None)
         data = (s.filter_normal(device=True),) if cfg.model == "autoencoder" else (s, None)
 
     # ---------------------------------------------------------------- train
@@ -139,7 +164,9 @@ def main(argv: Sequence[str]) -> int:
                 rs.save_checkpoint(self.model, ckpt_dir, epoch + 1, extra={"loss": (logs or {}).get("loss")})
 
     t0 = time.perf_counter()
-    if cfg.model == "autoencoder":
+    if plan is not None:   # continuous: one bounded segment per "epoch", positions checkpointed
+        hist = _continuous(model, data[0], plan, cfg, job, ckpt_dir, start_epoch, rank, world, rs)
+    elif cfg.model == "autoencoder":
         hist = model.fit(data[0], epochs=cfg.epochs, batch_size=cfg.batch_size, verbose=1 if rank == 0 else 0,
                          callbacks=[_Ckpt()], shuffle=True, seed=cfg.seed, initial_epoch=start_epoch,
                          steps_per_epoch=cfg.take)
@@ -152,11 +179,56 @@ def main(argv: Sequence[str]) -> int:
         model.save(os.path.join(ckpt_dir, cfg.model_file))
     if rank == 0:
         losses = hist.history.get("loss", [])
-        print(json.dumps({"job": "train", "model": cfg.model, "world_size": world, "resumed_from_epoch": start_epoch,
-                          "epochs": cfg.epochs, "final_loss": losses[-1] if losses else None,
-                          "seconds": round(dt, 3), "ckpt_dir": ckpt_dir}), flush=True)
+        line = {"job": "train", "model": cfg.model, "world_size": world, "resumed_from_epoch": start_epoch,
+                "epochs": cfg.epochs, "final_loss": losses[-1] if losses else None,
+                "seconds": round(dt, 3), "ckpt_dir": ckpt_dir}
+        if plan is not None:
+            line["positions"] = getattr(hist, "positions", {})
+            line["segment_records"] = hist.history.get("records", [])
+            line["segment_loss"] = losses
+        print(json.dumps(line), flush=True)
     shutdown()
     return 0
+
+
+def _continuous(model, data, plan, cfg, job, ckpt_dir, start_seg, rank, world, rs):
+    """Segments ``start_seg .. cfg.epochs - 1``: train the next bounded segment of every owned
+    partition (every record of it: no ``take`` cap, no shuffle -- the step boundaries are a pure
+    function of the positions), advance the positions, checkpoint them with the model."""
+    from ..nn.callbacks import History
+    from ..parallel.dp import _pg_active
+    hist = History()
+    hist.history = {"loss": [], "records": []}
+    for seg in range(start_seg, cfg.epochs):
+        h = model.fit(data, epochs=seg + 1, initial_epoch=seg, batch_size=cfg.batch_size, verbose=0,
+                      shuffle=False, seed=cfg.seed)
+        n = plan.segment_records()
+        plan.advance()
+        hist.history["loss"].extend(h.history.get("loss", []))
+        hist.history["records"].append(n)
+        offsets = plan.offsets()
+        if _pg_active():   # every rank's partitions: one map (the ranks' partitions are disjoint)
+            import torch.distributed as dist
+            parts = [None] * world
+            dist.all_gather_object(parts, offsets)
+            offsets = {k: v for d in parts for k, v in d.items()}
+        if ckpt_dir and (seg + 1) % int(job["ckpt_every"]) == 0:
+            loss = h.history.get("loss", [None])[-1]
+            rs.save_checkpoint(model, ckpt_dir, seg + 1, offsets=offsets, extra={"loss": loss, "segment_rows":
+                                                                                int(job["segment_rows"])})
+            if cfg.group:   # Kafka semantics too: the group's committed offsets follow the checkpoints
+                try:
+                    from ..kafka.client import KafkaClient
+                    c = KafkaClient(cfg.servers, cfg.kafka_config if not cfg.servers.startswith("fake://") else None)
+                    for k, v in plan.offsets().items():
+                        t, p = k.rsplit(":", 1)
+                        c.commit(cfg.group, t, int(p), int(v))
+                except Exception as e:  # noqa: BLE001 - advisory; the checkpoint is the source of truth
+                    print(f"[train] group commit failed: {e!r}", file=sys.stderr)
+        hist.positions = offsets
+    if not hasattr(hist, "positions"):
+        hist.positions = plan.offsets()
+    return hist
 
 
 if __name__ == "__main__":

@@ -270,7 +270,7 @@ def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optio
           eof: bool = True, config: Optional[Sequence[str]] = None, max_bytes: int = 4 << 20,
           framing: bool = True, commit: bool = False, resume: bool = False,
           idle_timeout_s: Optional[float] = None, workers: int = 1, native: bool = False,
-          shard=None, assign: str = "auto") -> Stream:
+          shard=None, assign: str = "auto", plan=None, ordered: bool = False) -> Stream:
     """Kafka topic(s) of (Confluent-framed) Avro car records -> raw feature chunks.
 
     ``topics``: ``"topic:partition:offset"`` specs; ``"topic:*:offset"`` is every partition.
@@ -287,13 +287,20 @@ def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optio
     order; Python reader only), ``"auto"``: split when ``eof`` else partitions.  Under a process
     group every rank resolves the same log snapshot (an all-reduce of the offsets), so starting
     an iteration of a sharded stream is collective -- as every ``fit`` epoch is.  The stream
-    carries ``stream.shard = (rank, world)``; ``fit`` then trains each rank on its own rows."""
+    carries ``stream.shard = (rank, world)``; ``fit`` then trains each rank on its own rows.
+
+    ``plan``: a ready share plan (e.g. :class:`streamml.kafka.assign.SegmentPlan`) instead of one
+    built from ``shard`` / ``assign``.  ``ordered`` (Python reader, ``workers`` > 1): batches in the
+    sequential reader's cursor order rather than completion order -- a deterministic row order."""
     from ..kafka import KafkaDataset
     from ..kafka.client import parse_topic_spec
     from .avro import AvroCodec
 
-    plan = None
-    if shard is not None:
+    # ``plan``: a ready share plan (e.g. kafka.assign.SegmentPlan: continuous training in bounded
+    # segments from checkpointed positions) instead of one built from ``shard`` / ``assign``
+    if plan is not None:
+        pass
+    elif shard is not None:
         from ..kafka.assign import ShardPlan, torch_sync
         if shard == "auto":
             import torch.distributed as dist
@@ -342,7 +349,7 @@ def kafka(servers: str, topics: Sequence[str], schema="cardata-v1", group: Optio
         ds = KafkaDataset(topics, servers=servers, group=group, eof=eof, config_global=config, codec=codec,
                           max_bytes=max_bytes, framing=framing, commit=commit, resume=resume,
                           idle_timeout_s=idle_timeout_s, with_text=False, str_keys=True, workers=workers,
-                          plan=plan)
+                          plan=plan, ordered=ordered)
         for b in ds:
             ok = b["ok"].astype(bool)
             x = b["numeric"][:, cols]

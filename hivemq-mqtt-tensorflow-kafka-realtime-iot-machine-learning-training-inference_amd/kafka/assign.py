@@ -187,3 +187,60 @@ def torch_sync(values, ops):
     """``ShardPlan.sync`` over the default ``torch.distributed`` process group."""
     from ..parallel.dp import agree
     return agree(values, None, ops)
+
+
+class SegmentPlan:
+    """Continuous training from an unbounded topic, one bounded *segment* at a time.
+
+    Rank ``rank`` owns the listed partitions ``i % world == rank`` (consumer-group style, as
+    ``"partitions"``) and each :meth:`resolve` -- one ``fit`` epoch over the stream -- hands it
+    ``[pos, min(pos + quota, log end))`` of every owned partition, from the plan's own positions.
+    The positions move only in :meth:`advance`, which the caller invokes once the model has
+    trained every record of the segment (``fit`` trains every row of every share,
+    :meth:`Autoencoder._fit_stream_dp`), and :meth:`offsets` is what a checkpoint stores with the
+    model (consumer offsets committed with checkpoints).  A job restarted from that
+    checkpoint re-reads exactly the records after it: every record is trained once, in the same
+    step boundaries, whatever crashed in between.  The reference's idea of training from the
+    commit log with no other data store (README.md:124-128), made restartable."""
+
+    def __init__(self, specs: Sequence[Tuple[str, int, int]], rank: int, world: int, quota: int,
+                 offsets: Optional[Dict[str, int]] = None):
+        if quota <= 0:
+            raise ValueError("segment quota must be positive")
+        self.specs = list(specs)
+        self.rank, self.world, self.quota = int(rank), int(world), int(quota)
+        self.mode = "partitions"
+        self.sync = None
+        self.positions: Dict[str, int] = {str(k): int(v) for k, v in (offsets or {}).items()}
+        self.last: List[Share] = []
+
+    @staticmethod
+    def key(topic: str, partition: int) -> str:
+        return f"{topic}:{int(partition)}"
+
+    def resolve(self, client, start_of: Callable[[str, int, int], int], bounded: bool = True) -> List[Share]:
+        specs = expand_specs(self.specs, client.partitions() if any(p == -1 for _, p, _ in self.specs) else {})
+        shares = []
+        for i, (t, p, o) in enumerate(specs):
+            if i % self.world != self.rank:
+                continue
+            pos = self.positions.get(self.key(t, p), int(o))
+            start = int(start_of(t, p, pos))   # honours auto.offset.reset below the log start
+            end = min(start + self.quota, int(client.latest(t, p)))
+            shares.append(Share(t, int(p), start, max(end, start)))
+        self.last = shares
+        return shares
+
+    def advance(self) -> None:
+        """The last resolved segment has been trained: its ends become the positions."""
+        for s in self.last:
+            self.positions[self.key(s.topic, s.partition)] = int(s.end)
+
+    def offsets(self) -> Dict[str, int]:
+        """This rank's partitions' positions (the checkpoint merges every rank's: they are disjoint;
+        positions loaded for other ranks' partitions are not reported back)."""
+        owned = {self.key(s.topic, s.partition) for s in self.last}
+        return {k: v for k, v in self.positions.items() if k in owned}
+
+    def segment_records(self) -> int:
+        return sum(s.rows for s in self.last)

@@ -31,7 +31,8 @@ class KafkaDataset:
                  eof: bool = True, config_global: Optional[Sequence[str]] = None, codec=None,
                  max_bytes: int = 4 << 20, max_wait_ms: int = 100, framing: bool = True,
                  commit: bool = False, resume: bool = False, idle_timeout_s: Optional[float] = None,
-                 with_text: bool = True, str_keys: bool = False, workers: int = 1, plan=None):
+                 with_text: bool = True, str_keys: bool = False, workers: int = 1, plan=None,
+                 ordered: bool = False):
         self.specs = [parse_topic_spec(t) for t in topics]
         self.plan = plan              # kafka.assign.ShardPlan: this rank's share of the partitions
         self.servers = servers
@@ -48,6 +49,10 @@ class KafkaDataset:
         self.with_text = with_text
         self.str_keys = str_keys
         self.workers = max(1, int(workers))
+        # ordered: the parallel reader yields batches in the sequential reader's order (cursor
+        # round robin) instead of completion order -- a deterministic row order for replayable
+        # training (a slow partition then holds the others back; bounded reads only)
+        self.ordered = bool(ordered)
         self._client: Optional[KafkaClient] = None
         self.records_read = 0
         self.bytes_read = 0
@@ -184,6 +189,9 @@ class KafkaDataset:
         import queue
         import threading
         nw = min(self.workers, len(cursors))
+        if self.ordered:
+            yield from self._iter_parallel_ordered(c, cursors, nw)
+            return
         q: "queue.Queue" = queue.Queue(maxsize=2 * nw)
         stop = threading.Event()
         done = object()
@@ -231,6 +239,62 @@ class KafkaDataset:
                 yield item
                 if self.commit:
                     c.commit(self.group, item["topic"], item["partition"], pos)
+        finally:
+            stop.set()
+            for t in threads:
+                t.join(timeout=5)
+
+    def _iter_parallel_ordered(self, c: KafkaClient, cursors: List[List], nw: int) -> Iterator[dict]:
+        """``workers`` threads fetch + decode as in :meth:`_iter_parallel`, into one small queue
+        per cursor; the consumer takes one batch per live cursor in cursor order -- exactly the
+        sequential reader's sequence of batches."""
+        import queue
+        import threading
+        qs = [queue.Queue(maxsize=2) for _ in cursors]
+        stop = threading.Event()
+        done = object()
+
+        def put(k, item):
+            while not stop.is_set():
+                try:
+                    qs[k].put(item, timeout=0.1)
+                    return
+                except queue.Full:
+                    continue
+
+        def work(mine: List[int]) -> None:
+            live = list(mine)
+            try:
+                cl = KafkaClient(self.servers, self.config)
+                while live and not stop.is_set():
+                    for k in list(live):
+                        batch = self._step(cl, cursors[k])
+                        if batch is False:
+                            live.remove(k)
+                            put(k, (done, None))
+                        elif batch is not None:
+                            put(k, (batch, cursors[k][2]))
+            except BaseException as e:  # surfaced in the consumer
+                for k in live:
+                    put(k, (e, None))
+
+        threads = [threading.Thread(target=work, args=(list(range(i, len(cursors), nw)),), daemon=True)
+                   for i in range(nw)]
+        for t in threads:
+            t.start()
+        live = list(range(len(cursors)))
+        try:
+            while live:
+                for k in list(live):
+                    item, pos = qs[k].get()
+                    if item is done:
+                        live.remove(k)
+                        continue
+                    if isinstance(item, BaseException):
+                        raise item
+                    yield item
+                    if self.commit:
+                        c.commit(self.group, item["topic"], item["partition"], pos)
         finally:
             stop.set()
             for t in threads:

@@ -10,7 +10,7 @@ from streamml.kafka.client import FakeBroker, KafkaClient, error_code, offset_re
 from streamml.kafka.dataset import KafkaDataset
 
 
-def _fill(b, topic, n, batch=1024, part=0):
+def _fill(b, topic, n, batch=1024, part=0):  # noqa: E302
     for i in range(0, n, batch):
         b.append(topic, part, [b"v%08d" % k for k in range(i, min(n, i + batch))])
 
@@ -164,5 +164,22 @@ def test_native_feed_resets_after_retention(monkeypatch):
         rows = np.concatenate([r for r, _ in feed.host_chunks(slab_rows=256)])
         np.testing.assert_array_equal(rows, x)
         assert feed.last_stats["reset_skipped"] == 2048
+    finally:
+        b.stop()
+
+
+def test_ordered_parallel_reader_matches_sequential_order():
+    """KafkaDataset(workers > 1, ordered=True) yields exactly the sequential reader's batches."""
+    b = FakeBroker()
+    try:
+        b.create_topic("o", 5)
+        for p in range(5):
+            _fill(b, "o", 3000 + 500 * p, part=p)
+        seq = [(bt["partition"], list(bt["offsets"])) for bt in
+               KafkaDataset(["o:*:0"], servers=b.address, eof=True, max_bytes=20_000)]
+        for _ in range(3):
+            par = [(bt["partition"], list(bt["offsets"])) for bt in
+                   KafkaDataset(["o:*:0"], servers=b.address, eof=True, max_bytes=20_000, workers=3, ordered=True)]
+            assert par == seq
     finally:
         b.stop()
