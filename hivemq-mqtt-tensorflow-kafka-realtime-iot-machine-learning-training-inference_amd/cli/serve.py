@@ -103,6 +103,25 @@ def _flags(p) -> None:
                         "SENSOR_DATA_S) directly instead of the Avro stream")
 
 
+def seed_group_offsets(client, topic: str, base: str, group: str, partitions, max_world: int = 16) -> dict:
+    """Rescaled serving: the consumer group of a replica that shares partitions is tied to the
+    replica count (``<base>.<rank>-of-<world>``), so after a rescale it starts with no committed
+    positions.  For every partition the group has no commit for, seed it with the MINIMUM position
+    committed by the base group or any ``<base>.<r>-of-<w>`` group (w <= ``max_world``): at-least-
+    once -- records between that minimum and another replica's position are scored again, none
+    is skipped.  Returns {partition: seeded offset}."""
+    seeded = {}
+    cands = [base] + [f"{base}.{r}-of-{w}" for w in range(2, max_world + 1) for r in range(w)]
+    for p in partitions:
+        if client.committed(group, topic, p) >= 0:
+            continue
+        pos = [o for o in (client.committed(g, topic, p) for g in cands if g != group) if o >= 0]
+        if pos:
+            client.commit(group, topic, p, min(pos))
+            seeded[int(p)] = min(pos)
+    return seeded
+
+
 def _serve_low_latency(ns, servers, cfg, model, mine, result_parts, summary, rank: int = 0,
                        hash_ranges=None) -> int:
     """One C++ loop per replica over the resident scorer: the autoencoder's, or -- ``--model
@@ -194,8 +213,11 @@ def main(argv: Sequence[str]) -> int:
     shares = serve_shares(n_parts, rank, world)
     mine = [p for p, _, _ in shares]
     partial = any(not (lo == 0 and hi == HASH_SPACE) for _, lo, hi in shares)
+    base_group = ns.group
     if partial:   # a shared partition's position is per replica: its own consumer group
         ns.group = f"{ns.group}.{rank}-of-{world}"
+    if not ns.from_beginning:
+        seed_group_offsets(KafkaClient(servers, cfg), ns.topic, base_group, ns.group, [p for p, _, _ in shares])
     print(f"replica {rank}/{world}: partitions {mine} of {n_parts} on {device}", flush=True)
     summary = {"replica": rank, "replicas": world, "partitions": mine, "events": 0, "anomalies": 0,
                "key_shares": [[p, lo / HASH_SPACE, hi / HASH_SPACE] for p, lo, hi in shares], "group": ns.group}

@@ -41,7 +41,8 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
                                float beta2, float eps, float gscale, int want_acc, unsigned long long* prof,
                                int nmodels, int64_t xmodel, const float* lrs, const int64_t* ragged,
                                uint64_t* const* dp_peers, int dp_ranks, int dp_rank0, int* dp_status,
-                               long long dp_timeout, hipStream_t stream, const MBStream* sr = nullptr);
+                               long long dp_timeout, hipStream_t stream, const MBStream* sr = nullptr,
+                               int precision = -1);   // 1 bf16 contractions, 0 fp32, -1 SML_MB_BF16
 
 // ---- LSTM recurrence (lstm.hip) ----
 hipError_t lstm_fwd_launch(const float* zx, const float* Uw, const float* h0, const float* c0, float* hseq,

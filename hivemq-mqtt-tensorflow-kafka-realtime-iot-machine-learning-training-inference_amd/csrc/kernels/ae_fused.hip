@@ -847,6 +847,9 @@ struct FragsP {
   // the 16x16x32 A operands, concatenated once per launch: tile 1's layer 1 takes its K halves
   // in the order [UP | inputs 0..15] so the shared UP B operand can sit between the tiles' own
   s16x8 w1a[2], w2a, w4ba, w4bua;
+  // one layer-1 A operand for BOTH tiles: [inputs 0..15 | UP of both tiles + bias]; the tile is picked
+  // by lane-masking the UP B operand instead (MA variants: 4 fewer persistent registers)
+  s16x8 w1s;
 };
 
 __device__ __forceinline__ int img_row_of_packed(int i) { return i == 7 ? 15 : i; }   // i = packed % 8
@@ -928,6 +931,10 @@ __device__ __forceinline__ void load_frags_packed(const AEArgs& a, int c, int g,
   const bf16x4 zb = {0, 0, 0, 0};
   F.w1a[0] = cat8(F.w1t, F.w1u[0]);
   F.w1a[1] = cat8(F.w1u[1], F.w1t);
+  bf16x4 w1ub;   // w1u[0] and w1u[1] have disjoint supports (lane groups g < 2 / g >= 2, + the bias)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w1ub[j] = (g >> 1) == 0 ? F.w1u[0][j] : F.w1u[1][j];
+  F.w1s = cat8(F.w1t, w1ub);
   F.w2a = cat8(F.w2t[0], F.w2t[1]);
   F.w4ba = cat8(F.w4b[0], F.w4b[1]);
   // the second K half meets an all-zero B half (d3's UP MFMA), so it can be any finite fragment:
@@ -1003,14 +1010,19 @@ __device__ __forceinline__ bf16x4 tr_read(char* slot, int c, int g) {
 // of the step; 1: the forward ones written to LDS as soon as they exist (EW), the tile halves of
 // dW2 / dW4 in one accumulator each (MA); 2: no LDS at all -- each operand is the A operand of one
 // 16x16x16 MFMA against the identity (C = A . I is the operand in the rows-on-K C layout, exact in
-// fp32, repacked to bf16 bit-exactly), plus MA.  The LDS-transpose loop spends half its issue
+// fp32, repacked to bf16 bit-exactly), plus MA; 3: EW for the 7 forward operands (LDS slots 0..6),
+// the MFMA identity for the 7 backward ones, plus MA.  The LDS-transpose loop spends half its issue
 // stalls waiting to issue LDS instructions (SQ_WAIT_INST_LDS, profiles/r06/SUMMARY.md §1).
-template <int PACK, int DC, bool TP, int TS = 10, int NP = 1, int XP = 0>
+// RX (tile-packed ring only): the fp32 inputs the loss needs (y - x) are read again from the pair's
+// ring slot at the output layer instead of being held in 9 registers across the whole forward
+// chain (`xring[p]`: the pair's slot base; the slot is only re-filled after the next iteration's DMA
+// issue).  The ring's rows are the normalised ones, bit-identical to the first read.
+template <int PACK, int DC, bool TP, int TS = 10, int NP = 1, int XP = 0, bool RX = false>
 __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP& F, char* scr, int c, int g,
                                                   const f32x4 (&xf)[NP][2][2], const float (&xup)[NP],
                                                   const int (&ix)[NP][2], f32x4 acc1[2], f32x4& acc2, f32x4& acc3,
                                                   f32x4 acc4[2], f32x4& acc2b, f32x4& acc4b, float& sq, float& ab,
-                                                  float& corr, float& rows) {
+                                                  float& corr, float& rows, const char* const* xring = nullptr) {
   // xup: the UP-layout copy of inputs 16 / 17 (lane group g: input 16 + (g & 1) of tile g >> 1)
   static_assert(PACK == PACK_REF && DC == 18, "reference model, D = 18 (outputs 16, 17 packed as UP)");
   static_assert(NP == 1 || NP == 2, "one or two pairs per iteration");
@@ -1019,7 +1031,7 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   const bool pad_lane = (g == 3);
   const bool lo = c < 8;   // lanes holding tile 0's half of a packed operand (as n or m = c)
   auto stand_in = [](int p, int u) { return TP && p == NP - 1 && u == 1; };
-  constexpr bool EW = XP == 1, MA = XP >= 1, TRM = XP == 2;
+  constexpr bool EW = XP == 1 || XP == 3, MA = XP >= 1, TRM = XP == 2;
   // identity B operand (lane (n = c, g) holds k = 4g..4g+3): 1 where k == n
   bf16x4 ident;
 #pragma unroll
@@ -1043,8 +1055,15 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   }
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    z1[p][0] = mfma32a(F.w1a[0], xb0[p][0], xub[p], zero4);
-    z1[p][1] = mfma32a(F.w1a[1], xub[p], xb0[p][1], zero4);
+    if constexpr (MA) {   // the shared A operand; tile u's UP lanes (g >> 1 == u) + the bias lane
+      const bf16x4 xu0 = pack4(f32x4{g < 2 ? xup[p] : 0.f, g == 0 ? 1.0f : 0.0f, 0.f, 0.f});
+      const bf16x4 xu1 = pack4(f32x4{g >= 2 ? xup[p] : 0.f, g == 0 ? 1.0f : 0.0f, 0.f, 0.f});
+      z1[p][0] = mfma32a(F.w1s, xb0[p][0], xu0, zero4);
+      z1[p][1] = mfma32a(F.w1s, xb0[p][1], xu1, zero4);
+    } else {
+      z1[p][0] = mfma32a(F.w1a[0], xb0[p][0], xub[p], zero4);
+      z1[p][1] = mfma32a(F.w1a[1], xub[p], xb0[p][1], zero4);
+    }
   }
 #pragma unroll
   for (int p = 0; p < NP; ++p)
@@ -1091,6 +1110,27 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
   // lane group g = output 16 + (g & 1) of tile g >> 1; w4u's rows m = 4q, so only C entry 0 is used)
   f32x4 dz4[NP][2], z4[NP][2], z4u[NP];
   float dz4up[NP], yup[NP];
+  f32x4 xl[NP][2];   // the loss's x: xf, or (RX) a second read of the ring slot
+  float xul[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    if constexpr (RX) {
+      typedef __attribute__((address_space(3))) const f32x2_t lds_f2;
+      typedef __attribute__((address_space(3))) const float lds_f;
+      constexpr int SLOTB = 64 * 18 + 16;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const char* row = xring[p] + u * SLOTB + c * 4 * 18 + 16 * g;
+        const f32x2_t v0 = *(lds_f2*)row, v1 = *(lds_f2*)(row + 8);
+        xl[p][u] = f32x4{v0[0], v0[1], v1[0], v1[1]};
+      }
+      xul[p] = *(lds_f*)(xring[p] + c * 4 * 18 + 4 * (16 + (g & 1)) + (g >= 2 ? SLOTB : 0));
+    } else {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) xl[p][u] = xf[p][u][0];
+      xul[p] = xup[p];
+    }
+  }
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
 #pragma unroll
@@ -1104,13 +1144,13 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         y[p][u][i] = relu_fast(z4[p][u][i]);
-        float e = y[p][u][i] - xf[p][u][0][i];
+        float e = y[p][u][i] - xl[p][u][i];
         if (stand_in(p, u)) e = 0.f;
         sq = fmaf(e, e, sq);
         dz4[p][u][i] = y[p][u][i] > 0.f ? e : 0.f;   // relu'; x 2/D folded into F.w4b / the acc4 slab
       }
     yup[p] = relu_fast(z4u[p][0]);
-    float eup = yup[p] - xup[p];
+    float eup = yup[p] - xul[p];
     if (TP && p == NP - 1) eup = g < 2 ? eup : 0.f;
     sq = fmaf(eup, eup, sq);
     dz4up[p] = yup[p] > 0.f ? eup : 0.f;
@@ -1212,13 +1252,23 @@ __device__ __forceinline__ void train_pair_packed(const AEArgs& a, const FragsP&
       h1r[1] = tr_read(sp + 4 * 512, c, g);
       h2r = tr_read(sp + 5 * 512, c, g);
       h3r = tr_read(sp + 6 * 512, c, g);
-      dz4r[0] = lds_transpose(dz4b[p][0], sp + 7 * 512, c, g);
-      dz4r[1] = lds_transpose(dz4b[p][1], sp + 8 * 512, c, g);
-      dz4ru = lds_transpose(dz4bu[p], sp + 9 * 512, c, g);
-      dz3r = lds_transpose(dz3b[p], sp + 7 * 512, c, g);
-      dz2r = lds_transpose(dz2b[p], sp + 8 * 512, c, g);
-      dz1r[0] = lds_transpose(dz1b[p][0], sp + 9 * 512, c, g);
-      dz1r[1] = lds_transpose(dz1b[p][1], sp + 7 * 512, c, g);
+      if constexpr (XP == 3) {   // the backward operands by MFMA against the identity
+        dz4r[0] = mfma_tr(dz4b[p][0]);
+        dz4r[1] = mfma_tr(dz4b[p][1]);
+        dz4ru = mfma_tr(dz4bu[p]);
+        dz3r = mfma_tr(dz3b[p]);
+        dz2r = mfma_tr(dz2b[p]);
+        dz1r[0] = mfma_tr(dz1b[p][0]);
+        dz1r[1] = mfma_tr(dz1b[p][1]);
+      } else {
+        dz4r[0] = lds_transpose(dz4b[p][0], sp + 7 * 512, c, g);
+        dz4r[1] = lds_transpose(dz4b[p][1], sp + 8 * 512, c, g);
+        dz4ru = lds_transpose(dz4bu[p], sp + 9 * 512, c, g);
+        dz3r = lds_transpose(dz3b[p], sp + 7 * 512, c, g);
+        dz2r = lds_transpose(dz2b[p], sp + 8 * 512, c, g);
+        dz1r[0] = lds_transpose(dz1b[p][0], sp + 9 * 512, c, g);
+        dz1r[1] = lds_transpose(dz1b[p][1], sp + 7 * 512, c, g);
+      }
     } else {
       xur = lds_transpose(xub[p], sp + (1 % TS) * 512, c, g);
 #pragma unroll
@@ -1477,13 +1527,16 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void ae_train_kernel(AEArgs a) {
             f32x4 xf[NPW][2][2];
             float xup[NPW];
             int ix[NPW][2];
+            const char* xr[NPW];
 #pragma unroll
             for (int k = 0; k < NPW; ++k) {
               load_pair(rs, xf[k], xup[k], ix[k]);
+              xr[k] = ring + 2 * rs * slotb;
               rs = rs + 1 == PS ? 0 : rs + 1;
             }
-            train_pair_packed<PACK, DC, false, TS, NPW, XP>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3, acc4,
-                                                            acc2b, acc4b, sq, ab, corr, rows);
+            constexpr bool RX = XM == 1 && OCC >= 4;
+            train_pair_packed<PACK, DC, false, TS, NPW, XP, RX>(a, FP, scr, c, g, xf, xup, ix, acc1, acc2, acc3,
+                                                                acc4, acc2b, acc4b, sq, ab, corr, rows, xr);
           }
           if (NPW == 2 && pi < npairs) {   // a last lone pair: the oldest of the PS - NPW in flight
             static_assert(NPW == 1 || PS - NPW - 1 >= 0, "ring depth");
@@ -1876,15 +1929,18 @@ static bool direct_pairs() {
 }
 // SML_AE_PAIR_OCC=2|3|4: waves per SIMD (2: two packed pairs per loop iteration) of the packed-pair kernel on the tile-packed ring
 // (read at every launch, like SML_AE_ILP)
+// Default 4 with XP 3: 4 waves per SIMD, forward operands through early LDS writes and backward
+// ones through the MFMA identity -- 51.6-53.4 vs 48.6-49.5 G rows/s for the round-5 loop (3, XP 0)
+// on the same boxes (profiles/r06/SUMMARY.md §1).
 static int pair_occ() {
   const char* e = getenv("SML_AE_PAIR_OCC");
-  return (e && (e[0] == '2' || e[0] == '4')) ? e[0] - '0' : 3;
+  return (e && (e[0] == '2' || e[0] == '3' || e[0] == '4')) ? e[0] - '0' : 4;
 }
-// SML_AE_PAIR_XP=0|1|2: the packed-pair weight-gradient operand path (train_pair_packed's XP;
-// 1 is implied at SML_AE_PAIR_OCC=4)
+// SML_AE_PAIR_XP=0|1|2|3: the packed-pair weight-gradient operand path (train_pair_packed's XP);
+// at SML_AE_PAIR_OCC=4, 0 means 1 (the 4-wave build needs the early writes' registers)
 static int pair_xp() {
   const char* e = getenv("SML_AE_PAIR_XP");
-  return (e && e[0] == '2') ? 2 : 0;
+  return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
 }
 static int train_occupancy() {
   const char* e = getenv("SML_AE_OCC");
@@ -1984,10 +2040,14 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
       const int xp = pair_xp();
       if (po == 2)   // two packed pairs per iteration, 2 waves / SIMD
         hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 8, 2, 18, 1, 3, 10, 2>), gd, bd, 0, stream, a);
-      else if (po == 4 && xp == 2)
-        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 4, 4, 18, 1, 3, 10, 1, 2>), gd, bd, 0, stream, a);
+      else if (po == 4 && xp >= 2)   // (XP 2 at 4 waves spills: the MFMA-transpose temporaries)
+        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 4, 4, 18, 1, 3, 10, 1, 3>), gd, bd, 0, stream, a);
+      else if (xp == 3)
+        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 1, 3, 10, 1, 3>), gd, bd, 0, stream, a);
       else if (po == 4)
         hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 4, 4, 18, 1, 3, 10, 1, 1>), gd, bd, 0, stream, a);
+      else if (xp == 1)
+        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 1, 3, 10, 1, 1>), gd, bd, 0, stream, a);
       else if (xp == 2)
         hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 1, 3, 10, 1, 2>), gd, bd, 0, stream, a);
       else
@@ -2000,7 +2060,10 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
       // rows trained once (fresh / streamed): packed pairs straight from the raw rows,
       // normalize_fn + argmax(x) in registers (no K8 pack pass)
       pair_grid();
-      hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 0, 3>), gd, bd, 0, stream, a);
+      if (pair_xp() == 3)
+        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 0, 3, 10, 1, 3>), gd, bd, 0, stream, a);
+      else
+        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 0, 3>), gd, bd, 0, stream, a);
     }
     else if (ring_ok && occ == 4 && D == 18)  // the cardata-v1 reference model: D fixed at compile time
       hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 3, 4, 18>), gd, bd, 0, stream, a);

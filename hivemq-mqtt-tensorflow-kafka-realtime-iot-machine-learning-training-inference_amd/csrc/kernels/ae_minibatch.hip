@@ -1256,7 +1256,7 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
                                float beta2, float eps, float gscale, int want_acc, unsigned long long* prof,
                                int nmodels, int64_t xmodel, const float* lrs, const int64_t* ragged,
                                uint64_t* const* dp_peers, int dp_ranks, int dp_rank0, int* dp_status,
-                               long long dp_timeout, hipStream_t stream, const MBStream* sr) {
+                               long long dp_timeout, hipStream_t stream, const MBStream* sr, int precision) {
   // ragged: per-model ring / steps were validated on the host (torch_bind.cpp)
   if (sr && (nmodels != 1 || ragged || dp_ranks > 1 || !sr->avail || !sr->total || !sr->consumed || !sr->status))
     return hipErrorInvalidValue;   // streaming: one model, one replica
@@ -1270,10 +1270,11 @@ hipError_t ae_minibatch_launch(const float* x, int64_t ld, int64_t ring, int64_t
            sr ? sr->avail : nullptr, sr ? sr->total : nullptr, sr ? sr->consumed : nullptr,
            sr ? sr->status : nullptr, sr ? sr->timeout_ticks : 0};
   const bool ref = acts[0] == ACT_TANH && acts[1] == ACT_RELU && acts[2] == ACT_TANH && acts[3] == ACT_RELU;
-  // SML_MB_BF16=1 (read per launch): phase A's contractions on bf16 MFMAs (kstep4) for the
+  // precision 1 (the model's compile(minibatch_precision="bf16")), or -1 with SML_MB_BF16=1 (read per
+  // launch, a process-wide default): phase A's contractions on bf16 MFMAs (kstep4) for the
   // reference-activation single-replica builds; fp32 (the Keras-exact path) otherwise
-  const char* bfe = getenv("SML_MB_BF16");
-  const bool bf = bfe && bfe[0] == '1' && ref && dp_ranks <= 1;
+  const char* bfe = precision < 0 ? getenv("SML_MB_BF16") : nullptr;
+  const bool bf = (precision == 1 || (bfe && bfe[0] == '1')) && ref && dp_ranks <= 1;
   void (*k)(MBArgs) = nullptr;
   size_t lds = 0;
   auto pick = [&](auto dpx) {

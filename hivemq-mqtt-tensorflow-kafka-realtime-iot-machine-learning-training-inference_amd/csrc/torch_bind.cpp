@@ -280,7 +280,8 @@ void train_minibatches_impl(const at::Tensor& x, const at::Tensor& cursor, const
                             bool want_acc, const c10::optional<at::Tensor>& prof,
                             const c10::optional<at::Tensor>& lrs, uint64_t dp_peers, int64_t dp_ranks,
                             int64_t dp_rank0, uint64_t dp_status, int64_t dp_timeout_ticks,
-                            const c10::optional<at::Tensor>& ragged, const sml::MBStream* sr, hipStream_t st) {
+                            const c10::optional<at::Tensor>& ragged, const sml::MBStream* sr, hipStream_t st,
+                            int64_t precision = -1) {
   // One model: params/m/v [1536], cursor/iter [1], x [ring, ld].  Fleet of M models:
   // params/m/v [M, 1536], cursor/iter [M], metrics [M, 4], x [ring, ld] (shared) or [M, ring, ld].
   check_ae_dims(dims, acts);
@@ -353,7 +354,7 @@ void train_minibatches_impl(const at::Tensor& x, const at::Tensor& cursor, const
                                          prof_ptr, (int)M, x.dim() == 3 ? x.stride(0) : 0, lrs_ptr, ragged_ptr,
                                          reinterpret_cast<uint64_t* const*>(dp_peers), (int)dp_ranks, (int)dp_rank0,
                                          reinterpret_cast<int*>(dp_status), (long long)dp_timeout_ticks,
-                                         st, sr));
+                                         st, sr, (int)precision));
 }
 
 void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c10::optional<at::Tensor>& scale,
@@ -363,10 +364,10 @@ void ae_train_minibatches(const at::Tensor& x, const at::Tensor& cursor, const c
                           double l1, double lr, double beta1, double beta2, double eps, double gscale, bool want_acc,
                           const c10::optional<at::Tensor>& prof, const c10::optional<at::Tensor>& lrs,
                           uint64_t dp_peers, int64_t dp_ranks, int64_t dp_rank0, uint64_t dp_status,
-                          int64_t dp_timeout_ticks, const c10::optional<at::Tensor>& ragged) {
+                          int64_t dp_timeout_ticks, const c10::optional<at::Tensor>& ragged, int64_t precision) {
   train_minibatches_impl(x, cursor, scale, shift, params, m, v, iter, metrics, batch, nsteps, std::move(dims),
                          std::move(acts), l1, lr, beta1, beta2, eps, gscale, want_acc, prof, lrs, dp_peers, dp_ranks,
-                         dp_rank0, dp_status, dp_timeout_ticks, ragged, nullptr, cur_stream(x));
+                         dp_rank0, dp_status, dp_timeout_ticks, ragged, nullptr, cur_stream(x), precision);
 }
 
 // A streaming epoch on ONE persistent ae_minibatch launch (runtime/stream_ring.h): the
@@ -401,7 +402,7 @@ class StreamRingPy {
              const at::Tensor& params, const at::Tensor& m, const at::Tensor& v, const at::Tensor& iter,
              const c10::optional<at::Tensor>& metrics, int64_t batch, int64_t max_steps, std::vector<int64_t> dims,
              std::vector<int64_t> acts, double l1, double lr, double beta1, double beta2, double eps, double gscale,
-             bool want_acc, double timeout_s) {
+             bool want_acc, double timeout_s, int64_t precision) {
     TORCH_CHECK(!running_, "StreamRing.train: an epoch is already running");
     TORCH_CHECK(ring_.pushed() == 0 && ring_.consumed() == 0, "StreamRing.train: reset() the ring first");
     TORCH_CHECK(ring_.rows() % batch == 0, "StreamRing: ring rows must be a multiple of the batch");
@@ -414,7 +415,7 @@ class StreamRingPy {
     const sml::MBStream sr = ring_.counters(timeout_s);
     train_minibatches_impl(ring(), cursor, scale, shift, params, m, v, iter, metrics, batch, max_steps,
                            std::move(dims), std::move(acts), l1, lr, beta1, beta2, eps, gscale, want_acc,
-                           c10::nullopt, c10::nullopt, 0, 1, 0, 0, 0, c10::nullopt, &sr, train_);
+                           c10::nullopt, c10::nullopt, 0, 1, 0, 0, 0, c10::nullopt, &sr, train_, precision);
     SML_CHECK_HIP(hipEventRecord(after_, train_));
     running_ = true;
   }
@@ -1343,7 +1344,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("acts"), py::arg("l1"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
         py::arg("gscale"), py::arg("want_acc"), py::arg("prof") = py::none(), py::arg("lrs") = py::none(),
         py::arg("dp_peers") = 0, py::arg("dp_ranks") = 1, py::arg("dp_rank0") = 0, py::arg("dp_status") = 0,
-        py::arg("dp_timeout_ticks") = 0, py::arg("ragged") = py::none());
+        py::arg("dp_timeout_ticks") = 0, py::arg("ragged") = py::none(), py::arg("precision") = -1);
   m.def("normalize_filter", &normalize_filter, "K8: normalise + keep rows with label == keep, order-preserving",
         py::arg("x"), py::arg("D"), py::arg("labels"), py::arg("keep"), py::arg("scale"), py::arg("shift"),
         py::arg("want_index") = false);
@@ -1381,7 +1382,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("train", &StreamRingPy::train, py::arg("cursor"), py::arg("scale"), py::arg("shift"), py::arg("params"),
            py::arg("m"), py::arg("v"), py::arg("iter"), py::arg("metrics"), py::arg("batch"), py::arg("max_steps"),
            py::arg("dims"), py::arg("acts"), py::arg("l1"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"),
-           py::arg("eps"), py::arg("gscale"), py::arg("want_acc"), py::arg("timeout_s") = 30.0)
+           py::arg("eps"), py::arg("gscale"), py::arg("want_acc"), py::arg("timeout_s") = 30.0,
+           py::arg("precision") = -1)
       .def("push", &StreamRingPy::push, py::arg("rows"), py::arg("timeout_s") = 30.0)
       .def("finish", &StreamRingPy::finish)
       .def("join", &StreamRingPy::join)

@@ -99,12 +99,14 @@ class Autoencoder:
         raise ValueError(f"unknown input_normalizer {self.input_normalizer!r}")
 
     def compile(self, optimizer="adam", loss="mean_squared_error", metrics=("accuracy",), learning_rate=None,
-                minibatch_precision: str = "fp32", **adam_kw) -> "Autoencoder":
+                minibatch_precision: Optional[str] = None, **adam_kw) -> "Autoencoder":
         """Keras ``compile``.  ``minibatch_precision`` picks the small-batch (Keras batch <= 128)
-        trainer's contraction precision: ``"fp32"`` (default, Keras-exact) or ``"bf16"`` (bf16
-        MFMA forward / activation gradients, fp32 weight gradients, master weights and Adam)."""
-        if minibatch_precision not in ("fp32", "bf16"):
-            raise ValueError("minibatch_precision must be 'fp32' or 'bf16'")
+        trainer's contraction precision: ``"fp32"`` (Keras-exact) or ``"bf16"`` (bf16 MFMA forward /
+        activation gradients, fp32 weight gradients, master weights and Adam); None (default) takes
+        the process default (``SML_MB_BF16=1``: bf16, else fp32).  The choice is passed to this
+        model's launches as an argument, so models of different precision can share a process."""
+        if minibatch_precision not in (None, "fp32", "bf16"):
+            raise ValueError("minibatch_precision must be 'fp32', 'bf16' or None")
         self.minibatch_precision = minibatch_precision
         if str(optimizer).lower() != "adam":
             raise ValueError("only the Adam optimizer is implemented (the reference uses 'adam')")
@@ -125,7 +127,8 @@ class Autoencoder:
         if self.device.type == "cuda":
             self._backend = FusedAE(self.spec, weights, self.device, max_blocks=self.max_blocks,
                                     want_acc="accuracy" in self.metrics, scale=sc, shift=sh, **self.hp)
-            self._backend.minibatch_bf16 = getattr(self, "minibatch_precision", "fp32") == "bf16"
+            prec = getattr(self, "minibatch_precision", None)
+            self._backend.minibatch_bf16 = None if prec is None else prec == "bf16"
         else:
             self._backend = TorchAE(self.spec.layer_sizes, self.spec.activations, self.spec.activity_l1, weights,
                                     device=self.device, **self.hp)
@@ -413,6 +416,21 @@ class Autoencoder:
     # ~19 passes over the same rows (profiles/r05/SUMMARY.md; with r03's one-tile direct
     # loop, 0.97 ms, it was 3)
     PACK_MIN_PASSES = 18
+    # ... but the direct step only runs on packed pairs when the launcher's predicate holds
+    # (ae_fused.hip: the reference model at D = 18, a batch of whole 32-row pairs, the default
+    # loop); otherwise it is the one-tile direct loop (0.97 ms), whose break-even is ~3 passes
+    PACK_MIN_PASSES_ONE_TILE = 3
+
+    def _direct_pairs(self, B: int) -> bool:
+        sp = self.spec
+        return (sp.input_dim == 18 and sp.encoding_dim <= 15 and sp.hidden_dim <= 7 and B % 32 == 0
+                and tuple(sp.activations) == ("tanh", "relu", "tanh", "relu")
+                and os.environ.get("SML_AE_DIRECT_PAIRS", "1") != "0"
+                and os.environ.get("SML_AE_ILP", "3") not in ("1", "2"))
+
+    def pack_min_passes(self, B: int) -> int:
+        """Passes over the same rows from which packing them once beats the direct step."""
+        return self.PACK_MIN_PASSES if self._direct_pairs(B) else self.PACK_MIN_PASSES_ONE_TILE
 
     def _fit_array_throughput(self, xd: torch.Tensor, B: int, steps_per_epoch: Optional[int], shuffle: bool,
                               seed: int, rank: int, epoch: int, world: int, allreduce, gstep: int,
@@ -438,7 +456,7 @@ class Autoencoder:
         if nfull:
             key = self.pack_key(xd, B, nfull)
             packed = pkey is None and getattr(self, "_tp_key", None) == key and be.ring_xpack is not None
-            if pkey is None and not packed and epochs_left < self.PACK_MIN_PASSES:
+            if pkey is None and not packed and epochs_left < self.pack_min_passes(B):
                 for i in range(nfull):   # rows in place, normalised inside the kernel
                     be.step(xd[i * B:(i + 1) * B], global_batch=B * world, allreduce=allreduce)
             else:

@@ -413,11 +413,16 @@ class LSTMPredictor:
             yd = torch.as_tensor(ys, dtype=torch.float32, device=self.device)
         n = len(xd)
         nb = math.ceil(n / batch_size)
+        ns = [n]
         if world > 1:
             # one all-reduce per step: every rank must run the same step count (shards may
-            # differ by a few windows -- the rank with more drops its excess, as drop_last)
+            # differ by a few windows -- the rank with more drops its excess, as drop_last).
+            # Every rank's row count, once: step b's global batch is the rows ALL ranks train in
+            # it, so a short last batch averages over exactly those rows
             from ..parallel.dp import agree
-            nb = agree([nb])[0]
+            r_ = dist.get_rank()
+            ns = agree([n if i == r_ else 0 for i in range(world)], None, ["sum"] * world)
+            nb = min(math.ceil(v / batch_size) for v in ns)
         if take is not None:
             nb = min(nb, take)
         from ..ops import lstm_persistent as lp
@@ -451,7 +456,8 @@ class LSTMPredictor:
                 xb = xd[order[sl]] if order is not None else xd[sl]
                 yb = yd[order[sl]] if order is not None else yd[sl]
                 maybe_inject(gstep, rank)
-                loss, corr = self.train_step(xb, yb, global_batch=len(xb) * world, allreduce=allreduce)
+                gb = sum(min(batch_size, max(0, v - b * batch_size)) for v in ns) if world > 1 else len(xb)
+                loss, corr = self.train_step(xb, yb, global_batch=gb, allreduce=allreduce)
                 gstep += 1
                 tot_loss += loss * len(xb)
                 tot_corr += corr

@@ -14,7 +14,6 @@ accumulated on device and read once per epoch, never per step.
 """
 from __future__ import annotations
 
-import contextlib
 
 import os
 
@@ -389,10 +388,10 @@ class FusedAE:
         # run while the resident kernel waits for the rows it produces.
         it = iter(chunks)
         xd = next(it, None)
-        with self._minibatch_precision():
-            sr.train(self._tcur, self.scale, self.shift, self.params, self.m, self.v, self.iter, self.metrics, B,
-                     nmax, self.spec.dims, self.spec.act_codes, float(self.spec.activity_l1), self.lr, self.beta_1,
-                     self.beta_2, self.epsilon, 1.0 / B, bool(self.want_acc), float(timeout_s))
+        sr.train(self._tcur, self.scale, self.shift, self.params, self.m, self.v, self.iter, self.metrics, B,
+                 nmax, self.spec.dims, self.spec.act_codes, float(self.spec.activity_l1), self.lr, self.beta_1,
+                 self.beta_2, self.epsilon, 1.0 / B, bool(self.want_acc), float(timeout_s),
+                 precision=self._mb_precision())
         pushed = 0
         try:
             while xd is not None and (limit is None or pushed < limit):
@@ -429,24 +428,13 @@ class FusedAE:
     # forward / activation-gradient contractions of each step on bf16 MFMAs (fp32 accumulation,
     # fp32 weight gradients, fp32 master weights and Adam): Autoencoder.fit(batch_size=100)
     # 27.3 -> 33.3 M rows/s, parameters within 0.4-1.5 % of the fp32 run after 400 steps
-    # (profiles/r05 SUMMARY §9).  The launcher reads SML_MB_BF16 per launch; this flag sets it
-    # around this model's launches (the in-kernel DP exchange always runs fp32).
-    minibatch_bf16 = False
+    # (profiles/r05 SUMMARY §9).  Passed to every launch of this model as an explicit argument
+    # (SML_MB_BF16=1 stays a process-wide default for models that leave it unset); the in-kernel
+    # DP exchange always runs fp32.
+    minibatch_bf16 = None
 
-    @contextlib.contextmanager
-    def _minibatch_precision(self):
-        if not self.minibatch_bf16:
-            yield
-            return
-        old = os.environ.get("SML_MB_BF16")
-        os.environ["SML_MB_BF16"] = "1"
-        try:
-            yield
-        finally:
-            if old is None:
-                os.environ.pop("SML_MB_BF16", None)
-            else:
-                os.environ["SML_MB_BF16"] = old
+    def _mb_precision(self) -> int:
+        return -1 if self.minibatch_bf16 is None else int(bool(self.minibatch_bf16))
 
     def _launch_minibatch(self, ring: torch.Tensor, cursor: torch.Tensor, B: int, nsteps: int,
                           prof: Optional[torch.Tensor] = None, dp=None) -> None:
@@ -457,11 +445,11 @@ class FusedAE:
             it0 = int(self.iter.item())
             kw = dp.kernel_args(it0)
             gscale = 1.0 / (B * dp.world)
-        with self._minibatch_precision():
-            self.C.ae_train_minibatches(ring, cursor, self.scale, self.shift, self.params, self.m, self.v,
-                                        self.iter, self.metrics, int(B), int(nsteps), self.spec.dims,
-                                        self.spec.act_codes, float(self.spec.activity_l1), self.lr, self.beta_1,
-                                        self.beta_2, self.epsilon, gscale, bool(self.want_acc), prof, None, **kw)
+        self.C.ae_train_minibatches(ring, cursor, self.scale, self.shift, self.params, self.m, self.v,
+                                    self.iter, self.metrics, int(B), int(nsteps), self.spec.dims,
+                                    self.spec.act_codes, float(self.spec.activity_l1), self.lr, self.beta_1,
+                                    self.beta_2, self.epsilon, gscale, bool(self.want_acc), prof, None,
+                                    precision=self._mb_precision(), **kw)
         if dp is not None:
             dp.note_iter(it0 + int(nsteps) - 1)
             dp.check()

@@ -64,12 +64,15 @@ def cpu_busy(sample_s: float = 0.05) -> Optional[dict]:
 
 def l3_cpus(k: int, slot: int = 0, avoid_busy: bool = True) -> Optional[List[int]]:
     """``k`` CPUs of this process's affinity set sharing one L3, one per physical core (None:
-    cache topology not readable, or no L3 domain with ``k`` allowed cores).  Spinning
-    latency-critical threads lose whole scheduler slices (ms) to any other runnable thread on
-    their CPU, so with ``avoid_busy`` each domain keeps its ``k`` least-busy cores (a 50 ms
-    /proc/stat sample; CPU 0, which services most housekeeping, last) and the domains are
-    ordered by that load.  ``slot`` (e.g. a replica's rank) picks among the qualifying domains
-    round-robin, so replicas do not share one."""
+    cache topology not readable, or no L3 domain with ``k`` allowed cores).
+
+    ``slot`` (e.g. a replica's rank) picks the domain round-robin in a DETERMINISTIC order (by
+    first CPU): replicas started one after another each sample the load on their own, so an
+    order derived from that sample would differ between them and two replicas could land on one
+    domain while another stays unused.  Inside the chosen domain, spinning latency-critical
+    threads lose whole scheduler slices (ms) to any other runnable thread on their CPU, so with
+    ``avoid_busy`` the ``k`` least-busy cores are taken (a 50 ms /proc/stat sample; CPU 0, which
+    services most housekeeping, last)."""
     groups = {}
     for c in sorted(os.sched_getaffinity(0)):
         try:
@@ -78,18 +81,16 @@ def l3_cpus(k: int, slot: int = 0, avoid_busy: bool = True) -> Optional[List[int
         except OSError:
             return None
         groups.setdefault(l3, {}).setdefault(core, c)   # first allowed CPU of each core
-    cands = [sorted(g.values()) for g in groups.values() if len(g) >= k]
+    cands = sorted((sorted(g.values()) for g in groups.values() if len(g) >= k), key=lambda cs: cs[0])
     if not cands:
         return None
+    dom = cands[slot % len(cands)]
     busy = cpu_busy() if avoid_busy else None
     if busy:
         def load(c):
             return busy.get(c, 0.0) + (0.5 if c == 0 else 0.0)
-        picked = [sorted(sorted(cs, key=lambda c: (load(c), c))[:k]) for cs in cands]
-        order = sorted(range(len(cands)), key=lambda i: (round(sum(load(c) for c in picked[i]), 2), cands[i][0]))
-        return picked[order[slot % len(order)]]
-    ok = sorted(cands, key=lambda cs: cs[0])
-    return ok[slot % len(ok)][:k]
+        return sorted(sorted(dom, key=lambda c: (load(c), c))[:k])
+    return dom[:k]
 
 
 def resolve_cpus(spec: Optional[str], slot: int = 0) -> Optional[Set[int]]:

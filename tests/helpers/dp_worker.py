@@ -28,6 +28,12 @@ def main(out_dir: str) -> None:
     m = LSTMPredictor.reference(look_back=4, device="cpu", seed=1)
     m.fit(xs, ys, epochs=1, batch_size=8, verbose=0)   # fit shards by rank itself
     np.savez(os.path.join(out_dir, f"lstm_{rank}.npz"), *m.fp.get())
+    # --- LSTM with uneven shards (61 windows: 31 / 30) and a short last batch (7 + 6 rows)
+    xu = rng.uniform(-1, 1, size=(61, 4, 18)).astype(np.float32)
+    yu = rng.uniform(-1, 1, size=(61, 18)).astype(np.float32)
+    mu = LSTMPredictor.reference(look_back=4, device="cpu", seed=2)
+    mu.fit(xu, yu, epochs=1, batch_size=8, verbose=0, shuffle=False)
+    np.savez(os.path.join(out_dir, f"lstm_uneven_{rank}.npz"), *mu.fp.get())
     # --- MNIST MLP: local batch 16
     from streamml.data.mnist import synthetic_mnist
     from streamml.models.mlp import MLPClassifier

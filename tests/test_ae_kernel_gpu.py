@@ -364,7 +364,7 @@ def test_tile_pair_loop_matches_one_tile_loop(cuda_device, monkeypatch, ntiles, 
     assert _relerr(out[ilp][1], out["1"][1]) < 1e-4
 
 
-@pytest.mark.parametrize("occ", ["2", "4", "3x2", "4x2"])
+@pytest.mark.parametrize("occ", ["2", "4", "3x2", "3x3", "4x3"])
 @pytest.mark.parametrize("ntiles,blocks", [(64 * 5, 16), (64 * 4, 16), (4096, 48), (2 * 4096 + 6, 48), (2, 16)])
 def test_pair_occupancy_variants_bit_identical(cuda_device, monkeypatch, ntiles, blocks, occ):
     """SML_AE_PAIR_OCC=2 (TWO packed pairs per loop iteration, one interleaved stream, 2 waves per

@@ -203,3 +203,11 @@ def test_autoencoder_minibatch_precision_option(cuda_device, monkeypatch):
     assert "SML_MB_BF16" not in os.environ
     assert not np.array_equal(ws["fp32"], ws["bf16"])
     assert np.linalg.norm(ws["bf16"] - ws["fp32"]) / np.linalg.norm(ws["fp32"]) < 3e-2
+    # the choice travels with the model's launches: an explicit "fp32" ignores the
+    # process default, an unset precision follows it
+    monkeypatch.setenv("SML_MB_BF16", "1")
+    for prec, want in (("fp32", "fp32"), (None, "bf16")):
+        m = Autoencoder(device=cuda_device, seed=4)
+        m.compile(minibatch_precision=prec)
+        m.fit(x, epochs=2, batch_size=100, verbose=0)
+        np.testing.assert_array_equal(np.concatenate([w.ravel() for w in m.get_weights()]), ws[want])

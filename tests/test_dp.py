@@ -78,3 +78,31 @@ def test_fit_dp_none_is_single_replica_inside_a_group(dp_run):
     for u, v in zip(w, ae.get_weights()):   # CPU torch thread counts differ: summation order only
         np.testing.assert_allclose(u, v, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(z["loss"], h.history["loss"], rtol=1e-5)
+
+
+@pytest.mark.dist
+def test_lstm_dp_short_last_batch_is_mean_over_trained_rows(dp_run):
+    """Uneven shards (31 / 30 windows) at batch 8: the last step trains 7 + 6 rows, and its
+    update must be the mean over those 13 rows -- the single-process step on the concatenated
+    rows -- not the average of the two ranks' means."""
+    import torch
+    from streamml.models.lstm import LSTMPredictor
+    from streamml.parallel.dp import shard_range
+    rng = np.random.default_rng(0)
+    rng.uniform(-1, 1, size=(256, 18))          # the worker's draws before the uneven set
+    rng.uniform(-1, 1, size=(64, 4, 18))
+    rng.uniform(-1, 1, size=(64, 18))
+    xu = rng.uniform(-1, 1, size=(61, 4, 18)).astype(np.float32)
+    yu = rng.uniform(-1, 1, size=(61, 18)).astype(np.float32)
+    sh = [shard_range(61, r, 2) for r in range(2)]
+    m = LSTMPredictor.reference(look_back=4, device="cpu", seed=2)
+    m.compile() if hasattr(m, "compile") and not getattr(m, "compiled", True) else None
+    for b in range(4):
+        idx = np.concatenate([np.arange(s0, s1)[b * 8:(b + 1) * 8] for s0, s1 in sh])
+        m.train_step(torch.as_tensor(xu[idx]), torch.as_tensor(yu[idx]))
+    a, _ = _load(dp_run / "lstm_uneven_0.npz")
+    b_, _ = _load(dp_run / "lstm_uneven_1.npz")
+    for u, v in zip(a, b_):
+        np.testing.assert_array_equal(u, v)
+    for u, v in zip(a, m.fp.get()):
+        np.testing.assert_allclose(u, v.detach().cpu().numpy() if hasattr(v, "detach") else v, rtol=1e-5, atol=1e-6)

@@ -27,6 +27,7 @@ def test_time_retention_deletes_old_segments_and_consumer_resets():
         assert b.start_offset("sensor-data", 0) == 4096 and b.end_offset("sensor-data", 0) == 4096
         assert b.deleted_records >= 4096 and b.deleted_segments >= 4
         assert b.start_offset("keep", 0) == 0          # other topics keep their log
+        b.create_topic("sensor-data", 2, retention_ms=-1)   # (no timing race with what follows)
         _fill(b, "sensor-data", 1000)                  # new records after the deletion
         c = KafkaClient(b.address)
         with pytest.raises(Exception) as ei:
@@ -181,5 +182,25 @@ def test_ordered_parallel_reader_matches_sequential_order():
             par = [(bt["partition"], list(bt["offsets"])) for bt in
                    KafkaDataset(["o:*:0"], servers=b.address, eof=True, max_bytes=20_000, workers=3, ordered=True)]
             assert par == seq
+    finally:
+        b.stop()
+
+
+def test_rescaled_serving_groups_seeded_from_previous_commits():
+    """serve: a replica's per-replica group (<base>.<r>-of-<w>, used when a partition is shared by
+    key) starts from the minimum position the previous layout committed (at-least-once)."""
+    from streamml.cli.serve import seed_group_offsets
+    b = FakeBroker()
+    try:
+        b.create_topic("s", 3)
+        c = KafkaClient(b.address)
+        c.commit("g.0-of-2", "s", 1, 700)       # old layout: two replicas shared partition 1
+        c.commit("g.1-of-2", "s", 1, 650)
+        c.commit("g", "s", 0, 900)
+        got = seed_group_offsets(c, "s", "g", "g.2-of-3", [0, 1, 2])
+        assert got == {0: 900, 1: 650}         # partition 2 was never consumed: left alone
+        assert c.committed("g.2-of-3", "s", 1) == 650 and c.committed("g.2-of-3", "s", 2) < 0
+        c.commit("g.2-of-3", "s", 1, 800)       # an existing commit is never overwritten
+        assert seed_group_offsets(c, "s", "g", "g.2-of-3", [1]) == {}
     finally:
         b.stop()

@@ -343,3 +343,24 @@ def test_l3_cpus_picks_distinct_cores_of_one_l3():
         l3 = {open(f"/sys/devices/system/cpu/cpu{x}/cache/index3/shared_cpu_list").read() for x in cs}
         cores = {open(f"/sys/devices/system/cpu/cpu{x}/topology/thread_siblings_list").read() for x in cs}
         assert len(l3) == 1 and len(cores) == k
+
+
+def test_l3_cpus_slots_take_distinct_domains_whatever_the_load(monkeypatch):
+    """Replicas started one after another each sample the CPU load on their own: the domain a
+    slot gets must not depend on that sample, only the cores inside it."""
+    import random
+    from streamml.utils import affinity
+    allowed = sorted(os.sched_getaffinity(0))
+    doms = set()
+    for c in allowed:
+        try:
+            doms.add(open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list").read())
+        except OSError:
+            return   # no cache topology in sysfs
+    rng = random.Random(0)
+    monkeypatch.setattr(affinity, "cpu_busy", lambda sample_s=0.05: {c: rng.random() for c in allowed})
+    got = []
+    for slot in range(len(doms)):
+        cs = affinity.l3_cpus(1, slot)
+        got.append(open(f"/sys/devices/system/cpu/cpu{cs[0]}/cache/index3/shared_cpu_list").read())
+    assert len(set(got)) == len(doms)
