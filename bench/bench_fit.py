@@ -132,18 +132,23 @@ def stream_e2e(device, rows: int = 2_000_000, batch: int = 100, partitions: int 
     return out
 
 
+def _encode(rows, failure_rate=0.01, distinct=1_000_000):
+    """The bench topic's distinct Confluent-Avro events: (buffer, offsets, count) chunks."""
+    from streamml.data import stream as S
+    from streamml.data.avro import AvroCodec
+    from streamml.data.produce import encode_chunk
+    codec = AvroCodec("cardata-v1")
+    chunk = min(rows, 250_000)
+    return [encode_chunk(codec, c.x, c.label) + (len(c.x),)
+            for c in S.synthetic(min(rows, distinct), chunk=chunk, seed=0, failure_rate=failure_rate)]
+
+
 def _fill_topic(b, topic, rows, partitions, failure_rate=0.01, distinct=1_000_000, staged=None):
     """Append ``rows`` Confluent-framed Avro events round-robin over ``partitions`` (up to
     ``distinct`` encoded once, then re-appended).  ``staged`` (a list): receives the encoded
     (buffer, offsets, count) chunks -- the same values, pre-staged in memory."""
-    from streamml.data import stream as S
-    from streamml.data.avro import AvroCodec
-    from streamml.data.produce import encode_chunk
     b.create_topic(topic, partitions)
-    codec = AvroCodec("cardata-v1")
-    chunk = min(rows, 250_000)
-    encoded = [encode_chunk(codec, c.x, c.label) + (len(c.x),)
-               for c in S.synthetic(min(rows, distinct), chunk=chunk, seed=0, failure_rate=failure_rate)]
+    encoded = _encode(rows, failure_rate, distinct)
     if staged is not None:
         staged.extend(encoded)
     left, i, nbytes = rows, 0, 0
@@ -178,8 +183,39 @@ def _cpu_quota():
         return None
 
 
+def _broker_process(rows: int, partitions: int, cpus):
+    """Start bench/broker_proc.py (pinned to ``cpus`` with taskset when given) and wait for its
+    address line.  Returns (Popen, info dict)."""
+    import json
+    import shutil
+    import subprocess
+    import sys
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "broker_proc.py")
+    cmd = [sys.executable, script, "--rows", str(rows), "--partitions", str(partitions)]
+    if cpus and shutil.which("taskset"):
+        cmd = ["taskset", "-c", ",".join(str(c) for c in sorted(cpus))] + cmd
+    proc = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    line = proc.stdout.readline()
+    if not line:
+        proc.kill()
+        raise RuntimeError("broker process exited before serving")
+    return proc, json.loads(line)
+
+
+def _split_cpus(broker_share: float = 0.25):
+    """This process's CPUs split in two disjoint sets: (consumer, broker).  With a cgroup quota
+    the split is sized by the quota (the CPUs both processes may keep busy), not the machine."""
+    allowed = sorted(os.sched_getaffinity(0))
+    quota = _cpu_quota()
+    usable = allowed[:max(4, int(quota))] if quota else allowed
+    nb = max(2, int(round(len(usable) * broker_share)))
+    if len(usable) <= nb + 1:
+        return set(allowed), None
+    return set(usable[:-nb]), set(usable[-nb:])
+
+
 def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, batch: int = 1 << 20,
-                       workers=(1, 2, 4, 8, 16, 32), train_workers: int = 0) -> dict:
+                       workers=(1, 2, 4, 8, 16, 32), train_workers: int = 0, broker: str = "process") -> dict:
     """Fresh rows at large batch: ``partitions`` partitions of Confluent
     Avro -> native C++ feed (one worker per partition group, pinned slabs, H2D in flight) ->
     ``fit(batch_size=batch, engine="throughput")`` over the stream, every epoch re-reading the
@@ -188,22 +224,59 @@ def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, bat
     Reports the host fetch + decode rate against the number of feed workers (the slabs are
     recycled uncopied: the decode alone) and the end-to-end trained rows/s at the best
     worker count.  Each row is ~155 bytes on the wire, so 100 M rows/s is 15.5 GB/s of
-    loopback Kafka traffic."""
+    loopback Kafka traffic.
+
+    ``broker="process"`` (default) serves the topic from bench/broker_proc.py, a child process on
+    CPUs of its own (the reference's brokers are remote pods): the curve then prices the
+    consumer's fetch + decode alone; ``"inproc"`` keeps the in-process broker."""
+    from streamml.kafka import fake_broker
+
+    name = f"bench-large-{rows}-{partitions}-{time.time_ns()}"
+    topic = "SENSOR_DATA_S_AVRO"
+    t0 = time.perf_counter()
+    quota = _cpu_quota()
+    proc, binfo = None, None
+    mask0 = os.sched_getaffinity(0)
+    if broker == "process":
+        # the broker in a child process on CPUs of its own (the reference's brokers are remote pods);
+        # this process's feed workers keep the rest
+        mine, theirs = _split_cpus()
+        proc, binfo = _broker_process(rows, partitions, theirs)
+        src_addr = binfo["addr"]
+        staged = _encode(rows)
+        nbytes = int(binfo["log_bytes"])
+        os.sched_setaffinity(0, mine)
+    else:
+        b = fake_broker(name)
+        src_addr = f"fake://{name}"
+        staged = []
+        nbytes = _fill_topic(b, topic, rows, partitions, staged=staged)
+    try:
+        out = _stream_large_batch_on(device, src_addr, topic, rows, partitions, batch, workers, train_workers,
+                                     staged, nbytes, quota, t0)
+    finally:
+        os.sched_setaffinity(0, mask0)
+        if proc is not None:
+            proc.stdin.close()
+            try:
+                proc.wait(timeout=30)
+            except Exception:  # noqa: BLE001
+                proc.kill()
+    out["broker"] = ({"mode": "separate process", "pid": binfo["pid"], "cpus": binfo["cpus"],
+                      "consumer_cpus": sorted(mine), "produce_s": binfo["produce_s"]}
+                     if proc is not None else {"mode": "in-process"})
+    return out
+
+
+def _stream_large_batch_on(device, src_addr, topic, rows, partitions, batch, workers, train_workers, staged, nbytes,
+                           quota, t0) -> dict:
     import torch
 
     from streamml.data import stream as S
-    from streamml.kafka import fake_broker
     from streamml.models.autoencoder import Autoencoder
 
     import numpy as np
 
-    name = f"bench-large-{rows}-{partitions}-{time.time_ns()}"
-    b = fake_broker(name)
-    topic = "SENSOR_DATA_S_AVRO"
-    t0 = time.perf_counter()
-    staged = []
-    nbytes = _fill_topic(b, topic, rows, partitions, staged=staged)
-    quota = _cpu_quota()
     out = {"rows": rows, "partitions": partitions, "batch": batch, "log_bytes": nbytes,
            "bytes_per_row": nbytes / rows, "produce_s": time.perf_counter() - t0,
            "cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_quota": quota}
@@ -215,7 +288,7 @@ def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, bat
     bases = np.cumsum([0] + sizes[:-1])
     offs = np.concatenate([np.zeros(1, np.int64)] + [np.asarray(s[1][1:s[2] + 1], np.int64) + int(base)
                                                     for s, base in zip(staged, bases)])
-    probe = S.kafka(f"fake://{name}", specs[:1], native=True).native_feed
+    probe = S.kafka(src_addr, specs[:1], native=True).native_feed
     dcurve = []
     for w in tuple(workers) + ((32,) if 32 not in workers else ()):
         r, _ = probe.decode_only(buf, offs, int(w), repeats=2, keep_label=0)
@@ -225,7 +298,7 @@ def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, bat
     # 2. fetch + decode from the broker (its connection threads share this process's CPUs)
     curve = []
     for w in workers:
-        src = S.kafka(f"fake://{name}", specs, max_bytes=8 << 20, workers=int(w), native=True)
+        src = S.kafka(src_addr, specs, max_bytes=8 << 20, workers=int(w), native=True)
         t1 = time.perf_counter()
         n = src.native_feed.count_rows()
         dt = time.perf_counter() - t1
@@ -236,7 +309,7 @@ def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, bat
     out["decode_curve"] = curve
     best = max(curve, key=lambda c: c["rows_per_s"])
     tw = int(train_workers or best["workers"])
-    src = S.kafka(f"fake://{name}", specs, max_bytes=8 << 20, workers=tw, native=True)
+    src = S.kafka(src_addr, specs, max_bytes=8 << 20, workers=tw, native=True)
     training = src.filter_normal(device=True)
     m = Autoencoder(device=device, input_normalizer="cardata")
     m.compile()
@@ -261,7 +334,7 @@ def stream_large_batch(device, rows: int = 32_000_000, partitions: int = 32, bat
     soffs = np.concatenate([offs[:-1] + k * len(buf) for k in range(reps)] + [np.array([reps * len(buf)], np.int64)])
     staged_runs = []
     for w in sorted({min(8, int(quota or 8)), max(1, min(16, int(quota or 16) - 2))}):
-        ssrc = S.kafka(f"fake://{name}", specs[:1], workers=int(w), native=True)
+        ssrc = S.kafka(src_addr, specs[:1], workers=int(w), native=True)
         ssrc.native_feed.stage(sbuf, soffs)
         st_train = ssrc.filter_normal(device=True)
         ms = Autoencoder(device=device, input_normalizer="cardata")
