@@ -173,10 +173,17 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 // 4q+p of each 16-lane group addressing row 4g+q, columns 4p..4p+3.
 // LDS ops of one wave complete in order, so no wait is needed between the write
 // and the transposed read beyond the one the compiler places before the use.
+// XOR swizzle: the 8-byte column of row r is stored at column (col ^ ((r >> 2) & 3)).  With plain
+// 32-byte rows the write put lanes c, c + 4, c + 8, c + 12 of a 16-lane group on the same banks
+// (4-way conflict on every ds_write_b64: SQ_LDS_BANK_CONFLICT 3.6-5.9 cycles per LDS instruction
+// in the LSTM backward, profiles/r06); swizzled, the write and the transposed read are both
+// conflict-free, and every lane still reads the same 8 bytes, so the result is bit-identical.
+__device__ __forceinline__ int tr_wr_off(int c, int g) { return c * 32 + 8 * (g ^ ((c >> 2) & 3)); }
+__device__ __forceinline__ int tr_rd_off(int c, int g) { return (4 * g + (c >> 2)) * 32 + 8 * ((c & 3) ^ g); }
 __device__ __forceinline__ bf16x4 lds_transpose(bf16x4 v, char* wave_scratch, int c, int g) {
-  lds_bf16x4* wr = (lds_bf16x4*)(wave_scratch + c * 32 + 8 * g);
+  lds_bf16x4* wr = (lds_bf16x4*)(wave_scratch + tr_wr_off(c, g));
   *wr = v;
-  lds_bf16x4* rd = (lds_bf16x4*)(wave_scratch + (4 * g + (c >> 2)) * 32 + 8 * (c & 3));
+  lds_bf16x4* rd = (lds_bf16x4*)(wave_scratch + tr_rd_off(c, g));
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(rd);
 }
 

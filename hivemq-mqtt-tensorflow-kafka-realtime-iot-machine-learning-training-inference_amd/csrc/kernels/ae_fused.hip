@@ -991,10 +991,10 @@ __device__ __forceinline__ void packed_fold_src(int s, int& s1, int& s2) {
 // of the step: write it to its own slot as soon as it exists (its registers die there), read the
 // transposed copy back right before the weight-gradient MFMA (EW variants).
 __device__ __forceinline__ void tr_write(bf16x4 v, char* slot, int c, int g) {
-  *(lds_bf16x4*)(slot + c * 32 + 8 * g) = v;
+  *(lds_bf16x4*)(slot + tr_wr_off(c, g)) = v;   // the swizzled layout of lds_transpose
 }
 __device__ __forceinline__ bf16x4 tr_read(char* slot, int c, int g) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(slot + (4 * g + (c >> 2)) * 32 + 8 * (c & 3)));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(slot + tr_rd_off(c, g)));
 }
 
 // NP packed pairs of whole tiles in ONE interleaved instruction stream (NP = 1 or 2).  Every
