@@ -91,7 +91,8 @@ def main():
     r["soak_summary"] = {
         "windows": len(ae), "scored": r["ae"]["scored"], "published": r["published"], "dropped": r["dropped"],
         "p99_us_per_window": [w["p99_us"] for w in ae], "max_us": r["ae"]["publish_to_result_max_us"],
-        "broker_rss_mb": r["broker_rss_mb"], "short_windows": sum(1 for w in ae[:-1] if w["scored"] < w["offered"])}
+        "broker_rss_mb": r["broker_rss_mb"], "short_windows": sum(1 for w in ae[:-1] if w["scored"] < w["offered"]),
+        "kafka_log": r.get("kafka_log"), "scorer_rss_mb": r.get("scorer_rss_mb")}
     line = json.dumps(r)
     if a.out:
         with open(a.out, "w") as f:

@@ -528,6 +528,7 @@ PYBIND11_MODULE(_io, m) {
            py::arg("max_events") = 0, py::arg("idle_timeout_s") = -1.0)
       .def("stop", &serve::ScoreLoop::stop)
       .def("positions", &serve::ScoreLoop::positions)
+      .def("latency_bytes", &serve::ScoreLoop::latency_bytes)
       .def("latency_records", [](serve::ScoreLoop& l) {
         const auto& v = l.latency_records();
         constexpr int C = serve::ScoreLoop::kLatCols;

@@ -1005,13 +1005,18 @@ void Broker::retention_loop() {
   while (running_) {
     retention_cv_.wait_for(g, std::chrono::milliseconds(std::max(cfg_.retention_check_ms, 10)));
     if (!running_) break;
-    enforce_locked(steady_ms());
+    std::vector<std::shared_ptr<const std::string>> dead;
+    enforce_locked(steady_ms(), dead);
+    g.unlock();   // a second's worth of segments is freed without stalling produce / fetch
+    dead.clear();
+    g.lock();
   }
 }
 
 size_t Broker::enforce_retention() {
+  std::vector<std::shared_ptr<const std::string>> dead;
   std::lock_guard<std::mutex> g(mu_);
-  return enforce_locked(steady_ms());
+  return enforce_locked(steady_ms(), dead);
 }
 
 // Kafka's log cleaner in delete mode: per partition, whole segments oldest first -- while the
@@ -1019,7 +1024,7 @@ size_t Broker::enforce_retention() {
 // without it (size; the newest segment is always kept).  A consumer positioned inside a deleted
 // range then gets OFFSET_OUT_OF_RANGE and follows its auto.offset.reset.  Segment bytes are
 // shared: a fetch still sending one keeps it alive until it is done.
-size_t Broker::enforce_locked(int64_t now_ms) {
+size_t Broker::enforce_locked(int64_t now_ms, std::vector<std::shared_ptr<const std::string>>& dead) {
   size_t dropped_total = 0;
   for (auto& tp : topics_) {
     int64_t ms = cfg_.retention_ms, by = cfg_.retention_bytes;
@@ -1042,15 +1047,16 @@ size_t Broker::enforce_locked(int64_t now_ms) {
         ++drop;
       }
       if (!drop) continue;
-      p.segs.erase(p.segs.begin(), p.segs.begin() + (std::ptrdiff_t)drop);
-      if (p.segs.capacity() > 4 * p.segs.size() + 64) p.segs.shrink_to_fit();
+      for (size_t i = 0; i < drop; ++i) {
+        dead.push_back(std::move(p.segs.front().bytes));
+        p.segs.pop_front();
+      }
       p.bytes = bytes;
       p.start = p.segs.empty() ? p.end : p.segs.front().base;
       if (p.tbase >= 0 && p.tbase < p.start) {   // append times of deleted offsets go too
         const int64_t k = std::min<int64_t>(p.start - p.tbase, (int64_t)p.tappend.size());
-        p.tappend.erase(p.tappend.begin(), p.tappend.begin() + (std::ptrdiff_t)k);
+        p.tappend.erase(p.tappend.begin(), p.tappend.begin() + (std::ptrdiff_t)k);   // deque: O(k)
         p.tbase += k;
-        if (p.tappend.capacity() > 4 * p.tappend.size() + 1024) p.tappend.shrink_to_fit();
       }
       deleted_segs_ += drop;
       deleted_recs_ += (uint64_t)recs;

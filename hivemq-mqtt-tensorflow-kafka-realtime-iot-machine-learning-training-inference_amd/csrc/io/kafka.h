@@ -20,6 +20,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -243,12 +244,12 @@ class Broker {
     std::shared_ptr<const std::string> bytes;
   };
   struct Partition {
-    std::vector<Segment> segs;   // a deque in effect: retention erases from the front in bulk
+    std::deque<Segment> segs;   // retention pops from the front: O(deleted), not O(retained)
     int64_t start = 0;  // offset of the first retained record
     int64_t end = 0;    // next offset to assign
     int64_t bytes = 0;  // encoded bytes of segs
     int64_t tbase = -1;              // first offset with a recorded append time
-    std::vector<int64_t> tappend;    // append times (ns) of offsets tbase, tbase + 1, ...
+    std::deque<int64_t> tappend;     // append times (ns) of offsets tbase, tbase + 1, ...
   };
   int64_t append_locked(Partition& p, const Record* recs, size_t n);
   // A fetch reply: the response framing in `meta`, with the (shared, immutable) segment
@@ -278,7 +279,8 @@ class Broker {
   std::condition_variable retention_cv_;
   std::atomic<uint64_t> deleted_segs_{0}, deleted_recs_{0};
   void retention_loop();
-  size_t enforce_locked(int64_t now_ms);
+  // Deleted segment bytes are moved into `dead` so the caller frees them after unlocking.
+  size_t enforce_locked(int64_t now_ms, std::vector<std::shared_ptr<const std::string>>& dead);
   // finished connection threads, joined by the accept loop (a long soak opens many connections)
   std::vector<std::shared_ptr<std::atomic<bool>>> worker_done_;
   std::condition_variable data_cv_;   // appends -> long-polling fetches

@@ -88,6 +88,9 @@ class ScoreLoop {
   // formatted records, and the record's json_stamp field (0 without one)
   static constexpr int kLatCols = 7;
   const std::vector<int64_t>& latency_records() const { return lat_; }
+  // bytes of latency records written so far: readable while the loop runs, so a soak can
+  // tell the measurement's own memory from the scorer's
+  size_t latency_bytes() const { return lat_bytes_.load(std::memory_order_relaxed); }
 
  private:
   std::string bootstrap_;
@@ -102,6 +105,7 @@ class ScoreLoop {
   std::unordered_map<std::string, uint32_t> key_ids_;
   std::vector<int64_t> pos_;
   std::vector<int64_t> lat_;
+  std::atomic<size_t> lat_bytes_{0};
   size_t rot_ = 0;   // first partition of the next multi-partition fetch (rotated, KIP-74)
   std::atomic<bool> stop_{false};
 };

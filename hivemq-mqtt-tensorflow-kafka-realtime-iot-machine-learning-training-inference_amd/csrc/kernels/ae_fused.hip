@@ -2059,8 +2059,14 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
              dims[1] <= 15 && dims[2] <= 7 && dims[3] <= 7) {
       // rows trained once (fresh / streamed): packed pairs straight from the raw rows,
       // normalize_fn + argmax(x) in registers (no K8 pack pass)
-      pair_grid();
-      if (pair_xp() == 3)
+      static const int docc = [] {   // SML_AE_DIRECT_OCC=4: the 4-wave build of the direct step (A/B)
+        const char* e = std::getenv("SML_AE_DIRECT_OCC");
+        return (e && e[0] == '4') ? 4 : 3;
+      }();
+      pair_grid(docc);
+      if (docc == 4)
+        hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 4, 4, 18, 0, 3, 10, 1, 3>), gd, bd, 0, stream, a);
+      else if (pair_xp() == 3)
         hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 0, 3, 10, 1, 3>), gd, bd, 0, stream, a);
       else
         hipLaunchKernelGGL((ae_train_kernel<PACK_REF, true, 6, 3, 18, 0, 3>), gd, bd, 0, stream, a);

@@ -157,14 +157,22 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
       const int G = 4 * L.u, j = lane & 31, p = lane >> 5;
       const int ca = p * L.u + j, cb = (2 + p) * L.u + j;
       const bool ok = j < L.u;
+      // Gate scales folded into the columns (both waves of a split layer load the same ones):
+      // sigmoid gates i, f, o carry -log2(e), so sigm(z) = 1 / (1 + 2^z') is one v_exp + add +
+      // v_rcp; a tanh layer's g~ carries -2 log2(e) (tanh(z) = 2 sigm(2z) - 1), so every lane
+      // activates both of its gates with the same three instructions before the halves swap.
+      // A relu layer's g~ stays unscaled.
+      constexpr float L2E = 1.4426950408889634f;
+      const float sa = -L2E, sb = p ? -L2E : (L.act == ACT_RELU ? 1.f : -2.f * L2E);
 #pragma unroll
       for (int k = 0; k < 32; ++k) {
-        wp[k] = (want_w && ok && k < L.in) ? f32x2{S.w[L.woff + k * G + ca], S.w[L.woff + k * G + cb]}
+        wp[k] = (want_w && ok && k < L.in) ? f32x2{S.w[L.woff + k * G + ca] * sa, S.w[L.woff + k * G + cb] * sb}
                                            : f32x2{0.f, 0.f};
-        wp[32 + k] = (want_u && ok && k < L.u) ? f32x2{S.w[L.uoff + k * G + ca], S.w[L.uoff + k * G + cb]}
-                                               : f32x2{0.f, 0.f};
+        wp[32 + k] = (want_u && ok && k < L.u)
+                         ? f32x2{S.w[L.uoff + k * G + ca] * sa, S.w[L.uoff + k * G + cb] * sb}
+                         : f32x2{0.f, 0.f};
       }
-      if (want_w && ok) bp = f32x2{S.w[L.boff + ca], S.w[L.boff + cb]};
+      if (want_w && ok) bp = f32x2{S.w[L.boff + ca] * sa, S.w[L.boff + cb] * sb};
     }
   }
   // register-resident weight halves of every LSTM layer: k = 32 * half + i of [W ; U]
@@ -251,6 +259,13 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
     float prev = 0.f;
     if (tid == 0) S.ctl[2] = ld_agent(&a.hcount[key]);
     if (tid >= 64 && tid < 64 + D) prev = ld_agent(&lastp[tid - 64]);
+    // The key's whole window ring, in storage order, in the same round trip as its count: the
+    // ring always holds the key's last T events, only its rotation depends on the count, so
+    // the rows are placed (rotated) once the count is known instead of read after it.
+    constexpr int WPT = MAXT * MAXW / NT;   // ring elements per thread (T * D <= MAXT * MAXW)
+    float rv[WPT];
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) rv[i] = (tid + i * NT < T * D) ? ld_agent(&hist[tid + i * NT]) : 0.f;
     if (tid >= 64 && tid < 64 + D) S.pred[tid - 64] = prev;   // parked until the count is known
     __syncthreads();
     const int cnt = S.ctl[2];
@@ -270,9 +285,17 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
     if (PIPE && tid < 2) s_prj[tid] = 0;
     // ---------------- the window, oldest first, into seqa [t][k] (the newest row from LDS)
     if (full) {
-      for (int e = tid; e < T * D; e += NT) {
-        const int t = e / D, k = e - t * D;
-        S.seqa[t * MAXW + k] = t == T - 1 ? S.xrow[k] : ld_agent(&hist[((cnt + 1 - T + t) % T) * D + k]);
+      // storage slot r holds events n = r (mod T); window step t holds event cnt + 1 - T + t, so
+      // t = (r - cnt - 1) mod T, and step T - 1 is this event (its slot still holds the evicted one)
+      const int rot = (cnt + 1) % T;
+#pragma unroll
+      for (int i = 0; i < WPT; ++i) {
+        const int e = tid + i * NT;
+        if (e < T * D) {
+          const int r = e / D, k = e - r * D;
+          const int t = r >= rot ? r - rot : r - rot + T;
+          S.seqa[t * MAXW + k] = t == T - 1 ? S.xrow[k] : rv[i];
+        }
       }
     }
     __syncthreads();
@@ -283,109 +306,142 @@ __global__ __launch_bounds__(NT) void lstm_serve_kernel(LstmServeArgs a) {
       typedef __attribute__((address_space(3))) volatile int lds_vint;
       lds_vint* rdy = (lds_vint*)s_rdy;   // ds_read / ds_write, never a flat access
       lds_vint* prj = (lds_vint*)s_prj;
+      // Dot products run over a compile-time number of float4 input groups (4 or 8; the
+      // padded columns and their weights are zero): a runtime trip count under `#pragma
+      // unroll` became a v_cndmask per accumulator per group (8 selects per 4 packed FMAs).
+      using I4 = std::integral_constant<int, 4>;
+      using I8 = std::integral_constant<int, 8>;
       if (split && lw >= 2 && lw - 2 < npipe) {
         // ---- input projection of layer pl: zx_t = x_t . W + b into the ring
         const int pl = lw - 2;
         const LstmServeLayer& L = a.L[pl];
-        const int nI4 = (L.in + 3) >> 2;
         const float* xin = pl == 0 ? S.seqa : S.H + (pl - 1) * MAXT * MAXW;
-        for (int t = 0; t < T; ++t) {
-          if (pl > 0)   // the layer below has published h_t
-            while (rdy[pl - 1] <= t) {
+        auto project = [&](auto ni4c) {
+          constexpr int NI4 = decltype(ni4c)::value;
+          int below = pl > 0 ? 0 : T, freed = ZX_RING;   // producer / consumer counters seen
+          for (int t = 0; t < T; ++t) {
+            if (below <= t || freed <= t) {
+              if (pl > 0)   // the layer below has published h_t
+                while ((below = rdy[pl - 1]) <= t) {
+                }
+              // ring slot free: the recurrence has finished step t - ZX_RING
+              while ((freed = rdy[pl] + ZX_RING) <= t) {
+              }
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             }
-          if (t >= ZX_RING)   // ring slot free: the recurrence has finished step t - ZX_RING
-            while (rdy[pl] <= t - ZX_RING) {
-            }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-          const float4* x4 = reinterpret_cast<const float4*>(xin + t * MAXW);
-          float4 xv[8];
+            const float4* x4 = reinterpret_cast<const float4*>(xin + t * MAXW);
+            float4 xv[NI4];
 #pragma unroll
-          for (int k4 = 0; k4 < 8; ++k4) xv[k4] = x4[k4];
-          f32x2 acc[4] = {bp, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+            for (int k4 = 0; k4 < NI4; ++k4) xv[k4] = x4[k4];
+            f32x2 acc[4] = {bp, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
-          for (int k4 = 0; k4 < 8; ++k4) {
-            if (k4 < nI4) {
+            for (int k4 = 0; k4 < NI4; ++k4) {
               acc[0] = fma2(xv[k4].x, wp[4 * k4 + 0], acc[0]);
               acc[1] = fma2(xv[k4].y, wp[4 * k4 + 1], acc[1]);
               acc[2] = fma2(xv[k4].z, wp[4 * k4 + 2], acc[2]);
               acc[3] = fma2(xv[k4].w, wp[4 * k4 + 3], acc[3]);
             }
+            s_zx[pl][t % ZX_RING][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) prj[pl] = t + 1;
           }
-          s_zx[pl][t % ZX_RING][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          if (lane == 0) prj[pl] = t + 1;
-        }
+        };
+        if (L.in > 16) project(I8{});
+        else project(I4{});
       } else if (lw < npipe) {
         const LstmServeLayer& L = a.L[lw];
-        const int u = L.u, relu = L.act == ACT_RELU;
-        const int nI4 = split ? 0 : (L.in + 3) >> 2, nU4 = (u + 3) >> 2;
+        const int u = L.u;
         const float* xin = lw == 0 ? S.seqa : S.H + (lw - 1) * MAXT * MAXW;
         float* hout = S.H + lw * MAXT * MAXW;
-        float c = 0.f;
-        for (int t = 0; t < T; ++t) {
-          if (split) {   // this step's input projection is in the ring
-            while (prj[lw] <= t) {
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-          } else if (lw > 0) {   // the layer below has published h_t
-            while (rdy[lw - 1] <= t) {
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-          }
-          // every LDS read first (padded columns are zero), then the FMAs under scalar
-          // branches: one LDS wait per step instead of one per read
-          const float4* x4 = reinterpret_cast<const float4*>(xin + t * MAXW);
-          const float4* h4 = reinterpret_cast<const float4*>(t > 0 ? hout + (t - 1) * MAXW : s_zrow);
-          float4 xv[8], hv[8];
-          f32x2 acc[8];
-          if (split) {
-            acc[0] = s_zx[lw][t % ZX_RING][lane];
-          } else {
-            acc[0] = bp;
-#pragma unroll
-            for (int k4 = 0; k4 < 8; ++k4) xv[k4] = x4[k4];
-          }
-#pragma unroll
-          for (int k4 = 0; k4 < 8; ++k4) hv[k4] = h4[k4];
-#pragma unroll
-          for (int q = 1; q < 8; ++q) acc[q] = f32x2{0.f, 0.f};
-          if (!split) {
-#pragma unroll
-            for (int k4 = 0; k4 < 8; ++k4) {
-              if (k4 < nI4) {
-                acc[(2 * k4) & 7] = fma2(xv[k4].x, wp[4 * k4 + 0], acc[(2 * k4) & 7]);
-                acc[(2 * k4 + 1) & 7] = fma2(xv[k4].y, wp[4 * k4 + 1], acc[(2 * k4 + 1) & 7]);
-                acc[(2 * k4) & 7] = fma2(xv[k4].z, wp[4 * k4 + 2], acc[(2 * k4) & 7]);
-                acc[(2 * k4 + 1) & 7] = fma2(xv[k4].w, wp[4 * k4 + 3], acc[(2 * k4 + 1) & 7]);
+        // NI4: input groups of the x . W part (0: split, the projection wave does it); NU4: of h . U
+        auto recur = [&](auto ni4c, auto nu4c, auto reluc) {
+          constexpr int NI4 = decltype(ni4c)::value, NU4 = decltype(nu4c)::value;
+          constexpr bool RELU = decltype(reluc)::value;
+          float c = 0.f;   // a tanh layer carries c scaled by 2 log2(e) (below)
+          int avail = 0;   // steps the producer (projection ring or the layer below) has published
+          for (int t = 0; t < T; ++t) {
+            // The producer runs ahead, so its counter is re-read only once the steps already
+            // seen are used up: no LDS round trip on the recurrence's chain in the common case.
+            if (avail <= t) {
+              if (NI4 == 0) {   // this step's input projection is in the ring
+                while ((avail = prj[lw]) <= t) {
+                }
+              } else if (lw > 0) {   // the layer below has published h_t
+                while ((avail = rdy[lw - 1]) <= t) {
+                }
+              } else {
+                avail = T;
               }
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             }
-          }
+            // every LDS read first (padded columns are zero), then the FMAs: one LDS wait per step
+            const float4* x4 = reinterpret_cast<const float4*>(xin + t * MAXW);
+            const float4* h4 = reinterpret_cast<const float4*>(t > 0 ? hout + (t - 1) * MAXW : s_zrow);
+            float4 xv[NI4 ? NI4 : 1], hv[NU4];
+            f32x2 acc[4];   // four chains: at most 8 + 8 dependent packed FMAs each, under the issue time
+            if constexpr (NI4 == 0) {
+              acc[0] = s_zx[lw][t % ZX_RING][lane];
+            } else {
+              acc[0] = bp;
 #pragma unroll
-          for (int k4 = 0; k4 < 8; ++k4) {
-            if (k4 < nU4) {
-              const int q0 = (2 * k4 + 4) & 7, q1 = (2 * k4 + 5) & 7;
-              acc[q0] = fma2(hv[k4].x, wp[32 + 4 * k4 + 0], acc[q0]);
-              acc[q1] = fma2(hv[k4].y, wp[32 + 4 * k4 + 1], acc[q1]);
-              acc[q0] = fma2(hv[k4].z, wp[32 + 4 * k4 + 2], acc[q0]);
-              acc[q1] = fma2(hv[k4].w, wp[32 + 4 * k4 + 3], acc[q1]);
+              for (int k4 = 0; k4 < NI4; ++k4) xv[k4] = x4[k4];
             }
+#pragma unroll
+            for (int k4 = 0; k4 < NU4; ++k4) hv[k4] = h4[k4];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) acc[q] = f32x2{0.f, 0.f};
+#pragma unroll
+            for (int k4 = 0; k4 < NI4; ++k4) {
+              acc[0] = fma2(xv[k4].x, wp[4 * k4 + 0], acc[0]);
+              acc[1] = fma2(xv[k4].y, wp[4 * k4 + 1], acc[1]);
+              acc[2] = fma2(xv[k4].z, wp[4 * k4 + 2], acc[2]);
+              acc[3] = fma2(xv[k4].w, wp[4 * k4 + 3], acc[3]);
+            }
+#pragma unroll
+            for (int k4 = 0; k4 < NU4; ++k4) {
+              acc[0] = fma2(hv[k4].x, wp[32 + 4 * k4 + 0], acc[0]);
+              acc[1] = fma2(hv[k4].y, wp[32 + 4 * k4 + 1], acc[1]);
+              acc[2] = fma2(hv[k4].z, wp[32 + 4 * k4 + 2], acc[2]);
+              acc[3] = fma2(hv[k4].w, wp[32 + 4 * k4 + 3], acc[3]);
+            }
+            const f32x2 z = (acc[0] + acc[1]) + (acc[2] + acc[3]);   // scaled pre-activations
+            // Each lane activates its own two gates, then ONE swap per value brings the (f, o)
+            // of lane + 32 to the p = 0 lanes (the only ones that keep c and write h):
+            //   p = 0: ea = sigm(i), eb = sigm(2 g~) (tanh layer; unused by relu)
+            //   p = 1: ea = sigm(f), eb = sigm(o)
+            const float ea = rcp_fast(1.f + __builtin_amdgcn_exp2f(z.x));
+            const float eb = rcp_fast(1.f + __builtin_amdgcn_exp2f(z.y));
+            const float fg = __uint_as_float(
+                __builtin_amdgcn_permlane32_swap(__float_as_uint(ea), __float_as_uint(ea), false, false)[1]);
+            const float og = __uint_as_float(
+                __builtin_amdgcn_permlane32_swap(__float_as_uint(eb), __float_as_uint(eb), false, false)[1]);
+            float h;
+            if constexpr (RELU) {
+              c = fmaf(fg, c, ea * relu_fast(z.y));
+              h = og * relu_fast(c);
+            } else {
+              // c' = K c with K = 2 log2(e): c' = f c' + i (K tanh(g~)), K tanh(g~) = 2K sigm(2g~) - K,
+              // and tanh(c) = 1 - 2 / (1 + 2^c'), so h = o - 2 o / (1 + 2^c')
+              constexpr float K = 2.8853900817779268f;
+              c = fmaf(fg, c, ea * fmaf(eb, 2.f * K, -K));
+              h = fmaf(-2.f * og, rcp_fast(1.f + __builtin_amdgcn_exp2f(c)), og);
+            }
+            if (lane < u) hout[t * MAXW + lane] = h;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) rdy[lw] = t + 1;
           }
-          const f32x2 z = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-          // p = 0 lanes: (i, g~) here, (f, o) from lane + 32
-          const float zf = xor32(z.x, lane), zo = xor32(z.y, lane);
-          const float ig = sigmoid_fast(z.x), fg = sigmoid_fast(zf), og = sigmoid_fast(zo);
-          float h;
-          if (relu) {
-            c = fmaf(fg, c, ig * fmaxf(z.y, 0.f));
-            h = og * fmaxf(c, 0.f);
-          } else {
-            c = fmaf(fg, c, ig * tanh_fast(z.y));
-            h = og * tanh_fast(c);
-          }
-          if (lane < u) hout[t * MAXW + lane] = h;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          if (lane == 0) rdy[lw] = t + 1;
-        }
+        };
+        auto with_u = [&](auto ni4c, auto reluc) {
+          if (u > 16) recur(ni4c, I8{}, reluc);
+          else recur(ni4c, I4{}, reluc);
+        };
+        auto with_i = [&](auto reluc) {
+          if (split) with_u(std::integral_constant<int, 0>{}, reluc);
+          else if (L.in > 16) with_u(I8{}, reluc);
+          else with_u(I4{}, reluc);
+        };
+        if (L.act == ACT_RELU) with_i(std::true_type{});
+        else with_i(std::false_type{});
         if (lw == npipe - 1) {   // Dense head on h_{T-1}
           const LstmServeLayer& Hd = a.L[npipe];
           const float* hl = hout + (T - 1) * MAXW;

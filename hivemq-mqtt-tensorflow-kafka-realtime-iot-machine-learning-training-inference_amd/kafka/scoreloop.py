@@ -102,6 +102,10 @@ class LowLatencyScorer:
     def positions(self):
         return list(self._loop.positions())
 
+    def latency_bytes(self) -> int:
+        """Bytes held by the latency records so far (safe to read while ``run`` is going)."""
+        return int(self._loop.latency_bytes())
+
     def latency_records(self) -> np.ndarray:
         """[n, 7] int64: (partition, offset, steady-clock ns the result became visible (produce
         ack), of the fetch response that carried the event, of its score, of its formatted

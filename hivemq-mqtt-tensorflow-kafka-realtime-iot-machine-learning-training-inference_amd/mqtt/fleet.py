@@ -126,7 +126,7 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
               threads: int = 4, qos: int = 0, lstm_scorer=None,
               name: str = "fleet", start_delay_s: Optional[float] = None, sources_per_agent: int = 1,
               max_wait_ms: int = 5, drain_timeout_s: float = 30.0, sample_s: float = 5.0,
-              window_s: Optional[float] = None) -> dict:
+              window_s: Optional[float] = None, retention_ms: int = 100_000) -> dict:
     """Run ``clients`` cars x ``messages`` events at ``clients / interval_s`` msg/s end to end.
 
     ``scorer``: a :class:`~streamml.ops.serve.ScoringServer` (or ``_io.EchoScorer`` on CPU);
@@ -139,7 +139,11 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
     Over time (a sustained run): every ``sample_s`` the broker nodes', agents' and this
     process's resident memory is sampled (``timeline.samples``), and the scored events are cut
     into ``window_s`` windows of result time (default: the send interval) with each window's
-    count against the offered count and its p50 / p99 / max latency (``timeline.<scorer>``)."""
+    count against the offered count and its p50 / p99 / max latency (``timeline.<scorer>``).
+
+    The topics keep the reference's ``retention.ms=100000`` (01_installConfluentPlatform.sh:180,
+    183; ``retention_ms``, -1 = unbounded): a sustained run's in-process Kafka log stays bounded
+    (``timeline.samples[].kafka_log_mb``), as the reference's brokers keep theirs."""
     from ..kafka import fake_broker
     from ..kafka.scoreloop import LowLatencyScorer
 
@@ -151,7 +155,7 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
     kb = fake_broker(name)
     topic, results, lresults = "sensor-data", "model-predictions", "lstm-predictions"
     for t in (topic, results) + ((lresults,) if lstm_scorer is not None else ()):
-        kb.create_topic(t, partitions)
+        kb.create_topic(t, partitions, retention_ms=retention_ms)
     total = clients * messages
     nodes = [_spawn(["broker", "--kafka", f"127.0.0.1:{kb.port}"], stdin=subprocess.PIPE) for _ in range(brokers)]
     agents_p: List[subprocess.Popen] = []
@@ -176,7 +180,12 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
                 samples.append({"t_s": round(time.time() - t_begin, 2),
                                 "broker_rss_mb": round(sum(_rss_mb(p.pid) for p in nodes), 1),
                                 "agents_rss_mb": round(sum(_rss_mb(p.pid) for p in agents_p), 1),
-                                "scorer_rss_mb": round(_rss_mb(os.getpid()), 1)})
+                                "scorer_rss_mb": round(_rss_mb(os.getpid()), 1),
+                                # the per-event latency records (the measurement, kept for the
+                                # percentiles): 56 B per scored event and scorer
+                                "latency_records_mb": round(sum(lp.latency_bytes() for lp in loops) / 1e6, 1),
+                                "kafka_log_mb": round(kb.log_bytes() / 1e6, 1),
+                                "kafka_deleted_records": int(kb.deleted_records)})
                 if stop_sampler.wait(sample_s):
                     return
 
@@ -237,6 +246,14 @@ def run_fleet(scorer, clients: int = 10_000, interval_s: float = 1.0, messages: 
     rss = [x["broker_rss_mb"] for x in samples if x["broker_rss_mb"] > 0]
     out["broker_rss_mb"] = {"first": rss[0] if rss else None, "last": rss[-1] if rss else None,
                             "max": max(rss) if rss else None}
+    net = [x["scorer_rss_mb"] - x["latency_records_mb"] for x in samples]
+    out["scorer_rss_mb"] = {"first": samples[0]["scorer_rss_mb"] if samples else None,
+                            "last": samples[-1]["scorer_rss_mb"] if samples else None,
+                            "last_less_latency_records": round(net[-1], 1) if net else None}
+    logmb = [x["kafka_log_mb"] for x in samples]
+    out["kafka_log"] = {"retention_ms": retention_ms, "max_mb": max(logmb) if logmb else None,
+                        "last_mb": logmb[-1] if logmb else None,
+                        "deleted_records": samples[-1]["kafka_deleted_records"] if samples else 0}
     out["timeline"] = {"samples": samples, "window_s": float(window_s or interval_s)}
     for tag, lp, o in zip(("ae", "lstm"), loops, outs):
         lat = lp.latency_records()
