@@ -2059,9 +2059,11 @@ hipError_t ae_train_launch(const float* x, int64_t n, int64_t ld, const float* s
              dims[1] <= 15 && dims[2] <= 7 && dims[3] <= 7) {
       // rows trained once (fresh / streamed): packed pairs straight from the raw rows,
       // normalize_fn + argmax(x) in registers (no K8 pack pass)
-      static const int docc = [] {   // SML_AE_DIRECT_OCC=4: the 4-wave build of the direct step (A/B)
+      // SML_AE_DIRECT_OCC=3: the 3-wave build (A/B).  Default the 4-wave one (128 VGPRs, 39 424 B
+      // LDS): 45.9 vs 45.3 G fresh rows/s on one box (profiles/r06/serve/fresh_direct_occ*.json)
+      static const int docc = [] {
         const char* e = std::getenv("SML_AE_DIRECT_OCC");
-        return (e && e[0] == '4') ? 4 : 3;
+        return (e && e[0] == '3') ? 3 : 4;
       }();
       pair_grid(docc);
       if (docc == 4)
