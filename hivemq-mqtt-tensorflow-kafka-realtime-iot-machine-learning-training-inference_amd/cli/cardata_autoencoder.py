@@ -46,6 +46,9 @@ def _flags(p):
                    help="under torchrun: each rank's share of the partitions (streamml.kafka.assign)")
     p.add_argument("--native-feed", action="store_true", help="ROCm: the C++ partition-parallel feed")
     p.add_argument("--feed-workers", type=int, default=4)
+    p.add_argument("--precision", default=None, choices=["fp32", "bf16"],
+                   help="small-batch trainer contractions (Keras batch <= 128): fp32 (Keras-exact, default) or "
+                        "bf16 MFMAs with fp32 master weights / Adam (compile(minibatch_precision=...))")
 
 
 def _world() -> int:
@@ -72,7 +75,7 @@ def _train(ns, servers, cfg, epochs, batch_size, out_path):
     device = ns.device if env.world_size == 1 else env.device
     ae = Autoencoder(input_dim=18, encoding_dim=14, hidden_dim=7, input_normalizer="cardata", device=device,
                      seed=ns.seed)
-    ae.compile(metrics=["accuracy"], loss="mean_squared_error", optimizer="adam")
+    ae.compile(metrics=["accuracy"], loss="mean_squared_error", optimizer="adam", minibatch_precision=ns.precision)
     sync_model_from_rank0(ae)
     if env.rank == 0:
         ae.summary()

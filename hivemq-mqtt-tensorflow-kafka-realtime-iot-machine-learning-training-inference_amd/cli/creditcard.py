@@ -36,6 +36,8 @@ def _flags(p):
     p.add_argument("--evaluate", action="store_true")
     p.add_argument("--threshold", type=float, default=5.0)
     p.add_argument("--save", default=None, help="write the trained model (.h5)")
+    p.add_argument("--precision", default=None, choices=["fp32", "bf16"],
+                   help="small-batch trainer contractions: fp32 (Keras-exact, default) or bf16 MFMAs")
 
 
 def main(argv: Sequence[str]) -> int:
@@ -62,7 +64,7 @@ def main(argv: Sequence[str]) -> int:
     print(f"consumed {len(x)} records ({int(y.sum())} fraud)", flush=True)
 
     ae = Autoencoder(input_dim=30, encoding_dim=14, hidden_dim=7, device=ns.device, seed=ns.seed)
-    ae.compile(metrics=["accuracy"], loss="mean_squared_error", optimizer="adam")
+    ae.compile(metrics=["accuracy"], loss="mean_squared_error", optimizer="adam", minibatch_precision=ns.precision)
     if not ns.evaluate:
         t0 = time.perf_counter()
         ae.fit(x.astype(np.float32), epochs=ns.epochs, batch_size=ns.batch_size, shuffle=False, verbose=2)

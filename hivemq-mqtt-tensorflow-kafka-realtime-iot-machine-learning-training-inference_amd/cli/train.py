@@ -38,7 +38,7 @@ from typing import Sequence
 
 
 JOB_KEYS = {"ckpt_dir": None, "ckpt_every": 1, "rows": 200000, "stack": "two_layer", "metrics_port": 0,
-            "segment_rows": 0}
+            "segment_rows": 0, "precision": ""}
 
 
 def _split(argv):
@@ -107,7 +107,7 @@ def main(argv: Sequence[str]) -> int:
             model = Autoencoder(cfg.input_dim, cfg.encoding_dim, cfg.hidden_dim, activity_l1=cfg.activity_l1,
                                 device=dev, seed=cfg.seed, input_normalizer="cardata")
             model.compile(learning_rate=cfg.learning_rate, beta_1=cfg.beta_1, beta_2=cfg.beta_2,
-                          epsilon=cfg.epsilon)
+                          epsilon=cfg.epsilon, minibatch_precision=job["precision"] or None)
         else:
             from ..models.lstm import LSTMPredictor
             ctor = LSTMPredictor.two_layer if job["stack"] == "two_layer" else LSTMPredictor.reference

@@ -39,6 +39,27 @@ def test_cardata_v3_inprocess(tmp_path, monkeypatch):
     assert msg.startswith(b"[") and msg.endswith(b"]")   # np.array2string row
 
 
+def test_precision_flag_reaches_the_small_batch_trainer(tmp_path, monkeypatch):
+    """``--precision bf16`` on the AE CLIs selects compile(minibatch_precision="bf16") (the
+    small-batch trainer's bf16 contractions); the default stays Keras-exact fp32 (None)."""
+    from streamml.models.autoencoder import Autoencoder
+    seen = []
+    orig = Autoencoder.compile
+
+    def spy(self, *a, **kw):
+        seen.append(kw.get("minibatch_precision"))
+        return orig(self, *a, **kw)
+
+    monkeypatch.setattr(Autoencoder, "compile", spy)
+    monkeypatch.setenv("SML_MODEL_STORE", str(tmp_path / "store"))
+    base = ["synthetic://12000", "CARSP", "0", "predsp"]
+    common = ["--device", "cpu", "--workdir", str(tmp_path), "--epochs", "1", "--take", "10"]
+    assert cli(["cardata-v3", *base, "train", "mp.h5", "proj", "--precision", "bf16", *common]) == 0
+    assert cli(["cardata-v3", *base, "train", "mq.h5", "proj", *common]) == 0
+    assert cli(["creditcard", "--device", "cpu", "--rows", "4000", "--epochs", "1", "--precision", "bf16"]) == 0
+    assert seen == ["bf16", None, "bf16"]
+
+
 def test_lstm_v2_and_v1_inprocess(tmp_path, monkeypatch):
     monkeypatch.setenv("SML_MODEL_STORE", str(tmp_path / "store"))
     base = ["synthetic://2500", "LSTMCARS", "0", "lstm-out"]
