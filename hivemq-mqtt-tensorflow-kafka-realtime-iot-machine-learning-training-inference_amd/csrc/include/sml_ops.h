@@ -117,6 +117,19 @@ hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, con
                                  const float* b, void* dx, float* dh0, float* dc0, float* partials, int64_t B, int T,
                                  int IN, int U, int act, int dh_last_only, int64_t x_seq, void* dz_scratch,
                                  int frag, hipStream_t stream);
+// unit-block split backward (lstm_fused_split.hip): U = 32 layers without dX (fp32 x, dh every step) in the
+// BX / DB bias modes run
+// with two waves per 16-sequence tile; lstm_fused_bwd_launch routes them there, and the caller sizes
+// the partials by lstm_fused_bwd_slabs (the split kernel's grid differs from lstm_fused_slabs)
+bool lstm_split_applies(int U, int IN, bool dx, bool x_bf16, bool dh_last_only);
+int lstm_split_grid(int64_t B);
+hipError_t lstm_split_bwd_launch(const void* dh, const void* cseq, const void* hseq, const void* x, bool x_bf16,
+                                 const float* h0, const float* c0, const float* W, const float* Uw, const float* b,
+                                 float* dh0, float* dc0, float* partials, int64_t B, int T, int IN, int act,
+                                 int dh_last_only, int64_t x_seq, int frag, hipStream_t st);
+inline int lstm_fused_bwd_slabs(int64_t B, int U, int IN, bool dx, bool x_bf16, bool dh_last_only) {
+  return lstm_split_applies(U, IN, dx, x_bf16, dh_last_only) ? lstm_split_grid(B) : lstm_fused_slabs(B, U, dx);
+}
 // fragment mode (frag = 1): h, a bf16 x and dh (unless dh_last_only) read fragment-native, dx written so;
 // instances for the stacked model's two layers (U 32 without dX from fp32 x, U 16 with dX from bf16 x)
 bool lstm_fused_frag_supported(int U, int IN, bool x_bf16, bool want_dx);

@@ -871,6 +871,9 @@ hipError_t lstm_fused_bwd_launch(const void* dh_bf16, const void* cseq_bf16, con
                                  int frag, hipStream_t stream) {
   if (frag && !lstm_fused_frag_supported(U, IN, x_bf16, dx != nullptr)) return hipErrorInvalidValue;
   if (U >= 64 && dz_scratch == nullptr) return hipErrorInvalidValue;   // lstm_fused_dz_bytes
+  if (lstm_split_applies(U, IN, dx != nullptr, x_bf16, dh_last_only != 0))   // two waves per tile (lstm_fused_split.hip)
+    return lstm_split_bwd_launch(dh_bf16, cseq_bf16, hseq_bf16, x, x_bf16, h0, c0, W, Uw, b, dh0, dc0, partials, B, T,
+                                 IN, act, dh_last_only, x_seq > 0 ? x_seq : (int64_t)T * IN, frag, stream);
   FusedBwdArgs a{(const __bf16*)dh_bf16, (const __bf16*)cseq_bf16, (const __bf16*)hseq_bf16, x, h0, c0, W, Uw, b, dx,
                  dh0, dc0, partials, B, T, IN, act, dh_last_only, x_seq > 0 ? x_seq : (int64_t)T * IN,
                  (__bf16*)dz_scratch, frag};

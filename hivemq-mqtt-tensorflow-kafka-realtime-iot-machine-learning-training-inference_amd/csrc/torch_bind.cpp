@@ -849,7 +849,7 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
     dc0 = at::empty({B, U}, opts);
   }
   const int S = sml::lstm_fused_slab((int)U, (int)IN);
-  const int G = sml::lstm_fused_slabs(B, (int)U, want_dx);
+  const int G = sml::lstm_fused_bwd_slabs(B, (int)U, (int)IN, want_dx, x.scalar_type() == at::kBFloat16, dh_last_only);
   const int* mp = grad_map(grad, map, S);
   auto partials = at::empty({G, S}, opts);   // every workgroup writes its slab (idle waves add nothing)
   auto out = mp ? *grad : at::empty({S}, opts);
@@ -1437,6 +1437,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_fused_frag_supported", &sml::lstm_fused_frag_supported,
         "whether lstm_fused_bwd(frag=True) has an instance for this layer", py::arg("U"), py::arg("IN"),
         py::arg("x_bf16"), py::arg("want_dx"));
+  m.def("lstm_split_applies", &sml::lstm_split_applies,
+        "whether lstm_fused_bwd runs this layer on the unit-block split kernel (two waves per tile)", py::arg("U"),
+        py::arg("IN"), py::arg("dx"), py::arg("x_bf16") = false, py::arg("dh_last_only") = false);
+  m.def("lstm_split_grid", &sml::lstm_split_grid, "workgroups (= weight-gradient slabs) of the split backward",
+        py::arg("B"));
   m.def("lstm_fused_bwd2", &lstm_fused_bwd2, "two stacked fused LSTM layers' backward (U 32 -> 16) in one launch",
         py::arg("x"), py::arg("h1"), py::arg("c1"), py::arg("h2"), py::arg("c2"), py::arg("dh2"), py::arg("W1"),
         py::arg("U1"), py::arg("b1"), py::arg("W2"), py::arg("U2"), py::arg("b2"), py::arg("act"),
