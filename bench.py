@@ -725,6 +725,12 @@ def main():
                      _bench_module("bench_fit").stream_dp, device, rank, world, rows_per_rank=args.stream_dp_rows,
                      batch=args.stream_dp_batch, collective=True)
         out.update({"stream_dp_rows_per_s": sdp.get("trained_rows_per_s"), "stream_dp": sdp})
+    # BASELINE config 3 under data parallelism: the two-layer seq-50 LSTM, every rank its own batch
+    if world > 1 and args.lstm_steps > 0:
+        ldp = ph.run("lstm_seq50_dp", 12, _bench_module("bench_lstm").measure_seq_dp, batch=65536, seq_len=50,
+                     steps=max(args.lstm_steps // 2, 5), warmup=3, device=device, settle_ms=args.settle_ms, rank=rank,
+                     world=world, collective=True)
+        out.update({"lstm_seq50_dp_windows_per_s": ldp.get("value"), "lstm_seq50_dp": ldp})
     ph.snapshot()
 
     # ---- rank 0 alone: every other rank parks on the rendezvous store (no GPU, no collective) ----
@@ -845,6 +851,7 @@ SUMMARY_FIELDS = (
     ("lstm_kafka_e2e_p99_us", ("lstm_kafka_e2e_p99_us",)),
     ("lstm_infer_p50_us", ("lstm_infer_p50_us",)),
     ("lstm_seq50_windows_per_s", ("lstm_seq50_windows_per_s",)),
+    ("lstm_seq50_dp_windows_per_s", ("lstm_seq50_dp_windows_per_s",)),
     ("lstm_seq50_infer_p50_us", ("lstm_seq50_infer_p50_us",)),
     ("lstm_seq50_infer_p99_us", ("lstm_seq50_infer_p99_us",)),
     ("lstm_ref_us_per_step", ("lstm_ref_us_per_step",)),

@@ -96,6 +96,66 @@ def measure_seq(batch: int = 65536, seq_len: int = 50, steps: int = 30, warmup: 
             "clock_settle": {"ms": settle_ms, "steps": settle_steps}}
 
 
+def measure_seq_dp(batch: int = 65536, seq_len: int = 50, steps: int = 10, warmup: int = 3, device=None,
+                   settle_ms: float = 100.0, rank: int = 0, world: int = 1) -> dict:
+    """BASELINE config 3 under data parallelism (weak scaling): every rank trains the two-layer stack on
+    its OWN ``batch`` windows per step (synthetic events seeded by rank), and the gradient of the
+    global batch is one flat fp32 bucket all-reduced per step (RCCL over xGMI on the 8-GPU node;
+    ``parallel.dp.allreduce_sum_``), after rank 0's initial parameters and Adam state are broadcast.
+    Collective: every rank calls it with the same arguments.  The elapsed time is the max over ranks;
+    the replicas' parameters are compared at the end (they must stay bit-identical)."""
+    import torch
+    from streamml.data.cardata import normalize_affine, synthetic_device_tensor
+    from streamml.data.stream import sliding_windows
+    from streamml.models.lstm import LSTMPredictor
+    from streamml.parallel import dp
+
+    dev = torch.device(device) if device is not None else torch.device("cuda", 0)
+    T, B = seq_len, batch
+    m = LSTMPredictor.two_layer(look_back=T, device=dev, seed=0)
+    dp.sync_model_from_rank0(m)
+    sc, sh = normalize_affine()
+    raw = synthetic_device_tensor(B * 2 + T + 1, dev, seed=1 + rank)
+    xn = raw * torch.tensor(sc, dtype=torch.float32, device=dev) + torch.tensor(sh, dtype=torch.float32, device=dev)
+    X, Y = sliding_windows(xn[:2 * B + T].contiguous(), T)
+    gb = B * world
+
+    def step(s):
+        i = s % 2
+        return m.train_step(X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B], global_batch=gb, allreduce=dp.allreduce_sum_)
+
+    settle_steps = 0
+    ts = time.perf_counter()
+    while True:   # clock settle, one decision for all ranks (collectives stay paired)
+        for _ in range(2):
+            step(settle_steps)
+            settle_steps += 1
+        torch.cuda.synchronize()
+        if dp.allreduce_max((time.perf_counter() - ts) * 1e3, dev) >= settle_ms:
+            break
+    for s in range(warmup):
+        step(s)
+    dp.barrier(dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        loss, _ = step(s)
+    torch.cuda.synchronize()
+    dp.barrier(dev)
+    el = dp.allreduce_max(time.perf_counter() - t0, dev)
+    flat = m.fp.flat.detach()
+    ref = flat.clone()
+    dp.broadcast_(ref, 0)
+    diverged = float((flat - ref).abs().max().item())
+    diverged = dp.allreduce_max(diverged, dev)
+    wps = gb * steps / el
+    return {"metric": "LSTM train windows/s (seq_len=%d, two_layer, data parallel)" % T, "value": wps,
+            "unit": "windows/s", "ms_per_step": el / steps * 1e3, "batch_per_rank": B, "global_batch": gb,
+            "world": world, "steps": steps, "scaling": "weak", "final_loss": float(loss),
+            "allreduce": "one flat fp32 gradient bucket per step (RCCL)", "replica_max_abs_diff": diverged,
+            "clock_settle": {"ms": settle_ms, "steps": settle_steps}}
+
+
 def measure_reference(batch: int = 1, epochs: int = 5, steps_per_epoch: int = 1000, autograd_steps: int = 300,
                       device=None) -> dict:
     """cardata-v2.py:172-209 as the reference runs it: look_back 1, batch 1, 1 000 steps x

@@ -218,7 +218,8 @@ int Feed::pop(int& slab, int64_t& rows, int timeout_ms) {
   std::unique_lock<std::mutex> g(mu_);
   auto ready = [&] { return !ready_.empty() || live_workers_ == 0 || !error_.empty(); };
   if (timeout_ms < 0) cv_ready_.wait(g, ready);
-  else cv_ready_.wait_for(g, std::chrono::milliseconds(timeout_ms), ready);
+  else   // system_clock deadline (pthread_cond_timedwait; see kafka.cpp retention_loop)
+    cv_ready_.wait_until(g, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms), ready);
   if (!error_.empty()) throw std::runtime_error(error_);
   if (!ready_.empty()) {
     slab = ready_.front().first;

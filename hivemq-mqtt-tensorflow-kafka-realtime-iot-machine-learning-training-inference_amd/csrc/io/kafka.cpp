@@ -1003,7 +1003,10 @@ static int64_t steady_ms() {
 void Broker::retention_loop() {
   std::unique_lock<std::mutex> g(mu_);
   while (running_) {
-    retention_cv_.wait_for(g, std::chrono::milliseconds(std::max(cfg_.retention_check_ms, 10)));
+    // system_clock: wait_for maps to pthread_cond_clockwait, which the ThreadSanitizer runtime here
+    // does not model (it then reports the broker mutex as double-locked; mqtt.cpp wait_ms)
+    retention_cv_.wait_until(g, std::chrono::system_clock::now() +
+                                    std::chrono::milliseconds(std::max(cfg_.retention_check_ms, 10)));
     if (!running_) break;
     std::vector<std::shared_ptr<const std::string>> dead;
     enforce_locked(steady_ms(), dead);

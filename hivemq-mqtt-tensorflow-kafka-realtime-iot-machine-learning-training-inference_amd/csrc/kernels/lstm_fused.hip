@@ -120,7 +120,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   __shared__ __attribute__((aligned(16))) bf16x4 wfl[KT * MT * 64];
   __shared__ __attribute__((aligned(16))) float sbias[G4];
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int w = threadIdx.x >> 6;
+  // wave-uniform (SGPR) wave index: the per-step operand addresses below are an SGPR base plus a
+  // per-lane 32-bit offset fixed for the tile (global_load saddr form) instead of 64-bit VGPR
+  // pointers advanced per step (~12 v_lshl_add_u64 per step and their registers, profiles/r06)
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // Persistent grid (lstm_fused_slabs): workgroup blockIdx.x takes 4-wave groups of 16-sequence
   // tiles blockIdx.x, + gridDim.x, ... -- the weight fragments are staged once per workgroup
   // and the weight gradients of all its tiles land in ONE slab (4x fewer slab bytes written
@@ -220,40 +223,69 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     bf16x4 hp[UB];     // h_{t-1}[sequence c][unit 16b + 4g + i]
     XR xt[KT];         // x_t[sequence c][feature 16kt + 4g + j]
   };
-  const __bf16* cw = a.cseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
   __bf16* dzw = DZS ? a.dzs + wave_id * T * (int64_t)(MT * 256) + lane * 4 : nullptr;
   constexpr bool XFR = FR && std::is_same_v<XT, __bf16>;   // x is a fragment-native h sequence
-  // fragment-mode bases of this tile (h / dh with UB tiles per step, x / dx with KT)
-  const __bf16* hfw = a.hseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
-  const __bf16* dhfw = a.dh + wave_id * T * (int64_t)(UB * 256) + lane * 4;
-  const __bf16* xfw = static_cast<const __bf16*>(a.x) + wave_id * T * (int64_t)(KT * 256) + lane * 4;
+  // Per-lane byte offsets of the tile, fixed over its steps (the uniform parts are added per access):
+  // cl = this lane's row of the tile, clamped into B (padding lanes read row B - 1).
+  int cl = 0;
+  int xo[KT][4];
+  constexpr int XS = sizeof(XT);
+  const unsigned lo8 = lane * 8;   // fragment-native: lane's 8 bytes of a 512-byte tile
+  auto ld8 = [&](const void* base, int64_t uoff, unsigned loff) {   // uniform base + offset, lane offset
+    return *reinterpret_cast<const bf16x4*>(static_cast<const char*>(base) + uoff + loff);
+  };
   // Loads are unconditional from in-bounds addresses (padding lanes read row B-1),
   // with zeros selected afterwards: no exec-masked branches and no waits in the loop.
   auto load_common = [&](int t, Step& st) {   // raw values; masks are applied in step()
     if (FR && !a.dh_last_only) {
 #pragma unroll
-      for (int b = 0; b < UB; ++b) st.dho[b] = ld_bf16x4(dhfw + (int64_t)t * (UB * 256) + b * 256);
-    } else {
-      const __bf16* dhp = a.dh_last_only ? a.dh + sq * U : a.dh + (sq * T + t) * (int64_t)U;
+      for (int b = 0; b < UB; ++b) st.dho[b] = ld8(a.dh, ((wave_id * T + t) * UB + b) * 512, lo8);
+    } else if (a.dh_last_only) {
 #pragma unroll
-      for (int b = 0; b < UB; ++b) st.dho[b] = ld_bf16x4(dhp + 16 * b + 4 * g);
+      for (int b = 0; b < UB; ++b) st.dho[b] = ld8(a.dh, s0 * (U * 2), (cl * U + 16 * b + 4 * g) * 2);
+    } else {
+#pragma unroll
+      for (int b = 0; b < UB; ++b) st.dho[b] = ld8(a.dh, (s0 * T + t) * (int64_t)(U * 2), (cl * T * U + 16 * b + 4 * g) * 2);
     }
     if constexpr (XFR) {
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt) st.xt[kt] = ld_bf16x4(xfw + (int64_t)t * (KT * 256) + kt * 256);
+      for (int kt = 0; kt < KT; ++kt) st.xt[kt] = ld8(a.x, ((wave_id * T + t) * KT + kt) * 512, lo8);
     } else {
-      const XT* p = static_cast<const XT*>(a.x) + sq * a.x_seq + (int64_t)t * IN;
+      const char* xt0 = static_cast<const char*>(a.x) + (s0 * a.x_seq + (int64_t)t * IN) * XS;   // uniform
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt) st.xt[kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN);
+      for (int kt = 0; kt < KT; ++kt) {
+        if constexpr (std::is_same_v<XT, float>) {
+          if constexpr (XV == 4) {
+            st.xt[kt] = *reinterpret_cast<const f32x4*>(xt0 + xo[kt][0]);
+          } else if constexpr (XV == 2) {
+            const f32x2_t lo = *reinterpret_cast<const f32x2_t*>(xt0 + xo[kt][0]);
+            const f32x2_t hi = *reinterpret_cast<const f32x2_t*>(xt0 + xo[kt][2]);
+            st.xt[kt] = XR{lo[0], lo[1], hi[0], hi[1]};
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) st.xt[kt][j] = *reinterpret_cast<const float*>(xt0 + xo[kt][j]);
+          }
+        } else {
+          if constexpr (XV == 4) {
+            st.xt[kt] = *reinterpret_cast<const bf16x4*>(xt0 + xo[kt][0]);
+          } else if constexpr (XV == 2) {
+            const s16x2_t lo = *reinterpret_cast<const s16x2_t*>(xt0 + xo[kt][0]);
+            const s16x2_t hi = *reinterpret_cast<const s16x2_t*>(xt0 + xo[kt][2]);
+            st.xt[kt] = XR{lo[0], lo[1], hi[0], hi[1]};
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) st.xt[kt][j] = *reinterpret_cast<const short*>(xt0 + xo[kt][j]);
+          }
+        }
+      }
     }
   };
   auto load_step = [&](int t, Step& st) {   // t >= 1
-    const __bf16* cp = cw + (int64_t)(t - 1) * (UB * 256);
-    const __bf16* hrow = a.hseq + (sq * T + t - 1) * (int64_t)U;
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
-      st.cprev[b] = ld_bf16x4(cp + b * 256);
-      st.hp[b] = FR ? ld_bf16x4(hfw + (int64_t)(t - 1) * (UB * 256) + b * 256) : ld_bf16x4(hrow + 16 * b + 4 * g);
+      st.cprev[b] = ld8(a.cseq, ((wave_id * T + t - 1) * UB + b) * 512, lo8);
+      st.hp[b] = FR ? ld8(a.hseq, ((wave_id * T + t - 1) * UB + b) * 512, lo8)
+                    : ld8(a.hseq, (s0 * T + t - 1) * (int64_t)(U * 2), (cl * T * U + 16 * b + 4 * g) * 2);
     }
     load_common(t, st);
   };
@@ -476,19 +508,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   seq = s0 + c;
   valid = seq < a.B;
   sq = valid ? seq : a.B - 1;
-  cw = a.cseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
+  cl = (int)(sq - s0);
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // clamped in-row columns, as load_row4 (the operand masks the ones past IN)
+      const int k0 = 16 * kt + 4 * g + (XV == 2 ? (j & 2) : (XV == 4 ? 0 : j));
+      xo[kt][j] = (int)((cl * a.x_seq + (k0 < IN ? k0 : 0)) * XS);
+    }
   if constexpr (DZS) dzw = a.dzs + wave_id * T * (int64_t)(MT * 256) + lane * 4;
-  if constexpr (FR) {
-    hfw = a.hseq + wave_id * T * (int64_t)(UB * 256) + lane * 4;
-    dhfw = a.dh + wave_id * T * (int64_t)(UB * 256) + lane * 4;
-    xfw = static_cast<const __bf16*>(a.x) + wave_id * T * (int64_t)(KT * 256) + lane * 4;
-  }
   any_active |= active;
   // fresh recurrence and weight-gradient pipeline per tile (the accumulators carry on)
 #pragma unroll
   for (int b = 0; b < UB; ++b) {
     dhr[b] = dcn[b] = zero4;
-    ctc[b] = active ? unpack4(ld_bf16x4(cw + (int64_t)(T - 1) * (UB * 256) + b * 256)) : zero4;
+    ctc[b] = active ? unpack4(ld8(a.cseq, ((wave_id * T + T - 1) * UB + b) * 512, lo8)) : zero4;
   }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) pdz[mt] = pack4(zero4);

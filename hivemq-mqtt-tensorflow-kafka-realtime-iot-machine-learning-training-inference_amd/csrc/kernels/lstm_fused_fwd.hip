@@ -300,9 +300,11 @@ __device__ __forceinline__ void gate_preacts_lx(const s16x8* lx, int ol, const b
 // rounding; z clamped at -20 so the product cannot overflow), 4 = x operand without the column mask /
 // bias-column OR; 8 = h stored fragment-native (512 contiguous bytes per wave and tile, as c) instead
 // of [B, T, U] rows; 16 / 32 = h / c not stored (upper bounds of the store cost).
+// ht / ct: wave-uniform bases of the step's h / c stores, hoff / coff: this lane's byte offsets (the
+// stores take the global_store saddr form: no 64-bit per-lane pointers carried through the time loop)
 template <int U, int ACT, int PROBE>
 __device__ __forceinline__ void cell_update_p(const f32x4 (&z)[4 * U / 16], f32x4 (&h)[U / 16], f32x4 (&cs)[U / 16],
-                                              bf16x4 (&hb)[U / 16], __bf16* ht, __bf16* ct) {
+                                              bf16x4 (&hb)[U / 16], char* ht, unsigned hoff, char* ct, unsigned coff) {
   constexpr int UB = U / 16;
 #pragma unroll
   for (int b = 0; b < UB; ++b) {
@@ -332,8 +334,8 @@ __device__ __forceinline__ void cell_update_p(const f32x4 (&z)[4 * U / 16], f32x
       h[b][i] = go * act_f(ACT, cs[b][i]);
     }
     hb[b] = pack4(h[b]);
-    if constexpr (!(PROBE & 32)) *reinterpret_cast<bf16x4*>(ct + b * 256) = pack4(cs[b]);
-    if constexpr (!(PROBE & 16)) *reinterpret_cast<bf16x4*>(ht + ((PROBE & 8) ? b * 256 : 16 * b)) = hb[b];
+    if constexpr (!(PROBE & 32)) *reinterpret_cast<bf16x4*>(ct + coff + b * 512) = pack4(cs[b]);
+    if constexpr (!(PROBE & 16)) *reinterpret_cast<bf16x4*>(ht + hoff + ((PROBE & 8) ? b * 512 : 32 * b)) = hb[b];
   }
 }
 
@@ -370,7 +372,8 @@ template <int U1, int KT1, int XV, int ACT1, bool BX1, int U2, int ACT2, int PF 
 __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd2_kernel(FusedFwd2Args a) {
   constexpr int MT1 = 4 * U1 / 16, UB1 = U1 / 16, MT2 = 4 * U2 / 16, UB2 = U2 / 16, KT2 = UB1;
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int64_t wv0 = ((int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * NT;   // first 16-sequence tile
+  // wave-uniform (SGPR) tile index: every per-step address is an SGPR base plus a per-lane 32-bit offset
+  const int64_t wv0 = ((int64_t)blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * NT;
   const int IN1 = a.IN1, T = a.T;
   // NT = 2: the x-side A fragments of both layers live in LDS (shared by the workgroup's waves)
   constexpr bool LX = NT > 1;
@@ -396,8 +399,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd2_kernel(FusedFwd
   for (int kt = 0; kt < KT1; ++kt) onex[kt] = BX1 ? ones_at_bias(kt, g, IN1) : bf16x4{0, 0, 0, 0};
   f32x4 h1[NT][UB1], c1[NT][UB1], h2[NT][UB2], c2[NT][UB2];
   bf16x4 hb1[NT][UB1], hb2[NT][UB2];
-  const float* xrow[NT];
-  __bf16 *hw1[NT], *hw2[NT], *cw1[NT], *cw2[NT], *hf1[NT], *hf2[NT];
+  int xo[NT][KT1][4];   // per-lane byte offsets of the x row pieces (tile row 0, step 0 = the uniform base)
 #pragma unroll
   for (int k = 0; k < NT; ++k) {
 #pragma unroll
@@ -414,23 +416,45 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd2_kernel(FusedFwd
     // buffers' padding (allocated to whole waves of NT tiles)
     const int64_t wv = wv0 + k;
     const int64_t seq = wv * 16 + c;
-    const int64_t sq = seq < a.B ? seq : a.B - 1;
+    const int cl = seq < a.B ? c : (int)(a.B - 1 - wv * 16);   // rows past B read row B - 1 (< 0: idle tile)
     SML_DCHECK(seq < (a.B + 16 * NT - 1) / (16 * NT) * (16 * NT));
-    xrow[k] = a.x + sq * a.x_seq;
-    hw1[k] = a.hseq1 + seq * T * (int64_t)U1 + 4 * g;
-    hw2[k] = a.hseq2 + seq * T * (int64_t)U2 + 4 * g;
-    cw1[k] = a.cseq1 + wv * T * (int64_t)(UB1 * 256) + lane * 4;
-    cw2[k] = a.cseq2 + wv * T * (int64_t)(UB2 * 256) + lane * 4;
-    hf1[k] = a.hseq1 + wv * T * (int64_t)(UB1 * 256) + lane * 4;
-    hf2[k] = a.hseq2 + wv * T * (int64_t)(UB2 * 256) + lane * 4;
+#pragma unroll
+    for (int kt = 0; kt < KT1; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {   // clamped in-row columns, as load_row4
+        const int k0 = 16 * kt + 4 * g + (XV == 2 ? (j & 2) : (XV == 4 ? 0 : j));
+        xo[k][kt][j] = (int)((cl * a.x_seq + (k0 < IN1 ? k0 : 0)) * 4);
+      }
   }
+  // byte offsets of this lane in the h / c stores: fragment-native 8 bytes per lane, rows 2 x (T U) per
+  // sequence + 8 per unit group
+  const unsigned fo = lane * 8, ro1 = (c * T * U1 + 4 * g) * 2, ro2 = (c * T * U2 + 4 * g) * 2;
+  auto tile_row = [&](int k) { return (wv0 + k) * 16; };   // uniform
   auto load_x = [&](int t, f32x4 (*v)[KT1]) {
 #pragma unroll
     for (int k = 0; k < NT; ++k) {
-      const float* p = xrow[k] + (int64_t)t * IN1;
+      const char* x0 = reinterpret_cast<const char*>(a.x) + (tile_row(k) * a.x_seq + (int64_t)t * IN1) * 4;
 #pragma unroll
-      for (int kt = 0; kt < KT1; ++kt) v[k][kt] = load_row4<XV>(p, 16 * kt + 4 * g, IN1);
+      for (int kt = 0; kt < KT1; ++kt) {
+        if constexpr (XV == 4) {
+          v[k][kt] = *reinterpret_cast<const f32x4*>(x0 + xo[k][kt][0]);
+        } else if constexpr (XV == 2) {
+          const f32x2_t lo = *reinterpret_cast<const f32x2_t*>(x0 + xo[k][kt][0]);
+          const f32x2_t hi = *reinterpret_cast<const f32x2_t*>(x0 + xo[k][kt][2]);
+          v[k][kt] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[k][kt][j] = *reinterpret_cast<const float*>(x0 + xo[k][kt][j]);
+        }
+      }
     }
+  };
+  // step t's store bases (uniform): c fragment-native; h fragment-native (HF / PROBE 8) or rows
+  auto cbase = [&](__bf16* base, int k, int t, int ub) {
+    return reinterpret_cast<char*>(base) + ((wv0 + k) * T + t) * (int64_t)(ub * 512);
+  };
+  auto hbase = [&](__bf16* base, int k, int t, int u, int ub, bool frag) {
+    return frag ? cbase(base, k, t, ub) : reinterpret_cast<char*>(base) + (tile_row(k) * T + t) * (int64_t)(u * 2);
   };
   f32x4 xr[PF][NT][KT1];
 #pragma unroll
@@ -456,12 +480,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd2_kernel(FusedFwd
       if constexpr (LX) gate_preacts_lx<MT1, UB1, BX1>(lx1, ol, ut1, bias1, xb[k], hb1[k], z1[k]);
       else gate_preacts<MT1, KT1, UB1, BX1>(wt1, ut1, bias1, xb[k], hb1[k], z1[k]);
     }
+    constexpr bool HFR = (PROBE & 8) || HF;
 #pragma unroll
     for (int k = 0; k < NT; ++k)
-      cell_update_p<U1, ACT1, PROBE | (HF ? 8 : 0)>(
-          z1[k], h1[k], c1[k], hb1[k],
-          ((PROBE & 8) || HF) ? hf1[k] + (int64_t)t * (UB1 * 256) : hw1[k] + (int64_t)t * U1,
-          cw1[k] + (int64_t)t * (UB1 * 256));
+      cell_update_p<U1, ACT1, PROBE | (HF ? 8 : 0)>(z1[k], h1[k], c1[k], hb1[k], hbase(a.hseq1, k, t, U1, UB1, HFR),
+                                                     HFR ? fo : ro1, cbase(a.cseq1, k, t, UB1), fo);
     // layer 2: x_t = layer 1's h_t, already the B operand (hb1)
     f32x4 z2[NT][MT2];
 #pragma unroll
@@ -471,10 +494,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd2_kernel(FusedFwd
     }
 #pragma unroll
     for (int k = 0; k < NT; ++k)
-      cell_update_p<U2, ACT2, PROBE | (HF ? 8 : 0)>(
-          z2[k], h2[k], c2[k], hb2[k],
-          ((PROBE & 8) || HF) ? hf2[k] + (int64_t)t * (UB2 * 256) : hw2[k] + (int64_t)t * U2,
-          cw2[k] + (int64_t)t * (UB2 * 256));
+      cell_update_p<U2, ACT2, PROBE | (HF ? 8 : 0)>(z2[k], h2[k], c2[k], hb2[k], hbase(a.hseq2, k, t, U2, UB2, HFR),
+                                                     HFR ? fo : ro2, cbase(a.cseq2, k, t, UB2), fo);
   };
   int t0 = 0;
   for (; t0 + PF <= T; t0 += PF) {

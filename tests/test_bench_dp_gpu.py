@@ -117,9 +117,12 @@ def test_bench_n_ranks_rehearsal(tmp_path, cuda_device, n):
     for k in ("infer", "small_allreduce", "keras_batch32_dp", "kafka_e2e", "lstm_kafka_e2e", "keras_batch32",
               "fit_large_batch",
               "fresh_rows", "fit_batch100", "stream_e2e", "stream_large_batch", "lstm_seq50", "lstm_ref",
-              "lstm_infer", "mqtt_e2e", "stream_dp",
+              "lstm_infer", "mqtt_e2e", "stream_dp", "lstm_seq50_dp",
               "total_wall"):
         assert k in ph, (k, ph, out["budget"])
+    ldp = out["lstm_seq50_dp"]   # config 3 under DP: every rank its own 65 536 windows, one bucket per step
+    assert ldp.get("replica_max_abs_diff") == 0.0 and ldp["global_batch"] == n * 65536, ldp
+    assert out["summary"]["lstm_seq50_dp_windows_per_s"] > 0
     assert not out["budget"]["skipped"], out["budget"]
     assert out["mqtt_connections"] == 2000 and out["mqtt_dropped"] == 0, out["mqtt_e2e"]
     _check_stream_dp(out, n)

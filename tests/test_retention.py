@@ -90,6 +90,10 @@ def test_offset_reset_policy_aliases():
 
 
 def test_connection_threads_are_reaped():
+    import os
+    # relative to the process's own threads at the start (torch / OpenMP pools of earlier tests
+    # in the same pytest process vary with the machine)
+    base = len(os.listdir(f"/proc/{os.getpid()}/task"))
     b = FakeBroker()
     try:
         b.create_topic("t", 1)
@@ -101,10 +105,10 @@ def test_connection_threads_are_reaped():
         gc.collect()
         time.sleep(0.2)
         KafkaClient(b.address).partitions()            # an accept reaps the finished threads
-        import threading  # noqa: F401 - the broker's threads are native; count them via /proc
-        import os
-        n = len(os.listdir(f"/proc/{os.getpid()}/task"))
-        assert n < 40, n
+        # the broker's threads are native; count them via /proc: the 50 finished connections'
+        # threads are gone, the broker's own few remain
+        n = len(os.listdir(f"/proc/{os.getpid()}/task")) - base
+        assert n < 25, (n, base)
     finally:
         b.stop()
 
