@@ -107,11 +107,15 @@ def seed_group_offsets(client, topic: str, base: str, group: str, partitions, ma
     """Rescaled serving: the consumer group of a replica that shares partitions is tied to the
     replica count (``<base>.<rank>-of-<world>``), so after a rescale it starts with no committed
     positions.  For every partition the group has no commit for, seed it with the MINIMUM position
-    committed by the base group or any ``<base>.<r>-of-<w>`` group (w <= ``max_world``): at-least-
-    once -- records between that minimum and another replica's position are scored again, none
-    is skipped.  Returns {partition: seeded offset}."""
+    committed by the base group or any ``<base>.<r>-of-<w>`` group of ANOTHER replica count
+    (w <= ``max_world``): at-least-once -- records between that minimum and another replica's
+    position are scored again, none is skipped.  The sibling groups of the current
+    count are not candidates: each tracks only ITS key share of a shared partition, so a sibling
+    that already ran would otherwise make this replica skip its own share.
+    Returns {partition: seeded offset}."""
     seeded = {}
-    cands = [base] + [f"{base}.{r}-of-{w}" for w in range(2, max_world + 1) for r in range(w)]
+    cur = group.rsplit("-of-", 1)[1] if "-of-" in group else None
+    cands = [base] + [f"{base}.{r}-of-{w}" for w in range(2, max_world + 1) for r in range(w) if str(w) != cur]
     for p in partitions:
         if client.committed(group, topic, p) >= 0:
             continue

@@ -206,5 +206,8 @@ def test_rescaled_serving_groups_seeded_from_previous_commits():
         assert c.committed("g.2-of-3", "s", 1) == 650 and c.committed("g.2-of-3", "s", 2) < 0
         c.commit("g.2-of-3", "s", 1, 800)       # an existing commit is never overwritten
         assert seed_group_offsets(c, "s", "g", "g.2-of-3", [1]) == {}
+        # a sibling of the same replica count owns another key share: never a seed
+        c.commit("g.0-of-3", "s", 2, 500)
+        assert seed_group_offsets(c, "s", "g", "g.1-of-3", [2]) == {}
     finally:
         b.stop()
