@@ -130,6 +130,13 @@ hipError_t lstm_split_bwd_launch(const void* dh, const void* cseq, const void* h
 inline int lstm_fused_bwd_slabs(int64_t B, int U, int IN, bool dx, bool x_bf16, bool dh_last_only) {
   return lstm_split_applies(U, IN, dx, x_bf16, dh_last_only) ? lstm_split_grid(B) : lstm_fused_slabs(B, U, dx);
 }
+// fused Dense head of the LSTM predictor (lstm_head.hip): forward, MSE + accuracy, dW / db (scattered
+// into grad through the dense slab map) and dh = dy . W^T (bf16 [n, 16]) in one pass + one fold launch;
+// h [n, 16] bf16 rows (stride ldh), W [16, N], N <= 32; part holds lstm_head_partials(n, N) floats
+int lstm_head_partials(int64_t n, int N);
+hipError_t lstm_head_launch(const void* h, int64_t ldh, const float* W, const float* b, const float* y, int64_t ldy,
+                            void* dh, int64_t n, int N, float gscale, float* part, float* grad, const int* map,
+                            float* acc, float* out, float div0, float div1, int64_t* counter, hipStream_t st);
 // fragment mode (frag = 1): h, a bf16 x and dh (unless dh_last_only) read fragment-native, dx written so;
 // instances for the stacked model's two layers (U 32 without dX from fp32 x, U 16 with dX from bf16 x)
 bool lstm_fused_frag_supported(int U, int IN, bool x_bf16, bool want_dx);

@@ -1035,6 +1035,42 @@ at::Tensor lstm_ref_train(const at::Tensor& flat, const at::Tensor& m, const at:
   return out;
 }
 
+// Fused LSTM Dense head (lstm_head.hip): returns dh = dy . W^T as bf16 [n, 16]; dW / db into grad
+// through map (the dense_wgrad slab layout), this step's [sum sq err, #correct] into acc, out =
+// acc / div, counter + 1.
+at::Tensor lstm_head(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b, const at::Tensor& y,
+                     double gscale, const at::Tensor& grad, const at::Tensor& map, const at::Tensor& acc,
+                     const c10::optional<at::Tensor>& out, double div0, double div1,
+                     const c10::optional<at::Tensor>& counter) {
+  check_dev(h, "h", at::kBFloat16);
+  check_dev(W, "W", at::kFloat);
+  check_dev(b, "b", at::kFloat);
+  check_dev(y, "y", at::kFloat);
+  check_dev(acc, "acc", at::kFloat);
+  TORCH_CHECK(h.dim() == 2 && h.size(1) == 16 && h.stride(1) == 1, "h must be [n, 16] bf16 rows");
+  const int64_t n = h.size(0), N = W.size(1);
+  TORCH_CHECK(W.is_contiguous() && W.size(0) == 16 && N >= 1 && N <= 32, "W must be [16, N <= 32]");
+  TORCH_CHECK(b.is_contiguous() && b.numel() == N, "b must be [N]");
+  TORCH_CHECK(y.dim() == 2 && y.size(0) == n && y.size(1) == N && y.stride(1) == 1, "y must be [n, N] rows");
+  TORCH_CHECK(acc.numel() >= 2, "acc needs 2 floats");
+  const int S = sml::dense_wgrad_slab(16, (int)N);
+  const int* mp = grad_map(grad, map, S);
+  if (out.has_value()) {
+    check_dev(*out, "out", at::kFloat);
+    TORCH_CHECK(out->numel() >= 2 && out->is_contiguous(), "out needs 2 contiguous floats");
+  }
+  if (counter.has_value()) check_dev(*counter, "counter", at::kLong);
+  c10::hip::HIPGuard guard(h.device().index());
+  auto dh = at::empty({n, 16}, h.options());
+  auto part = at::empty({sml::lstm_head_partials(n, (int)N)}, h.options().dtype(at::kFloat));
+  SML_CHECK_HIP(sml::lstm_head_launch(h.data_ptr(), h.stride(0), W.data_ptr<float>(), b.data_ptr<float>(),
+                                      y.data_ptr<float>(), y.stride(0), dh.data_ptr(), n, (int)N, (float)gscale,
+                                      part.data_ptr<float>(), grad.data_ptr<float>(), mp, acc.data_ptr<float>(),
+                                      opt_mut(out), (float)div0, (float)div1,
+                                      counter.has_value() ? counter->data_ptr<int64_t>() : nullptr, cur_stream(h)));
+  return dh;
+}
+
 // K3 + K6: (y_pred - y) * gscale -> grad, [sum sq err, #correct rows] += into acc.
 void mse_acc(const at::Tensor& yp, const at::Tensor& y, int64_t bcast, double gscale,
              const c10::optional<at::Tensor>& grad, const c10::optional<at::Tensor>& acc, bool reset,
@@ -1500,6 +1536,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         static_cast<sml::LSTMServe*>(p.s.get())->reset_keys();
       })
       .def_property_readonly("nkeys", [](LSTMServePy& p) { return p.nk; });
+  m.def("lstm_head", &lstm_head, "fused LSTM Dense head: forward, MSE + accuracy, dW / db, dh (one pass + fold)",
+        py::arg("h"), py::arg("W"), py::arg("b"), py::arg("y"), py::arg("gscale"), py::arg("grad"), py::arg("map"),
+        py::arg("acc"), py::arg("out") = py::none(), py::arg("div0") = 1.0, py::arg("div1") = 1.0,
+        py::arg("counter") = py::none());
   m.def("mse_acc", &mse_acc, "fused MSE fwd/bwd + categorical accuracy (K3 + K6)", py::arg("y_pred"), py::arg("y"),
         py::arg("bcast") = 1, py::arg("gscale") = 1.0, py::arg("grad") = py::none(), py::arg("acc") = py::none(),
         py::arg("reset") = false, py::arg("out") = py::none(), py::arg("div0") = 1.0, py::arg("div1") = 1.0,

@@ -64,6 +64,15 @@ def _fwd2() -> bool:
     return os.environ.get("SML_LSTM_FWD2", "1") != "0"
 
 
+def _headfuse() -> bool:
+    """SML_LSTM_HEADFUSE=0: the Dense head as six per-kernel launches (K1 forward, mse_acc + fold, K2
+    weight gradient + slab sum, K1 for dh) instead of the fused head (lstm_head.hip: one pass over the
+    rows + one fold launch; A/B, read per step).  The per-kernel path rounds exactly as the autograd
+    path does (tests/test_lstm_gpu.py test_fused_step_matches_autograd_step pins it); the fused
+    head sums in another order."""
+    return os.environ.get("SML_LSTM_HEADFUSE", "1") != "0"
+
+
 def _frag() -> bool:
     """SML_LSTM_FRAG=0: the stacked two-layer step keeps h1 / h2 / dX as [B, T, U] rows instead of the
     fragment-native layout (A/B; read per step).  Fragment-native, every per-step h / dh / x access of
@@ -302,19 +311,26 @@ class LSTMPredictor:
         hd = plan["head"]
         K, bh = (t.detach() for t in P[hd["params"]:hd["params"] + 2])
         hin = h.reshape(n * R, h.shape[-1]) if R else (hlast if frag else h[:, -1])   # bf16, in place when h_T
-        y_pred = C.dense_fwd(hin, K, bh, 0, False, 1024, False)
         yt = y.to(device=self.device, dtype=torch.float32).contiguous()
         acc = plan["acc"]
-        dy = torch.empty_like(y_pred)
         scale = n / float(global_batch or n)           # mean over the global batch under DP
         # this step's (loss, accuracy) and the Adam step count come out of the loss kernel's fold
         # launch (SML_LSTM_FOLD=0: a division, a copy and a counter add on the stream instead)
         fold = _FOLD
         metrics = torch.empty(2, device=self.device) if fold else None
-        C.mse_acc(y_pred, yt, R or 1, 2.0 / y_pred.numel() * scale, dy, acc, reset=True,   # acc = this step's sums
-                  out=metrics, div0=float(y_pred.numel()), div1=float(R or 1), counter=self.fp.iter if fold else None)
-        C.dense_wgrad(hin, dy, 0, True, 1024, grad, plan["head_map"])
-        dh = C.dense_fwd(dy, K, None, 0, True, 1024, True)   # dh = dy . K^T, bf16
+        n_out = hin.shape[0] * K.shape[1]
+        if not R and _headfuse() and K.shape[0] == 16 and K.shape[1] <= 32:
+            # the Dense head in one pass (lstm_head.hip): forward, MSE + accuracy, dW / db into the flat
+            # gradient, dh = dy . K^T -- 2 launches where the per-kernel path below takes 6
+            dh = C.lstm_head(hin, K, bh, yt, 2.0 / n_out * scale, grad, plan["head_map"], acc, out=metrics,
+                             div0=float(n_out), div1=1.0, counter=self.fp.iter if fold else None)
+        else:
+            y_pred = C.dense_fwd(hin, K, bh, 0, False, 1024, False)
+            dy = torch.empty_like(y_pred)
+            C.mse_acc(y_pred, yt, R or 1, 2.0 / n_out * scale, dy, acc, reset=True,   # acc = this step's sums
+                      out=metrics, div0=float(n_out), div1=float(R or 1), counter=self.fp.iter if fold else None)
+            C.dense_wgrad(hin, dy, 0, True, 1024, grad, plan["head_map"])
+            dh = C.dense_fwd(dy, K, None, 0, True, 1024, True)   # dh = dy . K^T, bf16
         layers = pre + post
         for i in range(len(layers) - 1, -1, -1):
             L = layers[i]
@@ -343,8 +359,11 @@ class LSTMPredictor:
         self.opt.step(allreduce=allreduce, counted=fold)
         if fold:
             return metrics[0], metrics[1]   # acc is overwritten by the next step, metrics is this step's own
-        correct = acc[1] / float(R) if R else acc[1].clone()
-        return acc[0] / y_pred.numel(), correct
+        # device-tensor divisors: an IEEE division, as the fold launch's (a Python-scalar divisor is a
+        # reciprocal multiply in torch's kernel, which can differ in the last bit)
+        div = torch.tensor([float(n_out), float(R or 1)], device=self.device)
+        correct = acc[1] / div[1] if R else acc[1].clone()
+        return acc[0] / div[0], correct
 
     # ------------------------------------------------------------------ training
     def fit(self, x, y=None, epochs: int = 1, batch_size: int = 1, verbose: int = 1, take: Optional[int] = None,

@@ -135,6 +135,7 @@ def test_fused_step_matches_autograd_step(cuda_device, monkeypatch, stack, B, T)
     autograd path runs them; the stacked backward is checked against them in
     test_stacked_backward_vs_two_launches.)"""
     monkeypatch.setenv("SML_LSTM_BWD2", "0")
+    monkeypatch.setenv("SML_LSTM_HEADFUSE", "0")   # the per-kernel head: the autograd path's rounding
     from streamml.data.stream import sliding_windows
     rows = torch.tensor(np.random.default_rng(B + T).uniform(-1, 1, (3 * B + T, 18)), dtype=torch.float32,
                         device=cuda_device)
@@ -507,3 +508,32 @@ def test_lstm_predictor_custom_widths_trains_on_gpu(cuda_device):
     assert _relerr(mg.predict(xs[:32]), mc.predict(xs[:32])) < 3e-2
     h = mg.fit(xs, ys, epochs=4, batch_size=64, verbose=0)
     assert h.history["loss"][-1] < h.history["loss"][0]
+
+
+@pytest.mark.parametrize("B,T,frag", [(65536 + 37, 6, True), (1000, 50, True), (100, 7, False), (33, 5, True)])
+def test_fused_head_matches_per_kernel_head(cuda_device, monkeypatch, B, T, frag):
+    """The fused Dense head (lstm_head.hip: forward, MSE + accuracy, dW / db, dh in one pass + one fold)
+    against the six per-kernel launches it replaces, over 3 train steps of the two-layer stack: the
+    same loss and accuracy, and every gradient and updated parameter to summation-order rounding
+    (the fused head contracts over rows per 16-row tile and folds workgroup partials in order)."""
+    from streamml.data.stream import sliding_windows
+    monkeypatch.setenv("SML_LSTM_FRAG", "1" if frag else "0")
+    rows = torch.tensor(np.random.default_rng(B + T).uniform(-1, 1, (3 * B + T, 18)), dtype=torch.float32,
+                        device=cuda_device)
+    X, Y = sliding_windows(rows, T)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SML_LSTM_HEADFUSE", v)
+        m = LSTMPredictor.two_layer(look_back=T, device=cuda_device, seed=6)
+        res = []
+        for s in range(3):
+            sl = slice(s * B, (s + 1) * B)
+            loss, corr = m.train_step(X[sl], Y[sl])
+            res.append((float(loss), float(corr), m.fp.grad.detach().clone()))
+        out[v] = (res, m.fp.flat.detach().clone(), int(m.fp.iter.item()))
+    for (lf, cf, gf), (lu, cu, gu) in zip(out["1"][0], out["0"][0]):
+        assert abs(lf - lu) <= 1e-5 * abs(lu), (lf, lu)
+        assert abs(cf - cu) <= 2, (cf, cu)   # a row whose two largest outputs tie within rounding may flip
+        assert _relerr(gf.cpu().numpy(), gu.cpu().numpy()) < 2e-3
+    assert _relerr(out["1"][1].cpu().numpy(), out["0"][1].cpu().numpy()) < 1e-3
+    assert out["1"][2] == out["0"][2] == 3   # one Adam step count per train step, from the fold launch
