@@ -61,11 +61,13 @@ __global__ __launch_bounds__(HW * 64) void lstm_head_kernel(HeadArgs a) {
   for (int t = 0; t < 2; ++t) {
     f32x4 u, v;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 4; ++j) {   // clamped addresses, values selected after the load (no branches)
       const int o1 = 16 * t + c, o2 = 16 * t + 4 * g + j;
-      u[j] = o1 < N ? a.W[(4 * g + j) * N + o1] : 0.f;
-      v[j] = o2 < N ? a.W[c * N + o2] : 0.f;
-      bias[t][j] = o2 < N ? a.b[o2] : 0.f;
+      const float wu = a.W[(4 * g + j) * N + (o1 < N ? o1 : 0)], wv = a.W[c * N + (o2 < N ? o2 : 0)];
+      const float bb = a.b[o2 < N ? o2 : 0];
+      u[j] = o1 < N ? wu : 0.f;
+      v[j] = o2 < N ? wv : 0.f;
+      bias[t][j] = o2 < N ? bb : 0.f;
     }
     a1[t] = pack4(u);
     a2[t] = pack4(v);
@@ -97,12 +99,14 @@ __global__ __launch_bounds__(HW * 64) void lstm_head_kernel(HeadArgs a) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i) {   // selects only: outputs past N compare as -inf
         const int o = 16 * t + 4 * g + i;
-        if (o < N) {
-          if (yp[t][i] > mp) { mp = yp[t][i]; ip = o; }
-          if (tg[t][i] > mt) { mt = tg[t][i]; it = o; }
-        }
+        const float pv = o < N ? yp[t][i] : -INFINITY, tv = o < N ? tg[t][i] : -INFINITY;
+        const bool bp = pv > mp, bt = tv > mt;
+        mp = bp ? pv : mp;
+        ip = bp ? o : ip;
+        mt = bt ? tv : mt;
+        it = bt ? o : it;
       }
 #pragma unroll
     for (int s = 16; s <= 32; s <<= 1) {   // merge the 4 lane groups holding the row's outputs
