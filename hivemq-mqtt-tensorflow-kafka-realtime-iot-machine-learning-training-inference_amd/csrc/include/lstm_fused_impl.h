@@ -88,6 +88,31 @@ __device__ __forceinline__ bf16x4 row_operand(bf16x4 raw, int k0, int IN) {
   return raw;
 }
 
+// The same operand with the mask as bits: lane-fixed keep words (0xFFFF per kept bf16 column,
+// row_keep) and the constant-1 bias columns merged in one v_bfi_b32 per register -- the per-element
+// selects of row_operand are 4 VALU per piece and step in the fused recurrences' hot loops.
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x2_t row_keep(int k0, int IN) {
+  u32x2_t k;
+  k[0] = (k0 < IN ? 0xFFFFu : 0u) | (k0 + 1 < IN ? 0xFFFF0000u : 0u);
+  k[1] = (k0 + 2 < IN ? 0xFFFFu : 0u) | (k0 + 3 < IN ? 0xFFFF0000u : 0u);
+  return k;
+}
+__device__ __forceinline__ bf16x4 row_operand_k(f32x4 raw, u32x2_t keep, bf16x4 ones) {
+  const u32x2_t p = __builtin_bit_cast(u32x2_t, pack4(raw)), o = __builtin_bit_cast(u32x2_t, ones);
+  u32x2_t r;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) r[i] = (p[i] & keep[i]) | (o[i] & ~keep[i]);
+  return __builtin_bit_cast(bf16x4, r);
+}
+__device__ __forceinline__ bf16x4 row_operand_k(bf16x4 raw, u32x2_t keep, bf16x4 ones) {
+  const u32x2_t p = __builtin_bit_cast(u32x2_t, raw), o = __builtin_bit_cast(u32x2_t, ones);
+  u32x2_t r;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) r[i] = (p[i] & keep[i]) | (o[i] & ~keep[i]);
+  return __builtin_bit_cast(bf16x4, r);
+}
+
 // x element type -> raw register type of a 4-element row piece
 template <typename XT> struct RowRaw { using type = f32x4; };
 template <> struct RowRaw<__bf16> { using type = bf16x4; };

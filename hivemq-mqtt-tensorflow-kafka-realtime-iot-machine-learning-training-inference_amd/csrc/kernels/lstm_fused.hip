@@ -210,8 +210,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
   for (int b = 0; b < UB; ++b) dhr[b] = dcn[b] = zero4;
   // BX / DB: the bf16 1.0 bits this lane ORs into its x operand (features IN, IN + 1)
   bf16x4 onex[KT];
+  u32x2_t xkeep[KT];   // the x operand's kept columns (row_operand_k)
 #pragma unroll
-  for (int kt = 0; kt < KT; ++kt) onex[kt] = DB ? ones_at_bias(kt, g, IN) : bf16x4{0, 0, 0, 0};
+  for (int kt = 0; kt < KT; ++kt) {
+    onex[kt] = DB ? ones_at_bias(kt, g, IN) : bf16x4{0, 0, 0, 0};
+    xkeep[kt] = row_keep(16 * kt + 4 * g, IN);
+  }
 
   // Per-step operands, all in C orientation (lane c = this lane's sequence): the
   // forward's inputs x_t and h_{t-1} (gates are recomputed from them instead of being
@@ -378,11 +382,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_bwd_kernel(FusedBwdA
     // operands and accumulation order (bit-identical pre-activations)
     bf16x4 xb[KT], hb[UB];
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-      xb[kt] = row_operand(cur.xt[kt], 16 * kt + 4 * g, IN);
-      if constexpr (DB) xb[kt] |= onex[kt];   // columns IN, IN + 1: 0 -> 1.0 (their weights: the bias / 0)
-    }
-    const bool take_dh = valid && (!a.dh_last_only || t == T - 1);
+    for (int kt = 0; kt < KT; ++kt)   // columns past IN zeroed; DB: IN, IN + 1 -> 1.0 (their weights: bias / 0)
+      xb[kt] = row_operand_k(cur.xt[kt], xkeep[kt], onex[kt]);
+    // Fragment mode (the stacked model): a padding lane's dh is exactly 0 -- layer 2's dX of a padding
+    // sequence, whose dz is 0 -- so only the last-step-only case needs the select (8 VALU per step)
+    const bool take_dh = (FR && !a.dh_last_only) ? true : valid && (!a.dh_last_only || t == T - 1);
 #pragma unroll
     for (int s = 0; s < UB; ++s) hb[s] = cur.hp[s];
     f32x4 z[MT];

@@ -395,8 +395,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd2_kernel(FusedFwd
   }
   if (wv0 * 16 >= a.B) return;  // wave-uniform
   bf16x4 onex[KT1];
+  u32x2_t xkeep[KT1];   // the x operand's kept columns (row_operand_k: one v_bfi per register)
 #pragma unroll
-  for (int kt = 0; kt < KT1; ++kt) onex[kt] = BX1 ? ones_at_bias(kt, g, IN1) : bf16x4{0, 0, 0, 0};
+  for (int kt = 0; kt < KT1; ++kt) {
+    onex[kt] = BX1 ? ones_at_bias(kt, g, IN1) : bf16x4{0, 0, 0, 0};
+    xkeep[kt] = row_keep(16 * kt + 4 * g, IN1);
+  }
   f32x4 h1[NT][UB1], c1[NT][UB1], h2[NT][UB2], c2[NT][UB2];
   bf16x4 hb1[NT][UB1], hb2[NT][UB2];
   int xo[NT][KT1][4];   // per-lane byte offsets of the x row pieces (tile row 0, step 0 = the uniform base)
@@ -468,8 +472,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void lstm_fused_fwd2_kernel(FusedFwd
         if constexpr (PROBE & 4) {
           xb[k][kt] = pack4(xin[k][kt]);
         } else {
-          xb[k][kt] = row_operand(xin[k][kt], 16 * kt + 4 * g, IN1);
-          if constexpr (BX1) xb[k][kt] |= onex[kt];
+          xb[k][kt] = row_operand_k(xin[k][kt], xkeep[kt], onex[kt]);
         }
       }
     load_x(t + PF < T ? t + PF : T - 1, xin);
