@@ -62,6 +62,9 @@ int dense_wgrad_grid(int64_t M, int max_blocks);
 int slab_sum_scratch(int G, int S);
 int slab_sum_level_launch(const float* in, int G, int S, float* out, hipStream_t stream);
 // map (optional, S ints): the final level writes element s to out[map[s]] (< 0: dropped)
+// two mapped slab sets reduced into one flat output in ONE launch (one-pass reduction, G <= 4096 each)
+hipError_t slab_sum2_launch(const float* p0, int G0, int S0, const int* map0, const float* p1, int G1, int S1,
+                            const int* map1, float* out, hipStream_t stream);
 hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, float* out, hipStream_t stream,
                            const int* map = nullptr);
 // w_t: W is the row-major [N, K] weight used transposed (Y = X . W^T)

@@ -402,12 +402,33 @@ int slab_sum_scratch(int G, int S) {
 // combine in LDS in fixed order (deterministic).  ONE launch instead of two or three levels:
 // each level of the multi-pass reduction cost ~5 us of launch and ramp at the LSTM's slab
 // counts (3 x 2 levels per seq-50 training step, profiles/r04).
+// Device body of one column chunk (blk) of one slab set: slab_sum1_kernel, and slab_sum2_kernel (two
+// independent slab sets in ONE launch -- the seq-50 step's two LSTM layers, whose sums both wait for
+// nothing but Adam: one ~5 us launch floor less per step)
+template <bool MAP>
+__device__ __forceinline__ void slab_sum1_body(const float* __restrict__ in, int G, int S, float* __restrict__ out,
+                                               const int* __restrict__ map, int blk);
+
 template <bool MAP>
 __global__ __launch_bounds__(256) void slab_sum1_kernel(const float* __restrict__ in, int G, int S,
                                                         float* __restrict__ out, const int* __restrict__ map) {
+  slab_sum1_body<MAP>(in, G, S, out, map, blockIdx.x);
+}
+
+__global__ __launch_bounds__(256) void slab_sum2_kernel(const float* __restrict__ in0, int G0, int S0,
+                                                        const int* __restrict__ map0, const float* __restrict__ in1,
+                                                        int G1, int S1, const int* __restrict__ map1, int nb0,
+                                                        float* __restrict__ out) {
+  if ((int)blockIdx.x < nb0) slab_sum1_body<true>(in0, G0, S0, out, map0, blockIdx.x);
+  else slab_sum1_body<true>(in1, G1, S1, out, map1, blockIdx.x - nb0);   // block-uniform branch
+}
+
+template <bool MAP>
+__device__ __forceinline__ void slab_sum1_body(const float* __restrict__ in, int G, int S, float* __restrict__ out,
+                                               const int* __restrict__ map, int blk) {
   __shared__ f32x4 red[16][16];
   const int qi = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const int quad = blockIdx.x * 16 + qi;
+  const int quad = blk * 16 + qi;
   f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   if (quad * 4 < S) {
     int g = grp, k = 0;
@@ -433,6 +454,15 @@ __global__ __launch_bounds__(256) void slab_sum1_kernel(const float* __restrict_
       *reinterpret_cast<f32x4*>(out + quad * 4) = t;
     }
   }
+}
+
+hipError_t slab_sum2_launch(const float* p0, int G0, int S0, const int* map0, const float* p1, int G1, int S1,
+                            const int* map1, float* out, hipStream_t stream) {
+  if (S0 % 4 != 0 || S1 % 4 != 0 || G0 < 1 || G1 < 1 || !map0 || !map1) return hipErrorInvalidValue;
+  const int nb0 = (S0 / 4 + 15) / 16, nb1 = (S1 / 4 + 15) / 16;
+  hipLaunchKernelGGL(slab_sum2_kernel, dim3(nb0 + nb1), dim3(256), 0, stream, p0, G0, S0, map0, p1, G1, S1, map1, nb0,
+                     out);
+  return hipGetLastError();
 }
 
 hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, float* out, hipStream_t stream,

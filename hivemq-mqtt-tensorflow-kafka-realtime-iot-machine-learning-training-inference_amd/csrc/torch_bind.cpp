@@ -808,7 +808,7 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
                                        const c10::optional<at::Tensor>& c0, const at::Tensor& W, const at::Tensor& Uw,
                                        const at::Tensor& b, int64_t act, bool want_dx, bool want_state_grads,
                                        bool dh_last_only, const c10::optional<at::Tensor>& grad,
-                                       const c10::optional<at::Tensor>& map, bool frag) {
+                                       const c10::optional<at::Tensor>& map, bool frag, bool defer_sum) {
   check_dev(dh, "dh", at::kBFloat16);
   check_dev(cseq, "c", at::kBFloat16);
   check_dev(hseq, "h", at::kBFloat16);
@@ -863,6 +863,17 @@ std::vector<at::Tensor> lstm_fused_bwd(const at::Tensor& dh, const at::Tensor& c
       want_dx ? dx_pad.data_ptr() : nullptr, want_state_grads ? dh0.data_ptr<float>() : nullptr,
       want_state_grads ? dc0.data_ptr<float>() : nullptr, partials.data_ptr<float>(), B, (int)T, (int)IN, (int)U,
       (int)act, dh_last_only ? 1 : 0, x_seq, dzb > 0 ? dzs.data_ptr() : nullptr, frag ? 1 : 0, st));
+  // defer_sum (with grad + map): the weight-gradient slabs come back unreduced as the second output, for
+  // slab_sum2 to reduce together with another layer's in one launch
+  TORCH_CHECK(!defer_sum || mp, "defer_sum needs grad and map");
+  if (defer_sum) {
+    at::Tensor dxo;
+    if (want_dx) {
+      dxo = dx_pad.narrow(0, 0, B);
+      if (dx_pad.size(2) != IN && !frag) dxo = dxo.narrow(2, 0, IN).contiguous();
+    }
+    return {dxo, partials, at::Tensor(), at::Tensor(), dh0, dc0};
+  }
   SML_CHECK_HIP(sml::slab_sum_launch(partials.data_ptr<float>(), G, S, scratch.data_ptr<float>(),
                                      out.data_ptr<float>(), st, mp));
   const int64_t G4 = 4 * U, LDW = (S / G4) - U - 1;
@@ -1069,6 +1080,20 @@ at::Tensor lstm_head(const at::Tensor& h, const at::Tensor& W, const at::Tensor&
                                       opt_mut(out), (float)div0, (float)div1,
                                       counter.has_value() ? counter->data_ptr<int64_t>() : nullptr, cur_stream(h)));
   return dh;
+}
+
+// Two layers' deferred weight-gradient slabs (lstm_fused_bwd defer_sum) reduced into grad in ONE launch.
+void slab_sum2(const at::Tensor& p0, const at::Tensor& map0, const at::Tensor& p1, const at::Tensor& map1,
+               const at::Tensor& grad) {
+  for (const auto* t : {&p0, &p1}) {
+    check_dev(*t, "partials", at::kFloat);
+    TORCH_CHECK(t->dim() == 2 && t->is_contiguous() && t->size(0) <= 4096, "partials must be [G <= 4096, S]");
+  }
+  const int* m0 = grad_map(grad, map0, (int)p0.size(1));
+  const int* m1 = grad_map(grad, map1, (int)p1.size(1));
+  c10::hip::HIPGuard guard(p0.device().index());
+  SML_CHECK_HIP(sml::slab_sum2_launch(p0.data_ptr<float>(), (int)p0.size(0), (int)p0.size(1), m0, p1.data_ptr<float>(),
+                                      (int)p1.size(0), (int)p1.size(1), m1, grad.data_ptr<float>(), cur_stream(p0)));
 }
 
 // K3 + K6: (y_pred - y) * gscale -> grad, [sum sq err, #correct rows] += into acc.
@@ -1492,7 +1517,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("c"), py::arg("h"), py::arg("x"), py::arg("h0") = py::none(), py::arg("c0") = py::none(),
         py::arg("W"), py::arg("U"), py::arg("b"), py::arg("act") = 1, py::arg("want_dx") = true,
         py::arg("want_state_grads") = false, py::arg("dh_last_only") = false, py::arg("grad") = py::none(),
-        py::arg("map") = py::none(), py::arg("frag") = false);
+        py::arg("map") = py::none(), py::arg("frag") = false, py::arg("defer_sum") = false);
+  m.def("slab_sum2", &slab_sum2, "two deferred weight-gradient slab sets reduced into grad in one launch",
+        py::arg("p0"), py::arg("map0"), py::arg("p1"), py::arg("map1"), py::arg("grad"));
   m.def("lstm_ref_train", &lstm_ref_train,
         "persistent trainer: nsteps Keras Adam steps of the reference LSTM stack (look_back 1) in one launch",
         py::arg("flat"), py::arg("m"), py::arg("v"), py::arg("iter"), py::arg("x"), py::arg("y"),

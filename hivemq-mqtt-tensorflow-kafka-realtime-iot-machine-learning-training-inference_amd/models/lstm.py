@@ -73,6 +73,12 @@ def _headfuse() -> bool:
     return os.environ.get("SML_LSTM_HEADFUSE", "1") != "0"
 
 
+def _slab2() -> bool:
+    """SML_LSTM_SLAB2=0: each LSTM layer's weight-gradient slabs reduced right after its backward (two
+    launches) instead of both in one launch before Adam (A/B; read per step)."""
+    return os.environ.get("SML_LSTM_SLAB2", "1") != "0"
+
+
 def _frag() -> bool:
     """SML_LSTM_FRAG=0: the stacked two-layer step keeps h1 / h2 / dX as [B, T, U] rows instead of the
     fragment-native layout (A/B; read per step).  Fragment-native, every per-step h / dh / x access of
@@ -332,6 +338,9 @@ class LSTMPredictor:
             C.dense_wgrad(hin, dy, 0, True, 1024, grad, plan["head_map"])
             dh = C.dense_fwd(dy, K, None, 0, True, 1024, True)   # dh = dy . K^T, bf16
         layers = pre + post
+        # two LSTM layers: both weight-gradient slab sums in ONE launch after the second backward
+        pair = len(layers) == 2 and not R and _slab2()
+        deferred = []
         for i in range(len(layers) - 1, -1, -1):
             L = layers[i]
             xin, hs, c = saved[i]
@@ -352,10 +361,14 @@ class LSTMPredictor:
                                       plan["maps"][0], plan["maps"][1])
                     break
             out = C.lstm_fused_bwd(dh, c, hs, xin, None, None, W, Uw, b, ACT[L["activation"]], i > 0, False,
-                                   last_only, grad, plan["maps"][i], frag and i < 2)
+                                   last_only, grad, plan["maps"][i], frag and i < 2, defer_sum=pair)
+            if pair:
+                deferred.append((out[1], plan["maps"][i]))
             dh = out[0]
             if R and i == len(pre):   # RepeatVector backward: the repeated steps' gradients summed
                 dh = (dh.view(n, -1) if R == 1 else dh.sum(1)).to(torch.bfloat16)
+        if len(deferred) == 2:
+            C.slab_sum2(deferred[0][0], deferred[0][1], deferred[1][0], deferred[1][1], grad)
         self.opt.step(allreduce=allreduce, counted=fold)
         if fold:
             return metrics[0], metrics[1]   # acc is overwritten by the next step, metrics is this step's own

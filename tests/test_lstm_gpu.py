@@ -537,3 +537,24 @@ def test_fused_head_matches_per_kernel_head(cuda_device, monkeypatch, B, T, frag
         assert _relerr(gf.cpu().numpy(), gu.cpu().numpy()) < 2e-3
     assert _relerr(out["1"][1].cpu().numpy(), out["0"][1].cpu().numpy()) < 1e-3
     assert out["1"][2] == out["0"][2] == 3   # one Adam step count per train step, from the fold launch
+
+
+def test_paired_slab_sum_equals_two_launches(cuda_device, monkeypatch):
+    """The two LSTM layers' weight-gradient slabs reduced in ONE launch after the second backward
+    (slab_sum2, the default) give the same bits as one slab sum per layer (SML_LSTM_SLAB2=0)."""
+    from streamml.data.stream import sliding_windows
+    rows = torch.tensor(np.random.default_rng(9).uniform(-1, 1, (3 * 1000 + 50, 18)), dtype=torch.float32,
+                        device=cuda_device)
+    X, Y = sliding_windows(rows, 50)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SML_LSTM_SLAB2", v)
+        m = LSTMPredictor.two_layer(look_back=50, device=cuda_device, seed=4)
+        grads = []
+        for s in range(3):
+            m.train_step(X[s * 1000:(s + 1) * 1000], Y[s * 1000:(s + 1) * 1000])
+            grads.append(m.fp.grad.detach().clone())
+        out[v] = (grads, m.fp.flat.detach().clone())
+    for a, b in zip(out["1"][0], out["0"][0]):
+        assert torch.equal(a, b)
+    assert torch.equal(out["1"][1], out["0"][1])
