@@ -23,6 +23,8 @@ namespace sml {
 namespace {
 
 constexpr int HW = 4;   // waves per workgroup
+constexpr int WS_ROW = 36;             // per-wave LDS partial: dW rows [16][WS_ROW] (32 used) ...
+constexpr int WS_DB = 16 * WS_ROW;     // ... then db [32], loss, correct
 
 struct HeadArgs {
   const __bf16* h;   // [n, 16] bf16, row stride ldh elements
@@ -51,7 +53,7 @@ __global__ __launch_bounds__(HW * 64) void lstm_head_kernel(HeadArgs a) {
   const int N = a.N;
   const int PS = 16 * N + N + 2;
   __shared__ __attribute__((aligned(16))) char scr[HW][3 * 512];
-  __shared__ float slab[16 * 32 + 32 + 2];
+  __shared__ float slab[HW][WS_DB + 34];
   char* sc = scr[w];
   // A fragments: a1[t] = W^T tile t ([m = output 16t + c][k = unit 4g + j]), a2[t] = W ([m = unit c]
   // [k = output 16t + 4g + j]), bias in the C rows of tile t (outputs 16t + 4g + i)
@@ -146,28 +148,31 @@ __global__ __launch_bounds__(HW * 64) void lstm_head_kernel(HeadArgs a) {
     }
   se = wave_sum(se);
   correct = wave_sum(correct);
-  for (int i = threadIdx.x; i < PS; i += HW * 64) slab[i] = 0.f;
-  for (int turn = 0; turn < HW; ++turn) {   // the waves add in a fixed order (deterministic)
-    __syncthreads();
-    if (turn == w) {
+  // Each wave stores its padded partial unconditionally (row stride WS_ROW: the 4 lane groups land in
+  // distinct banks), one barrier, then every entry is the fixed-order sum w0 + w1 + w2 + w3
+  // (deterministic; a first version added the waves in turns through guarded LDS read-modify-writes:
+  // 4 barriers and 16 dependent LDS round trips per wave).
+  float* ws = slab[w];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int unit = 4 * g + i, o = 16 * t + c;   // C of accW[t]: [m = unit][n = output]
-          if (o < N) slab[unit * N + o] += accW[t][i];
-          const int od = 16 * t + 4 * g + i;
-          if (c == 0 && od < N) slab[16 * N + od] += dbl[t][i];
-        }
-      if (lane == 0) {
-        slab[17 * N] += se;
-        slab[17 * N + 1] += correct;
-      }
+    for (int i = 0; i < 4; ++i) {
+      ws[(4 * g + i) * WS_ROW + 16 * t + c] = accW[t][i];   // C of accW[t]: [m = unit][n = output]
+      if (c == 0) ws[WS_DB + 16 * t + 4 * g + i] = dbl[t][i];
     }
+  if (lane == 0) {
+    ws[WS_DB + 32] = se;
+    ws[WS_DB + 33] = correct;
   }
   __syncthreads();
   float* out = a.part + (int64_t)blockIdx.x * PS;
-  for (int i = threadIdx.x; i < PS; i += HW * 64) out[i] = slab[i];
+  for (int i = threadIdx.x; i < PS; i += HW * 64) {
+    const int pi = i < 16 * N ? (i / N) * WS_ROW + i % N : WS_DB + (i < 17 * N ? i - 16 * N : 32 + i - 17 * N);
+    float v = slab[0][pi];
+#pragma unroll
+    for (int k = 1; k < HW; ++k) v += slab[k][pi];
+    out[i] = v;
+  }
 }
 
 // One workgroup per partial entry: thread k sums partials k, k + 256, ... in order, then a fixed-order
