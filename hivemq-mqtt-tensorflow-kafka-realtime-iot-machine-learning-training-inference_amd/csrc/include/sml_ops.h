@@ -24,6 +24,13 @@ hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, f
                               float* m, float* v, const int64_t* iter, float lr, float beta1, float beta2, float eps,
                               float gscale, float* metrics_acc, int flags, int64_t* cursor, int64_t cursor_step,
                               int64_t cursor_ring, hipStream_t stream);
+// the slab level sum + reduce_adam in one launch (counters: slab_adam_columns(S) zeroed uint32,
+// re-armed by the kernel; scratch: ceil(G / 32) * S floats); bit-identical to the two launches
+int slab_adam_columns(int S);
+hipError_t slab_adam_launch(const float* partials, int G, int S, int nparam, float* scratch, unsigned* counters,
+                            float* grad_out, float* params, float* m, float* v, const int64_t* iter, float lr,
+                            float beta1, float beta2, float eps, float gscale, float* metrics_acc, int flags,
+                            int64_t* cursor, int64_t cursor_step, int64_t cursor_ring, hipStream_t stream);
 
 // ---- persistent small-batch AE trainer (ae_minibatch.hip): nsteps Keras steps in one launch ----
 int ae_minibatch_max_batch();

@@ -1893,6 +1893,92 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
   for (int e = 0; e < 4; ++e)
     adam_one(tot[e], slot0 + e, nparam, grad_out, params, m, v, lr_t, hp, gscale, metrics_acc, flags);
 }
+
+// The wide-grid step's two reduction launches (slab_sum_kernel level: G -> gy = G / 32 chunk sums,
+// then reduce_adam_kernel over the gy sums) in ONE launch.  Grid (S / 256 column blocks, gy chunks):
+// every workgroup writes its chunk's sums exactly as the level kernel does, then counts itself in
+// its column's counter; the column's last workgroup (release / acquire fences at agent scope: the
+// sums come from every XCD's L2) sums the gy chunk sums in reduce_adam_kernel's order -- 16 virtual
+// groups k summing chunks k, k + 16, ... then group 0 + ... + group 15 -- and applies Adam.  So the
+// result is bit-identical to the two launches whichever workgroup ends last; only who does the
+// final sum depends on timing.  The last workgroup re-arms its counter (stream order separates steps).
+// Opt-in (SML_AE_FUSED_REDUCE=1): measured 80 us against the two launches' 5.9 + 5.9 us -- each
+// workgroup's release fence is a buffer_wbl2 of its XCD's L2, full of the train kernel's slabs.
+__global__ __launch_bounds__(256) void slab_adam_kernel(const float* __restrict__ partials, int G, int S, int nparam,
+                                                        float* scratch, unsigned* counters, float* grad_out,
+                                                        float* params, float* m, float* v, const int64_t* iter,
+                                                        AdamHP hp, float gscale, float* metrics_acc, int flags,
+                                                        CursorAdv adv) {
+  constexpr int CH = 32;   // == dense.hip kSlabChunk (the level kernel's chunk)
+  __shared__ f32x4 red[16][64];
+  __shared__ int last;
+  const int q = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int quad = blockIdx.x * 64 + q;
+  const bool on = quad * 4 < S;
+  const int gy = gridDim.y;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (on) {
+    f32x4 vals[CH / 4];
+    const int g0 = blockIdx.y * CH;
+#pragma unroll
+    for (int u = 0; u < CH / 4; ++u) {
+      const int gi = g0 + grp + 4 * u;
+      vals[u] = gi < G ? *reinterpret_cast<const f32x4*>(partials + (int64_t)gi * S + quad * 4)
+                       : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < CH / 4; ++u) acc += vals[u];
+  }
+  red[grp][q] = acc;
+  __syncthreads();
+  if (grp == 0 && on)
+    *reinterpret_cast<f32x4*>(scratch + (int64_t)blockIdx.y * S + quad * 4) = red[0][q] + red[1][q] + red[2][q] + red[3][q];
+  __threadfence();   // release: the chunk sums reach the device-coherent level before the count
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(counters + blockIdx.x, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+           (unsigned)gy - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();   // acquire: no stale line of another workgroup's chunk sums
+  // virtual groups k = 4 grp + j of reduce_adam_kernel, all 32 loads of a batch in flight at once
+  f32x4 a2[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (int base = 0; base < gy; base += 16 * 8) {
+    f32x4 vals[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int idx = base + 4 * grp + j + 16 * u;
+        vals[j][u] = (on && idx < gy) ? *reinterpret_cast<const f32x4*>(scratch + (int64_t)idx * S + quad * 4)
+                                      : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a2[j] += vals[j][u];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[4 * grp + j][q] = a2[j];
+  __syncthreads();
+  if (threadIdx.x == 0) counters[blockIdx.x] = 0u;
+  if ((flags & RA_ADVANCE) && adv.cursor && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t nx = adv.cursor[0] + adv.step;
+    adv.cursor[0] = nx >= adv.ring ? nx - adv.ring : nx;
+  }
+  if (grp != 0 || !on) return;
+  f32x4 tot = red[0][q];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) tot += red[k][q];
+  float lr_t = 0.f;
+  if (flags & RA_ADAM) {
+    const float t = (float)iter[0];
+    lr_t = hp.lr * sqrtf(1.0f - powf(hp.beta2, t)) / (1.0f - powf(hp.beta1, t));
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    adam_one(tot[e], quad * 4 + e, nparam, grad_out, params, m, v, lr_t, hp, gscale, metrics_acc, flags);
+}
 }  // namespace
 
 // ----------------------------------------------------------------------------
@@ -2122,6 +2208,21 @@ hipError_t reduce_adam_launch(const float* partials, int G, int S, int nparam, f
   const int grid = (S / 4 + 15) / 16;
   hipLaunchKernelGGL(reduce_adam_kernel, dim3(grid), dim3(256), 0, stream, partials, G, S, nparam, grad_out, params,
                      m, v, iter, hp, gscale, metrics_acc, flags, adv);
+  return hipGetLastError();
+}
+
+int slab_adam_columns(int S) { return (S / 4 + 63) / 64; }
+
+hipError_t slab_adam_launch(const float* partials, int G, int S, int nparam, float* scratch, unsigned* counters,
+                            float* grad_out, float* params, float* m, float* v, const int64_t* iter, float lr,
+                            float beta1, float beta2, float eps, float gscale, float* metrics_acc, int flags,
+                            int64_t* cursor, int64_t cursor_step, int64_t cursor_ring, hipStream_t stream) {
+  AdamHP hp{lr, beta1, beta2, eps};
+  CursorAdv adv{cursor, cursor_step, cursor_ring};
+  if (S % 4 != 0 || G < 1 || counters == nullptr || scratch == nullptr) return hipErrorInvalidValue;
+  const int gy = (G + 31) / 32;
+  hipLaunchKernelGGL(slab_adam_kernel, dim3(slab_adam_columns(S), gy), dim3(256), 0, stream, partials, G, S, nparam,
+                     scratch, counters, grad_out, params, m, v, iter, hp, gscale, metrics_acc, flags, adv);
   return hipGetLastError();
 }
 

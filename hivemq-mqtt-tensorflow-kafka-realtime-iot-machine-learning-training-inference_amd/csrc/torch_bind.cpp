@@ -233,17 +233,52 @@ std::vector<at::Tensor> normalize_filter(const at::Tensor& x, int64_t D, const c
   return {out, idx, total};
 }
 
+// SML_AE_FUSED_REDUCE=1: the wide-grid reduction in one launch (slab_adam_kernel, bit-identical
+// results) instead of two (level sum, then reduce_adam); read at every call.  Default off: the
+// agent-scope release fence every workgroup needs before its count writes back its XCD's whole L2
+// (buffer_wbl2), which the train kernel's ~19 MB of slabs have just filled -- the one launch took
+// 80 us against 5.9 + 5.9 us, 0.70 vs 0.66 ms per headline step (profiles/r06/SUMMARY.md §10).
+static bool fused_reduce_enabled() {
+  const char* e = std::getenv("SML_AE_FUSED_REDUCE");
+  return e && e[0] == '1';
+}
+
 void reduce_adam(const at::Tensor& partials, int64_t G, int64_t S, int64_t nparam,
                  const c10::optional<at::Tensor>& grad_out, const c10::optional<at::Tensor>& params,
                  const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
                  const c10::optional<at::Tensor>& iter, double lr, double beta1, double beta2, double eps,
                  double gscale, const c10::optional<at::Tensor>& metrics, int64_t flags,
                  const c10::optional<at::Tensor>& cursor, int64_t cursor_step, int64_t cursor_ring,
-                 const c10::optional<at::Tensor>& scratch) {
+                 const c10::optional<at::Tensor>& scratch, const c10::optional<at::Tensor>& counters) {
   check_dev(partials, "partials", at::kFloat);
   TORCH_CHECK(partials.numel() >= G * S, "partials smaller than G*S");
   const float* src = partials.data_ptr<float>();
-  if (scratch.has_value() && scratch->defined() && G > 64) {
+  const bool wide = scratch.has_value() && scratch->defined() && G > 64;
+  if (wide && counters.has_value() && counters->defined() && fused_reduce_enabled()) {
+    // wide grids, one launch: the level sum and the Adam pass joined by per-column counters
+    check_dev(*scratch, "scratch", at::kFloat);
+    check_dev(*counters, "counters", at::kInt);
+    TORCH_CHECK(counters->numel() >= sml::slab_adam_columns((int)S) && counters->is_contiguous(),
+                "reduce counters too small");
+    TORCH_CHECK(scratch->numel() >= ((G + 31) / 32) * S, "reduce scratch too small");
+    if (flags & 2) {
+      TORCH_CHECK(params.has_value() && m.has_value() && v.has_value() && iter.has_value(), "adam needs params/m/v/iter");
+      TORCH_CHECK(params->numel() >= nparam && m->numel() >= nparam && v->numel() >= nparam, "adam buffers too small");
+      check_dev(*iter, "iter", at::kLong);
+    }
+    if (flags & 1) TORCH_CHECK(grad_out.has_value() && grad_out->numel() >= S, "grad_out too small");
+    if (flags & 4) TORCH_CHECK(metrics.has_value() && metrics->numel() >= S - nparam, "metrics too small");
+    c10::hip::HIPGuard guard(partials.device().index());
+    const int64_t* iter_ptr = (iter.has_value() && iter->defined()) ? iter->data_ptr<int64_t>() : nullptr;
+    SML_CHECK_HIP(sml::slab_adam_launch(src, (int)G, (int)S, (int)nparam, scratch->data_ptr<float>(),
+                                        reinterpret_cast<unsigned*>(counters->data_ptr<int>()), opt_mut(grad_out),
+                                        opt_mut(params), opt_mut(m), opt_mut(v), iter_ptr, (float)lr, (float)beta1,
+                                        (float)beta2, (float)eps, (float)gscale, opt_mut(metrics), (int)flags,
+                                        (cursor.has_value() && cursor->defined()) ? cursor->data_ptr<int64_t>() : nullptr,
+                                        cursor_step, cursor_ring, cur_stream(partials)));
+    return;
+  }
+  if (wide) {
     // wide grids: one parallel level of the deterministic slab sum first (G -> ceil(G/32)
     // slabs over G/32 x S/256 workgroups), so the Adam kernel reads 32x fewer bytes
     check_dev(*scratch, "scratch", at::kFloat);
@@ -1417,7 +1452,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("S"), py::arg("nparam"), py::arg("grad_out"), py::arg("params"), py::arg("m"), py::arg("v"),
         py::arg("iter"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("gscale"),
         py::arg("metrics"), py::arg("flags"), py::arg("cursor") = py::none(), py::arg("cursor_step") = 0,
-        py::arg("cursor_ring") = 0, py::arg("scratch") = py::none());
+        py::arg("cursor_ring") = 0, py::arg("scratch") = py::none(), py::arg("counters") = py::none());
   py::class_<P2PPy>(m, "P2PExchange")
       .def(py::init<int, int, int, int64_t>(), py::arg("device"), py::arg("rank"), py::arg("world"),
            py::arg("slots"))

@@ -134,6 +134,8 @@ class FusedAE:
         self.iter = torch.zeros(1, dtype=torch.int64, device=dev)
         self.partials = torch.zeros(self.max_blocks * NSLOT, device=dev)
         self.reduce_scratch = torch.zeros(((self.max_blocks + 31) // 32) * NSLOT, device=dev)
+        # per-column arrival counters of the one-launch wide reduction (zero; re-armed by the kernel)
+        self.reduce_counters = torch.zeros(64, dtype=torch.int32, device=dev)
         self.grad = torch.zeros(NSLOT, device=dev)
         self.metrics = torch.zeros(NSLOT - NPARAM, device=dev)   # epoch accumulators
         self.cursor = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -187,7 +189,8 @@ class FusedAE:
         self.C.reduce_adam(src, int(G), NSLOT, NPARAM, self.grad, self.params, self.m, self.v, self.iter,
                            self.lr, self.beta_1, self.beta_2, self.epsilon, float(gscale), self.metrics, int(flags),
                            self.cursor, int(self.ring_batch), int(ring),
-                           self.reduce_scratch if partials is None else None)
+                           self.reduce_scratch if partials is None else None,
+                           self.reduce_counters if partials is None else None)
 
     # -- streaming ring consumption (device cursor; graph-capturable) ------------
     def attach_ring(self, ring: torch.Tensor, batch: int) -> None:
