@@ -70,8 +70,20 @@ int slab_sum_scratch(int G, int S);
 int slab_sum_level_launch(const float* in, int G, int S, float* out, hipStream_t stream);
 // map (optional, S ints): the final level writes element s to out[map[s]] (< 0: dropped)
 // two mapped slab sets reduced into one flat output in ONE launch (one-pass reduction, G <= 4096 each)
+// Adam fused into slab_sum2 (the last reduction of a train step): every mapped slot is updated where its
+// gradient becomes final, the `nrest` slots listed in `rest` (no slab covers them) from out[] as it
+// stands.  Bit-identical to slab_sum2 + reduce_adam (sml_adam.h).
+struct SlabAdam {
+  float* params = nullptr;
+  float* m = nullptr;
+  float* v = nullptr;
+  const int64_t* iter = nullptr;   // already advanced for this step
+  float lr = 0.f, b1 = 0.f, b2 = 0.f, eps = 0.f, gscale = 1.f;
+  const int* rest = nullptr;
+  int nrest = 0;
+};
 hipError_t slab_sum2_launch(const float* p0, int G0, int S0, const int* map0, const float* p1, int G1, int S1,
-                            const int* map1, float* out, hipStream_t stream);
+                            const int* map1, float* out, hipStream_t stream, const SlabAdam* adam = nullptr);
 hipError_t slab_sum_launch(const float* partials, int G, int S, float* scratch, float* out, hipStream_t stream,
                            const int* map = nullptr);
 // w_t: W is the row-major [N, K] weight used transposed (Y = X . W^T)

@@ -38,6 +38,7 @@
 #include <cstdlib>
 
 #include "sml_common.h"
+#include "sml_adam.h"
 
 using namespace sml;
 
@@ -1832,14 +1833,10 @@ struct CursorAdv {
   int64_t ring;
 };
 
-// One Adam update with every rounding pinned (explicit fmaf: the kernels that share it -- operands
-// loaded late or prefetched -- give bit-identical results whatever the compiler would contract)
+// One Adam update (sml_adam.h: roundings pinned, shared with dense.hip's fused slab-sum update)
 __device__ __forceinline__ void adam_update(float tot, float m0, float v0, float p0, float lr_t, const AdamHP& hp,
                                             float gscale, float& mm, float& vv, float& pn) {
-  const float gr = tot * gscale;
-  mm = fmaf(hp.beta1, m0, (1.0f - hp.beta1) * gr);
-  vv = fmaf(hp.beta2, v0, ((1.0f - hp.beta2) * gr) * gr);
-  pn = p0 - (lr_t * mm) / (sqrtf(vv) + hp.eps);
+  sml::adam_update(tot, m0, v0, p0, lr_t, hp.beta1, hp.beta2, hp.eps, gscale, mm, vv, pn);
 }
 
 __device__ __forceinline__ void adam_one(float tot, int slot, int nparam, float* grad_out, float* params, float* m,
@@ -1886,7 +1883,7 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
         pp[e] = params[slot0 + e];
       }
     const float t = (float)iter[0];
-    lr_t = hp.lr * sqrtf(1.0f - powf(hp.beta2, t)) / (1.0f - powf(hp.beta1, t));
+    lr_t = sml::adam_lr_t(hp.lr, hp.beta1, hp.beta2, t);
   }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (slot0 < S) {
@@ -2005,7 +2002,7 @@ __global__ __launch_bounds__(256) void slab_adam_kernel(const float* __restrict_
   float lr_t = 0.f;
   if (flags & RA_ADAM) {
     const float t = (float)iter[0];
-    lr_t = hp.lr * sqrtf(1.0f - powf(hp.beta2, t)) / (1.0f - powf(hp.beta1, t));
+    lr_t = sml::adam_lr_t(hp.lr, hp.beta1, hp.beta2, t);
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e)

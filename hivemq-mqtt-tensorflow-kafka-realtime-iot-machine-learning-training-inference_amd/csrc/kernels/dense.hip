@@ -29,6 +29,7 @@
 #include <cstdlib>
 
 #include "sml_common.h"
+#include "sml_adam.h"
 #include "sml_ops.h"
 
 namespace sml {
@@ -405,9 +406,19 @@ int slab_sum_scratch(int G, int S) {
 // Device body of one column chunk (blk) of one slab set: slab_sum1_kernel, and slab_sum2_kernel (two
 // independent slab sets in ONE launch -- the seq-50 step's two LSTM layers, whose sums both wait for
 // nothing but Adam: one ~5 us launch floor less per step)
-template <bool MAP>
+// ADAM (slab_sum2 only): each mapped slot's Adam update right where its gradient is final
+// (sml_adam.h; the gradient is still written to out), so the step needs no separate Adam launch
+__device__ __forceinline__ void slot_adam(const SlabAdam& ad, int d, float g, float lr_t) {
+  float mm, vv, pn;
+  adam_update(g, ad.m[d], ad.v[d], ad.params[d], lr_t, ad.b1, ad.b2, ad.eps, ad.gscale, mm, vv, pn);
+  ad.m[d] = mm;
+  ad.v[d] = vv;
+  ad.params[d] = pn;
+}
+
+template <bool MAP, bool ADAM = false>
 __device__ __forceinline__ void slab_sum1_body(const float* __restrict__ in, int G, int S, float* __restrict__ out,
-                                               const int* __restrict__ map, int blk);
+                                               const int* __restrict__ map, int blk, const SlabAdam& ad = SlabAdam{});
 
 template <bool MAP>
 __global__ __launch_bounds__(256) void slab_sum1_kernel(const float* __restrict__ in, int G, int S,
@@ -415,18 +426,33 @@ __global__ __launch_bounds__(256) void slab_sum1_kernel(const float* __restrict_
   slab_sum1_body<MAP>(in, G, S, out, map, blockIdx.x);
 }
 
+// ADAM: blocks [nb0 + nb1, ...) update the slots no slab map covers (ad.rest: the head's, written
+// to out by an earlier launch) -- every parameter gets exactly one update
+template <bool ADAM>
 __global__ __launch_bounds__(256) void slab_sum2_kernel(const float* __restrict__ in0, int G0, int S0,
                                                         const int* __restrict__ map0, const float* __restrict__ in1,
-                                                        int G1, int S1, const int* __restrict__ map1, int nb0,
-                                                        float* __restrict__ out) {
-  if ((int)blockIdx.x < nb0) slab_sum1_body<true>(in0, G0, S0, out, map0, blockIdx.x);
-  else slab_sum1_body<true>(in1, G1, S1, out, map1, blockIdx.x - nb0);   // block-uniform branch
+                                                        int G1, int S1, const int* __restrict__ map1, int nb0, int nb1,
+                                                        float* __restrict__ out, SlabAdam ad) {
+  const int bx = blockIdx.x;   // block-uniform branches
+  if (bx < nb0) {
+    slab_sum1_body<true, ADAM>(in0, G0, S0, out, map0, bx, ad);
+  } else if (bx < nb0 + nb1) {
+    slab_sum1_body<true, ADAM>(in1, G1, S1, out, map1, bx - nb0, ad);
+  } else if constexpr (ADAM) {
+    const int i = (bx - nb0 - nb1) * 256 + threadIdx.x;
+    if (i < ad.nrest) {
+      const int d = ad.rest[i];
+      slot_adam(ad, d, out[d], adam_lr_t(ad.lr, ad.b1, ad.b2, (float)ad.iter[0]));
+    }
+  }
 }
 
-template <bool MAP>
+template <bool MAP, bool ADAM>
 __device__ __forceinline__ void slab_sum1_body(const float* __restrict__ in, int G, int S, float* __restrict__ out,
-                                               const int* __restrict__ map, int blk) {
+                                               const int* __restrict__ map, int blk, const SlabAdam& ad) {
   __shared__ f32x4 red[16][16];
+  float tstep = 0.f;
+  if constexpr (ADAM) tstep = (float)ad.iter[0];   // issued before the slab loads
   const int qi = threadIdx.x & 15, grp = threadIdx.x >> 4;
   const int quad = blk * 16 + qi;
   f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -445,10 +471,14 @@ __device__ __forceinline__ void slab_sum1_body(const float* __restrict__ in, int
 #pragma unroll
     for (int j = 1; j < 16; ++j) t += red[j][qi];
     if constexpr (MAP) {
+      const float lr_t = ADAM ? adam_lr_t(ad.lr, ad.b1, ad.b2, tstep) : 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int d = map[quad * 4 + j];
-        if (d >= 0) out[d] = t[j];
+        if (d >= 0) {
+          out[d] = t[j];
+          if constexpr (ADAM) slot_adam(ad, d, t[j], lr_t);
+        }
       }
     } else {
       *reinterpret_cast<f32x4*>(out + quad * 4) = t;
@@ -457,11 +487,19 @@ __device__ __forceinline__ void slab_sum1_body(const float* __restrict__ in, int
 }
 
 hipError_t slab_sum2_launch(const float* p0, int G0, int S0, const int* map0, const float* p1, int G1, int S1,
-                            const int* map1, float* out, hipStream_t stream) {
+                            const int* map1, float* out, hipStream_t stream, const SlabAdam* adam) {
   if (S0 % 4 != 0 || S1 % 4 != 0 || G0 < 1 || G1 < 1 || !map0 || !map1) return hipErrorInvalidValue;
   const int nb0 = (S0 / 4 + 15) / 16, nb1 = (S1 / 4 + 15) / 16;
-  hipLaunchKernelGGL(slab_sum2_kernel, dim3(nb0 + nb1), dim3(256), 0, stream, p0, G0, S0, map0, p1, G1, S1, map1, nb0,
-                     out);
+  if (adam) {
+    if (!adam->params || !adam->m || !adam->v || !adam->iter || adam->nrest < 0 || (adam->nrest && !adam->rest))
+      return hipErrorInvalidValue;
+    const int nbr = (adam->nrest + 255) / 256;
+    hipLaunchKernelGGL(slab_sum2_kernel<true>, dim3(nb0 + nb1 + nbr), dim3(256), 0, stream, p0, G0, S0, map0, p1, G1,
+                       S1, map1, nb0, nb1, out, *adam);
+  } else {
+    hipLaunchKernelGGL(slab_sum2_kernel<false>, dim3(nb0 + nb1), dim3(256), 0, stream, p0, G0, S0, map0, p1, G1, S1,
+                       map1, nb0, nb1, out, SlabAdam{});
+  }
   return hipGetLastError();
 }
 

@@ -1118,17 +1118,43 @@ at::Tensor lstm_head(const at::Tensor& h, const at::Tensor& W, const at::Tensor&
 }
 
 // Two layers' deferred weight-gradient slabs (lstm_fused_bwd defer_sum) reduced into grad in ONE launch.
+// With params (+ m, v, iter, rest): Adam fused in (the step's last launch; iter already advanced).
 void slab_sum2(const at::Tensor& p0, const at::Tensor& map0, const at::Tensor& p1, const at::Tensor& map1,
-               const at::Tensor& grad) {
+               const at::Tensor& grad, const c10::optional<at::Tensor>& params, const c10::optional<at::Tensor>& m,
+               const c10::optional<at::Tensor>& v, const c10::optional<at::Tensor>& iter, double lr, double beta1,
+               double beta2, double eps, double gscale, const c10::optional<at::Tensor>& rest) {
   for (const auto* t : {&p0, &p1}) {
     check_dev(*t, "partials", at::kFloat);
     TORCH_CHECK(t->dim() == 2 && t->is_contiguous() && t->size(0) <= 4096, "partials must be [G <= 4096, S]");
   }
   const int* m0 = grad_map(grad, map0, (int)p0.size(1));
   const int* m1 = grad_map(grad, map1, (int)p1.size(1));
+  sml::SlabAdam ad;
+  const bool adam = params.has_value() && params->defined();
+  if (adam) {
+    TORCH_CHECK(m.has_value() && v.has_value() && iter.has_value() && rest.has_value(), "Adam needs m, v, iter, rest");
+    for (const auto* t : {&*params, &*m, &*v}) {
+      check_dev(*t, "adam buffer", at::kFloat);
+      TORCH_CHECK(t->is_contiguous() && t->numel() == grad.numel(), "Adam buffers must match grad");
+    }
+    check_dev(*iter, "iter", at::kLong);
+    check_dev(*rest, "rest", at::kInt);
+    // the kernel scatters through rest unchecked, as through the slab maps: the caller builds it in
+    // range (LSTMPredictor._fused_plan asserts it once; no device read here, so a step stays capturable)
+    TORCH_CHECK(rest->dim() == 1 && rest->is_contiguous() && rest->numel() <= grad.numel(),
+                "rest must be a flat int32 index list");
+    ad.params = params->data_ptr<float>();
+    ad.m = m->data_ptr<float>();
+    ad.v = v->data_ptr<float>();
+    ad.iter = iter->data_ptr<int64_t>();
+    ad.lr = (float)lr; ad.b1 = (float)beta1; ad.b2 = (float)beta2; ad.eps = (float)eps; ad.gscale = (float)gscale;
+    ad.rest = rest->numel() ? rest->data_ptr<int>() : nullptr;
+    ad.nrest = (int)rest->numel();
+  }
   c10::hip::HIPGuard guard(p0.device().index());
   SML_CHECK_HIP(sml::slab_sum2_launch(p0.data_ptr<float>(), (int)p0.size(0), (int)p0.size(1), m0, p1.data_ptr<float>(),
-                                      (int)p1.size(0), (int)p1.size(1), m1, grad.data_ptr<float>(), cur_stream(p0)));
+                                      (int)p1.size(0), (int)p1.size(1), m1, grad.data_ptr<float>(), cur_stream(p0),
+                                      adam ? &ad : nullptr));
 }
 
 // K3 + K6: (y_pred - y) * gscale -> grad, [sum sq err, #correct rows] += into acc.
@@ -1554,7 +1580,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("want_state_grads") = false, py::arg("dh_last_only") = false, py::arg("grad") = py::none(),
         py::arg("map") = py::none(), py::arg("frag") = false, py::arg("defer_sum") = false);
   m.def("slab_sum2", &slab_sum2, "two deferred weight-gradient slab sets reduced into grad in one launch",
-        py::arg("p0"), py::arg("map0"), py::arg("p1"), py::arg("map1"), py::arg("grad"));
+        py::arg("p0"), py::arg("map0"), py::arg("p1"), py::arg("map1"), py::arg("grad"), py::arg("params") = py::none(),
+        py::arg("m") = py::none(), py::arg("v") = py::none(), py::arg("iter") = py::none(), py::arg("lr") = 0.0,
+        py::arg("beta1") = 0.0, py::arg("beta2") = 0.0, py::arg("eps") = 0.0, py::arg("gscale") = 1.0,
+        py::arg("rest") = py::none());
   m.def("lstm_ref_train", &lstm_ref_train,
         "persistent trainer: nsteps Keras Adam steps of the reference LSTM stack (look_back 1) in one launch",
         py::arg("flat"), py::arg("m"), py::arg("v"), py::arg("iter"), py::arg("x"), py::arg("y"),

@@ -79,6 +79,13 @@ def _slab2() -> bool:
     return os.environ.get("SML_LSTM_SLAB2", "1") != "0"
 
 
+def _slab2adam() -> bool:
+    """SML_LSTM_SLAB2ADAM=0: Adam as its own launch after the paired slab sum (A/B; read per step).
+    Default: the paired slab sum applies Adam itself (dense.hip slab_sum2_kernel<ADAM>, bit-identical:
+    sml_adam.h), one launch fewer per step."""
+    return os.environ.get("SML_LSTM_SLAB2ADAM", "1") != "0"
+
+
 def _frag() -> bool:
     """SML_LSTM_FRAG=0: the stacked two-layer step keeps h1 / h2 / dX as [B, T, U] rows instead of the
     fragment-native layout (A/B; read per step).  Fragment-native, every per-step h / dh / x access of
@@ -263,8 +270,13 @@ class LSTMPredictor:
         head_map = torch.as_tensor(mp.astype(np.int32), device=self.device)
         for m_ in maps + [head_map]:   # the kernels scatter through these unchecked
             assert int(m_.max()) < self.fp.n_pad and int(m_.min()) >= -1
+        # the flat slots no LSTM slab map covers (the head's, the padding): updated from the gradient
+        # as it stands when the paired slab sum applies Adam itself
+        covered = np.concatenate([m_.cpu().numpy() for m_ in maps])
+        rest = np.setdiff1d(np.arange(self.fp.n_pad), covered[covered >= 0]).astype(np.int32)
+        assert rest.size == 0 or (int(rest.min()) >= 0 and int(rest.max()) < self.fp.n_pad)   # scattered unchecked
         self._plan = dict(pre=pre, post=post, repeat=repeat, head=head, maps=maps, head_map=head_map,
-                          acc=torch.zeros(2, device=self.device))
+                          acc=torch.zeros(2, device=self.device), rest=torch.as_tensor(rest, device=self.device))
         return self._plan
 
     def _fused_step(self, plan, x, y, global_batch, allreduce):
@@ -367,9 +379,17 @@ class LSTMPredictor:
             dh = out[0]
             if R and i == len(pre):   # RepeatVector backward: the repeated steps' gradients summed
                 dh = (dh.view(n, -1) if R == 1 else dh.sum(1)).to(torch.bfloat16)
-        if len(deferred) == 2:
-            C.slab_sum2(deferred[0][0], deferred[0][1], deferred[1][0], deferred[1][1], grad)
-        self.opt.step(allreduce=allreduce, counted=fold)
+        if len(deferred) == 2 and allreduce is None and fold and self.opt.on_gpu and _slab2adam():
+            # the step's last launch: both slab sums + Adam over every parameter (the step count was
+            # advanced by the head's fold launch)
+            o = self.opt
+            C.slab_sum2(deferred[0][0], deferred[0][1], deferred[1][0], deferred[1][1], grad, params=self.fp.flat,
+                        m=self.fp.m, v=self.fp.v, iter=self.fp.iter, lr=o.lr, beta1=o.b1, beta2=o.b2, eps=o.eps,
+                        gscale=1.0, rest=plan["rest"])
+        else:
+            if len(deferred) == 2:
+                C.slab_sum2(deferred[0][0], deferred[0][1], deferred[1][0], deferred[1][1], grad)
+            self.opt.step(allreduce=allreduce, counted=fold)
         if fold:
             return metrics[0], metrics[1]   # acc is overwritten by the next step, metrics is this step's own
         # device-tensor divisors: an IEEE division, as the fold launch's (a Python-scalar divisor is a

@@ -558,3 +558,31 @@ def test_paired_slab_sum_equals_two_launches(cuda_device, monkeypatch):
     for a, b in zip(out["1"][0], out["0"][0]):
         assert torch.equal(a, b)
     assert torch.equal(out["1"][1], out["0"][1])
+
+
+def test_slab_sum_with_adam_equals_separate_adam(cuda_device, monkeypatch):
+    """Adam applied by the paired slab-sum launch itself (slab_sum2_kernel<ADAM>: the LSTM slots where
+    their gradient becomes final, the head's and the padding from the gradient as it stands) gives
+    the same bits as the separate Adam launch (SML_LSTM_SLAB2ADAM=0), step after step."""
+    from streamml.data.stream import sliding_windows
+    rows = torch.tensor(np.random.default_rng(11).uniform(-1, 1, (4 * 1000 + 50, 18)), dtype=torch.float32,
+                        device=cuda_device)
+    X, Y = sliding_windows(rows, 50)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SML_LSTM_SLAB2ADAM", v)
+        m = LSTMPredictor.two_layer(look_back=50, device=cuda_device, seed=6)
+        losses = []
+        for s in range(4):
+            loss, acc = m.train_step(X[s * 1000:(s + 1) * 1000], Y[s * 1000:(s + 1) * 1000])
+            losses.append((float(loss), float(acc)))
+        fp = m.fp
+        out[v] = (losses, [t.detach().clone() for t in (fp.flat, fp.m, fp.v, fp.grad, fp.iter)])
+    assert out["1"][0] == out["0"][0]
+    for a, b in zip(out["1"][1], out["0"][1]):
+        assert torch.equal(a, b), (a - b).abs().max().item() if a.is_floating_point() else (a, b)
+    assert int(out["1"][1][4].item()) == 4
+    plan = m._fused_plan()   # every flat slot is updated exactly once: a slab map's or the rest list's
+    slots = np.concatenate([mp.cpu().numpy() for mp in plan["maps"]] + [plan["rest"].cpu().numpy()])
+    slots = slots[slots >= 0]
+    assert len(slots) == len(set(slots.tolist())) == m.fp.n_pad
