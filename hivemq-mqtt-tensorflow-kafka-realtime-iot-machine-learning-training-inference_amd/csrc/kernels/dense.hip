@@ -453,6 +453,15 @@ __device__ __forceinline__ void slab_sum1_body(const float* __restrict__ in, int
   __shared__ f32x4 red[16][16];
   float tstep = 0.f;
   if constexpr (ADAM) tstep = (float)ad.iter[0];   // issued before the slab loads
+  // the slab map's 4 entries of this thread's quad, loaded before the slab loads too (after the sum
+  // they were one more dependent round trip: map, then the scatter / the Adam operand gathers)
+  int dm[4] = {-1, -1, -1, -1};
+  if constexpr (MAP) {
+    if ((threadIdx.x >> 4) == 0 && (blk * 16 + (threadIdx.x & 15)) * 4 < S) {
+      const int4 mv = *reinterpret_cast<const int4*>(map + (blk * 16 + (threadIdx.x & 15)) * 4);
+      dm[0] = mv.x; dm[1] = mv.y; dm[2] = mv.z; dm[3] = mv.w;
+    }
+  }
   const int qi = threadIdx.x & 15, grp = threadIdx.x >> 4;
   const int quad = blk * 16 + qi;
   f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -464,6 +473,20 @@ __device__ __forceinline__ void slab_sum1_body(const float* __restrict__ in, int
     }
     for (; g < G; g += 16, k = (k + 1) & 3) acc[k] += *reinterpret_cast<const f32x4*>(in + (int64_t)g * S + quad * 4);
   }
+  // ADAM: the 12 operand gathers of the quad's slots, all issued at once (clamped index, no branches)
+  // before the barrier, so they overlap the other groups' tails and the LDS fold
+  float pm[4] = {0.f, 0.f, 0.f, 0.f}, pv[4] = {0.f, 0.f, 0.f, 0.f}, pp[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (ADAM) {
+    if (grp == 0 && quad * 4 < S) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int dd = dm[j] >= 0 ? dm[j] : 0;
+        pm[j] = ad.m[dd];
+        pv[j] = ad.v[dd];
+        pp[j] = ad.params[dd];
+      }
+    }
+  }
   red[grp][qi] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
   if (grp == 0 && quad * 4 < S) {
@@ -474,10 +497,16 @@ __device__ __forceinline__ void slab_sum1_body(const float* __restrict__ in, int
       const float lr_t = ADAM ? adam_lr_t(ad.lr, ad.b1, ad.b2, tstep) : 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int d = map[quad * 4 + j];
+        const int d = dm[j];
         if (d >= 0) {
           out[d] = t[j];
-          if constexpr (ADAM) slot_adam(ad, d, t[j], lr_t);
+          if constexpr (ADAM) {
+            float mm, vv, pn;
+            adam_update(t[j], pm[j], pv[j], pp[j], lr_t, ad.b1, ad.b2, ad.eps, ad.gscale, mm, vv, pn);
+            ad.m[d] = mm;
+            ad.v[d] = vv;
+            ad.params[d] = pn;
+          }
         }
       }
     } else {
