@@ -186,6 +186,10 @@ __global__ __launch_bounds__(256) void head_fold_kernel(const float* __restrict_
   const int PS = 16 * N + N + 2;
   const int s = blockIdx.x;
   __shared__ float red[256];
+  const int NP = N <= 16 ? 16 : 32;          // the dense slab's padded output width
+  // the entry's gradient slot, loaded before the partials (after the tree it was one more round trip)
+  int dst = -1;
+  if (threadIdx.x == 0 && s < 17 * N) dst = s < 16 * N ? map[(s / N) * NP + s % N] : map[16 * NP + (s - 16 * N)];
   float v = 0.f;
   for (int gi = threadIdx.x; gi < G; gi += 256) v += part[(int64_t)gi * PS + s];
   red[threadIdx.x] = v;
@@ -197,14 +201,8 @@ __global__ __launch_bounds__(256) void head_fold_kernel(const float* __restrict_
   }
   if (threadIdx.x == 0) {
     const float tot = red[0];
-    const int NP = N <= 16 ? 16 : 32;          // the dense slab's padded output width
-    if (s < 16 * N) {                          // dW[unit][output]
-      const int u = s / N, o = s % N;
-      const int m = map[u * NP + o];
-      if (m >= 0) grad[m] = tot;
-    } else if (s < 17 * N) {                   // db[output]
-      const int m = map[16 * NP + (s - 16 * N)];
-      if (m >= 0) grad[m] = tot;
+    if (s < 17 * N) {                          // dW[unit][output], then db[output]
+      if (dst >= 0) grad[dst] = tot;
     } else {
       const int k = s - 17 * N;                // 0: sum of squared errors, 1: correct rows
       acc[k] = tot;
